@@ -1,0 +1,122 @@
+"""Pin the CPU oracle (oracle/tpe_oracle.py) against vectors produced by the
+reference itself (tools/gen_golden.py).  Bit-exact wherever the reference is
+deterministic float64 numpy."""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+from oracle.spacedesc import params_from_desc, synthetic_loss
+
+
+def _none(v):
+    return None if v is None else v
+
+
+def test_adaptive_parzen_normal_exact(golden):
+    for case in golden('unit_vectors.json')['adaptive_parzen_normal']:
+        w, m, s = O.adaptive_parzen_normal(np.asarray(case['mus'], dtype=float), case['prior_weight'],
+                                           case['prior_mu'], case['prior_sigma'])
+        assert list(w) == case['w']
+        assert list(m) == case['mu']
+        assert list(s) == case['sigma']
+
+
+def test_linear_forgetting_exact(golden):
+    for case in golden('unit_vectors.json')['linear_forgetting_weights']:
+        assert list(O.linear_forgetting_weights(case['N'], case['LF'])) == case['w']
+
+
+def test_ap_filter_trials_exact(golden):
+    for case in golden('unit_vectors.json')['ap_filter_trials']:
+        b, a = O.ap_filter_trials(case['o_idxs'], case['o_vals'], case['l_idxs'], case['l_vals'], case['gamma'])
+        assert list(b) == case['below']
+        assert list(a) == case['above']
+
+
+def test_lpdf_exact(golden):
+    for case in golden('unit_vectors.json')['lpdf']:
+        if case['fn'] == 'categorical_lpdf':
+            out = O.categorical_lpdf(np.asarray(case['x']), case['p'])
+        else:
+            fn = O.gmm1_lpdf if case['fn'] == 'GMM1_lpdf' else O.lgmm1_lpdf
+            out = fn(np.asarray(case['x']), case['w'], case['mu'], case['sigma'],
+                     low=case['low'], high=case['high'], q=case['q'])
+        np.testing.assert_array_equal(out, np.asarray(case['out']))
+    ka = golden('unit_vectors.json')['known_answers']['gmm1_trunc']
+    # SURVEY.md §4 known answer
+    np.testing.assert_allclose(ka, [-0.6669088273212322, 0.22459306080875785, -0.08783249158139861], rtol=0, atol=0)
+
+
+def test_samplers_exact(golden):
+    for case in golden('unit_vectors.json')['samplers']:
+        rng = np.random.RandomState(case['seed'])
+        if case['fn'] == 'categorical':
+            out = O.categorical_sample(rng, case['p'], case['size'])
+        else:
+            fn = O.gmm1_sample if case['fn'] == 'GMM1' else O.lgmm1_sample
+            out = fn(rng, case['w'], case['mu'], case['sigma'], low=case['low'], high=case['high'],
+                     q=case['q'], size=case['size'])
+        np.testing.assert_array_equal(out, np.asarray(case['out']))
+
+
+def test_broadcast_best(golden):
+    for case in golden('unit_vectors.json')['broadcast_best']:
+        i = O.broadcast_best_index(case['l'], case['g'])
+        assert [case['samples'][i]] * len(case['samples']) == case['out']
+
+
+def test_kernel_vectors_fit_and_lpdf_exact(golden):
+    for case in golden('kernel_vectors.json'):
+        b = O.fit_posterior(case['dist'], case['args'], np.asarray(case['below']), 1.0)
+        a = O.fit_posterior(case['dist'], case['args'], np.asarray(case['above']), 1.0)
+        for post, ref in ((b, case['b_params']), (a, case['a_params'])):
+            for got, want in zip(post.params, ref):
+                assert list(np.asarray(got, dtype=float)) == [float(v) for v in want], case['dist']
+        cand = np.asarray(case['cand'])
+        np.testing.assert_array_equal(b.lpdf(cand), np.asarray(case['l']))
+        np.testing.assert_array_equal(a.lpdf(cand), np.asarray(case['g']))
+        below, above = O.ap_filter_trials(np.arange(case['N']), case['vals'], np.arange(case['N']),
+                                          case['losses'], 0.25)
+        assert list(below) == case['below'] and list(above) == case['above']
+
+
+def _history(h):
+    return [dict(tid=d['tid'], loss=d['loss'], vals=d['vals']) for d in h]
+
+
+def test_suggest_vectors_exact(golden):
+    g = golden('suggest_vectors.json')
+    for case in g['cases']:
+        params = params_from_desc(g['spaces'][case['space']])
+        if case.get('kind') == 'rand':
+            got = O.rand_suggest(params, case['seed'])
+        else:
+            got = O.tpe_suggest(params, _history(case['history']), case['seed'],
+                                n_EI_candidates=case['n_EI_candidates'])
+        want = case['result']
+        assert set(got) == set(want), (case['space'], case['seed'])
+        for k in want:
+            assert float(got[k]) == float(want[k]), (case['space'], case['seed'], k)
+
+
+def test_fmin_trajectories_exact(golden):
+    g = golden('fmin_traj.json')
+    for run in g['runs']:
+        params = params_from_desc(g['spaces'][run['space']])
+        if run['space'] == 'u1':
+            hist = O.fmin(lambda v: (float(v['x']) - 3) ** 2, params, run['max_evals'],
+                          np.random.RandomState(run['seed']))
+            assert [float(h['vals']['x'][0]) for h in hist] == run['x']
+            assert [h['loss'] for h in hist] == run['loss']
+        else:
+            tid = [0]
+
+            def fn(vals):
+                out = synthetic_loss(vals, tid[0])
+                tid[0] += 1
+                return out
+            hist = O.fmin(fn, params, run['max_evals'], np.random.RandomState(run['seed']))
+            got = [{k: float(v[0]) for k, v in h['vals'].items() if v} for h in hist]
+            want = [{k: float(v) for k, v in d.items()} for d in run['vals']]
+            assert got == want
+            assert [h['loss'] for h in hist] == run['loss']
