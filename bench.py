@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Headline benchmark: EI candidates scored/sec + tpe.suggest p50 latency.
+
+Workload (BASELINE.json configs[2], "config 3"): the conditional hp.choice
+tree space (svm{C, kernel{rbf: gamma, poly: degree}} | rf{...} | knn{...}),
+a 10,000-trial synthetic history, n_EI_candidates = 2^20 per GPU, one
+``tpe.suggest`` per step (host history/fit + device sample/score/select,
+entry to returned document).  N GPUs: weak scaling along the candidate axis —
+each rank scores 2^20 candidates of every active hyperparameter, total
+C = N * 2^20, per-level winner combined by one all-gather (dist.py).
+
+value  = sum over steps of (active hyperparameters x total candidates) / time
+roofline: the dominant kernel (k_above_f32, the above-mixture log-sum-exp)
+          timed per launch with HIP events on the engine's stream.
+cpu_baseline: the CPU oracle (numpy restatement of the reference, 1 core) on
+          a bounded sample of the same workload.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+C_PER_GPU = 1 << 20
+N_HISTORY = 10000
+SEED = 20241015
+
+
+def tree_space(hp):
+    return {'model': hp.choice('model', [
+        {'name': 'svm', 'C': hp.loguniform('svm_C', -5, 5),
+         'kernel': hp.choice('svm_kernel', [{'gamma': hp.loguniform('svm_rbf_gamma', -5, 2)},
+                                            {'degree': hp.quniform('svm_poly_degree', 2, 5, 1)}])},
+        {'name': 'rf', 'n_est': hp.quniform('rf_n_est', 10, 500, 10),
+         'depth': hp.choice('rf_depth', [None, hp.quniform('rf_depth_n', 2, 30, 1)]),
+         'crit': hp.choice('rf_crit', ['gini', 'entropy'])},
+        {'name': 'knn', 'k': hp.quniform('knn_k', 1, 50, 1), 'p': hp.uniform('knn_p', 1, 3)}])}
+
+
+def synthetic_loss(v, tid):
+    """Smooth synthetic objective favouring the svm/rbf branch; 1e-9*tid breaks ties."""
+    loss = 1.0
+    if v.get('model') == 0:
+        loss = 0.5 + 0.05 * (math.log(float(v['svm_C'])) - 1.0) ** 2
+        if v.get('svm_kernel') == 0:
+            loss -= 0.2 - 0.02 * (math.log(float(v['svm_rbf_gamma'])) + 2.0) ** 2
+    elif v.get('model') == 1:
+        loss = 0.8 + 1e-4 * abs(float(v['rf_n_est']) - 200)
+    else:
+        loss = 0.9 + 0.01 * abs(float(v['knn_k']) - 7)
+    return loss + 1e-9 * tid
+
+
+def make_history(n, seed):
+    from hyperopt_amd import base, hp, rand
+    domain = base.Domain(lambda d: 0.0, tree_space(hp))
+    trials = base.Trials()
+    rs = np.random.RandomState(seed)
+    docs = []
+    for tid in range(n):
+        d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
+        v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
+        d['state'] = base.JOB_STATE_DONE
+        d['result'] = {'status': 'ok', 'loss': synthetic_loss(v, tid)}
+        docs.append(d)
+    trials.insert_trial_docs(docs)
+    trials.refresh()
+    return domain, trials
+
+
+def cpu_baseline(domain, trials, budget_s=15.0):
+    """The oracle (numpy, 1 thread) on a bounded sample: whole suggests at
+    C=16384 on the same history, repeated until ~budget_s of CPU work."""
+    from oracle import tpe_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(1)
+    except Exception:  # pragma: no cover
+        limiter = None
+    params = []
+    for r in domain.table.rows:
+        parent = None if r.parents == [None] else tuple(r.parents[0])
+        params.append(dict(label=r.label, dist=r.dist, args=dict(r.args), parent=parent))
+    hist = [dict(tid=d['tid'], loss=d['result']['loss'], vals=d['misc']['vals']) for d in trials.trials]
+    C = 16384
+    n_scores, t0, calls = 0, time.time(), 0
+    while time.time() - t0 < budget_s:
+        out = O.tpe_suggest(params, hist, 1000 + calls, n_EI_candidates=C)
+        n_scores += len(out) * C
+        calls += 1
+    dt = time.time() - t0
+    if limiter is not None:
+        limiter.unregister()
+    return dict(value=n_scores / dt, unit='candidate-scores/s', cores=1, kind='port',
+                sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, %.1fs' % (calls, dt))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--history', type=int, default=N_HISTORY)
+    ap.add_argument('--cands', type=int, default=C_PER_GPU)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+
+    from hyperopt_amd import engine as engine_mod, tpe
+    from hyperopt_amd.engine import get_engine
+    get_engine(device)
+    domain, trials = make_history(args.history, SEED)
+    new_id = args.history
+    shard = (rank, world) if world > 1 else None
+    C_total = args.cands * world
+
+    def step(i):
+        return tpe.suggest([new_id], domain, trials, SEED + i, n_EI_candidates=C_total, shard=shard)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    lat = []
+    n_active = 0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        s0 = time.perf_counter()
+        docs = step(1000 + i)
+        lat.append(time.perf_counter() - s0)
+        n_active += sum(1 for v in docs[0]['misc']['vals'].values() if v)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = n_active * C_total / elapsed
+
+    # dominant-kernel roofline, measured live with HIP events on the engine stream
+    eng = engine_mod._ENGINES[str(device)]
+    eng.profile = {}
+    for i in range(5):
+        step(5000 + i)
+    torch.cuda.synchronize()
+    prof = eng.profile
+    eng.profile = None
+    above = prof.get('k_above_f32', [])
+    roof = None
+    if above:
+        ms = np.array([a[0] for a in above])
+        ce = np.array([a[1] for a in above], dtype=np.float64)
+        achieved_ce = float(ce.sum() / (ms.sum() * 1e-3))
+        flops_per_ce = 8.0
+        peak_tflops = 157.3
+        roof = dict(bound='valu', kernel='k_above_f32', achieved=achieved_ce * flops_per_ce / 1e12,
+                    peak=peak_tflops, unit='TFLOP/s', frac=achieved_ce * flops_per_ce / 1e12 / peak_tflops,
+                    traffic=None, ce_per_s=achieved_ce, ce_per_launch=float(ce.mean()),
+                    avg_launch_ms=float(ms.mean()), flops_per_ce=flops_per_ce,
+                    note='CE = one mixture component at one candidate (sub,sub,mul,fma,exp2,add); '
+                         'peak = MI355X fp32 vector spec; exp2 issues at ~1/4-1/6 of the FMA rate')
+        tr = os.path.join(ROOT, 'profiles', 'r01_traffic.json')
+        if os.path.exists(tr):
+            with open(tr) as f:
+                t = json.load(f)
+            roof['traffic'] = t.get('bytes_per_launch')
+            roof['traffic_source'] = 'profiles/r01_traffic.json'
+    stages = {k: float(np.mean([a[0] for a in v])) for k, v in prof.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(domain, trials)
+
+    if rank == 0:
+        out = {
+            'metric': 'EI candidates scored/sec (node) + tpe.suggest p50 latency, 1M cands x 10k trials',
+            'value': value, 'unit': 'candidate-scores/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': 'config3: conditional hp.choice tree, %d-trial history, '
+                                   'n_EI_candidates=%d per GPU (%d total), one tpe.suggest per step'
+                                   % (args.history, args.cands, C_total),
+                       'history': args.history, 'n_EI_candidates': C_total,
+                       'parallelism': 'candidate-shard x%d' % world},
+            'p50_suggest_ms': 1e3 * float(np.median(lat)), 'p99_suggest_ms': 1e3 * float(np.percentile(lat, 99)),
+            'active_hyperparameters_per_suggest': n_active / args.steps,
+            'stage_ms': stages, 'roofline': roof, 'cpu_baseline': cpu,
+        }
+        if cpu:
+            out['speedup_vs_cpu_baseline'] = value / cpu['value']
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,100 @@
+"""ctypes binding of libtpe_hip.so (declared in include/tpe_hip.h).
+
+The library is built in-tree (``__graft_entry__.build()`` or
+``python -m hyperopt_amd.build``).  There is no fallback: if the library is
+missing or does not load, every suggest call raises ``NativeUnavailable``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libtpe_hip.so')
+ABI_VERSION = 1
+
+FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
+F_HAS_LOW, F_HAS_HIGH = 1, 2
+PREC_F32, PREC_F64 = 0, 1
+
+# numpy mirrors of the C structs (the host builds arrays of them and copies
+# them to device memory in one transfer)
+PROBLEM_DTYPE = np.dtype([
+    ('family', '<i4'), ('flags', '<i4'), ('n_cand', '<i4'), ('n_upper', '<i4'),
+    ('cand_off', '<i8'), ('cand_base', '<i8'), ('part_off', '<i8'),
+    ('n_splits', '<i4'), ('tile_off', '<i4'), ('n_tiles', '<i4'), ('samp_off', '<i4'),
+    ('samp_len', '<i4'), ('below_off', '<i4'), ('below_len', '<i4'), ('above_off', '<i4'),
+    ('above_len', '<i4'), ('reserved', '<i4'),
+    ('low', '<f8'), ('high', '<f8'), ('q', '<f8'), ('below_base', '<f8'), ('above_base', '<f8'),
+    ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
+])
+assert PROBLEM_DTYPE.itemsize == 136
+TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4')])
+WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
+                       ('k_start', '<i4'), ('k_end', '<i4'), ('reserved', '<i4')])
+BEST_DTYPE = np.dtype([('score', '<f8'), ('l', '<f8'), ('g', '<f8'), ('idx', '<i8')])
+RESULT_DTYPE = np.dtype([('score', '<f8'), ('l', '<f8'), ('g', '<f8'), ('value', '<f8'),
+                         ('idx', '<i8'), ('global_idx', '<i8')])
+assert RESULT_DTYPE.itemsize == 48
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [
+        ('problems', ctypes.c_void_p), ('n_problems', ctypes.c_int32),
+        ('precision', ctypes.c_int32), ('sample', ctypes.c_int32), ('reserved', ctypes.c_int32),
+        ('comp32', ctypes.c_void_p), ('comp64', ctypes.c_void_p), ('samp', ctypes.c_void_p),
+        ('cand', ctypes.c_void_p), ('coord', ctypes.c_void_p),
+        ('tiles', ctypes.c_void_p), ('n_tiles', ctypes.c_int32), ('reserved2', ctypes.c_int32),
+        ('work', ctypes.c_void_p),
+        ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32),
+        ('n_work_qlog', ctypes.c_int32), ('reserved3', ctypes.c_int32),
+        ('part', ctypes.c_void_p), ('l_out', ctypes.c_void_p), ('g_out', ctypes.c_void_p),
+        ('tile_best', ctypes.c_void_p), ('result', ctypes.c_void_p),
+    ]
+
+
+EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
+           'tpe_run_batch', 'tpe_sample', 'tpe_score_above', 'tpe_finalize', 'tpe_select')
+
+
+class NativeUnavailable(RuntimeError):
+    """libtpe_hip.so is missing, fails to load, or finds no HIP device."""
+
+
+_LIB = None
+
+
+def load(path=LIB_PATH):
+    """Load (once) and type the C-ABI.  Raises NativeUnavailable, never falls back."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise NativeUnavailable('%s is not built (run __graft_entry__.build() or '
+                                'python -m hyperopt_amd.build)' % path)
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:
+        raise NativeUnavailable('cannot load %s: %s' % (path, e))
+    lib.tpe_abi_version.restype = ctypes.c_int
+    lib.tpe_last_error.restype = ctypes.c_char_p
+    lib.tpe_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    lib.tpe_tile_size.restype = ctypes.c_int
+    for name in ('tpe_run_batch', 'tpe_sample', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
+        fn = getattr(lib, name)
+        fn.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
+        fn.restype = ctypes.c_int
+    if lib.tpe_abi_version() != ABI_VERSION:
+        raise NativeUnavailable('ABI mismatch: library %d, bindings %d' % (lib.tpe_abi_version(), ABI_VERSION))
+    _LIB = lib
+    return lib
+
+
+def check(rc, lib, what):
+    if rc != 0:
+        msg = lib.tpe_last_error().decode(errors='replace')
+        raise RuntimeError('%s failed (%d): %s' % (what, rc, msg))
+
+
+def tile_size():
+    return load().tpe_tile_size()

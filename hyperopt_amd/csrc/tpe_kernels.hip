@@ -1,0 +1,560 @@
+// tpe_kernels.hip — gfx950 kernels + C-ABI of the TPE suggest engine.
+//
+// Replaces, per (new_id, hyperparameter) problem, the numpy operators of
+// gsmafra/hyperopt's tpe.suggest (see include/tpe_hip.h for the reference
+// file:line of each stage).  Four stages, each a batched launch over a flat
+// work list so that problems of very different size share one grid:
+//
+//   tpe_sample       Philox-4x32-10 candidates from the below mixture
+//   tpe_score_above  candidate x component log-sum-exp of the above mixture
+//                    (the O(C*K) hot loop; components are wave-uniform and are
+//                    read through the scalar cache, candidates live in VGPRs)
+//   tpe_finalize     below lpdf (<= 26 components), l - g, per-tile argmax
+//   tpe_select       per-problem argmax over tiles (first index on ties, NaN
+//                    wins, like np.argmax) and the chosen value
+//
+// No atomics: every reduction is in a fixed order, so results are bitwise
+// reproducible run to run and identical for any candidate sharding.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/tpe_hip.h"
+
+namespace {
+
+constexpr int kThreads = 256;          // 4 waves of 64
+constexpr int kR = 8;                  // candidates per thread
+constexpr int kTile = kThreads * kR;   // candidates per tile
+constexpr double kEPS = 1e-12;         // tpe.py:25
+constexpr double kLn2 = 0.69314718055994530942;
+
+thread_local char g_err[512];
+
+int fail(int code, const char* what) {
+  snprintf(g_err, sizeof(g_err), "%s", what);
+  return code;
+}
+
+int hip_check(const char* stage) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", stage, hipGetErrorString(e));
+    return TPE_E_HIP;
+  }
+  return TPE_OK;
+}
+
+// ---------------------------------------------------------------- Philox
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += W0; k1 += W1;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+// open-interval uniforms
+__device__ __forceinline__ float u01f(uint32_t r) { return ((float)(r >> 8) + 0.5f) * 5.9604644775390625e-08f; }
+__device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
+  const uint64_t m = ((uint64_t)a << 21) ^ (uint64_t)(b >> 11);   // 53 bits
+  return ((double)m + 0.5) * 1.1102230246251565e-16;
+}
+
+// ------------------------------------------------------- normal helpers
+__device__ __forceinline__ float phi_std(float z) { return 0.5f * erfcf(-z * 0.70710678118654752f); }
+__device__ __forceinline__ double phi_std(double z) { return 0.5 * erfc(-z * 0.70710678118654752); }
+__device__ __forceinline__ float erfcinv_(float v) { return erfcinvf(v); }
+__device__ __forceinline__ double erfcinv_(double v) { return erfcinv(v); }
+
+// standard normal truncated to [za, zb) by inversion.  The interval is mirrored
+// into the lower half-line first so both CDF values keep relative precision.
+template <typename T>
+__device__ __forceinline__ T trunc_std_normal(T za, T zb, T u) {
+  const bool flip = za > T(0);
+  if (flip) { const T t = -zb; zb = -za; za = t; }
+  const T fa = phi_std(za), fb = phi_std(zb);
+  const T p = fa + u * (fb - fa);
+  const T z = T(-1.41421356237309505) * erfcinv_(T(2) * p);
+  return flip ? -z : z;
+}
+
+// ---------------------------------------------------------- argmax order
+// np.argmax: NaN is the maximum (first NaN wins), otherwise the largest value,
+// first index on ties.
+__device__ __forceinline__ bool better(double s, int64_t i, double bs, int64_t bi) {
+  if (bi < 0) return i >= 0;
+  if (i < 0) return false;
+  const bool n = s != s, bn = bs != bs;
+  if (n || bn) return n && (!bn || i < bi);
+  return s > bs || (s == bs && i < bi);
+}
+
+// exact max-shifted log-sum-exp (log2 domain) over a short component range
+template <typename T, typename C4>
+__device__ __forceinline__ T lse2_exact(const C4* __restrict__ comp, int k0, int n, T t) {
+  T m = -INFINITY;
+  for (int k = 0; k < n; ++k) {
+    const C4 c = comp[k0 + k];
+    const T d = (t - (T)c.x) - (T)c.y;
+    const T z = d * (T)c.z;
+    const T v = (T)c.w - z * z;
+    m = v > m ? v : m;
+  }
+  if (!(m > -INFINITY)) return m;      // empty mixture or all -inf
+  T s = 0;
+  for (int k = 0; k < n; ++k) {
+    const C4 c = comp[k0 + k];
+    const T d = (t - (T)c.x) - (T)c.y;
+    const T z = d * (T)c.z;
+    s += exp2((T)c.w - z * z - m);
+  }
+  return m + log2(s);
+}
+
+// double version for comp64 {mu, a, c, 0}
+__device__ __forceinline__ double lse2_exact64(const double4* __restrict__ comp, int k0, int n, double t) {
+  double m = -INFINITY;
+  for (int k = 0; k < n; ++k) {
+    const double4 c = comp[k0 + k];
+    const double z = (t - c.x) * c.y;
+    const double v = c.z - z * z;
+    m = v > m ? v : m;
+  }
+  if (!(m > -INFINITY)) return m;
+  double s = 0;
+  for (int k = 0; k < n; ++k) {
+    const double4 c = comp[k0 + k];
+    const double z = (t - c.x) * c.y;
+    s += exp2(c.z - z * z - m);
+  }
+  return m + log2(s);
+}
+
+// quantized mixture mass: sum_k w Phi(zu) - w Phi(zl), reference operation order
+// (tpe.py:147-159 / :285-298).  LOG selects lognormal_cdf's constant folding.
+template <bool LOG>
+__device__ __forceinline__ double qmass(const double4* __restrict__ comp, int k0, int n, double tu, double tl) {
+  double prob = 0.0;
+  for (int k = 0; k < n; ++k) {
+    const double4 c = comp[k0 + k];
+    const double zu = (tu - c.x) / c.y;
+    const double zl = (tl - c.x) / c.y;
+    double inc, dec;
+    if (LOG) { inc = c.z * (.5 + .5 * erf(zu)); dec = c.z * (.5 + .5 * erf(zl)); }
+    else     { inc = c.z * (0.5 * (1 + erf(zu))); dec = c.z * (0.5 * (1 + erf(zl))); }
+    inc -= dec;
+    prob += inc;
+  }
+  return prob;
+}
+
+// quantization interval of one candidate in the kernel coordinate
+// (tpe.py:148-155 for GMM1_lpdf, :286-294 + lognormal_cdf :185 for LGMM1_lpdf)
+__device__ __forceinline__ void q_bounds(const tpe_problem& p, double x, double& tu, double& tl) {
+  double ub = x + p.q / 2.0, lb = x - p.q / 2.0;
+  if (p.family == TPE_FAM_QGAUSS) {
+    if (p.flags & TPE_F_HAS_HIGH) ub = fmin(ub, p.high);
+    if (p.flags & TPE_F_HAS_LOW) lb = fmax(lb, p.low);
+    tu = ub; tl = lb;
+  } else {
+    if (p.flags & TPE_F_HAS_HIGH) ub = fmin(ub, exp(p.high));
+    if (p.flags & TPE_F_HAS_LOW) lb = fmax(lb, exp(p.low));
+    lb = fmax(0.0, lb);
+    tu = log(fmax(ub, kEPS));
+    tl = log(fmax(lb, kEPS));
+  }
+}
+
+// ================================================================= sample
+__global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restrict__ P,
+                                                     const tpe_tile* __restrict__ tiles,
+                                                     const double* __restrict__ samp,
+                                                     double* __restrict__ cand, float* __restrict__ coord,
+                                                     int precision) {
+  const tpe_tile tl = tiles[blockIdx.x];
+  const tpe_problem& p = P[tl.problem];
+  const bool quant = p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
+  const bool logsp = p.family == TPE_FAM_LOGGAUSS || p.family == TPE_FAM_QLOGGAUSS;
+  const double lo = p.low, hi = p.high;
+  // f32 bounds: smallest float >= low, largest float < high
+  float lo_f = -INFINITY, hi_f = INFINITY;
+  if (p.flags & TPE_F_HAS_LOW) { lo_f = (float)lo; if ((double)lo_f < lo) lo_f = nextafterf(lo_f, INFINITY); }
+  if (p.flags & TPE_F_HAS_HIGH) {
+    hi_f = (float)hi;
+    while ((double)hi_f >= hi) hi_f = nextafterf(hi_f, -INFINITY);
+  }
+  for (int j = 0; j < kR; ++j) {
+    const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
+    if (i >= p.n_cand) break;
+    const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+    const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+    // component choice by inversion of the selection CDF
+    const double u1 = u01d(r.x, r.y);
+    const double* S = samp + 8 * (int64_t)p.samp_off;
+    if (p.samp_len <= 0) { cand[p.cand_off + i] = NAN; coord[p.cand_off + i] = NAN; continue; }
+    int k = 0;
+    while (k < p.samp_len - 1 && !(u1 < S[8 * k])) ++k;
+    const double* s = S + 8 * k;
+    const int64_t o = p.cand_off + i;
+    if (p.family == TPE_FAM_CATEGORICAL) {
+      cand[o] = (double)k;
+      coord[o] = (float)k;
+      continue;
+    }
+    const double mu = s[1], sg = s[2], za = s[3], zb = s[4];
+    double x;      // draw in sampling space (log space for LGMM1)
+    if (precision == TPE_PREC_F32) {
+      const float z = trunc_std_normal<float>((float)za, (float)zb, u01f(r.z));
+      float xf = (float)mu + (float)sg * z;
+      if (!(xf == xf)) xf = (float)mu;
+      xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
+      coord[o] = xf;
+      x = (double)xf;
+    } else {
+      double z = trunc_std_normal<double>(za, zb, u01d(r.z, r.w));
+      x = mu + sg * z;
+      if (!(x == x)) x = mu;
+      if ((p.flags & TPE_F_HAS_LOW) && x < lo) x = lo;
+      if ((p.flags & TPE_F_HAS_HIGH) && x >= hi) x = nextafter(hi, -INFINITY);
+      coord[o] = (float)x;
+    }
+    if (logsp) x = exp(x);
+    if (quant) x = rint(x / p.q) * p.q;      // np.round: half to even
+    cand[o] = x;
+  }
+}
+
+// ============================================================ score above
+// Continuous families, f32: s_i += 2^(c_k - (a_k ((t_i - mu_hi_k) - mu_lo_k))^2)
+__global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __restrict__ P,
+                                                        const tpe_work* __restrict__ W,
+                                                        const float4* __restrict__ comp,
+                                                        const float* __restrict__ coord,
+                                                        double* __restrict__ part) {
+  const tpe_work w = W[blockIdx.x];
+  const tpe_problem& p = P[w.problem];
+  const int n = p.n_cand;
+  float t[kR], s[kR];
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
+    t[j] = i < n ? coord[p.cand_off + i] : 0.f;
+    s[j] = 0.f;
+  }
+  const float4* __restrict__ C = comp + p.above_off;
+#pragma unroll 4
+  for (int k = w.k_start; k < w.k_end; ++k) {
+    const float4 c = C[k];
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const float d = (t[j] - c.x) - c.y;
+      const float z = d * c.z;
+      s[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(-z, z, c.w));
+    }
+  }
+  double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
+    if (i < n) out[i] = (double)s[j];
+  }
+}
+
+// Continuous families, f64 (parity precision)
+__global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __restrict__ P,
+                                                        const tpe_work* __restrict__ W,
+                                                        const double4* __restrict__ comp,
+                                                        const double* __restrict__ cand,
+                                                        double* __restrict__ part) {
+  const tpe_work w = W[blockIdx.x];
+  const tpe_problem& p = P[w.problem];
+  const int n = p.n_cand;
+  const bool logsp = p.family == TPE_FAM_LOGGAUSS;
+  double t[kR], s[kR];
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
+    const double x = i < n ? cand[p.cand_off + i] : 1.0;
+    t[j] = logsp ? log(x) : x;
+    s[j] = 0.0;
+  }
+  const double4* __restrict__ C = comp + p.above_off;
+  for (int k = w.k_start; k < w.k_end; ++k) {
+    const double4 c = C[k];
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const double z = (t[j] - c.x) * c.y;
+      s[j] += exp2(c.z - z * z);
+    }
+  }
+  double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
+    if (i < n) out[i] = s[j];
+  }
+}
+
+// Quantized families (always f64): partial mixture mass
+template <bool LOG>
+__global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restrict__ P,
+                                                      const tpe_work* __restrict__ W,
+                                                      const double4* __restrict__ comp,
+                                                      const double* __restrict__ cand,
+                                                      double* __restrict__ part) {
+  const tpe_work w = W[blockIdx.x];
+  const tpe_problem& p = P[w.problem];
+  const int n = p.n_cand;
+  constexpr int R = kR / 2;   // two erf per component: keep register use moderate
+  for (int h = 0; h < 2; ++h) {
+    double tu[R], tl[R], s[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int i = w.cand_start + (int)threadIdx.x + (h * R + j) * kThreads;
+      const double x = i < n ? cand[p.cand_off + i] : 0.0;
+      q_bounds(p, x, tu[j], tl[j]);
+      s[j] = 0.0;
+    }
+    const double4* __restrict__ C = comp + p.above_off;
+    for (int k = w.k_start; k < w.k_end; ++k) {
+      const double4 c = C[k];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const double zu = (tu[j] - c.x) / c.y;
+        const double zl = (tl[j] - c.x) / c.y;
+        double inc, dec;
+        if (LOG) { inc = c.z * (.5 + .5 * erf(zu)); dec = c.z * (.5 + .5 * erf(zl)); }
+        else     { inc = c.z * (0.5 * (1 + erf(zu))); dec = c.z * (0.5 * (1 + erf(zl))); }
+        inc -= dec;
+        s[j] += inc;
+      }
+    }
+    double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int i = w.cand_start + (int)threadIdx.x + (h * R + j) * kThreads;
+      if (i < n) out[i] = s[j];
+    }
+  }
+}
+
+// =============================================================== finalize
+__global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __restrict__ P,
+                                                       const tpe_tile* __restrict__ tiles,
+                                                       const float4* __restrict__ comp32,
+                                                       const double4* __restrict__ comp64,
+                                                       const double* __restrict__ cand,
+                                                       const float* __restrict__ coord,
+                                                       const double* __restrict__ part,
+                                                       double* __restrict__ l_out, double* __restrict__ g_out,
+                                                       tpe_best* __restrict__ tile_best, int precision) {
+  const tpe_tile tl = tiles[blockIdx.x];
+  const tpe_problem& p = P[tl.problem];
+  const int n = p.n_cand;
+  double bs = 0, bl = 0, bg = 0;
+  int64_t bi = -1;
+  for (int j = 0; j < kR; ++j) {
+    const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
+    if (i >= n) break;
+    const int64_t o = p.cand_off + i;
+    const double x = cand[o];
+    double l, g;
+    if (p.family == TPE_FAM_CATEGORICAL) {
+      const int c = (int)x;
+      if (c >= 0 && c < p.n_upper && (double)c == x) {
+        l = comp64[p.below_off + c].x;
+        g = comp64[p.above_off + c].x;
+      } else {
+        l = NAN; g = NAN;      // the reference raises IndexError here
+      }
+    } else if (p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS) {
+      double tu, tlo;
+      q_bounds(p, x, tu, tlo);
+      const double mb = p.family == TPE_FAM_QGAUSS ? qmass<false>(comp64, p.below_off, p.below_len, tu, tlo)
+                                                   : qmass<true>(comp64, p.below_off, p.below_len, tu, tlo);
+      double ma = 0.0;
+      for (int sp = 0; sp < p.n_splits; ++sp) ma += part[p.part_off + (int64_t)sp * n + i];
+      l = log(mb) + p.below_base;
+      g = log(ma) + p.above_base;
+    } else {
+      const bool logsp = p.family == TPE_FAM_LOGGAUSS;
+      double sa = 0.0;
+      for (int sp = 0; sp < p.n_splits; ++sp) sa += part[p.part_off + (int64_t)sp * n + i];
+      double lb2, la2;
+      if (precision == TPE_PREC_F32) {
+        const float t = coord[o];
+        lb2 = (double)lse2_exact<float, float4>(comp32, p.below_off, p.below_len, t);
+        // fixed-shift sum; if it under-flowed, redo this candidate max-shifted
+        la2 = sa > 1e-30 ? log2(sa) : (double)lse2_exact<float, float4>(comp32, p.above_off, p.above_len, t);
+      } else {
+        const double t = logsp ? log(x) : x;
+        lb2 = lse2_exact64(comp64, p.below_off, p.below_len, t);
+        la2 = sa > 1e-280 ? log2(sa) : lse2_exact64(comp64, p.above_off, p.above_len, t);
+      }
+      const double lnx = logsp ? log(x) : 0.0;
+      l = lb2 * kLn2 + p.below_base - lnx;
+      g = la2 * kLn2 + p.above_base - lnx;
+    }
+    const double sc = l - g;
+    if (l_out) { l_out[o] = l; g_out[o] = g; }
+    if (better(sc, i, bs, bi)) { bs = sc; bl = l; bg = g; bi = i; }
+  }
+  // wave reduction, then across the 4 waves through LDS
+  for (int off = 32; off > 0; off >>= 1) {
+    const double os = __shfl_xor(bs, off), ol = __shfl_xor(bl, off), og = __shfl_xor(bg, off);
+    const int64_t oi = __shfl_xor(bi, off);
+    if (better(os, oi, bs, bi)) { bs = os; bl = ol; bg = og; bi = oi; }
+  }
+  __shared__ tpe_best wb[kThreads / 64];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) wb[wave] = tpe_best{bs, bl, bg, bi};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tpe_best b = wb[0];
+    for (int q = 1; q < kThreads / 64; ++q)
+      if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
+    tile_best[blockIdx.x] = b;
+  }
+}
+
+// ================================================================= select
+__global__ __launch_bounds__(kThreads) void k_select(const tpe_problem* __restrict__ P,
+                                                     const tpe_best* __restrict__ tile_best,
+                                                     const double* __restrict__ cand,
+                                                     tpe_result* __restrict__ result) {
+  const tpe_problem& p = P[blockIdx.x];
+  tpe_best b{0, 0, 0, -1};
+  for (int t = threadIdx.x; t < p.n_tiles; t += kThreads) {
+    const tpe_best o = tile_best[p.tile_off + t];
+    if (better(o.score, o.idx, b.score, b.idx)) b = o;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    tpe_best o;
+    o.score = __shfl_xor(b.score, off); o.l = __shfl_xor(b.l, off); o.g = __shfl_xor(b.g, off);
+    o.idx = __shfl_xor(b.idx, off);
+    if (better(o.score, o.idx, b.score, b.idx)) b = o;
+  }
+  __shared__ tpe_best wb[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    b = wb[0];
+    for (int q = 1; q < kThreads / 64; ++q)
+      if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
+    tpe_result r;
+    r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
+    r.value = b.idx >= 0 ? cand[p.cand_off + b.idx] : 0.0;
+    r.global_idx = b.idx >= 0 ? p.cand_base + b.idx : -1;
+    result[blockIdx.x] = r;
+  }
+}
+
+int check_batch(const tpe_batch* b) {
+  if (!b) return fail(TPE_E_ARG, "null batch");
+  if (b->n_problems < 0 || b->n_tiles < 0 || b->n_work_cont < 0 || b->n_work_qgauss < 0 || b->n_work_qlog < 0)
+    return fail(TPE_E_ARG, "negative count");
+  const int64_t n_work = (int64_t)b->n_work_cont + b->n_work_qgauss + b->n_work_qlog;
+  if (b->precision != TPE_PREC_F32 && b->precision != TPE_PREC_F64) return fail(TPE_E_ARG, "bad precision");
+  if (b->n_problems > 0 && (!b->problems || !b->result)) return fail(TPE_E_ARG, "null problems/result");
+  if (b->n_tiles > 0 && (!b->tiles || !b->tile_best || !b->cand || !b->coord)) return fail(TPE_E_ARG, "null tile buffers");
+  if (n_work > 0 && (!b->work || !b->part)) return fail(TPE_E_ARG, "null work buffers");
+  if (n_work > 0 && b->precision == TPE_PREC_F32 && b->n_work_cont > 0 && !b->comp32)
+    return fail(TPE_E_ARG, "null comp32");
+  if ((n_work > 0 || b->n_tiles > 0) && !b->comp64 && b->precision == TPE_PREC_F64)
+    return fail(TPE_E_ARG, "null comp64");
+  if ((b->l_out == nullptr) != (b->g_out == nullptr)) return fail(TPE_E_ARG, "l_out and g_out go together");
+  return TPE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpe_abi_version(void) { return TPE_ABI_VERSION; }
+
+const char* tpe_last_error(void) { return g_err; }
+
+int tpe_device_count(int* n) {
+  int c = 0;
+  if (!n) return fail(TPE_E_ARG, "null out pointer");
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess || c == 0) { *n = 0; (void)hipGetLastError(); return fail(TPE_E_NODEV, "no HIP device"); }
+  *n = c;
+  return TPE_OK;
+}
+
+int tpe_tile_size(void) { return kTile; }
+
+int tpe_sample(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (!b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
+  if (b->n_tiles == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream,
+                     b->problems, b->tiles, b->samp, b->cand, b->coord, b->precision);
+  return hip_check("tpe_sample");
+}
+
+int tpe_score_above(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if ((int64_t)b->n_work_cont + b->n_work_qgauss + b->n_work_qlog == 0) return TPE_OK;
+  const int n_cont = b->n_work_cont, n_qg = b->n_work_qgauss, n_ql = b->n_work_qlog;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_cont) {
+    if (b->precision == TPE_PREC_F32)
+      hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
+                         (const float4*)b->comp32, b->coord, b->part);
+    else
+      hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
+                         (const double4*)b->comp64, b->cand, b->part);
+  }
+  if (n_qg)
+    hipLaunchKernelGGL((k_above_q<false>), dim3(n_qg), dim3(kThreads), 0, s, b->problems, b->work + n_cont,
+                       (const double4*)b->comp64, b->cand, b->part);
+  if (n_ql)
+    hipLaunchKernelGGL((k_above_q<true>), dim3(n_ql), dim3(kThreads), 0, s, b->problems, b->work + n_cont + n_qg,
+                       (const double4*)b->comp64, b->cand, b->part);
+  return hip_check("tpe_score_above");
+}
+
+int tpe_finalize(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (b->n_tiles == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
+                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->coord, b->part, b->l_out,
+                     b->g_out, b->tile_best, b->precision);
+  return hip_check("tpe_finalize");
+}
+
+int tpe_select(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (b->n_problems == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
+                     b->tile_best, b->cand, b->result);
+  return hip_check("tpe_select");
+}
+
+int tpe_run_batch(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (b->sample && (rc = tpe_sample(b, stream))) return rc;
+  if ((rc = tpe_score_above(b, stream))) return rc;
+  if ((rc = tpe_finalize(b, stream))) return rc;
+  return tpe_select(b, stream);
+}
+
+}  // extern "C"

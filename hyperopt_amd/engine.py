@@ -1,0 +1,370 @@
+"""Device engine: packs fitted posteriors into the C-ABI tables and runs them.
+
+One ``Engine.run`` call = one batched launch sequence (sample -> score ->
+select) over every (hyperparameter, new_id) *problem* of one tree level.  All
+device memory is owned here through torch tensors (torch is only the
+allocator / stream provider); the kernels are libtpe_hip.so.
+
+Device layout (HBM, all caller-owned, grow-only pools):
+  problems  tpe_problem[P]            136 B each
+  comp32    float4[K_total]           continuous families, f32 precision
+  comp64    double4[K_total]          quantized / categorical / f64 precision
+  samp      double[8][Kb_total]       below-mixture sampler rows
+  cand      double[C_total]           candidate values (returned to the user)
+  coord     float[C_total]            kernel coordinate (x or ln x) in f32
+  part      double[sum_p splits_p*C_p] above-mixture partial sums
+  tile_best tpe_best[T], result tpe_result[P]
+Mixtures are shared by every problem of the same hyperparameter (the history
+is common to all new_ids), so component tables scale with labels, not ids.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _native as N
+from . import parzen
+
+try:
+    import torch
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
+# target number of above-mixture work items per launch (>= 8 per CU on 256 CUs)
+TARGET_WORK = 2048
+MIN_COMPONENTS_PER_SPLIT = 128
+
+
+class LevelProblem(object):
+    """One hyperparameter of one tree level, active for ``ids``.
+
+    post     parzen.Posterior
+    label_ix stable label index (Philox counter word 2)
+    ids      int64 array of new_ids for which this label is active
+    inject   optional float64 [len(ids), n_cand] candidates (replay / tests)
+    """
+    __slots__ = ('post', 'label_ix', 'ids', 'inject')
+
+    def __init__(self, post, label_ix, ids, inject=None):
+        self.post, self.label_ix = post, int(label_ix)
+        self.ids = np.asarray(ids, dtype=np.int64)
+        self.inject = inject
+
+
+class Engine(object):
+    """Per-device engine.  ``precision`` is 'fp32' (default, performance) or
+    'fp64' (parity mode: float64 continuous families)."""
+
+    def __init__(self, device=None, precision='fp32'):
+        if torch is None:
+            raise N.NativeUnavailable('torch is required for device memory')
+        self.lib = N.load()
+        n = ctypes.c_int(0)
+        if self.lib.tpe_device_count(ctypes.byref(n)) != 0 or n.value == 0 or not torch.cuda.is_available():
+            raise N.NativeUnavailable('no HIP device visible: the TPE engine has no CPU fallback')
+        if device is None:
+            device = torch.device('cuda', torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.tile = self.lib.tpe_tile_size()
+        self.set_precision(precision)
+        self._bufs = {}
+        # when a dict: every run() times each stage with HIP events on the
+        # launch stream and appends (ms, CE of the launch) under the kernel name
+        self.profile = None
+
+    def set_precision(self, precision):
+        if precision not in ('fp32', 'fp64'):
+            raise ValueError("precision must be 'fp32' or 'fp64'")
+        self.precision = precision
+
+    # ------------------------------------------------------------ buffers
+    def _buf(self, name, n, dtype):
+        n = max(int(n), 1)
+        t = self._bufs.get(name)
+        if t is None or t.numel() < n or t.dtype != dtype:
+            cap = max(n, int(1.25 * (t.numel() if t is not None else 0)))
+            t = torch.empty(cap, dtype=dtype, device=self.device)
+            self._bufs[name] = t
+        return t
+
+    def _upload(self, name, arr, dtype=torch.uint8):
+        """Copy a numpy array (viewed as raw bytes) into a pooled device buffer."""
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        t = self._buf(name, raw.size, torch.uint8)
+        if raw.size:
+            t[:raw.size].copy_(torch.from_numpy(raw), non_blocking=False)
+        return t
+
+    # ------------------------------------------------------------- tables
+    def _build(self, problems, n_cand, seed, cand_base, n_cand_global):
+        """Host-side packing of one level (numpy, vectorised over ids)."""
+        f64 = self.precision == 'fp64'
+        T = self.tile
+        comp32, comp64, samp = [], [], []
+        n32 = n64 = ns = 0
+        rows = []                         # per LevelProblem: (table info)
+        for lp in problems:
+            post = lp.post
+            fam = post.family
+            info = dict(family=fam, flags=(N.F_HAS_LOW if post.low is not None else 0)
+                        | (N.F_HAS_HIGH if post.high is not None else 0),
+                        low=post.low if post.low is not None else 0.0,
+                        high=post.high if post.high is not None else 0.0,
+                        q=post.q if post.q is not None else 0.0, n_upper=post.upper)
+            st = parzen.sampler_table(post)
+            info['samp_off'], info['samp_len'] = ns, st.shape[0]
+            samp.append(st)
+            ns += st.shape[0]
+            if fam == N.FAM_CATEGORICAL:
+                for side in ('below', 'above'):
+                    p = np.asarray(getattr(post, side)[0], dtype=float)
+                    r = np.zeros((len(p), 4))
+                    with np.errstate(divide='ignore'):
+                        r[:, 0] = np.log(p)
+                    r[:, 1] = p
+                    info[side + '_off'], info[side + '_len'] = n64, len(p)
+                    info[side + '_base'] = 0.0
+                    comp64.append(r)
+                    n64 += len(p)
+            elif fam in (N.FAM_QGAUSS, N.FAM_QLOGGAUSS):
+                for side in ('below', 'above'):
+                    w, mu, sg = getattr(post, side)
+                    m, b, ww, base = parzen.quant_table(w, mu, sg, post)
+                    r = np.zeros((len(w), 4))
+                    r[:, 0], r[:, 1], r[:, 2] = m, b, ww
+                    info[side + '_off'], info[side + '_len'] = n64, len(w)
+                    info[side + '_base'] = base
+                    comp64.append(r)
+                    n64 += len(w)
+            else:
+                logf = fam == N.FAM_LOGGAUSS
+                for side in ('below', 'above'):
+                    w, mu, sg = getattr(post, side)
+                    m, a, c, base = parzen.gauss_table(w, mu, sg, post, logf)
+                    info[side + '_base'] = base
+                    if f64:
+                        r = np.zeros((len(w), 4))
+                        r[:, 0], r[:, 1], r[:, 2] = m, a, c
+                        info[side + '_off'], info[side + '_len'] = n64, len(w)
+                        comp64.append(r)
+                        n64 += len(w)
+                    else:
+                        r = np.zeros((len(w), 4), dtype=np.float32)
+                        hi = m.astype(np.float32)
+                        r[:, 0] = hi
+                        r[:, 1] = (m - hi.astype(np.float64)).astype(np.float32)
+                        r[:, 2] = a
+                        r[:, 3] = c
+                        info[side + '_off'], info[side + '_len'] = n32, len(w)
+                        comp32.append(r)
+                        n32 += len(w)
+            rows.append(info)
+
+        # problems: one row per (LevelProblem, id)
+        counts = np.array([len(lp.ids) for lp in problems], dtype=np.int64)
+        P = int(counts.sum())
+        prob = np.zeros(P, dtype=N.PROBLEM_DTYPE)
+        owner = np.repeat(np.arange(len(problems)), counts)
+        for field in ('family', 'flags', 'n_upper', 'samp_off', 'samp_len', 'below_off', 'below_len',
+                      'above_off', 'above_len', 'low', 'high', 'q', 'below_base', 'above_base'):
+            prob[field] = np.array([r[field] for r in rows])[owner] if P else 0
+        prob['n_cand'] = n_cand
+        ids = np.concatenate([lp.ids for lp in problems]) if P else np.zeros(0, np.int64)
+        prob['cand_off'] = np.arange(P, dtype=np.int64) * n_cand
+        prob['cand_base'] = cand_base
+        s64 = int(seed) & 0xFFFFFFFFFFFFFFFF
+        prob['key0'] = s64 & 0xFFFFFFFF
+        prob['key1'] = s64 >> 32
+        prob['ctr2'] = np.array([lp.label_ix for lp in problems], dtype=np.uint32)[owner] if P else 0
+        prob['ctr3'] = (ids & 0xFFFFFFFF).astype(np.uint32)
+        n_tiles_p = (n_cand + T - 1) // T if n_cand > 0 else 0
+        prob['n_tiles'] = n_tiles_p
+        prob['tile_off'] = np.arange(P, dtype=np.int64) * n_tiles_p
+
+        # splits of the above mixture: enough work items to fill the chip
+        fam = prob['family']
+        cont = (fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)
+        qg, ql = fam == N.FAM_QGAUSS, fam == N.FAM_QLOGGAUSS
+        scored = cont | qg | ql
+        # split count depends on the GLOBAL candidate count only, so every
+        # candidate sums its components in the same grouping whatever the
+        # sharding (bit-identical results for any number of GPUs)
+        C_ref = n_cand if n_cand_global is None else int(n_cand_global)
+        n_scored_tiles = int(scored.sum()) * ((C_ref + T - 1) // T)
+        target = max(1, math.ceil(TARGET_WORK / max(n_scored_tiles, 1)))
+        K = prob['above_len'].astype(np.int64)
+        splits = np.where(scored, np.clip(np.minimum(target, (K + MIN_COMPONENTS_PER_SPLIT - 1)
+                                                     // MIN_COMPONENTS_PER_SPLIT), 1, None), 0)
+        prob['n_splits'] = splits
+        part_sizes = splits * n_cand
+        prob['part_off'] = np.concatenate([[0], np.cumsum(part_sizes)[:-1]]) if P else 0
+        part_total = int(part_sizes.sum())
+
+        # tiles
+        tiles = np.zeros(P * n_tiles_p, dtype=N.TILE_DTYPE)
+        tiles['problem'] = np.repeat(np.arange(P), n_tiles_p)
+        tiles['cand_start'] = np.tile(np.arange(n_tiles_p) * T, P)
+
+        # work items, grouped [continuous | qgauss | qlog]
+        works = []
+        counts_w = []
+        for mask in (cont, qg, ql):
+            pidx = np.nonzero(mask)[0]
+            if len(pidx) == 0:
+                counts_w.append(0)
+                continue
+            sp = splits[pidx]
+            n_items = sp * n_tiles_p
+            tot = int(n_items.sum())
+            w = np.zeros(tot, dtype=N.WORK_DTYPE)
+            p_rep = np.repeat(pidx, n_items)
+            local = np.arange(tot) - np.repeat(np.cumsum(n_items) - n_items, n_items)
+            sp_rep = np.repeat(sp, n_items)
+            split = local // n_tiles_p
+            tile = local % n_tiles_p
+            k_rep = np.repeat(K[pidx], n_items)
+            w['problem'] = p_rep
+            w['split'] = split
+            w['cand_start'] = tile * T
+            w['k_start'] = (k_rep * split) // sp_rep
+            w['k_end'] = (k_rep * (split + 1)) // sp_rep
+            works.append(w)
+            counts_w.append(tot)
+        work = np.concatenate(works) if works else np.zeros(0, dtype=N.WORK_DTYPE)
+
+        return dict(prob=prob, tiles=tiles, work=work, counts_w=counts_w, part_total=part_total,
+                    comp32=np.concatenate(comp32) if comp32 else np.zeros((0, 4), np.float32),
+                    comp64=np.concatenate(comp64) if comp64 else np.zeros((0, 4)),
+                    samp=np.concatenate(samp) if samp else np.zeros((0, 8)), P=P)
+
+    # ---------------------------------------------------------------- run
+    def run(self, problems, n_cand, seed, cand_base=0, want_lg=False, return_cand=False, n_cand_global=None):
+        """Sample, score and select every problem of one level.
+
+        Returns a RESULT_DTYPE array with one row per (LevelProblem, id) in
+        order, plus (cand, l, g) float64 [P, n_cand] arrays when requested."""
+        n_cand = int(n_cand)
+        if n_cand < 0 or n_cand >= 2 ** 31:
+            raise ValueError('n_EI_candidates out of range: %r' % n_cand)
+        tb = self._build(problems, n_cand, seed, cand_base, n_cand_global)
+        P = tb['P']
+        if P == 0:
+            return np.zeros(0, dtype=N.RESULT_DTYPE)
+        C_total = P * n_cand
+        d_prob = self._upload('prob', tb['prob'])
+        d_tiles = self._upload('tiles', tb['tiles'])
+        d_work = self._upload('work', tb['work'])
+        d_c32 = self._upload('comp32', tb['comp32'])
+        d_c64 = self._upload('comp64', tb['comp64'])
+        d_samp = self._upload('samp', tb['samp'])
+        d_cand = self._buf('cand', C_total, torch.float64)
+        d_coord = self._buf('coord', C_total, torch.float32)
+        d_part = self._buf('part', tb['part_total'], torch.float64)
+        n_tiles = tb['tiles'].shape[0]
+        d_best = self._buf('best', n_tiles * 4, torch.float64)
+        d_res = self._buf('result', P * 6, torch.float64)
+        inject = any(lp.inject is not None for lp in problems)
+        if inject:
+            if not all(lp.inject is not None for lp in problems):
+                raise ValueError('either every problem of a level injects candidates or none does')
+            cand = np.concatenate([np.asarray(lp.inject, dtype=np.float64).reshape(len(lp.ids), n_cand)
+                                   for lp in problems]).reshape(-1)
+            fam = np.repeat(tb['prob']['family'], n_cand)
+            with np.errstate(divide='ignore', invalid='ignore'):
+                coord = np.where((fam == N.FAM_LOGGAUSS) | (fam == N.FAM_QLOGGAUSS), np.log(cand), cand)
+            cat = fam == N.FAM_CATEGORICAL
+            if cat.any():
+                upper = np.repeat(tb['prob']['n_upper'], n_cand)[cat]
+                cv = cand[cat]
+                if np.any((cv < 0) | (cv >= upper) | (cv != np.floor(cv))):
+                    raise IndexError('categorical candidate out of range')
+            d_cand[:C_total].copy_(torch.from_numpy(cand))
+            d_coord[:C_total].copy_(torch.from_numpy(coord.astype(np.float32)))
+        d_l = d_g = None
+        if want_lg:
+            d_l = self._buf('l_out', C_total, torch.float64)
+            d_g = self._buf('g_out', C_total, torch.float64)
+        b = N.Batch()
+        b.problems, b.n_problems = d_prob.data_ptr(), P
+        b.precision = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
+        b.sample = 0 if inject else 1
+        b.comp32, b.comp64, b.samp = d_c32.data_ptr(), d_c64.data_ptr(), d_samp.data_ptr()
+        b.cand, b.coord = d_cand.data_ptr(), d_coord.data_ptr()
+        b.tiles, b.n_tiles = d_tiles.data_ptr(), n_tiles
+        b.work = d_work.data_ptr()
+        b.n_work_cont, b.n_work_qgauss, b.n_work_qlog = tb['counts_w']
+        b.part = d_part.data_ptr()
+        b.l_out = d_l.data_ptr() if d_l is not None else None
+        b.g_out = d_g.data_ptr() if d_g is not None else None
+        b.tile_best, b.result = d_best.data_ptr(), d_res.data_ptr()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        if self.profile is None:
+            N.check(self.lib.tpe_run_batch(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, 'tpe_run_batch')
+        else:
+            self._run_profiled(b, stream, tb, n_cand)
+        res = d_res[:P * 6].cpu().numpy().view(N.RESULT_DTYPE).copy()
+        if not (want_lg or return_cand):
+            return res
+        out = [res]
+        if return_cand:
+            out.append(d_cand[:C_total].cpu().numpy().reshape(P, n_cand).copy())
+        if want_lg:
+            out.append(d_l[:C_total].cpu().numpy().reshape(P, n_cand).copy())
+            out.append(d_g[:C_total].cpu().numpy().reshape(P, n_cand).copy())
+        return tuple(out)
+
+
+    def _run_profiled(self, b, stream, tb, n_cand):
+        """The same launches as tpe_run_batch, one stage at a time, bracketed
+        by events on the launch stream (bench.py's roofline measurement)."""
+        prob = tb['prob']
+        fam = prob['family']
+        ce = (prob['above_len'].astype(np.float64) * n_cand)
+        groups = [((fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS),
+                   'k_above_f32' if self.precision == 'fp32' else 'k_above_f64'),
+                  (fam == N.FAM_QGAUSS, 'k_above_qgauss'), (fam == N.FAM_QLOGGAUSS, 'k_above_qlog')]
+        counts = list(tb['counts_w'])
+        stages = []
+        if b.sample:
+            stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
+        for gi, (mask, name) in enumerate(groups):
+            if counts[gi]:
+                stages.append((name, self.lib.tpe_score_above, gi, float(ce[mask].sum())))
+        stages.append(('k_finalize', self.lib.tpe_finalize, None, float(tb['P'] * n_cand)))
+        stages.append(('k_select', self.lib.tpe_select, None, float(tb['P'])))
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)]
+        cur = torch.cuda.current_stream(self.device)
+        evs[0].record(cur)
+        work0 = b.work
+        for i, (name, fn, gi, units) in enumerate(stages):
+            if gi is not None:
+                sub = N.Batch.from_buffer_copy(b)
+                sub.n_work_cont, sub.n_work_qgauss, sub.n_work_qlog = [c if j == gi else 0 for j, c in
+                                                                       enumerate(counts)]
+                sub.work = work0 + N.WORK_DTYPE.itemsize * sum(counts[:gi])   # this group's first item
+                N.check(fn(ctypes.byref(sub), ctypes.c_void_p(stream)), self.lib, name)
+            else:
+                N.check(fn(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, name)
+            evs[i + 1].record(cur)
+        evs[-1].synchronize()
+        for i, (name, fn, gi, units) in enumerate(stages):
+            self.profile.setdefault(name, []).append((evs[i].elapsed_time(evs[i + 1]), units))
+
+
+_ENGINES = {}
+
+
+def get_engine(device=None, precision='fp32'):
+    """Process-wide engine per device (buffers are reused across suggests)."""
+    if torch is None:
+        raise N.NativeUnavailable('torch is required for device memory')
+    if device is None:
+        if not torch.cuda.is_available():
+            raise N.NativeUnavailable('no HIP device visible: the TPE engine has no CPU fallback')
+        device = torch.device('cuda', torch.cuda.current_device())
+    key = str(device)
+    eng = _ENGINES.get(key)
+    if eng is None:
+        eng = _ENGINES[key] = Engine(device, precision)
+    eng.set_precision(precision)
+    return eng

@@ -1,0 +1,181 @@
+"""Structure-of-arrays view of a Trials history, cached incrementally.
+
+Replaces the per-call document walk of the reference — the best-doc-per-tid
+loop of tpe.py:820-842 and ``miscs_to_idxs_vals`` (base.py:108-123) — with a
+cache attached to the ``Trials`` object.  The cache is
+derivable state: it is rebuilt whenever the document list stops being an
+extension of what it saw, it is never pickled, and losses of documents that
+were not yet final are re-read on every call, so ``Trials`` stays the only
+source of truth (resume via pickled Trials keeps working).
+
+Fast path requirements (else the generic reference-order walk is used):
+documents in increasing tid order, unique tids, no ``misc['from_tid']``,
+and ``Domain.loss`` not overridden.
+"""
+import weakref
+
+import numpy as np
+
+from . import base
+
+_CACHES = weakref.WeakKeyDictionary()
+
+
+class History(object):
+    """tids (int64, ascending), losses (float64, +inf for missing), and per
+    label the (tid, value) observations in tid order."""
+    __slots__ = ('tids', 'losses', 'obs')
+
+    def __init__(self, tids, losses, obs):
+        self.tids, self.losses, self.obs = tids, losses, obs
+
+    def __len__(self):
+        return len(self.tids)
+
+
+class _Grow(object):
+    __slots__ = ('a', 'n')
+
+    def __init__(self, dtype):
+        self.a = np.empty(64, dtype=dtype)
+        self.n = 0
+
+    def append(self, v):
+        if self.n == self.a.shape[0]:
+            self.a = np.concatenate([self.a, np.empty_like(self.a)])
+        self.a[self.n] = v
+        self.n += 1
+
+    def view(self):
+        return self.a[:self.n]
+
+
+class _Cache(object):
+    def __init__(self, labels, categorical):
+        self.docs = []                 # document objects in list order
+        self.tids = _Grow(np.int64)
+        self.losses = _Grow(np.float64)
+        self.pending = []              # positions whose loss may still change
+        self.obs_pos = {k: _Grow(np.int64) for k in labels}
+        self.obs_val = {k: _Grow(np.int64 if categorical[k] else np.float64) for k in labels}
+        self.labels = labels
+        self.ok = True                 # fast path still valid
+
+    def extend(self, docs, start):
+        for i in range(start, len(docs)):
+            d = docs[i]
+            misc = d['misc']
+            if 'from_tid' in misc:
+                self.ok = False
+                return
+            tid = d['tid']
+            if self.tids.n and tid <= self.tids.a[self.tids.n - 1]:
+                self.ok = False
+                return
+            self.docs.append(d)
+            self.tids.append(tid)
+            loss = d['result'].get('loss')
+            final = d['state'] == base.JOB_STATE_DONE and loss is not None
+            self.losses.append(np.inf if loss is None else float(loss))
+            if not final:
+                self.pending.append(self.tids.n - 1)
+            vals = misc['vals']
+            for k in self.labels:
+                v = vals.get(k)
+                if v:
+                    self.obs_pos[k].append(self.tids.n - 1)
+                    self.obs_val[k].append(v[0])
+
+    def refresh_pending(self):
+        if not self.pending:
+            return
+        keep = []
+        L = self.losses.a
+        for i in self.pending:
+            d = self.docs[i]
+            loss = d['result'].get('loss')
+            L[i] = np.inf if loss is None else float(loss)
+            if not (d['state'] == base.JOB_STATE_DONE and loss is not None):
+                keep.append(i)
+        self.pending = keep
+
+
+def _generic(domain, docs, table):
+    """Reference-order walk (tpe.py:820-842 + base.py:108-123)."""
+    best_loss, best_doc = {}, {}
+    for doc in docs:
+        tid = doc['misc'].get('from_tid', doc['tid'])
+        loss = domain.loss(doc['result'], doc['spec'])
+        loss = float('inf') if loss is None else float(loss)
+        best_loss.setdefault(tid, loss)
+        if loss <= best_loss[tid]:
+            best_loss[tid] = loss
+            best_doc[tid] = doc
+    tids = sorted(best_doc)
+    losses = np.array([best_loss[t] for t in tids], dtype=np.float64)
+    obs = {}
+    for r in table.rows:
+        ot, ov = [], []
+        for t in tids:
+            misc = best_doc[t]['misc']
+            v = misc['vals'][r.label]
+            i = misc['idxs'][r.label]
+            assert len(i) == len(v) and (i == [] or i == [misc['tid']])
+            if v:
+                ot.append(i[0])
+                ov.append(v[0])
+        obs[r.label] = (np.array(ot, dtype=np.int64),
+                        np.array(ov, dtype=np.int64 if r.categorical else np.float64))
+    return History(np.array(tids, dtype=np.int64), losses, obs)
+
+
+def extract(domain, trials):
+    """History of ``trials`` for ``domain``'s parameters."""
+    docs = trials.trials
+    table = domain.table
+    if type(domain).loss is not base.Domain.loss:
+        return _generic(domain, docs, table)
+    cache = _CACHES.get(trials)
+    labels = table.labels
+    if cache is not None and (cache.labels != labels or not cache.ok):
+        cache = None
+    if cache is not None:
+        n = len(cache.docs)
+        if n > len(docs) or (n and (docs[0] is not cache.docs[0] or docs[n - 1] is not cache.docs[n - 1])):
+            cache = None
+    if cache is None:
+        cache = _Cache(labels, {r.label: r.categorical for r in table.rows})
+        start = 0
+    else:
+        start = len(cache.docs)
+    cache.extend(docs, start)
+    if not cache.ok:
+        _CACHES.pop(trials, None)
+        return _generic(domain, docs, table)
+    _CACHES[trials] = cache
+    cache.refresh_pending()
+    tids = cache.tids.view()
+    obs = {}
+    for k in labels:
+        pos = cache.obs_pos[k].view()
+        obs[k] = (tids[pos], cache.obs_val[k].view())
+    return History(tids, cache.losses.view(), obs)
+
+
+def split_below(history, gamma, gamma_cap=25):
+    """Tids of the ``n_below`` best losses (ap_filter_trials, tpe.py:625-629).
+
+    ``np.argsort`` on the same float64 loss array as the reference gives the
+    same order, including among tied losses."""
+    n = len(history.losses)
+    n_below = min(int(np.ceil(gamma * np.sqrt(n))), gamma_cap)
+    order = np.argsort(history.losses)
+    return history.tids[order[:n_below]]
+
+
+def below_mask(obs_tids, below_tids):
+    """Membership of each observation in the below set, in tid order
+    (tpe.py:629-636)."""
+    if len(below_tids) == 0 or len(obs_tids) == 0:
+        return np.zeros(len(obs_tids), dtype=bool)
+    return np.isin(obs_tids, below_tids)

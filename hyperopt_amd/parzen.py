@@ -1,0 +1,255 @@
+"""Host-side Parzen estimator and posterior construction.
+
+The fit stays on the host in float64 numpy because it must reproduce the
+reference's ``np.argsort`` permutation exactly (tie order among duplicate
+observations changes the mixture, SURVEY.md §7 "Tie semantics"); calling the
+same numpy routine on the same array is the only way to get that permutation.
+The O(C*K) work it feeds runs on the GPU (``engine``).
+
+References (gsmafra/hyperopt, /root/reference):
+  linear_forgetting_weights  tpe.py:381-394
+  adaptive_parzen_normal     tpe.py:398-475
+  adaptive_parzen_samplers   tpe.py:485-607
+  normal_cdf                 tpe.py:96-101 (p_accept, tpe.py:130-136)
+"""
+import math
+
+import numpy as np
+from scipy.special import erf
+
+from . import _native as N
+
+EPS = 1e-12
+DEFAULT_LF = 25
+
+
+def linear_forgetting_weights(n, lf):
+    """Oldest observations (tid order) get a linear ramp from 1/n, the newest
+    ``lf`` weigh 1 (tpe.py:381-394)."""
+    if n == 0:
+        return np.zeros(0)
+    if n < lf:
+        return np.ones(n)
+    return np.concatenate([np.linspace(1.0 / n, 1.0, num=n - lf), np.ones(lf)])
+
+
+def fit_parzen(obs, prior_weight, prior_mu, prior_sigma, lf=DEFAULT_LF):
+    """Adaptive Parzen mixture (w, mu, sigma), mu sorted ascending.
+
+    Same semantics and float64 operation order as tpe.py:398-475: the prior is
+    inserted at ``searchsorted`` (left) among the sorted observations, each
+    bandwidth is the larger neighbour gap (one-sided at the ends), bandwidths
+    are clipped to [prior_sigma / min(100, 1 + K), prior_sigma], the prior keeps
+    prior_sigma, and linear-forgetting weights follow the observations through
+    the sort."""
+    obs = np.array(obs, dtype=float)
+    n = obs.shape[0]
+    if n == 0:
+        mu = np.array([prior_mu], dtype=float)
+        sigma = np.array([prior_sigma], dtype=float)
+        pos = 0
+        order = None
+    elif n == 1:
+        order = None
+        if prior_mu < obs[0]:
+            pos, mu = 0, np.array([prior_mu, obs[0]])
+            sigma = np.array([prior_sigma, prior_sigma * .5])
+        else:
+            pos, mu = 1, np.array([obs[0], prior_mu])
+            sigma = np.array([prior_sigma * .5, prior_sigma])
+    else:
+        order = np.argsort(obs)
+        srt = obs[order]
+        pos = int(np.searchsorted(srt, prior_mu))
+        mu = np.empty(n + 1)
+        mu[:pos] = srt[:pos]
+        mu[pos] = prior_mu
+        mu[pos + 1:] = srt[pos:]
+        sigma = np.empty(n + 1)
+        sigma[1:-1] = np.maximum(mu[1:-1] - mu[:-2], mu[2:] - mu[1:-1])
+        sigma[0] = mu[1] - mu[0]
+        sigma[-1] = mu[-1] - mu[-2]
+    if lf and lf < n:
+        ramp = linear_forgetting_weights(n, lf)[order]
+        w = np.empty(n + 1)
+        w[:pos] = ramp[:pos]
+        w[pos] = prior_weight
+        w[pos + 1:] = ramp[pos:]
+    else:
+        w = np.ones(len(mu))
+        w[pos] = prior_weight
+    lo = prior_sigma / min(100.0, 1.0 + len(mu))
+    sigma = np.clip(sigma, lo, prior_sigma / 1.0)
+    sigma[pos] = prior_sigma
+    if not np.all(sigma > 0):
+        raise AssertionError('non-positive Parzen bandwidth (prior_sigma=%r)' % prior_sigma)
+    w /= w.sum()
+    return w, mu, sigma
+
+
+def normal_cdf(x, mu, sigma):
+    """0.5 * (1 + erf((x - mu) / max(sqrt2 sigma, EPS))) — tpe.py:96-101."""
+    return 0.5 * (1 + erf((x - mu) / np.maximum(np.sqrt(2) * sigma, EPS)))
+
+
+def p_accept(w, mu, sigma, low, high):
+    """Mixture mass inside [low, high) (tpe.py:130-136); 1 when unbounded."""
+    if low is None and high is None:
+        return 1
+    return np.sum(w * (normal_cdf(high, mu, sigma) - normal_cdf(low, mu, sigma)))
+
+
+# --------------------------------------------------------------------------
+# posterior families (adaptive_parzen_samplers, tpe.py:485-607)
+# --------------------------------------------------------------------------
+
+_FAMILY = {
+    'uniform': N.FAM_GAUSS, 'normal': N.FAM_GAUSS,
+    'quniform': N.FAM_QGAUSS, 'qnormal': N.FAM_QGAUSS,
+    'loguniform': N.FAM_LOGGAUSS, 'lognormal': N.FAM_LOGGAUSS,
+    'qloguniform': N.FAM_QLOGGAUSS, 'qlognormal': N.FAM_QLOGGAUSS,
+    'randint': N.FAM_CATEGORICAL, 'categorical': N.FAM_CATEGORICAL,
+}
+
+
+class Posterior(object):
+    """A fitted below/above pair for one hyperparameter.
+
+    family      engine family (``_native.FAM_*``)
+    low, high   truncation in sampling space (log space for LGMM1), or None
+    q           quantum or None
+    below/above (w, mu, sigma) float64 arrays, or (p,) for categorical
+    upper       number of categories (categorical)
+    """
+    __slots__ = ('dist', 'family', 'low', 'high', 'q', 'below', 'above', 'upper')
+
+    def __init__(self, dist, family, low, high, q, below, above, upper=0):
+        self.dist, self.family = dist, family
+        self.low, self.high, self.q = low, high, q
+        self.below, self.above, self.upper = below, above, upper
+
+    @property
+    def bounded(self):
+        return self.low is not None or self.high is not None
+
+
+def _cat_probs(dist, args, obs, prior_weight, lf):
+    upper = int(args['upper'])
+    lfw = linear_forgetting_weights(len(obs), lf)
+    if len(obs):
+        counts = np.bincount(np.asarray(obs, dtype=np.int64), lfw, upper)
+    else:
+        counts = np.zeros(upper, dtype='int')
+    if dist == 'randint':                                   # tpe.py:573-581
+        pseudo = counts + prior_weight
+    else:                                                   # tpe.py:590-607
+        pseudo = counts + upper * (prior_weight * np.asarray(args['p'], dtype=float))
+    return pseudo / np.sum(pseudo)
+
+
+def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT_LF):
+    """Fit the below and above posteriors of one hyperparameter."""
+    family = _FAMILY[dist]
+    a = args
+    if family == N.FAM_CATEGORICAL:
+        return Posterior(dist, family, None, None, None,
+                         (_cat_probs(dist, a, below_obs, prior_weight, lf),),
+                         (_cat_probs(dist, a, above_obs, prior_weight, lf),), int(a['upper']))
+    low = high = None
+    if dist in ('uniform', 'quniform', 'loguniform', 'qloguniform'):
+        low, high = float(a['low']), float(a['high'])
+        pmu, psig = 0.5 * (a['high'] + a['low']), 1.0 * (a['high'] - a['low'])
+    else:
+        pmu, psig = a['mu'], a['sigma']
+    q = a.get('q')
+    q = None if q is None else float(q)
+
+    def tr(obs):
+        obs = np.asarray(obs, dtype=float)
+        if dist in ('loguniform', 'lognormal'):
+            return np.log(obs)
+        if dist == 'qloguniform':                          # tpe.py:523-532
+            return np.log(np.maximum(obs, np.maximum(EPS, np.exp(a['low']))))
+        if dist == 'qlognormal':                           # tpe.py:564
+            return np.log(np.maximum(obs, EPS))
+        return obs
+
+    below = fit_parzen(tr(below_obs), prior_weight, pmu, psig, lf)
+    above = fit_parzen(tr(above_obs), prior_weight, pmu, psig, lf)
+    return Posterior(dist, family, low, high, q, below, above)
+
+
+# --------------------------------------------------------------------------
+# device tables (layout documented in include/tpe_hip.h)
+# --------------------------------------------------------------------------
+
+LOG2E = 1.0 / math.log(2.0)
+A_SCALE = math.sqrt(0.5 * LOG2E)
+
+
+def gauss_table(w, mu, sigma, post, log_family):
+    """Rows {mu, a, c} and the additive base of one continuous mixture.
+
+    GMM1_lpdf  (tpe.py:138-144): log coef = log(w / sqrt(2 pi sigma^2) / p_accept)
+    LGMM1_lpdf (tpe.py:278-281): log coef = log w - log(max(sigma,EPS) sqrt(2 pi))
+                                 (ln x subtracted per candidate; no p_accept)
+    In log2 units: term_k(t) = c_k - (a_k (t - mu_k))^2 with
+    a_k = sqrt(log2(e)/2) / max(sigma_k, EPS); c is shifted so max_k c_k = 0
+    and lpdf = ln2 * log2(sum_k 2^term_k) + base."""
+    se = np.maximum(sigma, EPS)
+    with np.errstate(divide='ignore'):
+        if log_family:
+            logcoef = np.log(w) - np.log(se * np.sqrt(2 * np.pi))
+        else:
+            pa = p_accept(w, mu, sigma, post.low, post.high)
+            logcoef = np.log(w / np.sqrt(2 * np.pi * sigma ** 2) / pa)
+    c = logcoef * LOG2E
+    finite = np.isfinite(c)
+    shift = float(np.max(c[finite])) if finite.any() else 0.0
+    return mu, A_SCALE / se, c - shift, shift * math.log(2.0)
+
+
+def quant_table(w, mu, sigma, post):
+    """Rows {mu, b = max(sqrt2 sigma, EPS), w} and base = -log(p_accept)
+    (tpe.py:145-160, :282-299)."""
+    pa = p_accept(w, mu, sigma, post.low, post.high)
+    with np.errstate(divide='ignore'):
+        base = -float(np.log(pa))
+    return mu, np.maximum(np.sqrt(2) * sigma, EPS), w, base
+
+
+def sampler_table(post):
+    """Below-mixture sampler rows {cum, mu, sigma, za, zb}.
+
+    Bounded GMM1/LGMM1 draw by rejection (tpe.py:82-87): a component with
+    probability w_k, a normal draw, accepted if low <= x < high.  Accepted
+    draws are exactly: component k with probability ∝ w_k * mass_k, then a
+    normal truncated to [low, high) — which the device samples directly."""
+    if post.family == N.FAM_CATEGORICAL:
+        p = np.asarray(post.below[0], dtype=float)
+        rows = np.zeros((len(p), 8))
+        cum = np.cumsum(p) / np.sum(p)
+        cum[-1] = 1.0
+        rows[:, 0] = cum
+        return rows
+    w, mu, sigma = post.below
+    rows = np.zeros((len(w), 8))
+    rows[:, 1] = mu
+    rows[:, 2] = sigma
+    if post.low is None and post.high is None:
+        sel = np.asarray(w, dtype=float)
+        rows[:, 3] = -np.inf
+        rows[:, 4] = np.inf
+    else:
+        za = (post.low - mu) / sigma
+        zb = (post.high - mu) / sigma
+        mass = 0.5 * (erf(zb / np.sqrt(2)) - erf(za / np.sqrt(2)))
+        sel = w * np.maximum(mass, 0.0)
+        if not np.any(sel > 0):          # all components outside the bounds
+            sel = np.asarray(w, dtype=float)
+        rows[:, 3] = za
+        rows[:, 4] = zb
+    cum = np.cumsum(sel) / np.sum(sel)
+    cum[-1] = 1.0
+    rows[:, 0] = cum
+    return rows

@@ -1,0 +1,188 @@
+"""Tree-structured Parzen Estimator suggest — MI355X engine behind the
+reference's algorithm-plugin contract.
+
+``suggest(new_ids, domain, trials, seed, prior_weight, n_startup_jobs,
+n_EI_candidates, gamma, linear_forgetting)`` keeps the signature, defaults and
+return value of the reference (tpe.py:762-772, 804-897): a list of new trial
+documents, one per new id, with ``misc['idxs']/misc['vals']`` set for the
+active hyperparameters.  ``fmin(algo=tpe.suggest)`` and
+``functools.partial(tpe.suggest, n_EI_candidates=...)`` work unchanged.
+
+Per call (the reference rebuilds and interprets a pyll posterior graph,
+tpe.py:814-881; here):
+  1. SoA history from the Trials cache (history.py)          tpe.py:820-842
+  2. below set = the n_below best losses                     tpe.py:613-641
+  3. Parzen fit of below/above per active hyperparameter     tpe.py:398-607
+  4. per tree level, ONE batched device launch sequence over every
+     (hyperparameter, new_id): sample C candidates from the below mixture,
+     score l(x) - g(x), argmax                                tpe.py:62-301, 749-759
+  5. trial documents                                          tpe.py:884-897
+
+Extensions over the reference (keyword-only, defaults keep its behaviour):
+  * ``len(new_ids) > 1``: one batched suggest (the reference asserts a single
+    id).  Id j draws from Philox stream (seed, label, new_id j), so a batched
+    call returns exactly what single-id calls with the same seed return.
+  * ``sampler``: 'philox' (device sampling, default) or 'replay' (the
+    reference's RandomState draws on the host, for exact trajectory parity).
+  * ``precision``: 'fp32' (default) or 'fp64' for the continuous families.
+  * ``shard=(rank, world)``: split every problem's candidates over ranks of
+    the default ``torch.distributed`` group (see dist.py).
+
+``linear_forgetting`` is accepted and, as in the reference, not used: the
+forgetting window is fixed at DEFAULT_LF=25 (tpe.py:27-29).
+"""
+import logging
+import time
+
+import numpy as np
+
+from . import _native as N
+from . import dist as _dist
+from . import history as _history
+from . import rand
+from . import replay
+from .engine import LevelProblem, get_engine
+from .parzen import DEFAULT_LF, fit_posterior
+
+logger = logging.getLogger(__name__)
+
+_default_prior_weight = 1.0
+_default_n_EI_candidates = 24
+_default_gamma = 0.25
+_default_n_startup_jobs = 20
+_default_linear_forgetting = DEFAULT_LF
+
+
+class _Fits(object):
+    """Lazily fitted posteriors of one suggest call (inactive labels are never fitted)."""
+
+    def __init__(self, table, hist, below_tids, prior_weight):
+        self.table, self.hist = table, hist
+        self.below_tids, self.prior_weight = below_tids, prior_weight
+        self.cache = {}
+
+    def get(self, row):
+        post = self.cache.get(row.label)
+        if post is None:
+            otids, ovals = self.hist.obs[row.label]
+            m = _history.below_mask(otids, self.below_tids)
+            post = fit_posterior(row.dist, row.args, ovals[m], ovals[~m], self.prior_weight, DEFAULT_LF)
+            self.cache[row.label] = post
+        return post
+
+
+def _value(row, v):
+    """Reference value types: np.int64 for categorical draws, np.float64 else."""
+    return np.int64(int(v)) if row.categorical else np.float64(v)
+
+
+def _run(engine, problems, C, seed, shard):
+    if shard is None:
+        return engine.run(problems, C, seed)
+    rank, world = shard
+    lo, hi = _dist.shard_range(C, rank, world)
+    res = engine.run(problems, hi - lo, seed, cand_base=lo, n_cand_global=C)
+    return _dist.allgather_results(res, device=engine.device)
+
+
+def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
+    ids = np.asarray(new_ids, dtype=np.int64)
+    chosen = [dict() for _ in new_ids]
+    for level in table.levels():
+        problems, rows, members = [], [], []
+        for row in level:
+            act = [i for i, c in enumerate(chosen) if table.active(row, c)]
+            for i, c in enumerate(chosen):
+                c.setdefault(row.label, None)
+            if not act:
+                continue
+            problems.append(LevelProblem(fits.get(row), row.index, ids[act]))
+            rows.append(row)
+            members.append(act)
+        if not problems:
+            continue
+        res = _run(engine, problems, C, seed, shard)
+        k = 0
+        for row, act in zip(rows, members):
+            for i in act:
+                r = res[k]
+                k += 1
+                if r['idx'] < 0:
+                    raise RuntimeError('no candidate selected for %r' % row.label)
+                chosen[i][row.label] = _value(row, r['value'])
+    return chosen
+
+
+def _choices_replay(table, fits, new_ids, seed, C, engine):
+    """Reference RandomState order: labels descending, ancestors first.  Draws
+    are made on the host in that order; a label whose parent is drawn but not
+    yet scored forces a device flush of the pending draws first."""
+    rng = np.random.RandomState(seed)
+    out = []
+    for new_id in new_ids:
+        chosen, pending, pending_labels = {}, [], set()
+
+        def flush():
+            if not pending:
+                return
+            problems = [LevelProblem(fits.get(row), row.index, [new_id], inject=cand[None, :])
+                        for row, cand in pending]
+            res = engine.run(problems, C, seed)
+            for (row, cand), r in zip(pending, res):
+                chosen[row.label] = cand[int(r['idx'])]
+            del pending[:]
+            pending_labels.clear()
+
+        for row in table.rng_order():
+            if any(p is not None and p[0] in pending_labels for p in row.parents):
+                flush()
+            if table.active(row, chosen):
+                pending.append((row, replay.draw(rng, fits.get(row), C)))
+                pending_labels.add(row.label)
+            else:
+                chosen[row.label] = None
+        flush()
+        out.append(dict((k, (None if v is None else _value(table.by_label[k], v))) for k, v in chosen.items()))
+    return out
+
+
+def suggest(new_ids, domain, trials, seed,
+            prior_weight=_default_prior_weight,
+            n_startup_jobs=_default_n_startup_jobs,
+            n_EI_candidates=_default_n_EI_candidates,
+            gamma=_default_gamma,
+            linear_forgetting=_default_linear_forgetting,
+            sampler='philox', precision='fp32', device=None, shard=None):
+    new_ids = list(new_ids)
+    if not new_ids:
+        return []
+    t0 = time.time()
+    hist = _history.extract(domain, trials)
+    if len(hist):
+        logger.info('TPE using %i/%i trials with best loss %f' % (len(hist), len(trials), float(np.min(hist.losses))))
+    else:
+        logger.info('TPE using 0 trials')
+    if len(hist) < n_startup_jobs:
+        return rand.suggest(new_ids, domain, trials, seed)
+    if sampler not in ('philox', 'replay'):
+        raise ValueError("sampler must be 'philox' or 'replay'")
+    engine = get_engine(device, precision)
+    table = domain.table
+    fits = _Fits(table, hist, _history.split_below(hist, gamma), prior_weight)
+    C = int(n_EI_candidates)
+    if sampler == 'philox':
+        choices = _choices_philox(table, fits, new_ids, seed, C, engine, shard)
+    else:
+        if shard is not None:
+            raise ValueError("sampler='replay' draws on the host; it does not shard")
+        choices = _choices_replay(table, fits, new_ids, seed, C, engine)
+    logger.info('tpe.suggest took %f seconds' % (time.time() - t0))
+    return rand.docs_from_choices(new_ids, domain, trials, choices)
+
+
+def suggest_replay(new_ids, domain, trials, seed, **kw):
+    """``suggest`` in exact-parity mode: the reference's RandomState candidate
+    draws and float64 scoring (trajectories identical to the reference)."""
+    kw.setdefault('sampler', 'replay')
+    kw.setdefault('precision', 'fp64')
+    return suggest(new_ids, domain, trials, seed, **kw)

@@ -1,0 +1,176 @@
+/*
+ * tpe_hip.h — C-ABI of the MI355X TPE suggest engine (libtpe_hip.so).
+ *
+ * This boundary replaces the numpy operators that gsmafra/hyperopt evaluates
+ * through its pyll interpreter on every tpe.suggest call (reference file:line
+ * below).  Plain C types only: device pointers, sizes, an opaque hipStream_t.
+ * No allocation, no host synchronisation and no C++ exception crosses it; every
+ * entry point returns 0 on success or a negative TPE_E* code, and
+ * tpe_last_error() gives a thread-local message.
+ *
+ * One tpe_run_batch() call evaluates a *batch of problems*.  A problem is one
+ * (new_id, hyperparameter) pair of one tree level — the unit the reference
+ * handles per parameter in build_posterior (tpe.py:663-701):
+ *
+ *   sample  C candidates from the "below" Parzen mixture     GMM1 / LGMM1 (tpe.py:62-93, 216-250),
+ *                                                           categorical (pyll/stochastic.py:104-142)
+ *   score   l(x) = lpdf_below(x),  g(x) = lpdf_above(x)      GMM1_lpdf (tpe.py:104-166),
+ *                                                           LGMM1_lpdf (tpe.py:259-301),
+ *                                                           categorical_lpdf (tpe.py:50-57)
+ *   select  argmax_x  l(x) - g(x), first index on ties      broadcast_best (tpe.py:749-759)
+ *
+ * The Parzen fit (adaptive_parzen_normal, tpe.py:398-475) and the below/above
+ * split (ap_filter_trials, tpe.py:613-641) are done by the caller, which
+ * uploads the fitted mixtures as the component tables described below.
+ */
+#ifndef TPE_HIP_H
+#define TPE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPE_ABI_VERSION 1
+
+/* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
+enum {
+  TPE_FAM_GAUSS = 0,       /* GMM1_lpdf, q=None   (uniform, normal)            */
+  TPE_FAM_LOGGAUSS = 1,    /* LGMM1_lpdf, q=None  (loguniform, lognormal)      */
+  TPE_FAM_QGAUSS = 2,      /* GMM1_lpdf, q        (quniform, qnormal)          */
+  TPE_FAM_QLOGGAUSS = 3,   /* LGMM1_lpdf, q       (qloguniform, qlognormal)    */
+  TPE_FAM_CATEGORICAL = 4  /* categorical_lpdf    (randint, choice, pchoice)   */
+};
+
+/* problem flags */
+enum {
+  TPE_F_HAS_LOW = 1,   /* low bound present (reference: low is not None)   */
+  TPE_F_HAS_HIGH = 2   /* high bound present                                */
+};
+
+/* precision of the continuous (non-quantized) families; quantized families
+ * always evaluate the mixture mass in float64 (cancellation of Phi(ub)-Phi(lb)) */
+enum { TPE_PREC_F32 = 0, TPE_PREC_F64 = 1 };
+
+/* error codes */
+enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3 };
+
+/*
+ * One problem (136 bytes).  Component tables (device, caller-owned):
+ *   comp32[k] = float4 {mu_hi, mu_lo, a, c}      families 0/1 at TPE_PREC_F32
+ *   comp64[k] = double4 {mu, a, c, 0}            families 0/1 at TPE_PREC_F64
+ *   comp64[k] = double4 {mu, b, w, 0}            families 2/3 (b = max(sqrt2*sigma, EPS))
+ *   comp64[k] = double4 {log p_k, p_k, 0, 0}     family 4
+ * For families 0/1 the mixture log-density is
+ *   lpdf(x) = ln2 * log2( sum_k 2^(c_k - (a_k * (t - mu_k))^2) ) + base  [- ln x for LOGGAUSS]
+ * with t = x (GAUSS) or ln x (LOGGAUSS); the host folds weights, 1/Z,
+ * p_accept and a per-mixture shift (max_k c_k = 0) into c_k and base.
+ * Families 2/3:  lpdf(x) = ln( sum_k w_k Phi(zu_k) - w_k Phi(zl_k) ) + base.
+ * samp[k] = double[8] {cum, mu, sigma, za, zb, 0, 0, 0}: below-mixture sampler
+ * table, cum = selection CDF (∝ w_k * mass_k when bounded), za/zb = truncation
+ * bounds standardised per component (±inf when unbounded); family 4 uses cum only.
+ */
+typedef struct tpe_problem {
+  int32_t family, flags;
+  int32_t n_cand;        /* candidates of this problem on this device          */
+  int32_t n_upper;       /* categorical: number of categories                  */
+  int64_t cand_off;      /* element offset into cand / coord / l_out / g_out   */
+  int64_t cand_base;     /* global index of local candidate 0 (shards, RNG)    */
+  int64_t part_off;      /* element offset into part                           */
+  int32_t n_splits;      /* component splits of the above mixture              */
+  int32_t tile_off;      /* first candidate tile of this problem               */
+  int32_t n_tiles;       /* candidate tiles of this problem                    */
+  int32_t samp_off;
+  int32_t samp_len;
+  int32_t below_off;
+  int32_t below_len;
+  int32_t above_off;
+  int32_t above_len;
+  int32_t reserved;
+  double low, high, q;   /* bounds in sampling space (log space for LGMM1)     */
+  double below_base;     /* additive constant of the below lpdf                */
+  double above_base;     /* additive constant of the above lpdf                */
+  uint32_t key0, key1;   /* Philox-4x32-10 key (suggest seed)                  */
+  uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
+} tpe_problem;
+
+/* candidate tile: 2048 consecutive candidates of one problem */
+typedef struct tpe_tile {
+  int32_t problem;
+  int32_t cand_start;
+} tpe_tile;
+
+/* above-mixture work item: one candidate tile x one component range */
+typedef struct tpe_work {
+  int32_t problem;
+  int32_t split;
+  int32_t cand_start;
+  int32_t k_start;
+  int32_t k_end;
+  int32_t reserved;
+} tpe_work;
+
+/* per-tile best, written by the finalize stage */
+typedef struct tpe_best {
+  double score, l, g;
+  int64_t idx;           /* local candidate index, -1 if none */
+} tpe_best;
+
+/* per-problem result */
+typedef struct tpe_result {
+  double score, l, g;
+  double value;          /* the chosen candidate                               */
+  int64_t idx;           /* local candidate index, -1 if the problem is empty  */
+  int64_t global_idx;    /* cand_base + idx                                     */
+} tpe_result;
+
+/* all device pointers of one batch (the struct itself lives in host memory) */
+typedef struct tpe_batch {
+  const tpe_problem* problems; int32_t n_problems;
+  int32_t precision;     /* TPE_PREC_F32 | TPE_PREC_F64                         */
+  int32_t sample;        /* 1: draw candidates on device (Philox); 0: caller filled cand/coord */
+  int32_t reserved;
+  const float* comp32;   /* [n][4]                                             */
+  const double* comp64;  /* [n][4]                                             */
+  const double* samp;    /* [n][8]                                             */
+  double* cand;          /* [total_cand] candidate values (returned to the user) */
+  float* coord;          /* [total_cand] kernel coordinate t in f32 (x or ln x) */
+  const tpe_tile* tiles; int32_t n_tiles; int32_t reserved2;
+  /* above-mixture work list, ordered [continuous | quantized Gauss | quantized log] */
+  const tpe_work* work;
+  int32_t n_work_cont, n_work_qgauss, n_work_qlog, reserved3;
+  double* part;          /* above-mixture partial sums                          */
+  double* l_out;         /* optional [total_cand]; NULL to skip                 */
+  double* g_out;         /* optional [total_cand]; NULL to skip                 */
+  tpe_best* tile_best;   /* [n_tiles]                                          */
+  tpe_result* result;    /* [n_problems]                                       */
+} tpe_batch;
+
+/* ABI version (TPE_ABI_VERSION) of the loaded library */
+int tpe_abi_version(void);
+
+/* thread-local message of the last failing call on this thread ("" if none) */
+const char* tpe_last_error(void);
+
+/* number of visible HIP devices (0 and TPE_E_NODEV when none) */
+int tpe_device_count(int* n);
+
+/* candidates per tile (2048) — the caller sizes tiles / work items with it */
+int tpe_tile_size(void);
+
+/* sample (optional) -> score -> select, enqueued on `stream` (hipStream_t);
+ * asynchronous: results are valid once the stream reaches this point. */
+int tpe_run_batch(const tpe_batch* batch, void* stream);
+
+/* the stages one by one (same semantics; used by tests and the profiler) */
+int tpe_sample(const tpe_batch* batch, void* stream);
+int tpe_score_above(const tpe_batch* batch, void* stream);
+int tpe_finalize(const tpe_batch* batch, void* stream);
+int tpe_select(const tpe_batch* batch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TPE_HIP_H */

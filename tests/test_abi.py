@@ -1,0 +1,102 @@
+"""C-ABI checks that need no GPU: the library loads, exports every function
+include/tpe_hip.h declares, and the Python mirrors of the C structs have the
+C compiler's layout (sizes and field offsets)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from hyperopt_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'tpe_hip.h')
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return re.findall(r'^\s*(?:const\s+)?\w+\s*\*?\s*(tpe_\w+)\s*\(', src, flags=re.M)
+
+
+def test_header_declares_bindings():
+    assert set(declared_functions()) == set(N.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    lib = N.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.tpe_abi_version() == N.ABI_VERSION
+    assert lib.tpe_tile_size() == 2048
+    n = ctypes.c_int(-1)
+    rc = lib.tpe_device_count(ctypes.byref(n))
+    assert rc in (0, -3) and n.value >= 0
+
+
+def test_null_batch_is_rejected_without_gpu():
+    lib = N.load()
+    assert lib.tpe_run_batch(None, None) == -1
+    assert b'null batch' in lib.tpe_last_error()
+    b = N.Batch()
+    b.n_problems = -1
+    assert lib.tpe_run_batch(ctypes.byref(b), None) == -1
+
+
+def _c_layout():
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "tpe_hip.h"
+#define F(T, f) printf("%s.%s %zu\n", #T, #f, offsetof(T, f));
+int main(void) {
+  printf("tpe_problem %zu\ntpe_tile %zu\ntpe_work %zu\ntpe_best %zu\ntpe_result %zu\ntpe_batch %zu\n",
+         sizeof(tpe_problem), sizeof(tpe_tile), sizeof(tpe_work), sizeof(tpe_best), sizeof(tpe_result),
+         sizeof(tpe_batch));
+  F(tpe_problem, cand_off) F(tpe_problem, part_off) F(tpe_problem, n_splits) F(tpe_problem, above_len)
+  F(tpe_problem, low) F(tpe_problem, above_base) F(tpe_problem, key0) F(tpe_problem, ctr3)
+  F(tpe_batch, comp32) F(tpe_batch, tiles) F(tpe_batch, n_tiles) F(tpe_batch, work) F(tpe_batch, n_work_qlog)
+  F(tpe_batch, part) F(tpe_batch, result)
+  F(tpe_result, value) F(tpe_result, global_idx)
+  return 0;
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, 'l.c')
+        open(c, 'w').write(prog)
+        exe = os.path.join(d, 'l')
+        subprocess.check_call(['gcc', '-I', os.path.dirname(HEADER), c, '-o', exe])
+        out = subprocess.check_output([exe]).decode()
+    return dict((line.split()[0], int(line.split()[1])) for line in out.strip().splitlines())
+
+
+def test_struct_layout_matches_c():
+    lay = _c_layout()
+    assert lay['tpe_problem'] == N.PROBLEM_DTYPE.itemsize
+    assert lay['tpe_tile'] == N.TILE_DTYPE.itemsize
+    assert lay['tpe_work'] == N.WORK_DTYPE.itemsize
+    assert lay['tpe_best'] == N.BEST_DTYPE.itemsize
+    assert lay['tpe_result'] == N.RESULT_DTYPE.itemsize
+    assert lay['tpe_batch'] == ctypes.sizeof(N.Batch)
+    for key, off in lay.items():
+        if '.' not in key:
+            continue
+        st, f = key.split('.')
+        if st == 'tpe_problem':
+            assert N.PROBLEM_DTYPE.fields[f][1] == off, key
+        elif st == 'tpe_result':
+            assert N.RESULT_DTYPE.fields[f][1] == off, key
+        elif st == 'tpe_batch':
+            assert getattr(N.Batch, f).offset == off, key
+
+
+def test_engine_refuses_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('a GPU is visible')
+    from hyperopt_amd.engine import Engine
+    with pytest.raises(N.NativeUnavailable):
+        Engine()

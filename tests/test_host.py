@@ -1,0 +1,133 @@
+"""Host-side logic (no GPU): space flattening, start-up path, history SoA,
+Parzen fit and posterior tables against the reference's golden vectors."""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+from oracle.spacedesc import params_from_desc
+from tests.helpers import amd_space, trials_from_history, doc_values
+
+import hyperopt_amd as H
+from hyperopt_amd import base, history, parzen, rand, space
+
+
+def _domain(desc):
+    return base.Domain(lambda x: 0.0, amd_space(desc))
+
+
+def test_param_table_matches_desc(golden):
+    g = golden('suggest_vectors.json')
+    for name, desc in g['spaces'].items():
+        d = _domain(desc)
+        ref = {p['label']: p for p in params_from_desc(desc)}
+        assert d.table.labels == sorted(ref)
+        for r in d.table.rows:
+            p = ref[r.label]
+            assert r.dist == p['dist']
+            assert r.parents == [None if p['parent'] is None else tuple(p['parent'])]
+        # RNG order == the oracle's (pinned by the reference's fixtures)
+        assert [r.label for r in d.table.rng_order()] == O._resolve_order(list(ref.values()))
+
+
+def test_rand_suggest_exact(golden):
+    g = golden('suggest_vectors.json')
+    for case in g['cases']:
+        if case.get('kind') != 'rand':
+            continue
+        d = _domain(g['spaces'][case['space']])
+        docs = rand.suggest([case['n']], d, base.Trials(), case['seed'])
+        got = doc_values(docs)
+        assert {k: float(v) for k, v in got.items()} == {k: float(v) for k, v in case['result'].items()}
+        assert docs[0]['tid'] == case['n'] and docs[0]['misc']['tid'] == case['n']
+        base.Trials().assert_valid_trial(docs[0])
+
+
+def test_history_matches_reference_walk(golden):
+    g = golden('suggest_vectors.json')
+    for case in g['cases'][:6]:
+        if case.get('kind') == 'rand':
+            continue
+        d = _domain(g['spaces'][case['space']])
+        trials = trials_from_history(case['history'], d)
+        h = history.extract(d, trials)
+        tids, losses, docs = O.history_arrays([dict(tid=x['tid'], loss=x['loss'], vals=x['vals'])
+                                               for x in case['history']])
+        assert list(h.tids) == tids and list(h.losses) == losses
+        # incremental path: extend by a document and compare again
+        h2 = history.extract(d, trials)
+        assert h2.tids is not None and list(h2.tids) == tids
+        gen = history._generic(d, trials.trials, d.table)
+        for k in d.table.labels:
+            assert list(gen.obs[k][0]) == list(h.obs[k][0])
+            assert list(map(float, gen.obs[k][1])) == list(map(float, h.obs[k][1]))
+
+
+def test_history_cache_tracks_loss_updates():
+    d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1)})
+    t = base.Trials()
+    docs = rand.suggest([0, 1, 2], d, t, 1)
+    t.insert_trial_docs(docs)
+    t.refresh()
+    h = history.extract(d, t)
+    assert np.all(np.isinf(h.losses))
+    for i, doc in enumerate(t.trials):
+        doc['state'] = base.JOB_STATE_DONE
+        doc['result'] = {'status': 'ok', 'loss': float(i)}
+    h = history.extract(d, t)
+    assert list(h.losses) == [0.0, 1.0, 2.0]
+
+
+def test_fit_posterior_exact(golden):
+    for case in golden('kernel_vectors.json'):
+        post = parzen.fit_posterior(case['dist'], case['args'], np.asarray(case['below']),
+                                    np.asarray(case['above']), 1.0)
+        for got, want in ((post.below, case['b_params']), (post.above, case['a_params'])):
+            for g_, w_ in zip(got, want):
+                assert list(np.asarray(g_, dtype=float)) == [float(v) for v in w_], case['dist']
+
+
+def test_parzen_unit_vectors_exact(golden):
+    for case in golden('unit_vectors.json')['adaptive_parzen_normal']:
+        w, m, s = parzen.fit_parzen(case['mus'], case['prior_weight'], case['prior_mu'], case['prior_sigma'])
+        assert list(w) == case['w'] and list(m) == case['mu'] and list(s) == case['sigma']
+    for case in golden('unit_vectors.json')['linear_forgetting_weights']:
+        assert list(parzen.linear_forgetting_weights(case['N'], case['LF'])) == case['w']
+
+
+def test_split_matches_ap_filter_trials(golden):
+    for case in golden('unit_vectors.json')['ap_filter_trials']:
+        h = history.History(np.asarray(case['l_idxs']), np.asarray(case['l_vals']), {})
+        bt = history.split_below(h, case['gamma'])
+        m = history.below_mask(np.asarray(case['o_idxs']), bt)
+        ov = np.asarray(case['o_vals'])
+        assert list(ov[m]) == case['below'] and list(ov[~m]) == case['above']
+
+
+def test_gauss_table_reproduces_lpdf(golden):
+    """The folded (mu, a, c, base) table evaluated in float64 on the host
+    reproduces GMM1_lpdf / LGMM1_lpdf — checks the table algebra the kernels use."""
+    for case in golden('kernel_vectors.json'):
+        if case['dist'] not in ('uniform', 'loguniform', 'normal', 'lognormal'):
+            continue
+        post = parzen.fit_posterior(case['dist'], case['args'], np.asarray(case['below']),
+                                    np.asarray(case['above']), 1.0)
+        logf = post.family == 1
+        x = np.asarray(case['cand'])
+        t = np.log(x) if logf else x
+        for mix, ref in ((post.below, case['l']), (post.above, case['g'])):
+            mu, a, c, b = parzen.gauss_table(*mix, post, logf)
+            v = c[None, :] - (a[None, :] * (t[:, None] - mu[None, :])) ** 2
+            m = v.max(axis=1)
+            lp = (m + np.log2(np.exp2(v - m[:, None]).sum(axis=1))) * np.log(2) + b - (t if logf else 0)
+            np.testing.assert_allclose(lp, ref, rtol=1e-10, atol=1e-10)
+
+
+def test_space_evaluate_and_duplicate_label():
+    sp = {'a': H.hp.choice('c', [H.hp.uniform('u', 0, 1), {'k': H.hp.randint('r', 3)}]),
+          'b': H.scope.int(H.hp.quniform('q', 0, 10, 1)) + 1}
+    assert space.evaluate(sp, {'c': 1, 'r': np.int64(2), 'q': 4.0}) == {'a': {'k': 2}, 'b': 5}
+    assert space.evaluate(sp, {'c': 0, 'u': np.float64(0.5), 'q': 3.0}) == {'a': 0.5, 'b': 4}
+    with pytest.raises(H.exceptions.DuplicateLabel):
+        base.Domain(lambda x: 0, [H.hp.uniform('x', 0, 1), H.hp.uniform('x', 0, 2)])
+    with pytest.raises(TypeError):
+        H.hp.uniform(3, 0, 1)
