@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libtpe_hip.so')
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH = 1, 2
@@ -24,11 +24,14 @@ PROBLEM_DTYPE = np.dtype([
     ('cand_off', '<i8'), ('cand_base', '<i8'), ('part_off', '<i8'),
     ('n_splits', '<i4'), ('tile_off', '<i4'), ('n_tiles', '<i4'), ('samp_off', '<i4'),
     ('samp_len', '<i4'), ('below_off', '<i4'), ('below_len', '<i4'), ('above_off', '<i4'),
-    ('above_len', '<i4'), ('reserved', '<i4'),
+    ('above_len', '<i4'), ('wide_off', '<i4'), ('wide_len', '<i4'), ('grid_off', '<i4'),
+    ('grid_n', '<i4'), ('reserved', '<i4'),
     ('low', '<f8'), ('high', '<f8'), ('q', '<f8'), ('below_base', '<f8'), ('above_base', '<f8'),
+    ('prior_mu', '<f4'), ('prior_a', '<f4'), ('prior_c', '<f4'), ('narrow_cmax', '<f4'),
+    ('narrow_amin', '<f4'), ('grid_lo', '<f4'), ('grid_inv', '<f4'), ('reserved_f', '<f4'),
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
 ])
-assert PROBLEM_DTYPE.itemsize == 136
+assert PROBLEM_DTYPE.itemsize == 184
 TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
                        ('k_start', '<i4'), ('k_end', '<i4'), ('reserved', '<i4')])
@@ -41,9 +44,14 @@ assert RESULT_DTYPE.itemsize == 48
 class Batch(ctypes.Structure):
     _fields_ = [
         ('problems', ctypes.c_void_p), ('n_problems', ctypes.c_int32),
-        ('precision', ctypes.c_int32), ('sample', ctypes.c_int32), ('reserved', ctypes.c_int32),
+        ('precision', ctypes.c_int32), ('sample', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
         ('comp32', ctypes.c_void_p), ('comp64', ctypes.c_void_p), ('samp', ctypes.c_void_p),
+        ('grid', ctypes.c_void_p),
         ('cand', ctypes.c_void_p), ('coord', ctypes.c_void_p),
+        ('keys', ctypes.c_void_p), ('vals', ctypes.c_void_p),
+        ('keys_sorted', ctypes.c_void_p), ('vals_sorted', ctypes.c_void_p),
+        ('sort_tmp', ctypes.c_void_p), ('sort_tmp_bytes', ctypes.c_uint64),
+        ('total_cand', ctypes.c_int64),
         ('tiles', ctypes.c_void_p), ('n_tiles', ctypes.c_int32), ('reserved2', ctypes.c_int32),
         ('work', ctypes.c_void_p),
         ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32),
@@ -54,7 +62,8 @@ class Batch(ctypes.Structure):
 
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
-           'tpe_run_batch', 'tpe_sample', 'tpe_score_above', 'tpe_finalize', 'tpe_select')
+           'tpe_sort_workspace_bytes', 'tpe_run_batch', 'tpe_sample', 'tpe_sort', 'tpe_score_above',
+           'tpe_finalize', 'tpe_select')
 
 
 class NativeUnavailable(RuntimeError):
@@ -80,7 +89,9 @@ def load(path=LIB_PATH):
     lib.tpe_last_error.restype = ctypes.c_char_p
     lib.tpe_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
     lib.tpe_tile_size.restype = ctypes.c_int
-    for name in ('tpe_run_batch', 'tpe_sample', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
+    lib.tpe_sort_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)]
+    lib.tpe_sort_workspace_bytes.restype = ctypes.c_int
+    for name in ('tpe_run_batch', 'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
         fn = getattr(lib, name)
         fn.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
         fn.restype = ctypes.c_int

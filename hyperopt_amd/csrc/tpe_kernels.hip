@@ -2,16 +2,20 @@
 //
 // Replaces, per (new_id, hyperparameter) problem, the numpy operators of
 // gsmafra/hyperopt's tpe.suggest (see include/tpe_hip.h for the reference
-// file:line of each stage).  Four stages, each a batched launch over a flat
+// file:line of each stage).  Five stages, each a batched launch over a flat
 // work list so that problems of very different size share one grid:
 //
-//   tpe_sample       Philox-4x32-10 candidates from the below mixture
+//   tpe_sample       Philox-4x32-10 candidates from the below mixture, plus the
+//                    sort keys (problem, ordered f32 kernel coordinate)
+//   tpe_sort         radix sort of the keys (rocPRIM) — candidates of one wave
+//                    become neighbours in value, which is what lets the hot
+//                    loop skip the above-mixture components that cannot matter
 //   tpe_score_above  candidate x component log-sum-exp of the above mixture
-//                    (the O(C*K) hot loop; components are wave-uniform and are
-//                    read through the scalar cache, candidates live in VGPRs)
+//                    (the O(C*K) loop; components are wave-uniform scalar
+//                    loads, candidates live in VGPRs, 8 per lane)
 //   tpe_finalize     below lpdf (<= 26 components), l - g, per-tile argmax
-//   tpe_select       per-problem argmax over tiles (first index on ties, NaN
-//                    wins, like np.argmax) and the chosen value
+//   tpe_select       per-problem argmax over tiles (first ORIGINAL index on
+//                    ties, NaN wins, like np.argmax) and the chosen value
 //
 // No atomics: every reduction is in a fixed order, so results are bitwise
 // reproducible run to run and identical for any candidate sharding.
@@ -21,15 +25,19 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "../../include/tpe_hip.h"
 
 namespace {
 
 constexpr int kThreads = 256;          // 4 waves of 64
-constexpr int kR = 8;                  // candidates per thread
+constexpr int kR = 8;                  // candidates per lane
+constexpr int kWaveCands = 64 * kR;    // 512 consecutive (sorted) candidates per wave
 constexpr int kTile = kThreads * kR;   // candidates per tile
 constexpr double kEPS = 1e-12;         // tpe.py:25
 constexpr double kLn2 = 0.69314718055994530942;
+constexpr float kPruneBits = 45.f;     // skipped terms are < 2^-45 of the sum
 
 thread_local char g_err[512];
 
@@ -71,22 +79,15 @@ __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
   return ((double)m + 0.5) * 1.1102230246251565e-16;
 }
 
-// ------------------------------------------------------- normal helpers
-__device__ __forceinline__ float phi_std(float z) { return 0.5f * erfcf(-z * 0.70710678118654752f); }
-__device__ __forceinline__ double phi_std(double z) { return 0.5 * erfc(-z * 0.70710678118654752); }
-__device__ __forceinline__ float erfcinv_(float v) { return erfcinvf(v); }
-__device__ __forceinline__ double erfcinv_(double v) { return erfcinv(v); }
-
-// standard normal truncated to [za, zb) by inversion.  The interval is mirrored
-// into the lower half-line first so both CDF values keep relative precision.
-template <typename T>
-__device__ __forceinline__ T trunc_std_normal(T za, T zb, T u) {
-  const bool flip = za > T(0);
-  if (flip) { const T t = -zb; zb = -za; za = t; }
-  const T fa = phi_std(za), fb = phi_std(zb);
-  const T p = fa + u * (fb - fa);
-  const T z = T(-1.41421356237309505) * erfcinv_(T(2) * p);
-  return flip ? -z : z;
+// order-preserving map float -> uint32 (and back)
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  if (f != f) u = 0x7FC00000u;                 // canonical NaN sorts last
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t o) {
+  const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+  return __uint_as_float(u);
 }
 
 // ---------------------------------------------------------- argmax order
@@ -100,24 +101,30 @@ __device__ __forceinline__ bool better(double s, int64_t i, double bs, int64_t b
   return s > bs || (s == bs && i < bi);
 }
 
-// exact max-shifted log-sum-exp (log2 domain) over a short component range
+// exact max-shifted log-sum-exp (log2 domain) over up to two component ranges
 template <typename T, typename C4>
-__device__ __forceinline__ T lse2_exact(const C4* __restrict__ comp, int k0, int n, T t) {
+__device__ __forceinline__ T lse2_exact(const C4* __restrict__ comp, int k0, int n, int k1, int n1, T t) {
   T m = -INFINITY;
-  for (int k = 0; k < n; ++k) {
-    const C4 c = comp[k0 + k];
-    const T d = (t - (T)c.x) - (T)c.y;
-    const T z = d * (T)c.z;
-    const T v = (T)c.w - z * z;
-    m = v > m ? v : m;
+  for (int r = 0; r < 2; ++r) {
+    const int base = r ? k1 : k0, cnt = r ? n1 : n;
+    for (int k = 0; k < cnt; ++k) {
+      const C4 c = comp[base + k];
+      const T d = (t - (T)c.x) - (T)c.y;
+      const T z = d * (T)c.z;
+      const T v = (T)c.w - z * z;
+      m = v > m ? v : m;
+    }
   }
   if (!(m > -INFINITY)) return m;      // empty mixture or all -inf
   T s = 0;
-  for (int k = 0; k < n; ++k) {
-    const C4 c = comp[k0 + k];
-    const T d = (t - (T)c.x) - (T)c.y;
-    const T z = d * (T)c.z;
-    s += exp2((T)c.w - z * z - m);
+  for (int r = 0; r < 2; ++r) {
+    const int base = r ? k1 : k0, cnt = r ? n1 : n;
+    for (int k = 0; k < cnt; ++k) {
+      const C4 c = comp[base + k];
+      const T d = (t - (T)c.x) - (T)c.y;
+      const T z = d * (T)c.z;
+      s += exp2((T)c.w - z * z - m);
+    }
   }
   return m + log2(s);
 }
@@ -144,18 +151,20 @@ __device__ __forceinline__ double lse2_exact64(const double4* __restrict__ comp,
 // quantized mixture mass: sum_k w Phi(zu) - w Phi(zl), reference operation order
 // (tpe.py:147-159 / :285-298).  LOG selects lognormal_cdf's constant folding.
 template <bool LOG>
+__device__ __forceinline__ double qterm(const double4& c, double tu, double tl) {
+  const double zu = (tu - c.x) / c.y;
+  const double zl = (tl - c.x) / c.y;
+  double inc, dec;
+  if (LOG) { inc = c.z * (.5 + .5 * erf(zu)); dec = c.z * (.5 + .5 * erf(zl)); }
+  else     { inc = c.z * (0.5 * (1 + erf(zu))); dec = c.z * (0.5 * (1 + erf(zl))); }
+  inc -= dec;
+  return inc;
+}
+
+template <bool LOG>
 __device__ __forceinline__ double qmass(const double4* __restrict__ comp, int k0, int n, double tu, double tl) {
   double prob = 0.0;
-  for (int k = 0; k < n; ++k) {
-    const double4 c = comp[k0 + k];
-    const double zu = (tu - c.x) / c.y;
-    const double zl = (tl - c.x) / c.y;
-    double inc, dec;
-    if (LOG) { inc = c.z * (.5 + .5 * erf(zu)); dec = c.z * (.5 + .5 * erf(zl)); }
-    else     { inc = c.z * (0.5 * (1 + erf(zu))); dec = c.z * (0.5 * (1 + erf(zl))); }
-    inc -= dec;
-    prob += inc;
-  }
+  for (int k = 0; k < n; ++k) prob += qterm<LOG>(comp[k0 + k], tu, tl);
   return prob;
 }
 
@@ -176,12 +185,20 @@ __device__ __forceinline__ void q_bounds(const tpe_problem& p, double x, double&
   }
 }
 
+// sorted position of candidate j (0..kR-1) of this lane inside a tile
+__device__ __forceinline__ int tile_pos(int cand_start, int j) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  return cand_start + wave * kWaveCands + lane + 64 * j;
+}
+
 // ================================================================= sample
+// Draws (when `draw`) and writes the sort keys: (problem << 32) | ordered(coord).
 __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restrict__ P,
                                                      const tpe_tile* __restrict__ tiles,
                                                      const double* __restrict__ samp,
                                                      double* __restrict__ cand, float* __restrict__ coord,
-                                                     int precision) {
+                                                     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                     int precision, int draw) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   const bool quant = p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
@@ -194,67 +211,109 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     hi_f = (float)hi;
     while ((double)hi_f >= hi) hi_f = nextafterf(hi_f, -INFINITY);
   }
+  const double* S = samp + 8 * (int64_t)p.samp_off;
+  const uint64_t khi = (uint64_t)(uint32_t)tl.problem << 32;
   for (int j = 0; j < kR; ++j) {
     const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
     if (i >= p.n_cand) break;
-    const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-    const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-    // component choice by inversion of the selection CDF
-    const double u1 = u01d(r.x, r.y);
-    const double* S = samp + 8 * (int64_t)p.samp_off;
-    if (p.samp_len <= 0) { cand[p.cand_off + i] = NAN; coord[p.cand_off + i] = NAN; continue; }
-    int k = 0;
-    while (k < p.samp_len - 1 && !(u1 < S[8 * k])) ++k;
-    const double* s = S + 8 * k;
     const int64_t o = p.cand_off + i;
-    if (p.family == TPE_FAM_CATEGORICAL) {
-      cand[o] = (double)k;
-      coord[o] = (float)k;
-      continue;
+    if (draw) {
+      if (p.samp_len <= 0) { cand[o] = NAN; coord[o] = NAN; }
+      else {
+        const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+        const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+        // component choice: first k with u < cum_k (binary search, <= 27 rows)
+        const double u1 = u01d(r.x, r.y);
+        int a = 0, b = p.samp_len - 1;
+        while (a < b) { const int m = (a + b) >> 1; if (u1 < S[8 * m]) b = m; else a = m + 1; }
+        const double* s = S + 8 * a;
+        if (p.family == TPE_FAM_CATEGORICAL) {
+          cand[o] = (double)a;
+          coord[o] = (float)a;
+        } else {
+          // truncated normal by inversion; fa, fb = Phi of the (mirrored) bounds
+          const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
+          const bool flip = s[5] != 0.0;
+          double x;      // draw in sampling space (log space for LGMM1)
+          if (precision == TPE_PREC_F32) {
+            const float pr = (float)fa + u01f(r.z) * ((float)fb - (float)fa);
+            float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+            if (flip) z = -z;
+            float xf = (float)mu + (float)sg * z;
+            if (!(xf == xf)) xf = (float)mu;
+            xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
+            coord[o] = xf;
+            x = (double)xf;
+          } else {
+            const double pr = fa + u01d(r.z, r.w) * (fb - fa);
+            double z = -1.41421356237309505 * erfcinv(2.0 * pr);
+            if (flip) z = -z;
+            x = mu + sg * z;
+            if (!(x == x)) x = mu;
+            if ((p.flags & TPE_F_HAS_LOW) && x < lo) x = lo;
+            if ((p.flags & TPE_F_HAS_HIGH) && x >= hi) x = nextafter(hi, -INFINITY);
+            coord[o] = (float)x;
+          }
+          if (logsp) x = exp(x);
+          if (quant) x = rint(x / p.q) * p.q;      // np.round: half to even
+          cand[o] = x;
+        }
+      }
     }
-    const double mu = s[1], sg = s[2], za = s[3], zb = s[4];
-    double x;      // draw in sampling space (log space for LGMM1)
-    if (precision == TPE_PREC_F32) {
-      const float z = trunc_std_normal<float>((float)za, (float)zb, u01f(r.z));
-      float xf = (float)mu + (float)sg * z;
-      if (!(xf == xf)) xf = (float)mu;
-      xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
-      coord[o] = xf;
-      x = (double)xf;
-    } else {
-      double z = trunc_std_normal<double>(za, zb, u01d(r.z, r.w));
-      x = mu + sg * z;
-      if (!(x == x)) x = mu;
-      if ((p.flags & TPE_F_HAS_LOW) && x < lo) x = lo;
-      if ((p.flags & TPE_F_HAS_HIGH) && x >= hi) x = nextafter(hi, -INFINITY);
-      coord[o] = (float)x;
-    }
-    if (logsp) x = exp(x);
-    if (quant) x = rint(x / p.q) * p.q;      // np.round: half to even
-    cand[o] = x;
+    keys[o] = khi | f2ord(coord[o]);
+    vals[o] = (uint32_t)o;
   }
 }
 
 // ============================================================ score above
-// Continuous families, f32: s_i += 2^(c_k - (a_k ((t_i - mu_hi_k) - mu_lo_k))^2)
+// Continuous families, f32, pruned: s_i = sum_k 2^(c_k - (a_k ((t_i - mu_hi_k) - mu_lo_k))^2)
+// over the wave's window of sorted components plus the wide components.
 __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __restrict__ P,
                                                         const tpe_work* __restrict__ W,
                                                         const float4* __restrict__ comp,
-                                                        const float* __restrict__ coord,
+                                                        const int32_t* __restrict__ grid,
+                                                        const uint64_t* __restrict__ keys,
                                                         double* __restrict__ part) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
   const int n = p.n_cand;
   float t[kR], s[kR];
+  float tmin = INFINITY, tmax = -INFINITY;
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
-    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
-    t[j] = i < n ? coord[p.cand_off + i] : 0.f;
+    const int i = tile_pos(w.cand_start, j);
+    t[j] = i < n ? ord2f((uint32_t)keys[p.cand_off + i]) : 0.f;
+    if (i < n) { tmin = fminf(tmin, t[j]); tmax = fmaxf(tmax, t[j]); }
     s[j] = 0.f;
   }
+  // this wave's component window
+  for (int off = 32; off > 0; off >>= 1) {
+    tmin = fminf(tmin, __shfl_xor(tmin, off));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, off));
+  }
+  int k_lo = w.k_start, k_hi = w.k_end;
+  if (!(tmin <= tmax)) {
+    k_hi = k_lo;                       // no valid candidate in this wave
+  } else if (p.narrow_amin > 0.f) {
+    const float dmax = fmaxf(fabsf(tmin - p.prior_mu), fabsf(tmax - p.prior_mu));
+    const float zp = p.prior_a * dmax;
+    const float lb = p.prior_c - zp * zp;
+    const float R = sqrtf(fmaxf(p.narrow_cmax - lb + kPruneBits, 0.f)) / p.narrow_amin;
+    const float vlo = tmin - R, vhi = tmax + R;
+    if (vlo == vlo && vhi == vhi && R < INFINITY) {
+      const float gl = (vlo - p.grid_lo) * p.grid_inv, gh = (vhi - p.grid_lo) * p.grid_inv;
+      const int bl = (int)fminf(fmaxf(floorf(gl) - 1.f, 0.f), (float)p.grid_n);
+      const int bh = (int)fminf(fmaxf(floorf(gh) + 2.f, 0.f), (float)p.grid_n);
+      const int32_t* G = grid + p.grid_off;
+      k_lo = max(k_lo, G[bl]);
+      k_hi = min(k_hi, G[bh]);
+    }
+  }
+  k_lo = __builtin_amdgcn_readfirstlane(k_lo);
+  k_hi = __builtin_amdgcn_readfirstlane(k_hi);
   const float4* __restrict__ C = comp + p.above_off;
 #pragma unroll 4
-  for (int k = w.k_start; k < w.k_end; ++k) {
+  for (int k = k_lo; k < k_hi; ++k) {
     const float4 c = C[k];
 #pragma unroll
     for (int j = 0; j < kR; ++j) {
@@ -263,19 +322,32 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
       s[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(-z, z, c.w));
     }
   }
+  if (w.split == 0) {                  // wide components once per candidate
+    const float4* __restrict__ Wd = comp + p.wide_off;
+    for (int k = 0; k < p.wide_len; ++k) {
+      const float4 c = Wd[k];
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {
+        const float d = (t[j] - c.x) - c.y;
+        const float z = d * c.z;
+        s[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(-z, z, c.w));
+      }
+    }
+  }
   double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
-    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
+    const int i = tile_pos(w.cand_start, j);
     if (i < n) out[i] = (double)s[j];
   }
 }
 
-// Continuous families, f64 (parity precision)
+// Continuous families, f64 (parity precision, unpruned)
 __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __restrict__ P,
                                                         const tpe_work* __restrict__ W,
                                                         const double4* __restrict__ comp,
                                                         const double* __restrict__ cand,
+                                                        const uint32_t* __restrict__ vals,
                                                         double* __restrict__ part) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
@@ -284,8 +356,8 @@ __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __res
   double t[kR], s[kR];
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
-    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
-    const double x = i < n ? cand[p.cand_off + i] : 1.0;
+    const int i = tile_pos(w.cand_start, j);
+    const double x = i < n ? cand[vals[p.cand_off + i]] : 1.0;
     t[j] = logsp ? log(x) : x;
     s[j] = 0.0;
   }
@@ -301,7 +373,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __res
   double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
-    const int i = w.cand_start + (int)threadIdx.x + j * kThreads;
+    const int i = tile_pos(w.cand_start, j);
     if (i < n) out[i] = s[j];
   }
 }
@@ -312,6 +384,7 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
                                                       const tpe_work* __restrict__ W,
                                                       const double4* __restrict__ comp,
                                                       const double* __restrict__ cand,
+                                                      const uint32_t* __restrict__ vals,
                                                       double* __restrict__ part) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
@@ -321,8 +394,8 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
     double tu[R], tl[R], s[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const int i = w.cand_start + (int)threadIdx.x + (h * R + j) * kThreads;
-      const double x = i < n ? cand[p.cand_off + i] : 0.0;
+      const int i = tile_pos(w.cand_start, h * R + j);
+      const double x = i < n ? cand[vals[p.cand_off + i]] : 0.0;
       q_bounds(p, x, tu[j], tl[j]);
       s[j] = 0.0;
     }
@@ -330,20 +403,12 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
     for (int k = w.k_start; k < w.k_end; ++k) {
       const double4 c = C[k];
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const double zu = (tu[j] - c.x) / c.y;
-        const double zl = (tl[j] - c.x) / c.y;
-        double inc, dec;
-        if (LOG) { inc = c.z * (.5 + .5 * erf(zu)); dec = c.z * (.5 + .5 * erf(zl)); }
-        else     { inc = c.z * (0.5 * (1 + erf(zu))); dec = c.z * (0.5 * (1 + erf(zl))); }
-        inc -= dec;
-        s[j] += inc;
-      }
+      for (int j = 0; j < R; ++j) s[j] += qterm<LOG>(c, tu[j], tl[j]);
     }
     double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const int i = w.cand_start + (int)threadIdx.x + (h * R + j) * kThreads;
+      const int i = tile_pos(w.cand_start, h * R + j);
       if (i < n) out[i] = s[j];
     }
   }
@@ -355,7 +420,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        const float4* __restrict__ comp32,
                                                        const double4* __restrict__ comp64,
                                                        const double* __restrict__ cand,
-                                                       const float* __restrict__ coord,
+                                                       const uint64_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ vals,
                                                        const double* __restrict__ part,
                                                        double* __restrict__ l_out, double* __restrict__ g_out,
                                                        tpe_best* __restrict__ tile_best, int precision) {
@@ -365,10 +431,12 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
   double bs = 0, bl = 0, bg = 0;
   int64_t bi = -1;
   for (int j = 0; j < kR; ++j) {
-    const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
-    if (i >= n) break;
-    const int64_t o = p.cand_off + i;
-    const double x = cand[o];
+    const int i = tile_pos(tl.cand_start, j);
+    if (i >= n) continue;
+    const int64_t so = p.cand_off + i;             // sorted position
+    const uint32_t oo = vals[so];                  // original position
+    const int64_t orig = (int64_t)oo - p.cand_off; // original local index
+    const double x = cand[oo];
     double l, g;
     if (p.family == TPE_FAM_CATEGORICAL) {
       const int c = (int)x;
@@ -393,10 +461,12 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
       for (int sp = 0; sp < p.n_splits; ++sp) sa += part[p.part_off + (int64_t)sp * n + i];
       double lb2, la2;
       if (precision == TPE_PREC_F32) {
-        const float t = coord[o];
-        lb2 = (double)lse2_exact<float, float4>(comp32, p.below_off, p.below_len, t);
+        const float t = ord2f((uint32_t)keys[so]);
+        lb2 = (double)lse2_exact<float, float4>(comp32, p.below_off, p.below_len, 0, 0, t);
         // fixed-shift sum; if it under-flowed, redo this candidate max-shifted
-        la2 = sa > 1e-30 ? log2(sa) : (double)lse2_exact<float, float4>(comp32, p.above_off, p.above_len, t);
+        la2 = sa > 1e-30 ? log2(sa)
+                         : (double)lse2_exact<float, float4>(comp32, p.above_off, p.above_len, p.wide_off,
+                                                             p.wide_len, t);
       } else {
         const double t = logsp ? log(x) : x;
         lb2 = lse2_exact64(comp64, p.below_off, p.below_len, t);
@@ -407,8 +477,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
       g = la2 * kLn2 + p.above_base - lnx;
     }
     const double sc = l - g;
-    if (l_out) { l_out[o] = l; g_out[o] = g; }
-    if (better(sc, i, bs, bi)) { bs = sc; bl = l; bg = g; bi = i; }
+    if (l_out) { l_out[oo] = l; g_out[oo] = g; }
+    if (better(sc, orig, bs, bi)) { bs = sc; bl = l; bg = g; bi = orig; }
   }
   // wave reduction, then across the 4 waves through LDS
   for (int off = 32; off > 0; off >>= 1) {
@@ -462,18 +532,23 @@ __global__ __launch_bounds__(kThreads) void k_select(const tpe_problem* __restri
 
 int check_batch(const tpe_batch* b) {
   if (!b) return fail(TPE_E_ARG, "null batch");
-  if (b->n_problems < 0 || b->n_tiles < 0 || b->n_work_cont < 0 || b->n_work_qgauss < 0 || b->n_work_qlog < 0)
+  if (b->n_problems < 0 || b->n_tiles < 0 || b->n_work_cont < 0 || b->n_work_qgauss < 0 || b->n_work_qlog < 0 ||
+      b->total_cand < 0)
     return fail(TPE_E_ARG, "negative count");
   const int64_t n_work = (int64_t)b->n_work_cont + b->n_work_qgauss + b->n_work_qlog;
   if (b->precision != TPE_PREC_F32 && b->precision != TPE_PREC_F64) return fail(TPE_E_ARG, "bad precision");
   if (b->n_problems > 0 && (!b->problems || !b->result)) return fail(TPE_E_ARG, "null problems/result");
-  if (b->n_tiles > 0 && (!b->tiles || !b->tile_best || !b->cand || !b->coord)) return fail(TPE_E_ARG, "null tile buffers");
+  if (b->n_tiles > 0 && (!b->tiles || !b->tile_best || !b->cand || !b->coord || !b->keys || !b->vals ||
+                         !b->keys_sorted || !b->vals_sorted))
+    return fail(TPE_E_ARG, "null candidate buffers");
   if (n_work > 0 && (!b->work || !b->part)) return fail(TPE_E_ARG, "null work buffers");
-  if (n_work > 0 && b->precision == TPE_PREC_F32 && b->n_work_cont > 0 && !b->comp32)
-    return fail(TPE_E_ARG, "null comp32");
+  if (b->n_work_cont > 0 && b->precision == TPE_PREC_F32 && (!b->comp32 || !b->grid))
+    return fail(TPE_E_ARG, "null comp32/grid");
   if ((n_work > 0 || b->n_tiles > 0) && !b->comp64 && b->precision == TPE_PREC_F64)
     return fail(TPE_E_ARG, "null comp64");
   if ((b->l_out == nullptr) != (b->g_out == nullptr)) return fail(TPE_E_ARG, "l_out and g_out go together");
+  if (b->total_cand >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one batch");
+  if (b->n_tiles > 0 && (b->sort_end_bit <= 16 || b->sort_end_bit > 64)) return fail(TPE_E_ARG, "bad sort_end_bit");
   return TPE_OK;
 }
 
@@ -496,36 +571,62 @@ int tpe_device_count(int* n) {
 
 int tpe_tile_size(void) { return kTile; }
 
+int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
+  if (!bytes || total_cand < 0) return fail(TPE_E_ARG, "bad arguments");
+  size_t sz = 0;
+  hipError_t e = rocprim::radix_sort_pairs<rocprim::default_config>(
+      nullptr, sz, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+      (size_t)total_cand, 16u, 64u, (hipStream_t)0);
+  if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  *bytes = (uint64_t)sz;
+  return TPE_OK;
+}
+
 int tpe_sample(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  if (!b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
+  if (b->sample && !b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
   if (b->n_tiles == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream,
-                     b->problems, b->tiles, b->samp, b->cand, b->coord, b->precision);
+  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
+                     b->samp, b->cand, b->coord, b->keys, b->vals, b->precision, b->sample);
   return hip_check("tpe_sample");
+}
+
+int tpe_sort(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (b->n_tiles == 0 || b->total_cand == 0) return TPE_OK;
+  size_t sz = (size_t)b->sort_tmp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs<rocprim::default_config>(
+      b->sort_tmp, sz, (const uint64_t*)b->keys, b->keys_sorted, (const uint32_t*)b->vals, b->vals_sorted,
+      (size_t)b->total_cand, 16u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "tpe_sort: %s (workspace %llu bytes)", hipGetErrorString(e),
+             (unsigned long long)b->sort_tmp_bytes);
+    return TPE_E_HIP;
+  }
+  return hip_check("tpe_sort");
 }
 
 int tpe_score_above(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  if ((int64_t)b->n_work_cont + b->n_work_qgauss + b->n_work_qlog == 0) return TPE_OK;
   const int n_cont = b->n_work_cont, n_qg = b->n_work_qgauss, n_ql = b->n_work_qlog;
   hipStream_t s = (hipStream_t)stream;
   if (n_cont) {
     if (b->precision == TPE_PREC_F32)
       hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
-                         (const float4*)b->comp32, b->coord, b->part);
+                         (const float4*)b->comp32, b->grid, b->keys_sorted, b->part);
     else
       hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
-                         (const double4*)b->comp64, b->cand, b->part);
+                         (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   }
   if (n_qg)
     hipLaunchKernelGGL((k_above_q<false>), dim3(n_qg), dim3(kThreads), 0, s, b->problems, b->work + n_cont,
-                       (const double4*)b->comp64, b->cand, b->part);
+                       (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   if (n_ql)
     hipLaunchKernelGGL((k_above_q<true>), dim3(n_ql), dim3(kThreads), 0, s, b->problems, b->work + n_cont + n_qg,
-                       (const double4*)b->comp64, b->cand, b->part);
+                       (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   return hip_check("tpe_score_above");
 }
 
@@ -534,8 +635,8 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_tiles == 0) return TPE_OK;
   hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
-                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->coord, b->part, b->l_out,
-                     b->g_out, b->tile_best, b->precision);
+                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->keys_sorted, b->vals_sorted,
+                     b->part, b->l_out, b->g_out, b->tile_best, b->precision);
   return hip_check("tpe_finalize");
 }
 
@@ -551,7 +652,8 @@ int tpe_select(const tpe_batch* b, void* stream) {
 int tpe_run_batch(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  if (b->sample && (rc = tpe_sample(b, stream))) return rc;
+  if ((rc = tpe_sample(b, stream))) return rc;
+  if ((rc = tpe_sort(b, stream))) return rc;
   if ((rc = tpe_score_above(b, stream))) return rc;
   if ((rc = tpe_finalize(b, stream))) return rc;
   return tpe_select(b, stream);

@@ -35,6 +35,17 @@ TARGET_WORK = 2048
 MIN_COMPONENTS_PER_SPLIT = 128
 
 
+def _rows32(mu, a, c):
+    """float4 {mu_hi, mu_lo, a, c} rows (mu split so t - mu keeps ~48 bits)."""
+    r = np.empty((len(mu), 4), dtype=np.float32)
+    hi = np.asarray(mu, dtype=np.float32)
+    r[:, 0] = hi
+    r[:, 1] = (np.asarray(mu, dtype=np.float64) - hi.astype(np.float64)).astype(np.float32)
+    r[:, 2] = a
+    r[:, 3] = c
+    return r
+
+
 class LevelProblem(object):
     """One hyperparameter of one tree level, active for ``ids``.
 
@@ -68,6 +79,7 @@ class Engine(object):
         self.tile = self.lib.tpe_tile_size()
         self.set_precision(precision)
         self._bufs = {}
+        self._pinned = None
         # when a dict: every run() times each stage with HIP events on the
         # launch stream and appends (ms, CE of the launch) under the kernel name
         self.profile = None
@@ -87,26 +99,44 @@ class Engine(object):
             self._bufs[name] = t
         return t
 
-    def _upload(self, name, arr, dtype=torch.uint8):
-        """Copy a numpy array (viewed as raw bytes) into a pooled device buffer."""
-        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
-        t = self._buf(name, raw.size, torch.uint8)
-        if raw.size:
-            t[:raw.size].copy_(torch.from_numpy(raw), non_blocking=False)
-        return t
+    def _upload_blob(self, arrays):
+        """Copy several numpy arrays to the device in ONE transfer: packed into
+        a pinned staging buffer at 256-B aligned offsets, then one async H2D
+        copy on the current stream.  Returns the device address of each."""
+        offs, total = [], 0
+        for a in arrays:
+            total = (total + 255) & ~255
+            offs.append(total)
+            total += a.nbytes
+        total = max(total, 1)
+        host = self._pinned
+        if host is None or host.numel() < total:
+            host = torch.empty(max(total, 2 * (host.numel() if host is not None else 0)),
+                               dtype=torch.uint8, pin_memory=True)
+            self._pinned = host
+        hv = host.numpy()
+        for a, o in zip(arrays, offs):
+            if a.nbytes:
+                hv[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        dev = self._buf('blob', total, torch.uint8)
+        dev[:total].copy_(host[:total], non_blocking=True)
+        base = dev.data_ptr()
+        return [base + o for o in offs]
 
     # ------------------------------------------------------------- tables
     def _build(self, problems, n_cand, seed, cand_base, n_cand_global):
         """Host-side packing of one level (numpy, vectorised over ids)."""
         f64 = self.precision == 'fp64'
         T = self.tile
-        comp32, comp64, samp = [], [], []
-        n32 = n64 = ns = 0
+        comp32, comp64, samp, grids = [], [], [], []
+        n32 = n64 = ns = ngrid = 0
         rows = []                         # per LevelProblem: (table info)
         for lp in problems:
             post = lp.post
             fam = post.family
-            info = dict(family=fam, flags=(N.F_HAS_LOW if post.low is not None else 0)
+            info = dict(wide_off=0, wide_len=0, grid_off=0, grid_n=0, prior_mu=0.0, prior_a=0.0, prior_c=0.0,
+                        narrow_cmax=0.0, narrow_amin=0.0, grid_lo=0.0, grid_inv=0.0,
+                        family=fam, flags=(N.F_HAS_LOW if post.low is not None else 0)
                         | (N.F_HAS_HIGH if post.high is not None else 0),
                         low=post.low if post.low is not None else 0.0,
                         high=post.high if post.high is not None else 0.0,
@@ -149,15 +179,22 @@ class Engine(object):
                         comp64.append(r)
                         n64 += len(w)
                     else:
-                        r = np.zeros((len(w), 4), dtype=np.float32)
-                        hi = m.astype(np.float32)
-                        r[:, 0] = hi
-                        r[:, 1] = (m - hi.astype(np.float64)).astype(np.float32)
-                        r[:, 2] = a
-                        r[:, 3] = c
+                        meta, wide, cn = None, None, c
+                        if side == 'above':
+                            cn, wide, meta = parzen.prune_tables(m, a, c)
+                        r = _rows32(m, a, cn)
                         info[side + '_off'], info[side + '_len'] = n32, len(w)
                         comp32.append(r)
                         n32 += len(w)
+                        if meta is not None:
+                            comp32.append(_rows32(m[wide], a[wide], c[wide]))
+                            info['wide_off'], info['wide_len'] = n32, len(wide)
+                            n32 += len(wide)
+                            g = meta.pop('grid')
+                            info['grid_off'], info['grid_n'] = ngrid, len(g) - 1
+                            grids.append(g)
+                            ngrid += len(g)
+                            info.update(meta)
             rows.append(info)
 
         # problems: one row per (LevelProblem, id)
@@ -166,7 +203,9 @@ class Engine(object):
         prob = np.zeros(P, dtype=N.PROBLEM_DTYPE)
         owner = np.repeat(np.arange(len(problems)), counts)
         for field in ('family', 'flags', 'n_upper', 'samp_off', 'samp_len', 'below_off', 'below_len',
-                      'above_off', 'above_len', 'low', 'high', 'q', 'below_base', 'above_base'):
+                      'above_off', 'above_len', 'low', 'high', 'q', 'below_base', 'above_base',
+                      'wide_off', 'wide_len', 'grid_off', 'grid_n', 'prior_mu', 'prior_a', 'prior_c',
+                      'narrow_cmax', 'narrow_amin', 'grid_lo', 'grid_inv'):
             prob[field] = np.array([r[field] for r in rows])[owner] if P else 0
         prob['n_cand'] = n_cand
         ids = np.concatenate([lp.ids for lp in problems]) if P else np.zeros(0, np.int64)
@@ -235,6 +274,7 @@ class Engine(object):
         return dict(prob=prob, tiles=tiles, work=work, counts_w=counts_w, part_total=part_total,
                     comp32=np.concatenate(comp32) if comp32 else np.zeros((0, 4), np.float32),
                     comp64=np.concatenate(comp64) if comp64 else np.zeros((0, 4)),
+                    grid=np.concatenate(grids) if grids else np.zeros(1, np.int32),
                     samp=np.concatenate(samp) if samp else np.zeros((0, 8)), P=P)
 
     # ---------------------------------------------------------------- run
@@ -251,12 +291,18 @@ class Engine(object):
         if P == 0:
             return np.zeros(0, dtype=N.RESULT_DTYPE)
         C_total = P * n_cand
-        d_prob = self._upload('prob', tb['prob'])
-        d_tiles = self._upload('tiles', tb['tiles'])
-        d_work = self._upload('work', tb['work'])
-        d_c32 = self._upload('comp32', tb['comp32'])
-        d_c64 = self._upload('comp64', tb['comp64'])
-        d_samp = self._upload('samp', tb['samp'])
+        p_prob, p_tiles, p_work, p_c32, p_c64, p_samp, p_grid = self._upload_blob(
+            [tb['prob'], tb['tiles'], tb['work'], tb['comp32'], tb['comp64'], tb['samp'], tb['grid']])
+        if C_total >= 2 ** 32:
+            raise ValueError('more than 2^32 candidates in one level: shard the batch')
+        d_keys = self._buf('keys', C_total, torch.int64)
+        d_vals = self._buf('vals', C_total, torch.int32)
+        d_keys_s = self._buf('keys_sorted', C_total, torch.int64)
+        d_vals_s = self._buf('vals_sorted', C_total, torch.int32)
+        ws = ctypes.c_uint64(0)
+        N.check(self.lib.tpe_sort_workspace_bytes(C_total, ctypes.byref(ws)), self.lib, 'tpe_sort_workspace_bytes')
+        d_sort = self._buf('sort_tmp', ws.value, torch.uint8)
+        pbits = max(1, int(math.ceil(math.log2(P)))) if P > 1 else 1
         d_cand = self._buf('cand', C_total, torch.float64)
         d_coord = self._buf('coord', C_total, torch.float32)
         d_part = self._buf('part', tb['part_total'], torch.float64)
@@ -285,13 +331,18 @@ class Engine(object):
             d_l = self._buf('l_out', C_total, torch.float64)
             d_g = self._buf('g_out', C_total, torch.float64)
         b = N.Batch()
-        b.problems, b.n_problems = d_prob.data_ptr(), P
+        b.problems, b.n_problems = p_prob, P
         b.precision = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
         b.sample = 0 if inject else 1
-        b.comp32, b.comp64, b.samp = d_c32.data_ptr(), d_c64.data_ptr(), d_samp.data_ptr()
+        b.sort_end_bit = 32 + pbits
+        b.comp32, b.comp64, b.samp, b.grid = p_c32, p_c64, p_samp, p_grid
+        b.keys, b.vals = d_keys.data_ptr(), d_vals.data_ptr()
+        b.keys_sorted, b.vals_sorted = d_keys_s.data_ptr(), d_vals_s.data_ptr()
+        b.sort_tmp, b.sort_tmp_bytes = d_sort.data_ptr(), d_sort.numel()
+        b.total_cand = C_total
         b.cand, b.coord = d_cand.data_ptr(), d_coord.data_ptr()
-        b.tiles, b.n_tiles = d_tiles.data_ptr(), n_tiles
-        b.work = d_work.data_ptr()
+        b.tiles, b.n_tiles = p_tiles, n_tiles
+        b.work = p_work
         b.n_work_cont, b.n_work_qgauss, b.n_work_qlog = tb['counts_w']
         b.part = d_part.data_ptr()
         b.l_out = d_l.data_ptr() if d_l is not None else None
@@ -325,8 +376,8 @@ class Engine(object):
                   (fam == N.FAM_QGAUSS, 'k_above_qgauss'), (fam == N.FAM_QLOGGAUSS, 'k_above_qlog')]
         counts = list(tb['counts_w'])
         stages = []
-        if b.sample:
-            stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
+        stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
+        stages.append(('sort', self.lib.tpe_sort, None, float(tb['P'] * n_cand)))
         for gi, (mask, name) in enumerate(groups):
             if counts[gi]:
                 stages.append((name, self.lib.tpe_score_above, gi, float(ce[mask].sum())))

@@ -15,7 +15,7 @@ References (gsmafra/hyperopt, /root/reference):
 import math
 
 import numpy as np
-from scipy.special import erf
+from scipy.special import erf, erfc
 
 from . import _native as N
 
@@ -219,12 +219,14 @@ def quant_table(w, mu, sigma, post):
 
 
 def sampler_table(post):
-    """Below-mixture sampler rows {cum, mu, sigma, za, zb}.
+    """Below-mixture sampler rows {cum, mu, sigma, fa, fb, flip}.
 
     Bounded GMM1/LGMM1 draw by rejection (tpe.py:82-87): a component with
     probability w_k, a normal draw, accepted if low <= x < high.  Accepted
     draws are exactly: component k with probability ∝ w_k * mass_k, then a
-    normal truncated to [low, high) — which the device samples directly."""
+    normal truncated to [low, high) — which the device samples by inversion,
+    p = fa + u (fb - fa), z = Phi^-1(p).  When the standardised interval lies
+    right of 0 it is mirrored (flip) so fa, fb keep relative precision."""
     if post.family == N.FAM_CATEGORICAL:
         p = np.asarray(post.below[0], dtype=float)
         rows = np.zeros((len(p), 8))
@@ -237,19 +239,58 @@ def sampler_table(post):
     rows[:, 1] = mu
     rows[:, 2] = sigma
     if post.low is None and post.high is None:
-        sel = np.asarray(w, dtype=float)
-        rows[:, 3] = -np.inf
-        rows[:, 4] = np.inf
+        za = np.full(len(w), -np.inf)
+        zb = np.full(len(w), np.inf)
     else:
         za = (post.low - mu) / sigma
         zb = (post.high - mu) / sigma
-        mass = 0.5 * (erf(zb / np.sqrt(2)) - erf(za / np.sqrt(2)))
-        sel = w * np.maximum(mass, 0.0)
-        if not np.any(sel > 0):          # all components outside the bounds
-            sel = np.asarray(w, dtype=float)
-        rows[:, 3] = za
-        rows[:, 4] = zb
+    flip = za > 0
+    a = np.where(flip, -zb, za)
+    b = np.where(flip, -za, zb)
+    fa = 0.5 * erfc(-a / np.sqrt(2))
+    fb = 0.5 * erfc(-b / np.sqrt(2))
+    mass = np.maximum(fb - fa, 0.0)
+    sel = np.asarray(w, dtype=float) * (mass if (post.low is not None or post.high is not None) else 1.0)
+    if not np.any(sel > 0):          # every component outside the bounds
+        sel = np.asarray(w, dtype=float)
     cum = np.cumsum(sel) / np.sum(sel)
     cum[-1] = 1.0
     rows[:, 0] = cum
+    rows[:, 3] = fa
+    rows[:, 4] = fb
+    rows[:, 5] = flip
     return rows
+
+
+PRUNE_MIN_K = 64      # smaller above mixtures are evaluated whole
+PRUNE_WIDE = 16       # widest components evaluated for every candidate
+
+
+def prune_tables(mu, a, c):
+    """Split a sorted continuous above mixture for the pruned f32 kernel.
+
+    Returns (narrow_c, wide_idx, meta): ``narrow_c`` is ``c`` with the wide
+    components set to -inf (they are evaluated from the separate wide list),
+    meta = dict(prior_mu, prior_a, prior_c, narrow_cmax, narrow_amin, grid_lo,
+    grid_inv, grid) — see include/tpe_hip.h (pruned above mixture)."""
+    K = len(mu)
+    if K <= PRUNE_MIN_K:
+        return c, np.zeros(0, dtype=np.int64), None
+    wide = np.argsort(a, kind='stable')[:PRUNE_WIDE]        # smallest a = widest sigma
+    anchor = wide[0]
+    narrow = np.ones(K, dtype=bool)
+    narrow[wide] = False
+    nc = np.array(c, dtype=np.float64)
+    nc[wide] = -np.inf
+    mu32 = np.asarray(mu, dtype=np.float32).astype(np.float64)
+    lo, hi = float(mu32[0]), float(mu32[-1])
+    G = int(min(4096, 4 * K))
+    inv = np.float32(G / (hi - lo)) if hi > lo else np.float32(0.0)
+    edges = lo + np.arange(G, dtype=np.float64) / (float(inv) if inv > 0 else 1.0)
+    grid = np.empty(G + 1, dtype=np.int32)
+    grid[:G] = np.searchsorted(mu32, edges, side='left') if inv > 0 else 0
+    grid[G] = K
+    meta = dict(prior_mu=float(mu[anchor]), prior_a=float(a[anchor]), prior_c=float(c[anchor]),
+                narrow_cmax=float(np.max(np.asarray(c)[narrow])), narrow_amin=float(np.min(np.asarray(a)[narrow])),
+                grid_lo=lo, grid_inv=float(inv), grid=grid)
+    return nc, wide, meta

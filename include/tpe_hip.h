@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 1
+#define TPE_ABI_VERSION 2
 
 /* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
 enum {
@@ -57,7 +57,7 @@ enum { TPE_PREC_F32 = 0, TPE_PREC_F64 = 1 };
 enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3 };
 
 /*
- * One problem (136 bytes).  Component tables (device, caller-owned):
+ * One problem (184 bytes).  Component tables (device, caller-owned):
  *   comp32[k] = float4 {mu_hi, mu_lo, a, c}      families 0/1 at TPE_PREC_F32
  *   comp64[k] = double4 {mu, a, c, 0}            families 0/1 at TPE_PREC_F64
  *   comp64[k] = double4 {mu, b, w, 0}            families 2/3 (b = max(sqrt2*sigma, EPS))
@@ -67,15 +67,26 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3 };
  * with t = x (GAUSS) or ln x (LOGGAUSS); the host folds weights, 1/Z,
  * p_accept and a per-mixture shift (max_k c_k = 0) into c_k and base.
  * Families 2/3:  lpdf(x) = ln( sum_k w_k Phi(zu_k) - w_k Phi(zl_k) ) + base.
- * samp[k] = double[8] {cum, mu, sigma, za, zb, 0, 0, 0}: below-mixture sampler
- * table, cum = selection CDF (∝ w_k * mass_k when bounded), za/zb = truncation
- * bounds standardised per component (±inf when unbounded); family 4 uses cum only.
+ *
+ * Pruned above mixture (families 0/1, f32): the above components are sorted by
+ * mu; the `wide_len` widest (incl. the prior) are copied to comp32[wide_off..]
+ * and set to c = -inf in the sorted list.  A wave of sorted candidates spanning
+ * [tmin, tmax] evaluates every wide component plus the sorted components with
+ * mu in [tmin - R, tmax + R], R = sqrt(narrow_cmax - lb + 45) / narrow_amin,
+ * lb = prior_c - (prior_a * max|t - prior_mu|)^2 a lower bound of log2 s(t):
+ * every skipped term is < 2^-45 of the sum.  grid[grid_off .. +grid_n] maps
+ * value buckets (grid_lo + g / grid_inv) to the first sorted component with
+ * mu >= the bucket edge.  narrow_amin <= 0 disables pruning.
+ *
+ * samp[k] = double[8] {cum, mu, sigma, fa, fb, flip, 0, 0}: below-mixture
+ * sampler table; cum = selection CDF (∝ w_k * mass_k when bounded); fa, fb =
+ * Phi of the (mirrored if flip) standardised truncation bounds; family 4 uses cum.
  */
 typedef struct tpe_problem {
   int32_t family, flags;
   int32_t n_cand;        /* candidates of this problem on this device          */
   int32_t n_upper;       /* categorical: number of categories                  */
-  int64_t cand_off;      /* element offset into cand / coord / l_out / g_out   */
+  int64_t cand_off;      /* element offset into cand / coord / keys / l_out    */
   int64_t cand_base;     /* global index of local candidate 0 (shards, RNG)    */
   int64_t part_off;      /* element offset into part                           */
   int32_t n_splits;      /* component splits of the above mixture              */
@@ -87,10 +98,16 @@ typedef struct tpe_problem {
   int32_t below_len;
   int32_t above_off;
   int32_t above_len;
+  int32_t wide_off;      /* always-evaluated wide components (pruned mode)     */
+  int32_t wide_len;
+  int32_t grid_off;
+  int32_t grid_n;
   int32_t reserved;
   double low, high, q;   /* bounds in sampling space (log space for LGMM1)     */
   double below_base;     /* additive constant of the below lpdf                */
   double above_base;     /* additive constant of the above lpdf                */
+  float prior_mu, prior_a, prior_c, narrow_cmax;
+  float narrow_amin, grid_lo, grid_inv, reserved_f;
   uint32_t key0, key1;   /* Philox-4x32-10 key (suggest seed)                  */
   uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
 } tpe_problem;
@@ -130,18 +147,25 @@ typedef struct tpe_batch {
   const tpe_problem* problems; int32_t n_problems;
   int32_t precision;     /* TPE_PREC_F32 | TPE_PREC_F64                         */
   int32_t sample;        /* 1: draw candidates on device (Philox); 0: caller filled cand/coord */
-  int32_t reserved;
+  int32_t sort_end_bit;  /* keys are sorted on bits [16, sort_end_bit)           */
   const float* comp32;   /* [n][4]                                             */
   const double* comp64;  /* [n][4]                                             */
   const double* samp;    /* [n][8]                                             */
+  const int32_t* grid;   /* pruning grids                                      */
   double* cand;          /* [total_cand] candidate values (returned to the user) */
   float* coord;          /* [total_cand] kernel coordinate t in f32 (x or ln x) */
+  uint64_t* keys;        /* [total_cand] (problem << 32 | ordered f32 t)        */
+  uint32_t* vals;        /* [total_cand] candidate position                    */
+  uint64_t* keys_sorted; /* [total_cand]                                        */
+  uint32_t* vals_sorted; /* [total_cand]                                        */
+  void* sort_tmp; uint64_t sort_tmp_bytes;   /* tpe_sort_workspace_bytes()     */
+  int64_t total_cand;
   const tpe_tile* tiles; int32_t n_tiles; int32_t reserved2;
   /* above-mixture work list, ordered [continuous | quantized Gauss | quantized log] */
   const tpe_work* work;
   int32_t n_work_cont, n_work_qgauss, n_work_qlog, reserved3;
   double* part;          /* above-mixture partial sums                          */
-  double* l_out;         /* optional [total_cand]; NULL to skip                 */
+  double* l_out;         /* optional [total_cand] (original order); NULL to skip */
   double* g_out;         /* optional [total_cand]; NULL to skip                 */
   tpe_best* tile_best;   /* [n_tiles]                                          */
   tpe_result* result;    /* [n_problems]                                       */
@@ -159,12 +183,16 @@ int tpe_device_count(int* n);
 /* candidates per tile (2048) — the caller sizes tiles / work items with it */
 int tpe_tile_size(void);
 
-/* sample (optional) -> score -> select, enqueued on `stream` (hipStream_t);
+/* device workspace (bytes) the candidate sort needs for `total_cand` candidates */
+int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes);
+
+/* sample (optional) -> sort -> score -> select, enqueued on `stream` (hipStream_t);
  * asynchronous: results are valid once the stream reaches this point. */
 int tpe_run_batch(const tpe_batch* batch, void* stream);
 
 /* the stages one by one (same semantics; used by tests and the profiler) */
-int tpe_sample(const tpe_batch* batch, void* stream);
+int tpe_sample(const tpe_batch* batch, void* stream);     /* draw + sort keys */
+int tpe_sort(const tpe_batch* batch, void* stream);
 int tpe_score_above(const tpe_batch* batch, void* stream);
 int tpe_finalize(const tpe_batch* batch, void* stream);
 int tpe_select(const tpe_batch* batch, void* stream);

@@ -188,3 +188,27 @@ def test_large_config3_shaped_problem(engine):
     _check_lpdf(g[0][sub], la, 1e-5, 'g')
     res2 = engine.run([LevelProblem(post, 0, [0])], C, seed=7)
     assert res2[0]['idx'] == res[0]['idx'] and res2[0]['score'] == res[0]['score']
+
+
+def test_pruning_and_underflow_extremes(engine):
+    """Above mixtures large enough to be pruned, clustered observations plus
+    isolated wide components, and candidates far in the tails (the fixed-shift
+    sum underflows there and the max-shifted fallback takes over)."""
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(21)
+    obs = np.concatenate([rs.normal(0.0, 0.05, 3000), rs.normal(3.0, 0.01, 500), [-40.0, 25.0]])
+    rs.shuffle(obs)
+    for dist, args in (('normal', dict(mu=0.0, sigma=5.0)), ('uniform', dict(low=-50.0, high=50.0))):
+        post = parzen.fit_posterior(dist, args, obs[:20], obs[20:], 1.0)
+        x = np.concatenate([rs.uniform(-1, 4, 3000), [-49.9, -40.0, -20.0, 0.0, 3.0, 24.9, 49.9],
+                            np.linspace(-45, 45, 1000)])
+        if dist == 'normal':
+            x = np.concatenate([x, [-300.0, 300.0, 1e4]])
+        low, high = (post.low, post.high)
+        lb = O.gmm1_lpdf(x, *post.below, low=low, high=high)
+        la = O.gmm1_lpdf(x, *post.above, low=low, high=high)
+        res, l, g = engine.run([LevelProblem(post, 0, [0], inject=x[None, :])], len(x), 1, want_lg=True)
+        _check_lpdf(l[0], lb, 1e-5, (dist, 'l'))
+        _check_lpdf(g[0], la, 1e-5, (dist, 'g'))
+        _check_argmax(int(res[0]['idx']), lb, la, 1e-5, dist)

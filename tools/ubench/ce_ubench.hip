@@ -76,6 +76,57 @@ __global__ __launch_bounds__(256) void ce_kernel_pk(const float4* __restrict__ c
   out[tid] = acc;
 }
 
+
+// exp2 by range reduction + degree-5 minimax polynomial (packed f32), t <= 0.
+// rint via the 1.5*2^23 magic constant: no v_rndne / v_cvt, the integer part is
+// read from the low mantissa bits and shifted straight into the exponent.
+__device__ __forceinline__ f2 exp2_poly(f2 t) {
+  const f2 M = f2{12582912.0f, 12582912.0f};
+  f2 r = t + M;
+  f2 n = r - M;
+  f2 f = t - n;                       // [-0.5, 0.5]
+  f2 p = f2{1.32764655e-3f, 1.32764655e-3f};
+  p = p * f + f2{9.67554096e-3f, 9.67554096e-3f};
+  p = p * f + f2{5.55071346e-2f, 5.55071346e-2f};
+  p = p * f + f2{2.40221202e-1f, 2.40221202e-1f};
+  p = p * f + f2{6.93146944e-1f, 6.93146944e-1f};
+  p = p * f + f2{1.00000012f, 1.00000012f};
+  int ix = __float_as_int(p.x) + (__float_as_int(r.x) << 23);
+  int iy = __float_as_int(p.y) + (__float_as_int(r.y) << 23);
+  return f2{__int_as_float(ix), __int_as_float(iy)};
+}
+
+// MODE 0: all v_exp_f32; MODE 1: all polynomial; MODE 2: 1 of every R2 pairs polynomial
+template <int R2, int MODE>
+__global__ __launch_bounds__(256) void ce_kernel_mix(const float4* __restrict__ comp, int K,
+                                                     const float* __restrict__ xin, float* __restrict__ out) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  f2 x[R2], s[R2];
+#pragma unroll
+  for (int r = 0; r < R2; ++r) { x[r] = f2{xin[tid * 2 * R2 + 2 * r], xin[tid * 2 * R2 + 2 * r + 1]}; s[r] = f2{0.f, 0.f}; }
+#pragma unroll 2
+  for (int k = 0; k < K; ++k) {
+    const float4 c = comp[k];
+    const f2 mh = f2{c.x, c.x}, ml = f2{c.y, c.y}, a = f2{c.z, c.z}, cw = f2{c.w, c.w};
+#pragma unroll
+    for (int r = 0; r < R2; ++r) {
+      f2 d = (x[r] - mh) - ml;
+      f2 z = d * a;
+      f2 t = cw - z * z;
+      f2 e;
+      if (MODE == 1 || (MODE == 2 && r == 0) || (MODE == 3 && r < 2))
+        e = exp2_poly(t);
+      else
+        e = f2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+      s[r] += e;
+    }
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int r = 0; r < R2; ++r) acc += s[r].x + s[r].y;
+  out[tid] = acc;
+}
+
 // fp64 quantized CE: w * (Phi(ub) - Phi(lb)) with two erf evaluations
 template <int R>
 __global__ __launch_bounds__(256) void qce_kernel(const double4* __restrict__ comp, int K,
@@ -157,6 +208,16 @@ int main() {
     printf("{\"variant\":\"full_ce_f32_R4\",\"ms\":%.4f,\"ce_per_s\":%.4e}\n", ms, ce / (ms * 1e-3));
     ms = time_ms([&] { ce_kernel<0, 16><<<blocks / 2, threads>>>(dc, K, dx, dout); }, 10);
     printf("{\"variant\":\"full_ce_f32_R16\",\"ms\":%.4f,\"ce_per_s\":%.4e}\n", ms, ce / (ms * 1e-3));
+  }
+  for (int rep = 0; rep < 2; ++rep) {
+    ms = time_ms([&] { ce_kernel_mix<R / 2, 0><<<blocks, threads>>>(dc, K, dx, dout); }, 10);
+    printf("{\"variant\":\"mix_all_vexp_pk\",\"ms\":%.4f,\"ce_per_s\":%.4e}\n", ms, ce / (ms * 1e-3));
+    ms = time_ms([&] { ce_kernel_mix<R / 2, 1><<<blocks, threads>>>(dc, K, dx, dout); }, 10);
+    printf("{\"variant\":\"mix_all_poly_pk\",\"ms\":%.4f,\"ce_per_s\":%.4e}\n", ms, ce / (ms * 1e-3));
+    ms = time_ms([&] { ce_kernel_mix<R / 2, 2><<<blocks, threads>>>(dc, K, dx, dout); }, 10);
+    printf("{\"variant\":\"mix_1of4_poly_pk\",\"ms\":%.4f,\"ce_per_s\":%.4e}\n", ms, ce / (ms * 1e-3));
+    ms = time_ms([&] { ce_kernel_mix<R / 2, 3><<<blocks, threads>>>(dc, K, dx, dout); }, 10);
+    printf("{\"variant\":\"mix_2of4_poly_pk\",\"ms\":%.4f,\"ce_per_s\":%.4e}\n", ms, ce / (ms * 1e-3));
   }
   const int Kq = 512;
   ms = time_ms([&] { qce_kernel<4><<<blocks, threads>>>(dq, Kq, dxd, doutd); }, 5);
