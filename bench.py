@@ -169,16 +169,23 @@ def main():
     roof = None
     if above:
         ms = np.array([a[0] for a in above])
-        ce = np.array([a[1] for a in above], dtype=np.float64)
-        achieved_ce = float(ce.sum() / (ms.sum() * 1e-3))
+        algo = np.array([a[1] for a in above], dtype=np.float64)
+        execd = np.array([a[2] for a in above], dtype=np.float64)
+        secs = ms.sum() * 1e-3
         flops_per_ce = 8.0
-        peak_tflops = 157.3
-        roof = dict(bound='valu', kernel='k_above_f32', achieved=achieved_ce * flops_per_ce / 1e12,
-                    peak=peak_tflops, unit='TFLOP/s', frac=achieved_ce * flops_per_ce / 1e12 / peak_tflops,
-                    traffic=None, ce_per_s=achieved_ce, ce_per_launch=float(ce.mean()),
-                    avg_launch_ms=float(ms.mean()), flops_per_ce=flops_per_ce,
-                    note='CE = one mixture component at one candidate (sub,sub,mul,fma,exp2,add); '
-                         'peak = MI355X fp32 vector spec; exp2 issues at ~1/4-1/6 of the FMA rate')
+        peak_tflops = 157.3           # MI355X fp32 vector peak (MI355X_MICROARCH.md)
+        ach = execd.sum() / secs * flops_per_ce / 1e12
+        roof = dict(bound='valu', kernel='k_above_f32', achieved=ach, peak=peak_tflops, unit='TFLOP/s',
+                    frac=ach / peak_tflops, traffic=None,
+                    executed_ce_per_launch=float(execd.mean()), algorithmic_ce_per_launch=float(algo.mean()),
+                    executed_ce_per_s=float(execd.sum() / secs), algorithmic_ce_per_s=float(algo.sum() / secs),
+                    pruned_fraction=float(1 - execd.sum() / algo.sum()), avg_launch_ms=float(ms.mean()),
+                    launches=int(len(ms)), flops_per_ce=flops_per_ce,
+                    ce_ceiling_measured=7.97e12, ce_ceiling_source='profiles/r01_ce_ubench.txt (mix_all_vexp_pk)',
+                    note='CE = one above-mixture component at one candidate (sub, sub, mul, fma, v_exp_f32, '
+                         'add = 8 flop); achieved counts the CEs the pruned kernel executes (device counter); '
+                         'algorithmic = C x K the reference evaluates; v_exp_f32 issues at ~1/5 of the FMA '
+                         'rate, so the measured instruction-mix ceiling is 7.97e12 CE/s = 64 TFLOP/s')
         tr = os.path.join(ROOT, 'profiles', 'r01_traffic.json')
         if os.path.exists(tr):
             with open(tr) as f:

@@ -28,10 +28,12 @@ PROBLEM_DTYPE = np.dtype([
     ('grid_n', '<i4'), ('reserved', '<i4'),
     ('low', '<f8'), ('high', '<f8'), ('q', '<f8'), ('below_base', '<f8'), ('above_base', '<f8'),
     ('prior_mu', '<f4'), ('prior_a', '<f4'), ('prior_c', '<f4'), ('narrow_cmax', '<f4'),
-    ('narrow_amin', '<f4'), ('grid_lo', '<f4'), ('grid_inv', '<f4'), ('reserved_f', '<f4'),
+    ('narrow_amin', '<f4'), ('grid_lo', '<f4'), ('grid_inv', '<f4'),
+    ('key_lo', '<f4'), ('key_inv', '<f4'), ('reserved_f', '<f4'),
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
 ])
-assert PROBLEM_DTYPE.itemsize == 184
+assert PROBLEM_DTYPE.itemsize == 192
+KEY_BITS = 12
 TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
                        ('k_start', '<i4'), ('k_end', '<i4'), ('reserved', '<i4')])
@@ -58,6 +60,7 @@ class Batch(ctypes.Structure):
         ('n_work_qlog', ctypes.c_int32), ('reserved3', ctypes.c_int32),
         ('part', ctypes.c_void_p), ('l_out', ctypes.c_void_p), ('g_out', ctypes.c_void_p),
         ('tile_best', ctypes.c_void_p), ('result', ctypes.c_void_p),
+        ('ce_count', ctypes.c_void_p),
     ]
 
 

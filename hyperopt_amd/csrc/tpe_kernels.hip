@@ -6,7 +6,7 @@
 // work list so that problems of very different size share one grid:
 //
 //   tpe_sample       Philox-4x32-10 candidates from the below mixture, plus the
-//                    sort keys (problem, ordered f32 kernel coordinate)
+//                    sort keys (problem, 4096 value buckets of the kernel coordinate)
 //   tpe_sort         radix sort of the keys (rocPRIM) — candidates of one wave
 //                    become neighbours in value, which is what lets the hot
 //                    loop skip the above-mixture components that cannot matter
@@ -38,6 +38,8 @@ constexpr int kTile = kThreads * kR;   // candidates per tile
 constexpr double kEPS = 1e-12;         // tpe.py:25
 constexpr double kLn2 = 0.69314718055994530942;
 constexpr float kPruneBits = 45.f;     // skipped terms are < 2^-45 of the sum
+constexpr int kKeyBits = 12;           // value buckets per problem in the sort key
+constexpr int kKeyBuckets = 1 << kKeyBits;
 
 thread_local char g_err[512];
 
@@ -79,17 +81,6 @@ __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
   return ((double)m + 0.5) * 1.1102230246251565e-16;
 }
 
-// order-preserving map float -> uint32 (and back)
-__device__ __forceinline__ uint32_t f2ord(float f) {
-  uint32_t u = __float_as_uint(f);
-  if (f != f) u = 0x7FC00000u;                 // canonical NaN sorts last
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float ord2f(uint32_t o) {
-  const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
-  return __uint_as_float(u);
-}
-
 // ---------------------------------------------------------- argmax order
 // np.argmax: NaN is the maximum (first NaN wins), otherwise the largest value,
 // first index on ties.
@@ -127,6 +118,20 @@ __device__ __forceinline__ T lse2_exact(const C4* __restrict__ comp, int k0, int
     }
   }
   return m + log2(s);
+}
+
+// one-pass fixed-shift sum (every c_k <= 0) with the exact two-pass fallback
+// when it under-flows; used for the short below mixture
+__device__ __forceinline__ float lse2_fixed(const float4* __restrict__ comp, int k0, int n, float t) {
+  float s = 0.f;
+  for (int k = 0; k < n; ++k) {
+    const float4 c = comp[k0 + k];
+    const float d = (t - c.x) - c.y;
+    const float z = d * c.z;
+    s += __builtin_amdgcn_exp2f(__builtin_fmaf(-z, z, c.w));
+  }
+  if (s > 1e-30f) return __log2f(s);
+  return lse2_exact<float, float4>(comp, k0, n, 0, 0, t);
 }
 
 // double version for comp64 {mu, a, c, 0}
@@ -197,7 +202,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      const tpe_tile* __restrict__ tiles,
                                                      const double* __restrict__ samp,
                                                      double* __restrict__ cand, float* __restrict__ coord,
-                                                     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                      int precision, int draw) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     while ((double)hi_f >= hi) hi_f = nextafterf(hi_f, -INFINITY);
   }
   const double* S = samp + 8 * (int64_t)p.samp_off;
-  const uint64_t khi = (uint64_t)(uint32_t)tl.problem << 32;
+  const uint32_t khi = (uint32_t)tl.problem << kKeyBits;
   for (int j = 0; j < kR; ++j) {
     const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
     if (i >= p.n_cand) break;
@@ -260,7 +265,10 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
         }
       }
     }
-    keys[o] = khi | f2ord(coord[o]);
+    // sort key: (problem, value bucket) — only locality matters for pruning
+    const float gb = floorf((coord[o] - p.key_lo) * p.key_inv);
+    const uint32_t bucket = gb > 0.f ? (gb < (float)(kKeyBuckets - 1) ? (uint32_t)gb : (uint32_t)(kKeyBuckets - 1)) : 0u;
+    keys[o] = khi | bucket;
     vals[o] = (uint32_t)o;
   }
 }
@@ -272,8 +280,10 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
                                                         const tpe_work* __restrict__ W,
                                                         const float4* __restrict__ comp,
                                                         const int32_t* __restrict__ grid,
-                                                        const uint64_t* __restrict__ keys,
-                                                        double* __restrict__ part) {
+                                                        const float* __restrict__ coord,
+                                                        const uint32_t* __restrict__ vals,
+                                                        double* __restrict__ part,
+                                                        unsigned long long* __restrict__ ce_count) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
   const int n = p.n_cand;
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
-    t[j] = i < n ? ord2f((uint32_t)keys[p.cand_off + i]) : 0.f;
+    t[j] = i < n ? coord[vals[p.cand_off + i]] : 0.f;
     if (i < n) { tmin = fminf(tmin, t[j]); tmax = fmaxf(tmax, t[j]); }
     s[j] = 0.f;
   }
@@ -339,6 +349,12 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
     if (i < n) out[i] = (double)s[j];
+  }
+  if (ce_count && (threadIdx.x & 63) == 0) {   // executed CE of this wave (profiling)
+    const int wave_first = w.cand_start + (int)(threadIdx.x >> 6) * kWaveCands;
+    const int valid = max(0, min(kWaveCands, n - wave_first));
+    const long long kk = (long long)max(0, k_hi - k_lo) + (w.split == 0 ? p.wide_len : 0);
+    atomicAdd(ce_count, (unsigned long long)(kk * valid));
   }
 }
 
@@ -420,7 +436,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        const float4* __restrict__ comp32,
                                                        const double4* __restrict__ comp64,
                                                        const double* __restrict__ cand,
-                                                       const uint64_t* __restrict__ keys,
+                                                       const float* __restrict__ coord,
                                                        const uint32_t* __restrict__ vals,
                                                        const double* __restrict__ part,
                                                        double* __restrict__ l_out, double* __restrict__ g_out,
@@ -461,8 +477,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
       for (int sp = 0; sp < p.n_splits; ++sp) sa += part[p.part_off + (int64_t)sp * n + i];
       double lb2, la2;
       if (precision == TPE_PREC_F32) {
-        const float t = ord2f((uint32_t)keys[so]);
-        lb2 = (double)lse2_exact<float, float4>(comp32, p.below_off, p.below_len, 0, 0, t);
+        const float t = coord[oo];
+        lb2 = (double)lse2_fixed(comp32, p.below_off, p.below_len, t);
         // fixed-shift sum; if it under-flowed, redo this candidate max-shifted
         la2 = sa > 1e-30 ? log2(sa)
                          : (double)lse2_exact<float, float4>(comp32, p.above_off, p.above_len, p.wide_off,
@@ -548,7 +564,9 @@ int check_batch(const tpe_batch* b) {
     return fail(TPE_E_ARG, "null comp64");
   if ((b->l_out == nullptr) != (b->g_out == nullptr)) return fail(TPE_E_ARG, "l_out and g_out go together");
   if (b->total_cand >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one batch");
-  if (b->n_tiles > 0 && (b->sort_end_bit <= 16 || b->sort_end_bit > 64)) return fail(TPE_E_ARG, "bad sort_end_bit");
+  if (b->sort_end_bit < 0 || b->sort_end_bit > 32) return fail(TPE_E_ARG, "bad sort_end_bit");
+  if (b->sort_end_bit == 0 && (b->keys_sorted != b->keys || b->vals_sorted != b->vals))
+    return fail(TPE_E_ARG, "unsorted batch must alias keys_sorted/vals_sorted to keys/vals");
   return TPE_OK;
 }
 
@@ -575,8 +593,8 @@ int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
   if (!bytes || total_cand < 0) return fail(TPE_E_ARG, "bad arguments");
   size_t sz = 0;
   hipError_t e = rocprim::radix_sort_pairs<rocprim::default_config>(
-      nullptr, sz, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-      (size_t)total_cand, 16u, 64u, (hipStream_t)0);
+      nullptr, sz, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+      (size_t)total_cand, 0u, 32u, (hipStream_t)0);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
   *bytes = (uint64_t)sz;
   return TPE_OK;
@@ -595,11 +613,12 @@ int tpe_sample(const tpe_batch* b, void* stream) {
 int tpe_sort(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  if (b->n_tiles == 0 || b->total_cand == 0) return TPE_OK;
+  // sort_end_bit == 0: no sort; the caller aliases keys_sorted/vals_sorted to keys/vals
+  if (b->n_tiles == 0 || b->total_cand == 0 || b->sort_end_bit == 0) return TPE_OK;
   size_t sz = (size_t)b->sort_tmp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<rocprim::default_config>(
-      b->sort_tmp, sz, (const uint64_t*)b->keys, b->keys_sorted, (const uint32_t*)b->vals, b->vals_sorted,
-      (size_t)b->total_cand, 16u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
+      b->sort_tmp, sz, (const uint32_t*)b->keys, b->keys_sorted, (const uint32_t*)b->vals, b->vals_sorted,
+      (size_t)b->total_cand, 0u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
   if (e != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "tpe_sort: %s (workspace %llu bytes)", hipGetErrorString(e),
              (unsigned long long)b->sort_tmp_bytes);
@@ -616,7 +635,7 @@ int tpe_score_above(const tpe_batch* b, void* stream) {
   if (n_cont) {
     if (b->precision == TPE_PREC_F32)
       hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
-                         (const float4*)b->comp32, b->grid, b->keys_sorted, b->part);
+                         (const float4*)b->comp32, b->grid, b->coord, b->vals_sorted, b->part, b->ce_count);
     else
       hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
                          (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
@@ -635,7 +654,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_tiles == 0) return TPE_OK;
   hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
-                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->keys_sorted, b->vals_sorted,
+                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->coord, b->vals_sorted,
                      b->part, b->l_out, b->g_out, b->tile_best, b->precision);
   return hip_check("tpe_finalize");
 }

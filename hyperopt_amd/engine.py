@@ -35,6 +35,17 @@ TARGET_WORK = 2048
 MIN_COMPONENTS_PER_SPLIT = 128
 
 
+def _coord_range(post):
+    """Value range of the kernel coordinate (x, or ln x for log families) the
+    candidates of ``post`` fall in: the bounds, else the below mixture +-8 sigma."""
+    if post.family == N.FAM_CATEGORICAL:
+        return 0.0, float(max(post.upper, 1))
+    if post.low is not None and post.high is not None:
+        return float(post.low), float(post.high)
+    w, mu, sg = post.below
+    return float(np.min(mu - 8 * sg)), float(np.max(mu + 8 * sg))
+
+
 def _rows32(mu, a, c):
     """float4 {mu_hi, mu_lo, a, c} rows (mu split so t - mu keeps ~48 bits)."""
     r = np.empty((len(mu), 4), dtype=np.float32)
@@ -134,8 +145,10 @@ class Engine(object):
         for lp in problems:
             post = lp.post
             fam = post.family
+            klo, khi = _coord_range(post)
             info = dict(wide_off=0, wide_len=0, grid_off=0, grid_n=0, prior_mu=0.0, prior_a=0.0, prior_c=0.0,
-                        narrow_cmax=0.0, narrow_amin=0.0, grid_lo=0.0, grid_inv=0.0,
+                        narrow_cmax=0.0, narrow_amin=0.0, grid_lo=0.0, grid_inv=0.0, key_lo=klo,
+                        key_inv=(1 << N.KEY_BITS) / (khi - klo) if khi > klo else 0.0,
                         family=fam, flags=(N.F_HAS_LOW if post.low is not None else 0)
                         | (N.F_HAS_HIGH if post.high is not None else 0),
                         low=post.low if post.low is not None else 0.0,
@@ -205,7 +218,7 @@ class Engine(object):
         for field in ('family', 'flags', 'n_upper', 'samp_off', 'samp_len', 'below_off', 'below_len',
                       'above_off', 'above_len', 'low', 'high', 'q', 'below_base', 'above_base',
                       'wide_off', 'wide_len', 'grid_off', 'grid_n', 'prior_mu', 'prior_a', 'prior_c',
-                      'narrow_cmax', 'narrow_amin', 'grid_lo', 'grid_inv'):
+                      'narrow_cmax', 'narrow_amin', 'grid_lo', 'grid_inv', 'key_lo', 'key_inv'):
             prob[field] = np.array([r[field] for r in rows])[owner] if P else 0
         prob['n_cand'] = n_cand
         ids = np.concatenate([lp.ids for lp in problems]) if P else np.zeros(0, np.int64)
@@ -295,14 +308,20 @@ class Engine(object):
             [tb['prob'], tb['tiles'], tb['work'], tb['comp32'], tb['comp64'], tb['samp'], tb['grid']])
         if C_total >= 2 ** 32:
             raise ValueError('more than 2^32 candidates in one level: shard the batch')
-        d_keys = self._buf('keys', C_total, torch.int64)
+        d_keys = self._buf('keys', C_total, torch.int32)
         d_vals = self._buf('vals', C_total, torch.int32)
-        d_keys_s = self._buf('keys_sorted', C_total, torch.int64)
-        d_vals_s = self._buf('vals_sorted', C_total, torch.int32)
-        ws = ctypes.c_uint64(0)
-        N.check(self.lib.tpe_sort_workspace_bytes(C_total, ctypes.byref(ws)), self.lib, 'tpe_sort_workspace_bytes')
-        d_sort = self._buf('sort_tmp', ws.value, torch.uint8)
-        pbits = max(1, int(math.ceil(math.log2(P)))) if P > 1 else 1
+        # sort only when some problem of the level prunes its above mixture
+        pbits = int(math.ceil(math.log2(P))) if P > 1 else 0
+        sort = bool(np.any(tb['prob']['narrow_amin'] > 0)) and N.KEY_BITS + pbits <= 32
+        if sort:
+            d_keys_s = self._buf('keys_sorted', C_total, torch.int32)
+            d_vals_s = self._buf('vals_sorted', C_total, torch.int32)
+            ws = ctypes.c_uint64(0)
+            N.check(self.lib.tpe_sort_workspace_bytes(C_total, ctypes.byref(ws)), self.lib,
+                    'tpe_sort_workspace_bytes')
+            d_sort = self._buf('sort_tmp', ws.value, torch.uint8)
+        else:
+            d_keys_s, d_vals_s, d_sort = d_keys, d_vals, None
         d_cand = self._buf('cand', C_total, torch.float64)
         d_coord = self._buf('coord', C_total, torch.float32)
         d_part = self._buf('part', tb['part_total'], torch.float64)
@@ -334,11 +353,12 @@ class Engine(object):
         b.problems, b.n_problems = p_prob, P
         b.precision = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
         b.sample = 0 if inject else 1
-        b.sort_end_bit = 32 + pbits
+        b.sort_end_bit = N.KEY_BITS + pbits if sort else 0
         b.comp32, b.comp64, b.samp, b.grid = p_c32, p_c64, p_samp, p_grid
         b.keys, b.vals = d_keys.data_ptr(), d_vals.data_ptr()
         b.keys_sorted, b.vals_sorted = d_keys_s.data_ptr(), d_vals_s.data_ptr()
-        b.sort_tmp, b.sort_tmp_bytes = d_sort.data_ptr(), d_sort.numel()
+        if d_sort is not None:
+            b.sort_tmp, b.sort_tmp_bytes = d_sort.data_ptr(), d_sort.numel()
         b.total_cand = C_total
         b.cand, b.coord = d_cand.data_ptr(), d_coord.data_ptr()
         b.tiles, b.n_tiles = p_tiles, n_tiles
@@ -377,12 +397,16 @@ class Engine(object):
         counts = list(tb['counts_w'])
         stages = []
         stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
-        stages.append(('sort', self.lib.tpe_sort, None, float(tb['P'] * n_cand)))
+        if b.sort_end_bit:
+            stages.append(('sort', self.lib.tpe_sort, None, float(tb['P'] * n_cand)))
         for gi, (mask, name) in enumerate(groups):
             if counts[gi]:
                 stages.append((name, self.lib.tpe_score_above, gi, float(ce[mask].sum())))
         stages.append(('k_finalize', self.lib.tpe_finalize, None, float(tb['P'] * n_cand)))
         stages.append(('k_select', self.lib.tpe_select, None, float(tb['P'])))
+        cnt = self._buf('ce_count', 1, torch.int64)
+        cnt.zero_()
+        b.ce_count = cnt.data_ptr()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)]
         cur = torch.cuda.current_stream(self.device)
         evs[0].record(cur)
@@ -398,8 +422,13 @@ class Engine(object):
                 N.check(fn(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, name)
             evs[i + 1].record(cur)
         evs[-1].synchronize()
+        executed = int(cnt.item())
+        b.ce_count = None
         for i, (name, fn, gi, units) in enumerate(stages):
-            self.profile.setdefault(name, []).append((evs[i].elapsed_time(evs[i + 1]), units))
+            rec = (evs[i].elapsed_time(evs[i + 1]), units)
+            if name == 'k_above_f32':
+                rec = rec + (float(executed),)
+            self.profile.setdefault(name, []).append(rec)
 
 
 _ENGINES = {}

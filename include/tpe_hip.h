@@ -57,7 +57,7 @@ enum { TPE_PREC_F32 = 0, TPE_PREC_F64 = 1 };
 enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3 };
 
 /*
- * One problem (184 bytes).  Component tables (device, caller-owned):
+ * One problem (192 bytes).  Component tables (device, caller-owned):
  *   comp32[k] = float4 {mu_hi, mu_lo, a, c}      families 0/1 at TPE_PREC_F32
  *   comp64[k] = double4 {mu, a, c, 0}            families 0/1 at TPE_PREC_F64
  *   comp64[k] = double4 {mu, b, w, 0}            families 2/3 (b = max(sqrt2*sigma, EPS))
@@ -107,7 +107,9 @@ typedef struct tpe_problem {
   double below_base;     /* additive constant of the below lpdf                */
   double above_base;     /* additive constant of the above lpdf                */
   float prior_mu, prior_a, prior_c, narrow_cmax;
-  float narrow_amin, grid_lo, grid_inv, reserved_f;
+  float narrow_amin, grid_lo, grid_inv;
+  float key_lo, key_inv; /* sort-key buckets: floor((t - key_lo) * key_inv), 4096 per problem */
+  float reserved_f;
   uint32_t key0, key1;   /* Philox-4x32-10 key (suggest seed)                  */
   uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
 } tpe_problem;
@@ -147,16 +149,16 @@ typedef struct tpe_batch {
   const tpe_problem* problems; int32_t n_problems;
   int32_t precision;     /* TPE_PREC_F32 | TPE_PREC_F64                         */
   int32_t sample;        /* 1: draw candidates on device (Philox); 0: caller filled cand/coord */
-  int32_t sort_end_bit;  /* keys are sorted on bits [16, sort_end_bit)           */
+  int32_t sort_end_bit;  /* keys sorted on bits [0, sort_end_bit); 0 = no sort  */
   const float* comp32;   /* [n][4]                                             */
   const double* comp64;  /* [n][4]                                             */
   const double* samp;    /* [n][8]                                             */
   const int32_t* grid;   /* pruning grids                                      */
   double* cand;          /* [total_cand] candidate values (returned to the user) */
   float* coord;          /* [total_cand] kernel coordinate t in f32 (x or ln x) */
-  uint64_t* keys;        /* [total_cand] (problem << 32 | ordered f32 t)        */
+  uint32_t* keys;        /* [total_cand] (problem << 12 | value bucket of t)    */
   uint32_t* vals;        /* [total_cand] candidate position                    */
-  uint64_t* keys_sorted; /* [total_cand]                                        */
+  uint32_t* keys_sorted; /* [total_cand] (== keys when not sorting)            */
   uint32_t* vals_sorted; /* [total_cand]                                        */
   void* sort_tmp; uint64_t sort_tmp_bytes;   /* tpe_sort_workspace_bytes()     */
   int64_t total_cand;
@@ -169,6 +171,8 @@ typedef struct tpe_batch {
   double* g_out;         /* optional [total_cand]; NULL to skip                 */
   tpe_best* tile_best;   /* [n_tiles]                                          */
   tpe_result* result;    /* [n_problems]                                       */
+  unsigned long long* ce_count; /* optional: += component evaluations executed by the
+                                   pruned kernel (profiling); NULL to skip          */
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
