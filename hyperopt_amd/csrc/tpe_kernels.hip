@@ -41,6 +41,11 @@ constexpr float kPruneBits = 45.f;     // skipped terms are < 2^-45 of the sum
 constexpr int kKeyBits = 12;           // value buckets per problem in the sort key
 constexpr int kKeyBuckets = 1 << kKeyBits;
 
+// onesweep radix sort from 1024 keys up (rocPRIM's default switches to a merge
+// sort up to 2^20 keys, ~5x slower here)
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 1024>;
+
 thread_local char g_err[512];
 
 int fail(int code, const char* what) {
@@ -350,11 +355,16 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
     const int i = tile_pos(w.cand_start, j);
     if (i < n) out[i] = (double)s[j];
   }
-  if (ce_count && (threadIdx.x & 63) == 0) {   // executed CE of this wave (profiling)
-    const int wave_first = w.cand_start + (int)(threadIdx.x >> 6) * kWaveCands;
-    const int valid = max(0, min(kWaveCands, n - wave_first));
-    const long long kk = (long long)max(0, k_hi - k_lo) + (w.split == 0 ? p.wide_len : 0);
-    atomicAdd(ce_count, (unsigned long long)(kk * valid));
+  if (ce_count) {                      // executed CE of this work item (profiling; no atomics)
+    __shared__ unsigned long long wce[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) {
+      const int wave_first = w.cand_start + (int)(threadIdx.x >> 6) * kWaveCands;
+      const int valid = max(0, min(kWaveCands, n - wave_first));
+      const long long kk = (long long)max(0, k_hi - k_lo) + (w.split == 0 ? p.wide_len : 0);
+      wce[threadIdx.x >> 6] = (unsigned long long)(kk * valid);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ce_count[blockIdx.x] = wce[0] + wce[1] + wce[2] + wce[3];
   }
 }
 
@@ -592,7 +602,7 @@ int tpe_tile_size(void) { return kTile; }
 int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
   if (!bytes || total_cand < 0) return fail(TPE_E_ARG, "bad arguments");
   size_t sz = 0;
-  hipError_t e = rocprim::radix_sort_pairs<rocprim::default_config>(
+  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
       nullptr, sz, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
       (size_t)total_cand, 0u, 32u, (hipStream_t)0);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
@@ -616,7 +626,7 @@ int tpe_sort(const tpe_batch* b, void* stream) {
   // sort_end_bit == 0: no sort; the caller aliases keys_sorted/vals_sorted to keys/vals
   if (b->n_tiles == 0 || b->total_cand == 0 || b->sort_end_bit == 0) return TPE_OK;
   size_t sz = (size_t)b->sort_tmp_bytes;
-  hipError_t e = rocprim::radix_sort_pairs<rocprim::default_config>(
+  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
       b->sort_tmp, sz, (const uint32_t*)b->keys, b->keys_sorted, (const uint32_t*)b->vals, b->vals_sorted,
       (size_t)b->total_cand, 0u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
   if (e != hipSuccess) {

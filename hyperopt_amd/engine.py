@@ -404,7 +404,7 @@ class Engine(object):
                 stages.append((name, self.lib.tpe_score_above, gi, float(ce[mask].sum())))
         stages.append(('k_finalize', self.lib.tpe_finalize, None, float(tb['P'] * n_cand)))
         stages.append(('k_select', self.lib.tpe_select, None, float(tb['P'])))
-        cnt = self._buf('ce_count', 1, torch.int64)
+        cnt = self._buf('ce_count', max(counts[0], 1), torch.int64)
         cnt.zero_()
         b.ce_count = cnt.data_ptr()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)]
@@ -422,7 +422,7 @@ class Engine(object):
                 N.check(fn(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, name)
             evs[i + 1].record(cur)
         evs[-1].synchronize()
-        executed = int(cnt.item())
+        executed = int(cnt[:counts[0]].sum().item()) if counts[0] else 0
         b.ce_count = None
         for i, (name, fn, gi, units) in enumerate(stages):
             rec = (evs[i].elapsed_time(evs[i + 1]), units)

@@ -171,8 +171,8 @@ typedef struct tpe_batch {
   double* g_out;         /* optional [total_cand]; NULL to skip                 */
   tpe_best* tile_best;   /* [n_tiles]                                          */
   tpe_result* result;    /* [n_problems]                                       */
-  unsigned long long* ce_count; /* optional: += component evaluations executed by the
-                                   pruned kernel (profiling); NULL to skip          */
+  unsigned long long* ce_count; /* optional [n_work_cont]: component evaluations executed
+                                   per work item by the pruned kernel; NULL to skip */
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
