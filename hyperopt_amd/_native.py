@@ -33,7 +33,6 @@ PROBLEM_DTYPE = np.dtype([
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
 ])
 assert PROBLEM_DTYPE.itemsize == 192
-KEY_BITS = 12
 TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
                        ('k_start', '<i4'), ('k_end', '<i4'), ('reserved', '<i4')])
@@ -47,6 +46,7 @@ class Batch(ctypes.Structure):
     _fields_ = [
         ('problems', ctypes.c_void_p), ('n_problems', ctypes.c_int32),
         ('precision', ctypes.c_int32), ('sample', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
+        ('key_bits', ctypes.c_int32), ('reserved0', ctypes.c_int32),
         ('comp32', ctypes.c_void_p), ('comp64', ctypes.c_void_p), ('samp', ctypes.c_void_p),
         ('grid', ctypes.c_void_p),
         ('cand', ctypes.c_void_p), ('coord', ctypes.c_void_p),
@@ -64,9 +64,35 @@ class Batch(ctypes.Structure):
     ]
 
 
+class LabelIn(ctypes.Structure):
+    _fields_ = [
+        ('family', ctypes.c_int32), ('flags', ctypes.c_int32), ('upper', ctypes.c_int32),
+        ('label_ix', ctypes.c_int32),
+        ('low', ctypes.c_double), ('high', ctypes.c_double), ('q', ctypes.c_double),
+        ('below_w', ctypes.c_void_p), ('below_mu', ctypes.c_void_p), ('below_sigma', ctypes.c_void_p),
+        ('below_k', ctypes.c_int64),
+        ('above_w', ctypes.c_void_p), ('above_mu', ctypes.c_void_p), ('above_sigma', ctypes.c_void_p),
+        ('above_k', ctypes.c_int64),
+        ('ids', ctypes.c_void_p), ('n_ids', ctypes.c_int64),
+    ]
+
+
+class PackInfo(ctypes.Structure):
+    _fields_ = [
+        ('off_problems', ctypes.c_int64), ('off_tiles', ctypes.c_int64), ('off_work', ctypes.c_int64),
+        ('off_comp32', ctypes.c_int64), ('off_comp64', ctypes.c_int64), ('off_samp', ctypes.c_int64),
+        ('off_grid', ctypes.c_int64), ('n_problems', ctypes.c_int64), ('n_tiles', ctypes.c_int64),
+        ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32), ('n_work_qlog', ctypes.c_int32),
+        ('any_pruned', ctypes.c_int32), ('part_total', ctypes.c_int64), ('blob_bytes', ctypes.c_int64),
+        ('key_bits', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
+    ]
+
+
+E_SPACE = -4
+
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
            'tpe_sort_workspace_bytes', 'tpe_run_batch', 'tpe_sample', 'tpe_sort', 'tpe_score_above',
-           'tpe_finalize', 'tpe_select')
+           'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_cat_probs', 'tpe_host_pack_level')
 
 
 class NativeUnavailable(RuntimeError):
@@ -98,6 +124,16 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
         fn.restype = ctypes.c_int
+    P = ctypes.c_void_p
+    lib.tpe_host_fit_parzen.argtypes = [P, ctypes.c_int64, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_int32, P, P, P]
+    lib.tpe_host_fit_parzen.restype = ctypes.c_int64
+    lib.tpe_host_cat_probs.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_double, ctypes.c_int32, P]
+    lib.tpe_host_cat_probs.restype = ctypes.c_int
+    lib.tpe_host_pack_level.argtypes = [ctypes.POINTER(LabelIn), ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64,
+                                        ctypes.POINTER(PackInfo)]
+    lib.tpe_host_pack_level.restype = ctypes.c_int
     if lib.tpe_abi_version() != ABI_VERSION:
         raise NativeUnavailable('ABI mismatch: library %d, bindings %d' % (lib.tpe_abi_version(), ABI_VERSION))
     _LIB = lib

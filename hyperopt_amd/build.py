@@ -5,24 +5,38 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, 'csrc', 'tpe_kernels.hip')
+HOST_SRC = os.path.join(HERE, 'csrc', 'tpe_host.cpp')
 OUT = os.path.join(HERE, 'libtpe_hip.so')
 ARCH = os.environ.get('TPE_OFFLOAD_ARCH', 'gfx950')
 
 
 def build(force=False, verbose=False):
-    if (not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= os.path.getmtime(SRC)
-            and os.path.getmtime(OUT) >= os.path.getmtime(os.path.join(HERE, '..', 'include', 'tpe_hip.h'))):
+    """hipcc the kernels, g++ the host runtime (-ffp-contract=off: numpy float64
+    semantics), link both into hyperopt_amd/libtpe_hip.so."""
+    deps = [SRC, HOST_SRC, os.path.join(HERE, '..', 'include', 'tpe_hip.h')]
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-    cmd = [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-shared', '-fPIC',
-           '-Wall', '-Wno-unused-command-line-argument', '-o', OUT + '.tmp', SRC]
-    if verbose:
-        print(' '.join(cmd))
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError('hipcc failed for %s' % SRC)
-    os.replace(OUT + '.tmp', OUT)
+    gxx = os.environ.get('CXX', 'g++')
+    tmp = OUT + '.tmp'
+    host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
+    dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o')
+    cmds = [
+        [gxx, '-O2', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall', '-c', HOST_SRC,
+         '-o', host_o],
+        [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
+         '-Wno-unused-command-line-argument', '-c', SRC, '-o', dev_o],
+        [hipcc, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-Wno-unused-command-line-argument', '-o', tmp,
+         dev_o, host_o],
+    ]
+    for cmd in cmds:
+        if verbose:
+            print(' '.join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError('build step failed: %s' % cmd[0])
+    os.replace(tmp, OUT)
     return OUT
 
 

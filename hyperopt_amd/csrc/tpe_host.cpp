@@ -1,0 +1,438 @@
+// tpe_host.cpp — native host runtime of the TPE suggest engine.
+//
+// Everything the host does per suggest between the history split and the
+// device launch: the adaptive Parzen fit (tpe.py:398-475), the categorical
+// pseudo-count posteriors (tpe.py:573-607), and the packing of one tree level
+// into the device tables of include/tpe_hip.h (component rows, sampler rows,
+// pruning grids, problems, candidate tiles, above-mixture work items) — written
+// straight into one staging blob that the caller uploads in a single copy.
+//
+// Float64 semantics follow numpy exactly where the reference's bits depend on
+// them: np.sum's pairwise summation (8192-element buffered chunks), linspace's
+// i*step + start with an exact endpoint, np.clip, and no FMA contraction (this
+// file is compiled with -ffp-contract=off).  The sort permutation of the fit
+// comes from the caller (np.argsort) so tie order is the reference's.
+#include <math.h>
+
+#include <cmath>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/tpe_hip.h"
+
+namespace {
+
+constexpr double kEPS = 1e-12;
+constexpr double kLog2e = 1.4426950408889634074;
+constexpr double kLn2 = 0.69314718055994530942;
+constexpr int kPruneMinK = 64;
+constexpr int kPruneWide = 16;
+constexpr int kTargetWork = 2048;
+constexpr int kMinComponentsPerSplit = 128;
+
+// numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src)
+double pairwise(const double* a, int64_t n) {
+  if (n < 8) {
+    double r = 0.;
+    for (int64_t i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return pairwise(a, n2) + pairwise(a + n2, n - n2);
+}
+
+// np.sum of a contiguous float64 vector: pairwise within 8192-element buffers
+double np_sum(const double* a, int64_t n) {
+  const int64_t B = 8192;
+  double res = 0.;
+  for (int64_t s = 0; s < n; s += B) {
+    const double p = pairwise(a + s, std::min(B, n - s));
+    res = s == 0 ? p : res + p;
+  }
+  return res;
+}
+
+// np.maximum / np.minimum propagate NaN
+inline double np_max(double a, double b) { return (a != a || b != b) ? NAN : (a > b ? a : b); }
+inline double np_min(double a, double b) { return (a != a || b != b) ? NAN : (a < b ? a : b); }
+
+// linear_forgetting_weights (tpe.py:381-394) via np.linspace semantics
+void lf_weights(int64_t n, int lf, double* out) {
+  if (n <= 0) return;
+  if (n < lf) {
+    for (int64_t i = 0; i < n; ++i) out[i] = 1.0;
+    return;
+  }
+  const int64_t num = n - lf;
+  const double start = 1.0 / (double)n, stop = 1.0;
+  if (num == 1) {
+    out[0] = start;
+  } else if (num > 1) {
+    const double step = (stop - start) / (double)(num - 1);
+    for (int64_t i = 0; i < num; ++i) {
+      double y = (double)i * step;
+      y += start;
+      out[i] = y;
+    }
+    out[num - 1] = stop;
+  }
+  for (int64_t i = num; i < n; ++i) out[i] = 1.0;
+}
+
+double normal_cdf(double x, double mu, double sigma) {   // tpe.py:96-101
+  const double bottom = np_max(sqrt(2.0) * sigma, kEPS);
+  return 0.5 * (1 + erf((x - mu) / bottom));
+}
+
+double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi) {
+  if (!bounded) return 1.0;
+  std::vector<double> t((size_t)k);
+  for (int64_t i = 0; i < k; ++i) t[i] = w[i] * (normal_cdf(hi, mu[i], sg[i]) - normal_cdf(lo, mu[i], sg[i]));
+  return np_sum(t.data(), k);
+}
+
+struct Blob {
+  std::vector<unsigned char> data;
+  int64_t add(const void* p, int64_t bytes) {
+    int64_t off = ((int64_t)data.size() + 255) & ~(int64_t)255;
+    data.resize((size_t)(off + bytes));
+    if (bytes) memcpy(data.data() + off, p, (size_t)bytes);
+    return off;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, double prior_weight,
+                            double prior_mu, double prior_sigma, int32_t lf, double* w, double* mu,
+                            double* sigma) {
+  if (n < 0 || (n >= 2 && !order) || !w || !mu || !sigma) return TPE_E_ARG;
+  int64_t pos;
+  const int64_t K = n + 1;
+  if (n == 0) {
+    mu[0] = prior_mu; sigma[0] = prior_sigma; pos = 0;
+  } else if (n == 1) {
+    if (prior_mu < obs[0]) { pos = 0; mu[0] = prior_mu; mu[1] = obs[0]; sigma[0] = prior_sigma; sigma[1] = prior_sigma * .5; }
+    else { pos = 1; mu[0] = obs[0]; mu[1] = prior_mu; sigma[0] = prior_sigma * .5; sigma[1] = prior_sigma; }
+  } else {
+    // np.searchsorted(sorted, prior_mu, side='left') = number of elements < prior_mu
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) / 2;
+      if (obs[order[m]] < prior_mu) lo = m + 1; else hi = m;
+    }
+    pos = lo;
+    for (int64_t i = 0; i < pos; ++i) mu[i] = obs[order[i]];
+    mu[pos] = prior_mu;
+    for (int64_t i = pos; i < n; ++i) mu[i + 1] = obs[order[i]];
+    for (int64_t i = 1; i < K - 1; ++i) sigma[i] = np_max(mu[i] - mu[i - 1], mu[i + 1] - mu[i]);
+    sigma[0] = mu[1] - mu[0];
+    sigma[K - 1] = mu[K - 1] - mu[K - 2];
+  }
+  if (lf && lf < n) {
+    std::vector<double> ramp((size_t)n);
+    lf_weights(n, lf, ramp.data());
+    for (int64_t i = 0; i < pos; ++i) w[i] = ramp[order[i]];
+    w[pos] = prior_weight;
+    for (int64_t i = pos; i < n; ++i) w[i + 1] = ramp[order[i]];
+  } else {
+    for (int64_t i = 0; i < K; ++i) w[i] = 1.0;
+    w[pos] = prior_weight;
+  }
+  const double smin = prior_sigma / std::min(100.0, 1.0 + (double)K);
+  const double smax = prior_sigma / 1.0;
+  for (int64_t i = 0; i < K; ++i) sigma[i] = np_min(np_max(sigma[i], smin), smax);   // np.clip
+  sigma[pos] = prior_sigma;
+  for (int64_t i = 0; i < K; ++i)
+    if (!(sigma[i] > 0)) return TPE_E_ARG;
+  const double tot = np_sum(w, K);
+  for (int64_t i = 0; i < K; ++i) w[i] = w[i] / tot;
+  return pos;
+}
+
+int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
+                       int32_t lf, double* out) {
+  if (upper <= 0 || n < 0 || !out) return TPE_E_ARG;
+  std::vector<double> counts((size_t)upper, 0.0);
+  if (n > 0) {
+    std::vector<double> lfw((size_t)n);
+    lf_weights(n, lf, lfw.data());
+    for (int64_t i = 0; i < n; ++i) {
+      if (obs[i] < 0 || obs[i] >= upper) return TPE_E_ARG;
+      counts[(size_t)obs[i]] += lfw[i];
+    }
+  }
+  for (int32_t k = 0; k < upper; ++k)
+    counts[k] = p_prior ? counts[k] + (double)upper * (prior_weight * p_prior[k]) : counts[k] + prior_weight;
+  const double tot = np_sum(counts.data(), upper);
+  for (int32_t k = 0; k < upper; ++k) out[k] = counts[k] / tot;
+  return TPE_OK;
+}
+
+int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
+                        int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
+                        tpe_pack_info* info) {
+  if (!info || n_labels < 0 || n_cand < 0 || (n_labels && !labels)) return TPE_E_ARG;
+  const bool f64 = precision == TPE_PREC_F64;
+  const int T = 2048;
+  std::vector<float> comp32;     // float4 rows
+  std::vector<double> comp64;    // double4 rows
+  std::vector<double> samp;      // 8 doubles per row
+  std::vector<int32_t> grid;
+  std::vector<tpe_problem> lab((size_t)n_labels);
+  int64_t P = 0;
+  for (int32_t li = 0; li < n_labels; ++li) P += labels[li].n_ids;
+  // sort key = problem << key_bits | value bucket: keep it within one 8-bit radix
+  // pass up to 8 problems, never below 32 buckets per problem
+  int pbits = 0;
+  while (((int64_t)1 << pbits) < P) ++pbits;
+  const int key_bits = std::max(5, 8 - pbits);
+  const int sort_end_bit = key_bits + pbits <= 32 ? key_bits + pbits : 0;
+  for (int32_t li = 0; li < n_labels; ++li) {
+    const tpe_label_in& L = labels[li];
+    tpe_problem& p = lab[li];
+    memset(&p, 0, sizeof(p));
+    p.family = L.family; p.flags = L.flags; p.n_upper = L.upper;
+    p.low = L.low; p.high = L.high; p.q = L.q;
+    const bool bounded = (L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) != 0;
+    // ---- sampler rows (below mixture) ----
+    p.samp_off = (int32_t)(samp.size() / 8);
+    if (L.family == TPE_FAM_CATEGORICAL) {
+      const int64_t k = L.below_k;
+      double acc = 0;
+      std::vector<double> cum((size_t)k);
+      for (int64_t i = 0; i < k; ++i) { acc += L.below_w[i]; cum[i] = acc; }
+      for (int64_t i = 0; i < k; ++i) {
+        double row[8] = {i == k - 1 ? 1.0 : cum[i] / acc, 0, 0, 0, 0, 0, 0, 0};
+        samp.insert(samp.end(), row, row + 8);
+      }
+      p.samp_len = (int32_t)k;
+    } else {
+      const int64_t k = L.below_k;
+      std::vector<double> sel((size_t)k), fa((size_t)k), fb((size_t)k), flip((size_t)k);
+      double tot = 0;
+      bool any = false;
+      for (int64_t i = 0; i < k; ++i) {
+        double za = -INFINITY, zb = INFINITY;
+        if (bounded) { za = (L.low - L.below_mu[i]) / L.below_sigma[i]; zb = (L.high - L.below_mu[i]) / L.below_sigma[i]; }
+        const bool fl = za > 0;
+        const double a = fl ? -zb : za, b = fl ? -za : zb;
+        fa[i] = 0.5 * erfc(-a / sqrt(2.0));
+        fb[i] = 0.5 * erfc(-b / sqrt(2.0));
+        flip[i] = fl ? 1.0 : 0.0;
+        sel[i] = bounded ? L.below_w[i] * std::max(fb[i] - fa[i], 0.0) : L.below_w[i];
+        any = any || sel[i] > 0;
+      }
+      if (!any) for (int64_t i = 0; i < k; ++i) sel[i] = L.below_w[i];
+      for (int64_t i = 0; i < k; ++i) tot += sel[i];
+      double acc = 0;
+      for (int64_t i = 0; i < k; ++i) {
+        acc += sel[i];
+        double row[8] = {i == k - 1 ? 1.0 : acc / tot, L.below_mu[i], L.below_sigma[i], fa[i], fb[i], flip[i], 0, 0};
+        samp.insert(samp.end(), row, row + 8);
+      }
+      p.samp_len = (int32_t)k;
+    }
+    // ---- sort-key range of the kernel coordinate ----
+    double klo, khi;
+    if (L.family == TPE_FAM_CATEGORICAL) { klo = 0; khi = std::max(L.upper, 1); }
+    else if ((L.flags & TPE_F_HAS_LOW) && (L.flags & TPE_F_HAS_HIGH)) { klo = L.low; khi = L.high; }
+    else {
+      klo = INFINITY; khi = -INFINITY;
+      for (int64_t i = 0; i < L.below_k; ++i) {
+        klo = std::min(klo, L.below_mu[i] - 8 * L.below_sigma[i]);
+        khi = std::max(khi, L.below_mu[i] + 8 * L.below_sigma[i]);
+      }
+    }
+    p.key_lo = (float)klo;
+    p.key_inv = khi > klo ? (float)((double)(1 << key_bits) / (khi - klo)) : 0.f;
+    // ---- component rows ----
+    for (int side = 0; side < 2; ++side) {
+      const double* w = side ? L.above_w : L.below_w;
+      const double* mu = side ? L.above_mu : L.below_mu;
+      const double* sg = side ? L.above_sigma : L.below_sigma;
+      const int64_t k = side ? L.above_k : L.below_k;
+      int32_t& off = side ? p.above_off : p.below_off;
+      int32_t& len = side ? p.above_len : p.below_len;
+      double& base = side ? p.above_base : p.below_base;
+      if (L.family == TPE_FAM_CATEGORICAL) {
+        off = (int32_t)(comp64.size() / 4); len = (int32_t)k; base = 0;
+        for (int64_t i = 0; i < k; ++i) {
+          const double row[4] = {log(w[i]), w[i], 0, 0};
+          comp64.insert(comp64.end(), row, row + 4);
+        }
+      } else if (L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) {
+        off = (int32_t)(comp64.size() / 4); len = (int32_t)k;
+        base = -log(p_accept(w, mu, sg, k, bounded, L.low, L.high));
+        for (int64_t i = 0; i < k; ++i) {
+          const double row[4] = {mu[i], np_max(sqrt(2.0) * sg[i], kEPS), w[i], 0};
+          comp64.insert(comp64.end(), row, row + 4);
+        }
+      } else {
+        const bool logf = L.family == TPE_FAM_LOGGAUSS;
+        std::vector<double> a((size_t)k), c((size_t)k);
+        const double pa = logf ? 1.0 : p_accept(w, mu, sg, k, bounded, L.low, L.high);
+        double shift = -INFINITY;
+        for (int64_t i = 0; i < k; ++i) {
+          const double se = np_max(sg[i], kEPS);
+          const double lc = logf ? log(w[i] / (se * sqrt(2 * M_PI))) : log(w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa);
+          c[i] = lc * kLog2e;
+          a[i] = sqrt(0.5 * kLog2e) / se;
+          if (c[i] > shift && std::isfinite(c[i])) shift = c[i];
+        }
+        if (!std::isfinite(shift)) shift = 0;
+        for (int64_t i = 0; i < k; ++i) c[i] -= shift;
+        base = shift * kLn2;
+        if (f64) {
+          off = (int32_t)(comp64.size() / 4); len = (int32_t)k;
+          for (int64_t i = 0; i < k; ++i) {
+            const double row[4] = {mu[i], a[i], c[i], 0};
+            comp64.insert(comp64.end(), row, row + 4);
+          }
+          continue;
+        }
+        // pruning (above side, f32): widest components listed apart, grid over mu
+        std::vector<int64_t> wide;
+        if (side == 1 && k > kPruneMinK) {
+          std::vector<int64_t> idx((size_t)k);
+          for (int64_t i = 0; i < k; ++i) idx[i] = i;
+          std::partial_sort(idx.begin(), idx.begin() + kPruneWide, idx.end(),
+                            [&](int64_t x, int64_t y) { return a[x] < a[y] || (a[x] == a[y] && x < y); });
+          wide.assign(idx.begin(), idx.begin() + kPruneWide);
+        }
+        off = (int32_t)(comp32.size() / 4); len = (int32_t)k;
+        std::vector<char> is_wide((size_t)k, 0);
+        for (int64_t i : wide) is_wide[i] = 1;
+        for (int64_t i = 0; i < k; ++i) {
+          const float hi = (float)mu[i];
+          const float row[4] = {hi, (float)(mu[i] - (double)hi), (float)a[i], is_wide[i] ? -INFINITY : (float)c[i]};
+          comp32.insert(comp32.end(), row, row + 4);
+        }
+        if (!wide.empty()) {
+          p.wide_off = (int32_t)(comp32.size() / 4);
+          p.wide_len = (int32_t)wide.size();
+          for (int64_t i : wide) {
+            const float hi = (float)mu[i];
+            const float row[4] = {hi, (float)(mu[i] - (double)hi), (float)a[i], (float)c[i]};
+            comp32.insert(comp32.end(), row, row + 4);
+          }
+          const int64_t anchor = wide[0];
+          double cmax = -INFINITY, amin = INFINITY;
+          for (int64_t i = 0; i < k; ++i)
+            if (!is_wide[i]) { cmax = std::max(cmax, c[i]); amin = std::min(amin, a[i]); }
+          p.prior_mu = (float)mu[anchor]; p.prior_a = (float)a[anchor]; p.prior_c = (float)c[anchor];
+          p.narrow_cmax = (float)cmax; p.narrow_amin = (float)amin;
+          const double lo = (double)(float)mu[0], hi = (double)(float)mu[k - 1];
+          const int64_t G = std::min<int64_t>(4096, 4 * k);
+          const float inv = hi > lo ? (float)((double)G / (hi - lo)) : 0.f;
+          p.grid_off = (int32_t)grid.size(); p.grid_n = (int32_t)G;
+          p.grid_lo = (float)lo; p.grid_inv = inv;
+          int64_t j = 0;
+          for (int64_t g = 0; g < G; ++g) {
+            const double edge = inv > 0 ? lo + (double)g / (double)inv : lo;
+            while (j < k && (double)(float)mu[j] < edge) ++j;     // searchsorted left
+            grid.push_back((int32_t)(inv > 0 ? j : 0));
+          }
+          grid.push_back((int32_t)k);
+        }
+      }
+    }
+  }
+  // ---- problems, tiles, work ----
+  const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
+  std::vector<tpe_problem> prob((size_t)P);
+  int64_t scored = 0;
+  {
+    int64_t r = 0;
+    for (int32_t li = 0; li < n_labels; ++li)
+      for (int64_t j = 0; j < labels[li].n_ids; ++j, ++r) {
+        tpe_problem q = lab[li];
+        q.n_cand = n_cand;
+        q.cand_off = r * (int64_t)n_cand;
+        q.cand_base = cand_base;
+        q.key0 = (uint32_t)seed; q.key1 = (uint32_t)(seed >> 32);
+        q.ctr2 = (uint32_t)labels[li].label_ix;
+        q.ctr3 = (uint32_t)labels[li].ids[j];
+        q.n_tiles = (int32_t)n_tiles_p;
+        q.tile_off = (int32_t)(r * n_tiles_p);
+        prob[r] = q;
+        if (q.family != TPE_FAM_CATEGORICAL) ++scored;
+      }
+  }
+  const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
+  const int64_t scored_tiles = scored * ((C_ref + T - 1) / T);
+  const int64_t target = std::max<int64_t>(1, (kTargetWork + std::max<int64_t>(scored_tiles, 1) - 1) /
+                                                  std::max<int64_t>(scored_tiles, 1));
+  int64_t part_total = 0;
+  bool any_pruned = false;
+  for (auto& q : prob) {
+    if (q.family == TPE_FAM_CATEGORICAL) { q.n_splits = 0; q.part_off = part_total; continue; }
+    const int64_t ks = (q.above_len + kMinComponentsPerSplit - 1) / kMinComponentsPerSplit;
+    q.n_splits = (int32_t)std::max<int64_t>(1, std::min(target, ks));
+    q.part_off = part_total;
+    part_total += (int64_t)q.n_splits * n_cand;
+    any_pruned = any_pruned || q.narrow_amin > 0.f;
+  }
+  std::vector<tpe_tile> tiles((size_t)(P * n_tiles_p));
+  for (int64_t r = 0, t = 0; r < P; ++r)
+    for (int64_t j = 0; j < n_tiles_p; ++j, ++t) { tiles[t].problem = (int32_t)r; tiles[t].cand_start = (int32_t)(j * T); }
+  std::vector<tpe_work> work;
+  int32_t counts[3] = {0, 0, 0};
+  const int fams[3][2] = {{TPE_FAM_GAUSS, TPE_FAM_LOGGAUSS}, {TPE_FAM_QGAUSS, -1}, {TPE_FAM_QLOGGAUSS, -1}};
+  for (int gi = 0; gi < 3; ++gi) {
+    const size_t before = work.size();
+    for (int64_t r = 0; r < P; ++r) {
+      const tpe_problem& q = prob[r];
+      if (q.family != fams[gi][0] && q.family != fams[gi][1]) continue;
+      for (int32_t s = 0; s < q.n_splits; ++s)
+        for (int64_t j = 0; j < n_tiles_p; ++j) {
+          tpe_work w;
+          w.problem = (int32_t)r; w.split = s; w.cand_start = (int32_t)(j * T);
+          w.k_start = (int32_t)(((int64_t)q.above_len * s) / q.n_splits);
+          w.k_end = (int32_t)(((int64_t)q.above_len * (s + 1)) / q.n_splits);
+          w.reserved = 0;
+          work.push_back(w);
+        }
+    }
+    counts[gi] = (int32_t)(work.size() - before);
+  }
+  // ---- blob ----
+  Blob B;
+  info->off_problems = B.add(prob.data(), (int64_t)(prob.size() * sizeof(tpe_problem)));
+  info->off_tiles = B.add(tiles.data(), (int64_t)(tiles.size() * sizeof(tpe_tile)));
+  info->off_work = B.add(work.data(), (int64_t)(work.size() * sizeof(tpe_work)));
+  info->off_comp32 = B.add(comp32.data(), (int64_t)(comp32.size() * sizeof(float)));
+  info->off_comp64 = B.add(comp64.data(), (int64_t)(comp64.size() * sizeof(double)));
+  info->off_samp = B.add(samp.data(), (int64_t)(samp.size() * sizeof(double)));
+  if (grid.empty()) grid.push_back(0);
+  info->off_grid = B.add(grid.data(), (int64_t)(grid.size() * sizeof(int32_t)));
+  info->n_problems = P;
+  info->n_tiles = (int64_t)tiles.size();
+  info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
+  info->any_pruned = any_pruned ? 1 : 0;
+  info->key_bits = key_bits;
+  info->sort_end_bit = any_pruned ? sort_end_bit : 0;
+  info->part_total = part_total;
+  info->blob_bytes = (int64_t)B.data.size();
+  if (!blob || blob_cap < info->blob_bytes) return TPE_E_SPACE;
+  memcpy(blob, B.data.data(), B.data.size());
+  return TPE_OK;
+}
+
+}  // extern "C"

@@ -38,8 +38,6 @@ constexpr int kTile = kThreads * kR;   // candidates per tile
 constexpr double kEPS = 1e-12;         // tpe.py:25
 constexpr double kLn2 = 0.69314718055994530942;
 constexpr float kPruneBits = 45.f;     // skipped terms are < 2^-45 of the sum
-constexpr int kKeyBits = 12;           // value buckets per problem in the sort key
-constexpr int kKeyBuckets = 1 << kKeyBits;
 
 // onesweep radix sort from 1024 keys up (rocPRIM's default switches to a merge
 // sort up to 2^20 keys, ~5x slower here)
@@ -208,7 +206,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      const double* __restrict__ samp,
                                                      double* __restrict__ cand, float* __restrict__ coord,
                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                     int precision, int draw) {
+                                                     int precision, int draw, int key_bits) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   const bool quant = p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
@@ -222,7 +220,8 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     while ((double)hi_f >= hi) hi_f = nextafterf(hi_f, -INFINITY);
   }
   const double* S = samp + 8 * (int64_t)p.samp_off;
-  const uint32_t khi = (uint32_t)tl.problem << kKeyBits;
+  const uint32_t khi = (uint32_t)tl.problem << key_bits;
+  const float kmax = (float)((1 << key_bits) - 1);
   for (int j = 0; j < kR; ++j) {
     const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
     if (i >= p.n_cand) break;
@@ -272,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     }
     // sort key: (problem, value bucket) — only locality matters for pruning
     const float gb = floorf((coord[o] - p.key_lo) * p.key_inv);
-    const uint32_t bucket = gb > 0.f ? (gb < (float)(kKeyBuckets - 1) ? (uint32_t)gb : (uint32_t)(kKeyBuckets - 1)) : 0u;
+    const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
     keys[o] = khi | bucket;
     vals[o] = (uint32_t)o;
   }
@@ -575,6 +574,7 @@ int check_batch(const tpe_batch* b) {
   if ((b->l_out == nullptr) != (b->g_out == nullptr)) return fail(TPE_E_ARG, "l_out and g_out go together");
   if (b->total_cand >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one batch");
   if (b->sort_end_bit < 0 || b->sort_end_bit > 32) return fail(TPE_E_ARG, "bad sort_end_bit");
+  if (b->key_bits < 0 || b->key_bits > 16) return fail(TPE_E_ARG, "bad key_bits");
   if (b->sort_end_bit == 0 && (b->keys_sorted != b->keys || b->vals_sorted != b->vals))
     return fail(TPE_E_ARG, "unsorted batch must alias keys_sorted/vals_sorted to keys/vals");
   return TPE_OK;
@@ -616,7 +616,7 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (b->sample && !b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
   if (b->n_tiles == 0) return TPE_OK;
   hipLaunchKernelGGL(k_sample, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
-                     b->samp, b->cand, b->coord, b->keys, b->vals, b->precision, b->sample);
+                     b->samp, b->cand, b->coord, b->keys, b->vals, b->precision, b->sample, b->key_bits);
   return hip_check("tpe_sample");
 }
 

@@ -110,35 +110,15 @@ class Engine(object):
             self._bufs[name] = t
         return t
 
-    def _upload_blob(self, arrays):
-        """Copy several numpy arrays to the device in ONE transfer: packed into
-        a pinned staging buffer at 256-B aligned offsets, then one async H2D
-        copy on the current stream.  Returns the device address of each."""
-        offs, total = [], 0
-        for a in arrays:
-            total = (total + 255) & ~255
-            offs.append(total)
-            total += a.nbytes
-        total = max(total, 1)
-        host = self._pinned
-        if host is None or host.numel() < total:
-            host = torch.empty(max(total, 2 * (host.numel() if host is not None else 0)),
-                               dtype=torch.uint8, pin_memory=True)
-            self._pinned = host
-        hv = host.numpy()
-        for a, o in zip(arrays, offs):
-            if a.nbytes:
-                hv[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-        dev = self._buf('blob', total, torch.uint8)
-        dev[:total].copy_(host[:total], non_blocking=True)
-        base = dev.data_ptr()
-        return [base + o for o in offs]
-
     # ------------------------------------------------------------- tables
-    def _build(self, problems, n_cand, seed, cand_base, n_cand_global):
-        """Host-side packing of one level (numpy, vectorised over ids)."""
+    def _build_numpy(self, problems, n_cand, seed, cand_base, n_cand_global):
+        """Host-side packing of one level in numpy — the specification that
+        the native packer (tpe_host_pack_level) is tested against."""
         f64 = self.precision == 'fp64'
         T = self.tile
+        P_all = sum(len(lp.ids) for lp in problems)
+        pbits = int(math.ceil(math.log2(P_all))) if P_all > 1 else 0
+        key_bits = max(5, 8 - pbits)
         comp32, comp64, samp, grids = [], [], [], []
         n32 = n64 = ns = ngrid = 0
         rows = []                         # per LevelProblem: (table info)
@@ -148,7 +128,7 @@ class Engine(object):
             klo, khi = _coord_range(post)
             info = dict(wide_off=0, wide_len=0, grid_off=0, grid_n=0, prior_mu=0.0, prior_a=0.0, prior_c=0.0,
                         narrow_cmax=0.0, narrow_amin=0.0, grid_lo=0.0, grid_inv=0.0, key_lo=klo,
-                        key_inv=(1 << N.KEY_BITS) / (khi - klo) if khi > klo else 0.0,
+                        key_inv=(1 << key_bits) / (khi - klo) if khi > klo else 0.0,
                         family=fam, flags=(N.F_HAS_LOW if post.low is not None else 0)
                         | (N.F_HAS_HIGH if post.high is not None else 0),
                         low=post.low if post.low is not None else 0.0,
@@ -290,6 +270,49 @@ class Engine(object):
                     grid=np.concatenate(grids) if grids else np.zeros(1, np.int32),
                     samp=np.concatenate(samp) if samp else np.zeros((0, 8)), P=P)
 
+    # ---------------------------------------------------------------- pack
+    def _pack(self, problems, n_cand, seed, cand_base, n_cand_global):
+        """Pack one level with the native host runtime straight into the pinned
+        staging buffer; returns (PackInfo, blob bytes)."""
+        n = len(problems)
+        labels = (N.LabelIn * max(n, 1))()
+        keep = []
+        for i, lp in enumerate(problems):
+            post, L = lp.post, labels[i]
+            L.family, L.upper, L.label_ix = post.family, int(post.upper), lp.label_ix
+            L.flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)
+            L.low = post.low if post.low is not None else 0.0
+            L.high = post.high if post.high is not None else 0.0
+            L.q = post.q if post.q is not None else 0.0
+            for side in ('below', 'above'):
+                arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in getattr(post, side)]
+                keep.append(arrs)
+                setattr(L, side + '_w', arrs[0].ctypes.data)
+                if len(arrs) == 3:
+                    setattr(L, side + '_mu', arrs[1].ctypes.data)
+                    setattr(L, side + '_sigma', arrs[2].ctypes.data)
+                setattr(L, side + '_k', len(arrs[0]))
+            ids = np.ascontiguousarray(lp.ids, dtype=np.int64)
+            keep.append(ids)
+            L.ids, L.n_ids = ids.ctypes.data, len(ids)
+        info = N.PackInfo()
+        prec = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
+        seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
+        ncg = int(n_cand_global) if n_cand_global is not None else 0
+        for attempt in range(2):
+            host = self._pinned
+            cap = host.numel() if host is not None else 0
+            rc = self.lib.tpe_host_pack_level(labels, n, int(n_cand), seed64, int(cand_base), ncg, prec,
+                                              host.data_ptr() if host is not None else None, cap,
+                                              ctypes.byref(info))
+            if rc == N.E_SPACE:
+                self._pinned = torch.empty(max(info.blob_bytes, 2 * cap), dtype=torch.uint8,
+                                           pin_memory=torch.cuda.is_available())
+                continue
+            N.check(rc, self.lib, 'tpe_host_pack_level')
+            break
+        return info
+
     # ---------------------------------------------------------------- run
     def run(self, problems, n_cand, seed, cand_base=0, want_lg=False, return_cand=False, n_cand_global=None):
         """Sample, score and select every problem of one level.
@@ -299,20 +322,28 @@ class Engine(object):
         n_cand = int(n_cand)
         if n_cand < 0 or n_cand >= 2 ** 31:
             raise ValueError('n_EI_candidates out of range: %r' % n_cand)
-        tb = self._build(problems, n_cand, seed, cand_base, n_cand_global)
-        P = tb['P']
+        info = self._pack(problems, n_cand, seed, cand_base, n_cand_global)
+        P = int(info.n_problems)
         if P == 0:
             return np.zeros(0, dtype=N.RESULT_DTYPE)
         C_total = P * n_cand
-        p_prob, p_tiles, p_work, p_c32, p_c64, p_samp, p_grid = self._upload_blob(
-            [tb['prob'], tb['tiles'], tb['work'], tb['comp32'], tb['comp64'], tb['samp'], tb['grid']])
         if C_total >= 2 ** 32:
             raise ValueError('more than 2^32 candidates in one level: shard the batch')
+        nbytes = int(info.blob_bytes)
+        dev = self._buf('blob', nbytes, torch.uint8)
+        dev[:nbytes].copy_(self._pinned[:nbytes], non_blocking=True)
+        base = dev.data_ptr()
+        prob = np.frombuffer(self._pinned.numpy(), dtype=N.PROBLEM_DTYPE, count=P, offset=int(info.off_problems))
+        d_cand = self._buf('cand', C_total, torch.float64)
+        d_coord = self._buf('coord', C_total, torch.float32)
+        d_part = self._buf('part', info.part_total, torch.float64)
+        n_tiles = int(info.n_tiles)
+        d_best = self._buf('best', n_tiles * 4, torch.float64)
+        d_res = self._buf('result', P * 6, torch.float64)
         d_keys = self._buf('keys', C_total, torch.int32)
         d_vals = self._buf('vals', C_total, torch.int32)
         # sort only when some problem of the level prunes its above mixture
-        pbits = int(math.ceil(math.log2(P))) if P > 1 else 0
-        sort = bool(np.any(tb['prob']['narrow_amin'] > 0)) and N.KEY_BITS + pbits <= 32
+        sort = info.sort_end_bit > 0
         if sort:
             d_keys_s = self._buf('keys_sorted', C_total, torch.int32)
             d_vals_s = self._buf('vals_sorted', C_total, torch.int32)
@@ -322,24 +353,18 @@ class Engine(object):
             d_sort = self._buf('sort_tmp', ws.value, torch.uint8)
         else:
             d_keys_s, d_vals_s, d_sort = d_keys, d_vals, None
-        d_cand = self._buf('cand', C_total, torch.float64)
-        d_coord = self._buf('coord', C_total, torch.float32)
-        d_part = self._buf('part', tb['part_total'], torch.float64)
-        n_tiles = tb['tiles'].shape[0]
-        d_best = self._buf('best', n_tiles * 4, torch.float64)
-        d_res = self._buf('result', P * 6, torch.float64)
         inject = any(lp.inject is not None for lp in problems)
         if inject:
             if not all(lp.inject is not None for lp in problems):
                 raise ValueError('either every problem of a level injects candidates or none does')
             cand = np.concatenate([np.asarray(lp.inject, dtype=np.float64).reshape(len(lp.ids), n_cand)
                                    for lp in problems]).reshape(-1)
-            fam = np.repeat(tb['prob']['family'], n_cand)
+            fam = np.repeat(prob['family'], n_cand)
             with np.errstate(divide='ignore', invalid='ignore'):
                 coord = np.where((fam == N.FAM_LOGGAUSS) | (fam == N.FAM_QLOGGAUSS), np.log(cand), cand)
             cat = fam == N.FAM_CATEGORICAL
             if cat.any():
-                upper = np.repeat(tb['prob']['n_upper'], n_cand)[cat]
+                upper = np.repeat(prob['n_upper'], n_cand)[cat]
                 cv = cand[cat]
                 if np.any((cv < 0) | (cv >= upper) | (cv != np.floor(cv))):
                     raise IndexError('categorical candidate out of range')
@@ -350,20 +375,21 @@ class Engine(object):
             d_l = self._buf('l_out', C_total, torch.float64)
             d_g = self._buf('g_out', C_total, torch.float64)
         b = N.Batch()
-        b.problems, b.n_problems = p_prob, P
+        b.problems, b.n_problems = base + info.off_problems, P
         b.precision = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
         b.sample = 0 if inject else 1
-        b.sort_end_bit = N.KEY_BITS + pbits if sort else 0
-        b.comp32, b.comp64, b.samp, b.grid = p_c32, p_c64, p_samp, p_grid
+        b.sort_end_bit, b.key_bits = info.sort_end_bit, info.key_bits
+        b.comp32, b.comp64 = base + info.off_comp32, base + info.off_comp64
+        b.samp, b.grid = base + info.off_samp, base + info.off_grid
         b.keys, b.vals = d_keys.data_ptr(), d_vals.data_ptr()
         b.keys_sorted, b.vals_sorted = d_keys_s.data_ptr(), d_vals_s.data_ptr()
         if d_sort is not None:
             b.sort_tmp, b.sort_tmp_bytes = d_sort.data_ptr(), d_sort.numel()
         b.total_cand = C_total
         b.cand, b.coord = d_cand.data_ptr(), d_coord.data_ptr()
-        b.tiles, b.n_tiles = p_tiles, n_tiles
-        b.work = p_work
-        b.n_work_cont, b.n_work_qgauss, b.n_work_qlog = tb['counts_w']
+        b.tiles, b.n_tiles = base + info.off_tiles, n_tiles
+        b.work = base + info.off_work
+        b.n_work_cont, b.n_work_qgauss, b.n_work_qlog = info.n_work_cont, info.n_work_qgauss, info.n_work_qlog
         b.part = d_part.data_ptr()
         b.l_out = d_l.data_ptr() if d_l is not None else None
         b.g_out = d_g.data_ptr() if d_g is not None else None
@@ -372,6 +398,7 @@ class Engine(object):
         if self.profile is None:
             N.check(self.lib.tpe_run_batch(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, 'tpe_run_batch')
         else:
+            tb = dict(prob=prob.copy(), counts_w=[info.n_work_cont, info.n_work_qgauss, info.n_work_qlog], P=P)
             self._run_profiled(b, stream, tb, n_cand)
         res = d_res[:P * 6].cpu().numpy().view(N.RESULT_DTYPE).copy()
         if not (want_lg or return_cand):
@@ -383,7 +410,6 @@ class Engine(object):
             out.append(d_l[:C_total].cpu().numpy().reshape(P, n_cand).copy())
             out.append(d_g[:C_total].cpu().numpy().reshape(P, n_cand).copy())
         return tuple(out)
-
 
     def _run_profiled(self, b, stream, tb, n_cand):
         """The same launches as tpe_run_batch, one stage at a time, bracketed

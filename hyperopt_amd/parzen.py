@@ -34,7 +34,26 @@ def linear_forgetting_weights(n, lf):
 
 
 def fit_parzen(obs, prior_weight, prior_mu, prior_sigma, lf=DEFAULT_LF):
-    """Adaptive Parzen mixture (w, mu, sigma), mu sorted ascending.
+    """Adaptive Parzen mixture (w, mu, sigma), mu sorted ascending — native
+    (tpe_host_fit_parzen) with numpy's own argsort permutation."""
+    obs = np.ascontiguousarray(obs, dtype=np.float64)
+    n = obs.shape[0]
+    order = np.argsort(obs) if n >= 2 else None
+    w = np.empty(n + 1)
+    mu = np.empty(n + 1)
+    sigma = np.empty(n + 1)
+    lib = N.load()
+    pos = lib.tpe_host_fit_parzen(obs.ctypes.data, n, order.ctypes.data if order is not None else None,
+                                  float(prior_weight), float(prior_mu), float(prior_sigma), int(lf or 0),
+                                  w.ctypes.data, mu.ctypes.data, sigma.ctypes.data)
+    if pos < 0:
+        raise AssertionError('non-positive Parzen bandwidth (prior_sigma=%r)' % prior_sigma)
+    return w, mu, sigma
+
+
+def fit_parzen_numpy(obs, prior_weight, prior_mu, prior_sigma, lf=DEFAULT_LF):
+    """Adaptive Parzen mixture (w, mu, sigma), mu sorted ascending — numpy
+    version (the specification the native fit is tested against).
 
     Same semantics and float64 operation order as tpe.py:398-475: the prior is
     inserted at ``searchsorted`` (left) among the sorted observations, each
@@ -134,6 +153,18 @@ class Posterior(object):
 
 
 def _cat_probs(dist, args, obs, prior_weight, lf):
+    upper = int(args['upper'])
+    obs = np.ascontiguousarray(obs, dtype=np.int64)
+    p = None if dist == 'randint' else np.ascontiguousarray(args['p'], dtype=np.float64)
+    out = np.empty(upper)
+    rc = N.load().tpe_host_cat_probs(obs.ctypes.data, len(obs), upper, p.ctypes.data if p is not None else None,
+                                     float(prior_weight), int(lf or 0), out.ctypes.data)
+    if rc != 0:
+        raise IndexError('categorical observation out of range [0, %d)' % upper)
+    return out
+
+
+def _cat_probs_numpy(dist, args, obs, prior_weight, lf):
     upper = int(args['upper'])
     lfw = linear_forgetting_weights(len(obs), lf)
     if len(obs):

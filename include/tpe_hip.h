@@ -54,7 +54,7 @@ enum {
 enum { TPE_PREC_F32 = 0, TPE_PREC_F64 = 1 };
 
 /* error codes */
-enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3 };
+enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE = -4 };
 
 /*
  * One problem (192 bytes).  Component tables (device, caller-owned):
@@ -108,7 +108,7 @@ typedef struct tpe_problem {
   double above_base;     /* additive constant of the above lpdf                */
   float prior_mu, prior_a, prior_c, narrow_cmax;
   float narrow_amin, grid_lo, grid_inv;
-  float key_lo, key_inv; /* sort-key buckets: floor((t - key_lo) * key_inv), 4096 per problem */
+  float key_lo, key_inv; /* sort-key bucket of t: floor((t - key_lo) * key_inv)  */
   float reserved_f;
   uint32_t key0, key1;   /* Philox-4x32-10 key (suggest seed)                  */
   uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
@@ -150,13 +150,15 @@ typedef struct tpe_batch {
   int32_t precision;     /* TPE_PREC_F32 | TPE_PREC_F64                         */
   int32_t sample;        /* 1: draw candidates on device (Philox); 0: caller filled cand/coord */
   int32_t sort_end_bit;  /* keys sorted on bits [0, sort_end_bit); 0 = no sort  */
+  int32_t key_bits;      /* value-bucket bits of the sort key (problem << key_bits | bucket) */
+  int32_t reserved0;
   const float* comp32;   /* [n][4]                                             */
   const double* comp64;  /* [n][4]                                             */
   const double* samp;    /* [n][8]                                             */
   const int32_t* grid;   /* pruning grids                                      */
   double* cand;          /* [total_cand] candidate values (returned to the user) */
   float* coord;          /* [total_cand] kernel coordinate t in f32 (x or ln x) */
-  uint32_t* keys;        /* [total_cand] (problem << 12 | value bucket of t)    */
+  uint32_t* keys;        /* [total_cand] (problem << key_bits | value bucket of t) */
   uint32_t* vals;        /* [total_cand] candidate position                    */
   uint32_t* keys_sorted; /* [total_cand] (== keys when not sorting)            */
   uint32_t* vals_sorted; /* [total_cand]                                        */
@@ -200,6 +202,48 @@ int tpe_sort(const tpe_batch* batch, void* stream);
 int tpe_score_above(const tpe_batch* batch, void* stream);
 int tpe_finalize(const tpe_batch* batch, void* stream);
 int tpe_select(const tpe_batch* batch, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Native host runtime (tpe_host.cpp): the Parzen fit and the packing of one
+ * tree level into the tables above.  Host pointers only.
+ * ---------------------------------------------------------------------- */
+
+/* one hyperparameter of a level: its fitted posterior and the new_ids it is
+ * active for (mixtures are float64 host arrays; categorical: below_w / above_w
+ * are the probabilities, *_k = number of categories) */
+typedef struct tpe_label_in {
+  int32_t family, flags, upper, label_ix;
+  double low, high, q;
+  const double* below_w; const double* below_mu; const double* below_sigma; int64_t below_k;
+  const double* above_w; const double* above_mu; const double* above_sigma; int64_t above_k;
+  const int64_t* ids; int64_t n_ids;
+} tpe_label_in;
+
+/* where tpe_host_pack_level put each table in the blob (byte offsets) */
+typedef struct tpe_pack_info {
+  int64_t off_problems, off_tiles, off_work, off_comp32, off_comp64, off_samp, off_grid;
+  int64_t n_problems, n_tiles;
+  int32_t n_work_cont, n_work_qgauss, n_work_qlog, any_pruned;
+  int64_t part_total, blob_bytes;
+  int32_t key_bits, sort_end_bit;   /* sort-key layout for tpe_batch (sort_end_bit 0: no sort) */
+} tpe_pack_info;
+
+/* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation
+ * `order` of obs (np.argsort; may be NULL when n < 2).  Writes n+1 components
+ * (w, mu, sigma) sorted by mu; returns the prior's position or a TPE_E* code. */
+int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, double prior_weight,
+                            double prior_mu, double prior_sigma, int32_t lf, double* w, double* mu, double* sigma);
+
+/* categorical posterior (tpe.py:573-607): p_prior NULL = randint pseudo-counts,
+ * else pchoice's counts + upper * prior_weight * p_prior */
+int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
+                       int32_t lf, double* out);
+
+/* pack one tree level into `blob` (all tables, 256-B aligned, ready for one
+ * host->device copy); TPE_E_SPACE (info->blob_bytes = size needed) if too small */
+int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
+                        int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
+                        tpe_pack_info* info);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,96 @@
+"""The native host runtime (tpe_host.cpp) against its numpy specification:
+bit-exact Parzen fits and categorical posteriors, and the packed level tables
+equal to the numpy packer (no GPU needed)."""
+import numpy as np
+import pytest
+
+from hyperopt_amd import _native as N
+from hyperopt_amd import parzen
+from hyperopt_amd.engine import Engine, LevelProblem
+
+
+def _cases():
+    rs = np.random.RandomState(0)
+    yield np.zeros(0), 1.0, 0.5, 1.0
+    yield np.array([0.3]), 1.0, 0.5, 1.0
+    yield np.array([0.7]), 1.0, 0.5, 1.0
+    yield np.array([0.5, 0.5]), 2.0, 0.5, 1.0
+    for n in (2, 3, 24, 25, 26, 27, 100, 1000, 8191, 8192, 8193, 20000):
+        yield rs.uniform(-3, 3, n), 1.0, 0.0, 6.0
+        yield np.round(rs.uniform(0, 20, n)), 1.0, 10.0, 20.0        # ties everywhere
+        yield rs.normal(0, 1, n) * 1e-3, 0.5, 1.0, 2.0                  # prior far right
+
+
+def test_native_fit_matches_numpy_bit_exact():
+    for obs, pw, pmu, psig in _cases():
+        a = parzen.fit_parzen(obs, pw, pmu, psig)
+        b = parzen.fit_parzen_numpy(obs, pw, pmu, psig)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_native_cat_probs_match_numpy_bit_exact():
+    rs = np.random.RandomState(1)
+    for n in (0, 1, 24, 25, 26, 300, 9000):
+        for upper in (2, 5, 17):
+            obs = rs.randint(0, upper, n)
+            for dist, args in (('randint', dict(upper=upper)),
+                               ('categorical', dict(upper=upper, p=list(rs.dirichlet(np.ones(upper)))))):
+                a = parzen._cat_probs(dist, args, obs, 1.0, 25)
+                b = parzen._cat_probs_numpy(dist, args, obs, 1.0, 25)
+                np.testing.assert_array_equal(a, b)
+    with pytest.raises(IndexError):
+        parzen._cat_probs('randint', dict(upper=3), np.array([0, 3]), 1.0, 25)
+
+
+def _engine(precision):
+    e = Engine.__new__(Engine)
+    e.lib, e.tile, e.precision, e._pinned, e._bufs, e.profile = N.load(), 2048, precision, None, {}, None
+    return e
+
+
+def _blob(e, info, off, dtype, count):
+    return np.frombuffer(e._pinned.numpy(), dtype=dtype, count=count, offset=int(off))
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'fp64'])
+def test_native_pack_matches_numpy_packer(precision):
+    rs = np.random.RandomState(2)
+    posts = [parzen.fit_posterior('loguniform', dict(low=-5.0, high=5.0), np.exp(rs.uniform(-5, 5, 20)),
+                                  np.exp(rs.uniform(-5, 5, 3000)), 1.0),
+             parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 5), rs.uniform(-1, 2, 40), 1.0),
+             parzen.fit_posterior('normal', dict(mu=0.0, sigma=2.0), rs.normal(0, 2, 9), rs.normal(0, 2, 500), 1.0),
+             parzen.fit_posterior('quniform', dict(low=0.0, high=10.0, q=1.0), np.round(rs.uniform(0, 10, 9)),
+                                  np.round(rs.uniform(0, 10, 300)), 1.0),
+             parzen.fit_posterior('qlognormal', dict(mu=1.0, sigma=0.5, q=0.25),
+                                  np.round(np.exp(rs.normal(1, .5, 9)) / .25) * .25,
+                                  np.round(np.exp(rs.normal(1, .5, 90)) / .25) * .25, 1.0),
+             parzen.fit_posterior('categorical', dict(p=[.2, .3, .5], upper=3), rs.randint(0, 3, 9),
+                                  rs.randint(0, 3, 90), 1.0)]
+    lps = [LevelProblem(p, i + 3, np.arange(i + 1) + 100) for i, p in enumerate(posts)]
+    e = _engine(precision)
+    for C in (24, 5000):
+        ref = e._build_numpy(lps, C, 77, 10, None)
+        info = e._pack(lps, C, 77, 10, None)
+        P = ref['P']
+        assert info.n_problems == P and info.n_tiles == len(ref['tiles'])
+        assert [info.n_work_cont, info.n_work_qgauss, info.n_work_qlog] == ref['counts_w']
+        assert info.part_total == ref['part_total']
+        prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, P)
+        for f in N.PROBLEM_DTYPE.names:
+            if f in ('reserved', 'reserved_f'):
+                continue
+            np.testing.assert_allclose(prob[f].astype(float), ref['prob'][f].astype(float), rtol=1e-6, atol=0,
+                                       err_msg=f)
+        np.testing.assert_array_equal(_blob(e, info, info.off_tiles, N.TILE_DTYPE, info.n_tiles), ref['tiles'])
+        nw = sum(ref['counts_w'])
+        np.testing.assert_array_equal(_blob(e, info, info.off_work, N.WORK_DTYPE, nw), ref['work'])
+        c32 = _blob(e, info, info.off_comp32, np.float32, ref['comp32'].size)
+        np.testing.assert_allclose(c32, ref['comp32'].reshape(-1), rtol=1e-6, atol=1e-6)
+        c64 = _blob(e, info, info.off_comp64, np.float64, ref['comp64'].size)
+        np.testing.assert_allclose(c64, ref['comp64'].reshape(-1), rtol=1e-12, atol=0)
+        smp = _blob(e, info, info.off_samp, np.float64, ref['samp'].size)
+        np.testing.assert_allclose(smp, ref['samp'].reshape(-1), rtol=1e-12, atol=1e-300)
+        if precision == 'fp32':
+            g = _blob(e, info, info.off_grid, np.int32, ref['grid'].size)
+            np.testing.assert_array_equal(g, ref['grid'])
