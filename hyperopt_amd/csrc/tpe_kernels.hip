@@ -319,8 +319,12 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
       const int bl = (int)fminf(fmaxf(floorf(gl) - 1.f, 0.f), (float)p.grid_n);
       const int bh = (int)fminf(fmaxf(floorf(gh) + 2.f, 0.f), (float)p.grid_n);
       const int32_t* G = grid + p.grid_off;
-      k_lo = max(k_lo, G[bl]);
-      k_hi = min(k_hi, G[bh]);
+      // pruned problems split the wave's WINDOW (not the whole mixture) over the
+      // work items of this tile, so every work item gets an equal share
+      const int wl = G[bl], wh = max(G[bh], G[bl]);
+      const long long len = wh - wl;
+      k_lo = wl + (int)((len * w.split) / p.n_splits);
+      k_hi = wl + (int)((len * (w.split + 1)) / p.n_splits);
     }
   }
   k_lo = __builtin_amdgcn_readfirstlane(k_lo);

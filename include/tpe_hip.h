@@ -76,7 +76,9 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  * lb = prior_c - (prior_a * max|t - prior_mu|)^2 a lower bound of log2 s(t):
  * every skipped term is < 2^-45 of the sum.  grid[grid_off .. +grid_n] maps
  * value buckets (grid_lo + g / grid_inv) to the first sorted component with
- * mu >= the bucket edge.  narrow_amin <= 0 disables pruning.
+ * mu >= the bucket edge.  narrow_amin <= 0 disables pruning.  With pruning,
+ * work item `split` of a tile evaluates the split-th of n_splits equal parts
+ * of each wave's window (k_start/k_end are ignored).
  *
  * samp[k] = double[8] {cum, mu, sigma, fa, fb, flip, 0, 0}: below-mixture
  * sampler table; cum = selection CDF (∝ w_k * mass_k when bounded); fa, fb =
