@@ -22,7 +22,7 @@ def build(force=False, verbose=False):
     host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
     dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o')
     cmds = [
-        [gxx, '-O2', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall', '-c', HOST_SRC,
+        [gxx, '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall', '-c', HOST_SRC,
          '-o', host_o],
         [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
          '-Wno-unused-command-line-argument', '-c', SRC, '-o', dev_o],

@@ -105,15 +105,21 @@ double p_accept(const double* w, const double* mu, const double* sg, int64_t k, 
   return np_sum(t.data(), k);
 }
 
-struct Blob {
-  std::vector<unsigned char> data;
-  int64_t add(const void* p, int64_t bytes) {
-    int64_t off = ((int64_t)data.size() + 255) & ~(int64_t)255;
-    data.resize((size_t)(off + bytes));
-    if (bytes) memcpy(data.data() + off, p, (size_t)bytes);
-    return off;
-  }
-};
+// log2 via frexp + atanh series (|s| <= 0.1716: truncation < 1e-11), ~4x
+// cheaper than libm; used only for the f32 component tables
+inline double fast_log2(double x) {
+  if (!(x > 0) || !std::isfinite(x) || x < 2.2250738585072014e-308) return log2(x);
+  uint64_t u;
+  memcpy(&u, &x, 8);
+  int e = (int)((u >> 52) & 0x7FF) - 1022;          // x = m * 2^e, m in [0.5, 1)
+  u = (u & 0x000FFFFFFFFFFFFFull) | 0x3FE0000000000000ull;
+  double m;
+  memcpy(&m, &u, 8);
+  if (m < 0.70710678118654752) { m *= 2.0; e -= 1; }
+  const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+  const double p = s * (2.0 + s2 * (2.0 / 3 + s2 * (2.0 / 5 + s2 * (2.0 / 7 + s2 * (2.0 / 9 + s2 * (2.0 / 11))))));
+  return (double)e + p * 1.4426950408889634074;
+}
 
 }  // namespace
 
@@ -196,8 +202,14 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<double> samp;      // 8 doubles per row
   std::vector<int32_t> grid;
   std::vector<tpe_problem> lab((size_t)n_labels);
-  int64_t P = 0;
-  for (int32_t li = 0; li < n_labels; ++li) P += labels[li].n_ids;
+  int64_t P = 0, ktot = 0;
+  for (int32_t li = 0; li < n_labels; ++li) {
+    P += labels[li].n_ids;
+    ktot += labels[li].below_k + labels[li].above_k + kPruneWide;
+  }
+  comp32.reserve((size_t)(4 * ktot));
+  comp64.reserve((size_t)(4 * ktot));
+  samp.reserve((size_t)(8 * ktot));
   // sort key = problem << key_bits | value bucket: keep it within one 8-bit radix
   // pass up to 8 problems, never below 32 buckets per problem
   int pbits = 0;
@@ -291,8 +303,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         double shift = -INFINITY;
         for (int64_t i = 0; i < k; ++i) {
           const double se = np_max(sg[i], kEPS);
-          const double lc = logf ? log(w[i] / (se * sqrt(2 * M_PI))) : log(w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa);
-          c[i] = lc * kLog2e;
+          const double arg = logf ? w[i] / (se * sqrt(2 * M_PI)) : w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa;
+          c[i] = f64 ? log(arg) * kLog2e : fast_log2(arg);
           a[i] = sqrt(0.5 * kLog2e) / se;
           if (c[i] > shift && std::isfinite(c[i])) shift = c[i];
         }
@@ -317,13 +329,18 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           wide.assign(idx.begin(), idx.begin() + kPruneWide);
         }
         off = (int32_t)(comp32.size() / 4); len = (int32_t)k;
+        {
+          const size_t b0 = comp32.size();
+          comp32.resize(b0 + 4 * (size_t)k);
+          float* r = comp32.data() + b0;
+          for (int64_t i = 0; i < k; ++i, r += 4) {
+            const float hi = (float)mu[i];
+            r[0] = hi; r[1] = (float)(mu[i] - (double)hi); r[2] = (float)a[i]; r[3] = (float)c[i];
+          }
+          for (int64_t i : wide) comp32[b0 + 4 * (size_t)i + 3] = -INFINITY;
+        }
         std::vector<char> is_wide((size_t)k, 0);
         for (int64_t i : wide) is_wide[i] = 1;
-        for (int64_t i = 0; i < k; ++i) {
-          const float hi = (float)mu[i];
-          const float row[4] = {hi, (float)(mu[i] - (double)hi), (float)a[i], is_wide[i] ? -INFINITY : (float)c[i]};
-          comp32.insert(comp32.end(), row, row + 4);
-        }
         if (!wide.empty()) {
           p.wide_off = (int32_t)(comp32.size() / 4);
           p.wide_len = (int32_t)wide.size();
@@ -412,16 +429,21 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
     counts[gi] = (int32_t)(work.size() - before);
   }
-  // ---- blob ----
-  Blob B;
-  info->off_problems = B.add(prob.data(), (int64_t)(prob.size() * sizeof(tpe_problem)));
-  info->off_tiles = B.add(tiles.data(), (int64_t)(tiles.size() * sizeof(tpe_tile)));
-  info->off_work = B.add(work.data(), (int64_t)(work.size() * sizeof(tpe_work)));
-  info->off_comp32 = B.add(comp32.data(), (int64_t)(comp32.size() * sizeof(float)));
-  info->off_comp64 = B.add(comp64.data(), (int64_t)(comp64.size() * sizeof(double)));
-  info->off_samp = B.add(samp.data(), (int64_t)(samp.size() * sizeof(double)));
+  // ---- blob: sections at 256-B aligned offsets, written straight into the caller's buffer ----
   if (grid.empty()) grid.push_back(0);
-  info->off_grid = B.add(grid.data(), (int64_t)(grid.size() * sizeof(int32_t)));
+  const void* src[7] = {prob.data(), tiles.data(), work.data(), comp32.data(), comp64.data(), samp.data(),
+                        grid.data()};
+  const int64_t len[7] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
+                          (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp32.size() * sizeof(float)),
+                          (int64_t)(comp64.size() * sizeof(double)), (int64_t)(samp.size() * sizeof(double)),
+                          (int64_t)(grid.size() * sizeof(int32_t))};
+  int64_t off[7], end = 0;
+  for (int i = 0; i < 7; ++i) {
+    off[i] = (end + 255) & ~(int64_t)255;
+    end = off[i] + len[i];
+  }
+  info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp32 = off[3];
+  info->off_comp64 = off[4]; info->off_samp = off[5]; info->off_grid = off[6];
   info->n_problems = P;
   info->n_tiles = (int64_t)tiles.size();
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
@@ -429,9 +451,10 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->key_bits = key_bits;
   info->sort_end_bit = any_pruned ? sort_end_bit : 0;
   info->part_total = part_total;
-  info->blob_bytes = (int64_t)B.data.size();
-  if (!blob || blob_cap < info->blob_bytes) return TPE_E_SPACE;
-  memcpy(blob, B.data.data(), B.data.size());
+  info->blob_bytes = end;
+  if (!blob || blob_cap < end) return TPE_E_SPACE;
+  for (int i = 0; i < 7; ++i)
+    if (len[i]) memcpy((unsigned char*)blob + off[i], src[i], (size_t)len[i]);
   return TPE_OK;
 }
 

@@ -165,12 +165,24 @@ def extract(domain, trials):
 def split_below(history, gamma, gamma_cap=25):
     """Tids of the ``n_below`` best losses (ap_filter_trials, tpe.py:625-629).
 
-    ``np.argsort`` on the same float64 loss array as the reference gives the
-    same order, including among tied losses."""
-    n = len(history.losses)
+    The below set only depends on WHICH losses are smallest, so an O(N)
+    ``np.argpartition`` gives it exactly unless the loss at the boundary is
+    tied with one outside it; then the reference's ``np.argsort`` order (same
+    numpy call on the same float64 array) decides, as in the reference."""
+    losses = history.losses
+    n = len(losses)
     n_below = min(int(np.ceil(gamma * np.sqrt(n))), gamma_cap)
-    order = np.argsort(history.losses)
-    return history.tids[order[:n_below]]
+    if n_below <= 0:
+        return history.tids[:0]
+    if n_below >= n:
+        return history.tids.copy()
+    part = np.argpartition(losses, n_below - 1)
+    kth = losses[part[n_below - 1]]
+    rest = losses[part[n_below:]]
+    if np.isnan(kth) or np.any(rest == kth) or np.isnan(losses).any():
+        order = np.argsort(losses)
+        return history.tids[order[:n_below]]
+    return history.tids[part[:n_below]]
 
 
 def below_mask(obs_tids, below_tids):
