@@ -16,6 +16,7 @@
 
 #include <cmath>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -30,7 +31,15 @@ constexpr double kLog2e = 1.4426950408889634074;
 constexpr double kLn2 = 0.69314718055994530942;
 constexpr int kPruneMinK = 64;
 constexpr int kPruneWide = 16;
-constexpr int kTargetWork = 2048;
+// above-mixture work items per level (>= 8 per CU); TPE_TARGET_WORK overrides (tuning)
+int target_work() {
+  static int v = [] {
+    const char* e = getenv("TPE_TARGET_WORK");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 2048;
+  }();
+  return v;
+}
 constexpr int kMinComponentsPerSplit = 128;
 
 // numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src)
@@ -394,7 +403,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
   const int64_t scored_tiles = scored * ((C_ref + T - 1) / T);
-  const int64_t target = std::max<int64_t>(1, (kTargetWork + std::max<int64_t>(scored_tiles, 1) - 1) /
+  const int64_t target = std::max<int64_t>(1, (target_work() + std::max<int64_t>(scored_tiles, 1) - 1) /
                                                   std::max<int64_t>(scored_tiles, 1));
   int64_t part_total = 0;
   bool any_pruned = false;

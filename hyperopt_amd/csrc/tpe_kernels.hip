@@ -193,6 +193,21 @@ __device__ __forceinline__ void q_bounds(const tpe_problem& p, double x, double&
   }
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// one component against kR candidates held as kR/2 packed pairs:
+// s += 2^(c - (a ((t - mu_hi) - mu_lo))^2)
+__device__ __forceinline__ void ce_step(const float4 c, const f2 (&t)[kR / 2], f2 (&s)[kR / 2]) {
+  const f2 mh = f2{c.x, c.x}, ml = f2{c.y, c.y}, a = f2{c.z, c.z}, cw = f2{c.w, c.w};
+#pragma unroll
+  for (int j = 0; j < kR / 2; ++j) {
+    const f2 d = (t[j] - mh) - ml;
+    const f2 z = d * a;
+    const f2 v = cw - z * z;
+    s[j] += f2{__builtin_amdgcn_exp2f(v.x), __builtin_amdgcn_exp2f(v.y)};
+  }
+}
+
 // sorted position of candidate j (0..kR-1) of this lane inside a tile
 __device__ __forceinline__ int tile_pos(int cand_start, int j) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -205,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      const tpe_tile* __restrict__ tiles,
                                                      const double* __restrict__ samp,
                                                      double* __restrict__ cand, float* __restrict__ coord,
-                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                     uint32_t* __restrict__ keys, uint64_t* __restrict__ vals,
                                                      int precision, int draw, int key_bits) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
@@ -273,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     const float gb = floorf((coord[o] - p.key_lo) * p.key_inv);
     const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
     keys[o] = khi | bucket;
-    vals[o] = (uint32_t)o;
+    vals[o] = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(coord[o]);
   }
 }
 
@@ -284,8 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
                                                         const tpe_work* __restrict__ W,
                                                         const float4* __restrict__ comp,
                                                         const int32_t* __restrict__ grid,
-                                                        const float* __restrict__ coord,
-                                                        const uint32_t* __restrict__ vals,
+                                                        const uint64_t* __restrict__ vals,
                                                         double* __restrict__ part,
                                                         unsigned long long* __restrict__ ce_count) {
   const tpe_work w = W[blockIdx.x];
@@ -296,7 +310,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
-    t[j] = i < n ? coord[vals[p.cand_off + i]] : 0.f;
+    t[j] = i < n ? __uint_as_float((uint32_t)vals[p.cand_off + i]) : 0.f;
     if (i < n) { tmin = fminf(tmin, t[j]); tmax = fmaxf(tmax, t[j]); }
     s[j] = 0.f;
   }
@@ -329,29 +343,19 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
   }
   k_lo = __builtin_amdgcn_readfirstlane(k_lo);
   k_hi = __builtin_amdgcn_readfirstlane(k_hi);
+  // candidate pairs in packed f32 (v_pk_add/mul/fma_f32); v_exp_f32 per lane value
+  f2 t2[kR / 2], s2[kR / 2];
+#pragma unroll
+  for (int j = 0; j < kR / 2; ++j) { t2[j] = f2{t[2 * j], t[2 * j + 1]}; s2[j] = f2{0.f, 0.f}; }
   const float4* __restrict__ C = comp + p.above_off;
 #pragma unroll 4
-  for (int k = k_lo; k < k_hi; ++k) {
-    const float4 c = C[k];
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-      const float d = (t[j] - c.x) - c.y;
-      const float z = d * c.z;
-      s[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(-z, z, c.w));
-    }
-  }
+  for (int k = k_lo; k < k_hi; ++k) ce_step(C[k], t2, s2);
   if (w.split == 0) {                  // wide components once per candidate
     const float4* __restrict__ Wd = comp + p.wide_off;
-    for (int k = 0; k < p.wide_len; ++k) {
-      const float4 c = Wd[k];
-#pragma unroll
-      for (int j = 0; j < kR; ++j) {
-        const float d = (t[j] - c.x) - c.y;
-        const float z = d * c.z;
-        s[j] += __builtin_amdgcn_exp2f(__builtin_fmaf(-z, z, c.w));
-      }
-    }
+    for (int k = 0; k < p.wide_len; ++k) ce_step(Wd[k], t2, s2);
   }
+#pragma unroll
+  for (int j = 0; j < kR / 2; ++j) { s[2 * j] = s2[j].x; s[2 * j + 1] = s2[j].y; }
   double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __res
                                                         const tpe_work* __restrict__ W,
                                                         const double4* __restrict__ comp,
                                                         const double* __restrict__ cand,
-                                                        const uint32_t* __restrict__ vals,
+                                                        const uint64_t* __restrict__ vals,
                                                         double* __restrict__ part) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
@@ -386,7 +390,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __res
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
-    const double x = i < n ? cand[vals[p.cand_off + i]] : 1.0;
+    const double x = i < n ? cand[vals[p.cand_off + i] >> 32] : 1.0;
     t[j] = logsp ? log(x) : x;
     s[j] = 0.0;
   }
@@ -413,7 +417,7 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
                                                       const tpe_work* __restrict__ W,
                                                       const double4* __restrict__ comp,
                                                       const double* __restrict__ cand,
-                                                      const uint32_t* __restrict__ vals,
+                                                      const uint64_t* __restrict__ vals,
                                                       double* __restrict__ part) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int i = tile_pos(w.cand_start, h * R + j);
-      const double x = i < n ? cand[vals[p.cand_off + i]] : 0.0;
+      const double x = i < n ? cand[vals[p.cand_off + i] >> 32] : 0.0;
       q_bounds(p, x, tu[j], tl[j]);
       s[j] = 0.0;
     }
@@ -449,8 +453,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        const float4* __restrict__ comp32,
                                                        const double4* __restrict__ comp64,
                                                        const double* __restrict__ cand,
-                                                       const float* __restrict__ coord,
-                                                       const uint32_t* __restrict__ vals,
+                                                       const uint64_t* __restrict__ vals,
                                                        const double* __restrict__ part,
                                                        double* __restrict__ l_out, double* __restrict__ g_out,
                                                        tpe_best* __restrict__ tile_best, int precision) {
@@ -463,7 +466,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
     const int i = tile_pos(tl.cand_start, j);
     if (i >= n) continue;
     const int64_t so = p.cand_off + i;             // sorted position
-    const uint32_t oo = vals[so];                  // original position
+    const uint64_t v = vals[so];
+    const uint32_t oo = (uint32_t)(v >> 32);       // original position
     const int64_t orig = (int64_t)oo - p.cand_off; // original local index
     const double x = cand[oo];
     double l, g;
@@ -490,7 +494,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
       for (int sp = 0; sp < p.n_splits; ++sp) sa += part[p.part_off + (int64_t)sp * n + i];
       double lb2, la2;
       if (precision == TPE_PREC_F32) {
-        const float t = coord[oo];
+        const float t = __uint_as_float((uint32_t)v);
         lb2 = (double)lse2_fixed(comp32, p.below_off, p.below_len, t);
         // fixed-shift sum; if it under-flowed, redo this candidate max-shifted
         la2 = sa > 1e-30 ? log2(sa)
@@ -607,7 +611,7 @@ int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
   if (!bytes || total_cand < 0) return fail(TPE_E_ARG, "bad arguments");
   size_t sz = 0;
   hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
-      nullptr, sz, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+      nullptr, sz, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
       (size_t)total_cand, 0u, 32u, (hipStream_t)0);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
   *bytes = (uint64_t)sz;
@@ -631,7 +635,7 @@ int tpe_sort(const tpe_batch* b, void* stream) {
   if (b->n_tiles == 0 || b->total_cand == 0 || b->sort_end_bit == 0) return TPE_OK;
   size_t sz = (size_t)b->sort_tmp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
-      b->sort_tmp, sz, (const uint32_t*)b->keys, b->keys_sorted, (const uint32_t*)b->vals, b->vals_sorted,
+      b->sort_tmp, sz, (const uint32_t*)b->keys, b->keys_sorted, (const uint64_t*)b->vals, b->vals_sorted,
       (size_t)b->total_cand, 0u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
   if (e != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "tpe_sort: %s (workspace %llu bytes)", hipGetErrorString(e),
@@ -649,7 +653,7 @@ int tpe_score_above(const tpe_batch* b, void* stream) {
   if (n_cont) {
     if (b->precision == TPE_PREC_F32)
       hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
-                         (const float4*)b->comp32, b->grid, b->coord, b->vals_sorted, b->part, b->ce_count);
+                         (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->ce_count);
     else
       hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
                          (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
@@ -668,7 +672,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_tiles == 0) return TPE_OK;
   hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
-                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->coord, b->vals_sorted,
+                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->vals_sorted,
                      b->part, b->l_out, b->g_out, b->tile_best, b->precision);
   return hip_check("tpe_finalize");
 }

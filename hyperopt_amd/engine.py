@@ -341,12 +341,12 @@ class Engine(object):
         d_best = self._buf('best', n_tiles * 4, torch.float64)
         d_res = self._buf('result', P * 6, torch.float64)
         d_keys = self._buf('keys', C_total, torch.int32)
-        d_vals = self._buf('vals', C_total, torch.int32)
+        d_vals = self._buf('vals', C_total, torch.int64)
         # sort only when some problem of the level prunes its above mixture
         sort = info.sort_end_bit > 0
         if sort:
             d_keys_s = self._buf('keys_sorted', C_total, torch.int32)
-            d_vals_s = self._buf('vals_sorted', C_total, torch.int32)
+            d_vals_s = self._buf('vals_sorted', C_total, torch.int64)
             ws = ctypes.c_uint64(0)
             N.check(self.lib.tpe_sort_workspace_bytes(C_total, ctypes.byref(ws)), self.lib,
                     'tpe_sort_workspace_bytes')

@@ -161,9 +161,9 @@ typedef struct tpe_batch {
   double* cand;          /* [total_cand] candidate values (returned to the user) */
   float* coord;          /* [total_cand] kernel coordinate t in f32 (x or ln x) */
   uint32_t* keys;        /* [total_cand] (problem << key_bits | value bucket of t) */
-  uint32_t* vals;        /* [total_cand] candidate position                    */
+  uint64_t* vals;        /* [total_cand] (position << 32) | f32 bits of t       */
   uint32_t* keys_sorted; /* [total_cand] (== keys when not sorting)            */
-  uint32_t* vals_sorted; /* [total_cand]                                        */
+  uint64_t* vals_sorted; /* [total_cand] (== vals when not sorting)            */
   void* sort_tmp; uint64_t sort_tmp_bytes;   /* tpe_sort_workspace_bytes()     */
   int64_t total_cand;
   const tpe_tile* tiles; int32_t n_tiles; int32_t reserved2;
