@@ -38,6 +38,7 @@ constexpr int kTile = kThreads * kR;   // candidates per tile
 constexpr double kEPS = 1e-12;         // tpe.py:25
 constexpr double kLn2 = 0.69314718055994530942;
 constexpr float kPruneBits = 45.f;     // skipped terms are < 2^-45 of the sum
+constexpr int kCumLds = 1024;          // sampler CDF rows staged in LDS
 
 // onesweep radix sort from 1024 keys up (rocPRIM's default switches to a merge
 // sort up to 2^20 keys, ~5x slower here)
@@ -237,6 +238,13 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
   const double* S = samp + 8 * (int64_t)p.samp_off;
   const uint32_t khi = (uint32_t)tl.problem << key_bits;
   const float kmax = (float)((1 << key_bits) - 1);
+  // selection CDF staged in LDS: the per-lane binary search then costs no
+  // dependent global loads (tables longer than kCumLds search global memory)
+  __shared__ double cum_lds[kCumLds];
+  const bool in_lds = draw && p.samp_len <= kCumLds;
+  if (in_lds)
+    for (int q = threadIdx.x; q < p.samp_len; q += kThreads) cum_lds[q] = S[8 * q];
+  __syncthreads();
   for (int j = 0; j < kR; ++j) {
     const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
     if (i >= p.n_cand) break;
@@ -249,7 +257,10 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
         // component choice: first k with u < cum_k (binary search, <= 27 rows)
         const double u1 = u01d(r.x, r.y);
         int a = 0, b = p.samp_len - 1;
-        while (a < b) { const int m = (a + b) >> 1; if (u1 < S[8 * m]) b = m; else a = m + 1; }
+        if (in_lds)
+          while (a < b) { const int m = (a + b) >> 1; if (u1 < cum_lds[m]) b = m; else a = m + 1; }
+        else
+          while (a < b) { const int m = (a + b) >> 1; if (u1 < S[8 * m]) b = m; else a = m + 1; }
         const double* s = S + 8 * a;
         if (p.family == TPE_FAM_CATEGORICAL) {
           cand[o] = (double)a;
@@ -456,7 +467,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        const uint64_t* __restrict__ vals,
                                                        const double* __restrict__ part,
                                                        double* __restrict__ l_out, double* __restrict__ g_out,
-                                                       tpe_best* __restrict__ tile_best, int precision) {
+                                                       tpe_best* __restrict__ tile_best, int precision,
+                                                       int sampled) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   const int n = p.n_cand;
@@ -469,7 +481,10 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
     const uint64_t v = vals[so];
     const uint32_t oo = (uint32_t)(v >> 32);       // original position
     const int64_t orig = (int64_t)oo - p.cand_off; // original local index
-    const double x = cand[oo];
+    // device-drawn continuous candidates: x (or ln x) is the f32 draw itself
+    const bool from_t = sampled && precision == TPE_PREC_F32 &&
+                        (p.family == TPE_FAM_GAUSS || p.family == TPE_FAM_LOGGAUSS);
+    const double x = from_t ? 0.0 : cand[oo];
     double l, g;
     if (p.family == TPE_FAM_CATEGORICAL) {
       const int c = (int)x;
@@ -505,7 +520,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
         lb2 = lse2_exact64(comp64, p.below_off, p.below_len, t);
         la2 = sa > 1e-280 ? log2(sa) : lse2_exact64(comp64, p.above_off, p.above_len, t);
       }
-      const double lnx = logsp ? log(x) : 0.0;
+      const double lnx = !logsp ? 0.0 : (from_t ? (double)__uint_as_float((uint32_t)v) : log(x));
       l = lb2 * kLn2 + p.below_base - lnx;
       g = la2 * kLn2 + p.above_base - lnx;
     }
@@ -673,7 +688,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   if (b->n_tiles == 0) return TPE_OK;
   hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
                      (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->vals_sorted,
-                     b->part, b->l_out, b->g_out, b->tile_best, b->precision);
+                     b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample);
   return hip_check("tpe_finalize");
 }
 
