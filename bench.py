@@ -101,6 +101,94 @@ def cpu_baseline(domain, trials, budget_s=15.0):
                 sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, %.1fs' % (calls, dt))
 
 
+# ---------------------------------------------------------------- other configs
+def soa_history(labels, n, seed, loss_fn):
+    """Synthetic structure-of-arrays history (history.History): every label
+    active in every trial, values ~ U(-5, 5), losses from ``loss_fn``."""
+    from hyperopt_amd.history import History
+    rs = np.random.RandomState(seed)
+    tids = np.arange(n, dtype=np.int64)
+    vals = {k: rs.uniform(-5, 5, n) for k in labels}
+    losses = loss_fn(vals) + 1e-9 * tids
+    return History(tids, losses, {k: (tids, v) for k, v in vals.items()})
+
+
+def flat_uniform_table(labels):
+    from hyperopt_amd import hp
+    from hyperopt_amd.space import ParamTable
+    return ParamTable({k: hp.uniform(k, -5, 5) for k in labels})
+
+
+def mixed10_space(hp):
+    return {'u0': hp.uniform('u0', -5, 5), 'u1': hp.uniform('u1', 0, 1), 'u2': hp.uniform('u2', -1, 3),
+            'l0': hp.loguniform('l0', -5, 0), 'l1': hp.loguniform('l1', -2, 2), 'l2': hp.loguniform('l2', 0, 3),
+            'q0': hp.quniform('q0', 0, 20, 1), 'q1': hp.quniform('q1', -4, 4, 0.5),
+            'c0': hp.choice('c0', list(range(5))), 'c1': hp.choice('c1', list(range(3)))}
+
+
+def config_workload(config, rank, world, args):
+    """(description, setup info, step(i) -> candidate-scores, cpu_baseline_fn or None)"""
+    from hyperopt_amd import base, hp, rand, tpe
+    if config == 1:
+        from hyperopt_amd import Trials, fmin
+
+        def step(i):
+            t = Trials()
+            fmin(lambda x: (x - 3) ** 2, hp.uniform('x', -10, 10), algo=tpe.suggest, max_evals=100, trials=t,
+                 rstate=np.random.RandomState(i))
+            return 80 * 24        # 80 TPE suggests (after 20 start-up) x 24 candidates
+        return 'config1: fmin(tpe.suggest), hp.uniform 1-D quadratic, 100 trials, n_EI_candidates=24', step, None
+    if config == 2:
+        domain = base.Domain(lambda d: 0.0, mixed10_space(hp))
+        trials = base.Trials()
+        rs = np.random.RandomState(SEED)
+        docs = []
+        for tid in range(1000):
+            d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
+            v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
+            d['state'] = base.JOB_STATE_DONE
+            d['result'] = {'status': 'ok', 'loss': sum((float(x) - 0.3) ** 2 for x in v.values()) + 1e-9 * tid}
+            docs.append(d)
+        trials.insert_trial_docs(docs)
+        trials.refresh()
+        C = 10000
+
+        def step(i):
+            docs = tpe.suggest([1000], domain, trials, SEED + i, n_EI_candidates=C * world,
+                               shard=(rank, world) if world > 1 else None)
+            return sum(1 for v in docs[0]['misc']['vals'].values() if v) * C * world
+        return 'config2: 10-dim mixed space, 1000-trial history, n_EI_candidates=10000', step, None
+    if config == 4:
+        labels = ['x%02d' % i for i in range(20)]
+        hist = soa_history(labels, 10000, SEED, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+        table = flat_uniform_table(labels)
+        n_ids, C = 4096, 4096
+        mine = np.arange(10000, 10000 + n_ids)[rank::world]
+
+        def step(i):
+            tpe.suggest_choices(table, hist, mine, SEED + i, n_EI_candidates=C)
+            return len(labels) * n_ids * C          # whole job (every rank does its share)
+        return ('config4: batched suggest, 4096 new_ids x 4096 candidates, 20-dim U(-5,5), 10k-trial '
+                'history, new_ids sharded over ranks'), step, None
+    if config == 5:
+        D, N, C = args.dims, args.history5, 4096
+        labels = ['x%04d' % i for i in range(D)]
+        mine_labels = labels[rank::world]
+        hist = soa_history(mine_labels, N, SEED, lambda v: np.zeros(N))
+        # the loss must be common to all ranks: recompute it from all dims deterministically
+        rs = np.random.RandomState(SEED + 1)
+        hist.losses[:] = rs.uniform(size=N) + 1e-9 * np.arange(N)
+        table = flat_uniform_table(mine_labels)
+
+        def step(i):
+            tpe.suggest_choices(table, hist, [N], SEED + i, n_EI_candidates=C)
+            return D * C
+        return ('config5: %d-dim U(-5,5), %d-trial history, n_EI_candidates=4096, hyperparameters sharded '
+                'over ranks' % (D, N)), step, None
+    raise ValueError(config)
+
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -109,6 +197,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--history', type=int, default=N_HISTORY)
     ap.add_argument('--cands', type=int, default=C_PER_GPU)
+    ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
+    ap.add_argument('--dims', type=int, default=1000, help='config 5 dimensions')
+    ap.add_argument('--history5', type=int, default=100000, help='config 5 history length')
     args = ap.parse_args()
 
     import torch
@@ -125,6 +216,8 @@ def main():
     from hyperopt_amd import engine as engine_mod, tpe
     from hyperopt_amd.engine import get_engine
     get_engine(device)
+    if args.config != 3:
+        return run_other(args, rank, world, device)
     domain, trials = make_history(args.history, SEED)
     new_id = args.history
     shard = (rank, world) if world > 1 else None
@@ -215,6 +308,44 @@ def main():
         }
         if cpu:
             out['speedup_vs_cpu_baseline'] = value / cpu['value']
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_other(args, rank, world, device):
+    """Configs 1, 2, 4, 5: same timing discipline, own metric line."""
+    import torch
+    import torch.distributed as dist
+    desc, step, _ = config_workload(args.config, rank, world, args)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    lat, units = [], 0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        s0 = time.perf_counter()
+        units = step(100 + i)
+        lat.append(time.perf_counter() - s0)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        out = {'metric': 'EI candidates scored/sec (node)', 'value': units * args.steps / elapsed,
+               'unit': 'candidate-scores/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+               'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
+               'scaling': 'strong' if args.config in (4, 5) else 'weak', 'vs_baseline': None, 'dtype': 'f32',
+               'data': 'synthetic', 'config': {'workload': desc, 'config': args.config},
+               'p50_step_ms': 1e3 * float(np.median(lat))}
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -474,17 +474,38 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
   const int n = p.n_cand;
   double bs = 0, bl = 0, bg = 0;
   int64_t bi = -1;
+  // issue every load of this lane's candidates up front (vals, split partial
+  // sums, candidate values) so their latencies overlap
+  const bool from_t = sampled && precision == TPE_PREC_F32 &&
+                      (p.family == TPE_FAM_GAUSS || p.family == TPE_FAM_LOGGAUSS);
+  uint64_t vv[kR];
+  double sav[kR], xv[kR];
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int i = tile_pos(tl.cand_start, j);
+    vv[j] = i < n ? vals[p.cand_off + i] : 0;
+    sav[j] = 0.0;
+  }
+  for (int sp = 0; sp < p.n_splits; ++sp) {
+    const double* __restrict__ ps = part + p.part_off + (int64_t)sp * n;
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const int i = tile_pos(tl.cand_start, j);
+      if (i < n) sav[j] += ps[i];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int i = tile_pos(tl.cand_start, j);
+    xv[j] = (!from_t && i < n) ? cand[(uint32_t)(vv[j] >> 32)] : 0.0;
+  }
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(tl.cand_start, j);
     if (i >= n) continue;
-    const int64_t so = p.cand_off + i;             // sorted position
-    const uint64_t v = vals[so];
+    const uint64_t v = vv[j];
     const uint32_t oo = (uint32_t)(v >> 32);       // original position
     const int64_t orig = (int64_t)oo - p.cand_off; // original local index
-    // device-drawn continuous candidates: x (or ln x) is the f32 draw itself
-    const bool from_t = sampled && precision == TPE_PREC_F32 &&
-                        (p.family == TPE_FAM_GAUSS || p.family == TPE_FAM_LOGGAUSS);
-    const double x = from_t ? 0.0 : cand[oo];
+    const double x = xv[j];
     double l, g;
     if (p.family == TPE_FAM_CATEGORICAL) {
       const int c = (int)x;
@@ -499,14 +520,12 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
       q_bounds(p, x, tu, tlo);
       const double mb = p.family == TPE_FAM_QGAUSS ? qmass<false>(comp64, p.below_off, p.below_len, tu, tlo)
                                                    : qmass<true>(comp64, p.below_off, p.below_len, tu, tlo);
-      double ma = 0.0;
-      for (int sp = 0; sp < p.n_splits; ++sp) ma += part[p.part_off + (int64_t)sp * n + i];
+      const double ma = sav[j];
       l = log(mb) + p.below_base;
       g = log(ma) + p.above_base;
     } else {
       const bool logsp = p.family == TPE_FAM_LOGGAUSS;
-      double sa = 0.0;
-      for (int sp = 0; sp < p.n_splits; ++sp) sa += part[p.part_off + (int64_t)sp * n + i];
+      const double sa = sav[j];
       double lb2, la2;
       if (precision == TPE_PREC_F32) {
         const float t = __uint_as_float((uint32_t)v);

@@ -164,20 +164,30 @@ def suggest(new_ids, domain, trials, seed,
         logger.info('TPE using 0 trials')
     if len(hist) < n_startup_jobs:
         return rand.suggest(new_ids, domain, trials, seed)
+    choices = suggest_choices(domain.table, hist, new_ids, seed, prior_weight=prior_weight,
+                              n_EI_candidates=n_EI_candidates, gamma=gamma, sampler=sampler,
+                              precision=precision, device=device, shard=shard)
+    logger.info('tpe.suggest took %f seconds' % (time.time() - t0))
+    return rand.docs_from_choices(new_ids, domain, trials, choices)
+
+
+def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weight,
+                    n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
+                    sampler='philox', precision='fp32', device=None, shard=None):
+    """The suggest core on a structure-of-arrays history (``history.History``):
+    per new id a {label: value or None} dict.  ``suggest`` wraps it with the
+    Trials document layout; columnar callers (and bench.py's large configs)
+    use it directly."""
     if sampler not in ('philox', 'replay'):
         raise ValueError("sampler must be 'philox' or 'replay'")
     engine = get_engine(device, precision)
-    table = domain.table
     fits = _Fits(table, hist, _history.split_below(hist, gamma), prior_weight)
     C = int(n_EI_candidates)
     if sampler == 'philox':
-        choices = _choices_philox(table, fits, new_ids, seed, C, engine, shard)
-    else:
-        if shard is not None:
-            raise ValueError("sampler='replay' draws on the host; it does not shard")
-        choices = _choices_replay(table, fits, new_ids, seed, C, engine)
-    logger.info('tpe.suggest took %f seconds' % (time.time() - t0))
-    return rand.docs_from_choices(new_ids, domain, trials, choices)
+        return _choices_philox(table, fits, list(new_ids), seed, C, engine, shard)
+    if shard is not None:
+        raise ValueError("sampler='replay' draws on the host; it does not shard")
+    return _choices_replay(table, fits, list(new_ids), seed, C, engine)
 
 
 def suggest_replay(new_ids, domain, trials, seed, **kw):
