@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libtpe_hip.so')
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH = 1, 2
@@ -37,6 +37,13 @@ TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
                        ('k_start', '<i4'), ('k_end', '<i4'), ('reserved', '<i4')])
 BEST_DTYPE = np.dtype([('score', '<f8'), ('l', '<f8'), ('g', '<f8'), ('idx', '<i8')])
+FIT_JOB_DTYPE = np.dtype([
+    ('obs', '<u8'), ('n_obs', '<i8'), ('seg_off', '<i8'), ('below_off', '<i4'), ('n_below', '<i4'),
+    ('family', '<i4'), ('flags', '<i4'), ('lf', '<i4'), ('problem_first', '<i4'), ('n_problems', '<i4'),
+    ('above_off', '<i4'), ('wide_off', '<i4'), ('grid_off', '<i4'), ('grid_n', '<i4'), ('reserved', '<i4'),
+    ('prior_mu', '<f8'), ('prior_sigma', '<f8'), ('prior_weight', '<f8'), ('low', '<f8'), ('high', '<f8'),
+])
+assert FIT_JOB_DTYPE.itemsize == 112
 RESULT_DTYPE = np.dtype([('score', '<f8'), ('l', '<f8'), ('g', '<f8'), ('value', '<f8'),
                          ('idx', '<i8'), ('global_idx', '<i8')])
 assert RESULT_DTYPE.itemsize == 48
@@ -61,6 +68,11 @@ class Batch(ctypes.Structure):
         ('part', ctypes.c_void_p), ('l_out', ctypes.c_void_p), ('g_out', ctypes.c_void_p),
         ('tile_best', ctypes.c_void_p), ('result', ctypes.c_void_p),
         ('ce_count', ctypes.c_void_p),
+        ('fit', ctypes.c_void_p), ('n_fit', ctypes.c_int32), ('reserved4', ctypes.c_int32),
+        ('below_idx', ctypes.c_void_p), ('fit_seg', ctypes.c_void_p), ('fit_total', ctypes.c_int64),
+        ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
+        ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
+        ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64),
     ]
 
 
@@ -74,6 +86,9 @@ class LabelIn(ctypes.Structure):
         ('above_w', ctypes.c_void_p), ('above_mu', ctypes.c_void_p), ('above_sigma', ctypes.c_void_p),
         ('above_k', ctypes.c_int64),
         ('ids', ctypes.c_void_p), ('n_ids', ctypes.c_int64),
+        ('dev_obs', ctypes.c_void_p), ('n_obs', ctypes.c_int64),
+        ('below_idx', ctypes.c_void_p), ('n_below', ctypes.c_int32), ('lf', ctypes.c_int32),
+        ('prior_mu', ctypes.c_double), ('prior_sigma', ctypes.c_double), ('prior_weight', ctypes.c_double),
     ]
 
 
@@ -85,14 +100,17 @@ class PackInfo(ctypes.Structure):
         ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32), ('n_work_qlog', ctypes.c_int32),
         ('any_pruned', ctypes.c_int32), ('part_total', ctypes.c_int64), ('blob_bytes', ctypes.c_int64),
         ('key_bits', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
+        ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
+        ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
+        ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64),
     ]
 
 
 E_SPACE = -4
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
-           'tpe_sort_workspace_bytes', 'tpe_run_batch', 'tpe_sample', 'tpe_sort', 'tpe_score_above',
-           'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_cat_probs', 'tpe_host_pack_level')
+           'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above',
+           'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_cat_probs', 'tpe_host_pack_level')
 
 
 class NativeUnavailable(RuntimeError):
@@ -120,7 +138,9 @@ def load(path=LIB_PATH):
     lib.tpe_tile_size.restype = ctypes.c_int
     lib.tpe_sort_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)]
     lib.tpe_sort_workspace_bytes.restype = ctypes.c_int
-    for name in ('tpe_run_batch', 'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
+    lib.tpe_fit_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]
+    lib.tpe_fit_workspace_bytes.restype = ctypes.c_int
+    for name in ('tpe_run_batch', 'tpe_fit_above', 'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
         fn = getattr(lib, name)
         fn.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
         fn.restype = ctypes.c_int

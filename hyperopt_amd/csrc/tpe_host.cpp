@@ -212,9 +212,20 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<int32_t> grid;
   std::vector<tpe_problem> lab((size_t)n_labels);
   int64_t P = 0, ktot = 0;
+  std::vector<char> dev_fit((size_t)n_labels, 0);   // above mixture fitted on the device
   for (int32_t li = 0; li < n_labels; ++li) {
-    P += labels[li].n_ids;
-    ktot += labels[li].below_k + labels[li].above_k + kPruneWide;
+    const tpe_label_in& L = labels[li];
+    P += L.n_ids;
+    if (L.dev_obs && !L.above_mu) {
+      if ((L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) || f64 || L.n_below < 0 || L.n_below > 64 ||
+          (L.n_below > 0 && !L.below_idx) || L.n_obs - L.n_below + 1 != L.above_k || L.above_k <= kPruneMinK ||
+          L.n_obs >= ((int64_t)1 << 31))
+        return TPE_E_ARG;
+      dev_fit[li] = 1;
+      ktot += L.below_k + kPruneWide;
+    } else {
+      ktot += L.below_k + L.above_k + kPruneWide;
+    }
   }
   comp32.reserve((size_t)(4 * ktot));
   comp64.reserve((size_t)(4 * ktot));
@@ -284,7 +295,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     p.key_lo = (float)klo;
     p.key_inv = khi > klo ? (float)((double)(1 << key_bits) / (khi - klo)) : 0.f;
     // ---- component rows ----
-    for (int side = 0; side < 2; ++side) {
+    for (int side = 0; side < 2 - dev_fit[li]; ++side) {
       const double* w = side ? L.above_w : L.below_w;
       const double* mu = side ? L.above_mu : L.below_mu;
       const double* sg = side ? L.above_sigma : L.below_sigma;
@@ -380,6 +391,48 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       }
     }
   }
+  // ---- device-fitted above mixtures: rows and grids after the host ones, fit jobs ----
+  if (grid.empty()) grid.push_back(0);
+  const int64_t host_rows = (int64_t)(comp32.size() / 4), host_grid = (int64_t)grid.size();
+  std::vector<tpe_fit_job> fit;
+  std::vector<int32_t> below_idx;
+  std::vector<int64_t> fit_seg(1, 0);
+  int64_t dev_rows = 0, dev_grid = 0;
+  {
+    int64_t r = 0;
+    for (int32_t li = 0; li < n_labels; ++li) {
+      const tpe_label_in& L = labels[li];
+      if (dev_fit[li]) {
+        tpe_problem& p = lab[li];
+        const int64_t K = L.above_k, G = std::min<int64_t>(4096, 4 * K);
+        p.above_off = (int32_t)(host_rows + dev_rows); p.above_len = (int32_t)K;
+        p.wide_off = (int32_t)(host_rows + dev_rows + K);
+        p.grid_off = (int32_t)(host_grid + dev_grid); p.grid_n = (int32_t)G;
+        p.narrow_amin = 1.f;       // pruned; the fit stage writes the real value
+        tpe_fit_job j;
+        memset(&j, 0, sizeof(j));
+        j.obs = L.dev_obs; j.n_obs = L.n_obs; j.seg_off = fit_seg.back();
+        j.below_off = (int32_t)below_idx.size(); j.n_below = L.n_below;
+        j.family = L.family; j.flags = L.flags; j.lf = L.lf;
+        j.problem_first = (int32_t)r; j.n_problems = (int32_t)L.n_ids;
+        j.above_off = p.above_off; j.wide_off = p.wide_off; j.grid_off = p.grid_off; j.grid_n = p.grid_n;
+        j.prior_mu = L.prior_mu; j.prior_sigma = L.prior_sigma; j.prior_weight = L.prior_weight;
+        j.low = L.low; j.high = L.high;
+        for (int32_t b = 0; b < L.n_below; ++b) {
+          if (L.below_idx[b] < 0 || L.below_idx[b] >= L.n_obs || (b && L.below_idx[b] <= L.below_idx[b - 1]))
+            return TPE_E_ARG;
+          below_idx.push_back(L.below_idx[b]);
+        }
+        fit.push_back(j);
+        fit_seg.push_back(fit_seg.back() + K - 1);
+        dev_rows += K + kPruneWide;
+        dev_grid += G + 1;
+      }
+      r += L.n_ids;
+    }
+  }
+  if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
+  if (below_idx.empty()) below_idx.push_back(0);
   // ---- problems, tiles, work ----
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
   std::vector<tpe_problem> prob((size_t)P);
@@ -438,21 +491,25 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
     counts[gi] = (int32_t)(work.size() - before);
   }
-  // ---- blob: sections at 256-B aligned offsets, written straight into the caller's buffer ----
-  if (grid.empty()) grid.push_back(0);
-  const void* src[7] = {prob.data(), tiles.data(), work.data(), comp32.data(), comp64.data(), samp.data(),
-                        grid.data()};
-  const int64_t len[7] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
-                          (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp32.size() * sizeof(float)),
-                          (int64_t)(comp64.size() * sizeof(double)), (int64_t)(samp.size() * sizeof(double)),
-                          (int64_t)(grid.size() * sizeof(int32_t))};
-  int64_t off[7], end = 0;
-  for (int i = 0; i < 7; ++i) {
+  // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
+  // comp32 rows sit at the END of the last two sections and are not copied ----
+  const int NS = 10;
+  const void* src[NS] = {prob.data(), tiles.data(), work.data(), comp64.data(), samp.data(), fit.data(),
+                         below_idx.data(), fit_seg.data(), grid.data(), comp32.data()};
+  const int64_t len[NS] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
+                           (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp64.size() * sizeof(double)),
+                           (int64_t)(samp.size() * sizeof(double)), (int64_t)(fit.size() * sizeof(tpe_fit_job)),
+                           (int64_t)(below_idx.size() * sizeof(int32_t)), (int64_t)(fit_seg.size() * sizeof(int64_t)),
+                           (int64_t)(grid.size() * sizeof(int32_t)), (int64_t)(comp32.size() * sizeof(float))};
+  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
+  int64_t off[NS], end = 0;
+  for (int i = 0; i < NS; ++i) {
     off[i] = (end + 255) & ~(int64_t)255;
-    end = off[i] + len[i];
+    end = off[i] + len[i] + reserve[i];
   }
-  info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp32 = off[3];
-  info->off_comp64 = off[4]; info->off_samp = off[5]; info->off_grid = off[6];
+  info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp64 = off[3];
+  info->off_samp = off[4]; info->off_fit = off[5]; info->off_below_idx = off[6]; info->off_fit_seg = off[7];
+  info->off_grid = off[8]; info->off_comp32 = off[9];
   info->n_problems = P;
   info->n_tiles = (int64_t)tiles.size();
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
@@ -460,9 +517,13 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->key_bits = key_bits;
   info->sort_end_bit = any_pruned ? sort_end_bit : 0;
   info->part_total = part_total;
+  info->n_fit = (int32_t)fit.size(); info->reserved = 0;
+  info->fit_total = fit_seg.back();
+  info->copy_end = off[8] + len[8];
+  info->copy2_len = len[9];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;
-  for (int i = 0; i < 7; ++i)
+  for (int i = 0; i < NS; ++i)
     if (len[i]) memcpy((unsigned char*)blob + off[i], src[i], (size_t)len[i]);
   return TPE_OK;
 }

@@ -5,6 +5,8 @@
 // file:line of each stage).  Five stages, each a batched launch over a flat
 // work list so that problems of very different size share one grid:
 //
+//   tpe_fit_above    (optional) Parzen fit of large continuous above mixtures
+//                    from device-resident observation columns
 //   tpe_sample       Philox-4x32-10 candidates from the below mixture, plus the
 //                    sort keys (problem, 4096 value buckets of the kernel coordinate)
 //   tpe_sort         radix sort of the keys (rocPRIM) — candidates of one wave
@@ -25,7 +27,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "../../include/tpe_hip.h"
 
@@ -597,6 +602,218 @@ __global__ __launch_bounds__(kThreads) void k_select(const tpe_problem* __restri
   }
 }
 
+
+// ============================================================ device Parzen fit
+// adaptive_parzen_normal (tpe.py:398-475) of the above observations of a label
+// (ap_filter_trials, tpe.py:613-641), directly into the pruned f32 layout.
+constexpr int kFitThreads = 512;
+constexpr int kFitGatherBlock = 256;
+constexpr int kFitMaxBelow = 64;
+constexpr int kPruneWide = 16;
+constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e))
+constexpr double kLog2e = 1.4426950408889634074;
+
+// gather: above observations (kernel coordinate) and their rank in tid order
+__global__ __launch_bounds__(kFitGatherBlock) void k_fit_gather(const tpe_fit_job* __restrict__ J,
+                                                                const int32_t* __restrict__ below_idx,
+                                                                double* __restrict__ keys,
+                                                                uint32_t* __restrict__ vals) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  __shared__ int32_t bl[kFitMaxBelow];
+  const int nb = j.n_below;
+  if (threadIdx.x < nb) bl[threadIdx.x] = below_idx[j.below_off + threadIdx.x];
+  __syncthreads();
+  const bool logf = j.family == TPE_FAM_LOGGAUSS;
+  for (int64_t i = (int64_t)blockIdx.x * kFitGatherBlock + threadIdx.x; i < j.n_obs;
+       i += (int64_t)gridDim.x * kFitGatherBlock) {
+    int before = 0;
+    bool below = false;
+    for (int b = 0; b < nb; ++b) {
+      before += bl[b] < i;
+      below = below || bl[b] == i;
+    }
+    if (below) continue;
+    const int64_t r = i - before;                  // rank among the above observations
+    const double x = j.obs[i];
+    keys[j.seg_off + r] = logf ? log(x) : x;       // tpe.py:523 / :556 (np.log of the observations)
+    vals[j.seg_off + r] = (uint32_t)r;
+  }
+}
+
+// deterministic block reductions (fixed tree order)
+template <typename T, typename Op>
+__device__ __forceinline__ T block_reduce(T v, Op op, T* lds) {
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
+  const int wv = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[wv] = v;
+  __syncthreads();
+  T r = lds[0];
+  for (int i = 1; i < kFitThreads / 64; ++i) r = op(r, lds[i]);
+  return r;
+}
+
+struct FitView {
+  const double* s;     // sorted above observations
+  int64_t n, pos;      // count, prior position (searchsorted left)
+  double pmu;
+  __device__ __forceinline__ double mu(int64_t i) const { return i < pos ? s[i] : (i == pos ? pmu : s[i - 1]); }
+};
+
+__device__ __forceinline__ double ncdf(double x, double mu, double sigma) {   // tpe.py:96-101
+  return 0.5 * (1.0 + erf((x - mu) / fmax(1.4142135623730951 * sigma, kEPS)));
+}
+
+__global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __restrict__ J,
+                                                           const double* __restrict__ keys_sorted,
+                                                           const uint32_t* __restrict__ vals_sorted,
+                                                           tpe_problem* __restrict__ P,
+                                                           float4* __restrict__ comp,
+                                                           int32_t* __restrict__ grid) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  __shared__ double red[kFitThreads / 64];
+  __shared__ int64_t wide_ix[kPruneWide];
+  __shared__ int n_wide;
+  const int64_t n = j.n_obs - j.n_below, K = n + 1;
+  FitView v;
+  v.s = keys_sorted + j.seg_off;
+  v.n = n;
+  v.pmu = j.prior_mu;
+  {  // np.searchsorted(srtd_mus, prior_mu) (side left): number of observations < prior_mu
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (v.s[m] < j.prior_mu) lo = m + 1; else hi = m;
+    }
+    v.pos = lo;
+  }
+  const uint32_t* __restrict__ rank = vals_sorted + j.seg_off;
+  const double smax = j.prior_sigma, smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);   // tpe.py:465-470
+  // linear forgetting (tpe.py:381-394): ramp = linspace(1/n, 1, n - lf) for the oldest, 1 after
+  const bool ramp = j.lf > 0 && j.lf < n;
+  const int64_t num = n - j.lf;
+  const double start = 1.0 / (double)n, step = num > 1 ? (1.0 - start) / (double)(num - 1) : 0.0;
+  const bool logf = j.family == TPE_FAM_LOGGAUSS;
+  const bool bounded = !logf && (j.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH));
+  auto sigma_of = [&](int64_t i) -> double {
+    if (i == v.pos) return j.prior_sigma;
+    double sg;
+    if (i == 0) sg = v.mu(1) - v.mu(0);
+    else if (i == K - 1) sg = v.mu(K - 1) - v.mu(K - 2);
+    else sg = fmax(v.mu(i) - v.mu(i - 1), v.mu(i + 1) - v.mu(i));
+    return fmin(fmax(sg, smin), smax);
+  };
+  auto weight_of = [&](int64_t i) -> double {
+    if (i == v.pos) return j.prior_weight;
+    if (!ramp) return 1.0;
+    const int64_t r = rank[i < v.pos ? i : i - 1];
+    if (r >= num) return 1.0;
+    if (r == num - 1) return 1.0;
+    if (num == 1) return start;
+    return __dadd_rn(__dmul_rn((double)r, step), start);        // linspace: i * step + start
+  };
+  // pass 1: normaliser, acceptance mass, shift, wide thresholds
+  constexpr int kThr = 5;                          // wide if sigma > smin * 2^(m+1)
+  double W = 0, M = 0, cm = -INFINITY, sm_all = 0;
+  double sm[kThr];
+  int cnt[kThr];
+#pragma unroll
+  for (int m = 0; m < kThr; ++m) { sm[m] = 0; cnt[m] = 0; }
+  for (int64_t i = threadIdx.x; i < K; i += kFitThreads) {
+    const double sg = sigma_of(i), w = weight_of(i), mu = v.mu(i);
+    W += w;
+    if (bounded) M += w * (ncdf(j.high, mu, sg) - ncdf(j.low, mu, sg));
+    cm = fmax(cm, log2(w / fmax(sg, kEPS)));
+    if (i != v.pos) {
+      sm_all = fmax(sm_all, sg);
+#pragma unroll
+      for (int m = 0; m < kThr; ++m) {
+        const double thr = smin * (double)(2 << m);
+        if (sg > thr) ++cnt[m]; else sm[m] = fmax(sm[m], sg);
+      }
+    }
+  }
+  auto add = [](double a, double b) { return a + b; };
+  auto mx = [](double a, double b) { return fmax(a, b); };
+  W = block_reduce(W, add, red);
+  M = block_reduce(M, add, red);
+  cm = block_reduce(cm, mx, red);
+  sm_all = block_reduce(sm_all, mx, red);
+  double thr = INFINITY, s_narrow = sm_all;
+  for (int m = 0; m < kThr; ++m) {
+    const double c = block_reduce((double)cnt[m], add, red);
+    const double s2 = block_reduce(sm[m], mx, red);
+    if (thr == INFINITY && c <= (double)(kPruneWide - 1)) { thr = smin * (double)(2 << m); s_narrow = s2; }
+  }
+  if (threadIdx.x == 0) n_wide = 0;
+  __syncthreads();
+  // pass 2: rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and
+  // sigma > thr) get c = -inf in the sorted list and are listed apart
+  float4* __restrict__ C = comp + j.above_off;
+  for (int64_t i = threadIdx.x; i < K; i += kFitThreads) {
+    const double sg = sigma_of(i), w = weight_of(i), mu = v.mu(i);
+    const double se = fmax(sg, kEPS);
+    const float hi = (float)mu;
+    const bool wide = i == v.pos || sg > thr;
+    C[i] = make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se),
+                       wide ? -INFINITY : (float)(log2(w / se) - cm));
+    if (wide) {
+      const int slot = atomicAdd(&n_wide, 1);
+      if (slot < kPruneWide) wide_ix[slot] = i;
+    }
+  }
+  __syncthreads();
+  const int nw = min(n_wide, kPruneWide);
+  if (threadIdx.x == 0) {                         // fixed order of the wide list
+    for (int a = 1; a < nw; ++a)
+      for (int b = a; b > 0 && wide_ix[b - 1] > wide_ix[b]; --b) {
+        const int64_t t = wide_ix[b]; wide_ix[b] = wide_ix[b - 1]; wide_ix[b - 1] = t;
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < nw) {
+    const int64_t i = wide_ix[threadIdx.x];
+    const double sg = sigma_of(i), w = weight_of(i), mu = v.mu(i), se = fmax(sg, kEPS);
+    const float hi = (float)mu;
+    comp[j.wide_off + threadIdx.x] =
+        make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - cm));
+  }
+  // grid over the f32 means: first component with mu32 >= bucket edge
+  const double glo = (double)(float)v.mu(0), ghi = (double)(float)v.mu(K - 1);
+  const int G = j.grid_n;
+  const float ginv = ghi > glo ? (float)((double)G / (ghi - glo)) : 0.f;
+  int32_t* __restrict__ Gp = grid + j.grid_off;
+  for (int g = threadIdx.x; g < G; g += kFitThreads) {
+    int64_t r = 0;
+    if (ginv > 0.f) {
+      const double edge = glo + (double)g / (double)ginv;
+      int64_t lo = 0, hi = K;
+      while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if ((double)(float)v.mu(m) < edge) lo = m + 1; else hi = m;
+      }
+      r = lo;
+    }
+    Gp[g] = (int32_t)r;
+  }
+  if (threadIdx.x == 0) Gp[G] = (int32_t)K;
+  // problem rows: lpdf = ln2 * log2(sum) + base; base = ln2*cm - ln(W sqrt(2 pi) p_accept)
+  if (threadIdx.x < j.n_problems) {
+    const double pa = bounded ? M / W : 1.0;
+    tpe_problem& p = P[j.problem_first + threadIdx.x];
+    p.above_base = kLn2 * cm - log(W) - 0.91893853320467274 - log(pa);
+    p.wide_len = nw;
+    const double pse = fmax(j.prior_sigma, kEPS);
+    p.prior_mu = (float)j.prior_mu;
+    p.prior_a = (float)(kAScale / pse);
+    p.prior_c = (float)(log2(j.prior_weight / pse) - cm);
+    p.narrow_cmax = 0.f;                           // max over all c after the shift: an upper bound
+    p.narrow_amin = (float)(kAScale / fmax(s_narrow, kEPS));
+    p.grid_lo = (float)glo;
+    p.grid_inv = ginv;
+  }
+}
+
 int check_batch(const tpe_batch* b) {
   if (!b) return fail(TPE_E_ARG, "null batch");
   if (b->n_problems < 0 || b->n_tiles < 0 || b->n_work_cont < 0 || b->n_work_qgauss < 0 || b->n_work_qlog < 0 ||
@@ -619,6 +836,11 @@ int check_batch(const tpe_batch* b) {
   if (b->key_bits < 0 || b->key_bits > 16) return fail(TPE_E_ARG, "bad key_bits");
   if (b->sort_end_bit == 0 && (b->keys_sorted != b->keys || b->vals_sorted != b->vals))
     return fail(TPE_E_ARG, "unsorted batch must alias keys_sorted/vals_sorted to keys/vals");
+  if (b->n_fit < 0 || b->fit_total < 0) return fail(TPE_E_ARG, "negative fit count");
+  if (b->n_fit > 0 && (!b->fit || !b->below_idx || !b->fit_seg || !b->fit_keys || !b->fit_keys_sorted ||
+                       !b->fit_vals || !b->fit_vals_sorted || !b->comp32 || !b->grid || !b->problems))
+    return fail(TPE_E_ARG, "null fit buffers");
+  if (b->n_fit > 0 && b->precision != TPE_PREC_F32) return fail(TPE_E_ARG, "device fit needs TPE_PREC_F32");
   return TPE_OK;
 }
 
@@ -650,6 +872,44 @@ int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
   *bytes = (uint64_t)sz;
   return TPE_OK;
+}
+
+int tpe_fit_workspace_bytes(int64_t total, int32_t n_fit, uint64_t* bytes) {
+  if (!bytes || total < 0 || n_fit < 0) return fail(TPE_E_ARG, "bad arguments");
+  size_t sz = 0;
+  hipError_t e = rocprim::segmented_radix_sort_pairs(
+      nullptr, sz, (const double*)nullptr, (double*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+      (unsigned int)total, (unsigned int)n_fit, (const int64_t*)nullptr, (const int64_t*)nullptr, 0u, 64u,
+      (hipStream_t)0);
+  if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  *bytes = (uint64_t)sz;
+  return TPE_OK;
+}
+
+int tpe_fit_above(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (b->n_fit == 0) return TPE_OK;
+  if (b->fit_total >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 fit observations");
+  hipStream_t s = (hipStream_t)stream;
+  // every job's below list fits the gather kernel's LDS copy (host-checked sizes)
+  const int gx = (int)std::min<int64_t>(4096, std::max<int64_t>(1, (b->fit_total / b->n_fit + kFitGatherBlock - 1) /
+                                                                         kFitGatherBlock));
+  hipLaunchKernelGGL(k_fit_gather, dim3(gx, b->n_fit), dim3(kFitGatherBlock), 0, s, b->fit, b->below_idx,
+                     b->fit_keys, b->fit_vals);
+  if ((rc = hip_check("tpe_fit_above/gather"))) return rc;
+  size_t sz = (size_t)b->fit_tmp_bytes;
+  hipError_t e = rocprim::segmented_radix_sort_pairs(
+      b->fit_tmp, sz, (const double*)b->fit_keys, b->fit_keys_sorted, (const uint32_t*)b->fit_vals,
+      b->fit_vals_sorted, (unsigned int)b->fit_total, (unsigned int)b->n_fit, b->fit_seg, b->fit_seg + 1, 0u, 64u, s);
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "tpe_fit_above/sort: %s", hipGetErrorString(e));
+    return TPE_E_HIP;
+  }
+  hipLaunchKernelGGL(k_fit_build, dim3(b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
+                     b->fit_vals_sorted, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32,
+                     const_cast<int32_t*>(b->grid));
+  return hip_check("tpe_fit_above/build");
 }
 
 int tpe_sample(const tpe_batch* b, void* stream) {
@@ -723,6 +983,7 @@ int tpe_select(const tpe_batch* b, void* stream) {
 int tpe_run_batch(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
+  if ((rc = tpe_fit_above(b, stream))) return rc;
   if ((rc = tpe_sample(b, stream))) return rc;
   if ((rc = tpe_sort(b, stream))) return rc;
   if ((rc = tpe_score_above(b, stream))) return rc;

@@ -19,6 +19,7 @@ is common to all new_ids), so component tables scale with labels, not ids.
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -33,6 +34,10 @@ except ImportError:  # pragma: no cover - torch is part of the image
 # target number of above-mixture work items per launch (>= 8 per CU on 256 CUs)
 TARGET_WORK = 2048
 MIN_COMPONENTS_PER_SPLIT = 128
+# continuous above mixtures with at least this many observations are fitted on
+# the device (tpe_fit_above) in fp32 mode; TPE_DEVICE_FIT_MIN overrides
+DEVICE_FIT_MIN = int(os.environ.get('TPE_DEVICE_FIT_MIN', '16384'))
+PRUNE_MIN_K = 64
 
 
 def _coord_range(post):
@@ -88,6 +93,7 @@ class Engine(object):
             device = torch.device('cuda', torch.cuda.current_device())
         self.device = torch.device(device)
         self.tile = self.lib.tpe_tile_size()
+        self.device_fit_min = DEVICE_FIT_MIN
         self.set_precision(precision)
         self._bufs = {}
         self._pinned = None
@@ -284,7 +290,16 @@ class Engine(object):
             L.low = post.low if post.low is not None else 0.0
             L.high = post.high if post.high is not None else 0.0
             L.q = post.q if post.q is not None else 0.0
-            for side in ('below', 'above'):
+            if post.above_dev is not None:
+                col, n_obs, bidx = post.above_dev
+                bidx = np.ascontiguousarray(bidx, dtype=np.int32)
+                keep.append(bidx)
+                L.above_w = L.above_mu = L.above_sigma = None
+                L.above_k = n_obs - len(bidx) + 1
+                L.dev_obs, L.n_obs = col.data_ptr(), n_obs
+                L.below_idx, L.n_below = bidx.ctypes.data, len(bidx)
+                L.prior_mu, L.prior_sigma, L.prior_weight, L.lf = post.prior
+            for side in (('below',) if post.above_dev is not None else ('below', 'above')):
                 arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in getattr(post, side)]
                 keep.append(arrs)
                 setattr(L, side + '_w', arrs[0].ctypes.data)
@@ -331,7 +346,11 @@ class Engine(object):
             raise ValueError('more than 2^32 candidates in one level: shard the batch')
         nbytes = int(info.blob_bytes)
         dev = self._buf('blob', nbytes, torch.uint8)
-        dev[:nbytes].copy_(self._pinned[:nbytes], non_blocking=True)
+        # host-written ranges only: device-fitted rows are produced by tpe_fit_above
+        c0, o2, c2 = int(info.copy_end), int(info.off_comp32), int(info.copy2_len)
+        dev[:c0].copy_(self._pinned[:c0], non_blocking=True)
+        if c2:
+            dev[o2:o2 + c2].copy_(self._pinned[o2:o2 + c2], non_blocking=True)
         base = dev.data_ptr()
         prob = np.frombuffer(self._pinned.numpy(), dtype=N.PROBLEM_DTYPE, count=P, offset=int(info.off_problems))
         d_cand = self._buf('cand', C_total, torch.float64)
@@ -394,6 +413,21 @@ class Engine(object):
         b.l_out = d_l.data_ptr() if d_l is not None else None
         b.g_out = d_g.data_ptr() if d_g is not None else None
         b.tile_best, b.result = d_best.data_ptr(), d_res.data_ptr()
+        if info.n_fit:
+            ft = int(info.fit_total)
+            d_fk = self._buf('fit_keys', ft, torch.float64)
+            d_fks = self._buf('fit_keys_sorted', ft, torch.float64)
+            d_fv = self._buf('fit_vals', ft, torch.int32)
+            d_fvs = self._buf('fit_vals_sorted', ft, torch.int32)
+            ws = ctypes.c_uint64(0)
+            N.check(self.lib.tpe_fit_workspace_bytes(ft, int(info.n_fit), ctypes.byref(ws)), self.lib,
+                    'tpe_fit_workspace_bytes')
+            d_ft = self._buf('fit_tmp', ws.value, torch.uint8)
+            b.fit, b.n_fit = base + info.off_fit, info.n_fit
+            b.below_idx, b.fit_seg, b.fit_total = base + info.off_below_idx, base + info.off_fit_seg, ft
+            b.fit_keys, b.fit_keys_sorted = d_fk.data_ptr(), d_fks.data_ptr()
+            b.fit_vals, b.fit_vals_sorted = d_fv.data_ptr(), d_fvs.data_ptr()
+            b.fit_tmp, b.fit_tmp_bytes = d_ft.data_ptr(), d_ft.numel()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         if self.profile is None:
             N.check(self.lib.tpe_run_batch(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, 'tpe_run_batch')
@@ -422,6 +456,8 @@ class Engine(object):
                   (fam == N.FAM_QGAUSS, 'k_above_qgauss'), (fam == N.FAM_QLOGGAUSS, 'k_above_qlog')]
         counts = list(tb['counts_w'])
         stages = []
+        if b.n_fit:
+            stages.append(('fit', self.lib.tpe_fit_above, None, float(b.fit_total)))
         stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
         if b.sort_end_bit:
             stages.append(('sort', self.lib.tpe_sort, None, float(tb['P'] * n_cand)))

@@ -23,11 +23,15 @@ _CACHES = weakref.WeakKeyDictionary()
 
 class History(object):
     """tids (int64, ascending), losses (float64, +inf for missing), and per
-    label the (tid, value) observations in tid order."""
-    __slots__ = ('tids', 'losses', 'obs')
+    label the (tid, value) observations in tid order.  ``dev`` holds the
+    device copies of the observation columns (devhist.DeviceColumns per
+    device); it lives as long as the append-only source it mirrors."""
+    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs')
 
-    def __init__(self, tids, losses, obs):
+    def __init__(self, tids, losses, obs, dev=None, sorted_obs=True):
         self.tids, self.losses, self.obs = tids, losses, obs
+        self.dev = {} if dev is None else dev
+        self.sorted_obs = sorted_obs     # every label's observation tids ascending
 
     def __len__(self):
         return len(self.tids)
@@ -60,6 +64,7 @@ class _Cache(object):
         self.obs_val = {k: _Grow(np.int64 if categorical[k] else np.float64) for k in labels}
         self.labels = labels
         self.ok = True                 # fast path still valid
+        self.dev = {}                  # device mirrors of the (append-only) columns
 
     def extend(self, docs, start):
         for i in range(start, len(docs)):
@@ -126,7 +131,8 @@ def _generic(domain, docs, table):
                 ov.append(v[0])
         obs[r.label] = (np.array(ot, dtype=np.int64),
                         np.array(ov, dtype=np.int64 if r.categorical else np.float64))
-    return History(np.array(tids, dtype=np.int64), losses, obs)
+    srt = all(len(o[0]) < 2 or bool(np.all(np.diff(o[0]) > 0)) for o in obs.values())
+    return History(np.array(tids, dtype=np.int64), losses, obs, sorted_obs=srt)
 
 
 def extract(domain, trials):
@@ -159,7 +165,7 @@ def extract(domain, trials):
     for k in labels:
         pos = cache.obs_pos[k].view()
         obs[k] = (tids[pos], cache.obs_val[k].view())
-    return History(tids, cache.losses.view(), obs)
+    return History(tids, cache.losses.view(), obs, dev=cache.dev)
 
 
 def split_below(history, gamma, gamma_cap=25):
@@ -185,9 +191,25 @@ def split_below(history, gamma, gamma_cap=25):
     return history.tids[part[:n_below]]
 
 
-def below_mask(obs_tids, below_tids):
+def below_index(obs_tids, below_tids, sorted_obs=True):
+    """Ascending positions (int32) of the below observations among a label's
+    observations (tpe.py:629-636: membership of the tid in the below set).
+    With ascending ``obs_tids`` (History.sorted_obs) this is O(n_below log n)."""
+    n = len(obs_tids)
+    if len(below_tids) == 0 or n == 0:
+        return np.zeros(0, dtype=np.int32)
+    if not sorted_obs:
+        return np.nonzero(np.isin(obs_tids, below_tids))[0].astype(np.int32)
+    b = np.asarray(below_tids, dtype=np.int64)
+    idx = np.searchsorted(obs_tids, b)
+    ok = idx < n
+    ok[ok] = obs_tids[idx[ok]] == b[ok]
+    return np.sort(idx[ok]).astype(np.int32)
+
+
+def below_mask(obs_tids, below_tids, sorted_obs=True):
     """Membership of each observation in the below set, in tid order
     (tpe.py:629-636)."""
-    if len(below_tids) == 0 or len(obs_tids) == 0:
-        return np.zeros(len(obs_tids), dtype=bool)
-    return np.isin(obs_tids, below_tids)
+    m = np.zeros(len(obs_tids), dtype=bool)
+    m[below_index(obs_tids, below_tids, sorted_obs)] = True
+    return m

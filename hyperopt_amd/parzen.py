@@ -139,13 +139,17 @@ class Posterior(object):
     q           quantum or None
     below/above (w, mu, sigma) float64 arrays, or (p,) for categorical
     upper       number of categories (categorical)
+    above_dev   None, or (device column, n_obs, below_idx int32) when the above
+                mixture is fitted on the device (engine: tpe_fit_above); then
+                ``above`` is None and ``prior`` = (mu, sigma, weight, lf)
     """
-    __slots__ = ('dist', 'family', 'low', 'high', 'q', 'below', 'above', 'upper')
+    __slots__ = ('dist', 'family', 'low', 'high', 'q', 'below', 'above', 'upper', 'above_dev', 'prior')
 
-    def __init__(self, dist, family, low, high, q, below, above, upper=0):
+    def __init__(self, dist, family, low, high, q, below, above, upper=0, above_dev=None, prior=None):
         self.dist, self.family = dist, family
         self.low, self.high, self.q = low, high, q
         self.below, self.above, self.upper = below, above, upper
+        self.above_dev, self.prior = above_dev, prior
 
     @property
     def bounded(self):
@@ -178,8 +182,13 @@ def _cat_probs_numpy(dist, args, obs, prior_weight, lf):
     return pseudo / np.sum(pseudo)
 
 
-def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT_LF):
-    """Fit the below and above posteriors of one hyperparameter."""
+DEVICE_FIT_FAMILIES = (N.FAM_GAUSS, N.FAM_LOGGAUSS)
+
+
+def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT_LF, above_dev=None):
+    """Fit the below and above posteriors of one hyperparameter.  With
+    ``above_dev`` = (device column, n_obs, below_idx) the above mixture is left
+    to the device fit (continuous families only; ``above_obs`` is ignored)."""
     family = _FAMILY[dist]
     a = args
     if family == N.FAM_CATEGORICAL:
@@ -206,6 +215,11 @@ def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT
         return obs
 
     below = fit_parzen(tr(below_obs), prior_weight, pmu, psig, lf)
+    if above_dev is not None:
+        if family not in DEVICE_FIT_FAMILIES:
+            raise ValueError('device fit supports continuous families only, not %r' % dist)
+        return Posterior(dist, family, low, high, q, below, None, above_dev=above_dev,
+                         prior=(float(pmu), float(psig), float(prior_weight), int(lf or 0)))
     above = fit_parzen(tr(above_obs), prior_weight, pmu, psig, lf)
     return Posterior(dist, family, low, high, q, below, above)
 

@@ -37,12 +37,13 @@ import time
 import numpy as np
 
 from . import _native as N
+from . import devhist
 from . import dist as _dist
 from . import history as _history
 from . import rand
 from . import replay
 from .engine import LevelProblem, get_engine
-from .parzen import DEFAULT_LF, fit_posterior
+from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, fit_posterior
 
 logger = logging.getLogger(__name__)
 
@@ -54,19 +55,31 @@ _default_linear_forgetting = DEFAULT_LF
 
 
 class _Fits(object):
-    """Lazily fitted posteriors of one suggest call (inactive labels are never fitted)."""
+    """Lazily fitted posteriors of one suggest call (inactive labels are never
+    fitted).  Large continuous above mixtures are left to the device fit when
+    the engine computes in fp32 (Engine.device_fit_min)."""
 
-    def __init__(self, table, hist, below_tids, prior_weight):
+    def __init__(self, table, hist, below_tids, prior_weight, engine=None):
         self.table, self.hist = table, hist
         self.below_tids, self.prior_weight = below_tids, prior_weight
+        self.engine = engine
         self.cache = {}
 
     def get(self, row):
         post = self.cache.get(row.label)
         if post is None:
             otids, ovals = self.hist.obs[row.label]
-            m = _history.below_mask(otids, self.below_tids)
-            post = fit_posterior(row.dist, row.args, ovals[m], ovals[~m], self.prior_weight, DEFAULT_LF)
+            bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
+            eng = self.engine
+            if (eng is not None and eng.precision == 'fp32' and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES
+                    and len(ovals) - len(bidx) >= max(eng.device_fit_min, 64)):
+                col = devhist.columns(self.hist, eng.device).column(row.label, ovals)
+                post = fit_posterior(row.dist, row.args, ovals[bidx], None, self.prior_weight, DEFAULT_LF,
+                                     above_dev=(col, len(ovals), bidx))
+            else:
+                m = np.zeros(len(ovals), dtype=bool)
+                m[bidx] = True
+                post = fit_posterior(row.dist, row.args, ovals[m], ovals[~m], self.prior_weight, DEFAULT_LF)
             self.cache[row.label] = post
         return post
 
@@ -181,7 +194,7 @@ def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weig
     if sampler not in ('philox', 'replay'):
         raise ValueError("sampler must be 'philox' or 'replay'")
     engine = get_engine(device, precision)
-    fits = _Fits(table, hist, _history.split_below(hist, gamma), prior_weight)
+    fits = _Fits(table, hist, _history.split_below(hist, gamma), prior_weight, engine)
     C = int(n_EI_candidates)
     if sampler == 'philox':
         return _choices_philox(table, fits, list(new_ids), seed, C, engine, shard)

@@ -21,7 +21,9 @@
  *
  * The Parzen fit (adaptive_parzen_normal, tpe.py:398-475) and the below/above
  * split (ap_filter_trials, tpe.py:613-641) are done by the caller, which
- * uploads the fitted mixtures as the component tables described below.
+ * uploads the fitted mixtures as the component tables described below — or,
+ * for large continuous above mixtures, left to the device: tpe_fit_above()
+ * fits them from device-resident observation columns (see tpe_fit_job).
  */
 #ifndef TPE_HIP_H
 #define TPE_HIP_H
@@ -32,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 2
+#define TPE_ABI_VERSION 3
 
 /* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
 enum {
@@ -146,6 +148,35 @@ typedef struct tpe_result {
   int64_t global_idx;    /* cand_base + idx                                     */
 } tpe_result;
 
+/*
+ * Device Parzen fit of one continuous above mixture (families 0/1, f32 tables):
+ * adaptive_parzen_normal (tpe.py:398-475) of the label's observations that are
+ * not in the below set (ap_filter_trials, tpe.py:613-641), written straight
+ * into the pruned comp32 layout above.  Stages (tpe_fit_above):
+ *   gather   above observations (t = x, or ln x for LOGGAUSS) + their rank in
+ *            tid order (the linear-forgetting weight index) into the fit sort
+ *            buffers at [seg_off, seg_off + n_obs - n_below)
+ *   sort     segmented radix sort by t (stable: equal values stay in tid order)
+ *   build    one workgroup per job: prior insertion (searchsorted left), sigma
+ *            from neighbour gaps, clip, LF weights, normalisation, {mu, a, c}
+ *            rows, wide list, grid; patches the job's problem rows (above_base,
+ *            wide_len, prior_*, narrow_*, grid_lo/inv)
+ * The host reserves above_off[0 .. K) + wide_off[0 .. 16) rows and grid_n + 1
+ * grid entries (K = n_obs - n_below + 1, grid_n = min(4096, 4K)).
+ */
+typedef struct tpe_fit_job {
+  const double* obs;     /* device: the label's observations in tid order (sampling space) */
+  int64_t n_obs;
+  int64_t seg_off;       /* first slot of this job in the fit sort buffers     */
+  int32_t below_off;     /* below_idx[below_off ..]: ascending indices into obs */
+  int32_t n_below;
+  int32_t family, flags, lf;
+  int32_t problem_first, n_problems;  /* problem rows this mixture serves      */
+  int32_t above_off, wide_off, grid_off, grid_n;
+  int32_t reserved;
+  double prior_mu, prior_sigma, prior_weight, low, high;
+} tpe_fit_job;
+
 /* all device pointers of one batch (the struct itself lives in host memory) */
 typedef struct tpe_batch {
   const tpe_problem* problems; int32_t n_problems;
@@ -177,6 +208,14 @@ typedef struct tpe_batch {
   tpe_result* result;    /* [n_problems]                                       */
   unsigned long long* ce_count; /* optional [n_work_cont]: component evaluations executed
                                    per work item by the pruned kernel; NULL to skip */
+  /* device Parzen fits (n_fit == 0: none); they patch rows of `problems` */
+  const tpe_fit_job* fit; int32_t n_fit; int32_t reserved4;
+  const int32_t* below_idx;   /* below indices of every job                        */
+  const int64_t* fit_seg;     /* [n_fit + 1] segment offsets into the fit buffers  */
+  int64_t fit_total;          /* fit_seg[n_fit]                                    */
+  double* fit_keys; double* fit_keys_sorted;        /* [fit_total]                */
+  uint32_t* fit_vals; uint32_t* fit_vals_sorted;    /* [fit_total]                */
+  void* fit_tmp; uint64_t fit_tmp_bytes;            /* tpe_fit_workspace_bytes()  */
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
@@ -194,11 +233,15 @@ int tpe_tile_size(void);
 /* device workspace (bytes) the candidate sort needs for `total_cand` candidates */
 int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes);
 
-/* sample (optional) -> sort -> score -> select, enqueued on `stream` (hipStream_t);
+/* device workspace (bytes) of the fit sort for `total` observations in `n_fit` segments */
+int tpe_fit_workspace_bytes(int64_t total, int32_t n_fit, uint64_t* bytes);
+
+/* fit (when n_fit > 0) -> sample (optional) -> sort -> score -> select, enqueued on `stream` (hipStream_t);
  * asynchronous: results are valid once the stream reaches this point. */
 int tpe_run_batch(const tpe_batch* batch, void* stream);
 
 /* the stages one by one (same semantics; used by tests and the profiler) */
+int tpe_fit_above(const tpe_batch* batch, void* stream);  /* device Parzen fits */
 int tpe_sample(const tpe_batch* batch, void* stream);     /* draw + sort keys */
 int tpe_sort(const tpe_batch* batch, void* stream);
 int tpe_score_above(const tpe_batch* batch, void* stream);
@@ -212,22 +255,37 @@ int tpe_select(const tpe_batch* batch, void* stream);
 
 /* one hyperparameter of a level: its fitted posterior and the new_ids it is
  * active for (mixtures are float64 host arrays; categorical: below_w / above_w
- * are the probabilities, *_k = number of categories) */
+ * are the probabilities, *_k = number of categories).
+ * Device-fitted above mixture (families 0/1, TPE_PREC_F32 only): above_w/mu/
+ * sigma NULL, dev_obs = the label's device observation column (n_obs values in
+ * tid order), below_idx = host array of the n_below ascending indices of the
+ * below observations in it, above_k = n_obs - n_below + 1; prior_* and lf are
+ * the fit parameters. */
 typedef struct tpe_label_in {
   int32_t family, flags, upper, label_ix;
   double low, high, q;
   const double* below_w; const double* below_mu; const double* below_sigma; int64_t below_k;
   const double* above_w; const double* above_mu; const double* above_sigma; int64_t above_k;
   const int64_t* ids; int64_t n_ids;
+  const double* dev_obs; int64_t n_obs;
+  const int32_t* below_idx; int32_t n_below; int32_t lf;
+  double prior_mu, prior_sigma, prior_weight;
 } tpe_label_in;
 
-/* where tpe_host_pack_level put each table in the blob (byte offsets) */
+/* where tpe_host_pack_level put each table in the blob (byte offsets).  The
+ * device-fitted rows (end of the grid and comp32 sections) are written by
+ * tpe_fit_above: only [0, copy_end) and [off_comp32, off_comp32 + copy2_len)
+ * need the host -> device copy. */
 typedef struct tpe_pack_info {
   int64_t off_problems, off_tiles, off_work, off_comp32, off_comp64, off_samp, off_grid;
   int64_t n_problems, n_tiles;
   int32_t n_work_cont, n_work_qgauss, n_work_qlog, any_pruned;
   int64_t part_total, blob_bytes;
   int32_t key_bits, sort_end_bit;   /* sort-key layout for tpe_batch (sort_end_bit 0: no sort) */
+  int64_t off_fit, off_below_idx, off_fit_seg;
+  int32_t n_fit, reserved;
+  int64_t fit_total;
+  int64_t copy_end, copy2_len;
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation

@@ -222,3 +222,103 @@ def test_pruning_and_underflow_extremes(engine):
         _check_lpdf(l[0], lb, 1e-5, (dist, 'l'))
         _check_lpdf(g[0], la, 1e-5, (dist, 'g'))
         _check_argmax(int(res[0]['idx']), lb, la, 1e-5, dist)
+
+
+def _device_post(engine, dist, args, obs, bidx):
+    """Posterior whose above mixture is fitted on the device (tpe_fit_above)."""
+    from hyperopt_amd import devhist, history, parzen
+    hist = history.History(np.arange(len(obs)), np.zeros(len(obs)), {'x': (np.arange(len(obs)), obs)})
+    col = devhist.columns(hist, engine.device).column('x', obs)
+    return parzen.fit_posterior(dist, args, obs[bidx], None, 1.0, above_dev=(col, len(obs), bidx)), col
+
+
+@pytest.mark.parametrize('dist,args', [('uniform', dict(low=-5.0, high=5.0)),
+                                       ('loguniform', dict(low=-4.0, high=3.0)),
+                                       ('normal', dict(mu=1.0, sigma=3.0)),
+                                       ('lognormal', dict(mu=0.0, sigma=1.0))])
+def test_device_fit_matches_oracle(engine, dist, args):
+    """Device Parzen fit of the above mixture (gather -> segmented sort ->
+    build) against the oracle's adaptive_parzen_normal + GMM1/LGMM1 lpdf, on
+    sampled and injected candidates; the below side stays the host fit, so the
+    draws equal the host-fit run's and the argmax lies in its eps-tie set."""
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(31)
+    n = 20000
+    if dist == 'uniform':     # clustered + isolated observations: wide components
+        obs = np.clip(np.concatenate([rs.normal(-2, 0.05, n // 2), rs.uniform(-5, 5, n // 2 - 3),
+                                      [-4.9, 4.95, 0.0]]), -5, 5)
+    elif dist == 'loguniform':
+        obs = np.exp(rs.uniform(-4, 3, n))
+    elif dist == 'normal':
+        obs = rs.normal(1.0, 3.0, n)
+    else:
+        obs = np.exp(rs.normal(0, 1, n))
+    rs.shuffle(obs)
+    bidx = np.sort(rs.choice(n, 25, replace=False)).astype(np.int32)
+    m = np.zeros(n, bool)
+    m[bidx] = True
+    host = parzen.fit_posterior(dist, args, obs[m], obs[~m], 1.0)
+    dev, _ = _device_post(engine, dist, args, obs, bidx)
+    logf = dist in ('loguniform', 'lognormal')
+    tr = np.log if logf else (lambda v: v)
+    pmu = 0.5 * (args['low'] + args['high']) if 'low' in args else args['mu']
+    psig = (args['high'] - args['low']) if 'low' in args else args['sigma']
+    above = O.adaptive_parzen_normal(tr(obs[~m]), 1.0, pmu, psig)
+    lpdf = O.lgmm1_lpdf if logf else O.gmm1_lpdf
+    low, high = host.low, host.high
+    C = 1 << 16
+    res_d, cand_d, l_d, g_d = engine.run([LevelProblem(dev, 0, [3])], C, seed=9, want_lg=True, return_cand=True)
+    res_h, cand_h, l_h, g_h = engine.run([LevelProblem(host, 0, [3])], C, seed=9, want_lg=True, return_cand=True)
+    np.testing.assert_array_equal(cand_d, cand_h)
+    np.testing.assert_array_equal(l_d, l_h)
+    sub = rs.choice(C, 3000, replace=False)
+    _check_lpdf(g_d[0][sub], lpdf(cand_d[0][sub], *above, low=low, high=high), 1e-5, (dist, 'g'))
+    _check_argmax(int(res_d[0]['idx']), l_h[0], g_h[0], 1e-5, dist)
+    # injected tails (wide components, fixed-shift underflow fallback)
+    lo_x = tr(np.min(obs)) - 3 * psig
+    hi_x = tr(np.max(obs)) + 3 * psig
+    if low is not None:
+        lo_x, hi_x = low, high
+    x = np.linspace(lo_x, hi_x, 4001)[:-1]
+    x = np.exp(x) if logf else x
+    res_i, l_i, g_i = engine.run([LevelProblem(dev, 0, [3], inject=x[None, :])], len(x), 1, want_lg=True)
+    _check_lpdf(g_i[0], lpdf(x, *above, low=low, high=high), 1e-5, (dist, 'g inj'))
+    # repeatable bit for bit
+    res_d2 = engine.run([LevelProblem(dev, 0, [3])], C, seed=9)
+    assert res_d2[0]['idx'] == res_d[0]['idx'] and res_d2[0]['score'] == res_d[0]['score']
+
+
+def test_device_fit_batched_labels_and_suggest():
+    """Several device-fitted labels (and host-fitted ones) in one level, through
+    tpe.suggest_choices: identical to suggest_choices with every fit on the host
+    up to the eps-tie set, and the column upload is incremental."""
+    from hyperopt_amd import hp, tpe
+    from hyperopt_amd.engine import get_engine
+    from hyperopt_amd.history import History
+    from hyperopt_amd.space import ParamTable
+    rs = np.random.RandomState(41)
+    N = 6000
+    labels = {'a': hp.uniform('a', -5, 5), 'b': hp.loguniform('b', -3, 2), 'c': hp.normal('c', 0, 2),
+              'd': hp.quniform('d', 0, 10, 1)}
+    vals = {'a': rs.uniform(-5, 5, N), 'b': np.exp(rs.uniform(-3, 2, N)), 'c': rs.normal(0, 2, N),
+            'd': np.round(rs.uniform(0, 10, N))}
+    tids = np.arange(N)
+    losses = (vals['a'] - 1) ** 2 + rs.uniform(0, 1e-3, N)
+    hist = History(tids, losses, {k: (tids, v) for k, v in vals.items()})
+    table = ParamTable(labels)
+    engine = get_engine()
+    old = engine.device_fit_min
+    try:
+        engine.device_fit_min = 1000
+        got = tpe.suggest_choices(table, hist, [N, N + 1], 5, n_EI_candidates=4096)
+        dc = hist.dev[str(engine.device)]
+        assert set(dc.cols) == {'a', 'b', 'c'} and all(v[1] == N for v in dc.cols.values())
+        engine.device_fit_min = 10 ** 9
+        ref = tpe.suggest_choices(table, hist, [N, N + 1], 5, n_EI_candidates=4096)
+    finally:
+        engine.device_fit_min = old
+    for g, r in zip(got, ref):
+        assert g['d'] == r['d']
+        for k in 'abc':
+            assert abs(g[k] - r[k]) <= 1e-3 * max(1.0, abs(r[k])), (k, g[k], r[k])

@@ -94,3 +94,47 @@ def test_native_pack_matches_numpy_packer(precision):
         if precision == 'fp32':
             g = _blob(e, info, info.off_grid, np.int32, ref['grid'].size)
             np.testing.assert_array_equal(g, ref['grid'])
+
+
+class _FakeColumn(object):
+    """Stand-in for a device column: the packer only records its address."""
+
+    def data_ptr(self):
+        return 0xD0000000
+
+
+def test_pack_reserves_device_fit_rows():
+    """A device-fitted above mixture (tpe_fit_job) gets its comp32 rows, wide
+    rows and grid at the END of those sections, outside the host copy ranges."""
+    rs = np.random.RandomState(5)
+    n_obs, bidx = 500, np.array([3, 10, 77], dtype=np.int32)
+    host = parzen.fit_posterior('normal', dict(mu=0.0, sigma=2.0), rs.normal(0, 2, 9), rs.normal(0, 2, 300), 1.0)
+    dev = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 3), None, 1.0,
+                               above_dev=(_FakeColumn(), n_obs, bidx))
+    assert dev.above is None and dev.prior == (0.5, 3.0, 1.0, 25)
+    lps = [LevelProblem(host, 1, [5, 6]), LevelProblem(dev, 2, [5, 6, 7])]
+    e = _engine('fp32')
+    info = e._pack(lps, 4096, 1, 0, None)
+    K = n_obs - len(bidx) + 1
+    assert info.n_fit == 1 and info.fit_total == K - 1 and info.sort_end_bit > 0
+    j = _blob(e, info, info.off_fit, N.FIT_JOB_DTYPE, 1)[0]
+    assert j['obs'] == 0xD0000000 and j['n_obs'] == n_obs and j['seg_off'] == 0 and j['n_below'] == 3
+    assert j['problem_first'] == 2 and j['n_problems'] == 3 and j['family'] == N.FAM_GAUSS
+    assert (j['prior_mu'], j['prior_sigma'], j['prior_weight'], j['lf']) == (0.5, 3.0, 1.0, 25)
+    assert (j['low'], j['high']) == (-1.0, 2.0)
+    np.testing.assert_array_equal(_blob(e, info, info.off_below_idx, np.int32, 3), bidx)
+    np.testing.assert_array_equal(_blob(e, info, info.off_fit_seg, np.int64, 2), [0, K - 1])
+    prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, 5)
+    host_rows = info.copy2_len // 16
+    for p in prob[2:]:
+        assert p['above_len'] == K and p['above_off'] == host_rows == j['above_off']
+        assert p['wide_off'] == host_rows + K == j['wide_off']
+        assert p['grid_off'] == j['grid_off'] and p['grid_n'] == j['grid_n'] == min(4096, 4 * K)
+        assert p['narrow_amin'] > 0
+    # host rows of the other label lie before the device region, its grid too
+    assert prob[0]['above_off'] + prob[0]['above_len'] <= host_rows
+    assert prob[0]['grid_off'] + prob[0]['grid_n'] + 1 <= j['grid_off']
+    assert info.copy_end == info.off_grid + 4 * j['grid_off']
+    assert info.blob_bytes == info.off_comp32 + 16 * (host_rows + K + 16)
+    with pytest.raises(RuntimeError):
+        _engine('fp64')._pack(lps, 4096, 1, 0, None)
