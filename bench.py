@@ -339,13 +339,21 @@ def run_other(args, rank, world, device):
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # per-stage device time of one more step (HIP events on the launch stream)
+    from hyperopt_amd import engine as engine_mod
+    eng = engine_mod._ENGINES[str(device)]
+    eng.profile = {}
+    step(10 ** 6)
+    torch.cuda.synchronize()
+    stages = {k: float(np.sum([a[0] for a in v])) for k, v in eng.profile.items()}
+    eng.profile = None
     if rank == 0:
         out = {'metric': 'EI candidates scored/sec (node)', 'value': units * args.steps / elapsed,
                'unit': 'candidate-scores/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
                'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
                'scaling': 'strong' if args.config in (4, 5) else 'weak', 'vs_baseline': None, 'dtype': 'f32',
                'data': 'synthetic', 'config': {'workload': desc, 'config': args.config},
-               'p50_step_ms': 1e3 * float(np.median(lat))}
+               'p50_step_ms': 1e3 * float(np.median(lat)), 'stage_ms_per_step': stages}
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
