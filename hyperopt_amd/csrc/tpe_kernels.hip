@@ -221,7 +221,10 @@ __device__ __forceinline__ int tile_pos(int cand_start, int j) {
 }
 
 // ================================================================= sample
-// Draws (when `draw`) and writes the sort keys: (problem << 32) | ordered(coord).
+// Draws (when `draw`) and writes the sort keys: (problem << key_bits) | value
+// bucket.  Grid (tiles, kR): block (x, y) handles the y-th 256-candidate slice
+// of tile x, one candidate per thread — a 2^20-candidate problem runs 4096
+// workgroups (16 waves per CU) rather than 512 latency-bound ones.
 __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restrict__ P,
                                                      const tpe_tile* __restrict__ tiles,
                                                      const double* __restrict__ samp,
@@ -250,62 +253,63 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
   if (in_lds)
     for (int q = threadIdx.x; q < p.samp_len; q += kThreads) cum_lds[q] = S[8 * q];
   __syncthreads();
-  for (int j = 0; j < kR; ++j) {
-    const int i = tl.cand_start + (int)threadIdx.x + j * kThreads;
-    if (i >= p.n_cand) break;
-    const int64_t o = p.cand_off + i;
-    if (draw) {
-      if (p.samp_len <= 0) { cand[o] = NAN; coord[o] = NAN; }
-      else {
-        const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-        const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-        // component choice: first k with u < cum_k (binary search, <= 27 rows)
-        const double u1 = u01d(r.x, r.y);
-        int a = 0, b = p.samp_len - 1;
-        if (in_lds)
-          while (a < b) { const int m = (a + b) >> 1; if (u1 < cum_lds[m]) b = m; else a = m + 1; }
-        else
-          while (a < b) { const int m = (a + b) >> 1; if (u1 < S[8 * m]) b = m; else a = m + 1; }
-        const double* s = S + 8 * a;
-        if (p.family == TPE_FAM_CATEGORICAL) {
-          cand[o] = (double)a;
-          coord[o] = (float)a;
-        } else {
-          // truncated normal by inversion; fa, fb = Phi of the (mirrored) bounds
-          const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
-          const bool flip = s[5] != 0.0;
-          double x;      // draw in sampling space (log space for LGMM1)
-          if (precision == TPE_PREC_F32) {
-            const float pr = (float)fa + u01f(r.z) * ((float)fb - (float)fa);
-            float z = -1.41421356237309505f * erfcinvf(2.f * pr);
-            if (flip) z = -z;
-            float xf = (float)mu + (float)sg * z;
-            if (!(xf == xf)) xf = (float)mu;
-            xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
-            coord[o] = xf;
-            x = (double)xf;
-          } else {
-            const double pr = fa + u01d(r.z, r.w) * (fb - fa);
-            double z = -1.41421356237309505 * erfcinv(2.0 * pr);
-            if (flip) z = -z;
-            x = mu + sg * z;
-            if (!(x == x)) x = mu;
-            if ((p.flags & TPE_F_HAS_LOW) && x < lo) x = lo;
-            if ((p.flags & TPE_F_HAS_HIGH) && x >= hi) x = nextafter(hi, -INFINITY);
-            coord[o] = (float)x;
-          }
-          if (logsp) x = exp(x);
-          if (quant) x = rint(x / p.q) * p.q;      // np.round: half to even
-          cand[o] = x;
-        }
+  const int i = tl.cand_start + (int)threadIdx.x + (int)blockIdx.y * kThreads;
+  if (i >= p.n_cand) return;
+  const int64_t o = p.cand_off + i;
+  float t;                                 // kernel coordinate of the candidate
+  if (!draw) {
+    t = coord[o];
+  } else if (p.samp_len <= 0) {
+    cand[o] = NAN; coord[o] = NAN; t = NAN;
+  } else {
+    const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+    const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+    // component choice: first k with u < cum_k (binary search, <= 27 rows)
+    const double u1 = u01d(r.x, r.y);
+    int a = 0, b = p.samp_len - 1;
+    if (in_lds)
+      while (a < b) { const int m = (a + b) >> 1; if (u1 < cum_lds[m]) b = m; else a = m + 1; }
+    else
+      while (a < b) { const int m = (a + b) >> 1; if (u1 < S[8 * m]) b = m; else a = m + 1; }
+    const double* s = S + 8 * a;
+    if (p.family == TPE_FAM_CATEGORICAL) {
+      cand[o] = (double)a;
+      t = (float)a;
+    } else {
+      // truncated normal by inversion; fa, fb = Phi of the (mirrored) bounds
+      const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
+      const bool flip = s[5] != 0.0;
+      double x;      // draw in sampling space (log space for LGMM1)
+      if (precision == TPE_PREC_F32) {
+        const float pr = (float)fa + u01f(r.z) * ((float)fb - (float)fa);
+        float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+        if (flip) z = -z;
+        float xf = (float)mu + (float)sg * z;
+        if (!(xf == xf)) xf = (float)mu;
+        xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
+        t = xf;
+        x = (double)xf;
+      } else {
+        const double pr = fa + u01d(r.z, r.w) * (fb - fa);
+        double z = -1.41421356237309505 * erfcinv(2.0 * pr);
+        if (flip) z = -z;
+        x = mu + sg * z;
+        if (!(x == x)) x = mu;
+        if ((p.flags & TPE_F_HAS_LOW) && x < lo) x = lo;
+        if ((p.flags & TPE_F_HAS_HIGH) && x >= hi) x = nextafter(hi, -INFINITY);
+        t = (float)x;
       }
+      if (logsp) x = exp(x);
+      if (quant) x = rint(x / p.q) * p.q;      // np.round: half to even
+      cand[o] = x;
     }
-    // sort key: (problem, value bucket) — only locality matters for pruning
-    const float gb = floorf((coord[o] - p.key_lo) * p.key_inv);
-    const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
-    keys[o] = khi | bucket;
-    vals[o] = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(coord[o]);
+    coord[o] = t;
   }
+  // sort key: (problem, value bucket) — only locality matters for pruning
+  const float gb = floorf((t - p.key_lo) * p.key_inv);
+  const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
+  keys[o] = khi | bucket;
+  vals[o] = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(t);
 }
 
 // ============================================================ score above
@@ -464,6 +468,13 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
 }
 
 // =============================================================== finalize
+// Grid (tiles, TPE_BEST_PER_TILE): one candidate per thread, 256-thread
+// workgroups, so the latency-bound stage (dependent loads, <= 26 below
+// components) keeps many workgroups in flight.  Each workgroup writes one
+// tile_best slot; candidates may be visited in any order because the argmax
+// compares ORIGINAL indices.
+static_assert(TPE_BEST_PER_TILE * kThreads == kTile, "finalize slices must cover a tile");
+
 __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __restrict__ P,
                                                        const tpe_tile* __restrict__ tiles,
                                                        const float4* __restrict__ comp32,
@@ -477,41 +488,32 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   const int n = p.n_cand;
-  double bs = 0, bl = 0, bg = 0;
-  int64_t bi = -1;
-  // issue every load of this lane's candidates up front (vals, split partial
-  // sums, candidate values) so their latencies overlap
-  const bool from_t = sampled && precision == TPE_PREC_F32 &&
-                      (p.family == TPE_FAM_GAUSS || p.family == TPE_FAM_LOGGAUSS);
-  uint64_t vv[kR];
-  double sav[kR], xv[kR];
-#pragma unroll
-  for (int j = 0; j < kR; ++j) {
-    const int i = tile_pos(tl.cand_start, j);
-    vv[j] = i < n ? vals[p.cand_off + i] : 0;
-    sav[j] = 0.0;
-  }
-  for (int sp = 0; sp < p.n_splits; ++sp) {
-    const double* __restrict__ ps = part + p.part_off + (int64_t)sp * n;
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-      const int i = tile_pos(tl.cand_start, j);
-      if (i < n) sav[j] += ps[i];
+  const int i = tl.cand_start + (int)threadIdx.x + (int)blockIdx.y * kThreads;
+  const bool valid = i < n;
+  // device-drawn candidates carry their coordinate t in the sort value: no
+  // gather of the candidate value (continuous families at f32, categorical)
+  const bool from_t = sampled && ((precision == TPE_PREC_F32 &&
+                                   (p.family == TPE_FAM_GAUSS || p.family == TPE_FAM_LOGGAUSS)) ||
+                                  p.family == TPE_FAM_CATEGORICAL);
+  const uint64_t v = valid ? vals[p.cand_off + i] : 0;
+  double sa = 0.0;
+  {
+    const double* __restrict__ ps = part + p.part_off + i;
+    const int ns = valid ? p.n_splits : 0;
+    int sp = 0;
+    for (; sp + 4 <= ns; sp += 4) {         // four loads in flight per step
+      const double a0 = ps[(int64_t)sp * n], a1 = ps[(int64_t)(sp + 1) * n];
+      const double a2 = ps[(int64_t)(sp + 2) * n], a3 = ps[(int64_t)(sp + 3) * n];
+      sa += a0; sa += a1; sa += a2; sa += a3;
     }
+    for (; sp < ns; ++sp) sa += ps[(int64_t)sp * n];
   }
-#pragma unroll
-  for (int j = 0; j < kR; ++j) {
-    const int i = tile_pos(tl.cand_start, j);
-    xv[j] = (!from_t && i < n) ? cand[(uint32_t)(vv[j] >> 32)] : 0.0;
-  }
-  for (int j = 0; j < kR; ++j) {
-    const int i = tile_pos(tl.cand_start, j);
-    if (i >= n) continue;
-    const uint64_t v = vv[j];
-    const uint32_t oo = (uint32_t)(v >> 32);       // original position
-    const int64_t orig = (int64_t)oo - p.cand_off; // original local index
-    const double x = xv[j];
-    double l, g;
+  const uint32_t oo = (uint32_t)(v >> 32);         // original position
+  const int64_t orig = valid ? (int64_t)oo - p.cand_off : -1;
+  const float tf = __uint_as_float((uint32_t)v);
+  const double x = !valid ? 0.0 : (from_t ? (double)tf : cand[oo]);
+  double l = 0, g = 0;
+  if (valid) {
     if (p.family == TPE_FAM_CATEGORICAL) {
       const int c = (int)x;
       if (c >= 0 && c < p.n_upper && (double)c == x) {
@@ -525,15 +527,13 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
       q_bounds(p, x, tu, tlo);
       const double mb = p.family == TPE_FAM_QGAUSS ? qmass<false>(comp64, p.below_off, p.below_len, tu, tlo)
                                                    : qmass<true>(comp64, p.below_off, p.below_len, tu, tlo);
-      const double ma = sav[j];
       l = log(mb) + p.below_base;
-      g = log(ma) + p.above_base;
+      g = log(sa) + p.above_base;
     } else {
       const bool logsp = p.family == TPE_FAM_LOGGAUSS;
-      const double sa = sav[j];
       double lb2, la2;
       if (precision == TPE_PREC_F32) {
-        const float t = __uint_as_float((uint32_t)v);
+        const float t = tf;
         lb2 = (double)lse2_fixed(comp32, p.below_off, p.below_len, t);
         // fixed-shift sum; if it under-flowed, redo this candidate max-shifted
         la2 = sa > 1e-30 ? log2(sa)
@@ -544,41 +544,49 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
         lb2 = lse2_exact64(comp64, p.below_off, p.below_len, t);
         la2 = sa > 1e-280 ? log2(sa) : lse2_exact64(comp64, p.above_off, p.above_len, t);
       }
-      const double lnx = !logsp ? 0.0 : (from_t ? (double)__uint_as_float((uint32_t)v) : log(x));
+      const double lnx = !logsp ? 0.0 : (from_t ? (double)tf : log(x));
       l = lb2 * kLn2 + p.below_base - lnx;
       g = la2 * kLn2 + p.above_base - lnx;
     }
-    const double sc = l - g;
     if (l_out) { l_out[oo] = l; g_out[oo] = g; }
-    if (better(sc, orig, bs, bi)) { bs = sc; bl = l; bg = g; bi = orig; }
   }
-  // wave reduction, then across the 4 waves through LDS
+  const double sc = l - g;
+  // wave argmax on (score, original index) only; the winning lane (unique
+  // index) then publishes its l and g
+  double bs = sc;
+  int64_t bi = orig;
   for (int off = 32; off > 0; off >>= 1) {
-    const double os = __shfl_xor(bs, off), ol = __shfl_xor(bl, off), og = __shfl_xor(bg, off);
+    const double os = __shfl_xor(bs, off);
     const int64_t oi = __shfl_xor(bi, off);
-    if (better(os, oi, bs, bi)) { bs = os; bl = ol; bg = og; bi = oi; }
+    if (better(os, oi, bs, bi)) { bs = os; bi = oi; }
   }
   __shared__ tpe_best wb[kThreads / 64];
   const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) wb[wave] = tpe_best{bs, bl, bg, bi};
+  if ((threadIdx.x & 63) == 0 && bi < 0) wb[wave] = tpe_best{0, 0, 0, -1};
+  if (bi >= 0 && orig == bi) wb[wave] = tpe_best{bs, l, g, bi};
   __syncthreads();
   if (threadIdx.x == 0) {
     tpe_best b = wb[0];
     for (int q = 1; q < kThreads / 64; ++q)
       if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
-    tile_best[blockIdx.x] = b;
+    tile_best[(int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y] = b;
   }
 }
 
 // ================================================================= select
-__global__ __launch_bounds__(kThreads) void k_select(const tpe_problem* __restrict__ P,
+// One 1024-thread workgroup per problem: reads the problem's
+// n_tiles * TPE_BEST_PER_TILE slot bests (4096 at 2^20 candidates).
+constexpr int kSelThreads = 1024;
+__global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __restrict__ P,
                                                      const tpe_best* __restrict__ tile_best,
                                                      const double* __restrict__ cand,
                                                      tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
   tpe_best b{0, 0, 0, -1};
-  for (int t = threadIdx.x; t < p.n_tiles; t += kThreads) {
-    const tpe_best o = tile_best[p.tile_off + t];
+  const int64_t nb = (int64_t)p.n_tiles * TPE_BEST_PER_TILE;
+  const tpe_best* __restrict__ tb = tile_best + (int64_t)p.tile_off * TPE_BEST_PER_TILE;
+  for (int64_t t = threadIdx.x; t < nb; t += kSelThreads) {
+    const tpe_best o = tb[t];
     if (better(o.score, o.idx, b.score, b.idx)) b = o;
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -587,12 +595,12 @@ __global__ __launch_bounds__(kThreads) void k_select(const tpe_problem* __restri
     o.idx = __shfl_xor(b.idx, off);
     if (better(o.score, o.idx, b.score, b.idx)) b = o;
   }
-  __shared__ tpe_best wb[kThreads / 64];
+  __shared__ tpe_best wb[kSelThreads / 64];
   if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = b;
   __syncthreads();
   if (threadIdx.x == 0) {
     b = wb[0];
-    for (int q = 1; q < kThreads / 64; ++q)
+    for (int q = 1; q < kSelThreads / 64; ++q)
       if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
     tpe_result r;
     r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
@@ -917,7 +925,7 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->sample && !b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
   if (b->n_tiles == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
+  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, kR), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
                      b->samp, b->cand, b->coord, b->keys, b->vals, b->precision, b->sample, b->key_bits);
   return hip_check("tpe_sample");
 }
@@ -965,7 +973,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_tiles == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
+  hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
                      (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->vals_sorted,
                      b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample);
   return hip_check("tpe_finalize");
@@ -975,7 +983,7 @@ int tpe_select(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_problems == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
+  hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
                      b->tile_best, b->cand, b->result);
   return hip_check("tpe_select");
 }

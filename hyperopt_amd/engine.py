@@ -13,7 +13,7 @@ Device layout (HBM, all caller-owned, grow-only pools):
   cand      double[C_total]           candidate values (returned to the user)
   coord     float[C_total]            kernel coordinate (x or ln x) in f32
   part      double[sum_p splits_p*C_p] above-mixture partial sums
-  tile_best tpe_best[T], result tpe_result[P]
+  tile_best tpe_best[T * BEST_PER_TILE], result tpe_result[P]
 Mixtures are shared by every problem of the same hyperparameter (the history
 is common to all new_ids), so component tables scale with labels, not ids.
 """
@@ -98,8 +98,11 @@ class Engine(object):
         self._bufs = {}
         self._pinned = None
         # when a dict: every run() times each stage with HIP events on the
-        # launch stream and appends (ms, CE of the launch) under the kernel name
+        # launch stream and appends (ms, CE of the launch) under the kernel name;
+        # profile_repeat > 1 re-issues each (idempotent) stage back to back and
+        # reports the mean (steady-state stage cost, tools/stage_bench.py)
         self.profile = None
+        self.profile_repeat = 1
 
     def set_precision(self, precision):
         if precision not in ('fp32', 'fp64'):
@@ -357,7 +360,7 @@ class Engine(object):
         d_coord = self._buf('coord', C_total, torch.float32)
         d_part = self._buf('part', info.part_total, torch.float64)
         n_tiles = int(info.n_tiles)
-        d_best = self._buf('best', n_tiles * 4, torch.float64)
+        d_best = self._buf('best', n_tiles * N.BEST_PER_TILE * 4, torch.float64)
         d_res = self._buf('result', P * 6, torch.float64)
         d_keys = self._buf('keys', C_total, torch.int32)
         d_vals = self._buf('vals', C_total, torch.int64)
@@ -473,21 +476,22 @@ class Engine(object):
         cur = torch.cuda.current_stream(self.device)
         evs[0].record(cur)
         work0 = b.work
+        rep = max(1, int(self.profile_repeat))
         for i, (name, fn, gi, units) in enumerate(stages):
+            arg = b
             if gi is not None:
-                sub = N.Batch.from_buffer_copy(b)
-                sub.n_work_cont, sub.n_work_qgauss, sub.n_work_qlog = [c if j == gi else 0 for j, c in
+                arg = N.Batch.from_buffer_copy(b)
+                arg.n_work_cont, arg.n_work_qgauss, arg.n_work_qlog = [c if j == gi else 0 for j, c in
                                                                        enumerate(counts)]
-                sub.work = work0 + N.WORK_DTYPE.itemsize * sum(counts[:gi])   # this group's first item
-                N.check(fn(ctypes.byref(sub), ctypes.c_void_p(stream)), self.lib, name)
-            else:
-                N.check(fn(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, name)
+                arg.work = work0 + N.WORK_DTYPE.itemsize * sum(counts[:gi])   # this group's first item
+            for _ in range(rep):
+                N.check(fn(ctypes.byref(arg), ctypes.c_void_p(stream)), self.lib, name)
             evs[i + 1].record(cur)
         evs[-1].synchronize()
         executed = int(cnt[:counts[0]].sum().item()) if counts[0] else 0
         b.ce_count = None
         for i, (name, fn, gi, units) in enumerate(stages):
-            rec = (evs[i].elapsed_time(evs[i + 1]), units)
+            rec = (evs[i].elapsed_time(evs[i + 1]) / rep, units)
             if name == 'k_above_f32':
                 rec = rec + (float(executed),)
             self.profile.setdefault(name, []).append(rec)

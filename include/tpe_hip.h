@@ -34,7 +34,10 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 3
+#define TPE_ABI_VERSION 4
+
+/* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
+#define TPE_BEST_PER_TILE 8
 
 /* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
 enum {
@@ -134,7 +137,7 @@ typedef struct tpe_work {
   int32_t reserved;
 } tpe_work;
 
-/* per-tile best, written by the finalize stage */
+/* best of one finalize slot (TPE_BEST_PER_TILE per tile), written by the finalize stage */
 typedef struct tpe_best {
   double score, l, g;
   int64_t idx;           /* local candidate index, -1 if none */
@@ -204,7 +207,7 @@ typedef struct tpe_batch {
   double* part;          /* above-mixture partial sums                          */
   double* l_out;         /* optional [total_cand] (original order); NULL to skip */
   double* g_out;         /* optional [total_cand]; NULL to skip                 */
-  tpe_best* tile_best;   /* [n_tiles]                                          */
+  tpe_best* tile_best;   /* [n_tiles * TPE_BEST_PER_TILE]                      */
   tpe_result* result;    /* [n_problems]                                       */
   unsigned long long* ce_count; /* optional [n_work_cont]: component evaluations executed
                                    per work item by the pruned kernel; NULL to skip */

@@ -1,0 +1,37 @@
+"""Steady-state per-stage device time of the headline suggest's levels: every
+stage re-issued back to back (Engine.profile_repeat), HIP events on the
+launch stream.  Prints one line per (level, stage)."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from hyperopt_amd import history as H, tpe  # noqa: E402
+from hyperopt_amd.engine import LevelProblem, get_engine  # noqa: E402
+
+
+def main():
+    rep = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    eng = get_engine(torch.device('cuda', 0))
+    domain, trials = bench.make_history(bench.N_HISTORY, bench.SEED)
+    hist = H.extract(domain, trials)
+    fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, eng)
+    T = domain.table
+    for lv in (['model'], ['svm_C', 'svm_kernel'], ['svm_rbf_gamma']):
+        probs = [LevelProblem(fits.get(T.by_label[l]), T.by_label[l].index, [bench.N_HISTORY]) for l in lv]
+        eng.run(probs, bench.C_PER_GPU, 5)
+        eng.profile, eng.profile_repeat = {}, rep
+        eng.run(probs, bench.C_PER_GPU, 5)
+        torch.cuda.synchronize()
+        for k, v in eng.profile.items():
+            print('%-28s %-16s %8.1f us' % ('+'.join(lv), k, 1e3 * float(np.mean([a[0] for a in v]))))
+        eng.profile, eng.profile_repeat = None, 1
+
+
+if __name__ == '__main__':
+    main()
