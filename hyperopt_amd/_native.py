@@ -107,11 +107,36 @@ class PackInfo(ctypes.Structure):
     ]
 
 
+class LevelWS(ctypes.Structure):
+    """tpe_level_ws: caller-owned buffers of tpe_level_run."""
+    _fields_ = [
+        ('pinned', ctypes.c_void_p), ('pinned_bytes', ctypes.c_int64),
+        ('blob', ctypes.c_void_p), ('blob_bytes', ctypes.c_int64),
+        ('cand', ctypes.c_void_p), ('coord', ctypes.c_void_p),
+        ('keys', ctypes.c_void_p), ('vals', ctypes.c_void_p), ('keys_sorted', ctypes.c_void_p),
+        ('vals_sorted', ctypes.c_void_p), ('cand_cap', ctypes.c_int64),
+        ('sort_tmp', ctypes.c_void_p), ('sort_tmp_bytes', ctypes.c_int64),
+        ('part', ctypes.c_void_p), ('part_cap', ctypes.c_int64),
+        ('tile_best', ctypes.c_void_p), ('best_cap', ctypes.c_int64),
+        ('result', ctypes.c_void_p), ('result_cap', ctypes.c_int64),
+        ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
+        ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p), ('fit_cap', ctypes.c_int64),
+        ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_int64),
+    ]
+
+
+class LevelNeed(ctypes.Structure):
+    """tpe_level_need: sizes one level needs."""
+    _fields_ = [(k, ctypes.c_int64) for k in ('pinned_bytes', 'blob_bytes', 'cand', 'sort_tmp_bytes', 'part',
+                                              'best', 'result', 'fit', 'fit_tmp_bytes')]
+
+
 E_SPACE = -4
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
            'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above',
-           'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_cat_probs', 'tpe_host_pack_level')
+           'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_cat_probs', 'tpe_host_pack_level',
+           'tpe_level_run')
 
 
 class NativeUnavailable(RuntimeError):
@@ -155,6 +180,10 @@ def load(path=LIB_PATH):
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64,
                                         ctypes.POINTER(PackInfo)]
     lib.tpe_host_pack_level.restype = ctypes.c_int
+    lib.tpe_level_run.argtypes = [ctypes.POINTER(LabelIn), ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                  ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(LevelWS),
+                                  ctypes.POINTER(LevelNeed), P, P]
+    lib.tpe_level_run.restype = ctypes.c_int
     if lib.tpe_abi_version() != ABI_VERSION:
         raise NativeUnavailable('ABI mismatch: library %d, bindings %d' % (lib.tpe_abi_version(), ABI_VERSION))
     _LIB = lib

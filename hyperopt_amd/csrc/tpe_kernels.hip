@@ -999,4 +999,95 @@ int tpe_run_batch(const tpe_batch* b, void* stream) {
   return tpe_select(b, stream);
 }
 
+int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
+                  int64_t n_cand_global, int32_t precision, const tpe_level_ws* ws, tpe_level_need* need,
+                  void* stream, tpe_result* out) {
+  if (!ws || !need || (n_labels > 0 && !out)) return fail(TPE_E_ARG, "null workspace/need/out");
+  memset(need, 0, sizeof(*need));
+  tpe_pack_info info;
+  memset(&info, 0, sizeof(info));
+  // pack straight into the pinned staging buffer; the result readback area
+  // follows the blob
+  int rc = tpe_host_pack_level(labels, n_labels, n_cand, seed, cand_base, n_cand_global, precision, ws->pinned,
+                               ws->pinned_bytes, &info);
+  if (rc != TPE_OK && rc != TPE_E_SPACE) return fail(rc, "tpe_host_pack_level: bad level description");
+  const int64_t P = info.n_problems, C = P * (int64_t)n_cand;
+  const int64_t res_off = (info.blob_bytes + 255) & ~(int64_t)255;
+  need->pinned_bytes = res_off + P * (int64_t)sizeof(tpe_result);
+  need->blob_bytes = info.blob_bytes;
+  need->cand = C;
+  need->part = info.part_total;
+  need->best = info.n_tiles * TPE_BEST_PER_TILE;
+  need->result = P;
+  need->fit = info.fit_total;
+  if (C >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one level: shard the batch");
+  uint64_t sz = 0;
+  if (info.sort_end_bit > 0 && C > 0) {
+    if ((rc = tpe_sort_workspace_bytes(C, &sz))) return rc;
+    need->sort_tmp_bytes = (int64_t)sz;
+  }
+  if (info.n_fit > 0) {
+    if ((rc = tpe_fit_workspace_bytes(info.fit_total, info.n_fit, &sz))) return rc;
+    need->fit_tmp_bytes = (int64_t)sz;
+  }
+  if (rc == TPE_E_SPACE || need->pinned_bytes > ws->pinned_bytes || need->blob_bytes > ws->blob_bytes ||
+      need->cand > ws->cand_cap || need->part > ws->part_cap || need->best > ws->best_cap ||
+      need->result > ws->result_cap || need->fit > ws->fit_cap || need->sort_tmp_bytes > ws->sort_tmp_bytes ||
+      need->fit_tmp_bytes > ws->fit_tmp_bytes)
+    return fail(TPE_E_SPACE, "level workspace too small (see tpe_level_need)");
+  if (P == 0) return TPE_OK;
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* host = (unsigned char*)ws->pinned;
+  unsigned char* dev = (unsigned char*)ws->blob;
+  // host-written ranges only: device-fitted rows are produced by tpe_fit_above
+  hipError_t e = hipMemcpyAsync(dev, host, (size_t)info.copy_end, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && info.copy2_len > 0)
+    e = hipMemcpyAsync(dev + info.off_comp32, host + info.off_comp32, (size_t)info.copy2_len, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  tpe_batch b;
+  memset(&b, 0, sizeof(b));
+  b.problems = (const tpe_problem*)(dev + info.off_problems);
+  b.n_problems = (int32_t)P;
+  b.precision = precision;
+  b.sample = 1;
+  b.sort_end_bit = info.sort_end_bit;
+  b.key_bits = info.key_bits;
+  b.comp32 = (const float*)(dev + info.off_comp32);
+  b.comp64 = (const double*)(dev + info.off_comp64);
+  b.samp = (const double*)(dev + info.off_samp);
+  b.grid = (const int32_t*)(dev + info.off_grid);
+  b.cand = ws->cand; b.coord = ws->coord; b.keys = ws->keys; b.vals = ws->vals;
+  if (info.sort_end_bit > 0) {
+    b.keys_sorted = ws->keys_sorted; b.vals_sorted = ws->vals_sorted;
+    b.sort_tmp = ws->sort_tmp; b.sort_tmp_bytes = (uint64_t)ws->sort_tmp_bytes;
+  } else {
+    b.keys_sorted = ws->keys; b.vals_sorted = ws->vals;
+  }
+  b.total_cand = C;
+  b.tiles = (const tpe_tile*)(dev + info.off_tiles);
+  b.n_tiles = (int32_t)info.n_tiles;
+  b.work = (const tpe_work*)(dev + info.off_work);
+  b.n_work_cont = info.n_work_cont; b.n_work_qgauss = info.n_work_qgauss; b.n_work_qlog = info.n_work_qlog;
+  b.part = ws->part;
+  b.tile_best = ws->tile_best;
+  b.result = ws->result;
+  if (info.n_fit > 0) {
+    b.fit = (const tpe_fit_job*)(dev + info.off_fit);
+    b.n_fit = info.n_fit;
+    b.below_idx = (const int32_t*)(dev + info.off_below_idx);
+    b.fit_seg = (const int64_t*)(dev + info.off_fit_seg);
+    b.fit_total = info.fit_total;
+    b.fit_keys = ws->fit_keys; b.fit_keys_sorted = ws->fit_keys_sorted;
+    b.fit_vals = ws->fit_vals; b.fit_vals_sorted = ws->fit_vals_sorted;
+    b.fit_tmp = ws->fit_tmp; b.fit_tmp_bytes = (uint64_t)ws->fit_tmp_bytes;
+  }
+  if ((rc = tpe_run_batch(&b, stream))) return rc;
+  tpe_result* rh = (tpe_result*)(host + res_off);
+  e = hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  memcpy(out, rh, (size_t)P * sizeof(tpe_result));
+  return TPE_OK;
+}
+
 }  // extern "C"

@@ -97,6 +97,7 @@ class Engine(object):
         self.set_precision(precision)
         self._bufs = {}
         self._pinned = None
+        self._ws = None                   # cached tpe_level_ws (run_level)
         # when a dict: every run() times each stage with HIP events on the
         # launch stream and appends (ms, CE of the launch) under the kernel name;
         # profile_repeat > 1 re-issues each (idempotent) stage back to back and
@@ -117,6 +118,7 @@ class Engine(object):
             cap = max(n, int(1.25 * (t.numel() if t is not None else 0)))
             t = torch.empty(cap, dtype=dtype, device=self.device)
             self._bufs[name] = t
+            self._ws = None
         return t
 
     # ------------------------------------------------------------- tables
@@ -280,9 +282,10 @@ class Engine(object):
                     samp=np.concatenate(samp) if samp else np.zeros((0, 8)), P=P)
 
     # ---------------------------------------------------------------- pack
-    def _pack(self, problems, n_cand, seed, cand_base, n_cand_global):
-        """Pack one level with the native host runtime straight into the pinned
-        staging buffer; returns (PackInfo, blob bytes)."""
+    @staticmethod
+    def _labels(problems):
+        """tpe_label_in array of one level (plus the arrays it points into,
+        which the caller keeps alive for the native call)."""
         n = len(problems)
         labels = (N.LabelIn * max(n, 1))()
         keep = []
@@ -313,6 +316,13 @@ class Engine(object):
             ids = np.ascontiguousarray(lp.ids, dtype=np.int64)
             keep.append(ids)
             L.ids, L.n_ids = ids.ctypes.data, len(ids)
+        return labels, keep
+
+    def _pack(self, problems, n_cand, seed, cand_base, n_cand_global):
+        """Pack one level with the native host runtime straight into the pinned
+        staging buffer; returns the PackInfo."""
+        n = len(problems)
+        labels, keep = self._labels(problems)
         info = N.PackInfo()
         prec = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
         seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -326,10 +336,92 @@ class Engine(object):
             if rc == N.E_SPACE:
                 self._pinned = torch.empty(max(info.blob_bytes, 2 * cap), dtype=torch.uint8,
                                            pin_memory=torch.cuda.is_available())
+                self._ws = None
                 continue
             N.check(rc, self.lib, 'tpe_host_pack_level')
             break
         return info
+
+    # ----------------------------------------------------- one-call level
+    def _level_ws(self):
+        """tpe_level_ws over the engine's pools (rebuilt when a pool grows)."""
+        ws = self._ws
+        if ws is not None:
+            return ws
+        B = self._bufs
+        ws = N.LevelWS()
+
+        def dev(name, itemsize):
+            t = B.get(name)
+            return (t.data_ptr(), t.numel() * t.element_size() // itemsize) if t is not None else (None, 0)
+        pin = self._pinned
+        ws.pinned, ws.pinned_bytes = (pin.data_ptr(), pin.numel()) if pin is not None else (None, 0)
+        ws.blob, ws.blob_bytes = dev('blob', 1)
+        ws.cand, n1 = dev('cand', 8)
+        ws.coord, n2 = dev('coord', 4)
+        ws.keys, n3 = dev('keys', 4)
+        ws.vals, n4 = dev('vals', 8)
+        ws.keys_sorted, n5 = dev('keys_sorted', 4)
+        ws.vals_sorted, n6 = dev('vals_sorted', 8)
+        ws.cand_cap = min(n1, n2, n3, n4, n5, n6)
+        ws.sort_tmp, ws.sort_tmp_bytes = dev('sort_tmp', 1)
+        ws.part, ws.part_cap = dev('part', 8)
+        ws.tile_best, ws.best_cap = dev('best', 32)
+        ws.result, ws.result_cap = dev('result', 48)
+        ws.fit_keys, f1 = dev('fit_keys', 8)
+        ws.fit_keys_sorted, f2 = dev('fit_keys_sorted', 8)
+        ws.fit_vals, f3 = dev('fit_vals', 4)
+        ws.fit_vals_sorted, f4 = dev('fit_vals_sorted', 4)
+        ws.fit_cap = min(f1, f2, f3, f4)
+        ws.fit_tmp, ws.fit_tmp_bytes = dev('fit_tmp', 1)
+        self._ws = ws
+        return ws
+
+    def _grow(self, need):
+        if need.pinned_bytes > (self._pinned.numel() if self._pinned is not None else 0):
+            self._pinned = torch.empty(int(need.pinned_bytes * 1.25) + 4096, dtype=torch.uint8,
+                                       pin_memory=torch.cuda.is_available())
+        self._buf('blob', need.blob_bytes, torch.uint8)
+        for name, dt in (('cand', torch.float64), ('coord', torch.float32), ('keys', torch.int32),
+                         ('vals', torch.int64), ('keys_sorted', torch.int32), ('vals_sorted', torch.int64)):
+            self._buf(name, need.cand, dt)
+        self._buf('sort_tmp', need.sort_tmp_bytes, torch.uint8)
+        self._buf('part', need.part, torch.float64)
+        self._buf('best', need.best * 4, torch.float64)
+        self._buf('result', need.result * 6, torch.float64)
+        for name, dt in (('fit_keys', torch.float64), ('fit_keys_sorted', torch.float64),
+                         ('fit_vals', torch.int32), ('fit_vals_sorted', torch.int32)):
+            self._buf(name, need.fit, dt)
+        self._buf('fit_tmp', need.fit_tmp_bytes, torch.uint8)
+        self._ws = None
+
+    def run_level(self, problems, n_cand, seed, cand_base=0, n_cand_global=None):
+        """``run`` for device-drawn candidates without per-candidate outputs:
+        one native call (tpe_level_run) packs, uploads, launches every stage
+        and reads the per-problem results back.  Returns RESULT_DTYPE [P]."""
+        n_cand = int(n_cand)
+        if n_cand < 0 or n_cand >= 2 ** 31:
+            raise ValueError('n_EI_candidates out of range: %r' % n_cand)
+        if self.profile is not None:
+            return self.run(problems, n_cand, seed, cand_base=cand_base, n_cand_global=n_cand_global)
+        labels, keep = self._labels(problems)
+        P = sum(len(lp.ids) for lp in problems)
+        out = np.empty(P, dtype=N.RESULT_DTYPE)
+        need = N.LevelNeed()
+        prec = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
+        seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
+        ncg = int(n_cand_global) if n_cand_global is not None else 0
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for attempt in range(3):
+            ws = self._level_ws()
+            rc = self.lib.tpe_level_run(labels, len(problems), n_cand, seed64, int(cand_base), ncg, prec,
+                                        ctypes.byref(ws), ctypes.byref(need), stream, out.ctypes.data)
+            if rc != N.E_SPACE:
+                break
+            self._grow(need)
+        N.check(rc, self.lib, 'tpe_level_run')
+        del keep
+        return out
 
     # ---------------------------------------------------------------- run
     def run(self, problems, n_cand, seed, cand_base=0, want_lg=False, return_cand=False, n_cand_global=None):

@@ -183,6 +183,8 @@ class ParamTable(object):
         for r in self.rows:
             r.depth = depth(r)
         self.n_levels = 1 + max((r.depth for r in self.rows), default=-1)
+        # labels that gate other labels (switch index parameters)
+        self.parent_labels = frozenset(p[0] for r in self.rows for p in r.parents if p is not None)
 
     def __len__(self):
         return len(self.rows)

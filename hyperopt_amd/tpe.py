@@ -91,14 +91,90 @@ def _value(row, v):
 
 def _run(engine, problems, C, seed, shard):
     if shard is None:
-        return engine.run(problems, C, seed)
+        return engine.run_level(problems, C, seed)
     rank, world = shard
     lo, hi = _dist.shard_range(C, rank, world)
-    res = engine.run(problems, hi - lo, seed, cand_base=lo, n_cand_global=C)
+    res = engine.run_level(problems, hi - lo, seed, cand_base=lo, n_cand_global=C)
     return _dist.allgather_results(res, device=engine.device)
 
 
+# speculative level fusion (_choices_fused): on by default; a gating
+# categorical's winner is predicted when the expected number of draws of the
+# predicted category is at least SPECULATE_MIN_DRAWS
+SPECULATE = True
+SPECULATE_MIN_DRAWS = 64.0
+
+
+def _predict_activity(table, fits, C):
+    """Predicted {label: category or None} of a conditional space, or None.
+
+    A switch index (categorical) scores every candidate by the same per-category
+    value log p_below[c] - log p_above[c] (categorical_lpdf, tpe.py:50-57), so
+    its argmax (broadcast_best, tpe.py:749-759) is the best category among the
+    categories drawn — with C candidates, the best category of the fitted
+    posteriors unless it goes undrawn (probability (1 - q)^C).  Labels that are
+    not gates get a placeholder.  Any non-categorical gate: no prediction."""
+    chosen = {}
+    for level in table.levels():
+        for row in level:
+            if not table.active(row, chosen):
+                chosen[row.label] = None
+            elif row.label not in table.parent_labels:
+                chosen[row.label] = -1
+            elif not row.categorical:
+                return None
+            else:
+                post = fits.get(row)
+                pb = np.asarray(post.below[0], dtype=np.float64)
+                pa = np.asarray(post.above[0], dtype=np.float64)
+                tot = pb.sum()
+                if not tot > 0:
+                    return None
+                with np.errstate(divide='ignore', invalid='ignore'):
+                    score = np.log(pb) - np.log(pa)
+                score[~(pb > 0)] = -np.inf           # never drawn
+                c = int(np.argmax(score))
+                if not (pb[c] > 0) or C * pb[c] / tot < SPECULATE_MIN_DRAWS:
+                    return None
+                chosen[row.label] = c
+    return chosen
+
+
+def _choices_fused(table, fits, new_ids, seed, C, engine, shard):
+    """Every tree level in ONE device batch under the predicted activity; the
+    gates' device winners are then checked against the prediction.  A problem's
+    draws depend only on (seed, label, new_id) and its scores on the fits, so a
+    verified batch chooses what the level-by-level evaluation chooses (up to
+    the fp32 summation order of pruned above mixtures, which follows the batch
+    layout).  Returns None on a misprediction (the caller then evaluates level
+    by level)."""
+    pred = _predict_activity(table, fits, C)
+    if pred is None:
+        return None
+    ids = np.asarray(new_ids, dtype=np.int64)
+    rows = [r for r in table.rows if pred[r.label] is not None]
+    problems = [LevelProblem(fits.get(r), r.index, ids) for r in rows]
+    res = _run(engine, problems, C, seed, shard)
+    n = len(ids)
+    order = [r.label for level in table.levels() for r in level]
+    chosen = [dict((k, None) for k in order) for _ in new_ids]
+    for k, row in enumerate(rows):
+        for i in range(n):
+            r = res[k * n + i]
+            if r['idx'] < 0:
+                raise RuntimeError('no candidate selected for %r' % row.label)
+            v = _value(row, r['value'])
+            if pred[row.label] >= 0 and int(v) != pred[row.label]:
+                return None
+            chosen[i][row.label] = v
+    return chosen
+
+
 def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
+    if SPECULATE and table.n_levels > 1:
+        fused = _choices_fused(table, fits, new_ids, seed, C, engine, shard)
+        if fused is not None:
+            return fused
     ids = np.asarray(new_ids, dtype=np.int64)
     chosen = [dict() for _ in new_ids]
     for level in table.levels():

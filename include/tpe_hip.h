@@ -308,6 +308,40 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
                         int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
                         tpe_pack_info* info);
 
+/* ------------------------------------------------------------------------
+ * One-call level runner: pack (host) -> H2D -> fit/sample/sort/score/select ->
+ * D2H of the per-problem results -> stream synchronise.  This is the whole
+ * per-tree-level device round trip of tpe.suggest (tpe.py:663-701 for every
+ * active hyperparameter of the level) behind one C call, so the host language
+ * pays one foreign call per level.  All memory is caller-owned; the runner
+ * never allocates.
+ * ---------------------------------------------------------------------- */
+typedef struct tpe_level_ws {
+  void* pinned; int64_t pinned_bytes;          /* page-locked host staging (tables + result readback) */
+  void* blob; int64_t blob_bytes;              /* device copy of the packed tables                      */
+  double* cand; float* coord;                  /* device candidate pools, cand_cap elements each        */
+  uint32_t* keys; uint64_t* vals; uint32_t* keys_sorted; uint64_t* vals_sorted; int64_t cand_cap;
+  void* sort_tmp; int64_t sort_tmp_bytes;
+  double* part; int64_t part_cap;              /* elements                                              */
+  tpe_best* tile_best; int64_t best_cap;       /* elements                                              */
+  tpe_result* result; int64_t result_cap;      /* elements (device)                                     */
+  double* fit_keys; double* fit_keys_sorted;
+  uint32_t* fit_vals; uint32_t* fit_vals_sorted; int64_t fit_cap;   /* elements                    */
+  void* fit_tmp; int64_t fit_tmp_bytes;
+} tpe_level_ws;
+
+/* what a level needs (written on success and on TPE_E_SPACE) */
+typedef struct tpe_level_need {
+  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes;
+} tpe_level_need;
+
+/* Run one tree level: `labels` as for tpe_host_pack_level; `out` receives one
+ * tpe_result per (label, id) in order.  TPE_E_SPACE: a workspace is too small —
+ * `need` holds every size; grow and call again (nothing was launched). */
+int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
+                  int64_t n_cand_global, int32_t precision, const tpe_level_ws* ws, tpe_level_need* need,
+                  void* stream, tpe_result* out);
+
 #ifdef __cplusplus
 }
 #endif

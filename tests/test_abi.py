@@ -100,3 +100,49 @@ def test_engine_refuses_without_device():
     from hyperopt_amd.engine import Engine
     with pytest.raises(N.NativeUnavailable):
         Engine()
+
+
+CTYPES_MIRRORS = (('tpe_batch', N.Batch), ('tpe_label_in', N.LabelIn), ('tpe_pack_info', N.PackInfo),
+                  ('tpe_level_ws', N.LevelWS), ('tpe_level_need', N.LevelNeed))
+
+
+def test_ctypes_mirrors_match_c():
+    """Every field offset and the size of each ctypes mirror equal gcc's."""
+    lines = []
+    for cname, cls in CTYPES_MIRRORS:
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f, _ in cls._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f, cname, f))
+    prog = '#include <stdio.h>\n#include <stddef.h>\n#include "tpe_hip.h"\nint main(void) {\n%s\nreturn 0; }\n' % (
+        '\n'.join(lines))
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, 'm.c')
+        open(c, 'w').write(prog)
+        exe = os.path.join(d, 'm')
+        subprocess.check_call(['gcc', '-I', os.path.dirname(HEADER), c, '-o', exe])
+        out = subprocess.check_output([exe]).decode()
+    lay = dict((line.split()[0], int(line.split()[1])) for line in out.strip().splitlines())
+    for cname, cls in CTYPES_MIRRORS:
+        assert lay[cname] == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert getattr(cls, f).offset == lay[cname + '.' + f], (cname, f)
+
+
+def test_level_run_reports_space_without_gpu():
+    """tpe_level_run sizes a level before touching the device: with empty
+    workspaces it returns TPE_E_SPACE and the needs of a 2^20-candidate level
+    (an unpruned one: the sort workspace query needs a device)."""
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import Engine, LevelProblem
+    rs = np.random.RandomState(0)
+    post = parzen.fit_posterior('uniform', dict(low=-5.0, high=5.0), rs.uniform(-5, 5, 10),
+                                rs.uniform(-5, 5, 50), 1.0)
+    labels, keep = Engine._labels([LevelProblem(post, 0, [7, 8])])
+    ws, need = N.LevelWS(), N.LevelNeed()
+    lib = N.load()
+    out = np.empty(2, dtype=N.RESULT_DTYPE)
+    rc = lib.tpe_level_run(labels, 1, 1 << 20, 5, 0, 0, N.PREC_F32, ctypes.byref(ws), ctypes.byref(need), None,
+                           out.ctypes.data)
+    assert rc == N.E_SPACE
+    assert need.cand == 2 << 20 and need.result == 2 and need.best == 2 * 512 * N.BEST_PER_TILE
+    assert need.blob_bytes > 0 and need.pinned_bytes >= need.blob_bytes + 2 * 48 and need.part >= 2 << 20

@@ -142,3 +142,60 @@ def test_partial_kwargs_and_startup():
     argmin = fmin(lambda d: (d['a'] - 1) ** 2 + d['b'], {'a': hp.uniform('a', -3, 3), 'b': hp.randint('b', 4)},
                   algo=algo, max_evals=40, trials=t, rstate=np.random.RandomState(0))
     assert len(t) == 40 and set(argmin) == {'a', 'b'}
+
+
+def _tree_history(n, seed=0):
+    """bench.py's config-3 tree space with an n-trial synthetic history."""
+    import bench
+    return bench.make_history(n, seed)
+
+
+def test_fused_levels_match_level_by_level():
+    """Speculative level fusion (one device batch for every tree level, gates
+    verified afterwards) chooses what the level-by-level evaluation chooses:
+    exactly at fp64 (unpruned, no near-tie flips), gates exactly at fp32."""
+    from hyperopt_amd import tpe
+    domain, trials = _tree_history(3000)
+    C = 1 << 16
+    for precision in ('fp64', 'fp32'):
+        for seed in (3, 4):
+            fused = doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=C, precision=precision))
+            tpe.SPECULATE = False
+            try:
+                seq = doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=C, precision=precision))
+            finally:
+                tpe.SPECULATE = True
+            assert set(fused) == set(seq), (fused, seq)
+            for k in seq:
+                if precision == 'fp64' or k in domain.table.parent_labels:
+                    assert fused[k] == seq[k], (precision, seed, k, fused[k], seq[k])
+
+
+def test_fused_levels_misprediction_falls_back():
+    """A wrong gate prediction is detected on the device results and the
+    suggest falls back to level-by-level evaluation."""
+    from hyperopt_amd import history as H, tpe
+    from hyperopt_amd.engine import get_engine
+    domain, trials = _tree_history(3000)
+    hist = H.extract(domain, trials)
+    eng = get_engine()
+    fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, eng)
+    pred = tpe._predict_activity(domain.table, fits, 1 << 16)
+    assert pred is not None and pred['model'] >= 0
+    good = tpe._choices_fused(domain.table, fits, [3000], 5, 1 << 16, eng, None)
+    assert good is not None and int(good[0]['model']) == pred['model']
+    wrong = dict(pred)
+    wrong['model'] = (pred['model'] + 1) % 3
+    orig = tpe._predict_activity
+    tpe._predict_activity = lambda *a: wrong
+    try:
+        assert tpe._choices_fused(domain.table, fits, [3000], 5, 1 << 16, eng, None) is None
+        got = tpe._choices_philox(domain.table, fits, [3000], 5, 1 << 16, eng, None)
+    finally:
+        tpe._predict_activity = orig
+    tpe.SPECULATE = False
+    try:
+        ref = tpe._choices_philox(domain.table, fits, [3000], 5, 1 << 16, eng, None)
+    finally:
+        tpe.SPECULATE = True
+    assert got == ref
