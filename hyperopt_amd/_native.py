@@ -11,22 +11,23 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libtpe_hip.so')
-ABI_VERSION = 4
+ABI_VERSION = 5
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH = 1, 2
+BATCH_NO_EXPAND = 1
 PREC_F32, PREC_F64 = 0, 1
 
 # numpy mirrors of the C structs (the host builds arrays of them and copies
 # them to device memory in one transfer)
 PROBLEM_DTYPE = np.dtype([
     ('family', '<i4'), ('flags', '<i4'), ('n_cand', '<i4'), ('n_upper', '<i4'),
-    ('cand_off', '<i8'), ('cand_base', '<i8'), ('part_off', '<i8'),
+    ('cand_off', '<i8'), ('cand_base', '<i8'), ('reserved64', '<i8'),
     ('n_splits', '<i4'), ('tile_off', '<i4'), ('n_tiles', '<i4'), ('samp_off', '<i4'),
     ('samp_len', '<i4'), ('below_off', '<i4'), ('below_len', '<i4'), ('above_off', '<i4'),
     ('above_len', '<i4'), ('wide_off', '<i4'), ('wide_len', '<i4'), ('grid_off', '<i4'),
-    ('grid_n', '<i4'), ('reserved', '<i4'),
+    ('grid_n', '<i4'), ('sort_slot', '<i4'),
     ('low', '<f8'), ('high', '<f8'), ('q', '<f8'), ('below_base', '<f8'), ('above_base', '<f8'),
     ('prior_mu', '<f4'), ('prior_a', '<f4'), ('prior_c', '<f4'), ('narrow_cmax', '<f4'),
     ('narrow_amin', '<f4'), ('grid_lo', '<f4'), ('grid_inv', '<f4'),
@@ -34,9 +35,9 @@ PROBLEM_DTYPE = np.dtype([
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
 ])
 assert PROBLEM_DTYPE.itemsize == 192
-TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4')])
+TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4'), ('work_first', '<i4'), ('n_splits', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
-                       ('k_start', '<i4'), ('k_end', '<i4'), ('reserved', '<i4')])
+                       ('k_start', '<i4'), ('k_end', '<i4'), ('n_splits', '<i4')])
 BEST_DTYPE = np.dtype([('score', '<f8'), ('l', '<f8'), ('g', '<f8'), ('idx', '<i8')])
 FIT_JOB_DTYPE = np.dtype([
     ('obs', '<u8'), ('n_obs', '<i8'), ('seg_off', '<i8'), ('below_off', '<i4'), ('n_below', '<i4'),
@@ -54,7 +55,7 @@ class Batch(ctypes.Structure):
     _fields_ = [
         ('problems', ctypes.c_void_p), ('n_problems', ctypes.c_int32),
         ('precision', ctypes.c_int32), ('sample', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
-        ('key_bits', ctypes.c_int32), ('reserved0', ctypes.c_int32),
+        ('key_bits', ctypes.c_int32), ('flags', ctypes.c_int32),
         ('comp32', ctypes.c_void_p), ('comp64', ctypes.c_void_p), ('samp', ctypes.c_void_p),
         ('grid', ctypes.c_void_p),
         ('cand', ctypes.c_void_p), ('coord', ctypes.c_void_p),
@@ -63,6 +64,7 @@ class Batch(ctypes.Structure):
         ('sort_tmp', ctypes.c_void_p), ('sort_tmp_bytes', ctypes.c_uint64),
         ('total_cand', ctypes.c_int64),
         ('tiles', ctypes.c_void_p), ('n_tiles', ctypes.c_int32), ('reserved2', ctypes.c_int32),
+        ('sort_count', ctypes.c_int64),
         ('work', ctypes.c_void_p),
         ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32),
         ('n_work_qlog', ctypes.c_int32), ('reserved3', ctypes.c_int32),
@@ -103,7 +105,7 @@ class PackInfo(ctypes.Structure):
         ('key_bits', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
         ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
         ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
-        ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64),
+        ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
     ]
 
 
@@ -181,7 +183,7 @@ def load(path=LIB_PATH):
                                         ctypes.POINTER(PackInfo)]
     lib.tpe_host_pack_level.restype = ctypes.c_int
     lib.tpe_level_run.argtypes = [ctypes.POINTER(LabelIn), ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
-                                  ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(LevelWS),
+                                  ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(LevelWS),
                                   ctypes.POINTER(LevelNeed), P, P]
     lib.tpe_level_run.restype = ctypes.c_int
     if lib.tpe_abi_version() != ABI_VERSION:

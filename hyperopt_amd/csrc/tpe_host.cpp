@@ -41,6 +41,13 @@ int target_work() {
   return v;
 }
 constexpr int kMinComponentsPerSplit = 128;
+constexpr int kFineKeyMinCand = 65536;
+constexpr int kTailMinTiles = 32;      // per-tile tail splits from 32 tiles (64k candidates) on
+// splits of the tile `e` tiles from either end of a pruned problem's sorted
+// range: the sparse tails are where waves span too wide a range for the local
+// expansion and evaluate their window exactly (measured on the config-3
+// problems: the exact work per tile peaks 1-4 tiles in and fades by ~10)
+inline int64_t tail_splits(int64_t e) { return e < 6 ? 16 : e < 8 ? 8 : e < 10 ? 4 : e < 12 ? 2 : 1; }
 
 // numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src)
 double pairwise(const double* a, int64_t n) {
@@ -230,12 +237,26 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   comp32.reserve((size_t)(4 * ktot));
   comp64.reserve((size_t)(4 * ktot));
   samp.reserve((size_t)(8 * ktot));
-  // sort key = problem << key_bits | value bucket: keep it within one 8-bit radix
-  // pass up to 8 problems, never below 32 buckets per problem
+  // Pruned problems (continuous f32 above mixtures of more than kPruneMinK
+  // components) are the only ones whose candidates are sorted; they own the
+  // candidate range [0, sort_count).  Sort key = sort_slot << key_bits | value
+  // bucket: one 8-bit radix pass up to 8 sorted problems, never below 32
+  // buckets per problem.  Large candidate sets get 4096 buckets (two passes):
+  // a wave of 512 sorted candidates then spans ~1/8 of a bucket's density,
+  // narrow enough for the above kernel's local expansion.
+  std::vector<char> pruned((size_t)n_labels, 0);
+  int64_t S = 0;
+  for (int32_t li = 0; li < n_labels; ++li) {
+    const tpe_label_in& L = labels[li];
+    pruned[li] = !f64 && (L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) &&
+                 (dev_fit[li] || L.above_k > kPruneMinK);
+    if (pruned[li]) S += L.n_ids;
+  }
   int pbits = 0;
-  while (((int64_t)1 << pbits) < P) ++pbits;
-  const int key_bits = std::max(5, 8 - pbits);
-  const int sort_end_bit = key_bits + pbits <= 32 ? key_bits + pbits : 0;
+  while (((int64_t)1 << pbits) < S) ++pbits;
+  int key_bits = std::max(5, 8 - pbits);
+  if (n_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(12, 16 - pbits));
+  const int sort_end_bit = S > 0 && key_bits + pbits <= 32 ? key_bits + pbits : 0;
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
     tpe_problem& p = lab[li];
@@ -438,12 +459,16 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<tpe_problem> prob((size_t)P);
   int64_t scored = 0;
   {
-    int64_t r = 0;
+    int64_t r = 0, s_next = 0, u_next = S * (int64_t)n_cand;
+    int32_t slot = 0;
     for (int32_t li = 0; li < n_labels; ++li)
       for (int64_t j = 0; j < labels[li].n_ids; ++j, ++r) {
         tpe_problem q = lab[li];
         q.n_cand = n_cand;
-        q.cand_off = r * (int64_t)n_cand;
+        int64_t& next = pruned[li] ? s_next : u_next;
+        q.cand_off = next;
+        next += n_cand;
+        q.sort_slot = pruned[li] ? slot++ : -1;
         q.cand_base = cand_base;
         q.key0 = (uint32_t)seed; q.key1 = (uint32_t)(seed >> 32);
         q.ctr2 = (uint32_t)labels[li].label_ix;
@@ -454,23 +479,43 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         if (q.family != TPE_FAM_CATEGORICAL) ++scored;
       }
   }
+  // splits of the above mixture per tile.  Bulk tiles: enough work items to fill
+  // the chip (a function of the GLOBAL candidate count, so every candidate sums
+  // its components in the same grouping whatever the sharding).  Pruned problems
+  // with many tiles: the bulk is cheap (local expansion), so one split, and the
+  // outermost tiles of the (local) sorted range — the sparse tails, whose waves
+  // span wide windows evaluated exactly — get geometrically more.
   const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
-  const int64_t scored_tiles = scored * ((C_ref + T - 1) / T);
+  const int64_t tiles_ref = (C_ref + T - 1) / T;
+  const int64_t scored_tiles = scored * tiles_ref;
   const int64_t target = std::max<int64_t>(1, (target_work() + std::max<int64_t>(scored_tiles, 1) - 1) /
                                                   std::max<int64_t>(scored_tiles, 1));
-  int64_t part_total = 0;
   bool any_pruned = false;
   for (auto& q : prob) {
-    if (q.family == TPE_FAM_CATEGORICAL) { q.n_splits = 0; q.part_off = part_total; continue; }
+    if (q.family == TPE_FAM_CATEGORICAL) { q.n_splits = 0; continue; }
     const int64_t ks = (q.above_len + kMinComponentsPerSplit - 1) / kMinComponentsPerSplit;
-    q.n_splits = (int32_t)std::max<int64_t>(1, std::min(target, ks));
-    q.part_off = part_total;
-    part_total += (int64_t)q.n_splits * n_cand;
+    const bool tails = q.sort_slot >= 0 && tiles_ref >= kTailMinTiles;
+    q.n_splits = tails ? 1 : (int32_t)std::max<int64_t>(1, std::min(target, ks));
     any_pruned = any_pruned || q.narrow_amin > 0.f;
   }
+  auto tile_splits = [&](const tpe_problem& q, int64_t j) -> int32_t {
+    if (q.family == TPE_FAM_CATEGORICAL) return 0;
+    if (!(q.sort_slot >= 0 && tiles_ref >= kTailMinTiles)) return q.n_splits;
+    const int64_t e = std::min<int64_t>(j, n_tiles_p - 1 - j);
+    const int64_t ns = tail_splits(e);
+    const int64_t cap = std::max<int64_t>(1, (q.above_len + 63) / 64);
+    return (int32_t)std::max<int64_t>(1, std::min(ns, cap));
+  };
   std::vector<tpe_tile> tiles((size_t)(P * n_tiles_p));
   for (int64_t r = 0, t = 0; r < P; ++r)
-    for (int64_t j = 0; j < n_tiles_p; ++j, ++t) { tiles[t].problem = (int32_t)r; tiles[t].cand_start = (int32_t)(j * T); }
+    for (int64_t j = 0; j < n_tiles_p; ++j, ++t) {
+      tiles[t].problem = (int32_t)r;
+      tiles[t].cand_start = (int32_t)(j * T);
+      tiles[t].work_first = 0;
+      tiles[t].n_splits = tile_splits(prob[r], j);
+    }
+  // work items grouped [continuous | quantized Gauss | quantized log]; a tile's
+  // items are consecutive, and an item's index is its row of `part`
   std::vector<tpe_work> work;
   int32_t counts[3] = {0, 0, 0};
   const int fams[3][2] = {{TPE_FAM_GAUSS, TPE_FAM_LOGGAUSS}, {TPE_FAM_QGAUSS, -1}, {TPE_FAM_QLOGGAUSS, -1}};
@@ -479,18 +524,23 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     for (int64_t r = 0; r < P; ++r) {
       const tpe_problem& q = prob[r];
       if (q.family != fams[gi][0] && q.family != fams[gi][1]) continue;
-      for (int32_t s = 0; s < q.n_splits; ++s)
-        for (int64_t j = 0; j < n_tiles_p; ++j) {
+      for (int64_t j = 0; j < n_tiles_p; ++j) {
+        tpe_tile& tl = tiles[(size_t)(r * n_tiles_p + j)];
+        tl.work_first = (int32_t)work.size();
+        for (int32_t sp = 0; sp < tl.n_splits; ++sp) {
           tpe_work w;
-          w.problem = (int32_t)r; w.split = s; w.cand_start = (int32_t)(j * T);
-          w.k_start = (int32_t)(((int64_t)q.above_len * s) / q.n_splits);
-          w.k_end = (int32_t)(((int64_t)q.above_len * (s + 1)) / q.n_splits);
-          w.reserved = 0;
+          w.problem = (int32_t)r; w.split = sp; w.cand_start = (int32_t)(j * T);
+          w.k_start = (int32_t)(((int64_t)q.above_len * sp) / tl.n_splits);
+          w.k_end = (int32_t)(((int64_t)q.above_len * (sp + 1)) / tl.n_splits);
+          w.n_splits = tl.n_splits;
           work.push_back(w);
         }
+      }
     }
     counts[gi] = (int32_t)(work.size() - before);
   }
+  if ((int64_t)work.size() >= ((int64_t)1 << 31)) return TPE_E_ARG;
+  const int64_t part_total = (int64_t)work.size() * T;
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
   // comp32 rows sit at the END of the last two sections and are not copied ----
   const int NS = 10;
@@ -520,6 +570,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->n_fit = (int32_t)fit.size(); info->reserved = 0;
   info->fit_total = fit_seg.back();
   info->copy_end = off[8] + len[8];
+  info->sort_count = S * (int64_t)n_cand;
   info->copy2_len = len[9];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;

@@ -230,7 +230,8 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      const double* __restrict__ samp,
                                                      double* __restrict__ cand, float* __restrict__ coord,
                                                      uint32_t* __restrict__ keys, uint64_t* __restrict__ vals,
-                                                     int precision, int draw, int key_bits) {
+                                                     uint64_t* __restrict__ vals_sorted, int precision, int draw,
+                                                     int key_bits) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   const bool quant = p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     while ((double)hi_f >= hi) hi_f = nextafterf(hi_f, -INFINITY);
   }
   const double* S = samp + 8 * (int64_t)p.samp_off;
-  const uint32_t khi = (uint32_t)tl.problem << key_bits;
+  const uint32_t khi = (uint32_t)p.sort_slot << key_bits;
   const float kmax = (float)((1 << key_bits) - 1);
   // selection CDF staged in LDS: the per-lane binary search then costs no
   // dependent global loads (tables longer than kCumLds search global memory)
@@ -305,23 +306,100 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     }
     coord[o] = t;
   }
-  // sort key: (problem, value bucket) — only locality matters for pruning
-  const float gb = floorf((t - p.key_lo) * p.key_inv);
-  const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
-  keys[o] = khi | bucket;
-  vals[o] = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(t);
+  const uint64_t v = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(t);
+  if (p.sort_slot >= 0) {
+    // sort key: (sorted problem, value bucket) — only locality matters for pruning
+    const float gb = floorf((t - p.key_lo) * p.key_inv);
+    const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
+    keys[o] = khi | bucket;
+    vals[o] = v;
+  } else {
+    vals_sorted[o] = v;                    // never sorted: straight to its final place
+  }
+}
+
+// row of `part` a work item writes: its tile's first work item + its split
+__device__ __forceinline__ int64_t part_row(const tpe_problem* __restrict__ P, const tpe_tile* __restrict__ tiles,
+                                            const tpe_work& w) {
+  const tpe_problem& p = P[w.problem];
+  return (int64_t)tiles[p.tile_off + w.cand_start / kTile].work_first + w.split;
 }
 
 // ============================================================ score above
 // Continuous families, f32, pruned: s_i = sum_k 2^(c_k - (a_k ((t_i - mu_hi_k) - mu_lo_k))^2)
 // over the wave's window of sorted components plus the wide components.
+//
+// Local expansion (TPE_BATCH_NO_EXPAND clear): the wave's 512 sorted candidates
+// span [t0 - h, t0 + h].  With u = (t - t0) / h and d = t0 - mu, every term is
+//   2^(c - a^2 d^2) * exp(B u + G u^2),  B = -2 ln2 a^2 d h,  G = -ln2 a^2 h^2,
+// whose Taylor coefficients follow (n+1) e_{n+1} = B e_n + 2 G e_{n-1}.  A
+// component with |B| <= kTaylorBMax and |G| <= kTaylorGMax is summed into the
+// wave's moments M_n = sum_k 2^(c_k - a_k^2 d_k^2) e_n(k) (one exp2 per
+// component per WAVE instead of one per candidate); each candidate then adds
+// sum_n M_n u^n.  The coefficients are bounded by those of exp(|B| u + |G| u^2),
+// whose tail after degree 10 is < 4e-8 at the box corner (0.6, 0.05), i.e.
+// < 1.2e-7 of the term (x e^(2(|B| + |G|))); every term is positive, so the
+// bound holds for the sum.  Other components are evaluated exactly for every
+// candidate (ce_step).  G grows with the wave's span squared: the bound on it
+// is what restricts the expansion to waves narrower than ~0.3 sigma.
+constexpr int kTaylorN = 11;
+constexpr float kTaylorBMax = 0.6f;
+constexpr float kTaylorGMax = 0.05f;
+constexpr float kLn2f = 0.693147180559945309f;
+
+__device__ __forceinline__ float4 readlane4(const float4 c, int lane) {
+  return make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.x), lane)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.y), lane)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.z), lane)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.w), lane)));
+}
+
+// components [kb, ke) (wave-uniform): expandable ones into M, the rest exactly;
+// returns the number of exactly evaluated components
+__device__ __forceinline__ int expand_range(const float4* __restrict__ C, int kb, int ke, float t0, float h,
+                                            float (&M)[kTaylorN], const f2 (&t2)[kR / 2], f2 (&s2)[kR / 2]) {
+  const int lane = threadIdx.x & 63;
+  int n_exact = 0;
+  for (int base = kb; base < ke; base += 64) {
+    const int k = base + lane;
+    const bool valid = k < ke;
+    const float4 c = valid ? C[k] : make_float4(0.f, 0.f, 0.f, -INFINITY);
+    const bool live = valid && c.w > -INFINITY;     // wide components sit in the sorted list at c = -inf
+    const float d = (t0 - c.x) - c.y;
+    const float z = c.z * d;
+    const float ah = c.z * h;
+    const float B = -2.f * kLn2f * (c.z * z) * h;
+    const float G = -kLn2f * ah * ah;
+    const bool expand = live && fabsf(B) <= kTaylorBMax && fabsf(G) <= kTaylorGMax;
+    const float h0 = expand ? __builtin_amdgcn_exp2f(c.w - z * z) : 0.f;
+    float em1 = 0.f, e = h0;
+    M[0] += e;
+#pragma unroll
+    for (int n = 1; n < kTaylorN; ++n) {
+      const float en = (B * e + 2.f * G * em1) * (1.f / (float)n);
+      em1 = e;
+      e = en;
+      M[n] += e;
+    }
+    unsigned long long rest = __ballot(live && !expand);
+    n_exact += __popcll(rest);
+    while (rest) {
+      const int bl = __builtin_ctzll(rest);
+      rest &= rest - 1;
+      ce_step(readlane4(c, bl), t2, s2);
+    }
+  }
+  return n_exact;
+}
+
 __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __restrict__ P,
+                                                        const tpe_tile* __restrict__ tiles,
                                                         const tpe_work* __restrict__ W,
                                                         const float4* __restrict__ comp,
                                                         const int32_t* __restrict__ grid,
                                                         const uint64_t* __restrict__ vals,
                                                         double* __restrict__ part,
-                                                        unsigned long long* __restrict__ ce_count) {
+                                                        unsigned long long* __restrict__ ce_count, int flags) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
   const int n = p.n_cand;
@@ -340,7 +418,8 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
     tmax = fmaxf(tmax, __shfl_xor(tmax, off));
   }
   int k_lo = w.k_start, k_hi = w.k_end;
-  if (!(tmin <= tmax)) {
+  const bool any = tmin <= tmax;
+  if (!any) {
     k_hi = k_lo;                       // no valid candidate in this wave
   } else if (p.narrow_amin > 0.f) {
     const float dmax = fmaxf(fabsf(tmin - p.prior_mu), fabsf(tmax - p.prior_mu));
@@ -357,46 +436,76 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
       // work items of this tile, so every work item gets an equal share
       const int wl = G[bl], wh = max(G[bh], G[bl]);
       const long long len = wh - wl;
-      k_lo = wl + (int)((len * w.split) / p.n_splits);
-      k_hi = wl + (int)((len * (w.split + 1)) / p.n_splits);
+      k_lo = wl + (int)((len * w.split) / w.n_splits);
+      k_hi = wl + (int)((len * (w.split + 1)) / w.n_splits);
     }
   }
   k_lo = __builtin_amdgcn_readfirstlane(k_lo);
   k_hi = __builtin_amdgcn_readfirstlane(k_hi);
+  const int wide_len = (w.split == 0 && any) ? p.wide_len : 0;   // wide components once per candidate
   // candidate pairs in packed f32 (v_pk_add/mul/fma_f32); v_exp_f32 per lane value
   f2 t2[kR / 2], s2[kR / 2];
 #pragma unroll
   for (int j = 0; j < kR / 2; ++j) { t2[j] = f2{t[2 * j], t[2 * j + 1]}; s2[j] = f2{0.f, 0.f}; }
   const float4* __restrict__ C = comp + p.above_off;
+  long long n_exact = 0, n_expanded = 0;
+  if (!(flags & TPE_BATCH_NO_EXPAND)) {
+    const float t0 = 0.5f * (tmin + tmax), h = 0.5f * (tmax - tmin);
+    float M[kTaylorN];
+#pragma unroll
+    for (int q = 0; q < kTaylorN; ++q) M[q] = 0.f;
+    n_exact = expand_range(C, k_lo, k_hi, t0, h, M, t2, s2);
+    n_exact += expand_range(comp + p.wide_off, 0, wide_len, t0, h, M, t2, s2);
+    n_expanded = (long long)(k_hi - k_lo) + wide_len - n_exact;
+#pragma unroll
+    for (int q = 0; q < kTaylorN; ++q)
+      for (int off = 32; off > 0; off >>= 1) M[q] += __shfl_xor(M[q], off);
+    const float hinv = h > 0.f ? 1.f / h : 0.f;
+    const f2 c0 = f2{t0, t0}, hv = f2{hinv, hinv};
+#pragma unroll
+    for (int j = 0; j < kR / 2; ++j) {
+      const f2 u = (t2[j] - c0) * hv;
+      f2 acc = f2{M[kTaylorN - 1], M[kTaylorN - 1]};
+#pragma unroll
+      for (int q = kTaylorN - 2; q >= 0; --q) acc = acc * u + f2{M[q], M[q]};
+      s2[j] += acc;
+    }
+  } else {
 #pragma unroll 4
-  for (int k = k_lo; k < k_hi; ++k) ce_step(C[k], t2, s2);
-  if (w.split == 0) {                  // wide components once per candidate
+    for (int k = k_lo; k < k_hi; ++k) ce_step(C[k], t2, s2);
     const float4* __restrict__ Wd = comp + p.wide_off;
-    for (int k = 0; k < p.wide_len; ++k) ce_step(Wd[k], t2, s2);
+    for (int k = 0; k < wide_len; ++k) ce_step(Wd[k], t2, s2);
+    n_exact = (long long)(k_hi - k_lo) + wide_len;
   }
 #pragma unroll
   for (int j = 0; j < kR / 2; ++j) { s[2 * j] = s2[j].x; s[2 * j + 1] = s2[j].y; }
-  double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
+  double* __restrict__ out = part + part_row(P, tiles, w) * kTile - w.cand_start;
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
     if (i < n) out[i] = (double)s[j];
   }
-  if (ce_count) {                      // executed CE of this work item (profiling; no atomics)
-    __shared__ unsigned long long wce[kThreads / 64];
+  if (ce_count) {       // profiling (no atomics): [exact CE, expanded components] of this work item
+    __shared__ unsigned long long wce[kThreads / 64][2];
     if ((threadIdx.x & 63) == 0) {
       const int wave_first = w.cand_start + (int)(threadIdx.x >> 6) * kWaveCands;
       const int valid = max(0, min(kWaveCands, n - wave_first));
-      const long long kk = (long long)max(0, k_hi - k_lo) + (w.split == 0 ? p.wide_len : 0);
-      wce[threadIdx.x >> 6] = (unsigned long long)(kk * valid);
+      wce[threadIdx.x >> 6][0] = (unsigned long long)(n_exact * valid);
+      wce[threadIdx.x >> 6][1] = (unsigned long long)n_expanded;
     }
     __syncthreads();
-    if (threadIdx.x == 0) ce_count[blockIdx.x] = wce[0] + wce[1] + wce[2] + wce[3];
+    if (threadIdx.x == 0) {
+      unsigned long long a0 = 0, a1 = 0;
+      for (int q = 0; q < kThreads / 64; ++q) { a0 += wce[q][0]; a1 += wce[q][1]; }
+      ce_count[2 * blockIdx.x] = a0;
+      ce_count[2 * blockIdx.x + 1] = a1;
+    }
   }
 }
 
 // Continuous families, f64 (parity precision, unpruned)
 __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __restrict__ P,
+                                                        const tpe_tile* __restrict__ tiles,
                                                         const tpe_work* __restrict__ W,
                                                         const double4* __restrict__ comp,
                                                         const double* __restrict__ cand,
@@ -423,7 +532,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __res
       s[j] += exp2(c.z - z * z);
     }
   }
-  double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
+  double* __restrict__ out = part + part_row(P, tiles, w) * kTile - w.cand_start;
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
@@ -434,6 +543,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f64(const tpe_problem* __res
 // Quantized families (always f64): partial mixture mass
 template <bool LOG>
 __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restrict__ P,
+                                                      const tpe_tile* __restrict__ tiles,
                                                       const tpe_work* __restrict__ W,
                                                       const double4* __restrict__ comp,
                                                       const double* __restrict__ cand,
@@ -458,7 +568,7 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
 #pragma unroll
       for (int j = 0; j < R; ++j) s[j] += qterm<LOG>(c, tu[j], tl[j]);
     }
-    double* __restrict__ out = part + p.part_off + (int64_t)w.split * n;
+    double* __restrict__ out = part + part_row(P, tiles, w) * kTile - w.cand_start;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int i = tile_pos(w.cand_start, h * R + j);
@@ -498,15 +608,16 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
   const uint64_t v = valid ? vals[p.cand_off + i] : 0;
   double sa = 0.0;
   {
-    const double* __restrict__ ps = part + p.part_off + i;
-    const int ns = valid ? p.n_splits : 0;
+    // the tile's partial-sum rows, in split order
+    const double* __restrict__ ps = part + (int64_t)tl.work_first * kTile + (i - tl.cand_start);
+    const int ns = valid ? tl.n_splits : 0;
     int sp = 0;
     for (; sp + 4 <= ns; sp += 4) {         // four loads in flight per step
-      const double a0 = ps[(int64_t)sp * n], a1 = ps[(int64_t)(sp + 1) * n];
-      const double a2 = ps[(int64_t)(sp + 2) * n], a3 = ps[(int64_t)(sp + 3) * n];
+      const double a0 = ps[(int64_t)sp * kTile], a1 = ps[(int64_t)(sp + 1) * kTile];
+      const double a2 = ps[(int64_t)(sp + 2) * kTile], a3 = ps[(int64_t)(sp + 3) * kTile];
       sa += a0; sa += a1; sa += a2; sa += a3;
     }
-    for (; sp < ns; ++sp) sa += ps[(int64_t)sp * n];
+    for (; sp < ns; ++sp) sa += ps[(int64_t)sp * kTile];
   }
   const uint32_t oo = (uint32_t)(v >> 32);         // original position
   const int64_t orig = valid ? (int64_t)oo - p.cand_off : -1;
@@ -841,6 +952,7 @@ int check_batch(const tpe_batch* b) {
   if ((b->l_out == nullptr) != (b->g_out == nullptr)) return fail(TPE_E_ARG, "l_out and g_out go together");
   if (b->total_cand >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one batch");
   if (b->sort_end_bit < 0 || b->sort_end_bit > 32) return fail(TPE_E_ARG, "bad sort_end_bit");
+  if (b->sort_count < 0 || b->sort_count > b->total_cand) return fail(TPE_E_ARG, "bad sort_count");
   if (b->key_bits < 0 || b->key_bits > 16) return fail(TPE_E_ARG, "bad key_bits");
   if (b->sort_end_bit == 0 && (b->keys_sorted != b->keys || b->vals_sorted != b->vals))
     return fail(TPE_E_ARG, "unsorted batch must alias keys_sorted/vals_sorted to keys/vals");
@@ -926,7 +1038,8 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (b->sample && !b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
   if (b->n_tiles == 0) return TPE_OK;
   hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, kR), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
-                     b->samp, b->cand, b->coord, b->keys, b->vals, b->precision, b->sample, b->key_bits);
+                     b->samp, b->cand, b->coord, b->keys, b->vals, b->vals_sorted, b->precision, b->sample,
+                     b->key_bits);
   return hip_check("tpe_sample");
 }
 
@@ -934,11 +1047,11 @@ int tpe_sort(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   // sort_end_bit == 0: no sort; the caller aliases keys_sorted/vals_sorted to keys/vals
-  if (b->n_tiles == 0 || b->total_cand == 0 || b->sort_end_bit == 0) return TPE_OK;
+  if (b->n_tiles == 0 || b->sort_count == 0 || b->sort_end_bit == 0) return TPE_OK;
   size_t sz = (size_t)b->sort_tmp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
       b->sort_tmp, sz, (const uint32_t*)b->keys, b->keys_sorted, (const uint64_t*)b->vals, b->vals_sorted,
-      (size_t)b->total_cand, 0u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
+      (size_t)b->sort_count, 0u, (unsigned)b->sort_end_bit, (hipStream_t)stream);
   if (e != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "tpe_sort: %s (workspace %llu bytes)", hipGetErrorString(e),
              (unsigned long long)b->sort_tmp_bytes);
@@ -954,17 +1067,18 @@ int tpe_score_above(const tpe_batch* b, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n_cont) {
     if (b->precision == TPE_PREC_F32)
-      hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
-                         (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->ce_count);
+      hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
+                         (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->ce_count, b->flags);
     else
-      hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->work,
+      hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
                          (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   }
   if (n_qg)
-    hipLaunchKernelGGL((k_above_q<false>), dim3(n_qg), dim3(kThreads), 0, s, b->problems, b->work + n_cont,
+    hipLaunchKernelGGL((k_above_q<false>), dim3(n_qg), dim3(kThreads), 0, s, b->problems, b->tiles, b->work + n_cont,
                        (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   if (n_ql)
-    hipLaunchKernelGGL((k_above_q<true>), dim3(n_ql), dim3(kThreads), 0, s, b->problems, b->work + n_cont + n_qg,
+    hipLaunchKernelGGL((k_above_q<true>), dim3(n_ql), dim3(kThreads), 0, s, b->problems, b->tiles,
+                       b->work + n_cont + n_qg,
                        (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   return hip_check("tpe_score_above");
 }
@@ -1000,8 +1114,8 @@ int tpe_run_batch(const tpe_batch* b, void* stream) {
 }
 
 int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
-                  int64_t n_cand_global, int32_t precision, const tpe_level_ws* ws, tpe_level_need* need,
-                  void* stream, tpe_result* out) {
+                  int64_t n_cand_global, int32_t precision, int32_t flags, const tpe_level_ws* ws,
+                  tpe_level_need* need, void* stream, tpe_result* out) {
   if (!ws || !need || (n_labels > 0 && !out)) return fail(TPE_E_ARG, "null workspace/need/out");
   memset(need, 0, sizeof(*need));
   tpe_pack_info info;
@@ -1022,8 +1136,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   need->fit = info.fit_total;
   if (C >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one level: shard the batch");
   uint64_t sz = 0;
-  if (info.sort_end_bit > 0 && C > 0) {
-    if ((rc = tpe_sort_workspace_bytes(C, &sz))) return rc;
+  if (info.sort_end_bit > 0 && info.sort_count > 0) {
+    if ((rc = tpe_sort_workspace_bytes(info.sort_count, &sz))) return rc;
     need->sort_tmp_bytes = (int64_t)sz;
   }
   if (info.n_fit > 0) {
@@ -1049,6 +1163,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.problems = (const tpe_problem*)(dev + info.off_problems);
   b.n_problems = (int32_t)P;
   b.precision = precision;
+  b.flags = flags;
   b.sample = 1;
   b.sort_end_bit = info.sort_end_bit;
   b.key_bits = info.key_bits;
@@ -1064,6 +1179,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.keys_sorted = ws->keys; b.vals_sorted = ws->vals;
   }
   b.total_cand = C;
+  b.sort_count = info.sort_count;
   b.tiles = (const tpe_tile*)(dev + info.off_tiles);
   b.n_tiles = (int32_t)info.n_tiles;
   b.work = (const tpe_work*)(dev + info.off_work);

@@ -38,6 +38,8 @@ MIN_COMPONENTS_PER_SPLIT = 128
 # the device (tpe_fit_above) in fp32 mode; TPE_DEVICE_FIT_MIN overrides
 DEVICE_FIT_MIN = int(os.environ.get('TPE_DEVICE_FIT_MIN', '16384'))
 PRUNE_MIN_K = 64
+FINE_KEY_MIN_CAND = 65536          # tpe_host.cpp kFineKeyMinCand: 12-bit sort buckets from here
+TAIL_MIN_TILES = 32                # tpe_host.cpp kTailMinTiles: per-tile tail splits from here
 
 
 def _coord_range(post):
@@ -104,6 +106,9 @@ class Engine(object):
         # reports the mean (steady-state stage cost, tools/stage_bench.py)
         self.profile = None
         self.profile_repeat = 1
+        # pruned f32 above kernel: local (Taylor) expansion of components whose
+        # series converges over a wave's candidate span (False: all exact)
+        self.expand = True
 
     def set_precision(self, precision):
         if precision not in ('fp32', 'fp64'):
@@ -127,9 +132,14 @@ class Engine(object):
         the native packer (tpe_host_pack_level) is tested against."""
         f64 = self.precision == 'fp64'
         T = self.tile
-        P_all = sum(len(lp.ids) for lp in problems)
-        pbits = int(math.ceil(math.log2(P_all))) if P_all > 1 else 0
+        # sorted (pruned) problems: continuous f32 above mixtures of > PRUNE_MIN_K components
+        pruned_l = [(not f64) and lp.post.family in (N.FAM_GAUSS, N.FAM_LOGGAUSS)
+                    and (lp.post.above_dev is not None or len(lp.post.above[0]) > PRUNE_MIN_K) for lp in problems]
+        S = sum(len(lp.ids) for lp, pr in zip(problems, pruned_l) if pr)
+        pbits = int(math.ceil(math.log2(S))) if S > 1 else 0
         key_bits = max(5, 8 - pbits)
+        if n_cand >= FINE_KEY_MIN_CAND:
+            key_bits = max(key_bits, min(12, 16 - pbits))
         comp32, comp64, samp, grids = [], [], [], []
         n32 = n64 = ns = ngrid = 0
         rows = []                         # per LevelProblem: (table info)
@@ -213,7 +223,12 @@ class Engine(object):
             prob[field] = np.array([r[field] for r in rows])[owner] if P else 0
         prob['n_cand'] = n_cand
         ids = np.concatenate([lp.ids for lp in problems]) if P else np.zeros(0, np.int64)
-        prob['cand_off'] = np.arange(P, dtype=np.int64) * n_cand
+        pr = np.repeat(np.array(pruned_l, dtype=bool), counts) if P else np.zeros(0, bool)
+        # sorted problems own the candidate range [0, S * n_cand)
+        slot = np.cumsum(pr) - 1
+        unslot = np.cumsum(~pr) - 1
+        prob['cand_off'] = np.where(pr, slot * n_cand, (S + unslot) * n_cand)
+        prob['sort_slot'] = np.where(pr, slot, -1)
         prob['cand_base'] = cand_base
         s64 = int(seed) & 0xFFFFFFFFFFFFFFFF
         prob['key0'] = s64 & 0xFFFFFFFF
@@ -224,56 +239,63 @@ class Engine(object):
         prob['n_tiles'] = n_tiles_p
         prob['tile_off'] = np.arange(P, dtype=np.int64) * n_tiles_p
 
-        # splits of the above mixture: enough work items to fill the chip
+        # splits of the above mixture per tile: bulk tiles fill the chip (a
+        # function of the GLOBAL candidate count); pruned problems with many
+        # tiles use one split and geometrically more on their outermost tiles
         fam = prob['family']
         cont = (fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)
         qg, ql = fam == N.FAM_QGAUSS, fam == N.FAM_QLOGGAUSS
         scored = cont | qg | ql
-        # split count depends on the GLOBAL candidate count only, so every
-        # candidate sums its components in the same grouping whatever the
-        # sharding (bit-identical results for any number of GPUs)
         C_ref = n_cand if n_cand_global is None else int(n_cand_global)
-        n_scored_tiles = int(scored.sum()) * ((C_ref + T - 1) // T)
+        tiles_ref = (C_ref + T - 1) // T
+        n_scored_tiles = int(scored.sum()) * tiles_ref
         target = max(1, math.ceil(TARGET_WORK / max(n_scored_tiles, 1)))
         K = prob['above_len'].astype(np.int64)
-        splits = np.where(scored, np.clip(np.minimum(target, (K + MIN_COMPONENTS_PER_SPLIT - 1)
-                                                     // MIN_COMPONENTS_PER_SPLIT), 1, None), 0)
+        tails = pr & (tiles_ref >= TAIL_MIN_TILES)
+        splits = np.where(scored, np.where(tails, 1, np.clip(np.minimum(target, (K + MIN_COMPONENTS_PER_SPLIT - 1)
+                                                                      // MIN_COMPONENTS_PER_SPLIT), 1, None)), 0)
         prob['n_splits'] = splits
-        part_sizes = splits * n_cand
-        prob['part_off'] = np.concatenate([[0], np.cumsum(part_sizes)[:-1]]) if P else 0
-        part_total = int(part_sizes.sum())
+        j = np.arange(n_tiles_p)
+        e = np.minimum(j, n_tiles_p - 1 - j)
+        tail_ns = np.select([e < 6, e < 8, e < 10, e < 12], [16, 8, 4, 2], 1)     # tpe_host.cpp tail_splits
+        ns_tile = np.zeros((P, n_tiles_p), dtype=np.int64)
+        for r in range(P):
+            if not scored[r]:
+                continue
+            if tails[r]:
+                ns_tile[r] = np.maximum(1, np.minimum(tail_ns, max(1, (K[r] + 63) // 64)))
+            else:
+                ns_tile[r] = splits[r]
 
         # tiles
         tiles = np.zeros(P * n_tiles_p, dtype=N.TILE_DTYPE)
         tiles['problem'] = np.repeat(np.arange(P), n_tiles_p)
         tiles['cand_start'] = np.tile(np.arange(n_tiles_p) * T, P)
+        tiles['n_splits'] = ns_tile.reshape(-1)
 
-        # work items, grouped [continuous | qgauss | qlog]
+        # work items, grouped [continuous | qgauss | qlog], a tile's items consecutive
         works = []
         counts_w = []
+        nw = 0
         for mask in (cont, qg, ql):
             pidx = np.nonzero(mask)[0]
-            if len(pidx) == 0:
-                counts_w.append(0)
-                continue
-            sp = splits[pidx]
-            n_items = sp * n_tiles_p
-            tot = int(n_items.sum())
-            w = np.zeros(tot, dtype=N.WORK_DTYPE)
-            p_rep = np.repeat(pidx, n_items)
-            local = np.arange(tot) - np.repeat(np.cumsum(n_items) - n_items, n_items)
-            sp_rep = np.repeat(sp, n_items)
-            split = local // n_tiles_p
-            tile = local % n_tiles_p
-            k_rep = np.repeat(K[pidx], n_items)
-            w['problem'] = p_rep
-            w['split'] = split
-            w['cand_start'] = tile * T
-            w['k_start'] = (k_rep * split) // sp_rep
-            w['k_end'] = (k_rep * (split + 1)) // sp_rep
-            works.append(w)
-            counts_w.append(tot)
+            rows_w = []
+            for r in pidx:
+                for t in range(n_tiles_p):
+                    ti = r * n_tiles_p + t
+                    tiles['work_first'][ti] = nw
+                    ns = int(ns_tile[r, t])
+                    for sp in range(ns):
+                        rows_w.append((r, sp, t * T, (K[r] * sp) // ns, (K[r] * (sp + 1)) // ns, ns))
+                        nw += 1
+            w = np.array(rows_w, dtype=np.int64).reshape(-1, 6)
+            wa = np.zeros(len(w), dtype=N.WORK_DTYPE)
+            for c, f in enumerate(N.WORK_DTYPE.names):
+                wa[f] = w[:, c]
+            works.append(wa)
+            counts_w.append(len(wa))
         work = np.concatenate(works) if works else np.zeros(0, dtype=N.WORK_DTYPE)
+        part_total = nw * T
 
         return dict(prob=prob, tiles=tiles, work=work, counts_w=counts_w, part_total=part_total,
                     comp32=np.concatenate(comp32) if comp32 else np.zeros((0, 4), np.float32),
@@ -415,7 +437,8 @@ class Engine(object):
         for attempt in range(3):
             ws = self._level_ws()
             rc = self.lib.tpe_level_run(labels, len(problems), n_cand, seed64, int(cand_base), ncg, prec,
-                                        ctypes.byref(ws), ctypes.byref(need), stream, out.ctypes.data)
+                                        0 if self.expand else N.BATCH_NO_EXPAND, ctypes.byref(ws),
+                                        ctypes.byref(need), stream, out.ctypes.data)
             if rc != N.E_SPACE:
                 break
             self._grow(need)
@@ -462,7 +485,7 @@ class Engine(object):
             d_keys_s = self._buf('keys_sorted', C_total, torch.int32)
             d_vals_s = self._buf('vals_sorted', C_total, torch.int64)
             ws = ctypes.c_uint64(0)
-            N.check(self.lib.tpe_sort_workspace_bytes(C_total, ctypes.byref(ws)), self.lib,
+            N.check(self.lib.tpe_sort_workspace_bytes(int(info.sort_count), ctypes.byref(ws)), self.lib,
                     'tpe_sort_workspace_bytes')
             d_sort = self._buf('sort_tmp', ws.value, torch.uint8)
         else:
@@ -482,8 +505,13 @@ class Engine(object):
                 cv = cand[cat]
                 if np.any((cv < 0) | (cv >= upper) | (cv != np.floor(cv))):
                     raise IndexError('categorical candidate out of range')
-            d_cand[:C_total].copy_(torch.from_numpy(cand))
-            d_coord[:C_total].copy_(torch.from_numpy(coord.astype(np.float32)))
+            # problem r's candidates live at cand_off[r] (sorted problems first)
+            at = (prob['cand_off'][:, None] + np.arange(n_cand)[None, :]).reshape(-1)
+            placed, placed_t = np.empty(C_total), np.empty(C_total, dtype=np.float32)
+            placed[at] = cand
+            placed_t[at] = coord.astype(np.float32)
+            d_cand[:C_total].copy_(torch.from_numpy(placed))
+            d_coord[:C_total].copy_(torch.from_numpy(placed_t))
         d_l = d_g = None
         if want_lg:
             d_l = self._buf('l_out', C_total, torch.float64)
@@ -491,6 +519,7 @@ class Engine(object):
         b = N.Batch()
         b.problems, b.n_problems = base + info.off_problems, P
         b.precision = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
+        b.flags = 0 if self.expand else N.BATCH_NO_EXPAND
         b.sample = 0 if inject else 1
         b.sort_end_bit, b.key_bits = info.sort_end_bit, info.key_bits
         b.comp32, b.comp64 = base + info.off_comp32, base + info.off_comp64
@@ -500,6 +529,7 @@ class Engine(object):
         if d_sort is not None:
             b.sort_tmp, b.sort_tmp_bytes = d_sort.data_ptr(), d_sort.numel()
         b.total_cand = C_total
+        b.sort_count = info.sort_count
         b.cand, b.coord = d_cand.data_ptr(), d_coord.data_ptr()
         b.tiles, b.n_tiles = base + info.off_tiles, n_tiles
         b.work = base + info.off_work
@@ -533,11 +563,15 @@ class Engine(object):
         if not (want_lg or return_cand):
             return res
         out = [res]
+        rows = (prob['cand_off'] // max(n_cand, 1)).astype(np.int64)    # sorted problems come first
+
+        def per_problem(d):
+            return d[:C_total].cpu().numpy().reshape(P, n_cand)[rows].copy()
         if return_cand:
-            out.append(d_cand[:C_total].cpu().numpy().reshape(P, n_cand).copy())
+            out.append(per_problem(d_cand))
         if want_lg:
-            out.append(d_l[:C_total].cpu().numpy().reshape(P, n_cand).copy())
-            out.append(d_g[:C_total].cpu().numpy().reshape(P, n_cand).copy())
+            out.append(per_problem(d_l))
+            out.append(per_problem(d_g))
         return tuple(out)
 
     def _run_profiled(self, b, stream, tb, n_cand):
@@ -561,7 +595,7 @@ class Engine(object):
                 stages.append((name, self.lib.tpe_score_above, gi, float(ce[mask].sum())))
         stages.append(('k_finalize', self.lib.tpe_finalize, None, float(tb['P'] * n_cand)))
         stages.append(('k_select', self.lib.tpe_select, None, float(tb['P'])))
-        cnt = self._buf('ce_count', max(counts[0], 1), torch.int64)
+        cnt = self._buf('ce_count', 2 * max(counts[0], 1), torch.int64)
         cnt.zero_()
         b.ce_count = cnt.data_ptr()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)]
@@ -580,12 +614,14 @@ class Engine(object):
                 N.check(fn(ctypes.byref(arg), ctypes.c_void_p(stream)), self.lib, name)
             evs[i + 1].record(cur)
         evs[-1].synchronize()
-        executed = int(cnt[:counts[0]].sum().item()) if counts[0] else 0
+        self.last_ce = cnt[:2 * counts[0]].view(-1, 2).cpu().numpy() if counts[0] else None   # per work item
+        cc = cnt[:2 * counts[0]].view(-1, 2).sum(0).tolist() if counts[0] else [0, 0]
+        executed, expanded = int(cc[0]), int(cc[1])
         b.ce_count = None
         for i, (name, fn, gi, units) in enumerate(stages):
             rec = (evs[i].elapsed_time(evs[i + 1]) / rep, units)
             if name == 'k_above_f32':
-                rec = rec + (float(executed),)
+                rec = rec + (float(executed), float(expanded))
             self.profile.setdefault(name, []).append(rec)
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 4
+#define TPE_ABI_VERSION 5
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -52,6 +52,11 @@ enum {
 enum {
   TPE_F_HAS_LOW = 1,   /* low bound present (reference: low is not None)   */
   TPE_F_HAS_HIGH = 2   /* high bound present                                */
+};
+
+/* tpe_batch.flags / tpe_level_run flags */
+enum {
+  TPE_BATCH_NO_EXPAND = 1  /* pruned f32 kernel: evaluate every component exactly (no local expansion) */
 };
 
 /* precision of the continuous (non-quantized) families; quantized families
@@ -82,8 +87,12 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  * every skipped term is < 2^-45 of the sum.  grid[grid_off .. +grid_n] maps
  * value buckets (grid_lo + g / grid_inv) to the first sorted component with
  * mu >= the bucket edge.  narrow_amin <= 0 disables pruning.  With pruning,
- * work item `split` of a tile evaluates the split-th of n_splits equal parts
- * of each wave's window (k_start/k_end are ignored).
+ * work item `split` of a tile evaluates the split-th of its n_splits equal
+ * parts of each wave's window (k_start/k_end are ignored).
+ *
+ * Sorted problems (sort_slot >= 0, the pruned ones) own the candidate range
+ * [0, sort_count) of the batch; the sort key is sort_slot << key_bits | value
+ * bucket.  Other problems' candidates follow and are never sorted.
  *
  * samp[k] = double[8] {cum, mu, sigma, fa, fb, flip, 0, 0}: below-mixture
  * sampler table; cum = selection CDF (∝ w_k * mass_k when bounded); fa, fb =
@@ -95,8 +104,8 @@ typedef struct tpe_problem {
   int32_t n_upper;       /* categorical: number of categories                  */
   int64_t cand_off;      /* element offset into cand / coord / keys / l_out    */
   int64_t cand_base;     /* global index of local candidate 0 (shards, RNG)    */
-  int64_t part_off;      /* element offset into part                           */
-  int32_t n_splits;      /* component splits of the above mixture              */
+  int64_t reserved64;
+  int32_t n_splits;      /* splits of the bulk tiles (tiles carry their own)   */
   int32_t tile_off;      /* first candidate tile of this problem               */
   int32_t n_tiles;       /* candidate tiles of this problem                    */
   int32_t samp_off;
@@ -109,7 +118,7 @@ typedef struct tpe_problem {
   int32_t wide_len;
   int32_t grid_off;
   int32_t grid_n;
-  int32_t reserved;
+  int32_t sort_slot;     /* rank among the batch's sorted problems, -1: unsorted */
   double low, high, q;   /* bounds in sampling space (log space for LGMM1)     */
   double below_base;     /* additive constant of the below lpdf                */
   double above_base;     /* additive constant of the above lpdf                */
@@ -121,20 +130,25 @@ typedef struct tpe_problem {
   uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
 } tpe_problem;
 
-/* candidate tile: 2048 consecutive candidates of one problem */
+/* candidate tile: 2048 consecutive candidates of one problem; its above-mixture
+ * partial sums are rows work_first .. work_first + n_splits - 1 of `part` */
 typedef struct tpe_tile {
   int32_t problem;
   int32_t cand_start;
+  int32_t work_first;    /* first work item (= part row) of this tile          */
+  int32_t n_splits;      /* its work items (0: no above stage)                 */
 } tpe_tile;
 
-/* above-mixture work item: one candidate tile x one component range */
+/* above-mixture work item: one candidate tile x one component range; writes
+ * the tile's partial sums to part[row * 2048 .. + 2048), row = its index in
+ * the batch's work list */
 typedef struct tpe_work {
   int32_t problem;
   int32_t split;
   int32_t cand_start;
   int32_t k_start;
   int32_t k_end;
-  int32_t reserved;
+  int32_t n_splits;      /* work items of this tile                            */
 } tpe_work;
 
 /* best of one finalize slot (TPE_BEST_PER_TILE per tile), written by the finalize stage */
@@ -187,7 +201,7 @@ typedef struct tpe_batch {
   int32_t sample;        /* 1: draw candidates on device (Philox); 0: caller filled cand/coord */
   int32_t sort_end_bit;  /* keys sorted on bits [0, sort_end_bit); 0 = no sort  */
   int32_t key_bits;      /* value-bucket bits of the sort key (problem << key_bits | bucket) */
-  int32_t reserved0;
+  int32_t flags;         /* TPE_BATCH_* options (0 = defaults)                  */
   const float* comp32;   /* [n][4]                                             */
   const double* comp64;  /* [n][4]                                             */
   const double* samp;    /* [n][8]                                             */
@@ -201,16 +215,18 @@ typedef struct tpe_batch {
   void* sort_tmp; uint64_t sort_tmp_bytes;   /* tpe_sort_workspace_bytes()     */
   int64_t total_cand;
   const tpe_tile* tiles; int32_t n_tiles; int32_t reserved2;
+  int64_t sort_count;    /* candidates [0, sort_count) are sorted (sorted problems first) */
   /* above-mixture work list, ordered [continuous | quantized Gauss | quantized log] */
   const tpe_work* work;
   int32_t n_work_cont, n_work_qgauss, n_work_qlog, reserved3;
-  double* part;          /* above-mixture partial sums                          */
+  double* part;          /* above-mixture partial sums: [n_work][2048]          */
   double* l_out;         /* optional [total_cand] (original order); NULL to skip */
   double* g_out;         /* optional [total_cand]; NULL to skip                 */
   tpe_best* tile_best;   /* [n_tiles * TPE_BEST_PER_TILE]                      */
   tpe_result* result;    /* [n_problems]                                       */
-  unsigned long long* ce_count; /* optional [n_work_cont]: component evaluations executed
-                                   per work item by the pruned kernel; NULL to skip */
+  unsigned long long* ce_count; /* optional [2 * n_work_cont]: per work item of the pruned
+                                   kernel, {exactly evaluated component x candidate pairs,
+                                   components summed by the local expansion}; NULL to skip */
   /* device Parzen fits (n_fit == 0: none); they patch rows of `problems` */
   const tpe_fit_job* fit; int32_t n_fit; int32_t reserved4;
   const int32_t* below_idx;   /* below indices of every job                        */
@@ -289,6 +305,7 @@ typedef struct tpe_pack_info {
   int32_t n_fit, reserved;
   int64_t fit_total;
   int64_t copy_end, copy2_len;
+  int64_t sort_count;               /* candidates of the sorted (pruned) problems */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation
@@ -339,8 +356,8 @@ typedef struct tpe_level_need {
  * tpe_result per (label, id) in order.  TPE_E_SPACE: a workspace is too small —
  * `need` holds every size; grow and call again (nothing was launched). */
 int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
-                  int64_t n_cand_global, int32_t precision, const tpe_level_ws* ws, tpe_level_need* need,
-                  void* stream, tpe_result* out);
+                  int64_t n_cand_global, int32_t precision, int32_t flags, const tpe_level_ws* ws,
+                  tpe_level_need* need, void* stream, tpe_result* out);
 
 #ifdef __cplusplus
 }

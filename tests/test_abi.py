@@ -56,7 +56,7 @@ int main(void) {
   printf("tpe_problem %zu\ntpe_tile %zu\ntpe_work %zu\ntpe_best %zu\ntpe_result %zu\ntpe_batch %zu\n",
          sizeof(tpe_problem), sizeof(tpe_tile), sizeof(tpe_work), sizeof(tpe_best), sizeof(tpe_result),
          sizeof(tpe_batch));
-  F(tpe_problem, cand_off) F(tpe_problem, part_off) F(tpe_problem, n_splits) F(tpe_problem, above_len)
+  F(tpe_problem, cand_off) F(tpe_problem, sort_slot) F(tpe_problem, n_splits) F(tpe_problem, above_len)
   F(tpe_problem, low) F(tpe_problem, above_base) F(tpe_problem, key0) F(tpe_problem, ctr3)
   F(tpe_batch, comp32) F(tpe_batch, tiles) F(tpe_batch, n_tiles) F(tpe_batch, work) F(tpe_batch, n_work_qlog)
   F(tpe_batch, part) F(tpe_batch, result)
@@ -141,7 +141,7 @@ def test_level_run_reports_space_without_gpu():
     ws, need = N.LevelWS(), N.LevelNeed()
     lib = N.load()
     out = np.empty(2, dtype=N.RESULT_DTYPE)
-    rc = lib.tpe_level_run(labels, 1, 1 << 20, 5, 0, 0, N.PREC_F32, ctypes.byref(ws), ctypes.byref(need), None,
+    rc = lib.tpe_level_run(labels, 1, 1 << 20, 5, 0, 0, N.PREC_F32, 0, ctypes.byref(ws), ctypes.byref(need), None,
                            out.ctypes.data)
     assert rc == N.E_SPACE
     assert need.cand == 2 << 20 and need.result == 2 and need.best == 2 * 512 * N.BEST_PER_TILE

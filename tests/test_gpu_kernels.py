@@ -322,3 +322,33 @@ def test_device_fit_batched_labels_and_suggest():
         assert g['d'] == r['d']
         for k in 'abc':
             assert abs(g[k] - r[k]) <= 1e-3 * max(1.0, abs(r[k])), (k, g[k], r[k])
+
+
+def test_local_expansion_matches_exact_and_is_used(engine):
+    """The pruned f32 kernel's local (Taylor) expansion: above-lpdf of 2^20
+    sampled candidates within 1e-5 of the all-exact kernel and within the fp32
+    tolerance of the oracle; most window components are expanded."""
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(13)
+    for dist, args, obs in (('uniform', dict(low=-5.0, high=5.0), rs.uniform(-5, 5, 6000)),
+                            ('loguniform', dict(low=-5.0, high=5.0), np.exp(rs.uniform(-5, 5, 6000)))):
+        post = parzen.fit_posterior(dist, args, obs[:25], obs[25:], 1.0)
+        C = 1 << 20
+        engine.profile = {}
+        res, cand, l, g = engine.run([LevelProblem(post, 0, [0])], C, seed=17, want_lg=True, return_cand=True)
+        rec = engine.profile['k_above_f32'][0]
+        engine.profile = None
+        executed, expanded = rec[2], rec[3]
+        engine.expand = False
+        try:
+            res_x, g_x = engine.run([LevelProblem(post, 0, [0])], C, seed=17, want_lg=True)[::2]
+        finally:
+            engine.expand = True
+        np.testing.assert_allclose(g[0], g_x[0], rtol=1e-5, atol=1e-5)     # both fp32 (parity tolerance)
+        assert expanded > 0 and executed < 0.2 * rec[1], (dist, executed, expanded, rec[1])
+        sub = rs.choice(C, 3000, replace=False)
+        lpdf = O.lgmm1_lpdf if dist == 'loguniform' else O.gmm1_lpdf
+        _check_lpdf(g[0][sub], lpdf(cand[0][sub], *post.above, low=post.low, high=post.high), 1e-5, dist)
+        score = l[0] - g[0]
+        assert int(res[0]['idx']) == int(np.argmax(score))

@@ -69,7 +69,7 @@ def test_native_pack_matches_numpy_packer(precision):
                                   rs.randint(0, 3, 90), 1.0)]
     lps = [LevelProblem(p, i + 3, np.arange(i + 1) + 100) for i, p in enumerate(posts)]
     e = _engine(precision)
-    for C in (24, 5000):
+    for C in (24, 5000, 1 << 17):      # 2^17: fine sort keys and per-tile tail splits
         ref = e._build_numpy(lps, C, 77, 10, None)
         info = e._pack(lps, C, 77, 10, None)
         P = ref['P']
@@ -78,7 +78,7 @@ def test_native_pack_matches_numpy_packer(precision):
         assert info.part_total == ref['part_total']
         prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, P)
         for f in N.PROBLEM_DTYPE.names:
-            if f in ('reserved', 'reserved_f'):
+            if f in ('reserved64', 'reserved_f'):
                 continue
             np.testing.assert_allclose(prob[f].astype(float), ref['prob'][f].astype(float), rtol=1e-6, atol=0,
                                        err_msg=f)

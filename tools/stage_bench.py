@@ -22,14 +22,23 @@ def main():
     hist = H.extract(domain, trials)
     fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, eng)
     T = domain.table
-    for lv in (['model'], ['svm_C', 'svm_kernel'], ['svm_rbf_gamma']):
+    for lv in (['model'], ['svm_C', 'svm_kernel'], ['svm_rbf_gamma'], ['svm_C'], ['svm_C', 'svm_kernel', 'svm_rbf_gamma', 'model']):
         probs = [LevelProblem(fits.get(T.by_label[l]), T.by_label[l].index, [bench.N_HISTORY]) for l in lv]
         eng.run(probs, bench.C_PER_GPU, 5)
         eng.profile, eng.profile_repeat = {}, rep
         eng.run(probs, bench.C_PER_GPU, 5)
         torch.cuda.synchronize()
         for k, v in eng.profile.items():
-            print('%-28s %-16s %8.1f us' % ('+'.join(lv), k, 1e3 * float(np.mean([a[0] for a in v]))))
+            extra = ''
+            if k == 'k_above_f32':
+                a = v[0]
+                extra = '  algorithmic CE %.3g, exact CE %.3g, expanded components %.3g' % (a[1], a[2], a[3])
+                ce = eng.last_ce[:, 0].astype(np.float64)
+                extra += '; exact CE per work item: mean %.3g p99 %.3g max %.3g (%d items)' % (
+                    ce.mean(), np.percentile(ce, 99), ce.max(), len(ce))
+                os.makedirs('gpurun_out', exist_ok=True)
+                np.save('gpurun_out/ce_%s.npy' % '+'.join(lv), eng.last_ce)
+            print('%-28s %-16s %8.1f us%s' % ('+'.join(lv), k, 1e3 * float(np.mean([a[0] for a in v])), extra))
         eng.profile, eng.profile_repeat = None, 1
 
 
