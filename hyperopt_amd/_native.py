@@ -16,7 +16,7 @@ BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate til
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH = 1, 2
-BATCH_NO_EXPAND = 1
+BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE = 1, 2, 4
 PREC_F32, PREC_F64 = 0, 1
 
 # numpy mirrors of the C structs (the host builds arrays of them and copies
@@ -63,8 +63,8 @@ class Batch(ctypes.Structure):
         ('keys_sorted', ctypes.c_void_p), ('vals_sorted', ctypes.c_void_p),
         ('sort_tmp', ctypes.c_void_p), ('sort_tmp_bytes', ctypes.c_uint64),
         ('total_cand', ctypes.c_int64),
-        ('tiles', ctypes.c_void_p), ('n_tiles', ctypes.c_int32), ('reserved2', ctypes.c_int32),
-        ('sort_count', ctypes.c_int64),
+        ('tiles', ctypes.c_void_p), ('n_tiles', ctypes.c_int32), ('n_fin_tiles', ctypes.c_int32),
+        ('sort_count', ctypes.c_int64), ('fin_tiles', ctypes.c_void_p),
         ('work', ctypes.c_void_p),
         ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32),
         ('n_work_qlog', ctypes.c_int32), ('reserved3', ctypes.c_int32),
@@ -106,6 +106,7 @@ class PackInfo(ctypes.Structure):
         ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
         ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
+        ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64),
     ]
 
 

@@ -541,17 +541,30 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   if ((int64_t)work.size() >= ((int64_t)1 << 31)) return TPE_E_ARG;
   const int64_t part_total = (int64_t)work.size() * T;
+  // tiles the finalize stage scores (device-drawn candidates): not categorical
+  // (the sample stage scores those), not one-split continuous f32 (the above
+  // stage does)
+  std::vector<int32_t> fin_tiles;
+  for (int64_t t = 0; t < (int64_t)tiles.size(); ++t) {
+    const tpe_problem& q = prob[tiles[t].problem];
+    const bool cat = q.family == TPE_FAM_CATEGORICAL && q.samp_len <= TPE_SAMPLE_LDS_ROWS;
+    const bool fused = !f64 && (q.family == TPE_FAM_GAUSS || q.family == TPE_FAM_LOGGAUSS) && tiles[t].n_splits == 1;
+    if (!cat && !fused) fin_tiles.push_back((int32_t)t);
+  }
+  const int64_t n_fin = (int64_t)fin_tiles.size();
+  if (fin_tiles.empty()) fin_tiles.push_back(0);
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
   // comp32 rows sit at the END of the last two sections and are not copied ----
-  const int NS = 10;
+  const int NS = 11;
   const void* src[NS] = {prob.data(), tiles.data(), work.data(), comp64.data(), samp.data(), fit.data(),
-                         below_idx.data(), fit_seg.data(), grid.data(), comp32.data()};
+                         below_idx.data(), fit_seg.data(), fin_tiles.data(), grid.data(), comp32.data()};
   const int64_t len[NS] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
                            (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp64.size() * sizeof(double)),
                            (int64_t)(samp.size() * sizeof(double)), (int64_t)(fit.size() * sizeof(tpe_fit_job)),
                            (int64_t)(below_idx.size() * sizeof(int32_t)), (int64_t)(fit_seg.size() * sizeof(int64_t)),
+                           (int64_t)(fin_tiles.size() * sizeof(int32_t)),
                            (int64_t)(grid.size() * sizeof(int32_t)), (int64_t)(comp32.size() * sizeof(float))};
-  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
+  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
   int64_t off[NS], end = 0;
   for (int i = 0; i < NS; ++i) {
     off[i] = (end + 255) & ~(int64_t)255;
@@ -559,7 +572,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp64 = off[3];
   info->off_samp = off[4]; info->off_fit = off[5]; info->off_below_idx = off[6]; info->off_fit_seg = off[7];
-  info->off_grid = off[8]; info->off_comp32 = off[9];
+  info->off_fin_tiles = off[8]; info->n_fin_tiles = n_fin;
+  info->off_grid = off[9]; info->off_comp32 = off[10];
   info->n_problems = P;
   info->n_tiles = (int64_t)tiles.size();
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
@@ -569,9 +583,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->part_total = part_total;
   info->n_fit = (int32_t)fit.size(); info->reserved = 0;
   info->fit_total = fit_seg.back();
-  info->copy_end = off[8] + len[8];
+  info->copy_end = off[9] + len[9];
   info->sort_count = S * (int64_t)n_cand;
-  info->copy2_len = len[9];
+  info->copy2_len = len[10];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;
   for (int i = 0; i < NS; ++i)

@@ -22,6 +22,7 @@
 // No atomics: every reduction is in a fixed order, so results are bitwise
 // reproducible run to run and identical for any candidate sharding.
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -43,7 +44,7 @@ constexpr int kTile = kThreads * kR;   // candidates per tile
 constexpr double kEPS = 1e-12;         // tpe.py:25
 constexpr double kLn2 = 0.69314718055994530942;
 constexpr float kPruneBits = 45.f;     // skipped terms are < 2^-45 of the sum
-constexpr int kCumLds = 1024;          // sampler CDF rows staged in LDS
+constexpr int kCumLds = TPE_SAMPLE_LDS_ROWS;   // sampler CDF rows staged in LDS
 
 // onesweep radix sort from 1024 keys up (rocPRIM's default switches to a merge
 // sort up to 2^20 keys, ~5x slower here)
@@ -129,10 +130,17 @@ __device__ __forceinline__ T lse2_exact(const C4* __restrict__ comp, int k0, int
   return m + log2(s);
 }
 
+// out-of-line copy for rarely taken paths inside register-heavy kernels
+__device__ __attribute__((noinline)) float lse2_exact_ool(const float4* __restrict__ comp, int k0, int n, int k1,
+                                                          int n1, float t) {
+  return lse2_exact<float, float4>(comp, k0, n, k1, n1, t);
+}
+
 // one-pass fixed-shift sum (every c_k <= 0) with the exact two-pass fallback
 // when it under-flows; used for the short below mixture
 __device__ __forceinline__ float lse2_fixed(const float4* __restrict__ comp, int k0, int n, float t) {
   float s = 0.f;
+#pragma unroll 4
   for (int k = 0; k < n; ++k) {
     const float4 c = comp[k0 + k];
     const float d = (t - c.x) - c.y;
@@ -209,7 +217,7 @@ __device__ __forceinline__ void ce_step(const float4 c, const f2 (&t)[kR / 2], f
   for (int j = 0; j < kR / 2; ++j) {
     const f2 d = (t[j] - mh) - ml;
     const f2 z = d * a;
-    const f2 v = cw - z * z;
+    const f2 v = __builtin_elementwise_fma(-z, z, cw);     // = lse2_fixed's fmaf(-z, z, c)
     s[j] += f2{__builtin_amdgcn_exp2f(v.x), __builtin_amdgcn_exp2f(v.y)};
   }
 }
@@ -221,29 +229,120 @@ __device__ __forceinline__ int tile_pos(int cand_start, int j) {
 }
 
 // ================================================================= sample
-// Draws (when `draw`) and writes the sort keys: (problem << key_bits) | value
-// bucket.  Grid (tiles, kR): block (x, y) handles the y-th 256-candidate slice
-// of tile x, one candidate per thread — a 2^20-candidate problem runs 4096
-// workgroups (16 waves per CU) rather than 512 latency-bound ones.
+// f32 truncation bounds of a problem: smallest float >= low, largest float < high
+__device__ __forceinline__ void f32_bounds(const tpe_problem& p, float& lo_f, float& hi_f) {
+  lo_f = -INFINITY; hi_f = INFINITY;
+  if (p.flags & TPE_F_HAS_LOW) { lo_f = (float)p.low; if ((double)lo_f < p.low) lo_f = nextafterf(lo_f, INFINITY); }
+  if (p.flags & TPE_F_HAS_HIGH) {
+    hi_f = (float)p.high;
+    while ((double)hi_f >= p.high) hi_f = nextafterf(hi_f, -INFINITY);
+  }
+}
+
+// component (category) choice of candidate i: first k with u < cum_k
+__device__ __forceinline__ int draw_category(const tpe_problem& p, const double* __restrict__ cum, int64_t i) {
+  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+  const double u1 = u01d(r.x, r.y);
+  int a = 0, b = p.samp_len - 1;
+  while (a < b) { const int m = (a + b) >> 1; if (u1 < cum[m]) b = m; else a = m + 1; }
+  return a;
+}
+
+// Candidate i of problem p (Philox-4x32-10 counter = its GLOBAL index): the value
+// x returned to the user and the kernel coordinate t (x, ln x before
+// quantisation for log families, the category for categorical).  `cum` is the
+// selection CDF (LDS copy or the table itself, stride `cs`).  k_select calls it
+// again for the winner, so the value never has to be stored.
+__device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __restrict__ S,
+                                         const double* __restrict__ cum, int cs, int64_t i, int precision,
+                                         float lo_f, float hi_f, double& x, float& t, int& comp) {
+  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+  // component choice: first k with u < cum_k (binary search, <= 27 rows)
+  const double u1 = u01d(r.x, r.y);
+  int a = 0, b = p.samp_len - 1;
+  while (a < b) { const int m = (a + b) >> 1; if (u1 < cum[cs * m]) b = m; else a = m + 1; }
+  comp = a;
+  if (p.family == TPE_FAM_CATEGORICAL) {
+    x = (double)a;
+    t = (float)a;
+    return;
+  }
+  const double* s = S + 8 * a;
+  // truncated normal by inversion; fa, fb = Phi of the (mirrored) bounds
+  const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
+  const bool flip = s[5] != 0.0;
+  if (precision == TPE_PREC_F32) {
+    const float pr = (float)fa + u01f(r.z) * ((float)fb - (float)fa);
+    float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+    if (flip) z = -z;
+    float xf = (float)mu + (float)sg * z;
+    if (!(xf == xf)) xf = (float)mu;
+    xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
+    t = xf;
+    x = (double)xf;
+  } else {
+    const double pr = fa + u01d(r.z, r.w) * (fb - fa);
+    double z = -1.41421356237309505 * erfcinv(2.0 * pr);
+    if (flip) z = -z;
+    x = mu + sg * z;
+    if (!(x == x)) x = mu;
+    if ((p.flags & TPE_F_HAS_LOW) && x < p.low) x = p.low;
+    if ((p.flags & TPE_F_HAS_HIGH) && x >= p.high) x = nextafter(p.high, -INFINITY);
+    t = (float)x;
+  }
+  if (p.family == TPE_FAM_LOGGAUSS || p.family == TPE_FAM_QLOGGAUSS) x = exp(x);
+  if (p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS) x = rint(x / p.q) * p.q;   // np.round
+}
+
+// block argmax of (score, original index) into one tile_best slot; the lane
+// that holds the winner (unique index) publishes its l and g
+__device__ __forceinline__ void block_best(double sc, int64_t orig, double l, double g, tpe_best* __restrict__ slot) {
+  double bs = sc;
+  int64_t bi = orig;
+  for (int off = 32; off > 0; off >>= 1) {
+    const double os = __shfl_xor(bs, off);
+    const int64_t oi = __shfl_xor(bi, off);
+    if (better(os, oi, bs, bi)) { bs = os; bi = oi; }
+  }
+  __shared__ tpe_best wb[kThreads / 64];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0 && bi < 0) wb[wave] = tpe_best{0, 0, 0, -1};
+  if (bi >= 0 && orig == bi) wb[wave] = tpe_best{bs, l, g, bi};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tpe_best b = wb[0];
+    for (int q = 1; q < kThreads / 64; ++q)
+      if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
+    *slot = b;
+  }
+}
+
+// Draws (when `draw`) and writes the sort keys: (sorted problem << key_bits) |
+// value bucket.  Grid (tiles, TPE_BEST_PER_TILE): block (x, y) handles the y-th
+// 256-candidate slice of tile x, one candidate per thread — a 2^20-candidate
+// problem runs 4096 workgroups (16 waves per CU).  Categorical problems are
+// scored here (categorical_lpdf is a table gather, tpe.py:50-57) and write
+// their slice's best straight to tile_best: nothing else of theirs is stored.
+// Candidate values are stored only where a later stage reads them (quantized
+// and f64 families) or on request (TPE_BATCH_WRITE_CAND).
 __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restrict__ P,
                                                      const tpe_tile* __restrict__ tiles,
                                                      const double* __restrict__ samp,
+                                                     const double4* __restrict__ comp64,
                                                      double* __restrict__ cand, float* __restrict__ coord,
                                                      uint32_t* __restrict__ keys, uint64_t* __restrict__ vals,
-                                                     uint64_t* __restrict__ vals_sorted, int precision, int draw,
-                                                     int key_bits) {
+                                                     uint64_t* __restrict__ vals_sorted,
+                                                     tpe_best* __restrict__ tile_best,
+                                                     double* __restrict__ l_out, double* __restrict__ g_out,
+                                                     int precision, int draw, int key_bits, int flags) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
-  const bool quant = p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
-  const bool logsp = p.family == TPE_FAM_LOGGAUSS || p.family == TPE_FAM_QLOGGAUSS;
-  const double lo = p.low, hi = p.high;
-  // f32 bounds: smallest float >= low, largest float < high
-  float lo_f = -INFINITY, hi_f = INFINITY;
-  if (p.flags & TPE_F_HAS_LOW) { lo_f = (float)lo; if ((double)lo_f < lo) lo_f = nextafterf(lo_f, INFINITY); }
-  if (p.flags & TPE_F_HAS_HIGH) {
-    hi_f = (float)hi;
-    while ((double)hi_f >= hi) hi_f = nextafterf(hi_f, -INFINITY);
-  }
+  const bool store_x = (flags & TPE_BATCH_WRITE_CAND) || precision == TPE_PREC_F64 ||
+                       p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
+  float lo_f, hi_f;
+  f32_bounds(p, lo_f, hi_f);
   const double* S = samp + 8 * (int64_t)p.samp_off;
   const uint32_t khi = (uint32_t)p.sort_slot << key_bits;
   const float kmax = (float)((1 << key_bits) - 1);
@@ -255,56 +354,61 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     for (int q = threadIdx.x; q < p.samp_len; q += kThreads) cum_lds[q] = S[8 * q];
   __syncthreads();
   const int i = tl.cand_start + (int)threadIdx.x + (int)blockIdx.y * kThreads;
-  if (i >= p.n_cand) return;
+  const bool valid = i < p.n_cand;
   const int64_t o = p.cand_off + i;
+  if (draw && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= kCumLds) {
+    // The score of a categorical candidate depends only on its category, so the
+    // slice's argmax (np.argmax: best score, then first index) is the best
+    // category among those drawn, at its first draw.  First index per category:
+    // wave ballots (the lowest set lane is the earliest candidate) for up to 64
+    // categories, LDS atomicMin (order-independent) beyond; then one thread
+    // picks the category from LDS.  No per-candidate gathers or shuffles.
+    __shared__ int first[kCumLds];
+    __shared__ double score[kCumLds];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int base = tl.cand_start + (int)blockIdx.y * kThreads;
+    const int c = valid ? draw_category(p, cum_lds, i) : -1;
+    if (valid && l_out) { l_out[o] = comp64[p.below_off + c].x; g_out[o] = comp64[p.above_off + c].x; }
+    if (valid && (flags & TPE_BATCH_WRITE_CAND)) cand[o] = (double)c;
+    const int U = p.samp_len;
+    for (int q = threadIdx.x; q < U; q += kThreads) {
+      first[q] = INT_MAX;
+      score[q] = comp64[p.below_off + q].x - comp64[p.above_off + q].x;
+    }
+    __syncthreads();
+    if (U <= 64) {
+      for (int cc = 0; cc < U; ++cc) {
+        const unsigned long long m = __ballot(c == cc);
+        if (lane == 0 && m) atomicMin(&first[cc], base + wave * 64 + __builtin_ctzll(m));
+      }
+    } else if (c >= 0) {
+      atomicMin(&first[c], i);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      tpe_best b{0, 0, 0, -1};
+      for (int cc = 0; cc < U; ++cc)
+        if (first[cc] != INT_MAX && better(score[cc], (int64_t)first[cc], b.score, b.idx)) {
+          b.score = score[cc];
+          b.l = comp64[p.below_off + cc].x;
+          b.g = comp64[p.above_off + cc].x;
+          b.idx = first[cc];
+        }
+      tile_best[(int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y] = b;
+    }
+    return;
+  }
+  if (!valid) return;
   float t;                                 // kernel coordinate of the candidate
   if (!draw) {
     t = coord[o];
   } else if (p.samp_len <= 0) {
-    cand[o] = NAN; coord[o] = NAN; t = NAN;
+    cand[o] = NAN; t = NAN;
   } else {
-    const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-    const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-    // component choice: first k with u < cum_k (binary search, <= 27 rows)
-    const double u1 = u01d(r.x, r.y);
-    int a = 0, b = p.samp_len - 1;
-    if (in_lds)
-      while (a < b) { const int m = (a + b) >> 1; if (u1 < cum_lds[m]) b = m; else a = m + 1; }
-    else
-      while (a < b) { const int m = (a + b) >> 1; if (u1 < S[8 * m]) b = m; else a = m + 1; }
-    const double* s = S + 8 * a;
-    if (p.family == TPE_FAM_CATEGORICAL) {
-      cand[o] = (double)a;
-      t = (float)a;
-    } else {
-      // truncated normal by inversion; fa, fb = Phi of the (mirrored) bounds
-      const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
-      const bool flip = s[5] != 0.0;
-      double x;      // draw in sampling space (log space for LGMM1)
-      if (precision == TPE_PREC_F32) {
-        const float pr = (float)fa + u01f(r.z) * ((float)fb - (float)fa);
-        float z = -1.41421356237309505f * erfcinvf(2.f * pr);
-        if (flip) z = -z;
-        float xf = (float)mu + (float)sg * z;
-        if (!(xf == xf)) xf = (float)mu;
-        xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
-        t = xf;
-        x = (double)xf;
-      } else {
-        const double pr = fa + u01d(r.z, r.w) * (fb - fa);
-        double z = -1.41421356237309505 * erfcinv(2.0 * pr);
-        if (flip) z = -z;
-        x = mu + sg * z;
-        if (!(x == x)) x = mu;
-        if ((p.flags & TPE_F_HAS_LOW) && x < lo) x = lo;
-        if ((p.flags & TPE_F_HAS_HIGH) && x >= hi) x = nextafter(hi, -INFINITY);
-        t = (float)x;
-      }
-      if (logsp) x = exp(x);
-      if (quant) x = rint(x / p.q) * p.q;      // np.round: half to even
-      cand[o] = x;
-    }
-    coord[o] = t;
+    double x;
+    int c;
+    draw_one(p, S, in_lds ? cum_lds : S, in_lds ? 1 : 8, i, precision, lo_f, hi_f, x, t, c);
+    if (store_x) cand[o] = x;
   }
   const uint64_t v = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(t);
   if (p.sort_slot >= 0) {
@@ -392,6 +496,41 @@ __device__ __forceinline__ int expand_range(const float4* __restrict__ C, int kb
   return n_exact;
 }
 
+// wave-reduce the moments and add sum_n M_n u^n to every candidate's sum
+__device__ __forceinline__ void add_moments(float (&M)[kTaylorN], float t0, float h, const f2 (&t2)[kR / 2],
+                                            f2 (&s2)[kR / 2]) {
+#pragma unroll
+  for (int q = 0; q < kTaylorN; ++q)
+    for (int off = 32; off > 0; off >>= 1) M[q] += __shfl_xor(M[q], off);
+  const float hinv = h > 0.f ? 1.f / h : 0.f;
+  const f2 c0 = f2{t0, t0}, hv = f2{hinv, hinv};
+#pragma unroll
+  for (int j = 0; j < kR / 2; ++j) {
+    const f2 u = (t2[j] - c0) * hv;
+    f2 acc = f2{M[kTaylorN - 1], M[kTaylorN - 1]};
+#pragma unroll
+    for (int q = kTaylorN - 2; q >= 0; --q) acc = acc * u + f2{M[q], M[q]};
+    s2[j] += acc;
+  }
+}
+
+// the below mixture (<= 26 components, the widest bandwidths of the problem)
+// at the wave's kR x 64 candidates: local expansion (exact fallback) unless
+// TPE_BATCH_NO_EXPAND
+__device__ __forceinline__ void below_sum(const float4* __restrict__ B, int n, float tmin, float tmax, int flags,
+                                          const f2 (&t2)[kR / 2], f2 (&sb2)[kR / 2]) {
+  if (flags & TPE_BATCH_NO_EXPAND) {
+    for (int k = 0; k < n; ++k) ce_step(B[k], t2, sb2);
+    return;
+  }
+  const float t0 = 0.5f * (tmin + tmax), h = 0.5f * (tmax - tmin);
+  float M[kTaylorN];
+#pragma unroll
+  for (int q = 0; q < kTaylorN; ++q) M[q] = 0.f;
+  expand_range(B, 0, n, t0, h, M, t2, sb2);
+  add_moments(M, t0, h, t2, sb2);
+}
+
 __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __restrict__ P,
                                                         const tpe_tile* __restrict__ tiles,
                                                         const tpe_work* __restrict__ W,
@@ -399,7 +538,10 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
                                                         const int32_t* __restrict__ grid,
                                                         const uint64_t* __restrict__ vals,
                                                         double* __restrict__ part,
-                                                        unsigned long long* __restrict__ ce_count, int flags) {
+                                                        tpe_best* __restrict__ tile_best,
+                                                        double* __restrict__ l_out, double* __restrict__ g_out,
+                                                        unsigned long long* __restrict__ ce_count, int flags,
+                                                        int sampled) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
   const int n = p.n_cand;
@@ -457,19 +599,7 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
     n_exact = expand_range(C, k_lo, k_hi, t0, h, M, t2, s2);
     n_exact += expand_range(comp + p.wide_off, 0, wide_len, t0, h, M, t2, s2);
     n_expanded = (long long)(k_hi - k_lo) + wide_len - n_exact;
-#pragma unroll
-    for (int q = 0; q < kTaylorN; ++q)
-      for (int off = 32; off > 0; off >>= 1) M[q] += __shfl_xor(M[q], off);
-    const float hinv = h > 0.f ? 1.f / h : 0.f;
-    const f2 c0 = f2{t0, t0}, hv = f2{hinv, hinv};
-#pragma unroll
-    for (int j = 0; j < kR / 2; ++j) {
-      const f2 u = (t2[j] - c0) * hv;
-      f2 acc = f2{M[kTaylorN - 1], M[kTaylorN - 1]};
-#pragma unroll
-      for (int q = kTaylorN - 2; q >= 0; --q) acc = acc * u + f2{M[q], M[q]};
-      s2[j] += acc;
-    }
+    add_moments(M, t0, h, t2, s2);
   } else {
 #pragma unroll 4
     for (int k = k_lo; k < k_hi; ++k) ce_step(C[k], t2, s2);
@@ -484,6 +614,58 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
   for (int j = 0; j < kR; ++j) {
     const int i = tile_pos(w.cand_start, j);
     if (i < n) out[i] = (double)s[j];
+  }
+  // Fused finalize: a one-split work item holds its whole tile's above sums, so
+  // it scores l - g for the tile and writes the tile's best to slot 0 (slots
+  // 1..7 empty); the packer leaves these tiles out of k_finalize's list.  (Multi-split tiles — the sparse tails — are finalized by
+  // k_finalize: a device-wide handshake between their work items would cost an
+  // L2 write-back per item on this multi-XCD part.)  The below mixture is summed
+  // by the same local expansion (its <= 26 components are the widest of the
+  // problem, so they expand over any wave narrow enough for the above side);
+  // k_finalize sums it directly, so the two agree to fp32 rounding.
+  const bool fin = sampled && !(flags & TPE_BATCH_NO_FUSE) && w.n_splits == 1;
+  const int tile = p.tile_off + w.cand_start / kTile;
+  if (fin) {
+    const bool logsp = p.family == TPE_FAM_LOGGAUSS;
+    double bs = 0, bl = 0, bg = 0;
+    int64_t bi = -1;
+    // below mixture for all kR candidates at once: one pass over its (<= 26)
+    // components, each loaded once per wave (component-outer, like the above sum)
+    f2 sb2[kR / 2];
+    uint32_t oo[kR];                   // original positions: reloaded together (one latency)
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const int i = tile_pos(w.cand_start, j);
+      oo[j] = i < n ? (uint32_t)(vals[p.cand_off + i] >> 32) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kR / 2; ++j) sb2[j] = f2{0.f, 0.f};
+    below_sum(comp + p.below_off, p.below_len, tmin, tmax, flags, t2, sb2);
+    {
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const int i = tile_pos(w.cand_start, j);
+      if (i >= n) continue;
+      const double sa = (double)s[j];
+      const float sb = (j & 1) ? sb2[j >> 1].y : sb2[j >> 1].x;
+      // an under-flowed fixed-shift sum (either side): max-shifted recompute
+      // over the whole mixture, out of line (rare; keeps this loop's registers)
+      const double lb2 = sb > 1e-30f ? (double)__log2f(sb)
+                                     : (double)lse2_exact_ool(comp, p.below_off, p.below_len, 0, 0, t[j]);
+      const double la2 = sa > 1e-30 ? log2(sa)
+                                     : (double)lse2_exact_ool(comp, p.above_off, p.above_len, p.wide_off,
+                                                              p.wide_len, t[j]);
+      const double lnx = logsp ? (double)t[j] : 0.0;
+      const double l = lb2 * kLn2 + p.below_base - lnx;
+      const double g = la2 * kLn2 + p.above_base - lnx;
+      if (l_out) { l_out[oo[j]] = l; g_out[oo[j]] = g; }
+      const int64_t orig = (int64_t)oo[j] - p.cand_off;
+      if (better(l - g, orig, bs, bi)) { bs = l - g; bl = l; bg = g; bi = orig; }
+    }
+    tpe_best* __restrict__ slot = tile_best + (int64_t)tile * TPE_BEST_PER_TILE;
+    block_best(bs, bi, bl, bg, slot);
+    if (threadIdx.x > 0 && threadIdx.x < TPE_BEST_PER_TILE) slot[threadIdx.x] = tpe_best{0, 0, 0, -1};
+    }
   }
   if (ce_count) {       // profiling (no atomics): [exact CE, expanded components] of this work item
     __shared__ unsigned long long wce[kThreads / 64][2];
@@ -585,18 +767,22 @@ __global__ __launch_bounds__(kThreads) void k_above_q(const tpe_problem* __restr
 // compares ORIGINAL indices.
 static_assert(TPE_BEST_PER_TILE * kThreads == kTile, "finalize slices must cover a tile");
 
-__global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __restrict__ P,
-                                                       const tpe_tile* __restrict__ tiles,
-                                                       const float4* __restrict__ comp32,
-                                                       const double4* __restrict__ comp64,
-                                                       const double* __restrict__ cand,
-                                                       const uint64_t* __restrict__ vals,
-                                                       const double* __restrict__ part,
-                                                       double* __restrict__ l_out, double* __restrict__ g_out,
-                                                       tpe_best* __restrict__ tile_best, int precision,
-                                                       int sampled) {
-  const tpe_tile tl = tiles[blockIdx.x];
+__device__ __forceinline__ void finalize_slice(const tpe_problem* __restrict__ P,
+                                               const tpe_tile* __restrict__ tiles,
+                                               const float4* __restrict__ comp32,
+                                               const double4* __restrict__ comp64,
+                                               const double* __restrict__ cand,
+                                               const uint64_t* __restrict__ vals,
+                                               const double* __restrict__ part,
+                                               double* __restrict__ l_out, double* __restrict__ g_out,
+                                               tpe_best* __restrict__ tile_best, int precision,
+                                               int sampled, int flags, int tile) {
+  const tpe_tile tl = tiles[tile];
   const tpe_problem& p = P[tl.problem];
+  // sampled categorical tiles are finalized by k_sample (one-split continuous
+  // f32 tiles by the above kernel: they are never in the finalize list)
+  if (sampled && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= kCumLds) return;
+
   const int n = p.n_cand;
   const int i = tl.cand_start + (int)threadIdx.x + (int)blockIdx.y * kThreads;
   const bool valid = i < n;
@@ -612,10 +798,12 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
     const double* __restrict__ ps = part + (int64_t)tl.work_first * kTile + (i - tl.cand_start);
     const int ns = valid ? tl.n_splits : 0;
     int sp = 0;
-    for (; sp + 4 <= ns; sp += 4) {         // four loads in flight per step
-      const double a0 = ps[(int64_t)sp * kTile], a1 = ps[(int64_t)(sp + 1) * kTile];
-      const double a2 = ps[(int64_t)(sp + 2) * kTile], a3 = ps[(int64_t)(sp + 3) * kTile];
-      sa += a0; sa += a1; sa += a2; sa += a3;
+    for (; sp + 8 <= ns; sp += 8) {         // eight loads in flight per step
+      double a[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = ps[(int64_t)(sp + q) * kTile];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sa += a[q];
     }
     for (; sp < ns; ++sp) sa += ps[(int64_t)sp * kTile];
   }
@@ -680,8 +868,26 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
     tpe_best b = wb[0];
     for (int q = 1; q < kThreads / 64; ++q)
       if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
-    tile_best[(int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y] = b;
+    tile_best[(int64_t)tile * TPE_BEST_PER_TILE + blockIdx.y] = b;
   }
+}
+
+// grid (n_fin, TPE_BEST_PER_TILE): tile fin_tiles[x] (every tile when fin_tiles
+// is NULL).  The packer lists only the tiles no upstream stage finalizes.
+__global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __restrict__ P,
+                                                       const tpe_tile* __restrict__ tiles,
+                                                       const int32_t* __restrict__ fin_tiles,
+                                                       const float4* __restrict__ comp32,
+                                                       const double4* __restrict__ comp64,
+                                                       const double* __restrict__ cand,
+                                                       const uint64_t* __restrict__ vals,
+                                                       const double* __restrict__ part,
+                                                       double* __restrict__ l_out, double* __restrict__ g_out,
+                                                       tpe_best* __restrict__ tile_best, int precision,
+                                                       int sampled, int flags) {
+  const int tile = fin_tiles ? fin_tiles[blockIdx.x] : (int)blockIdx.x;
+  finalize_slice(P, tiles, comp32, comp64, cand, vals, part, l_out, g_out, tile_best, precision, sampled, flags,
+                 tile);
 }
 
 // ================================================================= select
@@ -691,6 +897,7 @@ constexpr int kSelThreads = 1024;
 __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __restrict__ P,
                                                      const tpe_best* __restrict__ tile_best,
                                                      const double* __restrict__ cand,
+                                                     const double* __restrict__ samp, int precision, int sampled,
                                                      tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
   tpe_best b{0, 0, 0, -1};
@@ -715,7 +922,16 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
       if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
     tpe_result r;
     r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
-    r.value = b.idx >= 0 ? cand[p.cand_off + b.idx] : 0.0;
+    r.value = 0.0;
+    if (b.idx >= 0 && sampled && p.samp_len > 0) {   // re-draw the winner: its value was never stored
+      float lo_f, hi_f, t;
+      int c;
+      f32_bounds(p, lo_f, hi_f);
+      const double* S = samp + 8 * (int64_t)p.samp_off;
+      draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
+    } else if (b.idx >= 0) {
+      r.value = cand[p.cand_off + b.idx];
+    }
     r.global_idx = b.idx >= 0 ? p.cand_base + b.idx : -1;
     result[blockIdx.x] = r;
   }
@@ -1037,9 +1253,10 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->sample && !b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
   if (b->n_tiles == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, kR), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
-                     b->samp, b->cand, b->coord, b->keys, b->vals, b->vals_sorted, b->precision, b->sample,
-                     b->key_bits);
+  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
+                     b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
+                     b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
+                     b->flags);
   return hip_check("tpe_sample");
 }
 
@@ -1068,7 +1285,8 @@ int tpe_score_above(const tpe_batch* b, void* stream) {
   if (n_cont) {
     if (b->precision == TPE_PREC_F32)
       hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
-                         (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->ce_count, b->flags);
+                         (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->tile_best,
+                         b->l_out, b->g_out, b->ce_count, b->flags, b->sample);
     else
       hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
                          (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
@@ -1087,9 +1305,15 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_tiles == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_finalize, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream, b->problems, b->tiles,
+  // only the listed tiles, unless every tile may need this stage (caller-drawn
+  // candidates, no fused finalize)
+  const bool listed = b->fin_tiles && b->sample && !(b->flags & TPE_BATCH_NO_FUSE);
+  const int n_fin = listed ? b->n_fin_tiles : b->n_tiles;
+  if (n_fin == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_finalize, dim3(n_fin, TPE_BEST_PER_TILE), dim3(kThreads), 0,
+                     (hipStream_t)stream, b->problems, b->tiles, listed ? b->fin_tiles : nullptr,
                      (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->vals_sorted,
-                     b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample);
+                     b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample, b->flags);
   return hip_check("tpe_finalize");
 }
 
@@ -1098,7 +1322,7 @@ int tpe_select(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_problems == 0) return TPE_OK;
   hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
-                     b->tile_best, b->cand, b->result);
+                     b->tile_best, b->cand, b->samp, b->precision, b->sample, b->result);
   return hip_check("tpe_select");
 }
 
@@ -1182,6 +1406,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.sort_count = info.sort_count;
   b.tiles = (const tpe_tile*)(dev + info.off_tiles);
   b.n_tiles = (int32_t)info.n_tiles;
+  b.fin_tiles = (const int32_t*)(dev + info.off_fin_tiles);
+  b.n_fin_tiles = (int32_t)info.n_fin_tiles;
   b.work = (const tpe_work*)(dev + info.off_work);
   b.n_work_cont = info.n_work_cont; b.n_work_qgauss = info.n_work_qgauss; b.n_work_qlog = info.n_work_qlog;
   b.part = ws->part;

@@ -109,6 +109,9 @@ class Engine(object):
         # pruned f32 above kernel: local (Taylor) expansion of components whose
         # series converges over a wave's candidate span (False: all exact)
         self.expand = True
+        # continuous f32 tiles with one split: score in the above kernel (False:
+        # always in the finalize stage)
+        self.fuse = True
 
     def set_precision(self, precision):
         if precision not in ('fp32', 'fp64'):
@@ -364,6 +367,10 @@ class Engine(object):
             break
         return info
 
+    def _flags(self):
+        return (0 if self.expand else N.BATCH_NO_EXPAND) | (0 if self.fuse else N.BATCH_NO_FUSE) | \
+            int(os.environ.get('TPE_DEBUG_FLAGS', '0'))
+
     # ----------------------------------------------------- one-call level
     def _level_ws(self):
         """tpe_level_ws over the engine's pools (rebuilt when a pool grows)."""
@@ -437,7 +444,7 @@ class Engine(object):
         for attempt in range(3):
             ws = self._level_ws()
             rc = self.lib.tpe_level_run(labels, len(problems), n_cand, seed64, int(cand_base), ncg, prec,
-                                        0 if self.expand else N.BATCH_NO_EXPAND, ctypes.byref(ws),
+                                        self._flags(), ctypes.byref(ws),
                                         ctypes.byref(need), stream, out.ctypes.data)
             if rc != N.E_SPACE:
                 break
@@ -519,7 +526,7 @@ class Engine(object):
         b = N.Batch()
         b.problems, b.n_problems = base + info.off_problems, P
         b.precision = N.PREC_F64 if self.precision == 'fp64' else N.PREC_F32
-        b.flags = 0 if self.expand else N.BATCH_NO_EXPAND
+        b.flags = self._flags() | (N.BATCH_WRITE_CAND if (return_cand or want_lg) else 0)
         b.sample = 0 if inject else 1
         b.sort_end_bit, b.key_bits = info.sort_end_bit, info.key_bits
         b.comp32, b.comp64 = base + info.off_comp32, base + info.off_comp64
@@ -532,6 +539,7 @@ class Engine(object):
         b.sort_count = info.sort_count
         b.cand, b.coord = d_cand.data_ptr(), d_coord.data_ptr()
         b.tiles, b.n_tiles = base + info.off_tiles, n_tiles
+        b.fin_tiles, b.n_fin_tiles = base + info.off_fin_tiles, info.n_fin_tiles
         b.work = base + info.off_work
         b.n_work_cont, b.n_work_qgauss, b.n_work_qlog = info.n_work_cont, info.n_work_qgauss, info.n_work_qlog
         b.part = d_part.data_ptr()

@@ -39,6 +39,10 @@ extern "C" {
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
 
+/* categorical problems with at most this many categories are scored by the
+ * sample stage itself (device-drawn candidates) */
+#define TPE_SAMPLE_LDS_ROWS 1024
+
 /* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
 enum {
   TPE_FAM_GAUSS = 0,       /* GMM1_lpdf, q=None   (uniform, normal)            */
@@ -56,7 +60,12 @@ enum {
 
 /* tpe_batch.flags / tpe_level_run flags */
 enum {
-  TPE_BATCH_NO_EXPAND = 1  /* pruned f32 kernel: evaluate every component exactly (no local expansion) */
+  TPE_BATCH_NO_EXPAND = 1,  /* pruned f32 kernel: evaluate every component exactly (no local expansion) */
+  TPE_BATCH_WRITE_CAND = 2, /* store every drawn candidate value in cand (else only where a later stage
+                               reads it: quantized families and TPE_PREC_F64; the winner's value is
+                               re-drawn by the select stage) */
+  TPE_BATCH_NO_FUSE = 4     /* score every continuous tile in the finalize stage (no fused finalize
+                               in the above kernel) */
 };
 
 /* precision of the continuous (non-quantized) families; quantized families
@@ -206,7 +215,7 @@ typedef struct tpe_batch {
   const double* comp64;  /* [n][4]                                             */
   const double* samp;    /* [n][8]                                             */
   const int32_t* grid;   /* pruning grids                                      */
-  double* cand;          /* [total_cand] candidate values (returned to the user) */
+  double* cand;          /* [total_cand] candidate values (see TPE_BATCH_WRITE_CAND) */
   float* coord;          /* [total_cand] kernel coordinate t in f32 (x or ln x) */
   uint32_t* keys;        /* [total_cand] (problem << key_bits | value bucket of t) */
   uint64_t* vals;        /* [total_cand] (position << 32) | f32 bits of t       */
@@ -214,8 +223,13 @@ typedef struct tpe_batch {
   uint64_t* vals_sorted; /* [total_cand] (== vals when not sorting)            */
   void* sort_tmp; uint64_t sort_tmp_bytes;   /* tpe_sort_workspace_bytes()     */
   int64_t total_cand;
-  const tpe_tile* tiles; int32_t n_tiles; int32_t reserved2;
+  const tpe_tile* tiles; int32_t n_tiles; int32_t n_fin_tiles;
   int64_t sort_count;    /* candidates [0, sort_count) are sorted (sorted problems first) */
+  const int32_t* fin_tiles; /* [n_fin_tiles] tiles the finalize stage scores when the candidates
+                               are device-drawn (the others are scored by the sample stage —
+                               categorical — or the fused above stage — one-split continuous
+                               f32);
+                               NULL: every tile */
   /* above-mixture work list, ordered [continuous | quantized Gauss | quantized log] */
   const tpe_work* work;
   int32_t n_work_cont, n_work_qgauss, n_work_qlog, reserved3;
@@ -306,6 +320,7 @@ typedef struct tpe_pack_info {
   int64_t fit_total;
   int64_t copy_end, copy2_len;
   int64_t sort_count;               /* candidates of the sorted (pruned) problems */
+  int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation

@@ -18,6 +18,7 @@ from hyperopt_amd.engine import LevelProblem, get_engine  # noqa: E402
 def main():
     rep = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     eng = get_engine(torch.device('cuda', 0))
+    eng.fuse = os.environ.get('TPE_NO_FUSE') is None
     domain, trials = bench.make_history(bench.N_HISTORY, bench.SEED)
     hist = H.extract(domain, trials)
     fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, eng)
