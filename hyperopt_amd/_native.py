@@ -75,7 +75,7 @@ class Batch(ctypes.Structure):
         ('below_idx', ctypes.c_void_p), ('fit_seg', ctypes.c_void_p), ('fit_total', ctypes.c_int64),
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
-        ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64),
+        ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64), ('fit_max_seg', ctypes.c_int64),
     ]
 
 
@@ -106,7 +106,7 @@ class PackInfo(ctypes.Structure):
         ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
         ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
-        ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64),
+        ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_seg', ctypes.c_int64),
     ]
 
 

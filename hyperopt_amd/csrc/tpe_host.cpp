@@ -573,6 +573,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp64 = off[3];
   info->off_samp = off[4]; info->off_fit = off[5]; info->off_below_idx = off[6]; info->off_fit_seg = off[7];
   info->off_fin_tiles = off[8]; info->n_fin_tiles = n_fin;
+  info->fit_max_seg = 0;
+  for (size_t q = 1; q < fit_seg.size(); ++q) info->fit_max_seg = std::max(info->fit_max_seg, fit_seg[q] - fit_seg[q - 1]);
   info->off_grid = off[9]; info->off_comp32 = off[10];
   info->n_problems = P;
   info->n_tiles = (int64_t)tiles.size();

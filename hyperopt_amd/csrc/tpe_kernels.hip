@@ -609,12 +609,6 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
   }
 #pragma unroll
   for (int j = 0; j < kR / 2; ++j) { s[2 * j] = s2[j].x; s[2 * j + 1] = s2[j].y; }
-  double* __restrict__ out = part + part_row(P, tiles, w) * kTile - w.cand_start;
-#pragma unroll
-  for (int j = 0; j < kR; ++j) {
-    const int i = tile_pos(w.cand_start, j);
-    if (i < n) out[i] = (double)s[j];
-  }
   // Fused finalize: a one-split work item holds its whole tile's above sums, so
   // it scores l - g for the tile and writes the tile's best to slot 0 (slots
   // 1..7 empty); the packer leaves these tiles out of k_finalize's list.  (Multi-split tiles — the sparse tails — are finalized by
@@ -625,6 +619,14 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
   // k_finalize sums it directly, so the two agree to fp32 rounding.
   const bool fin = sampled && !(flags & TPE_BATCH_NO_FUSE) && w.n_splits == 1;
   const int tile = p.tile_off + w.cand_start / kTile;
+  if (!fin) {                          // partial sums for k_finalize
+    double* __restrict__ out = part + part_row(P, tiles, w) * kTile - w.cand_start;
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const int i = tile_pos(w.cand_start, j);
+      if (i < n) out[i] = (double)s[j];
+    }
+  }
   if (fin) {
     const bool logsp = p.family == TPE_FAM_LOGGAUSS;
     double bs = 0, bl = 0, bg = 0;
@@ -975,6 +977,47 @@ __global__ __launch_bounds__(kFitGatherBlock) void k_fit_gather(const tpe_fit_jo
   }
 }
 
+// Segments of up to kFitSortMax observations: one workgroup sorts a segment in
+// LDS (bitonic network on (key, rank) pairs — ranks are unique, so the order is
+// the stable order rocPRIM's radix sort gives).  Larger segments use rocPRIM.
+constexpr int kFitSortMax = 8192;
+constexpr int kFitSortThreads = 1024;
+__global__ __launch_bounds__(kFitSortThreads) void k_fit_sort_lds(const int64_t* __restrict__ seg,
+                                                                  const double* __restrict__ keys,
+                                                                  const uint32_t* __restrict__ vals,
+                                                                  double* __restrict__ keys_out,
+                                                                  uint32_t* __restrict__ vals_out) {
+  __shared__ double sk[kFitSortMax];
+  __shared__ uint32_t sv[kFitSortMax];
+  const int64_t b0 = seg[blockIdx.x];
+  const int n = (int)(seg[blockIdx.x + 1] - b0);
+  int N = 1;
+  while (N < n) N <<= 1;
+  for (int i = threadIdx.x; i < N; i += kFitSortThreads) {
+    sk[i] = i < n ? keys[b0 + i] : INFINITY;
+    sv[i] = i < n ? vals[b0 + i] : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  for (int k = 2; k <= N; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = threadIdx.x; i < N; i += kFitSortThreads) {
+        const int ixj = i ^ jj;
+        if (ixj > i) {
+          const double ka = sk[i], kb = sk[ixj];
+          const uint32_t va = sv[i], vb = sv[ixj];
+          const bool gt = ka > kb || (ka == kb && va > vb);
+          if (gt == ((i & k) == 0)) { sk[i] = kb; sk[ixj] = ka; sv[i] = vb; sv[ixj] = va; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < n; i += kFitSortThreads) {
+    keys_out[b0 + i] = sk[i];
+    vals_out[b0 + i] = sv[i];
+  }
+}
+
 // deterministic block reductions (fixed tree order)
 template <typename T, typename Op>
 __device__ __forceinline__ T block_reduce(T v, Op op, T* lds) {
@@ -1014,13 +1057,11 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __
   v.s = keys_sorted + j.seg_off;
   v.n = n;
   v.pmu = j.prior_mu;
-  {  // np.searchsorted(srtd_mus, prior_mu) (side left): number of observations < prior_mu
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int64_t m = (lo + hi) >> 1;
-      if (v.s[m] < j.prior_mu) lo = m + 1; else hi = m;
-    }
-    v.pos = lo;
+  {  // np.searchsorted(srtd_mus, prior_mu) (side left) = number of observations < prior_mu:
+     // a block count over the sorted keys (coalesced) instead of a serial binary search
+    double c = 0;
+    for (int64_t i = threadIdx.x; i < n; i += kFitThreads) c += v.s[i] < j.prior_mu ? 1.0 : 0.0;
+    v.pos = (int64_t)block_reduce(c, [](double a, double b) { return a + b; }, red);
   }
   const uint32_t* __restrict__ rank = vals_sorted + j.seg_off;
   const double smax = j.prior_sigma, smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);   // tpe.py:465-470
@@ -1068,18 +1109,39 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __
       }
     }
   }
-  auto add = [](double a, double b) { return a + b; };
-  auto mx = [](double a, double b) { return fmax(a, b); };
-  W = block_reduce(W, add, red);
-  M = block_reduce(M, add, red);
-  cm = block_reduce(cm, mx, red);
-  sm_all = block_reduce(sm_all, mx, red);
-  double thr = INFINITY, s_narrow = sm_all;
-  for (int m = 0; m < kThr; ++m) {
-    const double c = block_reduce((double)cnt[m], add, red);
-    const double s2 = block_reduce(sm[m], mx, red);
-    if (thr == INFINITY && c <= (double)(kPruneWide - 1)) { thr = smin * (double)(2 << m); s_narrow = s2; }
+  // all 14 reductions in one round: sums [W, M, cnt0..4], maxima [cm, sm_all, sm0..4]
+  constexpr int kNS = 2 + kThr, kNM = 2 + kThr;
+  double vs[kNS] = {W, M}, vm[kNM] = {cm, sm_all};
+#pragma unroll
+  for (int m = 0; m < kThr; ++m) { vs[2 + m] = (double)cnt[m]; vm[2 + m] = sm[m]; }
+  __shared__ double rs[kFitThreads / 64][kNS], rm[kFitThreads / 64][kNM];
+  for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+    for (int q = 0; q < kNS; ++q) vs[q] += __shfl_xor(vs[q], o);
+#pragma unroll
+    for (int q = 0; q < kNM; ++q) vm[q] = fmax(vm[q], __shfl_xor(vm[q], o));
   }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < kNS; ++q) rs[threadIdx.x >> 6][q] = vs[q];
+#pragma unroll
+    for (int q = 0; q < kNM; ++q) rm[threadIdx.x >> 6][q] = vm[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kNS; ++q) {
+    vs[q] = rs[0][q];
+    for (int wv = 1; wv < kFitThreads / 64; ++wv) vs[q] += rs[wv][q];
+  }
+#pragma unroll
+  for (int q = 0; q < kNM; ++q) {
+    vm[q] = rm[0][q];
+    for (int wv = 1; wv < kFitThreads / 64; ++wv) vm[q] = fmax(vm[q], rm[wv][q]);
+  }
+  W = vs[0]; M = vs[1]; cm = vm[0]; sm_all = vm[1];
+  double thr = INFINITY, s_narrow = sm_all;
+  for (int m = 0; m < kThr; ++m)
+    if (thr == INFINITY && vs[2 + m] <= (double)(kPruneWide - 1)) { thr = smin * (double)(2 << m); s_narrow = vm[2 + m]; }
   if (threadIdx.x == 0) n_wide = 0;
   __syncthreads();
   // pass 2: rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and
@@ -1113,23 +1175,34 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __
     comp[j.wide_off + threadIdx.x] =
         make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - cm));
   }
-  // grid over the f32 means: first component with mu32 >= bucket edge
+  // grid over the f32 means: grid[g] = first component with mu32 >= edge_g,
+  // edge_g = glo + g / ginv.  Scattered by component: component i owns the
+  // buckets whose edge lies in (mu32[i-1], mu32[i]] (i = K: the rest), found
+  // from the bucket estimate and corrected against the exact edge formula, so
+  // the work is O(K + G) with no dependent loads.
   const double glo = (double)(float)v.mu(0), ghi = (double)(float)v.mu(K - 1);
   const int G = j.grid_n;
   const float ginv = ghi > glo ? (float)((double)G / (ghi - glo)) : 0.f;
   int32_t* __restrict__ Gp = grid + j.grid_off;
-  for (int g = threadIdx.x; g < G; g += kFitThreads) {
-    int64_t r = 0;
-    if (ginv > 0.f) {
-      const double edge = glo + (double)g / (double)ginv;
-      int64_t lo = 0, hi = K;
-      while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if ((double)(float)v.mu(m) < edge) lo = m + 1; else hi = m;
-      }
-      r = lo;
+  if (ginv > 0.f) {
+    const double gi = (double)ginv;
+    auto edge = [&](int64_t g) { return glo + (double)g / gi; };
+    // first bucket whose edge is > x
+    auto first_above = [&](double x) -> int64_t {
+      if (!(x >= glo)) return 0;
+      int64_t g = (int64_t)floor((x - glo) * gi);
+      g = g < 0 ? 0 : (g > G ? G : g);
+      while (g > 0 && edge(g - 1) > x) --g;
+      while (g < G && !(edge(g) > x)) ++g;
+      return g;
+    };
+    for (int64_t i = threadIdx.x; i <= K; i += kFitThreads) {
+      const int64_t g0 = i == 0 ? 0 : first_above((double)(float)v.mu(i - 1));
+      const int64_t g1 = i == K ? G : first_above((double)(float)v.mu(i));    // edges <= mu32[i]: [g0, g1)
+      for (int64_t g = g0; g < g1; ++g) Gp[g] = (int32_t)i;
     }
-    Gp[g] = (int32_t)r;
+  } else {
+    for (int g = threadIdx.x; g < G; g += kFitThreads) Gp[g] = 0;
   }
   if (threadIdx.x == 0) Gp[G] = (int32_t)K;
   // problem rows: lpdf = ln2 * log2(sum) + base; base = ln2*cm - ln(W sqrt(2 pi) p_accept)
@@ -1234,13 +1307,20 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   hipLaunchKernelGGL(k_fit_gather, dim3(gx, b->n_fit), dim3(kFitGatherBlock), 0, s, b->fit, b->below_idx,
                      b->fit_keys, b->fit_vals);
   if ((rc = hip_check("tpe_fit_above/gather"))) return rc;
-  size_t sz = (size_t)b->fit_tmp_bytes;
-  hipError_t e = rocprim::segmented_radix_sort_pairs(
-      b->fit_tmp, sz, (const double*)b->fit_keys, b->fit_keys_sorted, (const uint32_t*)b->fit_vals,
-      b->fit_vals_sorted, (unsigned int)b->fit_total, (unsigned int)b->n_fit, b->fit_seg, b->fit_seg + 1, 0u, 64u, s);
-  if (e != hipSuccess) {
-    snprintf(g_err, sizeof(g_err), "tpe_fit_above/sort: %s", hipGetErrorString(e));
-    return TPE_E_HIP;
+  if (b->fit_max_seg <= kFitSortMax) {
+    hipLaunchKernelGGL(k_fit_sort_lds, dim3(b->n_fit), dim3(kFitSortThreads), 0, s, b->fit_seg, b->fit_keys,
+                       b->fit_vals, b->fit_keys_sorted, b->fit_vals_sorted);
+    if ((rc = hip_check("tpe_fit_above/sort"))) return rc;
+  } else {
+    size_t sz = (size_t)b->fit_tmp_bytes;
+    hipError_t e = rocprim::segmented_radix_sort_pairs(
+        b->fit_tmp, sz, (const double*)b->fit_keys, b->fit_keys_sorted, (const uint32_t*)b->fit_vals,
+        b->fit_vals_sorted, (unsigned int)b->fit_total, (unsigned int)b->n_fit, b->fit_seg, b->fit_seg + 1, 0u, 64u,
+        s);
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "tpe_fit_above/sort: %s", hipGetErrorString(e));
+      return TPE_E_HIP;
+    }
   }
   hipLaunchKernelGGL(k_fit_build, dim3(b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
                      b->fit_vals_sorted, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32,
@@ -1422,6 +1502,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.fit_keys = ws->fit_keys; b.fit_keys_sorted = ws->fit_keys_sorted;
     b.fit_vals = ws->fit_vals; b.fit_vals_sorted = ws->fit_vals_sorted;
     b.fit_tmp = ws->fit_tmp; b.fit_tmp_bytes = (uint64_t)ws->fit_tmp_bytes;
+    b.fit_max_seg = info.fit_max_seg;
   }
   if ((rc = tpe_run_batch(&b, stream))) return rc;
   tpe_result* rh = (tpe_result*)(host + res_off);

@@ -561,6 +561,7 @@ class Engine(object):
             b.fit_keys, b.fit_keys_sorted = d_fk.data_ptr(), d_fks.data_ptr()
             b.fit_vals, b.fit_vals_sorted = d_fv.data_ptr(), d_fvs.data_ptr()
             b.fit_tmp, b.fit_tmp_bytes = d_ft.data_ptr(), d_ft.numel()
+            b.fit_max_seg = info.fit_max_seg
         stream = torch.cuda.current_stream(self.device).cuda_stream
         if self.profile is None:
             N.check(self.lib.tpe_run_batch(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, 'tpe_run_batch')
@@ -584,7 +585,10 @@ class Engine(object):
 
     def _run_profiled(self, b, stream, tb, n_cand):
         """The same launches as tpe_run_batch, one stage at a time, bracketed
-        by events on the launch stream (bench.py's roofline measurement)."""
+        by events on the launch stream (bench.py's roofline measurement).
+        profile[name] gets (ms, units) per launch: units = algorithmic CE for
+        the above kernels (+ exact CE, expanded components and candidates for
+        k_above_f32), algorithmic bytes for the sort, candidates otherwise."""
         prob = tb['prob']
         fam = prob['family']
         ce = (prob['above_len'].astype(np.float64) * n_cand)
@@ -596,8 +600,11 @@ class Engine(object):
         if b.n_fit:
             stages.append(('fit', self.lib.tpe_fit_above, None, float(b.fit_total)))
         stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
-        if b.sort_end_bit:
-            stages.append(('sort', self.lib.tpe_sort, None, float(tb['P'] * n_cand)))
+        if b.sort_end_bit and b.sort_count:
+            # units: bytes of an LSD radix sort of (u32 key, u64 value) pairs —
+            # every 8-bit pass reads and writes both arrays
+            passes = (int(b.sort_end_bit) + 7) // 8
+            stages.append(('sort', self.lib.tpe_sort, None, float(passes * 2 * 12 * int(b.sort_count))))
         for gi, (mask, name) in enumerate(groups):
             if counts[gi]:
                 stages.append((name, self.lib.tpe_score_above, gi, float(ce[mask].sum())))
@@ -629,7 +636,8 @@ class Engine(object):
         for i, (name, fn, gi, units) in enumerate(stages):
             rec = (evs[i].elapsed_time(evs[i + 1]) / rep, units)
             if name == 'k_above_f32':
-                rec = rec + (float(executed), float(expanded))
+                n_c = float(((fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)).sum() * n_cand)
+                rec = rec + (float(executed), float(expanded), n_c)
             self.profile.setdefault(name, []).append(rec)
 
 

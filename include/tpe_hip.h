@@ -249,6 +249,7 @@ typedef struct tpe_batch {
   double* fit_keys; double* fit_keys_sorted;        /* [fit_total]                */
   uint32_t* fit_vals; uint32_t* fit_vals_sorted;    /* [fit_total]                */
   void* fit_tmp; uint64_t fit_tmp_bytes;            /* tpe_fit_workspace_bytes()  */
+  int64_t fit_max_seg;        /* longest fit segment (<= 8192: sorted in LDS, no fit_tmp use) */
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
@@ -321,6 +322,7 @@ typedef struct tpe_pack_info {
   int64_t copy_end, copy2_len;
   int64_t sort_count;               /* candidates of the sorted (pruned) problems */
   int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
+  int64_t fit_max_seg;                  /* tpe_batch.fit_max_seg */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation

@@ -14,4 +14,5 @@ run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&
 run valu SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE &&
 run wait SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU &&
-python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.json && cat gpurun_out/pmc/summary.json
+python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.json &&
+python3 -c "import json; print(json.dumps(json.load(open('gpurun_out/pmc/summary.json'))['traffic'], indent=1))"
