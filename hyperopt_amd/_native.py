@@ -95,6 +95,22 @@ class LabelIn(ctypes.Structure):
     ]
 
 
+def _dtype_of(struct):
+    """numpy mirror of a ctypes Structure (pointers as uint64): lets a whole
+    array of structs be filled with one tuple assignment per element."""
+    conv = {ctypes.c_int32: '<i4', ctypes.c_int64: '<i8', ctypes.c_double: '<f8', ctypes.c_void_p: '<u8',
+            ctypes.c_uint64: '<u8'}
+    names, formats, offsets = [], [], []
+    for name, ct in struct._fields_:
+        names.append(name)
+        formats.append(conv[ct])
+        offsets.append(getattr(struct, name).offset)
+    return np.dtype(dict(names=names, formats=formats, offsets=offsets, itemsize=ctypes.sizeof(struct)))
+
+
+LABEL_DTYPE = _dtype_of(LabelIn)
+
+
 class PackInfo(ctypes.Structure):
     _fields_ = [
         ('off_problems', ctypes.c_int64), ('off_tiles', ctypes.c_int64), ('off_work', ctypes.c_int64),
@@ -138,8 +154,8 @@ E_SPACE = -4
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
            'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above',
-           'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_cat_probs', 'tpe_host_pack_level',
-           'tpe_level_run')
+           'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
+           'tpe_host_cat_probs', 'tpe_host_pack_level', 'tpe_level_run')
 
 
 class NativeUnavailable(RuntimeError):
@@ -177,13 +193,16 @@ def load(path=LIB_PATH):
     lib.tpe_host_fit_parzen.argtypes = [P, ctypes.c_int64, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                         ctypes.c_int32, P, P, P]
     lib.tpe_host_fit_parzen.restype = ctypes.c_int64
+    D = ctypes.c_double
+    lib.tpe_host_fit_split.argtypes = [P, P, P, ctypes.c_int64, P, ctypes.c_int64, D, D, D, ctypes.c_int32, P, P]
+    lib.tpe_host_fit_split.restype = ctypes.c_int
     lib.tpe_host_cat_probs.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_double, ctypes.c_int32, P]
     lib.tpe_host_cat_probs.restype = ctypes.c_int
-    lib.tpe_host_pack_level.argtypes = [ctypes.POINTER(LabelIn), ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+    lib.tpe_host_pack_level.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64,
                                         ctypes.POINTER(PackInfo)]
     lib.tpe_host_pack_level.restype = ctypes.c_int
-    lib.tpe_level_run.argtypes = [ctypes.POINTER(LabelIn), ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+    lib.tpe_level_run.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(LevelWS),
                                   ctypes.POINTER(LevelNeed), P, P]
     lib.tpe_level_run.restype = ctypes.c_int

@@ -22,8 +22,8 @@ def build(force=False, verbose=False):
     host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
     dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o')
     cmds = [
-        [gxx, '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall', '-c', HOST_SRC,
-         '-o', host_o],
+        [gxx, '-O3', '-march=x86-64-v3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall',
+         '-c', HOST_SRC, '-o', host_o],
         [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
          '-Wno-unused-command-line-argument', '-c', SRC, '-o', dev_o],
         [hipcc, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-Wno-unused-command-line-argument', '-o', tmp,

@@ -121,20 +121,22 @@ double p_accept(const double* w, const double* mu, const double* sg, int64_t k, 
   return np_sum(t.data(), k);
 }
 
-// log2 via frexp + atanh series (|s| <= 0.1716: truncation < 1e-11), ~4x
-// cheaper than libm; used only for the f32 component tables
-inline double fast_log2(double x) {
-  if (!(x > 0) || !std::isfinite(x) || x < 2.2250738585072014e-308) return log2(x);
+// log2 of a positive normal double: exponent bits + atanh series of the
+// mantissa in [sqrt(1/2), sqrt(2)) (|s| <= 0.1716: truncation < 1e-11).  No
+// branches, so a loop of it vectorises; used only for the f32 component tables.
+inline double log2_normal(double x) {
   uint64_t u;
   memcpy(&u, &x, 8);
-  int e = (int)((u >> 52) & 0x7FF) - 1022;          // x = m * 2^e, m in [0.5, 1)
-  u = (u & 0x000FFFFFFFFFFFFFull) | 0x3FE0000000000000ull;
+  double e = (double)((int32_t)((u >> 52) & 0x7FF) - 1023);
+  u = (u & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;      // m in [1, 2)
   double m;
   memcpy(&m, &u, 8);
-  if (m < 0.70710678118654752) { m *= 2.0; e -= 1; }
+  const bool big = m > 1.4142135623730951;
+  m = big ? m * 0.5 : m;
+  e = big ? e + 1.0 : e;
   const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
   const double p = s * (2.0 + s2 * (2.0 / 3 + s2 * (2.0 / 5 + s2 * (2.0 / 7 + s2 * (2.0 / 9 + s2 * (2.0 / 11))))));
-  return (double)e + p * 1.4426950408889634074;
+  return e + p * 1.4426950408889634074;
 }
 
 }  // namespace
@@ -186,6 +188,54 @@ int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, 
   const double tot = np_sum(w, K);
   for (int64_t i = 0; i < K; ++i) w[i] = w[i] / tot;
   return pos;
+}
+
+int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* order, int64_t n,
+                       const int64_t* below_tids, int64_t n_bt, double prior_weight, double prior_mu,
+                       double prior_sigma, int32_t lf, double* out, int64_t* out_k) {
+  if (n < 0 || n_bt < 0 || (n && (!x || !tids || !order)) || (n_bt && !below_tids) || !out || !out_k)
+    return TPE_E_ARG;
+  // ap_filter_trials (tpe.py:629-636): is each observation's tid in the below
+  // set — both ascending, so one merge; each side keeps tid order
+  std::vector<double> side[2];
+  std::vector<int64_t> local((size_t)n);
+  std::vector<uint8_t> which((size_t)n);
+  side[0].reserve((size_t)std::min(n, n_bt));
+  side[1].reserve((size_t)n);
+  int64_t b = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i && tids[i] <= tids[i - 1]) return TPE_E_ARG;
+    while (b < n_bt && below_tids[b] < tids[i]) ++b;
+    const int sd = b < n_bt && below_tids[b] == tids[i] ? 0 : 1;
+    which[i] = (uint8_t)sd;
+    local[i] = (int64_t)side[sd].size();
+    side[sd].push_back(x[i]);
+  }
+  // each side's sort permutation: the label's order filtered (stable in it)
+  std::vector<int64_t> ord[2];
+  ord[0].reserve(side[0].size());
+  ord[1].reserve(side[1].size());
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t p = order[i];
+    if (p < 0 || p >= n) return TPE_E_ARG;
+    ord[which[p]].push_back(local[p]);
+  }
+  const int64_t cap = n + 1;
+  for (int sd = 0; sd < 2; ++sd) {
+    const std::vector<double>& v = side[sd];
+    const std::vector<int64_t>& o = ord[sd];
+    const int64_t m = (int64_t)v.size();
+    out_k[sd] = 0;
+    bool fallback = m >= 1 && v[o[0]] != v[o[0]];                       // NaN
+    for (int64_t i = 1; i < m && !fallback; ++i) fallback = !(v[o[i - 1]] < v[o[i]]);
+    if (fallback) continue;       // repeated values / NaN: np.argsort's order decides the weights
+    double* w = out + (3 * sd) * cap;
+    const int64_t pos = tpe_host_fit_parzen(v.data(), m, m >= 2 ? o.data() : nullptr, prior_weight, prior_mu,
+                                            prior_sigma, lf, w, w + cap, w + 2 * cap);
+    if (pos < 0) return (int)pos;
+    out_k[sd] = m + 1;
+  }
+  return TPE_OK;
 }
 
 int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
@@ -342,13 +392,42 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         std::vector<double> a((size_t)k), c((size_t)k);
         const double pa = logf ? 1.0 : p_accept(w, mu, sg, k, bounded, L.low, L.high);
         double shift = -INFINITY;
-        for (int64_t i = 0; i < k; ++i) {
-          const double se = np_max(sg[i], kEPS);
-          const double arg = logf ? w[i] / (se * sqrt(2 * M_PI)) : w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa;
-          c[i] = f64 ? log(arg) * kLog2e : fast_log2(arg);
-          a[i] = sqrt(0.5 * kLog2e) / se;
-          if (c[i] > shift && std::isfinite(c[i])) shift = c[i];
+        if (f64) {
+          for (int64_t i = 0; i < k; ++i) {
+            const double se = np_max(sg[i], kEPS);
+            const double arg = logf ? w[i] / (se * sqrt(2 * M_PI)) : w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa;
+            c[i] = log(arg) * kLog2e;
+            a[i] = sqrt(0.5 * kLog2e) / se;
+          }
+        } else {
+          // f32 tables: straight-line passes the compiler vectorises, the bit-level
+          // log2 for normal positive arguments, libm for the rest
+          double* __restrict__ cp = c.data();
+          double* __restrict__ ap = a.data();
+          const double s2pi = sqrt(2 * M_PI), as = sqrt(0.5 * kLog2e), ipa = 1.0 / pa;
+          if (logf)
+            for (int64_t i = 0; i < k; ++i) {
+              const double se = sg[i] > kEPS ? sg[i] : kEPS;
+              cp[i] = w[i] / (se * s2pi);
+              ap[i] = as / se;
+            }
+          else
+            for (int64_t i = 0; i < k; ++i) {
+              const double se = sg[i] > kEPS ? sg[i] : kEPS;
+              cp[i] = w[i] / (s2pi * fabs(sg[i])) * ipa;
+              ap[i] = as / se;
+            }
+          bool odd = false;
+          for (int64_t i = 0; i < k; ++i) odd |= !(cp[i] >= 2.2250738585072014e-308 && cp[i] <= 1.7976931348623157e308);
+          if (odd)
+            for (int64_t i = 0; i < k; ++i)
+              cp[i] = (cp[i] >= 2.2250738585072014e-308 && cp[i] <= 1.7976931348623157e308) ? log2_normal(cp[i])
+                                                                                              : log2(cp[i]);
+          else
+            for (int64_t i = 0; i < k; ++i) cp[i] = log2_normal(cp[i]);
         }
+        for (int64_t i = 0; i < k; ++i)
+          if (c[i] > shift && std::isfinite(c[i])) shift = c[i];
         if (!std::isfinite(shift)) shift = 0;
         for (int64_t i = 0; i < k; ++i) c[i] -= shift;
         base = shift * kLn2;
@@ -363,11 +442,17 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         // pruning (above side, f32): widest components listed apart, grid over mu
         std::vector<int64_t> wide;
         if (side == 1 && k > kPruneMinK) {
-          std::vector<int64_t> idx((size_t)k);
-          for (int64_t i = 0; i < k; ++i) idx[i] = i;
-          std::partial_sort(idx.begin(), idx.begin() + kPruneWide, idx.end(),
-                            [&](int64_t x, int64_t y) { return a[x] < a[y] || (a[x] == a[y] && x < y); });
-          wide.assign(idx.begin(), idx.begin() + kPruneWide);
+          // the kPruneWide smallest a (widest sigma), ascending by (a, index): one
+          // pass with a small insertion-sorted buffer (= a stable argsort prefix)
+          int64_t best[kPruneWide];
+          int nb = 0;
+          for (int64_t i = 0; i < k; ++i) {
+            if (nb == kPruneWide && !(a[i] < a[best[nb - 1]])) continue;   // ties keep the lower index
+            int q = nb < kPruneWide ? nb++ : nb - 1;
+            while (q > 0 && a[i] < a[best[q - 1]]) { best[q] = best[q - 1]; --q; }
+            best[q] = i;
+          }
+          wide.assign(best, best + nb);
         }
         off = (int32_t)(comp32.size() / 4); len = (int32_t)k;
         {
@@ -401,13 +486,29 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           const float inv = hi > lo ? (float)((double)G / (hi - lo)) : 0.f;
           p.grid_off = (int32_t)grid.size(); p.grid_n = (int32_t)G;
           p.grid_lo = (float)lo; p.grid_inv = inv;
-          int64_t j = 0;
-          for (int64_t g = 0; g < G; ++g) {
-            const double edge = inv > 0 ? lo + (double)g / (double)inv : lo;
-            while (j < k && (double)(float)mu[j] < edge) ++j;     // searchsorted left
-            grid.push_back((int32_t)(inv > 0 ? j : 0));
+          // grid[g] = first component with mu32 >= edge_g, edge_g = lo + g * (1 / inv)
+          // = #components whose first bucket with edge > mu32 is <= g: a counting
+          // pass (bucket estimate + exact edge correction) and a prefix sum —
+          // no data-dependent branches in the merge
+          const double step = inv > 0 ? 1.0 / (double)inv : 0.0;
+          const size_t g0 = grid.size();
+          grid.resize(g0 + (size_t)G + 1, 0);
+          int32_t* __restrict__ gp = grid.data() + g0;
+          if (inv > 0) {
+            std::vector<int32_t> hist((size_t)G + 1, 0);
+            const double dinv = (double)inv;
+            for (int64_t i = 0; i < k; ++i) {
+              const double x = (double)(float)mu[i];
+              int64_t g = (int64_t)((x - lo) * dinv) + 1;     // first bucket with edge > x, estimated
+              g = g < 0 ? 0 : (g > G ? G : g);
+              while (g > 0 && lo + (double)(g - 1) * step > x) --g;
+              while (g < G && !(lo + (double)g * step > x)) ++g;
+              ++hist[(size_t)g];
+            }
+            int32_t acc = 0;
+            for (int64_t g = 0; g < G; ++g) { acc += hist[(size_t)g]; gp[g] = acc; }
           }
-          grid.push_back((int32_t)k);
+          gp[G] = (int32_t)k;
         }
       }
     }

@@ -309,39 +309,39 @@ class Engine(object):
     # ---------------------------------------------------------------- pack
     @staticmethod
     def _labels(problems):
-        """tpe_label_in array of one level (plus the arrays it points into,
-        which the caller keeps alive for the native call)."""
+        """tpe_label_in array of one level (LABEL_DTYPE records; returns its
+        address) plus the arrays it points into, which the caller keeps alive
+        for the native call.  One tuple assignment per label."""
         n = len(problems)
-        labels = (N.LabelIn * max(n, 1))()
-        keep = []
+        recs = np.zeros(max(n, 1), dtype=N.LABEL_DTYPE)
+        keep = [recs]
         for i, lp in enumerate(problems):
-            post, L = lp.post, labels[i]
-            L.family, L.upper, L.label_ix = post.family, int(post.upper), lp.label_ix
-            L.flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)
-            L.low = post.low if post.low is not None else 0.0
-            L.high = post.high if post.high is not None else 0.0
-            L.q = post.q if post.q is not None else 0.0
+            post = lp.post
+            flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)
+            bw = [np.ascontiguousarray(a, dtype=np.float64) for a in post.below]
+            ids = np.ascontiguousarray(lp.ids, dtype=np.int64)
+            keep.append(bw)
+            keep.append(ids)
+            bptr = [a.ctypes.data for a in bw] + [0] * (3 - len(bw))
             if post.above_dev is not None:
                 col, n_obs, bidx = post.above_dev
                 bidx = np.ascontiguousarray(bidx, dtype=np.int32)
                 keep.append(bidx)
-                L.above_w = L.above_mu = L.above_sigma = None
-                L.above_k = n_obs - len(bidx) + 1
-                L.dev_obs, L.n_obs = col.data_ptr(), n_obs
-                L.below_idx, L.n_below = bidx.ctypes.data, len(bidx)
-                L.prior_mu, L.prior_sigma, L.prior_weight, L.lf = post.prior
-            for side in (('below',) if post.above_dev is not None else ('below', 'above')):
-                arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in getattr(post, side)]
-                keep.append(arrs)
-                setattr(L, side + '_w', arrs[0].ctypes.data)
-                if len(arrs) == 3:
-                    setattr(L, side + '_mu', arrs[1].ctypes.data)
-                    setattr(L, side + '_sigma', arrs[2].ctypes.data)
-                setattr(L, side + '_k', len(arrs[0]))
-            ids = np.ascontiguousarray(lp.ids, dtype=np.int64)
-            keep.append(ids)
-            L.ids, L.n_ids = ids.ctypes.data, len(ids)
-        return labels, keep
+                aptr, ak = [0, 0, 0], n_obs - len(bidx) + 1
+                dev = (col.data_ptr(), n_obs, bidx.ctypes.data, len(bidx))
+                prior = post.prior
+            else:
+                aw = [np.ascontiguousarray(a, dtype=np.float64) for a in post.above]
+                keep.append(aw)
+                aptr, ak = [a.ctypes.data for a in aw] + [0] * (3 - len(aw)), len(aw[0])
+                dev, prior = (0, 0, 0, 0), (0.0, 0.0, 0.0, 0)
+            recs[i] = (post.family, flags, int(post.upper), lp.label_ix,
+                       post.low if post.low is not None else 0.0, post.high if post.high is not None else 0.0,
+                       post.q if post.q is not None else 0.0,
+                       bptr[0], bptr[1], bptr[2], len(bw[0]), aptr[0], aptr[1], aptr[2], ak,
+                       ids.ctypes.data, len(ids), dev[0], dev[1], dev[2], dev[3], prior[3],
+                       prior[0], prior[1], prior[2])
+        return recs.ctypes.data, keep
 
     def _pack(self, problems, n_cand, seed, cand_base, n_cand_global):
         """Pack one level with the native host runtime straight into the pinned

@@ -26,12 +26,19 @@ class History(object):
     label the (tid, value) observations in tid order.  ``dev`` holds the
     device copies of the observation columns (devhist.DeviceColumns per
     device); it lives as long as the append-only source it mirrors."""
-    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs')
+    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache')
 
-    def __init__(self, tids, losses, obs, dev=None, sorted_obs=True):
+    def __init__(self, tids, losses, obs, dev=None, sorted_obs=True, cache=None):
         self.tids, self.losses, self.obs = tids, losses, obs
         self.dev = {} if dev is None else dev
         self.sorted_obs = sorted_obs     # every label's observation tids ascending
+        self._cache = cache
+
+    def value_order(self, label):
+        """A permutation sorting the label's (float) observation values
+        ascending, kept incrementally by the Trials cache; None without the
+        cache or when a value is NaN."""
+        return None if self._cache is None else self._cache.value_order(label)
 
     def __len__(self):
         return len(self.tids)
@@ -60,11 +67,12 @@ class _Cache(object):
         self.tids = _Grow(np.int64)
         self.losses = _Grow(np.float64)
         self.pending = []              # positions whose loss may still change
-        self.obs_pos = {k: _Grow(np.int64) for k in labels}
+        self.obs_tid = {k: _Grow(np.int64) for k in labels}     # tid of each observation (append-only)
         self.obs_val = {k: _Grow(np.int64 if categorical[k] else np.float64) for k in labels}
         self.labels = labels
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
+        self.orders = {}               # label -> value-sorting permutation of its observations
 
     def extend(self, docs, start):
         for i in range(start, len(docs)):
@@ -88,8 +96,29 @@ class _Cache(object):
             for k in self.labels:
                 v = vals.get(k)
                 if v:
-                    self.obs_pos[k].append(self.tids.n - 1)
+                    self.obs_tid[k].append(tid)
                     self.obs_val[k].append(v[0])
+
+    def value_order(self, k):
+        """Sorting permutation of obs_val[k], extended by a merge of the
+        observations appended since the last call (O(n) per suggest instead of
+        a sort).  Any sort of a column without repeated values is the one
+        np.argsort gives; the fit checks each side for repeats itself."""
+        vals = self.obs_val[k].view()
+        n = len(vals)
+        perm = self.orders.get(k)
+        if perm is None:
+            perm = np.argsort(vals, kind='stable')
+        elif len(perm) < n:
+            new = np.arange(len(perm), n)
+            nv = vals[new]
+            o = np.argsort(nv, kind='stable')
+            at = np.searchsorted(vals[perm], nv[o], side='right')
+            perm = np.insert(perm, at, new[o])
+        self.orders[k] = perm
+        if n and np.isnan(vals[perm[-1]]):       # NaN sorts last
+            return None
+        return perm
 
     def refresh_pending(self):
         if not self.pending:
@@ -161,11 +190,8 @@ def extract(domain, trials):
     _CACHES[trials] = cache
     cache.refresh_pending()
     tids = cache.tids.view()
-    obs = {}
-    for k in labels:
-        pos = cache.obs_pos[k].view()
-        obs[k] = (tids[pos], cache.obs_val[k].view())
-    return History(tids, cache.losses.view(), obs, dev=cache.dev)
+    obs = dict((k, (cache.obs_tid[k].view(), cache.obs_val[k].view())) for k in labels)
+    return History(tids, cache.losses.view(), obs, dev=cache.dev, cache=cache)
 
 
 def split_below(history, gamma, gamma_cap=25):

@@ -224,6 +224,56 @@ def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT
     return Posterior(dist, family, low, high, q, below, above)
 
 
+def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.0, lf=DEFAULT_LF):
+    """Continuous (non-quantized) label: the below/above split
+    (ap_filter_trials, tpe.py:613-641) and both Parzen fits in one native call
+    (tpe_host_fit_split), each side sorted by filtering ``order`` (a sorting
+    permutation of all the label's values, History.value_order).  A side whose
+    values repeat is refitted here with numpy's argsort permutation (the
+    reference's tie order), so the result equals fit_posterior's bit for bit.
+    ``below_tids`` ascending, ``obs_tids`` strictly ascending."""
+    family = _FAMILY[dist]
+    if family not in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
+        raise ValueError('fit_split fits continuous families only, not %r' % dist)
+    a = args
+    low = high = None
+    if dist in ('uniform', 'loguniform'):
+        low, high = float(a['low']), float(a['high'])
+        pmu, psig = 0.5 * (a['high'] + a['low']), 1.0 * (a['high'] - a['low'])
+    else:
+        pmu, psig = a['mu'], a['sigma']
+    x = np.ascontiguousarray(obs_vals, dtype=np.float64)
+    if family == N.FAM_LOGGAUSS:
+        x = np.log(x)                                     # monotone: `order` still sorts x
+    tids = np.ascontiguousarray(obs_tids, dtype=np.int64)
+    order = np.ascontiguousarray(order, dtype=np.int64)
+    bt = np.ascontiguousarray(below_tids, dtype=np.int64)
+    n = len(x)
+    if len(order) != n:
+        raise ValueError('order has %d entries for %d observations' % (len(order), n))
+    cap = n + 1
+    out = np.empty(6 * cap)
+    k = np.zeros(2, dtype=np.int64)
+    rc = N.load().tpe_host_fit_split(x.ctypes.data, tids.ctypes.data, order.ctypes.data, n, bt.ctypes.data,
+                                     len(bt), float(prior_weight), float(pmu), float(psig), int(lf or 0),
+                                     out.ctypes.data, k.ctypes.data)
+    if rc != 0:
+        raise AssertionError('tpe_host_fit_split failed (%d): tids not strictly ascending, a bad order, or a '
+                             'non-positive Parzen bandwidth (prior_sigma=%r)' % (rc, psig))
+    sides = []
+    mask = None
+    for sd in range(2):
+        m = int(k[sd])
+        if m:
+            r = out[3 * sd * cap:]
+            sides.append((r[:m], r[cap:cap + m], r[2 * cap:2 * cap + m]))
+            continue
+        if mask is None:
+            mask = np.isin(tids, bt)
+        sides.append(fit_parzen(x[mask] if sd == 0 else x[~mask], prior_weight, pmu, psig, lf))
+    return Posterior(dist, family, low, high, None, sides[0], sides[1])
+
+
 # --------------------------------------------------------------------------
 # device tables (layout documented in include/tpe_hip.h)
 # --------------------------------------------------------------------------
@@ -331,7 +381,7 @@ def prune_tables(mu, a, c):
     lo, hi = float(mu32[0]), float(mu32[-1])
     G = int(min(4096, 4 * K))
     inv = np.float32(G / (hi - lo)) if hi > lo else np.float32(0.0)
-    edges = lo + np.arange(G, dtype=np.float64) / (float(inv) if inv > 0 else 1.0)
+    edges = lo + np.arange(G, dtype=np.float64) * (1.0 / float(inv) if inv > 0 else 0.0)
     grid = np.empty(G + 1, dtype=np.int32)
     grid[:G] = np.searchsorted(mu32, edges, side='left') if inv > 0 else 0
     grid[G] = K

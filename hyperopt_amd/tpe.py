@@ -43,7 +43,7 @@ from . import history as _history
 from . import rand
 from . import replay
 from .engine import LevelProblem, get_engine
-from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, fit_posterior
+from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, fit_posterior, fit_split
 
 logger = logging.getLogger(__name__)
 
@@ -63,20 +63,35 @@ class _Fits(object):
         self.table, self.hist = table, hist
         self.below_tids, self.prior_weight = below_tids, prior_weight
         self.engine = engine
+        self.below_sorted = None
         self.cache = {}
 
     def get(self, row):
         post = self.cache.get(row.label)
         if post is None:
             otids, ovals = self.hist.obs[row.label]
-            bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
             eng = self.engine
-            if (eng is not None and eng.precision == 'fp32' and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES
-                    and len(ovals) - len(bidx) >= max(eng.device_fit_min, 64)):
-                col = devhist.columns(self.hist, eng.device).column(row.label, ovals)
-                post = fit_posterior(row.dist, row.args, ovals[bidx], None, self.prior_weight, DEFAULT_LF,
-                                     above_dev=(col, len(ovals), bidx))
+            f32 = eng is not None and eng.precision == 'fp32'
+            bidx = None
+            if (f32 and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES
+                    and len(ovals) >= max(eng.device_fit_min, 64)):
+                bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
+                if len(ovals) - len(bidx) >= max(eng.device_fit_min, 64):
+                    col = devhist.columns(self.hist, eng.device).column(row.label, ovals)
+                    post = fit_posterior(row.dist, row.args, ovals[bidx], None, self.prior_weight, DEFAULT_LF,
+                                         above_dev=(col, len(ovals), bidx))
+            if post is not None:
+                pass
+            elif (f32 and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and self.hist.sorted_obs
+                  and self.hist.value_order(row.label) is not None):
+                # fp32 device path: split + both fits in one native call
+                if self.below_sorted is None:
+                    self.below_sorted = np.sort(np.asarray(self.below_tids, dtype=np.int64))
+                post = fit_split(row.dist, row.args, otids, ovals, self.below_sorted,
+                                 self.hist.value_order(row.label), self.prior_weight, DEFAULT_LF)
             else:
+                if bidx is None:
+                    bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
                 m = np.zeros(len(ovals), dtype=bool)
                 m[bidx] = True
                 post = fit_posterior(row.dist, row.args, ovals[m], ovals[~m], self.prior_weight, DEFAULT_LF)

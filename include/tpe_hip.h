@@ -331,6 +331,20 @@ typedef struct tpe_pack_info {
 int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, double prior_weight,
                             double prior_mu, double prior_sigma, int32_t lf, double* w, double* mu, double* sigma);
 
+/* ap_filter_trials + adaptive_parzen_normal of both sides of one continuous
+ * label (tpe.py:613-641, 398-475, 485-568).  x: the label's (transformed)
+ * observations, tids strictly ascending; order: a permutation sorting x
+ * ascending (the history keeps it incrementally); below_tids ascending.  Each
+ * side's permutation is `order` filtered to that side — the permutation
+ * np.argsort gives when no value of the side repeats; a side with repeated
+ * values or NaN is NOT fitted (out_k[side] = 0): np.argsort's tie order
+ * decides its weights, so the caller fits it with tpe_host_fit_parzen and
+ * numpy's permutation.  out: 6 rows of n + 1 doubles — below w, mu, sigma,
+ * above w, mu, sigma; out_k[0] / out_k[1] = below / above component counts. */
+int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* order, int64_t n,
+                       const int64_t* below_tids, int64_t n_bt, double prior_weight, double prior_mu,
+                       double prior_sigma, int32_t lf, double* out, int64_t* out_k);
+
 /* categorical posterior (tpe.py:573-607): p_prior NULL = randint pseudo-counts,
  * else pchoice's counts + upper * prior_weight * p_prior */
 int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,

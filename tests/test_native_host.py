@@ -43,6 +43,58 @@ def test_native_cat_probs_match_numpy_bit_exact():
         parzen._cat_probs('randint', dict(upper=3), np.array([0, 3]), 1.0, 25)
 
 
+@pytest.mark.parametrize('dist,args', [
+    ('uniform', dict(low=-3.0, high=3.0)),
+    ('normal', dict(mu=0.5, sigma=2.0)),
+    ('loguniform', dict(low=-4.0, high=2.0)),
+    ('lognormal', dict(mu=0.0, sigma=1.0)),
+])
+def test_fit_split_matches_fit_posterior(dist, args):
+    """tpe_host_fit_split (merge split + the label's sorting permutation
+    filtered per side + fit) against the masked fit_posterior path, bit-exact;
+    sides with repeated values take numpy's permutation."""
+    rs = np.random.RandomState(3)
+    for n in (0, 1, 2, 25, 26, 300, 3000):
+        tids = np.sort(rs.choice(4 * n + 10, n, replace=False)).astype(np.int64)
+        for ties in (False, True):
+            v = rs.uniform(-3, 3, n)
+            if ties:
+                v = np.round(v * 2) / 2
+            vals = np.exp(v) if dist in ('loguniform', 'lognormal') else v
+            order = np.argsort(vals, kind='stable')
+            for nb in (0, 1, min(n, 25)):
+                below = rs.permutation(tids)[:nb]
+                a = parzen.fit_split(dist, args, tids, vals, np.sort(below), order, 1.0, 25)
+                m = np.isin(tids, below)
+                b = parzen.fit_posterior(dist, args, vals[m], vals[~m], 1.0, 25)
+                assert (a.family, a.low, a.high, a.q) == (b.family, b.low, b.high, b.q)
+                for sa, sb in ((a.below, b.below), (a.above, b.above)):
+                    for x, y in zip(sa, sb):
+                        np.testing.assert_array_equal(x, y)
+    with pytest.raises(AssertionError):
+        parzen.fit_split(dist, args, np.array([2, 1]), np.array([0.5, 0.7]), np.zeros(0, np.int64), np.array([0, 1]))
+    with pytest.raises(AssertionError):
+        parzen.fit_split(dist, args, np.array([1, 2]), np.array([0.5, 0.7]), np.zeros(0, np.int64), np.array([0, 2]))
+
+
+def test_value_order_incremental():
+    """The Trials cache's per-label sorting permutation, extended by merges as
+    documents arrive, always sorts the column (and is None with a NaN)."""
+    from hyperopt_amd import history as H
+    c = H._Cache(['x'], {'x': False})
+    rs = np.random.RandomState(5)
+    col = c.obs_val['x']
+    for step in range(40):
+        for _ in range(rs.randint(0, 7)):
+            col.append(rs.uniform() if rs.rand() > 0.2 else 0.5)
+        vals = col.view()
+        perm = c.value_order('x')
+        assert sorted(perm.tolist()) == list(range(len(vals)))
+        assert np.all(np.diff(vals[perm]) >= 0)
+    col.append(np.nan)
+    assert c.value_order('x') is None
+
+
 def _engine(precision):
     e = Engine.__new__(Engine)
     e.lib, e.tile, e.precision, e._pinned, e._bufs, e.profile = N.load(), 2048, precision, None, {}, None
