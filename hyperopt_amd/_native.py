@@ -10,20 +10,20 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libtpe_hip.so')
-ABI_VERSION = 5
+LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
+ABI_VERSION = 6
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH = 1, 2
-BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE = 1, 2, 4
+BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS = 1, 2, 4, 8
 PREC_F32, PREC_F64 = 0, 1
 
 # numpy mirrors of the C structs (the host builds arrays of them and copies
 # them to device memory in one transfer)
 PROBLEM_DTYPE = np.dtype([
     ('family', '<i4'), ('flags', '<i4'), ('n_cand', '<i4'), ('n_upper', '<i4'),
-    ('cand_off', '<i8'), ('cand_base', '<i8'), ('reserved64', '<i8'),
+    ('cand_off', '<i8'), ('cand_base', '<i8'), ('n_cand_global', '<i8'),
     ('n_splits', '<i4'), ('tile_off', '<i4'), ('n_tiles', '<i4'), ('samp_off', '<i4'),
     ('samp_len', '<i4'), ('below_off', '<i4'), ('below_len', '<i4'), ('above_off', '<i4'),
     ('above_len', '<i4'), ('wide_off', '<i4'), ('wide_len', '<i4'), ('grid_off', '<i4'),
@@ -76,6 +76,8 @@ class Batch(ctypes.Structure):
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
         ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64), ('fit_max_seg', ctypes.c_int64),
+        ('draw_pref', ctypes.c_void_p), ('draw_blocks', ctypes.c_int64), ('n_sorted', ctypes.c_int32),
+        ('reserved5', ctypes.c_int32),
     ]
 
 
@@ -123,6 +125,7 @@ class PackInfo(ctypes.Structure):
         ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
         ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_seg', ctypes.c_int64),
+        ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64),
     ]
 
 
@@ -141,13 +144,15 @@ class LevelWS(ctypes.Structure):
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p), ('fit_cap', ctypes.c_int64),
         ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_int64),
+        ('draw_pref', ctypes.c_void_p), ('draw_pref_cap', ctypes.c_int64),
     ]
 
 
 class LevelNeed(ctypes.Structure):
     """tpe_level_need: sizes one level needs."""
     _fields_ = [(k, ctypes.c_int64) for k in ('pinned_bytes', 'blob_bytes', 'cand', 'sort_tmp_bytes', 'part',
-                                              'best', 'result', 'fit', 'fit_tmp_bytes')]
+                                              'best', 'result', 'fit', 'fit_tmp_bytes',
+                                              'draw_pref')]
 
 
 E_SPACE = -4

@@ -10,22 +10,25 @@ OUT = os.path.join(HERE, 'libtpe_hip.so')
 ARCH = os.environ.get('TPE_OFFLOAD_ARCH', 'gfx950')
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, out=OUT, defines=()):
     """hipcc the kernels, g++ the host runtime (-ffp-contract=off: numpy float64
-    semantics), link both into hyperopt_amd/libtpe_hip.so."""
+    semantics), link both into hyperopt_amd/libtpe_hip.so (or `out`, with extra
+    -D `defines` on the kernels: A/B variants for tools/)."""
+    OUT = out
     deps = [SRC, HOST_SRC, os.path.join(HERE, '..', 'include', 'tpe_hip.h')]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
     gxx = os.environ.get('CXX', 'g++')
     tmp = OUT + '.tmp'
+    tag = os.path.splitext(os.path.basename(OUT))[0]
     host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
-    dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o')
+    dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o' if not defines else tag + '.o')
     cmds = [
         [gxx, '-O3', '-march=x86-64-v3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall',
          '-c', HOST_SRC, '-o', host_o],
         [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
-         '-Wno-unused-command-line-argument', '-c', SRC, '-o', dev_o],
+         '-Wno-unused-command-line-argument'] + ['-D' + d for d in defines] + ['-c', SRC, '-o', dev_o],
         [hipcc, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-Wno-unused-command-line-argument', '-o', tmp,
          dev_o, host_o],
     ]

@@ -559,6 +559,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
   std::vector<tpe_problem> prob((size_t)P);
   int64_t scored = 0;
+  const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
   {
     int64_t r = 0, s_next = 0, u_next = S * (int64_t)n_cand;
     int32_t slot = 0;
@@ -571,6 +572,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         next += n_cand;
         q.sort_slot = pruned[li] ? slot++ : -1;
         q.cand_base = cand_base;
+        q.n_cand_global = C_ref;
         q.key0 = (uint32_t)seed; q.key1 = (uint32_t)(seed >> 32);
         q.ctr2 = (uint32_t)labels[li].label_ix;
         q.ctr3 = (uint32_t)labels[li].ids[j];
@@ -586,7 +588,6 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // with many tiles: the bulk is cheap (local expansion), so one split, and the
   // outermost tiles of the (local) sorted range — the sparse tails, whose waves
   // span wide windows evaluated exactly — get geometrically more.
-  const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
   const int64_t tiles_ref = (C_ref + T - 1) / T;
   const int64_t scored_tiles = scored * tiles_ref;
   const int64_t target = std::max<int64_t>(1, (target_work() + std::max<int64_t>(scored_tiles, 1) - 1) /
@@ -688,6 +689,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->fit_total = fit_seg.back();
   info->copy_end = off[9] + len[9];
   info->sort_count = S * (int64_t)n_cand;
+  info->n_sorted = S;
+  info->draw_blocks = (C_ref + 1 + 63) / 64;
   info->copy2_len = len[10];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;

@@ -85,7 +85,8 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
 }
 
 // open-interval uniforms
-__device__ __forceinline__ float u01f(uint32_t r) { return ((float)(r >> 8) + 0.5f) * 5.9604644775390625e-08f; }
+// 23-bit float uniform in [2^-24, 1 - 2^-24]: (k + 0.5) is exact, so never 0 or 1
+__device__ __forceinline__ float u01f(uint32_t r) { return ((float)(r >> 9) + 0.5f) * 1.1920928955078125e-07f; }
 __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
   const uint64_t m = ((uint64_t)a << 21) ^ (uint64_t)(b >> 11);   // 53 bits
   return ((double)m + 0.5) * 1.1102230246251565e-16;
@@ -249,32 +250,24 @@ __device__ __forceinline__ int draw_category(const tpe_problem& p, const double*
   return a;
 }
 
-// Candidate i of problem p (Philox-4x32-10 counter = its GLOBAL index): the value
-// x returned to the user and the kernel coordinate t (x, ln x before
-// quantisation for log families, the category for categorical).  `cum` is the
-// selection CDF (LDS copy or the table itself, stride `cs`).  k_select calls it
-// again for the winner, so the value never has to be stored.
-__device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __restrict__ S,
-                                         const double* __restrict__ cum, int cs, int64_t i, int precision,
-                                         float lo_f, float hi_f, double& x, float& t, int& comp) {
-  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-  // component choice: first k with u < cum_k (binary search, <= 27 rows)
-  const double u1 = u01d(r.x, r.y);
+// first component k with u < cum_k (binary search; cum stride cs)
+__device__ __forceinline__ int find_comp(const tpe_problem& p, const double* __restrict__ cum, int cs, double u) {
   int a = 0, b = p.samp_len - 1;
-  while (a < b) { const int m = (a + b) >> 1; if (u1 < cum[cs * m]) b = m; else a = m + 1; }
-  comp = a;
-  if (p.family == TPE_FAM_CATEGORICAL) {
-    x = (double)a;
-    t = (float)a;
-    return;
-  }
+  while (a < b) { const int m = (a + b) >> 1; if (u < cum[cs * m]) b = m; else a = m + 1; }
+  return a;
+}
+
+// Value x and kernel coordinate t (x, or ln x before quantisation for log
+// families) of a draw from component a of the below mixture, by inversion of its
+// truncated normal at the uniform uf (f32) / ud (f64).
+__device__ __forceinline__ void draw_comp(const tpe_problem& p, const double* __restrict__ S, int a, float uf,
+                                          double ud, int precision, float lo_f, float hi_f, double& x, float& t) {
   const double* s = S + 8 * a;
   // truncated normal by inversion; fa, fb = Phi of the (mirrored) bounds
   const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
   const bool flip = s[5] != 0.0;
   if (precision == TPE_PREC_F32) {
-    const float pr = (float)fa + u01f(r.z) * ((float)fb - (float)fa);
+    const float pr = (float)fa + uf * ((float)fb - (float)fa);
     float z = -1.41421356237309505f * erfcinvf(2.f * pr);
     if (flip) z = -z;
     float xf = (float)mu + (float)sg * z;
@@ -283,7 +276,7 @@ __device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __r
     t = xf;
     x = (double)xf;
   } else {
-    const double pr = fa + u01d(r.z, r.w) * (fb - fa);
+    const double pr = fa + ud * (fb - fa);
     double z = -1.41421356237309505 * erfcinv(2.0 * pr);
     if (flip) z = -z;
     x = mu + sg * z;
@@ -294,6 +287,96 @@ __device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __r
   }
   if (p.family == TPE_FAM_LOGGAUSS || p.family == TPE_FAM_QLOGGAUSS) x = exp(x);
   if (p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS) x = rint(x / p.q) * p.q;   // np.round
+}
+
+// Candidate i of problem p, i.i.d. (Philox-4x32-10 counter = its GLOBAL index):
+// the value x returned to the user and the kernel coordinate t (the category
+// for categorical).  `cum` is the selection CDF (LDS copy or the table itself,
+// stride `cs`).  k_select calls it again for the winner, so the value never has
+// to be stored.
+__device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __restrict__ S,
+                                         const double* __restrict__ cum, int cs, int64_t i, int precision,
+                                         float lo_f, float hi_f, double& x, float& t, int& comp) {
+  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+  const int a = find_comp(p, cum, cs, u01d(r.x, r.y));
+  comp = a;
+  if (p.family == TPE_FAM_CATEGORICAL) {
+    x = (double)a;
+    t = (float)a;
+    return;
+  }
+  draw_comp(p, S, a, u01f(r.z), u01d(r.z, r.w), precision, lo_f, hi_f, x, t);
+}
+
+// ------------------------------------------------------------ ordered draws
+// (include/tpe_hip.h "Ordered draws").  Inclusive prefix sum, in lane order,
+// of E_i = -ln u_i over the canonical 64-index block `blk` of problem p (lane l
+// <-> global index 64 blk + l; indices past the global count add 0).
+// Wave-collective, fixed (Hillis-Steele) order, and not inlined, so the sample,
+// block-sum and select kernels compute bit-identical sums.
+__device__ __attribute__((noinline)) double exp_block_scan(const tpe_problem& p, int64_t blk) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t g = (uint64_t)blk * 64 + (uint64_t)lane;
+  double e = 0.0;
+  if ((int64_t)g <= p.n_cand_global) {
+    const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+    e = -log(u01d(r.x, r.y));
+  }
+  for (int d = 1; d < 64; d <<= 1) {
+    const double o = __shfl_up(e, d);
+    if (lane >= d) e += o;
+  }
+  return e;
+}
+
+// The draw at uniform order statistic U: component by the selection CDF, then
+// the component's inverse CDF at U's relative position inside the component.
+__device__ __forceinline__ void ordered_draw(const tpe_problem& p, const double* __restrict__ S,
+                                             const double* __restrict__ cum, int cs, double U, int precision,
+                                             float lo_f, float hi_f, double& x, float& t) {
+  const int a = find_comp(p, cum, cs, U);
+  const double lo = a > 0 ? cum[cs * (a - 1)] : 0.0, hi = cum[cs * a];
+  const double w = (U - lo) / (hi - lo);
+  const double ud = fmin(fmax(w, 1.1102230246251565e-16), 1.0 - 1.1102230246251565e-16);
+  const float uf = fminf(fmaxf((float)w, 5.9604644775390625e-08f), 0.99999994f);
+  draw_comp(p, S, a, uf, ud, precision, lo_f, hi_f, x, t);
+}
+
+// per sorted problem, the sum of every canonical 64-index block (one wave each)
+__global__ __launch_bounds__(kThreads) void k_draw_sums(const tpe_problem* __restrict__ P, int64_t draw_blocks,
+                                                        double* __restrict__ pref) {
+  const int64_t per = (draw_blocks + kThreads / 64 - 1) / (kThreads / 64);
+  const tpe_problem& p = P[blockIdx.x / per];
+  if (p.sort_slot < 0 || p.samp_len <= 0) return;
+  const int64_t blk = (int64_t)(blockIdx.x % per) * (kThreads / 64) + (threadIdx.x >> 6);
+  if (blk >= draw_blocks) return;
+  const double s = exp_block_scan(p, blk);
+  if ((threadIdx.x & 63) == 63) pref[(int64_t)p.sort_slot * (draw_blocks + 1) + blk] = s;
+}
+
+// exclusive prefix of the block sums in place (fixed order: chunk sums, one
+// serial pass over them, serial chunks) and the total at [draw_blocks]
+__global__ __launch_bounds__(kThreads) void k_draw_scan(const tpe_problem* __restrict__ P, int64_t draw_blocks,
+                                                        double* __restrict__ pref) {
+  const tpe_problem& p = P[blockIdx.x];
+  if (p.sort_slot < 0 || p.samp_len <= 0) return;
+  double* row = pref + (int64_t)p.sort_slot * (draw_blocks + 1);
+  const int64_t chunk = (draw_blocks + kThreads - 1) / kThreads;
+  const int64_t b0 = min(draw_blocks, (int64_t)threadIdx.x * chunk), b1 = min(draw_blocks, b0 + chunk);
+  double acc = 0.0;
+  for (int64_t b = b0; b < b1; ++b) acc += row[b];
+  __shared__ double part[kThreads];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double run = 0.0;
+    for (int q = 0; q < kThreads; ++q) { const double v = part[q]; part[q] = run; run += v; }
+    row[draw_blocks] = run;
+  }
+  __syncthreads();
+  double run = part[threadIdx.x];
+  for (int64_t b = b0; b < b1; ++b) { const double v = row[b]; row[b] = run; run += v; }
 }
 
 // block argmax of (score, original index) into one tile_best slot; the lane
@@ -336,7 +419,9 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      uint64_t* __restrict__ vals_sorted,
                                                      tpe_best* __restrict__ tile_best,
                                                      double* __restrict__ l_out, double* __restrict__ g_out,
-                                                     int precision, int draw, int key_bits, int flags) {
+                                                     int precision, int draw, int key_bits, int flags,
+                                                     const double* __restrict__ draw_pref, int64_t draw_blocks,
+                                                     int ordered) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   const bool store_x = (flags & TPE_BATCH_WRITE_CAND) || precision == TPE_PREC_F64 ||
@@ -398,12 +483,40 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     }
     return;
   }
+  // ordered draws of a sorted problem: no sort follows, candidates go straight
+  // to their final place
+  const bool od = ordered && draw && p.sort_slot >= 0;
+  double Sg = 0.0;                         // E_0 + .. + E_g of this candidate
+  if (od && p.samp_len > 0) {
+    // whole waves: the block scans are wave-collective
+    const int wbase = tl.cand_start + (int)blockIdx.y * kThreads + (int)(threadIdx.x & ~63);
+    if (wbase >= p.n_cand) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t g0 = p.cand_base + wbase;
+    const int64_t blk = g0 >> 6;
+    const int off = (int)(g0 & 63);
+    const double* row = draw_pref + (int64_t)p.sort_slot * (draw_blocks + 1);
+    const double sa = exp_block_scan(p, blk);
+    if (off == 0) {
+      Sg = row[blk] + sa;
+    } else {                               // the wave straddles two canonical blocks
+      const double sb = exp_block_scan(p, blk + 1);
+      const int src = (off + lane) & 63;
+      const double a = __shfl(sa, src), bq = __shfl(sb, src);
+      Sg = off + lane < 64 ? row[blk] + a : row[blk + 1] + bq;
+    }
+    Sg /= row[draw_blocks];                // U_g
+  }
   if (!valid) return;
   float t;                                 // kernel coordinate of the candidate
   if (!draw) {
     t = coord[o];
   } else if (p.samp_len <= 0) {
     cand[o] = NAN; t = NAN;
+  } else if (od) {
+    double x;
+    ordered_draw(p, S, in_lds ? cum_lds : S, in_lds ? 1 : 8, Sg, precision, lo_f, hi_f, x, t);
+    if (store_x) cand[o] = x;
   } else {
     double x;
     int c;
@@ -411,7 +524,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
     if (store_x) cand[o] = x;
   }
   const uint64_t v = ((uint64_t)o << 32) | (uint64_t)__float_as_uint(t);
-  if (p.sort_slot >= 0) {
+  if (p.sort_slot >= 0 && !od) {
     // sort key: (sorted problem, value bucket) — only locality matters for pruning
     const float gb = floorf((t - p.key_lo) * p.key_inv);
     const uint32_t bucket = gb > 0.f ? (uint32_t)fminf(gb, kmax) : 0u;
@@ -487,10 +600,28 @@ __device__ __forceinline__ int expand_range(const float4* __restrict__ C, int kb
     }
     unsigned long long rest = __ballot(live && !expand);
     n_exact += __popcll(rest);
-    while (rest) {
-      const int bl = __builtin_ctzll(rest);
-      rest &= rest - 1;
-      ce_step(readlane4(c, bl), t2, s2);
+#ifndef TPE_EXACT_CHUNK_ACC
+#define TPE_EXACT_CHUNK_ACC 1
+#endif
+    if (!TPE_EXACT_CHUNK_ACC) {
+      while (rest) {
+        const int bl = __builtin_ctzll(rest);
+        rest &= rest - 1;
+        ce_step(readlane4(c, bl), t2, s2);
+      }
+    } else if (rest) {
+      // this chunk's exact terms summed on their own, then added: small terms
+      // are not rounded away one by one against a large running sum
+      f2 acc[kR / 2];
+#pragma unroll
+      for (int j = 0; j < kR / 2; ++j) acc[j] = f2{0.f, 0.f};
+      while (rest) {
+        const int bl = __builtin_ctzll(rest);
+        rest &= rest - 1;
+        ce_step(readlane4(c, bl), t2, acc);
+      }
+#pragma unroll
+      for (int j = 0; j < kR / 2; ++j) s2[j] += acc[j];
     }
   }
   return n_exact;
@@ -531,7 +662,10 @@ __device__ __forceinline__ void below_sum(const float4* __restrict__ B, int n, f
   add_moments(M, t0, h, t2, sb2);
 }
 
-__global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __restrict__ P,
+#ifndef TPE_ABOVE_WAVES_PER_EU
+#define TPE_ABOVE_WAVES_PER_EU 5   // <= 96 VGPRs: 5 waves per SIMD
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(TPE_ABOVE_WAVES_PER_EU))) void k_above_f32(const tpe_problem* __restrict__ P,
                                                         const tpe_tile* __restrict__ tiles,
                                                         const tpe_work* __restrict__ W,
                                                         const float4* __restrict__ comp,
@@ -601,8 +735,16 @@ __global__ __launch_bounds__(kThreads) void k_above_f32(const tpe_problem* __res
     n_expanded = (long long)(k_hi - k_lo) + wide_len - n_exact;
     add_moments(M, t0, h, t2, s2);
   } else {
+    for (int kb = k_lo; kb < k_hi; kb += 64) {      // 64-component chunks, as in expand_range
+      f2 acc[kR / 2];
+#pragma unroll
+      for (int j = 0; j < kR / 2; ++j) acc[j] = f2{0.f, 0.f};
+      const int ke = min(kb + 64, k_hi);
 #pragma unroll 4
-    for (int k = k_lo; k < k_hi; ++k) ce_step(C[k], t2, s2);
+      for (int k = kb; k < ke; ++k) ce_step(C[k], t2, acc);
+#pragma unroll
+      for (int j = 0; j < kR / 2; ++j) s2[j] += acc[j];
+    }
     const float4* __restrict__ Wd = comp + p.wide_off;
     for (int k = 0; k < wide_len; ++k) ce_step(Wd[k], t2, s2);
     n_exact = (long long)(k_hi - k_lo) + wide_len;
@@ -900,7 +1042,8 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
                                                      const tpe_best* __restrict__ tile_best,
                                                      const double* __restrict__ cand,
                                                      const double* __restrict__ samp, int precision, int sampled,
-                                                     tpe_result* __restrict__ result) {
+                                                     const double* __restrict__ draw_pref, int64_t draw_blocks,
+                                                     int ordered, tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
   tpe_best b{0, 0, 0, -1};
   const int64_t nb = (int64_t)p.n_tiles * TPE_BEST_PER_TILE;
@@ -918,19 +1061,30 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
   __shared__ tpe_best wb[kSelThreads / 64];
   if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = b;
   __syncthreads();
+  if (threadIdx.x >= 64) return;
+  b = wb[0];
+  for (int q = 1; q < kSelThreads / 64; ++q)
+    if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
+  const bool redraw = b.idx >= 0 && sampled && p.samp_len > 0;   // the winner's value was never stored
+  const bool od = redraw && ordered && p.sort_slot >= 0;
+  double U = 0.0;
+  if (od) {                                // wave 0: the winner's canonical block scan
+    const int64_t g = p.cand_base + b.idx;
+    const double* row = draw_pref + (int64_t)p.sort_slot * (draw_blocks + 1);
+    const double sc = exp_block_scan(p, g >> 6);
+    U = (row[g >> 6] + __shfl(sc, (int)(g & 63))) / row[draw_blocks];
+  }
   if (threadIdx.x == 0) {
-    b = wb[0];
-    for (int q = 1; q < kSelThreads / 64; ++q)
-      if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
     tpe_result r;
     r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
     r.value = 0.0;
-    if (b.idx >= 0 && sampled && p.samp_len > 0) {   // re-draw the winner: its value was never stored
+    if (redraw) {
       float lo_f, hi_f, t;
       int c;
       f32_bounds(p, lo_f, hi_f);
       const double* S = samp + 8 * (int64_t)p.samp_off;
-      draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
+      if (od) ordered_draw(p, S, S, 8, U, precision, lo_f, hi_f, r.value, t);
+      else draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
     } else if (b.idx >= 0) {
       r.value = cand[p.cand_off + b.idx];
     }
@@ -1222,6 +1376,12 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __
   }
 }
 
+// device-drawn sorted problems at f32 draw ordered (include/tpe_hip.h "Ordered draws")
+bool ordered_draws(const tpe_batch* b) {
+  return b->sample && b->precision == TPE_PREC_F32 && (b->flags & TPE_BATCH_ORDERED_DRAWS) && b->n_sorted > 0 &&
+         b->sort_count > 0;
+}
+
 int check_batch(const tpe_batch* b) {
   if (!b) return fail(TPE_E_ARG, "null batch");
   if (b->n_problems < 0 || b->n_tiles < 0 || b->n_work_cont < 0 || b->n_work_qgauss < 0 || b->n_work_qlog < 0 ||
@@ -1250,6 +1410,9 @@ int check_batch(const tpe_batch* b) {
                        !b->fit_vals || !b->fit_vals_sorted || !b->comp32 || !b->grid || !b->problems))
     return fail(TPE_E_ARG, "null fit buffers");
   if (b->n_fit > 0 && b->precision != TPE_PREC_F32) return fail(TPE_E_ARG, "device fit needs TPE_PREC_F32");
+  if (b->n_sorted < 0 || b->draw_blocks < 0) return fail(TPE_E_ARG, "negative n_sorted/draw_blocks");
+  if (ordered_draws(b) && (!b->draw_pref || b->draw_blocks < 1))
+    return fail(TPE_E_ARG, "ordered draws need draw_pref and draw_blocks");
   return TPE_OK;
 }
 
@@ -1333,18 +1496,29 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->sample && !b->samp && b->n_tiles) return fail(TPE_E_ARG, "null sampler table");
   if (b->n_tiles == 0) return TPE_OK;
+  const bool od = ordered_draws(b);
+  if (od) {
+    const int64_t per = (b->draw_blocks + kThreads / 64 - 1) / (kThreads / 64);
+    if ((int64_t)b->n_problems * per >= ((int64_t)1 << 31)) return fail(TPE_E_ARG, "ordered-draw grid too large");
+    hipLaunchKernelGGL(k_draw_sums, dim3((unsigned)(b->n_problems * per)), dim3(kThreads), 0, (hipStream_t)stream,
+                       b->problems, b->draw_blocks, b->draw_pref);
+    hipLaunchKernelGGL(k_draw_scan, dim3(b->n_problems), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
+                       b->draw_blocks, b->draw_pref);
+    if ((rc = hip_check("tpe_sample/prefix"))) return rc;
+  }
   hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
                      b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
                      b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
-                     b->flags);
+                     b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0);
   return hip_check("tpe_sample");
 }
 
 int tpe_sort(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  // sort_end_bit == 0: no sort; the caller aliases keys_sorted/vals_sorted to keys/vals
-  if (b->n_tiles == 0 || b->sort_count == 0 || b->sort_end_bit == 0) return TPE_OK;
+  // sort_end_bit == 0: no sort; the caller aliases keys_sorted/vals_sorted to keys/vals.
+  // Ordered draws: the sample stage already wrote the final order.
+  if (b->n_tiles == 0 || b->sort_count == 0 || b->sort_end_bit == 0 || ordered_draws(b)) return TPE_OK;
   size_t sz = (size_t)b->sort_tmp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<SortConfig>(
       b->sort_tmp, sz, (const uint32_t*)b->keys, b->keys_sorted, (const uint64_t*)b->vals, b->vals_sorted,
@@ -1402,7 +1576,8 @@ int tpe_select(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_problems == 0) return TPE_OK;
   hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
-                     b->tile_best, b->cand, b->samp, b->precision, b->sample, b->result);
+                     b->tile_best, b->cand, b->samp, b->precision, b->sample, b->draw_pref, b->draw_blocks,
+                     ordered_draws(b) ? 1 : 0, b->result);
   return hip_check("tpe_select");
 }
 
@@ -1440,7 +1615,11 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   need->fit = info.fit_total;
   if (C >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 candidates in one level: shard the batch");
   uint64_t sz = 0;
-  if (info.sort_end_bit > 0 && info.sort_count > 0) {
+  // ordered draws replace the sort of the pruned problems' candidates
+  const bool od = precision == TPE_PREC_F32 && (flags & TPE_BATCH_ORDERED_DRAWS) && info.n_sorted > 0 &&
+                  info.sort_count > 0;
+  if (od) need->draw_pref = info.n_sorted * (info.draw_blocks + 1);
+  if (!od && info.sort_end_bit > 0 && info.sort_count > 0) {
     if ((rc = tpe_sort_workspace_bytes(info.sort_count, &sz))) return rc;
     need->sort_tmp_bytes = (int64_t)sz;
   }
@@ -1451,7 +1630,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   if (rc == TPE_E_SPACE || need->pinned_bytes > ws->pinned_bytes || need->blob_bytes > ws->blob_bytes ||
       need->cand > ws->cand_cap || need->part > ws->part_cap || need->best > ws->best_cap ||
       need->result > ws->result_cap || need->fit > ws->fit_cap || need->sort_tmp_bytes > ws->sort_tmp_bytes ||
-      need->fit_tmp_bytes > ws->fit_tmp_bytes)
+      need->fit_tmp_bytes > ws->fit_tmp_bytes || need->draw_pref > ws->draw_pref_cap)
     return fail(TPE_E_SPACE, "level workspace too small (see tpe_level_need)");
   if (P == 0) return TPE_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -1476,7 +1655,10 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.samp = (const double*)(dev + info.off_samp);
   b.grid = (const int32_t*)(dev + info.off_grid);
   b.cand = ws->cand; b.coord = ws->coord; b.keys = ws->keys; b.vals = ws->vals;
-  if (info.sort_end_bit > 0) {
+  if (od) {
+    b.keys_sorted = ws->keys; b.vals_sorted = ws->vals;
+    b.draw_pref = ws->draw_pref; b.draw_blocks = info.draw_blocks; b.n_sorted = (int32_t)info.n_sorted;
+  } else if (info.sort_end_bit > 0) {
     b.keys_sorted = ws->keys_sorted; b.vals_sorted = ws->vals_sorted;
     b.sort_tmp = ws->sort_tmp; b.sort_tmp_bytes = (uint64_t)ws->sort_tmp_bytes;
   } else {

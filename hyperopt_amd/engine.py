@@ -233,6 +233,7 @@ class Engine(object):
         prob['cand_off'] = np.where(pr, slot * n_cand, (S + unslot) * n_cand)
         prob['sort_slot'] = np.where(pr, slot, -1)
         prob['cand_base'] = cand_base
+        prob['n_cand_global'] = n_cand if not n_cand_global else int(n_cand_global)
         s64 = int(seed) & 0xFFFFFFFFFFFFFFFF
         prob['key0'] = s64 & 0xFFFFFFFF
         prob['key1'] = s64 >> 32
@@ -249,7 +250,7 @@ class Engine(object):
         cont = (fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)
         qg, ql = fam == N.FAM_QGAUSS, fam == N.FAM_QLOGGAUSS
         scored = cont | qg | ql
-        C_ref = n_cand if n_cand_global is None else int(n_cand_global)
+        C_ref = n_cand if not n_cand_global else int(n_cand_global)
         tiles_ref = (C_ref + T - 1) // T
         n_scored_tiles = int(scored.sum()) * tiles_ref
         target = max(1, math.ceil(TARGET_WORK / max(n_scored_tiles, 1)))
@@ -403,6 +404,7 @@ class Engine(object):
         ws.fit_vals_sorted, f4 = dev('fit_vals_sorted', 4)
         ws.fit_cap = min(f1, f2, f3, f4)
         ws.fit_tmp, ws.fit_tmp_bytes = dev('fit_tmp', 1)
+        ws.draw_pref, ws.draw_pref_cap = dev('draw_pref', 8)
         self._ws = ws
         return ws
 
@@ -422,6 +424,7 @@ class Engine(object):
                          ('fit_vals', torch.int32), ('fit_vals_sorted', torch.int32)):
             self._buf(name, need.fit, dt)
         self._buf('fit_tmp', need.fit_tmp_bytes, torch.uint8)
+        self._buf('draw_pref', need.draw_pref, torch.float64)
         self._ws = None
 
     def run_level(self, problems, n_cand, seed, cand_base=0, n_cand_global=None):
@@ -546,6 +549,10 @@ class Engine(object):
         b.l_out = d_l.data_ptr() if d_l is not None else None
         b.g_out = d_g.data_ptr() if d_g is not None else None
         b.tile_best, b.result = d_best.data_ptr(), d_res.data_ptr()
+        if info.n_sorted and not inject:
+            b.n_sorted, b.draw_blocks = info.n_sorted, info.draw_blocks
+            b.draw_pref = self._buf('draw_pref', int(info.n_sorted) * (int(info.draw_blocks) + 1),
+                                    torch.float64).data_ptr()
         if info.n_fit:
             ft = int(info.fit_total)
             d_fk = self._buf('fit_keys', ft, torch.float64)
@@ -600,7 +607,9 @@ class Engine(object):
         if b.n_fit:
             stages.append(('fit', self.lib.tpe_fit_above, None, float(b.fit_total)))
         stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
-        if b.sort_end_bit and b.sort_count:
+        ordered = (bool(b.draw_pref) and b.sample and b.precision == N.PREC_F32 and b.n_sorted > 0
+                   and (b.flags & N.BATCH_ORDERED_DRAWS))
+        if b.sort_end_bit and b.sort_count and not ordered:     # ordered draws need no sort
             # units: bytes of an LSD radix sort of (u32 key, u64 value) pairs —
             # every 8-bit pass reads and writes both arrays
             passes = (int(b.sort_end_bit) + 7) // 8

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 5
+#define TPE_ABI_VERSION 6
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -64,8 +64,10 @@ enum {
   TPE_BATCH_WRITE_CAND = 2, /* store every drawn candidate value in cand (else only where a later stage
                                reads it: quantized families and TPE_PREC_F64; the winner's value is
                                re-drawn by the select stage) */
-  TPE_BATCH_NO_FUSE = 4     /* score every continuous tile in the finalize stage (no fused finalize
+  TPE_BATCH_NO_FUSE = 4,    /* score every continuous tile in the finalize stage (no fused finalize
                                in the above kernel) */
+  TPE_BATCH_ORDERED_DRAWS = 8  /* sorted problems draw ordered candidates, no sort (else i.i.d.
+                                  draws + sort) — see "Ordered draws" below */
 };
 
 /* precision of the continuous (non-quantized) families; quantized families
@@ -103,6 +105,19 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  * [0, sort_count) of the batch; the sort key is sort_slot << key_bits | value
  * bucket.  Other problems' candidates follow and are never sorted.
  *
+ * Ordered draws (TPE_BATCH_ORDERED_DRAWS; device-drawn sorted problems at
+ * TPE_PREC_F32): instead of C i.i.d. draws that are then sorted, the
+ * sample stage draws the C order statistics of C uniforms,
+ * U_g = (E_0 + .. + E_g) / (E_0 + .. + E_Cg), E_i = -ln u_i (Philox counter =
+ * global index i), and maps each through the mixture: component k with
+ * cum_{k-1} <= U_g < cum_k, then the component's truncated-normal inverse CDF at
+ * (U_g - cum_{k-1}) / (cum_k - cum_{k-1}).  The multiset of candidates has the
+ * law of C i.i.d. mixture draws (so does its argmax); candidates come out sorted
+ * within each component, which is all the pruned kernel needs.  The prefix sums
+ * use fixed 64-index blocks of the GLOBAL index (draw_pref: per sorted problem,
+ * draw_blocks exclusive block prefixes + the total), so every shard count draws
+ * the same values bit for bit.
+ *
  * samp[k] = double[8] {cum, mu, sigma, fa, fb, flip, 0, 0}: below-mixture
  * sampler table; cum = selection CDF (∝ w_k * mass_k when bounded); fa, fb =
  * Phi of the (mirrored if flip) standardised truncation bounds; family 4 uses cum.
@@ -113,7 +128,7 @@ typedef struct tpe_problem {
   int32_t n_upper;       /* categorical: number of categories                  */
   int64_t cand_off;      /* element offset into cand / coord / keys / l_out    */
   int64_t cand_base;     /* global index of local candidate 0 (shards, RNG)    */
-  int64_t reserved64;
+  int64_t n_cand_global; /* candidates of the problem over all shards (= n_cand unsharded) */
   int32_t n_splits;      /* splits of the bulk tiles (tiles carry their own)   */
   int32_t tile_off;      /* first candidate tile of this problem               */
   int32_t n_tiles;       /* candidate tiles of this problem                    */
@@ -250,6 +265,8 @@ typedef struct tpe_batch {
   uint32_t* fit_vals; uint32_t* fit_vals_sorted;    /* [fit_total]                */
   void* fit_tmp; uint64_t fit_tmp_bytes;            /* tpe_fit_workspace_bytes()  */
   int64_t fit_max_seg;        /* longest fit segment (<= 8192: sorted in LDS, no fit_tmp use) */
+  /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
+  double* draw_pref; int64_t draw_blocks; int32_t n_sorted; int32_t reserved5;
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
@@ -323,6 +340,7 @@ typedef struct tpe_pack_info {
   int64_t sort_count;               /* candidates of the sorted (pruned) problems */
   int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
   int64_t fit_max_seg;                  /* tpe_batch.fit_max_seg */
+  int64_t n_sorted, draw_blocks;        /* tpe_batch.n_sorted / draw_blocks */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation
@@ -376,11 +394,12 @@ typedef struct tpe_level_ws {
   double* fit_keys; double* fit_keys_sorted;
   uint32_t* fit_vals; uint32_t* fit_vals_sorted; int64_t fit_cap;   /* elements                    */
   void* fit_tmp; int64_t fit_tmp_bytes;
+  double* draw_pref; int64_t draw_pref_cap;    /* elements                                              */
 } tpe_level_ws;
 
 /* what a level needs (written on success and on TPE_E_SPACE) */
 typedef struct tpe_level_need {
-  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes;
+  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes, draw_pref;
 } tpe_level_need;
 
 /* Run one tree level: `labels` as for tpe_host_pack_level; `out` receives one
