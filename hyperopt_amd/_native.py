@@ -160,7 +160,7 @@ E_SPACE = -4
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
            'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above',
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
-           'tpe_host_cat_probs', 'tpe_host_pack_level', 'tpe_level_run')
+           'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run')
 
 
 class NativeUnavailable(RuntimeError):
@@ -203,6 +203,9 @@ def load(path=LIB_PATH):
     lib.tpe_host_fit_split.restype = ctypes.c_int
     lib.tpe_host_cat_probs.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_double, ctypes.c_int32, P]
     lib.tpe_host_cat_probs.restype = ctypes.c_int
+    lib.tpe_host_cat_split.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int32, P, D, ctypes.c_int32,
+                                       P, P]
+    lib.tpe_host_cat_split.restype = ctypes.c_int
     lib.tpe_host_pack_level.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64,
                                         ctypes.POINTER(PackInfo)]

@@ -25,7 +25,8 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
     dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o' if not defines else tag + '.o')
     cmds = [
-        [gxx, '-O3', '-march=x86-64-v3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math', '-Wall',
+        [gxx, '-O3', '-march=x86-64-v3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
+         '-fno-trapping-math', '-Wall',
          '-c', HOST_SRC, '-o', host_o],
         [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
          '-Wno-unused-command-line-argument'] + ['-D' + d for d in defines] + ['-c', SRC, '-o', dev_o],

@@ -42,6 +42,15 @@ int target_work() {
 }
 constexpr int kMinComponentsPerSplit = 128;
 constexpr int kFineKeyMinCand = 65536;
+// value-bucket bits of large candidate sets; TPE_FINE_KEY_BITS overrides (tuning)
+int fine_key_bits() {
+  static int v = [] {
+    const char* e = getenv("TPE_FINE_KEY_BITS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 && x <= 16 ? x : 12;
+  }();
+  return v;
+}
 constexpr int kTailMinTiles = 32;      // per-tile tail splits from 32 tiles (64k candidates) on
 // splits of the tile `e` tiles from either end of a pruned problem's sorted
 // range: the sparse tails are where waves span too wide a range for the local
@@ -109,9 +118,13 @@ void lf_weights(int64_t n, int lf, double* out) {
   for (int64_t i = num; i < n; ++i) out[i] = 1.0;
 }
 
+// erf(z) bit for bit: libm's erf is exactly +-1 from |z| = 6 on (erfc(6) < 2^-55),
+// so the (common) far-from-the-bound components skip the call
+inline double erf_fast(double z) { return fabs(z) >= 6.0 ? copysign(1.0, z) : erf(z); }
+
 double normal_cdf(double x, double mu, double sigma) {   // tpe.py:96-101
   const double bottom = np_max(sqrt(2.0) * sigma, kEPS);
-  return 0.5 * (1 + erf((x - mu) / bottom));
+  return 0.5 * (1 + erf_fast((x - mu) / bottom));
 }
 
 double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi) {
@@ -257,6 +270,27 @@ int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const doubl
   return TPE_OK;
 }
 
+int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const int64_t* below_tids, int64_t n_bt,
+                       int32_t upper, const double* p_prior, double prior_weight, int32_t lf, double* out_below,
+                       double* out_above) {
+  if (n < 0 || n_bt < 0 || (n && (!obs || !tids)) || (n_bt && !below_tids) || !out_below || !out_above)
+    return TPE_E_ARG;
+  // ap_filter_trials (tpe.py:629-636): one merge of ascending tids; sides keep tid order
+  std::vector<int64_t> side[2];
+  side[0].reserve((size_t)std::min(n, n_bt));
+  side[1].reserve((size_t)n);
+  int64_t b = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i && tids[i] <= tids[i - 1]) return TPE_E_ARG;
+    while (b < n_bt && below_tids[b] < tids[i]) ++b;
+    side[b < n_bt && below_tids[b] == tids[i] ? 0 : 1].push_back(obs[i]);
+  }
+  const int rc = tpe_host_cat_probs(side[0].data(), (int64_t)side[0].size(), upper, p_prior, prior_weight, lf,
+                                    out_below);
+  if (rc) return rc;
+  return tpe_host_cat_probs(side[1].data(), (int64_t)side[1].size(), upper, p_prior, prior_weight, lf, out_above);
+}
+
 int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
                         int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
                         tpe_pack_info* info) {
@@ -305,7 +339,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   int pbits = 0;
   while (((int64_t)1 << pbits) < S) ++pbits;
   int key_bits = std::max(5, 8 - pbits);
-  if (n_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(12, 16 - pbits));
+  if (n_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(fine_key_bits(), 16 - pbits));
   const int sort_end_bit = S > 0 && key_bits + pbits <= 32 ? key_bits + pbits : 0;
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
@@ -418,7 +452,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
               ap[i] = as / se;
             }
           bool odd = false;
-          for (int64_t i = 0; i < k; ++i) odd |= !(cp[i] >= 2.2250738585072014e-308 && cp[i] <= 1.7976931348623157e308);
+          for (int64_t i = 0; i < k; ++i) odd |= !((cp[i] >= 2.2250738585072014e-308) & (cp[i] <= 1.7976931348623157e308));
           if (odd)
             for (int64_t i = 0; i < k; ++i)
               cp[i] = (cp[i] >= 2.2250738585072014e-308 && cp[i] <= 1.7976931348623157e308) ? log2_normal(cp[i])
@@ -426,8 +460,10 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           else
             for (int64_t i = 0; i < k; ++i) cp[i] = log2_normal(cp[i]);
         }
-        for (int64_t i = 0; i < k; ++i)
-          if (c[i] > shift && std::isfinite(c[i])) shift = c[i];
+        for (int64_t i = 0; i < k; ++i) {
+          const double v = (c[i] > -INFINITY) & (c[i] < INFINITY) ? c[i] : -INFINITY;   // finite only
+          shift = v > shift ? v : shift;
+        }
         if (!std::isfinite(shift)) shift = 0;
         for (int64_t i = 0; i < k; ++i) c[i] -= shift;
         base = shift * kLn2;
@@ -495,7 +531,10 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           grid.resize(g0 + (size_t)G + 1, 0);
           int32_t* __restrict__ gp = grid.data() + g0;
           if (inv > 0) {
-            std::vector<int32_t> hist((size_t)G + 1, 0);
+            // four interleaved histograms: sorted mu puts neighbours in the same
+            // bucket, and one array would chain every increment through memory
+            const size_t H = (size_t)G + 1;
+            std::vector<int32_t> hist(4 * H, 0);
             const double dinv = (double)inv;
             for (int64_t i = 0; i < k; ++i) {
               const double x = (double)(float)mu[i];
@@ -503,10 +542,13 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
               g = g < 0 ? 0 : (g > G ? G : g);
               while (g > 0 && lo + (double)(g - 1) * step > x) --g;
               while (g < G && !(lo + (double)g * step > x)) ++g;
-              ++hist[(size_t)g];
+              ++hist[(size_t)(i & 3) * H + (size_t)g];
             }
             int32_t acc = 0;
-            for (int64_t g = 0; g < G; ++g) { acc += hist[(size_t)g]; gp[g] = acc; }
+            for (int64_t g = 0; g < G; ++g) {
+              acc += hist[(size_t)g] + hist[H + (size_t)g] + hist[2 * H + (size_t)g] + hist[3 * H + (size_t)g];
+              gp[g] = acc;
+            }
           }
           gp[G] = (int32_t)k;
         }

@@ -137,6 +137,41 @@ __device__ __attribute__((noinline)) float lse2_exact_ool(const float4* __restri
   return lse2_exact<float, float4>(comp, k0, n, k1, n1, t);
 }
 
+// Max-shifted log2-sum of a PRUNED above mixture at t (the fixed-shift sum
+// under-flowed: t is far from every component).  m0 = the best term among the
+// wide components and t's grid neighbours bounds the sum from below, so a narrow
+// component with mu outside t +- sqrt(narrow_cmax - m0 + 45) / narrow_amin is
+// under 2^-45 of it — the above kernel's pruning rule with a much tighter bound:
+// a few components instead of all K, serially per candidate.
+__device__ __attribute__((noinline)) float lse2_pruned(const tpe_problem& p, const float4* __restrict__ comp,
+                                                       const int32_t* __restrict__ grid, float t) {
+  const float4* __restrict__ C = comp + p.above_off;
+  const float4* __restrict__ Wd = comp + p.wide_off;
+  const int32_t* __restrict__ G = grid + p.grid_off;
+  float m0 = -INFINITY;
+  for (int k = 0; k < p.wide_len; ++k) {
+    const float4 c = Wd[k];
+    const float z = ((t - c.x) - c.y) * c.z;
+    m0 = fmaxf(m0, c.w - z * z);
+  }
+  const int gb = (int)fminf(fmaxf(floorf((t - p.grid_lo) * p.grid_inv), 0.f), (float)p.grid_n);
+  const int kc = G[gb];
+  for (int k = max(kc - 2, 0); k < min(kc + 2, p.above_len); ++k) {
+    const float4 c = C[k];
+    const float z = ((t - c.x) - c.y) * c.z;
+    m0 = fmaxf(m0, c.w - z * z);
+  }
+  const float R = sqrtf(fmaxf(p.narrow_cmax - m0 + kPruneBits, 0.f)) / p.narrow_amin;
+  const float vlo = t - R, vhi = t + R;
+  if (!(m0 > -INFINITY) || !(vlo == vlo && vhi == vhi && R < INFINITY))
+    return lse2_exact<float, float4>(comp, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
+  const float gl = (vlo - p.grid_lo) * p.grid_inv, gh = (vhi - p.grid_lo) * p.grid_inv;
+  const int bl = (int)fminf(fmaxf(floorf(gl) - 1.f, 0.f), (float)p.grid_n);
+  const int bh = (int)fminf(fmaxf(floorf(gh) + 2.f, 0.f), (float)p.grid_n);
+  const int kl = G[bl], kh = max(G[bh], G[bl]);
+  return lse2_exact<float, float4>(comp, p.above_off + kl, kh - kl, p.wide_off, p.wide_len, t);
+}
+
 // one-pass fixed-shift sum (every c_k <= 0) with the exact two-pass fallback
 // when it under-flows; used for the short below mixture
 __device__ __forceinline__ float lse2_fixed(const float4* __restrict__ comp, int k0, int n, float t) {
@@ -797,8 +832,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(TPE_AB
       const double lb2 = sb > 1e-30f ? (double)__log2f(sb)
                                      : (double)lse2_exact_ool(comp, p.below_off, p.below_len, 0, 0, t[j]);
       const double la2 = sa > 1e-30 ? log2(sa)
-                                     : (double)lse2_exact_ool(comp, p.above_off, p.above_len, p.wide_off,
-                                                              p.wide_len, t[j]);
+                         : p.narrow_amin > 0.f ? (double)lse2_pruned(p, comp, grid, t[j])
+                                               : (double)lse2_exact_ool(comp, p.above_off, p.above_len, p.wide_off,
+                                                                        p.wide_len, t[j]);
       const double lnx = logsp ? (double)t[j] : 0.0;
       const double l = lb2 * kLn2 + p.below_base - lnx;
       const double g = la2 * kLn2 + p.above_base - lnx;
@@ -915,6 +951,7 @@ __device__ __forceinline__ void finalize_slice(const tpe_problem* __restrict__ P
                                                const tpe_tile* __restrict__ tiles,
                                                const float4* __restrict__ comp32,
                                                const double4* __restrict__ comp64,
+                                               const int32_t* __restrict__ grid,
                                                const double* __restrict__ cand,
                                                const uint64_t* __restrict__ vals,
                                                const double* __restrict__ part,
@@ -980,8 +1017,9 @@ __device__ __forceinline__ void finalize_slice(const tpe_problem* __restrict__ P
         lb2 = (double)lse2_fixed(comp32, p.below_off, p.below_len, t);
         // fixed-shift sum; if it under-flowed, redo this candidate max-shifted
         la2 = sa > 1e-30 ? log2(sa)
-                         : (double)lse2_exact<float, float4>(comp32, p.above_off, p.above_len, p.wide_off,
-                                                             p.wide_len, t);
+              : p.narrow_amin > 0.f ? (double)lse2_pruned(p, comp32, grid, t)
+                                    : (double)lse2_exact<float, float4>(comp32, p.above_off, p.above_len, p.wide_off,
+                                                                        p.wide_len, t);
       } else {
         const double t = logsp ? log(x) : x;
         lb2 = lse2_exact64(comp64, p.below_off, p.below_len, t);
@@ -1023,6 +1061,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        const int32_t* __restrict__ fin_tiles,
                                                        const float4* __restrict__ comp32,
                                                        const double4* __restrict__ comp64,
+                                                       const int32_t* __restrict__ grid,
                                                        const double* __restrict__ cand,
                                                        const uint64_t* __restrict__ vals,
                                                        const double* __restrict__ part,
@@ -1030,8 +1069,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        tpe_best* __restrict__ tile_best, int precision,
                                                        int sampled, int flags) {
   const int tile = fin_tiles ? fin_tiles[blockIdx.x] : (int)blockIdx.x;
-  finalize_slice(P, tiles, comp32, comp64, cand, vals, part, l_out, g_out, tile_best, precision, sampled, flags,
-                 tile);
+  finalize_slice(P, tiles, comp32, comp64, grid, cand, vals, part, l_out, g_out, tile_best, precision, sampled,
+                 flags, tile);
 }
 
 // ================================================================= select
@@ -1566,7 +1605,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   if (n_fin == 0) return TPE_OK;
   hipLaunchKernelGGL(k_finalize, dim3(n_fin, TPE_BEST_PER_TILE), dim3(kThreads), 0,
                      (hipStream_t)stream, b->problems, b->tiles, listed ? b->fin_tiles : nullptr,
-                     (const float4*)b->comp32, (const double4*)b->comp64, b->cand, b->vals_sorted,
+                     (const float4*)b->comp32, (const double4*)b->comp64, b->grid, b->cand, b->vals_sorted,
                      b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample, b->flags);
   return hip_check("tpe_finalize");
 }

@@ -76,7 +76,7 @@ class LevelProblem(object):
 
     def __init__(self, post, label_ix, ids, inject=None):
         self.post, self.label_ix = post, int(label_ix)
-        self.ids = np.asarray(ids, dtype=np.int64)
+        self.ids = np.ascontiguousarray(ids, dtype=np.int64)
         self.inject = inject
 
 
@@ -319,6 +319,17 @@ class Engine(object):
         for i, lp in enumerate(problems):
             post = lp.post
             flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)
+            ids = lp.ids                          # int64, contiguous (LevelProblem)
+            if post.ptrs is not None and post.above_dev is None:
+                # native fits: the addresses are known; the posterior owns the arrays
+                keep.append(post)
+                pt = post.ptrs
+                recs[i] = (post.family, flags, int(post.upper), lp.label_ix,
+                           post.low if post.low is not None else 0.0, post.high if post.high is not None else 0.0,
+                           post.q if post.q is not None else 0.0,
+                           pt[0], pt[1], pt[2], pt[3], pt[4], pt[5], pt[6], pt[7],
+                           ids.ctypes.data, len(ids), 0, 0, 0, 0, 0, 0.0, 0.0, 0.0)
+                continue
             bw = [np.ascontiguousarray(a, dtype=np.float64) for a in post.below]
             ids = np.ascontiguousarray(lp.ids, dtype=np.int64)
             keep.append(bw)

@@ -34,6 +34,9 @@ class History(object):
         self.sorted_obs = sorted_obs     # every label's observation tids ascending
         self._cache = cache
 
+    def smallest(self, m):
+        return None if self._cache is None else self._cache.smallest(m)
+
     def value_order(self, label):
         """A permutation sorting the label's (float) observation values
         ascending, kept incrementally by the Trials cache; None without the
@@ -73,6 +76,8 @@ class _Cache(object):
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
         self.orders = {}               # label -> value-sorting permutation of its observations
+        self.top = None                # positions of the smallest losses, sorted by (loss, position)
+        self.top_n = 0                 # documents merged into `top`
 
     def extend(self, docs, start):
         for i in range(start, len(docs)):
@@ -120,9 +125,35 @@ class _Cache(object):
             return None
         return perm
 
+    TOP = 64
+
+    def smallest(self, m):
+        """Positions of the m smallest losses ordered by (loss, position), kept
+        by merging the documents appended since the last call; None when a
+        loss may still change (pending documents) or is NaN, or m is too large."""
+        n = self.losses.n
+        if self.pending or m > self.TOP:
+            return None
+        L = self.losses.view()
+        if self.top is None or self.top_n > n:
+            self.top, self.top_n = np.zeros(0, dtype=np.int64), 0
+        if self.top_n < n:
+            new = np.arange(self.top_n, n, dtype=np.int64)
+            if np.isnan(L[new]).any():
+                self.top = None
+                return None
+            if len(new) > 4 * self.TOP:      # (re)build: every loss <= the TOP-th smallest
+                kth = np.partition(L[new], self.TOP - 1)[self.TOP - 1]
+                new = new[L[new] <= kth]
+            cand = np.concatenate([self.top, new])
+            o = np.lexsort((cand, L[cand]))[:self.TOP]
+            self.top, self.top_n = cand[o], n
+        return self.top[:m]
+
     def refresh_pending(self):
         if not self.pending:
             return
+        self.top = None                # pending losses may change: rebuild the ranking
         keep = []
         L = self.losses.a
         for i in self.pending:
@@ -208,6 +239,9 @@ def split_below(history, gamma, gamma_cap=25):
         return history.tids[:0]
     if n_below >= n:
         return history.tids.copy()
+    top = history.smallest(n_below + 1)
+    if top is not None and len(top) == n_below + 1 and losses[top[n_below - 1]] != losses[top[n_below]]:
+        return history.tids[top[:n_below]]           # the same set as below, without a pass over N
     part = np.argpartition(losses, n_below - 1)
     kth = losses[part[n_below - 1]]
     rest = losses[part[n_below:]]

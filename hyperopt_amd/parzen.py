@@ -143,13 +143,17 @@ class Posterior(object):
                 mixture is fitted on the device (engine: tpe_fit_above); then
                 ``above`` is None and ``prior`` = (mu, sigma, weight, lf)
     """
-    __slots__ = ('dist', 'family', 'low', 'high', 'q', 'below', 'above', 'upper', 'above_dev', 'prior')
+    __slots__ = ('dist', 'family', 'low', 'high', 'q', 'below', 'above', 'upper', 'above_dev', 'prior', 'ptrs')
 
-    def __init__(self, dist, family, low, high, q, below, above, upper=0, above_dev=None, prior=None):
+    def __init__(self, dist, family, low, high, q, below, above, upper=0, above_dev=None, prior=None, ptrs=None):
         self.dist, self.family = dist, family
         self.low, self.high, self.q = low, high, q
         self.below, self.above, self.upper = below, above, upper
         self.above_dev, self.prior = above_dev, prior
+        # optional (below w, mu, sigma, K_below, above w, mu, sigma, K_above) host
+        # addresses of the arrays above (set by the native fits: spares the
+        # packer one ctypes address lookup per array)
+        self.ptrs = ptrs
 
     @property
     def bounded(self):
@@ -262,16 +266,42 @@ def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.
                              'non-positive Parzen bandwidth (prior_sigma=%r)' % (rc, psig))
     sides = []
     mask = None
+    base = out.ctypes.data
+    ptrs = []
     for sd in range(2):
         m = int(k[sd])
         if m:
             r = out[3 * sd * cap:]
             sides.append((r[:m], r[cap:cap + m], r[2 * cap:2 * cap + m]))
+            a0 = base + 3 * sd * cap * 8
+            ptrs += [a0, a0 + cap * 8, a0 + 2 * cap * 8, m]
             continue
         if mask is None:
             mask = np.isin(tids, bt)
         sides.append(fit_parzen(x[mask] if sd == 0 else x[~mask], prior_weight, pmu, psig, lf))
-    return Posterior(dist, family, low, high, None, sides[0], sides[1])
+    return Posterior(dist, family, low, high, None, sides[0], sides[1],
+                     ptrs=tuple(ptrs) if len(ptrs) == 8 else None)      # both sides native
+
+
+def cat_split(dist, args, obs_tids, obs_vals, below_tids, prior_weight=1.0, lf=DEFAULT_LF):
+    """Categorical label: the below/above split and both pseudo-count
+    posteriors in one native call (tpe_host_cat_split); equal to
+    fit_posterior's.  ``below_tids`` ascending, ``obs_tids`` strictly
+    ascending."""
+    upper = int(args['upper'])
+    obs = np.ascontiguousarray(obs_vals, dtype=np.int64)
+    tids = np.ascontiguousarray(obs_tids, dtype=np.int64)
+    bt = np.ascontiguousarray(below_tids, dtype=np.int64)
+    p = None if dist == 'randint' else np.ascontiguousarray(args['p'], dtype=np.float64)
+    out = np.empty(2 * upper)
+    base = out.ctypes.data
+    rc = N.load().tpe_host_cat_split(obs.ctypes.data, tids.ctypes.data, len(obs), bt.ctypes.data, len(bt), upper,
+                                     p.ctypes.data if p is not None else None, float(prior_weight), int(lf or 0),
+                                     base, base + 8 * upper)
+    if rc != 0:
+        raise IndexError('categorical observation out of range [0, %d) or tids not ascending' % upper)
+    return Posterior(dist, N.FAM_CATEGORICAL, None, None, None, (out[:upper],), (out[upper:],), upper,
+                     ptrs=(base, 0, 0, upper, base + 8 * upper, 0, 0, upper))
 
 
 # --------------------------------------------------------------------------

@@ -190,10 +190,21 @@ class ParamTable(object):
         return len(self.rows)
 
     def levels(self):
-        out = [[] for _ in range(self.n_levels)]
-        for r in self.rows:
-            out[r.depth].append(r)
-        return out
+        """Rows grouped by tree depth (computed once; the table is immutable)."""
+        out = self.__dict__.get('_levels')
+        if out is None:
+            out = [[] for _ in range(self.n_levels)]
+            for r in self.rows:
+                out[r.depth].append(r)
+            self._levels = out
+        return [list(level) for level in out]
+
+    def level_order(self):
+        """Labels level by level (the key order of a choices dict)."""
+        order = self.__dict__.get('_level_order')
+        if order is None:
+            order = self._level_order = [r.label for level in self.levels() for r in level]
+        return order
 
     def rng_order(self):
         """Order in which the reference's shared RandomState is consumed:

@@ -32,6 +32,7 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
 forgetting window is fixed at DEFAULT_LF=25 (tpe.py:27-29).
 """
 import logging
+import math
 import time
 
 import numpy as np
@@ -43,7 +44,7 @@ from . import history as _history
 from . import rand
 from . import replay
 from .engine import LevelProblem, get_engine
-from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, fit_posterior, fit_split
+from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, cat_split, fit_posterior, fit_split
 
 logger = logging.getLogger(__name__)
 
@@ -66,6 +67,11 @@ class _Fits(object):
         self.below_sorted = None
         self.cache = {}
 
+    def _below_sorted(self):
+        if self.below_sorted is None:
+            self.below_sorted = np.sort(np.asarray(self.below_tids, dtype=np.int64))
+        return self.below_sorted
+
     def get(self, row):
         post = self.cache.get(row.label)
         if post is None:
@@ -82,12 +88,14 @@ class _Fits(object):
                                          above_dev=(col, len(ovals), bidx))
             if post is not None:
                 pass
+            elif row.categorical and self.hist.sorted_obs:
+                # split + both pseudo-count posteriors in one native call (exact)
+                post = cat_split(row.dist, row.args, otids, ovals, self._below_sorted(), self.prior_weight,
+                                 DEFAULT_LF)
             elif (f32 and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and self.hist.sorted_obs
                   and self.hist.value_order(row.label) is not None):
                 # fp32 device path: split + both fits in one native call
-                if self.below_sorted is None:
-                    self.below_sorted = np.sort(np.asarray(self.below_tids, dtype=np.int64))
-                post = fit_split(row.dist, row.args, otids, ovals, self.below_sorted,
+                post = fit_split(row.dist, row.args, otids, ovals, self._below_sorted(),
                                  self.hist.value_order(row.label), self.prior_weight, DEFAULT_LF)
             else:
                 if bidx is None:
@@ -140,16 +148,20 @@ def _predict_activity(table, fits, C):
                 return None
             else:
                 post = fits.get(row)
-                pb = np.asarray(post.below[0], dtype=np.float64)
-                pa = np.asarray(post.above[0], dtype=np.float64)
-                tot = pb.sum()
+                pb = post.below[0].tolist()
+                pa = post.above[0].tolist()
+                tot = math.fsum(pb)
                 if not tot > 0:
                     return None
-                with np.errstate(divide='ignore', invalid='ignore'):
-                    score = np.log(pb) - np.log(pa)
-                score[~(pb > 0)] = -np.inf           # never drawn
-                c = int(np.argmax(score))
-                if not (pb[c] > 0) or C * pb[c] / tot < SPECULATE_MIN_DRAWS:
+                # np.argmax of log pb - log pa over the drawable categories (pb > 0)
+                c, best = -1, None
+                for k, (b, a) in enumerate(zip(pb, pa)):
+                    if not b > 0:
+                        continue
+                    sc = math.log(b) - math.log(a) if a > 0 else math.inf
+                    if best is None or sc > best or (sc != sc and best == best):
+                        c, best = k, sc
+                if c < 0 or C * pb[c] / tot < SPECULATE_MIN_DRAWS:
                     return None
                 chosen[row.label] = c
     return chosen
@@ -171,14 +183,14 @@ def _choices_fused(table, fits, new_ids, seed, C, engine, shard):
     problems = [LevelProblem(fits.get(r), r.index, ids) for r in rows]
     res = _run(engine, problems, C, seed, shard)
     n = len(ids)
-    order = [r.label for level in table.levels() for r in level]
-    chosen = [dict((k, None) for k in order) for _ in new_ids]
+    order = table.level_order()
+    chosen = [dict.fromkeys(order) for _ in new_ids]
+    idx, val = res['idx'].tolist(), res['value'].tolist()
     for k, row in enumerate(rows):
         for i in range(n):
-            r = res[k * n + i]
-            if r['idx'] < 0:
+            if idx[k * n + i] < 0:
                 raise RuntimeError('no candidate selected for %r' % row.label)
-            v = _value(row, r['value'])
+            v = _value(row, val[k * n + i])
             if pred[row.label] >= 0 and int(v) != pred[row.label]:
                 return None
             chosen[i][row.label] = v
@@ -262,16 +274,18 @@ def suggest(new_ids, domain, trials, seed,
         return []
     t0 = time.time()
     hist = _history.extract(domain, trials)
-    if len(hist):
-        logger.info('TPE using %i/%i trials with best loss %f' % (len(hist), len(trials), float(np.min(hist.losses))))
-    else:
-        logger.info('TPE using 0 trials')
+    if logger.isEnabledFor(logging.INFO):
+        if len(hist):
+            logger.info('TPE using %i/%i trials with best loss %f', len(hist), len(trials),
+                        float(np.min(hist.losses)))
+        else:
+            logger.info('TPE using 0 trials')
     if len(hist) < n_startup_jobs:
         return rand.suggest(new_ids, domain, trials, seed)
     choices = suggest_choices(domain.table, hist, new_ids, seed, prior_weight=prior_weight,
                               n_EI_candidates=n_EI_candidates, gamma=gamma, sampler=sampler,
                               precision=precision, device=device, shard=shard)
-    logger.info('tpe.suggest took %f seconds' % (time.time() - t0))
+    logger.info('tpe.suggest took %f seconds', time.time() - t0)
     return rand.docs_from_choices(new_ids, domain, trials, choices)
 
 

@@ -368,6 +368,13 @@ int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* orde
 int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
                        int32_t lf, double* out);
 
+/* ap_filter_trials + the categorical posteriors of both sides of one label
+ * (tpe.py:613-641, 573-607): obs/tids in strictly ascending tid order,
+ * below_tids ascending; out_below / out_above: `upper` probabilities each */
+int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const int64_t* below_tids, int64_t n_bt,
+                       int32_t upper, const double* p_prior, double prior_weight, int32_t lf, double* out_below,
+                       double* out_above);
+
 /* pack one tree level into `blob` (all tables, 256-B aligned, ready for one
  * host->device copy); TPE_E_SPACE (info->blob_bytes = size needed) if too small */
 int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,

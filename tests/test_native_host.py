@@ -190,3 +190,41 @@ def test_pack_reserves_device_fit_rows():
     assert info.blob_bytes == info.off_comp32 + 16 * (host_rows + K + 16)
     with pytest.raises(RuntimeError):
         _engine('fp64')._pack(lps, 4096, 1, 0, None)
+
+
+def test_cat_split_matches_fit_posterior():
+    """tpe_host_cat_split (merge split + both pseudo-count posteriors) equals
+    the masked fit_posterior path bit for bit."""
+    rs = np.random.RandomState(4)
+    for n in (0, 1, 24, 25, 26, 300):
+        tids = np.sort(rs.choice(4 * n + 10, n, replace=False)).astype(np.int64)
+        for upper in (2, 7):
+            obs = rs.randint(0, upper, n)
+            for dist, args in (('randint', dict(upper=upper)),
+                               ('categorical', dict(upper=upper, p=list(rs.dirichlet(np.ones(upper)))))):
+                below = np.sort(rs.permutation(tids)[:min(n, 25)])
+                a = parzen.cat_split(dist, args, tids, obs, below, 1.0, 25)
+                m = np.isin(tids, below)
+                b = parzen.fit_posterior(dist, args, obs[m], obs[~m], 1.0, 25)
+                np.testing.assert_array_equal(a.below[0], b.below[0])
+                np.testing.assert_array_equal(a.above[0], b.above[0])
+                assert a.upper == b.upper and a.family == b.family
+
+
+def test_split_below_incremental_matches_full():
+    """The Trials cache's incremental smallest-loss ranking gives split_below
+    the same below set as the full argpartition/argsort path, as documents
+    arrive (ties at the boundary fall back to the reference's argsort)."""
+    from hyperopt_amd import history as H
+    rs = np.random.RandomState(9)
+    c = H._Cache(['x'], {'x': False})
+    for step in range(60):
+        for _ in range(rs.randint(1, 40)):
+            c.tids.append(c.tids.n)
+            c.losses.append(float(rs.randint(0, 50)) if rs.rand() < 0.3 else rs.uniform())
+        hist = H.History(c.tids.view(), c.losses.view(), {}, cache=c)
+        plain = H.History(c.tids.view(), c.losses.view(), {})
+        for gamma in (0.25, 1.0):
+            a = H.split_below(hist, gamma)
+            b = H.split_below(plain, gamma)
+            assert sorted(a.tolist()) == sorted(b.tolist()), (step, gamma)

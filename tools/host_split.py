@@ -36,6 +36,8 @@ def main():
     wrap(H, 'extract', 'extract')
     wrap(H, 'split_below', 'split_below')
     wrap(tpe.rand, 'docs_from_choices', 'docs')
+    wrap(tpe, '_predict_activity', 'predict(+gate fits)')
+    wrap(eng, '_labels', 'run_level/_labels')
     for i in range(5):
         tpe.suggest([bench.N_HISTORY], domain, trials, i, n_EI_candidates=bench.C_PER_GPU)
     acc.clear()
@@ -48,7 +50,29 @@ def main():
     print('suggest p50 %.3f ms, mean %.3f ms' % (1e3 * np.median(lat), 1e3 * tot / steps))
     for k, v in sorted(acc.items(), key=lambda kv: -kv[1]):
         print('  %-12s %7.1f us/suggest' % (k, 1e6 * v / steps))
-    print('  %-12s %7.1f us/suggest' % ('other', 1e6 * (tot - sum(acc.values())) / steps))
+    nested = [k for k in acc if '/' in k or k.startswith('predict')]
+    print('  %-12s %7.1f us/suggest' % ('other', 1e6 * (tot - sum(v for k, v in acc.items() if k not in nested))
+                                       / steps))
+    # the C packer alone on this host (the level runner's host share)
+    import ctypes
+    from hyperopt_amd import _native as N
+    from hyperopt_amd.engine import LevelProblem
+    hist = H.extract(domain, trials)
+    fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, eng)
+    T = domain.table
+    probs = [LevelProblem(fits.get(T.by_label[l]), T.by_label[l].index, [bench.N_HISTORY])
+             for l in ['svm_C', 'svm_kernel', 'svm_rbf_gamma', 'model']]
+    labels, keep = eng._labels(probs)
+    info = N.PackInfo()
+    pin = eng._pinned
+    best = 1e9
+    for _ in range(20):
+        t0 = time.perf_counter()
+        for _ in range(20):
+            eng.lib.tpe_host_pack_level(labels, len(probs), bench.C_PER_GPU, 5, 0, 0, 0, pin.data_ptr(), pin.numel(),
+                                        ctypes.byref(info))
+        best = min(best, (time.perf_counter() - t0) / 20)
+    print('  tpe_host_pack_level alone (4 labels, min of 20x20): %.1f us' % (1e6 * best))
 
 
 if __name__ == '__main__':
