@@ -11,11 +11,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 6
+ABI_VERSION = 7
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH = 1, 2
+F_HAS_LOW, F_HAS_HIGH, F_POOLED = 1, 2, 4
 BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS = 1, 2, 4, 8
 PREC_F32, PREC_F64 = 0, 1
 
@@ -31,7 +31,7 @@ PROBLEM_DTYPE = np.dtype([
     ('low', '<f8'), ('high', '<f8'), ('q', '<f8'), ('below_base', '<f8'), ('above_base', '<f8'),
     ('prior_mu', '<f4'), ('prior_a', '<f4'), ('prior_c', '<f4'), ('narrow_cmax', '<f4'),
     ('narrow_amin', '<f4'), ('grid_lo', '<f4'), ('grid_inv', '<f4'),
-    ('key_lo', '<f4'), ('key_inv', '<f4'), ('reserved_f', '<f4'),
+    ('key_lo', '<f4'), ('key_inv', '<f4'), ('pool_first', '<i4'),
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
 ])
 assert PROBLEM_DTYPE.itemsize == 192
@@ -77,7 +77,7 @@ class Batch(ctypes.Structure):
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
         ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64), ('fit_max_seg', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_blocks', ctypes.c_int64), ('n_sorted', ctypes.c_int32),
-        ('reserved5', ctypes.c_int32),
+        ('reserved5', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
     ]
 
 
@@ -125,7 +125,7 @@ class PackInfo(ctypes.Structure):
         ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
         ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_seg', ctypes.c_int64),
-        ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64),
+        ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64), ('n_pooled', ctypes.c_int64),
     ]
 
 
@@ -145,6 +145,7 @@ class LevelWS(ctypes.Structure):
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p), ('fit_cap', ctypes.c_int64),
         ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_pref_cap', ctypes.c_int64),
+        ('pool_best', ctypes.c_void_p), ('pool_best_cap', ctypes.c_int64),
     ]
 
 
@@ -152,7 +153,7 @@ class LevelNeed(ctypes.Structure):
     """tpe_level_need: sizes one level needs."""
     _fields_ = [(k, ctypes.c_int64) for k in ('pinned_bytes', 'blob_bytes', 'cand', 'sort_tmp_bytes', 'part',
                                               'best', 'result', 'fit', 'fit_tmp_bytes',
-                                              'draw_pref')]
+                                              'draw_pref', 'pool_best')]
 
 
 E_SPACE = -4

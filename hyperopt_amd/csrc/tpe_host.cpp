@@ -297,10 +297,13 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (!info || n_labels < 0 || n_cand < 0 || (n_labels && !labels)) return TPE_E_ARG;
   const bool f64 = precision == TPE_PREC_F64;
   const int T = 2048;
-  std::vector<float> comp32;     // float4 rows
-  std::vector<double> comp64;    // double4 rows
-  std::vector<double> samp;      // 8 doubles per row
-  std::vector<int32_t> grid;
+  // staging tables: per-thread, reused across calls (no first-touch page faults
+  // on the large ones — a batched level has ~10^5 problems, tiles and work items)
+  static thread_local std::vector<float> comp32;     // float4 rows
+  static thread_local std::vector<double> comp64;    // double4 rows
+  static thread_local std::vector<double> samp;      // 8 doubles per row
+  static thread_local std::vector<int32_t> grid;
+  comp32.clear(); comp64.clear(); samp.clear(); grid.clear();
   std::vector<tpe_problem> lab((size_t)n_labels);
   int64_t P = 0, ktot = 0;
   std::vector<char> dev_fit((size_t)n_labels, 0);   // above mixture fitted on the device
@@ -328,18 +331,25 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // buckets per problem.  Large candidate sets get 4096 buckets (two passes):
   // a wave of 512 sorted candidates then spans ~1/8 of a bucket's density,
   // narrow enough for the above kernel's local expansion.
-  std::vector<char> pruned((size_t)n_labels, 0);
-  int64_t S = 0;
+  // A pruned label active for several ids is POOLED: its problems share one
+  // sort slot and are sorted as one population (include/tpe_hip.h).
+  std::vector<char> pruned((size_t)n_labels, 0), pooled((size_t)n_labels, 0);
+  int64_t S = 0, n_sorted_prob = 0, n_pooled = 0, max_slot_cand = 0;   // S: sort slots
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
     pruned[li] = !f64 && (L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) &&
                  (dev_fit[li] || L.above_k > kPruneMinK);
-    if (pruned[li]) S += L.n_ids;
+    pooled[li] = pruned[li] && L.n_ids >= 2;
+    if (!pruned[li]) continue;
+    S += pooled[li] ? 1 : L.n_ids;
+    n_sorted_prob += L.n_ids;
+    if (pooled[li]) n_pooled += L.n_ids;
+    max_slot_cand = std::max(max_slot_cand, (pooled[li] ? L.n_ids : 1) * (int64_t)n_cand);
   }
   int pbits = 0;
   while (((int64_t)1 << pbits) < S) ++pbits;
   int key_bits = std::max(5, 8 - pbits);
-  if (n_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(fine_key_bits(), 16 - pbits));
+  if (max_slot_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(fine_key_bits(), 16 - pbits));
   const int sort_end_bit = S > 0 && key_bits + pbits <= 32 ? key_bits + pbits : 0;
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
@@ -599,20 +609,25 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (below_idx.empty()) below_idx.push_back(0);
   // ---- problems, tiles, work ----
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
-  std::vector<tpe_problem> prob((size_t)P);
+  static thread_local std::vector<tpe_problem> prob;
+  prob.resize((size_t)P);
   int64_t scored = 0;
   const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
   {
-    int64_t r = 0, s_next = 0, u_next = S * (int64_t)n_cand;
+    int64_t r = 0, s_next = 0, u_next = n_sorted_prob * (int64_t)n_cand;
     int32_t slot = 0;
-    for (int32_t li = 0; li < n_labels; ++li)
+    for (int32_t li = 0; li < n_labels; ++li) {
+      const int32_t pool_slot = pooled[li] ? slot++ : -1, pool_first = (int32_t)r;
       for (int64_t j = 0; j < labels[li].n_ids; ++j, ++r) {
-        tpe_problem q = lab[li];
+        tpe_problem& q = prob[r];
+        q = lab[li];
         q.n_cand = n_cand;
         int64_t& next = pruned[li] ? s_next : u_next;
         q.cand_off = next;
         next += n_cand;
-        q.sort_slot = pruned[li] ? slot++ : -1;
+        q.sort_slot = pooled[li] ? pool_slot : pruned[li] ? slot++ : -1;
+        q.pool_first = pooled[li] ? pool_first : -1;
+        if (pooled[li]) q.flags |= TPE_F_POOLED;
         q.cand_base = cand_base;
         q.n_cand_global = C_ref;
         q.key0 = (uint32_t)seed; q.key1 = (uint32_t)(seed >> 32);
@@ -620,9 +635,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         q.ctr3 = (uint32_t)labels[li].ids[j];
         q.n_tiles = (int32_t)n_tiles_p;
         q.tile_off = (int32_t)(r * n_tiles_p);
-        prob[r] = q;
         if (q.family != TPE_FAM_CATEGORICAL) ++scored;
       }
+    }
   }
   // splits of the above mixture per tile.  Bulk tiles: enough work items to fill
   // the chip (a function of the GLOBAL candidate count, so every candidate sums
@@ -650,7 +665,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     const int64_t cap = std::max<int64_t>(1, (q.above_len + 63) / 64);
     return (int32_t)std::max<int64_t>(1, std::min(ns, cap));
   };
-  std::vector<tpe_tile> tiles((size_t)(P * n_tiles_p));
+  static thread_local std::vector<tpe_tile> tiles;
+  tiles.resize((size_t)(P * n_tiles_p));
   for (int64_t r = 0, t = 0; r < P; ++r)
     for (int64_t j = 0; j < n_tiles_p; ++j, ++t) {
       tiles[t].problem = (int32_t)r;
@@ -660,7 +676,13 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
   // work items grouped [continuous | quantized Gauss | quantized log]; a tile's
   // items are consecutive, and an item's index is its row of `part`
-  std::vector<tpe_work> work;
+  static thread_local std::vector<tpe_work> work;
+  work.clear();
+  {
+    int64_t nw = 0;
+    for (const tpe_tile& tl : tiles) nw += tl.n_splits;
+    work.reserve((size_t)nw);
+  }
   int32_t counts[3] = {0, 0, 0};
   const int fams[3][2] = {{TPE_FAM_GAUSS, TPE_FAM_LOGGAUSS}, {TPE_FAM_QGAUSS, -1}, {TPE_FAM_QLOGGAUSS, -1}};
   for (int gi = 0; gi < 3; ++gi) {
@@ -688,7 +710,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // tiles the finalize stage scores (device-drawn candidates): not categorical
   // (the sample stage scores those), not one-split continuous f32 (the above
   // stage does)
-  std::vector<int32_t> fin_tiles;
+  static thread_local std::vector<int32_t> fin_tiles;
+  fin_tiles.clear();
   for (int64_t t = 0; t < (int64_t)tiles.size(); ++t) {
     const tpe_problem& q = prob[tiles[t].problem];
     const bool cat = q.family == TPE_FAM_CATEGORICAL && q.samp_len <= TPE_SAMPLE_LDS_ROWS;
@@ -730,8 +753,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->n_fit = (int32_t)fit.size(); info->reserved = 0;
   info->fit_total = fit_seg.back();
   info->copy_end = off[9] + len[9];
-  info->sort_count = S * (int64_t)n_cand;
+  info->sort_count = n_sorted_prob * (int64_t)n_cand;
   info->n_sorted = S;
+  info->n_pooled = n_pooled;
   info->draw_blocks = (C_ref + 1 + 63) / 64;
   info->copy2_len = len[10];
   info->blob_bytes = end;

@@ -414,6 +414,34 @@ __global__ __launch_bounds__(kThreads) void k_draw_scan(const tpe_problem* __res
   for (int64_t b = b0; b < b1; ++b) { const double v = row[b]; row[b] = run; run += v; }
 }
 
+// ------------------------------------------------------------ pooled labels
+// (include/tpe_hip.h "Pooled labels").  u64 key of (score, candidate index):
+// the order-preserving integer of the f64 score (NaN canonicalised: the
+// maximum, as in np.argmax) with its low idx_bits replaced by the complemented
+// index, so atomicMax keeps the best score and, among equal (truncated) scores,
+// the first index.  0 = no candidate.
+__device__ __forceinline__ int pool_idx_bits(int n_cand) { return n_cand > 1 ? 32 - __clz(n_cand - 1) : 1; }
+
+__device__ __forceinline__ unsigned long long pool_key(double score, int64_t idx, int idx_bits) {
+  if (score != score) score = __longlong_as_double(0x7FF8000000000000ll);
+  unsigned long long u = (unsigned long long)__double_as_longlong(score);
+  u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  const unsigned long long mask = (1ull << idx_bits) - 1;
+  return (u & ~mask) | (mask - (unsigned long long)idx);
+}
+
+// fold candidate `oo` (absolute position in the candidate arrays) of a pooled
+// label into its own problem's best; a relaxed read skips most atomics
+__device__ __forceinline__ void pool_update(const tpe_problem* __restrict__ P, const tpe_problem& p,
+                                            unsigned long long* __restrict__ pool_best, int64_t oo, double score) {
+  const int64_t base = P[p.pool_first].cand_off;
+  const int64_t rel = oo - base;
+  const int64_t r = p.pool_first + rel / p.n_cand;
+  const unsigned long long key = pool_key(score, rel % p.n_cand, pool_idx_bits(p.n_cand));
+  if (key > __hip_atomic_load(pool_best + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(pool_best + r, key);
+}
+
 // block argmax of (score, original index) into one tile_best slot; the lane
 // that holds the winner (unique index) publishes its l and g
 __device__ __forceinline__ void block_best(double sc, int64_t orig, double l, double g, tpe_best* __restrict__ slot) {
@@ -456,9 +484,11 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      double* __restrict__ l_out, double* __restrict__ g_out,
                                                      int precision, int draw, int key_bits, int flags,
                                                      const double* __restrict__ draw_pref, int64_t draw_blocks,
-                                                     int ordered) {
+                                                     int ordered, unsigned long long* __restrict__ pool_best) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
+  if ((p.flags & TPE_F_POOLED) && tl.cand_start == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    pool_best[tl.problem] = 0ull;          // scored after this kernel: no race
   const bool store_x = (flags & TPE_BATCH_WRITE_CAND) || precision == TPE_PREC_F64 ||
                        p.family == TPE_FAM_QGAUSS || p.family == TPE_FAM_QLOGGAUSS;
   float lo_f, hi_f;
@@ -710,7 +740,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(TPE_AB
                                                         tpe_best* __restrict__ tile_best,
                                                         double* __restrict__ l_out, double* __restrict__ g_out,
                                                         unsigned long long* __restrict__ ce_count, int flags,
-                                                        int sampled) {
+                                                        int sampled, unsigned long long* __restrict__ pool_best) {
   const tpe_work w = W[blockIdx.x];
   const tpe_problem& p = P[w.problem];
   const int n = p.n_cand;
@@ -839,12 +869,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(TPE_AB
       const double l = lb2 * kLn2 + p.below_base - lnx;
       const double g = la2 * kLn2 + p.above_base - lnx;
       if (l_out) { l_out[oo[j]] = l; g_out[oo[j]] = g; }
+      if (p.flags & TPE_F_POOLED) { pool_update(P, p, pool_best, (int64_t)oo[j], l - g); continue; }
       const int64_t orig = (int64_t)oo[j] - p.cand_off;
       if (better(l - g, orig, bs, bi)) { bs = l - g; bl = l; bg = g; bi = orig; }
     }
-    tpe_best* __restrict__ slot = tile_best + (int64_t)tile * TPE_BEST_PER_TILE;
-    block_best(bs, bi, bl, bg, slot);
-    if (threadIdx.x > 0 && threadIdx.x < TPE_BEST_PER_TILE) slot[threadIdx.x] = tpe_best{0, 0, 0, -1};
+    if (!(p.flags & TPE_F_POOLED)) {       // (problem-uniform branch: block_best synchronises)
+      tpe_best* __restrict__ slot = tile_best + (int64_t)tile * TPE_BEST_PER_TILE;
+      block_best(bs, bi, bl, bg, slot);
+      if (threadIdx.x > 0 && threadIdx.x < TPE_BEST_PER_TILE) slot[threadIdx.x] = tpe_best{0, 0, 0, -1};
+    }
     }
   }
   if (ce_count) {       // profiling (no atomics): [exact CE, expanded components] of this work item
@@ -957,7 +990,8 @@ __device__ __forceinline__ void finalize_slice(const tpe_problem* __restrict__ P
                                                const double* __restrict__ part,
                                                double* __restrict__ l_out, double* __restrict__ g_out,
                                                tpe_best* __restrict__ tile_best, int precision,
-                                               int sampled, int flags, int tile) {
+                                               int sampled, int flags, int tile,
+                                               unsigned long long* __restrict__ pool_best) {
   const tpe_tile tl = tiles[tile];
   const tpe_problem& p = P[tl.problem];
   // sampled categorical tiles are finalized by k_sample (one-split continuous
@@ -1031,6 +1065,10 @@ __device__ __forceinline__ void finalize_slice(const tpe_problem* __restrict__ P
     }
     if (l_out) { l_out[oo] = l; g_out[oo] = g; }
   }
+  if (p.flags & TPE_F_POOLED) {            // problem-uniform: no block reduction follows
+    if (valid) pool_update(P, p, pool_best, (int64_t)oo, l - g);
+    return;
+  }
   const double sc = l - g;
   // wave argmax on (score, original index) only; the winning lane (unique
   // index) then publishes its l and g
@@ -1067,23 +1105,99 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const tpe_problem* __rest
                                                        const double* __restrict__ part,
                                                        double* __restrict__ l_out, double* __restrict__ g_out,
                                                        tpe_best* __restrict__ tile_best, int precision,
-                                                       int sampled, int flags) {
+                                                       int sampled, int flags,
+                                                       unsigned long long* __restrict__ pool_best) {
   const int tile = fin_tiles ? fin_tiles[blockIdx.x] : (int)blockIdx.x;
   finalize_slice(P, tiles, comp32, comp64, grid, cand, vals, part, l_out, g_out, tile_best, precision, sampled,
-                 flags, tile);
+                 flags, tile, pool_best);
 }
 
 // ================================================================= select
 // One 1024-thread workgroup per problem: reads the problem's
 // n_tiles * TPE_BEST_PER_TILE slot bests (4096 at 2^20 candidates).
 constexpr int kSelThreads = 1024;
+
+// block-wide max / sum over kSelThreads threads (lds: kSelThreads / 64 slots)
+template <typename T, bool MAX>
+__device__ __forceinline__ T sel_reduce(T v, T* lds) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const T o = __shfl_xor(v, off);
+    v = MAX ? (o > v ? o : v) : v + o;
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = lds[0];
+  for (int q = 1; q < kSelThreads / 64; ++q) v = MAX ? (lds[q] > v ? lds[q] : v) : v + lds[q];
+  return v;
+}
+
+// exact max-shifted log2-sum of comp rows [k0, k0 + n) and [k1, k1 + n1) at t,
+// spread over the workgroup (f64 sum)
+__device__ double sel_lse2(const float4* __restrict__ comp, int k0, int n, int k1, int n1, float t, double* lds) {
+  float m = -INFINITY;
+  for (int k = threadIdx.x; k < n + n1; k += kSelThreads) {
+    const float4 c = k < n ? comp[k0 + k] : comp[k1 + k - n];
+    const float z = ((t - c.x) - c.y) * c.z;
+    m = fmaxf(m, c.w - z * z);
+  }
+  const double mm = sel_reduce<double, true>((double)m, lds);
+  if (!(mm > -INFINITY)) return mm;
+  double sum = 0.0;
+  for (int k = threadIdx.x; k < n + n1; k += kSelThreads) {
+    const float4 c = k < n ? comp[k0 + k] : comp[k1 + k - n];
+    const float z = ((t - c.x) - c.y) * c.z;
+    sum += exp2((double)(c.w - z * z) - mm);
+  }
+  return mm + log2(sel_reduce<double, false>(sum, lds));
+}
+
+// pooled problem: the winner from pool_best, its value re-drawn, its l and g
+// evaluated exactly over the whole mixtures (one workgroup)
+__device__ void select_pooled(const tpe_problem& p, const unsigned long long* __restrict__ pool_best,
+                              const float4* __restrict__ comp32, const double* __restrict__ samp,
+                              const double* __restrict__ cand, int precision, int sampled,
+                              tpe_result* __restrict__ result) {
+  __shared__ double lds[kSelThreads / 64];
+  const unsigned long long key = pool_best[blockIdx.x];
+  const unsigned long long mask = (1ull << pool_idx_bits(p.n_cand)) - 1;
+  const int64_t idx = key ? (int64_t)(mask - (key & mask)) : -1;
+  tpe_result r;
+  r.score = 0; r.l = 0; r.g = 0; r.value = 0; r.idx = idx; r.global_idx = -1;
+  if (idx >= 0) {
+    float lo_f, hi_f, t;
+    int c;
+    if (sampled && p.samp_len > 0) {
+      f32_bounds(p, lo_f, hi_f);
+      const double* S = samp + 8 * (int64_t)p.samp_off;
+      draw_one(p, S, S, 8, idx, precision, lo_f, hi_f, r.value, t, c);
+    } else {                               // caller-drawn candidates
+      r.value = cand[p.cand_off + idx];
+      t = (float)(p.family == TPE_FAM_LOGGAUSS ? log(r.value) : r.value);
+    }
+    const double lb2 = sel_lse2(comp32, p.below_off, p.below_len, 0, 0, t, lds);
+    const double la2 = sel_lse2(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t, lds);
+    const double lnx = p.family == TPE_FAM_LOGGAUSS ? (double)t : 0.0;
+    r.l = lb2 * kLn2 + p.below_base - lnx;
+    r.g = la2 * kLn2 + p.above_base - lnx;
+    r.score = r.l - r.g;
+    r.global_idx = p.cand_base + idx;
+  }
+  if (threadIdx.x == 0) result[blockIdx.x] = r;
+}
 __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __restrict__ P,
                                                      const tpe_best* __restrict__ tile_best,
                                                      const double* __restrict__ cand,
                                                      const double* __restrict__ samp, int precision, int sampled,
                                                      const double* __restrict__ draw_pref, int64_t draw_blocks,
-                                                     int ordered, tpe_result* __restrict__ result) {
+                                                     int ordered, const unsigned long long* __restrict__ pool_best,
+                                                     const float4* __restrict__ comp32,
+                                                     tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
+  if (p.flags & TPE_F_POOLED) {            // problem-uniform
+    select_pooled(p, pool_best, comp32, samp, cand, precision, sampled, result);
+    return;
+  }
   tpe_best b{0, 0, 0, -1};
   const int64_t nb = (int64_t)p.n_tiles * TPE_BEST_PER_TILE;
   const tpe_best* __restrict__ tb = tile_best + (int64_t)p.tile_off * TPE_BEST_PER_TILE;
@@ -1548,7 +1662,7 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
                      b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
                      b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
-                     b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0);
+                     b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0, b->pool_best);
   return hip_check("tpe_sample");
 }
 
@@ -1579,7 +1693,7 @@ int tpe_score_above(const tpe_batch* b, void* stream) {
     if (b->precision == TPE_PREC_F32)
       hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
                          (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->tile_best,
-                         b->l_out, b->g_out, b->ce_count, b->flags, b->sample);
+                         b->l_out, b->g_out, b->ce_count, b->flags, b->sample, b->pool_best);
     else
       hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
                          (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
@@ -1606,7 +1720,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   hipLaunchKernelGGL(k_finalize, dim3(n_fin, TPE_BEST_PER_TILE), dim3(kThreads), 0,
                      (hipStream_t)stream, b->problems, b->tiles, listed ? b->fin_tiles : nullptr,
                      (const float4*)b->comp32, (const double4*)b->comp64, b->grid, b->cand, b->vals_sorted,
-                     b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample, b->flags);
+                     b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample, b->flags, b->pool_best);
   return hip_check("tpe_finalize");
 }
 
@@ -1616,7 +1730,7 @@ int tpe_select(const tpe_batch* b, void* stream) {
   if (b->n_problems == 0) return TPE_OK;
   hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
                      b->tile_best, b->cand, b->samp, b->precision, b->sample, b->draw_pref, b->draw_blocks,
-                     ordered_draws(b) ? 1 : 0, b->result);
+                     ordered_draws(b) ? 1 : 0, b->pool_best, (const float4*)b->comp32, b->result);
   return hip_check("tpe_select");
 }
 
@@ -1656,7 +1770,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   uint64_t sz = 0;
   // ordered draws replace the sort of the pruned problems' candidates
   const bool od = precision == TPE_PREC_F32 && (flags & TPE_BATCH_ORDERED_DRAWS) && info.n_sorted > 0 &&
-                  info.sort_count > 0;
+                  info.sort_count > 0 && info.n_pooled == 0;
+  if (info.n_pooled > 0) need->pool_best = P;
   if (od) need->draw_pref = info.n_sorted * (info.draw_blocks + 1);
   if (!od && info.sort_end_bit > 0 && info.sort_count > 0) {
     if ((rc = tpe_sort_workspace_bytes(info.sort_count, &sz))) return rc;
@@ -1669,7 +1784,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   if (rc == TPE_E_SPACE || need->pinned_bytes > ws->pinned_bytes || need->blob_bytes > ws->blob_bytes ||
       need->cand > ws->cand_cap || need->part > ws->part_cap || need->best > ws->best_cap ||
       need->result > ws->result_cap || need->fit > ws->fit_cap || need->sort_tmp_bytes > ws->sort_tmp_bytes ||
-      need->fit_tmp_bytes > ws->fit_tmp_bytes || need->draw_pref > ws->draw_pref_cap)
+      need->fit_tmp_bytes > ws->fit_tmp_bytes || need->draw_pref > ws->draw_pref_cap ||
+      need->pool_best > ws->pool_best_cap)
     return fail(TPE_E_SPACE, "level workspace too small (see tpe_level_need)");
   if (P == 0) return TPE_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -1713,6 +1829,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.n_work_cont = info.n_work_cont; b.n_work_qgauss = info.n_work_qgauss; b.n_work_qlog = info.n_work_qlog;
   b.part = ws->part;
   b.tile_best = ws->tile_best;
+  if (info.n_pooled > 0) b.pool_best = ws->pool_best;
   b.result = ws->result;
   if (info.n_fit > 0) {
     b.fit = (const tpe_fit_job*)(dev + info.off_fit);

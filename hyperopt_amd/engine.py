@@ -138,10 +138,15 @@ class Engine(object):
         # sorted (pruned) problems: continuous f32 above mixtures of > PRUNE_MIN_K components
         pruned_l = [(not f64) and lp.post.family in (N.FAM_GAUSS, N.FAM_LOGGAUSS)
                     and (lp.post.above_dev is not None or len(lp.post.above[0]) > PRUNE_MIN_K) for lp in problems]
-        S = sum(len(lp.ids) for lp, pr in zip(problems, pruned_l) if pr)
+        # a pruned label active for several ids is pooled: one sort slot for all its problems
+        pooled_l = [pr and len(lp.ids) >= 2 for lp, pr in zip(problems, pruned_l)]
+        S = sum((1 if po else len(lp.ids)) for lp, pr, po in zip(problems, pruned_l, pooled_l) if pr)
+        n_sorted = sum(len(lp.ids) for lp, pr in zip(problems, pruned_l) if pr)
+        max_slot = max([n_cand * (len(lp.ids) if po else 1) for lp, pr, po in zip(problems, pruned_l, pooled_l)
+                        if pr], default=0)
         pbits = int(math.ceil(math.log2(S))) if S > 1 else 0
         key_bits = max(5, 8 - pbits)
-        if n_cand >= FINE_KEY_MIN_CAND:
+        if max_slot >= FINE_KEY_MIN_CAND:
             key_bits = max(key_bits, min(12, 16 - pbits))
         comp32, comp64, samp, grids = [], [], [], []
         n32 = n64 = ns = ngrid = 0
@@ -227,11 +232,27 @@ class Engine(object):
         prob['n_cand'] = n_cand
         ids = np.concatenate([lp.ids for lp in problems]) if P else np.zeros(0, np.int64)
         pr = np.repeat(np.array(pruned_l, dtype=bool), counts) if P else np.zeros(0, bool)
-        # sorted problems own the candidate range [0, S * n_cand)
-        slot = np.cumsum(pr) - 1
+        # sorted problems own the candidate range [0, n_sorted * n_cand)
+        srank = np.cumsum(pr) - 1
         unslot = np.cumsum(~pr) - 1
-        prob['cand_off'] = np.where(pr, slot * n_cand, (S + unslot) * n_cand)
-        prob['sort_slot'] = np.where(pr, slot, -1)
+        prob['cand_off'] = np.where(pr, srank * n_cand, (n_sorted + unslot) * n_cand)
+        slots, pool_first, nxt, r = [], [], 0, 0
+        for lp, p_, po in zip(problems, pruned_l, pooled_l):
+            k = len(lp.ids)
+            if po:
+                slots += [nxt] * k
+                nxt += 1
+            elif p_:
+                slots += list(range(nxt, nxt + k))
+                nxt += k
+            else:
+                slots += [-1] * k
+            pool_first += [r if po else -1] * k
+            r += k
+        prob['sort_slot'] = slots if P else -1
+        prob['pool_first'] = pool_first if P else -1
+        pooled = np.repeat(np.array(pooled_l, dtype=bool), counts) if P else np.zeros(0, bool)
+        prob['flags'] = prob['flags'] | np.where(pooled, N.F_POOLED, 0)
         prob['cand_base'] = cand_base
         prob['n_cand_global'] = n_cand if not n_cand_global else int(n_cand_global)
         s64 = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -416,6 +437,7 @@ class Engine(object):
         ws.fit_cap = min(f1, f2, f3, f4)
         ws.fit_tmp, ws.fit_tmp_bytes = dev('fit_tmp', 1)
         ws.draw_pref, ws.draw_pref_cap = dev('draw_pref', 8)
+        ws.pool_best, ws.pool_best_cap = dev('pool_best', 8)
         self._ws = ws
         return ws
 
@@ -436,6 +458,7 @@ class Engine(object):
             self._buf(name, need.fit, dt)
         self._buf('fit_tmp', need.fit_tmp_bytes, torch.uint8)
         self._buf('draw_pref', need.draw_pref, torch.float64)
+        self._buf('pool_best', need.pool_best, torch.int64)
         self._ws = None
 
     def run_level(self, problems, n_cand, seed, cand_base=0, n_cand_global=None):
@@ -560,7 +583,9 @@ class Engine(object):
         b.l_out = d_l.data_ptr() if d_l is not None else None
         b.g_out = d_g.data_ptr() if d_g is not None else None
         b.tile_best, b.result = d_best.data_ptr(), d_res.data_ptr()
-        if info.n_sorted and not inject:
+        if info.n_pooled:
+            b.pool_best = self._buf('pool_best', P, torch.int64).data_ptr()
+        if info.n_sorted and not inject and not info.n_pooled:
             b.n_sorted, b.draw_blocks = info.n_sorted, info.draw_blocks
             b.draw_pref = self._buf('draw_pref', int(info.n_sorted) * (int(info.draw_blocks) + 1),
                                     torch.float64).data_ptr()

@@ -26,22 +26,37 @@ class History(object):
     label the (tid, value) observations in tid order.  ``dev`` holds the
     device copies of the observation columns (devhist.DeviceColumns per
     device); it lives as long as the append-only source it mirrors."""
-    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache')
+    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache', '_orders')
 
     def __init__(self, tids, losses, obs, dev=None, sorted_obs=True, cache=None):
         self.tids, self.losses, self.obs = tids, losses, obs
         self.dev = {} if dev is None else dev
         self.sorted_obs = sorted_obs     # every label's observation tids ascending
         self._cache = cache
+        self._orders = None
 
     def smallest(self, m):
         return None if self._cache is None else self._cache.smallest(m)
 
     def value_order(self, label):
         """A permutation sorting the label's (float) observation values
-        ascending, kept incrementally by the Trials cache; None without the
-        cache or when a value is NaN."""
-        return None if self._cache is None else self._cache.value_order(label)
+        ascending — kept incrementally by the Trials cache, else computed once
+        per History; None when a value is NaN."""
+        if self._cache is not None:
+            return self._cache.value_order(label)
+        # no Trials cache (columnar callers): one stable argsort per label and History
+        if self._orders is None:
+            self._orders = {}
+        perm = self._orders.get(label)
+        if perm is None:
+            vals = self.obs[label][1]
+            if vals.dtype.kind != 'f':
+                return None
+            perm = np.argsort(vals)          # any sorting permutation (ties: see fit_split)
+            if len(perm) and np.isnan(vals[perm[-1]]):
+                perm = False
+            self._orders[label] = perm
+        return None if perm is False else perm
 
     def __len__(self):
         return len(self.tids)
@@ -113,7 +128,7 @@ class _Cache(object):
         n = len(vals)
         perm = self.orders.get(k)
         if perm is None:
-            perm = np.argsort(vals, kind='stable')
+            perm = np.argsort(vals)
         elif len(perm) < n:
             new = np.arange(len(perm), n)
             nv = vals[new]

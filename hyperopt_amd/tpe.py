@@ -112,6 +112,11 @@ def _value(row, v):
     return np.int64(int(v)) if row.categorical else np.float64(v)
 
 
+def _column(row, values):
+    """_value over a float64 array of results (numpy scalars, one C loop)."""
+    return list(values.astype(np.int64)) if row.categorical else list(np.asarray(values, dtype=np.float64))
+
+
 def _run(engine, problems, C, seed, shard):
     if shard is None:
         return engine.run_level(problems, C, seed)
@@ -185,15 +190,16 @@ def _choices_fused(table, fits, new_ids, seed, C, engine, shard):
     n = len(ids)
     order = table.level_order()
     chosen = [dict.fromkeys(order) for _ in new_ids]
-    idx, val = res['idx'].tolist(), res['value'].tolist()
+    idx = res['idx']
     for k, row in enumerate(rows):
-        for i in range(n):
-            if idx[k * n + i] < 0:
-                raise RuntimeError('no candidate selected for %r' % row.label)
-            v = _value(row, val[k * n + i])
-            if pred[row.label] >= 0 and int(v) != pred[row.label]:
-                return None
-            chosen[i][row.label] = v
+        if (idx[k * n:(k + 1) * n] < 0).any():
+            raise RuntimeError('no candidate selected for %r' % row.label)
+        col = _column(row, res['value'][k * n:(k + 1) * n])
+        if pred[row.label] >= 0 and any(int(v) != pred[row.label] for v in col):
+            return None
+        lab = row.label
+        for d, v in zip(chosen, col):
+            d[lab] = v
     return chosen
 
 
@@ -203,16 +209,18 @@ def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
         if fused is not None:
             return fused
     ids = np.asarray(new_ids, dtype=np.int64)
-    chosen = [dict() for _ in new_ids]
+    chosen = [dict.fromkeys(table.level_order()) for _ in new_ids]
+    every = list(range(len(new_ids)))
     for level in table.levels():
         problems, rows, members = [], [], []
         for row in level:
-            act = [i for i, c in enumerate(chosen) if table.active(row, c)]
-            for i, c in enumerate(chosen):
-                c.setdefault(row.label, None)
+            if row.parents == [None]:          # unconditional: active for every id
+                act = every
+            else:
+                act = [i for i, c in enumerate(chosen) if table.active(row, c)]
             if not act:
                 continue
-            problems.append(LevelProblem(fits.get(row), row.index, ids[act]))
+            problems.append(LevelProblem(fits.get(row), row.index, ids if act is every else ids[act]))
             rows.append(row)
             members.append(act)
         if not problems:
@@ -220,12 +228,13 @@ def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
         res = _run(engine, problems, C, seed, shard)
         k = 0
         for row, act in zip(rows, members):
-            for i in act:
-                r = res[k]
-                k += 1
-                if r['idx'] < 0:
-                    raise RuntimeError('no candidate selected for %r' % row.label)
-                chosen[i][row.label] = _value(row, r['value'])
+            if (res['idx'][k:k + len(act)] < 0).any():
+                raise RuntimeError('no candidate selected for %r' % row.label)
+            col = _column(row, res['value'][k:k + len(act)])
+            k += len(act)
+            lab = row.label
+            for i, v in zip(act, col):
+                chosen[i][lab] = v
     return chosen
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 6
+#define TPE_ABI_VERSION 7
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -55,7 +55,8 @@ enum {
 /* problem flags */
 enum {
   TPE_F_HAS_LOW = 1,   /* low bound present (reference: low is not None)   */
-  TPE_F_HAS_HIGH = 2   /* high bound present                                */
+  TPE_F_HAS_HIGH = 2,  /* high bound present                                */
+  TPE_F_POOLED = 4     /* candidates pooled with the other ids of the label (see "Pooled labels") */
 };
 
 /* tpe_batch.flags / tpe_level_run flags */
@@ -105,6 +106,16 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  * [0, sort_count) of the batch; the sort key is sort_slot << key_bits | value
  * bucket.  Other problems' candidates follow and are never sorted.
  *
+ * Pooled labels (a pruned label active for several ids of the level — batched
+ * suggest): its problems share the mixtures, so their candidates are sorted as ONE
+ * population (one sort slot, key bits sized for n_ids x n_cand) and every wave
+ * spans a narrow range however small n_cand is.  A sorted position may then hold
+ * any of the label's problems' candidates: the scoring stages fold each candidate
+ * into its own problem's pool_best[problem] (atomicMax of a u64 key: the f64 score
+ * mapped to an order-preserving integer, its low bits replaced by the
+ * complemented candidate index — np.argmax order at ~2^-40 relative score
+ * resolution), and k_select re-evaluates the winner's l and g exactly.
+ *
  * Ordered draws (TPE_BATCH_ORDERED_DRAWS; device-drawn sorted problems at
  * TPE_PREC_F32): instead of C i.i.d. draws that are then sorted, the
  * sample stage draws the C order statistics of C uniforms,
@@ -149,7 +160,7 @@ typedef struct tpe_problem {
   float prior_mu, prior_a, prior_c, narrow_cmax;
   float narrow_amin, grid_lo, grid_inv;
   float key_lo, key_inv; /* sort-key bucket of t: floor((t - key_lo) * key_inv)  */
-  float reserved_f;
+  int32_t pool_first;    /* pooled: the label's first problem (else -1)         */
   uint32_t key0, key1;   /* Philox-4x32-10 key (suggest seed)                  */
   uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
 } tpe_problem;
@@ -267,6 +278,7 @@ typedef struct tpe_batch {
   int64_t fit_max_seg;        /* longest fit segment (<= 8192: sorted in LDS, no fit_tmp use) */
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
   double* draw_pref; int64_t draw_blocks; int32_t n_sorted; int32_t reserved5;
+  unsigned long long* pool_best;   /* [n_problems] (pooled problems; see "Pooled labels") */
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
@@ -341,6 +353,7 @@ typedef struct tpe_pack_info {
   int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
   int64_t fit_max_seg;                  /* tpe_batch.fit_max_seg */
   int64_t n_sorted, draw_blocks;        /* tpe_batch.n_sorted / draw_blocks */
+  int64_t n_pooled;                     /* pooled problems (tpe_batch.pool_best needed) */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation
@@ -402,11 +415,13 @@ typedef struct tpe_level_ws {
   uint32_t* fit_vals; uint32_t* fit_vals_sorted; int64_t fit_cap;   /* elements                    */
   void* fit_tmp; int64_t fit_tmp_bytes;
   double* draw_pref; int64_t draw_pref_cap;    /* elements                                              */
+  unsigned long long* pool_best; int64_t pool_best_cap;   /* elements                                   */
 } tpe_level_ws;
 
 /* what a level needs (written on success and on TPE_E_SPACE) */
 typedef struct tpe_level_need {
-  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes, draw_pref;
+  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes, draw_pref,
+      pool_best;
 } tpe_level_need;
 
 /* Run one tree level: `labels` as for tpe_host_pack_level; `out` receives one

@@ -207,6 +207,41 @@ def test_ordered_draws_distribution(engine):
         assert abs(res_iid[0]['score'] - res[0]['score']) <= 0.05 * max(1.0, abs(res[0]['score'])), dist
 
 
+def test_pooled_label_matches_single_problems(engine):
+    """A pruned label active for several ids is pooled (one sort for all its
+    problems, per-problem winners by atomicMax): every id draws what it draws
+    alone, its winner lies in the oracle's eps-tie set of those draws, the
+    reported l and g are the oracle's at the winner, and a rerun is
+    bit-identical."""
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(17)
+    for dist, args in (('uniform', dict(low=-5.0, high=5.0)), ('loguniform', dict(low=-4.0, high=3.0))):
+        below, above = rs.uniform(-4, 3, 20), rs.uniform(-4, 3, 3000)
+        if dist == 'loguniform':
+            below, above = np.exp(below), np.exp(above)
+        post = parzen.fit_posterior(dist, args, below, above, 1.0)
+        lpdf = O.lgmm1_lpdf if dist == 'loguniform' else O.gmm1_lpdf
+        ids = list(range(40, 49))
+        C = 3000
+        res, cand, l, g = engine.run([LevelProblem(post, 2, ids)], C, seed=5, want_lg=True, return_cand=True)
+        again = engine.run([LevelProblem(post, 2, ids)], C, seed=5)
+        np.testing.assert_array_equal(again, res)
+        for i, nid in enumerate(ids):
+            one, cand1 = engine.run([LevelProblem(post, 2, [nid])], C, seed=5, return_cand=True)
+            np.testing.assert_array_equal(cand1[0], cand[i])               # the id's own Philox stream
+            lb = lpdf(cand[i], *post.below, low=post.low, high=post.high)
+            la = lpdf(cand[i], *post.above, low=post.low, high=post.high)
+            _check_lpdf(l[i], lb, 1e-5, (dist, 'pooled l'))
+            _check_lpdf(g[i], la, 1e-5, (dist, 'pooled g'))
+            k = int(res[i]['idx'])
+            _check_argmax(k, lb, la, 1e-5, (dist, 'pooled'))
+            assert res[i]['value'] == cand[i][k] and res[i]['global_idx'] == k
+            assert abs(res[i]['l'] - lb[k]) <= 1e-5 * max(1.0, abs(lb[k]))
+            assert abs(res[i]['g'] - la[k]) <= 1e-5 * max(1.0, abs(la[k]))
+            assert abs(res[i]['score'] - one[0]['score']) <= 4e-5 * max(1.0, abs(one[0]['score']))
+
+
 def test_sharding_matches_single_device(engine):
     """Philox counters are global candidate indices, so every shard count draws
     the same candidate set.  Scores agree to fp32 rounding (pruned windows and

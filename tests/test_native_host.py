@@ -130,8 +130,6 @@ def test_native_pack_matches_numpy_packer(precision):
         assert info.part_total == ref['part_total']
         prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, P)
         for f in N.PROBLEM_DTYPE.names:
-            if f == 'reserved_f':
-                continue
             np.testing.assert_allclose(prob[f].astype(float), ref['prob'][f].astype(float), rtol=1e-6, atol=0,
                                        err_msg=f)
         np.testing.assert_array_equal(_blob(e, info, info.off_tiles, N.TILE_DTYPE, info.n_tiles), ref['tiles'])
