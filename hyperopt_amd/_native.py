@@ -15,7 +15,7 @@ ABI_VERSION = 7
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH, F_POOLED = 1, 2, 4
+F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY = 1, 2, 4, 8
 BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS = 1, 2, 4, 8
 PREC_F32, PREC_F64 = 0, 1
 

@@ -370,6 +370,21 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         samp.insert(samp.end(), row, row + 8);
       }
       p.samp_len = (int32_t)k;
+      // lazy scoring (TPE_F_CAT_LAZY): the winner is the best-scoring drawable
+      // category (np.argmax order: NaN first, then value, then index)
+      if (k <= 64 && L.above_k == k) {
+        const double* row0 = samp.data() + 8 * (size_t)p.samp_off;
+        int64_t c1 = -1;
+        double s1 = 0, p1 = 0;
+        for (int64_t i = 0; i < k; ++i) {
+          const double lo = i ? row0[8 * (i - 1)] : 0.0, pi = row0[8 * i] - lo;
+          if (!(pi > 0)) continue;
+          const double sc = log(L.below_w[i]) - log(L.above_w[i]);
+          const bool win = c1 < 0 || (sc != sc ? s1 == s1 : sc > s1);
+          if (win) { c1 = i; s1 = sc; p1 = pi; }
+        }
+        if (c1 >= 0 && p1 >= 1.0 / 65536) p.flags |= TPE_F_CAT_LAZY;
+      }
     } else {
       const int64_t k = L.below_k;
       std::vector<double> sel((size_t)k), fa((size_t)k), fb((size_t)k), flip((size_t)k);

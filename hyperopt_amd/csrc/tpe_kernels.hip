@@ -507,6 +507,8 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
   const bool valid = i < p.n_cand;
   const int64_t o = p.cand_off + i;
   if (draw && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= kCumLds) {
+    // lazy categorical: the select stage scans the first draws itself
+    if ((p.flags & TPE_F_CAT_LAZY) && !(flags & TPE_BATCH_WRITE_CAND) && !l_out) return;
     // The score of a categorical candidate depends only on its category, so the
     // slice's argmax (np.argmax: best score, then first index) is the best
     // category among those drawn, at its first draw.  First index per category:
@@ -1152,6 +1154,53 @@ __device__ double sel_lse2(const float4* __restrict__ comp, int k0, int n, int k
   return mm + log2(sel_reduce<double, false>(sum, lds));
 }
 
+// lazy categorical (TPE_F_CAT_LAZY): draws scanned in index order, 1024 per
+// round, keeping each category's first index; stops once no undrawn drawable
+// category could beat the current best (np.argmax order via better(): an
+// undrawn category's index would exceed every drawn one) — after the first
+// round unless the best-scoring category is rare.
+__device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__ samp,
+                                const double4* __restrict__ comp64, tpe_result* __restrict__ result) {
+  __shared__ double cum[64], score[64];
+  __shared__ int first[64];
+  __shared__ int done;
+  const int K = p.samp_len;
+  const double* S = samp + 8 * (int64_t)p.samp_off;
+  if ((int)threadIdx.x < K) {
+    cum[threadIdx.x] = S[8 * threadIdx.x];
+    score[threadIdx.x] = comp64[p.below_off + threadIdx.x].x - comp64[p.above_off + threadIdx.x].x;
+    first[threadIdx.x] = INT_MAX;
+  }
+  __syncthreads();
+  tpe_best b{0, 0, 0, -1};
+  for (int base = 0; base < p.n_cand; base += kSelThreads) {
+    const int i = base + (int)threadIdx.x;
+    if (i < p.n_cand) atomicMin(&first[draw_category(p, cum, i)], i);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      b = tpe_best{0, 0, 0, -1};
+      for (int c = 0; c < K; ++c)
+        if (first[c] != INT_MAX && better(score[c], (int64_t)first[c], b.score, b.idx))
+          b = tpe_best{score[c], comp64[p.below_off + c].x, comp64[p.above_off + c].x, (int64_t)first[c]};
+      int more = b.idx < 0;
+      for (int c = 0; c < K && !more; ++c) {
+        const bool drawable = cum[c] > (c ? cum[c - 1] : 0.0);
+        more = first[c] == INT_MAX && drawable && better(score[c], INT64_MAX, b.score, b.idx);
+      }
+      done = !more;
+    }
+    __syncthreads();
+    if (done) break;
+  }
+  if (threadIdx.x == 0) {
+    tpe_result r;
+    r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
+    r.value = b.idx >= 0 ? (double)draw_category(p, cum, b.idx) : 0.0;
+    r.global_idx = b.idx >= 0 ? p.cand_base + b.idx : -1;
+    result[blockIdx.x] = r;
+  }
+}
+
 // pooled problem: the winner from pool_best, its value re-drawn, its l and g
 // evaluated exactly over the whole mixtures (one workgroup)
 __device__ void select_pooled(const tpe_problem& p, const unsigned long long* __restrict__ pool_best,
@@ -1192,8 +1241,13 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
                                                      const double* __restrict__ draw_pref, int64_t draw_blocks,
                                                      int ordered, const unsigned long long* __restrict__ pool_best,
                                                      const float4* __restrict__ comp32,
+                                                     const double4* __restrict__ comp64, int lazy_ok,
                                                      tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
+  if (lazy_ok && sampled && (p.flags & TPE_F_CAT_LAZY) && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= 64) {
+    select_cat_lazy(p, samp, comp64, result);
+    return;
+  }
   if (p.flags & TPE_F_POOLED) {            // problem-uniform
     select_pooled(p, pool_best, comp32, samp, cand, precision, sampled, result);
     return;
@@ -1730,7 +1784,8 @@ int tpe_select(const tpe_batch* b, void* stream) {
   if (b->n_problems == 0) return TPE_OK;
   hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
                      b->tile_best, b->cand, b->samp, b->precision, b->sample, b->draw_pref, b->draw_blocks,
-                     ordered_draws(b) ? 1 : 0, b->pool_best, (const float4*)b->comp32, b->result);
+                     ordered_draws(b) ? 1 : 0, b->pool_best, (const float4*)b->comp32, (const double4*)b->comp64,
+                     (!(b->flags & TPE_BATCH_WRITE_CAND) && !b->l_out) ? 1 : 0, b->result);
   return hip_check("tpe_select");
 }
 

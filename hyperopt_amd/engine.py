@@ -165,6 +165,19 @@ class Engine(object):
                         q=post.q if post.q is not None else 0.0, n_upper=post.upper)
             st = parzen.sampler_table(post)
             info['samp_off'], info['samp_len'] = ns, st.shape[0]
+            if fam == N.FAM_CATEGORICAL and 0 < st.shape[0] <= 64 and len(post.above[0]) == st.shape[0]:
+                # TPE_F_CAT_LAZY: best-scoring drawable category selected with p >= 2^-16
+                c1, s1, p1 = -1, 0.0, 0.0
+                for i in range(st.shape[0]):
+                    pi = st[i, 0] - (st[i - 1, 0] if i else 0.0)
+                    if not pi > 0:
+                        continue
+                    pa = float(post.above[0][i])
+                    sc = math.log(float(post.below[0][i])) - (math.log(pa) if pa > 0 else -math.inf)
+                    if c1 < 0 or ((s1 == s1) if sc != sc else sc > s1):
+                        c1, s1, p1 = i, sc, pi
+                if c1 >= 0 and p1 >= 1.0 / 65536:
+                    info['flags'] |= N.F_CAT_LAZY
             samp.append(st)
             ns += st.shape[0]
             if fam == N.FAM_CATEGORICAL:

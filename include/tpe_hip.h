@@ -56,7 +56,11 @@ enum {
 enum {
   TPE_F_HAS_LOW = 1,   /* low bound present (reference: low is not None)   */
   TPE_F_HAS_HIGH = 2,  /* high bound present                                */
-  TPE_F_POOLED = 4     /* candidates pooled with the other ids of the label (see "Pooled labels") */
+  TPE_F_POOLED = 4,    /* candidates pooled with the other ids of the label (see "Pooled labels") */
+  TPE_F_CAT_LAZY = 8   /* categorical, <= 64 categories, best-scoring drawable category with selection
+                          probability >= 2^-16: device-drawn batches without per-candidate outputs
+                          score it in the select stage by scanning draws in index order until no
+                          undrawn category can still win (usually one 1024-draw chunk) */
 };
 
 /* tpe_batch.flags / tpe_level_run flags */

@@ -242,6 +242,30 @@ def test_pooled_label_matches_single_problems(engine):
             assert abs(res[i]['score'] - one[0]['score']) <= 4e-5 * max(1.0, abs(one[0]['score']))
 
 
+def test_lazy_categorical_matches_full_scan(engine):
+    """TPE_F_CAT_LAZY: the select stage scans draws in index order until no
+    undrawn category can win; the result equals the full per-candidate path
+    (forced by asking for the candidates) — common, rare-but-lazy (several
+    rounds), too-rare (not lazy), undrawable and all-tied categories."""
+    from hyperopt_amd import _native as N
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    cases = [([0.2, 0.5, 0.3], [0.4, 0.3, 0.3]),
+             ([0.9997, 0.0003], [0.9999999, 1e-7]),
+             ([0.99999, 0.00001], [0.99999999, 1e-8]),
+             ([0.5, 0.0, 0.5], [0.3, 0.4, 0.3]),
+             ([0.25, 0.25, 0.5], [0.25, 0.25, 0.5])]
+    for pb, pa in cases:
+        post = parzen.Posterior('categorical', N.FAM_CATEGORICAL, None, None, None, (np.array(pb),),
+                                (np.array(pa),), len(pb))
+        for C in (1000, 1 << 18):
+            lazy = engine.run_level([LevelProblem(post, 4, [0, 1, 2])], C, seed=3)
+            full, cand = engine.run([LevelProblem(post, 4, [0, 1, 2])], C, seed=3, return_cand=True)
+            np.testing.assert_array_equal(lazy, full)
+            for k in range(3):
+                assert full[k]['value'] == cand[k][int(full[k]['idx'])]
+
+
 def test_sharding_matches_single_device(engine):
     """Philox counters are global candidate indices, so every shard count draws
     the same candidate set.  Scores agree to fp32 rounding (pruned windows and
