@@ -3,7 +3,6 @@
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 1
 run() {  # name counters...
   local name=$1; shift
   rm -rf gpurun_out/pmc/$name
