@@ -226,3 +226,24 @@ def test_split_below_incremental_matches_full():
             a = H.split_below(hist, gamma)
             b = H.split_below(plain, gamma)
             assert sorted(a.tolist()) == sorted(b.tolist()), (step, gamma)
+
+
+def test_lazy_categorical_flag_native_matches_numpy():
+    """TPE_F_CAT_LAZY is set by both packers alike: on when the best-scoring
+    drawable category has selection probability >= 2^-16, off when it is rarer,
+    and ignored by every non-categorical problem."""
+    cases = [([0.2, 0.5, 0.3], [0.4, 0.3, 0.3], True),
+             ([0.9997, 0.0003], [0.9999999, 1e-7], True),
+             ([0.99999, 0.00001], [0.99999999, 1e-8], False),
+             ([0.5, 0.0, 0.5], [0.3, 0.4, 0.3], True),
+             ([0.25, 0.25, 0.5], [0.25, 0.25, 0.5], True)]
+    e = _engine('fp32')
+    for pb, pa, lazy in cases:
+        post = parzen.Posterior('categorical', N.FAM_CATEGORICAL, None, None, None, (np.array(pb),),
+                                (np.array(pa),), len(pb))
+        lps = [LevelProblem(post, 4, [0, 1])]
+        ref = e._build_numpy(lps, 4096, 3, 10, None)
+        info = e._pack(lps, 4096, 3, 10, None)
+        prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, info.n_problems)
+        np.testing.assert_array_equal(prob['flags'], ref['prob']['flags'])
+        assert all(bool(f & N.F_CAT_LAZY) == lazy for f in prob['flags']), (pb, pa)
