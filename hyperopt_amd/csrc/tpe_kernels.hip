@@ -1161,27 +1161,33 @@ __device__ double sel_lse2(const float4* __restrict__ comp, int k0, int n, int k
 // round unless the best-scoring category is rare.
 __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__ samp,
                                 const double4* __restrict__ comp64, tpe_result* __restrict__ result) {
-  __shared__ double cum[64], score[64];
+  __shared__ double cum[64], score[64], lsh[64], gsh[64];   // l, g in LDS: no global loads in the serial scan
   __shared__ int first[64];
   __shared__ int done;
   const int K = p.samp_len;
   const double* S = samp + 8 * (int64_t)p.samp_off;
   if ((int)threadIdx.x < K) {
     cum[threadIdx.x] = S[8 * threadIdx.x];
-    score[threadIdx.x] = comp64[p.below_off + threadIdx.x].x - comp64[p.above_off + threadIdx.x].x;
+    lsh[threadIdx.x] = comp64[p.below_off + threadIdx.x].x;
+    gsh[threadIdx.x] = comp64[p.above_off + threadIdx.x].x;
+    score[threadIdx.x] = lsh[threadIdx.x] - gsh[threadIdx.x];
     first[threadIdx.x] = INT_MAX;
   }
   __syncthreads();
   tpe_best b{0, 0, 0, -1};
   for (int base = 0; base < p.n_cand; base += kSelThreads) {
     const int i = base + (int)threadIdx.x;
-    if (i < p.n_cand) atomicMin(&first[draw_category(p, cum, i)], i);
+    const int c = i < p.n_cand ? draw_category(p, cum, i) : -1;
+    for (int cc = 0; cc < K; ++cc) {       // one LDS atomic per wave and category
+      const unsigned long long m = __ballot(c == cc);
+      if ((threadIdx.x & 63) == 0 && m) atomicMin(&first[cc], base + (int)(threadIdx.x & ~63) + __builtin_ctzll(m));
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       b = tpe_best{0, 0, 0, -1};
       for (int c = 0; c < K; ++c)
         if (first[c] != INT_MAX && better(score[c], (int64_t)first[c], b.score, b.idx))
-          b = tpe_best{score[c], comp64[p.below_off + c].x, comp64[p.above_off + c].x, (int64_t)first[c]};
+          b = tpe_best{score[c], lsh[c], gsh[c], (int64_t)first[c]};
       int more = b.idx < 0;
       for (int c = 0; c < K && !more; ++c) {
         const bool drawable = cum[c] > (c ? cum[c - 1] : 0.0);
