@@ -1154,8 +1154,8 @@ __device__ double sel_lse2(const float4* __restrict__ comp, int k0, int n, int k
   return mm + log2(sel_reduce<double, false>(sum, lds));
 }
 
-// lazy categorical (TPE_F_CAT_LAZY): draws scanned in index order, 1024 per
-// round, keeping each category's first index; stops once no undrawn drawable
+// lazy categorical (TPE_F_CAT_LAZY): draws scanned in index order, 4096 per
+// round (4 per thread), keeping each category's first index; stops once no undrawn drawable
 // category could beat the current best (np.argmax order via better(): an
 // undrawn category's index would exceed every drawn one) — after the first
 // round unless the best-scoring category is rare.
@@ -1175,13 +1175,21 @@ __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__
   }
   __syncthreads();
   tpe_best b{0, 0, 0, -1};
-  for (int base = 0; base < p.n_cand; base += kSelThreads) {
-    const int i = base + (int)threadIdx.x;
-    const int c = i < p.n_cand ? draw_category(p, cum, i) : -1;
-    for (int cc = 0; cc < K; ++cc) {       // one LDS atomic per wave and category
-      const unsigned long long m = __ballot(c == cc);
-      if ((threadIdx.x & 63) == 0 && m) atomicMin(&first[cc], base + (int)(threadIdx.x & ~63) + __builtin_ctzll(m));
+  constexpr int kLazyPer = 4;              // draws per thread per round
+  for (int base = 0; base < p.n_cand; base += kLazyPer * kSelThreads) {
+    int c[kLazyPer];
+#pragma unroll
+    for (int j = 0; j < kLazyPer; ++j) {
+      const int i = base + j * kSelThreads + (int)threadIdx.x;
+      c[j] = i < p.n_cand ? draw_category(p, cum, i) : -1;
     }
+#pragma unroll
+    for (int j = 0; j < kLazyPer; ++j)
+      for (int cc = 0; cc < K; ++cc) {     // one LDS atomic per wave and category
+        const unsigned long long m = __ballot(c[j] == cc);
+        if ((threadIdx.x & 63) == 0 && m)
+          atomicMin(&first[cc], base + j * kSelThreads + (int)(threadIdx.x & ~63) + __builtin_ctzll(m));
+      }
     __syncthreads();
     if (threadIdx.x == 0) {
       b = tpe_best{0, 0, 0, -1};
@@ -1287,6 +1295,22 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
     const double sc = exp_block_scan(p, g >> 6);
     U = (row[g >> 6] + __shfl(sc, (int)(g & 63))) / row[draw_blocks];
   }
+  // i.i.d. redraw with <= 64 below components: the component search of draw_one
+  // as one wave-wide compare + ballot (first k with u < cum_k, else K-1: the
+  // binary search's answer on a non-decreasing CDF) instead of a chain of
+  // dependent global loads on lane 0
+  const bool wave_search = redraw && !od && p.samp_len <= 64;
+  int comp = 0;
+  U4 rw{0, 0, 0, 0};
+  if (wave_search) {
+    const double* S = samp + 8 * (int64_t)p.samp_off;
+    const uint64_t g = (uint64_t)p.cand_base + (uint64_t)b.idx;
+    rw = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+    const int lane = (int)threadIdx.x;
+    const bool hit = lane < p.samp_len && u01d(rw.x, rw.y) < S[8 * lane];
+    const unsigned long long m = __ballot(hit);
+    comp = m ? __builtin_ctzll(m) : p.samp_len - 1;
+  }
   if (threadIdx.x == 0) {
     tpe_result r;
     r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
@@ -1297,7 +1321,9 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
       f32_bounds(p, lo_f, hi_f);
       const double* S = samp + 8 * (int64_t)p.samp_off;
       if (od) ordered_draw(p, S, S, 8, U, precision, lo_f, hi_f, r.value, t);
-      else draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
+      else if (!wave_search) draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
+      else if (p.family == TPE_FAM_CATEGORICAL) r.value = (double)comp;
+      else draw_comp(p, S, comp, u01f(rw.z), u01d(rw.z, rw.w), precision, lo_f, hi_f, r.value, t);
     } else if (b.idx >= 0) {
       r.value = cand[p.cand_off + b.idx];
     }
