@@ -1258,6 +1258,18 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
                                                      const double4* __restrict__ comp64, int lazy_ok,
                                                      tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
+#ifdef TPE_SELECT_TRACE                    // debug builds only: per-block path and duration
+  const uint64_t t_start = wall_clock64();
+  struct Tr {
+    uint64_t t0; const tpe_problem& q;
+    __device__ ~Tr() {
+      if (threadIdx.x == 0)
+        printf("k_select blk %d fam %d flags %d samp_len %d n_tiles %d n_cand %d ticks %llu\n", (int)blockIdx.x,
+               (int)q.family, (int)q.flags, (int)q.samp_len, (int)q.n_tiles, (int)q.n_cand,
+               (unsigned long long)(wall_clock64() - t0));
+    }
+  } tr{t_start, p};
+#endif
   if (lazy_ok && sampled && (p.flags & TPE_F_CAT_LAZY) && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= 64) {
     select_cat_lazy(p, samp, comp64, result);
     return;
@@ -1265,6 +1277,14 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
   if (p.flags & TPE_F_POOLED) {            // problem-uniform
     select_pooled(p, pool_best, comp32, samp, cand, precision, sampled, result);
     return;
+  }
+  // the sampler rows of a <= 64-component mixture staged in LDS while the tile
+  // bests load, so the winner's redraw needs no dependent global loads
+  __shared__ double srow[64 * 8];
+  const bool staged = sampled && p.samp_len > 0 && p.samp_len <= 64;
+  if (staged) {
+    const double* S = samp + 8 * (int64_t)p.samp_off;
+    for (int q = threadIdx.x; q < 8 * p.samp_len; q += kSelThreads) srow[q] = S[q];
   }
   tpe_best b{0, 0, 0, -1};
   const int64_t nb = (int64_t)p.n_tiles * TPE_BEST_PER_TILE;
@@ -1299,11 +1319,11 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
   // as one wave-wide compare + ballot (first k with u < cum_k, else K-1: the
   // binary search's answer on a non-decreasing CDF) instead of a chain of
   // dependent global loads on lane 0
-  const bool wave_search = redraw && !od && p.samp_len <= 64;
+  const bool wave_search = redraw && !od && staged;
   int comp = 0;
   U4 rw{0, 0, 0, 0};
   if (wave_search) {
-    const double* S = samp + 8 * (int64_t)p.samp_off;
+    const double* S = srow;
     const uint64_t g = (uint64_t)p.cand_base + (uint64_t)b.idx;
     rw = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
     const int lane = (int)threadIdx.x;
@@ -1323,7 +1343,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
       if (od) ordered_draw(p, S, S, 8, U, precision, lo_f, hi_f, r.value, t);
       else if (!wave_search) draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
       else if (p.family == TPE_FAM_CATEGORICAL) r.value = (double)comp;
-      else draw_comp(p, S, comp, u01f(rw.z), u01d(rw.z, rw.w), precision, lo_f, hi_f, r.value, t);
+      else draw_comp(p, srow, comp, u01f(rw.z), u01d(rw.z, rw.w), precision, lo_f, hi_f, r.value, t);
     } else if (b.idx >= 0) {
       r.value = cand[p.cand_off + b.idx];
     }
