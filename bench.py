@@ -57,8 +57,11 @@ def synthetic_loss(v, tid):
     return loss + 1e-9 * tid
 
 
-def make_history(n, seed):
+def make_history(n, seed, loss=None):
+    """``n`` prior draws of the config-3 tree space (rand.suggest) with losses
+    from ``loss(vals, tid)`` (default synthetic_loss)."""
     from hyperopt_amd import base, hp, rand
+    loss = synthetic_loss if loss is None else loss
     domain = base.Domain(lambda d: 0.0, tree_space(hp))
     trials = base.Trials()
     rs = np.random.RandomState(seed)
@@ -67,16 +70,37 @@ def make_history(n, seed):
         d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
         v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
         d['state'] = base.JOB_STATE_DONE
-        d['result'] = {'status': 'ok', 'loss': synthetic_loss(v, tid)}
+        d['result'] = {'status': 'ok', 'loss': loss(v, tid)}
         docs.append(d)
     trials.insert_trial_docs(docs)
     trials.refresh()
     return domain, trials
 
 
-def cpu_baseline(domain, trials, budget_s=15.0):
-    """The oracle (numpy, 1 thread) on a bounded sample: whole suggests at
-    C=16384 on the same history, repeated until ~budget_s of CPU work."""
+def host_cpu():
+    """Model and core counts of this host (the GPU box's host when run there)."""
+    model = ''
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    return dict(model=model, logical_cpus=os.cpu_count(), usable_cpus=aff)
+
+
+def cpu_baseline(domain, trials, budget_s=12.0, max_procs=16):
+    """The oracle (numpy restatement of the reference, tools/oracle_vs_reference.py
+    times it against the reference itself) on a bounded sample of the same
+    workload: whole suggests at C = 16384 on the same 10k-trial history, for
+    ~budget_s each (1) on one core and (2) candidate-chunked over a process pool
+    of min(max_procs, usable cores) — chunking is exact, logsum_rows is
+    row-wise (tpe.py:253-256); sampling stays serial, as in the reference.
+    Called before the GPU is initialised (the pool forks)."""
+    import multiprocessing as mp
     from oracle import tpe_oracle as O
     try:
         from threadpoolctl import threadpool_limits
@@ -89,16 +113,29 @@ def cpu_baseline(domain, trials, budget_s=15.0):
         params.append(dict(label=r.label, dist=r.dist, args=dict(r.args), parent=parent))
     hist = [dict(tid=d['tid'], loss=d['result']['loss'], vals=d['misc']['vals']) for d in trials.trials]
     C = 16384
-    n_scores, t0, calls = 0, time.time(), 0
-    while time.time() - t0 < budget_s:
-        out = O.tpe_suggest(params, hist, 1000 + calls, n_EI_candidates=C)
-        n_scores += len(out) * C
-        calls += 1
-    dt = time.time() - t0
+
+    def run(pool, chunks):
+        n_scores, calls, t0 = 0, 0, time.time()
+        while time.time() - t0 < budget_s:
+            out = O.tpe_suggest(params, hist, 1000 + calls, n_EI_candidates=C, pool=pool, chunks=chunks)
+            n_scores += len(out) * C
+            calls += 1
+        dt = time.time() - t0
+        return n_scores / dt, calls, dt
+
+    v1, c1, d1 = run(None, 1)
+    cpu = host_cpu()
+    P = max(1, min(max_procs, cpu['usable_cpus']))
+    with mp.get_context('fork').Pool(P) as pool:
+        vp, cp, dp = run(pool, P)
     if limiter is not None:
         limiter.unregister()
-    return dict(value=n_scores / dt, unit='candidate-scores/s', cores=1, kind='port',
-                sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, %.1fs' % (calls, dt))
+    return dict(value=v1, unit='candidate-scores/s', cores=1, kind='port',
+                sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, %.1fs, 1 core' % (c1, d1),
+                all_core=dict(value=vp, cores=P, speedup=vp / v1,
+                              sample='%d oracle tpe_suggest calls, C=16384, candidate scoring chunked over %d '
+                                     'processes, %.1fs' % (cp, P, dp)),
+                host=cpu)
 
 
 # ------------------------------------------------------------------ roofline
@@ -278,6 +315,14 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    pre = None
+    cpu = None
+    if args.config == 3:
+        pre = make_history(args.history, SEED)
+        # the CPU baseline runs first, before anything initialises the GPU
+        # (its process pool forks); rank 0 at N = 1 only
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(*pre)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
@@ -289,7 +334,7 @@ def main():
     get_engine(device)
     if args.config != 3:
         return run_other(args, rank, world, device)
-    domain, trials = make_history(args.history, SEED)
+    domain, trials = pre
     new_id = args.history
     shard = (rank, world) if world > 1 else None
     C_total = args.cands * world
@@ -332,9 +377,6 @@ def main():
     roof, kernels = roofline(prof)
     stages = {k: float(np.mean([a[0] for a in v])) for k, v in prof.items()}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(domain, trials)
 
     if rank == 0:
         out = {

@@ -8,6 +8,9 @@ SRC = os.path.join(HERE, 'csrc', 'tpe_kernels.hip')
 HOST_SRC = os.path.join(HERE, 'csrc', 'tpe_host.cpp')
 OUT = os.path.join(HERE, 'libtpe_hip.so')
 ARCH = os.environ.get('TPE_OFFLOAD_ARCH', 'gfx950')
+# host ISA baseline of the runtime (any x86-64 host); the vectorised pack loops
+# carry their own AVX2 clones (target_clones), picked at load time
+HOST_MARCH = os.environ.get('TPE_HOST_MARCH', 'x86-64-v2')
 
 
 def build(force=False, verbose=False, out=OUT, defines=()):
@@ -25,7 +28,7 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
     dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o' if not defines else tag + '.o')
     cmds = [
-        [gxx, '-O3', '-march=x86-64-v3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
+        [gxx, '-O3', '-march=' + HOST_MARCH, '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
          '-fno-trapping-math', '-Wall',
          '-c', HOST_SRC, '-o', host_o],
         [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',

@@ -291,6 +291,10 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
   return tpe_host_cat_probs(side[1].data(), (int64_t)side[1].size(), upper, p_prior, prior_weight, lf, out_above);
 }
 
+// the pack's straight-line table loops vectorise: an AVX2 clone is picked at
+// load time on hosts that have it (-ffp-contract=off holds in both clones, so
+// the tables are bit-identical)
+__attribute__((target_clones("avx2", "default")))
 int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
                         int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
                         tpe_pack_info* info) {
@@ -655,11 +659,14 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
   }
   // splits of the above mixture per tile.  Bulk tiles: enough work items to fill
-  // the chip (a function of the GLOBAL candidate count, so every candidate sums
-  // its components in the same grouping whatever the sharding).  Pruned problems
-  // with many tiles: the bulk is cheap (local expansion), so one split, and the
+  // the chip (a function of the GLOBAL candidate count).  Pruned problems with
+  // many tiles: the bulk is cheap (local expansion), so one split, and the
   // outermost tiles of the (local) sorted range — the sparse tails, whose waves
-  // span wide windows evaluated exactly — get geometrically more.
+  // span wide windows evaluated exactly — get geometrically more.  A shard sorts
+  // and windows only its own candidates and counts its tails in its own tiles,
+  // so under candidate sharding the fp32 sums (and near-tie winners) can differ
+  // from a single-device run in the last bits: sharded winners agree within the
+  // eps-tie set, not bit for bit (the draws themselves are identical).
   const int64_t tiles_ref = (C_ref + T - 1) / T;
   const int64_t scored_tiles = scored * tiles_ref;
   const int64_t target = std::max<int64_t>(1, (target_work() + std::max<int64_t>(scored_tiles, 1) - 1) /

@@ -513,6 +513,7 @@ class Engine(object):
         if n_cand < 0 or n_cand >= 2 ** 31:
             raise ValueError('n_EI_candidates out of range: %r' % n_cand)
         info = self._pack(problems, n_cand, seed, cand_base, n_cand_global)
+        self._last_info = info
         P = int(info.n_problems)
         if P == 0:
             return np.zeros(0, dtype=N.RESULT_DTYPE)
@@ -638,6 +639,19 @@ class Engine(object):
             out.append(per_problem(d_l))
             out.append(per_problem(d_g))
         return tuple(out)
+
+    def device_tables(self):
+        """(problems, comp32) of the last ``run`` as the device holds them after
+        its stages ran — device-fitted above rows and the problem fields the fit
+        patches included (tests of the device Parzen fit read them back)."""
+        info = self._last_info
+        nb = int(info.blob_bytes)
+        blob = self._bufs['blob'][:nb].cpu().numpy()
+        prob = np.frombuffer(blob, dtype=N.PROBLEM_DTYPE, count=int(info.n_problems),
+                             offset=int(info.off_problems)).copy()
+        o = int(info.off_comp32)
+        comp32 = np.frombuffer(blob[o:o + (nb - o) // 16 * 16], dtype=np.float32).reshape(-1, 4).copy()
+        return prob, comp32
 
     def _run_profiled(self, b, stream, tb, n_cand):
         """The same launches as tpe_run_batch, one stage at a time, bracketed

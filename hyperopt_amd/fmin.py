@@ -137,7 +137,8 @@ def fmin_path(objective, space, max_evals, path):
     try:
         with open(path, 'rb') as f:
             trials = pickle.load(f)
-    except (OSError, IOError, EOFError):
+    except Exception:                 # any unreadable file starts fresh, as the reference's bare except
+        logger.info('No trial file at %s, creating a new one', path)
         trials = base.Trials()
     try:
         fmin(objective, space=space, algo=tpe.suggest, max_evals=len(trials) + max_evals, trials=trials)

@@ -222,7 +222,13 @@ def extract(domain, trials):
         cache = None
     if cache is not None:
         n = len(cache.docs)
-        if n > len(docs) or (n and (docs[0] is not cache.docs[0] or docs[n - 1] is not cache.docs[n - 1])):
+        # the cache assumes Trials is append-only (FMinIter's use): documents
+        # already seen stay where they are and keep their values.  Dropped
+        # (ERROR) or replaced documents shift or change the documents it
+        # checks — both ends and 7 evenly spaced positions — and force a rebuild.
+        if n > len(docs) or (n and any(docs[i] is not cache.docs[i] for i in
+                                       {0, n - 1, n // 8, n // 4, 3 * n // 8, n // 2, 5 * n // 8, 3 * n // 4,
+                                        7 * n // 8})):
             cache = None
     if cache is None:
         cache = _Cache(labels, {r.label: r.categorical for r in table.rows})

@@ -470,12 +470,29 @@ def history_arrays(history):
     return tids, losses, docs
 
 
+def _lpdf_chunk(job):
+    post, cand = job
+    return post.lpdf(cand)
+
+
+def _lpdf(post, cand, pool, chunks):
+    """post.lpdf(cand), optionally split over a process pool by candidate
+    chunks — bit-identical, because every lpdf is computed row by row
+    (logsum_rows, tpe.py:253-256; the quantized per-component loop is
+    elementwise)."""
+    if pool is None or chunks < 2 or post.kind == 'categorical' or len(cand) < 2 * chunks:
+        return post.lpdf(cand)
+    return np.concatenate(pool.map(_lpdf_chunk, [(post, c) for c in np.array_split(cand, chunks)]))
+
+
 def tpe_suggest(params, history, seed, prior_weight=1.0, n_startup_jobs=20,
-                n_EI_candidates=24, gamma=0.25, LF=DEFAULT_LF, trace=None):
+                n_EI_candidates=24, gamma=0.25, LF=DEFAULT_LF, trace=None, pool=None, chunks=1):
     """tpe.py:804-897 for one new id.  Returns {label: value} of active labels.
 
     If ``trace`` is a dict it receives, per label, the fitted posteriors, the
-    candidates, l, g and the chosen index (for kernel-level fixtures)."""
+    candidates, l, g and the chosen index (for kernel-level fixtures).  With a
+    ``pool`` (multiprocessing) the candidate scoring is split into ``chunks``
+    (the all-core CPU baseline); the result is identical."""
     tids, losses, docs = history_arrays(history)
     if len(docs) < n_startup_jobs:
         return rand_suggest(params, seed)
@@ -493,8 +510,8 @@ def tpe_suggest(params, history, seed, prior_weight=1.0, n_startup_jobs=20,
         post_b = fit_posterior(p['dist'], p['args'], below, prior_weight, LF)
         post_a = fit_posterior(p['dist'], p['args'], above, prior_weight, LF)
         cand = post_b.sample(rng, n_EI_candidates)
-        l = post_b.lpdf(cand)
-        g = post_a.lpdf(cand)
+        l = _lpdf(post_b, cand, pool, chunks)
+        g = _lpdf(post_a, cand, pool, chunks)
         best = broadcast_best_index(l, g)
         chosen[label] = cand[best]
         if trace is not None:

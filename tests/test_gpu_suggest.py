@@ -199,3 +199,49 @@ def test_fused_levels_misprediction_falls_back():
     finally:
         tpe.SPECULATE = True
     assert got == ref
+
+
+def _resume_space():
+    from hyperopt_amd import hp
+    return {'x': hp.uniform('x', -5, 5), 'q': hp.quniform('q', 0, 10, 1),
+            'c': hp.choice('c', [0, {'y': hp.loguniform('y', -2, 1)}])}
+
+
+def _resume_obj(d):
+    return (d['x'] - 1) ** 2 + 0.05 * abs(d['q'] - 4) + (0.1 if d['c'] == 0 else float(d['c']['y']))
+
+
+def test_fmin_resume_through_tpe_matches_uninterrupted():
+    """Checkpoint / resume through TPE (fmin.py:147-175): 30 evals, pickle,
+    reload (the SoA history cache is rebuilt from the documents), 30 more with
+    the same RandomState stream == one uninterrupted 60-eval run — replay mode
+    (reference-exact) and the default Philox device sampler (deterministic)."""
+    import pickle
+    from hyperopt_amd import fmin, tpe, Trials
+    for algo in (tpe.suggest_replay, functools.partial(tpe.suggest, n_EI_candidates=4096)):
+        rs = np.random.RandomState(21)
+        t = Trials()
+        fmin(_resume_obj, _resume_space(), algo=algo, max_evals=30, trials=t, rstate=rs)
+        t2 = pickle.loads(pickle.dumps(t))
+        fmin(_resume_obj, _resume_space(), algo=algo, max_evals=60, trials=t2, rstate=rs)
+        ref = Trials()
+        fmin(_resume_obj, _resume_space(), algo=algo, max_evals=60, trials=ref, rstate=np.random.RandomState(21))
+        got = [d['misc']['vals'] for d in t2.trials]
+        want = [d['misc']['vals'] for d in ref.trials]
+        assert got == want and t2.losses() == ref.losses(), algo
+
+
+def test_fmin_path_resumes_through_tpe(tmp_path, monkeypatch):
+    """fmin_path: 25 evaluations (20 start-up + 5 TPE), dump, reload, 10 more
+    TPE evaluations; the first 25 documents survive unchanged."""
+    import importlib
+    F = importlib.import_module('hyperopt_amd.fmin')
+    monkeypatch.setenv('HYPEROPT_FMIN_SEED', '7')
+    path = str(tmp_path / 'trials.pkl')
+    t1 = F.fmin_path(_resume_obj, _resume_space(), 25, path)
+    first = [d['misc']['vals'] for d in t1.trials]
+    t2 = F.fmin_path(_resume_obj, _resume_space(), 10, path)
+    assert len(t2) == 35 and [d['misc']['vals'] for d in t2.trials][:25] == first
+    assert [d['tid'] for d in t2.trials] == list(range(35))
+    for d in t2.trials:
+        t2.assert_valid_trial(d)

@@ -1,0 +1,94 @@
+#!/usr/bin/env bash
+# One runner for every GPU-box task (the library is built on the CPU side
+# beforehand and travels in-tree).  Usage:
+#
+#   tools/gpu.sh TASK [TASK ...]        tasks run in order; the first failure ends the script
+#
+#   tests      -m gpu parity suite                       (PYTEST_ARGS)
+#   smoke      __graft_entry__.smoke()
+#   bench      headline bench.py                         (BENCH_ARGS)
+#   trace      rocprofv3 --kernel-trace --stats of a short headline bench run (BENCH_ARGS)
+#   pmc        PMC counter passes on the headline bench, one rocprofv3 run per group
+#   stage      steady-state per-stage device times        (REP)
+#   configs    bench.py --config 1, 2, 4, 5
+#   hostsplit  host-side time split of the headline suggest
+#   counters   rocprofv3 -L (the counters this box offers) -> gpurun_out/counters.txt
+#   libab      stage times + headline p50 per library variant in LIBS
+#              (hyperopt_amd/libtpe_hip_<name>.so; "default" = libtpe_hip.so)
+#
+# Outputs go to gpurun_out/<task>_<TAG>.*; every GPU step has its own time limit.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r02}
+O=gpurun_out
+
+step() {  # limit_seconds logfile cmd...
+  local lim=$1 log=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "FAILED ($rc): $*"; tail -40 "$log"
+    exit $rc
+  fi
+}
+
+prof_run() {  # name counters...
+  local name=$1; shift
+  rm -rf $O/pmc_${TAG}/$name
+  step 300 $O/pmc_${TAG}/$name.log rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
+      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
+}
+
+for task in "$@"; do
+  case $task in
+    tests)
+      step 900 $O/tests_${TAG}.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+          ${PYTEST_ARGS:-}
+      grep -E "PASSED|FAILED|ERROR|passed|failed" $O/tests_${TAG}.log | tail -60 ;;
+    smoke)
+      step 300 $O/smoke_${TAG}.log python -c "import __graft_entry__ as g; g.smoke()"
+      tail -3 $O/smoke_${TAG}.log ;;
+    bench)
+      step 600 $O/bench_${TAG}.err python bench.py ${BENCH_ARGS:-}
+      grep '^{' $O/bench_${TAG}.err > $O/bench_${TAG}.json; cat $O/bench_${TAG}.json ;;
+    trace)
+      rm -rf $O/trace_${TAG}
+      step 600 $O/trace_${TAG}.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_${TAG} -o run -- \
+          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-}
+      python3 tools/trace_summary.py $(find $O/trace_${TAG} -name "*kernel_trace.csv") > $O/trace_${TAG}_summary.txt
+      head -25 $O/trace_${TAG}_summary.txt ;;
+    pmc)
+      mkdir -p $O/pmc_${TAG}
+      prof_run fetch FETCH_SIZE
+      prof_run write WRITE_SIZE
+      prof_run valu SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+      prof_run wait SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU
+      if [ -n "${PMC_EXTRA:-}" ]; then prof_run extra $PMC_EXTRA; fi
+      python3 tools/pmc_summary.py $O/pmc_${TAG} > $O/pmc_${TAG}/summary.json
+      python3 -c "import json; print(json.dumps(json.load(open('$O/pmc_${TAG}/summary.json'))['traffic'], indent=1))" ;;
+    stage)
+      step 300 $O/stage_${TAG}.txt python tools/stage_bench.py ${REP:-20}
+      cat $O/stage_${TAG}.txt ;;
+    configs)
+      for c in 1 2 4 5; do
+        step 600 $O/cfg${c}_${TAG}.err python bench.py --config $c --steps ${CFG_STEPS:-5} --warmup 1
+        grep '^{' $O/cfg${c}_${TAG}.err > $O/cfg${c}_${TAG}.json; cat $O/cfg${c}_${TAG}.json
+      done ;;
+    hostsplit)
+      step 300 $O/hostsplit_${TAG}.txt python tools/host_split.py ${STEPS:-200}
+      cat $O/hostsplit_${TAG}.txt ;;
+    libab)
+      for v in ${LIBS:-default}; do
+        if [ "$v" = default ]; then lib=$PWD/hyperopt_amd/libtpe_hip.so; else lib=$PWD/hyperopt_amd/libtpe_hip_$v.so; fi
+        step 300 $O/stage_${TAG}_$v.txt env TPE_HIP_LIB=$lib python tools/stage_bench.py ${REP:-20}
+        step 300 $O/bench_${TAG}_$v.err env TPE_HIP_LIB=$lib python bench.py --no-cpu-baseline --steps 100
+        echo "$v: $(grep -o '"p50_suggest_ms": [0-9.]*\|"stage_ms": {[^}]*}' $O/bench_${TAG}_$v.err | tr '\n' ' ')"
+      done ;;
+    counters)
+      step 120 $O/counters.txt rocprofv3 -L
+      grep -o "SQ_[A-Z0-9_]*\|TCC_[A-Z0-9_]*\|TCP_[A-Z0-9_]*" $O/counters.txt | sort -u | tr '\n' ' ' | head -c 6000; echo ;;
+    *)
+      echo "unknown task $task"; exit 2 ;;
+  esac
+done
