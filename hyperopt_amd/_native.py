@@ -11,11 +11,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 7
+ABI_VERSION = 8
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY = 1, 2, 4, 8
+F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE = 1, 2, 4, 8, 16
+TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
 BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS = 1, 2, 4, 8
 PREC_F32, PREC_F64 = 0, 1
 
@@ -33,8 +34,12 @@ PROBLEM_DTYPE = np.dtype([
     ('narrow_amin', '<f4'), ('grid_lo', '<f4'), ('grid_inv', '<f4'),
     ('key_lo', '<f4'), ('key_inv', '<f4'), ('pool_first', '<i4'),
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
+    ('tab_mode', '<i4'), ('tab_off', '<i4', (2,)), ('tab_n', '<i4', (2,)), ('tab_lo', '<f4', (2,)),
+    ('tab_inv', '<f4', (2,)), ('reserved6', '<i4'), ('lat_lo', '<i8'),
 ])
-assert PROBLEM_DTYPE.itemsize == 192
+assert PROBLEM_DTYPE.itemsize == 240
+TAB_JOB_DTYPE = np.dtype([('problem', '<i4'), ('side', '<i4'), ('kind', '<i4'), ('n', '<i4'), ('off', '<i4'),
+                          ('block0', '<i4')])
 TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4'), ('work_first', '<i4'), ('n_splits', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
                        ('k_start', '<i4'), ('k_end', '<i4'), ('n_splits', '<i4')])
@@ -78,6 +83,8 @@ class Batch(ctypes.Structure):
         ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64), ('fit_max_seg', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_blocks', ctypes.c_int64), ('n_sorted', ctypes.c_int32),
         ('reserved5', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
+        ('tab_jobs', ctypes.c_void_p), ('n_tab_jobs', ctypes.c_int32), ('tab_blocks', ctypes.c_int32),
+        ('tab', ctypes.c_void_p), ('tab_units', ctypes.c_int64),
     ]
 
 
@@ -126,6 +133,8 @@ class PackInfo(ctypes.Structure):
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
         ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_seg', ctypes.c_int64),
         ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64), ('n_pooled', ctypes.c_int64),
+        ('off_tab_jobs', ctypes.c_int64), ('n_tab_jobs', ctypes.c_int64), ('tab_blocks', ctypes.c_int64),
+        ('tab_units', ctypes.c_int64),
     ]
 
 
@@ -146,6 +155,7 @@ class LevelWS(ctypes.Structure):
         ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_pref_cap', ctypes.c_int64),
         ('pool_best', ctypes.c_void_p), ('pool_best_cap', ctypes.c_int64),
+        ('tab', ctypes.c_void_p), ('tab_cap', ctypes.c_int64),
     ]
 
 
@@ -153,13 +163,13 @@ class LevelNeed(ctypes.Structure):
     """tpe_level_need: sizes one level needs."""
     _fields_ = [(k, ctypes.c_int64) for k in ('pinned_bytes', 'blob_bytes', 'cand', 'sort_tmp_bytes', 'part',
                                               'best', 'result', 'fit', 'fit_tmp_bytes',
-                                              'draw_pref', 'pool_best')]
+                                              'draw_pref', 'pool_best', 'tab')]
 
 
 E_SPACE = -4
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
-           'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above',
+           'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above', 'tpe_tables',
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run')
 
@@ -191,7 +201,7 @@ def load(path=LIB_PATH):
     lib.tpe_sort_workspace_bytes.restype = ctypes.c_int
     lib.tpe_fit_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]
     lib.tpe_fit_workspace_bytes.restype = ctypes.c_int
-    for name in ('tpe_run_batch', 'tpe_fit_above', 'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
+    for name in ('tpe_run_batch', 'tpe_fit_above', 'tpe_tables', 'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
         fn = getattr(lib, name)
         fn.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
         fn.restype = ctypes.c_int

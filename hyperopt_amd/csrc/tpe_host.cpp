@@ -52,6 +52,22 @@ int fine_key_bits() {
   return v;
 }
 constexpr int kTailMinTiles = 32;      // per-tile tail splits from 32 tiles (64k candidates) on
+// tabulated scoring (include/tpe_hip.h "Tabulated scoring")
+constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e)): a = kAScale / max(sigma, EPS)
+constexpr double kTabEta = 0.05;                  // a_max * h <= kTabEta for every cell of half-width h
+constexpr int64_t kTabMaxCells = 65536;           // per side; more: per-candidate scoring
+constexpr int64_t kTabMaxLattice = 1 << 18;       // lattice values per quantized label
+// TPE_TABLES=0 turns tabulated scoring off (A/B and tests); read per call
+bool tables_enabled() {
+  const char* e = getenv("TPE_TABLES");
+  return !(e && e[0] == '0');
+}
+// cells of one side: a_max * h <= kTabEta over [lo, hi) (sig_min: the side's smallest bandwidth)
+int64_t tab_cells(double lo, double hi, double sig_min) {
+  const double a_max = kAScale / std::max(sig_min, kEPS);
+  const double n = std::ceil((hi - lo) * a_max / (2.0 * kTabEta));
+  return n >= 1.0 && n < 1e15 ? (int64_t)n : -1;
+}
 // splits of the tile `e` tiles from either end of a pruned problem's sorted
 // range: the sparse tails are where waves span too wide a range for the local
 // expansion and evaluate their window exactly (measured on the config-3
@@ -150,6 +166,19 @@ inline double log2_normal(double x) {
   const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
   const double p = s * (2.0 + s2 * (2.0 / 3 + s2 * (2.0 / 5 + s2 * (2.0 / 7 + s2 * (2.0 / 9 + s2 * (2.0 / 11))))));
   return e + p * 1.4426950408889634074;
+}
+
+// value range of a label's kernel coordinate (x, or ln x for log families)
+// that its candidates fall in: the bounds, else the below mixture +- 8 sigma
+// (f32 draws stay within 5.5 sigma of their component); categories [0, upper)
+void coord_range(const tpe_label_in& L, double& klo, double& khi) {
+  if (L.family == TPE_FAM_CATEGORICAL) { klo = 0; khi = std::max(L.upper, 1); return; }
+  if ((L.flags & TPE_F_HAS_LOW) && (L.flags & TPE_F_HAS_HIGH)) { klo = L.low; khi = L.high; return; }
+  klo = INFINITY; khi = -INFINITY;
+  for (int64_t i = 0; i < L.below_k; ++i) {
+    klo = std::min(klo, L.below_mu[i] - 8 * L.below_sigma[i]);
+    khi = std::max(khi, L.below_mu[i] + 8 * L.below_sigma[i]);
+  }
 }
 
 }  // namespace
@@ -328,8 +357,54 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   comp32.reserve((size_t)(4 * ktot));
   comp64.reserve((size_t)(4 * ktot));
   samp.reserve((size_t)(8 * ktot));
+  // ---- tabulated scoring: which labels score from tables, and their geometry ----
+  const bool tab_on = tables_enabled();
+  std::vector<int32_t> tmode((size_t)n_labels, TPE_TAB_NONE);
+  std::vector<int64_t> tn0((size_t)n_labels, 0), tn1((size_t)n_labels, 0), tlat((size_t)n_labels, 0);
+  std::vector<double> tklo((size_t)n_labels, 0), tkhi((size_t)n_labels, 0);
+  for (int32_t li = 0; li < n_labels && tab_on && n_cand > 0; ++li) {
+    const tpe_label_in& L = labels[li];
+    const double ct = (double)L.n_ids * (double)n_cand;     // candidates of the label in this level
+    if (L.n_ids <= 0 || L.family == TPE_FAM_CATEGORICAL || L.below_k <= 0) continue;
+    double klo, khi;
+    coord_range(L, klo, khi);
+    if (!(std::isfinite(klo) && std::isfinite(khi) && khi > klo)) continue;
+    tklo[li] = klo; tkhi[li] = khi;
+    if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && !f64) {
+      double s0 = INFINITY, s1 = INFINITY;
+      for (int64_t i = 0; i < L.below_k; ++i) s0 = std::min(s0, L.below_sigma[i]);
+      if (dev_fit[li])           // the device fit clips every bandwidth to >= prior_sigma / min(100, 1 + K)
+        s1 = L.prior_sigma / std::min(100.0, 1.0 + (double)L.above_k);
+      else
+        for (int64_t i = 0; i < L.above_k; ++i) s1 = std::min(s1, L.above_sigma[i]);
+      const int64_t n0 = tab_cells(klo, khi, s0), n1 = L.above_k > 0 ? tab_cells(klo, khi, s1) : -1;
+      if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= (double)(n0 + n1)) {
+        tmode[li] = TPE_TAB_CELLS; tn0[li] = n0; tn1[li] = n1;
+      }
+    } else if ((L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) && L.q > 0 && L.above_k > 0 &&
+               !(L.flags & TPE_F_NO_TABLE)) {
+      // every value a device draw can take: bounded draws stay in [low, high];
+      // unbounded ones within 8.3 sigma of their component (53-bit uniforms)
+      double tlo = klo, thi = khi;
+      if (!((L.flags & TPE_F_HAS_LOW) && (L.flags & TPE_F_HAS_HIGH))) {
+        tlo = INFINITY; thi = -INFINITY;
+        for (int64_t i = 0; i < L.below_k; ++i) {
+          tlo = std::min(tlo, L.below_mu[i] - 9 * L.below_sigma[i]);
+          thi = std::max(thi, L.below_mu[i] + 9 * L.below_sigma[i]);
+        }
+      }
+      const bool lg = L.family == TPE_FAM_QLOGGAUSS;
+      const double xlo = lg ? exp(tlo) : tlo, xhi = lg ? exp(thi) : thi;
+      const double mlo = std::floor(xlo / L.q) - 1.0, mhi = std::ceil(xhi / L.q) + 1.0;
+      const double nl = mhi - mlo + 1.0;
+      if (std::isfinite(nl) && nl >= 1.0 && nl <= (double)kTabMaxLattice && std::fabs(mlo) < 9e15 &&
+          ct >= 2.0 * nl) {
+        tmode[li] = TPE_TAB_LATTICE; tn0[li] = (int64_t)nl; tlat[li] = (int64_t)mlo;
+      }
+    }
+  }
   // Pruned problems (continuous f32 above mixtures of more than kPruneMinK
-  // components) are the only ones whose candidates are sorted; they own the
+  // components, not tabulated) are the only ones whose candidates are sorted; they own the
   // candidate range [0, sort_count).  Sort key = sort_slot << key_bits | value
   // bucket: one 8-bit radix pass up to 8 sorted problems, never below 32
   // buckets per problem.  Large candidate sets get 4096 buckets (two passes):
@@ -342,7 +417,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
     pruned[li] = !f64 && (L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) &&
-                 (dev_fit[li] || L.above_k > kPruneMinK);
+                 (dev_fit[li] || L.above_k > kPruneMinK) && tmode[li] == TPE_TAB_NONE;
     pooled[li] = pruned[li] && L.n_ids >= 2;
     if (!pruned[li]) continue;
     S += pooled[li] ? 1 : L.n_ids;
@@ -417,15 +492,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
     // ---- sort-key range of the kernel coordinate ----
     double klo, khi;
-    if (L.family == TPE_FAM_CATEGORICAL) { klo = 0; khi = std::max(L.upper, 1); }
-    else if ((L.flags & TPE_F_HAS_LOW) && (L.flags & TPE_F_HAS_HIGH)) { klo = L.low; khi = L.high; }
-    else {
-      klo = INFINITY; khi = -INFINITY;
-      for (int64_t i = 0; i < L.below_k; ++i) {
-        klo = std::min(klo, L.below_mu[i] - 8 * L.below_sigma[i]);
-        khi = std::max(khi, L.below_mu[i] + 8 * L.below_sigma[i]);
-      }
-    }
+    coord_range(L, klo, khi);
     p.key_lo = (float)klo;
     p.key_inv = khi > klo ? (float)((double)(1 << key_bits) / (khi - klo)) : 0.f;
     // ---- component rows ----
@@ -626,6 +693,29 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
   if (below_idx.empty()) below_idx.push_back(0);
+  // ---- score tables: 16-B units (a cell row is 4 units, 64-B aligned; a lattice row 1) ----
+  int64_t tab_units = 0;
+  for (int32_t li = 0; li < n_labels; ++li) {
+    tpe_problem& p = lab[li];
+    p.tab_mode = tmode[li];
+    if (tmode[li] == TPE_TAB_CELLS) {
+      for (int sd = 0; sd < 2; ++sd) {
+        const int64_t n = sd ? tn1[li] : tn0[li];
+        tab_units = (tab_units + 3) & ~(int64_t)3;
+        p.tab_off[sd] = (int32_t)tab_units;
+        p.tab_n[sd] = (int32_t)n;
+        p.tab_lo[sd] = (float)tklo[li];
+        p.tab_inv[sd] = (float)((double)n / (tkhi[li] - tklo[li]));
+        tab_units += 4 * n;
+      }
+    } else if (tmode[li] == TPE_TAB_LATTICE) {
+      p.tab_off[0] = (int32_t)tab_units;
+      p.tab_n[0] = (int32_t)tn0[li];
+      p.lat_lo = tlat[li];
+      tab_units += tn0[li];
+    }
+  }
+  if (tab_units >= ((int64_t)1 << 31)) return TPE_E_ARG;
   // ---- problems, tiles, work ----
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
   static thread_local std::vector<tpe_problem> prob;
@@ -654,7 +744,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         q.ctr3 = (uint32_t)labels[li].ids[j];
         q.n_tiles = (int32_t)n_tiles_p;
         q.tile_off = (int32_t)(r * n_tiles_p);
-        if (q.family != TPE_FAM_CATEGORICAL) ++scored;
+        if (q.family != TPE_FAM_CATEGORICAL && q.tab_mode == TPE_TAB_NONE) ++scored;
       }
     }
   }
@@ -673,14 +763,14 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
                                                   std::max<int64_t>(scored_tiles, 1));
   bool any_pruned = false;
   for (auto& q : prob) {
-    if (q.family == TPE_FAM_CATEGORICAL) { q.n_splits = 0; continue; }
+    if (q.family == TPE_FAM_CATEGORICAL || q.tab_mode != TPE_TAB_NONE) { q.n_splits = 0; continue; }
     const int64_t ks = (q.above_len + kMinComponentsPerSplit - 1) / kMinComponentsPerSplit;
     const bool tails = q.sort_slot >= 0 && tiles_ref >= kTailMinTiles;
     q.n_splits = tails ? 1 : (int32_t)std::max<int64_t>(1, std::min(target, ks));
-    any_pruned = any_pruned || q.narrow_amin > 0.f;
+    any_pruned = any_pruned || q.sort_slot >= 0;
   }
   auto tile_splits = [&](const tpe_problem& q, int64_t j) -> int32_t {
-    if (q.family == TPE_FAM_CATEGORICAL) return 0;
+    if (q.family == TPE_FAM_CATEGORICAL || q.tab_mode != TPE_TAB_NONE) return 0;
     if (!(q.sort_slot >= 0 && tiles_ref >= kTailMinTiles)) return q.n_splits;
     const int64_t e = std::min<int64_t>(j, n_tiles_p - 1 - j);
     const int64_t ns = tail_splits(e);
@@ -711,7 +801,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     const size_t before = work.size();
     for (int64_t r = 0; r < P; ++r) {
       const tpe_problem& q = prob[r];
-      if (q.family != fams[gi][0] && q.family != fams[gi][1]) continue;
+      if ((q.family != fams[gi][0] && q.family != fams[gi][1]) || q.tab_mode != TPE_TAB_NONE) continue;
       for (int64_t j = 0; j < n_tiles_p; ++j) {
         tpe_tile& tl = tiles[(size_t)(r * n_tiles_p + j)];
         tl.work_first = (int32_t)work.size();
@@ -738,22 +828,44 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     const tpe_problem& q = prob[tiles[t].problem];
     const bool cat = q.family == TPE_FAM_CATEGORICAL && q.samp_len <= TPE_SAMPLE_LDS_ROWS;
     const bool fused = !f64 && (q.family == TPE_FAM_GAUSS || q.family == TPE_FAM_LOGGAUSS) && tiles[t].n_splits == 1;
-    if (!cat && !fused) fin_tiles.push_back((int32_t)t);
+    if (!cat && !fused && q.tab_mode == TPE_TAB_NONE) fin_tiles.push_back((int32_t)t);
   }
+  // table jobs: per tabulated label, one per cell side (4 cells per block) or
+  // one lattice job (one value per block); `problem` = the label's first row
+  static thread_local std::vector<tpe_tab_job> tab_jobs;
+  tab_jobs.clear();
+  int64_t tab_blocks = 0;
+  for (int32_t li = 0, r = 0; li < n_labels; r += (int32_t)labels[li].n_ids, ++li) {
+    const tpe_problem& p = lab[li];
+    if (p.tab_mode == TPE_TAB_NONE || labels[li].n_ids <= 0) continue;
+    const int sides = p.tab_mode == TPE_TAB_CELLS ? 2 : 1;
+    for (int sd = 0; sd < sides; ++sd) {
+      tpe_tab_job j;
+      j.problem = r; j.side = sd; j.kind = p.tab_mode; j.n = p.tab_n[sd]; j.off = p.tab_off[sd];
+      j.block0 = (int32_t)tab_blocks;
+      tab_blocks += p.tab_mode == TPE_TAB_CELLS ? (j.n + 3) / 4 : j.n;
+      tab_jobs.push_back(j);
+    }
+  }
+  if (tab_blocks >= ((int64_t)1 << 31)) return TPE_E_ARG;
+  const int64_t n_tab_jobs = (int64_t)tab_jobs.size();
+  if (tab_jobs.empty()) tab_jobs.push_back(tpe_tab_job{0, 0, 0, 0, 0, 0});
   const int64_t n_fin = (int64_t)fin_tiles.size();
   if (fin_tiles.empty()) fin_tiles.push_back(0);
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
   // comp32 rows sit at the END of the last two sections and are not copied ----
-  const int NS = 11;
+  const int NS = 12;
   const void* src[NS] = {prob.data(), tiles.data(), work.data(), comp64.data(), samp.data(), fit.data(),
-                         below_idx.data(), fit_seg.data(), fin_tiles.data(), grid.data(), comp32.data()};
+                         below_idx.data(), fit_seg.data(), fin_tiles.data(), tab_jobs.data(), grid.data(),
+                         comp32.data()};
   const int64_t len[NS] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
                            (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp64.size() * sizeof(double)),
                            (int64_t)(samp.size() * sizeof(double)), (int64_t)(fit.size() * sizeof(tpe_fit_job)),
                            (int64_t)(below_idx.size() * sizeof(int32_t)), (int64_t)(fit_seg.size() * sizeof(int64_t)),
                            (int64_t)(fin_tiles.size() * sizeof(int32_t)),
+                           (int64_t)(tab_jobs.size() * sizeof(tpe_tab_job)),
                            (int64_t)(grid.size() * sizeof(int32_t)), (int64_t)(comp32.size() * sizeof(float))};
-  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
+  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
   int64_t off[NS], end = 0;
   for (int i = 0; i < NS; ++i) {
     off[i] = (end + 255) & ~(int64_t)255;
@@ -764,7 +876,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->off_fin_tiles = off[8]; info->n_fin_tiles = n_fin;
   info->fit_max_seg = 0;
   for (size_t q = 1; q < fit_seg.size(); ++q) info->fit_max_seg = std::max(info->fit_max_seg, fit_seg[q] - fit_seg[q - 1]);
-  info->off_grid = off[9]; info->off_comp32 = off[10];
+  info->off_tab_jobs = off[9]; info->n_tab_jobs = n_tab_jobs; info->tab_blocks = tab_blocks;
+  info->tab_units = tab_units;
+  info->off_grid = off[10]; info->off_comp32 = off[11];
   info->n_problems = P;
   info->n_tiles = (int64_t)tiles.size();
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
@@ -774,12 +888,12 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->part_total = part_total;
   info->n_fit = (int32_t)fit.size(); info->reserved = 0;
   info->fit_total = fit_seg.back();
-  info->copy_end = off[9] + len[9];
+  info->copy_end = off[10] + len[10];
   info->sort_count = n_sorted_prob * (int64_t)n_cand;
   info->n_sorted = S;
   info->n_pooled = n_pooled;
   info->draw_blocks = (C_ref + 1 + 63) / 64;
-  info->copy2_len = len[10];
+  info->copy2_len = len[11];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;
   for (int i = 0; i < NS; ++i)

@@ -7,8 +7,11 @@
 //
 //   tpe_fit_above    (optional) Parzen fit of large continuous above mixtures
 //                    from device-resident observation columns
-//   tpe_sample       Philox-4x32-10 candidates from the below mixture, plus the
-//                    sort keys (problem, 4096 value buckets of the kernel coordinate)
+//   tpe_tables       per-label score tables (continuous: Taylor moments per
+//                    value cell; quantized: exact l, g per lattice value)
+//   tpe_sample       Philox-4x32-10 candidates from the below mixture; tabulated
+//                    and categorical labels are scored right here, the others
+//                    get sort keys (problem, 4096 value buckets of the coordinate)
 //   tpe_sort         radix sort of the keys (rocPRIM) — candidates of one wave
 //                    become neighbours in value, which is what lets the hot
 //                    loop skip the above-mixture components that cannot matter
@@ -465,6 +468,30 @@ __device__ __forceinline__ void block_best(double sc, int64_t orig, double l, do
   }
 }
 
+// ----------------------------------------------------------- score tables
+// (include/tpe_hip.h "Tabulated scoring").  Cell row: 16 floats {M0..M10, m,
+// c, 1/h, flag, 0}.
+constexpr int kTabMoments = 11;        // degree-10 Taylor moments per cell
+constexpr float kTabDrop = 50.f;       // terms below 2^-50 of the cell's largest are dropped
+
+// log2 of one mixture side's sum at t from its cell table; NAN when t lies
+// outside the cells, in a flagged cell, or the series is not positive (the
+// caller then sums the mixture exactly)
+__device__ __forceinline__ float cell_log2(const tpe_problem& p, int side, const float4* __restrict__ tab, float t) {
+  const float gj = floorf((t - p.tab_lo[side]) * p.tab_inv[side]);
+  if (!(gj >= 0.f && gj < (float)p.tab_n[side])) return NAN;
+  const float4* __restrict__ r = tab + p.tab_off[side] + 4 * (int)gj;
+  const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+  if (d.z != 0.f) return NAN;
+  const float u = (t - d.x) * d.y;
+  float sm = c.z;
+  sm = __builtin_fmaf(sm, u, c.y); sm = __builtin_fmaf(sm, u, c.x);
+  sm = __builtin_fmaf(sm, u, b.w); sm = __builtin_fmaf(sm, u, b.z); sm = __builtin_fmaf(sm, u, b.y);
+  sm = __builtin_fmaf(sm, u, b.x); sm = __builtin_fmaf(sm, u, a.w); sm = __builtin_fmaf(sm, u, a.z);
+  sm = __builtin_fmaf(sm, u, a.y); sm = __builtin_fmaf(sm, u, a.x);
+  return sm > 0.f ? c.w + __log2f(sm) : NAN;
+}
+
 // Draws (when `draw`) and writes the sort keys: (sorted problem << key_bits) |
 // value bucket.  Grid (tiles, TPE_BEST_PER_TILE): block (x, y) handles the y-th
 // 256-candidate slice of tile x, one candidate per thread — a 2^20-candidate
@@ -484,7 +511,10 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      double* __restrict__ l_out, double* __restrict__ g_out,
                                                      int precision, int draw, int key_bits, int flags,
                                                      const double* __restrict__ draw_pref, int64_t draw_blocks,
-                                                     int ordered, unsigned long long* __restrict__ pool_best) {
+                                                     int ordered, unsigned long long* __restrict__ pool_best,
+                                                     const float4* __restrict__ comp32,
+                                                     const int32_t* __restrict__ grid,
+                                                     const float4* __restrict__ tab) {
   const tpe_tile tl = tiles[blockIdx.x];
   const tpe_problem& p = P[tl.problem];
   if ((p.flags & TPE_F_POOLED) && tl.cand_start == 0 && blockIdx.y == 0 && threadIdx.x == 0)
@@ -548,6 +578,53 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
         }
       tile_best[(int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y] = b;
     }
+    return;
+  }
+  if (p.tab_mode != TPE_TAB_NONE) {
+    // tabulated scoring: the draw is scored from the label's tables and the
+    // slice's best goes straight to its tile_best slot (no candidate stores)
+    double x = 0.0, l = 0.0, g = 0.0;
+    float t = 0.f;
+    if (valid) {
+      if (!draw) {
+        t = coord[o];
+        x = cand[o];
+      } else if (p.samp_len > 0) {
+        int c;
+        draw_one(p, S, in_lds ? cum_lds : S, in_lds ? 1 : 8, i, precision, lo_f, hi_f, x, t, c);
+      } else {
+        x = NAN; t = NAN;
+      }
+      if (p.tab_mode == TPE_TAB_CELLS) {
+        float lb2 = cell_log2(p, 0, tab, t), la2 = cell_log2(p, 1, tab, t);
+        if (!(lb2 == lb2)) lb2 = lse2_exact_ool(comp32, p.below_off, p.below_len, 0, 0, t);
+        if (!(la2 == la2))
+          la2 = p.narrow_amin > 0.f ? lse2_pruned(p, comp32, grid, t)
+                                    : lse2_exact_ool(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
+        const double lnx = p.family == TPE_FAM_LOGGAUSS ? (double)t : 0.0;
+        l = (double)lb2 * kLn2 + p.below_base - lnx;
+        g = (double)la2 * kLn2 + p.above_base - lnx;
+      } else {
+        const double mq = rint(x / p.q);
+        const double jq = mq - (double)p.lat_lo;
+        if (mq * p.q == x && jq >= 0.0 && jq < (double)p.tab_n[0]) {
+          const double2 r = reinterpret_cast<const double2*>(tab)[p.tab_off[0] + (int64_t)jq];
+          l = r.x;
+          g = r.y;
+        } else {
+          // unreachable for device draws (the lattice spans every value they can
+          // take; caller-drawn candidates disable the table, TPE_F_NO_TABLE): the
+          // candidate drops out (an f64 mass sum here would triple this
+          // kernel's registers)
+          l = -INFINITY;
+          g = 0.0;
+        }
+      }
+      if (l_out) { l_out[o] = l; g_out[o] = g; }
+      if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
+    }
+    block_best(valid ? l - g : 0.0, valid ? (int64_t)i : -1, l, g,
+               tile_best + (int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y);
     return;
   }
   // ordered draws of a sorted problem: no sort follows, candidates go straight
@@ -999,6 +1076,7 @@ __device__ __forceinline__ void finalize_slice(const tpe_problem* __restrict__ P
   // sampled categorical tiles are finalized by k_sample (one-split continuous
   // f32 tiles by the above kernel: they are never in the finalize list)
   if (sampled && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= kCumLds) return;
+  if (p.tab_mode != TPE_TAB_NONE) return;          // scored by the sample stage from its tables
 
   const int n = p.n_cand;
   const int i = tl.cand_start + (int)threadIdx.x + (int)blockIdx.y * kThreads;
@@ -1353,6 +1431,155 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
 }
 
 
+// ============================================================ score tables
+// (include/tpe_hip.h "Tabulated scoring")
+__device__ __forceinline__ int tab_job_of(const tpe_tab_job* __restrict__ J, int n, int b) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (J[m].block0 <= b) lo = m; else hi = m - 1;
+  }
+  return lo;
+}
+
+// one wave: the moment row of cell j of side `side` (0 below, 1 above) of p
+__device__ void cell_row(const tpe_problem& p, int side, int j, const float4* __restrict__ comp,
+                         const int32_t* __restrict__ grid, float* __restrict__ row) {
+  const int lane = threadIdx.x & 63;
+  const float inv = p.tab_inv[side];
+  const float c = p.tab_lo[side] + ((float)j + 0.5f) / inv;
+  const float h = 0.5f / inv;
+  // components: sorted rows [k0, k0 + n0) and the wide rows [k1, k1 + n1)
+  int k0, n0, k1 = 0, n1 = 0;
+  if (side == 0) {
+    k0 = p.below_off; n0 = p.below_len;
+  } else if (p.narrow_amin > 0.f) {
+    // pruned above mixture: m0 (the best term at c among the wide components and
+    // c's grid neighbours) bounds the cell's largest term from below, so a narrow
+    // component with |c - mu| > sqrt(narrow_cmax - m0 + 50) / narrow_amin is
+    // under 2^-50 of it
+    const int32_t* __restrict__ G = grid + p.grid_off;
+    float m0 = -INFINITY;
+    if (lane < p.wide_len) {
+      const float4 q = comp[p.wide_off + lane];
+      const float z = ((c - q.x) - q.y) * q.z;
+      m0 = q.w - z * z;
+    }
+    const int gb = (int)fminf(fmaxf(floorf((c - p.grid_lo) * p.grid_inv), 0.f), (float)p.grid_n);
+    const int kn = G[gb] - 2 + (lane - 16);
+    if (lane >= 16 && lane < 20 && kn >= 0 && kn < p.above_len) {
+      const float4 q = comp[p.above_off + kn];
+      const float z = ((c - q.x) - q.y) * q.z;
+      m0 = fmaxf(m0, q.w - z * z);
+    }
+    for (int off = 32; off > 0; off >>= 1) m0 = fmaxf(m0, __shfl_xor(m0, off));
+    const float R = sqrtf(fmaxf(p.narrow_cmax - m0 + kTabDrop, 0.f)) / p.narrow_amin;
+    k1 = p.wide_off; n1 = p.wide_len;
+    if (!(m0 > -INFINITY) || !(R < INFINITY)) {
+      k0 = p.above_off; n0 = p.above_len;
+    } else {
+      const float gl = (c - R - p.grid_lo) * p.grid_inv, gh = (c + R - p.grid_lo) * p.grid_inv;
+      const int bl = (int)fminf(fmaxf(floorf(gl) - 1.f, 0.f), (float)p.grid_n);
+      const int bh = (int)fminf(fmaxf(floorf(gh) + 2.f, 0.f), (float)p.grid_n);
+      const int kl = G[bl], kh = max(G[bh], G[bl]);
+      k0 = p.above_off + kl; n0 = kh - kl;
+    }
+  } else {
+    k0 = p.above_off; n0 = p.above_len; k1 = p.wide_off; n1 = p.wide_len;
+  }
+  k0 = __builtin_amdgcn_readfirstlane(k0); n0 = __builtin_amdgcn_readfirstlane(n0);
+  const int n = n0 + n1;
+  // pass 1: the largest term at c
+  float mx = -INFINITY;
+  for (int i = lane; i < n; i += 64) {
+    const float4 q = i < n0 ? comp[k0 + i] : comp[k1 + i - n0];
+    const float z = ((c - q.x) - q.y) * q.z;
+    mx = fmaxf(mx, q.w - z * z);
+  }
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  // pass 2: Taylor moments (about c, in u = (t - c) / h) of every term within
+  // 2^-50 of it; a significant term outside the series' convergence box flags
+  // the cell (its candidates are summed exactly)
+  double M[kTabMoments];
+#pragma unroll
+  for (int q = 0; q < kTabMoments; ++q) M[q] = 0.0;
+  bool bad = !(mx > -INFINITY);
+  const float cut = mx - kTabDrop;
+  for (int i = lane; i < n && !bad; i += 64) {
+    const float4 q = i < n0 ? comp[k0 + i] : comp[k1 + i - n0];
+    const float z = ((c - q.x) - q.y) * q.z;
+    const float v = q.w - z * z;
+    if (!(v >= cut)) continue;
+    const float ah = q.z * h;
+    const float B = -2.f * kLn2f * z * ah;
+    const float G = -kLn2f * ah * ah;
+    if (fabsf(B) > kTaylorBMax || fabsf(G) > kTaylorGMax) { bad = true; break; }
+    float e = __builtin_amdgcn_exp2f(v - mx), em1 = 0.f;
+    M[0] += (double)e;
+#pragma unroll
+    for (int k = 1; k < kTabMoments; ++k) {
+      const float en = (B * e + 2.f * G * em1) * (1.f / (float)k);
+      em1 = e;
+      e = en;
+      M[k] += (double)e;
+    }
+  }
+  const bool any_bad = __ballot(bad) != 0ull;
+#pragma unroll
+  for (int q = 0; q < kTabMoments; ++q)
+    for (int off = 32; off > 0; off >>= 1) M[q] += __shfl_xor(M[q], off);
+  float val = 0.f;
+#pragma unroll
+  for (int q = 0; q < kTabMoments; ++q)
+    if (lane == q) val = (float)M[q];
+  if (lane == 11) val = mx;
+  if (lane == 12) val = c;
+  if (lane == 13) val = 1.f / h;
+  if (lane == 14) val = any_bad ? 1.f : 0.f;
+  if (lane < 16) row[lane] = val;
+}
+
+// one workgroup: {l, g} of lattice value lat_lo + j of a quantized problem, the
+// reference's per-component mass terms (tpe.py:147-159 / :285-298) summed in a
+// fixed order
+template <bool LOG>
+__device__ void lattice_row(const tpe_problem& p, int j, const double4* __restrict__ comp64,
+                            double2* __restrict__ rows) {
+  const double x = (double)(p.lat_lo + (int64_t)j) * p.q;
+  double tu, tl;
+  q_bounds(p, x, tu, tl);
+  double sb = 0.0, sa = 0.0;
+  for (int k = threadIdx.x; k < p.below_len; k += kThreads) sb += qterm<LOG>(comp64[p.below_off + k], tu, tl);
+  for (int k = threadIdx.x; k < p.above_len; k += kThreads) sa += qterm<LOG>(comp64[p.above_off + k], tu, tl);
+  for (int off = 32; off > 0; off >>= 1) { sb += __shfl_xor(sb, off); sa += __shfl_xor(sa, off); }
+  __shared__ double red[2][kThreads / 64];
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sb; red[1][threadIdx.x >> 6] = sa; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double b = red[0][0], a = red[1][0];
+    for (int w = 1; w < kThreads / 64; ++w) { b += red[0][w]; a += red[1][w]; }
+    rows[j] = make_double2(log(b) + p.below_base, log(a) + p.above_base);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_tables(const tpe_problem* __restrict__ P,
+                                                     const tpe_tab_job* __restrict__ J, int n_jobs,
+                                                     const float4* __restrict__ comp32,
+                                                     const double4* __restrict__ comp64,
+                                                     const int32_t* __restrict__ grid, float4* __restrict__ tab) {
+  const tpe_tab_job jb = J[tab_job_of(J, n_jobs, (int)blockIdx.x)];
+  const tpe_problem& p = P[jb.problem];
+  const int b = (int)blockIdx.x - jb.block0;
+  if (jb.kind == TPE_TAB_CELLS) {
+    const int cell = b * 4 + (int)(threadIdx.x >> 6);
+    if (cell < jb.n) cell_row(p, jb.side, cell, comp32, grid, reinterpret_cast<float*>(tab + jb.off + 4 * cell));
+  } else if (p.family == TPE_FAM_QLOGGAUSS) {
+    lattice_row<true>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off));
+  } else {
+    lattice_row<false>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off));
+  }
+}
+
 // ============================================================ device Parzen fit
 // adaptive_parzen_normal (tpe.py:398-475) of the above observations of a label
 // (ap_filter_trials, tpe.py:613-641), directly into the pruned f32 layout.
@@ -1672,6 +1899,9 @@ int check_batch(const tpe_batch* b) {
   if (b->n_sorted < 0 || b->draw_blocks < 0) return fail(TPE_E_ARG, "negative n_sorted/draw_blocks");
   if (ordered_draws(b) && (!b->draw_pref || b->draw_blocks < 1))
     return fail(TPE_E_ARG, "ordered draws need draw_pref and draw_blocks");
+  if (b->n_tab_jobs < 0 || b->tab_blocks < 0 || b->tab_units < 0) return fail(TPE_E_ARG, "negative table count");
+  if (b->n_tab_jobs > 0 && (!b->tab_jobs || !b->tab || !b->comp32 || !b->comp64))
+    return fail(TPE_E_ARG, "null table buffers");
   return TPE_OK;
 }
 
@@ -1750,6 +1980,16 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   return hip_check("tpe_fit_above/build");
 }
 
+int tpe_tables(const tpe_batch* b, void* stream) {
+  int rc = check_batch(b);
+  if (rc) return rc;
+  if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
+  hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
+                     b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64, b->grid,
+                     (float4*)b->tab);
+  return hip_check("tpe_tables");
+}
+
 int tpe_sample(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
@@ -1768,7 +2008,8 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
                      b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
                      b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
-                     b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0, b->pool_best);
+                     b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0, b->pool_best, (const float4*)b->comp32,
+                     b->grid, (const float4*)b->tab);
   return hip_check("tpe_sample");
 }
 
@@ -1845,6 +2086,7 @@ int tpe_run_batch(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if ((rc = tpe_fit_above(b, stream))) return rc;
+  if ((rc = tpe_tables(b, stream))) return rc;
   if ((rc = tpe_sample(b, stream))) return rc;
   if ((rc = tpe_sort(b, stream))) return rc;
   if ((rc = tpe_score_above(b, stream))) return rc;
@@ -1879,6 +2121,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   const bool od = precision == TPE_PREC_F32 && (flags & TPE_BATCH_ORDERED_DRAWS) && info.n_sorted > 0 &&
                   info.sort_count > 0 && info.n_pooled == 0;
   if (info.n_pooled > 0) need->pool_best = P;
+  need->tab = info.tab_units;
   if (od) need->draw_pref = info.n_sorted * (info.draw_blocks + 1);
   if (!od && info.sort_end_bit > 0 && info.sort_count > 0) {
     if ((rc = tpe_sort_workspace_bytes(info.sort_count, &sz))) return rc;
@@ -1892,7 +2135,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
       need->cand > ws->cand_cap || need->part > ws->part_cap || need->best > ws->best_cap ||
       need->result > ws->result_cap || need->fit > ws->fit_cap || need->sort_tmp_bytes > ws->sort_tmp_bytes ||
       need->fit_tmp_bytes > ws->fit_tmp_bytes || need->draw_pref > ws->draw_pref_cap ||
-      need->pool_best > ws->pool_best_cap)
+      need->pool_best > ws->pool_best_cap || need->tab > ws->tab_cap)
     return fail(TPE_E_SPACE, "level workspace too small (see tpe_level_need)");
   if (P == 0) return TPE_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -1937,6 +2180,13 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.part = ws->part;
   b.tile_best = ws->tile_best;
   if (info.n_pooled > 0) b.pool_best = ws->pool_best;
+  if (info.n_tab_jobs > 0) {
+    b.tab_jobs = (const tpe_tab_job*)(dev + info.off_tab_jobs);
+    b.n_tab_jobs = (int32_t)info.n_tab_jobs;
+    b.tab_blocks = (int32_t)info.tab_blocks;
+    b.tab = ws->tab;
+    b.tab_units = info.tab_units;
+  }
   b.result = ws->result;
   if (info.n_fit > 0) {
     b.fit = (const tpe_fit_job*)(dev + info.off_fit);

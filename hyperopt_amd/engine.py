@@ -53,6 +53,54 @@ def _coord_range(post):
     return float(np.min(mu - 8 * sg)), float(np.max(mu + 8 * sg))
 
 
+TAB_ETA = 0.05                     # tpe_host.cpp kTabEta: a_max * h <= eta per cell
+TAB_MAX_CELLS = 65536
+TAB_MAX_LATTICE = 1 << 18
+A_SCALE_LIT = 0.84932180028801907  # tpe_host.cpp kAScale (the same double)
+
+
+def _tab_plan(lp, n_cand, f64):
+    """Tabulated scoring of one level label (tpe_host.cpp, "tabulated scoring"):
+    dict(mode, n=(cells or lattice values per side), lo, hi, lat_lo)."""
+    post = lp.post
+    none = dict(mode=N.TAB_NONE, n=(0, 0), lo=0.0, hi=0.0, lat_lo=0)
+    if os.environ.get('TPE_TABLES', '1').startswith('0') or n_cand <= 0 or len(lp.ids) == 0:
+        return none
+    fam = post.family
+    if fam == N.FAM_CATEGORICAL or len(post.below[0]) == 0:
+        return none
+    klo, khi = _coord_range(post)
+    if not (math.isfinite(klo) and math.isfinite(khi) and khi > klo):
+        return none
+    ct = float(len(lp.ids)) * float(n_cand)
+
+    def cells(sig):
+        n = math.ceil((khi - klo) * (A_SCALE_LIT / max(sig, parzen.EPS)) / (2.0 * TAB_ETA))
+        return int(n) if 1.0 <= n < 1e15 else -1
+    if fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS) and not f64:
+        s0 = float(np.min(post.below[2]))
+        if post.above_dev is not None:
+            col, n_obs, bidx = post.above_dev
+            s1 = post.prior[1] / min(100.0, 1.0 + float(n_obs - len(bidx) + 1))
+        else:
+            s1 = float(np.min(post.above[2]))
+        n0, n1 = cells(s0), cells(s1)
+        if 0 < n0 <= TAB_MAX_CELLS and 0 < n1 <= TAB_MAX_CELLS and ct >= n0 + n1:
+            return dict(mode=N.TAB_CELLS, n=(n0, n1), lo=klo, hi=khi, lat_lo=0)
+    elif fam in (N.FAM_QGAUSS, N.FAM_QLOGGAUSS) and post.q and post.q > 0 and lp.inject is None:
+        tlo, thi = klo, khi
+        if post.low is None or post.high is None:
+            w, mu, sg = post.below
+            tlo, thi = float(np.min(mu - 9 * sg)), float(np.max(mu + 9 * sg))
+        lg = fam == N.FAM_QLOGGAUSS
+        xlo, xhi = (math.exp(tlo), math.exp(thi)) if lg else (tlo, thi)
+        mlo, mhi = math.floor(xlo / post.q) - 1.0, math.ceil(xhi / post.q) + 1.0
+        nl = mhi - mlo + 1.0
+        if math.isfinite(nl) and 1.0 <= nl <= TAB_MAX_LATTICE and abs(mlo) < 9e15 and ct >= 2.0 * nl:
+            return dict(mode=N.TAB_LATTICE, n=(int(nl), 0), lo=klo, hi=khi, lat_lo=int(mlo))
+    return none
+
+
 def _rows32(mu, a, c):
     """float4 {mu_hi, mu_lo, a, c} rows (mu split so t - mu keeps ~48 bits)."""
     r = np.empty((len(mu), 4), dtype=np.float32)
@@ -135,9 +183,12 @@ class Engine(object):
         the native packer (tpe_host_pack_level) is tested against."""
         f64 = self.precision == 'fp64'
         T = self.tile
-        # sorted (pruned) problems: continuous f32 above mixtures of > PRUNE_MIN_K components
+        plans = [_tab_plan(lp, n_cand, f64) for lp in problems]
+        # sorted (pruned) problems: continuous f32 above mixtures of > PRUNE_MIN_K
+        # components that are not tabulated
         pruned_l = [(not f64) and lp.post.family in (N.FAM_GAUSS, N.FAM_LOGGAUSS)
-                    and (lp.post.above_dev is not None or len(lp.post.above[0]) > PRUNE_MIN_K) for lp in problems]
+                    and (lp.post.above_dev is not None or len(lp.post.above[0]) > PRUNE_MIN_K)
+                    and pl['mode'] == N.TAB_NONE for lp, pl in zip(problems, plans)]
         # a pruned label active for several ids is pooled: one sort slot for all its problems
         pooled_l = [pr and len(lp.ids) >= 2 for lp, pr in zip(problems, pruned_l)]
         S = sum((1 if po else len(lp.ids)) for lp, pr, po in zip(problems, pruned_l, pooled_l) if pr)
@@ -232,6 +283,32 @@ class Engine(object):
                             info.update(meta)
             rows.append(info)
 
+        # score tables: 16-B units, a cell row 4 units (64-B aligned), a lattice row 1
+        units, jobs, blocks, r0 = 0, [], 0, 0
+        for lp, pl, info in zip(problems, plans, rows):
+            info['tab_mode'], info['tab_off'], info['tab_n'] = pl['mode'], [0, 0], [0, 0]
+            info['tab_lo'], info['tab_inv'], info['lat_lo'] = [0.0, 0.0], [0.0, 0.0], 0
+            if pl['mode'] == N.TAB_CELLS:
+                for sd in range(2):
+                    n = pl['n'][sd]
+                    units = (units + 3) & ~3
+                    info['tab_off'][sd], info['tab_n'][sd] = units, n
+                    info['tab_lo'][sd] = float(np.float32(pl['lo']))
+                    info['tab_inv'][sd] = float(np.float32(n / (pl['hi'] - pl['lo'])))
+                    units += 4 * n
+            elif pl['mode'] == N.TAB_LATTICE:
+                info['tab_off'][0], info['tab_n'][0], info['lat_lo'] = units, pl['n'][0], pl['lat_lo']
+                units += pl['n'][0]
+            if pl['mode'] != N.TAB_NONE and len(lp.ids):
+                for sd in range(2 if pl['mode'] == N.TAB_CELLS else 1):
+                    jobs.append((r0, sd, pl['mode'], info['tab_n'][sd], info['tab_off'][sd], blocks))
+                    blocks += (info['tab_n'][sd] + 3) // 4 if pl['mode'] == N.TAB_CELLS else info['tab_n'][sd]
+            r0 += len(lp.ids)
+        tab_jobs = np.array(jobs, dtype=np.int64).reshape(-1, 6)
+        tj = np.zeros(len(tab_jobs), dtype=N.TAB_JOB_DTYPE)
+        for c, f in enumerate(N.TAB_JOB_DTYPE.names):
+            tj[f] = tab_jobs[:, c]
+
         # problems: one row per (LevelProblem, id)
         counts = np.array([len(lp.ids) for lp in problems], dtype=np.int64)
         P = int(counts.sum())
@@ -240,7 +317,8 @@ class Engine(object):
         for field in ('family', 'flags', 'n_upper', 'samp_off', 'samp_len', 'below_off', 'below_len',
                       'above_off', 'above_len', 'low', 'high', 'q', 'below_base', 'above_base',
                       'wide_off', 'wide_len', 'grid_off', 'grid_n', 'prior_mu', 'prior_a', 'prior_c',
-                      'narrow_cmax', 'narrow_amin', 'grid_lo', 'grid_inv', 'key_lo', 'key_inv'):
+                      'narrow_cmax', 'narrow_amin', 'grid_lo', 'grid_inv', 'key_lo', 'key_inv',
+                      'tab_mode', 'tab_off', 'tab_n', 'tab_lo', 'tab_inv', 'lat_lo'):
             prob[field] = np.array([r[field] for r in rows])[owner] if P else 0
         prob['n_cand'] = n_cand
         ids = np.concatenate([lp.ids for lp in problems]) if P else np.zeros(0, np.int64)
@@ -281,8 +359,9 @@ class Engine(object):
         # function of the GLOBAL candidate count); pruned problems with many
         # tiles use one split and geometrically more on their outermost tiles
         fam = prob['family']
-        cont = (fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)
-        qg, ql = fam == N.FAM_QGAUSS, fam == N.FAM_QLOGGAUSS
+        untab = prob['tab_mode'] == N.TAB_NONE
+        cont = ((fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)) & untab
+        qg, ql = (fam == N.FAM_QGAUSS) & untab, (fam == N.FAM_QLOGGAUSS) & untab
         scored = cont | qg | ql
         C_ref = n_cand if not n_cand_global else int(n_cand_global)
         tiles_ref = (C_ref + T - 1) // T
@@ -335,7 +414,8 @@ class Engine(object):
         work = np.concatenate(works) if works else np.zeros(0, dtype=N.WORK_DTYPE)
         part_total = nw * T
 
-        return dict(prob=prob, tiles=tiles, work=work, counts_w=counts_w, part_total=part_total,
+        return dict(prob=prob, tiles=tiles, work=work, counts_w=counts_w, part_total=part_total, tab_jobs=tj,
+                    tab_units=units, tab_blocks=blocks,
                     comp32=np.concatenate(comp32) if comp32 else np.zeros((0, 4), np.float32),
                     comp64=np.concatenate(comp64) if comp64 else np.zeros((0, 4)),
                     grid=np.concatenate(grids) if grids else np.zeros(1, np.int32),
@@ -353,6 +433,8 @@ class Engine(object):
         for i, lp in enumerate(problems):
             post = lp.post
             flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)
+            if lp.inject is not None:        # caller-drawn candidates need not lie on a quantization lattice
+                flags |= N.F_NO_TABLE
             ids = lp.ids                          # int64, contiguous (LevelProblem)
             if post.ptrs is not None and post.above_dev is None:
                 # native fits: the addresses are known; the posterior owns the arrays
@@ -451,6 +533,7 @@ class Engine(object):
         ws.fit_tmp, ws.fit_tmp_bytes = dev('fit_tmp', 1)
         ws.draw_pref, ws.draw_pref_cap = dev('draw_pref', 8)
         ws.pool_best, ws.pool_best_cap = dev('pool_best', 8)
+        ws.tab, ws.tab_cap = dev('tab', 16)
         self._ws = ws
         return ws
 
@@ -472,6 +555,7 @@ class Engine(object):
         self._buf('fit_tmp', need.fit_tmp_bytes, torch.uint8)
         self._buf('draw_pref', need.draw_pref, torch.float64)
         self._buf('pool_best', need.pool_best, torch.int64)
+        self._buf('tab', 4 * need.tab, torch.float32)
         self._ws = None
 
     def run_level(self, problems, n_cand, seed, cand_base=0, n_cand_global=None):
@@ -599,6 +683,10 @@ class Engine(object):
         b.tile_best, b.result = d_best.data_ptr(), d_res.data_ptr()
         if info.n_pooled:
             b.pool_best = self._buf('pool_best', P, torch.int64).data_ptr()
+        if info.n_tab_jobs:
+            b.tab_jobs, b.n_tab_jobs, b.tab_blocks = base + info.off_tab_jobs, info.n_tab_jobs, info.tab_blocks
+            b.tab = self._buf('tab', 4 * int(info.tab_units), torch.float32).data_ptr()
+            b.tab_units = info.tab_units
         if info.n_sorted and not inject and not info.n_pooled:
             b.n_sorted, b.draw_blocks = info.n_sorted, info.draw_blocks
             b.draw_pref = self._buf('draw_pref', int(info.n_sorted) * (int(info.draw_blocks) + 1),
@@ -669,6 +757,8 @@ class Engine(object):
         stages = []
         if b.n_fit:
             stages.append(('fit', self.lib.tpe_fit_above, None, float(b.fit_total)))
+        if b.n_tab_jobs:
+            stages.append(('k_tables', self.lib.tpe_tables, None, float(b.tab_units)))
         stages.append(('k_sample', self.lib.tpe_sample, None, float(tb['P'] * n_cand)))
         ordered = (bool(b.draw_pref) and b.sample and b.precision == N.PREC_F32 and b.n_sorted > 0
                    and (b.flags & N.BATCH_ORDERED_DRAWS))

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 7
+#define TPE_ABI_VERSION 8
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -57,10 +57,19 @@ enum {
   TPE_F_HAS_LOW = 1,   /* low bound present (reference: low is not None)   */
   TPE_F_HAS_HIGH = 2,  /* high bound present                                */
   TPE_F_POOLED = 4,    /* candidates pooled with the other ids of the label (see "Pooled labels") */
-  TPE_F_CAT_LAZY = 8   /* categorical, <= 64 categories, best-scoring drawable category with selection
+  TPE_F_CAT_LAZY = 8,  /* categorical, <= 64 categories, best-scoring drawable category with selection
                           probability >= 2^-16: device-drawn batches without per-candidate outputs
                           score it in the select stage by scanning draws in index order until no
                           undrawn category can still win (usually one 1024-draw chunk) */
+  TPE_F_NO_TABLE = 16  /* tpe_label_in: score this label per candidate (no lattice table), e.g. when
+                          the caller supplies candidates that need not lie on the quantization lattice */
+};
+
+/* tabulated scoring of a problem (tpe_problem.tab_mode, see "Tabulated scoring") */
+enum {
+  TPE_TAB_NONE = 0,     /* scored by the above / finalize stages (per candidate)                  */
+  TPE_TAB_CELLS = 1,    /* continuous f32: per-cell Taylor moment tables of both mixtures          */
+  TPE_TAB_LATTICE = 2   /* quantized: exact {l, g} per lattice value of the candidate range        */
 };
 
 /* tpe_batch.flags / tpe_level_run flags */
@@ -133,6 +142,28 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  * draw_blocks exclusive block prefixes + the total), so every shard count draws
  * the same values bit for bit.
  *
+ * Tabulated scoring (tab_mode != TPE_TAB_NONE): the score of a candidate is a
+ * function of its value alone, so each hyperparameter's l and g are tabulated
+ * once per level — shared by every new_id of the label — and the sample stage
+ * scores each draw from the tables (no candidate stores, no sort, no above or
+ * finalize work):
+ *   TPE_TAB_CELLS (families 0/1, f32): side s (0 below, 1 above) splits
+ *     [tab_lo[s], tab_lo[s] + tab_n[s] / tab_inv[s]) into tab_n[s] cells of
+ *     half-width h with a_max * h <= 0.05 (a_max: the narrowest component).
+ *     About its centre c a component's term is 2^v exp(B u + G u^2),
+ *     u = (t - c) / h, |G| <= 0.0017; a cell row holds the degree-10 Taylor
+ *     moments of the sum of the terms within 2^-50 of its largest one
+ *     (|B| <= 0.6, truncation < 4e-8 relative) — a 64-B row of floats
+ *     {M0..M10, m (log2 shift), c, 1/h, flag, 0}: log2 s(t) = m + log2(sum_n
+ *     M_n u^n).  flag != 0 (a significant term too narrow to expand) and t
+ *     outside the cells fall back to the exact sum.
+ *   TPE_TAB_LATTICE (families 2/3): every candidate is x = m q (np.round,
+ *     tpe.py:90-93, 248-249); row m - lat_lo of the table (tab_n[0] rows of
+ *     double2 {l, g}, float64, reference operation order per component) holds
+ *     its scores; other values (injected candidates) are scored directly.
+ * Tables live in `tab` (16-B units; tab_off[s] = first unit) and are built by
+ * the table stage from the problem's component rows (after the device fit).
+ *
  * samp[k] = double[8] {cum, mu, sigma, fa, fb, flip, 0, 0}: below-mixture
  * sampler table; cum = selection CDF (∝ w_k * mass_k when bounded); fa, fb =
  * Phi of the (mirrored if flip) standardised truncation bounds; family 4 uses cum.
@@ -167,7 +198,25 @@ typedef struct tpe_problem {
   int32_t pool_first;    /* pooled: the label's first problem (else -1)         */
   uint32_t key0, key1;   /* Philox-4x32-10 key (suggest seed)                  */
   uint32_t ctr2, ctr3;   /* Philox counter high words (label index, new id)    */
+  int32_t tab_mode;      /* TPE_TAB_*                                          */
+  int32_t tab_off[2];    /* first 16-B unit of the below / above table in `tab` (lattice: [0]) */
+  int32_t tab_n[2];      /* cells per side (lattice: tab_n[0] = lattice values) */
+  float tab_lo[2], tab_inv[2];  /* cell j of side s: [tab_lo[s] + j / tab_inv[s], + 1 / tab_inv[s]) */
+  int32_t reserved6;
+  int64_t lat_lo;        /* lattice: index m of table row 0 (value lat_lo * q) */
 } tpe_problem;
+
+/* one table of the table stage: a side of a TPE_TAB_CELLS label (4 cells per
+ * 256-thread block) or a TPE_TAB_LATTICE label (1 lattice value per block).
+ * `problem` is the label's first problem row (its mixtures are the label's). */
+typedef struct tpe_tab_job {
+  int32_t problem;
+  int32_t side;          /* cells: 0 below, 1 above                             */
+  int32_t kind;          /* TPE_TAB_CELLS | TPE_TAB_LATTICE                     */
+  int32_t n;             /* cells / lattice values                              */
+  int32_t off;           /* first 16-B unit of the table                        */
+  int32_t block0;        /* first block of this job in the table stage's grid   */
+} tpe_tab_job;
 
 /* candidate tile: 2048 consecutive candidates of one problem; its above-mixture
  * partial sums are rows work_first .. work_first + n_splits - 1 of `part` */
@@ -283,6 +332,9 @@ typedef struct tpe_batch {
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
   double* draw_pref; int64_t draw_blocks; int32_t n_sorted; int32_t reserved5;
   unsigned long long* pool_best;   /* [n_problems] (pooled problems; see "Pooled labels") */
+  /* tabulated scoring: table jobs and the table storage (16-B units) */
+  const tpe_tab_job* tab_jobs; int32_t n_tab_jobs; int32_t tab_blocks;
+  void* tab; int64_t tab_units;
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
@@ -303,12 +355,13 @@ int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes);
 /* device workspace (bytes) of the fit sort for `total` observations in `n_fit` segments */
 int tpe_fit_workspace_bytes(int64_t total, int32_t n_fit, uint64_t* bytes);
 
-/* fit (when n_fit > 0) -> sample (optional) -> sort -> score -> select, enqueued on `stream` (hipStream_t);
+/* fit (when n_fit > 0) -> tables -> sample (optional) -> sort -> score -> select, enqueued on `stream` (hipStream_t);
  * asynchronous: results are valid once the stream reaches this point. */
 int tpe_run_batch(const tpe_batch* batch, void* stream);
 
 /* the stages one by one (same semantics; used by tests and the profiler) */
 int tpe_fit_above(const tpe_batch* batch, void* stream);  /* device Parzen fits */
+int tpe_tables(const tpe_batch* batch, void* stream);     /* score tables of tabulated labels */
 int tpe_sample(const tpe_batch* batch, void* stream);     /* draw + sort keys */
 int tpe_sort(const tpe_batch* batch, void* stream);
 int tpe_score_above(const tpe_batch* batch, void* stream);
@@ -358,6 +411,7 @@ typedef struct tpe_pack_info {
   int64_t fit_max_seg;                  /* tpe_batch.fit_max_seg */
   int64_t n_sorted, draw_blocks;        /* tpe_batch.n_sorted / draw_blocks */
   int64_t n_pooled;                     /* pooled problems (tpe_batch.pool_best needed) */
+  int64_t off_tab_jobs, n_tab_jobs, tab_blocks, tab_units;   /* tabulated scoring (tpe_batch.tab_*) */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation
@@ -420,12 +474,13 @@ typedef struct tpe_level_ws {
   void* fit_tmp; int64_t fit_tmp_bytes;
   double* draw_pref; int64_t draw_pref_cap;    /* elements                                              */
   unsigned long long* pool_best; int64_t pool_best_cap;   /* elements                                   */
+  void* tab; int64_t tab_cap;                  /* score tables, 16-B units                              */
 } tpe_level_ws;
 
 /* what a level needs (written on success and on TPE_E_SPACE) */
 typedef struct tpe_level_need {
   int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes, draw_pref,
-      pool_best;
+      pool_best, tab;
 } tpe_level_need;
 
 /* Run one tree level: `labels` as for tpe_host_pack_level; `out` receives one

@@ -128,10 +128,12 @@ def test_ctypes_mirrors_match_c():
             assert getattr(cls, f).offset == lay[cname + '.' + f], (cname, f)
 
 
-def test_level_run_reports_space_without_gpu():
+def test_level_run_reports_space_without_gpu(monkeypatch):
     """tpe_level_run sizes a level before touching the device: with empty
     workspaces it returns TPE_E_SPACE and the needs of a 2^20-candidate level
-    (an unpruned one: the sort workspace query needs a device)."""
+    (an unpruned one: the sort workspace query needs a device) — tabulated
+    (score tables, no above-mixture partial sums) and, with TPE_TABLES=0,
+    per candidate."""
     from hyperopt_amd import parzen
     from hyperopt_amd.engine import Engine, LevelProblem
     rs = np.random.RandomState(0)
@@ -145,4 +147,10 @@ def test_level_run_reports_space_without_gpu():
                            out.ctypes.data)
     assert rc == N.E_SPACE
     assert need.cand == 2 << 20 and need.result == 2 and need.best == 2 * 512 * N.BEST_PER_TILE
-    assert need.blob_bytes > 0 and need.pinned_bytes >= need.blob_bytes + 2 * 48 and need.part >= 2 << 20
+    assert need.blob_bytes > 0 and need.pinned_bytes >= need.blob_bytes + 2 * 48
+    # 50 above components over [-5, 5): cells of the narrowest bandwidth's scale, both sides
+    assert need.part == 0 and need.tab > 0 and need.tab % 4 == 0
+    monkeypatch.setenv('TPE_TABLES', '0')
+    rc = lib.tpe_level_run(labels, 1, 1 << 20, 5, 0, 0, N.PREC_F32, 0, ctypes.byref(ws), ctypes.byref(need), None,
+                           out.ctypes.data)
+    assert rc == N.E_SPACE and need.tab == 0 and need.part >= 2 << 20

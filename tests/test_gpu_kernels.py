@@ -24,6 +24,16 @@ def engine():
     return Engine(precision='fp32')
 
 
+@pytest.fixture(params=['tables', 'per_candidate'])
+def scoring(request, monkeypatch):
+    """Tabulated scoring (include/tpe_hip.h "Tabulated scoring", the default for
+    large candidate sets) and the per-candidate path it replaces (TPE_TABLES=0:
+    sorted candidates, pruned above kernel, finalize) — both must hold parity."""
+    if request.param == 'per_candidate':
+        monkeypatch.setenv('TPE_TABLES', '0')
+    return request.param
+
+
 def _post(case):
     from hyperopt_amd import parzen
     return parzen.fit_posterior(case['dist'], case['args'], np.asarray(case['below']),
@@ -145,7 +155,7 @@ def test_philox_sampler_distribution(engine):
     engine.set_precision('fp32')
 
 
-def test_ordered_draws_distribution(engine):
+def test_ordered_draws_distribution(engine, monkeypatch):
     """TPE_BATCH_ORDERED_DRAWS: pruned (sorted) problems draw ordered
     candidates (uniform order statistics through the mixture, include/tpe_hip.h
     "Ordered draws") instead of i.i.d. draws + sort: the draws follow the exact
@@ -158,6 +168,7 @@ def test_ordered_draws_distribution(engine):
     from hyperopt_amd.dist import combine_results, shard_range
     from hyperopt_amd.engine import LevelProblem
     from scipy.special import erf
+    monkeypatch.setenv('TPE_TABLES', '0')          # ordered draws replace the sort of per-candidate scoring
     rs = np.random.RandomState(8)
     C = 1 << 18
     Phi = lambda z: 0.5 * (1 + erf(z / np.sqrt(2)))
@@ -207,7 +218,7 @@ def test_ordered_draws_distribution(engine):
         assert abs(res_iid[0]['score'] - res[0]['score']) <= 0.05 * max(1.0, abs(res[0]['score'])), dist
 
 
-def test_pooled_label_matches_single_problems(engine):
+def test_pooled_label_matches_single_problems(engine, scoring):
     """A pruned label active for several ids is pooled (one sort for all its
     problems, per-problem winners by atomicMax): every id draws what it draws
     alone, its winner lies in the oracle's eps-tie set of those draws, the
@@ -266,7 +277,7 @@ def test_lazy_categorical_matches_full_scan(engine):
                 assert full[k]['value'] == cand[k][int(full[k]['idx'])]
 
 
-def test_sharding_matches_single_device(engine):
+def test_sharding_matches_single_device(engine, scoring):
     """Philox counters are global candidate indices, so every shard count draws
     the same candidate set.  Scores agree to fp32 rounding (pruned windows and
     split groupings follow the shard's own sorted waves), the argmax agrees up
@@ -299,7 +310,7 @@ def test_sharding_matches_single_device(engine):
             assert comb['value'][p] == cand[p][comb['global_idx'][p]]
 
 
-def test_large_config3_shaped_problem(engine):
+def test_large_config3_shaped_problem(engine, scoring):
     """Config-3-sized problem (C = 2^20 candidates, 10k-trial history):
     size-independent checks — lpdf of a random subset vs the oracle, argmax is
     the max of all returned scores, and a rerun is bit-identical."""
@@ -321,7 +332,7 @@ def test_large_config3_shaped_problem(engine):
     assert res2[0]['idx'] == res[0]['idx'] and res2[0]['score'] == res[0]['score']
 
 
-def test_pruning_and_underflow_extremes(engine):
+def test_pruning_and_underflow_extremes(engine, scoring):
     """Above mixtures large enough to be pruned, clustered observations plus
     isolated wide components, and candidates far in the tails (the fixed-shift
     sum underflows there and the max-shifted fallback takes over)."""
@@ -357,7 +368,7 @@ def _device_post(engine, dist, args, obs, bidx):
                                        ('loguniform', dict(low=-4.0, high=3.0)),
                                        ('normal', dict(mu=1.0, sigma=3.0)),
                                        ('lognormal', dict(mu=0.0, sigma=1.0))])
-def test_device_fit_matches_oracle(engine, dist, args):
+def test_device_fit_matches_oracle(engine, dist, args, scoring):
     """Device Parzen fit of the above mixture (gather -> segmented sort ->
     build) against the oracle's adaptive_parzen_normal + GMM1/LGMM1 lpdf, on
     sampled and injected candidates; the below side stays the host fit, so the
@@ -445,12 +456,13 @@ def test_device_fit_batched_labels_and_suggest():
             assert abs(g[k] - r[k]) <= 1e-3 * max(1.0, abs(r[k])), (k, g[k], r[k])
 
 
-def test_local_expansion_matches_exact_and_is_used(engine):
+def test_local_expansion_matches_exact_and_is_used(engine, monkeypatch):
     """The pruned f32 kernel's local (Taylor) expansion: above-lpdf of 2^20
     sampled candidates within 1e-5 of the all-exact kernel and within the fp32
     tolerance of the oracle; most window components are expanded."""
     from hyperopt_amd import parzen
     from hyperopt_amd.engine import LevelProblem
+    monkeypatch.setenv('TPE_TABLES', '0')          # the per-candidate pruned kernel
     rs = np.random.RandomState(13)
     for dist, args, obs in (('uniform', dict(low=-5.0, high=5.0), rs.uniform(-5, 5, 6000)),
                             ('loguniform', dict(low=-5.0, high=5.0), np.exp(rs.uniform(-5, 5, 6000)))):
@@ -473,3 +485,58 @@ def test_local_expansion_matches_exact_and_is_used(engine):
         _check_lpdf(g[0][sub], lpdf(cand[0][sub], *post.above, low=post.low, high=post.high), 1e-5, dist)
         score = l[0] - g[0]
         assert int(res[0]['idx']) == int(np.argmax(score))
+
+
+@pytest.mark.parametrize('dist,args', [('uniform', dict(low=-5.0, high=5.0)),
+                                       ('loguniform', dict(low=-4.0, high=3.0)),
+                                       ('normal', dict(mu=1.0, sigma=3.0)),
+                                       ('lognormal', dict(mu=0.0, sigma=1.0)),
+                                       ('quniform', dict(low=0.0, high=20.0, q=1.0)),
+                                       ('qloguniform', dict(low=0.0, high=5.0, q=2.0)),
+                                       ('qnormal', dict(mu=2.0, sigma=4.0, q=0.5)),
+                                       ('qlognormal', dict(mu=1.0, sigma=0.7, q=0.25))])
+def test_tabulated_scoring_matches_oracle(engine, dist, args):
+    """Tabulated scoring (cells: Taylor moments per value cell, fp32; lattice:
+    exact {l, g} per quantized value, fp64) on device draws against the
+    oracle's lpdf, the argmax inside the oracle's eps-tie set, the table mode
+    actually taken, and the result equal to the per-candidate path's up to
+    the tolerance."""
+    import os
+    from hyperopt_amd import _native as N
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(61)
+    q = args.get('q')
+    log = dist.startswith('log') or dist.startswith('qlog')
+    lo, hi = (args['low'], args['high']) if 'low' in args else (args['mu'] - 3 * args['sigma'],
+                                                               args['mu'] + 3 * args['sigma'])
+    obs = rs.uniform(lo, hi, 4000)
+    obs = np.exp(obs) if log else obs
+    if q:
+        obs = np.round(obs / q) * q
+    post = parzen.fit_posterior(dist, args, obs[:30], obs[30:], 1.0)
+    C = 1 << 16
+    res, cand, l, g = engine.run([LevelProblem(post, 5, [11])], C, seed=13, want_lg=True, return_cand=True)
+    prob, _ = engine.device_tables()
+    assert prob[0]['tab_mode'] == (N.TAB_LATTICE if q else N.TAB_CELLS), dist
+    tol = 1e-9 if q else 1e-5
+    lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
+    kw = dict(low=post.low, high=post.high, q=q)
+    u, inv = np.unique(cand[0], return_inverse=True)
+    sub = np.arange(len(u)) if len(u) < 4000 else rs.choice(len(u), 3000, replace=False)
+    lb = lpdf(u[sub], *post.below, **kw)
+    la = lpdf(u[sub], *post.above, **kw)
+    first = np.zeros(len(u), dtype=np.int64)
+    first[inv[::-1]] = np.arange(C)[::-1]              # first candidate of each distinct value
+    _check_lpdf(l[0][first[sub]], lb, tol, (dist, 'l'))
+    _check_lpdf(g[0][first[sub]], la, tol, (dist, 'g'))
+    if len(u) < 4000:                                  # lattice: every candidate scored by the oracle
+        _check_argmax(int(res[0]['idx']), lb[inv], la[inv], tol, dist)
+    k = int(res[0]['idx'])
+    assert res[0]['value'] == cand[0][k] and int(np.argmax(l[0] - g[0])) == k
+    os.environ['TPE_TABLES'] = '0'
+    try:
+        ref = engine.run([LevelProblem(post, 5, [11])], C, seed=13)
+    finally:
+        os.environ.pop('TPE_TABLES', None)
+    assert abs(ref[0]['score'] - res[0]['score']) <= 4 * tol * max(1.0, abs(res[0]['score'])), dist

@@ -144,6 +144,16 @@ def test_native_pack_matches_numpy_packer(precision):
         if precision == 'fp32':
             g = _blob(e, info, info.off_grid, np.int32, ref['grid'].size)
             np.testing.assert_array_equal(g, ref['grid'])
+        # score tables (include/tpe_hip.h "Tabulated scoring"): the same jobs and storage
+        assert (info.n_tab_jobs, info.tab_units, info.tab_blocks) == (len(ref['tab_jobs']), ref['tab_units'],
+                                                                     ref['tab_blocks'])
+        np.testing.assert_array_equal(_blob(e, info, info.off_tab_jobs, N.TAB_JOB_DTYPE, info.n_tab_jobs),
+                                      ref['tab_jobs'])
+        modes = set(prob['tab_mode'].tolist())
+        if C == 1 << 17:      # every continuous f32 label and the lattice labels tabulate at this size
+            assert N.TAB_LATTICE in modes and (N.TAB_CELLS in modes) == (precision == 'fp32'), modes
+        if C == 24:           # fewer candidates than cells: per-candidate scoring
+            assert N.TAB_CELLS not in modes
 
 
 class _FakeColumn(object):
