@@ -139,73 +139,76 @@ def cpu_baseline(domain, trials, budget_s=12.0, max_procs=16):
 
 
 # ------------------------------------------------------------------ roofline
-PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 vector peak (MI355X_MICROARCH.md)
-PEAK_HBM_GBS = 8000.0         # MI355X HBM3E (MI355X_MICROARCH.md)
-# k_above_f32 executed work: an exactly evaluated component x candidate (CE) is
-# sub, sub, mul, fma, exp2, add = 8 flop; a component summed by the local
-# expansion costs ~45 flop once per wave (d, z, B, G, exp2, 10-step recurrence,
-# 11 moment sums); every candidate then evaluates two degree-10 polynomials
-# (above and below sums, 40 flop) plus ~20 flop of fused finalize arithmetic.
-FLOP_PER_CE, FLOP_PER_EXPANDED, FLOP_PER_CAND = 8.0, 45.0, 60.0
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+# VALU issue peak: a wave64 VALU instruction issues over 2 cycles on a SIMD32
+# (MI355X_MICROARCH.md, Wave scheduling): 0.5 wave-instructions / cycle / SIMD
+# x 4 SIMDs x 256 CUs x 2.4 GHz
+PEAK_VALU_GINST = 0.5 * 4 * 256 * 2.4      # = 1228.8 G wave-instructions/s
+# counter summary of the same bench command (tools/gpu.sh pmc -> tools/pmc_summary.py)
+PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r02_pmc_summary.json')
+VALU_KERNELS = ('k_sample', 'k_tables', 'k_select', 'k_above_f32', 'k_finalize')
 
 
-def _traffic(kernel):
-    tr = os.path.join(ROOT, 'profiles', 'r01_traffic.json')
-    if not os.path.exists(tr):
-        return None, None
-    with open(tr) as f:
-        t = json.load(f)
-    t = t.get(kernel, t if t.get('kernel') == kernel else None)
-    return (t.get('bytes_per_launch'), 'profiles/r01_traffic.json') if t else (None, None)
+def _pmc():
+    if not os.path.exists(PMC_SUMMARY):
+        return {}
+    with open(PMC_SUMMARY) as f:
+        return json.load(f)
 
 
 def roofline(prof):
-    """Roofline of every measured kernel and of the dominant one (largest total
-    device time): algorithmic work per launch / the launch's average duration
-    (HIP events on the engine stream)."""
+    """Roofline of every measured stage and of the dominant one (largest total
+    device time): work per launch / the launch's average duration, the
+    duration timed live with HIP events on the engine stream.
+
+    VALU-bound kernels are priced by EXECUTED work: the VALU wave-instructions
+    one launch issues (SQ_INSTS_VALU per dispatch of the same bench command,
+    profiles/r02_pmc_summary.json) against the issue peak; the sort (when a
+    level still sorts) by its HBM bytes.  The algorithmic CE rate (C x K
+    component evaluations the reference performs) is reported beside it: the
+    tabulated kernels do not evaluate C x K terms, so that rate exceeds the
+    direct-evaluation ceiling and is context, not a roofline fraction."""
+    pmc = _pmc()
     kernels = {}
     for name, recs in prof.items():
         ms = np.array([r[0] for r in recs])
-        if not len(ms) or name in ('k_select', 'fit'):
+        if not len(ms) or name == 'fit':
             continue
         secs = ms.sum() * 1e-3
         k = dict(avg_launch_ms=float(ms.mean()), launches=int(len(ms)), total_ms=float(ms.sum()))
+        c = pmc.get(name, {})
         if name == 'sort':
             nbytes = np.array([r[1] for r in recs])
             ach = nbytes.sum() / secs / 1e9
             k.update(bound='hbm', achieved=ach, peak=PEAK_HBM_GBS, unit='GB/s', frac=ach / PEAK_HBM_GBS,
                      bytes_per_launch=float(nbytes.mean()),
-                     note='rocPRIM onesweep radix sort of (u32 bucket key, u64 position|t) pairs: each 8-bit '
-                          'pass reads and writes 12 B per candidate')
-        elif name == 'k_above_f32':
-            algo = np.array([r[1] for r in recs])
-            ce = np.array([r[2] for r in recs])
-            ex = np.array([r[3] for r in recs])
-            nc = np.array([r[4] for r in recs])
-            flops = FLOP_PER_CE * ce + FLOP_PER_EXPANDED * ex + FLOP_PER_CAND * nc
-            ach = flops.sum() / secs / 1e12
-            k.update(bound='valu', achieved=ach, peak=PEAK_FP32_TFLOPS, unit='TFLOP/s', frac=ach / PEAK_FP32_TFLOPS,
-                     executed_flop_per_launch=float(flops.mean()), exact_ce_per_launch=float(ce.mean()),
-                     expanded_components_per_launch=float(ex.mean()),
-                     algorithmic_ce_per_launch=float(algo.mean()), algorithmic_ce_per_s=float(algo.sum() / secs),
-                     direct_ce_ceiling=7.97e12, direct_ce_ceiling_source='profiles/r01_ce_ubench.txt',
-                     speedup_vs_direct_ceiling=float(algo.sum() / secs / 7.97e12),
-                     note='executed work after pruning and the local (Taylor) expansion; algorithmic CE = C x K '
-                          'the reference evaluates; direct evaluation of every CE is bounded by v_exp_f32 at '
-                          '7.97e12 CE/s (measured), which this kernel exceeds by speedup_vs_direct_ceiling')
+                     note='rocPRIM onesweep radix sort of (u32 bucket key, u64 position|t) pairs')
+        elif name in VALU_KERNELS and 'SQ_INSTS_VALU' in c:
+            inst = float(c['SQ_INSTS_VALU'])
+            ach = inst / (ms.mean() * 1e-3) / 1e9
+            k.update(bound='valu', achieved=ach, peak=PEAK_VALU_GINST, unit='G VALU wave-instructions/s',
+                     frac=ach / PEAK_VALU_GINST, executed_valu_per_launch=inst,
+                     executed_source='profiles/r02_pmc_summary.json (SQ_INSTS_VALU per dispatch)')
+            if 'SQ_INSTS_VALU_TRANS_F32' in c:
+                k['trans_f32_per_launch'] = float(c['SQ_INSTS_VALU_TRANS_F32'])
         else:
-            k.update(bound=None, note='latency-bound stage (per-candidate sampling / finalize)')
+            k.update(bound=None)
+        if name == 'k_sample' and len(recs[0]) > 2:
+            ce = np.array([r[2] for r in recs])
+            k.update(algorithmic_ce_per_launch=float(ce.mean()), algorithmic_ce_per_s=float(ce.sum() / secs),
+                     direct_ce_ceiling=7.97e12, direct_ce_ceiling_source='profiles/r01_ce_ubench.txt')
+        if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
+            k['traffic'] = (2 * c['FETCH_SIZE'] + c['WRITE_SIZE']) * 1024.0
         kernels[name] = k
-    if not kernels:
-        return None, kernels
     dom = max((n for n in kernels if kernels[n].get('bound')), key=lambda n: kernels[n]['total_ms'], default=None)
     if dom is None:
         return None, kernels
     r = dict(kernels[dom])
     r['kernel'] = dom
-    r['traffic'], src = _traffic(dom)
-    if src:
-        r['traffic_source'] = src
+    r.setdefault('traffic', None)
+    if r['traffic'] is not None:
+        r['traffic_source'] = 'profiles/r02_pmc_summary.json: (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 ' \
+                              'FETCH_SIZE correction, MI355X_MICROARCH.md)'
     return r, kernels
 
 

@@ -85,6 +85,8 @@ class Batch(ctypes.Structure):
         ('reserved5', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
         ('tab_jobs', ctypes.c_void_p), ('n_tab_jobs', ctypes.c_int32), ('tab_blocks', ctypes.c_int32),
         ('tab', ctypes.c_void_p), ('tab_units', ctypes.c_int64),
+        ('samp_tiles', ctypes.c_void_p), ('n_samp_tiles', ctypes.c_int32), ('n_samp_eager', ctypes.c_int32),
+        ('tab_tiles', ctypes.c_void_p), ('n_tab_tiles', ctypes.c_int32), ('reserved7', ctypes.c_int32),
     ]
 
 
@@ -135,6 +137,8 @@ class PackInfo(ctypes.Structure):
         ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64), ('n_pooled', ctypes.c_int64),
         ('off_tab_jobs', ctypes.c_int64), ('n_tab_jobs', ctypes.c_int64), ('tab_blocks', ctypes.c_int64),
         ('tab_units', ctypes.c_int64),
+        ('off_samp_tiles', ctypes.c_int64), ('n_samp_tiles', ctypes.c_int64), ('n_samp_eager', ctypes.c_int64),
+        ('off_tab_tiles', ctypes.c_int64), ('n_tab_tiles', ctypes.c_int64),
     ]
 
 

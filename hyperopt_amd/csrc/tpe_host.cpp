@@ -168,6 +168,67 @@ inline double log2_normal(double x) {
   return e + p * 1.4426950408889634074;
 }
 
+// adaptive_parzen_normal (tpe.py:398-475) of n observations given already
+// sorted: sv[i] = obs[order[i]] and rank[i] = order[i] (the observation's
+// position in tid order, which indexes the linear-forgetting ramp).  Writes
+// n + 1 components; returns the prior's position or TPE_E_ARG.  `clean`: sv
+// strictly increasing (no NaN, no repeats) — the neighbour gaps are then
+// finite and positive, and np.maximum / np.minimum reduce to branch-free
+// max / min that vectorise (same values).
+template <bool CLEAN>
+int64_t fit_sorted(const double* __restrict__ sv, const int64_t* __restrict__ rank, int64_t n, double prior_weight,
+                   double prior_mu, double prior_sigma, int32_t lf, double* __restrict__ w, double* __restrict__ mu,
+                   double* __restrict__ sigma) {
+  auto mx = [](double a, double b) { return CLEAN ? (a > b ? a : b) : np_max(a, b); };
+  auto mn = [](double a, double b) { return CLEAN ? (a < b ? a : b) : np_min(a, b); };
+  int64_t pos;
+  const int64_t K = n + 1;
+  if (n == 0) {
+    mu[0] = prior_mu; sigma[0] = prior_sigma; pos = 0;
+  } else if (n == 1) {
+    if (prior_mu < sv[0]) { pos = 0; mu[0] = prior_mu; mu[1] = sv[0]; sigma[0] = prior_sigma; sigma[1] = prior_sigma * .5; }
+    else { pos = 1; mu[0] = sv[0]; mu[1] = prior_mu; sigma[0] = prior_sigma * .5; sigma[1] = prior_sigma; }
+  } else {
+    // np.searchsorted(sorted, prior_mu, side='left') = number of elements < prior_mu
+    pos = std::lower_bound(sv, sv + n, prior_mu) - sv;
+    memcpy(mu, sv, (size_t)pos * sizeof(double));
+    mu[pos] = prior_mu;
+    memcpy(mu + pos + 1, sv + pos, (size_t)(n - pos) * sizeof(double));
+    for (int64_t i = 1; i < K - 1; ++i) sigma[i] = mx(mu[i] - mu[i - 1], mu[i + 1] - mu[i]);
+    sigma[0] = mu[1] - mu[0];
+    sigma[K - 1] = mu[K - 1] - mu[K - 2];
+  }
+  if (lf && lf < n) {
+    // linear_forgetting_weights (tpe.py:381-394): np.linspace(1/n, 1, n - lf)
+    // (i * step + start, exact endpoint), then ones — looked up by rank
+    const int64_t num = n - lf;
+    const double start = 1.0 / (double)n;
+    const double step = num > 1 ? (1.0 - start) / (double)(num - 1) : 0.0;
+    auto ramp = [&](int64_t r) -> double {
+      double y = (double)r * step;
+      y += start;
+      y = (r == num - 1 && num > 1) ? 1.0 : y;
+      return r >= num ? 1.0 : y;
+    };
+    for (int64_t i = 0; i < pos; ++i) w[i] = ramp(rank[i]);
+    w[pos] = prior_weight;
+    for (int64_t i = pos; i < n; ++i) w[i + 1] = ramp(rank[i]);
+  } else {
+    for (int64_t i = 0; i < K; ++i) w[i] = 1.0;
+    w[pos] = prior_weight;
+  }
+  const double smin = prior_sigma / std::min(100.0, 1.0 + (double)K);
+  const double smax = prior_sigma / 1.0;
+  for (int64_t i = 0; i < K; ++i) sigma[i] = mn(mx(sigma[i], smin), smax);   // np.clip
+  sigma[pos] = prior_sigma;
+  int ok = 1;
+  for (int64_t i = 0; i < K; ++i) ok &= sigma[i] > 0;
+  if (!ok) return TPE_E_ARG;
+  const double tot = np_sum(w, K);
+  for (int64_t i = 0; i < K; ++i) w[i] = w[i] / tot;
+  return pos;
+}
+
 // value range of a label's kernel coordinate (x, or ln x for log families)
 // that its candidates fall in: the bounds, else the below mixture +- 8 sigma
 // (f32 draws stay within 5.5 sigma of their component); categories [0, upper)
@@ -189,47 +250,19 @@ int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, 
                             double prior_mu, double prior_sigma, int32_t lf, double* w, double* mu,
                             double* sigma) {
   if (n < 0 || (n >= 2 && !order) || !w || !mu || !sigma) return TPE_E_ARG;
-  int64_t pos;
-  const int64_t K = n + 1;
-  if (n == 0) {
-    mu[0] = prior_mu; sigma[0] = prior_sigma; pos = 0;
-  } else if (n == 1) {
-    if (prior_mu < obs[0]) { pos = 0; mu[0] = prior_mu; mu[1] = obs[0]; sigma[0] = prior_sigma; sigma[1] = prior_sigma * .5; }
-    else { pos = 1; mu[0] = obs[0]; mu[1] = prior_mu; sigma[0] = prior_sigma * .5; sigma[1] = prior_sigma; }
-  } else {
-    // np.searchsorted(sorted, prior_mu, side='left') = number of elements < prior_mu
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int64_t m = (lo + hi) / 2;
-      if (obs[order[m]] < prior_mu) lo = m + 1; else hi = m;
-    }
-    pos = lo;
-    for (int64_t i = 0; i < pos; ++i) mu[i] = obs[order[i]];
-    mu[pos] = prior_mu;
-    for (int64_t i = pos; i < n; ++i) mu[i + 1] = obs[order[i]];
-    for (int64_t i = 1; i < K - 1; ++i) sigma[i] = np_max(mu[i] - mu[i - 1], mu[i + 1] - mu[i]);
-    sigma[0] = mu[1] - mu[0];
-    sigma[K - 1] = mu[K - 1] - mu[K - 2];
+  static thread_local std::vector<double> sv;
+  static thread_local std::vector<int64_t> rank;
+  sv.resize((size_t)n);
+  rank.resize((size_t)n);
+  double* svp = sv.data();
+  int64_t* rkp = rank.data();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = n >= 2 ? order[i] : i;
+    if (r < 0 || r >= n) return TPE_E_ARG;
+    rkp[i] = r;
+    svp[i] = obs[r];
   }
-  if (lf && lf < n) {
-    std::vector<double> ramp((size_t)n);
-    lf_weights(n, lf, ramp.data());
-    for (int64_t i = 0; i < pos; ++i) w[i] = ramp[order[i]];
-    w[pos] = prior_weight;
-    for (int64_t i = pos; i < n; ++i) w[i + 1] = ramp[order[i]];
-  } else {
-    for (int64_t i = 0; i < K; ++i) w[i] = 1.0;
-    w[pos] = prior_weight;
-  }
-  const double smin = prior_sigma / std::min(100.0, 1.0 + (double)K);
-  const double smax = prior_sigma / 1.0;
-  for (int64_t i = 0; i < K; ++i) sigma[i] = np_min(np_max(sigma[i], smin), smax);   // np.clip
-  sigma[pos] = prior_sigma;
-  for (int64_t i = 0; i < K; ++i)
-    if (!(sigma[i] > 0)) return TPE_E_ARG;
-  const double tot = np_sum(w, K);
-  for (int64_t i = 0; i < K; ++i) w[i] = w[i] / tot;
-  return pos;
+  return fit_sorted<false>(svp, rkp, n, prior_weight, prior_mu, prior_sigma, lf, w, mu, sigma);
 }
 
 int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* order, int64_t n,
@@ -237,43 +270,56 @@ int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* orde
                        double prior_sigma, int32_t lf, double* out, int64_t* out_k) {
   if (n < 0 || n_bt < 0 || (n && (!x || !tids || !order)) || (n_bt && !below_tids) || !out || !out_k)
     return TPE_E_ARG;
-  // ap_filter_trials (tpe.py:629-636): is each observation's tid in the below
-  // set — both ascending, so one merge; each side keeps tid order
-  std::vector<double> side[2];
-  std::vector<int64_t> local((size_t)n);
-  std::vector<uint8_t> which((size_t)n);
-  side[0].reserve((size_t)std::min(n, n_bt));
-  side[1].reserve((size_t)n);
-  int64_t b = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    if (i && tids[i] <= tids[i - 1]) return TPE_E_ARG;
-    while (b < n_bt && below_tids[b] < tids[i]) ++b;
-    const int sd = b < n_bt && below_tids[b] == tids[i] ? 0 : 1;
-    which[i] = (uint8_t)sd;
-    local[i] = (int64_t)side[sd].size();
-    side[sd].push_back(x[i]);
+  for (int64_t i = 1; i < n; ++i)
+    if (tids[i] <= tids[i - 1]) return TPE_E_ARG;
+  // ap_filter_trials (tpe.py:629-636): the below set's members among this
+  // label's observations (both tid lists ascending: one merge), coded per
+  // tid-order position t as its rank within its side: r >= 0 above, ~r below
+  static thread_local std::vector<int64_t> code_tl;
+  code_tl.resize((size_t)n);
+  int64_t* code = code_tl.data();
+  int64_t nb = 0;
+  {
+    int64_t b = 0;
+    for (int64_t t = 0; t < n; ++t) {
+      while (b < n_bt && below_tids[b] < tids[t]) ++b;
+      const bool below = b < n_bt && below_tids[b] == tids[t];
+      code[t] = below ? ~nb : t - nb;
+      nb += below;
+    }
   }
-  // each side's sort permutation: the label's order filtered (stable in it)
-  std::vector<int64_t> ord[2];
-  ord[0].reserve(side[0].size());
-  ord[1].reserve(side[1].size());
+  const int64_t na = n - nb;
+  // each side in value order (the label's sorting permutation filtered) with
+  // its tid-order ranks — the order np.argsort gives when no value repeats
+  static thread_local std::vector<double> sv[2];
+  static thread_local std::vector<int64_t> rk[2];
+  sv[0].resize((size_t)nb); rk[0].resize((size_t)nb);
+  sv[1].resize((size_t)na); rk[1].resize((size_t)na);
+  double* svp[2] = {sv[0].data(), sv[1].data()};     // (thread_local storage read once)
+  int64_t* rkp[2] = {rk[0].data(), rk[1].data()};
+  const int64_t lim[2] = {nb, na};
+  int64_t cnt[2] = {0, 0};
   for (int64_t i = 0; i < n; ++i) {
-    const int64_t p = order[i];
-    if (p < 0 || p >= n) return TPE_E_ARG;
-    ord[which[p]].push_back(local[p]);
+    const int64_t t = order[i];
+    if (t < 0 || t >= n) return TPE_E_ARG;
+    const int64_t c = code[t];
+    const int sd = c >= 0;
+    if (cnt[sd] >= lim[sd]) return TPE_E_ARG;      // not a permutation
+    svp[sd][cnt[sd]] = x[t];
+    rkp[sd][cnt[sd]] = sd ? c : ~c;
+    ++cnt[sd];
   }
   const int64_t cap = n + 1;
   for (int sd = 0; sd < 2; ++sd) {
-    const std::vector<double>& v = side[sd];
-    const std::vector<int64_t>& o = ord[sd];
-    const int64_t m = (int64_t)v.size();
+    const double* v = sv[sd].data();
+    const int64_t m = sd ? na : nb;
     out_k[sd] = 0;
-    bool fallback = m >= 1 && v[o[0]] != v[o[0]];                       // NaN
-    for (int64_t i = 1; i < m && !fallback; ++i) fallback = !(v[o[i - 1]] < v[o[i]]);
-    if (fallback) continue;       // repeated values / NaN: np.argsort's order decides the weights
+    bool fallback = m >= 1 && v[0] != v[0];                              // NaN sorts last in `order`...
+    for (int64_t i = 1; i < m && !fallback; ++i) fallback = !(v[i - 1] < v[i]);   // ...or repeated values
+    if (fallback) continue;       // np.argsort's order decides the weights: the caller refits the side
     double* w = out + (3 * sd) * cap;
-    const int64_t pos = tpe_host_fit_parzen(v.data(), m, m >= 2 ? o.data() : nullptr, prior_weight, prior_mu,
-                                            prior_sigma, lf, w, w + cap, w + 2 * cap);
+    const int64_t pos = fit_sorted<true>(v, rk[sd].data(), m, prior_weight, prior_mu, prior_sigma, lf, w, w + cap,
+                                         w + 2 * cap);
     if (pos < 0) return (int)pos;
     out_k[sd] = m + 1;
   }
@@ -283,18 +329,29 @@ int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* orde
 int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
                        int32_t lf, double* out) {
   if (upper <= 0 || n < 0 || !out) return TPE_E_ARG;
-  std::vector<double> counts((size_t)upper, 0.0);
-  if (n > 0) {
-    std::vector<double> lfw((size_t)n);
-    lf_weights(n, lf, lfw.data());
-    for (int64_t i = 0; i < n; ++i) {
-      if (obs[i] < 0 || obs[i] >= upper) return TPE_E_ARG;
-      counts[(size_t)obs[i]] += lfw[i];
+  // np.bincount(obs, linear_forgetting_weights(n, lf), upper): per category the
+  // weights summed in observation order — four interleaved passes would change
+  // that order, so one pass, with the ramp computed on the fly
+  static thread_local std::vector<double> counts_tl;
+  counts_tl.assign((size_t)upper, 0.0);
+  double* counts = counts_tl.data();
+  const bool ramp = lf && n >= lf;
+  const int64_t num = ramp ? n - lf : 0;
+  const double start = n > 0 ? 1.0 / (double)n : 0.0;
+  const double step = num > 1 ? (1.0 - start) / (double)(num - 1) : 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t c = obs[i];
+    if (c < 0 || c >= upper) return TPE_E_ARG;
+    double wi = 1.0;
+    if (i < num) {
+      if (num == 1) wi = start;
+      else if (i < num - 1) { wi = (double)i * step; wi += start; }
     }
+    counts[c] += wi;
   }
   for (int32_t k = 0; k < upper; ++k)
     counts[k] = p_prior ? counts[k] + (double)upper * (prior_weight * p_prior[k]) : counts[k] + prior_weight;
-  const double tot = np_sum(counts.data(), upper);
+  const double tot = np_sum(counts, upper);
   for (int32_t k = 0; k < upper; ++k) out[k] = counts[k] / tot;
   return TPE_OK;
 }
@@ -305,7 +362,8 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
   if (n < 0 || n_bt < 0 || (n && (!obs || !tids)) || (n_bt && !below_tids) || !out_below || !out_above)
     return TPE_E_ARG;
   // ap_filter_trials (tpe.py:629-636): one merge of ascending tids; sides keep tid order
-  std::vector<int64_t> side[2];
+  static thread_local std::vector<int64_t> side[2];
+  side[0].clear(); side[1].clear();
   side[0].reserve((size_t)std::min(n, n_bt));
   side[1].reserve((size_t)n);
   int64_t b = 0;
@@ -849,23 +907,45 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   if (tab_blocks >= ((int64_t)1 << 31)) return TPE_E_ARG;
   const int64_t n_tab_jobs = (int64_t)tab_jobs.size();
+  // sample-stage tile lists: untabulated tiles (lazy categorical last) and tabulated tiles
+  static thread_local std::vector<int32_t> samp_tiles, tab_tiles;
+  samp_tiles.clear(); tab_tiles.clear();
+  for (int pass = 0; pass < 2; ++pass)
+    for (int64_t t = 0; t < (int64_t)tiles.size(); ++t) {
+      const tpe_problem& q = prob[tiles[t].problem];
+      if (q.tab_mode != TPE_TAB_NONE) {
+        if (pass == 0) tab_tiles.push_back((int32_t)t);
+        continue;
+      }
+      const bool lazy = q.family == TPE_FAM_CATEGORICAL && (q.flags & TPE_F_CAT_LAZY) && q.samp_len <= 64;
+      if (lazy == (pass == 1)) samp_tiles.push_back((int32_t)t);
+    }
+  int64_t n_samp_eager = 0;
+  for (int32_t t : samp_tiles) {
+    const tpe_problem& q = prob[tiles[t].problem];
+    n_samp_eager += !(q.family == TPE_FAM_CATEGORICAL && (q.flags & TPE_F_CAT_LAZY) && q.samp_len <= 64);
+  }
+  const int64_t n_samp_tiles = (int64_t)samp_tiles.size(), n_tab_tiles = (int64_t)tab_tiles.size();
+  if (samp_tiles.empty()) samp_tiles.push_back(0);
+  if (tab_tiles.empty()) tab_tiles.push_back(0);
   if (tab_jobs.empty()) tab_jobs.push_back(tpe_tab_job{0, 0, 0, 0, 0, 0});
   const int64_t n_fin = (int64_t)fin_tiles.size();
   if (fin_tiles.empty()) fin_tiles.push_back(0);
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
   // comp32 rows sit at the END of the last two sections and are not copied ----
-  const int NS = 12;
+  const int NS = 14;
   const void* src[NS] = {prob.data(), tiles.data(), work.data(), comp64.data(), samp.data(), fit.data(),
-                         below_idx.data(), fit_seg.data(), fin_tiles.data(), tab_jobs.data(), grid.data(),
-                         comp32.data()};
+                         below_idx.data(), fit_seg.data(), fin_tiles.data(), tab_jobs.data(), samp_tiles.data(),
+                         tab_tiles.data(), grid.data(), comp32.data()};
   const int64_t len[NS] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
                            (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp64.size() * sizeof(double)),
                            (int64_t)(samp.size() * sizeof(double)), (int64_t)(fit.size() * sizeof(tpe_fit_job)),
                            (int64_t)(below_idx.size() * sizeof(int32_t)), (int64_t)(fit_seg.size() * sizeof(int64_t)),
                            (int64_t)(fin_tiles.size() * sizeof(int32_t)),
                            (int64_t)(tab_jobs.size() * sizeof(tpe_tab_job)),
+                           (int64_t)(samp_tiles.size() * sizeof(int32_t)), (int64_t)(tab_tiles.size() * sizeof(int32_t)),
                            (int64_t)(grid.size() * sizeof(int32_t)), (int64_t)(comp32.size() * sizeof(float))};
-  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
+  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
   int64_t off[NS], end = 0;
   for (int i = 0; i < NS; ++i) {
     off[i] = (end + 255) & ~(int64_t)255;
@@ -878,7 +958,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   for (size_t q = 1; q < fit_seg.size(); ++q) info->fit_max_seg = std::max(info->fit_max_seg, fit_seg[q] - fit_seg[q - 1]);
   info->off_tab_jobs = off[9]; info->n_tab_jobs = n_tab_jobs; info->tab_blocks = tab_blocks;
   info->tab_units = tab_units;
-  info->off_grid = off[10]; info->off_comp32 = off[11];
+  info->off_samp_tiles = off[10]; info->n_samp_tiles = n_samp_tiles; info->n_samp_eager = n_samp_eager;
+  info->off_tab_tiles = off[11]; info->n_tab_tiles = n_tab_tiles;
+  info->off_grid = off[12]; info->off_comp32 = off[13];
   info->n_problems = P;
   info->n_tiles = (int64_t)tiles.size();
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
@@ -888,12 +970,12 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->part_total = part_total;
   info->n_fit = (int32_t)fit.size(); info->reserved = 0;
   info->fit_total = fit_seg.back();
-  info->copy_end = off[10] + len[10];
+  info->copy_end = off[12] + len[12];
   info->sort_count = n_sorted_prob * (int64_t)n_cand;
   info->n_sorted = S;
   info->n_pooled = n_pooled;
   info->draw_blocks = (C_ref + 1 + 63) / 64;
-  info->copy2_len = len[11];
+  info->copy2_len = len[13];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;
   for (int i = 0; i < NS; ++i)

@@ -512,11 +512,14 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
                                                      int precision, int draw, int key_bits, int flags,
                                                      const double* __restrict__ draw_pref, int64_t draw_blocks,
                                                      int ordered, unsigned long long* __restrict__ pool_best,
-                                                     const float4* __restrict__ comp32,
-                                                     const int32_t* __restrict__ grid,
-                                                     const float4* __restrict__ tab) {
-  const tpe_tile tl = tiles[blockIdx.x];
+                                                     const int32_t* __restrict__ list) {
+  const int tile = list ? list[blockIdx.x] : (int)blockIdx.x;
+  const tpe_tile tl = tiles[tile];
   const tpe_problem& p = P[tl.problem];
+  if (p.tab_mode != TPE_TAB_NONE) return;   // k_sample_tab's
+  if (draw && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= kCumLds && (p.flags & TPE_F_CAT_LAZY) &&
+      !(flags & TPE_BATCH_WRITE_CAND) && !l_out)
+    return;                                // lazy categorical: the select stage scans the first draws itself
   if ((p.flags & TPE_F_POOLED) && tl.cand_start == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     pool_best[tl.problem] = 0ull;          // scored after this kernel: no race
   const bool store_x = (flags & TPE_BATCH_WRITE_CAND) || precision == TPE_PREC_F64 ||
@@ -537,8 +540,6 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
   const bool valid = i < p.n_cand;
   const int64_t o = p.cand_off + i;
   if (draw && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= kCumLds) {
-    // lazy categorical: the select stage scans the first draws itself
-    if ((p.flags & TPE_F_CAT_LAZY) && !(flags & TPE_BATCH_WRITE_CAND) && !l_out) return;
     // The score of a categorical candidate depends only on its category, so the
     // slice's argmax (np.argmax: best score, then first index) is the best
     // category among those drawn, at its first draw.  First index per category:
@@ -576,55 +577,8 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
           b.g = comp64[p.above_off + cc].x;
           b.idx = first[cc];
         }
-      tile_best[(int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y] = b;
+      tile_best[(int64_t)tile * TPE_BEST_PER_TILE + blockIdx.y] = b;
     }
-    return;
-  }
-  if (p.tab_mode != TPE_TAB_NONE) {
-    // tabulated scoring: the draw is scored from the label's tables and the
-    // slice's best goes straight to its tile_best slot (no candidate stores)
-    double x = 0.0, l = 0.0, g = 0.0;
-    float t = 0.f;
-    if (valid) {
-      if (!draw) {
-        t = coord[o];
-        x = cand[o];
-      } else if (p.samp_len > 0) {
-        int c;
-        draw_one(p, S, in_lds ? cum_lds : S, in_lds ? 1 : 8, i, precision, lo_f, hi_f, x, t, c);
-      } else {
-        x = NAN; t = NAN;
-      }
-      if (p.tab_mode == TPE_TAB_CELLS) {
-        float lb2 = cell_log2(p, 0, tab, t), la2 = cell_log2(p, 1, tab, t);
-        if (!(lb2 == lb2)) lb2 = lse2_exact_ool(comp32, p.below_off, p.below_len, 0, 0, t);
-        if (!(la2 == la2))
-          la2 = p.narrow_amin > 0.f ? lse2_pruned(p, comp32, grid, t)
-                                    : lse2_exact_ool(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
-        const double lnx = p.family == TPE_FAM_LOGGAUSS ? (double)t : 0.0;
-        l = (double)lb2 * kLn2 + p.below_base - lnx;
-        g = (double)la2 * kLn2 + p.above_base - lnx;
-      } else {
-        const double mq = rint(x / p.q);
-        const double jq = mq - (double)p.lat_lo;
-        if (mq * p.q == x && jq >= 0.0 && jq < (double)p.tab_n[0]) {
-          const double2 r = reinterpret_cast<const double2*>(tab)[p.tab_off[0] + (int64_t)jq];
-          l = r.x;
-          g = r.y;
-        } else {
-          // unreachable for device draws (the lattice spans every value they can
-          // take; caller-drawn candidates disable the table, TPE_F_NO_TABLE): the
-          // candidate drops out (an f64 mass sum here would triple this
-          // kernel's registers)
-          l = -INFINITY;
-          g = 0.0;
-        }
-      }
-      if (l_out) { l_out[o] = l; g_out[o] = g; }
-      if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
-    }
-    block_best(valid ? l - g : 0.0, valid ? (int64_t)i : -1, l, g,
-               tile_best + (int64_t)blockIdx.x * TPE_BEST_PER_TILE + blockIdx.y);
     return;
   }
   // ordered draws of a sorted problem: no sort follows, candidates go straight
@@ -677,6 +631,124 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
   } else {
     vals_sorted[o] = v;                    // never sorted: straight to its final place
   }
+}
+
+// Tabulated problems (include/tpe_hip.h "Tabulated scoring"): kTabBlocks
+// workgroups per 2048-candidate tile, kTabPer candidates per thread; each draw
+// (or injected candidate) is scored from the label's tables, every thread
+// keeps its best and each workgroup's best goes to its tile_best slot (the
+// slots past kTabBlocks are empty).  Nothing per candidate is stored unless
+// asked for (l_out / TPE_BATCH_WRITE_CAND).
+#ifndef TPE_TAB_PER
+#define TPE_TAB_PER 2
+#endif
+constexpr int kTabPer = TPE_TAB_PER;                 // candidates per thread
+constexpr int kTabBlocks = kTile / (kThreads * kTabPer);   // workgroups per tile (slot = blockIdx.y)
+static_assert(kTabBlocks >= 1 && kTabBlocks <= TPE_BEST_PER_TILE && kTabBlocks * kThreads * kTabPer == kTile,
+              "tabulated sample tiling");
+
+// PREC is a template parameter: with the f64 inverse-CDF path reachable, the
+// candidate loop needs ~4x the registers
+template <int PREC>
+__global__ __launch_bounds__(kThreads) void k_sample_tab(const tpe_problem* __restrict__ P,
+                                                         const tpe_tile* __restrict__ tiles,
+                                                         const int32_t* __restrict__ list,
+                                                         const double* __restrict__ samp,
+                                                         double* __restrict__ cand, const float* __restrict__ coord,
+                                                         tpe_best* __restrict__ tile_best,
+                                                         double* __restrict__ l_out, double* __restrict__ g_out,
+                                                         int draw, int flags,
+                                                         const float4* __restrict__ comp32,
+                                                         const int32_t* __restrict__ grid,
+                                                         const float4* __restrict__ tab) {
+  const int tile = list ? list[blockIdx.x] : (int)blockIdx.x;
+  const tpe_tile tl = tiles[tile];
+  const tpe_problem& p = P[tl.problem];
+  if (p.tab_mode == TPE_TAB_NONE) return;  // k_sample's
+  float lo_f, hi_f;
+  f32_bounds(p, lo_f, hi_f);
+  const double* S = samp + 8 * (int64_t)p.samp_off;
+  __shared__ double cum_lds[kCumLds];
+  const bool in_lds = draw && p.samp_len <= kCumLds;
+  if (in_lds)
+    for (int q = threadIdx.x; q < p.samp_len; q += kThreads) cum_lds[q] = S[8 * q];
+  __syncthreads();
+  const bool cells = p.tab_mode == TPE_TAB_CELLS;
+  const bool logc = p.family == TPE_FAM_LOGGAUSS;
+  double bs = 0.0, bl = 0.0, bg = 0.0;
+  int64_t bi = -1;
+  // candidate j (0 .. kTabPer-1) of this thread: its value x and coordinate t
+  auto fetch = [&](int i, int64_t o, double& x, float& t) {
+    if (!draw) {
+      t = coord[o];
+      x = cand[o];
+    } else if (p.samp_len > 0) {
+      int c;
+      draw_one(p, S, in_lds ? cum_lds : S, in_lds ? 1 : 8, i, PREC, lo_f, hi_f, x, t, c);
+    } else {
+      x = NAN; t = NAN;
+    }
+  };
+  auto emit = [&](int i, int64_t o, double x, double l, double g) {
+    if (l_out) { l_out[o] = l; g_out[o] = g; }
+    if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
+    if (better(l - g, i, bs, bi)) { bs = l - g; bl = l; bg = g; bi = i; }
+  };
+  uint32_t exact = 0;                      // candidates the cell tables do not cover (rare)
+  const int first = tl.cand_start + (int)blockIdx.y * (kThreads * kTabPer) + (int)threadIdx.x;
+  for (int j = 0; j < kTabPer; ++j) {
+    const int i = first + j * kThreads;
+    if (i >= p.n_cand) break;
+    const int64_t o = p.cand_off + i;
+    double x, l, g;
+    float t;
+    fetch(i, o, x, t);
+    if (cells) {
+      const float lb2 = cell_log2(p, 0, tab, t), la2 = cell_log2(p, 1, tab, t);
+      if (!(lb2 == lb2) || !(la2 == la2)) { exact |= 1u << j; continue; }
+      const double lnx = logc ? (double)t : 0.0;
+      l = (double)lb2 * kLn2 + p.below_base - lnx;
+      g = (double)la2 * kLn2 + p.above_base - lnx;
+    } else {
+      const double mq = rint(x / p.q);
+      const double jq = mq - (double)p.lat_lo;
+      if (mq * p.q == x && jq >= 0.0 && jq < (double)p.tab_n[0]) {
+        const double2 r = reinterpret_cast<const double2*>(tab)[p.tab_off[0] + (int64_t)jq];
+        l = r.x;
+        g = r.y;
+      } else {
+        // unreachable for device draws (the lattice spans every value they can
+        // take; caller-drawn candidates disable the table, TPE_F_NO_TABLE): the
+        // candidate drops out (an f64 mass sum here would triple this
+        // kernel's registers)
+        l = -INFINITY;
+        g = 0.0;
+      }
+    }
+    emit(i, o, x, l, g);
+  }
+  // candidates outside the cells or in flagged ones: re-drawn and summed exactly
+  // (out of line, after the main loop)
+  while (exact) {
+    const int j = __builtin_ctz(exact);
+    exact &= exact - 1;
+    const int i = first + j * kThreads;
+    const int64_t o = p.cand_off + i;
+    double x;
+    float t;
+    fetch(i, o, x, t);
+    float lb2 = cell_log2(p, 0, tab, t), la2 = cell_log2(p, 1, tab, t);
+    if (!(lb2 == lb2)) lb2 = lse2_exact_ool(comp32, p.below_off, p.below_len, 0, 0, t);
+    if (!(la2 == la2))
+      la2 = p.narrow_amin > 0.f ? lse2_pruned(p, comp32, grid, t)
+                                : lse2_exact_ool(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
+    const double lnx = logc ? (double)t : 0.0;
+    emit(i, o, x, (double)lb2 * kLn2 + p.below_base - lnx, (double)la2 * kLn2 + p.above_base - lnx);
+  }
+  tpe_best* __restrict__ slot = tile_best + (int64_t)tile * TPE_BEST_PER_TILE;
+  block_best(bs, bi, bl, bg, slot + blockIdx.y);
+  if (blockIdx.y == 0 && threadIdx.x >= kTabBlocks && threadIdx.x < TPE_BEST_PER_TILE)
+    slot[threadIdx.x] = tpe_best{0, 0, 0, -1};
 }
 
 // row of `part` a work item writes: its tile's first work item + its split
@@ -2005,11 +2077,29 @@ int tpe_sample(const tpe_batch* b, void* stream) {
                        b->draw_blocks, b->draw_pref);
     if ((rc = hip_check("tpe_sample/prefix"))) return rc;
   }
-  hipLaunchKernelGGL(k_sample, dim3(b->n_tiles, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
-                     b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
-                     b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
-                     b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0, b->pool_best, (const float4*)b->comp32,
-                     b->grid, (const float4*)b->tab);
+  // generic kernel over the untabulated tiles (without the lazy categorical
+  // ones when the select stage scans those), tabulated tiles apart; no lists:
+  // both kernels over every tile, each skipping the other's
+  const bool lazy = b->sample && !(b->flags & TPE_BATCH_WRITE_CAND) && !b->l_out;
+  const int n_gen = b->samp_tiles ? (lazy ? b->n_samp_eager : b->n_samp_tiles) : b->n_tiles;
+  const int n_tab = b->tab_tiles ? b->n_tab_tiles : (b->n_tab_jobs > 0 ? b->n_tiles : 0);
+  if (n_gen > 0)
+    hipLaunchKernelGGL(k_sample, dim3(n_gen, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
+                       b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
+                       b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
+                       b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0, b->pool_best,
+                       b->samp_tiles);
+  if (n_tab > 0) {
+    if (!b->tab) return fail(TPE_E_ARG, "tabulated tiles without score tables");
+    if (b->precision == TPE_PREC_F64)
+      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F64>, dim3(n_tab, kTabBlocks), dim3(kThreads), 0, (hipStream_t)stream,
+                         b->problems, b->tiles, b->tab_tiles, b->samp, b->cand, b->coord, b->tile_best, b->l_out,
+                         b->g_out, b->sample, b->flags, (const float4*)b->comp32, b->grid, (const float4*)b->tab);
+    else
+      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F32>, dim3(n_tab, kTabBlocks), dim3(kThreads), 0, (hipStream_t)stream,
+                         b->problems, b->tiles, b->tab_tiles, b->samp, b->cand, b->coord, b->tile_best, b->l_out,
+                         b->g_out, b->sample, b->flags, (const float4*)b->comp32, b->grid, (const float4*)b->tab);
+  }
   return hip_check("tpe_sample");
 }
 
@@ -2180,6 +2270,11 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.part = ws->part;
   b.tile_best = ws->tile_best;
   if (info.n_pooled > 0) b.pool_best = ws->pool_best;
+  b.samp_tiles = (const int32_t*)(dev + info.off_samp_tiles);
+  b.n_samp_tiles = (int32_t)info.n_samp_tiles;
+  b.n_samp_eager = (int32_t)info.n_samp_eager;
+  b.tab_tiles = (const int32_t*)(dev + info.off_tab_tiles);
+  b.n_tab_tiles = (int32_t)info.n_tab_tiles;
   if (info.n_tab_jobs > 0) {
     b.tab_jobs = (const tpe_tab_job*)(dev + info.off_tab_jobs);
     b.n_tab_jobs = (int32_t)info.n_tab_jobs;

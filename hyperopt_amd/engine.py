@@ -683,6 +683,8 @@ class Engine(object):
         b.tile_best, b.result = d_best.data_ptr(), d_res.data_ptr()
         if info.n_pooled:
             b.pool_best = self._buf('pool_best', P, torch.int64).data_ptr()
+        b.samp_tiles, b.n_samp_tiles, b.n_samp_eager = base + info.off_samp_tiles, info.n_samp_tiles, info.n_samp_eager
+        b.tab_tiles, b.n_tab_tiles = base + info.off_tab_tiles, info.n_tab_tiles
         if info.n_tab_jobs:
             b.tab_jobs, b.n_tab_jobs, b.tab_blocks = base + info.off_tab_jobs, info.n_tab_jobs, info.tab_blocks
             b.tab = self._buf('tab', 4 * int(info.tab_units), torch.float32).data_ptr()
@@ -797,6 +799,12 @@ class Engine(object):
         b.ce_count = None
         for i, (name, fn, gi, units) in enumerate(stages):
             rec = (evs[i].elapsed_time(evs[i + 1]) / rep, units)
+            if name == 'k_sample':
+                # algorithmic component evaluations of the tabulated problems (C x K
+                # per problem: what the reference evaluates; the tables do not)
+                tabp = prob['tab_mode'] != N.TAB_NONE
+                rec = rec + (float(((prob['below_len'] + prob['above_len'])[tabp]).astype(np.float64).sum()
+                                   * n_cand),)
             if name == 'k_above_f32':
                 n_c = float(((fam == N.FAM_GAUSS) | (fam == N.FAM_LOGGAUSS)).sum() * n_cand)
                 rec = rec + (float(executed), float(expanded), n_c)

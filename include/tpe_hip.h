@@ -335,6 +335,12 @@ typedef struct tpe_batch {
   /* tabulated scoring: table jobs and the table storage (16-B units) */
   const tpe_tab_job* tab_jobs; int32_t n_tab_jobs; int32_t tab_blocks;
   void* tab; int64_t tab_units;
+  /* sample-stage tile lists (NULL: every tile through the generic sample kernel):
+   * samp_tiles[0 .. n_samp_tiles) = the untabulated tiles, lazy categorical ones
+   * last (the first n_samp_eager of them skip those when the lazy scan applies);
+   * tab_tiles[0 .. n_tab_tiles) = the tabulated tiles (one 2048-candidate block each) */
+  const int32_t* samp_tiles; int32_t n_samp_tiles; int32_t n_samp_eager;
+  const int32_t* tab_tiles; int32_t n_tab_tiles; int32_t reserved7;
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
@@ -412,6 +418,7 @@ typedef struct tpe_pack_info {
   int64_t n_sorted, draw_blocks;        /* tpe_batch.n_sorted / draw_blocks */
   int64_t n_pooled;                     /* pooled problems (tpe_batch.pool_best needed) */
   int64_t off_tab_jobs, n_tab_jobs, tab_blocks, tab_units;   /* tabulated scoring (tpe_batch.tab_*) */
+  int64_t off_samp_tiles, n_samp_tiles, n_samp_eager, off_tab_tiles, n_tab_tiles;   /* tpe_batch tile lists */
 } tpe_pack_info;
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation

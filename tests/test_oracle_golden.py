@@ -120,3 +120,20 @@ def test_fmin_trajectories_exact(golden):
             want = [{k: float(v) for k, v in d.items()} for d in run['vals']]
             assert got == want
             assert [h['loss'] for h in hist] == run['loss']
+
+
+def test_oracle_runs_at_reference_speed():
+    """bench.py's cpu_baseline times the oracle (kind "port") because the
+    reference cannot run on the GPU box; tools/oracle_vs_reference.py timed both
+    here on the same suggests (config 2, and the cpu_baseline workload: the
+    config-3 tree, 10k history, C = 16384): identical outputs, and the port's
+    time within +-15 % of the reference's."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), '..', 'profiles', 'r02_oracle_vs_reference.json')
+    with open(path) as f:
+        runs = json.load(f)['runs']
+    assert {r['space'] for r in runs} == {'mixed10', 'tree'}
+    for r in runs:
+        assert r['identical_outputs'], r['space']
+        assert 0.85 <= r['ratio'] <= 1.15, (r['space'], r['ratio'])
