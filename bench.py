@@ -156,6 +156,17 @@ def _pmc():
         return json.load(f)
 
 
+# a profiled stage and the kernels it launches (counters are summed per dispatch)
+STAGE_KERNELS = {'k_sample': ('k_sample', 'k_sample_tab')}
+
+
+def _stage_counters(pmc, stage):
+    parts = [pmc[k] for k in STAGE_KERNELS.get(stage, (stage,)) if k in pmc]
+    if len(parts) <= 1:
+        return parts[0] if parts else {}
+    return {c: sum(p.get(c, 0.0) for p in parts) for c in set().union(*parts) if c != 'dispatches'}
+
+
 def roofline(prof):
     """Roofline of every measured stage and of the dominant one (largest total
     device time): work per launch / the launch's average duration, the
@@ -176,7 +187,7 @@ def roofline(prof):
             continue
         secs = ms.sum() * 1e-3
         k = dict(avg_launch_ms=float(ms.mean()), launches=int(len(ms)), total_ms=float(ms.sum()))
-        c = pmc.get(name, {})
+        c = _stage_counters(pmc, name)
         if name == 'sort':
             nbytes = np.array([r[1] for r in recs])
             ach = nbytes.sum() / secs / 1e9
@@ -205,6 +216,7 @@ def roofline(prof):
         return None, kernels
     r = dict(kernels[dom])
     r['kernel'] = dom
+    r['stage_kernels'] = [k for k in STAGE_KERNELS.get(dom, (dom,)) if k in _pmc()] or [dom]
     r.setdefault('traffic', None)
     if r['traffic'] is not None:
         r['traffic_source'] = 'profiles/r02_pmc_summary.json: (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 ' \

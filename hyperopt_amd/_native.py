@@ -17,7 +17,7 @@ BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate til
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE = 1, 2, 4, 8, 16
 TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
-BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS = 1, 2, 4, 8
+BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS, BATCH_TAB_EXACT = 1, 2, 4, 8, 16
 PREC_F32, PREC_F64 = 0, 1
 
 # numpy mirrors of the C structs (the host builds arrays of them and copies

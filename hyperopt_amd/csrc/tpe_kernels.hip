@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
@@ -138,6 +139,30 @@ __device__ __forceinline__ T lse2_exact(const C4* __restrict__ comp, int k0, int
 __device__ __attribute__((noinline)) float lse2_exact_ool(const float4* __restrict__ comp, int k0, int n, int k1,
                                                           int n1, float t) {
   return lse2_exact<float, float4>(comp, k0, n, k1, n1, t);
+}
+
+// the same sum at a wave-uniform t, the wave's lanes striding over the
+// components (inline, few registers: the tabulated sample kernel's fallback)
+__device__ __forceinline__ float lse2_wave(const float4* __restrict__ comp, int k0, int n0, int k1, int n1, float t) {
+  const int lane = threadIdx.x & 63, n = n0 + n1;
+  float m = -INFINITY;
+#pragma unroll 1
+  for (int i = lane; i < n; i += 64) {
+    const float4 c = i < n0 ? comp[k0 + i] : comp[k1 + i - n0];
+    const float z = ((t - c.x) - c.y) * c.z;
+    m = fmaxf(m, c.w - z * z);
+  }
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if (!(m > -INFINITY)) return m;
+  float s = 0.f;
+#pragma unroll 1
+  for (int i = lane; i < n; i += 64) {
+    const float4 c = i < n0 ? comp[k0 + i] : comp[k1 + i - n0];
+    const float z = ((t - c.x) - c.y) * c.z;
+    s += exp2f(c.w - z * z - m);
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  return m + log2f(s);
 }
 
 // Max-shifted log2-sum of a PRUNED above mixture at t (the fixed-shift sum
@@ -298,6 +323,17 @@ __device__ __forceinline__ int find_comp(const tpe_problem& p, const double* __r
 // Value x and kernel coordinate t (x, or ln x before quantisation for log
 // families) of a draw from component a of the below mixture, by inversion of its
 // truncated normal at the uniform uf (f32) / ud (f64).
+// f32 inversion of sampler row s (truncated normal; fa, fb = Phi of the
+// mirrored bounds) at the uniform uf: the kernel coordinate of the draw
+__device__ __forceinline__ float comp_coord_f32(const double* __restrict__ s, float uf, float lo_f, float hi_f) {
+  const float pr = (float)s[3] + uf * ((float)s[4] - (float)s[3]);
+  float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+  if (s[5] != 0.0) z = -z;
+  float xf = (float)s[1] + (float)s[2] * z;
+  if (!(xf == xf)) xf = (float)s[1];
+  return fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
+}
+
 __device__ __forceinline__ void draw_comp(const tpe_problem& p, const double* __restrict__ S, int a, float uf,
                                           double ud, int precision, float lo_f, float hi_f, double& x, float& t) {
   const double* s = S + 8 * a;
@@ -305,14 +341,8 @@ __device__ __forceinline__ void draw_comp(const tpe_problem& p, const double* __
   const double mu = s[1], sg = s[2], fa = s[3], fb = s[4];
   const bool flip = s[5] != 0.0;
   if (precision == TPE_PREC_F32) {
-    const float pr = (float)fa + uf * ((float)fb - (float)fa);
-    float z = -1.41421356237309505f * erfcinvf(2.f * pr);
-    if (flip) z = -z;
-    float xf = (float)mu + (float)sg * z;
-    if (!(xf == xf)) xf = (float)mu;
-    xf = fminf(fmaxf(xf, lo_f), hi_f);   // low <= draw < high (tpe.py:86)
-    t = xf;
-    x = (double)xf;
+    t = comp_coord_f32(s, uf, lo_f, hi_f);
+    x = (double)t;
   } else {
     const double pr = fa + ud * (fb - fa);
     double z = -1.41421356237309505 * erfcinv(2.0 * pr);
@@ -345,6 +375,16 @@ __device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __r
     return;
   }
   draw_comp(p, S, a, u01f(r.z), u01d(r.z, r.w), precision, lo_f, hi_f, x, t);
+}
+
+// draw_one's kernel coordinate alone (f32, continuous families): no f64 value
+__device__ __forceinline__ float draw_coord_f32(const tpe_problem& p, const double* __restrict__ S,
+                                                const double* __restrict__ cum, int cs, int64_t i, float lo_f,
+                                                float hi_f) {
+  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+  const int a = find_comp(p, cum, cs, u01d(r.x, r.y));
+  return comp_coord_f32(S + 8 * a, u01f(r.z), lo_f, hi_f);
 }
 
 // ------------------------------------------------------------ ordered draws
@@ -473,24 +513,6 @@ __device__ __forceinline__ void block_best(double sc, int64_t orig, double l, do
 // c, 1/h, flag, 0}.
 constexpr int kTabMoments = 11;        // degree-10 Taylor moments per cell
 constexpr float kTabDrop = 50.f;       // terms below 2^-50 of the cell's largest are dropped
-
-// log2 of one mixture side's sum at t from its cell table; NAN when t lies
-// outside the cells, in a flagged cell, or the series is not positive (the
-// caller then sums the mixture exactly)
-__device__ __forceinline__ float cell_log2(const tpe_problem& p, int side, const float4* __restrict__ tab, float t) {
-  const float gj = floorf((t - p.tab_lo[side]) * p.tab_inv[side]);
-  if (!(gj >= 0.f && gj < (float)p.tab_n[side])) return NAN;
-  const float4* __restrict__ r = tab + p.tab_off[side] + 4 * (int)gj;
-  const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-  if (d.z != 0.f) return NAN;
-  const float u = (t - d.x) * d.y;
-  float sm = c.z;
-  sm = __builtin_fmaf(sm, u, c.y); sm = __builtin_fmaf(sm, u, c.x);
-  sm = __builtin_fmaf(sm, u, b.w); sm = __builtin_fmaf(sm, u, b.z); sm = __builtin_fmaf(sm, u, b.y);
-  sm = __builtin_fmaf(sm, u, b.x); sm = __builtin_fmaf(sm, u, a.w); sm = __builtin_fmaf(sm, u, a.z);
-  sm = __builtin_fmaf(sm, u, a.y); sm = __builtin_fmaf(sm, u, a.x);
-  return sm > 0.f ? c.w + __log2f(sm) : NAN;
-}
 
 // Draws (when `draw`) and writes the sort keys: (sorted problem << key_bits) |
 // value bucket.  Grid (tiles, TPE_BEST_PER_TILE): block (x, y) handles the y-th
@@ -633,122 +655,274 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
   }
 }
 
-// Tabulated problems (include/tpe_hip.h "Tabulated scoring"): kTabBlocks
-// workgroups per 2048-candidate tile, kTabPer candidates per thread; each draw
-// (or injected candidate) is scored from the label's tables, every thread
-// keeps its best and each workgroup's best goes to its tile_best slot (the
-// slots past kTabBlocks are empty).  Nothing per candidate is stored unless
+// Tabulated problems (include/tpe_hip.h "Tabulated scoring").  One 1024-thread
+// workgroup per CU-sized group of `per_wg` tabulated tiles (list order: a
+// problem's tiles are contiguous).  On entering a problem the workgroup stages
+// its selection CDF, a guide table into it, compact f32 sampler rows and —
+// when they fit — both cell tables in LDS, so a candidate's draw and score
+// issue no global loads: Philox, a guide-started CDF scan, the f32 inverse CDF,
+// two table rows and their Horner sums.  Every thread keeps its best; a run of
+// tiles of one problem leaves its best in slot 0 of the run's first tile (the
+// other slots of its tiles are empty).  Nothing per candidate is stored unless
 // asked for (l_out / TPE_BATCH_WRITE_CAND).
-#ifndef TPE_TAB_PER
-#define TPE_TAB_PER 2
-#endif
-constexpr int kTabPer = TPE_TAB_PER;                 // candidates per thread
-constexpr int kTabBlocks = kTile / (kThreads * kTabPer);   // workgroups per tile (slot = blockIdx.y)
-static_assert(kTabBlocks >= 1 && kTabBlocks <= TPE_BEST_PER_TILE && kTabBlocks * kThreads * kTabPer == kTile,
-              "tabulated sample tiling");
+constexpr int kTabThreads = 1024;
+constexpr int kTabLdsCells = 1536;                  // 96 KiB of 64-B cell rows
+constexpr int kGuide = 64;                          // CDF guide entries
+constexpr int kTabMaxTilesPerWg = 16;
+static_assert(kTile % kTabThreads == 0, "tabulated sample tiling");
+constexpr int kTabPer = kTile / kTabThreads;         // candidates per thread per tile
+
+// first k with u < cum_k (k <= len - 1), starting at the guide entry of u:
+// the binary search's answer (find_comp) on a non-decreasing CDF
+__device__ __forceinline__ int guided_comp(const double* __restrict__ cum, const int* __restrict__ guide, int len,
+                                           double u) {
+  int k = guide[min((int)(u * (double)kGuide), kGuide - 1)];
+  while (k < len - 1 && !(u < cum[k])) ++k;
+  return k;
+}
+
+// log2 of one mixture side's sum at t from its cell rows (LDS or global); NAN
+// when t lies outside the cells, in a flagged cell, or the series is not
+// positive (the caller then sums the mixture exactly)
+// (row j's k-th float4 at rows[k * stride + j * step]: global rows are
+// contiguous, stride 1 / step 4; LDS rows are split in planes, stride
+// kTabLdsCells / step 1, so random rows of a wave spread over the banks)
+__device__ __forceinline__ float cell_log2_lds(float lo, float inv, int n, const float4* __restrict__ rows,
+                                               int stride, int step, float t) {
+  const float gj = floorf((t - lo) * inv);
+  if (!(gj >= 0.f && gj < (float)n)) return NAN;
+  const float4* __restrict__ r = rows + step * (int)gj;
+  const float4 a = r[0], b = r[stride], c = r[2 * stride], d = r[3 * stride];
+  if (d.z != 0.f) return NAN;
+  const float u = (t - d.x) * d.y;
+  float sm = c.z;
+  sm = __builtin_fmaf(sm, u, c.y); sm = __builtin_fmaf(sm, u, c.x);
+  sm = __builtin_fmaf(sm, u, b.w); sm = __builtin_fmaf(sm, u, b.z); sm = __builtin_fmaf(sm, u, b.y);
+  sm = __builtin_fmaf(sm, u, b.x); sm = __builtin_fmaf(sm, u, a.w); sm = __builtin_fmaf(sm, u, a.z);
+  sm = __builtin_fmaf(sm, u, a.y); sm = __builtin_fmaf(sm, u, a.x);
+  return sm > 0.f ? c.w + __log2f(sm) : NAN;
+}
 
 // PREC is a template parameter: with the f64 inverse-CDF path reachable, the
-// candidate loop needs ~4x the registers
+// candidate loop needs several times the registers
 template <int PREC>
-__global__ __launch_bounds__(kThreads) void k_sample_tab(const tpe_problem* __restrict__ P,
-                                                         const tpe_tile* __restrict__ tiles,
-                                                         const int32_t* __restrict__ list,
-                                                         const double* __restrict__ samp,
-                                                         double* __restrict__ cand, const float* __restrict__ coord,
-                                                         tpe_best* __restrict__ tile_best,
-                                                         double* __restrict__ l_out, double* __restrict__ g_out,
-                                                         int draw, int flags,
-                                                         const float4* __restrict__ comp32,
-                                                         const int32_t* __restrict__ grid,
-                                                         const float4* __restrict__ tab) {
-  const int tile = list ? list[blockIdx.x] : (int)blockIdx.x;
-  const tpe_tile tl = tiles[tile];
-  const tpe_problem& p = P[tl.problem];
-  if (p.tab_mode == TPE_TAB_NONE) return;  // k_sample's
-  float lo_f, hi_f;
-  f32_bounds(p, lo_f, hi_f);
-  const double* S = samp + 8 * (int64_t)p.samp_off;
+__global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* __restrict__ P,
+                                                            const tpe_tile* __restrict__ tiles,
+                                                            const int32_t* __restrict__ list, int n_list,
+                                                            int per_wg, const double* __restrict__ samp,
+                                                            double* __restrict__ cand,
+                                                            const float* __restrict__ coord,
+                                                            tpe_best* __restrict__ tile_best,
+                                                            double* __restrict__ l_out, double* __restrict__ g_out,
+                                                            int draw, int flags,
+                                                            const float4* __restrict__ comp32,
+                                                            const float4* __restrict__ tab) {
+  __shared__ float4 tab_lds[4 * kTabLdsCells];
   __shared__ double cum_lds[kCumLds];
-  const bool in_lds = draw && p.samp_len <= kCumLds;
-  if (in_lds)
-    for (int q = threadIdx.x; q < p.samp_len; q += kThreads) cum_lds[q] = S[8 * q];
-  __syncthreads();
-  const bool cells = p.tab_mode == TPE_TAB_CELLS;
-  const bool logc = p.family == TPE_FAM_LOGGAUSS;
+  __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
+  __shared__ int guide[kGuide];
+  __shared__ tpe_best wb[kTabThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool need_x = l_out != nullptr || (flags & TPE_BATCH_WRITE_CAND);
+  int cur = -1, run_tile = -1;            // problem staged, first tile of its run
+  bool in_lds = false, tab_in_lds = false;
   double bs = 0.0, bl = 0.0, bg = 0.0;
   int64_t bi = -1;
-  // candidate j (0 .. kTabPer-1) of this thread: its value x and coordinate t
-  auto fetch = [&](int i, int64_t o, double& x, float& t) {
-    if (!draw) {
-      t = coord[o];
-      x = cand[o];
-    } else if (p.samp_len > 0) {
-      int c;
-      draw_one(p, S, in_lds ? cum_lds : S, in_lds ? 1 : 8, i, PREC, lo_f, hi_f, x, t, c);
-    } else {
-      x = NAN; t = NAN;
-    }
-  };
   auto emit = [&](int i, int64_t o, double x, double l, double g) {
     if (l_out) { l_out[o] = l; g_out[o] = g; }
     if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
     if (better(l - g, i, bs, bi)) { bs = l - g; bl = l; bg = g; bi = i; }
   };
-  uint32_t exact = 0;                      // candidates the cell tables do not cover (rare)
-  const int first = tl.cand_start + (int)blockIdx.y * (kThreads * kTabPer) + (int)threadIdx.x;
-  for (int j = 0; j < kTabPer; ++j) {
-    const int i = first + j * kThreads;
-    if (i >= p.n_cand) break;
-    const int64_t o = p.cand_off + i;
-    double x, l, g;
-    float t;
-    fetch(i, o, x, t);
-    if (cells) {
-      const float lb2 = cell_log2(p, 0, tab, t), la2 = cell_log2(p, 1, tab, t);
-      if (!(lb2 == lb2) || !(la2 == la2)) { exact |= 1u << j; continue; }
-      const double lnx = logc ? (double)t : 0.0;
-      l = (double)lb2 * kLn2 + p.below_base - lnx;
-      g = (double)la2 * kLn2 + p.above_base - lnx;
-    } else {
-      const double mq = rint(x / p.q);
-      const double jq = mq - (double)p.lat_lo;
-      if (mq * p.q == x && jq >= 0.0 && jq < (double)p.tab_n[0]) {
-        const double2 r = reinterpret_cast<const double2*>(tab)[p.tab_off[0] + (int64_t)jq];
-        l = r.x;
-        g = r.y;
-      } else {
-        // unreachable for device draws (the lattice spans every value they can
-        // take; caller-drawn candidates disable the table, TPE_F_NO_TABLE): the
-        // candidate drops out (an f64 mass sum here would triple this
-        // kernel's registers)
-        l = -INFINITY;
-        g = 0.0;
+  // the run's best -> slot 0 of its first tile (block reduction)
+  auto flush = [&]() {
+    for (int off = 32; off > 0; off >>= 1) {
+      const double os = __shfl_xor(bs, off), ol = __shfl_xor(bl, off), og = __shfl_xor(bg, off);
+      const int64_t oi = __shfl_xor(bi, off);
+      if (better(os, oi, bs, bi)) { bs = os; bl = ol; bg = og; bi = oi; }
+    }
+    if (lane == 0) { wb[wave].score = bs; wb[wave].l = bl; wb[wave].g = bg; wb[wave].idx = bi; }
+    __syncthreads();
+    if (wave == 0) {                         // lanes 0..15 hold the waves' bests
+      const int q = lane < kTabThreads / 64 ? lane : 0;
+      double s2 = wb[q].score, l2 = wb[q].l, g2 = wb[q].g;
+      int64_t i2 = lane < kTabThreads / 64 ? wb[q].idx : -1;
+      for (int off = 8; off > 0; off >>= 1) {
+        const double os = __shfl_xor(s2, off), ol = __shfl_xor(l2, off), og = __shfl_xor(g2, off);
+        const int64_t oi = __shfl_xor(i2, off);
+        if (better(os, oi, s2, i2)) { s2 = os; l2 = ol; g2 = og; i2 = oi; }
+      }
+      if (lane == 0) {
+        tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
+        d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
       }
     }
-    emit(i, o, x, l, g);
+    bs = 0.0; bl = 0.0; bg = 0.0; bi = -1;
+  };
+  // this workgroup's tile descriptors, fetched in one round
+  __shared__ int s_tile[kTabMaxTilesPerWg], s_prob[kTabMaxTilesPerWg], s_start[kTabMaxTilesPerWg];
+  const int n_my = min(per_wg, n_list - (int)blockIdx.x * per_wg);
+  if ((int)threadIdx.x < n_my) {
+    const int li = (int)blockIdx.x * per_wg + (int)threadIdx.x;
+    const int tile = list ? list[li] : li;
+    const tpe_tile tl = tiles[tile];
+    s_tile[threadIdx.x] = tile; s_prob[threadIdx.x] = tl.problem; s_start[threadIdx.x] = tl.cand_start;
   }
-  // candidates outside the cells or in flagged ones: re-drawn and summed exactly
-  // (out of line, after the main loop)
-  while (exact) {
-    const int j = __builtin_ctz(exact);
-    exact &= exact - 1;
-    const int i = first + j * kThreads;
-    const int64_t o = p.cand_off + i;
-    double x;
-    float t;
-    fetch(i, o, x, t);
-    float lb2 = cell_log2(p, 0, tab, t), la2 = cell_log2(p, 1, tab, t);
-    if (!(lb2 == lb2)) lb2 = lse2_exact_ool(comp32, p.below_off, p.below_len, 0, 0, t);
-    if (!(la2 == la2))
-      la2 = p.narrow_amin > 0.f ? lse2_pruned(p, comp32, grid, t)
-                                : lse2_exact_ool(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
-    const double lnx = logc ? (double)t : 0.0;
-    emit(i, o, x, (double)lb2 * kLn2 + p.below_base - lnx, (double)la2 * kLn2 + p.above_base - lnx);
+  __syncthreads();
+  for (int gi = 0; gi < n_my; ++gi) {
+    // (uniform: readfirstlane keeps the problem's fields in scalar registers)
+    const int tile = __builtin_amdgcn_readfirstlane(s_tile[gi]), pid = __builtin_amdgcn_readfirstlane(s_prob[gi]);
+    const tpe_problem& p = P[pid];
+    if (p.tab_mode == TPE_TAB_NONE) continue;        // no list: every tile, k_sample's skipped
+    const bool cells = p.tab_mode == TPE_TAB_CELLS;
+    if (pid != cur) {
+      if (cur >= 0) flush();
+      __syncthreads();                               // LDS free for the next problem
+      const double* S = samp + 8 * (int64_t)p.samp_off;
+      in_lds = draw && p.samp_len > 0 && p.samp_len <= kCumLds;
+      if (in_lds) {
+        for (int q = threadIdx.x; q < p.samp_len; q += kTabThreads) {
+          const double* s = S + 8 * q;
+          cum_lds[q] = s[0];
+          const float sg = (float)s[2];
+          row_lds[q] = make_float4((float)s[1], s[5] != 0.0 ? -sg : sg, (float)s[3], (float)s[4]);
+        }
+      }
+      tab_in_lds = PREC == TPE_PREC_F32 && cells && p.tab_n[0] + p.tab_n[1] <= kTabLdsCells;
+      if (tab_in_lds) {                              // plane k of cell j at tab_lds[k * kTabLdsCells + j]
+        const int n0 = 4 * p.tab_n[0], n1 = 4 * p.tab_n[1];
+        for (int q = threadIdx.x; q < n0 + n1; q += kTabThreads) {
+          const float4 v = q < n0 ? tab[(int64_t)p.tab_off[0] + q] : tab[(int64_t)p.tab_off[1] + q - n0];
+          tab_lds[(q & 3) * kTabLdsCells + (q >> 2)] = v;
+        }
+      }
+      __syncthreads();
+      if (in_lds && threadIdx.x < kGuide) {          // first k with cum_k > b / kGuide
+        const double v = (double)threadIdx.x / (double)kGuide;
+        int a = 0, b = p.samp_len - 1;
+        while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
+        guide[threadIdx.x] = a;
+      }
+      __syncthreads();
+      cur = pid;
+      run_tile = tile;
+    }
+    const int cand_start = __builtin_amdgcn_readfirstlane(s_start[gi]);
+    if (threadIdx.x < TPE_BEST_PER_TILE)
+      tile_best[(int64_t)tile * TPE_BEST_PER_TILE + threadIdx.x] = tpe_best{0, 0, 0, -1};
+    float lo_f, hi_f;
+    f32_bounds(p, lo_f, hi_f);
+    const double* S = samp + 8 * (int64_t)p.samp_off;
+    const bool logc = p.family == TPE_FAM_LOGGAUSS;
+    const int first = cand_start + (int)threadIdx.x;
+    uint32_t exact = 0;                              // candidates the cell tables do not cover (rare)
+    float tj[kTabPer];
+    // cells; TL: the tables are in LDS (separate instantiations, so every table
+    // read is a plain LDS or global load, never a generic one)
+    auto cells_pass = [&](auto TL) {
+        const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
+        const int n0 = p.tab_n[0], n1 = p.tab_n[1];
+        constexpr bool kL = decltype(TL)::value;
+        constexpr int stride = kL ? kTabLdsCells : 1, step = kL ? 1 : 4;
+        const float4* __restrict__ r0;
+        const float4* __restrict__ r1;
+        if constexpr (kL) { r0 = tab_lds; r1 = tab_lds + n0; }
+        else { r0 = tab + p.tab_off[0]; r1 = tab + p.tab_off[1]; }
+#pragma unroll
+        for (int j = 0; j < kTabPer; ++j) {
+          const int i = first + j * kTabThreads;
+          tj[j] = NAN;
+          if (i >= p.n_cand) continue;
+          const int64_t o = p.cand_off + i;
+          float t;
+          if (!draw) {
+            t = coord[o];
+          } else if (in_lds) {
+            const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+            const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+            const int a = guided_comp(cum_lds, guide, p.samp_len, u01d(r.x, r.y));
+            const float4 s = row_lds[a];
+            const float pr = s.z + u01f(r.z) * (s.w - s.z);
+            const float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+            float xf = s.x + s.y * z;
+            if (!(xf == xf)) xf = s.x;
+            t = fminf(fmaxf(xf, lo_f), hi_f);
+          } else if (p.samp_len > 0) {
+            t = draw_coord_f32(p, S, S, 8, i, lo_f, hi_f);
+          } else {
+            t = NAN;
+          }
+          tj[j] = t;
+          const float lb2 = cell_log2_lds(lo0, inv0, n0, r0, stride, step, t),
+                    la2 = cell_log2_lds(lo1, inv1, n1, r1, stride, step, t);
+          if (!(lb2 == lb2) || !(la2 == la2)) { exact |= 1u << j; continue; }
+          const double lnx = logc ? (double)t : 0.0;
+          const double x = !need_x ? 0.0 : !draw ? cand[o] : logc ? exp((double)t) : (double)t;
+          emit(i, o, x, (double)lb2 * kLn2 + p.below_base - lnx, (double)la2 * kLn2 + p.above_base - lnx);
+        }
+        // candidates outside the cells or in flagged ones: summed exactly by the
+        // whole wave, one candidate at a time
+#pragma unroll
+        for (int j = 0; j < kTabPer; ++j) {
+          unsigned long long need = __ballot((exact >> j) & 1u);
+          while (need) {
+            const int src = __builtin_ctzll(need);
+            need &= need - 1;
+            const float t = __shfl(tj[j], src);
+            float lb2 = cell_log2_lds(lo0, inv0, n0, r0, stride, step, t),
+                    la2 = cell_log2_lds(lo1, inv1, n1, r1, stride, step, t);
+            if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
+            if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
+            if (lane == src) {
+              const int i = first + j * kTabThreads;
+              const int64_t o = p.cand_off + i;
+              const double lnx = logc ? (double)t : 0.0;
+              const double x = !need_x ? 0.0 : !draw ? cand[o] : logc ? exp((double)t) : (double)t;
+              emit(i, o, x, (double)lb2 * kLn2 + p.below_base - lnx, (double)la2 * kLn2 + p.above_base - lnx);
+            }
+          }
+        }
+    };
+    if constexpr (PREC == TPE_PREC_F32) {
+      if (cells) {
+        if (tab_in_lds) cells_pass(std::true_type{});
+        else cells_pass(std::false_type{});
+      }
+    }
+    if (!cells) {                                    // lattice: exact {l, g} per quantized value
+      for (int j = 0; j < kTabPer; ++j) {
+        const int i = first + j * kTabThreads;
+        if (i >= p.n_cand) break;
+        const int64_t o = p.cand_off + i;
+        double x, l, g;
+        float t;
+        if (!draw) {
+          x = cand[o];
+        } else if (p.samp_len > 0) {
+          int c;
+          if (in_lds) draw_one(p, S, cum_lds, 1, i, PREC, lo_f, hi_f, x, t, c);
+          else draw_one(p, S, S, 8, i, PREC, lo_f, hi_f, x, t, c);
+        } else {
+          x = NAN;
+        }
+        const double mq = rint(x / p.q);
+        const double jq = mq - (double)p.lat_lo;
+        if (mq * p.q == x && jq >= 0.0 && jq < (double)p.tab_n[0]) {
+          const double2 r = reinterpret_cast<const double2*>(tab)[p.tab_off[0] + (int64_t)jq];
+          l = r.x;
+          g = r.y;
+        } else {
+          // unreachable for device draws (the lattice spans every value they can
+          // take; caller-drawn candidates disable the table, TPE_F_NO_TABLE): the
+          // candidate drops out (an f64 mass sum here would triple this
+          // kernel's registers)
+          l = -INFINITY;
+          g = 0.0;
+        }
+        emit(i, o, x, l, g);
+      }
+    }
   }
-  tpe_best* __restrict__ slot = tile_best + (int64_t)tile * TPE_BEST_PER_TILE;
-  block_best(bs, bi, bl, bg, slot + blockIdx.y);
-  if (blockIdx.y == 0 && threadIdx.x >= kTabBlocks && threadIdx.x < TPE_BEST_PER_TILE)
-    slot[threadIdx.x] = tpe_best{0, 0, 0, -1};
+  if (cur >= 0) flush();
 }
 
 // row of `part` a work item writes: its tile's first work item + its split
@@ -1516,7 +1690,7 @@ __device__ __forceinline__ int tab_job_of(const tpe_tab_job* __restrict__ J, int
 
 // one wave: the moment row of cell j of side `side` (0 below, 1 above) of p
 __device__ void cell_row(const tpe_problem& p, int side, int j, const float4* __restrict__ comp,
-                         const int32_t* __restrict__ grid, float* __restrict__ row) {
+                         const int32_t* __restrict__ grid, float* __restrict__ row, bool all_exact) {
   const int lane = threadIdx.x & 63;
   const float inv = p.tab_inv[side];
   const float c = p.tab_lo[side] + ((float)j + 0.5f) / inv;
@@ -1607,7 +1781,7 @@ __device__ void cell_row(const tpe_problem& p, int side, int j, const float4* __
   if (lane == 11) val = mx;
   if (lane == 12) val = c;
   if (lane == 13) val = 1.f / h;
-  if (lane == 14) val = any_bad ? 1.f : 0.f;
+  if (lane == 14) val = any_bad || all_exact ? 1.f : 0.f;
   if (lane < 16) row[lane] = val;
 }
 
@@ -1638,13 +1812,15 @@ __global__ __launch_bounds__(kThreads) void k_tables(const tpe_problem* __restri
                                                      const tpe_tab_job* __restrict__ J, int n_jobs,
                                                      const float4* __restrict__ comp32,
                                                      const double4* __restrict__ comp64,
-                                                     const int32_t* __restrict__ grid, float4* __restrict__ tab) {
+                                                     const int32_t* __restrict__ grid, float4* __restrict__ tab,
+                                                     bool all_exact) {
   const tpe_tab_job jb = J[tab_job_of(J, n_jobs, (int)blockIdx.x)];
   const tpe_problem& p = P[jb.problem];
   const int b = (int)blockIdx.x - jb.block0;
   if (jb.kind == TPE_TAB_CELLS) {
     const int cell = b * 4 + (int)(threadIdx.x >> 6);
-    if (cell < jb.n) cell_row(p, jb.side, cell, comp32, grid, reinterpret_cast<float*>(tab + jb.off + 4 * cell));
+    if (cell < jb.n)
+      cell_row(p, jb.side, cell, comp32, grid, reinterpret_cast<float*>(tab + jb.off + 4 * cell), all_exact);
   } else if (p.family == TPE_FAM_QLOGGAUSS) {
     lattice_row<true>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off));
   } else {
@@ -1977,6 +2153,22 @@ int check_batch(const tpe_batch* b) {
   return TPE_OK;
 }
 
+// compute units of the current device (cached per device; 256 on MI355X)
+int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { (void)hipGetLastError(); return 256; }
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+      (void)hipGetLastError();
+      n = 256;
+    }
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 }  // namespace
 
 extern "C" {
@@ -2058,7 +2250,7 @@ int tpe_tables(const tpe_batch* b, void* stream) {
   if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
   hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
                      b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64, b->grid,
-                     (float4*)b->tab);
+                     (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0);
   return hip_check("tpe_tables");
 }
 
@@ -2091,14 +2283,17 @@ int tpe_sample(const tpe_batch* b, void* stream) {
                        b->samp_tiles);
   if (n_tab > 0) {
     if (!b->tab) return fail(TPE_E_ARG, "tabulated tiles without score tables");
+    // one workgroup per CU-sized group of tiles (each stages its problem once)
+    const int per = std::min(kTabMaxTilesPerWg, std::max(1, (n_tab + cu_count() - 1) / cu_count()));
+    const int wgs = (n_tab + per - 1) / per;
     if (b->precision == TPE_PREC_F64)
-      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F64>, dim3(n_tab, kTabBlocks), dim3(kThreads), 0, (hipStream_t)stream,
-                         b->problems, b->tiles, b->tab_tiles, b->samp, b->cand, b->coord, b->tile_best, b->l_out,
-                         b->g_out, b->sample, b->flags, (const float4*)b->comp32, b->grid, (const float4*)b->tab);
+      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F64>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
+                         b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
+                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab);
     else
-      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F32>, dim3(n_tab, kTabBlocks), dim3(kThreads), 0, (hipStream_t)stream,
-                         b->problems, b->tiles, b->tab_tiles, b->samp, b->cand, b->coord, b->tile_best, b->l_out,
-                         b->g_out, b->sample, b->flags, (const float4*)b->comp32, b->grid, (const float4*)b->tab);
+      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F32>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
+                         b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
+                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab);
   }
   return hip_check("tpe_sample");
 }

@@ -80,8 +80,10 @@ enum {
                                re-drawn by the select stage) */
   TPE_BATCH_NO_FUSE = 4,    /* score every continuous tile in the finalize stage (no fused finalize
                                in the above kernel) */
-  TPE_BATCH_ORDERED_DRAWS = 8  /* sorted problems draw ordered candidates, no sort (else i.i.d.
+  TPE_BATCH_ORDERED_DRAWS = 8, /* sorted problems draw ordered candidates, no sort (else i.i.d.
                                   draws + sort) — see "Ordered draws" below */
+  TPE_BATCH_TAB_EXACT = 16     /* test hook: flag every table cell, so every candidate of a
+                                  TPE_TAB_CELLS problem takes the exact-sum fallback */
 };
 
 /* precision of the continuous (non-quantized) families; quantized families

@@ -540,3 +540,37 @@ def test_tabulated_scoring_matches_oracle(engine, dist, args):
     finally:
         os.environ.pop('TPE_TABLES', None)
     assert abs(ref[0]['score'] - res[0]['score']) <= 4 * tol * max(1.0, abs(res[0]['score'])), dist
+
+
+@pytest.mark.parametrize('dist,args', [('uniform', dict(low=-5.0, high=5.0)),
+                                       ('loguniform', dict(low=-4.0, high=3.0)),
+                                       ('normal', dict(mu=1.0, sigma=3.0))])
+def test_tabulated_exact_fallback_matches_oracle(engine, dist, args, monkeypatch):
+    """The cells' exact fallback (a wave sums the whole mixture for one
+    candidate at a time): TPE_BATCH_TAB_EXACT flags every cell, so every
+    candidate takes it; l, g against the oracle and the winner against the
+    table path's."""
+    from hyperopt_amd import _native as N
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(67)
+    log = dist.startswith('log')
+    lo, hi = (args['low'], args['high']) if 'low' in args else (args['mu'] - 3 * args['sigma'],
+                                                               args['mu'] + 3 * args['sigma'])
+    obs = rs.uniform(lo, hi, 3000)
+    obs = np.exp(obs) if log else obs
+    post = parzen.fit_posterior(dist, args, obs[:30], obs[30:], 1.0)
+    C = 1 << 16
+    base = engine.run([LevelProblem(post, 5, [11])], C, seed=19)
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(N.BATCH_TAB_EXACT))
+    res, cand, l, g = engine.run([LevelProblem(post, 5, [11])], C, seed=19, want_lg=True, return_cand=True)
+    prob, _ = engine.device_tables()
+    assert prob[0]['tab_mode'] == N.TAB_CELLS, dist
+    lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
+    kw = dict(low=post.low, high=post.high, q=None)
+    sub = rs.choice(C, 2000, replace=False)
+    _check_lpdf(l[0][sub], lpdf(cand[0][sub], *post.below, **kw), 1e-5, (dist, 'l'))
+    _check_lpdf(g[0][sub], lpdf(cand[0][sub], *post.above, **kw), 1e-5, (dist, 'g'))
+    k = int(res[0]['idx'])
+    assert res[0]['value'] == cand[0][k] and int(np.argmax(l[0] - g[0])) == k
+    assert abs(base[0]['score'] - res[0]['score']) <= 4e-5 * max(1.0, abs(res[0]['score'])), dist

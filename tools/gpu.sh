@@ -4,7 +4,7 @@
 #
 #   tools/gpu.sh TASK [TASK ...]        tasks run in order; the first failure ends the script
 #
-#   tests      -m gpu parity suite                       (PYTEST_ARGS)
+#   tests      -m gpu parity suite                       (PYTEST_ARGS; PYTEST_K = one -k expression)
 #   smoke      __graft_entry__.smoke()
 #   bench      headline bench.py                         (BENCH_ARGS)
 #   trace      rocprofv3 --kernel-trace --stats of a short headline bench run (BENCH_ARGS)
@@ -44,7 +44,7 @@ for task in "$@"; do
   case $task in
     tests)
       step 900 $O/tests_${TAG}.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-          ${PYTEST_ARGS:-}
+          ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"}
       grep -E "PASSED|FAILED|ERROR|passed|failed" $O/tests_${TAG}.log | tail -60 ;;
     smoke)
       step 300 $O/smoke_${TAG}.log python -c "import __graft_entry__ as g; g.smoke()"

@@ -8,7 +8,7 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ('k_above_f32', 'k_above_f64', 'k_above_q', 'k_sample', 'k_tables', 'k_finalize', 'k_select',
+    for k in ('k_above_f32', 'k_above_f64', 'k_above_q', 'k_sample_tab', 'k_sample', 'k_tables', 'k_finalize', 'k_select',
               'k_fit_build', 'k_fit_gather', 'k_fit_sort_lds'):
         if k in name:
             return k
@@ -30,7 +30,7 @@ def main(root):
     # exact for 16-B stores).  'sort' = every rocPRIM dispatch of one tpe_sort
     # call; the bench makes one sort per suggest, i.e. per k_select dispatch.
     traffic = {}
-    for k in ('k_above_f32', 'k_sample', 'k_tables', 'k_finalize', 'k_select'):
+    for k in ('k_above_f32', 'k_sample', 'k_sample_tab', 'k_tables', 'k_finalize', 'k_select'):
         a = out.get(k, {})
         if 'FETCH_SIZE' in a and 'WRITE_SIZE' in a:
             traffic[k] = dict(kernel=k, fetch_kb=a['FETCH_SIZE'], write_kb=a['WRITE_SIZE'],

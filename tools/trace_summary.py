@@ -11,6 +11,9 @@ def short(name):
             if k in name:
                 return 'rocprim:' + k
         return 'rocprim:' + name[:60]
+    if name.startswith('void '):
+        name = name[5:]
+    name = name.replace('(anonymous namespace)::', '')
     if '::' in name:
         name = name.split('(')[1] if name.startswith('(') else name
     return name.split('(')[0].split('::')[-1][:48]
