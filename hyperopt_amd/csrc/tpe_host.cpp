@@ -229,6 +229,48 @@ int64_t fit_sorted(const double* __restrict__ sv, const int64_t* __restrict__ ra
   return pos;
 }
 
+// positions of the below set's members among a label's observation tids
+// (both ascending; ap_filter_trials' membership test, tpe.py:629-636), in
+// ascending order: binary searches when the below set is small (the usual
+// 25 of thousands), else one merge
+void below_positions(const int64_t* __restrict__ tids, int64_t n, const int64_t* __restrict__ bt, int64_t n_bt,
+                     std::vector<int64_t>& pos) {
+  pos.clear();
+  if (n_bt * 16 < n) {
+    const int64_t* lo = tids;
+    for (int64_t j = 0; j < n_bt; ++j) {
+      lo = std::lower_bound(lo, tids + n, bt[j]);
+      if (lo == tids + n) break;
+      if (*lo == bt[j]) pos.push_back(lo - tids);
+    }
+  } else {
+    int64_t b = 0;
+    for (int64_t t = 0; t < n; ++t) {
+      while (b < n_bt && bt[b] < tids[t]) ++b;
+      if (b < n_bt && bt[b] == tids[t]) pos.push_back(t);
+    }
+  }
+}
+
+// tids strictly ascending (one branch-free pass)
+bool strictly_ascending(const int64_t* __restrict__ tids, int64_t n) {
+  int bad = 0;
+  for (int64_t i = 1; i < n; ++i) bad |= tids[i] <= tids[i - 1];
+  return !bad;
+}
+
+// per-thread staging of tpe_host_pack_level, reused across calls (no
+// first-touch page faults on the large tables of a batched level)
+struct PackScratch {
+  std::vector<float> comp32;
+  std::vector<double> comp64, samp;
+  std::vector<int32_t> grid, fin_tiles, samp_tiles, tab_tiles;
+  std::vector<tpe_problem> prob;
+  std::vector<tpe_tile> tiles;
+  std::vector<tpe_work> work;
+  std::vector<tpe_tab_job> tab_jobs;
+};
+
 // value range of a label's kernel coordinate (x, or ln x for log families)
 // that its candidates fall in: the bounds, else the below mixture +- 8 sigma
 // (f32 draws stay within 5.5 sigma of their component); categories [0, upper)
@@ -265,67 +307,76 @@ int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, 
   return fit_sorted<false>(svp, rkp, n, prior_weight, prior_mu, prior_sigma, lf, w, mu, sigma);
 }
 
+// (AVX2 clones: -ffp-contract=off holds in both, so the results are identical)
+__attribute__((target_clones("avx2", "default")))
 int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* order, int64_t n,
                        const int64_t* below_tids, int64_t n_bt, double prior_weight, double prior_mu,
                        double prior_sigma, int32_t lf, double* out, int64_t* out_k) {
   if (n < 0 || n_bt < 0 || (n && (!x || !tids || !order)) || (n_bt && !below_tids) || !out || !out_k)
     return TPE_E_ARG;
-  for (int64_t i = 1; i < n; ++i)
-    if (tids[i] <= tids[i - 1]) return TPE_E_ARG;
-  // ap_filter_trials (tpe.py:629-636): the below set's members among this
-  // label's observations (both tid lists ascending: one merge), coded per
-  // tid-order position t as its rank within its side: r >= 0 above, ~r below
-  static thread_local std::vector<int64_t> code_tl;
+  if (!strictly_ascending(tids, n)) return TPE_E_ARG;
+  // (thread-local staging, looked up once: a TLS access in a loop costs a call)
+  static thread_local std::vector<int64_t> pos_tl, code_tl, rk_tl[2];
+  static thread_local std::vector<double> sv_tl[2];
+  std::vector<int64_t>& pos = pos_tl;
+  below_positions(tids, n, below_tids, n_bt, pos);
+  // every tid-order position t coded as its rank within its side: r >= 0 above,
+  // ~r below (segment fills between the below positions)
   code_tl.resize((size_t)n);
-  int64_t* code = code_tl.data();
-  int64_t nb = 0;
+  int64_t* __restrict__ code = code_tl.data();
+  const int64_t nb = (int64_t)pos.size(), na = n - nb;
   {
-    int64_t b = 0;
-    for (int64_t t = 0; t < n; ++t) {
-      while (b < n_bt && below_tids[b] < tids[t]) ++b;
-      const bool below = b < n_bt && below_tids[b] == tids[t];
-      code[t] = below ? ~nb : t - nb;
-      nb += below;
+    int64_t t0 = 0;
+    for (int64_t j = 0; j <= nb; ++j) {
+      const int64_t t1 = j < nb ? pos[(size_t)j] : n;
+      for (int64_t t = t0; t < t1; ++t) code[t] = t - j;
+      if (j < nb) code[t1] = ~j;
+      t0 = t1 + 1;
     }
   }
-  const int64_t na = n - nb;
   // each side in value order (the label's sorting permutation filtered) with
   // its tid-order ranks — the order np.argsort gives when no value repeats
-  static thread_local std::vector<double> sv[2];
-  static thread_local std::vector<int64_t> rk[2];
-  sv[0].resize((size_t)nb); rk[0].resize((size_t)nb);
-  sv[1].resize((size_t)na); rk[1].resize((size_t)na);
-  double* svp[2] = {sv[0].data(), sv[1].data()};     // (thread_local storage read once)
-  int64_t* rkp[2] = {rk[0].data(), rk[1].data()};
-  const int64_t lim[2] = {nb, na};
-  int64_t cnt[2] = {0, 0};
+  sv_tl[0].resize((size_t)nb + 1); rk_tl[0].resize((size_t)nb + 1);
+  sv_tl[1].resize((size_t)na + 1); rk_tl[1].resize((size_t)na + 1);
+  double* __restrict__ sb = sv_tl[0].data();
+  double* __restrict__ sa = sv_tl[1].data();
+  int64_t* __restrict__ rb = rk_tl[0].data();
+  int64_t* __restrict__ ra = rk_tl[1].data();
+  int64_t cb = 0, ca = 0;
+  int bad = 0;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t t = order[i];
-    if (t < 0 || t >= n) return TPE_E_ARG;
-    const int64_t c = code[t];
-    const int sd = c >= 0;
-    if (cnt[sd] >= lim[sd]) return TPE_E_ARG;      // not a permutation
-    svp[sd][cnt[sd]] = x[t];
-    rkp[sd][cnt[sd]] = sd ? c : ~c;
-    ++cnt[sd];
+    bad |= (uint64_t)t >= (uint64_t)n;
+    const int64_t tt = bad ? 0 : t;
+    const int64_t c = code[tt];
+    const double v = x[tt];
+    // branch-free: write both sides' next slot (each has one spare), advance one
+    sb[cb] = v; rb[cb] = ~c;
+    sa[ca] = v; ra[ca] = c;
+    const int64_t above = c >= 0;
+    ca += above; cb += 1 - above;
+    bad |= (ca > na) | (cb > nb);
   }
+  if (bad) return TPE_E_ARG;                          // not a permutation
   const int64_t cap = n + 1;
   for (int sd = 0; sd < 2; ++sd) {
-    const double* v = sv[sd].data();
+    const double* __restrict__ v = sd ? sa : sb;
     const int64_t m = sd ? na : nb;
     out_k[sd] = 0;
-    bool fallback = m >= 1 && v[0] != v[0];                              // NaN sorts last in `order`...
-    for (int64_t i = 1; i < m && !fallback; ++i) fallback = !(v[i - 1] < v[i]);   // ...or repeated values
-    if (fallback) continue;       // np.argsort's order decides the weights: the caller refits the side
+    // NaN sorts last in `order`; a repeated value leaves the tie order to np.argsort
+    int fallback = m >= 1 && v[0] != v[0];
+    for (int64_t i = 1; i < m; ++i) fallback |= !(v[i - 1] < v[i]);
+    if (fallback) continue;       // the caller refits the side with numpy's permutation
     double* w = out + (3 * sd) * cap;
-    const int64_t pos = fit_sorted<true>(v, rk[sd].data(), m, prior_weight, prior_mu, prior_sigma, lf, w, w + cap,
-                                         w + 2 * cap);
-    if (pos < 0) return (int)pos;
+    const int64_t p = fit_sorted<true>(v, sd ? ra : rb, m, prior_weight, prior_mu, prior_sigma, lf, w, w + cap,
+                                       w + 2 * cap);
+    if (p < 0) return (int)p;
     out_k[sd] = m + 1;
   }
   return TPE_OK;
 }
 
+__attribute__((target_clones("avx2", "default")))
 int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
                        int32_t lf, double* out) {
   if (upper <= 0 || n < 0 || !out) return TPE_E_ARG;
@@ -361,21 +412,30 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
                        double* out_above) {
   if (n < 0 || n_bt < 0 || (n && (!obs || !tids)) || (n_bt && !below_tids) || !out_below || !out_above)
     return TPE_E_ARG;
-  // ap_filter_trials (tpe.py:629-636): one merge of ascending tids; sides keep tid order
-  static thread_local std::vector<int64_t> side[2];
-  side[0].clear(); side[1].clear();
-  side[0].reserve((size_t)std::min(n, n_bt));
-  side[1].reserve((size_t)n);
-  int64_t b = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    if (i && tids[i] <= tids[i - 1]) return TPE_E_ARG;
-    while (b < n_bt && below_tids[b] < tids[i]) ++b;
-    side[b < n_bt && below_tids[b] == tids[i] ? 0 : 1].push_back(obs[i]);
+  if (!strictly_ascending(tids, n)) return TPE_E_ARG;
+  // ap_filter_trials (tpe.py:629-636): the below members' positions, then both
+  // sides in tid order (the above side as the segments between them)
+  static thread_local std::vector<int64_t> pos_tl, side_tl[2];
+  std::vector<int64_t>& pos = pos_tl;
+  below_positions(tids, n, below_tids, n_bt, pos);
+  const int64_t nb = (int64_t)pos.size();
+  std::vector<int64_t>& below = side_tl[0];
+  std::vector<int64_t>& above = side_tl[1];
+  below.resize((size_t)nb);
+  above.resize((size_t)(n - nb));
+  int64_t* __restrict__ bp = below.data();
+  int64_t* __restrict__ ap = above.data();
+  int64_t t0 = 0, k = 0;
+  for (int64_t j = 0; j <= nb; ++j) {
+    const int64_t t1 = j < nb ? pos[(size_t)j] : n;
+    if (t1 > t0) memcpy(ap + k, obs + t0, (size_t)(t1 - t0) * sizeof(int64_t));
+    k += t1 - t0;
+    if (j < nb) bp[j] = obs[t1];
+    t0 = t1 + 1;
   }
-  const int rc = tpe_host_cat_probs(side[0].data(), (int64_t)side[0].size(), upper, p_prior, prior_weight, lf,
-                                    out_below);
+  const int rc = tpe_host_cat_probs(bp, nb, upper, p_prior, prior_weight, lf, out_below);
   if (rc) return rc;
-  return tpe_host_cat_probs(side[1].data(), (int64_t)side[1].size(), upper, p_prior, prior_weight, lf, out_above);
+  return tpe_host_cat_probs(ap, n - nb, upper, p_prior, prior_weight, lf, out_above);
 }
 
 // the pack's straight-line table loops vectorise: an AVX2 clone is picked at
@@ -390,10 +450,14 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   const int T = 2048;
   // staging tables: per-thread, reused across calls (no first-touch page faults
   // on the large ones — a batched level has ~10^5 problems, tiles and work items)
-  static thread_local std::vector<float> comp32;     // float4 rows
-  static thread_local std::vector<double> comp64;    // double4 rows
-  static thread_local std::vector<double> samp;      // 8 doubles per row
-  static thread_local std::vector<int32_t> grid;
+  // (one thread-local lookup: references to its members stay in registers —
+  // a thread_local named inside a loop costs a TLS call per use in a shared object)
+  static thread_local PackScratch tls_scratch;
+  PackScratch& ps = tls_scratch;
+  auto& comp32 = ps.comp32;     // float4 rows
+  auto& comp64 = ps.comp64;     // double4 rows
+  auto& samp = ps.samp;         // 8 doubles per row
+  auto& grid = ps.grid;
   comp32.clear(); comp64.clear(); samp.clear(); grid.clear();
   std::vector<tpe_problem> lab((size_t)n_labels);
   int64_t P = 0, ktot = 0;
@@ -629,9 +693,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           }
           continue;
         }
-        // pruning (above side, f32): widest components listed apart, grid over mu
+        // pruning (above side, f32, scored per candidate): widest components
+        // listed apart, grid over mu.  A tabulated label's cells sum every
+        // component (k_tables), so it has neither.
         std::vector<int64_t> wide;
-        if (side == 1 && k > kPruneMinK) {
+        if (side == 1 && k > kPruneMinK && tmode[li] == TPE_TAB_NONE) {
           // the kPruneWide smallest a (widest sigma), ascending by (a, index): one
           // pass with a small insertion-sorted buffer (= a stable argsort prefix)
           int64_t best[kPruneWide];
@@ -776,7 +842,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (tab_units >= ((int64_t)1 << 31)) return TPE_E_ARG;
   // ---- problems, tiles, work ----
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
-  static thread_local std::vector<tpe_problem> prob;
+  auto& prob = ps.prob;
   prob.resize((size_t)P);
   int64_t scored = 0;
   const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
@@ -835,18 +901,24 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     const int64_t cap = std::max<int64_t>(1, (q.above_len + 63) / 64);
     return (int32_t)std::max<int64_t>(1, std::min(ns, cap));
   };
-  static thread_local std::vector<tpe_tile> tiles;
+  auto& tiles = ps.tiles;
   tiles.resize((size_t)(P * n_tiles_p));
-  for (int64_t r = 0, t = 0; r < P; ++r)
-    for (int64_t j = 0; j < n_tiles_p; ++j, ++t) {
-      tiles[t].problem = (int32_t)r;
-      tiles[t].cand_start = (int32_t)(j * T);
-      tiles[t].work_first = 0;
-      tiles[t].n_splits = tile_splits(prob[r], j);
+  {
+    tpe_tile* __restrict__ tp = tiles.data();
+    for (int64_t r = 0; r < P; ++r) {
+      tpe_tile* __restrict__ row = tp + r * n_tiles_p;
+      const bool none = prob[r].family == TPE_FAM_CATEGORICAL || prob[r].tab_mode != TPE_TAB_NONE;
+      for (int64_t j = 0; j < n_tiles_p; ++j) {
+        row[j].problem = (int32_t)r;
+        row[j].cand_start = (int32_t)(j * T);
+        row[j].work_first = 0;
+        row[j].n_splits = none ? 0 : tile_splits(prob[r], j);
+      }
     }
+  }
   // work items grouped [continuous | quantized Gauss | quantized log]; a tile's
   // items are consecutive, and an item's index is its row of `part`
-  static thread_local std::vector<tpe_work> work;
+  auto& work = ps.work;
   work.clear();
   {
     int64_t nw = 0;
@@ -880,17 +952,18 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // tiles the finalize stage scores (device-drawn candidates): not categorical
   // (the sample stage scores those), not one-split continuous f32 (the above
   // stage does)
-  static thread_local std::vector<int32_t> fin_tiles;
+  auto& fin_tiles = ps.fin_tiles;
   fin_tiles.clear();
-  for (int64_t t = 0; t < (int64_t)tiles.size(); ++t) {
-    const tpe_problem& q = prob[tiles[t].problem];
-    const bool cat = q.family == TPE_FAM_CATEGORICAL && q.samp_len <= TPE_SAMPLE_LDS_ROWS;
-    const bool fused = !f64 && (q.family == TPE_FAM_GAUSS || q.family == TPE_FAM_LOGGAUSS) && tiles[t].n_splits == 1;
-    if (!cat && !fused && q.tab_mode == TPE_TAB_NONE) fin_tiles.push_back((int32_t)t);
+  for (int64_t r = 0; r < P; ++r) {                  // (per problem: a problem's tiles are consecutive)
+    const tpe_problem& q = prob[r];
+    if ((q.family == TPE_FAM_CATEGORICAL && q.samp_len <= TPE_SAMPLE_LDS_ROWS) || q.tab_mode != TPE_TAB_NONE) continue;
+    const bool cont = !f64 && (q.family == TPE_FAM_GAUSS || q.family == TPE_FAM_LOGGAUSS);
+    for (int64_t t = r * n_tiles_p; t < (r + 1) * n_tiles_p; ++t)
+      if (!(cont && tiles[t].n_splits == 1)) fin_tiles.push_back((int32_t)t);
   }
   // table jobs: per tabulated label, one per cell side (4 cells per block) or
   // one lattice job (one value per block); `problem` = the label's first row
-  static thread_local std::vector<tpe_tab_job> tab_jobs;
+  auto& tab_jobs = ps.tab_jobs;
   tab_jobs.clear();
   int64_t tab_blocks = 0;
   for (int32_t li = 0, r = 0; li < n_labels; r += (int32_t)labels[li].n_ids, ++li) {
@@ -908,23 +981,27 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (tab_blocks >= ((int64_t)1 << 31)) return TPE_E_ARG;
   const int64_t n_tab_jobs = (int64_t)tab_jobs.size();
   // sample-stage tile lists: untabulated tiles (lazy categorical last) and tabulated tiles
-  static thread_local std::vector<int32_t> samp_tiles, tab_tiles;
+  auto& samp_tiles = ps.samp_tiles;
+  auto& tab_tiles = ps.tab_tiles;
   samp_tiles.clear(); tab_tiles.clear();
+  auto append_range = [&](std::vector<int32_t>& v, int64_t r) {
+    const size_t b = v.size();
+    v.resize(b + (size_t)n_tiles_p);
+    int32_t* __restrict__ d = v.data() + b;
+    for (int64_t j = 0; j < n_tiles_p; ++j) d[j] = (int32_t)(r * n_tiles_p + j);
+  };
+  int64_t n_samp_eager = 0;
   for (int pass = 0; pass < 2; ++pass)
-    for (int64_t t = 0; t < (int64_t)tiles.size(); ++t) {
-      const tpe_problem& q = prob[tiles[t].problem];
+    for (int64_t r = 0; r < P; ++r) {
+      const tpe_problem& q = prob[r];
       if (q.tab_mode != TPE_TAB_NONE) {
-        if (pass == 0) tab_tiles.push_back((int32_t)t);
+        if (pass == 0) append_range(tab_tiles, r);
         continue;
       }
       const bool lazy = q.family == TPE_FAM_CATEGORICAL && (q.flags & TPE_F_CAT_LAZY) && q.samp_len <= 64;
-      if (lazy == (pass == 1)) samp_tiles.push_back((int32_t)t);
+      if (lazy == (pass == 1)) append_range(samp_tiles, r);
+      if (pass == 0 && !lazy) n_samp_eager += n_tiles_p;
     }
-  int64_t n_samp_eager = 0;
-  for (int32_t t : samp_tiles) {
-    const tpe_problem& q = prob[tiles[t].problem];
-    n_samp_eager += !(q.family == TPE_FAM_CATEGORICAL && (q.flags & TPE_F_CAT_LAZY) && q.samp_len <= 64);
-  }
   const int64_t n_samp_tiles = (int64_t)samp_tiles.size(), n_tab_tiles = (int64_t)tab_tiles.size();
   if (samp_tiles.empty()) samp_tiles.push_back(0);
   if (tab_tiles.empty()) tab_tiles.push_back(0);

@@ -202,7 +202,7 @@ class Engine(object):
         comp32, comp64, samp, grids = [], [], [], []
         n32 = n64 = ns = ngrid = 0
         rows = []                         # per LevelProblem: (table info)
-        for lp in problems:
+        for lp, pl in zip(problems, plans):
             post = lp.post
             fam = post.family
             klo, khi = _coord_range(post)
@@ -266,7 +266,7 @@ class Engine(object):
                         n64 += len(w)
                     else:
                         meta, wide, cn = None, None, c
-                        if side == 'above':
+                        if side == 'above' and pl['mode'] == N.TAB_NONE:     # tabulated: no pruning
                             cn, wide, meta = parzen.prune_tables(m, a, c)
                         r = _rows32(m, a, cn)
                         info[side + '_off'], info[side + '_len'] = n32, len(w)

@@ -26,7 +26,7 @@ class History(object):
     label the (tid, value) observations in tid order.  ``dev`` holds the
     device copies of the observation columns (devhist.DeviceColumns per
     device); it lives as long as the append-only source it mirrors."""
-    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache', '_orders')
+    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache', '_orders', '_logs')
 
     def __init__(self, tids, losses, obs, dev=None, sorted_obs=True, cache=None):
         self.tids, self.losses, self.obs = tids, losses, obs
@@ -34,9 +34,23 @@ class History(object):
         self.sorted_obs = sorted_obs     # every label's observation tids ascending
         self._cache = cache
         self._orders = None
+        self._logs = None
 
     def smallest(self, m):
         return None if self._cache is None else self._cache.smallest(m)
+
+    def log_values(self, label):
+        """np.log of the label's observation values (the kernel coordinate of
+        the log families) — extended incrementally by the Trials cache, else
+        computed once per History."""
+        if self._cache is not None:
+            return self._cache.log_values(label)
+        if self._logs is None:
+            self._logs = {}
+        v = self._logs.get(label)
+        if v is None:
+            v = self._logs[label] = np.log(np.asarray(self.obs[label][1], dtype=np.float64))
+        return v
 
     def value_order(self, label):
         """A permutation sorting the label's (float) observation values
@@ -91,6 +105,7 @@ class _Cache(object):
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
         self.orders = {}               # label -> value-sorting permutation of its observations
+        self.logs = {}                 # label -> _Grow of np.log of its observation values
         self.top = None                # positions of the smallest losses, sorted by (loss, position)
         self.top_n = 0                 # documents merged into `top`
 
@@ -118,6 +133,23 @@ class _Cache(object):
                 if v:
                     self.obs_tid[k].append(tid)
                     self.obs_val[k].append(v[0])
+
+    def log_values(self, k):
+        """np.log(obs_val[k]), the values appended since the last call logged
+        and appended (elementwise, so equal to one np.log of the column)."""
+        vals = self.obs_val[k].view()
+        n = len(vals)
+        g = self.logs.get(k)
+        if g is None or g.n > n:
+            g = self.logs[k] = _Grow(np.float64)
+        if g.n < n:
+            if g.a.shape[0] < n:
+                a = np.empty(max(n, 2 * g.a.shape[0]), dtype=np.float64)
+                a[:g.n] = g.a[:g.n]
+                g.a = a
+            g.a[g.n:n] = np.log(vals[g.n:n])
+            g.n = n
+        return g.view()
 
     def value_order(self, k):
         """Sorting permutation of obs_val[k], extended by a merge of the

@@ -228,14 +228,16 @@ def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT
     return Posterior(dist, family, low, high, q, below, above)
 
 
-def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.0, lf=DEFAULT_LF):
+def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.0, lf=DEFAULT_LF, coord=None):
     """Continuous (non-quantized) label: the below/above split
     (ap_filter_trials, tpe.py:613-641) and both Parzen fits in one native call
     (tpe_host_fit_split), each side sorted by filtering ``order`` (a sorting
     permutation of all the label's values, History.value_order).  A side whose
     values repeat is refitted here with numpy's argsort permutation (the
     reference's tie order), so the result equals fit_posterior's bit for bit.
-    ``below_tids`` ascending, ``obs_tids`` strictly ascending."""
+    ``below_tids`` ascending, ``obs_tids`` strictly ascending; ``coord``:
+    optionally the values' kernel coordinate already computed (np.log of
+    them for the log families, History.log_values)."""
     family = _FAMILY[dist]
     if family not in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
         raise ValueError('fit_split fits continuous families only, not %r' % dist)
@@ -246,9 +248,12 @@ def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.
         pmu, psig = 0.5 * (a['high'] + a['low']), 1.0 * (a['high'] - a['low'])
     else:
         pmu, psig = a['mu'], a['sigma']
-    x = np.ascontiguousarray(obs_vals, dtype=np.float64)
-    if family == N.FAM_LOGGAUSS:
-        x = np.log(x)                                     # monotone: `order` still sorts x
+    if coord is not None:
+        x = np.ascontiguousarray(coord, dtype=np.float64)
+    else:
+        x = np.ascontiguousarray(obs_vals, dtype=np.float64)
+        if family == N.FAM_LOGGAUSS:
+            x = np.log(x)                                 # monotone: `order` still sorts x
     tids = np.ascontiguousarray(obs_tids, dtype=np.int64)
     order = np.ascontiguousarray(order, dtype=np.int64)
     bt = np.ascontiguousarray(below_tids, dtype=np.int64)

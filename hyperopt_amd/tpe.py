@@ -96,7 +96,9 @@ class _Fits(object):
                   and self.hist.value_order(row.label) is not None):
                 # fp32 device path: split + both fits in one native call
                 post = fit_split(row.dist, row.args, otids, ovals, self._below_sorted(),
-                                 self.hist.value_order(row.label), self.prior_weight, DEFAULT_LF)
+                                 self.hist.value_order(row.label), self.prior_weight, DEFAULT_LF,
+                                 coord=(self.hist.log_values(row.label) if _FAMILY[row.dist] == N.FAM_LOGGAUSS
+                                        else None))
             else:
                 if bidx is None:
                     bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)

@@ -95,6 +95,19 @@ def test_value_order_incremental():
     assert c.value_order('x') is None
 
 
+def test_log_values_incremental():
+    """The cache's np.log column (fit_split's kernel coordinate for the log
+    families), extended as documents arrive, equals one np.log of the column."""
+    from hyperopt_amd import history as H
+    c = H._Cache(['x'], {'x': False})
+    rs = np.random.RandomState(6)
+    col = c.obs_val['x']
+    for step in range(30):
+        for _ in range(rs.randint(0, 90)):
+            col.append(rs.uniform(1e-3, 1e3))
+        np.testing.assert_array_equal(c.log_values('x'), np.log(col.view()))
+
+
 def _engine(precision):
     e = Engine.__new__(Engine)
     e.lib, e.tile, e.precision, e._pinned, e._bufs, e.profile = N.load(), 2048, precision, None, {}, None
