@@ -961,8 +961,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     for (int64_t t = r * n_tiles_p; t < (r + 1) * n_tiles_p; ++t)
       if (!(cont && tiles[t].n_splits == 1)) fin_tiles.push_back((int32_t)t);
   }
-  // table jobs: per tabulated label, one per cell side (4 cells per block) or
-  // one lattice job (one value per block); `problem` = the label's first row
+  // table jobs: per tabulated label, one per cell side or one lattice job
+  // (TPE_TAB_PER_BLOCK rows per block); `problem` = the label's first row
   auto& tab_jobs = ps.tab_jobs;
   tab_jobs.clear();
   int64_t tab_blocks = 0;
@@ -974,7 +974,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       tpe_tab_job j;
       j.problem = r; j.side = sd; j.kind = p.tab_mode; j.n = p.tab_n[sd]; j.off = p.tab_off[sd];
       j.block0 = (int32_t)tab_blocks;
-      tab_blocks += p.tab_mode == TPE_TAB_CELLS ? (j.n + 3) / 4 : j.n;
+      tab_blocks += (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK;
       tab_jobs.push_back(j);
     }
   }

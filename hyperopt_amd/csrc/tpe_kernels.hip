@@ -512,6 +512,7 @@ __device__ __forceinline__ void block_best(double sc, int64_t orig, double l, do
 // (include/tpe_hip.h "Tabulated scoring").  Cell row: 16 floats {M0..M10, m,
 // c, 1/h, flag, 0}.
 constexpr int kTabMoments = 11;        // degree-10 Taylor moments per cell
+constexpr int kTabStageRowsDecl = 6144; // component rows a table workgroup stages in LDS (k_tables)
 constexpr float kTabDrop = 50.f;       // terms below 2^-50 of the cell's largest are dropped
 
 // Draws (when `draw`) and writes the sort keys: (sorted problem << key_bits) |
@@ -1680,6 +1681,11 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
 // ============================================================ score tables
 // (include/tpe_hip.h "Tabulated scoring")
 __device__ __forceinline__ int tab_job_of(const tpe_tab_job* __restrict__ J, int n, int b) {
+  if (n <= 64) {                                    // one load round: the last job starting at or before b
+    const int lane = threadIdx.x & 63;
+    const unsigned long long m = __ballot(lane < n && J[lane < n ? lane : 0].block0 <= b);
+    return m ? 63 - __builtin_clzll(m) : 0;
+  }
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int m = (lo + hi + 1) >> 1;
@@ -1688,143 +1694,337 @@ __device__ __forceinline__ int tab_job_of(const tpe_tab_job* __restrict__ J, int
   return lo;
 }
 
-// one wave: the moment row of cell j of side `side` (0 below, 1 above) of p
-__device__ void cell_row(const tpe_problem& p, int side, int j, const float4* __restrict__ comp,
-                         const int32_t* __restrict__ grid, float* __restrict__ row, bool all_exact) {
+// Taylor moments of one significant term (v >= cut) into M
+__device__ __forceinline__ void add_moments(double (&M)[kTabMoments], float v, float z, float a, float h, float mx,
+                                            bool& bad) {
+  const float ah = a * h;
+  const float B = -2.f * kLn2f * z * ah;
+  const float G = -kLn2f * ah * ah;
+  if (fabsf(B) > kTaylorBMax || fabsf(G) > kTaylorGMax) { bad = true; return; }
+  float e = __builtin_amdgcn_exp2f(v - mx), em1 = 0.f;
+  M[0] += (double)e;
+#pragma unroll
+  for (int k = 1; k < kTabMoments; ++k) {
+    const float en = (B * e + 2.f * G * em1) * (1.f / (float)k);
+    em1 = e;
+    e = en;
+    M[k] += (double)e;
+  }
+}
+
+// one wave: each lane's share of the Taylor moments of a cell centred at c
+// (half-width h) from the component rows r0[0, n0) and r1[0, n1) (LDS or
+// global; CONTIG: r1 == r0 + n0, read as one array, four rows in flight per
+// lane); mx = the cell's largest term (wave-uniform), bad = some lane's
+// significant term lies outside the series' convergence box
+template <bool CONTIG>
+__device__ __forceinline__ void cell_moments(const float4* __restrict__ r0, int n0, const float4* __restrict__ r1,
+                                             int n1, float c, float h, double (&M)[kTabMoments], float& mx_out,
+                                             bool& bad_out) {
   const int lane = threadIdx.x & 63;
-  const float inv = p.tab_inv[side];
-  const float c = p.tab_lo[side] + ((float)j + 0.5f) / inv;
-  const float h = 0.5f / inv;
-  // components: sorted rows [k0, k0 + n0) and the wide rows [k1, k1 + n1)
-  int k0, n0, k1 = 0, n1 = 0;
-  if (side == 0) {
-    k0 = p.below_off; n0 = p.below_len;
-  } else if (p.narrow_amin > 0.f) {
-    // pruned above mixture: m0 (the best term at c among the wide components and
-    // c's grid neighbours) bounds the cell's largest term from below, so a narrow
-    // component with |c - mu| > sqrt(narrow_cmax - m0 + 50) / narrow_amin is
-    // under 2^-50 of it
-    const int32_t* __restrict__ G = grid + p.grid_off;
-    float m0 = -INFINITY;
-    if (lane < p.wide_len) {
-      const float4 q = comp[p.wide_off + lane];
-      const float z = ((c - q.x) - q.y) * q.z;
-      m0 = q.w - z * z;
-    }
-    const int gb = (int)fminf(fmaxf(floorf((c - p.grid_lo) * p.grid_inv), 0.f), (float)p.grid_n);
-    const int kn = G[gb] - 2 + (lane - 16);
-    if (lane >= 16 && lane < 20 && kn >= 0 && kn < p.above_len) {
-      const float4 q = comp[p.above_off + kn];
-      const float z = ((c - q.x) - q.y) * q.z;
-      m0 = fmaxf(m0, q.w - z * z);
-    }
-    for (int off = 32; off > 0; off >>= 1) m0 = fmaxf(m0, __shfl_xor(m0, off));
-    const float R = sqrtf(fmaxf(p.narrow_cmax - m0 + kTabDrop, 0.f)) / p.narrow_amin;
-    k1 = p.wide_off; n1 = p.wide_len;
-    if (!(m0 > -INFINITY) || !(R < INFINITY)) {
-      k0 = p.above_off; n0 = p.above_len;
-    } else {
-      const float gl = (c - R - p.grid_lo) * p.grid_inv, gh = (c + R - p.grid_lo) * p.grid_inv;
-      const int bl = (int)fminf(fmaxf(floorf(gl) - 1.f, 0.f), (float)p.grid_n);
-      const int bh = (int)fminf(fmaxf(floorf(gh) + 2.f, 0.f), (float)p.grid_n);
-      const int kl = G[bl], kh = max(G[bh], G[bl]);
-      k0 = p.above_off + kl; n0 = kh - kl;
-    }
-  } else {
-    k0 = p.above_off; n0 = p.above_len; k1 = p.wide_off; n1 = p.wide_len;
-  }
-  k0 = __builtin_amdgcn_readfirstlane(k0); n0 = __builtin_amdgcn_readfirstlane(n0);
   const int n = n0 + n1;
+  auto at = [&](int i) -> float4 { return CONTIG ? r0[i] : (i < n0 ? r0[i] : r1[i - n0]); };
   // pass 1: the largest term at c
-  float mx = -INFINITY;
-  for (int i = lane; i < n; i += 64) {
-    const float4 q = i < n0 ? comp[k0 + i] : comp[k1 + i - n0];
-    const float z = ((c - q.x) - q.y) * q.z;
-    mx = fmaxf(mx, q.w - z * z);
+  float mx0 = -INFINITY, mx1 = -INFINITY, mx2 = -INFINITY, mx3 = -INFINITY;
+  int i = lane;
+  for (; i + 192 < n; i += 256) {
+    const float4 q0 = at(i), q1 = at(i + 64), q2 = at(i + 128), q3 = at(i + 192);
+    float z;
+    z = ((c - q0.x) - q0.y) * q0.z; mx0 = fmaxf(mx0, q0.w - z * z);
+    z = ((c - q1.x) - q1.y) * q1.z; mx1 = fmaxf(mx1, q1.w - z * z);
+    z = ((c - q2.x) - q2.y) * q2.z; mx2 = fmaxf(mx2, q2.w - z * z);
+    z = ((c - q3.x) - q3.y) * q3.z; mx3 = fmaxf(mx3, q3.w - z * z);
   }
+  for (; i < n; i += 64) {
+    const float4 q = at(i);
+    const float z = ((c - q.x) - q.y) * q.z;
+    mx0 = fmaxf(mx0, q.w - z * z);
+  }
+  float mx = fmaxf(fmaxf(mx0, mx1), fmaxf(mx2, mx3));
   for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   // pass 2: Taylor moments (about c, in u = (t - c) / h) of every term within
   // 2^-50 of it; a significant term outside the series' convergence box flags
   // the cell (its candidates are summed exactly)
-  double M[kTabMoments];
 #pragma unroll
   for (int q = 0; q < kTabMoments; ++q) M[q] = 0.0;
   bool bad = !(mx > -INFINITY);
   const float cut = mx - kTabDrop;
-  for (int i = lane; i < n && !bad; i += 64) {
-    const float4 q = i < n0 ? comp[k0 + i] : comp[k1 + i - n0];
+  i = lane;
+  for (; i + 192 < n && !bad; i += 256) {
+    const float4 q0 = at(i), q1 = at(i + 64), q2 = at(i + 128), q3 = at(i + 192);
+    const float z0 = ((c - q0.x) - q0.y) * q0.z, z1 = ((c - q1.x) - q1.y) * q1.z;
+    const float z2 = ((c - q2.x) - q2.y) * q2.z, z3 = ((c - q3.x) - q3.y) * q3.z;
+    const float v0 = q0.w - z0 * z0, v1 = q1.w - z1 * z1, v2 = q2.w - z2 * z2, v3 = q3.w - z3 * z3;
+    if (v0 >= cut) add_moments(M, v0, z0, q0.z, h, mx, bad);
+    if (v1 >= cut) add_moments(M, v1, z1, q1.z, h, mx, bad);
+    if (v2 >= cut) add_moments(M, v2, z2, q2.z, h, mx, bad);
+    if (v3 >= cut) add_moments(M, v3, z3, q3.z, h, mx, bad);
+  }
+  for (; i < n && !bad; i += 64) {
+    const float4 q = at(i);
     const float z = ((c - q.x) - q.y) * q.z;
     const float v = q.w - z * z;
-    if (!(v >= cut)) continue;
-    const float ah = q.z * h;
-    const float B = -2.f * kLn2f * z * ah;
-    const float G = -kLn2f * ah * ah;
-    if (fabsf(B) > kTaylorBMax || fabsf(G) > kTaylorGMax) { bad = true; break; }
-    float e = __builtin_amdgcn_exp2f(v - mx), em1 = 0.f;
-    M[0] += (double)e;
-#pragma unroll
-    for (int k = 1; k < kTabMoments; ++k) {
-      const float en = (B * e + 2.f * G * em1) * (1.f / (float)k);
-      em1 = e;
-      e = en;
-      M[k] += (double)e;
-    }
+    if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
   }
-  const bool any_bad = __ballot(bad) != 0ull;
-#pragma unroll
-  for (int q = 0; q < kTabMoments; ++q)
-    for (int off = 32; off > 0; off >>= 1) M[q] += __shfl_xor(M[q], off);
-  float val = 0.f;
-#pragma unroll
-  for (int q = 0; q < kTabMoments; ++q)
-    if (lane == q) val = (float)M[q];
-  if (lane == 11) val = mx;
-  if (lane == 12) val = c;
-  if (lane == 13) val = 1.f / h;
-  if (lane == 14) val = any_bad || all_exact ? 1.f : 0.f;
-  if (lane < 16) row[lane] = val;
+  mx_out = mx;
+  bad_out = __ballot(bad) != 0ull;
 }
 
-// one workgroup: {l, g} of lattice value lat_lo + j of a quantized problem, the
+// Chunked passes over LDS-staged rows: rows [64 g, 64 g + 64) form chunk g,
+// summarised by meta[g] = {min mu, max mu, min a, max c}.  No term of chunk g
+// at c exceeds bound_g = max c - (min a * dist(c, [min mu, max mu]))^2, so a
+// pass visits only the chunks whose bound reaches its threshold (a wave-uniform
+// set): pass 1 those that could exceed the best term of the most promising
+// chunk, pass 2 those that could be within 2^-50 of the maximum.  kChunkSlack
+// (log2 units) covers the f32 rounding of the bounds.  Same results as the
+// full scan: the skipped terms are below every threshold.
+constexpr int kChunkMax = (kTabStageRowsDecl + 63) / 64;
+constexpr float kChunkSlack = 1.f;
+
+__device__ __forceinline__ float chunk_bound(const float4 m, float c) {
+  const float d = fmaxf(fmaxf(m.x - c, c - m.y), 0.f);
+  const float ad = m.z * d;
+  return d > 0.f ? m.w - ad * ad : m.w;
+}
+
+// one wave: {min mu, max mu, min a, max c} of chunks lane, lane + 64, ... (each
+// lane walks its chunk's rows in a rotated order: conflict-free LDS banks)
+__device__ __forceinline__ void chunk_meta(const float4* __restrict__ rows, int n, float4* __restrict__ meta,
+                                           int first_chunk, int step) {
+  const int lane = threadIdx.x & 63;
+  const int nch = (n + 63) / 64;
+  for (int g = first_chunk * 64 + lane; g < nch; g += step * 64) {
+    float lo = INFINITY, hi = -INFINITY, amin = INFINITY, cmax = -INFINITY;
+    const int last = min(n, g * 64 + 64) - 1;          // rows past n read the last row again
+    for (int i0 = 0; i0 < 64; i0 += 8) {
+      float4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = rows[min(g * 64 + ((i0 + u + lane) & 63), last)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float mu = q[u].x + q[u].y;
+        lo = fminf(lo, mu); hi = fmaxf(hi, mu); amin = fminf(amin, q[u].z); cmax = fmaxf(cmax, q[u].w);
+      }
+    }
+    meta[g] = make_float4(lo, hi, amin, cmax);
+  }
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+
+__device__ __forceinline__ void cell_moments_chunked(const float4* __restrict__ rows, int n,
+                                                     const float4* __restrict__ meta, float c, float h,
+                                                     double (&M)[kTabMoments], float& mx_out, bool& bad_out) {
+  const int lane = threadIdx.x & 63;
+  const int nch = (n + 63) / 64;
+  // bounds of chunks lane and lane + 64 (kChunkMax <= 128)
+  const float b0 = lane < nch ? chunk_bound(meta[lane], c) : -INFINITY;
+  const float b1 = lane + 64 < nch ? chunk_bound(meta[lane + 64], c) : -INFINITY;
+  auto term = [&](int r) -> float {
+    const float4 q = rows[r];
+    const float z = ((c - q.x) - q.y) * q.z;
+    return q.w - z * z;
+  };
+  // the most promising chunk first: its best term bounds the maximum from below
+  const float bmax = wave_max(fmaxf(b0, b1));
+  const unsigned long long h0 = __ballot(b0 == bmax), h1 = __ballot(b1 == bmax);
+  const int gbest = h0 ? __builtin_ctzll(h0) : 64 + __builtin_ctzll(h1);
+  float m = -INFINITY;
+  {
+    const int r = gbest * 64 + lane;
+    if (r < n) m = term(r);
+  }
+  const float m0 = wave_max(m);
+  // pass 1: chunks that could hold a larger term
+  for (int half = 0; half < 2; ++half) {
+    unsigned long long set = __ballot((half ? b1 : b0) > m0 - kChunkSlack);
+    while (set) {
+      const int g = half * 64 + __builtin_ctzll(set);
+      set &= set - 1;
+      if (g == gbest) continue;
+      const int r = g * 64 + lane;
+      if (r < n) m = fmaxf(m, term(r));
+    }
+  }
+  const float mx = wave_max(m);
+  // pass 2: chunks that could hold a term within 2^-50 of the maximum
+  bool bad = !(mx > -INFINITY);
+  const float cut = mx - kTabDrop;
+  for (int half = 0; half < 2 && !__ballot(bad); ++half) {
+    unsigned long long set = __ballot((half ? b1 : b0) >= cut - kChunkSlack);
+    while (set) {
+      const int g = half * 64 + __builtin_ctzll(set);
+      set &= set - 1;
+      const int r = g * 64 + lane;
+      if (r >= n || bad) continue;
+      const float4 q = rows[r];
+      const float z = ((c - q.x) - q.y) * q.z;
+      const float v = q.w - z * z;
+      if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
+    }
+  }
+  mx_out = mx;
+  bad_out = __ballot(bad) != 0ull;
+}
+
+// the above rows of a PRUNED mixture (device-fitted) that can matter at c: m0
+// (the best term at c among the wide components and c's grid neighbours)
+// bounds the cell's largest term from below, so a narrow component with
+// |c - mu| > sqrt(narrow_cmax - m0 + 50) / narrow_amin is under 2^-50 of it
+__device__ __forceinline__ void pruned_range(const tpe_problem& p, const float4* __restrict__ comp,
+                                             const int32_t* __restrict__ grid, float c, int& k0, int& n0) {
+  const int lane = threadIdx.x & 63;
+  const int32_t* __restrict__ G = grid + p.grid_off;
+  float m0 = -INFINITY;
+  if (lane < p.wide_len) {
+    const float4 q = comp[p.wide_off + lane];
+    const float z = ((c - q.x) - q.y) * q.z;
+    m0 = q.w - z * z;
+  }
+  const int gb = (int)fminf(fmaxf(floorf((c - p.grid_lo) * p.grid_inv), 0.f), (float)p.grid_n);
+  const int kn = G[gb] - 2 + (lane - 16);
+  if (lane >= 16 && lane < 20 && kn >= 0 && kn < p.above_len) {
+    const float4 q = comp[p.above_off + kn];
+    const float z = ((c - q.x) - q.y) * q.z;
+    m0 = fmaxf(m0, q.w - z * z);
+  }
+  for (int off = 32; off > 0; off >>= 1) m0 = fmaxf(m0, __shfl_xor(m0, off));
+  const float R = sqrtf(fmaxf(p.narrow_cmax - m0 + kTabDrop, 0.f)) / p.narrow_amin;
+  if (!(m0 > -INFINITY) || !(R < INFINITY)) {
+    k0 = p.above_off; n0 = p.above_len;
+  } else {
+    const float gl = (c - R - p.grid_lo) * p.grid_inv, gh = (c + R - p.grid_lo) * p.grid_inv;
+    const int bl = (int)fminf(fmaxf(floorf(gl) - 1.f, 0.f), (float)p.grid_n);
+    const int bh = (int)fminf(fmaxf(floorf(gh) + 2.f, 0.f), (float)p.grid_n);
+    const int kl = G[bl], kh = max(G[bh], G[bl]);
+    k0 = p.above_off + kl; n0 = kh - kl;
+  }
+  k0 = __builtin_amdgcn_readfirstlane(k0); n0 = __builtin_amdgcn_readfirstlane(n0);
+}
+
+// one wave: {l, g} of lattice value lat_lo + j of a quantized problem, the
 // reference's per-component mass terms (tpe.py:147-159 / :285-298) summed in a
-// fixed order
+// fixed order (lane-strided, then a butterfly)
 template <bool LOG>
 __device__ void lattice_row(const tpe_problem& p, int j, const double4* __restrict__ comp64,
                             double2* __restrict__ rows) {
+  const int lane = threadIdx.x & 63;
   const double x = (double)(p.lat_lo + (int64_t)j) * p.q;
   double tu, tl;
   q_bounds(p, x, tu, tl);
   double sb = 0.0, sa = 0.0;
-  for (int k = threadIdx.x; k < p.below_len; k += kThreads) sb += qterm<LOG>(comp64[p.below_off + k], tu, tl);
-  for (int k = threadIdx.x; k < p.above_len; k += kThreads) sa += qterm<LOG>(comp64[p.above_off + k], tu, tl);
+  for (int k = lane; k < p.below_len; k += 64) sb += qterm<LOG>(comp64[p.below_off + k], tu, tl);
+  for (int k = lane; k < p.above_len; k += 64) sa += qterm<LOG>(comp64[p.above_off + k], tu, tl);
   for (int off = 32; off > 0; off >>= 1) { sb += __shfl_xor(sb, off); sa += __shfl_xor(sa, off); }
-  __shared__ double red[2][kThreads / 64];
-  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sb; red[1][threadIdx.x >> 6] = sa; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double b = red[0][0], a = red[1][0];
-    for (int w = 1; w < kThreads / 64; ++w) { b += red[0][w]; a += red[1][w]; }
-    rows[j] = make_double2(log(b) + p.below_base, log(a) + p.above_base);
-  }
+  if (lane == 0) rows[j] = make_double2(log(sb) + p.below_base, log(sa) + p.above_base);
 }
 
-__global__ __launch_bounds__(kThreads) void k_tables(const tpe_problem* __restrict__ P,
-                                                     const tpe_tab_job* __restrict__ J, int n_jobs,
-                                                     const float4* __restrict__ comp32,
-                                                     const double4* __restrict__ comp64,
-                                                     const int32_t* __restrict__ grid, float4* __restrict__ tab,
-                                                     bool all_exact) {
+// 1024-thread workgroups, one wave per cell row / lattice value
+// (TPE_TAB_PER_BLOCK per workgroup).  A cell job's workgroup first stages its
+// side's component rows in LDS (unless pruned or too many), so both passes of
+// every cell read LDS only.
+constexpr int kTabTblThreads = 64 * TPE_TAB_PER_BLOCK;
+constexpr int kTabStageRows = kTabStageRowsDecl;    // 96 KiB of float4 rows
+static_assert(TPE_TAB_PER_BLOCK * kTabMoments * 64 * 8 <= kTabStageRows * 16, "moment reduction fits the staging LDS");
+__global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __restrict__ P,
+                                                          const tpe_tab_job* __restrict__ J, int n_jobs,
+                                                          const float4* __restrict__ comp32,
+                                                          const double4* __restrict__ comp64,
+                                                          const int32_t* __restrict__ grid,
+                                                          float4* __restrict__ tab, bool all_exact) {
+  __shared__ float4 rows_lds[kTabStageRows];
+#ifdef TPE_TABLES_TRACE                     // debug builds only: per-phase wave timing
+  uint64_t tt[6];
+  tt[0] = wall_clock64();
+#define TT(k) tt[k] = wall_clock64()
+#else
+#define TT(k) (void)0
+#endif
   const tpe_tab_job jb = J[tab_job_of(J, n_jobs, (int)blockIdx.x)];
   const tpe_problem& p = P[jb.problem];
   const int b = (int)blockIdx.x - jb.block0;
+  const int j = b * TPE_TAB_PER_BLOCK + (int)(threadIdx.x >> 6);
   if (jb.kind == TPE_TAB_CELLS) {
-    const int cell = b * 4 + (int)(threadIdx.x >> 6);
-    if (cell < jb.n)
-      cell_row(p, jb.side, cell, comp32, grid, reinterpret_cast<float*>(tab + jb.off + 4 * cell), all_exact);
-  } else if (p.family == TPE_FAM_QLOGGAUSS) {
-    lattice_row<true>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off));
-  } else {
-    lattice_row<false>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off));
+    const int side = jb.side;
+    const bool pruned = side == 1 && p.narrow_amin > 0.f;
+    const int k0 = side ? p.above_off : p.below_off, n0 = side ? p.above_len : p.below_len;
+    const int k1 = side ? p.wide_off : 0, n1 = side ? p.wide_len : 0;
+    const bool stage = !pruned && n0 + n1 <= kTabStageRows;      // workgroup-uniform
+    __shared__ float4 meta_lds[kChunkMax];
+    TT(1);
+    if (stage) {
+      for (int q = threadIdx.x; q < n0 + n1; q += kTabTblThreads)
+        rows_lds[q] = q < n0 ? comp32[k0 + q] : comp32[k1 + q - n0];
+      __syncthreads();
+      TT(2);
+      if (threadIdx.x < 128) chunk_meta(rows_lds, n0 + n1, meta_lds, (int)(threadIdx.x >> 6), 2);
+      __syncthreads();
+    }
+    TT(3);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool live = j < jb.n;                                   // wave-uniform
+    const float inv = p.tab_inv[side];
+    const float c = p.tab_lo[side] + ((float)j + 0.5f) / inv;
+    const float h = 0.5f / inv;
+    double M[kTabMoments];
+#pragma unroll
+    for (int q = 0; q < kTabMoments; ++q) M[q] = 0.0;
+    float mx = -INFINITY;
+    bool bad = false;
+    if (live) {
+      if (stage) {
+        cell_moments_chunked(rows_lds, n0 + n1, meta_lds, c, h, M, mx, bad);
+      } else if (!pruned) {
+        cell_moments<false>(comp32 + k0, n0, comp32 + k1, n1, c, h, M, mx, bad);
+      } else {
+        int kk, nn;
+        pruned_range(p, comp32, grid, c, kk, nn);
+        cell_moments<false>(comp32 + kk, nn, comp32 + k1, n1, c, h, M, mx, bad);
+      }
+    }
+    TT(4);
+    // every wave is past its passes: the staged rows' LDS takes each wave's
+    // per-lane moments, and 4 lanes per moment sum them (16 lanes each, then
+    // two shuffles) — no 64-lane butterflies of 11 doubles
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(rows_lds) + wave * (kTabMoments * 64);
+    if (!live) return;
+#pragma unroll
+    for (int q = 0; q < kTabMoments; ++q) red[q * 64 + lane] = M[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int q = lane >> 2, part = lane & 3;
+    double sum = 0.0;
+    if (q < kTabMoments)
+      for (int i = 0; i < 16; ++i) sum += red[q * 64 + part * 16 + i];
+    sum += __shfl_xor(sum, 1);
+    sum += __shfl_xor(sum, 2);
+    float val = 0.f;
+    if (part == 0 && q < kTabMoments) val = (float)sum;
+    // row lanes: moment q from lane 4q, then {mx, c, 1/h, flag, 0}
+    float* row = reinterpret_cast<float*>(tab + jb.off + 4 * j);
+    const float mv = __shfl(val, 4 * (lane < kTabMoments ? lane : 0));
+    float out = lane < kTabMoments ? mv : 0.f;
+    if (lane == 11) out = mx;
+    if (lane == 12) out = c;
+    if (lane == 13) out = 1.f / h;
+    if (lane == 14) out = bad || all_exact ? 1.f : 0.f;
+    if (lane < 16) row[lane] = out;
+#ifdef TPE_TABLES_TRACE
+    TT(5);
+    if (lane == 0 && (blockIdx.x % 16) == 0 && wave < 2)
+      printf("k_tables blk %d wave %d side %d rows %d: lookup %llu stage %llu meta %llu passes %llu reduce %llu\n",
+             (int)blockIdx.x, wave, side, n0 + n1, (unsigned long long)(tt[1] - tt[0]),
+             (unsigned long long)(stage ? tt[2] - tt[1] : 0), (unsigned long long)(stage ? tt[3] - tt[2] : 0),
+             (unsigned long long)(tt[4] - tt[3]), (unsigned long long)(tt[5] - tt[4]));
+#endif
+  } else if (j < jb.n) {
+    if (p.family == TPE_FAM_QLOGGAUSS) lattice_row<true>(p, j, comp64, reinterpret_cast<double2*>(tab + jb.off));
+    else lattice_row<false>(p, j, comp64, reinterpret_cast<double2*>(tab + jb.off));
   }
 }
 
@@ -1836,7 +2036,6 @@ constexpr int kFitGatherBlock = 256;
 constexpr int kFitMaxBelow = 64;
 constexpr int kPruneWide = 16;
 constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e))
-constexpr double kLog2e = 1.4426950408889634074;
 
 // gather: above observations (kernel coordinate) and their rank in tid order
 __global__ __launch_bounds__(kFitGatherBlock) void k_fit_gather(const tpe_fit_job* __restrict__ J,
@@ -2153,6 +2352,31 @@ int check_batch(const tpe_batch* b) {
   return TPE_OK;
 }
 
+constexpr int64_t kOneCopyMaxGap = 256 << 10;    // bytes a single upload may carry over
+
+// TPE_RESULT_COPY=1: read the results back with a copy (else the select stage
+// writes them into the pinned buffer directly)
+bool direct_results() {
+  const char* v = getenv("TPE_RESULT_COPY");
+  return !(v && v[0] == '1');
+}
+
+// device address of a pinned host buffer (the last one asked about is
+// cached), or nullptr when it is not device-addressable pinned memory
+char* device_alias(void* host) {
+  static void* last_h = nullptr;
+  static char* last_d = nullptr;
+  if (host == last_h) return last_d;
+  hipPointerAttribute_t a;
+  char* d = nullptr;
+  if (hipPointerGetAttributes(&a, host) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer)
+    d = (char*)a.devicePointer;
+  (void)hipGetLastError();
+  last_h = host;
+  last_d = d;
+  return d;
+}
+
 // compute units of the current device (cached per device; 256 on MI355X)
 int cu_count() {
   static int cache[64] = {0};
@@ -2248,9 +2472,11 @@ int tpe_tables(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
-                     b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64, b->grid,
-                     (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0);
+  const char* twice = getenv("TPE_DEBUG_TABLES_TWICE");      // (timing experiments: a warm second launch)
+  for (int r = 0; r < (twice && twice[0] == '1' ? 2 : 1); ++r)
+    hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks), dim3(kTabTblThreads), 0, (hipStream_t)stream, b->problems,
+                       b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64, b->grid,
+                       (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0);
   return hip_check("tpe_tables");
 }
 
@@ -2426,10 +2652,20 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   hipStream_t s = (hipStream_t)stream;
   unsigned char* host = (unsigned char*)ws->pinned;
   unsigned char* dev = (unsigned char*)ws->blob;
-  // host-written ranges only: device-fitted rows are produced by tpe_fit_above
-  hipError_t e = hipMemcpyAsync(dev, host, (size_t)info.copy_end, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && info.copy2_len > 0)
-    e = hipMemcpyAsync(dev + info.off_comp32, host + info.off_comp32, (size_t)info.copy2_len, hipMemcpyHostToDevice, s);
+  // host-written ranges: [0, copy_end) and the host comp32 rows.  One copy
+  // spanning both when the reserve between them (the device-fitted grid) is
+  // small: what it carries there is overwritten by the fit stage, which runs
+  // after the copy in stream order
+  hipError_t e;
+  const int64_t gap = info.off_comp32 - info.copy_end;
+  if (info.copy2_len > 0 && gap <= kOneCopyMaxGap) {
+    e = hipMemcpyAsync(dev, host, (size_t)(info.off_comp32 + info.copy2_len), hipMemcpyHostToDevice, s);
+  } else {
+    e = hipMemcpyAsync(dev, host, (size_t)info.copy_end, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && info.copy2_len > 0)
+      e = hipMemcpyAsync(dev + info.off_comp32, host + info.off_comp32, (size_t)info.copy2_len,
+                         hipMemcpyHostToDevice, s);
+  }
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
   tpe_batch b;
   memset(&b, 0, sizeof(b));
@@ -2477,7 +2713,12 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.tab = ws->tab;
     b.tab_units = info.tab_units;
   }
-  b.result = ws->result;
+  // the select stage writes the results straight into the pinned staging
+  // buffer when the device can address it (no readback copy)
+  tpe_result* rh = (tpe_result*)(host + res_off);
+  char* dbase = direct_results() ? device_alias(ws->pinned) : nullptr;
+  tpe_result* rd = dbase ? (tpe_result*)(dbase + res_off) : nullptr;
+  b.result = rd ? rd : ws->result;
   if (info.n_fit > 0) {
     b.fit = (const tpe_fit_job*)(dev + info.off_fit);
     b.n_fit = info.n_fit;
@@ -2490,8 +2731,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.fit_max_seg = info.fit_max_seg;
   }
   if ((rc = tpe_run_batch(&b, stream))) return rc;
-  tpe_result* rh = (tpe_result*)(host + res_off);
-  e = hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
+  e = rd ? hipSuccess : hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));

@@ -302,7 +302,7 @@ class Engine(object):
             if pl['mode'] != N.TAB_NONE and len(lp.ids):
                 for sd in range(2 if pl['mode'] == N.TAB_CELLS else 1):
                     jobs.append((r0, sd, pl['mode'], info['tab_n'][sd], info['tab_off'][sd], blocks))
-                    blocks += (info['tab_n'][sd] + 3) // 4 if pl['mode'] == N.TAB_CELLS else info['tab_n'][sd]
+                    blocks += -(-info['tab_n'][sd] // N.TAB_PER_BLOCK)
             r0 += len(lp.ids)
         tab_jobs = np.array(jobs, dtype=np.int64).reshape(-1, 6)
         tj = np.zeros(len(tab_jobs), dtype=N.TAB_JOB_DTYPE)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 8
+#define TPE_ABI_VERSION 9
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -42,6 +42,9 @@ extern "C" {
 /* categorical problems with at most this many categories are scored by the
  * sample stage itself (device-drawn candidates) */
 #define TPE_SAMPLE_LDS_ROWS 1024
+/* cell rows / lattice values a table workgroup computes (tpe_batch.tab_blocks
+ * = sum over jobs of ceil(n / TPE_TAB_PER_BLOCK)) */
+#define TPE_TAB_PER_BLOCK 16
 
 /* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
 enum {

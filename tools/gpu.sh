@@ -12,6 +12,8 @@
 #   stage      steady-state per-stage device times        (REP)
 #   configs    bench.py --config 1, 2, 4, 5
 #   hostsplit  host-side time split of the headline suggest
+#   pmcloop    PMC counter passes on tools/suggest_loop.py (the real suggest flow)
+#   apitrace   HIP API + kernel + copy trace of tools/suggest_loop.py -> timeline of the last suggests
 #   counters   rocprofv3 -L (the counters this box offers) -> gpurun_out/counters.txt
 #   libab      stage times + headline p50 per library variant in LIBS
 #              (hyperopt_amd/libtpe_hip_<name>.so; "default" = libtpe_hip.so)
@@ -85,6 +87,25 @@ for task in "$@"; do
         step 300 $O/bench_${TAG}_$v.err env TPE_HIP_LIB=$lib python bench.py --no-cpu-baseline --steps 100
         echo "$v: $(grep -o '"p50_suggest_ms": [0-9.]*\|"stage_ms": {[^}]*}' $O/bench_${TAG}_$v.err | tr '\n' ' ')"
       done ;;
+    pmcloop)
+      # counters of the suggest flow itself (cold kernels between host phases)
+      mkdir -p $O/pmcloop_${TAG}
+      for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
+                 "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU" \
+                 "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        nm=$(echo $grp | cut -d' ' -f1)
+        rm -rf $O/pmcloop_${TAG}/$nm
+        step 300 $O/pmcloop_${TAG}/$nm.log rocprofv3 --pmc $grp --kernel-trace --output-format csv \
+            -d $O/pmcloop_${TAG}/$nm -o run -- python3 tools/suggest_loop.py 30
+      done
+      python3 tools/pmc_summary.py $O/pmcloop_${TAG} > $O/pmcloop_${TAG}/summary.json
+      python3 -c "import json; d=json.load(open('$O/pmcloop_${TAG}/summary.json')); [print(k, json.dumps(v)) for k, v in d.items() if k.startswith('k_')]" ;;
+    apitrace)
+      rm -rf $O/api_${TAG}
+      step 300 $O/api_${TAG}.log rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv \
+          -d $O/api_${TAG} -o run -- python3 tools/suggest_loop.py 30
+      python3 tools/api_timeline.py $O/api_${TAG} 2 > $O/api_${TAG}_timeline.txt
+      cat $O/api_${TAG}_timeline.txt | head -120 ;;
     counters)
       step 120 $O/counters.txt rocprofv3 -L
       grep -o "SQ_[A-Z0-9_]*\|TCC_[A-Z0-9_]*\|TCP_[A-Z0-9_]*" $O/counters.txt | sort -u | tr '\n' ' ' | head -c 6000; echo ;;
