@@ -381,6 +381,34 @@ def main():
         elapsed = float(t.item())
     value = n_active * C_total / elapsed
 
+    # strong scaling: the BASELINE 2^20 candidates in total, split over the ranks
+    strong = None
+    if world > 1:
+        C_strong = args.cands
+
+        def step_strong(i):
+            return tpe.suggest([new_id], domain, trials, SEED + i, n_EI_candidates=C_strong, shard=shard)
+
+        for i in range(args.warmup):
+            step_strong(7000 + i)
+        barrier()
+        lat_s, act_s = [], 0
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            s0 = time.perf_counter()
+            d = step_strong(8000 + i)
+            lat_s.append(time.perf_counter() - s0)
+            act_s += sum(1 for v in d[0]['misc']['vals'].values() if v)
+        barrier()
+        el_s = time.perf_counter() - t0
+        t = torch.tensor([el_s], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_s = float(t.item())
+        strong = dict(n_EI_candidates_total=C_strong, per_rank=C_strong // world, value=act_s * C_strong / el_s,
+                      unit='candidate-scores/s', ms_per_step=1e3 * el_s / args.steps,
+                      p50_suggest_ms=1e3 * float(np.median(lat_s)),
+                      p99_suggest_ms=1e3 * float(np.percentile(lat_s, 99)))
+
     # dominant-kernel roofline, measured live with HIP events on the engine stream
     eng = engine_mod._ENGINES[str(device)]
     eng.profile = {}
@@ -407,6 +435,11 @@ def main():
             'p50_suggest_ms': 1e3 * float(np.median(lat)), 'p99_suggest_ms': 1e3 * float(np.percentile(lat, 99)),
             'active_hyperparameters_per_suggest': n_active / args.steps,
             'stage_ms': stages, 'roofline': roof, 'kernels': kernels, 'cpu_baseline': cpu,
+            # the same 2^20 candidates in total over N ranks (N = 1: the line itself)
+            'strong_scaling': strong if strong is not None else dict(
+                n_EI_candidates_total=C_total, per_rank=C_total, value=value, unit='candidate-scores/s',
+                ms_per_step=1e3 * elapsed / args.steps, p50_suggest_ms=1e3 * float(np.median(lat)),
+                p99_suggest_ms=1e3 * float(np.percentile(lat, 99))),
         }
         if cpu:
             out['speedup_vs_cpu_baseline'] = value / cpu['value']

@@ -176,7 +176,15 @@ E_SPACE = -4
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
            'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above', 'tpe_tables',
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
-           'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run')
+           'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
+           'tpe_replay_mixture', 'tpe_replay_categorical')
+
+
+class MTState(ctypes.Structure):
+    """tpe_mt_state: numpy's legacy RandomState (MT19937 key, position and the
+    cached polar-method gauss)."""
+    _fields_ = [('key', ctypes.c_uint32 * 624), ('pos', ctypes.c_int32), ('has_gauss', ctypes.c_int32),
+                ('gauss', ctypes.c_double)]
 
 
 class NativeUnavailable(RuntimeError):
@@ -222,6 +230,11 @@ def load(path=LIB_PATH):
     lib.tpe_host_cat_split.argtypes = [P, P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int32, P, D, ctypes.c_int32,
                                        P, P]
     lib.tpe_host_cat_split.restype = ctypes.c_int
+    I64 = ctypes.c_int64
+    lib.tpe_replay_mixture.argtypes = [P, P, P, P, I64, ctypes.c_int32, D, D, I64, P]
+    lib.tpe_replay_mixture.restype = ctypes.c_int
+    lib.tpe_replay_categorical.argtypes = [P, P, I64, I64, P]
+    lib.tpe_replay_categorical.restype = ctypes.c_int
     lib.tpe_host_pack_level.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64,
                                         ctypes.POINTER(PackInfo)]

@@ -1061,3 +1061,174 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- replay draws
+// numpy legacy RandomState stream (include/tpe_hip.h "Exact-replay candidate
+// draws"); compiled with -ffp-contract=off: loc + scale * g and the polar
+// method's arithmetic round exactly as numpy's C does
+namespace {
+
+constexpr int kMtN = 624, kMtM = 397;
+
+void mt_regen(tpe_mt_state* s) {
+  uint32_t* k = s->key;
+  auto mix = [](uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  };
+  int i = 0;
+  for (; i < kMtN - kMtM; ++i) k[i] = mix(k[i], k[i + 1], k[i + kMtM]);
+  for (; i < kMtN - 1; ++i) k[i] = mix(k[i], k[i + 1], k[i + kMtM - kMtN]);
+  k[kMtN - 1] = mix(k[kMtN - 1], k[0], k[kMtM - 1]);
+  s->pos = 0;
+}
+
+inline uint32_t mt_next32(tpe_mt_state* s) {
+  if (s->pos >= kMtN) mt_regen(s);
+  uint32_t y = s->key[s->pos++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+// random_sample: 53-bit double from two words
+inline double mt_double(tpe_mt_state* s) {
+  const int32_t a = (int32_t)(mt_next32(s) >> 5), b = (int32_t)(mt_next32(s) >> 6);
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+// legacy polar-method gauss with the cached second value
+double mt_gauss(tpe_mt_state* s) {
+  if (s->has_gauss) {
+    const double t = s->gauss;
+    s->has_gauss = 0;
+    s->gauss = 0.0;
+    return t;
+  }
+  double x1, x2, r2;
+  do {
+    x1 = 2.0 * mt_double(s) - 1.0;
+    x2 = 2.0 * mt_double(s) - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+  } while (r2 >= 1.0 || r2 == 0.0);
+  const double f = sqrt(-2.0 * log(r2) / r2);
+  s->gauss = f * x1;
+  s->has_gauss = 1;
+  return f * x2;
+}
+
+// multinomial(1, p) as numpy draws it: for j = 0 .. k-2 a binomial(1, p_j /
+// remaining) (remaining -= p_j after each), stopping at the first success.
+// numpy's binomial(1, p') is an inversion (p' <= 1/2; else 1 - inversion(1 -
+// p')) with bound = min(1, np + 10 sqrt(np q + 1)) = 1: X = 0 when U <= qn, X
+// = 1 when qn < U and U - qn <= px1, else a fresh U; qn = exp(1 log q) and px1
+// = (1 p qn) / (1 q).  Those depend on p alone, so a Multinom1 computes them
+// once per mixture and a draw only compares uniforms — the same values and
+// the same uniform consumption as numpy's per-call arithmetic.
+struct Multinom1 {
+  struct Step { double qn, px1; int kind; };   // kind 0: never (p' == 0), 1: inversion, 2: 1 - inversion
+  std::vector<Step> steps;
+  int64_t k = 0;
+  void init(const double* p, int64_t kk) {
+    k = kk;
+    steps.resize((size_t)std::max<int64_t>(k - 1, 0));
+    double remaining = 1.0;
+    for (int64_t j = 0; j < k - 1; ++j) {
+      const double pj = p[j] / remaining;
+      Step st{0.0, 0.0, 0};
+      if (pj != 0.0) {
+        const double pp = pj <= 0.5 ? pj : 1.0 - pj;
+        const double q = 1.0 - pp;
+        st.qn = exp(1.0 * log(q));
+        st.px1 = ((double)1 * pp * st.qn) / ((double)1 * q);
+        st.kind = pj <= 0.5 ? 1 : 2;
+      }
+      steps[(size_t)j] = st;
+      remaining -= p[j];
+    }
+  }
+  // binomial by inversion with n = 1 (see above)
+  static int64_t inversion(tpe_mt_state* s, const Step& st) {
+    for (;;) {
+      double U = mt_double(s);
+      if (!(U > st.qn)) return 0;
+      U -= st.qn;
+      if (!(U > st.px1)) return 1;
+    }
+  }
+  int64_t draw(tpe_mt_state* s) const {
+    for (int64_t j = 0; j < k - 1; ++j) {
+      const Step& st = steps[(size_t)j];
+      if (st.kind == 0) continue;
+      const int64_t x = inversion(s, st);
+      if ((st.kind == 1 ? x : 1 - x) > 0) return j;
+    }
+    return k - 1;
+  }
+};
+
+// numpy's checks on pvals: every p in [0, 1] (no NaN) and a Kahan sum of all
+// but the last <= 1 + 1e-12
+bool pvals_ok(const double* p, int64_t k) {
+  if (k < 1) return false;
+  for (int64_t j = 0; j < k; ++j)
+    if (!(p[j] >= 0.0 && p[j] <= 1.0)) return false;
+  double sum = 0.0, c = 0.0;
+  for (int64_t j = 0; j < k - 1; ++j) {
+    const double y = p[j] - c;
+    const double t = sum + y;
+    c = (t - sum) - y;
+    sum = t;
+  }
+  return !(sum > 1.0 + 1e-12);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpe_replay_mixture(tpe_mt_state* st, const double* w, const double* mu, const double* sigma, int64_t k,
+                       int32_t bounded, double low, double high, int64_t n, double* out) {
+  if (!st || k < 1 || n < 0 || (n && !out) || !w || !mu || !sigma || !pvals_ok(w, k)) return TPE_E_ARG;
+  for (int64_t j = 0; j < k; ++j)
+    if (!(sigma[j] >= 0.0)) return TPE_E_ARG;                // numpy: scale < 0 raises
+  if (st->pos < 0 || st->pos > kMtN) return TPE_E_ARG;
+  if (!bounded) {
+    // rng.multinomial(1, w, (n,)) then rng.normal(mu[idx], sigma[idx])
+    static thread_local std::vector<int64_t> idx_tl;
+    std::vector<int64_t>& idx = idx_tl;
+    idx.resize((size_t)n);
+    Multinom1 m;
+    m.init(w, k);
+    for (int64_t i = 0; i < n; ++i) idx[(size_t)i] = m.draw(st);
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t c = idx[(size_t)i];
+      out[i] = mu[c] + sigma[c] * mt_gauss(st);
+    }
+    return TPE_OK;
+  }
+  if (!(low < high)) return TPE_E_ARG;
+  Multinom1 m;
+  m.init(w, k);
+  // (the reference rejects forever when [low, high) holds no mass; this stops
+  // after 2^40 tries with TPE_E_ARG)
+  for (int64_t i = 0, tries = 0; i < n; ++tries) {
+    if (tries >= ((int64_t)1 << 40)) return TPE_E_ARG;
+    const int64_t c = m.draw(st);
+    const double d = mu[c] + sigma[c] * mt_gauss(st);
+    if (low <= d && d < high) out[i++] = d;
+  }
+  return TPE_OK;
+}
+
+int tpe_replay_categorical(tpe_mt_state* st, const double* p, int64_t k, int64_t n, int64_t* out) {
+  if (!st || n < 0 || (n && !out) || !p || !pvals_ok(p, k) || st->pos < 0 || st->pos > kMtN) return TPE_E_ARG;
+  Multinom1 m;
+  m.init(p, k);
+  for (int64_t i = 0; i < n; ++i) out[i] = m.draw(st);
+  return TPE_OK;
+}
+
+}  // extern "C"

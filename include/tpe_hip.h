@@ -458,6 +458,35 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
                        int32_t upper, const double* p_prior, double prior_weight, int32_t lf, double* out_below,
                        double* out_above);
 
+/* ------------------------------------------------------------------------
+ * Exact-replay candidate draws (host): numpy's legacy RandomState stream —
+ * MT19937 (the 624-word key and position of RandomState.get_state()),
+ * random_sample's 53-bit double, the polar-method gauss with its cached
+ * second value, and multinomial(n=1, p) as numpy computes it (a binomial by
+ * inversion per category, p_j over the remaining mass, until the draw is
+ * placed).  The state is read and written in place, so draws interleave with
+ * the caller's own use of the same RandomState.  Reference call sites:
+ * tpe.py:73-74 / :224-231 (unbounded: n multinomials, then n normals),
+ * tpe.py:82-87 / :240-244 (bounded: multinomial + normal per draw, rejected
+ * outside [low, high)), pyll/stochastic.py:126-131 (categorical).
+ * ---------------------------------------------------------------------- */
+typedef struct tpe_mt_state {
+  uint32_t key[624];
+  int32_t pos;           /* next key word (624: regenerate first)        */
+  int32_t has_gauss;     /* a cached second polar-method value is pending */
+  double gauss;
+} tpe_mt_state;
+
+/* n draws from the mixture (w, mu, sigma)[k]: the normal deviate d of each
+ * accepted draw (bounded: low <= d < high, in the mixture's own coordinate —
+ * the caller applies exp / rounding, vectorised, as the reference does);
+ * TPE_E_ARG on bad weights (numpy raises ValueError) */
+int tpe_replay_mixture(tpe_mt_state* st, const double* w, const double* mu, const double* sigma, int64_t k,
+                       int32_t bounded, double low, double high, int64_t n, double* out);
+
+/* n categorical draws (one multinomial(1, p) row each): the chosen index */
+int tpe_replay_categorical(tpe_mt_state* st, const double* p, int64_t k, int64_t n, int64_t* out);
+
 /* pack one tree level into `blob` (all tables, 256-B aligned, ready for one
  * host->device copy); TPE_E_SPACE (info->blob_bytes = size needed) if too small */
 int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,

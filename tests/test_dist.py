@@ -82,3 +82,48 @@ def test_gloo_world2_allgather():
         assert p.exitcode == 0
     for rank, gidx, val in out:
         assert gidx == [11, 100] and val == [1.0, 0.0]
+
+
+def _from_rec(r):
+    out = np.zeros(len(r['score']), dtype=N.RESULT_DTYPE)
+    for f, v in r.items():
+        out[f] = v
+    return out
+
+
+def _engine_worker(rank, world, port, cases, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from hyperopt_amd.dist import allgather_results
+    out = []
+    for case in cases:
+        res = allgather_results(_from_rec(case['shards'][rank]))
+        out.append({f: res[f].tolist() for f in ('score', 'value', 'global_idx')})
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_combines_recorded_engine_shards():
+    """Real device outputs (tests/golden/shard_results.json, recorded on an
+    MI355X by tools/gen_shard_fixture.py: the config-3 tree's fused level run
+    unsharded and as two candidate shards) combined over a world-2 gloo group
+    equal the unsharded run on every problem."""
+    from tests.conftest import load_golden
+    cases = load_golden('shard_results.json')
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, 2, port, cases, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got in out:
+        for case, g in zip(cases, got):
+            full = case['full']
+            assert g['global_idx'] == full['global_idx'], (rank, case['C'], case['seed'])
+            assert g['value'] == full['value'] and g['score'] == full['score']

@@ -270,3 +270,47 @@ def test_lazy_categorical_flag_native_matches_numpy():
         prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, info.n_problems)
         np.testing.assert_array_equal(prob['flags'], ref['prob']['flags'])
         assert all(bool(f & N.F_CAT_LAZY) == lazy for f in prob['flags']), (pb, pa)
+
+
+def test_native_replay_matches_golden_samplers(golden):
+    """tpe_replay_mixture / tpe_replay_categorical (native MT19937, legacy
+    polar gauss, multinomial by binomial inversion) reproduce the reference's
+    own sampler outputs (tests/golden/unit_vectors.json, generated by the
+    reference's GMM1/LGMM1/categorical) bit for bit."""
+    from hyperopt_amd import replay as R
+    for case in golden('unit_vectors.json')['samplers']:
+        rng = np.random.RandomState(case['seed'])
+        if case['fn'] == 'categorical':
+            out = R.draw_categorical(rng, case['p'], case['size'])
+        else:
+            out = R.draw_mixture(rng, case['w'], case['mu'], case['sigma'], case['low'], case['high'], case['q'],
+                                 case['fn'] == 'LGMM1', case['size'])
+        np.testing.assert_array_equal(np.ravel(out), np.ravel(np.asarray(case['out'])))
+
+
+def test_native_replay_continues_randomstate():
+    """Native draws equal numpy's RandomState draws on random mixtures
+    (bounded/unbounded, log, quantized, zero weights, a pending cached gauss)
+    and leave the RandomState exactly where numpy would."""
+    from hyperopt_amd import replay as R
+    rs = np.random.RandomState(0)
+    for t in range(150):
+        k = rs.randint(1, 30)
+        w = rs.dirichlet(np.ones(k) * rs.choice([0.1, 1.0, 5.0]))
+        if k > 1 and rs.rand() < 0.2:
+            w[rs.randint(k)] = 0.0
+            w /= w.sum()
+        mu, sg = rs.uniform(-3, 3, k), rs.uniform(0.05, 2, k)
+        low, high = (-2.0, 2.5) if rs.rand() < 0.5 else (None, None)
+        q, lg, n = [None, 0.5][rs.randint(2)], rs.rand() < 0.3, rs.randint(0, 300)
+        seed = rs.randint(1 << 30)
+        a, b = np.random.RandomState(seed), np.random.RandomState(seed)
+        a.normal(), b.normal()
+        np.testing.assert_array_equal(R.draw_mixture(a, w, mu, sg, low, high, q, lg, n),
+                                      R.draw_mixture_numpy(b, w, mu, sg, low, high, q, lg, n))
+        assert a.uniform() == b.uniform() and a.normal() == b.normal(), t
+        p = rs.dirichlet(np.ones(k))
+        np.testing.assert_array_equal(R.draw_categorical(a, p, n), R.draw_categorical_numpy(b, p, n))
+        assert a.randint(1 << 30) == b.randint(1 << 30), t
+    with pytest.raises(ValueError):                   # numpy's own error for bad weights
+        R.draw_mixture(np.random.RandomState(1), [1.5, -0.5], [0.0, 1.0], [1.0, 1.0], None, None, None, False, 3)

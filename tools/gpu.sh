@@ -12,6 +12,7 @@
 #   stage      steady-state per-stage device times        (REP)
 #   configs    bench.py --config 1, 2, 4, 5
 #   hostsplit  host-side time split of the headline suggest
+#   hostprof   cProfile of the headline suggest on the device
 #   pmcloop    PMC counter passes on tools/suggest_loop.py (the real suggest flow)
 #   apitrace   HIP API + kernel + copy trace of tools/suggest_loop.py -> timeline of the last suggests
 #   counters   rocprofv3 -L (the counters this box offers) -> gpurun_out/counters.txt
@@ -77,6 +78,9 @@ for task in "$@"; do
         step 600 $O/cfg${c}_${TAG}.err python bench.py --config $c --steps ${CFG_STEPS:-5} --warmup 1
         grep '^{' $O/cfg${c}_${TAG}.err > $O/cfg${c}_${TAG}.json; cat $O/cfg${c}_${TAG}.json
       done ;;
+    hostprof)
+      step 300 $O/hostprof_${TAG}.txt python tools/host_prof.py ${STEPS:-300}
+      head -60 $O/hostprof_${TAG}.txt ;;
     hostsplit)
       step 300 $O/hostsplit_${TAG}.txt python tools/host_split.py ${STEPS:-200}
       cat $O/hostsplit_${TAG}.txt ;;
