@@ -57,6 +57,22 @@ def synthetic_loss(v, tid):
     return loss + 1e-9 * tid
 
 
+def rf_loss(v, tid):
+    """A synthetic loss that steers the tree to its rf branch (quantized
+    rf_n_est / rf_depth_n labels at the full candidate count)."""
+    import math
+    loss = 1.0
+    if v.get('model') == 1:
+        loss = 0.3 + 1e-3 * abs(float(v['rf_n_est']) - 180) + 0.05 * int(v['rf_crit'])
+        if v.get('rf_depth') == 1:
+            loss -= 0.1 - 0.005 * abs(float(v['rf_depth_n']) - 12)
+    elif v.get('model') == 2:
+        loss = 0.6 + 0.01 * abs(float(v['knn_k']) - 7) + 0.05 * (float(v['knn_p']) - 2) ** 2
+    elif v.get('model') == 0:
+        loss = 0.8 + 0.01 * (math.log(float(v['svm_C']))) ** 2
+    return loss + 1e-9 * tid
+
+
 def make_history(n, seed, loss=None):
     """``n`` prior draws of the config-3 tree space (rand.suggest) with losses
     from ``loss(vals, tid)`` (default synthetic_loss)."""
@@ -318,6 +334,7 @@ def main():
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-quantized', action='store_true', help='skip the rf-branch (quantized) report')
     ap.add_argument('--history', type=int, default=N_HISTORY)
     ap.add_argument('--cands', type=int, default=C_PER_GPU)
     ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
@@ -421,6 +438,25 @@ def main():
     stages = {k: float(np.mean([a[0] for a in v])) for k, v in prof.items()}
 
 
+    # one quantized-branch workload beside the line: the same tree and sizes with
+    # a history steered to the rf branch (quantized labels at 2^20 candidates)
+    quant = None
+    if world == 1 and not args.no_quantized:
+        qdom, qtr = make_history(args.history, SEED, loss=rf_loss)
+        for i in range(args.warmup):
+            tpe.suggest([new_id], qdom, qtr, SEED + 9000 + i, n_EI_candidates=C_total)
+        torch.cuda.synchronize()
+        ql, qd = [], None
+        for i in range(10):
+            s0 = time.perf_counter()
+            qd = tpe.suggest([new_id], qdom, qtr, SEED + 9100 + i, n_EI_candidates=C_total)
+            ql.append(time.perf_counter() - s0)
+        vals = {k: float(v[0]) for k, v in qd[0]['misc']['vals'].items() if v}
+        quant = dict(workload='config3 tree, rf-steered %d-trial history (quantized rf_n_est/rf_depth_n), '
+                              'n_EI_candidates=%d' % (args.history, C_total),
+                     p50_suggest_ms=1e3 * float(np.median(ql)), active_labels=sorted(vals),
+                     model=int(vals.get('model', -1)))
+
     if rank == 0:
         out = {
             'metric': 'EI candidates scored/sec (node) + tpe.suggest p50 latency, 1M cands x 10k trials',
@@ -435,6 +471,7 @@ def main():
             'p50_suggest_ms': 1e3 * float(np.median(lat)), 'p99_suggest_ms': 1e3 * float(np.percentile(lat, 99)),
             'active_hyperparameters_per_suggest': n_active / args.steps,
             'stage_ms': stages, 'roofline': roof, 'kernels': kernels, 'cpu_baseline': cpu,
+            'quantized_branch': quant,
             # the same 2^20 candidates in total over N ranks (N = 1: the line itself)
             'strong_scaling': strong if strong is not None else dict(
                 n_EI_candidates_total=C_total, per_rank=C_total, value=value, unit='candidate-scores/s',

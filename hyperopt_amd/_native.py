@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 9
+ABI_VERSION = 10
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -87,7 +87,8 @@ class Batch(ctypes.Structure):
         ('tab_jobs', ctypes.c_void_p), ('n_tab_jobs', ctypes.c_int32), ('tab_blocks', ctypes.c_int32),
         ('tab', ctypes.c_void_p), ('tab_units', ctypes.c_int64),
         ('samp_tiles', ctypes.c_void_p), ('n_samp_tiles', ctypes.c_int32), ('n_samp_eager', ctypes.c_int32),
-        ('tab_tiles', ctypes.c_void_p), ('n_tab_tiles', ctypes.c_int32), ('reserved7', ctypes.c_int32),
+        ('tab_tiles', ctypes.c_void_p), ('n_tab_tiles', ctypes.c_int32), ('early_select', ctypes.c_int32),
+        ('run_best', ctypes.c_void_p), ('n_late', ctypes.c_int32), ('reserved8', ctypes.c_int32),
     ]
 
 

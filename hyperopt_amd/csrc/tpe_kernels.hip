@@ -717,7 +717,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
                                                             double* __restrict__ l_out, double* __restrict__ g_out,
                                                             int draw, int flags,
                                                             const float4* __restrict__ comp32,
-                                                            const float4* __restrict__ tab) {
+                                                            const float4* __restrict__ tab,
+                                                            tpe_result* __restrict__ run_best) {
   __shared__ float4 tab_lds[4 * kTabLdsCells];
   __shared__ double cum_lds[kCumLds];
   __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
@@ -753,8 +754,30 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         if (better(os, oi, s2, i2)) { s2 = os; l2 = ol; g2 = og; i2 = oi; }
       }
       if (lane == 0) {
-        tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
-        d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
+        if (run_best) {
+          // early selection: the run's best with its value re-drawn (the
+          // select stage's redraw), straight to host-visible memory
+          const tpe_problem& q = P[cur];
+          tpe_result r;
+          r.score = s2; r.l = l2; r.g = g2; r.idx = i2; r.value = 0.0;
+          r.global_idx = i2 >= 0 ? q.cand_base + i2 : -1;
+          if (i2 >= 0) {
+            if (draw && q.samp_len > 0) {
+              float lo_f, hi_f, t;
+              int c;
+              f32_bounds(q, lo_f, hi_f);
+              const double* S = samp + 8 * (int64_t)q.samp_off;
+              if (in_lds) draw_one(q, S, cum_lds, 1, i2, PREC, lo_f, hi_f, r.value, t, c);
+              else draw_one(q, S, S, 8, i2, PREC, lo_f, hi_f, r.value, t, c);
+            } else {
+              r.value = cand[q.cand_off + i2];
+            }
+          }
+          run_best[run_tile] = r;
+        } else {
+          tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
+          d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
+        }
       }
     }
     bs = 0.0; bl = 0.0; bg = 0.0; bi = -1;
@@ -808,7 +831,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       run_tile = tile;
     }
     const int cand_start = __builtin_amdgcn_readfirstlane(s_start[gi]);
-    if (threadIdx.x < TPE_BEST_PER_TILE)
+    if (!run_best && threadIdx.x < TPE_BEST_PER_TILE)   // (early selection: runs report to run_best)
       tile_best[(int64_t)tile * TPE_BEST_PER_TILE + threadIdx.x] = tpe_best{0, 0, 0, -1};
     float lo_f, hi_f;
     f32_bounds(p, lo_f, hi_f);
@@ -1479,13 +1502,19 @@ __device__ double sel_lse2(const float4* __restrict__ comp, int k0, int n, int k
   return mm + log2(sel_reduce<double, false>(sum, lds));
 }
 
+// a lazy categorical problem (TPE_F_CAT_LAZY): selected by a scan of its
+// first draws, never by its tiles
+__device__ __forceinline__ bool lazy_eligible(const tpe_problem& p) {
+  return (p.flags & TPE_F_CAT_LAZY) && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= 64;
+}
+
 // lazy categorical (TPE_F_CAT_LAZY): draws scanned in index order, 4096 per
 // round (4 per thread), keeping each category's first index; stops once no undrawn drawable
 // category could beat the current best (np.argmax order via better(): an
 // undrawn category's index would exceed every drawn one) — after the first
 // round unless the best-scoring category is rare.
 __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__ samp,
-                                const double4* __restrict__ comp64, tpe_result* __restrict__ result) {
+                                const double4* __restrict__ comp64, tpe_result* __restrict__ out) {
   __shared__ double cum[64], score[64], lsh[64], gsh[64];   // l, g in LDS: no global loads in the serial scan
   __shared__ int first[64];
   __shared__ int done;
@@ -1536,18 +1565,18 @@ __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__
     r.score = b.score; r.l = b.l; r.g = b.g; r.idx = b.idx;
     r.value = b.idx >= 0 ? (double)draw_category(p, cum, b.idx) : 0.0;
     r.global_idx = b.idx >= 0 ? p.cand_base + b.idx : -1;
-    result[blockIdx.x] = r;
+    *out = r;
   }
 }
 
 // pooled problem: the winner from pool_best, its value re-drawn, its l and g
 // evaluated exactly over the whole mixtures (one workgroup)
-__device__ void select_pooled(const tpe_problem& p, const unsigned long long* __restrict__ pool_best,
+__device__ void select_pooled(const tpe_problem& p, int pid, const unsigned long long* __restrict__ pool_best,
                               const float4* __restrict__ comp32, const double* __restrict__ samp,
                               const double* __restrict__ cand, int precision, int sampled,
-                              tpe_result* __restrict__ result) {
+                              tpe_result* __restrict__ out) {
   __shared__ double lds[kSelThreads / 64];
-  const unsigned long long key = pool_best[blockIdx.x];
+  const unsigned long long key = pool_best[pid];
   const unsigned long long mask = (1ull << pool_idx_bits(p.n_cand)) - 1;
   const int64_t idx = key ? (int64_t)(mask - (key & mask)) : -1;
   tpe_result r;
@@ -1571,38 +1600,16 @@ __device__ void select_pooled(const tpe_problem& p, const unsigned long long* __
     r.score = r.l - r.g;
     r.global_idx = p.cand_base + idx;
   }
-  if (threadIdx.x == 0) result[blockIdx.x] = r;
+  if (threadIdx.x == 0) *out = r;
 }
-__global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __restrict__ P,
-                                                     const tpe_best* __restrict__ tile_best,
-                                                     const double* __restrict__ cand,
-                                                     const double* __restrict__ samp, int precision, int sampled,
-                                                     const double* __restrict__ draw_pref, int64_t draw_blocks,
-                                                     int ordered, const unsigned long long* __restrict__ pool_best,
-                                                     const float4* __restrict__ comp32,
-                                                     const double4* __restrict__ comp64, int lazy_ok,
-                                                     tpe_result* __restrict__ result) {
-  const tpe_problem& p = P[blockIdx.x];
-#ifdef TPE_SELECT_TRACE                    // debug builds only: per-block path and duration
-  const uint64_t t_start = wall_clock64();
-  struct Tr {
-    uint64_t t0; const tpe_problem& q;
-    __device__ ~Tr() {
-      if (threadIdx.x == 0)
-        printf("k_select blk %d fam %d flags %d samp_len %d n_tiles %d n_cand %d ticks %llu\n", (int)blockIdx.x,
-               (int)q.family, (int)q.flags, (int)q.samp_len, (int)q.n_tiles, (int)q.n_cand,
-               (unsigned long long)(wall_clock64() - t0));
-    }
-  } tr{t_start, p};
-#endif
-  if (lazy_ok && sampled && (p.flags & TPE_F_CAT_LAZY) && p.family == TPE_FAM_CATEGORICAL && p.samp_len <= 64) {
-    select_cat_lazy(p, samp, comp64, result);
-    return;
-  }
-  if (p.flags & TPE_F_POOLED) {            // problem-uniform
-    select_pooled(p, pool_best, comp32, samp, cand, precision, sampled, result);
-    return;
-  }
+// the winner of a problem scored per tile: the best of its tiles' slots
+// (np.argmax order), its value re-drawn (never stored), l and g as scored.
+// One kSelThreads workgroup; every thread returns (k_select, and the sample
+// stage's last workgroup of a tabulated problem).
+__device__ void select_generic(const tpe_problem& p, const tpe_best* __restrict__ tile_best,
+                               const double* __restrict__ cand, const double* __restrict__ samp, int precision,
+                               int sampled, const double* __restrict__ draw_pref, int64_t draw_blocks, int ordered,
+                               tpe_result* __restrict__ out) {
   // the sampler rows of a <= 64-component mixture staged in LDS while the tile
   // bests load, so the winner's redraw needs no dependent global loads
   __shared__ double srow[64 * 8];
@@ -1627,7 +1634,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
   __shared__ tpe_best wb[kSelThreads / 64];
   if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = b;
   __syncthreads();
-  if (threadIdx.x >= 64) return;
+  if (threadIdx.x < 64) {                  // wave 0 finishes (no early return: callers continue)
   b = wb[0];
   for (int q = 1; q < kSelThreads / 64; ++q)
     if (better(wb[q].score, wb[q].idx, b.score, b.idx)) b = wb[q];
@@ -1673,10 +1680,46 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
       r.value = cand[p.cand_off + b.idx];
     }
     r.global_idx = b.idx >= 0 ? p.cand_base + b.idx : -1;
-    result[blockIdx.x] = r;
+    *out = r;
   }
+  }
+  __syncthreads();                         // (srow / wb reusable by the caller's next selection)
 }
 
+__global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __restrict__ P,
+                                                     const tpe_best* __restrict__ tile_best,
+                                                     const double* __restrict__ cand,
+                                                     const double* __restrict__ samp, int precision, int sampled,
+                                                     const double* __restrict__ draw_pref, int64_t draw_blocks,
+                                                     int ordered, const unsigned long long* __restrict__ pool_best,
+                                                     const float4* __restrict__ comp32,
+                                                     const double4* __restrict__ comp64, int lazy_ok,
+                                                     int early, tpe_result* __restrict__ result) {
+  const tpe_problem& p = P[blockIdx.x];
+#ifdef TPE_SELECT_TRACE                    // debug builds only: per-block path and duration
+  const uint64_t t_start = wall_clock64();
+  struct Tr {
+    uint64_t t0; const tpe_problem& q;
+    __device__ ~Tr() {
+      if (threadIdx.x == 0)
+        printf("k_select blk %d fam %d flags %d samp_len %d n_tiles %d n_cand %d ticks %llu\n", (int)blockIdx.x,
+               (int)q.family, (int)q.flags, (int)q.samp_len, (int)q.n_tiles, (int)q.n_cand,
+               (unsigned long long)(wall_clock64() - t0));
+    }
+  } tr{t_start, p};
+#endif
+  const bool lazy = lazy_ok && sampled && lazy_eligible(p);
+  if (early && (lazy || p.tab_mode != TPE_TAB_NONE)) return;   // selected by the table / sample stage
+  if (lazy) {
+    select_cat_lazy(p, samp, comp64, result + blockIdx.x);
+    return;
+  }
+  if (p.flags & TPE_F_POOLED) {            // problem-uniform
+    select_pooled(p, blockIdx.x, pool_best, comp32, samp, cand, precision, sampled, result + blockIdx.x);
+    return;
+  }
+  select_generic(p, tile_best, cand, samp, precision, sampled, draw_pref, draw_blocks, ordered, result + blockIdx.x);
+}
 
 // ============================================================ score tables
 // (include/tpe_hip.h "Tabulated scoring")
@@ -1934,8 +1977,17 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
                                                           const float4* __restrict__ comp32,
                                                           const double4* __restrict__ comp64,
                                                           const int32_t* __restrict__ grid,
-                                                          float4* __restrict__ tab, bool all_exact) {
+                                                          float4* __restrict__ tab, bool all_exact,
+                                                          int tab_blocks, const double* __restrict__ samp,
+                                                          int lazy_ok, tpe_result* __restrict__ result) {
   __shared__ float4 rows_lds[kTabStageRows];
+  if ((int)blockIdx.x >= tab_blocks) {
+    // early selection: one block per problem selects a lazy categorical
+    // problem right here (it needs no tables)
+    const tpe_problem& q = P[(int)blockIdx.x - tab_blocks];
+    if (lazy_ok && lazy_eligible(q)) select_cat_lazy(q, samp, comp64, result + ((int)blockIdx.x - tab_blocks));
+    return;
+  }
 #ifdef TPE_TABLES_TRACE                     // debug builds only: per-phase wave timing
   uint64_t tt[6];
   tt[0] = wall_clock64();
@@ -2310,6 +2362,12 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __
 }
 
 // device-drawn sorted problems at f32 draw ordered (include/tpe_hip.h "Ordered draws")
+// the select stage may scan a lazy categorical problem's first draws (nothing
+// per candidate requested)
+bool lazy_ok(const tpe_batch* b) {
+  return b->sample && !(b->flags & TPE_BATCH_WRITE_CAND) && !b->l_out;
+}
+
 bool ordered_draws(const tpe_batch* b) {
   return b->sample && b->precision == TPE_PREC_F32 && (b->flags & TPE_BATCH_ORDERED_DRAWS) && b->n_sorted > 0 &&
          b->sort_count > 0;
@@ -2349,6 +2407,9 @@ int check_batch(const tpe_batch* b) {
   if (b->n_tab_jobs < 0 || b->tab_blocks < 0 || b->tab_units < 0) return fail(TPE_E_ARG, "negative table count");
   if (b->n_tab_jobs > 0 && (!b->tab_jobs || !b->tab || !b->comp32 || !b->comp64))
     return fail(TPE_E_ARG, "null table buffers");
+  if (b->early_select && (!b->run_best || b->n_tab_jobs <= 0 || !b->sample || !b->samp || !b->tab_tiles ||
+                          b->n_late < 0 || b->n_late > b->n_problems))
+    return fail(TPE_E_ARG, "early selection needs tables, device draws, tile lists and run_best");
   return TPE_OK;
 }
 
@@ -2391,6 +2452,21 @@ int cu_count() {
     cache[dev] = n;
   }
   return cache[dev];
+}
+
+// tabulated tiles per sample-stage workgroup (the early selection's run
+// enumeration on the host uses the same partition)
+int tab_tiles_per_wg(int n_tab) {
+  return std::min(kTabMaxTilesPerWg, std::max(1, (n_tab + cu_count() - 1) / cu_count()));
+}
+
+// np.argmax order of (score, index) on the host: better() of the kernels
+bool host_better(double s, int64_t i, double bs, int64_t bi) {
+  if (bi < 0) return i >= 0;
+  if (i < 0) return false;
+  const bool n = s != s, bn = bs != bs;
+  if (n || bn) return n && (!bn || i < bi);
+  return s > bs || (s == bs && i < bi);
 }
 
 }  // namespace
@@ -2473,10 +2549,12 @@ int tpe_tables(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
   const char* twice = getenv("TPE_DEBUG_TABLES_TWICE");      // (timing experiments: a warm second launch)
+  const int extra = b->early_select ? b->n_problems : 0;
   for (int r = 0; r < (twice && twice[0] == '1' ? 2 : 1); ++r)
-    hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks), dim3(kTabTblThreads), 0, (hipStream_t)stream, b->problems,
-                       b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64, b->grid,
-                       (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0);
+    hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks + extra), dim3(kTabTblThreads), 0, (hipStream_t)stream,
+                       b->problems, b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64,
+                       b->grid, (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0, b->tab_blocks, b->samp,
+                       lazy_ok(b) ? 1 : 0, b->result);
   return hip_check("tpe_tables");
 }
 
@@ -2510,16 +2588,19 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (n_tab > 0) {
     if (!b->tab) return fail(TPE_E_ARG, "tabulated tiles without score tables");
     // one workgroup per CU-sized group of tiles (each stages its problem once)
-    const int per = std::min(kTabMaxTilesPerWg, std::max(1, (n_tab + cu_count() - 1) / cu_count()));
+    const int per = tab_tiles_per_wg(n_tab);
     const int wgs = (n_tab + per - 1) / per;
+    tpe_result* run_best = b->early_select ? b->run_best : nullptr;
     if (b->precision == TPE_PREC_F64)
       hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F64>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
-                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab);
+                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
+                         run_best);
     else
       hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F32>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
-                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab);
+                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
+                         run_best);
   }
   return hip_check("tpe_sample");
 }
@@ -2585,11 +2666,11 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
 int tpe_select(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  if (b->n_problems == 0) return TPE_OK;
+  if (b->n_problems == 0 || (b->early_select && b->n_late == 0)) return TPE_OK;
   hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
                      b->tile_best, b->cand, b->samp, b->precision, b->sample, b->draw_pref, b->draw_blocks,
                      ordered_draws(b) ? 1 : 0, b->pool_best, (const float4*)b->comp32, (const double4*)b->comp64,
-                     (!(b->flags & TPE_BATCH_WRITE_CAND) && !b->l_out) ? 1 : 0, b->result);
+                     lazy_ok(b) ? 1 : 0, b->early_select ? 1 : 0, b->result);
   return hip_check("tpe_select");
 }
 
@@ -2619,7 +2700,9 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   if (rc != TPE_OK && rc != TPE_E_SPACE) return fail(rc, "tpe_host_pack_level: bad level description");
   const int64_t P = info.n_problems, C = P * (int64_t)n_cand;
   const int64_t res_off = (info.blob_bytes + 255) & ~(int64_t)255;
-  need->pinned_bytes = res_off + P * (int64_t)sizeof(tpe_result);
+  // early selection's per-run bests follow the results (host-visible)
+  const int64_t rb_off = (res_off + P * (int64_t)sizeof(tpe_result) + 255) & ~(int64_t)255;
+  need->pinned_bytes = rb_off + (info.n_tab_jobs > 0 ? info.n_tiles * (int64_t)sizeof(tpe_result) : 0);
   need->blob_bytes = info.blob_bytes;
   need->cand = C;
   need->part = info.part_total;
@@ -2718,6 +2801,22 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   tpe_result* rh = (tpe_result*)(host + res_off);
   char* dbase = direct_results() ? device_alias(ws->pinned) : nullptr;
   tpe_result* rd = dbase ? (tpe_result*)(dbase + res_off) : nullptr;
+  // early selection (include/tpe_hip.h): the sample stage reports each run of
+  // tabulated tiles to host-visible memory, the table stage selects the lazy
+  // categoricals, and only the rest go through the select stage
+  const tpe_problem* hp = (const tpe_problem*)(host + info.off_problems);
+  if (info.n_tab_jobs > 0 && dbase) {
+    b.early_select = 1;
+    b.run_best = (tpe_result*)(dbase + rb_off);
+    const bool lz = !(flags & TPE_BATCH_WRITE_CAND);
+    int32_t late = 0;
+    for (int64_t r = 0; r < P; ++r) {
+      const tpe_problem& q = hp[r];
+      const bool lazy = lz && (q.flags & TPE_F_CAT_LAZY) && q.family == TPE_FAM_CATEGORICAL && q.samp_len <= 64;
+      late += !(lazy || q.tab_mode != TPE_TAB_NONE);
+    }
+    b.n_late = late;
+  }
   b.result = rd ? rd : ws->result;
   if (info.n_fit > 0) {
     b.fit = (const tpe_fit_job*)(dev + info.off_fit);
@@ -2734,6 +2833,23 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   e = rd ? hipSuccess : hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  if (b.early_select) {
+    // each tabulated problem: the best of its runs (np.argmax order), runs
+    // enumerated exactly as the sample stage partitions the tile list
+    const tpe_result* rb = (const tpe_result*)(host + rb_off);
+    const int32_t* list = (const int32_t*)(host + info.off_tab_tiles);
+    const tpe_tile* tl = (const tpe_tile*)(host + info.off_tiles);
+    const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab);
+    for (int64_t r = 0; r < P; ++r)
+      if (hp[r].tab_mode != TPE_TAB_NONE) { rh[r] = tpe_result{0, 0, 0, 0, -1, -1}; }
+    for (int i = 0; i < n_tab; ++i) {
+      const int t = list[i], pr = tl[t].problem;
+      if (i % per != 0 && tl[list[i - 1]].problem == pr) continue;        // not a run's first tile
+      const tpe_result& c = rb[t];
+      tpe_result& w = rh[pr];
+      if (host_better(c.score, c.idx, w.score, w.idx)) w = c;
+    }
+  }
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));
   return TPE_OK;
 }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 9
+#define TPE_ABI_VERSION 10
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -345,7 +345,18 @@ typedef struct tpe_batch {
    * last (the first n_samp_eager of them skip those when the lazy scan applies);
    * tab_tiles[0 .. n_tab_tiles) = the tabulated tiles (one 2048-candidate block each) */
   const int32_t* samp_tiles; int32_t n_samp_tiles; int32_t n_samp_eager;
-  const int32_t* tab_tiles; int32_t n_tab_tiles; int32_t reserved7;
+  const int32_t* tab_tiles; int32_t n_tab_tiles;
+  /* early selection (needs tables, sampled candidates, tab_tiles and
+   * run_best): the sample stage writes, for every run of consecutive tiles of
+   * one tabulated problem a workgroup processes, the run's best candidate —
+   * score, l, g, index and its drawn value — to run_best[first tile of the run]
+   * (host-visible memory; the caller reduces a problem's runs with np.argmax
+   * semantics: tpe_level_run does); each lazy categorical problem is selected
+   * by the table stage; the select stage runs only for the n_late others (not
+   * at all when n_late == 0).  0: the select stage selects every problem. */
+  int32_t early_select;
+  tpe_result* run_best;  /* [n_tiles], device address of host-visible memory */
+  int32_t n_late; int32_t reserved8;
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */

@@ -131,18 +131,8 @@ def _check_problem(eng, fits, row, hist, ids, C, seed, winners, rs, what, **kw):
 
 # ----------------------------------------------------------------- config 3
 def _tree_loss_rf(v, tid):
-    """Favours the rf branch (quantized n_est / depth labels) of the tree."""
-    import math
-    loss = 1.0
-    if v.get('model') == 1:
-        loss = 0.3 + 1e-3 * abs(float(v['rf_n_est']) - 180) + 0.05 * int(v['rf_crit'])
-        if v.get('rf_depth') == 1:
-            loss -= 0.1 - 0.005 * abs(float(v['rf_depth_n']) - 12)
-    elif v.get('model') == 2:
-        loss = 0.6 + 0.01 * abs(float(v['knn_k']) - 7) + 0.05 * (float(v['knn_p']) - 2) ** 2
-    elif v.get('model') == 0:
-        loss = 0.8 + 0.01 * (math.log(float(v['svm_C']))) ** 2
-    return loss + 1e-9 * tid
+    import bench
+    return bench.rf_loss(v, tid)
 
 
 @pytest.mark.parametrize('branch', ['svm', 'rf'])

@@ -1,6 +1,7 @@
 """Timeline of the last suggests in a rocprofv3 --hip-trace --kernel-trace
 --memory-copy-trace capture (csv): every HIP API call, kernel and copy between
-consecutive k_select kernels, relative to the window start (us)."""
+the ends of consecutive hipStreamSynchronize calls (one per tpe_level_run),
+relative to the window start (us)."""
 import csv
 import glob
 import os
@@ -20,7 +21,7 @@ def main(root, n_show=2):
         '(anonymous namespace)::', '').replace('void ', '').split('(')[0][:40]) for r in rows(root, '*kernel_trace.csv')]
     cpy = [(int(r['Start_Timestamp']), int(r['End_Timestamp']), 'C ' + r.get('Direction', 'copy') + ' ' +
             r.get('Size', '')) for r in rows(root, '*memory_copy_trace.csv')]
-    sel = sorted(k for k in ker if 'k_select' in k[2])
+    sel = sorted(a for a in api if a[2] == 'hipStreamSynchronize')
     if len(sel) < n_show + 1:
         print('not enough suggests traced')
         return

@@ -40,7 +40,7 @@ prof_run() {  # name counters...
   local name=$1; shift
   rm -rf $O/pmc_${TAG}/$name
   step 300 $O/pmc_${TAG}/$name.log rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
-      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
+      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-quantized ${BENCH_ARGS:-}
 }
 
 for task in "$@"; do
@@ -58,7 +58,7 @@ for task in "$@"; do
     trace)
       rm -rf $O/trace_${TAG}
       step 600 $O/trace_${TAG}.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_${TAG} -o run -- \
-          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-}
+          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-quantized ${BENCH_ARGS:-}
       python3 tools/trace_summary.py $(find $O/trace_${TAG} -name "*kernel_trace.csv") > $O/trace_${TAG}_summary.txt
       head -25 $O/trace_${TAG}_summary.txt ;;
     pmc)
@@ -88,7 +88,7 @@ for task in "$@"; do
       for v in ${LIBS:-default}; do
         if [ "$v" = default ]; then lib=$PWD/hyperopt_amd/libtpe_hip.so; else lib=$PWD/hyperopt_amd/libtpe_hip_$v.so; fi
         step 300 $O/stage_${TAG}_$v.txt env TPE_HIP_LIB=$lib python tools/stage_bench.py ${REP:-20}
-        step 300 $O/bench_${TAG}_$v.err env TPE_HIP_LIB=$lib python bench.py --no-cpu-baseline --steps 100
+        step 300 $O/bench_${TAG}_$v.err env TPE_HIP_LIB=$lib python bench.py --no-cpu-baseline --no-quantized --steps 100
         echo "$v: $(grep -o '"p50_suggest_ms": [0-9.]*\|"stage_ms": {[^}]*}' $O/bench_${TAG}_$v.err | tr '\n' ' ')"
       done ;;
     pmcloop)
