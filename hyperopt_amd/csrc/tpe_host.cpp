@@ -56,6 +56,7 @@ constexpr int kTailMinTiles = 32;      // per-tile tail splits from 32 tiles (64
 constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e)): a = kAScale / max(sigma, EPS)
 constexpr double kTabEta = 0.05;                  // a_max * h <= kTabEta for every cell of half-width h
 constexpr int64_t kTabMaxCells = 65536;           // per side; more: per-candidate scoring
+constexpr double kTabMinRatio = 8.0, kTabMinRatioDevFit = 64.0;   // candidates per cell row for tables
 constexpr int64_t kTabMaxLattice = 1 << 18;       // lattice values per quantized label
 // TPE_TABLES=0 turns tabulated scoring off (A/B and tests); read per call
 bool tables_enabled() {
@@ -500,7 +501,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       else
         for (int64_t i = 0; i < L.above_k; ++i) s1 = std::min(s1, L.above_sigma[i]);
       const int64_t n0 = tab_cells(klo, khi, s0), n1 = L.above_k > 0 ? tab_cells(klo, khi, s1) : -1;
-      if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= (double)(n0 + n1)) {
+      // a cell row costs ~10x a candidate's score (two passes plus the f64
+      // moments), more against the pruned, locally expanded per-candidate path
+      // of a device-fitted mixture: tables pay from kTabMinRatio candidates a cell
+      const double ratio = dev_fit[li] ? kTabMinRatioDevFit : kTabMinRatio;
+      if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= ratio * (double)(n0 + n1)) {
         tmode[li] = TPE_TAB_CELLS; tn0[li] = n0; tn1[li] = n1;
       }
     } else if ((L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) && L.q > 0 && L.above_k > 0 &&

@@ -1077,7 +1077,7 @@ __device__ __forceinline__ void below_sum(const float4* __restrict__ B, int n, f
 }
 
 #ifndef TPE_ABOVE_WAVES_PER_EU
-#define TPE_ABOVE_WAVES_PER_EU 5   // <= 96 VGPRs: 5 waves per SIMD
+#define TPE_ABOVE_WAVES_PER_EU 4   // <= 128 VGPRs: no scratch spills (5 waves spilled 48 B per lane)
 #endif
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(TPE_ABOVE_WAVES_PER_EU))) void k_above_f32(const tpe_problem* __restrict__ P,
                                                         const tpe_tile* __restrict__ tiles,

@@ -56,6 +56,7 @@ def _coord_range(post):
 TAB_ETA = 0.05                     # tpe_host.cpp kTabEta: a_max * h <= eta per cell
 TAB_MAX_CELLS = 65536
 TAB_MAX_LATTICE = 1 << 18
+TAB_MIN_RATIO, TAB_MIN_RATIO_DEVFIT = 8.0, 64.0   # tpe_host.cpp kTabMinRatio*: candidates per cell row
 A_SCALE_LIT = 0.84932180028801907  # tpe_host.cpp kAScale (the same double)
 
 
@@ -85,7 +86,8 @@ def _tab_plan(lp, n_cand, f64):
         else:
             s1 = float(np.min(post.above[2]))
         n0, n1 = cells(s0), cells(s1)
-        if 0 < n0 <= TAB_MAX_CELLS and 0 < n1 <= TAB_MAX_CELLS and ct >= n0 + n1:
+        ratio = TAB_MIN_RATIO_DEVFIT if post.above_dev is not None else TAB_MIN_RATIO
+        if 0 < n0 <= TAB_MAX_CELLS and 0 < n1 <= TAB_MAX_CELLS and ct >= ratio * (n0 + n1):
             return dict(mode=N.TAB_CELLS, n=(n0, n1), lo=klo, hi=khi, lat_lo=0)
     elif fam in (N.FAM_QGAUSS, N.FAM_QLOGGAUSS) and post.q and post.q > 0 and lp.inject is None:
         tlo, thi = klo, khi
