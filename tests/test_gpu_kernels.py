@@ -403,7 +403,9 @@ def test_device_fit_matches_oracle(engine, dist, args, scoring):
     res_d, cand_d, l_d, g_d = engine.run([LevelProblem(dev, 0, [3])], C, seed=9, want_lg=True, return_cand=True)
     res_h, cand_h, l_h, g_h = engine.run([LevelProblem(host, 0, [3])], C, seed=9, want_lg=True, return_cand=True)
     np.testing.assert_array_equal(cand_d, cand_h)
-    np.testing.assert_array_equal(l_d, l_h)
+    # the same below fit: equal l (bit for bit when both runs score the same way;
+    # a device-fitted label needs more candidates per table row before tables pay)
+    _check_lpdf(l_d[0], l_h[0], 1e-5, (dist, 'l'))
     sub = rs.choice(C, 3000, replace=False)
     _check_lpdf(g_d[0][sub], lpdf(cand_d[0][sub], *above, low=low, high=high), 1e-5, (dist, 'g'))
     _check_argmax(int(res_d[0]['idx']), l_h[0], g_h[0], 1e-5, dist)
@@ -515,7 +517,7 @@ def test_tabulated_scoring_matches_oracle(engine, dist, args):
     if q:
         obs = np.round(obs / q) * q
     post = parzen.fit_posterior(dist, args, obs[:30], obs[30:], 1.0)
-    C = 1 << 16
+    C = 1 << 18                                        # >= 8 candidates per table row
     res, cand, l, g = engine.run([LevelProblem(post, 5, [11])], C, seed=13, want_lg=True, return_cand=True)
     prob, _ = engine.device_tables()
     assert prob[0]['tab_mode'] == (N.TAB_LATTICE if q else N.TAB_CELLS), dist
@@ -560,7 +562,7 @@ def test_tabulated_exact_fallback_matches_oracle(engine, dist, args, monkeypatch
     obs = rs.uniform(lo, hi, 3000)
     obs = np.exp(obs) if log else obs
     post = parzen.fit_posterior(dist, args, obs[:30], obs[30:], 1.0)
-    C = 1 << 16
+    C = 1 << 18
     base = engine.run([LevelProblem(post, 5, [11])], C, seed=19)
     monkeypatch.setenv('TPE_DEBUG_FLAGS', str(N.BATCH_TAB_EXACT))
     res, cand, l, g = engine.run([LevelProblem(post, 5, [11])], C, seed=19, want_lg=True, return_cand=True)
