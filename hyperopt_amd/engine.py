@@ -432,6 +432,7 @@ class Engine(object):
         n = len(problems)
         recs = np.zeros(max(n, 1), dtype=N.LABEL_DTYPE)
         keep = [recs]
+        id_addr = {}                              # the level's problems usually share one ids array
         for i, lp in enumerate(problems):
             post = lp.post
             flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)
@@ -442,11 +443,14 @@ class Engine(object):
                 # native fits: the addresses are known; the posterior owns the arrays
                 keep.append(post)
                 pt = post.ptrs
+                ia = id_addr.get(id(ids))
+                if ia is None:
+                    ia = id_addr[id(ids)] = ids.ctypes.data
                 recs[i] = (post.family, flags, int(post.upper), lp.label_ix,
                            post.low if post.low is not None else 0.0, post.high if post.high is not None else 0.0,
                            post.q if post.q is not None else 0.0,
                            pt[0], pt[1], pt[2], pt[3], pt[4], pt[5], pt[6], pt[7],
-                           ids.ctypes.data, len(ids), 0, 0, 0, 0, 0, 0.0, 0.0, 0.0)
+                           ia, len(ids), 0, 0, 0, 0, 0, 0.0, 0.0, 0.0)
                 continue
             bw = [np.ascontiguousarray(a, dtype=np.float64) for a in post.below]
             ids = np.ascontiguousarray(lp.ids, dtype=np.int64)

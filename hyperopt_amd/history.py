@@ -39,6 +39,27 @@ class History(object):
     def smallest(self, m):
         return None if self._cache is None else self._cache.smallest(m)
 
+    def native_columns(self, label, log=False):
+        """(tids, coordinate, value order) host addresses of a label's columns
+        for the native fits — the cache's buffers, no per-call lookups — or
+        None without a Trials cache.  Call after value_order(label)."""
+        c = self._cache
+        if c is None:
+            return None
+        if log:
+            self.log_values(label)
+            xa = c.logs[label].addr
+        else:
+            xa = c.obs_val[label].addr
+        return c.obs_tid[label].addr, xa, c.order_addr(label)
+
+    def cat_columns(self, label):
+        """(tids, values) addresses of a categorical label (see native_columns)."""
+        c = self._cache
+        if c is None:
+            return None
+        return c.obs_tid[label].addr, c.obs_val[label].addr
+
     def log_values(self, label):
         """np.log of the label's observation values (the kernel coordinate of
         the log families) — extended incrementally by the Trials cache, else
@@ -77,15 +98,19 @@ class History(object):
 
 
 class _Grow(object):
-    __slots__ = ('a', 'n')
+    """Append-only column; ``addr`` = host address of its buffer (kept with
+    the buffer, so native calls need no per-call pointer lookup)."""
+    __slots__ = ('a', 'n', 'addr')
 
     def __init__(self, dtype):
         self.a = np.empty(64, dtype=dtype)
         self.n = 0
+        self.addr = self.a.ctypes.data
 
     def append(self, v):
         if self.n == self.a.shape[0]:
             self.a = np.concatenate([self.a, np.empty_like(self.a)])
+            self.addr = self.a.ctypes.data
         self.a[self.n] = v
         self.n += 1
 
@@ -105,6 +130,7 @@ class _Cache(object):
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
         self.orders = {}               # label -> value-sorting permutation of its observations
+        self.order_addrs = {}          # label -> (that permutation, its address)
         self.logs = {}                 # label -> _Grow of np.log of its observation values
         self.top = None                # positions of the smallest losses, sorted by (loss, position)
         self.top_n = 0                 # documents merged into `top`
@@ -147,9 +173,18 @@ class _Cache(object):
                 a = np.empty(max(n, 2 * g.a.shape[0]), dtype=np.float64)
                 a[:g.n] = g.a[:g.n]
                 g.a = a
+                g.addr = a.ctypes.data
             g.a[g.n:n] = np.log(vals[g.n:n])
             g.n = n
         return g.view()
+
+    def order_addr(self, k):
+        """Address of value_order(k)'s array (valid right after that call)."""
+        perm = self.orders.get(k)
+        a = self.order_addrs.get(k)
+        if a is None or a[0] is not perm:
+            a = self.order_addrs[k] = (perm, perm.ctypes.data)
+        return a[1]
 
     def value_order(self, k):
         """Sorting permutation of obs_val[k], extended by a merge of the

@@ -228,7 +228,8 @@ def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT
     return Posterior(dist, family, low, high, q, below, above)
 
 
-def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.0, lf=DEFAULT_LF, coord=None):
+def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.0, lf=DEFAULT_LF, coord=None,
+              addrs=None):
     """Continuous (non-quantized) label: the below/above split
     (ap_filter_trials, tpe.py:613-641) and both Parzen fits in one native call
     (tpe_host_fit_split), each side sorted by filtering ``order`` (a sorting
@@ -237,7 +238,9 @@ def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.
     reference's tie order), so the result equals fit_posterior's bit for bit.
     ``below_tids`` ascending, ``obs_tids`` strictly ascending; ``coord``:
     optionally the values' kernel coordinate already computed (np.log of
-    them for the log families, History.log_values)."""
+    them for the log families, History.log_values); ``addrs``: optionally the
+    host addresses (tids, coordinate, order, below_tids) of those same arrays
+    (History.native_columns), sparing the per-call pointer lookups."""
     family = _FAMILY[dist]
     if family not in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
         raise ValueError('fit_split fits continuous families only, not %r' % dist)
@@ -261,17 +264,18 @@ def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.
     if len(order) != n:
         raise ValueError('order has %d entries for %d observations' % (len(order), n))
     cap = n + 1
-    out = np.empty(6 * cap)
-    k = np.zeros(2, dtype=np.int64)
-    rc = N.load().tpe_host_fit_split(x.ctypes.data, tids.ctypes.data, order.ctypes.data, n, bt.ctypes.data,
-                                     len(bt), float(prior_weight), float(pmu), float(psig), int(lf or 0),
-                                     out.ctypes.data, k.ctypes.data)
+    out = np.empty(6 * cap + 2)                       # (+ the two component counts, as int64)
+    base = out.ctypes.data
+    if addrs is None:
+        addrs = (tids.ctypes.data, x.ctypes.data, order.ctypes.data, bt.ctypes.data)
+    rc = N.load().tpe_host_fit_split(addrs[1], addrs[0], addrs[2], n, addrs[3], len(bt), float(prior_weight),
+                                     float(pmu), float(psig), int(lf or 0), base, base + 8 * 6 * cap)
+    k = out[6 * cap:].view(np.int64)
     if rc != 0:
         raise AssertionError('tpe_host_fit_split failed (%d): tids not strictly ascending, a bad order, or a '
                              'non-positive Parzen bandwidth (prior_sigma=%r)' % (rc, psig))
     sides = []
     mask = None
-    base = out.ctypes.data
     ptrs = []
     for sd in range(2):
         m = int(k[sd])
@@ -288,11 +292,12 @@ def fit_split(dist, args, obs_tids, obs_vals, below_tids, order, prior_weight=1.
                      ptrs=tuple(ptrs) if len(ptrs) == 8 else None)      # both sides native
 
 
-def cat_split(dist, args, obs_tids, obs_vals, below_tids, prior_weight=1.0, lf=DEFAULT_LF):
+def cat_split(dist, args, obs_tids, obs_vals, below_tids, prior_weight=1.0, lf=DEFAULT_LF, addrs=None):
     """Categorical label: the below/above split and both pseudo-count
     posteriors in one native call (tpe_host_cat_split); equal to
     fit_posterior's.  ``below_tids`` ascending, ``obs_tids`` strictly
-    ascending."""
+    ascending; ``addrs``: optionally (tids, values, below_tids) host addresses
+    of those arrays (History.cat_columns)."""
     upper = int(args['upper'])
     obs = np.ascontiguousarray(obs_vals, dtype=np.int64)
     tids = np.ascontiguousarray(obs_tids, dtype=np.int64)
@@ -300,7 +305,9 @@ def cat_split(dist, args, obs_tids, obs_vals, below_tids, prior_weight=1.0, lf=D
     p = None if dist == 'randint' else np.ascontiguousarray(args['p'], dtype=np.float64)
     out = np.empty(2 * upper)
     base = out.ctypes.data
-    rc = N.load().tpe_host_cat_split(obs.ctypes.data, tids.ctypes.data, len(obs), bt.ctypes.data, len(bt), upper,
+    if addrs is None:
+        addrs = (tids.ctypes.data, obs.ctypes.data, bt.ctypes.data)
+    rc = N.load().tpe_host_cat_split(addrs[1], addrs[0], len(obs), addrs[2], len(bt), upper,
                                      p.ctypes.data if p is not None else None, float(prior_weight), int(lf or 0),
                                      base, base + 8 * upper)
     if rc != 0:

@@ -70,6 +70,7 @@ class _Fits(object):
     def _below_sorted(self):
         if self.below_sorted is None:
             self.below_sorted = np.sort(np.asarray(self.below_tids, dtype=np.int64))
+            self.below_addr = self.below_sorted.ctypes.data
         return self.below_sorted
 
     def get(self, row):
@@ -90,15 +91,20 @@ class _Fits(object):
                 pass
             elif row.categorical and self.hist.sorted_obs:
                 # split + both pseudo-count posteriors in one native call (exact)
-                post = cat_split(row.dist, row.args, otids, ovals, self._below_sorted(), self.prior_weight,
-                                 DEFAULT_LF)
+                bs = self._below_sorted()
+                cols = self.hist.cat_columns(row.label)
+                post = cat_split(row.dist, row.args, otids, ovals, bs, self.prior_weight, DEFAULT_LF,
+                                 addrs=None if cols is None else cols + (self.below_addr,))
             elif (f32 and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and self.hist.sorted_obs
                   and self.hist.value_order(row.label) is not None):
                 # fp32 device path: split + both fits in one native call
-                post = fit_split(row.dist, row.args, otids, ovals, self._below_sorted(),
-                                 self.hist.value_order(row.label), self.prior_weight, DEFAULT_LF,
-                                 coord=(self.hist.log_values(row.label) if _FAMILY[row.dist] == N.FAM_LOGGAUSS
-                                        else None))
+                logc = _FAMILY[row.dist] == N.FAM_LOGGAUSS
+                bs = self._below_sorted()
+                order = self.hist.value_order(row.label)
+                cols = self.hist.native_columns(row.label, log=logc)
+                post = fit_split(row.dist, row.args, otids, ovals, bs, order, self.prior_weight, DEFAULT_LF,
+                                 coord=self.hist.log_values(row.label) if logc else None,
+                                 addrs=None if cols is None else cols + (self.below_addr,))
             else:
                 if bidx is None:
                     bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
