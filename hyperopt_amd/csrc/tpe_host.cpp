@@ -260,6 +260,17 @@ bool strictly_ascending(const int64_t* __restrict__ tids, int64_t n) {
   return !bad;
 }
 
+// smallest of n doubles (four independent chains: vectorisable; the values
+// are positive bandwidths, so min is order-independent)
+inline double min_of(const double* __restrict__ v, int64_t n) {
+  double m[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+  int64_t i = 0;
+  for (; i + 4 <= n; i += 4)
+    for (int j = 0; j < 4; ++j) m[j] = v[i + j] < m[j] ? v[i + j] : m[j];
+  for (; i < n; ++i) m[0] = v[i] < m[0] ? v[i] : m[0];
+  return std::min(std::min(m[0], m[1]), std::min(m[2], m[3]));
+}
+
 // per-thread staging of tpe_host_pack_level, reused across calls (no
 // first-touch page faults on the large tables of a batched level)
 struct PackScratch {
@@ -495,11 +506,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     tklo[li] = klo; tkhi[li] = khi;
     if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && !f64) {
       double s0 = INFINITY, s1 = INFINITY;
-      for (int64_t i = 0; i < L.below_k; ++i) s0 = std::min(s0, L.below_sigma[i]);
+      s0 = min_of(L.below_sigma, L.below_k);
       if (dev_fit[li])           // the device fit clips every bandwidth to >= prior_sigma / min(100, 1 + K)
         s1 = L.prior_sigma / std::min(100.0, 1.0 + (double)L.above_k);
       else
-        for (int64_t i = 0; i < L.above_k; ++i) s1 = std::min(s1, L.above_sigma[i]);
+        s1 = min_of(L.above_sigma, L.above_k);
       const int64_t n0 = tab_cells(klo, khi, s0), n1 = L.above_k > 0 ? tab_cells(klo, khi, s1) : -1;
       // a cell row costs ~10x a candidate's score (two passes plus the f64
       // moments), more against the pruned, locally expanded per-candidate path
@@ -674,18 +685,35 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
               cp[i] = w[i] / (s2pi * fabs(sg[i])) * ipa;
               ap[i] = as / se;
             }
-          bool odd = false;
-          for (int64_t i = 0; i < k; ++i) odd |= !((cp[i] >= 2.2250738585072014e-308) & (cp[i] <= 1.7976931348623157e308));
+          // normal positive ratios (the rule): one branch-free pass; libm for the rest
+          int odd = 0;
+          for (int64_t i = 0; i < k; ++i) {
+            const double r = cp[i];
+            odd |= !((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308));
+            cp[i] = log2_normal(r > 0 ? r : 1.0);
+          }
           if (odd)
-            for (int64_t i = 0; i < k; ++i)
-              cp[i] = (cp[i] >= 2.2250738585072014e-308 && cp[i] <= 1.7976931348623157e308) ? log2_normal(cp[i])
-                                                                                              : log2(cp[i]);
-          else
-            for (int64_t i = 0; i < k; ++i) cp[i] = log2_normal(cp[i]);
+            for (int64_t i = 0; i < k; ++i) {
+              const double r = w[i] / (logf ? ((sg[i] > kEPS ? sg[i] : kEPS) * s2pi) : (s2pi * fabs(sg[i]))) *
+                               (logf ? 1.0 : ipa);
+              if (!((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308))) cp[i] = log2(r);
+            }
         }
-        for (int64_t i = 0; i < k; ++i) {
-          const double v = (c[i] > -INFINITY) & (c[i] < INFINITY) ? c[i] : -INFINITY;   // finite only
-          shift = v > shift ? v : shift;
+        {
+          // the largest finite c (four chains: vectorisable)
+          double m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+          const double* __restrict__ cc = c.data();
+          int64_t i = 0;
+          for (; i + 4 <= k; i += 4)
+            for (int j = 0; j < 4; ++j) {
+              const double v = (cc[i + j] > -INFINITY) & (cc[i + j] < INFINITY) ? cc[i + j] : -INFINITY;
+              m4[j] = v > m4[j] ? v : m4[j];
+            }
+          for (; i < k; ++i) {
+            const double v = (cc[i] > -INFINITY) & (cc[i] < INFINITY) ? cc[i] : -INFINITY;
+            m4[0] = v > m4[0] ? v : m4[0];
+          }
+          shift = std::max(std::max(m4[0], m4[1]), std::max(m4[2], m4[3]));
         }
         if (!std::isfinite(shift)) shift = 0;
         for (int64_t i = 0; i < k; ++i) c[i] -= shift;
