@@ -162,7 +162,7 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_VALU_GINST = 0.5 * 4 * 256 * 2.4      # = 1228.8 G wave-instructions/s
 # counter summary of the same bench command (tools/gpu.sh pmc -> tools/pmc_summary.py)
 PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r02_pmc_summary.json')
-VALU_KERNELS = ('k_sample', 'k_tables', 'k_select', 'k_above_f32', 'k_finalize')
+VALU_KERNELS = ('k_sample', 'k_tables', 'k_select', 'above', 'k_finalize')
 
 
 def _pmc():
@@ -173,7 +173,8 @@ def _pmc():
 
 
 # a profiled stage and the kernels it launches (counters are summed per dispatch)
-STAGE_KERNELS = {'k_sample': ('k_sample', 'k_sample_tab')}
+STAGE_KERNELS = {'k_sample': ('k_sample', 'k_sample_tab'),
+                 'above': ('k_above_f32', 'k_above_f64', 'k_above_q')}
 
 
 def _stage_counters(pmc, stage):
@@ -426,7 +427,9 @@ def main():
                       p50_suggest_ms=1e3 * float(np.median(lat_s)),
                       p99_suggest_ms=1e3 * float(np.percentile(lat_s, 99)))
 
-    # dominant-kernel roofline, measured live with HIP events on the engine stream
+    # dominant-kernel roofline, measured live: the level runner's own HIP events
+    # between the stages it issues, on its stream (tpe_level_profile) — stages
+    # the production flow skips (k_select under early selection) are absent
     eng = engine_mod._ENGINES[str(device)]
     eng.profile = {}
     for i in range(5):

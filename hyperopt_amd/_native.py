@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 10
+ABI_VERSION = 11
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -178,7 +178,16 @@ EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_si
            'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above', 'tpe_tables',
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
-           'tpe_replay_mixture', 'tpe_replay_categorical')
+           'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read')
+
+# tpe_level_run stages (tpe_level_profile_read order)
+STAGES = ('fit', 'k_tables', 'k_sample', 'sort', 'above', 'k_finalize', 'k_select')
+
+
+class StageProf(ctypes.Structure):
+    """tpe_stage_prof: one stage of the last profiled tpe_level_run."""
+    _fields_ = [('ms', ctypes.c_double), ('units', ctypes.c_double), ('ce', ctypes.c_double),
+                ('launches', ctypes.c_int32), ('reserved', ctypes.c_int32)]
 
 
 class MTState(ctypes.Structure):
@@ -244,6 +253,10 @@ def load(path=LIB_PATH):
                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(LevelWS),
                                   ctypes.POINTER(LevelNeed), P, P]
     lib.tpe_level_run.restype = ctypes.c_int
+    lib.tpe_level_profile.argtypes = [ctypes.c_int32]
+    lib.tpe_level_profile.restype = ctypes.c_int
+    lib.tpe_level_profile_read.argtypes = [ctypes.POINTER(StageProf), ctypes.c_int32]
+    lib.tpe_level_profile_read.restype = ctypes.c_int
     if lib.tpe_abi_version() != ABI_VERSION:
         raise NativeUnavailable('ABI mismatch: library %d, bindings %d' % (lib.tpe_abi_version(), ABI_VERSION))
     _LIB = lib

@@ -62,6 +62,15 @@ int fail(int code, const char* what) {
   return code;
 }
 
+// kernel launches issued by this thread (the stage profiler tells launched
+// stages from skipped ones by it)
+thread_local int64_t g_launches = 0;
+#define TPE_LAUNCH(...)     \
+  do {                      \
+    ++g_launches;           \
+    hipLaunchKernelGGL(__VA_ARGS__); \
+  } while (0)
+
 int hip_check(const char* stage) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -2520,11 +2529,11 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   // every job's below list fits the gather kernel's LDS copy (host-checked sizes)
   const int gx = (int)std::min<int64_t>(4096, std::max<int64_t>(1, (b->fit_total / b->n_fit + kFitGatherBlock - 1) /
                                                                          kFitGatherBlock));
-  hipLaunchKernelGGL(k_fit_gather, dim3(gx, b->n_fit), dim3(kFitGatherBlock), 0, s, b->fit, b->below_idx,
+  TPE_LAUNCH(k_fit_gather, dim3(gx, b->n_fit), dim3(kFitGatherBlock), 0, s, b->fit, b->below_idx,
                      b->fit_keys, b->fit_vals);
   if ((rc = hip_check("tpe_fit_above/gather"))) return rc;
   if (b->fit_max_seg <= kFitSortMax) {
-    hipLaunchKernelGGL(k_fit_sort_lds, dim3(b->n_fit), dim3(kFitSortThreads), 0, s, b->fit_seg, b->fit_keys,
+    TPE_LAUNCH(k_fit_sort_lds, dim3(b->n_fit), dim3(kFitSortThreads), 0, s, b->fit_seg, b->fit_keys,
                        b->fit_vals, b->fit_keys_sorted, b->fit_vals_sorted);
     if ((rc = hip_check("tpe_fit_above/sort"))) return rc;
   } else {
@@ -2537,8 +2546,9 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
       snprintf(g_err, sizeof(g_err), "tpe_fit_above/sort: %s", hipGetErrorString(e));
       return TPE_E_HIP;
     }
+    ++g_launches;
   }
-  hipLaunchKernelGGL(k_fit_build, dim3(b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
+  TPE_LAUNCH(k_fit_build, dim3(b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
                      b->fit_vals_sorted, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32,
                      const_cast<int32_t*>(b->grid));
   return hip_check("tpe_fit_above/build");
@@ -2548,10 +2558,8 @@ int tpe_tables(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
-  const char* twice = getenv("TPE_DEBUG_TABLES_TWICE");      // (timing experiments: a warm second launch)
   const int extra = b->early_select ? b->n_problems : 0;
-  for (int r = 0; r < (twice && twice[0] == '1' ? 2 : 1); ++r)
-    hipLaunchKernelGGL(k_tables, dim3(b->tab_blocks + extra), dim3(kTabTblThreads), 0, (hipStream_t)stream,
+  TPE_LAUNCH(k_tables, dim3(b->tab_blocks + extra), dim3(kTabTblThreads), 0, (hipStream_t)stream,
                        b->problems, b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64,
                        b->grid, (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0, b->tab_blocks, b->samp,
                        lazy_ok(b) ? 1 : 0, b->result);
@@ -2567,9 +2575,9 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (od) {
     const int64_t per = (b->draw_blocks + kThreads / 64 - 1) / (kThreads / 64);
     if ((int64_t)b->n_problems * per >= ((int64_t)1 << 31)) return fail(TPE_E_ARG, "ordered-draw grid too large");
-    hipLaunchKernelGGL(k_draw_sums, dim3((unsigned)(b->n_problems * per)), dim3(kThreads), 0, (hipStream_t)stream,
+    TPE_LAUNCH(k_draw_sums, dim3((unsigned)(b->n_problems * per)), dim3(kThreads), 0, (hipStream_t)stream,
                        b->problems, b->draw_blocks, b->draw_pref);
-    hipLaunchKernelGGL(k_draw_scan, dim3(b->n_problems), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
+    TPE_LAUNCH(k_draw_scan, dim3(b->n_problems), dim3(kThreads), 0, (hipStream_t)stream, b->problems,
                        b->draw_blocks, b->draw_pref);
     if ((rc = hip_check("tpe_sample/prefix"))) return rc;
   }
@@ -2580,7 +2588,7 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   const int n_gen = b->samp_tiles ? (lazy ? b->n_samp_eager : b->n_samp_tiles) : b->n_tiles;
   const int n_tab = b->tab_tiles ? b->n_tab_tiles : (b->n_tab_jobs > 0 ? b->n_tiles : 0);
   if (n_gen > 0)
-    hipLaunchKernelGGL(k_sample, dim3(n_gen, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
+    TPE_LAUNCH(k_sample, dim3(n_gen, TPE_BEST_PER_TILE), dim3(kThreads), 0, (hipStream_t)stream,
                        b->problems, b->tiles, b->samp, (const double4*)b->comp64, b->cand, b->coord, b->keys, b->vals,
                        b->vals_sorted, b->tile_best, b->l_out, b->g_out, b->precision, b->sample, b->key_bits,
                        b->flags, b->draw_pref, b->draw_blocks, od ? 1 : 0, b->pool_best,
@@ -2592,12 +2600,12 @@ int tpe_sample(const tpe_batch* b, void* stream) {
     const int wgs = (n_tab + per - 1) / per;
     tpe_result* run_best = b->early_select ? b->run_best : nullptr;
     if (b->precision == TPE_PREC_F64)
-      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F64>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
+      TPE_LAUNCH(k_sample_tab<TPE_PREC_F64>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
                          run_best);
     else
-      hipLaunchKernelGGL(k_sample_tab<TPE_PREC_F32>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
+      TPE_LAUNCH(k_sample_tab<TPE_PREC_F32>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
                          run_best);
@@ -2620,6 +2628,7 @@ int tpe_sort(const tpe_batch* b, void* stream) {
              (unsigned long long)b->sort_tmp_bytes);
     return TPE_E_HIP;
   }
+  ++g_launches;
   return hip_check("tpe_sort");
 }
 
@@ -2630,18 +2639,18 @@ int tpe_score_above(const tpe_batch* b, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n_cont) {
     if (b->precision == TPE_PREC_F32)
-      hipLaunchKernelGGL(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
+      TPE_LAUNCH(k_above_f32, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
                          (const float4*)b->comp32, b->grid, b->vals_sorted, b->part, b->tile_best,
                          b->l_out, b->g_out, b->ce_count, b->flags, b->sample, b->pool_best);
     else
-      hipLaunchKernelGGL(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
+      TPE_LAUNCH(k_above_f64, dim3(n_cont), dim3(kThreads), 0, s, b->problems, b->tiles, b->work,
                          (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   }
   if (n_qg)
-    hipLaunchKernelGGL((k_above_q<false>), dim3(n_qg), dim3(kThreads), 0, s, b->problems, b->tiles, b->work + n_cont,
+    TPE_LAUNCH((k_above_q<false>), dim3(n_qg), dim3(kThreads), 0, s, b->problems, b->tiles, b->work + n_cont,
                        (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   if (n_ql)
-    hipLaunchKernelGGL((k_above_q<true>), dim3(n_ql), dim3(kThreads), 0, s, b->problems, b->tiles,
+    TPE_LAUNCH((k_above_q<true>), dim3(n_ql), dim3(kThreads), 0, s, b->problems, b->tiles,
                        b->work + n_cont + n_qg,
                        (const double4*)b->comp64, b->cand, b->vals_sorted, b->part);
   return hip_check("tpe_score_above");
@@ -2656,7 +2665,7 @@ int tpe_finalize(const tpe_batch* b, void* stream) {
   const bool listed = b->fin_tiles && b->sample && !(b->flags & TPE_BATCH_NO_FUSE);
   const int n_fin = listed ? b->n_fin_tiles : b->n_tiles;
   if (n_fin == 0) return TPE_OK;
-  hipLaunchKernelGGL(k_finalize, dim3(n_fin, TPE_BEST_PER_TILE), dim3(kThreads), 0,
+  TPE_LAUNCH(k_finalize, dim3(n_fin, TPE_BEST_PER_TILE), dim3(kThreads), 0,
                      (hipStream_t)stream, b->problems, b->tiles, listed ? b->fin_tiles : nullptr,
                      (const float4*)b->comp32, (const double4*)b->comp64, b->grid, b->cand, b->vals_sorted,
                      b->part, b->l_out, b->g_out, b->tile_best, b->precision, b->sample, b->flags, b->pool_best);
@@ -2667,7 +2676,7 @@ int tpe_select(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_problems == 0 || (b->early_select && b->n_late == 0)) return TPE_OK;
-  hipLaunchKernelGGL(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
+  TPE_LAUNCH(k_select, dim3(b->n_problems), dim3(kSelThreads), 0, (hipStream_t)stream, b->problems,
                      b->tile_best, b->cand, b->samp, b->precision, b->sample, b->draw_pref, b->draw_blocks,
                      ordered_draws(b) ? 1 : 0, b->pool_best, (const float4*)b->comp32, (const double4*)b->comp64,
                      lazy_ok(b) ? 1 : 0, b->early_select ? 1 : 0, b->result);
@@ -2684,6 +2693,82 @@ int tpe_run_batch(const tpe_batch* b, void* stream) {
   if ((rc = tpe_score_above(b, stream))) return rc;
   if ((rc = tpe_finalize(b, stream))) return rc;
   return tpe_select(b, stream);
+}
+
+// ---------------------------------------------------------------- stage profiler
+// HIP events between the stages tpe_level_run issues, on its stream; read after
+// the runner's own stream synchronise (include/tpe_hip.h)
+static struct {
+  int on;
+  int valid;
+  hipEvent_t ev[TPE_N_STAGES + 1];
+  tpe_stage_prof last[TPE_N_STAGES];
+} g_prof;
+
+int tpe_level_profile(int32_t enable) {
+  if (enable && !g_prof.ev[0]) {
+    for (int i = 0; i <= TPE_N_STAGES; ++i) {
+      hipError_t e = hipEventCreate(&g_prof.ev[i]);
+      if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    }
+  }
+  g_prof.on = enable ? 1 : 0;
+  if (enable) g_prof.valid = 0;         // (disabling keeps the last run readable)
+  return TPE_OK;
+}
+
+int tpe_level_profile_read(tpe_stage_prof* out, int32_t n) {
+  if (!out || n < 0) return fail(TPE_E_ARG, "tpe_level_profile_read: null output");
+  if (!g_prof.valid) return fail(TPE_E_ARG, "tpe_level_profile_read: no profiled level run");
+  memcpy(out, g_prof.last, sizeof(tpe_stage_prof) * (size_t)std::min<int32_t>(n, TPE_N_STAGES));
+  return TPE_OK;
+}
+
+// tpe_run_batch's stages, each followed by an event
+static int run_batch_profiled(const tpe_batch* b, void* stream) {
+  typedef int (*stage_fn)(const tpe_batch*, void*);
+  static const stage_fn fns[TPE_N_STAGES] = {tpe_fit_above, tpe_tables, tpe_sample, tpe_sort,
+                                             tpe_score_above, tpe_finalize, tpe_select};
+  hipStream_t s = (hipStream_t)stream;
+  if (hipEventRecord(g_prof.ev[0], s) != hipSuccess) return hip_check("tpe_level_profile");
+  for (int i = 0; i < TPE_N_STAGES; ++i) {
+    const int64_t n0 = g_launches;
+    int rc = fns[i](b, stream);
+    if (rc) return rc;
+    g_prof.last[i].launches = (int32_t)(g_launches - n0);
+    if (hipEventRecord(g_prof.ev[i + 1], s) != hipSuccess) return hip_check("tpe_level_profile");
+  }
+  return TPE_OK;
+}
+
+// after the stream synchronise: event times and each stage's work
+static int profile_collect(const tpe_batch& b, const tpe_pack_info& info, const tpe_problem* hp, int64_t n_cand) {
+  const int64_t P = info.n_problems;
+  double ce_tab = 0, ce_above = 0;
+  for (int64_t r = 0; r < P; ++r) {
+    if (hp[r].tab_mode != TPE_TAB_NONE)
+      ce_tab += (double)(hp[r].below_len + hp[r].above_len) * (double)n_cand;
+    else if (hp[r].family != TPE_FAM_CATEGORICAL)
+      ce_above += (double)hp[r].above_len * (double)n_cand;
+  }
+  const double C = (double)P * (double)n_cand;
+  const double units[TPE_N_STAGES] = {
+      (double)info.fit_total, (double)info.tab_units, C,
+      (double)((b.sort_end_bit + 7) / 8) * 2.0 * 12.0 * (double)b.sort_count, ce_above, C, (double)P};
+  for (int i = 0; i < TPE_N_STAGES; ++i) {
+    tpe_stage_prof& q = g_prof.last[i];
+    float ms = 0.f;
+    if (q.launches > 0) {
+      hipError_t e = hipEventElapsedTime(&ms, g_prof.ev[i], g_prof.ev[i + 1]);
+      if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    }
+    q.ms = ms;
+    q.units = units[i];
+    q.ce = i == TPE_STAGE_SAMPLE ? ce_tab : (i == TPE_STAGE_ABOVE ? ce_above : 0.0);
+    q.reserved = 0;
+  }
+  g_prof.valid = 1;
+  return TPE_OK;
 }
 
 int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
@@ -2829,7 +2914,12 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.fit_tmp = ws->fit_tmp; b.fit_tmp_bytes = (uint64_t)ws->fit_tmp_bytes;
     b.fit_max_seg = info.fit_max_seg;
   }
-  if ((rc = tpe_run_batch(&b, stream))) return rc;
+  if (g_prof.on) {
+    g_prof.valid = 0;
+    if ((rc = check_batch(&b)) || (rc = run_batch_profiled(&b, stream))) return rc;
+  } else if ((rc = tpe_run_batch(&b, stream))) {
+    return rc;
+  }
   e = rd ? hipSuccess : hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
@@ -2851,7 +2941,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     }
   }
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));
-  return TPE_OK;
+  return g_prof.on ? profile_collect(b, info, hp, n_cand) : TPE_OK;
 }
 
 }  // extern "C"

@@ -571,8 +571,6 @@ class Engine(object):
         n_cand = int(n_cand)
         if n_cand < 0 or n_cand >= 2 ** 31:
             raise ValueError('n_EI_candidates out of range: %r' % n_cand)
-        if self.profile is not None:
-            return self.run(problems, n_cand, seed, cand_base=cand_base, n_cand_global=n_cand_global)
         labels, keep = self._labels(problems)
         P = sum(len(lp.ids) for lp in problems)
         out = np.empty(P, dtype=N.RESULT_DTYPE)
@@ -581,6 +579,9 @@ class Engine(object):
         seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
         ncg = int(n_cand_global) if n_cand_global is not None else 0
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        prof = self.profile is not None
+        if prof:
+            N.check(self.lib.tpe_level_profile(1), self.lib, 'tpe_level_profile')
         for attempt in range(3):
             ws = self._level_ws()
             rc = self.lib.tpe_level_run(labels, len(problems), n_cand, seed64, int(cand_base), ncg, prec,
@@ -589,9 +590,23 @@ class Engine(object):
             if rc != N.E_SPACE:
                 break
             self._grow(need)
+        if prof:
+            self.lib.tpe_level_profile(0)
         N.check(rc, self.lib, 'tpe_level_run')
         del keep
+        if prof and P:
+            self._record_level_profile()
         return out
+
+    def _record_level_profile(self):
+        """profile[stage] gets (ms, units, algorithmic CE) of every stage the
+        last tpe_level_run launched, timed by the runner's own HIP events on
+        its stream (tpe_level_profile): the production flow, stage by stage."""
+        recs = (N.StageProf * len(N.STAGES))()
+        N.check(self.lib.tpe_level_profile_read(recs, len(N.STAGES)), self.lib, 'tpe_level_profile_read')
+        for name, r in zip(N.STAGES, recs):
+            if r.launches:
+                self.profile.setdefault(name, []).append((float(r.ms), float(r.units), float(r.ce)))
 
     # ---------------------------------------------------------------- run
     def run(self, problems, n_cand, seed, cand_base=0, want_lg=False, return_cand=False, n_cand_global=None):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 10
+#define TPE_ABI_VERSION 11
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -541,6 +541,43 @@ typedef struct tpe_level_need {
 int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
                   int64_t n_cand_global, int32_t precision, int32_t flags, const tpe_level_ws* ws,
                   tpe_level_need* need, void* stream, tpe_result* out);
+
+/* ------------------------------------------------------------------------
+ * Stage profiler of tpe_level_run (bench.py's live roofline).  While enabled,
+ * the runner brackets each stage it calls with HIP events on its own stream and,
+ * after its stream synchronise, keeps the per-stage device times of that run.
+ * The stages are timed exactly as the production flow issues them: a stage
+ * that launches nothing (no fits, no sort, early selection leaving no late
+ * problems for the select stage) reports launches = 0 and ms = 0.
+ * Process-wide setting; not meant for concurrent runners.
+ * ---------------------------------------------------------------------- */
+#define TPE_STAGE_FIT      0
+#define TPE_STAGE_TABLES   1
+#define TPE_STAGE_SAMPLE   2
+#define TPE_STAGE_SORT     3
+#define TPE_STAGE_ABOVE    4
+#define TPE_STAGE_FINALIZE 5
+#define TPE_STAGE_SELECT   6
+#define TPE_N_STAGES       7
+
+typedef struct tpe_stage_prof {
+  double ms;         /* device time between the stage's bracketing events         */
+  double units;      /* stage work: fit observations | table units (16 B) |
+                        candidates | sort bytes (8-bit LSD passes x 2 x 12 B x keys) |
+                        above CE | candidates | problems                            */
+  double ce;         /* algorithmic component evaluations the stage stands in for:
+                        sample = tabulated problems' (K_below + K_above) x C,
+                        above = scored problems' K_above x C; else 0                */
+  int32_t launches;  /* kernels (and library sorts) the stage launched             */
+  int32_t reserved;
+} tpe_stage_prof;
+
+/* enable (1) / disable (0) the profiler; creates its events on first use */
+int tpe_level_profile(int32_t enable);
+
+/* the last profiled tpe_level_run: min(n, TPE_N_STAGES) records in stage
+ * order; TPE_E_ARG if no run completed since the profiler was enabled */
+int tpe_level_profile_read(tpe_stage_prof* out, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -103,7 +103,8 @@ def test_engine_refuses_without_device():
 
 
 CTYPES_MIRRORS = (('tpe_batch', N.Batch), ('tpe_label_in', N.LabelIn), ('tpe_pack_info', N.PackInfo),
-                  ('tpe_level_ws', N.LevelWS), ('tpe_level_need', N.LevelNeed))
+                  ('tpe_level_ws', N.LevelWS), ('tpe_level_need', N.LevelNeed), ('tpe_mt_state', N.MTState),
+                  ('tpe_stage_prof', N.StageProf))
 
 
 def test_ctypes_mirrors_match_c():

@@ -162,6 +162,19 @@ def test_config3_suggest_full_size(branch):
                        'config3/%s %s' % (branch, label))
     again = tpe.suggest([new_id], domain, trials, seed, n_EI_candidates=C)[0]
     assert again['misc']['vals'] == doc['misc']['vals']                      # deterministic
+    # the stage profiler (bench.py's roofline) times the production flow and
+    # changes nothing: tables + tabulated sampling with early selection, no
+    # select stage
+    eng.profile = {}
+    try:
+        prof_doc = tpe.suggest([new_id], domain, trials, seed, n_EI_candidates=C)[0]
+        prof = eng.profile
+    finally:
+        eng.profile = None
+    assert prof_doc['misc']['vals'] == doc['misc']['vals']
+    assert 'k_tables' in prof and 'k_sample' in prof and 'k_select' not in prof, sorted(prof)
+    ms, units, ce = prof['k_sample'][0]
+    assert ms > 0 and units == len(vals) * C and ce > 0, prof['k_sample']
 
 
 # ----------------------------------------------------------------- config 4
