@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 11
+ABI_VERSION = 12
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -173,12 +173,37 @@ class LevelNeed(ctypes.Structure):
 
 
 E_SPACE = -4
+E_FALLBACK = -5          # tpe_suggest_tree: the space / history needs the general (host) path
+TREE_MAX_PARENTS = 4
+TREE_NO_SPECULATE = 1 << 8
+
+
+class TreeLabel(ctypes.Structure):
+    """tpe_tree_label: one hyperparameter of a tree space (tpe_suggest_tree)."""
+    _fields_ = [
+        ('family', ctypes.c_int32), ('flags', ctypes.c_int32), ('upper', ctypes.c_int32),
+        ('label_ix', ctypes.c_int32),
+        ('low', ctypes.c_double), ('high', ctypes.c_double), ('prior_mu', ctypes.c_double),
+        ('prior_sigma', ctypes.c_double),
+        ('p_prior', ctypes.c_void_p), ('tids', ctypes.c_void_p), ('values', ctypes.c_void_p),
+        ('order', ctypes.c_void_p), ('n_obs', ctypes.c_int64),
+        ('depth', ctypes.c_int32), ('n_parents', ctypes.c_int32),
+        ('parent', ctypes.c_int32 * TREE_MAX_PARENTS), ('parent_cat', ctypes.c_int32 * TREE_MAX_PARENTS),
+    ]
+
+
+TREE_LABEL_DTYPE = np.dtype(dict(
+    names=[f for f, _ in TreeLabel._fields_],
+    formats=['<i4', '<i4', '<i4', '<i4', '<f8', '<f8', '<f8', '<f8', '<u8', '<u8', '<u8', '<u8', '<i8', '<i4', '<i4',
+             ('<i4', (TREE_MAX_PARENTS,)), ('<i4', (TREE_MAX_PARENTS,))],
+    offsets=[getattr(TreeLabel, f).offset for f, _ in TreeLabel._fields_], itemsize=ctypes.sizeof(TreeLabel)))
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
            'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above', 'tpe_tables',
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
-           'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read')
+           'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read',
+           'tpe_suggest_tree')
 
 # tpe_level_run stages (tpe_level_profile_read order)
 STAGES = ('fit', 'k_tables', 'k_sample', 'sort', 'above', 'k_finalize', 'k_select')
@@ -253,6 +278,10 @@ def load(path=LIB_PATH):
                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(LevelWS),
                                   ctypes.POINTER(LevelNeed), P, P]
     lib.tpe_level_run.restype = ctypes.c_int
+    I32 = ctypes.c_int32
+    lib.tpe_suggest_tree.argtypes = [P, I32, P, I64, D, I32, P, I32, I32, ctypes.c_uint64, D, I64, I32,
+                                     ctypes.POINTER(LevelWS), ctypes.POINTER(LevelNeed), P, P, P, P]
+    lib.tpe_suggest_tree.restype = ctypes.c_int
     lib.tpe_level_profile.argtypes = [ctypes.c_int32]
     lib.tpe_level_profile.restype = ctypes.c_int
     lib.tpe_level_profile_read.argtypes = [ctypes.POINTER(StageProf), ctypes.c_int32]

@@ -2484,6 +2484,9 @@ extern "C" {
 
 int tpe_abi_version(void) { return TPE_ABI_VERSION; }
 
+// error hand-off for the library's other host translation units (tpe_suggest.cpp)
+__attribute__((visibility("hidden"))) int tpe_internal_fail(int code, const char* what) { return fail(code, what); }
+
 const char* tpe_last_error(void) { return g_err; }
 
 int tpe_device_count(int* n) {

@@ -1,0 +1,304 @@
+// tpe_suggest.cpp — one native call per tpe.suggest of a conditional tree space
+// (include/tpe_hip.h, tpe_suggest_tree).
+//
+// The reference interprets a pyll posterior graph per suggest (tpe.py:804-897):
+// for every hyperparameter it splits the history into below/above
+// (ap_filter_trials, tpe.py:613-641), fits both Parzen estimators
+// (adaptive_parzen_normal tpe.py:398-475, categorical posteriors tpe.py:573-607),
+// and evaluates the conditional tree lazily (switch nodes, vectorize.py:19-37,
+// pyll/base.py:762-781) so that only the active branch is sampled and scored.
+// Here the host side of that is one C++ call: fits of the labels the tree
+// needs (tpe_host_fit_split / tpe_host_cat_split), the gate prediction of the
+// speculative level fusion, and the level runs (tpe_level_run) — the same
+// decisions hyperopt_amd.tpe._choices_fused / _choices_philox make, without a
+// Python round trip per label.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/tpe_hip.h"
+
+extern "C" int tpe_internal_fail(int code, const char* what);   // tpe_kernels.hip (hidden)
+
+namespace {
+
+constexpr int kInactive = -2;   // label not active (None)
+constexpr int kActive = -1;     // active label that gates nothing (placeholder)
+
+// fitted posterior of one label: continuous (w, mu, sigma) per side or the
+// categorical probabilities (mu / sigma null)
+struct Fit {
+  bool done = false;
+  std::vector<double> buf;
+  int64_t k[2] = {0, 0};
+  const double* w[2] = {nullptr, nullptr};
+  const double* mu[2] = {nullptr, nullptr};
+  const double* sg[2] = {nullptr, nullptr};
+};
+
+struct Tree {
+  const tpe_tree_label* L;
+  int32_t n;
+  const int64_t* below;
+  int64_t n_below;
+  double prior_weight;
+  int32_t lf;
+  int64_t device_fit_min;
+  std::vector<Fit>* fits;
+  std::vector<char> gate;       // label gates another label
+  int32_t max_depth;
+};
+
+int fit_label(Tree& T, int i) {
+  Fit& f = (*T.fits)[(size_t)i];
+  if (f.done) return TPE_OK;
+  const tpe_tree_label& L = T.L[i];
+  const int64_t n = L.n_obs;
+  if (n < 0 || (n > 0 && (!L.tids || !L.values))) return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad columns");
+  if (L.family == TPE_FAM_CATEGORICAL) {
+    if (L.upper <= 0) return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: categorical label without categories");
+    f.buf.resize(2 * (size_t)L.upper);
+    const int rc = tpe_host_cat_split((const int64_t*)L.values, L.tids, n, T.below, T.n_below, L.upper, L.p_prior,
+                                      T.prior_weight, T.lf, f.buf.data(), f.buf.data() + L.upper);
+    if (rc != TPE_OK)
+      return tpe_internal_fail(TPE_E_ARG, "categorical observation out of range or tids not ascending");
+    f.k[0] = f.k[1] = L.upper;
+    f.w[0] = f.buf.data();
+    f.w[1] = f.buf.data() + L.upper;
+    f.mu[0] = f.mu[1] = f.sg[0] = f.sg[1] = nullptr;
+  } else if (L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) {
+    if (n > 0 && !L.order) return TPE_E_FALLBACK;                              // a NaN value
+    if (T.device_fit_min > 0 && n >= std::max<int64_t>(T.device_fit_min, 64)) return TPE_E_FALLBACK;
+    const size_t cap = (size_t)n + 1;
+    f.buf.resize(6 * cap);
+    const int rc = tpe_host_fit_split((const double*)L.values, L.tids, L.order, n, T.below, T.n_below, T.prior_weight,
+                                      L.prior_mu, L.prior_sigma, T.lf, f.buf.data(), f.k);
+    if (rc != TPE_OK)
+      return tpe_internal_fail(TPE_E_ARG, "tpe_host_fit_split failed: tids not strictly ascending, a bad order, or a "
+                                          "non-positive Parzen bandwidth");
+    if (f.k[0] == 0 || f.k[1] == 0) return TPE_E_FALLBACK;                     // repeated values: numpy's tie order
+    for (int sd = 0; sd < 2; ++sd) {
+      double* b = f.buf.data() + 3 * (size_t)sd * cap;
+      f.w[sd] = b;
+      f.mu[sd] = b + cap;
+      f.sg[sd] = b + 2 * cap;
+    }
+  } else {
+    return TPE_E_FALLBACK;                                                     // quantized: numpy's tie order
+  }
+  f.done = true;
+  return TPE_OK;
+}
+
+// ParamTable.active: some parent chose this label's option (`chosen`: the
+// per-label codes of one id — a category, kActive or kInactive)
+bool is_active(const tpe_tree_label& L, const int* chosen) {
+  if (L.n_parents == 0) return true;
+  for (int j = 0; j < L.n_parents; ++j) {
+    const int c = chosen[L.parent[j]];
+    if (c >= 0 && c == L.parent_cat[j]) return true;
+  }
+  return false;
+}
+
+// hyperopt_amd.tpe._predict_activity: per label kInactive / kActive / the
+// predicted category of a gate; false when some gate cannot be predicted.  A
+// gate's candidates all score log pb[c] - log pa[c] (categorical_lpdf,
+// tpe.py:50-57), so its argmax (broadcast_best, tpe.py:749-759) is the best
+// drawable category unless it goes undrawn among the C draws.
+int predict(Tree& T, int64_t n_cand, double min_draws, std::vector<int>& pred, bool& ok) {
+  ok = false;
+  pred.assign((size_t)T.n, kInactive);
+  for (int d = 0; d <= T.max_depth; ++d) {
+    for (int i = 0; i < T.n; ++i) {
+      const tpe_tree_label& L = T.L[i];
+      if (L.depth != d) continue;
+      if (!is_active(L, pred.data())) { pred[(size_t)i] = kInactive; continue; }
+      if (!T.gate[(size_t)i]) { pred[(size_t)i] = kActive; continue; }
+      if (L.family != TPE_FAM_CATEGORICAL) return TPE_OK;
+      const int rc = fit_label(T, i);
+      if (rc != TPE_OK) return rc;
+      const Fit& f = (*T.fits)[(size_t)i];
+      const double* pb = f.w[0];
+      const double* pa = f.w[1];
+      double tot = 0.0;
+      for (int k = 0; k < L.upper; ++k) tot += pb[k];
+      if (!(tot > 0)) return TPE_OK;
+      int c = -1;
+      double best = 0.0;
+      for (int k = 0; k < L.upper; ++k) {
+        if (!(pb[k] > 0)) continue;
+        const double sc = pa[k] > 0 ? std::log(pb[k]) - std::log(pa[k]) : INFINITY;
+        // np.argmax: the first maximum, a NaN beats everything
+        if (c < 0 || sc > best || (sc != sc && best == best)) { c = k; best = sc; }
+      }
+      if (c < 0 || (double)n_cand * pb[c] / tot < min_draws) return TPE_OK;
+      pred[(size_t)i] = c;
+    }
+  }
+  ok = true;
+  return TPE_OK;
+}
+
+// one level's label record (tpe_label_in) from a fit
+void label_rec(const tpe_tree_label& L, const Fit& f, const int64_t* ids, int64_t n_ids, tpe_label_in& r) {
+  memset(&r, 0, sizeof(r));
+  r.family = L.family;
+  r.flags = L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH);
+  r.upper = L.upper;
+  r.label_ix = L.label_ix;
+  r.low = L.low;
+  r.high = L.high;
+  r.below_w = f.w[0]; r.below_mu = f.mu[0]; r.below_sigma = f.sg[0]; r.below_k = f.k[0];
+  r.above_w = f.w[1]; r.above_mu = f.mu[1]; r.above_sigma = f.sg[1]; r.above_k = f.k[1];
+  r.ids = ids;
+  r.n_ids = n_ids;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
+                     double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
+                     uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
+                     const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
+                     int32_t* path) {
+  if (n_labels < 0 || n_ids < 0 || n_cand < 0 || n_below < 0 || (n_labels > 0 && !labels) || (n_ids > 0 && !ids) ||
+      (n_below > 0 && !below_tids) || !ws || !need || !path || (n_labels > 0 && n_ids > 0 && (!values || !active)))
+    return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad arguments");
+  path[0] = path[1] = 0;
+  static thread_local std::vector<Fit> fits_tl;
+  static thread_local std::vector<tpe_label_in> recs_tl;
+  static thread_local std::vector<tpe_result> res_tl;
+  static thread_local std::vector<int64_t> ids_tl;
+  static thread_local std::vector<int> chosen_tl, pred_tl;
+  std::vector<Fit>& fits = fits_tl;
+  if (fits.size() < (size_t)n_labels) fits.resize((size_t)n_labels);
+  for (int i = 0; i < n_labels; ++i) fits[(size_t)i].done = false;
+  Tree T{labels, n_labels, below_tids, n_below, prior_weight, lf, device_fit_min, &fits, {}, 0};
+  T.gate.assign((size_t)n_labels, 0);
+  for (int i = 0; i < n_labels; ++i) {
+    const tpe_tree_label& L = labels[i];
+    if (L.n_parents < 0 || L.n_parents > TPE_TREE_MAX_PARENTS || L.depth < 0 || L.label_ix != i)
+      return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad label record");
+    for (int j = 0; j < L.n_parents; ++j) {
+      if (L.parent[j] < 0 || L.parent[j] >= n_labels || labels[L.parent[j]].depth >= L.depth)
+        return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: a parent must be a label of a lower level");
+      T.gate[(size_t)L.parent[j]] = 1;
+    }
+    T.max_depth = std::max(T.max_depth, L.depth);
+  }
+  for (int i = 0; i < n_labels; ++i)
+    if (T.gate[(size_t)i] && labels[i].family != TPE_FAM_CATEGORICAL) return TPE_E_FALLBACK;
+  if (n_labels == 0 || n_ids == 0) return TPE_OK;
+  const int32_t run_flags = flags & ~TPE_TREE_NO_SPECULATE;
+  std::vector<tpe_label_in>& recs = recs_tl;
+  std::vector<tpe_result>& res = res_tl;
+  auto run = [&](int32_t n_recs) -> int {
+    int64_t P = 0;
+    for (int32_t r = 0; r < n_recs; ++r) P += recs[(size_t)r].n_ids;
+    res.resize((size_t)std::max<int64_t>(P, 1));
+    ++path[1];
+    return tpe_level_run(recs.data(), n_recs, n_cand, seed, 0, 0, TPE_PREC_F32, run_flags, ws, need, stream,
+                         res.data());
+  };
+
+  // speculative fusion (hyperopt_amd.tpe._choices_fused): every level in one
+  // batch under the predicted activity, verified on the gates' results
+  if (!(flags & TPE_TREE_NO_SPECULATE) && speculate_min_draws >= 0 && T.max_depth > 0) {
+    bool ok = false;
+    std::vector<int>& pred = pred_tl;
+    int rc = predict(T, n_cand, speculate_min_draws, pred, ok);
+    if (rc != TPE_OK) return rc;
+    if (ok) {
+      recs.resize((size_t)n_labels);
+      int32_t nr = 0;
+      for (int i = 0; i < n_labels; ++i) {
+        if (pred[(size_t)i] == kInactive) continue;
+        if ((rc = fit_label(T, i)) != TPE_OK) return rc;
+        label_rec(labels[i], fits[(size_t)i], ids, n_ids, recs[(size_t)nr++]);
+      }
+      if ((rc = run(nr)) != TPE_OK) return rc;
+      bool verified = true;
+      int32_t r = 0;
+      for (int i = 0; i < n_labels && verified; ++i) {
+        if (pred[(size_t)i] == kInactive) continue;
+        for (int j = 0; j < n_ids; ++j) {
+          const tpe_result& q = res[(size_t)r * n_ids + j];
+          if (q.idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
+          if (pred[(size_t)i] >= 0 && (int64_t)q.value != pred[(size_t)i]) verified = false;
+        }
+        ++r;
+      }
+      if (verified) {
+        r = 0;
+        for (int i = 0; i < n_labels; ++i) {
+          const bool on = pred[(size_t)i] != kInactive;
+          for (int j = 0; j < n_ids; ++j) {
+            values[(size_t)j * n_labels + i] = on ? res[(size_t)r * n_ids + j].value : NAN;
+            active[(size_t)j * n_labels + i] = on ? 1 : 0;
+          }
+          r += on;
+        }
+        path[0] = 1;
+        return TPE_OK;
+      }
+    }
+  }
+
+  // level by level (hyperopt_amd.tpe._choices_philox)
+  std::vector<int>& chosen = chosen_tl;
+  chosen.assign((size_t)n_ids * n_labels, kInactive);
+  for (size_t q = 0; q < (size_t)n_ids * n_labels; ++q) { values[q] = NAN; active[q] = 0; }
+  std::vector<int64_t>& lvl_ids = ids_tl;
+  for (int d = 0; d <= T.max_depth; ++d) {
+    recs.clear();
+    lvl_ids.clear();
+    std::vector<std::pair<int, int64_t>> members;   // (label, first position in lvl_ids)
+    for (int i = 0; i < n_labels; ++i) {
+      const tpe_tree_label& L = labels[i];
+      if (L.depth != d) continue;
+      const int64_t first = (int64_t)lvl_ids.size();
+      for (int j = 0; j < n_ids; ++j)
+        if (is_active(L, chosen.data() + (size_t)j * n_labels)) lvl_ids.push_back(j);
+      if ((int64_t)lvl_ids.size() == first) continue;
+      const int rc = fit_label(T, i);
+      if (rc != TPE_OK) return rc;
+      members.emplace_back(i, first);
+    }
+    if (members.empty()) continue;
+    // the level's id arrays (positions -> new ids), stable now that lvl_ids is complete
+    std::vector<int64_t> lvl_new((size_t)lvl_ids.size());
+    for (size_t q = 0; q < lvl_ids.size(); ++q) lvl_new[q] = ids[lvl_ids[q]];
+    recs.resize(members.size());
+    for (size_t m = 0; m < members.size(); ++m) {
+      const int64_t first = members[m].second;
+      const int64_t end = m + 1 < members.size() ? members[m + 1].second : (int64_t)lvl_ids.size();
+      label_rec(labels[members[m].first], fits[(size_t)members[m].first], lvl_new.data() + first, end - first,
+                recs[m]);
+    }
+    const int rc = run((int32_t)members.size());
+    if (rc != TPE_OK) return rc;
+    for (size_t q = 0; q < lvl_ids.size(); ++q) {
+      if (res[q].idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
+    }
+    for (size_t m = 0; m < members.size(); ++m) {
+      const int i = members[m].first;
+      const int64_t first = members[m].second;
+      const int64_t end = m + 1 < members.size() ? members[m + 1].second : (int64_t)lvl_ids.size();
+      for (int64_t q = first; q < end; ++q) {
+        const int64_t j = lvl_ids[(size_t)q];
+        const double v = res[(size_t)q].value;
+        values[(size_t)j * n_labels + i] = v;
+        active[(size_t)j * n_labels + i] = 1;
+        chosen[(size_t)j * n_labels + i] = T.gate[(size_t)i] ? (int)(int64_t)v : kActive;
+      }
+    }
+  }
+  return TPE_OK;
+}
+
+}  // extern "C"

@@ -598,6 +598,49 @@ class Engine(object):
             self._record_level_profile()
         return out
 
+    def suggest_tree(self, labels, below_sorted, prior_weight, lf, ids, n_cand, seed, min_draws, flags=0):
+        """A whole tpe.suggest of a tree space in one native call
+        (tpe_suggest_tree): fits, gate prediction and level runs.  ``labels``:
+        TREE_LABEL_DTYPE records in label order; ``below_sorted``: int64
+        ascending below tids.  Returns (values, active) [n_ids x n_labels], or
+        None when the space or history needs the general path
+        (TPE_E_FALLBACK)."""
+        if self.precision != 'fp32':
+            return None
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        n_cand = int(n_cand)
+        if n_cand < 0 or n_cand >= 2 ** 31:
+            raise ValueError('n_EI_candidates out of range: %r' % n_cand)
+        nl, n = len(labels), len(ids)
+        values = np.empty((n, nl))
+        active = np.empty((n, nl), dtype=np.int8)
+        path = (ctypes.c_int32 * 2)()
+        need = N.LevelNeed()
+        seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        prof = self.profile is not None
+        if prof:
+            N.check(self.lib.tpe_level_profile(1), self.lib, 'tpe_level_profile')
+        fl = self._flags() | int(flags)
+        for attempt in range(8):          # a later tree level may need larger pools than the first
+            ws = self._level_ws()
+            rc = self.lib.tpe_suggest_tree(labels.ctypes.data, nl, below_sorted.ctypes.data, len(below_sorted),
+                                           float(prior_weight), int(lf), ids.ctypes.data, n, n_cand, seed64,
+                                           float(min_draws), int(self.device_fit_min), fl, ctypes.byref(ws),
+                                           ctypes.byref(need), stream, values.ctypes.data, active.ctypes.data, path)
+            if rc != N.E_SPACE:
+                break
+            self._grow(need)
+        if prof:
+            self.lib.tpe_level_profile(0)
+        if rc == N.E_FALLBACK:
+            return None
+        N.check(rc, self.lib, 'tpe_suggest_tree')
+        self.last_tree_path = (int(path[0]), int(path[1]))
+        if prof and path[1]:
+            self._record_level_profile()
+        return values, active
+
     def _record_level_profile(self):
         """profile[stage] gets (ms, units, algorithmic CE) of every stage the
         last tpe_level_run launched, timed by the runner's own HIP events on

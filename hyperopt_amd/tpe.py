@@ -32,6 +32,7 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
 forgetting window is fixed at DEFAULT_LF=25 (tpe.py:27-29).
 """
 import logging
+import os
 import math
 import time
 
@@ -246,6 +247,129 @@ def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
     return chosen
 
 
+# one native call per suggest (tpe_suggest_tree) for the spaces it covers;
+# TPE_NATIVE_TREE=0 keeps every suggest on the general path (A/B, tests)
+NATIVE_TREE = os.environ.get('TPE_NATIVE_TREE', '1') != '0'
+
+
+def _tree_static(table):
+    """TREE_LABEL_DTYPE records of a ParamTable's static fields (family,
+    bounds, prior, gating structure), built once per table; None when the
+    tree has a label with more parents than the record holds."""
+    st = table.__dict__.get('_tree_static')
+    if st is not None:
+        return st if st[0] is not None else None
+    arr = np.zeros(len(table.rows), dtype=N.TREE_LABEL_DTYPE)
+    keep, meta = [], []
+    for r in table.rows:
+        rec = arr[r.index]
+        fam = _FAMILY[r.dist]
+        a = r.args
+        rec['family'], rec['label_ix'] = fam, r.index
+        if fam == N.FAM_CATEGORICAL:
+            rec['upper'] = int(a['upper'])
+            if r.dist != 'randint':
+                p = np.ascontiguousarray(a['p'], dtype=np.float64)
+                keep.append(p)
+                rec['p_prior'] = p.ctypes.data
+        elif r.dist in ('uniform', 'loguniform', 'quniform', 'qloguniform'):
+            rec['flags'] = N.F_HAS_LOW | N.F_HAS_HIGH
+            rec['low'], rec['high'] = float(a['low']), float(a['high'])
+            rec['prior_mu'], rec['prior_sigma'] = 0.5 * (a['high'] + a['low']), 1.0 * (a['high'] - a['low'])
+        else:
+            rec['prior_mu'], rec['prior_sigma'] = float(a['mu']), float(a['sigma'])
+        rec['depth'] = r.depth
+        ps = [p for p in r.parents if p is not None]
+        if len(ps) > N.TREE_MAX_PARENTS:
+            table._tree_static = (None, None, None)
+            return None
+        rec['n_parents'] = len(ps)
+        for j, (pl, pc) in enumerate(ps):
+            rec['parent'][j] = table.by_label[pl].index
+            rec['parent_cat'][j] = int(pc)
+        meta.append((r.label, r.index, fam))
+    st = table._tree_static = (arr, keep, meta)
+    return st
+
+
+def _tree_labels(table, hist):
+    """The table's tree records with the history's observation columns filled
+    in (tids, kernel coordinate, value order) — memoised on the Trials cache
+    while no document is appended (the columns' buffers stay put until then).
+    Quantized labels carry no columns: tpe_suggest_tree sends them to the
+    general path whenever they need a fit."""
+    st = _tree_static(table)
+    if st is None:
+        return None
+    arr0, _, meta = st
+    cache = hist._cache
+    key = None
+    if cache is not None:
+        key = (len(cache.docs), id(table))
+        memo = getattr(cache, 'tree_memo', None)
+        if memo is not None and memo[0] == key:
+            return memo[1]
+    arr = arr0.copy()
+    keep = []
+    for label, ix, fam in meta:
+        rec = arr[ix]
+        otids, ovals = hist.obs[label]
+        if fam == N.FAM_CATEGORICAL:
+            cols = hist.cat_columns(label)
+            if cols is None:
+                t, v = np.ascontiguousarray(otids, dtype=np.int64), np.ascontiguousarray(ovals, dtype=np.int64)
+                keep += [t, v]
+                cols = (t.ctypes.data, v.ctypes.data)
+            rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
+        elif fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
+            order = hist.value_order(label)
+            rec['n_obs'] = len(otids)
+            logc = fam == N.FAM_LOGGAUSS
+            cols = hist.native_columns(label, log=logc) if order is not None else None
+            if cols is None:
+                t = np.ascontiguousarray(otids, dtype=np.int64)
+                x = np.ascontiguousarray(hist.log_values(label) if logc else ovals, dtype=np.float64)
+                keep += [t, x]
+                cols = (t.ctypes.data, x.ctypes.data, 0)
+                if order is not None:
+                    o = np.ascontiguousarray(order, dtype=np.int64)
+                    keep.append(o)
+                    cols = cols[:2] + (o.ctypes.data,)
+            rec['tids'], rec['values'], rec['order'] = cols
+    out = (arr, keep)
+    if cache is not None:
+        cache.tree_memo = (key, out)
+    return out
+
+
+def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight):
+    """``_choices_philox`` in one native call (tpe_suggest_tree), or None when
+    the space or history needs the general path."""
+    if not hist.sorted_obs:
+        return None
+    tl = _tree_labels(table, hist)
+    if tl is None:
+        return None
+    below = np.sort(np.asarray(below_tids, dtype=np.int64))
+    res = engine.suggest_tree(tl[0], below, prior_weight, DEFAULT_LF, new_ids, C, seed,
+                              SPECULATE_MIN_DRAWS if SPECULATE else -1.0)
+    if res is None:
+        return None
+    values, active = res
+    vi = np.where(active != 0, values, 0.0).astype(np.int64)
+    order = table.level_order()
+    cols = _tree_static(table)[2]
+    out = []
+    for j in range(len(new_ids)):
+        d = dict.fromkeys(order)
+        act, v, iv = active[j], values[j], vi[j]
+        for label, ix, fam in cols:
+            if act[ix]:
+                d[label] = iv[ix] if fam == N.FAM_CATEGORICAL else v[ix]
+        out.append(d)
+    return out
+
+
 def _choices_replay(table, fits, new_ids, seed, C, engine):
     """Reference RandomState order: labels descending, ancestors first.  Draws
     are made on the host in that order; a label whose parent is drawn but not
@@ -316,8 +440,13 @@ def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weig
     if sampler not in ('philox', 'replay'):
         raise ValueError("sampler must be 'philox' or 'replay'")
     engine = get_engine(device, precision)
-    fits = _Fits(table, hist, _history.split_below(hist, gamma), prior_weight, engine)
+    below_tids = _history.split_below(hist, gamma)
     C = int(n_EI_candidates)
+    if sampler == 'philox' and shard is None and NATIVE_TREE and precision == 'fp32':
+        out = _choices_native(table, hist, below_tids, list(new_ids), seed, C, engine, prior_weight)
+        if out is not None:
+            return out
+    fits = _Fits(table, hist, below_tids, prior_weight, engine)
     if sampler == 'philox':
         return _choices_philox(table, fits, list(new_ids), seed, C, engine, shard)
     if shard is not None:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 11
+#define TPE_ABI_VERSION 12
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -541,6 +541,60 @@ typedef struct tpe_level_need {
 int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
                   int64_t n_cand_global, int32_t precision, int32_t flags, const tpe_level_ws* ws,
                   tpe_level_need* need, void* stream, tpe_result* out);
+
+/* ------------------------------------------------------------------------
+ * One native call per tpe.suggest of a conditional (hp.choice) tree space:
+ * the below/above split and Parzen fit of every label it needs
+ * (ap_filter_trials + adaptive_parzen_normal / the categorical posteriors,
+ * tpe.py:613-641, 398-607), the speculative fusion of the tree levels (gate
+ * winners predicted from the fitted categorical posteriors, every level in one
+ * device batch, predictions verified on the results; level by level on a
+ * misprediction — the activity rule of vectorize.py:19-37 /
+ * pyll/base.py:762-781), and the level runs (tpe_level_run).  The host keeps
+ * only the history view and the trial documents.
+ *
+ * Covered: continuous (GAUSS / LOGGAUSS) and categorical labels fitted on the
+ * host at TPE_PREC_F32, categorical gates.  Anything else returns
+ * TPE_E_FALLBACK (nothing is written; a device batch may have run): the caller
+ * takes its general path — quantized labels and sides with repeated values
+ * (numpy's argsort tie order decides their weights), missing value orders
+ * (NaN), labels large enough for the device Parzen fit, non-categorical gates.
+ * ---------------------------------------------------------------------- */
+#define TPE_TREE_MAX_PARENTS 4
+enum { TPE_E_FALLBACK = -5 };
+
+/* one hyperparameter of the tree, in label order (label_ix = its position) */
+typedef struct tpe_tree_label {
+  int32_t family, flags, upper, label_ix;   /* family: TPE_FAM_*; flags: TPE_F_HAS_LOW / TPE_F_HAS_HIGH */
+  double low, high;                         /* sampling-space bounds (log space for LOGGAUSS)           */
+  double prior_mu, prior_sigma;             /* adaptive_parzen_normal prior (continuous)                */
+  const double* p_prior;                    /* categorical: pchoice probabilities (NULL: randint)       */
+  const int64_t* tids;                      /* observation tids, strictly ascending                     */
+  const void* values;                       /* continuous: f64 kernel coordinate (x, or ln x for
+                                               LOGGAUSS); categorical: int64 categories                 */
+  const int64_t* order;                     /* continuous: permutation sorting `values` ascending        */
+  int64_t n_obs;
+  int32_t depth, n_parents;                 /* tree level (roots 0); 0 parents = unconditional           */
+  int32_t parent[TPE_TREE_MAX_PARENTS];     /* active iff some parent[j] (a label index) chose          */
+  int32_t parent_cat[TPE_TREE_MAX_PARENTS]; /* category parent_cat[j]                                   */
+} tpe_tree_label;
+
+/* tpe_suggest_tree flags: the tpe_level_run flags, plus */
+enum { TPE_TREE_NO_SPECULATE = 1 << 8 };    /* level by level only (no fused batch)                    */
+
+/* below_tids ascending (the n_below best trials, tpe.py:625-629); ids: the
+ * n_ids new trial ids; speculate_min_draws: a gate is predicted when its
+ * predicted category is expected among >= this many of the n_cand draws;
+ * device_fit_min > 0: labels with that many observations are left to the host
+ * path (device Parzen fit).  values / active: [n_ids x n_labels] — the chosen
+ * value (categories as doubles) and whether the label is active; path[0] = 1
+ * when the fused batch was used, path[1] = level runs issued.  TPE_E_SPACE:
+ * grow the workspace to `need` and call again. */
+int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
+                     double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
+                     uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
+                     const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
+                     int32_t* path);
 
 /* ------------------------------------------------------------------------
  * Stage profiler of tpe_level_run (bench.py's live roofline).  While enabled,

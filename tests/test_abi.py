@@ -104,7 +104,7 @@ def test_engine_refuses_without_device():
 
 CTYPES_MIRRORS = (('tpe_batch', N.Batch), ('tpe_label_in', N.LabelIn), ('tpe_pack_info', N.PackInfo),
                   ('tpe_level_ws', N.LevelWS), ('tpe_level_need', N.LevelNeed), ('tpe_mt_state', N.MTState),
-                  ('tpe_stage_prof', N.StageProf))
+                  ('tpe_stage_prof', N.StageProf), ('tpe_tree_label', N.TreeLabel))
 
 
 def test_ctypes_mirrors_match_c():
@@ -155,3 +155,62 @@ def test_level_run_reports_space_without_gpu(monkeypatch):
     rc = lib.tpe_level_run(labels, 1, 1 << 20, 5, 0, 0, N.PREC_F32, 0, ctypes.byref(ws), ctypes.byref(need), None,
                            out.ctypes.data)
     assert rc == N.E_SPACE and need.tab == 0 and need.part >= 2 << 20
+
+
+def test_tree_labels_dtype_matches_ctypes():
+    assert N.TREE_LABEL_DTYPE.itemsize == ctypes.sizeof(N.TreeLabel)
+    for f, _ in N.TreeLabel._fields_:
+        assert N.TREE_LABEL_DTYPE.fields[f][1] == getattr(N.TreeLabel, f).offset, f
+
+
+def _tree_call(table, hist, C, min_draws=64.0, flags=0):
+    from hyperopt_amd import history as H, tpe
+    arr, keep = tpe._tree_labels(table, hist)
+    below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
+    ws, need = N.LevelWS(), N.LevelNeed()
+    vals = np.empty((1, len(arr)))
+    act = np.empty((1, len(arr)), dtype=np.int8)
+    path = (ctypes.c_int32 * 2)()
+    ids = np.array([len(hist)], dtype=np.int64)
+    rc = N.load().tpe_suggest_tree(arr.ctypes.data, len(arr), below.ctypes.data, len(below), 1.0, 25, ids.ctypes.data,
+                                   1, C, 5, min_draws, 16384, flags, ctypes.byref(ws), ctypes.byref(need), None,
+                                   vals.ctypes.data, act.ctypes.data, path)
+    return rc, need, path
+
+
+def test_suggest_tree_fits_and_predicts_without_gpu():
+    """tpe_suggest_tree on the config-3 tree: native fits and the gate
+    prediction run on the host and size the fused batch before any device
+    call (empty workspaces -> TPE_E_SPACE): one problem per label the Python
+    prediction (tpe._predict_activity) keeps active; level by level, the
+    first level's single problem."""
+    import bench
+    from hyperopt_amd import history as H, tpe
+    domain, trials = bench.make_history(3000, 0)
+    hist = H.extract(domain, trials)
+    C = 1 << 16
+    rc, need, path = _tree_call(domain.table, hist, C)
+    assert rc == N.E_SPACE and path[1] == 1, rc
+    fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, None)
+    pred = tpe._predict_activity(domain.table, fits, C)
+    n_act = sum(v is not None for v in pred.values())
+    assert need.result == n_act == 4 and need.cand == n_act * C
+    rc, need, path = _tree_call(domain.table, hist, C, flags=N.TREE_NO_SPECULATE)
+    assert rc == N.E_SPACE and need.result == 1 and need.cand == C
+
+
+def test_suggest_tree_hands_quantized_labels_back():
+    """A root quantized label needs numpy's tie order: TPE_E_FALLBACK before
+    anything is sized or launched."""
+    from hyperopt_amd import base, hp, history as H, rand
+    domain = base.Domain(lambda d: 0.0, {'q': hp.quniform('q', 0, 10, 1), 'x': hp.uniform('x', -1, 1)})
+    trials = base.Trials()
+    rs = np.random.RandomState(0)
+    for tid in range(40):
+        d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
+        d['state'] = base.JOB_STATE_DONE
+        d['result'] = {'status': 'ok', 'loss': float(rs.uniform())}
+        trials.insert_trial_docs([d])
+    trials.refresh()
+    rc, need, path = _tree_call(domain.table, H.extract(domain, trials), 1024)
+    assert rc == N.E_FALLBACK and path[1] == 0

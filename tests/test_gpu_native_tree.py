@@ -1,0 +1,97 @@
+"""The one-call native suggest (tpe_suggest_tree) against the general path.
+
+Both paths fit with the same native routines (tpe_host_fit_split /
+tpe_host_cat_split) and run the same level batches, so every suggestion must
+be identical: fused (speculative) batches, level-by-level evaluation, the
+no-prediction case, batched new_ids, columnar histories without a Trials
+cache, and the hand-over to the general path (quantized labels).
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import doc_values
+
+pytestmark = pytest.mark.gpu
+
+
+def _both(fn):
+    from hyperopt_amd import tpe
+    from hyperopt_amd.engine import get_engine
+    eng = get_engine()
+    eng.last_tree_path = None
+    nat = fn()
+    path = eng.last_tree_path
+    tpe.NATIVE_TREE = False
+    try:
+        gen = fn()
+    finally:
+        tpe.NATIVE_TREE = True
+    return nat, gen, path
+
+
+def test_native_tree_fused_matches_general_path():
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(3000, 0)
+    for seed in (1, 2, 3):
+        for C in (1 << 16, 1 << 20):
+            nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=C)))
+            assert path is not None and path[0] == 1 and path[1] == 1, path     # one fused batch
+            assert nat == gen, (seed, C, nat, gen)
+            assert set(nat) == {'model', 'svm_C', 'svm_kernel', 'svm_rbf_gamma'}
+
+
+def test_native_tree_level_by_level_and_no_prediction():
+    """SPECULATE off (level by level) and a candidate count too small for a
+    gate prediction (C * p < 64 draws): the native level runs equal the
+    general path's."""
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(3000, 0)
+    tpe.SPECULATE = False
+    try:
+        nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, 9, n_EI_candidates=1 << 14)))
+    finally:
+        tpe.SPECULATE = True
+    assert path[0] == 0 and path[1] >= 2 and nat == gen, (path, nat, gen)
+    nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, 9, n_EI_candidates=64)))
+    assert path[0] == 0 and path[1] >= 2 and nat == gen, (path, nat, gen)
+
+
+def test_native_tree_batched_ids():
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(2000, 1)
+    ids = list(range(2000, 2006))
+    for spec in (True, False):
+        tpe.SPECULATE = spec
+        try:
+            nat, gen, path = _both(lambda: [doc_values([d]) for d in
+                                            tpe.suggest(ids, domain, trials, 4, n_EI_candidates=4096)])
+        finally:
+            tpe.SPECULATE = True
+        assert nat == gen and path is not None, (spec, path)
+
+
+def test_native_tree_columnar_history():
+    """suggest_choices on a structure-of-arrays history (no Trials cache):
+    flat 5-dim space, 64 ids."""
+    import bench
+    from hyperopt_amd import tpe
+    labels = ['x%d' % i for i in range(5)]
+    hist = bench.soa_history(labels, 4000, 3, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+    table = bench.flat_uniform_table(labels)
+    ids = np.arange(4000, 4064)
+    nat, gen, path = _both(lambda: tpe.suggest_choices(table, hist, ids, 11, n_EI_candidates=2048))
+    assert path == (0, 1) and nat == gen
+
+
+def test_native_tree_hands_quantized_labels_to_general_path():
+    """The rf branch (quantized rf_n_est / rf_depth_n): tpe_suggest_tree
+    returns TPE_E_FALLBACK and the suggest takes the general path."""
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(3000, 0, loss=bench.rf_loss)
+    nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, 5, n_EI_candidates=1 << 16)))
+    assert path is None and nat == gen
+    assert int(nat['model']) == 1

@@ -33,6 +33,8 @@ def main():
         setattr(obj, name, w)
     wrap(tpe._Fits, 'get', 'fits')
     wrap(eng, 'run_level', 'run_level')
+    wrap(eng, 'suggest_tree', 'suggest_tree (native fits+levels)')
+    wrap(tpe, '_tree_labels', 'suggest_tree/_tree_labels')
     wrap(H, 'extract', 'extract')
     wrap(H, 'split_below', 'split_below')
     wrap(tpe.rand, 'docs_from_choices', 'docs')
