@@ -104,6 +104,8 @@ __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
   const uint64_t m = ((uint64_t)a << 21) ^ (uint64_t)(b >> 11);   // 53 bits
   return ((double)m + 0.5) * 1.1102230246251565e-16;
 }
+// 32-bit uniform as a double in (0, 1) (exact)
+__device__ __forceinline__ double u01w(uint32_t a) { return ((double)a + 0.5) * 2.3283064365386963e-10; }
 
 // ---------------------------------------------------------- argmax order
 // np.argmax: NaN is the maximum (first NaN wins), otherwise the largest value,
@@ -302,6 +304,54 @@ __device__ __forceinline__ int tile_pos(int cand_start, int j) {
 }
 
 // ================================================================= sample
+// Phi^-1(pr) in f32 = -sqrt2 erfinv(1 - 2 pr), erfinv by Giles' single-precision
+// approximation ("Approximating the erfinv function", GPU Computing Gems 2010)
+// with its log argument (1 - x)(1 + x) = 4 pr (1 - pr) formed from pr itself (no
+// cancellation in the tails).  Relative error <= 3e-7 over the f32 uniforms
+// (checked against scipy.special.ndtri); one v_log_f32, the tail branch adds a
+// sqrt.  Every f32 draw inverts through this one function.
+__device__ __forceinline__ float ndtri_f32(float pr) {
+  const float x = 1.f - 2.f * pr;
+  float w = -__logf(4.f * pr * (1.f - pr));
+  float q;
+  if (w < 5.f) {
+    w -= 2.5f;
+    q = 2.81022636e-08f;
+    q = __builtin_fmaf(q, w, 3.43273939e-07f); q = __builtin_fmaf(q, w, -3.5233877e-06f);
+    q = __builtin_fmaf(q, w, -4.39150654e-06f); q = __builtin_fmaf(q, w, 0.00021858087f);
+    q = __builtin_fmaf(q, w, -0.00125372503f); q = __builtin_fmaf(q, w, -0.00417768164f);
+    q = __builtin_fmaf(q, w, 0.246640727f); q = __builtin_fmaf(q, w, 1.50140941f);
+  } else {
+    w = __builtin_sqrtf(w) - 3.f;
+    q = -0.000200214257f;
+    q = __builtin_fmaf(q, w, 0.000100950558f); q = __builtin_fmaf(q, w, 0.00134934322f);
+    q = __builtin_fmaf(q, w, -0.00367342844f); q = __builtin_fmaf(q, w, 0.00573950773f);
+    q = __builtin_fmaf(q, w, -0.0076224613f); q = __builtin_fmaf(q, w, 0.00943887047f);
+    q = __builtin_fmaf(q, w, 1.00167406f); q = __builtin_fmaf(q, w, 2.83297682f);
+  }
+  return -1.41421356237309505f * (q * x);
+}
+
+// The uniforms of candidate i (Philox-4x32-10, counter = its GLOBAL index g, so
+// draws do not depend on sharding or on which kernel re-draws them): `us`
+// selects the component (category), `uf` / `ud` invert its truncated normal in
+// f32 / f64.  f32 draws of the non-categorical families take two candidates per
+// Philox block — g even: words (x, y) of block g / 2, g odd: (z, w) — a 32-bit
+// selection uniform and 23 bits of inversion; f64 draws and categories take one
+// block per candidate (53-bit selection, 53-bit inversion).
+struct DrawU { double us; float uf; double ud; };
+__device__ __forceinline__ DrawU draw_uniforms(const tpe_problem& p, int64_t i, int precision) {
+  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
+  if (precision == TPE_PREC_F32 && p.family != TPE_FAM_CATEGORICAL) {
+    const uint64_t blk = g >> 1;
+    const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+    const bool odd = g & 1;
+    return DrawU{u01w(odd ? r.z : r.x), u01f(odd ? r.w : r.y), 0.0};
+  }
+  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+  return DrawU{u01d(r.x, r.y), u01f(r.z), u01d(r.z, r.w)};
+}
+
 // f32 truncation bounds of a problem: smallest float >= low, largest float < high
 __device__ __forceinline__ void f32_bounds(const tpe_problem& p, float& lo_f, float& hi_f) {
   lo_f = -INFINITY; hi_f = INFINITY;
@@ -336,7 +386,7 @@ __device__ __forceinline__ int find_comp(const tpe_problem& p, const double* __r
 // mirrored bounds) at the uniform uf: the kernel coordinate of the draw
 __device__ __forceinline__ float comp_coord_f32(const double* __restrict__ s, float uf, float lo_f, float hi_f) {
   const float pr = (float)s[3] + uf * ((float)s[4] - (float)s[3]);
-  float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+  float z = ndtri_f32(pr);
   if (s[5] != 0.0) z = -z;
   float xf = (float)s[1] + (float)s[2] * z;
   if (!(xf == xf)) xf = (float)s[1];
@@ -374,26 +424,24 @@ __device__ __forceinline__ void draw_comp(const tpe_problem& p, const double* __
 __device__ __forceinline__ void draw_one(const tpe_problem& p, const double* __restrict__ S,
                                          const double* __restrict__ cum, int cs, int64_t i, int precision,
                                          float lo_f, float hi_f, double& x, float& t, int& comp) {
-  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-  const int a = find_comp(p, cum, cs, u01d(r.x, r.y));
+  const DrawU u = draw_uniforms(p, i, precision);
+  const int a = find_comp(p, cum, cs, u.us);
   comp = a;
   if (p.family == TPE_FAM_CATEGORICAL) {
     x = (double)a;
     t = (float)a;
     return;
   }
-  draw_comp(p, S, a, u01f(r.z), u01d(r.z, r.w), precision, lo_f, hi_f, x, t);
+  draw_comp(p, S, a, u.uf, u.ud, precision, lo_f, hi_f, x, t);
 }
 
 // draw_one's kernel coordinate alone (f32, continuous families): no f64 value
 __device__ __forceinline__ float draw_coord_f32(const tpe_problem& p, const double* __restrict__ S,
                                                 const double* __restrict__ cum, int cs, int64_t i, float lo_f,
                                                 float hi_f) {
-  const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-  const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-  const int a = find_comp(p, cum, cs, u01d(r.x, r.y));
-  return comp_coord_f32(S + 8 * a, u01f(r.z), lo_f, hi_f);
+  const DrawU u = draw_uniforms(p, i, TPE_PREC_F32);
+  const int a = find_comp(p, cum, cs, u.us);
+  return comp_coord_f32(S + 8 * a, u.uf, lo_f, hi_f);
 }
 
 // ------------------------------------------------------------ ordered draws
@@ -681,6 +729,7 @@ constexpr int kGuide = 64;                          // CDF guide entries
 constexpr int kTabMaxTilesPerWg = 16;
 static_assert(kTile % kTabThreads == 0, "tabulated sample tiling");
 constexpr int kTabPer = kTile / kTabThreads;         // candidates per thread per tile
+static_assert(kTabPer % 2 == 0, "a thread draws its candidates in Philox pairs");
 
 // first k with u < cum_k (k <= len - 1), starting at the guide entry of u:
 // the binary search's answer (find_comp) on a non-decreasing CDF
@@ -846,7 +895,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     f32_bounds(p, lo_f, hi_f);
     const double* S = samp + 8 * (int64_t)p.samp_off;
     const bool logc = p.family == TPE_FAM_LOGGAUSS;
-    const int first = cand_start + (int)threadIdx.x;
+    // a thread's candidates are consecutive: an f32 Philox block serves two of them
+    const int first = cand_start + kTabPer * (int)threadIdx.x;
     uint32_t exact = 0;                              // candidates the cell tables do not cover (rare)
     float tj[kTabPer];
     // cells; TL: the tables are in LDS (separate instantiations, so every table
@@ -860,9 +910,27 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         const float4* __restrict__ r1;
         if constexpr (kL) { r0 = tab_lds; r1 = tab_lds + n0; }
         else { r0 = tab + p.tab_off[0]; r1 = tab + p.tab_off[1]; }
+        // the pair's uniforms (draw_uniforms' f32 definition): one Philox block
+        // per two candidates when the first one's global index is even
+        DrawU du[kTabPer];
+        if (draw && in_lds) {
+          const uint64_t g0 = (uint64_t)p.cand_base + (uint64_t)first;
+          if ((g0 & 1) == 0) {
+#pragma unroll
+            for (int j = 0; j < kTabPer; j += 2) {
+              const uint64_t blk = (g0 + (uint64_t)j) >> 1;
+              const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+              du[j] = DrawU{u01w(r.x), u01f(r.y), 0.0};
+              du[j + 1] = DrawU{u01w(r.z), u01f(r.w), 0.0};
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < kTabPer; ++j) du[j] = draw_uniforms(p, first + j, TPE_PREC_F32);
+          }
+        }
 #pragma unroll
         for (int j = 0; j < kTabPer; ++j) {
-          const int i = first + j * kTabThreads;
+          const int i = first + j;
           tj[j] = NAN;
           if (i >= p.n_cand) continue;
           const int64_t o = p.cand_off + i;
@@ -870,12 +938,10 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           if (!draw) {
             t = coord[o];
           } else if (in_lds) {
-            const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
-            const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-            const int a = guided_comp(cum_lds, guide, p.samp_len, u01d(r.x, r.y));
+            const int a = guided_comp(cum_lds, guide, p.samp_len, du[j].us);
             const float4 s = row_lds[a];
-            const float pr = s.z + u01f(r.z) * (s.w - s.z);
-            const float z = -1.41421356237309505f * erfcinvf(2.f * pr);
+            const float pr = s.z + du[j].uf * (s.w - s.z);
+            const float z = ndtri_f32(pr);
             float xf = s.x + s.y * z;
             if (!(xf == xf)) xf = s.x;
             t = fminf(fmaxf(xf, lo_f), hi_f);
@@ -906,7 +972,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
             if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
             if (lane == src) {
-              const int i = first + j * kTabThreads;
+              const int i = first + j;
               const int64_t o = p.cand_off + i;
               const double lnx = logc ? (double)t : 0.0;
               const double x = !need_x ? 0.0 : !draw ? cand[o] : logc ? exp((double)t) : (double)t;
@@ -923,7 +989,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     }
     if (!cells) {                                    // lattice: exact {l, g} per quantized value
       for (int j = 0; j < kTabPer; ++j) {
-        const int i = first + j * kTabThreads;
+        const int i = first + j;
         if (i >= p.n_cand) break;
         const int64_t o = p.cand_off + i;
         double x, l, g;
@@ -1662,13 +1728,12 @@ __device__ void select_generic(const tpe_problem& p, const tpe_best* __restrict_
   // dependent global loads on lane 0
   const bool wave_search = redraw && !od && staged;
   int comp = 0;
-  U4 rw{0, 0, 0, 0};
+  DrawU rw{0.0, 0.f, 0.0};
   if (wave_search) {
     const double* S = srow;
-    const uint64_t g = (uint64_t)p.cand_base + (uint64_t)b.idx;
-    rw = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+    rw = draw_uniforms(p, b.idx, precision);
     const int lane = (int)threadIdx.x;
-    const bool hit = lane < p.samp_len && u01d(rw.x, rw.y) < S[8 * lane];
+    const bool hit = lane < p.samp_len && rw.us < S[8 * lane];
     const unsigned long long m = __ballot(hit);
     comp = m ? __builtin_ctzll(m) : p.samp_len - 1;
   }
@@ -1684,7 +1749,7 @@ __device__ void select_generic(const tpe_problem& p, const tpe_best* __restrict_
       if (od) ordered_draw(p, S, S, 8, U, precision, lo_f, hi_f, r.value, t);
       else if (!wave_search) draw_one(p, S, S, 8, b.idx, precision, lo_f, hi_f, r.value, t, c);
       else if (p.family == TPE_FAM_CATEGORICAL) r.value = (double)comp;
-      else draw_comp(p, srow, comp, u01f(rw.z), u01d(rw.z, rw.w), precision, lo_f, hi_f, r.value, t);
+      else draw_comp(p, srow, comp, rw.uf, rw.ud, precision, lo_f, hi_f, r.value, t);
     } else if (b.idx >= 0) {
       r.value = cand[p.cand_off + b.idx];
     }
@@ -2089,6 +2154,28 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
   }
 }
 
+// ============================================================ level upload
+// The packed level (pinned host memory, device-addressable) copied into the
+// device blob by the compute queue itself: the first stage then follows in
+// queue order, without the copy engine's hand-off to the compute queue (the
+// ~10 us gap an hipMemcpyAsync upload left before the first kernel of a level).
+// System-scope loads: the host rewrites the staging buffer every level.
+constexpr int kUploadThreads = 256;
+
+__global__ __launch_bounds__(kUploadThreads) void k_upload(const unsigned long long* __restrict__ src,
+                                                           unsigned long long* __restrict__ dst, int64_t n8,
+                                                           const unsigned long long* __restrict__ src2,
+                                                           unsigned long long* __restrict__ dst2, int64_t m8) {
+  const int64_t stride = (int64_t)gridDim.x * kUploadThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kUploadThreads + threadIdx.x; i < n8 + m8; i += stride) {
+    const bool first = i < n8;
+    const unsigned long long* s = first ? src + i : src2 + (i - n8);
+    const unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (first) dst[i] = v;
+    else dst2[i - n8] = v;
+  }
+}
+
 // ============================================================ device Parzen fit
 // adaptive_parzen_normal (tpe.py:398-475) of the above observations of a label
 // (ap_filter_trials, tpe.py:613-641), directly into the pruned f32 layout.
@@ -2429,6 +2516,16 @@ constexpr int64_t kOneCopyMaxGap = 256 << 10;    // bytes a single upload may ca
 bool direct_results() {
   const char* v = getenv("TPE_RESULT_COPY");
   return !(v && v[0] == '1');
+}
+
+// TPE_UPLOAD_COPY=1: upload a level with hipMemcpyAsync (else the k_upload
+// kernel copies it from the device-addressable staging buffer)
+bool kernel_upload() {
+  static const int on = [] {
+    const char* v = getenv("TPE_UPLOAD_COPY");
+    return !(v && v[0] == '1');
+  }();
+  return on != 0;
 }
 
 // device address of a pinned host buffer (the last one asked about is
@@ -2829,7 +2926,22 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   // after the copy in stream order
   hipError_t e;
   const int64_t gap = info.off_comp32 - info.copy_end;
-  if (info.copy2_len > 0 && gap <= kOneCopyMaxGap) {
+  char* dbase = direct_results() ? device_alias(ws->pinned) : nullptr;
+  // ranges to upload: [0, n1) and [o2, o2 + n2) (one range when the gap is small)
+  int64_t n1 = info.copy_end, o2 = info.off_comp32, n2 = info.copy2_len;
+  if (n2 > 0 && gap <= kOneCopyMaxGap) { n1 = o2 + n2; n2 = 0; }
+  const int64_t n1r = (n1 + 7) & ~(int64_t)7, n2r = (n2 + 7) & ~(int64_t)7;
+  if (dbase && kernel_upload() && n1r <= ws->blob_bytes && (n2 == 0 || o2 + n2r <= ws->blob_bytes) &&
+      n1r + n2r <= ((int64_t)64 << 20)) {
+    const int64_t n8 = n1r / 8, m8 = n2r / 8;
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>((n8 + m8 + kUploadThreads - 1) / kUploadThreads, 1),
+                                            2048);
+    TPE_LAUNCH(k_upload, dim3(grid), dim3(kUploadThreads), 0, s, (const unsigned long long*)dbase,
+               (unsigned long long*)dev, n8, (const unsigned long long*)(dbase + o2),
+               (unsigned long long*)(dev + o2), m8);
+    if ((rc = hip_check("k_upload"))) return rc;
+    e = hipSuccess;
+  } else if (info.copy2_len > 0 && gap <= kOneCopyMaxGap) {
     e = hipMemcpyAsync(dev, host, (size_t)(info.off_comp32 + info.copy2_len), hipMemcpyHostToDevice, s);
   } else {
     e = hipMemcpyAsync(dev, host, (size_t)info.copy_end, hipMemcpyHostToDevice, s);
@@ -2887,7 +2999,6 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   // the select stage writes the results straight into the pinned staging
   // buffer when the device can address it (no readback copy)
   tpe_result* rh = (tpe_result*)(host + res_off);
-  char* dbase = direct_results() ? device_alias(ws->pinned) : nullptr;
   tpe_result* rd = dbase ? (tpe_result*)(dbase + res_off) : nullptr;
   // early selection (include/tpe_hip.h): the sample stage reports each run of
   // tabulated tiles to host-visible memory, the table stage selects the lazy

@@ -12,6 +12,7 @@
 #   stage      steady-state per-stage device times        (REP)
 #   configs    bench.py --config 1, 2, 4, 5
 #   hostsplit  host-side time split of the headline suggest
+#   nativesplit native fits / tpe_suggest_tree / device stages of the headline suggest
 #   hostprof   cProfile of the headline suggest on the device
 #   pmcloop    PMC counter passes on tools/suggest_loop.py (the real suggest flow)
 #   apitrace   HIP API + kernel + copy trace of tools/suggest_loop.py -> timeline of the last suggests
@@ -81,6 +82,9 @@ for task in "$@"; do
     hostprof)
       step 300 $O/hostprof_${TAG}.txt python tools/host_prof.py ${STEPS:-300}
       head -60 $O/hostprof_${TAG}.txt ;;
+    nativesplit)
+      step 300 $O/nativesplit_${TAG}.txt python tools/native_split.py ${STEPS:-200}
+      cat $O/nativesplit_${TAG}.txt ;;
     hostsplit)
       step 300 $O/hostsplit_${TAG}.txt python tools/host_split.py ${STEPS:-200}
       cat $O/hostsplit_${TAG}.txt ;;

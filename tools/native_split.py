@@ -1,0 +1,89 @@
+"""Where the time of one native config-3 suggest (tpe_suggest_tree) goes:
+the native fits of the four labels the svm/rbf branch needs, timed by calling
+tpe_host_cat_split / tpe_host_fit_split directly; the packer alone; the whole
+tpe_suggest_tree call; and the device stages of the same call (stage profiler).
+Run on the GPU box: python tools/native_split.py [reps]"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from hyperopt_amd import _native as N, engine as E, history as H, tpe  # noqa: E402
+
+
+def best_of(fn, reps=200, inner=10):
+    b = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for _ in range(inner):
+            fn()
+        b = min(b, (time.perf_counter() - t0) / inner)
+    return 1e6 * b
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    eng = E.get_engine(torch.device('cuda', 0))
+    lib = N.load()
+    domain, trials = bench.make_history(bench.N_HISTORY, bench.SEED)
+    hist = H.extract(domain, trials)
+    table = domain.table
+    below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
+    arr, keep = tpe._tree_labels(table, hist)
+    tot_fit = 0.0
+    for lab in ('model', 'svm_kernel', 'svm_C', 'svm_rbf_gamma'):
+        r = arr[table.by_label[lab].index]
+        n = int(r['n_obs'])
+        if r['family'] == N.FAM_CATEGORICAL:
+            up = int(r['upper'])
+            out = np.empty(2 * up)
+            p = int(r['p_prior']) or None
+
+            def f():
+                lib.tpe_host_cat_split(int(r['values']), int(r['tids']), n, below.ctypes.data, len(below), up, p,
+                                       1.0, 25, out.ctypes.data, out.ctypes.data + 8 * up)
+        else:
+            out = np.empty(6 * (n + 1))
+            k = np.empty(2, dtype=np.int64)
+
+            def f():
+                lib.tpe_host_fit_split(int(r['values']), int(r['tids']), int(r['order']), n, below.ctypes.data,
+                                       len(below), 1.0, float(r['prior_mu']), float(r['prior_sigma']), 25,
+                                       out.ctypes.data, k.ctypes.data)
+        t = best_of(f, reps)
+        tot_fit += t
+        print('  fit %-14s n_obs %6d  %7.1f us' % (lab, n, t))
+    print('  fits total                     %7.1f us' % tot_fit)
+    ids = np.array([bench.N_HISTORY], dtype=np.int64)
+    C = bench.C_PER_GPU
+
+    def sug():
+        eng.suggest_tree(arr, below, 1.0, 25, ids, C, 5, tpe.SPECULATE_MIN_DRAWS)
+    for _ in range(20):
+        sug()
+    torch.cuda.synchronize()
+    lat = []
+    for i in range(reps):
+        t0 = time.perf_counter()
+        sug()
+        lat.append(time.perf_counter() - t0)
+    print('  tpe_suggest_tree (Engine.suggest_tree)  p50 %7.1f us  min %7.1f us' %
+          (1e6 * np.median(lat), 1e6 * np.min(lat)))
+    eng.profile = {}
+    for _ in range(20):
+        sug()
+    prof = eng.profile
+    eng.profile = None
+    for k, v in prof.items():
+        print('  device stage %-10s %7.1f us' % (k, 1e3 * np.median([a[0] for a in v])))
+
+
+if __name__ == '__main__':
+    main()
