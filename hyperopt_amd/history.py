@@ -134,6 +134,7 @@ class _Cache(object):
         self.logs = {}                 # label -> _Grow of np.log of its observation values
         self.top = None                # positions of the smallest losses, sorted by (loss, position)
         self.top_n = 0                 # documents merged into `top`
+        self.hist = None               # History view of the current documents (no pending losses)
 
     def extend(self, docs, start):
         for i in range(start, len(docs)):
@@ -302,6 +303,8 @@ def extract(domain, trials):
         start = 0
     else:
         start = len(cache.docs)
+        if start == len(docs) and not cache.pending and cache.hist is not None:
+            return cache.hist             # nothing appended, no loss can change: the same view
     cache.extend(docs, start)
     if not cache.ok:
         _CACHES.pop(trials, None)
@@ -310,7 +313,9 @@ def extract(domain, trials):
     cache.refresh_pending()
     tids = cache.tids.view()
     obs = dict((k, (cache.obs_tid[k].view(), cache.obs_val[k].view())) for k in labels)
-    return History(tids, cache.losses.view(), obs, dev=cache.dev, cache=cache)
+    hist = History(tids, cache.losses.view(), obs, dev=cache.dev, cache=cache)
+    cache.hist = hist if not cache.pending else None
+    return hist
 
 
 def split_below(history, gamma, gamma_cap=25):

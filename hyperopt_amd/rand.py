@@ -8,7 +8,6 @@ to the reference's.  Prior draws follow pyll/stochastic.py:30-142.
 """
 import numpy as np
 
-from .base import miscs_update_idxs_vals
 
 
 def prior_draw(rng, dist, a, size):
@@ -54,10 +53,16 @@ def docs_from_choices(new_ids, domain, trials, choices):
     """Trial documents for ``new_ids`` from per-id {label: value or None}."""
     rval = []
     for new_id, chosen in zip(new_ids, choices):
-        idxs = dict((k, [new_id] if v is not None else []) for k, v in chosen.items())
-        vals = dict((k, [v] if v is not None else []) for k, v in chosen.items())
-        misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir)
-        miscs_update_idxs_vals([misc], idxs, vals)
+        # the misc miscs_update_idxs_vals builds for one id (base.py:77-105), directly
+        idxs, vals = {}, {}
+        for k, v in chosen.items():
+            if v is None:
+                idxs[k] = []
+                vals[k] = []
+            else:
+                idxs[k] = [new_id]
+                vals[k] = [v]
+        misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir, idxs=idxs, vals=vals)
         rval.extend(trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc]))
     return rval
 

@@ -362,10 +362,10 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     out = []
     for j in range(len(new_ids)):
         d = dict.fromkeys(order)
-        act, v, iv = active[j], values[j], vi[j]
+        act, v, iv = active[j].tolist(), values[j], vi[j]
         for label, ix, fam in cols:
             if act[ix]:
-                d[label] = iv[ix] if fam == N.FAM_CATEGORICAL else v[ix]
+                d[label] = iv[ix] if fam == N.FAM_CATEGORICAL else v[ix]   # np.int64 / np.float64 scalars
         out.append(d)
     return out
 
