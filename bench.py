@@ -10,10 +10,12 @@ each rank scores 2^20 candidates of every active hyperparameter, total
 C = N * 2^20, per-level winner combined by one all-gather (dist.py).
 
 value  = sum over steps of (active hyperparameters x total candidates) / time
-roofline: the dominant kernel (k_above_f32, the above-mixture log-sum-exp)
-          timed per launch with HIP events on the engine's stream.
-cpu_baseline: the CPU oracle (numpy restatement of the reference, 1 core) on
-          a bounded sample of the same workload.
+roofline: the dominant stage by device time (k_sample_tab on config 3),
+          timed per launch with HIP events the level runner records on its own
+          stream (tpe_level_profile), priced by executed VALU instructions
+          (SQ_INSTS_VALU of a separate PMC pass) against the issue peak.
+cpu_baseline: the CPU oracle (numpy restatement of the reference) on a bounded
+          sample of the same workload, 1 core and candidate-chunked over all cores.
 """
 import argparse
 import json
