@@ -779,6 +779,11 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
                                                             tpe_result* __restrict__ run_best) {
   __shared__ float4 tab_lds[4 * kTabLdsCells];
   __shared__ double cum_lds[kCumLds];
+#ifdef TPE_SAMPLE_TRACE                      // debug builds only: per-phase workgroup timing
+  uint64_t st[5] = {(uint64_t)wall_clock64(), 0, 0, 0, 0};
+  __shared__ int s_exact;
+  if (threadIdx.x == 0) s_exact = 0;
+#endif
   __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
   __shared__ int guide[kGuide];
   __shared__ tpe_best wb[kTabThreads / 64];
@@ -786,51 +791,70 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   const bool need_x = l_out != nullptr || (flags & TPE_BATCH_WRITE_CAND);
   int cur = -1, run_tile = -1;            // problem staged, first tile of its run
   bool in_lds = false, tab_in_lds = false;
-  double bs = 0.0, bl = 0.0, bg = 0.0;
+  double bs = 0.0, bl = 0.0, bg = 0.0, bv = 0.0;
   int64_t bi = -1;
-  auto emit = [&](int i, int64_t o, double x, double l, double g) {
+  // bv: the best candidate's draw — its kernel coordinate t for cells (the value
+  // is t, or e^t for log families: draw_comp's f32 definition) or its value for
+  // the lattice — so the run's winner needs no redraw
+  auto emit = [&](int i, int64_t o, double x, double l, double g, double v) {
     if (l_out) { l_out[o] = l; g_out[o] = g; }
     if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
-    if (better(l - g, i, bs, bi)) { bs = l - g; bl = l; bg = g; bi = i; }
+    if (better(l - g, i, bs, bi)) { bs = l - g; bl = l; bg = g; bi = i; bv = v; }
   };
+  // cells candidates: a thread keeps its best by d = log2 l~ - log2 g~ in f32
+  // (the order of l - g up to f32 rounding of d: a near-tie inside the eps-tie
+  // set), with the two log2 sums and the coordinate; l, g and the f64 score are
+  // formed once per run (flush) — no f64 work per candidate
+  float fd = 0.f, flb = 0.f, fla = 0.f, ft = 0.f;
+  int fi = -1;
+  auto track = [&](int i, float lb2, float la2, float t) {
+    const float d = lb2 - la2;
+    bool win;                                // better() in f32: NaN first, then larger, then lower index
+    if (fi < 0) win = true;
+    else if (d != d || fd != fd) win = d != d && (fd == fd || i < fi);
+    else win = d > fd || (d == fd && i < fi);
+    if (win) { fd = d; fi = i; flb = lb2; fla = la2; ft = t; }
+  };
+  // the run's problem fields the flush needs (no global reads at the run's end)
+  int64_t run_cand_base = 0, run_cand_off = 0;
+  double run_bb = 0.0, run_ab = 0.0;
+  bool run_logc = false, run_exp = false, run_drawn = false;
   // the run's best -> slot 0 of its first tile (block reduction)
   auto flush = [&]() {
+    if (fi >= 0) {
+      const double lnx = run_logc ? (double)ft : 0.0;
+      const double l = (double)flb * kLn2 + run_bb - lnx, g = (double)fla * kLn2 + run_ab - lnx;
+      if (better(l - g, fi, bs, bi)) { bs = l - g; bl = l; bg = g; bi = fi; bv = (double)ft; }
+    }
+    fi = -1;
     for (int off = 32; off > 0; off >>= 1) {
       const double os = __shfl_xor(bs, off), ol = __shfl_xor(bl, off), og = __shfl_xor(bg, off);
+      const double ov = __shfl_xor(bv, off);
       const int64_t oi = __shfl_xor(bi, off);
-      if (better(os, oi, bs, bi)) { bs = os; bl = ol; bg = og; bi = oi; }
+      if (better(os, oi, bs, bi)) { bs = os; bl = ol; bg = og; bi = oi; bv = ov; }
     }
-    if (lane == 0) { wb[wave].score = bs; wb[wave].l = bl; wb[wave].g = bg; wb[wave].idx = bi; }
+    __shared__ double wv[kTabThreads / 64];
+    if (lane == 0) { wb[wave].score = bs; wb[wave].l = bl; wb[wave].g = bg; wb[wave].idx = bi; wv[wave] = bv; }
     __syncthreads();
     if (wave == 0) {                         // lanes 0..15 hold the waves' bests
       const int q = lane < kTabThreads / 64 ? lane : 0;
-      double s2 = wb[q].score, l2 = wb[q].l, g2 = wb[q].g;
+      double s2 = wb[q].score, l2 = wb[q].l, g2 = wb[q].g, v2 = wv[q];
       int64_t i2 = lane < kTabThreads / 64 ? wb[q].idx : -1;
       for (int off = 8; off > 0; off >>= 1) {
         const double os = __shfl_xor(s2, off), ol = __shfl_xor(l2, off), og = __shfl_xor(g2, off);
+        const double ov = __shfl_xor(v2, off);
         const int64_t oi = __shfl_xor(i2, off);
-        if (better(os, oi, s2, i2)) { s2 = os; l2 = ol; g2 = og; i2 = oi; }
+        if (better(os, oi, s2, i2)) { s2 = os; l2 = ol; g2 = og; i2 = oi; v2 = ov; }
       }
       if (lane == 0) {
         if (run_best) {
-          // early selection: the run's best with its value re-drawn (the
-          // select stage's redraw), straight to host-visible memory
-          const tpe_problem& q = P[cur];
+          // early selection: the run's best with its value (the draw it kept —
+          // what the select stage's redraw would give), straight to
+          // host-visible memory
           tpe_result r;
           r.score = s2; r.l = l2; r.g = g2; r.idx = i2; r.value = 0.0;
-          r.global_idx = i2 >= 0 ? q.cand_base + i2 : -1;
-          if (i2 >= 0) {
-            if (draw && q.samp_len > 0) {
-              float lo_f, hi_f, t;
-              int c;
-              f32_bounds(q, lo_f, hi_f);
-              const double* S = samp + 8 * (int64_t)q.samp_off;
-              if (in_lds) draw_one(q, S, cum_lds, 1, i2, PREC, lo_f, hi_f, r.value, t, c);
-              else draw_one(q, S, S, 8, i2, PREC, lo_f, hi_f, r.value, t, c);
-            } else {
-              r.value = cand[q.cand_off + i2];
-            }
-          }
+          r.global_idx = i2 >= 0 ? run_cand_base + i2 : -1;
+          if (i2 >= 0) r.value = run_drawn ? (run_exp ? exp(v2) : v2) : cand[run_cand_off + i2];
           run_best[run_tile] = r;
         } else {
           tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
@@ -838,7 +862,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         }
       }
     }
-    bs = 0.0; bl = 0.0; bg = 0.0; bi = -1;
+    bs = 0.0; bl = 0.0; bg = 0.0; bv = 0.0; bi = -1;
   };
   // this workgroup's tile descriptors, fetched in one round
   __shared__ int s_tile[kTabMaxTilesPerWg], s_prob[kTabMaxTilesPerWg], s_start[kTabMaxTilesPerWg];
@@ -871,8 +895,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       }
       tab_in_lds = PREC == TPE_PREC_F32 && cells && p.tab_n[0] + p.tab_n[1] <= kTabLdsCells;
       if (tab_in_lds) {                              // plane k of cell j at tab_lds[k * kTabLdsCells + j]
+        // workgroups start at different 16-KiB windows of the tables (every CU
+        // of the problem stages the same rows: spread the first touches)
         const int n0 = 4 * p.tab_n[0], n1 = 4 * p.tab_n[1];
-        for (int q = threadIdx.x; q < n0 + n1; q += kTabThreads) {
+        const int nw = (n0 + n1 + kTabThreads - 1) / kTabThreads;
+        const int rot = (int)blockIdx.x % nw;
+        for (int u = 0; u < nw; ++u) {
+          const int q = ((u + rot) % nw) * kTabThreads + (int)threadIdx.x;
+          if (q >= n0 + n1) continue;
           const float4 v = q < n0 ? tab[(int64_t)p.tab_off[0] + q] : tab[(int64_t)p.tab_off[1] + q - n0];
           tab_lds[(q & 3) * kTabLdsCells + (q >> 2)] = v;
         }
@@ -887,6 +917,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       __syncthreads();
       cur = pid;
       run_tile = tile;
+      run_cand_base = p.cand_base; run_cand_off = p.cand_off;
+      run_bb = p.below_base; run_ab = p.above_base;
+      run_logc = p.family == TPE_FAM_LOGGAUSS;
+      run_exp = cells && run_logc;
+      run_drawn = draw && p.samp_len > 0;
+#ifdef TPE_SAMPLE_TRACE
+      if (!st[1]) st[1] = wall_clock64();
+#endif
     }
     const int cand_start = __builtin_amdgcn_readfirstlane(s_start[gi]);
     if (!run_best && threadIdx.x < TPE_BEST_PER_TILE)   // (early selection: runs report to run_best)
@@ -954,15 +992,22 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           const float lb2 = cell_log2_lds(lo0, inv0, n0, r0, stride, step, t),
                     la2 = cell_log2_lds(lo1, inv1, n1, r1, stride, step, t);
           if (!(lb2 == lb2) || !(la2 == la2)) { exact |= 1u << j; continue; }
-          const double lnx = logc ? (double)t : 0.0;
-          const double x = !need_x ? 0.0 : !draw ? cand[o] : logc ? exp((double)t) : (double)t;
-          emit(i, o, x, (double)lb2 * kLn2 + p.below_base - lnx, (double)la2 * kLn2 + p.above_base - lnx);
+          track(i, lb2, la2, t);
+          if (need_x) {                          // per-candidate outputs on request (tests)
+            const double lnx = logc ? (double)t : 0.0;
+            const double x = !draw ? cand[o] : logc ? exp((double)t) : (double)t;
+            if (l_out) { l_out[o] = (double)lb2 * kLn2 + p.below_base - lnx; g_out[o] = (double)la2 * kLn2 + p.above_base - lnx; }
+            if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
+          }
         }
         // candidates outside the cells or in flagged ones: summed exactly by the
         // whole wave, one candidate at a time
 #pragma unroll
         for (int j = 0; j < kTabPer; ++j) {
           unsigned long long need = __ballot((exact >> j) & 1u);
+#ifdef TPE_SAMPLE_TRACE
+          if (lane == 0) atomicAdd(&s_exact, (int)__popcll(need));
+#endif
           while (need) {
             const int src = __builtin_ctzll(need);
             need &= need - 1;
@@ -974,9 +1019,13 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             if (lane == src) {
               const int i = first + j;
               const int64_t o = p.cand_off + i;
-              const double lnx = logc ? (double)t : 0.0;
-              const double x = !need_x ? 0.0 : !draw ? cand[o] : logc ? exp((double)t) : (double)t;
-              emit(i, o, x, (double)lb2 * kLn2 + p.below_base - lnx, (double)la2 * kLn2 + p.above_base - lnx);
+              track(i, lb2, la2, t);
+              if (need_x) {
+                const double lnx = logc ? (double)t : 0.0;
+                const double x = !draw ? cand[o] : logc ? exp((double)t) : (double)t;
+                if (l_out) { l_out[o] = (double)lb2 * kLn2 + p.below_base - lnx; g_out[o] = (double)la2 * kLn2 + p.above_base - lnx; }
+                if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
+              }
             }
           }
         }
@@ -1017,11 +1066,27 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           l = -INFINITY;
           g = 0.0;
         }
-        emit(i, o, x, l, g);
+        emit(i, o, x, l, g, x);
       }
     }
   }
+#ifdef TPE_SAMPLE_TRACE
+  st[2] = wall_clock64();
+  __shared__ unsigned long long s_wend[kTabThreads / 64];
+  if (lane == 0) s_wend[wave] = st[2];
+  __syncthreads();
+  st[4] = 0;
+  for (int q = 0; q < kTabThreads / 64; ++q) st[4] = st[4] > s_wend[q] ? st[4] : s_wend[q];
+#endif
   if (cur >= 0) flush();
+#ifdef TPE_SAMPLE_TRACE
+  st[3] = wall_clock64();
+  if (threadIdx.x == 0 && (blockIdx.x % 16) == 0)
+    printf("k_sample_tab wg %d start %llu stage %llu tiles %llu flush %llu slowest_wave_tiles %llu exact %d\n",
+           (int)blockIdx.x, (unsigned long long)st[0], (unsigned long long)(st[1] - st[0]),
+           (unsigned long long)(st[2] - st[1]), (unsigned long long)(st[3] - st[2]),
+           (unsigned long long)(st[4] - st[1]), s_exact);
+#endif
 }
 
 // row of `part` a work item writes: its tile's first work item + its split

@@ -150,6 +150,7 @@ class Engine(object):
         self._bufs = {}
         self._pinned = None
         self._ws = None                   # cached tpe_level_ws (run_level)
+        self._tree_out = ((ctypes.c_int32 * 2)(), N.LevelNeed())   # suggest_tree's path / need records
         # when a dict: every run() times each stage with HIP events on the
         # launch stream and appends (ms, CE of the launch) under the kernel name;
         # profile_repeat > 1 re-issues each (idempotent) stage back to back and
@@ -614,8 +615,7 @@ class Engine(object):
         nl, n = len(labels), len(ids)
         values = np.empty((n, nl))
         active = np.empty((n, nl), dtype=np.int8)
-        path = (ctypes.c_int32 * 2)()
-        need = N.LevelNeed()
+        path, need = self._tree_out
         seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
         stream = torch.cuda.current_stream(self.device).cuda_stream
         prof = self.profile is not None

@@ -356,16 +356,15 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     if res is None:
         return None
     values, active = res
-    vi = np.where(active != 0, values, 0.0).astype(np.int64)
     order = table.level_order()
     cols = _tree_static(table)[2]
+    i64, f64 = np.int64, np.float64
     out = []
-    for j in range(len(new_ids)):
+    for act, v in zip(active.tolist(), values.tolist()):
         d = dict.fromkeys(order)
-        act, v, iv = active[j].tolist(), values[j], vi[j]
         for label, ix, fam in cols:
-            if act[ix]:
-                d[label] = iv[ix] if fam == N.FAM_CATEGORICAL else v[ix]   # np.int64 / np.float64 scalars
+            if act[ix]:              # the reference's value types: np.int64 categories, np.float64 values
+                d[label] = i64(v[ix]) if fam == N.FAM_CATEGORICAL else f64(v[ix])
         out.append(d)
     return out
 
