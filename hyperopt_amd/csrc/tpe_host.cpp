@@ -56,6 +56,7 @@ constexpr int kTailMinTiles = 32;      // per-tile tail splits from 32 tiles (64
 constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e)): a = kAScale / max(sigma, EPS)
 constexpr double kTabEta = 0.05;                  // a_max * h <= kTabEta for every cell of half-width h
 constexpr int64_t kTabMaxCells = 65536;           // per side; more: per-candidate scoring
+constexpr int64_t kTabRowUnits = 3;               // 16-B units of a cell row (include/tpe_hip.h)
 constexpr double kTabMinRatio = 8.0, kTabMinRatioDevFit = 64.0;   // candidates per cell row for tables
 constexpr int64_t kTabMaxLattice = 1 << 18;       // lattice values per quantized label
 // TPE_TABLES=0 turns tabulated scoring off (A/B and tests); read per call
@@ -850,7 +851,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
   if (below_idx.empty()) below_idx.push_back(0);
-  // ---- score tables: 16-B units (a cell row is 4 units, 64-B aligned; a lattice row 1) ----
+  // ---- score tables: 16-B units (a cell row is 3 units, a lattice row 1) ----
   int64_t tab_units = 0;
   for (int32_t li = 0; li < n_labels; ++li) {
     tpe_problem& p = lab[li];
@@ -858,12 +859,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     if (tmode[li] == TPE_TAB_CELLS) {
       for (int sd = 0; sd < 2; ++sd) {
         const int64_t n = sd ? tn1[li] : tn0[li];
-        tab_units = (tab_units + 3) & ~(int64_t)3;
         p.tab_off[sd] = (int32_t)tab_units;
         p.tab_n[sd] = (int32_t)n;
         p.tab_lo[sd] = (float)tklo[li];
         p.tab_inv[sd] = (float)((double)n / (tkhi[li] - tklo[li]));
-        tab_units += 4 * n;
+        tab_units += kTabRowUnits * n;
       }
     } else if (tmode[li] == TPE_TAB_LATTICE) {
       p.tab_off[0] = (int32_t)tab_units;

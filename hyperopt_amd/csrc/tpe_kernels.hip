@@ -724,7 +724,8 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
 // other slots of its tiles are empty).  Nothing per candidate is stored unless
 // asked for (l_out / TPE_BATCH_WRITE_CAND).
 constexpr int kTabThreads = 1024;
-constexpr int kTabLdsCells = 1536;                  // 96 KiB of 64-B cell rows
+constexpr int kTabLdsCells = 2048;                  // 96 KiB of 48-B cell rows
+static_assert(TPE_TAB_ROW_UNITS == 3 && kTabMoments == 11, "a cell row: 11 moments and the shift in 3 float4");
 constexpr int kGuide = 64;                          // CDF guide entries
 constexpr int kTabMaxTilesPerWg = 16;
 static_assert(kTile % kTabThreads == 0, "tabulated sample tiling");
@@ -741,19 +742,19 @@ __device__ __forceinline__ int guided_comp(const double* __restrict__ cum, const
 }
 
 // log2 of one mixture side's sum at t from its cell rows (LDS or global); NAN
-// when t lies outside the cells, in a flagged cell, or the series is not
-// positive (the caller then sums the mixture exactly)
+// when t lies outside the cells, in a flagged cell (NaN shift), or the series is
+// not positive (the caller then sums the mixture exactly).  w = 1 / inv, ih =
+// 1 / h: the cell centre and u as k_tables forms them.
 // (row j's k-th float4 at rows[k * stride + j * step]: global rows are
-// contiguous, stride 1 / step 4; LDS rows are split in planes, stride
+// contiguous, stride 1 / step 3; LDS rows are split in planes, stride
 // kTabLdsCells / step 1, so random rows of a wave spread over the banks)
-__device__ __forceinline__ float cell_log2_lds(float lo, float inv, int n, const float4* __restrict__ rows,
-                                               int stride, int step, float t) {
+__device__ __forceinline__ float cell_log2_lds(float lo, float inv, float w, float ih, int n,
+                                               const float4* __restrict__ rows, int stride, int step, float t) {
   const float gj = floorf((t - lo) * inv);
   if (!(gj >= 0.f && gj < (float)n)) return NAN;
   const float4* __restrict__ r = rows + step * (int)gj;
-  const float4 a = r[0], b = r[stride], c = r[2 * stride], d = r[3 * stride];
-  if (d.z != 0.f) return NAN;
-  const float u = (t - d.x) * d.y;
+  const float4 a = r[0], b = r[stride], c = r[2 * stride];
+  const float u = (t - __builtin_fmaf(gj + 0.5f, w, lo)) * ih;
   float sm = c.z;
   sm = __builtin_fmaf(sm, u, c.y); sm = __builtin_fmaf(sm, u, c.x);
   sm = __builtin_fmaf(sm, u, b.w); sm = __builtin_fmaf(sm, u, b.z); sm = __builtin_fmaf(sm, u, b.y);
@@ -777,7 +778,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
                                                             const float4* __restrict__ comp32,
                                                             const float4* __restrict__ tab,
                                                             tpe_result* __restrict__ run_best) {
-  __shared__ float4 tab_lds[4 * kTabLdsCells];
+  __shared__ float4 tab_lds[TPE_TAB_ROW_UNITS * kTabLdsCells];
   __shared__ double cum_lds[kCumLds];
 #ifdef TPE_SAMPLE_TRACE                      // debug builds only: per-phase workgroup timing
   uint64_t st[5] = {(uint64_t)wall_clock64(), 0, 0, 0, 0};
@@ -897,14 +898,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       if (tab_in_lds) {                              // plane k of cell j at tab_lds[k * kTabLdsCells + j]
         // workgroups start at different 16-KiB windows of the tables (every CU
         // of the problem stages the same rows: spread the first touches)
-        const int n0 = 4 * p.tab_n[0], n1 = 4 * p.tab_n[1];
+        const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], n1 = TPE_TAB_ROW_UNITS * p.tab_n[1];
         const int nw = (n0 + n1 + kTabThreads - 1) / kTabThreads;
         const int rot = (int)blockIdx.x % nw;
         for (int u = 0; u < nw; ++u) {
           const int q = ((u + rot) % nw) * kTabThreads + (int)threadIdx.x;
           if (q >= n0 + n1) continue;
           const float4 v = q < n0 ? tab[(int64_t)p.tab_off[0] + q] : tab[(int64_t)p.tab_off[1] + q - n0];
-          tab_lds[(q & 3) * kTabLdsCells + (q >> 2)] = v;
+          tab_lds[(q % TPE_TAB_ROW_UNITS) * kTabLdsCells + q / TPE_TAB_ROW_UNITS] = v;
         }
       }
       __syncthreads();
@@ -941,9 +942,10 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     // read is a plain LDS or global load, never a generic one)
     auto cells_pass = [&](auto TL) {
         const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
+        const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
         const int n0 = p.tab_n[0], n1 = p.tab_n[1];
         constexpr bool kL = decltype(TL)::value;
-        constexpr int stride = kL ? kTabLdsCells : 1, step = kL ? 1 : 4;
+        constexpr int stride = kL ? kTabLdsCells : 1, step = kL ? 1 : TPE_TAB_ROW_UNITS;
         const float4* __restrict__ r0;
         const float4* __restrict__ r1;
         if constexpr (kL) { r0 = tab_lds; r1 = tab_lds + n0; }
@@ -989,8 +991,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             t = NAN;
           }
           tj[j] = t;
-          const float lb2 = cell_log2_lds(lo0, inv0, n0, r0, stride, step, t),
-                    la2 = cell_log2_lds(lo1, inv1, n1, r1, stride, step, t);
+          const float lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, r0, stride, step, t),
+                    la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, r1, stride, step, t);
           if (!(lb2 == lb2) || !(la2 == la2)) { exact |= 1u << j; continue; }
           track(i, lb2, la2, t);
           if (need_x) {                          // per-candidate outputs on request (tests)
@@ -1012,8 +1014,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             const int src = __builtin_ctzll(need);
             need &= need - 1;
             const float t = __shfl(tj[j], src);
-            float lb2 = cell_log2_lds(lo0, inv0, n0, r0, stride, step, t),
-                    la2 = cell_log2_lds(lo1, inv1, n1, r1, stride, step, t);
+            float lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, r0, stride, step, t),
+                    la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, r1, stride, step, t);
             if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
             if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
             if (lane == src) {
@@ -2157,9 +2159,10 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     TT(3);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool live = j < jb.n;                                   // wave-uniform
-    const float inv = p.tab_inv[side];
-    const float c = p.tab_lo[side] + ((float)j + 0.5f) / inv;
-    const float h = 0.5f / inv;
+    // cell centre and half-width exactly as the sample stage forms them (cell_log2_lds)
+    const float w = 1.f / p.tab_inv[side];
+    const float c = __builtin_fmaf((float)j + 0.5f, w, p.tab_lo[side]);
+    const float h = 0.5f * w;
     double M[kTabMoments];
 #pragma unroll
     for (int q = 0; q < kTabMoments; ++q) M[q] = 0.0;
@@ -2196,15 +2199,12 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     sum += __shfl_xor(sum, 2);
     float val = 0.f;
     if (part == 0 && q < kTabMoments) val = (float)sum;
-    // row lanes: moment q from lane 4q, then {mx, c, 1/h, flag, 0}
-    float* row = reinterpret_cast<float*>(tab + jb.off + 4 * j);
+    // row lanes: moment q from lane 4q, then the shift mx (NaN: the cell is flagged)
+    float* row = reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * j);
     const float mv = __shfl(val, 4 * (lane < kTabMoments ? lane : 0));
     float out = lane < kTabMoments ? mv : 0.f;
-    if (lane == 11) out = mx;
-    if (lane == 12) out = c;
-    if (lane == 13) out = 1.f / h;
-    if (lane == 14) out = bad || all_exact ? 1.f : 0.f;
-    if (lane < 16) row[lane] = out;
+    if (lane == kTabMoments) out = bad || all_exact ? NAN : mx;
+    if (lane <= kTabMoments) row[lane] = out;
 #ifdef TPE_TABLES_TRACE
     TT(5);
     if (lane == 0 && (blockIdx.x % 16) == 0 && wave < 2)

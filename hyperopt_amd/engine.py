@@ -286,7 +286,7 @@ class Engine(object):
                             info.update(meta)
             rows.append(info)
 
-        # score tables: 16-B units, a cell row 4 units (64-B aligned), a lattice row 1
+        # score tables: 16-B units, a cell row 3 units, a lattice row 1
         units, jobs, blocks, r0 = 0, [], 0, 0
         for lp, pl, info in zip(problems, plans, rows):
             info['tab_mode'], info['tab_off'], info['tab_n'] = pl['mode'], [0, 0], [0, 0]
@@ -294,11 +294,10 @@ class Engine(object):
             if pl['mode'] == N.TAB_CELLS:
                 for sd in range(2):
                     n = pl['n'][sd]
-                    units = (units + 3) & ~3
                     info['tab_off'][sd], info['tab_n'][sd] = units, n
                     info['tab_lo'][sd] = float(np.float32(pl['lo']))
                     info['tab_inv'][sd] = float(np.float32(n / (pl['hi'] - pl['lo'])))
-                    units += 4 * n
+                    units += N.TAB_ROW_UNITS * n
             elif pl['mode'] == N.TAB_LATTICE:
                 info['tab_off'][0], info['tab_n'][0], info['lat_lo'] = units, pl['n'][0], pl['lat_lo']
                 units += pl['n'][0]

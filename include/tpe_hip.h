@@ -45,6 +45,8 @@ extern "C" {
 /* cell rows / lattice values a table workgroup computes (tpe_batch.tab_blocks
  * = sum over jobs of ceil(n / TPE_TAB_PER_BLOCK)) */
 #define TPE_TAB_PER_BLOCK 16
+/* 16-B units of one cell row of a TPE_TAB_CELLS table */
+#define TPE_TAB_ROW_UNITS 3
 
 /* problem families: {Gaussian, log-Gaussian} x {continuous, quantized} + categorical */
 enum {
@@ -158,10 +160,12 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  *     About its centre c a component's term is 2^v exp(B u + G u^2),
  *     u = (t - c) / h, |G| <= 0.0017; a cell row holds the degree-10 Taylor
  *     moments of the sum of the terms within 2^-50 of its largest one
- *     (|B| <= 0.6, truncation < 4e-8 relative) — a 64-B row of floats
- *     {M0..M10, m (log2 shift), c, 1/h, flag, 0}: log2 s(t) = m + log2(sum_n
- *     M_n u^n).  flag != 0 (a significant term too narrow to expand) and t
- *     outside the cells fall back to the exact sum.
+ *     (|B| <= 0.6, truncation < 4e-8 relative) — a 48-B row of floats
+ *     {M0..M10, m (log2 shift)}: log2 s(t) = m + log2(sum_n M_n u^n).  Cell j's
+ *     centre and half-width are c = fma(j + 0.5, w, tab_lo), h = w / 2 with
+ *     w = 1 / tab_inv, all in f32 (the table and the sample stages compute them
+ *     alike).  m = NaN (a significant term too narrow to expand) and t outside
+ *     the cells fall back to the exact sum.
  *   TPE_TAB_LATTICE (families 2/3): every candidate is x = m q (np.round,
  *     tpe.py:90-93, 248-249); row m - lat_lo of the table (tab_n[0] rows of
  *     double2 {l, g}, float64, reference operation order per component) holds

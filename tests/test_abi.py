@@ -150,7 +150,7 @@ def test_level_run_reports_space_without_gpu(monkeypatch):
     assert need.cand == 2 << 20 and need.result == 2 and need.best == 2 * 512 * N.BEST_PER_TILE
     assert need.blob_bytes > 0 and need.pinned_bytes >= need.blob_bytes + 2 * 48
     # 50 above components over [-5, 5): cells of the narrowest bandwidth's scale, both sides
-    assert need.part == 0 and need.tab > 0 and need.tab % 4 == 0
+    assert need.part == 0 and need.tab > 0 and need.tab % N.TAB_ROW_UNITS == 0
     monkeypatch.setenv('TPE_TABLES', '0')
     rc = lib.tpe_level_run(labels, 1, 1 << 20, 5, 0, 0, N.PREC_F32, 0, ctypes.byref(ws), ctypes.byref(need), None,
                            out.ctypes.data)
