@@ -88,8 +88,11 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
-    const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    // one 32x32 -> 64-bit product per multiplier (v_mad_u64_u32) instead of a
+    // mul_hi / mul_lo pair
+    const uint64_t p0 = (uint64_t)M0 * (uint64_t)c0, p1 = (uint64_t)M1 * (uint64_t)c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += W0; k1 += W1;
@@ -928,19 +931,29 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 #endif
     }
     const int cand_start = __builtin_amdgcn_readfirstlane(s_start[gi]);
-    if (!run_best && threadIdx.x < TPE_BEST_PER_TILE)   // (early selection: runs report to run_best)
+    // cells: the next listed tile continuing this one is taken along (4
+    // candidates per thread in flight instead of 2: more independent chains to
+    // hide the LDS and transcendental latencies of one candidate)
+    const bool pair = PREC == TPE_PREC_F32 && cells && gi + 1 < n_my &&
+                      __builtin_amdgcn_readfirstlane(s_prob[gi + 1]) == pid &&
+                      __builtin_amdgcn_readfirstlane(s_start[gi + 1]) == cand_start + kTile;
+    if (!run_best && threadIdx.x < TPE_BEST_PER_TILE) {   // (early selection: runs report to run_best)
       tile_best[(int64_t)tile * TPE_BEST_PER_TILE + threadIdx.x] = tpe_best{0, 0, 0, -1};
+      if (pair) tile_best[(int64_t)s_tile[gi + 1] * TPE_BEST_PER_TILE + threadIdx.x] = tpe_best{0, 0, 0, -1};
+    }
     float lo_f, hi_f;
     f32_bounds(p, lo_f, hi_f);
     const double* S = samp + 8 * (int64_t)p.samp_off;
     const bool logc = p.family == TPE_FAM_LOGGAUSS;
     // a thread's candidates are consecutive: an f32 Philox block serves two of them
-    const int first = cand_start + kTabPer * (int)threadIdx.x;
+    const int first = cand_start + (pair ? 2 * kTabPer : kTabPer) * (int)threadIdx.x;
     uint32_t exact = 0;                              // candidates the cell tables do not cover (rare)
-    float tj[kTabPer];
+    float tj[2 * kTabPer];
     // cells; TL: the tables are in LDS (separate instantiations, so every table
-    // read is a plain LDS or global load, never a generic one)
-    auto cells_pass = [&](auto TL) {
+    // read is a plain LDS or global load, never a generic one); NPC: candidates
+    // per thread (kTabPer, or 2 kTabPer for a tile pair)
+    auto cells_pass = [&](auto TL, auto NPC) {
+        constexpr int NP = decltype(NPC)::value;
         const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
         const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
         const int n0 = p.tab_n[0], n1 = p.tab_n[1];
@@ -952,12 +965,12 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         else { r0 = tab + p.tab_off[0]; r1 = tab + p.tab_off[1]; }
         // the pair's uniforms (draw_uniforms' f32 definition): one Philox block
         // per two candidates when the first one's global index is even
-        DrawU du[kTabPer];
+        DrawU du[NP];
         if (draw && in_lds) {
           const uint64_t g0 = (uint64_t)p.cand_base + (uint64_t)first;
           if ((g0 & 1) == 0) {
 #pragma unroll
-            for (int j = 0; j < kTabPer; j += 2) {
+            for (int j = 0; j < NP; j += 2) {
               const uint64_t blk = (g0 + (uint64_t)j) >> 1;
               const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
               du[j] = DrawU{u01w(r.x), u01f(r.y), 0.0};
@@ -965,11 +978,11 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             }
           } else {
 #pragma unroll
-            for (int j = 0; j < kTabPer; ++j) du[j] = draw_uniforms(p, first + j, TPE_PREC_F32);
+            for (int j = 0; j < NP; ++j) du[j] = draw_uniforms(p, first + j, TPE_PREC_F32);
           }
         }
 #pragma unroll
-        for (int j = 0; j < kTabPer; ++j) {
+        for (int j = 0; j < NP; ++j) {
           const int i = first + j;
           tj[j] = NAN;
           if (i >= p.n_cand) continue;
@@ -1005,7 +1018,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         // candidates outside the cells or in flagged ones: summed exactly by the
         // whole wave, one candidate at a time
 #pragma unroll
-        for (int j = 0; j < kTabPer; ++j) {
+        for (int j = 0; j < NP; ++j) {
           unsigned long long need = __ballot((exact >> j) & 1u);
 #ifdef TPE_SAMPLE_TRACE
           if (lane == 0) atomicAdd(&s_exact, (int)__popcll(need));
@@ -1034,10 +1047,13 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     };
     if constexpr (PREC == TPE_PREC_F32) {
       if (cells) {
-        if (tab_in_lds) cells_pass(std::true_type{});
-        else cells_pass(std::false_type{});
+        using P2 = std::integral_constant<int, kTabPer>;
+        using P4 = std::integral_constant<int, 2 * kTabPer>;
+        if (tab_in_lds) { if (pair) cells_pass(std::true_type{}, P4{}); else cells_pass(std::true_type{}, P2{}); }
+        else { if (pair) cells_pass(std::false_type{}, P4{}); else cells_pass(std::false_type{}, P2{}); }
       }
     }
+    if (pair) ++gi;                                  // the pair's second tile is done
     if (!cells) {                                    // lattice: exact {l, g} per quantized value
       for (int j = 0; j < kTabPer; ++j) {
         const int i = first + j;
