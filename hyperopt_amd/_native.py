@@ -17,7 +17,7 @@ BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate til
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
 F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE = 1, 2, 4, 8, 16
 TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
-TAB_PER_BLOCK = 16                 # include/tpe_hip.h TPE_TAB_PER_BLOCK
+TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
 BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS, BATCH_TAB_EXACT = 1, 2, 4, 8, 16
 PREC_F32, PREC_F64 = 0, 1

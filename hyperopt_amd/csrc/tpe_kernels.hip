@@ -572,7 +572,7 @@ __device__ __forceinline__ void block_best(double sc, int64_t orig, double l, do
 // (include/tpe_hip.h "Tabulated scoring").  Cell row: 16 floats {M0..M10, m,
 // c, 1/h, flag, 0}.
 constexpr int kTabMoments = 11;        // degree-10 Taylor moments per cell
-constexpr int kTabStageRowsDecl = 6144; // component rows a table workgroup stages in LDS (k_tables)
+constexpr int kTabStageRowsDecl = 4096; // component rows a table workgroup stages in LDS (k_tables; 64 KiB: two workgroups per CU)
 constexpr float kTabDrop = 50.f;       // terms below 2^-50 of the cell's largest are dropped
 
 // Draws (when `draw`) and writes the sort keys: (sorted problem << key_bits) |
@@ -1688,11 +1688,12 @@ __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__
   __syncthreads();
   tpe_best b{0, 0, 0, -1};
   constexpr int kLazyPer = 4;              // draws per thread per round
-  for (int base = 0; base < p.n_cand; base += kLazyPer * kSelThreads) {
+  const int nt = (int)blockDim.x;          // (k_select: 1024 threads, the table stage: 512)
+  for (int base = 0; base < p.n_cand; base += kLazyPer * nt) {
     int c[kLazyPer];
 #pragma unroll
     for (int j = 0; j < kLazyPer; ++j) {
-      const int i = base + j * kSelThreads + (int)threadIdx.x;
+      const int i = base + j * nt + (int)threadIdx.x;
       c[j] = i < p.n_cand ? draw_category(p, cum, i) : -1;
     }
 #pragma unroll
@@ -1700,7 +1701,7 @@ __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__
       for (int cc = 0; cc < K; ++cc) {     // one LDS atomic per wave and category
         const unsigned long long m = __ballot(c[j] == cc);
         if ((threadIdx.x & 63) == 0 && m)
-          atomicMin(&first[cc], base + j * kSelThreads + (int)(threadIdx.x & ~63) + __builtin_ctzll(m));
+          atomicMin(&first[cc], base + j * nt + (int)(threadIdx.x & ~63) + __builtin_ctzll(m));
       }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2122,12 +2123,12 @@ __device__ void lattice_row(const tpe_problem& p, int j, const double4* __restri
   if (lane == 0) rows[j] = make_double2(log(sb) + p.below_base, log(sa) + p.above_base);
 }
 
-// 1024-thread workgroups, one wave per cell row / lattice value
+// 512-thread workgroups, one wave per cell row / lattice value
 // (TPE_TAB_PER_BLOCK per workgroup).  A cell job's workgroup first stages its
 // side's component rows in LDS (unless pruned or too many), so both passes of
 // every cell read LDS only.
 constexpr int kTabTblThreads = 64 * TPE_TAB_PER_BLOCK;
-constexpr int kTabStageRows = kTabStageRowsDecl;    // 96 KiB of float4 rows
+constexpr int kTabStageRows = kTabStageRowsDecl;    // 64 KiB of float4 rows
 static_assert(TPE_TAB_PER_BLOCK * kTabMoments * 64 * 8 <= kTabStageRows * 16, "moment reduction fits the staging LDS");
 __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __restrict__ P,
                                                           const tpe_tab_job* __restrict__ J, int n_jobs,
@@ -2142,7 +2143,15 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     // early selection: one block per problem selects a lazy categorical
     // problem right here (it needs no tables)
     const tpe_problem& q = P[(int)blockIdx.x - tab_blocks];
+#ifdef TPE_TABLES_TRACE
+    const uint64_t t_lazy = wall_clock64();
+#endif
     if (lazy_ok && lazy_eligible(q)) select_cat_lazy(q, samp, comp64, result + ((int)blockIdx.x - tab_blocks));
+#ifdef TPE_TABLES_TRACE
+    if (threadIdx.x == 0)
+      printf("k_tables lazy blk %d problem %d: %llu\n", (int)blockIdx.x, (int)blockIdx.x - tab_blocks,
+             (unsigned long long)(wall_clock64() - t_lazy));
+#endif
     return;
   }
 #ifdef TPE_TABLES_TRACE                     // debug builds only: per-phase wave timing

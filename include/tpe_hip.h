@@ -44,7 +44,7 @@ extern "C" {
 #define TPE_SAMPLE_LDS_ROWS 1024
 /* cell rows / lattice values a table workgroup computes (tpe_batch.tab_blocks
  * = sum over jobs of ceil(n / TPE_TAB_PER_BLOCK)) */
-#define TPE_TAB_PER_BLOCK 16
+#define TPE_TAB_PER_BLOCK 8
 /* 16-B units of one cell row of a TPE_TAB_CELLS table */
 #define TPE_TAB_ROW_UNITS 3
 
