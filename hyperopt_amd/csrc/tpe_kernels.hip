@@ -1687,18 +1687,21 @@ __device__ void select_cat_lazy(const tpe_problem& p, const double* __restrict__
   }
   __syncthreads();
   tpe_best b{0, 0, 0, -1};
-  constexpr int kLazyPer = 4;              // draws per thread per round
-  const int nt = (int)blockDim.x;          // (k_select: 1024 threads, the table stage: 512)
-  for (int base = 0; base < p.n_cand; base += kLazyPer * nt) {
-    int c[kLazyPer];
+  // 4096 draws per round whatever the workgroup size (k_select: 1024 threads x 4,
+  // the table stage: 512 x 8)
+  constexpr int kLazyRound = 4096, kLazyMaxPer = 8;
+  const int nt = (int)blockDim.x;
+  const int per = kLazyRound / nt;
+  for (int base = 0; base < p.n_cand; base += kLazyRound) {
+    int c[kLazyMaxPer];
 #pragma unroll
-    for (int j = 0; j < kLazyPer; ++j) {
+    for (int j = 0; j < kLazyMaxPer; ++j) {
       const int i = base + j * nt + (int)threadIdx.x;
-      c[j] = i < p.n_cand ? draw_category(p, cum, i) : -1;
+      c[j] = j < per && i < p.n_cand ? draw_category(p, cum, i) : -1;
     }
 #pragma unroll
-    for (int j = 0; j < kLazyPer; ++j)
-      for (int cc = 0; cc < K; ++cc) {     // one LDS atomic per wave and category
+    for (int j = 0; j < kLazyMaxPer; ++j)
+      for (int cc = 0; cc < K && j < per; ++cc) {     // one LDS atomic per wave and category
         const unsigned long long m = __ballot(c[j] == cc);
         if ((threadIdx.x & 63) == 0 && m)
           atomicMin(&first[cc], base + j * nt + (int)(threadIdx.x & ~63) + __builtin_ctzll(m));
