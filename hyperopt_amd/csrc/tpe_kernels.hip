@@ -111,6 +111,15 @@ __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
 __device__ __forceinline__ double u01w(uint32_t a) { return ((double)a + 0.5) * 2.3283064365386963e-10; }
 
 // ---------------------------------------------------------- argmax order
+// better() on an f32 key with a 32-bit index (the cells candidates of k_sample_tab)
+__device__ __forceinline__ bool better32(float d, int i, float bd, int bi) {
+  if (bi < 0) return i >= 0;
+  if (i < 0) return false;
+  const bool n = d != d, bn = bd != bd;
+  if (n || bn) return n && (!bn || i < bi);
+  return d > bd || (d == bd && i < bi);
+}
+
 // np.argmax: NaN is the maximum (first NaN wins), otherwise the largest value,
 // first index on ties.
 __device__ __forceinline__ bool better(double s, int64_t i, double bs, int64_t bi) {
@@ -787,6 +796,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   uint64_t st[5] = {(uint64_t)wall_clock64(), 0, 0, 0, 0};
   __shared__ int s_exact;
   if (threadIdx.x == 0) s_exact = 0;
+  uint64_t g_ft[3] = {0, 0, 0};              // flush: after the fold, after its barrier, after the record
 #endif
   __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
   __shared__ int guide[kGuide];
@@ -813,24 +823,84 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   int fi = -1;
   auto track = [&](int i, float lb2, float la2, float t) {
     const float d = lb2 - la2;
-    bool win;                                // better() in f32: NaN first, then larger, then lower index
-    if (fi < 0) win = true;
-    else if (d != d || fd != fd) win = d != d && (fd == fd || i < fi);
-    else win = d > fd || (d == fd && i < fi);
-    if (win) { fd = d; fi = i; flb = lb2; fla = la2; ft = t; }
+    if (better32(d, i, fd, fi)) { fd = d; fi = i; flb = lb2; fla = la2; ft = t; }
   };
   // the run's problem fields the flush needs (no global reads at the run's end)
   int64_t run_cand_base = 0, run_cand_off = 0;
   double run_bb = 0.0, run_ab = 0.0;
-  bool run_logc = false, run_exp = false, run_drawn = false;
+  bool run_logc = false, run_exp = false, run_drawn = false, run_cells = false;
   // the run's best -> slot 0 of its first tile (block reduction)
-  auto flush = [&]() {
-    if (fi >= 0) {
-      const double lnx = run_logc ? (double)ft : 0.0;
-      const double l = (double)flb * kLn2 + run_bb - lnx, g = (double)fla * kLn2 + run_ab - lnx;
-      if (better(l - g, fi, bs, bi)) { bs = l - g; bl = l; bg = g; bi = fi; bv = (double)ft; }
+  // the run's record (lane 0 of wave 0): l, g and the f64 score of its best
+  auto record = [&](double s2, double l2, double g2, int64_t i2, double v2) {
+    if (run_best) {
+      // early selection: the run's best with its value (the draw it kept — what
+      // the select stage's redraw would give), straight to host-visible memory
+      tpe_result r;
+      r.score = s2; r.l = l2; r.g = g2; r.idx = i2; r.value = 0.0;
+      r.global_idx = i2 >= 0 ? run_cand_base + i2 : -1;
+      if (i2 >= 0) r.value = run_drawn ? (run_exp ? exp(v2) : v2) : cand[run_cand_off + i2];
+      run_best[run_tile] = r;
+#ifdef TPE_SAMPLE_TRACE
+      g_ft[2] = wall_clock64();
+#endif
+    } else {
+      tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
+      d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
     }
-    fi = -1;
+  };
+  __shared__ float wf[4][kTabThreads / 64];
+  __shared__ int wfi[kTabThreads / 64];
+  // the run's best -> its record (block reduction)
+  auto flush = [&]() {
+#ifdef TPE_SAMPLE_TRACE
+    if (threadIdx.x == 0) g_ft[0] = wall_clock64();
+#endif
+    if (run_cells) {
+      // cells run: argmax of the f32 keys (two 32-bit shuffles per round, not five
+      // 64-bit ones), then the winner's log2 sums and draw by lane read-out
+      float d = fd;
+      int i = fi;
+      for (int off = 32; off > 0; off >>= 1) {
+        const float od = __shfl_xor(d, off);
+        const int oi = __shfl_xor(i, off);
+        if (better32(od, oi, d, i)) { d = od; i = oi; }
+      }
+      const unsigned long long m = __ballot(i >= 0 && fi == i);
+      const int src = m ? (int)__builtin_ctzll(m) : 0;
+      const float wlb = __shfl(flb, src), wla = __shfl(fla, src), wt = __shfl(ft, src);
+      if (lane == 0) { wf[0][wave] = d; wf[1][wave] = wlb; wf[2][wave] = wla; wf[3][wave] = wt; wfi[wave] = i; }
+      __syncthreads();
+#ifdef TPE_SAMPLE_TRACE
+      if (threadIdx.x == 0) g_ft[1] = wall_clock64();
+#endif
+      if (wave == 0) {                       // lanes 0..15 hold the waves' bests
+        const bool in = lane < kTabThreads / 64;
+        const int q = in ? lane : 0;
+        float d2 = wf[0][q];
+        int i2 = in ? wfi[q] : -1;
+        for (int off = 8; off > 0; off >>= 1) {
+          const float od = __shfl_xor(d2, off);
+          const int oi = __shfl_xor(i2, off);
+          if (better32(od, oi, d2, i2)) { d2 = od; i2 = oi; }
+        }
+        const unsigned long long m2 = __ballot(in && i2 >= 0 && wfi[q] == i2);
+        const int w2 = m2 ? (int)__builtin_ctzll(m2) : 0;
+        if (lane == 0) {
+          double s2 = 0.0, l2 = 0.0, g2 = 0.0, v2 = 0.0;
+          if (i2 >= 0) {
+            const float t = wf[3][w2];
+            const double lnx = run_logc ? (double)t : 0.0;
+            l2 = (double)wf[1][w2] * kLn2 + run_bb - lnx;
+            g2 = (double)wf[2][w2] * kLn2 + run_ab - lnx;
+            s2 = l2 - g2;
+            v2 = (double)t;
+          }
+          record(s2, l2, g2, (int64_t)i2, v2);
+        }
+      }
+      fi = -1;
+      return;
+    }
     for (int off = 32; off > 0; off >>= 1) {
       const double os = __shfl_xor(bs, off), ol = __shfl_xor(bl, off), og = __shfl_xor(bg, off);
       const double ov = __shfl_xor(bv, off);
@@ -840,6 +910,9 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     __shared__ double wv[kTabThreads / 64];
     if (lane == 0) { wb[wave].score = bs; wb[wave].l = bl; wb[wave].g = bg; wb[wave].idx = bi; wv[wave] = bv; }
     __syncthreads();
+#ifdef TPE_SAMPLE_TRACE
+    if (threadIdx.x == 0) g_ft[1] = wall_clock64();
+#endif
     if (wave == 0) {                         // lanes 0..15 hold the waves' bests
       const int q = lane < kTabThreads / 64 ? lane : 0;
       double s2 = wb[q].score, l2 = wb[q].l, g2 = wb[q].g, v2 = wv[q];
@@ -850,21 +923,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         const int64_t oi = __shfl_xor(i2, off);
         if (better(os, oi, s2, i2)) { s2 = os; l2 = ol; g2 = og; i2 = oi; v2 = ov; }
       }
-      if (lane == 0) {
-        if (run_best) {
-          // early selection: the run's best with its value (the draw it kept —
-          // what the select stage's redraw would give), straight to
-          // host-visible memory
-          tpe_result r;
-          r.score = s2; r.l = l2; r.g = g2; r.idx = i2; r.value = 0.0;
-          r.global_idx = i2 >= 0 ? run_cand_base + i2 : -1;
-          if (i2 >= 0) r.value = run_drawn ? (run_exp ? exp(v2) : v2) : cand[run_cand_off + i2];
-          run_best[run_tile] = r;
-        } else {
-          tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
-          d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
-        }
-      }
+      if (lane == 0) record(s2, l2, g2, i2, v2);
     }
     bs = 0.0; bl = 0.0; bg = 0.0; bv = 0.0; bi = -1;
   };
@@ -926,6 +985,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       run_logc = p.family == TPE_FAM_LOGGAUSS;
       run_exp = cells && run_logc;
       run_drawn = draw && p.samp_len > 0;
+      run_cells = PREC == TPE_PREC_F32 && cells;
 #ifdef TPE_SAMPLE_TRACE
       if (!st[1]) st[1] = wall_clock64();
 #endif
@@ -1100,10 +1160,12 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 #ifdef TPE_SAMPLE_TRACE
   st[3] = wall_clock64();
   if (threadIdx.x == 0 && (blockIdx.x % 16) == 0)
-    printf("k_sample_tab wg %d start %llu stage %llu tiles %llu flush %llu slowest_wave_tiles %llu exact %d\n",
+    printf("k_sample_tab wg %d start %llu stage %llu tiles %llu flush %llu slowest_wave_tiles %llu exact %d "
+           "fold %llu wave-reduce+barrier %llu wg-reduce+record %llu\n",
            (int)blockIdx.x, (unsigned long long)st[0], (unsigned long long)(st[1] - st[0]),
            (unsigned long long)(st[2] - st[1]), (unsigned long long)(st[3] - st[2]),
-           (unsigned long long)(st[4] - st[1]), s_exact);
+           (unsigned long long)(st[4] - st[1]), s_exact, (unsigned long long)(g_ft[0] - st[4]),
+           (unsigned long long)(g_ft[1] - g_ft[0]), (unsigned long long)(g_ft[2] - g_ft[1]));
 #endif
 }
 
