@@ -320,8 +320,8 @@ int64_t tpe_host_fit_parzen(const double* obs, int64_t n, const int64_t* order, 
   return fit_sorted<false>(svp, rkp, n, prior_weight, prior_mu, prior_sigma, lf, w, mu, sigma);
 }
 
-// (AVX2 clones: -ffp-contract=off holds in both, so the results are identical)
-__attribute__((target_clones("avx2", "default")))
+// (AVX-512 / AVX2 clones: -ffp-contract=off holds in all, so the results are identical)
+__attribute__((target_clones("avx512f", "avx2", "default")))
 int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* order, int64_t n,
                        const int64_t* below_tids, int64_t n_bt, double prior_weight, double prior_mu,
                        double prior_sigma, int32_t lf, double* out, int64_t* out_k) {
@@ -389,7 +389,7 @@ int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* orde
   return TPE_OK;
 }
 
-__attribute__((target_clones("avx2", "default")))
+__attribute__((target_clones("avx512f", "avx2", "default")))
 int tpe_host_cat_probs(const int64_t* obs, int64_t n, int32_t upper, const double* p_prior, double prior_weight,
                        int32_t lf, double* out) {
   if (upper <= 0 || n < 0 || !out) return TPE_E_ARG;
@@ -454,7 +454,7 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
 // the pack's straight-line table loops vectorise: an AVX2 clone is picked at
 // load time on hosts that have it (-ffp-contract=off holds in both clones, so
 // the tables are bit-identical)
-__attribute__((target_clones("avx2", "default")))
+__attribute__((target_clones("avx512f", "avx2", "default")))
 int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
                         int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
                         tpe_pack_info* info) {

@@ -95,3 +95,16 @@ def test_native_tree_hands_quantized_labels_to_general_path():
     nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, 5, n_EI_candidates=1 << 16)))
     assert path is None and nat == gen
     assert int(nat['model']) == 1
+
+
+def test_engine_stream_follows_torch():
+    """Engine._stream (the raw current-stream accessor) is torch's current
+    stream, also inside a torch.cuda.stream context."""
+    import torch
+    from hyperopt_amd.engine import get_engine
+    eng = get_engine()
+    assert eng._stream() == torch.cuda.current_stream(eng.device).cuda_stream
+    s = torch.cuda.Stream(device=eng.device)
+    with torch.cuda.stream(s):
+        assert eng._stream() == s.cuda_stream
+    assert eng._stream() == torch.cuda.current_stream(eng.device).cuda_stream

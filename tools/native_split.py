@@ -61,6 +61,18 @@ def main():
         tot_fit += t
         print('  fit %-14s n_obs %6d  %7.1f us' % (lab, n, t))
     print('  fits total                     %7.1f us' % tot_fit)
+    # the packer alone on the four labels' native fits (what tpe_suggest_tree packs)
+    from hyperopt_amd.engine import LevelProblem
+    fits = tpe._Fits(table, hist, H.split_below(hist, 0.25), 1.0, eng)
+    probs = [LevelProblem(fits.get(table.by_label[l]), table.by_label[l].index, [bench.N_HISTORY])
+             for l in ('model', 'svm_C', 'svm_kernel', 'svm_rbf_gamma')]
+    labels_in, keep_in = eng._labels(probs)
+    info = N.PackInfo()
+    pin = eng._pinned
+    if pin is not None:
+        t = best_of(lambda: lib.tpe_host_pack_level(labels_in, len(probs), bench.C_PER_GPU, 5, 0, 0, 0,
+                                                    pin.data_ptr(), pin.numel(), ctypes.byref(info)), reps)
+        print('  tpe_host_pack_level (4 labels)  %7.1f us' % t)
     ids = np.array([bench.N_HISTORY], dtype=np.int64)
     C = bench.C_PER_GPU
 
