@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 12
+ABI_VERSION = 13
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -190,13 +190,17 @@ class TreeLabel(ctypes.Structure):
         ('order', ctypes.c_void_p), ('n_obs', ctypes.c_int64),
         ('depth', ctypes.c_int32), ('n_parents', ctypes.c_int32),
         ('parent', ctypes.c_int32 * TREE_MAX_PARENTS), ('parent_cat', ctypes.c_int32 * TREE_MAX_PARENTS),
+        ('q', ctypes.c_double),
+        ('host_w', ctypes.c_void_p * 2), ('host_mu', ctypes.c_void_p * 2), ('host_sigma', ctypes.c_void_p * 2),
+        ('host_k', ctypes.c_int64 * 2),
     ]
 
 
 TREE_LABEL_DTYPE = np.dtype(dict(
     names=[f for f, _ in TreeLabel._fields_],
     formats=['<i4', '<i4', '<i4', '<i4', '<f8', '<f8', '<f8', '<f8', '<u8', '<u8', '<u8', '<u8', '<i8', '<i4', '<i4',
-             ('<i4', (TREE_MAX_PARENTS,)), ('<i4', (TREE_MAX_PARENTS,))],
+             ('<i4', (TREE_MAX_PARENTS,)), ('<i4', (TREE_MAX_PARENTS,)), '<f8', ('<u8', (2,)), ('<u8', (2,)),
+             ('<u8', (2,)), ('<i8', (2,))],
     offsets=[getattr(TreeLabel, f).offset for f, _ in TreeLabel._fields_], itemsize=ctypes.sizeof(TreeLabel)))
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
@@ -281,7 +285,7 @@ def load(path=LIB_PATH):
     lib.tpe_level_run.restype = ctypes.c_int
     I32 = ctypes.c_int32
     lib.tpe_suggest_tree.argtypes = [P, I32, P, I64, D, I32, P, I32, I32, ctypes.c_uint64, D, I64, I32,
-                                     ctypes.POINTER(LevelWS), ctypes.POINTER(LevelNeed), P, P, P, P]
+                                     ctypes.POINTER(LevelWS), ctypes.POINTER(LevelNeed), P, P, P, P, P]
     lib.tpe_suggest_tree.restype = ctypes.c_int
     lib.tpe_level_profile.argtypes = [ctypes.c_int32]
     lib.tpe_level_profile.restype = ctypes.c_int

@@ -49,6 +49,7 @@ struct Tree {
   std::vector<Fit>* fits;
   std::vector<char> gate;       // label gates another label
   int32_t max_depth;
+  int8_t* need_fit;             // labels the caller must fit (TPE_E_FALLBACK)
 };
 
 int fit_label(Tree& T, int i) {
@@ -56,6 +57,23 @@ int fit_label(Tree& T, int i) {
   if (f.done) return TPE_OK;
   const tpe_tree_label& L = T.L[i];
   const int64_t n = L.n_obs;
+  if (L.host_k[0] > 0) {                      // the caller's fit
+    if (L.host_k[1] <= 0 || !L.host_w[0] || !L.host_w[1] ||
+        (L.family != TPE_FAM_CATEGORICAL && (!L.host_mu[0] || !L.host_mu[1] || !L.host_sigma[0] || !L.host_sigma[1])))
+      return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: incomplete caller fit");
+    for (int sd = 0; sd < 2; ++sd) {
+      f.k[sd] = L.host_k[sd];
+      f.w[sd] = L.host_w[sd];
+      f.mu[sd] = L.family == TPE_FAM_CATEGORICAL ? nullptr : L.host_mu[sd];
+      f.sg[sd] = L.family == TPE_FAM_CATEGORICAL ? nullptr : L.host_sigma[sd];
+    }
+    f.done = true;
+    return TPE_OK;
+  }
+  auto host_fit = [&]() {                     // numpy's tie order decides this fit: the caller's
+    if (T.need_fit) T.need_fit[i] = 1;
+    return TPE_E_FALLBACK;
+  };
   if (n < 0 || (n > 0 && (!L.tids || !L.values))) return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad columns");
   if (L.family == TPE_FAM_CATEGORICAL) {
     if (L.upper <= 0) return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: categorical label without categories");
@@ -69,7 +87,7 @@ int fit_label(Tree& T, int i) {
     f.w[1] = f.buf.data() + L.upper;
     f.mu[0] = f.mu[1] = f.sg[0] = f.sg[1] = nullptr;
   } else if (L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) {
-    if (n > 0 && !L.order) return TPE_E_FALLBACK;                              // a NaN value
+    if (n > 0 && !L.order) return host_fit();                                  // a NaN value
     if (T.device_fit_min > 0 && n >= std::max<int64_t>(T.device_fit_min, 64)) return TPE_E_FALLBACK;
     const size_t cap = (size_t)n + 1;
     f.buf.resize(6 * cap);
@@ -78,7 +96,7 @@ int fit_label(Tree& T, int i) {
     if (rc != TPE_OK)
       return tpe_internal_fail(TPE_E_ARG, "tpe_host_fit_split failed: tids not strictly ascending, a bad order, or a "
                                           "non-positive Parzen bandwidth");
-    if (f.k[0] == 0 || f.k[1] == 0) return TPE_E_FALLBACK;                     // repeated values: numpy's tie order
+    if (f.k[0] == 0 || f.k[1] == 0) return host_fit();                         // repeated values: numpy's tie order
     for (int sd = 0; sd < 2; ++sd) {
       double* b = f.buf.data() + 3 * (size_t)sd * cap;
       f.w[sd] = b;
@@ -86,7 +104,7 @@ int fit_label(Tree& T, int i) {
       f.sg[sd] = b + 2 * cap;
     }
   } else {
-    return TPE_E_FALLBACK;                                                     // quantized: numpy's tie order
+    return host_fit();                                                         // quantized: numpy's tie order
   }
   f.done = true;
   return TPE_OK;
@@ -151,6 +169,7 @@ void label_rec(const tpe_tree_label& L, const Fit& f, const int64_t* ids, int64_
   r.label_ix = L.label_ix;
   r.low = L.low;
   r.high = L.high;
+  r.q = L.q;
   r.below_w = f.w[0]; r.below_mu = f.mu[0]; r.below_sigma = f.sg[0]; r.below_k = f.k[0];
   r.above_w = f.w[1]; r.above_mu = f.mu[1]; r.above_sigma = f.sg[1]; r.above_k = f.k[1];
   r.ids = ids;
@@ -165,11 +184,12 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
                      double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
                      uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
                      const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
-                     int32_t* path) {
+                     int32_t* path, int8_t* need_fit) {
   if (n_labels < 0 || n_ids < 0 || n_cand < 0 || n_below < 0 || (n_labels > 0 && !labels) || (n_ids > 0 && !ids) ||
       (n_below > 0 && !below_tids) || !ws || !need || !path || (n_labels > 0 && n_ids > 0 && (!values || !active)))
     return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad arguments");
   path[0] = path[1] = 0;
+  if (need_fit) memset(need_fit, 0, (size_t)std::max(n_labels, 0));
   static thread_local std::vector<Fit> fits_tl;
   static thread_local std::vector<tpe_label_in> recs_tl;
   static thread_local std::vector<tpe_result> res_tl;
@@ -178,7 +198,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
   std::vector<Fit>& fits = fits_tl;
   if (fits.size() < (size_t)n_labels) fits.resize((size_t)n_labels);
   for (int i = 0; i < n_labels; ++i) fits[(size_t)i].done = false;
-  Tree T{labels, n_labels, below_tids, n_below, prior_weight, lf, device_fit_min, &fits, {}, 0};
+  Tree T{labels, n_labels, below_tids, n_below, prior_weight, lf, device_fit_min, &fits, {}, 0, need_fit};
   T.gate.assign((size_t)n_labels, 0);
   for (int i = 0; i < n_labels; ++i) {
     const tpe_tree_label& L = labels[i];
@@ -216,11 +236,16 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
     if (ok) {
       recs.resize((size_t)n_labels);
       int32_t nr = 0;
+      bool pending = false;                 // labels flagged for the caller's fit: all of them at once
       for (int i = 0; i < n_labels; ++i) {
         if (pred[(size_t)i] == kInactive) continue;
-        if ((rc = fit_label(T, i)) != TPE_OK) return rc;
+        if ((rc = fit_label(T, i)) != TPE_OK) {
+          if (rc == TPE_E_FALLBACK && need_fit && need_fit[i]) { pending = true; continue; }
+          return rc;
+        }
         label_rec(labels[i], fits[(size_t)i], ids, n_ids, recs[(size_t)nr++]);
       }
+      if (pending) return TPE_E_FALLBACK;
       if ((rc = run(nr)) != TPE_OK) return rc;
       bool verified = true;
       int32_t r = 0;
@@ -258,6 +283,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
     recs.clear();
     lvl_ids.clear();
     std::vector<std::pair<int, int64_t>> members;   // (label, first position in lvl_ids)
+    bool pending = false;                   // labels flagged for the caller's fit: all of the level's at once
     for (int i = 0; i < n_labels; ++i) {
       const tpe_tree_label& L = labels[i];
       if (L.depth != d) continue;
@@ -266,9 +292,13 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
         if (is_active(L, chosen.data() + (size_t)j * n_labels)) lvl_ids.push_back(j);
       if ((int64_t)lvl_ids.size() == first) continue;
       const int rc = fit_label(T, i);
-      if (rc != TPE_OK) return rc;
+      if (rc != TPE_OK) {
+        if (rc == TPE_E_FALLBACK && need_fit && need_fit[i]) { pending = true; continue; }
+        return rc;
+      }
       members.emplace_back(i, first);
     }
+    if (pending) return TPE_E_FALLBACK;
     if (members.empty()) continue;
     // the level's id arrays (positions -> new ids), stable now that lvl_ids is complete
     std::vector<int64_t> lvl_new((size_t)lvl_ids.size());

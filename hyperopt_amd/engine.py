@@ -615,10 +615,11 @@ class Engine(object):
         (tpe_suggest_tree): fits, gate prediction and level runs.  ``labels``:
         TREE_LABEL_DTYPE records in label order; ``below_sorted``: int64
         ascending below tids.  Returns (values, active) [n_ids x n_labels], or
-        None when the space or history needs the general path
-        (TPE_E_FALLBACK)."""
+        (None, need_fit) on TPE_E_FALLBACK: need_fit [n_labels] flags the
+        labels the caller must fit and pass back (none: take the general
+        path)."""
         if self.precision != 'fp32':
-            return None
+            return None, np.zeros(len(labels), dtype=np.int8)
         ids = np.ascontiguousarray(ids, dtype=np.int64)
         n_cand = int(n_cand)
         if n_cand < 0 or n_cand >= 2 ** 31:
@@ -626,6 +627,7 @@ class Engine(object):
         nl, n = len(labels), len(ids)
         values = np.empty((n, nl))
         active = np.empty((n, nl), dtype=np.int8)
+        need_fit = np.zeros(nl, dtype=np.int8)
         path, need = self._tree_out
         seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
         stream = self._stream()
@@ -638,14 +640,15 @@ class Engine(object):
             rc = self.lib.tpe_suggest_tree(labels.ctypes.data, nl, below_sorted.ctypes.data, len(below_sorted),
                                            float(prior_weight), int(lf), ids.ctypes.data, n, n_cand, seed64,
                                            float(min_draws), int(self.device_fit_min), fl, ctypes.byref(ws),
-                                           ctypes.byref(need), stream, values.ctypes.data, active.ctypes.data, path)
+                                           ctypes.byref(need), stream, values.ctypes.data, active.ctypes.data, path,
+                                           need_fit.ctypes.data)
             if rc != N.E_SPACE:
                 break
             self._grow(need)
         if prof:
             self.lib.tpe_level_profile(0)
         if rc == N.E_FALLBACK:
-            return None
+            return None, need_fit
         N.check(rc, self.lib, 'tpe_suggest_tree')
         self.last_tree_path = (int(path[0]), int(path[1]))
         if prof and path[1]:

@@ -278,6 +278,8 @@ def _tree_static(table):
             rec['prior_mu'], rec['prior_sigma'] = 0.5 * (a['high'] + a['low']), 1.0 * (a['high'] - a['low'])
         else:
             rec['prior_mu'], rec['prior_sigma'] = float(a['mu']), float(a['sigma'])
+        if a.get('q') is not None:
+            rec['q'] = float(a['q'])
         rec['depth'] = r.depth
         ps = [p for p in r.parents if p is not None]
         if len(ps) > N.TREE_MAX_PARENTS:
@@ -344,18 +346,46 @@ def _tree_labels(table, hist):
 
 def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight):
     """``_choices_philox`` in one native call (tpe_suggest_tree), or None when
-    the space or history needs the general path."""
+    the space or history needs the general path.  Labels the native fits cannot
+    reproduce (quantized ones, sides with repeated values: numpy's argsort tie
+    order decides their weights) come back flagged; they are fitted here
+    exactly as the general path fits them and handed to a second call."""
     if not hist.sorted_obs:
         return None
     tl = _tree_labels(table, hist)
     if tl is None:
         return None
     below = np.sort(np.asarray(below_tids, dtype=np.int64))
-    res = engine.suggest_tree(tl[0], below, prior_weight, DEFAULT_LF, new_ids, C, seed,
-                              SPECULATE_MIN_DRAWS if SPECULATE else -1.0)
-    if res is None:
+    arr, fits, host = tl[0], None, {}
+    # (a level-by-level run learns a deeper level's needs only after the levels above it)
+    for attempt in range(table.n_levels + 1):
+        values, active = engine.suggest_tree(arr, below, prior_weight, DEFAULT_LF, new_ids, C, seed,
+                                             SPECULATE_MIN_DRAWS if SPECULATE else -1.0)
+        if values is not None:
+            break
+        need = np.flatnonzero(active)          # (need_fit on TPE_E_FALLBACK)
+        if not len(need) or any(ix in host for ix in need.tolist()):
+            return None
+        if fits is None:
+            fits = _Fits(table, hist, below_tids, prior_weight, engine)
+            arr = arr.copy()
+        for ix in need.tolist():
+            row = table.rows[ix]
+            post = fits.get(row)
+            if post.above is None:             # (device-fitted: the general path)
+                return None
+            rec = arr[ix]
+            keep = host[ix] = []               # (keeps the fitted arrays alive for the call)
+            for sd, side in enumerate((post.below, post.above)):
+                cols = [np.ascontiguousarray(c, dtype=np.float64) for c in side]
+                keep.append(cols)
+                rec['host_k'][sd] = len(cols[0])
+                rec['host_w'][sd] = cols[0].ctypes.data
+                if not row.categorical:
+                    rec['host_mu'][sd] = cols[1].ctypes.data
+                    rec['host_sigma'][sd] = cols[2].ctypes.data
+    else:
         return None
-    values, active = res
     order = table.level_order()
     cols = _tree_static(table)[2]
     i64, f64 = np.int64, np.float64

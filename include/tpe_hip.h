@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 12
+#define TPE_ABI_VERSION 13
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -558,11 +558,15 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
  * only the history view and the trial documents.
  *
  * Covered: continuous (GAUSS / LOGGAUSS) and categorical labels fitted on the
- * host at TPE_PREC_F32, categorical gates.  Anything else returns
- * TPE_E_FALLBACK (nothing is written; a device batch may have run): the caller
- * takes its general path — quantized labels and sides with repeated values
- * (numpy's argsort tie order decides their weights), missing value orders
- * (NaN), labels large enough for the device Parzen fit, non-categorical gates.
+ * host at TPE_PREC_F32, categorical gates, and any label whose fit the caller
+ * supplies (host_w/mu/sigma/k).  A label the tree needs that it cannot fit —
+ * quantized labels and sides with repeated values (numpy's argsort tie order
+ * decides their weights), missing value orders (NaN) — is flagged in need_fit
+ * and TPE_E_FALLBACK returned: the caller fits those labels (exactly as the
+ * reference) and calls again with their fits.  Labels large enough for the
+ * device Parzen fit and non-categorical gates return TPE_E_FALLBACK with no
+ * flag: the caller takes its general path.  (On TPE_E_FALLBACK nothing is
+ * written; a device batch may have run.)
  * ---------------------------------------------------------------------- */
 #define TPE_TREE_MAX_PARENTS 4
 enum { TPE_E_FALLBACK = -5 };
@@ -581,6 +585,11 @@ typedef struct tpe_tree_label {
   int32_t depth, n_parents;                 /* tree level (roots 0); 0 parents = unconditional           */
   int32_t parent[TPE_TREE_MAX_PARENTS];     /* active iff some parent[j] (a label index) chose          */
   int32_t parent_cat[TPE_TREE_MAX_PARENTS]; /* category parent_cat[j]                                   */
+  double q;                                 /* quantum of the quantized families (else 0)                */
+  const double* host_w[2];                  /* a caller-made fit, [0] below / [1] above (host_k[0] > 0):  */
+  const double* host_mu[2];                 /* used as is (categorical: host_w = the probabilities)     */
+  const double* host_sigma[2];
+  int64_t host_k[2];
 } tpe_tree_label;
 
 /* tpe_suggest_tree flags: the tpe_level_run flags, plus */
@@ -592,13 +601,14 @@ enum { TPE_TREE_NO_SPECULATE = 1 << 8 };    /* level by level only (no fused bat
  * device_fit_min > 0: labels with that many observations are left to the host
  * path (device Parzen fit).  values / active: [n_ids x n_labels] — the chosen
  * value (categories as doubles) and whether the label is active; path[0] = 1
- * when the fused batch was used, path[1] = level runs issued.  TPE_E_SPACE:
- * grow the workspace to `need` and call again. */
+ * when the fused batch was used, path[1] = level runs issued; need_fit
+ * [n_labels]: set to 1 for the labels the caller must fit (TPE_E_FALLBACK).
+ * TPE_E_SPACE: grow the workspace to `need` and call again. */
 int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
                      double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
                      uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
                      const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
-                     int32_t* path);
+                     int32_t* path, int8_t* need_fit);
 
 /* ------------------------------------------------------------------------
  * Stage profiler of tpe_level_run (bench.py's live roofline).  While enabled,

@@ -171,11 +171,12 @@ def _tree_call(table, hist, C, min_draws=64.0, flags=0):
     vals = np.empty((1, len(arr)))
     act = np.empty((1, len(arr)), dtype=np.int8)
     path = (ctypes.c_int32 * 2)()
+    need_fit = np.zeros(len(arr), dtype=np.int8)
     ids = np.array([len(hist)], dtype=np.int64)
     rc = N.load().tpe_suggest_tree(arr.ctypes.data, len(arr), below.ctypes.data, len(below), 1.0, 25, ids.ctypes.data,
                                    1, C, 5, min_draws, 16384, flags, ctypes.byref(ws), ctypes.byref(need), None,
-                                   vals.ctypes.data, act.ctypes.data, path)
-    return rc, need, path
+                                   vals.ctypes.data, act.ctypes.data, path, need_fit.ctypes.data)
+    return rc, need, path, need_fit
 
 
 def test_suggest_tree_fits_and_predicts_without_gpu():
@@ -189,19 +190,20 @@ def test_suggest_tree_fits_and_predicts_without_gpu():
     domain, trials = bench.make_history(3000, 0)
     hist = H.extract(domain, trials)
     C = 1 << 16
-    rc, need, path = _tree_call(domain.table, hist, C)
+    rc, need, path, _ = _tree_call(domain.table, hist, C)
     assert rc == N.E_SPACE and path[1] == 1, rc
     fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, None)
     pred = tpe._predict_activity(domain.table, fits, C)
     n_act = sum(v is not None for v in pred.values())
     assert need.result == n_act == 4 and need.cand == n_act * C
-    rc, need, path = _tree_call(domain.table, hist, C, flags=N.TREE_NO_SPECULATE)
+    rc, need, path, _ = _tree_call(domain.table, hist, C, flags=N.TREE_NO_SPECULATE)
     assert rc == N.E_SPACE and need.result == 1 and need.cand == C
 
 
 def test_suggest_tree_hands_quantized_labels_back():
     """A root quantized label needs numpy's tie order: TPE_E_FALLBACK before
-    anything is sized or launched."""
+    anything is sized or launched, the label flagged for the caller's fit; with
+    that fit in its record the call proceeds to sizing the level."""
     from hyperopt_amd import base, hp, history as H, rand
     domain = base.Domain(lambda d: 0.0, {'q': hp.quniform('q', 0, 10, 1), 'x': hp.uniform('x', -1, 1)})
     trials = base.Trials()
@@ -212,5 +214,24 @@ def test_suggest_tree_hands_quantized_labels_back():
         d['result'] = {'status': 'ok', 'loss': float(rs.uniform())}
         trials.insert_trial_docs([d])
     trials.refresh()
-    rc, need, path = _tree_call(domain.table, H.extract(domain, trials), 1024)
+    hist = H.extract(domain, trials)
+    rc, need, path, need_fit = _tree_call(domain.table, hist, 1024)
     assert rc == N.E_FALLBACK and path[1] == 0
+    q = domain.table.by_label['q'].index
+    assert need_fit.tolist() == [1 if i == q else 0 for i in range(len(need_fit))]
+    from hyperopt_amd import tpe
+    fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, None)
+    post = fits.get(domain.table.by_label['q'])
+    arr, keep = tpe._tree_labels(domain.table, hist)
+    arr = arr.copy()
+    cols = [[np.ascontiguousarray(c) for c in side] for side in (post.below, post.above)]
+    for sd in range(2):
+        arr[q]['host_k'][sd] = len(cols[sd][0])
+        arr[q]['host_w'][sd], arr[q]['host_mu'][sd], arr[q]['host_sigma'][sd] = [c.ctypes.data for c in cols[sd]]
+    orig = tpe._tree_labels
+    tpe._tree_labels = lambda t, h: (arr, keep)
+    try:
+        rc, need, path, need_fit = _tree_call(domain.table, hist, 1024)
+    finally:
+        tpe._tree_labels = orig
+    assert rc == N.E_SPACE and not need_fit.any() and need.result == 2

@@ -86,15 +86,33 @@ def test_native_tree_columnar_history():
     assert path == (0, 1) and nat == gen
 
 
-def test_native_tree_hands_quantized_labels_to_general_path():
-    """The rf branch (quantized rf_n_est / rf_depth_n): tpe_suggest_tree
-    returns TPE_E_FALLBACK and the suggest takes the general path."""
+def test_native_tree_takes_caller_fits_of_quantized_labels():
+    """The rf branch (quantized rf_n_est / rf_depth_n): tpe_suggest_tree flags
+    the quantized labels, the host fits them exactly as the general path does
+    (numpy's tie order) and the second call runs the tree natively — same
+    suggestion as the general path.  Also the mixed 10-dim space of config 2."""
     import bench
-    from hyperopt_amd import tpe
+    from hyperopt_amd import base, hp, tpe
     domain, trials = bench.make_history(3000, 0, loss=bench.rf_loss)
-    nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, 5, n_EI_candidates=1 << 16)))
-    assert path is None and nat == gen
-    assert int(nat['model']) == 1
+    for seed in (5, 6):
+        nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=1 << 16)))
+        assert path is not None and nat == gen, (seed, path, nat, gen)
+        assert int(nat['model']) == 1
+    d2 = base.Domain(lambda d: 0.0, bench.mixed10_space(hp))
+    from hyperopt_amd import rand
+    t2 = base.Trials()
+    rs = np.random.RandomState(0)
+    docs = []
+    for tid in range(300):
+        d = rand.suggest([tid], d2, t2, rs.randint(2 ** 31 - 1))[0]
+        v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
+        d['state'] = base.JOB_STATE_DONE
+        d['result'] = {'status': 'ok', 'loss': sum((float(x) - 0.3) ** 2 for x in v.values()) + 1e-9 * tid}
+        docs.append(d)
+    t2.insert_trial_docs(docs)
+    t2.refresh()
+    nat, gen, path = _both(lambda: doc_values(tpe.suggest([300], d2, t2, 3, n_EI_candidates=10000)))
+    assert path is not None and nat == gen, (nat, gen)
 
 
 def test_engine_stream_follows_torch():
