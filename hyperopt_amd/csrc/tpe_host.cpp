@@ -1007,7 +1007,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       tpe_tab_job j;
       j.problem = r; j.side = sd; j.kind = p.tab_mode; j.n = p.tab_n[sd]; j.off = p.tab_off[sd];
       j.block0 = (int32_t)tab_blocks;
-      tab_blocks += (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK;
+      // cells: TPE_TAB_PER_BLOCK rows per block; lattice: one block per value
+      tab_blocks += j.kind == TPE_TAB_CELLS ? (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK : j.n;
       tab_jobs.push_back(j);
     }
   }

@@ -2171,21 +2171,29 @@ __device__ __forceinline__ void pruned_range(const tpe_problem& p, const float4*
   k0 = __builtin_amdgcn_readfirstlane(k0); n0 = __builtin_amdgcn_readfirstlane(n0);
 }
 
-// one wave: {l, g} of lattice value lat_lo + j of a quantized problem, the
+// one workgroup: {l, g} of lattice value lat_lo + j of a quantized problem, the
 // reference's per-component mass terms (tpe.py:147-159 / :285-298) summed in a
-// fixed order (lane-strided, then a butterfly)
+// fixed order (thread-strided, a butterfly per wave, the waves' partials in
+// wave order) — every wave of the block takes a share of the components (the
+// two f64 erf per term make a row long for one wave)
 template <bool LOG>
 __device__ void lattice_row(const tpe_problem& p, int j, const double4* __restrict__ comp64,
-                            double2* __restrict__ rows) {
-  const int lane = threadIdx.x & 63;
+                            double2* __restrict__ rows, double* __restrict__ lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const double x = (double)(p.lat_lo + (int64_t)j) * p.q;
   double tu, tl;
   q_bounds(p, x, tu, tl);
   double sb = 0.0, sa = 0.0;
-  for (int k = lane; k < p.below_len; k += 64) sb += qterm<LOG>(comp64[p.below_off + k], tu, tl);
-  for (int k = lane; k < p.above_len; k += 64) sa += qterm<LOG>(comp64[p.above_off + k], tu, tl);
+  for (int k = threadIdx.x; k < p.below_len; k += blockDim.x) sb += qterm<LOG>(comp64[p.below_off + k], tu, tl);
+  for (int k = threadIdx.x; k < p.above_len; k += blockDim.x) sa += qterm<LOG>(comp64[p.above_off + k], tu, tl);
   for (int off = 32; off > 0; off >>= 1) { sb += __shfl_xor(sb, off); sa += __shfl_xor(sa, off); }
-  if (lane == 0) rows[j] = make_double2(log(sb) + p.below_base, log(sa) + p.above_base);
+  if (lane == 0) { lds[2 * wave] = sb; lds[2 * wave + 1] = sa; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double b = 0.0, a = 0.0;
+    for (int w = 0; w < nw; ++w) { b += lds[2 * w]; a += lds[2 * w + 1]; }
+    rows[j] = make_double2(log(b) + p.below_base, log(a) + p.above_base);
+  }
 }
 
 // 512-thread workgroups, one wave per cell row / lattice value
@@ -2303,9 +2311,10 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
              (unsigned long long)(stage ? tt[2] - tt[1] : 0), (unsigned long long)(stage ? tt[3] - tt[2] : 0),
              (unsigned long long)(tt[4] - tt[3]), (unsigned long long)(tt[5] - tt[4]));
 #endif
-  } else if (j < jb.n) {
-    if (p.family == TPE_FAM_QLOGGAUSS) lattice_row<true>(p, j, comp64, reinterpret_cast<double2*>(tab + jb.off));
-    else lattice_row<false>(p, j, comp64, reinterpret_cast<double2*>(tab + jb.off));
+  } else if (b < jb.n) {                             // lattice: block b computes value b
+    double* lds = reinterpret_cast<double*>(rows_lds);
+    if (p.family == TPE_FAM_QLOGGAUSS) lattice_row<true>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off), lds);
+    else lattice_row<false>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off), lds);
   }
 }
 

@@ -316,7 +316,8 @@ class Engine(object):
             if pl['mode'] != N.TAB_NONE and len(lp.ids):
                 for sd in range(2 if pl['mode'] == N.TAB_CELLS else 1):
                     jobs.append((r0, sd, pl['mode'], info['tab_n'][sd], info['tab_off'][sd], blocks))
-                    blocks += -(-info['tab_n'][sd] // N.TAB_PER_BLOCK)
+                    n = info['tab_n'][sd]        # cells: TAB_PER_BLOCK rows a block; lattice: a block a value
+                    blocks += -(-n // N.TAB_PER_BLOCK) if pl['mode'] == N.TAB_CELLS else n
             r0 += len(lp.ids)
         tab_jobs = np.array(jobs, dtype=np.int64).reshape(-1, 6)
         tj = np.zeros(len(tab_jobs), dtype=N.TAB_JOB_DTYPE)

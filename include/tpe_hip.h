@@ -42,8 +42,9 @@ extern "C" {
 /* categorical problems with at most this many categories are scored by the
  * sample stage itself (device-drawn candidates) */
 #define TPE_SAMPLE_LDS_ROWS 1024
-/* cell rows / lattice values a table workgroup computes (tpe_batch.tab_blocks
- * = sum over jobs of ceil(n / TPE_TAB_PER_BLOCK)) */
+/* cell rows a table workgroup computes; a lattice value takes a whole
+ * workgroup (tpe_batch.tab_blocks = sum over cell jobs of ceil(n /
+ * TPE_TAB_PER_BLOCK) + sum over lattice jobs of n) */
 #define TPE_TAB_PER_BLOCK 8
 /* 16-B units of one cell row of a TPE_TAB_CELLS table */
 #define TPE_TAB_ROW_UNITS 3
