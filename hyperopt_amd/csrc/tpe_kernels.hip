@@ -1114,7 +1114,50 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       }
     }
     if (pair) ++gi;                                  // the pair's second tile is done
-    if (!cells) {                                    // lattice: exact {l, g} per quantized value
+    if (!cells && PREC == TPE_PREC_F32 && draw && in_lds) {
+      // lattice, f32 draws: drawn as the cells path draws (draw_uniforms' pairs,
+      // the staged sampler rows, ndtri_f32), quantised as draw_comp quantises
+      // (np.round(x / q) * q), the lattice row of that multiple looked up
+      DrawU du[kTabPer];
+      const uint64_t g0 = (uint64_t)p.cand_base + (uint64_t)first;
+      if ((g0 & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < kTabPer; j += 2) {
+          const uint64_t blk = (g0 + (uint64_t)j) >> 1;
+          const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+          du[j] = DrawU{u01w(r.x), u01f(r.y), 0.0};
+          du[j + 1] = DrawU{u01w(r.z), u01f(r.w), 0.0};
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kTabPer; ++j) du[j] = draw_uniforms(p, first + j, TPE_PREC_F32);
+      }
+      const bool lg = p.family == TPE_FAM_QLOGGAUSS;
+      const double2* __restrict__ lat = reinterpret_cast<const double2*>(tab) + p.tab_off[0];
+#pragma unroll
+      for (int j = 0; j < kTabPer; ++j) {
+        const int i = first + j;
+        if (i >= p.n_cand) break;
+        const int a = guided_comp(cum_lds, guide, p.samp_len, du[j].us);
+        const float4 sr = row_lds[a];
+        const float pr = sr.z + du[j].uf * (sr.w - sr.z);
+        const float z = ndtri_f32(pr);
+        float xf = sr.x + sr.y * z;
+        if (!(xf == xf)) xf = sr.x;
+        const float t = fminf(fmaxf(xf, lo_f), hi_f);
+        const double xu = lg ? exp((double)t) : (double)t;
+        const double mq = rint(xu / p.q);
+        const double x = mq * p.q;
+        const double jq = mq - (double)p.lat_lo;
+        double l = -INFINITY, g = 0.0;             // (outside the lattice: unreachable for device draws)
+        if (jq >= 0.0 && jq < (double)p.tab_n[0]) {
+          const double2 r = lat[(int64_t)jq];
+          l = r.x;
+          g = r.y;
+        }
+        emit(i, p.cand_off + i, x, l, g, x);
+      }
+    } else if (!cells) {                             // lattice: exact {l, g} per quantized value
       for (int j = 0; j < kTabPer; ++j) {
         const int i = first + j;
         if (i >= p.n_cand) break;
