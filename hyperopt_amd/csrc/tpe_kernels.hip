@@ -777,6 +777,13 @@ __device__ __forceinline__ float cell_log2_lds(float lo, float inv, float w, flo
 
 // PREC is a template parameter: with the f64 inverse-CDF path reachable, the
 // candidate loop needs several times the registers
+// f64 exp out of line: inlined, its polynomial's f64 constants were hoisted
+// into VGPR pairs at k_sample_tab's start (no literal operands in VOP3) and
+// pushed the cells loop into scratch spills
+__device__ __noinline__ double exp_call(double x) { return exp(x); }
+// (likewise the empty slot's constant, stored out of line)
+__device__ __noinline__ void clear_best(tpe_best* d) { *d = tpe_best{0, 0, 0, -1}; }
+
 template <int PREC>
 __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* __restrict__ P,
                                                             const tpe_tile* __restrict__ tiles,
@@ -838,7 +845,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       tpe_result r;
       r.score = s2; r.l = l2; r.g = g2; r.idx = i2; r.value = 0.0;
       r.global_idx = i2 >= 0 ? run_cand_base + i2 : -1;
-      if (i2 >= 0) r.value = run_drawn ? (run_exp ? exp(v2) : v2) : cand[run_cand_off + i2];
+      if (i2 >= 0) r.value = run_drawn ? (run_exp ? exp_call(v2) : v2) : cand[run_cand_off + i2];
       run_best[run_tile] = r;
 #ifdef TPE_SAMPLE_TRACE
       g_ft[2] = wall_clock64();
@@ -855,6 +862,11 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 #ifdef TPE_SAMPLE_TRACE
     if (threadIdx.x == 0) g_ft[0] = wall_clock64();
 #endif
+    // lane, wave and their LDS addresses formed here (hoisted to the kernel's
+    // start they stayed live across the candidate loops and were spilled)
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = tid >> 6;
     if (run_cells) {
       // cells run: argmax of the f32 keys (two 32-bit shuffles per round, not five
       // 64-bit ones), then the winner's log2 sums and draw by lane read-out
@@ -998,8 +1010,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
                       __builtin_amdgcn_readfirstlane(s_prob[gi + 1]) == pid &&
                       __builtin_amdgcn_readfirstlane(s_start[gi + 1]) == cand_start + kTile;
     if (!run_best && threadIdx.x < TPE_BEST_PER_TILE) {   // (early selection: runs report to run_best)
-      tile_best[(int64_t)tile * TPE_BEST_PER_TILE + threadIdx.x] = tpe_best{0, 0, 0, -1};
-      if (pair) tile_best[(int64_t)s_tile[gi + 1] * TPE_BEST_PER_TILE + threadIdx.x] = tpe_best{0, 0, 0, -1};
+      clear_best(tile_best + (int64_t)tile * TPE_BEST_PER_TILE + threadIdx.x);
+      if (pair) clear_best(tile_best + (int64_t)s_tile[gi + 1] * TPE_BEST_PER_TILE + threadIdx.x);
     }
     float lo_f, hi_f;
     f32_bounds(p, lo_f, hi_f);
@@ -1070,7 +1082,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           track(i, lb2, la2, t);
           if (need_x) {                          // per-candidate outputs on request (tests)
             const double lnx = logc ? (double)t : 0.0;
-            const double x = !draw ? cand[o] : logc ? exp((double)t) : (double)t;
+            const double x = !draw ? cand[o] : logc ? exp_call((double)t) : (double)t;
             if (l_out) { l_out[o] = (double)lb2 * kLn2 + p.below_base - lnx; g_out[o] = (double)la2 * kLn2 + p.above_base - lnx; }
             if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
           }
@@ -1097,7 +1109,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
               track(i, lb2, la2, t);
               if (need_x) {
                 const double lnx = logc ? (double)t : 0.0;
-                const double x = !draw ? cand[o] : logc ? exp((double)t) : (double)t;
+                const double x = !draw ? cand[o] : logc ? exp_call((double)t) : (double)t;
                 if (l_out) { l_out[o] = (double)lb2 * kLn2 + p.below_base - lnx; g_out[o] = (double)la2 * kLn2 + p.above_base - lnx; }
                 if (flags & TPE_BATCH_WRITE_CAND) cand[o] = x;
               }

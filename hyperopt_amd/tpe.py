@@ -356,36 +356,49 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     if tl is None:
         return None
     below = np.sort(np.asarray(below_tids, dtype=np.int64))
-    arr, fits, host = tl[0], None, {}
+    st = {'arr': tl[0]}
+    host = {}
+
+    def give(ix):                              # the general path's fit of label ix, for the native call
+        if not host and 'fits' not in st:
+            st['fits'] = _Fits(table, hist, below_tids, prior_weight, engine)
+            st['arr'] = st['arr'].copy()
+        row = table.rows[ix]
+        post = st['fits'].get(row)
+        if post.above is None:                 # (device-fitted: the general path)
+            return False
+        rec = st['arr'][ix]
+        keep = host[ix] = []                   # (keeps the fitted arrays alive for the call)
+        for sd, side in enumerate((post.below, post.above)):
+            cols = [np.ascontiguousarray(c, dtype=np.float64) for c in side]
+            keep.append(cols)
+            rec['host_k'][sd] = len(cols[0])
+            rec['host_w'][sd] = cols[0].ctypes.data
+            if not row.categorical:
+                rec['host_mu'][sd] = cols[1].ctypes.data
+                rec['host_sigma'][sd] = cols[2].ctypes.data
+        return True
+    # the labels the previous call had to fit here are fitted up front (the active
+    # branch seldom changes between suggests): no refused first call
+    for ix in getattr(table, 'native_fit_hint', ()):
+        if not give(ix):
+            table.native_fit_hint = ()
+            return None
     # (a level-by-level run learns a deeper level's needs only after the levels above it)
     for attempt in range(table.n_levels + 1):
-        values, active = engine.suggest_tree(arr, below, prior_weight, DEFAULT_LF, new_ids, C, seed,
+        values, active = engine.suggest_tree(st['arr'], below, prior_weight, DEFAULT_LF, new_ids, C, seed,
                                              SPECULATE_MIN_DRAWS if SPECULATE else -1.0)
         if values is not None:
             break
         need = np.flatnonzero(active)          # (need_fit on TPE_E_FALLBACK)
         if not len(need) or any(ix in host for ix in need.tolist()):
             return None
-        if fits is None:
-            fits = _Fits(table, hist, below_tids, prior_weight, engine)
-            arr = arr.copy()
         for ix in need.tolist():
-            row = table.rows[ix]
-            post = fits.get(row)
-            if post.above is None:             # (device-fitted: the general path)
+            if not give(ix):
                 return None
-            rec = arr[ix]
-            keep = host[ix] = []               # (keeps the fitted arrays alive for the call)
-            for sd, side in enumerate((post.below, post.above)):
-                cols = [np.ascontiguousarray(c, dtype=np.float64) for c in side]
-                keep.append(cols)
-                rec['host_k'][sd] = len(cols[0])
-                rec['host_w'][sd] = cols[0].ctypes.data
-                if not row.categorical:
-                    rec['host_mu'][sd] = cols[1].ctypes.data
-                    rec['host_sigma'][sd] = cols[2].ctypes.data
     else:
         return None
+    table.native_fit_hint = tuple(host)
     order = table.level_order()
     cols = _tree_static(table)[2]
     i64, f64 = np.int64, np.float64
