@@ -398,7 +398,9 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
                 return None
     else:
         return None
-    table.native_fit_hint = tuple(host)
+    # (only labels some id used: a branch switch drops the old branch's)
+    used = np.asarray(active).any(axis=0)
+    table.native_fit_hint = tuple(ix for ix in host if used[ix])
     order = table.level_order()
     cols = _tree_static(table)[2]
     i64, f64 = np.int64, np.float64

@@ -115,6 +115,28 @@ def test_native_tree_takes_caller_fits_of_quantized_labels():
     assert path is not None and nat == gen, (nat, gen)
 
 
+def test_native_tree_stale_fit_hint():
+    """The labels a call had to fit on the host are fitted up front by the next
+    call on the same space (ParamTable.native_fit_hint).  A branch switch leaves
+    the hint naming labels the new branch does not use: still the general path's
+    suggestion, both ways, and the hint follows the branch."""
+    import bench
+    from hyperopt_amd import tpe
+    domain, rf_trials = bench.make_history(3000, 0, loss=bench.rf_loss)
+    _, svm_trials = bench.make_history(3000, 0)
+    table = domain.table
+    for trials, model, seed in ((rf_trials, 1, 11), (svm_trials, 0, 12), (rf_trials, 1, 13), (rf_trials, 1, 14)):
+        nat, gen, path = _both(lambda: doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=1 << 16)))
+        assert path is not None and nat == gen, (seed, path, nat, gen)
+        assert int(nat['model']) == model
+        named = {table.rows[ix].label for ix in getattr(table, 'native_fit_hint', ())}
+        assert named <= {'rf_n_est', 'rf_depth_n', 'svm_poly_degree', 'knn_k'}, named
+        if model == 1:
+            assert 'rf_n_est' in named, named
+        else:
+            assert not named & {'rf_n_est', 'rf_depth_n'}, named
+
+
 def test_engine_stream_follows_torch():
     """Engine._stream (the raw current-stream accessor) is torch's current
     stream, also inside a torch.cuda.stream context."""
