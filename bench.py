@@ -268,6 +268,25 @@ def mixed10_space(hp):
             'c0': hp.choice('c0', list(range(5))), 'c1': hp.choice('c1', list(range(3)))}
 
 
+def mixed10_history(n, seed):
+    """Config 2's history: ``n`` prior draws of the 10-dim mixed space with
+    loss sum((v - 0.3)^2) + 1e-9 * tid."""
+    from hyperopt_amd import base, hp, rand
+    domain = base.Domain(lambda d: 0.0, mixed10_space(hp))
+    trials = base.Trials()
+    rs = np.random.RandomState(seed)
+    docs = []
+    for tid in range(n):
+        d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
+        v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
+        d['state'] = base.JOB_STATE_DONE
+        d['result'] = {'status': 'ok', 'loss': sum((float(x) - 0.3) ** 2 for x in v.values()) + 1e-9 * tid}
+        docs.append(d)
+    trials.insert_trial_docs(docs)
+    trials.refresh()
+    return domain, trials
+
+
 def config_workload(config, rank, world, args):
     """(description, setup info, step(i) -> candidate-scores, cpu_baseline_fn or None)"""
     from hyperopt_amd import base, hp, rand, tpe
@@ -281,18 +300,7 @@ def config_workload(config, rank, world, args):
             return 80 * 24        # 80 TPE suggests (after 20 start-up) x 24 candidates
         return 'config1: fmin(tpe.suggest), hp.uniform 1-D quadratic, 100 trials, n_EI_candidates=24', step, None
     if config == 2:
-        domain = base.Domain(lambda d: 0.0, mixed10_space(hp))
-        trials = base.Trials()
-        rs = np.random.RandomState(SEED)
-        docs = []
-        for tid in range(1000):
-            d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
-            v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
-            d['state'] = base.JOB_STATE_DONE
-            d['result'] = {'status': 'ok', 'loss': sum((float(x) - 0.3) ** 2 for x in v.values()) + 1e-9 * tid}
-            docs.append(d)
-        trials.insert_trial_docs(docs)
-        trials.refresh()
+        domain, trials = mixed10_history(1000, SEED)
         C = 10000
 
         def step(i):

@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 13
+ABI_VERSION = 14
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -51,8 +51,9 @@ FIT_JOB_DTYPE = np.dtype([
     ('family', '<i4'), ('flags', '<i4'), ('lf', '<i4'), ('problem_first', '<i4'), ('n_problems', '<i4'),
     ('above_off', '<i4'), ('wide_off', '<i4'), ('grid_off', '<i4'), ('grid_n', '<i4'), ('reserved', '<i4'),
     ('prior_mu', '<f8'), ('prior_sigma', '<f8'), ('prior_weight', '<f8'), ('low', '<f8'), ('high', '<f8'),
+    ('ord_key_in', '<u8'), ('ord_idx_in', '<u8'), ('n_ord_in', '<i8'), ('ord_key_out', '<u8'), ('ord_idx_out', '<u8'),
 ])
-assert FIT_JOB_DTYPE.itemsize == 112
+assert FIT_JOB_DTYPE.itemsize == 152
 RESULT_DTYPE = np.dtype([('score', '<f8'), ('l', '<f8'), ('g', '<f8'), ('value', '<f8'),
                          ('idx', '<i8'), ('global_idx', '<i8')])
 assert RESULT_DTYPE.itemsize == 48
@@ -82,7 +83,7 @@ class Batch(ctypes.Structure):
         ('below_idx', ctypes.c_void_p), ('fit_seg', ctypes.c_void_p), ('fit_total', ctypes.c_int64),
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
-        ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_uint64), ('fit_max_seg', ctypes.c_int64),
+        ('fit_max_new', ctypes.c_int64), ('fit_max_obs', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_blocks', ctypes.c_int64), ('n_sorted', ctypes.c_int32),
         ('reserved5', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
         ('tab_jobs', ctypes.c_void_p), ('n_tab_jobs', ctypes.c_int32), ('tab_blocks', ctypes.c_int32),
@@ -106,6 +107,8 @@ class LabelIn(ctypes.Structure):
         ('dev_obs', ctypes.c_void_p), ('n_obs', ctypes.c_int64),
         ('below_idx', ctypes.c_void_p), ('n_below', ctypes.c_int32), ('lf', ctypes.c_int32),
         ('prior_mu', ctypes.c_double), ('prior_sigma', ctypes.c_double), ('prior_weight', ctypes.c_double),
+        ('ord_key_in', ctypes.c_void_p), ('ord_idx_in', ctypes.c_void_p), ('n_ord_in', ctypes.c_int64),
+        ('ord_key_out', ctypes.c_void_p), ('ord_idx_out', ctypes.c_void_p),
     ]
 
 
@@ -136,7 +139,8 @@ class PackInfo(ctypes.Structure):
         ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
         ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
-        ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_seg', ctypes.c_int64),
+        ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_new', ctypes.c_int64),
+        ('fit_max_obs', ctypes.c_int64),
         ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64), ('n_pooled', ctypes.c_int64),
         ('off_tab_jobs', ctypes.c_int64), ('n_tab_jobs', ctypes.c_int64), ('tab_blocks', ctypes.c_int64),
         ('tab_units', ctypes.c_int64),
@@ -148,7 +152,7 @@ class PackInfo(ctypes.Structure):
 class LevelWS(ctypes.Structure):
     """tpe_level_ws: caller-owned buffers of tpe_level_run."""
     _fields_ = [
-        ('pinned', ctypes.c_void_p), ('pinned_bytes', ctypes.c_int64),
+        ('pinned', ctypes.c_void_p), ('pinned_bytes', ctypes.c_int64), ('pinned_dev', ctypes.c_void_p),
         ('blob', ctypes.c_void_p), ('blob_bytes', ctypes.c_int64),
         ('cand', ctypes.c_void_p), ('coord', ctypes.c_void_p),
         ('keys', ctypes.c_void_p), ('vals', ctypes.c_void_p), ('keys_sorted', ctypes.c_void_p),
@@ -159,7 +163,6 @@ class LevelWS(ctypes.Structure):
         ('result', ctypes.c_void_p), ('result_cap', ctypes.c_int64),
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p), ('fit_cap', ctypes.c_int64),
-        ('fit_tmp', ctypes.c_void_p), ('fit_tmp_bytes', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_pref_cap', ctypes.c_int64),
         ('pool_best', ctypes.c_void_p), ('pool_best_cap', ctypes.c_int64),
         ('tab', ctypes.c_void_p), ('tab_cap', ctypes.c_int64),
@@ -169,7 +172,7 @@ class LevelWS(ctypes.Structure):
 class LevelNeed(ctypes.Structure):
     """tpe_level_need: sizes one level needs."""
     _fields_ = [(k, ctypes.c_int64) for k in ('pinned_bytes', 'blob_bytes', 'cand', 'sort_tmp_bytes', 'part',
-                                              'best', 'result', 'fit', 'fit_tmp_bytes',
+                                              'best', 'result', 'fit',
                                               'draw_pref', 'pool_best', 'tab')]
 
 
@@ -196,6 +199,20 @@ class TreeLabel(ctypes.Structure):
     ]
 
 
+COMM_ID_BYTES = 128          # TPE_COMM_ID_BYTES
+EXCHANGE_HEADER = 64         # TPE_EXCHANGE_HEADER
+GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+
+
+class Exchange(ctypes.Structure):
+    """tpe_exchange: the candidate-shard exchange of a sharded tpe_suggest_tree."""
+    _fields_ = [
+        ('rank', ctypes.c_int32), ('world', ctypes.c_int32), ('comm', ctypes.c_void_p),
+        ('gather', GATHER_FN), ('ctx', ctypes.c_void_p), ('dev', ctypes.c_void_p), ('dev_bytes', ctypes.c_int64),
+        ('always', ctypes.c_int32), ('reserved', ctypes.c_int32),
+    ]
+
+
 TREE_LABEL_DTYPE = np.dtype(dict(
     names=[f for f, _ in TreeLabel._fields_],
     formats=['<i4', '<i4', '<i4', '<i4', '<f8', '<f8', '<f8', '<f8', '<u8', '<u8', '<u8', '<u8', '<i8', '<i4', '<i4',
@@ -203,12 +220,12 @@ TREE_LABEL_DTYPE = np.dtype(dict(
              ('<u8', (2,)), ('<i8', (2,))],
     offsets=[getattr(TreeLabel, f).offset for f, _ in TreeLabel._fields_], itemsize=ctypes.sizeof(TreeLabel)))
 
-EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size',
-           'tpe_sort_workspace_bytes', 'tpe_fit_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above', 'tpe_tables',
+EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size', 'tpe_pinned_device_address',
+           'tpe_sort_workspace_bytes', 'tpe_run_batch', 'tpe_fit_above', 'tpe_tables',
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
            'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read',
-           'tpe_suggest_tree')
+           'tpe_suggest_tree', 'tpe_comm_unique_id', 'tpe_comm_init', 'tpe_comm_destroy', 'tpe_combine_results')
 
 # tpe_level_run stages (tpe_level_profile_read order)
 STAGES = ('fit', 'k_tables', 'k_sample', 'sort', 'above', 'k_finalize', 'k_select')
@@ -250,10 +267,10 @@ def load(path=LIB_PATH):
     lib.tpe_last_error.restype = ctypes.c_char_p
     lib.tpe_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
     lib.tpe_tile_size.restype = ctypes.c_int
+    lib.tpe_pinned_device_address.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+    lib.tpe_pinned_device_address.restype = ctypes.c_int
     lib.tpe_sort_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64)]
     lib.tpe_sort_workspace_bytes.restype = ctypes.c_int
-    lib.tpe_fit_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]
-    lib.tpe_fit_workspace_bytes.restype = ctypes.c_int
     for name in ('tpe_run_batch', 'tpe_fit_above', 'tpe_tables', 'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select'):
         fn = getattr(lib, name)
         fn.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
@@ -284,9 +301,18 @@ def load(path=LIB_PATH):
                                   ctypes.POINTER(LevelNeed), P, P]
     lib.tpe_level_run.restype = ctypes.c_int
     I32 = ctypes.c_int32
-    lib.tpe_suggest_tree.argtypes = [P, I32, P, I64, D, I32, P, I32, I32, ctypes.c_uint64, D, I64, I32,
+    lib.tpe_suggest_tree.argtypes = [P, I32, P, I64, D, I32, P, I32, I32, I64, I64, ctypes.POINTER(Exchange),
+                                     ctypes.c_uint64, D, I64, I32,
                                      ctypes.POINTER(LevelWS), ctypes.POINTER(LevelNeed), P, P, P, P, P]
     lib.tpe_suggest_tree.restype = ctypes.c_int
+    lib.tpe_comm_unique_id.argtypes = [P]
+    lib.tpe_comm_unique_id.restype = ctypes.c_int
+    lib.tpe_comm_init.argtypes = [I32, I32, P, I32, ctypes.POINTER(ctypes.c_void_p)]
+    lib.tpe_comm_init.restype = ctypes.c_int
+    lib.tpe_comm_destroy.argtypes = [P]
+    lib.tpe_comm_destroy.restype = ctypes.c_int
+    lib.tpe_combine_results.argtypes = [P, I32, I64, P]
+    lib.tpe_combine_results.restype = ctypes.c_int
     lib.tpe_level_profile.argtypes = [ctypes.c_int32]
     lib.tpe_level_profile.restype = ctypes.c_int
     lib.tpe_level_profile_read.argtypes = [ctypes.POINTER(StageProf), ctypes.c_int32]

@@ -9,6 +9,7 @@ derivable SoA cache of the history for the suggest hot path (``history``).
 """
 import datetime
 import logging
+import operator
 
 import numpy as np
 
@@ -143,12 +144,20 @@ class Trials(object):
         raise NotImplementedError('')
 
     def refresh(self):
-        """Drop ERROR trials (and other experiments' trials) from the view."""
+        """Drop ERROR trials (and other experiments' trials) from the view.
+
+        ``_view_gen`` counts the refreshes whose view is NOT the previous view
+        plus appended documents (a document dropped, replaced or reordered):
+        derived caches of the view (history.py) rebuild when it moves."""
+        old = getattr(self, '_trials', None)
         if self._exp_key is None:
             self._trials = [tt for tt in self._dynamic_trials if tt['state'] != JOB_STATE_ERROR]
         else:
             self._trials = [tt for tt in self._dynamic_trials
                             if tt['state'] != JOB_STATE_ERROR and tt['exp_key'] == self._exp_key]
+        new = self._trials
+        if old is not None and not (len(new) >= len(old) and all(map(operator.is_, old, new))):
+            self._view_gen = getattr(self, '_view_gen', 0) + 1
         self._ids.update([tt['tid'] for tt in self._trials])
 
     @property

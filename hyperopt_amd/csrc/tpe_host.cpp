@@ -481,7 +481,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     if (L.dev_obs && !L.above_mu) {
       if ((L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) || f64 || L.n_below < 0 || L.n_below > 64 ||
           (L.n_below > 0 && !L.below_idx) || L.n_obs - L.n_below + 1 != L.above_k || L.above_k <= kPruneMinK ||
-          L.n_obs >= ((int64_t)1 << 31))
+          L.n_obs >= ((int64_t)1 << 31) || L.n_ord_in < 0 || L.n_ord_in > L.n_obs ||
+          (L.n_ord_in > 0 && (!L.ord_key_in || !L.ord_idx_in)) ||
+          (L.n_ord_in < L.n_obs && (!L.ord_key_out || !L.ord_idx_out)))
         return TPE_E_ARG;
       dev_fit[li] = 1;
       ktot += L.below_k + kPruneWide;
@@ -815,7 +817,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<tpe_fit_job> fit;
   std::vector<int32_t> below_idx;
   std::vector<int64_t> fit_seg(1, 0);
-  int64_t dev_rows = 0, dev_grid = 0;
+  int64_t dev_rows = 0, dev_grid = 0, fit_max_new = 0, fit_max_obs = 0;
   {
     int64_t r = 0;
     for (int32_t li = 0; li < n_labels; ++li) {
@@ -836,13 +838,20 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         j.above_off = p.above_off; j.wide_off = p.wide_off; j.grid_off = p.grid_off; j.grid_n = p.grid_n;
         j.prior_mu = L.prior_mu; j.prior_sigma = L.prior_sigma; j.prior_weight = L.prior_weight;
         j.low = L.low; j.high = L.high;
+        j.ord_key_in = L.ord_key_in; j.ord_idx_in = L.ord_idx_in; j.n_ord_in = L.n_ord_in;
+        j.ord_key_out = L.ord_key_out; j.ord_idx_out = L.ord_idx_out;
         for (int32_t b = 0; b < L.n_below; ++b) {
           if (L.below_idx[b] < 0 || L.below_idx[b] >= L.n_obs || (b && L.below_idx[b] <= L.below_idx[b - 1]))
             return TPE_E_ARG;
           below_idx.push_back(L.below_idx[b]);
         }
         fit.push_back(j);
-        fit_seg.push_back(fit_seg.back() + K - 1);
+        // scratch segment: the compacted above order, the new observations' merge
+        // passes and the below positions all fit in it
+        const int64_t n_new = L.n_obs - L.n_ord_in;
+        fit_seg.push_back(fit_seg.back() + std::max<int64_t>(std::max<int64_t>(K - 1, n_new), L.n_below));
+        fit_max_new = std::max(fit_max_new, n_new);
+        fit_max_obs = std::max<int64_t>(fit_max_obs, L.n_obs);
         dev_rows += K + kPruneWide;
         dev_grid += G + 1;
       }
@@ -1065,8 +1074,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp64 = off[3];
   info->off_samp = off[4]; info->off_fit = off[5]; info->off_below_idx = off[6]; info->off_fit_seg = off[7];
   info->off_fin_tiles = off[8]; info->n_fin_tiles = n_fin;
-  info->fit_max_seg = 0;
-  for (size_t q = 1; q < fit_seg.size(); ++q) info->fit_max_seg = std::max(info->fit_max_seg, fit_seg[q] - fit_seg[q - 1]);
+  info->fit_max_new = fit_max_new;
+  info->fit_max_obs = fit_max_obs;
   info->off_tab_jobs = off[9]; info->n_tab_jobs = n_tab_jobs; info->tab_blocks = tab_blocks;
   info->tab_units = tab_units;
   info->off_samp_tiles = off[10]; info->n_samp_tiles = n_samp_tiles; info->n_samp_eager = n_samp_eager;

@@ -33,9 +33,11 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "../../include/tpe_hip.h"
 
@@ -2399,76 +2401,219 @@ __global__ __launch_bounds__(kUploadThreads) void k_upload(const unsigned long l
 // adaptive_parzen_normal (tpe.py:398-475) of the above observations of a label
 // (ap_filter_trials, tpe.py:613-641), directly into the pruned f32 layout.
 constexpr int kFitThreads = 512;
-constexpr int kFitGatherBlock = 256;
-constexpr int kFitMaxBelow = 64;
 constexpr int kPruneWide = 16;
 constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e))
 
-// gather: above observations (kernel coordinate) and their rank in tid order
-__global__ __launch_bounds__(kFitGatherBlock) void k_fit_gather(const tpe_fit_job* __restrict__ J,
-                                                                const int32_t* __restrict__ below_idx,
-                                                                double* __restrict__ keys,
-                                                                uint32_t* __restrict__ vals) {
-  const tpe_fit_job& j = J[blockIdx.y];
-  __shared__ int32_t bl[kFitMaxBelow];
-  const int nb = j.n_below;
-  if (threadIdx.x < nb) bl[threadIdx.x] = below_idx[j.below_off + threadIdx.x];
-  __syncthreads();
-  const bool logf = j.family == TPE_FAM_LOGGAUSS;
-  for (int64_t i = (int64_t)blockIdx.x * kFitGatherBlock + threadIdx.x; i < j.n_obs;
-       i += (int64_t)gridDim.x * kFitGatherBlock) {
-    int before = 0;
-    bool below = false;
-    for (int b = 0; b < nb; ++b) {
-      before += bl[b] < i;
-      below = below || bl[b] == i;
-    }
-    if (below) continue;
-    const int64_t r = i - before;                  // rank among the above observations
-    const double x = j.obs[i];
-    keys[j.seg_off + r] = logf ? log(x) : x;       // tpe.py:523 / :556 (np.log of the observations)
-    vals[j.seg_off + r] = (uint32_t)r;
-  }
+// ---- resident value order (include/tpe_hip.h "Device value order") ----
+// The order of the reference's argsort of the above observations (tpe.py:427),
+// stable: t ascending, NaN last (np.argsort), equal t by position in tid order.
+__device__ __forceinline__ bool ord_lt(double ka, uint32_t ia, double kb, uint32_t ib) {
+  if (ka < kb) return true;
+  if (ka > kb) return false;
+  const bool na = ka != ka, nb = kb != kb;           // (equal or unordered)
+  if (na != nb) return nb;
+  return ia < ib;
 }
 
-// Segments of up to kFitSortMax observations: one workgroup sorts a segment in
-// LDS (bitonic network on (key, rank) pairs — ranks are unique, so the order is
-// the stable order rocPRIM's radix sort gives).  Larger segments use rocPRIM.
-constexpr int kFitSortMax = 8192;
-constexpr int kFitSortThreads = 1024;
-__global__ __launch_bounds__(kFitSortThreads) void k_fit_sort_lds(const int64_t* __restrict__ seg,
-                                                                  const double* __restrict__ keys,
-                                                                  const uint32_t* __restrict__ vals,
-                                                                  double* __restrict__ keys_out,
-                                                                  uint32_t* __restrict__ vals_out) {
-  __shared__ double sk[kFitSortMax];
-  __shared__ uint32_t sv[kFitSortMax];
-  const int64_t b0 = seg[blockIdx.x];
-  const int n = (int)(seg[blockIdx.x + 1] - b0);
+// the column holds the kernel coordinate itself (the host's np.log for the log
+// families, tpe.py:523 / :556), so the order and the rows see numpy's values
+__device__ __forceinline__ double fit_coord(const tpe_fit_job& j, int64_t i) { return j.obs[i]; }
+
+// chunks: the new observations obs[n_ord_in ..] of each job, kOrdChunk at a
+// time, sorted in LDS by a bitonic network on (t, i) -> fit scratch buffer 0
+constexpr int kOrdChunk = 8192;
+constexpr int kOrdChunkThreads = 1024;
+__global__ __launch_bounds__(kOrdChunkThreads) void k_ord_chunks(const tpe_fit_job* __restrict__ J,
+                                                                 double* __restrict__ keys,
+                                                                 uint32_t* __restrict__ idx) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  const int64_t m = j.n_ord_in, k = j.n_obs - m, c0 = (int64_t)blockIdx.x * kOrdChunk;
+  if (c0 >= k) return;
+  __shared__ double sk[kOrdChunk];
+  __shared__ uint32_t sv[kOrdChunk];
+  const int n = (int)min<int64_t>(kOrdChunk, k - c0);
   int N = 1;
   while (N < n) N <<= 1;
-  for (int i = threadIdx.x; i < N; i += kFitSortThreads) {
-    sk[i] = i < n ? keys[b0 + i] : INFINITY;
-    sv[i] = i < n ? vals[b0 + i] : 0xFFFFFFFFu;
+  for (int i = threadIdx.x; i < N; i += kOrdChunkThreads) {   // padding sorts after every element
+    const bool in = i < n;
+    sk[i] = in ? fit_coord(j, m + c0 + i) : NAN;
+    sv[i] = in ? (uint32_t)(m + c0 + i) : 0xFFFFFFFFu;
   }
   __syncthreads();
-  for (int k = 2; k <= N; k <<= 1) {
-    for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      for (int i = threadIdx.x; i < N; i += kFitSortThreads) {
-        const int ixj = i ^ jj;
-        if (ixj > i) {
-          const double ka = sk[i], kb = sk[ixj];
-          const uint32_t va = sv[i], vb = sv[ixj];
-          const bool gt = ka > kb || (ka == kb && va > vb);
-          if (gt == ((i & k) == 0)) { sk[i] = kb; sk[ixj] = ka; sv[i] = vb; sv[ixj] = va; }
+  for (int w = 2; w <= N; w <<= 1) {
+    for (int h = w >> 1; h > 0; h >>= 1) {
+      for (int i = threadIdx.x; i < N; i += kOrdChunkThreads) {
+        const int p = i ^ h;
+        if (p > i) {
+          const double ka = sk[i], kb = sk[p];
+          const uint32_t va = sv[i], vb = sv[p];
+          if (ord_lt(kb, vb, ka, va) == ((i & w) == 0)) { sk[i] = kb; sk[p] = ka; sv[i] = vb; sv[p] = va; }
         }
       }
       __syncthreads();
     }
   }
-  for (int i = threadIdx.x; i < n; i += kFitSortThreads) {
-    keys_out[b0 + i] = sk[i];
-    vals_out[b0 + i] = sv[i];
+  double* __restrict__ ok = keys + j.seg_off + c0;
+  uint32_t* __restrict__ ov = idx + j.seg_off + c0;
+  for (int i = threadIdx.x; i < n; i += kOrdChunkThreads) { ok[i] = sk[i]; ov[i] = sv[i]; }
+}
+
+// merge-path merge, one tile of kMergeTile outputs per workgroup: the tile's
+// A and B ranges (found by a binary search on each tile edge's diagonal) are
+// staged in LDS, each thread merges kMergePer outputs from its own diagonal,
+// and the merged tile is written back coalesced.
+//   L > 0: a pass over each job's sorted new batch (runs of L, pairs merged)
+//          in src -> dst at the job's scratch segment
+//   L = 0: the resident order ord_in [n_ord_in] with the sorted batch in src
+//          -> ord_out [n_obs]
+constexpr int kMergeThreads = 256;
+constexpr int kMergePer = 8;
+constexpr int kMergeTile = kMergeThreads * kMergePer;
+static_assert(kOrdChunk % kMergeTile == 0, "merge tiles never straddle a run pair");
+__global__ __launch_bounds__(kMergeThreads) void k_ord_merge(const tpe_fit_job* __restrict__ J,
+                                                             const double* __restrict__ sk,
+                                                             const uint32_t* __restrict__ sv,
+                                                             double* __restrict__ dk, uint32_t* __restrict__ dv,
+                                                             int64_t L) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  const int64_t k = j.n_obs - j.n_ord_in, t0 = (int64_t)blockIdx.x * kMergeTile;
+  if (k <= 0) return;
+  const double *ak, *bk;
+  const uint32_t *av, *bv;
+  double* ok;
+  uint32_t* ov;
+  int64_t na, nb, d0;
+  if (L > 0) {
+    if (t0 >= k) return;
+    const int64_t base = t0 / (2 * L) * (2 * L), mid = min(base + L, k), end = min(base + 2 * L, k);
+    ak = sk + j.seg_off + base; av = sv + j.seg_off + base; na = mid - base;
+    bk = sk + j.seg_off + mid; bv = sv + j.seg_off + mid; nb = end - mid;
+    ok = dk + j.seg_off + base; ov = dv + j.seg_off + base;
+    d0 = t0 - base;
+  } else {
+    if (t0 >= j.n_obs) return;
+    ak = j.ord_key_in; av = j.ord_idx_in; na = j.n_ord_in;
+    bk = sk + j.seg_off; bv = sv + j.seg_off; nb = k;
+    ok = j.ord_key_out; ov = j.ord_idx_out;
+    d0 = t0;
+  }
+  const int64_t d1 = min(d0 + kMergeTile, na + nb);
+  __shared__ int64_t split[2];
+  if (threadIdx.x < 2) {              // A elements among the first d outputs
+    const int64_t d = threadIdx.x ? d1 : d0;
+    int64_t lo = max<int64_t>(0, d - nb), hi = min(d, na);
+    while (lo < hi) {
+      const int64_t md = (lo + hi) >> 1;
+      if (ord_lt(ak[md], av[md], bk[d - 1 - md], bv[d - 1 - md])) lo = md + 1;
+      else hi = md;
+    }
+    split[threadIdx.x] = lo;
+  }
+  __syncthreads();
+  const int64_t a0 = split[0], b0 = d0 - a0;
+  const int nA = (int)(split[1] - a0), n = (int)(d1 - d0), nB = n - nA;
+  __shared__ double lk[kMergeTile];
+  __shared__ uint32_t lv[kMergeTile];
+  for (int i = threadIdx.x; i < n; i += kMergeThreads) {
+    if (i < nA) { lk[i] = ak[a0 + i]; lv[i] = av[a0 + i]; }
+    else { lk[i] = bk[b0 + i - nA]; lv[i] = bv[b0 + i - nA]; }
+  }
+  __syncthreads();
+  const int dd = min(threadIdx.x * kMergePer, n);
+  int lo = max(0, dd - nB), hi = min(dd, nA);
+  while (lo < hi) {
+    const int md = (lo + hi) >> 1;
+    if (ord_lt(lk[md], lv[md], lk[nA + dd - 1 - md], lv[nA + dd - 1 - md])) lo = md + 1;
+    else hi = md;
+  }
+  int ia = lo, ib = dd - lo;
+  const int cnt = min(kMergePer, n - dd);
+  double rk[kMergePer];
+  uint32_t rv[kMergePer];
+#pragma unroll
+  for (int e = 0; e < kMergePer; ++e) {
+    if (e < cnt) {
+      const bool take_a = ia < nA && (ib >= nB || ord_lt(lk[ia], lv[ia], lk[nA + ib], lv[nA + ib]));
+      const int at = take_a ? ia : nA + ib;
+      rk[e] = lk[at];
+      rv[e] = lv[at];
+      ia += take_a;
+      ib += !take_a;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kMergePer; ++e)
+    if (e < cnt) { lk[dd + e] = rk[e]; lv[dd + e] = rv[e]; }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += kMergeThreads) { ok[d0 + i] = lk[i]; ov[d0 + i] = lv[i]; }
+}
+
+// the job's current order (merged this level, or the resident one)
+__device__ __forceinline__ const double* ord_keys(const tpe_fit_job& j) {
+  return j.n_ord_in < j.n_obs ? j.ord_key_out : j.ord_key_in;
+}
+__device__ __forceinline__ const uint32_t* ord_idx(const tpe_fit_job& j) {
+  return j.n_ord_in < j.n_obs ? j.ord_idx_out : j.ord_idx_in;
+}
+
+// position of each below observation in the job's order (binary search for its
+// own (t, i) pair) -> pos[seg_off + b]
+constexpr int kFitMaxBelow = 64;
+__global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* __restrict__ J,
+                                                            const int32_t* __restrict__ below_idx,
+                                                            uint32_t* __restrict__ pos) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  const int b = threadIdx.x;
+  if (b >= j.n_below) return;
+  const uint32_t i = (uint32_t)below_idx[j.below_off + b];
+  const double t = fit_coord(j, i);
+  const double* __restrict__ ok = ord_keys(j);
+  const uint32_t* __restrict__ ov = ord_idx(j);
+  int64_t lo = 0, hi = j.n_obs;
+  while (lo < hi) {
+    const int64_t md = (lo + hi) >> 1;
+    if (ord_lt(ok[md], ov[md], t, i)) lo = md + 1;
+    else hi = md;
+  }
+  pos[j.seg_off + b] = (uint32_t)lo;
+}
+
+// compact: the order without the below observations, each with its rank among
+// the above observations in tid order -> (keys_sorted, ranks) at seg_off
+constexpr int kCompactThreads = 256;
+constexpr int kCompactTile = 4096;
+__global__ __launch_bounds__(kCompactThreads) void k_ord_compact(const tpe_fit_job* __restrict__ J,
+                                                                 const int32_t* __restrict__ below_idx,
+                                                                 const uint32_t* __restrict__ pos,
+                                                                 double* __restrict__ keys_sorted,
+                                                                 uint32_t* __restrict__ ranks) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  const int64_t s0 = (int64_t)blockIdx.x * kCompactTile;
+  if (s0 >= j.n_obs) return;
+  __shared__ uint32_t bp[kFitMaxBelow], bi[kFitMaxBelow];
+  const int nb = j.n_below;
+  if (threadIdx.x < nb) {
+    bp[threadIdx.x] = pos[j.seg_off + threadIdx.x];
+    bi[threadIdx.x] = (uint32_t)below_idx[j.below_off + threadIdx.x];
+  }
+  __syncthreads();
+  const double* __restrict__ ok = ord_keys(j);
+  const uint32_t* __restrict__ ov = ord_idx(j);
+  const int64_t s1 = min(s0 + kCompactTile, j.n_obs);
+  for (int64_t s = s0 + threadIdx.x; s < s1; s += kCompactThreads) {
+    const uint32_t i = ov[s];
+    int before = 0, older = 0;
+    bool below = false;
+    for (int b = 0; b < nb; ++b) {
+      before += bp[b] < (uint32_t)s;
+      below = below || bp[b] == (uint32_t)s;
+      older += bi[b] < i;
+    }
+    if (below) continue;
+    const int64_t o = j.seg_off + s - before;
+    keys_sorted[o] = ok[s];
+    ranks[o] = i - (uint32_t)older;
   }
 }
 
@@ -2747,19 +2892,15 @@ bool kernel_upload() {
   return on != 0;
 }
 
-// device address of a pinned host buffer (the last one asked about is
-// cached), or nullptr when it is not device-addressable pinned memory
+// device address of a pinned host buffer, or nullptr when it is not
+// device-addressable pinned memory (no cache: callers pass the address they
+// looked up once per allocation in tpe_level_ws.pinned_dev)
 char* device_alias(void* host) {
-  static void* last_h = nullptr;
-  static char* last_d = nullptr;
-  if (host == last_h) return last_d;
   hipPointerAttribute_t a;
   char* d = nullptr;
   if (hipPointerGetAttributes(&a, host) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer)
     d = (char*)a.devicePointer;
   (void)hipGetLastError();
-  last_h = host;
-  last_d = d;
   return d;
 }
 
@@ -2816,6 +2957,12 @@ int tpe_device_count(int* n) {
 
 int tpe_tile_size(void) { return kTile; }
 
+int tpe_pinned_device_address(void* host, void** dev) {
+  if (!host || !dev) return fail(TPE_E_ARG, "tpe_pinned_device_address: null pointer");
+  *dev = device_alias(host);
+  return TPE_OK;
+}
+
 int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
   if (!bytes || total_cand < 0) return fail(TPE_E_ARG, "bad arguments");
   size_t sz = 0;
@@ -2827,46 +2974,44 @@ int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes) {
   return TPE_OK;
 }
 
-int tpe_fit_workspace_bytes(int64_t total, int32_t n_fit, uint64_t* bytes) {
-  if (!bytes || total < 0 || n_fit < 0) return fail(TPE_E_ARG, "bad arguments");
-  size_t sz = 0;
-  hipError_t e = rocprim::segmented_radix_sort_pairs(
-      nullptr, sz, (const double*)nullptr, (double*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-      (unsigned int)total, (unsigned int)n_fit, (const int64_t*)nullptr, (const int64_t*)nullptr, 0u, 64u,
-      (hipStream_t)0);
-  if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
-  *bytes = (uint64_t)sz;
-  return TPE_OK;
-}
-
 int tpe_fit_above(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
   if (b->n_fit == 0) return TPE_OK;
   if (b->fit_total >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 fit observations");
+  if (b->fit_max_new < 0 || b->fit_max_obs < b->fit_max_new || b->fit_max_obs >= ((int64_t)1 << 31))
+    return fail(TPE_E_ARG, "bad fit_max_new / fit_max_obs");
   hipStream_t s = (hipStream_t)stream;
-  // every job's below list fits the gather kernel's LDS copy (host-checked sizes)
-  const int gx = (int)std::min<int64_t>(4096, std::max<int64_t>(1, (b->fit_total / b->n_fit + kFitGatherBlock - 1) /
-                                                                         kFitGatherBlock));
-  TPE_LAUNCH(k_fit_gather, dim3(gx, b->n_fit), dim3(kFitGatherBlock), 0, s, b->fit, b->below_idx,
-                     b->fit_keys, b->fit_vals);
-  if ((rc = hip_check("tpe_fit_above/gather"))) return rc;
-  if (b->fit_max_seg <= kFitSortMax) {
-    TPE_LAUNCH(k_fit_sort_lds, dim3(b->n_fit), dim3(kFitSortThreads), 0, s, b->fit_seg, b->fit_keys,
-                       b->fit_vals, b->fit_keys_sorted, b->fit_vals_sorted);
-    if ((rc = hip_check("tpe_fit_above/sort"))) return rc;
-  } else {
-    size_t sz = (size_t)b->fit_tmp_bytes;
-    hipError_t e = rocprim::segmented_radix_sort_pairs(
-        b->fit_tmp, sz, (const double*)b->fit_keys, b->fit_keys_sorted, (const uint32_t*)b->fit_vals,
-        b->fit_vals_sorted, (unsigned int)b->fit_total, (unsigned int)b->n_fit, b->fit_seg, b->fit_seg + 1, 0u, 64u,
-        s);
-    if (e != hipSuccess) {
-      snprintf(g_err, sizeof(g_err), "tpe_fit_above/sort: %s", hipGetErrorString(e));
-      return TPE_E_HIP;
+  if (b->fit_max_new > 0) {
+    // the observations appended since each order was written: sorted chunks,
+    // merged pairwise until one run per job, then merged into the resident order
+    const int64_t chunks = (b->fit_max_new + kOrdChunk - 1) / kOrdChunk;
+    TPE_LAUNCH(k_ord_chunks, dim3((unsigned)chunks, b->n_fit), dim3(kOrdChunkThreads), 0, s, b->fit, b->fit_keys,
+               b->fit_vals);
+    if ((rc = hip_check("tpe_fit_above/chunks"))) return rc;
+    double* src_k = b->fit_keys;
+    uint32_t* src_v = b->fit_vals;
+    double* dst_k = b->fit_keys_sorted;
+    uint32_t* dst_v = b->fit_vals_sorted;
+    const unsigned tiles_new = (unsigned)((b->fit_max_new + kMergeTile - 1) / kMergeTile);
+    for (int64_t L = kOrdChunk; L < b->fit_max_new; L *= 2) {
+      TPE_LAUNCH(k_ord_merge, dim3(tiles_new, b->n_fit), dim3(kMergeThreads), 0, s, b->fit, src_k, src_v, dst_k,
+                 dst_v, L);
+      std::swap(src_k, dst_k);
+      std::swap(src_v, dst_v);
     }
-    ++g_launches;
+    const unsigned tiles_obs = (unsigned)((b->fit_max_obs + kMergeTile - 1) / kMergeTile);
+    TPE_LAUNCH(k_ord_merge, dim3(tiles_obs, b->n_fit), dim3(kMergeThreads), 0, s, b->fit, src_k, src_v,
+               (double*)nullptr, (uint32_t*)nullptr, (int64_t)0);
+    if ((rc = hip_check("tpe_fit_above/merge"))) return rc;
   }
+  // below positions in fit_vals (free once the merge has run), compaction into
+  // the sorted buffers, then the build
+  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, b->fit_vals);
+  const unsigned tiles_c = (unsigned)((b->fit_max_obs + kCompactTile - 1) / kCompactTile);
+  TPE_LAUNCH(k_ord_compact, dim3(tiles_c, b->n_fit), dim3(kCompactThreads), 0, s, b->fit, b->below_idx, b->fit_vals,
+             b->fit_keys_sorted, b->fit_vals_sorted);
+  if ((rc = hip_check("tpe_fit_above/compact"))) return rc;
   TPE_LAUNCH(k_fit_build, dim3(b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
                      b->fit_vals_sorted, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32,
                      const_cast<int32_t*>(b->grid));
@@ -3125,14 +3270,10 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     if ((rc = tpe_sort_workspace_bytes(info.sort_count, &sz))) return rc;
     need->sort_tmp_bytes = (int64_t)sz;
   }
-  if (info.n_fit > 0) {
-    if ((rc = tpe_fit_workspace_bytes(info.fit_total, info.n_fit, &sz))) return rc;
-    need->fit_tmp_bytes = (int64_t)sz;
-  }
   if (rc == TPE_E_SPACE || need->pinned_bytes > ws->pinned_bytes || need->blob_bytes > ws->blob_bytes ||
       need->cand > ws->cand_cap || need->part > ws->part_cap || need->best > ws->best_cap ||
       need->result > ws->result_cap || need->fit > ws->fit_cap || need->sort_tmp_bytes > ws->sort_tmp_bytes ||
-      need->fit_tmp_bytes > ws->fit_tmp_bytes || need->draw_pref > ws->draw_pref_cap ||
+      need->draw_pref > ws->draw_pref_cap ||
       need->pool_best > ws->pool_best_cap || need->tab > ws->tab_cap)
     return fail(TPE_E_SPACE, "level workspace too small (see tpe_level_need)");
   if (P == 0) return TPE_OK;
@@ -3145,7 +3286,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   // after the copy in stream order
   hipError_t e;
   const int64_t gap = info.off_comp32 - info.copy_end;
-  char* dbase = direct_results() ? device_alias(ws->pinned) : nullptr;
+  char* dbase = !direct_results() ? nullptr : (ws->pinned_dev ? (char*)ws->pinned_dev : device_alias(ws->pinned));
   // ranges to upload: [0, n1) and [o2, o2 + n2) (one range when the gap is small)
   int64_t n1 = info.copy_end, o2 = info.off_comp32, n2 = info.copy2_len;
   if (n2 > 0 && gap <= kOneCopyMaxGap) { n1 = o2 + n2; n2 = 0; }
@@ -3244,8 +3385,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.fit_total = info.fit_total;
     b.fit_keys = ws->fit_keys; b.fit_keys_sorted = ws->fit_keys_sorted;
     b.fit_vals = ws->fit_vals; b.fit_vals_sorted = ws->fit_vals_sorted;
-    b.fit_tmp = ws->fit_tmp; b.fit_tmp_bytes = (uint64_t)ws->fit_tmp_bytes;
-    b.fit_max_seg = info.fit_max_seg;
+    b.fit_max_new = info.fit_max_new; b.fit_max_obs = info.fit_max_obs;
   }
   if (g_prof.on) {
     g_prof.valid = 0;
@@ -3275,6 +3415,137 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   }
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));
   return g_prof.on ? profile_collect(b, info, hp, n_cand) : TPE_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- shard exchange
+// RCCL entry points, resolved from librccl on first use (include/tpe_hip.h)
+namespace {
+struct Rccl {
+  bool tried = false, ok = false;
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+};
+Rccl& rccl() {
+  static Rccl r;
+  if (!r.tried) {
+    r.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (h) {
+      r.get_id = (decltype(r.get_id))dlsym(h, "ncclGetUniqueId");
+      r.init = (decltype(r.init))dlsym(h, "ncclCommInitRank");
+      r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+      r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+      r.err = (decltype(r.err))dlsym(h, "ncclGetErrorString");
+      r.ok = r.get_id && r.init && r.all_gather && r.destroy && r.err;
+    }
+  }
+  return r;
+}
+int rccl_fail(const char* what, ncclResult_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, rccl().err ? rccl().err(e) : "rccl error");
+  return TPE_E_HIP;
+}
+}  // namespace
+
+extern "C" {
+
+int tpe_comm_unique_id(void* id) {
+  if (!id) return fail(TPE_E_ARG, "tpe_comm_unique_id: null id");
+  Rccl& r = rccl();
+  if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
+  ncclUniqueId u;
+  const ncclResult_t e = r.get_id(&u);
+  if (e != ncclSuccess) return rccl_fail("ncclGetUniqueId", e);
+  static_assert(sizeof(u) == TPE_COMM_ID_BYTES, "unique id size");
+  memcpy(id, &u, sizeof(u));
+  return TPE_OK;
+}
+
+int tpe_comm_init(int32_t rank, int32_t world, const void* id, int32_t device, void** comm) {
+  if (!id || !comm || world < 1 || rank < 0 || rank >= world) return fail(TPE_E_ARG, "tpe_comm_init: bad arguments");
+  Rccl& r = rccl();
+  if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
+  if (hipSetDevice(device) != hipSuccess) return hip_check("tpe_comm_init/hipSetDevice");
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t c = nullptr;
+  const ncclResult_t e = r.init(&c, world, u, rank);
+  if (e != ncclSuccess) return rccl_fail("ncclCommInitRank", e);
+  *comm = (void*)c;
+  return TPE_OK;
+}
+
+int tpe_comm_destroy(void* comm) {
+  if (!comm) return TPE_OK;
+  Rccl& r = rccl();
+  if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
+  const ncclResult_t e = r.destroy((ncclComm_t)comm);
+  return e == ncclSuccess ? TPE_OK : rccl_fail("ncclCommDestroy", e);
+}
+
+int tpe_combine_results(const tpe_result* all, int32_t world, int64_t P, tpe_result* out) {
+  if (world < 1 || P < 0 || (P > 0 && (!all || !out))) return fail(TPE_E_ARG, "tpe_combine_results: bad arguments");
+  for (int64_t p = 0; p < P; ++p) {
+    tpe_result w = all[p];
+    for (int32_t r = 1; r < world; ++r) {
+      const tpe_result& c = all[(size_t)r * P + p];
+      if (c.idx < 0) continue;
+      if (w.idx < 0 || host_better(c.score, c.global_idx, w.score, w.global_idx)) w = c;
+    }
+    out[p] = w;
+  }
+  return TPE_OK;
+}
+
+// one exchange of a sharded level (tpe_suggest.cpp): every rank's status and
+// P results -> the global winners in res, the worst status in *status
+__attribute__((visibility("hidden"))) int tpe_internal_exchange(const tpe_exchange* ex, void* stream, int32_t my_status,
+                                                                tpe_result* res, int64_t P, int32_t* status) {
+  const int64_t per = TPE_EXCHANGE_HEADER + P * (int64_t)sizeof(tpe_result);
+  const int W = ex->world;
+  static thread_local std::vector<unsigned char> mine, all;
+  mine.assign((size_t)per, 0);
+  all.resize((size_t)per * W);
+  memcpy(mine.data(), &my_status, sizeof(my_status));
+  if (P > 0) memcpy(mine.data() + TPE_EXCHANGE_HEADER, res, (size_t)P * sizeof(tpe_result));
+  if (ex->comm) {
+    Rccl& r = rccl();
+    if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
+    if (!ex->dev || ex->dev_bytes < per * W) return fail(TPE_E_ARG, "tpe_exchange: device scratch too small");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned char* d = (unsigned char*)ex->dev;
+    hipError_t e = hipMemcpyAsync(d + (size_t)per * ex->rank, mine.data(), (size_t)per, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    // in place: rank r's block already sits at its slot of the receive buffer
+    const ncclResult_t ne = r.all_gather(d + (size_t)per * ex->rank, d, (size_t)per, ncclUint8, (ncclComm_t)ex->comm, s);
+    if (ne != ncclSuccess) return rccl_fail("ncclAllGather", ne);
+    e = hipMemcpyAsync(all.data(), d, (size_t)per * W, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  } else {
+    if (!ex->gather) return fail(TPE_E_ARG, "tpe_exchange: neither a communicator nor a gather function");
+    if (ex->gather(ex->ctx, mine.data(), per, all.data()) != 0) return fail(TPE_E_HIP, "tpe_exchange: gather failed");
+  }
+  int32_t worst = TPE_OK;
+  static thread_local std::vector<tpe_result> recs;
+  recs.resize((size_t)std::max<int64_t>(P * W, 1));
+  for (int r = 0; r < W; ++r) {
+    int32_t st;
+    memcpy(&st, all.data() + (size_t)per * r, sizeof(st));
+    // a hard error outranks a workspace retry (every rank then fails, none waits)
+    if (st != TPE_OK && (worst == TPE_OK || worst == TPE_E_SPACE)) worst = st;
+    if (P > 0) memcpy(recs.data() + (size_t)r * P, all.data() + (size_t)per * r + TPE_EXCHANGE_HEADER,
+                      (size_t)P * sizeof(tpe_result));
+  }
+  *status = worst;
+  if (worst != TPE_OK || P == 0) return TPE_OK;
+  return tpe_combine_results(recs.data(), W, P, res);
 }
 
 }  // extern "C"

@@ -21,6 +21,8 @@
 #include "../../include/tpe_hip.h"
 
 extern "C" int tpe_internal_fail(int code, const char* what);   // tpe_kernels.hip (hidden)
+extern "C" int tpe_internal_exchange(const tpe_exchange* ex, void* stream, int32_t my_status, tpe_result* res,
+                                     int64_t P, int32_t* status);     // tpe_kernels.hip (hidden)
 
 namespace {
 
@@ -182,12 +184,18 @@ extern "C" {
 
 int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
                      double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
+                     int64_t cand_base, int64_t n_cand_global, const tpe_exchange* ex,
                      uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
                      const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
                      int32_t* path, int8_t* need_fit) {
   if (n_labels < 0 || n_ids < 0 || n_cand < 0 || n_below < 0 || (n_labels > 0 && !labels) || (n_ids > 0 && !ids) ||
-      (n_below > 0 && !below_tids) || !ws || !need || !path || (n_labels > 0 && n_ids > 0 && (!values || !active)))
+      (n_below > 0 && !below_tids) || !ws || !need || !path || (n_labels > 0 && n_ids > 0 && (!values || !active)) ||
+      cand_base < 0 || n_cand_global < 0 || (n_cand_global > 0 && cand_base + n_cand > n_cand_global) ||
+      (ex && (ex->world < 1 || ex->rank < 0 || ex->rank >= ex->world)))
     return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad arguments");
+  // the candidates of the whole suggest (all shards): what the gate prediction counts
+  const int64_t c_all = n_cand_global > 0 ? n_cand_global : n_cand;
+  const bool exchange = ex && (ex->world > 1 || ex->always);
   path[0] = path[1] = 0;
   if (need_fit) memset(need_fit, 0, (size_t)std::max(n_labels, 0));
   static thread_local std::vector<Fit> fits_tl;
@@ -211,8 +219,15 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
     }
     T.max_depth = std::max(T.max_depth, L.depth);
   }
-  for (int i = 0; i < n_labels; ++i)
-    if (T.gate[(size_t)i] && labels[i].family != TPE_FAM_CATEGORICAL) return TPE_E_FALLBACK;
+  // spaces for the general path, refused before any fit or run: non-categorical
+  // gates, and continuous labels large enough for the device Parzen fit
+  for (int i = 0; i < n_labels; ++i) {
+    const tpe_tree_label& L = labels[i];
+    if (T.gate[(size_t)i] && L.family != TPE_FAM_CATEGORICAL) return TPE_E_FALLBACK;
+    if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && L.host_k[0] <= 0 && device_fit_min > 0 &&
+        L.n_obs >= std::max<int64_t>(device_fit_min, 64))
+      return TPE_E_FALLBACK;
+  }
   if (n_labels == 0 || n_ids == 0) return TPE_OK;
   const int32_t run_flags = flags & ~TPE_TREE_NO_SPECULATE;
   std::vector<tpe_label_in>& recs = recs_tl;
@@ -222,8 +237,19 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
     for (int32_t r = 0; r < n_recs; ++r) P += recs[(size_t)r].n_ids;
     res.resize((size_t)std::max<int64_t>(P, 1));
     ++path[1];
-    return tpe_level_run(recs.data(), n_recs, n_cand, seed, 0, 0, TPE_PREC_F32, run_flags, ws, need, stream,
-                         res.data());
+    int rc = tpe_level_run(recs.data(), n_recs, n_cand, seed, cand_base, n_cand_global, TPE_PREC_F32, run_flags, ws,
+                           need, stream, res.data());
+    if (!exchange) return rc;
+    // every rank takes part in the exchange, whatever its own status
+    if (rc != TPE_OK)
+      for (int64_t q = 0; q < P; ++q) res[(size_t)q] = tpe_result{0, 0, 0, 0, -1, -1};
+    int32_t all_rc = TPE_OK;
+    const int xrc = tpe_internal_exchange(ex, stream, rc, res.data(), P, &all_rc);
+    if (xrc != TPE_OK) return xrc;
+    if (rc != TPE_OK) return rc;
+    if (all_rc == TPE_E_SPACE) return tpe_internal_fail(TPE_E_SPACE, "another rank needs a larger workspace");
+    if (all_rc != TPE_OK) return tpe_internal_fail(all_rc, "a level run failed on another rank");
+    return TPE_OK;
   };
 
   // speculative fusion (hyperopt_amd.tpe._choices_fused): every level in one
@@ -231,7 +257,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
   if (!(flags & TPE_TREE_NO_SPECULATE) && speculate_min_draws >= 0 && T.max_depth > 0) {
     bool ok = false;
     std::vector<int>& pred = pred_tl;
-    int rc = predict(T, n_cand, speculate_min_draws, pred, ok);
+    int rc = predict(T, c_all, speculate_min_draws, pred, ok);
     if (rc != TPE_OK) return rc;
     if (ok) {
       recs.resize((size_t)n_labels);

@@ -83,7 +83,7 @@ def _tab_plan(lp, n_cand, f64):
     if fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS) and not f64:
         s0 = float(np.min(post.below[2]))
         if post.above_dev is not None:
-            col, n_obs, bidx = post.above_dev
+            n_obs, bidx = post.above_dev[1:3]
             s1 = post.prior[1] / min(100.0, 1.0 + float(n_obs - len(bidx) + 1))
         else:
             s1 = float(np.min(post.above[2]))
@@ -463,7 +463,7 @@ class Engine(object):
                            post.low if post.low is not None else 0.0, post.high if post.high is not None else 0.0,
                            post.q if post.q is not None else 0.0,
                            pt[0], pt[1], pt[2], pt[3], pt[4], pt[5], pt[6], pt[7],
-                           ia, len(ids), 0, 0, 0, 0, 0, 0.0, 0.0, 0.0)
+                           ia, len(ids), 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 0, 0, 0, 0)
                 continue
             bw = [np.ascontiguousarray(a, dtype=np.float64) for a in post.below]
             ids = np.ascontiguousarray(lp.ids, dtype=np.int64)
@@ -471,24 +471,35 @@ class Engine(object):
             keep.append(ids)
             bptr = [a.ctypes.data for a in bw] + [0] * (3 - len(bw))
             if post.above_dev is not None:
-                col, n_obs, bidx = post.above_dev
+                col, n_obs, bidx, order = post.above_dev
                 bidx = np.ascontiguousarray(bidx, dtype=np.int32)
                 keep.append(bidx)
                 aptr, ak = [0, 0, 0], n_obs - len(bidx) + 1
                 dev = (col.data_ptr(), n_obs, bidx.ctypes.data, len(bidx))
                 prior = post.prior
+                ordp = order.ptrs(n_obs)          # the label's resident value order (ValueOrder)
             else:
                 aw = [np.ascontiguousarray(a, dtype=np.float64) for a in post.above]
                 keep.append(aw)
                 aptr, ak = [a.ctypes.data for a in aw] + [0] * (3 - len(aw)), len(aw[0])
-                dev, prior = (0, 0, 0, 0), (0.0, 0.0, 0.0, 0)
+                dev, prior, ordp = (0, 0, 0, 0), (0.0, 0.0, 0.0, 0), (0, 0, 0, 0, 0)
             recs[i] = (post.family, flags, int(post.upper), lp.label_ix,
                        post.low if post.low is not None else 0.0, post.high if post.high is not None else 0.0,
                        post.q if post.q is not None else 0.0,
                        bptr[0], bptr[1], bptr[2], len(bw[0]), aptr[0], aptr[1], aptr[2], ak,
                        ids.ctypes.data, len(ids), dev[0], dev[1], dev[2], dev[3], prior[3],
-                       prior[0], prior[1], prior[2])
+                       prior[0], prior[1], prior[2]) + ordp
         return recs.ctypes.data, keep
+
+    @staticmethod
+    def _commit_orders(problems):
+        """A level with these problems was enqueued: the device-fitted labels'
+        merged value orders are now their resident orders (stream order makes
+        them valid for every later launch on the stream)."""
+        for lp in problems:
+            ad = lp.post.above_dev
+            if ad is not None:
+                ad[3].commit(ad[1])
 
     def _pack(self, problems, n_cand, seed, cand_base, n_cand_global):
         """Pack one level with the native host runtime straight into the pinned
@@ -532,6 +543,11 @@ class Engine(object):
             return (t.data_ptr(), t.numel() * t.element_size() // itemsize) if t is not None else (None, 0)
         pin = self._pinned
         ws.pinned, ws.pinned_bytes = (pin.data_ptr(), pin.numel()) if pin is not None else (None, 0)
+        if pin is not None:            # the staging buffer's device address, once per allocation
+            dp = ctypes.c_void_p()
+            N.check(self.lib.tpe_pinned_device_address(pin.data_ptr(), ctypes.byref(dp)), self.lib,
+                    'tpe_pinned_device_address')
+            ws.pinned_dev = dp.value
         ws.blob, ws.blob_bytes = dev('blob', 1)
         ws.cand, n1 = dev('cand', 8)
         ws.coord, n2 = dev('coord', 4)
@@ -549,7 +565,6 @@ class Engine(object):
         ws.fit_vals, f3 = dev('fit_vals', 4)
         ws.fit_vals_sorted, f4 = dev('fit_vals_sorted', 4)
         ws.fit_cap = min(f1, f2, f3, f4)
-        ws.fit_tmp, ws.fit_tmp_bytes = dev('fit_tmp', 1)
         ws.draw_pref, ws.draw_pref_cap = dev('draw_pref', 8)
         ws.pool_best, ws.pool_best_cap = dev('pool_best', 8)
         ws.tab, ws.tab_cap = dev('tab', 16)
@@ -571,7 +586,6 @@ class Engine(object):
         for name, dt in (('fit_keys', torch.float64), ('fit_keys_sorted', torch.float64),
                          ('fit_vals', torch.int32), ('fit_vals_sorted', torch.int32)):
             self._buf(name, need.fit, dt)
-        self._buf('fit_tmp', need.fit_tmp_bytes, torch.uint8)
         self._buf('draw_pref', need.draw_pref, torch.float64)
         self._buf('pool_best', need.pool_best, torch.int64)
         self._buf('tab', 4 * need.tab, torch.float32)
@@ -606,19 +620,23 @@ class Engine(object):
         if prof:
             self.lib.tpe_level_profile(0)
         N.check(rc, self.lib, 'tpe_level_run')
+        self._commit_orders(problems)
         del keep
         if prof and P:
             self._record_level_profile()
         return out
 
-    def suggest_tree(self, labels, below_sorted, prior_weight, lf, ids, n_cand, seed, min_draws, flags=0):
+    def suggest_tree(self, labels, below_sorted, prior_weight, lf, ids, n_cand, seed, min_draws, flags=0,
+                     shard=None, exchange=None):
         """A whole tpe.suggest of a tree space in one native call
         (tpe_suggest_tree): fits, gate prediction and level runs.  ``labels``:
         TREE_LABEL_DTYPE records in label order; ``below_sorted``: int64
-        ascending below tids.  Returns (values, active) [n_ids x n_labels], or
-        (None, need_fit) on TPE_E_FALLBACK: need_fit [n_labels] flags the
-        labels the caller must fit and pass back (none: take the general
-        path)."""
+        ascending below tids; ``shard`` = (rank, world) with ``exchange`` (a
+        dist._Exchange): this rank scores its range of the ``n_cand``
+        candidates and the native call exchanges every level's results.
+        Returns (values, active) [n_ids x n_labels], or (None, need_fit) on
+        TPE_E_FALLBACK: need_fit [n_labels] flags the labels the caller must
+        fit and pass back (none: take the general path)."""
         if self.precision != 'fp32':
             return None, np.zeros(len(labels), dtype=np.int8)
         ids = np.ascontiguousarray(ids, dtype=np.int64)
@@ -636,11 +654,17 @@ class Engine(object):
         if prof:
             N.check(self.lib.tpe_level_profile(1), self.lib, 'tpe_level_profile')
         fl = self._flags() | int(flags)
+        c_loc, base, c_glob, ex = n_cand, 0, 0, None
+        if shard is not None:
+            from .dist import shard_range
+            base, hi = shard_range(n_cand, shard[0], shard[1])
+            c_loc, c_glob = hi - base, n_cand
+            ex = exchange.ptr(nl * n)
         for attempt in range(8):          # a later tree level may need larger pools than the first
             ws = self._level_ws()
             rc = self.lib.tpe_suggest_tree(labels.ctypes.data, nl, below_sorted.ctypes.data, len(below_sorted),
-                                           float(prior_weight), int(lf), ids.ctypes.data, n, n_cand, seed64,
-                                           float(min_draws), int(self.device_fit_min), fl, ctypes.byref(ws),
+                                           float(prior_weight), int(lf), ids.ctypes.data, n, c_loc, base, c_glob, ex,
+                                           seed64, float(min_draws), int(self.device_fit_min), fl, ctypes.byref(ws),
                                            ctypes.byref(need), stream, values.ctypes.data, active.ctypes.data, path,
                                            need_fit.ctypes.data)
             if rc != N.E_SPACE:
@@ -778,22 +802,18 @@ class Engine(object):
             d_fks = self._buf('fit_keys_sorted', ft, torch.float64)
             d_fv = self._buf('fit_vals', ft, torch.int32)
             d_fvs = self._buf('fit_vals_sorted', ft, torch.int32)
-            ws = ctypes.c_uint64(0)
-            N.check(self.lib.tpe_fit_workspace_bytes(ft, int(info.n_fit), ctypes.byref(ws)), self.lib,
-                    'tpe_fit_workspace_bytes')
-            d_ft = self._buf('fit_tmp', ws.value, torch.uint8)
             b.fit, b.n_fit = base + info.off_fit, info.n_fit
             b.below_idx, b.fit_seg, b.fit_total = base + info.off_below_idx, base + info.off_fit_seg, ft
             b.fit_keys, b.fit_keys_sorted = d_fk.data_ptr(), d_fks.data_ptr()
             b.fit_vals, b.fit_vals_sorted = d_fv.data_ptr(), d_fvs.data_ptr()
-            b.fit_tmp, b.fit_tmp_bytes = d_ft.data_ptr(), d_ft.numel()
-            b.fit_max_seg = info.fit_max_seg
+            b.fit_max_new, b.fit_max_obs = info.fit_max_new, info.fit_max_obs
         stream = self._stream()
         if self.profile is None:
             N.check(self.lib.tpe_run_batch(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, 'tpe_run_batch')
         else:
             tb = dict(prob=prob.copy(), counts_w=[info.n_work_cont, info.n_work_qgauss, info.n_work_qlog], P=P)
             self._run_profiled(b, stream, tb, n_cand)
+        self._commit_orders(problems)
         res = d_res[:P * 6].cpu().numpy().view(N.RESULT_DTYPE).copy()
         if not (want_lg or return_cand):
             return res

@@ -11,6 +11,12 @@ source of truth (resume via pickled Trials keeps working).
 Fast path requirements (else the generic reference-order walk is used):
 documents in increasing tid order, unique tids, no ``misc['from_tid']``,
 and ``Domain.loss`` not overridden.
+
+Completed documents are treated as immutable once seen, as FMinIter treats
+them; every change that goes through ``Trials`` (insert, refresh dropping or
+replacing documents) and every change to a pending document (values or
+loss) is picked up.  A completed document edited in place must be replaced
+in the Trials list (then ``refresh()``), not mutated.
 """
 import weakref
 
@@ -119,11 +125,13 @@ class _Grow(object):
 
 
 class _Cache(object):
-    def __init__(self, labels, categorical):
+    def __init__(self, labels, categorical, gen=0):
+        self.gen = gen                 # Trials._view_gen the cache was built against
         self.docs = []                 # document objects in list order
         self.tids = _Grow(np.int64)
         self.losses = _Grow(np.float64)
         self.pending = []              # positions whose loss may still change
+        self.pending_vals = {}         # position -> (misc['vals'] object, its values) of a pending document
         self.obs_tid = {k: _Grow(np.int64) for k in labels}     # tid of each observation (append-only)
         self.obs_val = {k: _Grow(np.int64 if categorical[k] else np.float64) for k in labels}
         self.labels = labels
@@ -152,14 +160,29 @@ class _Cache(object):
             loss = d['result'].get('loss')
             final = d['state'] == base.JOB_STATE_DONE and loss is not None
             self.losses.append(np.inf if loss is None else float(loss))
+            vals = misc['vals']
             if not final:
                 self.pending.append(self.tids.n - 1)
-            vals = misc['vals']
+                self.pending_vals[self.tids.n - 1] = (vals, self._snap(vals))
             for k in self.labels:
                 v = vals.get(k)
                 if v:
                     self.obs_tid[k].append(tid)
                     self.obs_val[k].append(v[0])
+
+    def _snap(self, vals):
+        return tuple(tuple(vals.get(k) or ()) for k in self.labels)
+
+    def pending_vals_changed(self):
+        """A pending document's values were edited or replaced (a running
+        trial's document is still written to; the reference re-reads every
+        document, tpe.py:820-842)."""
+        for i in self.pending:
+            vals, snap = self.pending_vals[i]
+            cur = self.docs[i]['misc']['vals']
+            if cur is not vals or self._snap(cur) != snap:
+                return True
+        return False
 
     def log_values(self, k):
         """np.log(obs_val[k]), the values appended since the last call logged
@@ -245,6 +268,8 @@ class _Cache(object):
             L[i] = np.inf if loss is None else float(loss)
             if not (d['state'] == base.JOB_STATE_DONE and loss is not None):
                 keep.append(i)
+            else:
+                self.pending_vals.pop(i, None)
         self.pending = keep
 
 
@@ -286,20 +311,23 @@ def extract(domain, trials):
         return _generic(domain, docs, table)
     cache = _CACHES.get(trials)
     labels = table.labels
-    if cache is not None and (cache.labels != labels or not cache.ok):
+    gen = getattr(trials, '_view_gen', 0)
+    if cache is not None and (cache.labels != labels or not cache.ok or cache.gen != gen):
         cache = None
     if cache is not None:
         n = len(cache.docs)
-        # the cache assumes Trials is append-only (FMinIter's use): documents
-        # already seen stay where they are and keep their values.  Dropped
-        # (ERROR) or replaced documents shift or change the documents it
-        # checks — both ends and 7 evenly spaced positions — and force a rebuild.
+        # the cache follows an append-only view (FMinIter's use): completed
+        # documents stay where they are and keep their values.  A refresh that
+        # drops, replaces or reorders documents moves Trials._view_gen (above);
+        # a view list edited without a refresh shifts or changes the documents
+        # checked here — both ends and 7 evenly spaced positions; a pending
+        # document is re-read in full (its values and, below, its loss).
         if n > len(docs) or (n and any(docs[i] is not cache.docs[i] for i in
                                        {0, n - 1, n // 8, n // 4, 3 * n // 8, n // 2, 5 * n // 8, 3 * n // 4,
-                                        7 * n // 8})):
+                                        7 * n // 8})) or cache.pending_vals_changed():
             cache = None
     if cache is None:
-        cache = _Cache(labels, {r.label: r.categorical for r in table.rows})
+        cache = _Cache(labels, {r.label: r.categorical for r in table.rows}, gen)
         start = 0
     else:
         start = len(cache.docs)

@@ -139,7 +139,7 @@ class Posterior(object):
     q           quantum or None
     below/above (w, mu, sigma) float64 arrays, or (p,) for categorical
     upper       number of categories (categorical)
-    above_dev   None, or (device column, n_obs, below_idx int32) when the above
+    above_dev   None, or (device column, n_obs, below_idx int32, devhist.ValueOrder) when the above
                 mixture is fitted on the device (engine: tpe_fit_above); then
                 ``above`` is None and ``prior`` = (mu, sigma, weight, lf)
     """
@@ -191,7 +191,7 @@ DEVICE_FIT_FAMILIES = (N.FAM_GAUSS, N.FAM_LOGGAUSS)
 
 def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT_LF, above_dev=None):
     """Fit the below and above posteriors of one hyperparameter.  With
-    ``above_dev`` = (device column, n_obs, below_idx) the above mixture is left
+    ``above_dev`` = (device column, n_obs, below_idx, value order) the above mixture is left
     to the device fit (continuous families only; ``above_obs`` is ignored)."""
     family = _FAMILY[dist]
     a = args

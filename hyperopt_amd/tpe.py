@@ -85,9 +85,12 @@ class _Fits(object):
                     and len(ovals) >= max(eng.device_fit_min, 64)):
                 bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
                 if len(ovals) - len(bidx) >= max(eng.device_fit_min, 64):
-                    col = devhist.columns(self.hist, eng.device).column(row.label, ovals)
+                    dc = devhist.columns(self.hist, eng.device)
+                    # the kernel coordinate (numpy's log for the log families, as the host fits use)
+                    logc = _FAMILY[row.dist] == N.FAM_LOGGAUSS
+                    col = dc.column(row.label, self.hist.log_values(row.label) if logc else ovals)
                     post = fit_posterior(row.dist, row.args, ovals[bidx], None, self.prior_weight, DEFAULT_LF,
-                                         above_dev=(col, len(ovals), bidx))
+                                         above_dev=(col, len(ovals), bidx, dc.order(row.label)))
             if post is not None:
                 pass
             elif row.categorical and self.hist.sorted_obs:
@@ -305,12 +308,12 @@ def _tree_labels(table, hist):
         return None
     arr0, _, meta = st
     cache = hist._cache
-    key = None
     if cache is not None:
-        key = (len(cache.docs), id(table))
+        # keyed on the table OBJECT (the memo keeps it alive, so a new table can
+        # never reuse its id) and the document count
         memo = getattr(cache, 'tree_memo', None)
-        if memo is not None and memo[0] == key:
-            return memo[1]
+        if memo is not None and memo[0] is table and memo[1] == len(cache.docs):
+            return memo[2]
     arr = arr0.copy()
     keep = []
     for label, ix, fam in meta:
@@ -340,21 +343,33 @@ def _tree_labels(table, hist):
             rec['tids'], rec['values'], rec['order'] = cols
     out = (arr, keep)
     if cache is not None:
-        cache.tree_memo = (key, out)
+        cache.tree_memo = (table, len(cache.docs), out)
     return out
 
 
-def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight):
+def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None):
     """``_choices_philox`` in one native call (tpe_suggest_tree), or None when
     the space or history needs the general path.  Labels the native fits cannot
     reproduce (quantized ones, sides with repeated values: numpy's argsort tie
     order decides their weights) come back flagged; they are fitted here
-    exactly as the general path fits them and handed to a second call."""
+    exactly as the general path fits them and handed to a second call.
+    ``shard`` = (rank, world): candidate-sharded over the default process
+    group, the level results exchanged inside the native call (dist.py)."""
+    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard)
+    if out is None:
+        table.native_fit_hint = ()             # the general path takes it: nothing to pre-fit next time
+    return out
+
+
+def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard):
     if not hist.sorted_obs:
         return None
     tl = _tree_labels(table, hist)
     if tl is None:
         return None
+    ex = None
+    if shard is not None:
+        ex = _dist.exchange_for(engine)
     below = np.sort(np.asarray(below_tids, dtype=np.int64))
     st = {'arr': tl[0]}
     host = {}
@@ -382,12 +397,12 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     # branch seldom changes between suggests): no refused first call
     for ix in getattr(table, 'native_fit_hint', ()):
         if not give(ix):
-            table.native_fit_hint = ()
             return None
     # (a level-by-level run learns a deeper level's needs only after the levels above it)
     for attempt in range(table.n_levels + 1):
         values, active = engine.suggest_tree(st['arr'], below, prior_weight, DEFAULT_LF, new_ids, C, seed,
-                                             SPECULATE_MIN_DRAWS if SPECULATE else -1.0)
+                                             SPECULATE_MIN_DRAWS if SPECULATE else -1.0, shard=shard,
+                                             exchange=ex)
         if values is not None:
             break
         need = np.flatnonzero(active)          # (need_fit on TPE_E_FALLBACK)
@@ -486,8 +501,8 @@ def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weig
     engine = get_engine(device, precision)
     below_tids = _history.split_below(hist, gamma)
     C = int(n_EI_candidates)
-    if sampler == 'philox' and shard is None and NATIVE_TREE and precision == 'fp32':
-        out = _choices_native(table, hist, below_tids, list(new_ids), seed, C, engine, prior_weight)
+    if sampler == 'philox' and NATIVE_TREE and precision == 'fp32':
+        out = _choices_native(table, hist, below_tids, list(new_ids), seed, C, engine, prior_weight, shard)
         if out is not None:
             return out
     fits = _Fits(table, hist, below_tids, prior_weight, engine)

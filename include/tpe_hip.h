@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 13
+#define TPE_ABI_VERSION 14
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -267,22 +267,39 @@ typedef struct tpe_result {
  * Device Parzen fit of one continuous above mixture (families 0/1, f32 tables):
  * adaptive_parzen_normal (tpe.py:398-475) of the label's observations that are
  * not in the below set (ap_filter_trials, tpe.py:613-641), written straight
- * into the pruned comp32 layout above.  Stages (tpe_fit_above):
- *   gather   above observations (t = x, or ln x for LOGGAUSS) + their rank in
- *            tid order (the linear-forgetting weight index) into the fit sort
- *            buffers at [seg_off, seg_off + n_obs - n_below)
- *   sort     segmented radix sort by t (stable: equal values stay in tid order)
+ * into the pruned comp32 layout above.
+ *
+ * Device value order.  The reference argsorts the above observations on every
+ * suggest (tpe.py:427).  Here each device-fitted label keeps a RESIDENT value
+ * order of ALL its observations in HBM — (t, i) pairs sorted by t ascending,
+ * NaN last, ties by i (t = x, or ln x for LOGGAUSS; i = position in tid
+ * order) — owned by the caller and extended, not rebuilt: the history is
+ * append-only, so a suggest only merges the observations appended since the
+ * order was last written (obs[n_ord_in .. n_obs)).  Stages (tpe_fit_above):
+ *   chunks   the new observations, 8192 at a time, sorted in LDS (bitonic)
+ *   passes   merge-path merges of the sorted chunks (only when a job has more
+ *            than 8192 new observations, i.e. the first suggest)
+ *   merge    merge-path merge of the resident order ord_*_in [n_ord_in] with the
+ *            sorted new batch into ord_*_out [n_obs] (skipped when nothing is new:
+ *            the order is then read from ord_*_in)
+ *   compact  the order without the below observations, each with its rank among
+ *            the above observations in tid order (the linear-forgetting weight
+ *            index) — exactly the stable argsort of the above observations
  *   build    one workgroup per job: prior insertion (searchsorted left), sigma
  *            from neighbour gaps, clip, LF weights, normalisation, {mu, a, c}
  *            rows, wide list, grid; patches the job's problem rows (above_base,
  *            wide_len, prior_*, narrow_*, grid_lo/inv)
+ * No sort of the whole history runs after the first suggest: a steady-state
+ * suggest costs one merge pass over each label's order (none when nothing was
+ * appended) plus the compaction and the build.
  * The host reserves above_off[0 .. K) + wide_off[0 .. 16) rows and grid_n + 1
  * grid entries (K = n_obs - n_below + 1, grid_n = min(4096, 4K)).
  */
 typedef struct tpe_fit_job {
-  const double* obs;     /* device: the label's observations in tid order (sampling space) */
+  const double* obs;     /* device: the label's observations in tid order, in the kernel
+                            coordinate t (x, or the caller's np.log(x) for LOGGAUSS) */
   int64_t n_obs;
-  int64_t seg_off;       /* first slot of this job in the fit sort buffers     */
+  int64_t seg_off;       /* first slot of this job in the fit scratch buffers (fit_seg)   */
   int32_t below_off;     /* below_idx[below_off ..]: ascending indices into obs */
   int32_t n_below;
   int32_t family, flags, lf;
@@ -290,6 +307,10 @@ typedef struct tpe_fit_job {
   int32_t above_off, wide_off, grid_off, grid_n;
   int32_t reserved;
   double prior_mu, prior_sigma, prior_weight, low, high;
+  /* resident value order (device, caller-owned): the first n_ord_in observations
+   * sorted, and where the order of all n_obs goes when n_ord_in < n_obs */
+  const double* ord_key_in; const uint32_t* ord_idx_in; int64_t n_ord_in;
+  double* ord_key_out; uint32_t* ord_idx_out;
 } tpe_fit_job;
 
 /* all device pointers of one batch (the struct itself lives in host memory) */
@@ -333,12 +354,13 @@ typedef struct tpe_batch {
   /* device Parzen fits (n_fit == 0: none); they patch rows of `problems` */
   const tpe_fit_job* fit; int32_t n_fit; int32_t reserved4;
   const int32_t* below_idx;   /* below indices of every job                        */
-  const int64_t* fit_seg;     /* [n_fit + 1] segment offsets into the fit buffers  */
+  const int64_t* fit_seg;     /* [n_fit + 1] segment offsets into the fit scratch: a job's
+                                 segment holds max(n_obs - n_below, n_obs - n_ord_in, n_below) */
   int64_t fit_total;          /* fit_seg[n_fit]                                    */
-  double* fit_keys; double* fit_keys_sorted;        /* [fit_total]                */
+  double* fit_keys; double* fit_keys_sorted;        /* [fit_total] scratch (ping-pong) */
   uint32_t* fit_vals; uint32_t* fit_vals_sorted;    /* [fit_total]                */
-  void* fit_tmp; uint64_t fit_tmp_bytes;            /* tpe_fit_workspace_bytes()  */
-  int64_t fit_max_seg;        /* longest fit segment (<= 8192: sorted in LDS, no fit_tmp use) */
+  int64_t fit_max_new;        /* most new observations of one job (n_obs - n_ord_in) */
+  int64_t fit_max_obs;        /* most observations of one job                       */
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
   double* draw_pref; int64_t draw_blocks; int32_t n_sorted; int32_t reserved5;
   unsigned long long* pool_best;   /* [n_problems] (pooled problems; see "Pooled labels") */
@@ -376,11 +398,12 @@ int tpe_device_count(int* n);
 /* candidates per tile (2048) — the caller sizes tiles / work items with it */
 int tpe_tile_size(void);
 
+/* device address of page-locked host memory (NULL when the device cannot
+ * address it): look it up once per allocation for tpe_level_ws.pinned_dev */
+int tpe_pinned_device_address(void* host, void** dev);
+
 /* device workspace (bytes) the candidate sort needs for `total_cand` candidates */
 int tpe_sort_workspace_bytes(int64_t total_cand, uint64_t* bytes);
-
-/* device workspace (bytes) of the fit sort for `total` observations in `n_fit` segments */
-int tpe_fit_workspace_bytes(int64_t total, int32_t n_fit, uint64_t* bytes);
 
 /* fit (when n_fit > 0) -> tables -> sample (optional) -> sort -> score -> select, enqueued on `stream` (hipStream_t);
  * asynchronous: results are valid once the stream reaches this point. */
@@ -404,10 +427,13 @@ int tpe_select(const tpe_batch* batch, void* stream);
  * active for (mixtures are float64 host arrays; categorical: below_w / above_w
  * are the probabilities, *_k = number of categories).
  * Device-fitted above mixture (families 0/1, TPE_PREC_F32 only): above_w/mu/
- * sigma NULL, dev_obs = the label's device observation column (n_obs values in
- * tid order), below_idx = host array of the n_below ascending indices of the
+ * sigma NULL, dev_obs = the label's device observation column (n_obs kernel
+ * coordinates t in tid order: x, or np.log(x) for LOGGAUSS), below_idx = host array of the n_below ascending indices of the
  * below observations in it, above_k = n_obs - n_below + 1; prior_* and lf are
- * the fit parameters. */
+ * the fit parameters; ord_* = the label's resident value order (tpe_fit_job:
+ * ord_*_in may be NULL when n_ord_in = 0, ord_*_out may be NULL when
+ * n_ord_in = n_obs).  After the level has run, ord_*_out holds the order of
+ * all n_obs observations whenever n_ord_in < n_obs. */
 typedef struct tpe_label_in {
   int32_t family, flags, upper, label_ix;
   double low, high, q;
@@ -417,6 +443,8 @@ typedef struct tpe_label_in {
   const double* dev_obs; int64_t n_obs;
   const int32_t* below_idx; int32_t n_below; int32_t lf;
   double prior_mu, prior_sigma, prior_weight;
+  const double* ord_key_in; const uint32_t* ord_idx_in; int64_t n_ord_in;
+  double* ord_key_out; uint32_t* ord_idx_out;
 } tpe_label_in;
 
 /* where tpe_host_pack_level put each table in the blob (byte offsets).  The
@@ -435,7 +463,8 @@ typedef struct tpe_pack_info {
   int64_t copy_end, copy2_len;
   int64_t sort_count;               /* candidates of the sorted (pruned) problems */
   int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
-  int64_t fit_max_seg;                  /* tpe_batch.fit_max_seg */
+  int64_t fit_max_new;                  /* tpe_batch.fit_max_new */
+  int64_t fit_max_obs;                  /* tpe_batch.fit_max_obs */
   int64_t n_sorted, draw_blocks;        /* tpe_batch.n_sorted / draw_blocks */
   int64_t n_pooled;                     /* pooled problems (tpe_batch.pool_best needed) */
   int64_t off_tab_jobs, n_tab_jobs, tab_blocks, tab_units;   /* tabulated scoring (tpe_batch.tab_*) */
@@ -519,6 +548,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
  * ---------------------------------------------------------------------- */
 typedef struct tpe_level_ws {
   void* pinned; int64_t pinned_bytes;          /* page-locked host staging (tables + result readback) */
+  void* pinned_dev;                            /* its device address (tpe_pinned_device_address), or NULL:
+                                                  looked up by the call                                 */
   void* blob; int64_t blob_bytes;              /* device copy of the packed tables                      */
   double* cand; float* coord;                  /* device candidate pools, cand_cap elements each        */
   uint32_t* keys; uint64_t* vals; uint32_t* keys_sorted; uint64_t* vals_sorted; int64_t cand_cap;
@@ -528,7 +559,6 @@ typedef struct tpe_level_ws {
   tpe_result* result; int64_t result_cap;      /* elements (device)                                     */
   double* fit_keys; double* fit_keys_sorted;
   uint32_t* fit_vals; uint32_t* fit_vals_sorted; int64_t fit_cap;   /* elements                    */
-  void* fit_tmp; int64_t fit_tmp_bytes;
   double* draw_pref; int64_t draw_pref_cap;    /* elements                                              */
   unsigned long long* pool_best; int64_t pool_best_cap;   /* elements                                   */
   void* tab; int64_t tab_cap;                  /* score tables, 16-B units                              */
@@ -536,8 +566,7 @@ typedef struct tpe_level_ws {
 
 /* what a level needs (written on success and on TPE_E_SPACE) */
 typedef struct tpe_level_need {
-  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, fit_tmp_bytes, draw_pref,
-      pool_best, tab;
+  int64_t pinned_bytes, blob_bytes, cand, sort_tmp_bytes, part, best, result, fit, draw_pref, pool_best, tab;
 } tpe_level_need;
 
 /* Run one tree level: `labels` as for tpe_host_pack_level; `out` receives one
@@ -596,9 +625,54 @@ typedef struct tpe_tree_label {
 /* tpe_suggest_tree flags: the tpe_level_run flags, plus */
 enum { TPE_TREE_NO_SPECULATE = 1 << 8 };    /* level by level only (no fused batch)                    */
 
+/* ------------------------------------------------------------------------
+ * Candidate-shard exchange (multi-GPU, one process per GPU).  A sharded
+ * suggest gives every rank the contiguous global candidate range
+ * [cand_base, cand_base + n_cand) of each problem (Philox counters are global
+ * indices, so the candidates are the ones a single GPU draws there).  After
+ * each level run, the ranks all-gather their per-problem results — a header
+ * with the rank's status, then P tpe_result records — and every rank reduces
+ * them to the global winners with np.argmax semantics (NaN first, then the
+ * largest score, then the lowest global index; the reference's per-parameter
+ * argmax, tpe.py:749-759), so every rank takes the same tree decisions.  A
+ * rank whose level run needs a larger workspace still takes part (status
+ * TPE_E_SPACE, empty results) and then every rank returns TPE_E_SPACE: the
+ * callers grow and call again in lock-step.
+ * The all-gather is an RCCL all-gather over xGMI on the device scratch `dev`
+ * when `comm` is set (tpe_comm_init), else the caller's host all-gather.
+ * ---------------------------------------------------------------------- */
+#define TPE_COMM_ID_BYTES 128
+#define TPE_EXCHANGE_HEADER 64   /* bytes before a rank's result records in the exchange */
+typedef int (*tpe_gather_fn)(void* ctx, const void* mine, int64_t bytes, void* all);
+typedef struct tpe_exchange {
+  int32_t rank, world;
+  void* comm;             /* RCCL communicator (tpe_comm_init), or NULL                          */
+  tpe_gather_fn gather;   /* host all-gather: `bytes` from every rank into all[world * bytes], in
+                             rank order; returns 0 on success (used when comm is NULL)          */
+  void* ctx;
+  void* dev; int64_t dev_bytes;   /* RCCL path: device scratch of world * (TPE_EXCHANGE_HEADER +
+                                     P * sizeof(tpe_result)) bytes for the largest level          */
+  int32_t always;         /* exchange even when world == 1 (tests of the exchange itself)       */
+  int32_t reserved;
+} tpe_exchange;
+
+/* RCCL communicator of one process per GPU: rank 0 makes the id, the caller
+ * broadcasts its TPE_COMM_ID_BYTES bytes, every rank calls tpe_comm_init on
+ * its device.  librccl is loaded on first use (no link-time dependency). */
+int tpe_comm_unique_id(void* id);
+int tpe_comm_init(int32_t rank, int32_t world, const void* id, int32_t device, void** comm);
+int tpe_comm_destroy(void* comm);
+
+/* the exchange's reduction on the host: all[world][P] -> out[P], np.argmax
+ * order over (score, global_idx), empty records (idx < 0) skipped */
+int tpe_combine_results(const tpe_result* all, int32_t world, int64_t P, tpe_result* out);
+
 /* below_tids ascending (the n_below best trials, tpe.py:625-629); ids: the
- * n_ids new trial ids; speculate_min_draws: a gate is predicted when its
- * predicted category is expected among >= this many of the n_cand draws;
+ * n_ids new trial ids; n_cand candidates per problem on this rank, global
+ * indices [cand_base, cand_base + n_cand) of n_cand_global (unsharded: 0, 0);
+ * ex: the shard exchange (NULL unsharded); speculate_min_draws: a gate is
+ * predicted when its predicted category is expected among >= this many of the
+ * n_cand_global draws;
  * device_fit_min > 0: labels with that many observations are left to the host
  * path (device Parzen fit).  values / active: [n_ids x n_labels] — the chosen
  * value (categories as doubles) and whether the label is active; path[0] = 1
@@ -607,6 +681,7 @@ enum { TPE_TREE_NO_SPECULATE = 1 << 8 };    /* level by level only (no fused bat
  * TPE_E_SPACE: grow the workspace to `need` and call again. */
 int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
                      double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
+                     int64_t cand_base, int64_t n_cand_global, const tpe_exchange* ex,
                      uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
                      const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
                      int32_t* path, int8_t* need_fit);

@@ -104,7 +104,7 @@ def test_engine_refuses_without_device():
 
 CTYPES_MIRRORS = (('tpe_batch', N.Batch), ('tpe_label_in', N.LabelIn), ('tpe_pack_info', N.PackInfo),
                   ('tpe_level_ws', N.LevelWS), ('tpe_level_need', N.LevelNeed), ('tpe_mt_state', N.MTState),
-                  ('tpe_stage_prof', N.StageProf), ('tpe_tree_label', N.TreeLabel))
+                  ('tpe_stage_prof', N.StageProf), ('tpe_tree_label', N.TreeLabel), ('tpe_exchange', N.Exchange))
 
 
 def test_ctypes_mirrors_match_c():
@@ -163,7 +163,7 @@ def test_tree_labels_dtype_matches_ctypes():
         assert N.TREE_LABEL_DTYPE.fields[f][1] == getattr(N.TreeLabel, f).offset, f
 
 
-def _tree_call(table, hist, C, min_draws=64.0, flags=0):
+def _tree_call(table, hist, C, min_draws=64.0, flags=0, shard=None, ex=None, fit_min=16384):
     from hyperopt_amd import history as H, tpe
     arr, keep = tpe._tree_labels(table, hist)
     below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
@@ -173,9 +173,15 @@ def _tree_call(table, hist, C, min_draws=64.0, flags=0):
     path = (ctypes.c_int32 * 2)()
     need_fit = np.zeros(len(arr), dtype=np.int8)
     ids = np.array([len(hist)], dtype=np.int64)
+    c_loc, base, c_glob = C, 0, 0
+    if shard is not None:
+        from hyperopt_amd.dist import shard_range
+        base, hi = shard_range(C, *shard)
+        c_loc, c_glob = hi - base, C
     rc = N.load().tpe_suggest_tree(arr.ctypes.data, len(arr), below.ctypes.data, len(below), 1.0, 25, ids.ctypes.data,
-                                   1, C, 5, min_draws, 16384, flags, ctypes.byref(ws), ctypes.byref(need), None,
-                                   vals.ctypes.data, act.ctypes.data, path, need_fit.ctypes.data)
+                                   1, c_loc, base, c_glob, ex, 5, min_draws, fit_min, flags, ctypes.byref(ws),
+                                   ctypes.byref(need), None, vals.ctypes.data, act.ctypes.data, path,
+                                   need_fit.ctypes.data)
     return rc, need, path, need_fit
 
 
@@ -235,3 +241,86 @@ def test_suggest_tree_hands_quantized_labels_back():
     finally:
         tpe._tree_labels = orig
     assert rc == N.E_SPACE and not need_fit.any() and need.result == 2
+
+
+def test_suggest_tree_refuses_device_fit_sizes_up_front():
+    """A continuous label large enough for the device Parzen fit sends the
+    space to the general path before any fit or level run (no level issued,
+    no label flagged for the caller)."""
+    import bench
+    from hyperopt_amd import history as H
+    domain, trials = bench.make_history(3000, 0)
+    hist = H.extract(domain, trials)
+    n_max = max(len(hist.obs[r.label][0]) for r in domain.table.rows
+                if r.dist in ('uniform', 'loguniform', 'normal', 'lognormal'))
+    rc, need, path, need_fit = _tree_call(domain.table, hist, 1 << 16, fit_min=n_max)
+    assert rc == N.E_FALLBACK and path[1] == 0 and not need_fit.any()
+
+
+def test_combine_results_native_matches_numpy():
+    """tpe_combine_results (the native exchange's reduction) == dist.combine_results
+    (np.argmax over (score, global index), empty records skipped)."""
+    from hyperopt_amd.dist import combine_results
+    lib = N.load()
+    rs = np.random.RandomState(4)
+    for trial in range(300):
+        world, P = rs.randint(1, 6), rs.randint(1, 7)
+        st = np.zeros((world, P), dtype=N.RESULT_DTYPE)
+        st['score'] = rs.choice([0.0, 1.0, 2.0, np.nan, -np.inf, np.inf], size=(world, P))
+        st['global_idx'] = rs.permutation(world * P * 3)[:world * P].reshape(world, P)
+        st['idx'] = np.where(rs.uniform(size=(world, P)) < 0.15, -1, st['global_idx'])
+        st['value'] = rs.uniform(size=(world, P))
+        out = np.empty(P, dtype=N.RESULT_DTYPE)
+        assert lib.tpe_combine_results(st.ctypes.data, world, P, out.ctypes.data) == 0
+        ref = combine_results(st)
+        np.testing.assert_array_equal(out['global_idx'], ref['global_idx'])
+        np.testing.assert_array_equal(out['value'], ref['value'])
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import bench
+        from hyperopt_amd import dist as D, history as H
+
+        class _Eng(object):                 # what _Exchange needs of an Engine (host gather: no device)
+            lib = N.load()
+            _dev_index = 0
+        ex = D._Exchange(_Eng(), None)
+        domain, trials = bench.make_history(600, 0)
+        hist = H.extract(domain, trials)
+        # empty workspaces: every rank's first level run needs more room; the
+        # ranks still exchange (statuses, empty records) and all return E_SPACE
+        rc, need, path, _ = _tree_call(domain.table, hist, 1 << 16, shard=(rank, world), ex=ex.ptr(32))
+        q.put((rank, rc, int(path[1]), int(need.cand), None))
+    except Exception as e:
+        q.put((rank, None, None, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_tree_exchanges_status_without_gpu():
+    """Two gloo ranks run tpe_suggest_tree sharded (each half of the 2^16
+    candidates): the native call issues the exchange through the host gather
+    callback after its first level run and both ranks return TPE_E_SPACE in
+    lock-step, each sized for its own half."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, rc, levels, cand, err in got:
+        assert err is None, err
+        assert rc == N.E_SPACE and levels == 1 and cand == 4 * (1 << 15), (rank, rc, levels, cand)

@@ -281,3 +281,90 @@ def test_config5_device_fit_full_size():
 
 
 O_A_SCALE = float(np.sqrt(0.5 / np.log(2.0)))      # sqrt(log2(e) / 2): a_k = A / max(sigma_k, EPS)
+
+
+def test_device_value_order_incremental():
+    """The resident device value order of device-fitted labels (tpe_fit_above:
+    chunk sort -> merge passes -> merge into the resident order) over 5
+    suggests that each append 200 observations (1,000 in all): after every
+    suggest each label's order is np.argsort(kind='stable') of its kernel
+    coordinate (ties by tid order; repeated values included), the suggestion
+    equals a from-scratch fit's bit for bit, and at the end the device rows
+    match the oracle's adaptive_parzen_normal."""
+    from hyperopt_amd import base, devhist, hp, history as H, tpe
+    from hyperopt_amd.engine import LevelProblem, get_engine
+    eng = get_engine()
+    N0, step, n_steps, C, seed = 20000, 200, 5, 4096, 17
+    Nt = N0 + step * n_steps
+    assert N0 - 25 >= eng.device_fit_min
+    table = base.Domain(lambda d: 0.0, {'u': hp.uniform('u', -5, 5), 'l': hp.loguniform('l', -3, 2)}).table
+    rs = np.random.RandomState(3)
+    u = rs.uniform(-5, 5, Nt)
+    u[::7] = np.round(u[::7], 1)                     # repeated values: ties broken by tid order
+    lv = np.exp(rs.uniform(-3, 2, Nt))
+    lv[::13] = np.round(lv[::13], 2)
+    tids = np.arange(Nt, dtype=np.int64)
+    losses = rs.uniform(size=Nt) + 1e-9 * tids
+    dev = {}                                         # the Trials cache's device state, kept across suggests
+    vals = {'u': u, 'l': lv}
+
+    def hist_of(n, d):
+        return H.History(tids[:n], losses[:n].copy(), {k: (tids[:n], v[:n]) for k, v in vals.items()}, dev=d)
+    for s in range(n_steps + 1):
+        n = N0 + s * step
+        hist = hist_of(n, dev)
+        got = tpe.suggest_choices(table, hist, [n], seed + s, n_EI_candidates=C)[0]
+        dc = devhist.columns(hist, eng.device)
+        for label, v in vals.items():
+            t = np.log(v[:n]) if label == 'l' else v[:n]
+            keys, idx = dc.order(label).host()
+            want = np.argsort(t, kind='stable')
+            np.testing.assert_array_equal(idx, want, err_msg='%s step %d' % (label, s))
+            np.testing.assert_array_equal(keys, t[want], err_msg='%s step %d' % (label, s))
+        fresh = tpe.suggest_choices(table, hist_of(n, {}), [n], seed + s, n_EI_candidates=C)[0]
+        assert got == fresh, (s, got, fresh)
+    # the device rows of the final history against the oracle
+    hist = hist_of(Nt, dev)
+    fits = tpe._Fits(table, hist, H.split_below(hist, 0.25), 1.0, eng)
+    rows = [table.by_label[k] for k in ('l', 'u')]
+    posts = [fits.get(r) for r in rows]
+    assert all(p.above_dev is not None and p.above_dev[3].n == Nt for p in posts)
+    eng.run([LevelProblem(p, r.index, [Nt]) for p, r in zip(posts, rows)], C, seed)
+    prob, comp32 = eng.device_tables()
+    for j, r in enumerate(rows):
+        w_o, mu_o, sg_o = _oracle_fits(r, hist)[1].params
+        p = prob[j]
+        K = int(p['above_len'])
+        assert K == len(mu_o), (r.label, K, len(mu_o))
+        rw = comp32[int(p['above_off']):int(p['above_off']) + K].astype(np.float64)
+        np.testing.assert_allclose(rw[:, 0] + rw[:, 1], mu_o, rtol=1e-12, atol=1e-12, err_msg=r.label)
+        np.testing.assert_allclose(O_A_SCALE / rw[:, 2], np.maximum(sg_o, O.EPS), rtol=2e-7, err_msg=r.label)
+
+
+# ----------------------------------------------------------------- config 2
+@pytest.mark.parametrize('seed', [2024, 77])
+def test_config2_suggest_full_size(seed):
+    """Config 2: tpe.suggest on the 10-dim mixed space (3 uniform, 3
+    loguniform, 2 quniform, 2 choice) with the bench's 1000-trial history and
+    C = 10,000 (the native tree path with caller-made fits of the quantized
+    labels): every one of the 10 winners against the oracle — lpdf within
+    1e-5 (continuous, fp32) / 1e-9 (quantized, f64), the winner in the eps-tie
+    set, categorical choices exact."""
+    import bench
+    from hyperopt_amd import history as H, hp, tpe
+    from hyperopt_amd.engine import get_engine
+    domain, trials = bench.mixed10_history(1000, bench.SEED)
+    C, new_id = 10000, 1000
+    eng = get_engine()
+    eng.last_tree_path = None
+    doc = tpe.suggest([new_id], domain, trials, seed, n_EI_candidates=C)[0]
+    trials.assert_valid_trial(doc)
+    assert eng.last_tree_path is not None                    # the production (native tree) path ran
+    vals = {k: v[0] for k, v in doc['misc']['vals'].items() if v}
+    assert sorted(vals) == sorted(bench.mixed10_space(hp)), vals
+    hist = H.extract(domain, trials)
+    fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, eng)
+    rs = np.random.RandomState(seed)
+    for label, v in sorted(vals.items()):
+        _check_problem(eng, fits, domain.table.by_label[label], hist, [new_id], C, seed, [v], rs,
+                       'config2 %s' % label, k_top=2048, n_rand=2048)

@@ -360,8 +360,10 @@ def _device_post(engine, dist, args, obs, bidx):
     """Posterior whose above mixture is fitted on the device (tpe_fit_above)."""
     from hyperopt_amd import devhist, history, parzen
     hist = history.History(np.arange(len(obs)), np.zeros(len(obs)), {'x': (np.arange(len(obs)), obs)})
-    col = devhist.columns(hist, engine.device).column('x', obs)
-    return parzen.fit_posterior(dist, args, obs[bidx], None, 1.0, above_dev=(col, len(obs), bidx)), col
+    dc = devhist.columns(hist, engine.device)
+    col = dc.column('x', np.log(obs) if dist in ('loguniform', 'lognormal') else obs)   # kernel coordinate
+    return parzen.fit_posterior(dist, args, obs[bidx], None, 1.0,
+                                above_dev=(col, len(obs), bidx, dc.order('x'))), col
 
 
 @pytest.mark.parametrize('dist,args', [('uniform', dict(low=-5.0, high=5.0)),

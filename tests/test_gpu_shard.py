@@ -30,13 +30,17 @@ def _worker(rank, world, port, q):
     try:
         import bench
         from hyperopt_amd import tpe
+        from hyperopt_amd.engine import get_engine
         domain, trials = bench.make_history(N_HIST, 0)
-        out = []
+        out, paths = [], []
         for precision, C, seed in CASES:
+            eng = get_engine(precision=precision)
+            eng.last_tree_path = None
             docs = tpe.suggest([N_HIST], domain, trials, seed, n_EI_candidates=C, precision=precision,
                                shard=(rank, world))
             out.append({k: float(v) for k, v in doc_values(docs).items()})
-        q.put((rank, out, None))
+            paths.append(eng.last_tree_path)
+        q.put((rank, (out, paths), None))
     except Exception as e:          # report, do not hang the parent
         q.put((rank, None, repr(e)))
     finally:
@@ -74,7 +78,11 @@ def test_two_process_shard_matches_unsharded():
     for _ in procs:
         rank, out, err = q.get(timeout=240)
         assert err is None, (rank, err)
-        got[rank] = out
+        got[rank], paths = out
+        # fp32: the native tree path, its level results exchanged inside the native
+        # call (gloo: the host gather); fp64 takes the general path
+        for (precision, C, seed), path in zip(CASES, paths):
+            assert (path is not None) == (precision == 'fp32'), (rank, precision, path)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -95,3 +103,49 @@ def test_two_process_shard_matches_unsharded():
             post = fits.get(row)
             s_ref, s_got = _score(post, v), _score(post, sharded[k])
             assert abs(s_ref - s_got) <= 1e-5 * max(1.0, abs(s_ref)), (precision, C, seed, k, v, sharded[k])
+
+
+def _rccl_worker(port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1)
+    try:
+        import bench
+        from hyperopt_amd import dist as D, tpe
+        from hyperopt_amd.engine import get_engine
+        domain, trials = bench.make_history(N_HIST, 0)
+        ref = [doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=1 << 18)) for s in (21, 22)]
+        D.EXCHANGE_ALWAYS = True
+        eng = get_engine()
+        got = []
+        for s in (21, 22):
+            eng.last_tree_path = None
+            got.append(doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=1 << 18, shard=(0, 1))))
+            assert eng.last_tree_path is not None
+        ex = D.exchange_for(eng)
+        q.put(([{k: float(v) for k, v in r.items()} for r in ref], [{k: float(v) for k, v in g.items()} for g in got],
+               ex.comm is not None, None))
+        ex.close()
+    except Exception as e:
+        q.put((None, None, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_one_rank():
+    """The RCCL exchange path of the native tree (tpe_comm_init from C, an
+    in-place ncclAllGather of the level results on the suggest's stream, the
+    host reduction) on a one-rank nccl group — the one GPU of the box — with
+    the exchange forced on: the suggestions equal the unsharded ones."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    ref, got, rccl, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    assert rccl, 'the exchange did not take the RCCL path'
+    assert ref == got

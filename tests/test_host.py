@@ -77,6 +77,72 @@ def test_history_cache_tracks_loss_updates():
     assert list(h.losses) == [0.0, 1.0, 2.0]
 
 
+def _same_as_walk(d, t):
+    h = history.extract(d, t)
+    gen = history._generic(d, t.trials, d.table)
+    assert list(h.tids) == list(gen.tids) and list(h.losses) == list(gen.losses)
+    for k in d.table.labels:
+        assert list(h.obs[k][0]) == list(gen.obs[k][0]), k
+        assert list(map(float, h.obs[k][1])) == list(map(float, gen.obs[k][1])), k
+    return h
+
+
+def _done_trials(d, n, seed=3):
+    t = base.Trials()
+    rs = np.random.RandomState(seed)
+    for tid in range(n):
+        doc = rand.suggest([tid], d, t, rs.randint(2 ** 31 - 1))[0]
+        doc['state'] = base.JOB_STATE_DONE
+        doc['result'] = {'status': 'ok', 'loss': float(rs.uniform())}
+        t.insert_trial_docs([doc])
+    t.refresh()
+    return t
+
+
+def test_history_cache_rebuilds_on_view_changes():
+    """Changes to a Trials view that are not appends rebuild the SoA cache:
+    a middle document replaced by one with other values, a middle document
+    dropped (ERROR) at refresh, a pending document's values edited in place
+    — each gives the reference walk's history (tpe.py:820-842)."""
+    import copy
+    d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1), 'c': H.hp.choice('c', [0, 1, 2])})
+    t = _done_trials(d, 200)
+    h0 = _same_as_walk(d, t)
+    # replaced in the middle (off the sampled positions), then refreshed
+    i = 37
+    new = copy.deepcopy(t._dynamic_trials[i])
+    new['misc']['vals']['x'] = [0.123456]
+    t._dynamic_trials[i] = new
+    t.refresh()
+    h1 = _same_as_walk(d, t)
+    assert h1 is not h0 and 0.123456 in list(h1.obs['x'][1])
+    # dropped in the middle: its state turns ERROR, refresh removes it from the view
+    t._dynamic_trials[101]['state'] = base.JOB_STATE_ERROR
+    t.refresh()
+    h2 = _same_as_walk(d, t)
+    assert len(h2) == 199 and 101 not in list(h2.tids)
+    # a pending document's values edited in place (the running trial's doc)
+    doc = rand.suggest([500], d, t, 5)[0]
+    t.insert_trial_docs([doc])
+    t.refresh()
+    _same_as_walk(d, t)
+    t.trials[-1]['misc']['vals']['x'] = [0.654321]
+    h3 = _same_as_walk(d, t)
+    assert 0.654321 in list(h3.obs['x'][1])
+    # plain appends keep the cache (no rebuild: the same value columns, extended)
+    t.trials[-1]['state'] = base.JOB_STATE_DONE
+    t.trials[-1]['result'] = {'status': 'ok', 'loss': 0.5}
+    h4 = _same_as_walk(d, t)
+    more = rand.suggest([501], d, t, 6)[0]
+    more['state'] = base.JOB_STATE_DONE
+    more['result'] = {'status': 'ok', 'loss': 0.25}
+    t.insert_trial_docs([more])
+    t.refresh()
+    cache = history._CACHES[t]
+    h5 = _same_as_walk(d, t)
+    assert history._CACHES[t] is cache and len(h5) == len(h4) + 1
+
+
 def test_fit_posterior_exact(golden):
     for case in golden('kernel_vectors.json'):
         post = parzen.fit_posterior(case['dist'], case['args'], np.asarray(case['below']),
@@ -131,3 +197,26 @@ def test_space_evaluate_and_duplicate_label():
         base.Domain(lambda x: 0, [H.hp.uniform('x', 0, 1), H.hp.uniform('x', 0, 2)])
     with pytest.raises(TypeError):
         H.hp.uniform(3, 0, 1)
+
+
+def test_tree_memo_follows_the_table_object():
+    """The native tree records are memoised per (table object, document
+    count): a second Domain with the same labels and other bounds on the same
+    Trials gets its own records (its bounds and priors), never the first's."""
+    from hyperopt_amd import base, hp, history as H, rand, tpe
+    d1 = base.Domain(lambda d: 0.0, {'x': hp.uniform('x', -5, 5), 'c': hp.choice('c', [0, 1])})
+    trials = base.Trials()
+    rs = np.random.RandomState(0)
+    for tid in range(30):
+        doc = rand.suggest([tid], d1, trials, rs.randint(2 ** 31 - 1))[0]
+        doc['state'] = base.JOB_STATE_DONE
+        doc['result'] = {'status': 'ok', 'loss': float(tid)}
+        trials.insert_trial_docs([doc])
+    trials.refresh()
+    a1 = tpe._tree_labels(d1.table, H.extract(d1, trials))[0]
+    assert tpe._tree_labels(d1.table, H.extract(d1, trials))[0] is a1          # memo hit
+    d2 = base.Domain(lambda d: 0.0, {'x': hp.uniform('x', -1, 2), 'c': hp.choice('c', [0, 1])})
+    a2 = tpe._tree_labels(d2.table, H.extract(d2, trials))[0]
+    ix = d2.table.by_label['x'].index
+    assert (a2[ix]['low'], a2[ix]['high'], a2[ix]['prior_mu']) == (-1.0, 2.0, 0.5)
+    assert (a1[ix]['low'], a1[ix]['high']) == (-5.0, 5.0)

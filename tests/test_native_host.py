@@ -176,6 +176,17 @@ class _FakeColumn(object):
         return 0xD0000000
 
 
+class _FakeOrder(object):
+    """Stand-in for a devhist.ValueOrder with ``n`` observations already sorted."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def ptrs(self, n_obs):
+        return (0xE0000000 if self.n else 0, 0xE1000000 if self.n else 0, self.n,
+                0xE2000000 if self.n < n_obs else 0, 0xE3000000 if self.n < n_obs else 0)
+
+
 def test_pack_reserves_device_fit_rows():
     """A device-fitted above mixture (tpe_fit_job) gets its comp32 rows, wide
     rows and grid at the END of those sections, outside the host copy ranges."""
@@ -183,20 +194,24 @@ def test_pack_reserves_device_fit_rows():
     n_obs, bidx = 500, np.array([3, 10, 77], dtype=np.int32)
     host = parzen.fit_posterior('normal', dict(mu=0.0, sigma=2.0), rs.normal(0, 2, 9), rs.normal(0, 2, 300), 1.0)
     dev = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 3), None, 1.0,
-                               above_dev=(_FakeColumn(), n_obs, bidx))
+                               above_dev=(_FakeColumn(), n_obs, bidx, _FakeOrder(0)))
     assert dev.above is None and dev.prior == (0.5, 3.0, 1.0, 25)
     lps = [LevelProblem(host, 1, [5, 6]), LevelProblem(dev, 2, [5, 6, 7])]
     e = _engine('fp32')
     info = e._pack(lps, 4096, 1, 0, None)
     K = n_obs - len(bidx) + 1
-    assert info.n_fit == 1 and info.fit_total == K - 1 and info.sort_end_bit > 0
+    # a fresh order: every observation is new, the scratch segment holds them all
+    assert info.n_fit == 1 and info.fit_total == n_obs and info.sort_end_bit > 0
+    assert info.fit_max_new == n_obs and info.fit_max_obs == n_obs
     j = _blob(e, info, info.off_fit, N.FIT_JOB_DTYPE, 1)[0]
     assert j['obs'] == 0xD0000000 and j['n_obs'] == n_obs and j['seg_off'] == 0 and j['n_below'] == 3
+    assert (j['ord_key_in'], j['ord_idx_in'], j['n_ord_in']) == (0, 0, 0)
+    assert (j['ord_key_out'], j['ord_idx_out']) == (0xE2000000, 0xE3000000)
     assert j['problem_first'] == 2 and j['n_problems'] == 3 and j['family'] == N.FAM_GAUSS
     assert (j['prior_mu'], j['prior_sigma'], j['prior_weight'], j['lf']) == (0.5, 3.0, 1.0, 25)
     assert (j['low'], j['high']) == (-1.0, 2.0)
     np.testing.assert_array_equal(_blob(e, info, info.off_below_idx, np.int32, 3), bidx)
-    np.testing.assert_array_equal(_blob(e, info, info.off_fit_seg, np.int64, 2), [0, K - 1])
+    np.testing.assert_array_equal(_blob(e, info, info.off_fit_seg, np.int64, 2), [0, n_obs])
     prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, 5)
     host_rows = info.copy2_len // 16
     for p in prob[2:]:
@@ -211,6 +226,34 @@ def test_pack_reserves_device_fit_rows():
     assert info.blob_bytes == info.off_comp32 + 16 * (host_rows + K + 16)
     with pytest.raises(RuntimeError):
         _engine('fp64')._pack(lps, 4096, 1, 0, None)
+
+
+def test_pack_device_fit_resident_order():
+    """A label whose value order already holds some observations merges only
+    the rest: its scratch segment is sized by the compacted above order, and a
+    fully sorted order passes no output buffers."""
+    rs = np.random.RandomState(6)
+    n_obs, bidx = 600, np.array([1, 50], dtype=np.int32)
+    K = n_obs - len(bidx) + 1
+    for n_sorted, out in ((n_obs - 7, True), (n_obs, False)):
+        dev = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 2), None, 1.0,
+                                   above_dev=(_FakeColumn(), n_obs, bidx, _FakeOrder(n_sorted)))
+        e = _engine('fp32')
+        info = e._pack([LevelProblem(dev, 0, [9])], 4096, 1, 0, None)
+        assert info.fit_total == K - 1 and info.fit_max_new == n_obs - n_sorted and info.fit_max_obs == n_obs
+        j = _blob(e, info, info.off_fit, N.FIT_JOB_DTYPE, 1)[0]
+        assert (j['ord_key_in'], j['ord_idx_in'], j['n_ord_in']) == (0xE0000000, 0xE1000000, n_sorted)
+        assert (j['ord_key_out'] != 0) == out and (j['ord_idx_out'] != 0) == out
+    # an order whose output buffers are missing is refused
+    bad = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 2), None, 1.0,
+                               above_dev=(_FakeColumn(), n_obs, bidx, _NoOut(n_obs - 1)))
+    with pytest.raises(RuntimeError):
+        _engine('fp32')._pack([LevelProblem(bad, 0, [9])], 4096, 1, 0, None)
+
+
+class _NoOut(_FakeOrder):
+    def ptrs(self, n_obs):
+        return (0xE0000000, 0xE1000000, self.n, 0, 0)
 
 
 def test_cat_split_matches_fit_posterior():
