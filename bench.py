@@ -12,10 +12,15 @@ C = N * 2^20, per-level winner combined by one all-gather (dist.py).
 value  = sum over steps of (active hyperparameters x total candidates) / time
 roofline: the dominant stage by device time (k_sample_tab on config 3),
           timed per launch with HIP events the level runner records on its own
-          stream (tpe_level_profile), priced by executed VALU instructions
-          (SQ_INSTS_VALU of a separate PMC pass) against the issue peak.
+          stream (tpe_level_profile), priced by the ALGORITHMIC VALU work of its
+          candidates (TAB_CAND_OPS per candidate) against the issue peak; the
+          executed-instruction fraction (SQ_INSTS_VALU of a separate PMC pass of
+          the same build, pmc_stale flags a mismatch) beside it.
 cpu_baseline: the CPU oracle (numpy restatement of the reference) on a bounded
-          sample of the same workload, 1 core and candidate-chunked over all cores.
+          sample of the same workload, candidate-chunked over a measured process
+          sweep (the best pool is the figure; 1 core beside it).
+p50_suggest_ms_appending: the same suggest in an FMinIter loop (one finished
+          document inserted before every suggest, fmin.py:88-92).
 """
 import argparse
 import json
@@ -110,14 +115,16 @@ def host_cpu():
     return dict(model=model, logical_cpus=os.cpu_count(), usable_cpus=aff)
 
 
-def cpu_baseline(domain, trials, budget_s=12.0, max_procs=16):
+def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64), sweep_s=6.0):
     """The oracle (numpy restatement of the reference, tools/oracle_vs_reference.py
     times it against the reference itself) on a bounded sample of the same
-    workload: whole suggests at C = 16384 on the same 10k-trial history, for
-    ~budget_s each (1) on one core and (2) candidate-chunked over a process pool
-    of min(max_procs, usable cores) — chunking is exact, logsum_rows is
-    row-wise (tpe.py:253-256); sampling stays serial, as in the reference.
-    Called before the GPU is initialised (the pool forks)."""
+    workload: whole suggests at C = 16384 on the same 10k-trial history,
+    (1) on one core for ~budget_s and (2) candidate-chunked over process pools
+    of each size in ``sweep`` (capped at the usable cores) for ~sweep_s each —
+    chunking is exact, logsum_rows is row-wise (tpe.py:253-256); sampling stays
+    serial, as in the reference.  The reported figure is the best pool of the
+    sweep (the knee: more processes than the host's CPU share buy nothing).
+    Called before the GPU is initialised (the pools fork)."""
     import multiprocessing as mp
     from oracle import tpe_oracle as O
     try:
@@ -132,27 +139,33 @@ def cpu_baseline(domain, trials, budget_s=12.0, max_procs=16):
     hist = [dict(tid=d['tid'], loss=d['result']['loss'], vals=d['misc']['vals']) for d in trials.trials]
     C = 16384
 
-    def run(pool, chunks):
+    def run(pool, chunks, secs):
         n_scores, calls, t0 = 0, 0, time.time()
-        while time.time() - t0 < budget_s:
+        while time.time() - t0 < secs:
             out = O.tpe_suggest(params, hist, 1000 + calls, n_EI_candidates=C, pool=pool, chunks=chunks)
             n_scores += len(out) * C
             calls += 1
         dt = time.time() - t0
         return n_scores / dt, calls, dt
 
-    v1, c1, d1 = run(None, 1)
+    v1, c1, d1 = run(None, 1, budget_s)
     cpu = host_cpu()
-    P = max(1, min(max_procs, cpu['usable_cpus']))
-    with mp.get_context('fork').Pool(P) as pool:
-        vp, cp, dp = run(pool, P)
+    pts = []
+    for P in sorted(set(max(1, min(p, cpu['usable_cpus'])) for p in sweep)):
+        with mp.get_context('fork').Pool(P) as pool:
+            run(pool, P, 0.5)                       # pool warm-up (imports, first tasks)
+            vp, cp, dp = run(pool, P, sweep_s)
+        pts.append(dict(processes=P, value=vp, calls=cp, secs=dp))
     if limiter is not None:
         limiter.unregister()
-    return dict(value=v1, unit='candidate-scores/s', cores=1, kind='port',
-                sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, %.1fs, 1 core' % (c1, d1),
-                all_core=dict(value=vp, cores=P, speedup=vp / v1,
-                              sample='%d oracle tpe_suggest calls, C=16384, candidate scoring chunked over %d '
-                                     'processes, %.1fs' % (cp, P, dp)),
+    best = max(pts, key=lambda p: p['value'])
+    return dict(value=best['value'], unit='candidate-scores/s', cores=best['processes'], kind='port',
+                sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, candidate scoring chunked '
+                       'over %d processes, %.1fs (best of the process sweep)'
+                       % (best['calls'], best['processes'], best['secs']),
+                sweep=[dict(processes=p['processes'], value=p['value']) for p in pts],
+                single_core=dict(value=v1, cores=1,
+                                 sample='%d oracle tpe_suggest calls, C=16384, %.1fs, 1 core' % (c1, d1)),
                 host=cpu)
 
 
@@ -163,8 +176,36 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 # x 4 SIMDs x 256 CUs x 2.4 GHz
 PEAK_VALU_GINST = 0.5 * 4 * 256 * 2.4      # = 1228.8 G wave-instructions/s
 # counter summary of the same bench command (tools/gpu.sh pmc -> tools/pmc_summary.py)
-PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r02_pmc_summary.json')
+PMC_SUMMARY_REL = 'profiles/r03_pmc_summary.json'
+PMC_SUMMARY = os.path.join(ROOT, PMC_SUMMARY_REL)
 VALU_KERNELS = ('k_sample', 'k_tables', 'k_select', 'above', 'k_finalize')
+
+
+LIB_PATH = os.path.join(ROOT, 'hyperopt_amd', 'libtpe_hip.so')
+
+# Algorithmic work of one tabulated candidate (k_sample_tab), in VALU lane
+# operations — the operations the method needs, whatever the code executes
+# ("Roofline"); a wave-instruction does 64 of them.
+TAB_CAND_OPS = {
+    'philox': 40,        # half a Philox-4x32-10 block: 10 rounds x (2 mad_u64 + 4 xor + 2 key adds) / 2
+    'uniforms': 5,       # 32-bit selection uniform, 23-bit inversion uniform
+    'guide_scan': 6,     # guide-table bucket, one LDS read, ~1.5 compare steps of the CDF scan
+    'ndtri_f32': 19,     # p from the truncation bounds, log(4p(1-p)), degree-8 polynomial, sign
+    'affine': 1,         # t = mu + sigma * z
+    'cells': 26,         # per side: cell index, bounds test, centre, u = (t - c) / h, row address
+    'horner': 20,        # per side: degree-10 Horner sum of the moments
+    'log2': 4,           # per side: log2 of the sum + shift m
+    'compare': 6,        # l2 - g2, flag tests, running best (value, index)
+}
+TAB_CAND_OPS_TOTAL = sum(TAB_CAND_OPS.values())
+
+
+def lib_hash(path=LIB_PATH):
+    import hashlib
+    if not os.path.exists(path):
+        return None
+    with open(path, 'rb') as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
 def _pmc():
@@ -213,14 +254,28 @@ def roofline(prof):
             k.update(bound='hbm', achieved=ach, peak=PEAK_HBM_GBS, unit='GB/s', frac=ach / PEAK_HBM_GBS,
                      bytes_per_launch=float(nbytes.mean()),
                      note='rocPRIM onesweep radix sort of (u32 bucket key, u64 position|t) pairs')
+        elif name == 'k_sample' and len(recs[0]) > 2 and recs[0][2] > 0:
+            # tabulated scoring: the algorithmic VALU work of the candidates
+            # (TAB_CAND_OPS per candidate) / the launch time / the issue peak
+            cands = float(np.mean([r[1] for r in recs]))
+            alg = cands * TAB_CAND_OPS_TOTAL / 64.0
+            ach = alg / (ms.mean() * 1e-3) / 1e9
+            k.update(bound='valu', achieved=ach, peak=PEAK_VALU_GINST, unit='G VALU wave-instructions/s',
+                     frac=ach / PEAK_VALU_GINST, work='algorithmic',
+                     algorithmic_valu_per_launch=alg, candidates_per_launch=cands,
+                     ops_per_candidate=TAB_CAND_OPS_TOTAL, ops_model=TAB_CAND_OPS)
+            if 'SQ_INSTS_VALU' in c:
+                inst = float(c['SQ_INSTS_VALU'])
+                exe = inst / (ms.mean() * 1e-3) / 1e9
+                k.update(executed_valu_per_launch=inst, executed_achieved=exe,
+                         frac_executed=exe / PEAK_VALU_GINST, executed_per_algorithmic=inst / alg,
+                         executed_source=PMC_SUMMARY_REL + ' (SQ_INSTS_VALU per dispatch)')
         elif name in VALU_KERNELS and 'SQ_INSTS_VALU' in c:
             inst = float(c['SQ_INSTS_VALU'])
             ach = inst / (ms.mean() * 1e-3) / 1e9
             k.update(bound='valu', achieved=ach, peak=PEAK_VALU_GINST, unit='G VALU wave-instructions/s',
-                     frac=ach / PEAK_VALU_GINST, executed_valu_per_launch=inst,
-                     executed_source='profiles/r02_pmc_summary.json (SQ_INSTS_VALU per dispatch)')
-            if 'SQ_INSTS_VALU_TRANS_F32' in c:
-                k['trans_f32_per_launch'] = float(c['SQ_INSTS_VALU_TRANS_F32'])
+                     frac=ach / PEAK_VALU_GINST, work='executed', executed_valu_per_launch=inst,
+                     executed_source=PMC_SUMMARY_REL + ' (SQ_INSTS_VALU per dispatch)')
         else:
             k.update(bound=None)
         if name == 'k_sample' and len(recs[0]) > 2:
@@ -238,8 +293,11 @@ def roofline(prof):
     r['stage_kernels'] = [k for k in STAGE_KERNELS.get(dom, (dom,)) if k in _pmc()] or [dom]
     r.setdefault('traffic', None)
     if r['traffic'] is not None:
-        r['traffic_source'] = 'profiles/r02_pmc_summary.json: (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 ' \
+        r['traffic_source'] = PMC_SUMMARY_REL + ': (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 ' \
                               'FETCH_SIZE correction, MI355X_MICROARCH.md)'
+    # the counters belong to the library that runs (its hash is in the summary)
+    built = pmc.get('lib_sha256')
+    r['pmc_stale'] = bool(pmc) and (built is None or built != lib_hash())
     return r, kernels
 
 
@@ -346,6 +404,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-quantized', action='store_true', help='skip the rf-branch (quantized) report')
+    ap.add_argument('--no-appending', action='store_true', help='skip the FMinIter-style appending loop')
     ap.add_argument('--history', type=int, default=N_HISTORY)
     ap.add_argument('--cands', type=int, default=C_PER_GPU)
     ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
@@ -470,6 +529,34 @@ def main():
                      p50_suggest_ms=1e3 * float(np.median(ql)), active_labels=sorted(vals),
                      model=int(vals.get('model', -1)))
 
+    # the suggest as FMinIter.run issues it (fmin.py:88-92): every suggest follows
+    # the insertion of the previous suggestion, evaluated (synthetic loss) — the
+    # history grows by one document per step, so each suggest extends the SoA
+    # cache, its value orders and the tree records instead of reusing them
+    appending = None
+    if not args.no_appending:
+        from hyperopt_amd import base as base_mod
+        n_app = max(10, min(args.steps, 50))
+        lat_a, tid = [], new_id
+        for i in range(n_app + 2):
+            s0 = time.perf_counter()
+            docs = tpe.suggest([tid], domain, trials, SEED + 20000 + i, n_EI_candidates=C_total, shard=shard)
+            dt = time.perf_counter() - s0
+            if i >= 2:                      # (the first two: warm-up)
+                lat_a.append(dt)
+            trials.insert_trial_docs(docs)
+            trials.refresh()
+            d = trials.trials[-1]
+            v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
+            d['state'] = base_mod.JOB_STATE_DONE
+            d['result'] = {'status': 'ok', 'loss': synthetic_loss(v, tid)}
+            tid += 1
+        appending = dict(p50_suggest_ms=1e3 * float(np.median(lat_a)),
+                         p99_suggest_ms=1e3 * float(np.percentile(lat_a, 99)), suggests=n_app,
+                         history_from=new_id, history_to=tid,
+                         note='one evaluated document inserted (and trials.refresh()) before every suggest, '
+                              'as FMinIter.run does; the suggest alone is timed')
+
     if rank == 0:
         out = {
             'metric': 'EI candidates scored/sec (node) + tpe.suggest p50 latency, 1M cands x 10k trials',
@@ -482,6 +569,8 @@ def main():
                        'history': args.history, 'n_EI_candidates': C_total,
                        'parallelism': 'candidate-shard x%d' % world},
             'p50_suggest_ms': 1e3 * float(np.median(lat)), 'p99_suggest_ms': 1e3 * float(np.percentile(lat, 99)),
+            'p50_suggest_ms_appending': appending['p50_suggest_ms'] if appending else None,
+            'appending': appending,
             'active_hyperparameters_per_suggest': n_active / args.steps,
             'stage_ms': stages, 'roofline': roof, 'kernels': kernels, 'cpu_baseline': cpu,
             'quantized_branch': quant,

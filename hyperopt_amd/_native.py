@@ -176,6 +176,7 @@ class LevelNeed(ctypes.Structure):
                                               'draw_pref', 'pool_best', 'tab')]
 
 
+E_HIP = -2
 E_SPACE = -4
 E_FALLBACK = -5          # tpe_suggest_tree: the space / history needs the general (host) path
 TREE_MAX_PARENTS = 4
@@ -196,6 +197,8 @@ class TreeLabel(ctypes.Structure):
         ('q', ctypes.c_double),
         ('host_w', ctypes.c_void_p * 2), ('host_mu', ctypes.c_void_p * 2), ('host_sigma', ctypes.c_void_p * 2),
         ('host_k', ctypes.c_int64 * 2),
+        ('dev_obs', ctypes.c_void_p), ('ord_key_in', ctypes.c_void_p), ('ord_idx_in', ctypes.c_void_p),
+        ('n_ord_in', ctypes.c_int64), ('ord_key_out', ctypes.c_void_p), ('ord_idx_out', ctypes.c_void_p),
     ]
 
 
@@ -217,7 +220,7 @@ TREE_LABEL_DTYPE = np.dtype(dict(
     names=[f for f, _ in TreeLabel._fields_],
     formats=['<i4', '<i4', '<i4', '<i4', '<f8', '<f8', '<f8', '<f8', '<u8', '<u8', '<u8', '<u8', '<i8', '<i4', '<i4',
              ('<i4', (TREE_MAX_PARENTS,)), ('<i4', (TREE_MAX_PARENTS,)), '<f8', ('<u8', (2,)), ('<u8', (2,)),
-             ('<u8', (2,)), ('<i8', (2,))],
+             ('<u8', (2,)), ('<i8', (2,)), '<u8', '<u8', '<u8', '<i8', '<u8', '<u8'],
     offsets=[getattr(TreeLabel, f).offset for f, _ in TreeLabel._fields_], itemsize=ctypes.sizeof(TreeLabel)))
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size', 'tpe_pinned_device_address',

@@ -810,9 +810,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
   __shared__ int guide[kGuide];
   __shared__ tpe_best wb[kTabThreads / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  [[maybe_unused]] const int wave = threadIdx.x >> 6;
   const bool need_x = l_out != nullptr || (flags & TPE_BATCH_WRITE_CAND);
-  int cur = -1, run_tile = -1;            // problem staged, first tile of its run
+  int cur = -1, run_tile = -1;            // problem of the run, first tile of its run
+  // what the LDS holds: the sampler and table rows of a label (every problem
+  // of a label shares them — a batched suggest's ids run through the same
+  // label back to back, and each only flushes its own winner)
+  int st_samp = -1, st_len = -1, st_t0 = -1, st_t1 = -1, st_n0 = -1, st_n1 = -1, st_mode = -1;
   bool in_lds = false, tab_in_lds = false;
   double bs = 0.0, bl = 0.0, bg = 0.0, bv = 0.0;
   int64_t bi = -1;
@@ -959,39 +964,45 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     const bool cells = p.tab_mode == TPE_TAB_CELLS;
     if (pid != cur) {
       if (cur >= 0) flush();
-      __syncthreads();                               // LDS free for the next problem
-      const double* S = samp + 8 * (int64_t)p.samp_off;
-      in_lds = draw && p.samp_len > 0 && p.samp_len <= kCumLds;
-      if (in_lds) {
-        for (int q = threadIdx.x; q < p.samp_len; q += kTabThreads) {
-          const double* s = S + 8 * q;
-          cum_lds[q] = s[0];
-          const float sg = (float)s[2];
-          row_lds[q] = make_float4((float)s[1], s[5] != 0.0 ? -sg : sg, (float)s[3], (float)s[4]);
+      const bool same = p.samp_off == st_samp && p.samp_len == st_len && p.tab_off[0] == st_t0 &&
+                        p.tab_off[1] == st_t1 && p.tab_n[0] == st_n0 && p.tab_n[1] == st_n1 && p.tab_mode == st_mode;
+      if (!same) {
+        st_samp = p.samp_off; st_len = p.samp_len; st_t0 = p.tab_off[0]; st_t1 = p.tab_off[1];
+        st_n0 = p.tab_n[0]; st_n1 = p.tab_n[1]; st_mode = p.tab_mode;
+        __syncthreads();                               // LDS free for the next label's rows
+        const double* S = samp + 8 * (int64_t)p.samp_off;
+        in_lds = draw && p.samp_len > 0 && p.samp_len <= kCumLds;
+        if (in_lds) {
+          for (int q = threadIdx.x; q < p.samp_len; q += kTabThreads) {
+            const double* s = S + 8 * q;
+            cum_lds[q] = s[0];
+            const float sg = (float)s[2];
+            row_lds[q] = make_float4((float)s[1], s[5] != 0.0 ? -sg : sg, (float)s[3], (float)s[4]);
+          }
         }
-      }
-      tab_in_lds = PREC == TPE_PREC_F32 && cells && p.tab_n[0] + p.tab_n[1] <= kTabLdsCells;
-      if (tab_in_lds) {                              // plane k of cell j at tab_lds[k * kTabLdsCells + j]
-        // workgroups start at different 16-KiB windows of the tables (every CU
-        // of the problem stages the same rows: spread the first touches)
-        const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], n1 = TPE_TAB_ROW_UNITS * p.tab_n[1];
-        const int nw = (n0 + n1 + kTabThreads - 1) / kTabThreads;
-        const int rot = (int)blockIdx.x % nw;
-        for (int u = 0; u < nw; ++u) {
-          const int q = ((u + rot) % nw) * kTabThreads + (int)threadIdx.x;
-          if (q >= n0 + n1) continue;
-          const float4 v = q < n0 ? tab[(int64_t)p.tab_off[0] + q] : tab[(int64_t)p.tab_off[1] + q - n0];
-          tab_lds[(q % TPE_TAB_ROW_UNITS) * kTabLdsCells + q / TPE_TAB_ROW_UNITS] = v;
+        tab_in_lds = PREC == TPE_PREC_F32 && cells && p.tab_n[0] + p.tab_n[1] <= kTabLdsCells;
+        if (tab_in_lds) {                              // plane k of cell j at tab_lds[k * kTabLdsCells + j]
+          // workgroups start at different 16-KiB windows of the tables (every CU
+          // of the problem stages the same rows: spread the first touches)
+          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], n1 = TPE_TAB_ROW_UNITS * p.tab_n[1];
+          const int nw = (n0 + n1 + kTabThreads - 1) / kTabThreads;
+          const int rot = (int)blockIdx.x % nw;
+          for (int u = 0; u < nw; ++u) {
+            const int q = ((u + rot) % nw) * kTabThreads + (int)threadIdx.x;
+            if (q >= n0 + n1) continue;
+            const float4 v = q < n0 ? tab[(int64_t)p.tab_off[0] + q] : tab[(int64_t)p.tab_off[1] + q - n0];
+            tab_lds[(q % TPE_TAB_ROW_UNITS) * kTabLdsCells + q / TPE_TAB_ROW_UNITS] = v;
+          }
         }
+        __syncthreads();
+        if (in_lds && threadIdx.x < kGuide) {          // first k with cum_k > b / kGuide
+          const double v = (double)threadIdx.x / (double)kGuide;
+          int a = 0, b = p.samp_len - 1;
+          while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
+          guide[threadIdx.x] = a;
+        }
+        __syncthreads();
       }
-      __syncthreads();
-      if (in_lds && threadIdx.x < kGuide) {          // first k with cum_k > b / kGuide
-        const double v = (double)threadIdx.x / (double)kGuide;
-        int a = 0, b = p.samp_len - 1;
-        while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
-        guide[threadIdx.x] = a;
-      }
-      __syncthreads();
       cur = pid;
       run_tile = tile;
       run_cand_base = p.cand_base; run_cand_off = p.cand_off;
@@ -2400,7 +2411,6 @@ __global__ __launch_bounds__(kUploadThreads) void k_upload(const unsigned long l
 // ============================================================ device Parzen fit
 // adaptive_parzen_normal (tpe.py:398-475) of the above observations of a label
 // (ap_filter_trials, tpe.py:613-641), directly into the pruned f32 layout.
-constexpr int kFitThreads = 512;
 constexpr int kPruneWide = 16;
 constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e))
 
@@ -2557,26 +2567,46 @@ __device__ __forceinline__ const uint32_t* ord_idx(const tpe_fit_job& j) {
   return j.n_ord_in < j.n_obs ? j.ord_idx_out : j.ord_idx_in;
 }
 
+// Per-job scalars of the build, at the head of the job's fit_keys segment
+// (free once the merge has run): the prior's position, the combined chunk
+// statistics, then the chunks' statistics (FitPart, 12 doubles each).
+constexpr int kFitHdrPos = 0, kFitHdrStats = 1, kFitHdrParts = 8;
+
 // position of each below observation in the job's order (binary search for its
-// own (t, i) pair) -> pos[seg_off + b]
+// own (t, i) pair) -> pos[seg_off + b]; and the prior's position among the
+// above observations (np.searchsorted(side='left') of prior_mu, tpe.py:427-431):
+// the observations < prior_mu in the whole order less the below ones
 constexpr int kFitMaxBelow = 64;
 __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* __restrict__ J,
                                                             const int32_t* __restrict__ below_idx,
-                                                            uint32_t* __restrict__ pos) {
+                                                            uint32_t* __restrict__ pos, double* __restrict__ hdr) {
   const tpe_fit_job& j = J[blockIdx.x];
   const int b = threadIdx.x;
-  if (b >= j.n_below) return;
-  const uint32_t i = (uint32_t)below_idx[j.below_off + b];
-  const double t = fit_coord(j, i);
   const double* __restrict__ ok = ord_keys(j);
   const uint32_t* __restrict__ ov = ord_idx(j);
-  int64_t lo = 0, hi = j.n_obs;
-  while (lo < hi) {
-    const int64_t md = (lo + hi) >> 1;
-    if (ord_lt(ok[md], ov[md], t, i)) lo = md + 1;
-    else hi = md;
+  bool under = false;
+  if (b < j.n_below) {
+    const uint32_t i = (uint32_t)below_idx[j.below_off + b];
+    const double t = fit_coord(j, i);
+    under = t < j.prior_mu;
+    int64_t lo = 0, hi = j.n_obs;
+    while (lo < hi) {
+      const int64_t md = (lo + hi) >> 1;
+      if (ord_lt(ok[md], ov[md], t, i)) lo = md + 1;
+      else hi = md;
+    }
+    pos[j.seg_off + b] = (uint32_t)lo;
   }
-  pos[j.seg_off + b] = (uint32_t)lo;
+  const int n_under = __popcll(__ballot(under));
+  if (b == 0) {
+    int64_t lo = 0, hi = j.n_obs;                   // observations with t < prior_mu (NaN last)
+    while (lo < hi) {
+      const int64_t md = (lo + hi) >> 1;
+      if (ok[md] < j.prior_mu) lo = md + 1;
+      else hi = md;
+    }
+    hdr[j.seg_off + kFitHdrPos] = (double)(lo - n_under);
+  }
 }
 
 // compact: the order without the below observations, each with its rank among
@@ -2617,205 +2647,303 @@ __global__ __launch_bounds__(kCompactThreads) void k_ord_compact(const tpe_fit_j
   }
 }
 
-// deterministic block reductions (fixed tree order)
-template <typename T, typename Op>
-__device__ __forceinline__ T block_reduce(T v, Op op, T* lds) {
-  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
-  const int wv = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) lds[wv] = v;
-  __syncthreads();
-  T r = lds[0];
-  for (int i = 1; i < kFitThreads / 64; ++i) r = op(r, lds[i]);
-  return r;
-}
-
-struct FitView {
-  const double* s;     // sorted above observations
-  int64_t n, pos;      // count, prior position (searchsorted left)
-  double pmu;
-  __device__ __forceinline__ double mu(int64_t i) const { return i < pos ? s[i] : (i == pos ? pmu : s[i - 1]); }
+// ---- build: adaptive_parzen_normal over the compacted above order ----
+// Three launches over (chunk of kFitChunk components) x job, so a 100k-
+// component mixture spreads over ~50 workgroups instead of one:
+//   k_fit_stats  per chunk: the normaliser W, the acceptance mass M, the
+//                shift cm = max log2(w / sigma), the wide-threshold statistics
+//   k_fit_emit   the job's chunk statistics combined (fixed chunk order, the
+//                same in every workgroup), then the chunk's {mu, a, c} rows,
+//                its wide candidates and its grid buckets
+//   k_fit_wide   the wide list (fixed index order) and the problem rows
+constexpr int kFitChunk = 2048;
+constexpr int kFitThreads = 256;
+constexpr int kFitPer = kFitChunk / kFitThreads;
+constexpr int kThr = 5;                          // wide if sigma > smin * 2^(m+1), m < kThr
+struct FitPart {                                 // one chunk's statistics (fit scratch, 8-B aligned)
+  double W, M;
+  double rmax;                                   // max w / max(sigma, EPS): cm = log2(rmax) (log2 is monotone)
+  double sm_all;
+  double sm[kThr];
+  int32_t cnt[kThr];
+  int32_t pad;
 };
 
-__device__ __forceinline__ double ncdf(double x, double mu, double sigma) {   // tpe.py:96-101
-  return 0.5 * (1.0 + erf((x - mu) / fmax(1.4142135623730951 * sigma, kEPS)));
-}
-
-__global__ __launch_bounds__(kFitThreads) void k_fit_build(const tpe_fit_job* __restrict__ J,
-                                                           const double* __restrict__ keys_sorted,
-                                                           const uint32_t* __restrict__ vals_sorted,
-                                                           tpe_problem* __restrict__ P,
-                                                           float4* __restrict__ comp,
-                                                           int32_t* __restrict__ grid) {
-  const tpe_fit_job& j = J[blockIdx.x];
-  __shared__ double red[kFitThreads / 64];
-  __shared__ int64_t wide_ix[kPruneWide];
-  __shared__ int n_wide;
-  const int64_t n = j.n_obs - j.n_below, K = n + 1;
-  FitView v;
-  v.s = keys_sorted + j.seg_off;
-  v.n = n;
-  v.pmu = j.prior_mu;
-  {  // np.searchsorted(srtd_mus, prior_mu) (side left) = number of observations < prior_mu:
-     // a block count over the sorted keys (coalesced) instead of a serial binary search
-    double c = 0;
-    for (int64_t i = threadIdx.x; i < n; i += kFitThreads) c += v.s[i] < j.prior_mu ? 1.0 : 0.0;
-    v.pos = (int64_t)block_reduce(c, [](double a, double b) { return a + b; }, red);
-  }
-  const uint32_t* __restrict__ rank = vals_sorted + j.seg_off;
-  const double smax = j.prior_sigma, smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);   // tpe.py:465-470
-  // linear forgetting (tpe.py:381-394): ramp = linspace(1/n, 1, n - lf) for the oldest, 1 after
-  const bool ramp = j.lf > 0 && j.lf < n;
-  const int64_t num = n - j.lf;
-  const double start = 1.0 / (double)n, step = num > 1 ? (1.0 - start) / (double)(num - 1) : 0.0;
-  const bool logf = j.family == TPE_FAM_LOGGAUSS;
-  const bool bounded = !logf && (j.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH));
-  auto sigma_of = [&](int64_t i) -> double {
-    if (i == v.pos) return j.prior_sigma;
+// the view of one job's sorted above observations with the prior inserted at
+// pos (np.searchsorted(side='left'), tpe.py:427-431) and its bandwidth rules
+struct FitCtx {
+  const double* s;       // sorted above observations
+  const uint32_t* rank;  // their ranks in tid order
+  int64_t n, K, pos;
+  double pmu, psig, pw, smin, smax, start, step;
+  int64_t num;
+  bool ramp, bounded;
+  double low, high;
+  __device__ __forceinline__ double mu(int64_t i) const { return i < pos ? s[i] : (i == pos ? pmu : s[i - 1]); }
+  __device__ __forceinline__ double sigma(int64_t i) const {          // tpe.py:441-470
+    if (i == pos) return psig;
     double sg;
-    if (i == 0) sg = v.mu(1) - v.mu(0);
-    else if (i == K - 1) sg = v.mu(K - 1) - v.mu(K - 2);
-    else sg = fmax(v.mu(i) - v.mu(i - 1), v.mu(i + 1) - v.mu(i));
+    if (i == 0) sg = mu(1) - mu(0);
+    else if (i == K - 1) sg = mu(K - 1) - mu(K - 2);
+    else sg = fmax(mu(i) - mu(i - 1), mu(i + 1) - mu(i));
     return fmin(fmax(sg, smin), smax);
-  };
-  auto weight_of = [&](int64_t i) -> double {
-    if (i == v.pos) return j.prior_weight;
+  }
+  __device__ __forceinline__ double weight(int64_t i) const {         // tpe.py:381-394, 454-460
+    if (i == pos) return pw;
     if (!ramp) return 1.0;
-    const int64_t r = rank[i < v.pos ? i : i - 1];
+    const int64_t r = rank[i < pos ? i : i - 1];
     if (r >= num) return 1.0;
     if (r == num - 1) return 1.0;
     if (num == 1) return start;
     return __dadd_rn(__dmul_rn((double)r, step), start);        // linspace: i * step + start
-  };
-  // pass 1: normaliser, acceptance mass, shift, wide thresholds
-  constexpr int kThr = 5;                          // wide if sigma > smin * 2^(m+1)
-  double W = 0, M = 0, cm = -INFINITY, sm_all = 0;
+  }
+};
+
+// (f64 erf out of line: inlined twice, its polynomial constants were hoisted
+// into VGPR pairs and took the stats kernel to 143 VGPRs)
+// |z| >= 6: erf(z) rounds to +-1 in f64 (1 - erf(6) = 2.2e-17 < half an ulp of 1)
+__device__ __noinline__ double erf_call(double z) { return erf(z); }
+__device__ __forceinline__ double erf_sat(double z) { return fabs(z) >= 6.0 ? copysign(1.0, z) : erf_call(z); }
+__device__ __forceinline__ double ncdf(double x, double mu, double sigma) {   // tpe.py:96-101
+  return 0.5 * (1.0 + erf_sat((x - mu) / fmax(1.4142135623730951 * sigma, kEPS)));
+}
+
+__device__ FitCtx fit_ctx(const tpe_fit_job& j, const double* __restrict__ keys_sorted,
+                          const uint32_t* __restrict__ ranks, int64_t pos) {
+  FitCtx c;
+  c.n = j.n_obs - j.n_below;
+  c.K = c.n + 1;
+  c.s = keys_sorted + j.seg_off;
+  c.rank = ranks + j.seg_off;
+  c.pos = pos;
+  c.pmu = j.prior_mu; c.psig = j.prior_sigma; c.pw = j.prior_weight;
+  c.smax = j.prior_sigma;
+  c.smin = j.prior_sigma / fmin(100.0, 1.0 + (double)c.K);                   // tpe.py:465-470
+  c.ramp = j.lf > 0 && j.lf < c.n;
+  c.num = c.n - j.lf;
+  c.start = 1.0 / (double)c.n;
+  c.step = c.num > 1 ? (1.0 - c.start) / (double)(c.num - 1) : 0.0;
+  c.bounded = j.family != TPE_FAM_LOGGAUSS && (j.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH));
+  c.low = j.low; c.high = j.high;
+  return c;
+}
+
+__device__ __forceinline__ FitPart* fit_parts(const tpe_fit_job& j, double* scratch) {
+  return reinterpret_cast<FitPart*>(scratch + j.seg_off + kFitHdrParts);
+}
+static_assert(sizeof(FitPart) == 12 * sizeof(double), "FitPart: 12 doubles");
+
+struct FitStats {
+  double W, M, cm, thr, s_narrow;
+};
+
+__global__ __launch_bounds__(kFitThreads) void k_fit_stats(const tpe_fit_job* __restrict__ J,
+                                                           const double* __restrict__ keys_sorted,
+                                                           const uint32_t* __restrict__ ranks,
+                                                           double* __restrict__ scratch,
+                                                           uint32_t* __restrict__ wide_scratch) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
+  if (c0 >= K) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) wide_scratch[j.seg_off] = 0u;   // the wide list's counter
+  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)scratch[j.seg_off + kFitHdrPos]);
+  double W = 0, M = 0, cm = 0.0, sm_all = 0;      // (cm: the largest ratio w / sigma)
   double sm[kThr];
   int cnt[kThr];
 #pragma unroll
   for (int m = 0; m < kThr; ++m) { sm[m] = 0; cnt[m] = 0; }
-  for (int64_t i = threadIdx.x; i < K; i += kFitThreads) {
-    const double sg = sigma_of(i), w = weight_of(i), mu = v.mu(i);
+#pragma unroll 1
+  for (int e = 0; e < kFitPer; ++e) {
+    const int64_t i = c0 + e * kFitThreads + threadIdx.x;
+    if (i >= K) break;
+    const double sg = c.sigma(i), w = c.weight(i);
     W += w;
-    if (bounded) M += w * (ncdf(j.high, mu, sg) - ncdf(j.low, mu, sg));
-    cm = fmax(cm, log2(w / fmax(sg, kEPS)));
-    if (i != v.pos) {
+    if (c.bounded) {
+      const double mu = c.mu(i);
+      M += w * (ncdf(c.high, mu, sg) - ncdf(c.low, mu, sg));
+    }
+    cm = fmax(cm, w / fmax(sg, kEPS));
+    if (i != c.pos) {
       sm_all = fmax(sm_all, sg);
 #pragma unroll
       for (int m = 0; m < kThr; ++m) {
-        const double thr = smin * (double)(2 << m);
+        const double thr = c.smin * (double)(2 << m);
         if (sg > thr) ++cnt[m]; else sm[m] = fmax(sm[m], sg);
       }
     }
   }
-  // all 14 reductions in one round: sums [W, M, cnt0..4], maxima [cm, sm_all, sm0..4]
-  constexpr int kNS = 2 + kThr, kNM = 2 + kThr;
-  double vs[kNS] = {W, M}, vm[kNM] = {cm, sm_all};
-#pragma unroll
-  for (int m = 0; m < kThr; ++m) { vs[2 + m] = (double)cnt[m]; vm[2 + m] = sm[m]; }
-  __shared__ double rs[kFitThreads / 64][kNS], rm[kFitThreads / 64][kNM];
   for (int o = 32; o > 0; o >>= 1) {
+    W += __shfl_xor(W, o); M += __shfl_xor(M, o);
+    cm = fmax(cm, __shfl_xor(cm, o)); sm_all = fmax(sm_all, __shfl_xor(sm_all, o));
 #pragma unroll
-    for (int q = 0; q < kNS; ++q) vs[q] += __shfl_xor(vs[q], o);
-#pragma unroll
-    for (int q = 0; q < kNM; ++q) vm[q] = fmax(vm[q], __shfl_xor(vm[q], o));
+    for (int m = 0; m < kThr; ++m) { sm[m] = fmax(sm[m], __shfl_xor(sm[m], o)); cnt[m] += __shfl_xor(cnt[m], o); }
   }
+  __shared__ FitPart wp[kFitThreads / 64];
+  const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    wp[wave].W = W; wp[wave].M = M; wp[wave].rmax = cm; wp[wave].sm_all = sm_all;
 #pragma unroll
-    for (int q = 0; q < kNS; ++q) rs[threadIdx.x >> 6][q] = vs[q];
-#pragma unroll
-    for (int q = 0; q < kNM; ++q) rm[threadIdx.x >> 6][q] = vm[q];
+    for (int m = 0; m < kThr; ++m) { wp[wave].sm[m] = sm[m]; wp[wave].cnt[m] = cnt[m]; }
   }
   __syncthreads();
+  if (threadIdx.x == 0) {
+    FitPart r = wp[0];
+    for (int w = 1; w < kFitThreads / 64; ++w) {
+      r.W += wp[w].W; r.M += wp[w].M; r.rmax = fmax(r.rmax, wp[w].rmax); r.sm_all = fmax(r.sm_all, wp[w].sm_all);
 #pragma unroll
-  for (int q = 0; q < kNS; ++q) {
-    vs[q] = rs[0][q];
-    for (int wv = 1; wv < kFitThreads / 64; ++wv) vs[q] += rs[wv][q];
+      for (int m = 0; m < kThr; ++m) { r.sm[m] = fmax(r.sm[m], wp[w].sm[m]); r.cnt[m] += wp[w].cnt[m]; }
+    }
+    r.pad = 0;
+    fit_parts(j, scratch)[blockIdx.x] = r;
   }
+}
+
+// the job's chunk statistics combined once (fixed chunk order) into the header
+__global__ __launch_bounds__(64) void k_fit_combine(const tpe_fit_job* __restrict__ J, double* __restrict__ scratch) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  const int64_t K = j.n_obs - j.n_below + 1;
+  const int nc = (int)((K + kFitChunk - 1) / kFitChunk);
+  const FitPart* __restrict__ parts = fit_parts(j, scratch);
+  __shared__ FitPart lp[64];
+  __shared__ FitPart acc;
+  for (int c0 = 0; c0 < nc; c0 += 64) {
+    const int m = min(64, nc - c0);
+    if ((int)threadIdx.x < m) lp[threadIdx.x] = parts[c0 + threadIdx.x];      // one round of loads
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      FitPart r = c0 ? acc : lp[0];
+      for (int q = c0 ? 0 : 1; q < m; ++q) {
+        const FitPart& p = lp[q];
+        r.W += p.W; r.M += p.M; r.rmax = fmax(r.rmax, p.rmax); r.sm_all = fmax(r.sm_all, p.sm_all);
 #pragma unroll
-  for (int q = 0; q < kNM; ++q) {
-    vm[q] = rm[0][q];
-    for (int wv = 1; wv < kFitThreads / 64; ++wv) vm[q] = fmax(vm[q], rm[wv][q]);
+        for (int t = 0; t < kThr; ++t) { r.sm[t] = fmax(r.sm[t], p.sm[t]); r.cnt[t] += p.cnt[t]; }
+      }
+      acc = r;
+    }
+    __syncthreads();
   }
-  W = vs[0]; M = vs[1]; cm = vm[0]; sm_all = vm[1];
-  double thr = INFINITY, s_narrow = sm_all;
-  for (int m = 0; m < kThr; ++m)
-    if (thr == INFINITY && vs[2 + m] <= (double)(kPruneWide - 1)) { thr = smin * (double)(2 << m); s_narrow = vm[2 + m]; }
-  if (threadIdx.x == 0) n_wide = 0;
-  __syncthreads();
-  // pass 2: rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and
-  // sigma > thr) get c = -inf in the sorted list and are listed apart
+  if (threadIdx.x == 0) {
+    const double smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);
+    double thr = INFINITY, s_narrow = acc.sm_all;
+    for (int m = 0; m < kThr; ++m)
+      if (thr == INFINITY && acc.cnt[m] <= kPruneWide - 1) { thr = smin * (double)(2 << m); s_narrow = acc.sm[m]; }
+    double* __restrict__ hdr = scratch + j.seg_off + kFitHdrStats;
+    hdr[0] = acc.W; hdr[1] = acc.M; hdr[2] = log2(acc.rmax); hdr[3] = thr; hdr[4] = s_narrow;
+  }
+}
+
+__global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __restrict__ J,
+                                                          const double* __restrict__ keys_sorted,
+                                                          const uint32_t* __restrict__ ranks,
+                                                          const double* __restrict__ scratch,
+                                                          uint32_t* __restrict__ wide_scratch,
+                                                          float4* __restrict__ comp) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
+  if (c0 >= K) return;
+  const double* __restrict__ hdr = scratch + j.seg_off;
+  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)hdr[kFitHdrPos]);
+  const double cm = hdr[kFitHdrStats + 2], thr = hdr[kFitHdrStats + 3];
+  // rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and sigma >
+  // thr) get c = -inf in the sorted list and are listed apart
   float4* __restrict__ C = comp + j.above_off;
-  for (int64_t i = threadIdx.x; i < K; i += kFitThreads) {
-    const double sg = sigma_of(i), w = weight_of(i), mu = v.mu(i);
+  uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
+#pragma unroll 2
+  for (int e = 0; e < kFitPer; ++e) {
+    const int64_t i = c0 + e * kFitThreads + threadIdx.x;
+    if (i >= K) break;
+    const double sg = c.sigma(i), w = c.weight(i), mu = c.mu(i);
     const double se = fmax(sg, kEPS);
     const float hi = (float)mu;
-    const bool wide = i == v.pos || sg > thr;
+    const bool wide = i == c.pos || sg > thr;
     C[i] = make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se),
                        wide ? -INFINITY : (float)(log2(w / se) - cm));
     if (wide) {
-      const int slot = atomicAdd(&n_wide, 1);
-      if (slot < kPruneWide) wide_ix[slot] = i;
+      const uint32_t slot = atomicAdd(&wl[0], 1u);
+      if (slot < (uint32_t)kPruneWide) wl[1 + slot] = (uint32_t)i;
     }
   }
-  __syncthreads();
-  const int nw = min(n_wide, kPruneWide);
-  if (threadIdx.x == 0) {                         // fixed order of the wide list
-    for (int a = 1; a < nw; ++a)
+}
+
+// grid over the f32 means: grid[g] = the first component with mu32 >= edge_g,
+// edge_g = glo + g / ginv — a binary search per bucket over the sorted means
+// (the prior inserted), grid[G] = K
+constexpr int kGridThreads = 256;
+constexpr int kFitMaxGrid = 4096;                // grid_n = min(4096, 4K) (tpe_host_pack_level)
+__global__ __launch_bounds__(kGridThreads) void k_fit_grid(const tpe_fit_job* __restrict__ J,
+                                                           const double* __restrict__ keys_sorted,
+                                                           const uint32_t* __restrict__ ranks,
+                                                           const double* __restrict__ scratch,
+                                                           int32_t* __restrict__ grid) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  const int G = j.grid_n;
+  const int g = (int)blockIdx.x * kGridThreads + (int)threadIdx.x;
+  if (g > G) return;
+  const int64_t n = j.n_obs - j.n_below, K = n + 1;
+  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)scratch[j.seg_off + kFitHdrPos]);
+  int32_t* __restrict__ Gp = grid + j.grid_off;
+  if (g == G) { Gp[G] = (int32_t)K; return; }
+  const double glo = (double)(float)c.mu(0), ghi = (double)(float)c.mu(K - 1);
+  const float ginv = ghi > glo ? (float)((double)G / (ghi - glo)) : 0.f;
+  if (!(ginv > 0.f)) { Gp[g] = 0; return; }
+  const double edge = glo + (double)g / (double)ginv;
+  int64_t lo = 0, hi = K;                        // first i with !(mu32[i] < edge)
+  while (lo < hi) {
+    const int64_t md = (lo + hi) >> 1;
+    if ((double)(float)c.mu(md) < edge) lo = md + 1;
+    else hi = md;
+  }
+  Gp[g] = (int32_t)lo;
+}
+
+// the wide list in index order, its rows, and the job's problem rows:
+// lpdf = ln2 * log2(sum) + base; base = ln2*cm - ln(W sqrt(2 pi) p_accept)
+__global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__ J,
+                                                 const double* __restrict__ keys_sorted,
+                                                 const uint32_t* __restrict__ ranks,
+                                                 const double* __restrict__ scratch,
+                                                 const uint32_t* __restrict__ wide_scratch,
+                                                 tpe_problem* __restrict__ P, float4* __restrict__ comp) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  const int64_t n = j.n_obs - j.n_below, K = n + 1;
+  __shared__ int64_t wide_ix[kPruneWide];
+  __shared__ int s_nw;
+  const uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
+  const double* __restrict__ hdr = scratch + j.seg_off;
+  if (threadIdx.x == 0) {
+    const int nw = (int)min(wl[0], (uint32_t)kPruneWide);
+    for (int a = 0; a < nw; ++a) wide_ix[a] = wl[1 + a];
+    for (int a = 1; a < nw; ++a)                  // fixed order of the wide list
       for (int b = a; b > 0 && wide_ix[b - 1] > wide_ix[b]; --b) {
         const int64_t t = wide_ix[b]; wide_ix[b] = wide_ix[b - 1]; wide_ix[b - 1] = t;
       }
+    s_nw = nw;
   }
   __syncthreads();
-  if (threadIdx.x < nw) {
+  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)hdr[kFitHdrPos]);
+  const FitStats st{hdr[kFitHdrStats], hdr[kFitHdrStats + 1], hdr[kFitHdrStats + 2], hdr[kFitHdrStats + 3],
+                    hdr[kFitHdrStats + 4]};
+  const int nw = s_nw;
+  if ((int)threadIdx.x < nw) {
     const int64_t i = wide_ix[threadIdx.x];
-    const double sg = sigma_of(i), w = weight_of(i), mu = v.mu(i), se = fmax(sg, kEPS);
+    const double sg = c.sigma(i), w = c.weight(i), mu = c.mu(i), se = fmax(sg, kEPS);
     const float hi = (float)mu;
     comp[j.wide_off + threadIdx.x] =
-        make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - cm));
+        make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - st.cm));
   }
-  // grid over the f32 means: grid[g] = first component with mu32 >= edge_g,
-  // edge_g = glo + g / ginv.  Scattered by component: component i owns the
-  // buckets whose edge lies in (mu32[i-1], mu32[i]] (i = K: the rest), found
-  // from the bucket estimate and corrected against the exact edge formula, so
-  // the work is O(K + G) with no dependent loads.
-  const double glo = (double)(float)v.mu(0), ghi = (double)(float)v.mu(K - 1);
-  const int G = j.grid_n;
-  const float ginv = ghi > glo ? (float)((double)G / (ghi - glo)) : 0.f;
-  int32_t* __restrict__ Gp = grid + j.grid_off;
-  if (ginv > 0.f) {
-    const double gi = (double)ginv;
-    auto edge = [&](int64_t g) { return glo + (double)g / gi; };
-    // first bucket whose edge is > x
-    auto first_above = [&](double x) -> int64_t {
-      if (!(x >= glo)) return 0;
-      int64_t g = (int64_t)floor((x - glo) * gi);
-      g = g < 0 ? 0 : (g > G ? G : g);
-      while (g > 0 && edge(g - 1) > x) --g;
-      while (g < G && !(edge(g) > x)) ++g;
-      return g;
-    };
-    for (int64_t i = threadIdx.x; i <= K; i += kFitThreads) {
-      const int64_t g0 = i == 0 ? 0 : first_above((double)(float)v.mu(i - 1));
-      const int64_t g1 = i == K ? G : first_above((double)(float)v.mu(i));    // edges <= mu32[i]: [g0, g1)
-      for (int64_t g = g0; g < g1; ++g) Gp[g] = (int32_t)i;
-    }
-  } else {
-    for (int g = threadIdx.x; g < G; g += kFitThreads) Gp[g] = 0;
-  }
-  if (threadIdx.x == 0) Gp[G] = (int32_t)K;
-  // problem rows: lpdf = ln2 * log2(sum) + base; base = ln2*cm - ln(W sqrt(2 pi) p_accept)
-  if (threadIdx.x < j.n_problems) {
-    const double pa = bounded ? M / W : 1.0;
+  if ((int)threadIdx.x < j.n_problems) {
+    const double glo = (double)(float)c.mu(0), ghi = (double)(float)c.mu(K - 1);
+    const float ginv = ghi > glo ? (float)((double)j.grid_n / (ghi - glo)) : 0.f;
+    const double pa = c.bounded ? st.M / st.W : 1.0;
     tpe_problem& p = P[j.problem_first + threadIdx.x];
-    p.above_base = kLn2 * cm - log(W) - 0.91893853320467274 - log(pa);
+    p.above_base = kLn2 * st.cm - log(st.W) - 0.91893853320467274 - log(pa);
     p.wide_len = nw;
     const double pse = fmax(j.prior_sigma, kEPS);
     p.prior_mu = (float)j.prior_mu;
     p.prior_a = (float)(kAScale / pse);
-    p.prior_c = (float)(log2(j.prior_weight / pse) - cm);
+    p.prior_c = (float)(log2(j.prior_weight / pse) - st.cm);
     p.narrow_cmax = 0.f;                           // max over all c after the shift: an upper bound
-    p.narrow_amin = (float)(kAScale / fmax(s_narrow, kEPS));
+    p.narrow_amin = (float)(kAScale / fmax(st.s_narrow, kEPS));
     p.grid_lo = (float)glo;
     p.grid_inv = ginv;
   }
@@ -3007,14 +3135,25 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   }
   // below positions in fit_vals (free once the merge has run), compaction into
   // the sorted buffers, then the build
-  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, b->fit_vals);
+  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, b->fit_vals, b->fit_keys);
   const unsigned tiles_c = (unsigned)((b->fit_max_obs + kCompactTile - 1) / kCompactTile);
   TPE_LAUNCH(k_ord_compact, dim3(tiles_c, b->n_fit), dim3(kCompactThreads), 0, s, b->fit, b->below_idx, b->fit_vals,
              b->fit_keys_sorted, b->fit_vals_sorted);
   if ((rc = hip_check("tpe_fit_above/compact"))) return rc;
-  TPE_LAUNCH(k_fit_build, dim3(b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
-                     b->fit_vals_sorted, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32,
-                     const_cast<int32_t*>(b->grid));
+  // the build: chunk statistics (into fit_keys, free once the merge has run),
+  // rows + grid, the wide list (its counter and indices in fit_vals, free once
+  // the compaction has run) and the problem rows
+  const unsigned chunks_k = (unsigned)((b->fit_max_obs + 1 + kFitChunk - 1) / kFitChunk);
+  TPE_LAUNCH(k_fit_stats, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
+             b->fit_vals_sorted, b->fit_keys, b->fit_vals);
+  TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys);
+  TPE_LAUNCH(k_fit_emit, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
+             b->fit_vals_sorted, b->fit_keys, b->fit_vals, (float4*)b->comp32);
+  TPE_LAUNCH(k_fit_wide, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys_sorted, b->fit_vals_sorted,
+             b->fit_keys, b->fit_vals, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32);
+  const unsigned gblocks = (unsigned)((kFitMaxGrid + 1 + kGridThreads - 1) / kGridThreads);
+  TPE_LAUNCH(k_fit_grid, dim3(gblocks, b->n_fit), dim3(kGridThreads), 0, s, b->fit, b->fit_keys_sorted,
+             b->fit_vals_sorted, b->fit_keys, const_cast<int32_t*>(b->grid));
   return hip_check("tpe_fit_above/build");
 }
 
@@ -3208,16 +3347,21 @@ static int run_batch_profiled(const tpe_batch* b, void* stream) {
 // after the stream synchronise: event times and each stage's work
 static int profile_collect(const tpe_batch& b, const tpe_pack_info& info, const tpe_problem* hp, int64_t n_cand) {
   const int64_t P = info.n_problems;
-  double ce_tab = 0, ce_above = 0;
+  double ce_tab = 0, ce_above = 0, drawn = 0;
+  const bool lz = b.early_select && !(b.flags & TPE_BATCH_WRITE_CAND);
   for (int64_t r = 0; r < P; ++r) {
     if (hp[r].tab_mode != TPE_TAB_NONE)
       ce_tab += (double)(hp[r].below_len + hp[r].above_len) * (double)n_cand;
     else if (hp[r].family != TPE_FAM_CATEGORICAL)
       ce_above += (double)hp[r].above_len * (double)n_cand;
+    // candidates the sample stage draws (lazy categoricals are scanned by the table stage)
+    const bool lazy = lz && (hp[r].flags & TPE_F_CAT_LAZY) && hp[r].family == TPE_FAM_CATEGORICAL &&
+                      hp[r].samp_len <= 64;
+    if (!lazy) drawn += (double)n_cand;
   }
   const double C = (double)P * (double)n_cand;
   const double units[TPE_N_STAGES] = {
-      (double)info.fit_total, (double)info.tab_units, C,
+      (double)info.fit_total, (double)info.tab_units, drawn,
       (double)((b.sort_end_bit + 7) / 8) * 2.0 * 12.0 * (double)b.sort_count, ce_above, C, (double)P};
   for (int i = 0; i < TPE_N_STAGES; ++i) {
     tpe_stage_prof& q = g_prof.last[i];

@@ -33,7 +33,9 @@ constexpr int kActive = -1;     // active label that gates nothing (placeholder)
 // categorical probabilities (mu / sigma null)
 struct Fit {
   bool done = false;
+  bool dev = false;              // above side: the device Parzen fit (below_idx, the record's column)
   std::vector<double> buf;
+  std::vector<int32_t> below_idx;
   int64_t k[2] = {0, 0};
   const double* w[2] = {nullptr, nullptr};
   const double* mu[2] = {nullptr, nullptr};
@@ -88,6 +90,41 @@ int fit_label(Tree& T, int i) {
     f.w[0] = f.buf.data();
     f.w[1] = f.buf.data() + L.upper;
     f.mu[0] = f.mu[1] = f.sg[0] = f.sg[1] = nullptr;
+  } else if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && L.dev_obs &&
+             T.device_fit_min > 0 && n >= std::max<int64_t>(T.device_fit_min, 64)) {
+    // device Parzen fit of the above side; the below side (ap_filter_trials,
+    // tpe.py:629-636: the observations whose tid is below) fitted here.  It has
+    // at most 25 observations, all of weight 1 (no linear-forgetting ramp below
+    // 26, tpe.py:381-394), so any sort of it gives numpy's fit: tied values are
+    // interchangeable
+    f.below_idx.clear();
+    const double* x = (const double*)L.values;
+    for (int64_t b = 0; b < T.n_below; ++b) {              // each below tid among the ascending tids
+      const int64_t* at = std::lower_bound(L.tids, L.tids + n, T.below[b]);
+      if (at != L.tids + n && *at == T.below[b]) f.below_idx.push_back((int32_t)(at - L.tids));
+    }
+    const int64_t nb = (int64_t)f.below_idx.size();
+    if (nb > 64 || n - nb + 1 <= 64) return TPE_E_FALLBACK;
+    std::vector<double> bx((size_t)nb);
+    std::vector<int64_t> ord((size_t)nb);
+    for (int64_t q = 0; q < nb; ++q) { bx[(size_t)q] = x[f.below_idx[(size_t)q]]; ord[(size_t)q] = q; }
+    for (int64_t q = 1; q < nb; ++q)                        // stable insertion sort (NaN last)
+      for (int64_t r = q; r > 0; --r) {
+        const double a = bx[(size_t)ord[(size_t)r - 1]], c = bx[(size_t)ord[(size_t)r]];
+        if (!(a > c || (a != a && c == c))) break;
+        std::swap(ord[(size_t)r - 1], ord[(size_t)r]);
+      }
+    const size_t cap = (size_t)nb + 1;
+    f.buf.resize(3 * cap);
+    const int64_t rc = tpe_host_fit_parzen(bx.data(), nb, nb >= 2 ? ord.data() : nullptr, T.prior_weight, L.prior_mu,
+                                           L.prior_sigma, T.lf, f.buf.data(), f.buf.data() + cap,
+                                           f.buf.data() + 2 * cap);
+    if (rc < 0) return tpe_internal_fail(TPE_E_ARG, "tpe_host_fit_parzen failed on a below side");
+    f.k[0] = nb + 1;
+    f.w[0] = f.buf.data(); f.mu[0] = f.buf.data() + cap; f.sg[0] = f.buf.data() + 2 * cap;
+    f.k[1] = n - nb + 1;
+    f.w[1] = f.mu[1] = f.sg[1] = nullptr;
+    f.dev = true;
   } else if (L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) {
     if (n > 0 && !L.order) return host_fit();                                  // a NaN value
     if (T.device_fit_min > 0 && n >= std::max<int64_t>(T.device_fit_min, 64)) return TPE_E_FALLBACK;
@@ -163,7 +200,8 @@ int predict(Tree& T, int64_t n_cand, double min_draws, std::vector<int>& pred, b
 }
 
 // one level's label record (tpe_label_in) from a fit
-void label_rec(const tpe_tree_label& L, const Fit& f, const int64_t* ids, int64_t n_ids, tpe_label_in& r) {
+void label_rec(const Tree& T, const tpe_tree_label& L, const Fit& f, const int64_t* ids, int64_t n_ids,
+               tpe_label_in& r) {
   memset(&r, 0, sizeof(r));
   r.family = L.family;
   r.flags = L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH);
@@ -176,6 +214,16 @@ void label_rec(const tpe_tree_label& L, const Fit& f, const int64_t* ids, int64_
   r.above_w = f.w[1]; r.above_mu = f.mu[1]; r.above_sigma = f.sg[1]; r.above_k = f.k[1];
   r.ids = ids;
   r.n_ids = n_ids;
+  if (f.dev) {                                  // the device fit of the above side (tpe_fit_above)
+    r.dev_obs = L.dev_obs;
+    r.n_obs = L.n_obs;
+    r.below_idx = f.below_idx.data();
+    r.n_below = (int32_t)f.below_idx.size();
+    r.lf = T.lf;
+    r.prior_mu = L.prior_mu; r.prior_sigma = L.prior_sigma; r.prior_weight = T.prior_weight;
+    r.ord_key_in = L.ord_key_in; r.ord_idx_in = L.ord_idx_in; r.n_ord_in = L.n_ord_in;
+    r.ord_key_out = L.ord_key_out; r.ord_idx_out = L.ord_idx_out;
+  }
 }
 
 }  // namespace
@@ -224,8 +272,8 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
   for (int i = 0; i < n_labels; ++i) {
     const tpe_tree_label& L = labels[i];
     if (T.gate[(size_t)i] && L.family != TPE_FAM_CATEGORICAL) return TPE_E_FALLBACK;
-    if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && L.host_k[0] <= 0 && device_fit_min > 0 &&
-        L.n_obs >= std::max<int64_t>(device_fit_min, 64))
+    if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && L.host_k[0] <= 0 && !L.dev_obs &&
+        device_fit_min > 0 && L.n_obs >= std::max<int64_t>(device_fit_min, 64))
       return TPE_E_FALLBACK;
   }
   if (n_labels == 0 || n_ids == 0) return TPE_OK;
@@ -269,7 +317,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
           if (rc == TPE_E_FALLBACK && need_fit && need_fit[i]) { pending = true; continue; }
           return rc;
         }
-        label_rec(labels[i], fits[(size_t)i], ids, n_ids, recs[(size_t)nr++]);
+        label_rec(T, labels[i], fits[(size_t)i], ids, n_ids, recs[(size_t)nr++]);
       }
       if (pending) return TPE_E_FALLBACK;
       if ((rc = run(nr)) != TPE_OK) return rc;
@@ -333,7 +381,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
     for (size_t m = 0; m < members.size(); ++m) {
       const int64_t first = members[m].second;
       const int64_t end = m + 1 < members.size() ? members[m + 1].second : (int64_t)lvl_ids.size();
-      label_rec(labels[members[m].first], fits[(size_t)members[m].first], lvl_new.data() + first, end - first,
+      label_rec(T, labels[members[m].first], fits[(size_t)members[m].first], lvl_new.data() + first, end - first,
                 recs[m]);
     }
     const int rc = run((int32_t)members.size());

@@ -26,10 +26,11 @@ class ValueOrder(object):
     observations merges the new ones into the other pair (tpe_fit_above), and
     ``commit`` makes that pair current.  The reference re-sorts every
     suggest (tpe.py:427); this sorts each observation once."""
-    __slots__ = ('device', 'keys', 'idx', 'cur', 'n')
+    __slots__ = ('device', 'keys', 'idx', 'cur', 'n', 'owner')
 
-    def __init__(self, device):
+    def __init__(self, device, owner=None):
         self.device = device
+        self.owner = owner            # the DeviceColumns whose version a change bumps
         self.keys = [None, None]
         self.idx = [None, None]
         self.cur = 0
@@ -41,6 +42,7 @@ class ValueOrder(object):
             cap = max(n, 1024, 2 * (t.numel() if t is not None else 0))
             self.keys[side] = torch.empty(cap, dtype=torch.float64, device=self.device)
             self.idx[side] = torch.empty(cap, dtype=torch.int32, device=self.device)
+            self._bump()
 
     def ptrs(self, n_obs):
         """(key_in, idx_in, n_in, key_out, idx_out) device addresses for a run
@@ -58,6 +60,11 @@ class ValueOrder(object):
         """A run with ``ptrs(n_obs)`` was enqueued: its output is the order."""
         if self.n != n_obs:
             self.cur, self.n = 1 - self.cur, n_obs
+            self._bump()
+
+    def _bump(self):
+        if self.owner is not None:
+            self.owner.version += 1
 
     def host(self):
         """(t, position) of the current order, copied to the host (tests)."""
@@ -76,6 +83,7 @@ class DeviceColumns(object):
     def __init__(self, device):
         self.device = device
         self.cols = {}                # label -> [tensor, n uploaded, ValueOrder]
+        self.version = 0              # bumped whenever a column or an order moves (memos of their addresses)
 
     def column(self, label, values):
         """Device tensor whose first ``len(values)`` entries are ``values``
@@ -84,7 +92,8 @@ class DeviceColumns(object):
         ent = self.cols.get(label)
         if ent is None or ent[1] > n:
             ent = self.cols[label] = [torch.empty(max(n, 1024), dtype=torch.float64, device=self.device), 0,
-                                      ValueOrder(self.device)]
+                                      ValueOrder(self.device, self)]
+            self.version += 1
         t, m = ent[0], ent[1]
         if n > m:
             if n > t.numel():
@@ -94,6 +103,7 @@ class DeviceColumns(object):
             src = torch.from_numpy(np.ascontiguousarray(values[m:n], dtype=np.float64))
             t[m:n].copy_(src)
             ent[1] = n
+            self.version += 1
         return t
 
     def order(self, label):

@@ -32,7 +32,7 @@ class History(object):
     label the (tid, value) observations in tid order.  ``dev`` holds the
     device copies of the observation columns (devhist.DeviceColumns per
     device); it lives as long as the append-only source it mirrors."""
-    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache', '_orders', '_logs')
+    __slots__ = ('tids', 'losses', 'obs', 'dev', 'sorted_obs', '_cache', '_orders', '_logs', 'tree_memo')
 
     def __init__(self, tids, losses, obs, dev=None, sorted_obs=True, cache=None):
         self.tids, self.losses, self.obs = tids, losses, obs
@@ -41,6 +41,7 @@ class History(object):
         self._cache = cache
         self._orders = None
         self._logs = None
+        self.tree_memo = None          # tpe._tree_labels of this (immutable) view without a Trials cache
 
     def smallest(self, m):
         return None if self._cache is None else self._cache.smallest(m)

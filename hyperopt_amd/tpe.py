@@ -297,25 +297,40 @@ def _tree_static(table):
     return st
 
 
-def _tree_labels(table, hist):
+def _dev_fit_min(engine):
+    """Observations from which a continuous label's above side is fitted on
+    the device (Engine.device_fit_min, fp32 only), or None."""
+    if engine is None or engine.precision != 'fp32' or engine.device_fit_min <= 0:
+        return None
+    return max(int(engine.device_fit_min), 64)
+
+
+def _tree_labels(table, hist, engine=None):
     """The table's tree records with the history's observation columns filled
-    in (tids, kernel coordinate, value order) — memoised on the Trials cache
-    while no document is appended (the columns' buffers stay put until then).
-    Quantized labels carry no columns: tpe_suggest_tree sends them to the
-    general path whenever they need a fit."""
+    in (tids, kernel coordinate, value order) and, for the continuous labels
+    large enough for the device Parzen fit, the device column and resident
+    value order (devhist) — memoised per (table object, document count) on the
+    Trials cache, or on the History itself without one, while the device
+    columns and orders stay put (DeviceColumns.version).  Quantized labels
+    carry no columns: tpe_suggest_tree sends them to the caller whenever they
+    need a fit.  Returns (records, keep-alive list, [(ValueOrder, n_obs) of
+    the device-fitted labels by label index]) or None."""
     st = _tree_static(table)
     if st is None:
         return None
     arr0, _, meta = st
+    dev_min = _dev_fit_min(engine)
     cache = hist._cache
-    if cache is not None:
-        # keyed on the table OBJECT (the memo keeps it alive, so a new table can
-        # never reuse its id) and the document count
-        memo = getattr(cache, 'tree_memo', None)
-        if memo is not None and memo[0] is table and memo[1] == len(cache.docs):
-            return memo[2]
+    holder, n_docs = (cache, len(cache.docs)) if cache is not None else (hist, -1)
+    dc = devhist.columns(hist, engine.device) if dev_min is not None else None
+    # keyed on the table OBJECT (the memo keeps it alive, so a new table can
+    # never reuse its id), the document count and the device state's version
+    memo = getattr(holder, 'tree_memo', None)
+    if (memo is not None and memo[0] is table and memo[1] == n_docs and memo[2] == dev_min
+            and (dc is None or memo[4] == dc.version)):
+        return memo[3]
     arr = arr0.copy()
-    keep = []
+    keep, devs = [], {}
     for label, ix, fam in meta:
         rec = arr[ix]
         otids, ovals = hist.obs[label]
@@ -327,9 +342,24 @@ def _tree_labels(table, hist):
                 cols = (t.ctypes.data, v.ctypes.data)
             rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
         elif fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
-            order = hist.value_order(label)
-            rec['n_obs'] = len(otids)
+            rec['n_obs'] = n = len(otids)
             logc = fam == N.FAM_LOGGAUSS
+            if dev_min is not None and n >= dev_min:
+                # device fit of the above side: the device column (kernel coordinate)
+                # and its resident order; the host keeps the columns for the below side
+                x = np.ascontiguousarray(hist.log_values(label) if logc else ovals, dtype=np.float64)
+                t = np.ascontiguousarray(otids, dtype=np.int64)
+                keep += [t, x]
+                col = dc.column(label, x)
+                order = dc.order(label)
+                kin, iin, n_in, kout, iout = order.ptrs(n)
+                rec['tids'], rec['values'], rec['order'] = t.ctypes.data, x.ctypes.data, 0
+                rec['dev_obs'], rec['ord_key_in'], rec['ord_idx_in'], rec['n_ord_in'] = col.data_ptr(), kin, iin, n_in
+                rec['ord_key_out'], rec['ord_idx_out'] = kout, iout
+                keep.append(col)
+                devs[ix] = (order, n)
+                continue
+            order = hist.value_order(label)
             cols = hist.native_columns(label, log=logc) if order is not None else None
             if cols is None:
                 t = np.ascontiguousarray(otids, dtype=np.int64)
@@ -341,9 +371,8 @@ def _tree_labels(table, hist):
                     keep.append(o)
                     cols = cols[:2] + (o.ctypes.data,)
             rec['tids'], rec['values'], rec['order'] = cols
-    out = (arr, keep)
-    if cache is not None:
-        cache.tree_memo = (table, len(cache.docs), out)
+    out = (arr, keep, devs)
+    holder.tree_memo = (table, n_docs, dev_min, out, dc.version if dc is not None else None)
     return out
 
 
@@ -364,7 +393,7 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
 def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard):
     if not hist.sorted_obs:
         return None
-    tl = _tree_labels(table, hist)
+    tl = _tree_labels(table, hist, engine)
     if tl is None:
         return None
     ex = None
@@ -416,6 +445,10 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     # (only labels some id used: a branch switch drops the old branch's)
     used = np.asarray(active).any(axis=0)
     table.native_fit_hint = tuple(ix for ix in host if used[ix])
+    # the device-fitted labels that ran hold their merged value orders now
+    for ix, (order, n) in tl[2].items():
+        if used[ix]:
+            order.commit(n)
     order = table.level_order()
     cols = _tree_static(table)[2]
     i64, f64 = np.int64, np.float64

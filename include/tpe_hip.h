@@ -593,10 +593,12 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
  * quantized labels and sides with repeated values (numpy's argsort tie order
  * decides their weights), missing value orders (NaN) — is flagged in need_fit
  * and TPE_E_FALLBACK returned: the caller fits those labels (exactly as the
- * reference) and calls again with their fits.  Labels large enough for the
- * device Parzen fit and non-categorical gates return TPE_E_FALLBACK with no
- * flag: the caller takes its general path.  (On TPE_E_FALLBACK nothing is
- * written; a device batch may have run.)
+ * reference) and calls again with their fits.  Continuous labels large enough
+ * for the device Parzen fit run it (tpe_fit_above) when their record carries
+ * the device column; without it, and with non-categorical gates, the call
+ * returns TPE_E_FALLBACK with no flag before any fit or run: the caller takes
+ * its general path.  (On TPE_E_FALLBACK nothing is written; a device batch may
+ * have run when a deeper level flagged a label.)
  * ---------------------------------------------------------------------- */
 #define TPE_TREE_MAX_PARENTS 4
 enum { TPE_E_FALLBACK = -5 };
@@ -620,6 +622,12 @@ typedef struct tpe_tree_label {
   const double* host_mu[2];                 /* used as is (categorical: host_w = the probabilities)     */
   const double* host_sigma[2];
   int64_t host_k[2];
+  /* device Parzen fit of the above side (continuous labels with n_obs >= device_fit_min): the
+   * label's device column (n_obs kernel coordinates in tid order) and its resident value order
+   * (tpe_label_in); NULL dev_obs: such a label sends the space to the caller's general path */
+  const double* dev_obs;
+  const double* ord_key_in; const uint32_t* ord_idx_in; int64_t n_ord_in;
+  double* ord_key_out; uint32_t* ord_idx_out;
 } tpe_tree_label;
 
 /* tpe_suggest_tree flags: the tpe_level_run flags, plus */
@@ -673,8 +681,10 @@ int tpe_combine_results(const tpe_result* all, int32_t world, int64_t P, tpe_res
  * ex: the shard exchange (NULL unsharded); speculate_min_draws: a gate is
  * predicted when its predicted category is expected among >= this many of the
  * n_cand_global draws;
- * device_fit_min > 0: labels with that many observations are left to the host
- * path (device Parzen fit).  values / active: [n_ids x n_labels] — the chosen
+ * device_fit_min > 0: continuous labels with that many observations get the
+ * device Parzen fit of their above side (their below side, <= 25 observations
+ * with equal weights, is fitted here) when the record carries dev_obs, else the
+ * space is left to the caller's general path.  values / active: [n_ids x n_labels] — the chosen
  * value (categories as doubles) and whether the label is active; path[0] = 1
  * when the fused batch was used, path[1] = level runs issued; need_fit
  * [n_labels]: set to 1 for the labels the caller must fit (TPE_E_FALLBACK).
@@ -706,9 +716,11 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
 
 typedef struct tpe_stage_prof {
   double ms;         /* device time between the stage's bracketing events         */
-  double units;      /* stage work: fit observations | table units (16 B) |
-                        candidates | sort bytes (8-bit LSD passes x 2 x 12 B x keys) |
-                        above CE | candidates | problems                            */
+  double units;      /* stage work: fit scratch slots | table units (16 B) |
+                        candidates drawn by the sample kernels (lazy categoricals,
+                        scanned by the table stage, excluded) | sort bytes (8-bit
+                        LSD passes x 2 x 12 B x keys) | above CE | candidates |
+                        problems                                                    */
   double ce;         /* algorithmic component evaluations the stage stands in for:
                         sample = tabulated problems' (K_below + K_above) x C,
                         above = scored problems' K_above x C; else 0                */

@@ -163,9 +163,9 @@ def test_tree_labels_dtype_matches_ctypes():
         assert N.TREE_LABEL_DTYPE.fields[f][1] == getattr(N.TreeLabel, f).offset, f
 
 
-def _tree_call(table, hist, C, min_draws=64.0, flags=0, shard=None, ex=None, fit_min=16384):
+def _tree_call(table, hist, C, min_draws=64.0, flags=0, shard=None, ex=None, fit_min=16384, engine=None):
     from hyperopt_amd import history as H, tpe
-    arr, keep = tpe._tree_labels(table, hist)
+    arr, keep, _ = tpe._tree_labels(table, hist, engine)
     below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
     ws, need = N.LevelWS(), N.LevelNeed()
     vals = np.empty((1, len(arr)))
@@ -228,14 +228,14 @@ def test_suggest_tree_hands_quantized_labels_back():
     from hyperopt_amd import tpe
     fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, None)
     post = fits.get(domain.table.by_label['q'])
-    arr, keep = tpe._tree_labels(domain.table, hist)
+    arr, keep, _ = tpe._tree_labels(domain.table, hist)
     arr = arr.copy()
     cols = [[np.ascontiguousarray(c) for c in side] for side in (post.below, post.above)]
     for sd in range(2):
         arr[q]['host_k'][sd] = len(cols[sd][0])
         arr[q]['host_w'][sd], arr[q]['host_mu'][sd], arr[q]['host_sigma'][sd] = [c.ctypes.data for c in cols[sd]]
     orig = tpe._tree_labels
-    tpe._tree_labels = lambda t, h: (arr, keep)
+    tpe._tree_labels = lambda t, h, e=None: (arr, keep, {})
     try:
         rc, need, path, need_fit = _tree_call(domain.table, hist, 1024)
     finally:
@@ -324,3 +324,34 @@ def test_sharded_tree_exchanges_status_without_gpu():
     for rank, rc, levels, cand, err in got:
         assert err is None, err
         assert rc == N.E_SPACE and levels == 1 and cand == 4 * (1 << 15), (rank, rc, levels, cand)
+
+
+def test_suggest_tree_sizes_device_fits_without_gpu():
+    """A flat continuous space whose labels are large enough for the device
+    Parzen fit runs natively: tpe_suggest_tree fits every below side on the
+    host (<= 25 observations) and sizes the device fits (columns and resident
+    value orders in the records; host tensors stand in for device ones — the
+    call stops before touching them)."""
+    import bench
+    import torch
+    from hyperopt_amd import devhist, tpe
+
+    class _Eng(object):
+        precision, device_fit_min, device = 'fp32', 100, torch.device('cpu')
+    labels = ['x%d' % i for i in range(3)]
+    hist = bench.soa_history(labels, 400, 1, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+    table = bench.flat_uniform_table(labels)
+    arr, keep, devs = tpe._tree_labels(table, hist, _Eng())
+    assert sorted(devs) == [0, 1, 2] and all(n == 400 for _, n in devs.values())
+    assert np.all(arr['dev_obs'] != 0) and np.all(arr['n_ord_in'] == 0) and np.all(arr['ord_key_out'] != 0)
+    rc, need, path, need_fit = _tree_call(table, hist, 4096, fit_min=100, engine=_Eng())
+    # (pruned above mixtures: without a device the sort-workspace query that
+    # follows the sizing fails instead of returning TPE_E_SPACE)
+    assert rc in (N.E_SPACE, N.E_HIP) and path[1] == 1 and not need_fit.any(), rc
+    assert need.result == 3 and need.fit >= 3 * 400          # every label's fit scratch (all observations new)
+    # the memo: the same records while nothing moved; a committed order moves them
+    assert tpe._tree_labels(table, hist, _Eng())[0] is arr
+    devs[0][0].commit(400)
+    arr2 = tpe._tree_labels(table, hist, _Eng())[0]
+    assert arr2 is not arr and arr2[0]['n_ord_in'] == 400 and arr2[0]['ord_key_out'] == 0
+    assert devhist.columns(hist, torch.device('cpu')).order('x0').n == 400

@@ -86,6 +86,55 @@ def test_native_tree_columnar_history():
     assert path == (0, 1) and nat == gen
 
 
+def test_native_tree_device_fit_labels():
+    """Labels large enough for the device Parzen fit run natively too (below
+    sides fitted in C, above sides by tpe_fit_above from the resident value
+    orders): a flat 40-dim space over a 20k-trial history and a tree space
+    with a log-family label, identical to the general path, twice (the second
+    call on the merged orders, then one more observation appended)."""
+    import bench
+    from hyperopt_amd import base, hp, history as H, tpe
+    from hyperopt_amd.engine import get_engine
+    eng = get_engine()
+    assert eng.device_fit_min <= 20000
+    labels = ['x%02d' % i for i in range(40)]
+    hist = bench.soa_history(labels, 20000, 5, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+    table = bench.flat_uniform_table(labels)
+    for seed in (3, 4):
+        nat, gen, path = _both(lambda: tpe.suggest_choices(table, hist, [20000], seed, n_EI_candidates=4096))
+        assert path == (0, 1) and nat == gen, seed
+    # conditional tree, log-family device label, appended documents (Trials cache)
+    space = {'m': hp.choice('m', [{'a': hp.loguniform('a', -3, 2)}, {'b': hp.uniform('b', 0, 1)}]),
+             'u': hp.uniform('u', -2, 2)}
+    domain = base.Domain(lambda d: 0.0, space)
+    trials = base.Trials()
+    rs = np.random.RandomState(8)
+    docs = []
+    for tid in range(36000):
+        m = int(rs.uniform() < 0.3)
+        vals = {'m': [m], 'a': [] if m else [float(np.exp(rs.uniform(-3, 2)))], 'b': [float(rs.uniform())] if m else [],
+                'u': [float(rs.uniform(-2, 2))]}
+        idxs = {k: ([tid] if v else []) for k, v in vals.items()}
+        d = trials.new_trial_docs([tid], [None], [{'status': 'ok', 'loss': float(rs.uniform()) + 1e-9 * tid}],
+                                  [dict(tid=tid, cmd=None, workdir=None, idxs=idxs, vals=vals)])[0]
+        d['state'] = base.JOB_STATE_DONE
+        docs.append(d)
+    trials.insert_trial_docs(docs)
+    trials.refresh()
+    for step in range(2):
+        nid = 36000 + step
+        nat, gen, path = _both(lambda: doc_values(tpe.suggest([nid], domain, trials, 40 + step,
+                                                              n_EI_candidates=1 << 16)))
+        assert path is not None and nat == gen, (step, nat, gen)
+        hist = H.extract(domain, trials)
+        assert len(hist.obs['a'][0]) >= eng.device_fit_min
+        d = tpe.suggest([nid], domain, trials, 50 + step, n_EI_candidates=1024)[0]
+        d['state'] = base.JOB_STATE_DONE
+        d['result'] = {'status': 'ok', 'loss': 0.01}
+        trials.insert_trial_docs([d])
+        trials.refresh()
+
+
 def test_native_tree_takes_caller_fits_of_quantized_labels():
     """The rf branch (quantized rf_n_est / rf_depth_n): tpe_suggest_tree flags
     the quantized labels, the host fits them exactly as the general path does

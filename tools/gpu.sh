@@ -14,6 +14,7 @@
 #   hostsplit  host-side time split of the headline suggest
 #   nativesplit native fits / tpe_suggest_tree / device stages of the headline suggest
 #   hostprof   cProfile of the headline suggest on the device
+#   cfgprof    cProfile of one step of config CONFIG (default 5)
 #   pmcloop    PMC counter passes on tools/suggest_loop.py (the real suggest flow)
 #   apitrace   HIP API + kernel + copy trace of tools/suggest_loop.py -> timeline of the last suggests
 #   counters   rocprofv3 -L (the counters this box offers) -> gpurun_out/counters.txt
@@ -41,7 +42,7 @@ prof_run() {  # name counters...
   local name=$1; shift
   rm -rf $O/pmc_${TAG}/$name
   step 300 $O/pmc_${TAG}/$name.log rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
-      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-quantized ${BENCH_ARGS:-}
+      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-quantized --no-appending ${BENCH_ARGS:-}
 }
 
 for task in "$@"; do
@@ -59,7 +60,7 @@ for task in "$@"; do
     trace)
       rm -rf $O/trace_${TAG}
       step 600 $O/trace_${TAG}.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_${TAG} -o run -- \
-          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-quantized ${BENCH_ARGS:-}
+          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-quantized --no-appending ${BENCH_ARGS:-}
       python3 tools/trace_summary.py $(find $O/trace_${TAG} -name "*kernel_trace.csv") > $O/trace_${TAG}_summary.txt
       head -25 $O/trace_${TAG}_summary.txt ;;
     pmc)
@@ -79,6 +80,9 @@ for task in "$@"; do
         step 600 $O/cfg${c}_${TAG}.err python bench.py --config $c --steps ${CFG_STEPS:-5} --warmup 1
         grep '^{' $O/cfg${c}_${TAG}.err > $O/cfg${c}_${TAG}.json; cat $O/cfg${c}_${TAG}.json
       done ;;
+    cfgprof)
+      step 600 $O/cfgprof${CONFIG:-5}_${TAG}.txt python tools/config_prof.py ${CONFIG:-5} --steps ${STEPS:-5}
+      head -45 $O/cfgprof${CONFIG:-5}_${TAG}.txt ;;
     hostprof)
       step 300 $O/hostprof_${TAG}.txt python tools/host_prof.py ${STEPS:-300}
       head -60 $O/hostprof_${TAG}.txt ;;

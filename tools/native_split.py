@@ -36,7 +36,7 @@ def main():
     hist = H.extract(domain, trials)
     table = domain.table
     below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
-    arr, keep = tpe._tree_labels(table, hist)
+    arr, keep, _ = tpe._tree_labels(table, hist)
     tot_fit = 0.0
     for lab in ('model', 'svm_kernel', 'svm_C', 'svm_rbf_gamma'):
         r = arr[table.by_label[lab].index]

@@ -9,7 +9,8 @@ from collections import defaultdict
 
 def short(name):
     for k in ('k_above_f32', 'k_above_f64', 'k_above_q', 'k_sample_tab', 'k_sample', 'k_tables', 'k_finalize', 'k_select',
-              'k_fit_build', 'k_fit_gather', 'k_fit_sort_lds'):
+              'k_fit_stats', 'k_fit_emit', 'k_fit_combine', 'k_fit_wide', 'k_ord_chunks', 'k_ord_merge', 'k_ord_below',
+              'k_ord_compact', 'k_upload'):
         if k in name:
             return k
     return 'rocprim' if 'rocprim' in name else name[:40]
@@ -44,6 +45,11 @@ def main(root):
     for t in traffic.values():
         t['correction'] = 'FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM)'
     out['traffic'] = traffic
+    # the build these counters belong to (bench.py flags a summary of another build as stale)
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'hyperopt_amd', 'libtpe_hip.so')
+    if os.path.exists(lib):
+        out['lib_sha256'] = hashlib.sha256(open(lib, 'rb').read()).hexdigest()
     print(json.dumps(out, indent=1, sort_keys=True))
 
 
