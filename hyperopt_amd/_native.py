@@ -11,11 +11,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 14
+ABI_VERSION = 15
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE = 1, 2, 4, 8, 16
+F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT = 1, 2, 4, 8, 16, 32
 TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
 TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
@@ -146,6 +146,7 @@ class PackInfo(ctypes.Structure):
         ('tab_units', ctypes.c_int64),
         ('off_samp_tiles', ctypes.c_int64), ('n_samp_tiles', ctypes.c_int64), ('n_samp_eager', ctypes.c_int64),
         ('off_tab_tiles', ctypes.c_int64), ('n_tab_tiles', ctypes.c_int64),
+        ('off_expand', ctypes.c_int64), ('n_expand', ctypes.c_int64), ('copy_start', ctypes.c_int64),
     ]
 
 
@@ -228,7 +229,8 @@ EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_si
            'tpe_sample', 'tpe_sort', 'tpe_score_above', 'tpe_finalize', 'tpe_select', 'tpe_host_fit_parzen', 'tpe_host_fit_split',
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
            'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read',
-           'tpe_suggest_tree', 'tpe_comm_unique_id', 'tpe_comm_init', 'tpe_comm_destroy', 'tpe_combine_results')
+           'tpe_suggest_tree', 'tpe_comm_unique_id', 'tpe_comm_init', 'tpe_comm_destroy', 'tpe_combine_results',
+           'tpe_host_threads')
 
 # tpe_level_run stages (tpe_level_profile_read order)
 STAGES = ('fit', 'k_tables', 'k_sample', 'sort', 'above', 'k_finalize', 'k_select')
@@ -316,6 +318,8 @@ def load(path=LIB_PATH):
     lib.tpe_comm_destroy.restype = ctypes.c_int
     lib.tpe_combine_results.argtypes = [P, I32, I64, P]
     lib.tpe_combine_results.restype = ctypes.c_int
+    lib.tpe_host_threads.argtypes = [I32, ctypes.POINTER(I32)]
+    lib.tpe_host_threads.restype = ctypes.c_int
     lib.tpe_level_profile.argtypes = [ctypes.c_int32]
     lib.tpe_level_profile.restype = ctypes.c_int
     lib.tpe_level_profile_read.argtypes = [ctypes.POINTER(StageProf), ctypes.c_int32]

@@ -7,6 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, 'csrc', 'tpe_kernels.hip')
 HOST_SRC = os.path.join(HERE, 'csrc', 'tpe_host.cpp')
 SUGGEST_SRC = os.path.join(HERE, 'csrc', 'tpe_suggest.cpp')
+POOL_SRC = os.path.join(HERE, 'csrc', 'tpe_pool.cpp')
 OUT = os.path.join(HERE, 'libtpe_hip.so')
 ARCH = os.environ.get('TPE_OFFLOAD_ARCH', 'gfx950')
 # host ISA baseline of the runtime (any x86-64 host); the vectorised pack loops
@@ -19,7 +20,8 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     semantics), link both into hyperopt_amd/libtpe_hip.so (or `out`, with extra
     -D `defines` on the kernels: A/B variants for tools/)."""
     OUT = out
-    deps = [SRC, HOST_SRC, SUGGEST_SRC, os.path.join(HERE, '..', 'include', 'tpe_hip.h')]
+    deps = [SRC, HOST_SRC, SUGGEST_SRC, POOL_SRC, os.path.join(HERE, 'csrc', 'tpe_pool.h'),
+            os.path.join(HERE, '..', 'include', 'tpe_hip.h'), os.path.abspath(__file__)]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
@@ -28,18 +30,25 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     tag = os.path.splitext(os.path.basename(OUT))[0]
     host_o = os.path.join(HERE, 'csrc', 'tpe_host.o')
     suggest_o = os.path.join(HERE, 'csrc', 'tpe_suggest.o')
+    pool_o = os.path.join(HERE, 'csrc', 'tpe_pool.o')
     dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o' if not defines else tag + '.o')
-    cmds = [
-        [gxx, '-O3', '-march=' + HOST_MARCH, '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
-         '-fno-trapping-math', '-Wall',
-         '-c', HOST_SRC, '-o', host_o],
-        [gxx, '-O3', '-march=' + HOST_MARCH, '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
-         '-fno-trapping-math', '-Wall', '-c', SUGGEST_SRC, '-o', suggest_o],
-        [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
-         '-Wno-unused-command-line-argument'] + ['-D' + d for d in defines] + ['-c', SRC, '-o', dev_o],
-        [hipcc, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-Wno-unused-command-line-argument', '-o', tmp,
-         dev_o, host_o, suggest_o],
+    hdr = [os.path.join(HERE, '..', 'include', 'tpe_hip.h'), os.path.join(HERE, 'csrc', 'tpe_pool.h')]
+    host_flags = [gxx, '-O3', '-march=' + HOST_MARCH, '-std=c++17', '-fPIC', '-Wall']
+    numpy_fp = ['-ffp-contract=off', '-fno-fast-math', '-fno-trapping-math']
+    # (object, its sources, compile command): an object is rebuilt when a source
+    # is newer than it (force: always)
+    objs = [
+        (host_o, [HOST_SRC] + hdr, host_flags + numpy_fp + ['-c', HOST_SRC, '-o', host_o]),
+        (suggest_o, [SUGGEST_SRC] + hdr, host_flags + numpy_fp + ['-c', SUGGEST_SRC, '-o', suggest_o]),
+        (pool_o, [POOL_SRC] + hdr, host_flags + ['-pthread', '-c', POOL_SRC, '-o', pool_o]),
+        (dev_o, [SRC] + hdr, [hipcc, '-O3', '--offload-arch=' + ARCH, '-std=c++17', '-fPIC', '-Wall',
+                              '-Wno-unused-command-line-argument'] + ['-D' + d for d in defines] +
+         ['-c', SRC, '-o', dev_o]),
     ]
+    cmds = [c for o, srcs, c in objs
+            if force or not os.path.exists(o) or any(os.path.getmtime(s) > os.path.getmtime(o) for s in srcs)]
+    cmds.append([hipcc, '-shared', '-fPIC', '--offload-arch=' + ARCH, '-Wno-unused-command-line-argument', '-o', tmp,
+                 dev_o, host_o, suggest_o, pool_o, '-pthread'])
     for cmd in cmds:
         if verbose:
             print(' '.join(cmd))

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/tpe_hip.h"
+#include "tpe_pool.h"
 
 namespace {
 
@@ -59,6 +60,13 @@ constexpr int64_t kTabMaxCells = 65536;           // per side; more: per-candida
 constexpr int64_t kTabRowUnits = 3;               // 16-B units of a cell row (include/tpe_hip.h)
 constexpr double kTabMinRatio = 8.0, kTabMinRatioDevFit = 64.0;   // candidates per cell row for tables
 constexpr int64_t kTabMaxLattice = 1 << 18;       // lattice values per quantized label
+// expanded levels (include/tpe_hip.h): from this many problems the device
+// writes the problems and tiles itself; TPE_EXPAND=0 turns it off (A/B, tests)
+constexpr int64_t kExpandMinProblems = 256;
+bool expand_enabled() {
+  const char* e = getenv("TPE_EXPAND");
+  return !(e && e[0] == '0');
+}
 // TPE_TABLES=0 turns tabulated scoring off (A/B and tests); read per call
 bool tables_enabled() {
   const char* e = getenv("TPE_TABLES");
@@ -112,29 +120,6 @@ double np_sum(const double* a, int64_t n) {
 // np.maximum / np.minimum propagate NaN
 inline double np_max(double a, double b) { return (a != a || b != b) ? NAN : (a > b ? a : b); }
 inline double np_min(double a, double b) { return (a != a || b != b) ? NAN : (a < b ? a : b); }
-
-// linear_forgetting_weights (tpe.py:381-394) via np.linspace semantics
-void lf_weights(int64_t n, int lf, double* out) {
-  if (n <= 0) return;
-  if (n < lf) {
-    for (int64_t i = 0; i < n; ++i) out[i] = 1.0;
-    return;
-  }
-  const int64_t num = n - lf;
-  const double start = 1.0 / (double)n, stop = 1.0;
-  if (num == 1) {
-    out[0] = start;
-  } else if (num > 1) {
-    const double step = (stop - start) / (double)(num - 1);
-    for (int64_t i = 0; i < num; ++i) {
-      double y = (double)i * step;
-      y += start;
-      out[i] = y;
-    }
-    out[num - 1] = stop;
-  }
-  for (int64_t i = num; i < n; ++i) out[i] = 1.0;
-}
 
 // erf(z) bit for bit: libm's erf is exactly +-1 from |z| = 6 on (erfc(6) < 2^-55),
 // so the (common) far-from-the-bound components skip the call
@@ -282,6 +267,9 @@ struct PackScratch {
   std::vector<tpe_tile> tiles;
   std::vector<tpe_work> work;
   std::vector<tpe_tab_job> tab_jobs;
+  std::vector<tpe_problem> xtmpl;       // expanded levels: one problem template per label
+  std::vector<int32_t> xfirst;          // ... each label's first problem (n_labels + 1)
+  std::vector<uint32_t> xctr;           // ... each problem's new id (Philox counter word 3)
 };
 
 // value range of a label's kernel coordinate (x, or ln x for log families)
@@ -294,6 +282,282 @@ void coord_range(const tpe_label_in& L, double& klo, double& khi) {
   for (int64_t i = 0; i < L.below_k; ++i) {
     klo = std::min(klo, L.below_mu[i] - 8 * L.below_sigma[i]);
     khi = std::max(khi, L.below_mu[i] + 8 * L.below_sigma[i]);
+  }
+}
+
+// one label's sections of tpe_host_pack_level (sampler rows, component rows,
+// wide rows, pruning grid) at the offsets the packer assigned; labels are
+// independent, so the packer runs this on its worker threads.  (A function of
+// its own so that it carries the AVX-512 / AVX2 clones: a lambda would not.)
+struct LabelSec { int64_t samp, c64[2], c32[2], wide, grid; };
+struct FillCtx {
+  const tpe_label_in* labels;
+  const LabelSec* sec;
+  tpe_problem* lab;
+  double* samp;
+  double* comp64;
+  float* comp32;
+  int32_t* grid;
+  const char* dev_fit;
+  const int32_t* tmode;
+  int key_bits;
+  bool f64;
+};
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+void fill_label(const FillCtx& cx, int32_t li) {
+  const tpe_label_in* labels = cx.labels;
+  const bool f64 = cx.f64;
+  const int key_bits = cx.key_bits;
+  const char* dev_fit = cx.dev_fit;
+  const int32_t* tmode = cx.tmode;
+  const tpe_label_in& L = labels[li];
+  const LabelSec& sc = cx.sec[li];
+  tpe_problem& p = cx.lab[li];
+  memset(&p, 0, sizeof(p));
+  p.family = L.family; p.flags = L.flags; p.n_upper = L.upper;
+  p.low = L.low; p.high = L.high; p.q = L.q;
+  const bool bounded = (L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) != 0;
+  // ---- sampler rows (below mixture) ----
+  p.samp_off = (int32_t)sc.samp;
+  double* srow = cx.samp + 8 * (size_t)sc.samp;
+  if (L.family == TPE_FAM_CATEGORICAL) {
+    const int64_t k = L.below_k;
+    double acc = 0;
+    std::vector<double> cum((size_t)k);
+    for (int64_t i = 0; i < k; ++i) { acc += L.below_w[i]; cum[i] = acc; }
+    for (int64_t i = 0; i < k; ++i) {
+      const double row[8] = {i == k - 1 ? 1.0 : cum[i] / acc, 0, 0, 0, 0, 0, 0, 0};
+      memcpy(srow + 8 * i, row, sizeof(row));
+    }
+    p.samp_len = (int32_t)k;
+    // lazy scoring (TPE_F_CAT_LAZY): the winner is the best-scoring drawable
+    // category (np.argmax order: NaN first, then value, then index)
+    if (k <= 64 && L.above_k == k) {
+      const double* row0 = srow;
+      int64_t c1 = -1;
+      double s1 = 0, p1 = 0;
+      for (int64_t i = 0; i < k; ++i) {
+        const double lo = i ? row0[8 * (i - 1)] : 0.0, pi = row0[8 * i] - lo;
+        if (!(pi > 0)) continue;
+        const double sc1 = log(L.below_w[i]) - log(L.above_w[i]);
+        const bool win = c1 < 0 || (sc1 != sc1 ? s1 == s1 : sc1 > s1);
+        if (win) { c1 = i; s1 = sc1; p1 = pi; }
+      }
+      if (c1 >= 0 && p1 >= 1.0 / 65536) p.flags |= TPE_F_CAT_LAZY;
+    }
+  } else {
+    const int64_t k = L.below_k;
+    std::vector<double> sel((size_t)k), fa((size_t)k), fb((size_t)k), flip((size_t)k);
+    double tot = 0;
+    bool any = false;
+    for (int64_t i = 0; i < k; ++i) {
+      double za = -INFINITY, zb = INFINITY;
+      if (bounded) { za = (L.low - L.below_mu[i]) / L.below_sigma[i]; zb = (L.high - L.below_mu[i]) / L.below_sigma[i]; }
+      const bool fl = za > 0;
+      const double a = fl ? -zb : za, b = fl ? -za : zb;
+      fa[i] = 0.5 * erfc(-a / sqrt(2.0));
+      fb[i] = 0.5 * erfc(-b / sqrt(2.0));
+      flip[i] = fl ? 1.0 : 0.0;
+      sel[i] = bounded ? L.below_w[i] * std::max(fb[i] - fa[i], 0.0) : L.below_w[i];
+      any = any || sel[i] > 0;
+    }
+    if (!any) for (int64_t i = 0; i < k; ++i) sel[i] = L.below_w[i];
+    for (int64_t i = 0; i < k; ++i) tot += sel[i];
+    double acc = 0;
+    for (int64_t i = 0; i < k; ++i) {
+      acc += sel[i];
+      const double row[8] = {i == k - 1 ? 1.0 : acc / tot, L.below_mu[i], L.below_sigma[i], fa[i], fb[i], flip[i], 0, 0};
+      memcpy(srow + 8 * i, row, sizeof(row));
+    }
+    p.samp_len = (int32_t)k;
+  }
+  // ---- sort-key range of the kernel coordinate ----
+  double klo, khi;
+  coord_range(L, klo, khi);
+  p.key_lo = (float)klo;
+  p.key_inv = khi > klo ? (float)((double)(1 << key_bits) / (khi - klo)) : 0.f;
+  // ---- component rows ----
+  for (int side = 0; side < 2 - dev_fit[li]; ++side) {
+    const double* w = side ? L.above_w : L.below_w;
+    const double* mu = side ? L.above_mu : L.below_mu;
+    const double* sg = side ? L.above_sigma : L.below_sigma;
+    const int64_t k = side ? L.above_k : L.below_k;
+    int32_t& off = side ? p.above_off : p.below_off;
+    int32_t& len = side ? p.above_len : p.below_len;
+    double& base = side ? p.above_base : p.below_base;
+    if (L.family == TPE_FAM_CATEGORICAL) {
+      off = (int32_t)sc.c64[side]; len = (int32_t)k; base = 0;
+      double* r = cx.comp64 + 4 * (size_t)off;
+      for (int64_t i = 0; i < k; ++i) {
+        const double row[4] = {log(w[i]), w[i], 0, 0};
+        memcpy(r + 4 * i, row, sizeof(row));
+      }
+    } else if (L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) {
+      off = (int32_t)sc.c64[side]; len = (int32_t)k;
+      base = -log(p_accept(w, mu, sg, k, bounded, L.low, L.high));
+      double* r = cx.comp64 + 4 * (size_t)off;
+      for (int64_t i = 0; i < k; ++i) {
+        const double row[4] = {mu[i], np_max(sqrt(2.0) * sg[i], kEPS), w[i], 0};
+        memcpy(r + 4 * i, row, sizeof(row));
+      }
+    } else {
+      const bool logf = L.family == TPE_FAM_LOGGAUSS;
+      std::vector<double> a((size_t)k), c((size_t)k);
+      const double pa = logf ? 1.0 : p_accept(w, mu, sg, k, bounded, L.low, L.high);
+      double shift = -INFINITY;
+      if (f64) {
+        for (int64_t i = 0; i < k; ++i) {
+          const double se = np_max(sg[i], kEPS);
+          const double arg = logf ? w[i] / (se * sqrt(2 * M_PI)) : w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa;
+          c[i] = log(arg) * kLog2e;
+          a[i] = sqrt(0.5 * kLog2e) / se;
+        }
+      } else {
+        // f32 tables: straight-line passes the compiler vectorises, the bit-level
+        // log2 for normal positive arguments, libm for the rest
+        double* __restrict__ cp = c.data();
+        double* __restrict__ ap = a.data();
+        const double s2pi = sqrt(2 * M_PI), as = sqrt(0.5 * kLog2e), ipa = 1.0 / pa;
+        // one division per component: 1 / max(sigma, EPS) (the rows are f32; the
+        // ratio's double rounding differs from w / (sigma sqrt(2 pi)) by an ulp)
+        {
+          const double cst = logf ? 1.0 / s2pi : ipa / s2pi;
+          int tiny = 0;
+          for (int64_t i = 0; i < k; ++i) {
+            const double se = sg[i] > kEPS ? sg[i] : kEPS;
+            const double inv = 1.0 / se;
+            tiny |= !(sg[i] > kEPS);
+            cp[i] = w[i] * inv * cst;
+            ap[i] = as * inv;
+          }
+          if (tiny && !logf)       // |sigma| < EPS: the reference divides by |sigma| itself
+            for (int64_t i = 0; i < k; ++i)
+              if (!(sg[i] > kEPS)) cp[i] = w[i] / (s2pi * fabs(sg[i])) * ipa;
+        }
+        // normal positive ratios (the rule): one branch-free pass; libm for the rest
+        int odd = 0;
+        for (int64_t i = 0; i < k; ++i) {
+          const double r = cp[i];
+          odd |= !((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308));
+          cp[i] = log2_normal(r > 0 ? r : 1.0);
+        }
+        if (odd)
+          for (int64_t i = 0; i < k; ++i) {
+            const double r = w[i] / (logf ? ((sg[i] > kEPS ? sg[i] : kEPS) * s2pi) : (s2pi * fabs(sg[i]))) *
+                             (logf ? 1.0 : ipa);
+            if (!((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308))) cp[i] = log2(r);
+          }
+      }
+      {
+        // the largest finite c (four chains: vectorisable)
+        double m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        const double* __restrict__ cc = c.data();
+        int64_t i = 0;
+        for (; i + 4 <= k; i += 4)
+          for (int j = 0; j < 4; ++j) {
+            const double v = (cc[i + j] > -INFINITY) & (cc[i + j] < INFINITY) ? cc[i + j] : -INFINITY;
+            m4[j] = v > m4[j] ? v : m4[j];
+          }
+        for (; i < k; ++i) {
+          const double v = (cc[i] > -INFINITY) & (cc[i] < INFINITY) ? cc[i] : -INFINITY;
+          m4[0] = v > m4[0] ? v : m4[0];
+        }
+        shift = std::max(std::max(m4[0], m4[1]), std::max(m4[2], m4[3]));
+      }
+      if (!std::isfinite(shift)) shift = 0;
+      for (int64_t i = 0; i < k; ++i) c[i] -= shift;
+      base = shift * kLn2;
+      if (f64) {
+        off = (int32_t)sc.c64[side]; len = (int32_t)k;
+        double* r = cx.comp64 + 4 * (size_t)off;
+        for (int64_t i = 0; i < k; ++i) {
+          const double row[4] = {mu[i], a[i], c[i], 0};
+          memcpy(r + 4 * i, row, sizeof(row));
+        }
+        continue;
+      }
+      // pruning (above side, f32, scored per candidate): widest components
+      // listed apart, grid over mu.  A tabulated label's cells sum every
+      // component (k_tables), so it has neither.
+      std::vector<int64_t> wide;
+      if (side == 1 && k > kPruneMinK && tmode[li] == TPE_TAB_NONE) {
+        // the kPruneWide smallest a (widest sigma), ascending by (a, index): one
+        // pass with a small insertion-sorted buffer (= a stable argsort prefix)
+        int64_t best[kPruneWide];
+        int nb = 0;
+        for (int64_t i = 0; i < k; ++i) {
+          if (nb == kPruneWide && !(a[i] < a[best[nb - 1]])) continue;   // ties keep the lower index
+          int q = nb < kPruneWide ? nb++ : nb - 1;
+          while (q > 0 && a[i] < a[best[q - 1]]) { best[q] = best[q - 1]; --q; }
+          best[q] = i;
+        }
+        wide.assign(best, best + nb);
+      }
+      off = (int32_t)sc.c32[side]; len = (int32_t)k;
+      {
+        const size_t b0 = 4 * (size_t)sc.c32[side];
+        float* r = cx.comp32 + b0;
+        for (int64_t i = 0; i < k; ++i, r += 4) {
+          const float hi = (float)mu[i];
+          r[0] = hi; r[1] = (float)(mu[i] - (double)hi); r[2] = (float)a[i]; r[3] = (float)c[i];
+        }
+        for (int64_t i : wide) cx.comp32[b0 + 4 * (size_t)i + 3] = -INFINITY;
+      }
+      std::vector<char> is_wide((size_t)k, 0);
+      for (int64_t i : wide) is_wide[i] = 1;
+      if (!wide.empty()) {
+        p.wide_off = (int32_t)sc.wide;
+        p.wide_len = (int32_t)wide.size();
+        float* wr = cx.comp32 + 4 * (size_t)sc.wide;
+        for (int64_t i : wide) {
+          const float hi = (float)mu[i];
+          const float row[4] = {hi, (float)(mu[i] - (double)hi), (float)a[i], (float)c[i]};
+          memcpy(wr, row, sizeof(row));
+          wr += 4;
+        }
+        const int64_t anchor = wide[0];
+        double cmax = -INFINITY, amin = INFINITY;
+        for (int64_t i = 0; i < k; ++i)
+          if (!is_wide[i]) { cmax = std::max(cmax, c[i]); amin = std::min(amin, a[i]); }
+        p.prior_mu = (float)mu[anchor]; p.prior_a = (float)a[anchor]; p.prior_c = (float)c[anchor];
+        p.narrow_cmax = (float)cmax; p.narrow_amin = (float)amin;
+        const double lo = (double)(float)mu[0], hi = (double)(float)mu[k - 1];
+        const int64_t G = std::min<int64_t>(4096, 4 * k);
+        const float inv = hi > lo ? (float)((double)G / (hi - lo)) : 0.f;
+        p.grid_off = (int32_t)sc.grid; p.grid_n = (int32_t)G;
+        p.grid_lo = (float)lo; p.grid_inv = inv;
+        // grid[g] = first component with mu32 >= edge_g, edge_g = lo + g * (1 / inv)
+        // = #components whose first bucket with edge > mu32 is <= g: a counting
+        // pass (bucket estimate + exact edge correction) and a prefix sum —
+        // no data-dependent branches in the merge
+        const double step = inv > 0 ? 1.0 / (double)inv : 0.0;
+        const size_t g0 = (size_t)sc.grid;
+        int32_t* __restrict__ gp = cx.grid + g0;
+        if (!(inv > 0)) memset(gp, 0, (size_t)G * sizeof(int32_t));
+        if (inv > 0) {
+          // four interleaved histograms: sorted mu puts neighbours in the same
+          // bucket, and one array would chain every increment through memory
+          const size_t H = (size_t)G + 1;
+          std::vector<int32_t> hist(4 * H, 0);
+          const double dinv = (double)inv;
+          for (int64_t i = 0; i < k; ++i) {
+            const double x = (double)(float)mu[i];
+            int64_t g = (int64_t)((x - lo) * dinv) + 1;     // first bucket with edge > x, estimated
+            g = g < 0 ? 0 : (g > G ? G : g);
+            while (g > 0 && lo + (double)(g - 1) * step > x) --g;
+            while (g < G && !(lo + (double)g * step > x)) ++g;
+            ++hist[(size_t)(i & 3) * H + (size_t)g];
+          }
+          int32_t acc = 0;
+          for (int64_t g = 0; g < G; ++g) {
+            acc += hist[(size_t)g] + hist[H + (size_t)g] + hist[2 * H + (size_t)g] + hist[3 * H + (size_t)g];
+            gp[g] = acc;
+          }
+        }
+        gp[G] = (int32_t)k;
+      }
+    }
   }
 }
 
@@ -471,9 +735,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   auto& comp64 = ps.comp64;     // double4 rows
   auto& samp = ps.samp;         // 8 doubles per row
   auto& grid = ps.grid;
-  comp32.clear(); comp64.clear(); samp.clear(); grid.clear();
   std::vector<tpe_problem> lab((size_t)n_labels);
-  int64_t P = 0, ktot = 0;
+  int64_t P = 0;
   std::vector<char> dev_fit((size_t)n_labels, 0);   // above mixture fitted on the device
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
@@ -486,14 +749,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           (L.n_ord_in < L.n_obs && (!L.ord_key_out || !L.ord_idx_out)))
         return TPE_E_ARG;
       dev_fit[li] = 1;
-      ktot += L.below_k + kPruneWide;
-    } else {
-      ktot += L.below_k + L.above_k + kPruneWide;
     }
   }
-  comp32.reserve((size_t)(4 * ktot));
-  comp64.reserve((size_t)(4 * ktot));
-  samp.reserve((size_t)(8 * ktot));
   // ---- tabulated scoring: which labels score from tables, and their geometry ----
   const bool tab_on = tables_enabled();
   std::vector<int32_t> tmode((size_t)n_labels, TPE_TAB_NONE);
@@ -571,249 +828,48 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   int key_bits = std::max(5, 8 - pbits);
   if (max_slot_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(fine_key_bits(), 16 - pbits));
   const int sort_end_bit = S > 0 && key_bits + pbits <= 32 ? key_bits + pbits : 0;
+  // ---- per-label sections: every label's sampler rows, component rows, wide
+  // rows and pruning grid get their offsets first (label order, as appended
+  // one after another), then each label fills its own sections — on the host
+  // worker threads when the level has enough components (labels independent) ----
+  std::vector<LabelSec> sec((size_t)n_labels);
+  int64_t n_samp = 0, n_c64 = 0, n_c32 = 0, n_grid = 0, work_k = 0;
   for (int32_t li = 0; li < n_labels; ++li) {
     const tpe_label_in& L = labels[li];
-    tpe_problem& p = lab[li];
-    memset(&p, 0, sizeof(p));
-    p.family = L.family; p.flags = L.flags; p.n_upper = L.upper;
-    p.low = L.low; p.high = L.high; p.q = L.q;
-    const bool bounded = (L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) != 0;
-    // ---- sampler rows (below mixture) ----
-    p.samp_off = (int32_t)(samp.size() / 8);
-    if (L.family == TPE_FAM_CATEGORICAL) {
-      const int64_t k = L.below_k;
-      double acc = 0;
-      std::vector<double> cum((size_t)k);
-      for (int64_t i = 0; i < k; ++i) { acc += L.below_w[i]; cum[i] = acc; }
-      for (int64_t i = 0; i < k; ++i) {
-        double row[8] = {i == k - 1 ? 1.0 : cum[i] / acc, 0, 0, 0, 0, 0, 0, 0};
-        samp.insert(samp.end(), row, row + 8);
-      }
-      p.samp_len = (int32_t)k;
-      // lazy scoring (TPE_F_CAT_LAZY): the winner is the best-scoring drawable
-      // category (np.argmax order: NaN first, then value, then index)
-      if (k <= 64 && L.above_k == k) {
-        const double* row0 = samp.data() + 8 * (size_t)p.samp_off;
-        int64_t c1 = -1;
-        double s1 = 0, p1 = 0;
-        for (int64_t i = 0; i < k; ++i) {
-          const double lo = i ? row0[8 * (i - 1)] : 0.0, pi = row0[8 * i] - lo;
-          if (!(pi > 0)) continue;
-          const double sc = log(L.below_w[i]) - log(L.above_w[i]);
-          const bool win = c1 < 0 || (sc != sc ? s1 == s1 : sc > s1);
-          if (win) { c1 = i; s1 = sc; p1 = pi; }
-        }
-        if (c1 >= 0 && p1 >= 1.0 / 65536) p.flags |= TPE_F_CAT_LAZY;
-      }
-    } else {
-      const int64_t k = L.below_k;
-      std::vector<double> sel((size_t)k), fa((size_t)k), fb((size_t)k), flip((size_t)k);
-      double tot = 0;
-      bool any = false;
-      for (int64_t i = 0; i < k; ++i) {
-        double za = -INFINITY, zb = INFINITY;
-        if (bounded) { za = (L.low - L.below_mu[i]) / L.below_sigma[i]; zb = (L.high - L.below_mu[i]) / L.below_sigma[i]; }
-        const bool fl = za > 0;
-        const double a = fl ? -zb : za, b = fl ? -za : zb;
-        fa[i] = 0.5 * erfc(-a / sqrt(2.0));
-        fb[i] = 0.5 * erfc(-b / sqrt(2.0));
-        flip[i] = fl ? 1.0 : 0.0;
-        sel[i] = bounded ? L.below_w[i] * std::max(fb[i] - fa[i], 0.0) : L.below_w[i];
-        any = any || sel[i] > 0;
-      }
-      if (!any) for (int64_t i = 0; i < k; ++i) sel[i] = L.below_w[i];
-      for (int64_t i = 0; i < k; ++i) tot += sel[i];
-      double acc = 0;
-      for (int64_t i = 0; i < k; ++i) {
-        acc += sel[i];
-        double row[8] = {i == k - 1 ? 1.0 : acc / tot, L.below_mu[i], L.below_sigma[i], fa[i], fb[i], flip[i], 0, 0};
-        samp.insert(samp.end(), row, row + 8);
-      }
-      p.samp_len = (int32_t)k;
-    }
-    // ---- sort-key range of the kernel coordinate ----
-    double klo, khi;
-    coord_range(L, klo, khi);
-    p.key_lo = (float)klo;
-    p.key_inv = khi > klo ? (float)((double)(1 << key_bits) / (khi - klo)) : 0.f;
-    // ---- component rows ----
+    LabelSec& q = sec[(size_t)li];
+    q.samp = n_samp; n_samp += L.below_k;
+    q.c64[0] = q.c64[1] = q.c32[0] = q.c32[1] = q.wide = q.grid = -1;
+    const bool rows64 = L.family == TPE_FAM_CATEGORICAL || L.family == TPE_FAM_QGAUSS ||
+                        L.family == TPE_FAM_QLOGGAUSS || f64;
     for (int side = 0; side < 2 - dev_fit[li]; ++side) {
-      const double* w = side ? L.above_w : L.below_w;
-      const double* mu = side ? L.above_mu : L.below_mu;
-      const double* sg = side ? L.above_sigma : L.below_sigma;
       const int64_t k = side ? L.above_k : L.below_k;
-      int32_t& off = side ? p.above_off : p.below_off;
-      int32_t& len = side ? p.above_len : p.below_len;
-      double& base = side ? p.above_base : p.below_base;
-      if (L.family == TPE_FAM_CATEGORICAL) {
-        off = (int32_t)(comp64.size() / 4); len = (int32_t)k; base = 0;
-        for (int64_t i = 0; i < k; ++i) {
-          const double row[4] = {log(w[i]), w[i], 0, 0};
-          comp64.insert(comp64.end(), row, row + 4);
-        }
-      } else if (L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) {
-        off = (int32_t)(comp64.size() / 4); len = (int32_t)k;
-        base = -log(p_accept(w, mu, sg, k, bounded, L.low, L.high));
-        for (int64_t i = 0; i < k; ++i) {
-          const double row[4] = {mu[i], np_max(sqrt(2.0) * sg[i], kEPS), w[i], 0};
-          comp64.insert(comp64.end(), row, row + 4);
-        }
-      } else {
-        const bool logf = L.family == TPE_FAM_LOGGAUSS;
-        std::vector<double> a((size_t)k), c((size_t)k);
-        const double pa = logf ? 1.0 : p_accept(w, mu, sg, k, bounded, L.low, L.high);
-        double shift = -INFINITY;
-        if (f64) {
-          for (int64_t i = 0; i < k; ++i) {
-            const double se = np_max(sg[i], kEPS);
-            const double arg = logf ? w[i] / (se * sqrt(2 * M_PI)) : w[i] / sqrt(2 * M_PI * sg[i] * sg[i]) / pa;
-            c[i] = log(arg) * kLog2e;
-            a[i] = sqrt(0.5 * kLog2e) / se;
-          }
-        } else {
-          // f32 tables: straight-line passes the compiler vectorises, the bit-level
-          // log2 for normal positive arguments, libm for the rest
-          double* __restrict__ cp = c.data();
-          double* __restrict__ ap = a.data();
-          const double s2pi = sqrt(2 * M_PI), as = sqrt(0.5 * kLog2e), ipa = 1.0 / pa;
-          if (logf)
-            for (int64_t i = 0; i < k; ++i) {
-              const double se = sg[i] > kEPS ? sg[i] : kEPS;
-              cp[i] = w[i] / (se * s2pi);
-              ap[i] = as / se;
-            }
-          else
-            for (int64_t i = 0; i < k; ++i) {
-              const double se = sg[i] > kEPS ? sg[i] : kEPS;
-              cp[i] = w[i] / (s2pi * fabs(sg[i])) * ipa;
-              ap[i] = as / se;
-            }
-          // normal positive ratios (the rule): one branch-free pass; libm for the rest
-          int odd = 0;
-          for (int64_t i = 0; i < k; ++i) {
-            const double r = cp[i];
-            odd |= !((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308));
-            cp[i] = log2_normal(r > 0 ? r : 1.0);
-          }
-          if (odd)
-            for (int64_t i = 0; i < k; ++i) {
-              const double r = w[i] / (logf ? ((sg[i] > kEPS ? sg[i] : kEPS) * s2pi) : (s2pi * fabs(sg[i]))) *
-                               (logf ? 1.0 : ipa);
-              if (!((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308))) cp[i] = log2(r);
-            }
-        }
-        {
-          // the largest finite c (four chains: vectorisable)
-          double m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-          const double* __restrict__ cc = c.data();
-          int64_t i = 0;
-          for (; i + 4 <= k; i += 4)
-            for (int j = 0; j < 4; ++j) {
-              const double v = (cc[i + j] > -INFINITY) & (cc[i + j] < INFINITY) ? cc[i + j] : -INFINITY;
-              m4[j] = v > m4[j] ? v : m4[j];
-            }
-          for (; i < k; ++i) {
-            const double v = (cc[i] > -INFINITY) & (cc[i] < INFINITY) ? cc[i] : -INFINITY;
-            m4[0] = v > m4[0] ? v : m4[0];
-          }
-          shift = std::max(std::max(m4[0], m4[1]), std::max(m4[2], m4[3]));
-        }
-        if (!std::isfinite(shift)) shift = 0;
-        for (int64_t i = 0; i < k; ++i) c[i] -= shift;
-        base = shift * kLn2;
-        if (f64) {
-          off = (int32_t)(comp64.size() / 4); len = (int32_t)k;
-          for (int64_t i = 0; i < k; ++i) {
-            const double row[4] = {mu[i], a[i], c[i], 0};
-            comp64.insert(comp64.end(), row, row + 4);
-          }
-          continue;
-        }
-        // pruning (above side, f32, scored per candidate): widest components
-        // listed apart, grid over mu.  A tabulated label's cells sum every
-        // component (k_tables), so it has neither.
-        std::vector<int64_t> wide;
-        if (side == 1 && k > kPruneMinK && tmode[li] == TPE_TAB_NONE) {
-          // the kPruneWide smallest a (widest sigma), ascending by (a, index): one
-          // pass with a small insertion-sorted buffer (= a stable argsort prefix)
-          int64_t best[kPruneWide];
-          int nb = 0;
-          for (int64_t i = 0; i < k; ++i) {
-            if (nb == kPruneWide && !(a[i] < a[best[nb - 1]])) continue;   // ties keep the lower index
-            int q = nb < kPruneWide ? nb++ : nb - 1;
-            while (q > 0 && a[i] < a[best[q - 1]]) { best[q] = best[q - 1]; --q; }
-            best[q] = i;
-          }
-          wide.assign(best, best + nb);
-        }
-        off = (int32_t)(comp32.size() / 4); len = (int32_t)k;
-        {
-          const size_t b0 = comp32.size();
-          comp32.resize(b0 + 4 * (size_t)k);
-          float* r = comp32.data() + b0;
-          for (int64_t i = 0; i < k; ++i, r += 4) {
-            const float hi = (float)mu[i];
-            r[0] = hi; r[1] = (float)(mu[i] - (double)hi); r[2] = (float)a[i]; r[3] = (float)c[i];
-          }
-          for (int64_t i : wide) comp32[b0 + 4 * (size_t)i + 3] = -INFINITY;
-        }
-        std::vector<char> is_wide((size_t)k, 0);
-        for (int64_t i : wide) is_wide[i] = 1;
-        if (!wide.empty()) {
-          p.wide_off = (int32_t)(comp32.size() / 4);
-          p.wide_len = (int32_t)wide.size();
-          for (int64_t i : wide) {
-            const float hi = (float)mu[i];
-            const float row[4] = {hi, (float)(mu[i] - (double)hi), (float)a[i], (float)c[i]};
-            comp32.insert(comp32.end(), row, row + 4);
-          }
-          const int64_t anchor = wide[0];
-          double cmax = -INFINITY, amin = INFINITY;
-          for (int64_t i = 0; i < k; ++i)
-            if (!is_wide[i]) { cmax = std::max(cmax, c[i]); amin = std::min(amin, a[i]); }
-          p.prior_mu = (float)mu[anchor]; p.prior_a = (float)a[anchor]; p.prior_c = (float)c[anchor];
-          p.narrow_cmax = (float)cmax; p.narrow_amin = (float)amin;
-          const double lo = (double)(float)mu[0], hi = (double)(float)mu[k - 1];
-          const int64_t G = std::min<int64_t>(4096, 4 * k);
-          const float inv = hi > lo ? (float)((double)G / (hi - lo)) : 0.f;
-          p.grid_off = (int32_t)grid.size(); p.grid_n = (int32_t)G;
-          p.grid_lo = (float)lo; p.grid_inv = inv;
-          // grid[g] = first component with mu32 >= edge_g, edge_g = lo + g * (1 / inv)
-          // = #components whose first bucket with edge > mu32 is <= g: a counting
-          // pass (bucket estimate + exact edge correction) and a prefix sum —
-          // no data-dependent branches in the merge
-          const double step = inv > 0 ? 1.0 / (double)inv : 0.0;
-          const size_t g0 = grid.size();
-          grid.resize(g0 + (size_t)G + 1, 0);
-          int32_t* __restrict__ gp = grid.data() + g0;
-          if (inv > 0) {
-            // four interleaved histograms: sorted mu puts neighbours in the same
-            // bucket, and one array would chain every increment through memory
-            const size_t H = (size_t)G + 1;
-            std::vector<int32_t> hist(4 * H, 0);
-            const double dinv = (double)inv;
-            for (int64_t i = 0; i < k; ++i) {
-              const double x = (double)(float)mu[i];
-              int64_t g = (int64_t)((x - lo) * dinv) + 1;     // first bucket with edge > x, estimated
-              g = g < 0 ? 0 : (g > G ? G : g);
-              while (g > 0 && lo + (double)(g - 1) * step > x) --g;
-              while (g < G && !(lo + (double)g * step > x)) ++g;
-              ++hist[(size_t)(i & 3) * H + (size_t)g];
-            }
-            int32_t acc = 0;
-            for (int64_t g = 0; g < G; ++g) {
-              acc += hist[(size_t)g] + hist[H + (size_t)g] + hist[2 * H + (size_t)g] + hist[3 * H + (size_t)g];
-              gp[g] = acc;
-            }
-          }
-          gp[G] = (int32_t)k;
-        }
+      work_k += k;
+      if (rows64) { q.c64[side] = n_c64; n_c64 += k; continue; }
+      q.c32[side] = n_c32; n_c32 += k;
+      if (side == 1 && k > kPruneMinK && tmode[li] == TPE_TAB_NONE) {   // wide rows + grid (pruned)
+        q.wide = n_c32; n_c32 += std::min<int64_t>(kPruneWide, k);
+        q.grid = n_grid; n_grid += std::min<int64_t>(4096, 4 * k) + 1;
       }
     }
   }
+  // (trivially typed: a resize to the same size as the last call touches nothing)
+  comp32.resize((size_t)(4 * n_c32));
+  comp64.resize((size_t)(4 * n_c64));
+  samp.resize((size_t)(8 * n_samp));
+  grid.resize((size_t)std::max<int64_t>(n_grid, 1));
+  grid[0] = 0;
+  const FillCtx fcx{labels, sec.data(), lab.data(), samp.data(), comp64.data(), comp32.data(), grid.data(),
+                    dev_fit.data(), tmode.data(), key_bits, f64};
+  {
+    // (a few hundred components per label make a worker's hand-off worth it)
+    if (n_labels >= 2 && work_k >= 4096)
+      tpe_pool::parallel_for(n_labels, [](void* c, int i) { fill_label(*(const FillCtx*)c, (int32_t)i); },
+                             (void*)&fcx);
+    else
+      for (int32_t li = 0; li < n_labels; ++li) fill_label(fcx, li);
+  }
   // ---- device-fitted above mixtures: rows and grids after the host ones, fit jobs ----
-  if (grid.empty()) grid.push_back(0);
-  const int64_t host_rows = (int64_t)(comp32.size() / 4), host_grid = (int64_t)grid.size();
+  const int64_t host_rows = n_c32, host_grid = (int64_t)grid.size();
   std::vector<tpe_fit_job> fit;
   std::vector<int32_t> below_idx;
   std::vector<int64_t> fit_seg(1, 0);
@@ -885,10 +941,49 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // ---- problems, tiles, work ----
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
   auto& prob = ps.prob;
-  prob.resize((size_t)P);
   int64_t scored = 0;
   const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
-  {
+  // ---- expanded levels (include/tpe_hip.h "Expanded levels"): when every label
+  // of a large level scores from tables, its problems differ from their label's
+  // only in (cand_off, ctr3, tile_off) and its tiles are {problem, j * T, 0, 0}
+  // in order: the host writes one template per label and the new ids, the
+  // device (k_expand) writes the problems and tiles — ~240 B + 32 B per (label,
+  // id) neither packed nor uploaded ----
+  bool expand = expand_enabled() && !f64 && P >= kExpandMinProblems && n_tiles_p > 0;
+  for (int32_t li = 0; li < n_labels && expand; ++li)
+    if (labels[li].n_ids > 0 && tmode[li] == TPE_TAB_NONE) expand = false;
+  auto& xtmpl = ps.xtmpl;
+  auto& xfirst = ps.xfirst;
+  auto& xctr = ps.xctr;
+  xtmpl.clear(); xfirst.clear(); xctr.clear();
+  if (expand) {
+    xtmpl.resize((size_t)n_labels);
+    xfirst.resize((size_t)n_labels + 1);
+    xctr.resize((size_t)P);
+    int64_t r = 0;
+    for (int32_t li = 0; li < n_labels; ++li) {
+      tpe_problem q = lab[li];
+      q.n_cand = n_cand;
+      q.cand_off = 0;                     // k_expand: problem r's candidates at r * n_cand
+      q.sort_slot = -1;
+      q.pool_first = -1;
+      q.cand_base = cand_base;
+      q.n_cand_global = C_ref;
+      q.key0 = (uint32_t)seed; q.key1 = (uint32_t)(seed >> 32);
+      q.ctr2 = (uint32_t)labels[li].label_ix;
+      q.ctr3 = 0;                         // k_expand: the problem's new id
+      q.n_tiles = (int32_t)n_tiles_p;
+      q.tile_off = 0;                     // k_expand: r * n_tiles
+      q.n_splits = 0;                     // tabulated: no above stage
+      xtmpl[(size_t)li] = q;
+      xfirst[(size_t)li] = (int32_t)r;
+      for (int64_t j = 0; j < labels[li].n_ids; ++j) xctr[(size_t)r++] = (uint32_t)labels[li].ids[j];
+    }
+    xfirst[(size_t)n_labels] = (int32_t)r;
+  }
+  const int64_t Ph = expand ? 0 : P;      // problems (and their tiles) the host writes
+  prob.resize((size_t)Ph);
+  if (!expand) {
     int64_t r = 0, s_next = 0, u_next = n_sorted_prob * (int64_t)n_cand;
     int32_t slot = 0;
     for (int32_t li = 0; li < n_labels; ++li) {
@@ -944,10 +1039,10 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     return (int32_t)std::max<int64_t>(1, std::min(ns, cap));
   };
   auto& tiles = ps.tiles;
-  tiles.resize((size_t)(P * n_tiles_p));
+  tiles.resize((size_t)(Ph * n_tiles_p));
   {
     tpe_tile* __restrict__ tp = tiles.data();
-    for (int64_t r = 0; r < P; ++r) {
+    for (int64_t r = 0; r < Ph; ++r) {
       tpe_tile* __restrict__ row = tp + r * n_tiles_p;
       const bool none = prob[r].family == TPE_FAM_CATEGORICAL || prob[r].tab_mode != TPE_TAB_NONE;
       for (int64_t j = 0; j < n_tiles_p; ++j) {
@@ -971,7 +1066,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   const int fams[3][2] = {{TPE_FAM_GAUSS, TPE_FAM_LOGGAUSS}, {TPE_FAM_QGAUSS, -1}, {TPE_FAM_QLOGGAUSS, -1}};
   for (int gi = 0; gi < 3; ++gi) {
     const size_t before = work.size();
-    for (int64_t r = 0; r < P; ++r) {
+    for (int64_t r = 0; r < Ph; ++r) {
       const tpe_problem& q = prob[r];
       if ((q.family != fams[gi][0] && q.family != fams[gi][1]) || q.tab_mode != TPE_TAB_NONE) continue;
       for (int64_t j = 0; j < n_tiles_p; ++j) {
@@ -996,7 +1091,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // stage does)
   auto& fin_tiles = ps.fin_tiles;
   fin_tiles.clear();
-  for (int64_t r = 0; r < P; ++r) {                  // (per problem: a problem's tiles are consecutive)
+  for (int64_t r = 0; r < Ph; ++r) {                 // (per problem: a problem's tiles are consecutive)
     const tpe_problem& q = prob[r];
     if ((q.family == TPE_FAM_CATEGORICAL && q.samp_len <= TPE_SAMPLE_LDS_ROWS) || q.tab_mode != TPE_TAB_NONE) continue;
     const bool cont = !f64 && (q.family == TPE_FAM_GAUSS || q.family == TPE_FAM_LOGGAUSS);
@@ -1035,7 +1130,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   };
   int64_t n_samp_eager = 0;
   for (int pass = 0; pass < 2; ++pass)
-    for (int64_t r = 0; r < P; ++r) {
+    for (int64_t r = 0; r < Ph; ++r) {
       const tpe_problem& q = prob[r];
       if (q.tab_mode != TPE_TAB_NONE) {
         if (pass == 0) append_range(tab_tiles, r);
@@ -1045,7 +1140,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       if (lazy == (pass == 1)) append_range(samp_tiles, r);
       if (pass == 0 && !lazy) n_samp_eager += n_tiles_p;
     }
-  const int64_t n_samp_tiles = (int64_t)samp_tiles.size(), n_tab_tiles = (int64_t)tab_tiles.size();
+  // (expanded: every tile is tabulated, in order — the identity list, not stored)
+  const int64_t n_samp_tiles = (int64_t)samp_tiles.size(),
+                n_tab_tiles = expand ? P * n_tiles_p : (int64_t)tab_tiles.size();
   if (samp_tiles.empty()) samp_tiles.push_back(0);
   if (tab_tiles.empty()) tab_tiles.push_back(0);
   if (tab_jobs.empty()) tab_jobs.push_back(tpe_tab_job{0, 0, 0, 0, 0, 0});
@@ -1053,19 +1150,29 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (fin_tiles.empty()) fin_tiles.push_back(0);
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
   // comp32 rows sit at the END of the last two sections and are not copied ----
-  const int NS = 14;
+  const int NS = 15;
+  // expanded levels: templates, first problems, new ids (one section, 256-B aligned parts)
+  const int64_t x_tmpl = (int64_t)(xtmpl.size() * sizeof(tpe_problem));
+  const int64_t x_first_off = (x_tmpl + 255) & ~(int64_t)255;
+  const int64_t x_ctr_off = (x_first_off + (int64_t)(xfirst.size() * sizeof(int32_t)) + 255) & ~(int64_t)255;
+  const int64_t x_len = expand ? x_ctr_off + (int64_t)(xctr.size() * sizeof(uint32_t)) : 0;
   const void* src[NS] = {prob.data(), tiles.data(), work.data(), comp64.data(), samp.data(), fit.data(),
                          below_idx.data(), fit_seg.data(), fin_tiles.data(), tab_jobs.data(), samp_tiles.data(),
-                         tab_tiles.data(), grid.data(), comp32.data()};
+                         tab_tiles.data(), nullptr, grid.data(), comp32.data()};
   const int64_t len[NS] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
                            (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp64.size() * sizeof(double)),
                            (int64_t)(samp.size() * sizeof(double)), (int64_t)(fit.size() * sizeof(tpe_fit_job)),
                            (int64_t)(below_idx.size() * sizeof(int32_t)), (int64_t)(fit_seg.size() * sizeof(int64_t)),
                            (int64_t)(fin_tiles.size() * sizeof(int32_t)),
                            (int64_t)(tab_jobs.size() * sizeof(tpe_tab_job)),
-                           (int64_t)(samp_tiles.size() * sizeof(int32_t)), (int64_t)(tab_tiles.size() * sizeof(int32_t)),
+                           (int64_t)(samp_tiles.size() * sizeof(int32_t)),
+                           expand ? 0 : (int64_t)(tab_tiles.size() * sizeof(int32_t)), x_len,
                            (int64_t)(grid.size() * sizeof(int32_t)), (int64_t)(comp32.size() * sizeof(float))};
-  const int64_t reserve[NS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
+  // device-only space: the expanded problems and tiles (k_expand) at the start,
+  // the device-fitted grid and comp32 rows at the end
+  const int64_t reserve[NS] = {expand ? P * (int64_t)sizeof(tpe_problem) : 0,
+                               expand ? P * n_tiles_p * (int64_t)sizeof(tpe_tile) : 0,
+                               0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
   int64_t off[NS], end = 0;
   for (int i = 0; i < NS; ++i) {
     off[i] = (end + 255) & ~(int64_t)255;
@@ -1080,9 +1187,12 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->tab_units = tab_units;
   info->off_samp_tiles = off[10]; info->n_samp_tiles = n_samp_tiles; info->n_samp_eager = n_samp_eager;
   info->off_tab_tiles = off[11]; info->n_tab_tiles = n_tab_tiles;
-  info->off_grid = off[12]; info->off_comp32 = off[13];
+  info->off_grid = off[13]; info->off_comp32 = off[14];
+  info->off_expand = expand ? off[12] : 0;
+  info->n_expand = expand ? n_labels : 0;
+  info->copy_start = expand ? off[2] : 0;
   info->n_problems = P;
-  info->n_tiles = (int64_t)tiles.size();
+  info->n_tiles = P * n_tiles_p;
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
   info->any_pruned = any_pruned ? 1 : 0;
   info->key_bits = key_bits;
@@ -1090,16 +1200,22 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->part_total = part_total;
   info->n_fit = (int32_t)fit.size(); info->reserved = 0;
   info->fit_total = fit_seg.back();
-  info->copy_end = off[12] + len[12];
+  info->copy_end = off[13] + len[13];
   info->sort_count = n_sorted_prob * (int64_t)n_cand;
   info->n_sorted = S;
   info->n_pooled = n_pooled;
   info->draw_blocks = (C_ref + 1 + 63) / 64;
-  info->copy2_len = len[13];
+  info->copy2_len = len[14];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;
   for (int i = 0; i < NS; ++i)
-    if (len[i]) memcpy((unsigned char*)blob + off[i], src[i], (size_t)len[i]);
+    if (len[i] && src[i]) memcpy((unsigned char*)blob + off[i], src[i], (size_t)len[i]);
+  if (expand) {
+    unsigned char* x = (unsigned char*)blob + off[12];
+    memcpy(x, xtmpl.data(), (size_t)x_tmpl);
+    memcpy(x + x_first_off, xfirst.data(), xfirst.size() * sizeof(int32_t));
+    memcpy(x + x_ctr_off, xctr.data(), xctr.size() * sizeof(uint32_t));
+  }
   return TPE_OK;
 }
 

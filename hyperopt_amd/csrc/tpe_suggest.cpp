@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/tpe_hip.h"
+#include "tpe_pool.h"
 
 extern "C" int tpe_internal_fail(int code, const char* what);   // tpe_kernels.hip (hidden)
 extern "C" int tpe_internal_exchange(const tpe_exchange* ex, void* stream, int32_t my_status, tpe_result* res,
@@ -56,7 +57,10 @@ struct Tree {
   int8_t* need_fit;             // labels the caller must fit (TPE_E_FALLBACK)
 };
 
-int fit_label(Tree& T, int i) {
+// spec: a speculative fit on a pool worker (prefit): labels the caller must
+// fit are left alone (no need_fit flag), and a failure only leaves the fit
+// undone — the label's real fit, on the calling thread, reports it
+int fit_label(Tree& T, int i, bool spec = false) {
   Fit& f = (*T.fits)[(size_t)i];
   if (f.done) return TPE_OK;
   const tpe_tree_label& L = T.L[i];
@@ -75,7 +79,7 @@ int fit_label(Tree& T, int i) {
     return TPE_OK;
   }
   auto host_fit = [&]() {                     // numpy's tie order decides this fit: the caller's
-    if (T.need_fit) T.need_fit[i] = 1;
+    if (T.need_fit && !spec) T.need_fit[i] = 1;
     return TPE_E_FALLBACK;
   };
   if (n < 0 || (n > 0 && (!L.tids || !L.values))) return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: bad columns");
@@ -147,6 +151,49 @@ int fit_label(Tree& T, int i) {
   }
   f.done = true;
   return TPE_OK;
+}
+
+// Labels worth a speculative fit on the pool: the natively fitted ones with
+// enough observations for the fit to cost more than a dispatch (categorical, and
+// continuous with a value order below the device-fit size).  Every label of a
+// flat space is needed; in a tree the inactive branches' labels are fitted too
+// (their observations are the trials that took that branch, so the extra work
+// is bounded by the history) — what matters is that the suggest waits for the
+// slowest label, not for the sum over the labels the active branch needs.
+constexpr int64_t kPrefitMinObs = 256;
+
+bool prefit_worthy(const Tree& T, int i) {
+  const tpe_tree_label& L = T.L[i];
+  if (L.host_k[0] > 0 || L.n_obs < kPrefitMinObs || !L.tids || !L.values) return false;
+  if (L.family == TPE_FAM_CATEGORICAL) return L.upper > 0;
+  if (L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) return false;
+  if (!L.order) return false;
+  return !(T.device_fit_min > 0 && L.n_obs >= std::max<int64_t>(T.device_fit_min, 64));
+}
+
+struct PrefitCtx {
+  Tree* T;
+  const int* ix;
+};
+
+void prefit_one(void* c, int j) {
+  PrefitCtx* p = (PrefitCtx*)c;
+  fit_label(*p->T, p->ix[j], true);
+}
+
+void prefit(Tree& T) {
+  static thread_local std::vector<int> ix_tl;
+  std::vector<int>& ix = ix_tl;
+  ix.clear();
+  bool hinted = false;                  // the caller's hint (TPE_F_PREFIT), else every worthy label
+  for (int i = 0; i < T.n && !hinted; ++i) hinted = (T.L[i].flags & TPE_F_PREFIT) != 0;
+  for (int i = 0; i < T.n; ++i)
+    if ((!hinted || (T.L[i].flags & TPE_F_PREFIT)) && prefit_worthy(T, i)) ix.push_back(i);
+  if (ix.size() < 2 || tpe_pool::workers() == 0) return;   // (on demand, on this thread)
+  // largest first: the slowest fits start first
+  std::sort(ix.begin(), ix.end(), [&](int a, int b) { return T.L[a].n_obs > T.L[b].n_obs; });
+  PrefitCtx c{&T, ix.data()};
+  tpe_pool::parallel_for((int)ix.size(), prefit_one, &c);
 }
 
 // ParamTable.active: some parent chose this label's option (`chosen`: the
@@ -277,6 +324,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
       return TPE_E_FALLBACK;
   }
   if (n_labels == 0 || n_ids == 0) return TPE_OK;
+  prefit(T);
   const int32_t run_flags = flags & ~TPE_TREE_NO_SPECULATE;
   std::vector<tpe_label_in>& recs = recs_tl;
   std::vector<tpe_result>& res = res_tl;

@@ -376,7 +376,7 @@ def _tree_labels(table, hist, engine=None):
     return out
 
 
-def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None):
+def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None, columns=False):
     """``_choices_philox`` in one native call (tpe_suggest_tree), or None when
     the space or history needs the general path.  Labels the native fits cannot
     reproduce (quantized ones, sides with repeated values: numpy's argsort tie
@@ -384,13 +384,13 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     exactly as the general path fits them and handed to a second call.
     ``shard`` = (rank, world): candidate-sharded over the default process
     group, the level results exchanged inside the native call (dist.py)."""
-    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard)
+    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns)
     if out is None:
         table.native_fit_hint = ()             # the general path takes it: nothing to pre-fit next time
     return out
 
 
-def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard):
+def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False):
     if not hist.sorted_obs:
         return None
     tl = _tree_labels(table, hist, engine)
@@ -400,6 +400,15 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     if shard is not None:
         ex = _dist.exchange_for(engine)
     below = np.sort(np.asarray(below_tids, dtype=np.int64))
+    # the labels the previous suggest used are fitted up front on the native
+    # worker threads (TPE_F_PREFIT; the active branch seldom changes)
+    hint = getattr(table, 'native_used', None)
+    pf = getattr(table, '_prefit_applied', None)
+    if hint is not None and (pf is None or pf[0] is not tl[0] or pf[1] != hint):
+        fl = tl[0]['flags']
+        fl &= ~N.F_PREFIT
+        fl[list(hint)] |= N.F_PREFIT
+        table._prefit_applied = (tl[0], hint)
     st = {'arr': tl[0]}
     host = {}
 
@@ -445,12 +454,17 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     # (only labels some id used: a branch switch drops the old branch's)
     used = np.asarray(active).any(axis=0)
     table.native_fit_hint = tuple(ix for ix in host if used[ix])
+    table.native_used = tuple(np.flatnonzero(used).tolist())
     # the device-fitted labels that ran hold their merged value orders now
     for ix, (order, n) in tl[2].items():
         if used[ix]:
             order.commit(n)
+    if columns:
+        return ChoiceColumns(table.labels, values, np.asarray(active, dtype=bool))
     order = table.level_order()
     cols = _tree_static(table)[2]
+    if len(values) > 4:
+        return _choice_dicts(order, cols, values, active)
     i64, f64 = np.int64, np.float64
     out = []
     for act, v in zip(active.tolist(), values.tolist()):
@@ -460,6 +474,23 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
                 d[label] = i64(v[ix]) if fam == N.FAM_CATEGORICAL else f64(v[ix])
         out.append(d)
     return out
+
+
+def _choice_dicts(order, cols, values, active):
+    """Per-id {label: value or None} dicts of a batched suggest, built column
+    by column: numpy makes each column's scalars (np.int64 categories, np.float64
+    values, the reference's types) and one ``dict(zip(...))`` per id assembles
+    them in level order — no per-label Python work per id."""
+    act = np.asarray(active, dtype=bool)
+    by_label = {}
+    for label, ix, fam in cols:
+        col = values[:, ix]
+        vals = list(col.astype(np.int64)) if fam == N.FAM_CATEGORICAL else list(col)
+        a = act[:, ix]
+        if not a.all():
+            vals = [v if on else None for v, on in zip(vals, a.tolist())]
+        by_label[label] = vals
+    return [dict(zip(order, t)) for t in zip(*[by_label[k] for k in order])]
 
 
 def _choices_replay(table, fits, new_ids, seed, C, engine):
@@ -522,28 +553,65 @@ def suggest(new_ids, domain, trials, seed,
     return rand.docs_from_choices(new_ids, domain, trials, choices)
 
 
+class ChoiceColumns(object):
+    """Columnar result of a batched suggest (``suggest_choices(...,
+    columns=True)``): ``labels`` in table order, ``values`` float64
+    [n_ids x n_labels] (a categorical label's chosen index as a float, NaN
+    where inactive) and ``active`` bool [n_ids x n_labels].  ``dicts()`` gives
+    the per-id {label: value or None} dicts ``suggest_choices`` returns."""
+    __slots__ = ('labels', 'values', 'active', '_cat')
+
+    def __init__(self, labels, values, active, categorical=None):
+        self.labels, self.values, self.active = list(labels), values, active
+        self._cat = categorical
+
+    def __len__(self):
+        return len(self.values)
+
+    def dicts(self, table):
+        cols = [(r.label, r.index, N.FAM_CATEGORICAL if r.categorical else N.FAM_GAUSS) for r in table.rows]
+        return _choice_dicts(table.level_order(), cols, self.values, self.active)
+
+    @classmethod
+    def from_dicts(cls, table, dicts):
+        n, L = len(dicts), len(table.rows)
+        values = np.full((n, L), np.nan)
+        active = np.zeros((n, L), dtype=bool)
+        for j, d in enumerate(dicts):
+            for r in table.rows:
+                v = d.get(r.label)
+                if v is not None:
+                    values[j, r.index] = float(v)
+                    active[j, r.index] = True
+        return cls(table.labels, values, active)
+
+
 def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weight,
                     n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
-                    sampler='philox', precision='fp32', device=None, shard=None):
+                    sampler='philox', precision='fp32', device=None, shard=None, columns=False):
     """The suggest core on a structure-of-arrays history (``history.History``):
     per new id a {label: value or None} dict.  ``suggest`` wraps it with the
     Trials document layout; columnar callers (and bench.py's large configs)
-    use it directly."""
+    use it directly.  ``columns=True``: the same choices as one ChoiceColumns
+    (SoA in, SoA out — no per-id Python objects for a batch of thousands)."""
     if sampler not in ('philox', 'replay'):
         raise ValueError("sampler must be 'philox' or 'replay'")
     engine = get_engine(device, precision)
     below_tids = _history.split_below(hist, gamma)
     C = int(n_EI_candidates)
     if sampler == 'philox' and NATIVE_TREE and precision == 'fp32':
-        out = _choices_native(table, hist, below_tids, list(new_ids), seed, C, engine, prior_weight, shard)
+        out = _choices_native(table, hist, below_tids, list(new_ids), seed, C, engine, prior_weight, shard,
+                              columns)
         if out is not None:
             return out
     fits = _Fits(table, hist, below_tids, prior_weight, engine)
     if sampler == 'philox':
-        return _choices_philox(table, fits, list(new_ids), seed, C, engine, shard)
-    if shard is not None:
+        out = _choices_philox(table, fits, list(new_ids), seed, C, engine, shard)
+    elif shard is not None:
         raise ValueError("sampler='replay' draws on the host; it does not shard")
-    return _choices_replay(table, fits, list(new_ids), seed, C, engine)
+    else:
+        out = _choices_replay(table, fits, list(new_ids), seed, C, engine)
+    return ChoiceColumns.from_dicts(table, out) if columns else out
 
 
 def suggest_replay(new_ids, domain, trials, seed, **kw):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 14
+#define TPE_ABI_VERSION 15
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -67,8 +67,11 @@ enum {
                           probability >= 2^-16: device-drawn batches without per-candidate outputs
                           score it in the select stage by scanning draws in index order until no
                           undrawn category can still win (usually one 1024-draw chunk) */
-  TPE_F_NO_TABLE = 16  /* tpe_label_in: score this label per candidate (no lattice table), e.g. when
+  TPE_F_NO_TABLE = 16, /* tpe_label_in: score this label per candidate (no lattice table), e.g. when
                           the caller supplies candidates that need not lie on the quantization lattice */
+  TPE_F_PREFIT = 32    /* tpe_tree_label: fit this label up front on the host worker threads (the
+                          caller's hint: the labels its previous suggest on the space used); no label
+                          flagged: every natively fitted label with enough observations */
 };
 
 /* tabulated scoring of a problem (tpe_problem.tab_mode, see "Tabulated scoring") */
@@ -469,7 +472,23 @@ typedef struct tpe_pack_info {
   int64_t n_pooled;                     /* pooled problems (tpe_batch.pool_best needed) */
   int64_t off_tab_jobs, n_tab_jobs, tab_blocks, tab_units;   /* tabulated scoring (tpe_batch.tab_*) */
   int64_t off_samp_tiles, n_samp_tiles, n_samp_eager, off_tab_tiles, n_tab_tiles;   /* tpe_batch tile lists */
+  /* expanded level (see "Expanded levels"; n_expand = 0: not expanded): off_expand holds
+   * tpe_problem templates[n_expand], then (at the next 256-B boundary) int32 first[n_expand + 1],
+   * then (at the next 256-B boundary) uint32 new_id[n_problems]; the problems and tiles sections
+   * (and the tabulated tile list, the identity) are device-only: the upload starts at copy_start */
+  int64_t off_expand, n_expand, copy_start;
 } tpe_pack_info;
+
+/* ------------------------------------------------------------------------
+ * Expanded levels.  A batched level (>= 256 problems) whose labels all score
+ * from tables (cells or lattice) has problems that differ from their label's
+ * only in cand_off (= r * n_cand), ctr3 (the new id) and tile_off (= r *
+ * n_tiles), and tiles {r, j * 2048, 0, 0} in order, all of them tabulated.
+ * tpe_host_pack_level then writes one problem template per label and the new
+ * ids instead of ~270 B per (label, id), and tpe_level_run's device writes the
+ * problems and tiles (k_expand) right after the upload: a 20-label x 4096-id
+ * level packs and uploads ~0.4 MB of descriptors instead of ~22 MB.
+ * ---------------------------------------------------------------------- */
 
 /* adaptive_parzen_normal (tpe.py:398-475) with the caller's sort permutation
  * `order` of obs (np.argsort; may be NULL when n < 2).  Writes n+1 components
@@ -695,6 +714,15 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
                      uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
                      const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
                      int32_t* path, int8_t* need_fit);
+
+/* Host worker threads of the native runtime, the calling thread included
+ * (default: TPE_HOST_THREADS, else 4; at most 16).  tpe_suggest_tree fits the
+ * labels of a suggest on them in parallel (each label's fit is the same
+ * single-threaded computation wherever it runs, so results do not depend on
+ * the count).  n <= 1: everything on the calling thread; n < 0: query only.
+ * *previous (if not NULL) gets the count before the call.  Not to be called
+ * while another thread is inside tpe_suggest_tree. */
+int tpe_host_threads(int32_t n, int32_t* previous);
 
 /* ------------------------------------------------------------------------
  * Stage profiler of tpe_level_run (bench.py's live roofline).  While enabled,

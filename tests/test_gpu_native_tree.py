@@ -84,6 +84,35 @@ def test_native_tree_columnar_history():
     ids = np.arange(4000, 4064)
     nat, gen, path = _both(lambda: tpe.suggest_choices(table, hist, ids, 11, n_EI_candidates=2048))
     assert path == (0, 1) and nat == gen
+    # the columnar result (SoA out) holds the same choices, native and general
+    for native in (True, False):
+        tpe.NATIVE_TREE = native
+        try:
+            cc = tpe.suggest_choices(table, hist, ids, 11, n_EI_candidates=2048, columns=True)
+        finally:
+            tpe.NATIVE_TREE = True
+        assert cc.labels == table.labels and cc.values.shape == (len(ids), 5) and cc.active.all()
+        assert cc.dicts(table) == nat
+        assert all(type(v) is np.float64 for v in cc.dicts(table)[0].values())
+
+
+def test_native_tree_batched_result_types():
+    """More than a few ids take the column-wise dict assembly: the same values
+    and the reference's value types (np.int64 categories, np.float64 values,
+    None when inactive) in level order."""
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(2000, 1)
+    ids = list(range(2000, 2012))
+    nat, gen, path = _both(lambda: tpe.suggest_choices(domain.table, __import__('hyperopt_amd').history.extract(
+        domain, trials), ids, 4, n_EI_candidates=4096))
+    assert nat == gen and path is not None
+    order = domain.table.level_order()
+    for d in nat:
+        assert list(d) == order
+        for r in domain.table.rows:
+            v = d[r.label]
+            assert v is None or type(v) is (np.int64 if r.categorical else np.float64), (r.label, type(v))
 
 
 def test_native_tree_device_fit_labels():
