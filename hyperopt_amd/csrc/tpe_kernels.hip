@@ -2408,6 +2408,49 @@ __global__ __launch_bounds__(kUploadThreads) void k_upload(const unsigned long l
   }
 }
 
+// ============================================================ expanded levels
+// (include/tpe_hip.h "Expanded levels").  The problems of an expanded level
+// differ from their label's template only in cand_off, tile_off and ctr3, and
+// its tiles are {r, j * kTile, 0, 0} in order.  One thread per 8-byte word of
+// the problem rows (consecutive threads write consecutive words) and one per
+// tile.
+constexpr int kExpandThreads = 256;
+constexpr int kProbWords = (int)(sizeof(tpe_problem) / 8);
+static_assert(sizeof(tpe_problem) % 8 == 0, "problem rows in 8-byte words");
+
+__global__ __launch_bounds__(kExpandThreads) void k_expand(const tpe_problem* __restrict__ tmpl,
+                                                           const int32_t* __restrict__ first, int n_lab,
+                                                           const uint32_t* __restrict__ new_id,
+                                                           tpe_problem* __restrict__ prob, tpe_tile* __restrict__ tiles,
+                                                           int64_t P, int32_t n_tiles, int32_t n_cand) {
+  const int64_t i = (int64_t)blockIdx.x * kExpandThreads + threadIdx.x;
+  if (i < P * kProbWords) {
+    const int64_t r = i / kProbWords;
+    const int w = (int)(i - r * kProbWords);
+    int a = 0, b = n_lab - 1;                    // the last label whose first problem is <= r
+    while (a < b) {
+      const int m = (a + b + 1) >> 1;
+      if ((int64_t)first[m] <= r) a = m; else b = m - 1;
+    }
+    uint64_t v = reinterpret_cast<const uint64_t*>(tmpl + a)[w];
+    const int byte = 8 * w;
+    auto put32 = [&](int off, uint32_t x) {
+      if (off >= byte && off < byte + 8) {
+        const int sh = 8 * (off - byte);
+        v = (v & ~(0xffffffffull << sh)) | ((uint64_t)x << sh);
+      }
+    };
+    if (byte == (int)offsetof(tpe_problem, cand_off)) v = (uint64_t)(r * (int64_t)n_cand);
+    put32((int)offsetof(tpe_problem, tile_off), (uint32_t)(r * (int64_t)n_tiles));
+    put32((int)offsetof(tpe_problem, ctr3), new_id[r]);
+    reinterpret_cast<uint64_t*>(prob + r)[w] = v;
+  }
+  if (i < P * (int64_t)n_tiles) {
+    const int64_t r = i / n_tiles;
+    tiles[i] = tpe_tile{(int32_t)r, (int32_t)((i - r * n_tiles) * kTile), 0, 0};
+  }
+}
+
 // ============================================================ device Parzen fit
 // adaptive_parzen_normal (tpe.py:398-475) of the above observations of a label
 // (ap_filter_trials, tpe.py:613-641), directly into the pruned f32 layout.
@@ -2995,8 +3038,10 @@ int check_batch(const tpe_batch* b) {
   if (b->n_tab_jobs < 0 || b->tab_blocks < 0 || b->tab_units < 0) return fail(TPE_E_ARG, "negative table count");
   if (b->n_tab_jobs > 0 && (!b->tab_jobs || !b->tab || !b->comp32 || !b->comp64))
     return fail(TPE_E_ARG, "null table buffers");
-  if (b->early_select && (!b->run_best || b->n_tab_jobs <= 0 || !b->sample || !b->samp || !b->tab_tiles ||
-                          b->n_late < 0 || b->n_late > b->n_problems))
+  // (no tabulated tile list: every tile is tabulated, in order — an expanded level)
+  if (b->early_select && (!b->run_best || b->n_tab_jobs <= 0 || !b->sample || !b->samp ||
+                          (!b->tab_tiles && b->n_tab_tiles != b->n_tiles) || b->n_late < 0 ||
+                          b->n_late > b->n_problems))
     return fail(TPE_E_ARG, "early selection needs tables, device draws, tile lists and run_best");
   return TPE_OK;
 }
@@ -3345,19 +3390,24 @@ static int run_batch_profiled(const tpe_batch* b, void* stream) {
 }
 
 // after the stream synchronise: event times and each stage's work
-static int profile_collect(const tpe_batch& b, const tpe_pack_info& info, const tpe_problem* hp, int64_t n_cand) {
+// hp: the host-written problems, or (expanded level) the label templates with
+// the first problem of each label in xfirst
+static int profile_collect(const tpe_batch& b, const tpe_pack_info& info, const tpe_problem* hp,
+                           const int32_t* xfirst, int64_t n_cand) {
   const int64_t P = info.n_problems;
   double ce_tab = 0, ce_above = 0, drawn = 0;
   const bool lz = b.early_select && !(b.flags & TPE_BATCH_WRITE_CAND);
-  for (int64_t r = 0; r < P; ++r) {
+  const int64_t rows = xfirst ? info.n_expand : P;
+  for (int64_t r = 0; r < rows; ++r) {
+    const double n = xfirst ? (double)(xfirst[r + 1] - xfirst[r]) : 1.0;   // problems of this row
     if (hp[r].tab_mode != TPE_TAB_NONE)
-      ce_tab += (double)(hp[r].below_len + hp[r].above_len) * (double)n_cand;
+      ce_tab += n * (double)(hp[r].below_len + hp[r].above_len) * (double)n_cand;
     else if (hp[r].family != TPE_FAM_CATEGORICAL)
-      ce_above += (double)hp[r].above_len * (double)n_cand;
+      ce_above += n * (double)hp[r].above_len * (double)n_cand;
     // candidates the sample stage draws (lazy categoricals are scanned by the table stage)
     const bool lazy = lz && (hp[r].flags & TPE_F_CAT_LAZY) && hp[r].family == TPE_FAM_CATEGORICAL &&
                       hp[r].samp_len <= 64;
-    if (!lazy) drawn += (double)n_cand;
+    if (!lazy) drawn += n * (double)n_cand;
   }
   const double C = (double)P * (double)n_cand;
   const double units[TPE_N_STAGES] = {
@@ -3431,29 +3481,57 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   hipError_t e;
   const int64_t gap = info.off_comp32 - info.copy_end;
   char* dbase = !direct_results() ? nullptr : (ws->pinned_dev ? (char*)ws->pinned_dev : device_alias(ws->pinned));
-  // ranges to upload: [0, n1) and [o2, o2 + n2) (one range when the gap is small)
+  // ranges to upload: [c0, n1) and [o2, o2 + n2) (one range when the gap is
+  // small); c0 = copy_start: an expanded level's problems and tiles are the
+  // device's (k_expand below)
+  const int64_t c0 = info.copy_start;
+  if (c0 < 0 || (c0 & 255) || c0 > info.copy_end || (info.n_expand > 0) != (c0 > 0))
+    return fail(TPE_E_ARG, "tpe_level_run: bad copy_start");
   int64_t n1 = info.copy_end, o2 = info.off_comp32, n2 = info.copy2_len;
   if (n2 > 0 && gap <= kOneCopyMaxGap) { n1 = o2 + n2; n2 = 0; }
-  const int64_t n1r = (n1 + 7) & ~(int64_t)7, n2r = (n2 + 7) & ~(int64_t)7;
-  if (dbase && kernel_upload() && n1r <= ws->blob_bytes && (n2 == 0 || o2 + n2r <= ws->blob_bytes) &&
+  const int64_t n1r = (n1 - c0 + 7) & ~(int64_t)7, n2r = (n2 + 7) & ~(int64_t)7;
+  if (dbase && kernel_upload() && c0 + n1r <= ws->blob_bytes && (n2 == 0 || o2 + n2r <= ws->blob_bytes) &&
       n1r + n2r <= ((int64_t)64 << 20)) {
     const int64_t n8 = n1r / 8, m8 = n2r / 8;
     const int grid = (int)std::min<int64_t>(std::max<int64_t>((n8 + m8 + kUploadThreads - 1) / kUploadThreads, 1),
                                             2048);
-    TPE_LAUNCH(k_upload, dim3(grid), dim3(kUploadThreads), 0, s, (const unsigned long long*)dbase,
-               (unsigned long long*)dev, n8, (const unsigned long long*)(dbase + o2),
+    TPE_LAUNCH(k_upload, dim3(grid), dim3(kUploadThreads), 0, s, (const unsigned long long*)(dbase + c0),
+               (unsigned long long*)(dev + c0), n8, (const unsigned long long*)(dbase + o2),
                (unsigned long long*)(dev + o2), m8);
     if ((rc = hip_check("k_upload"))) return rc;
     e = hipSuccess;
   } else if (info.copy2_len > 0 && gap <= kOneCopyMaxGap) {
-    e = hipMemcpyAsync(dev, host, (size_t)(info.off_comp32 + info.copy2_len), hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(dev + c0, host + c0, (size_t)(info.off_comp32 + info.copy2_len - c0), hipMemcpyHostToDevice, s);
   } else {
-    e = hipMemcpyAsync(dev, host, (size_t)info.copy_end, hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(dev + c0, host + c0, (size_t)(info.copy_end - c0), hipMemcpyHostToDevice, s);
     if (e == hipSuccess && info.copy2_len > 0)
       e = hipMemcpyAsync(dev + info.off_comp32, host + info.off_comp32, (size_t)info.copy2_len,
                          hipMemcpyHostToDevice, s);
   }
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  // expanded level: the templates, first problems and new ids (uploaded above)
+  const tpe_problem* xtmpl = nullptr;
+  const int32_t* xfirst = nullptr;
+  const int64_t n_tiles_p = P > 0 ? info.n_tiles / P : 0;
+  if (info.n_expand > 0) {
+    const int64_t nl = info.n_expand;
+    const int64_t first_off = ((int64_t)(nl * sizeof(tpe_problem)) + 255) & ~(int64_t)255;
+    const int64_t ctr_off = (first_off + (nl + 1) * (int64_t)sizeof(int32_t) + 255) & ~(int64_t)255;
+    xtmpl = (const tpe_problem*)(host + info.off_expand);
+    xfirst = (const int32_t*)(host + info.off_expand + first_off);
+    if (nl >= ((int64_t)1 << 31) || xfirst[0] != 0 || xfirst[nl] != P || n_tiles_p * P != info.n_tiles ||
+        n_tiles_p < 1 || n_cand > n_tiles_p * kTile || info.n_tab_tiles != info.n_tiles)
+      return fail(TPE_E_ARG, "tpe_level_run: bad expanded level");
+    for (int64_t l = 0; l < nl; ++l)
+      if (xfirst[l + 1] < xfirst[l] || xtmpl[l].tab_mode == TPE_TAB_NONE)
+        return fail(TPE_E_ARG, "tpe_level_run: bad expanded level");
+    const int64_t n_thr = std::max<int64_t>(P * kProbWords, info.n_tiles);
+    TPE_LAUNCH(k_expand, dim3((unsigned)((n_thr + kExpandThreads - 1) / kExpandThreads)), dim3(kExpandThreads), 0, s,
+               (const tpe_problem*)(dev + info.off_expand), (const int32_t*)(dev + info.off_expand + first_off),
+               (int)nl, (const uint32_t*)(dev + info.off_expand + ctr_off), (tpe_problem*)(dev + info.off_problems),
+               (tpe_tile*)(dev + info.off_tiles), P, (int32_t)n_tiles_p, n_cand);
+    if ((rc = hip_check("k_expand"))) return rc;
+  }
   tpe_batch b;
   memset(&b, 0, sizeof(b));
   b.problems = (const tpe_problem*)(dev + info.off_problems);
@@ -3491,7 +3569,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.samp_tiles = (const int32_t*)(dev + info.off_samp_tiles);
   b.n_samp_tiles = (int32_t)info.n_samp_tiles;
   b.n_samp_eager = (int32_t)info.n_samp_eager;
-  b.tab_tiles = (const int32_t*)(dev + info.off_tab_tiles);
+  b.tab_tiles = xtmpl ? nullptr : (const int32_t*)(dev + info.off_tab_tiles);   // (expanded: every tile, in order)
   b.n_tab_tiles = (int32_t)info.n_tab_tiles;
   if (info.n_tab_jobs > 0) {
     b.tab_jobs = (const tpe_tab_job*)(dev + info.off_tab_jobs);
@@ -3507,13 +3585,14 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   // early selection (include/tpe_hip.h): the sample stage reports each run of
   // tabulated tiles to host-visible memory, the table stage selects the lazy
   // categoricals, and only the rest go through the select stage
-  const tpe_problem* hp = (const tpe_problem*)(host + info.off_problems);
+  // (expanded level: no host-written problems; every problem is tabulated)
+  const tpe_problem* hp = xtmpl ? nullptr : (const tpe_problem*)(host + info.off_problems);
   if (info.n_tab_jobs > 0 && dbase) {
     b.early_select = 1;
     b.run_best = (tpe_result*)(dbase + rb_off);
     const bool lz = !(flags & TPE_BATCH_WRITE_CAND);
     int32_t late = 0;
-    for (int64_t r = 0; r < P; ++r) {
+    for (int64_t r = 0; hp && r < P; ++r) {
       const tpe_problem& q = hp[r];
       const bool lazy = lz && (q.flags & TPE_F_CAT_LAZY) && q.family == TPE_FAM_CATEGORICAL && q.samp_len <= 64;
       late += !(lazy || q.tab_mode != TPE_TAB_NONE);
@@ -3543,22 +3622,25 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   if (b.early_select) {
     // each tabulated problem: the best of its runs (np.argmax order), runs
     // enumerated exactly as the sample stage partitions the tile list
+    // (expanded level: the identity list, tile t of problem t / n_tiles_p)
     const tpe_result* rb = (const tpe_result*)(host + rb_off);
-    const int32_t* list = (const int32_t*)(host + info.off_tab_tiles);
-    const tpe_tile* tl = (const tpe_tile*)(host + info.off_tiles);
+    const int32_t* list = xtmpl ? nullptr : (const int32_t*)(host + info.off_tab_tiles);
+    const tpe_tile* tl = xtmpl ? nullptr : (const tpe_tile*)(host + info.off_tiles);
+    auto tile_of = [&](int i) { return list ? list[i] : i; };
+    auto prob_of = [&](int t) { return tl ? tl[t].problem : (int)(t / n_tiles_p); };
     const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab);
     for (int64_t r = 0; r < P; ++r)
-      if (hp[r].tab_mode != TPE_TAB_NONE) { rh[r] = tpe_result{0, 0, 0, 0, -1, -1}; }
+      if (!hp || hp[r].tab_mode != TPE_TAB_NONE) { rh[r] = tpe_result{0, 0, 0, 0, -1, -1}; }
     for (int i = 0; i < n_tab; ++i) {
-      const int t = list[i], pr = tl[t].problem;
-      if (i % per != 0 && tl[list[i - 1]].problem == pr) continue;        // not a run's first tile
+      const int t = tile_of(i), pr = prob_of(t);
+      if (i % per != 0 && prob_of(tile_of(i - 1)) == pr) continue;        // not a run's first tile
       const tpe_result& c = rb[t];
       tpe_result& w = rh[pr];
       if (host_better(c.score, c.idx, w.score, w.idx)) w = c;
     }
   }
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));
-  return g_prof.on ? profile_collect(b, info, hp, n_cand) : TPE_OK;
+  return g_prof.on ? profile_collect(b, info, xtmpl ? xtmpl : hp, xfirst, n_cand) : TPE_OK;
 }
 
 }  // extern "C"

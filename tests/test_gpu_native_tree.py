@@ -226,3 +226,26 @@ def test_engine_stream_follows_torch():
     with torch.cuda.stream(s):
         assert eng._stream() == s.cuda_stream
     assert eng._stream() == torch.cuda.current_stream(eng.device).cuda_stream
+
+
+def test_expanded_level_matches_host_written_level(monkeypatch):
+    """An expanded level (>= 256 problems, every label tabulated: the device
+    writes the problems and tiles from one template per label, k_expand) gives
+    exactly the suggestions of the same level with every problem and tile
+    written by the host (TPE_EXPAND=0), for ids that do not start at 0 and a
+    candidate count that leaves the last tile partial."""
+    import bench
+    from hyperopt_amd import tpe
+    labels = ['x%02d' % i for i in range(6)]
+    hist = bench.soa_history(labels, 3000, bench.SEED, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+    table = bench.flat_uniform_table(labels)
+    ids = np.arange(7000, 7000 + 300)
+    C = 3000
+    outs = []
+    for env in ('1', '0'):
+        monkeypatch.setenv('TPE_EXPAND', env)
+        cc = tpe.suggest_choices(table, hist, ids, 21, n_EI_candidates=C, columns=True)
+        outs.append(np.asarray(cc.values))
+    assert outs[0].shape == (len(ids), len(labels))
+    assert np.array_equal(outs[0], outs[1])
+    assert np.all(np.isfinite(outs[0])) and np.all(outs[0] >= -5) and np.all(outs[0] < 5)
