@@ -41,6 +41,8 @@
 
 #include "../../include/tpe_hip.h"
 
+extern "C" void tpe_internal_phase(int i);   // tpe_suggest.cpp: host phase clock (hidden)
+
 namespace {
 
 constexpr int kThreads = 256;          // 4 waves of 64
@@ -740,19 +742,54 @@ __global__ __launch_bounds__(kThreads) void k_sample(const tpe_problem* __restri
 constexpr int kTabThreads = 1024;
 constexpr int kTabLdsCells = 2048;                  // 96 KiB of 48-B cell rows
 static_assert(TPE_TAB_ROW_UNITS == 3 && kTabMoments == 11, "a cell row: 11 moments and the shift in 3 float4");
-constexpr int kGuide = 64;                          // CDF guide entries
+constexpr int kGuide = 256;                         // CDF guide entries
 constexpr int kTabMaxTilesPerWg = 16;
 static_assert(kTile % kTabThreads == 0, "tabulated sample tiling");
 constexpr int kTabPer = kTile / kTabThreads;         // candidates per thread per tile
 static_assert(kTabPer % 2 == 0, "a thread draws its candidates in Philox pairs");
 
-// first k with u < cum_k (k <= len - 1), starting at the guide entry of u:
-// the binary search's answer (find_comp) on a non-decreasing CDF
-__device__ __forceinline__ int guided_comp(const double* __restrict__ cum, const int* __restrict__ guide, int len,
-                                           double u) {
-  int k = guide[min((int)(u * (double)kGuide), kGuide - 1)];
+// Guide entry b of a selection CDF: k0 = the first k with cum_k > b / kGuide
+// (where the answer for any u in [b, b + 1) / kGuide starts) and the CDF values
+// of its first two steps, +inf where a step would pass the last component.
+struct GuideEnt {
+  double c0, c1;          // cum[k0], cum[k0 + 1] (or +inf)
+  int k0, pad0, pad1, pad2;
+};
+static_assert(sizeof(GuideEnt) == 32, "guide entries: two 16-B LDS reads");
+
+// first k with u < cum_k (k <= len - 1): the binary search's answer
+// (find_comp) on a non-decreasing CDF.  The guide entry settles it in two
+// steps; `more` flags the (rare) u that needs a third (guided_more).
+__device__ __forceinline__ int guided_comp(const GuideEnt* __restrict__ guide, double u, bool& more) {
+  const GuideEnt e = guide[min((int)(u * (double)kGuide), kGuide - 1)];
+  const bool s0 = !(u < e.c0), s1 = s0 && !(u < e.c1);
+  more = s1;
+  return e.k0 + (int)s0 + (int)s1;
+}
+// the steps past the guide entry's two (lanes with `more`)
+__device__ __forceinline__ int guided_more(const double* __restrict__ cum, int len, double u, int k) {
   while (k < len - 1 && !(u < cum[k])) ++k;
   return k;
+}
+
+// log2 of one mixture side's sum at t from its cell rows (LDS), cell_log2_lds
+// without branches: the row of a clamped cell index is read and the result
+// replaced by NAN when t lies outside the cells, in a flagged cell or the
+// series is not positive (the same arithmetic for every t inside)
+__device__ __forceinline__ float cell_log2_nb(float lo, float inv, float w, float ih, int n,
+                                              const float4* __restrict__ rows, int stride, float t) {
+  const float gj = floorf((t - lo) * inv);
+  const bool in = gj >= 0.f && gj < (float)n;
+  const float4* __restrict__ r = rows + (in ? (int)gj : 0);
+  const float4 a = r[0], b = r[stride], c = r[2 * stride];
+  const float u = (t - __builtin_fmaf(gj + 0.5f, w, lo)) * ih;
+  float sm = c.z;
+  sm = __builtin_fmaf(sm, u, c.y); sm = __builtin_fmaf(sm, u, c.x);
+  sm = __builtin_fmaf(sm, u, b.w); sm = __builtin_fmaf(sm, u, b.z); sm = __builtin_fmaf(sm, u, b.y);
+  sm = __builtin_fmaf(sm, u, b.x); sm = __builtin_fmaf(sm, u, a.w); sm = __builtin_fmaf(sm, u, a.z);
+  sm = __builtin_fmaf(sm, u, a.y); sm = __builtin_fmaf(sm, u, a.x);
+  const float v = c.w + __log2f(sm);
+  return in && sm > 0.f ? v : NAN;
 }
 
 // log2 of one mixture side's sum at t from its cell rows (LDS or global); NAN
@@ -808,7 +845,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   uint64_t g_ft[3] = {0, 0, 0};              // flush: after the fold, after its barrier, after the record
 #endif
   __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
-  __shared__ int guide[kGuide];
+  __shared__ GuideEnt guide[kGuide];
   __shared__ tpe_best wb[kTabThreads / 64];
   const int lane = threadIdx.x & 63;
   [[maybe_unused]] const int wave = threadIdx.x >> 6;
@@ -995,11 +1032,17 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           }
         }
         __syncthreads();
-        if (in_lds && threadIdx.x < kGuide) {          // first k with cum_k > b / kGuide
+        if (in_lds && threadIdx.x < kGuide) {          // first k with cum_k > b / kGuide, its two steps
           const double v = (double)threadIdx.x / (double)kGuide;
-          int a = 0, b = p.samp_len - 1;
+          const int len = p.samp_len;
+          int a = 0, b = len - 1;
           while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
-          guide[threadIdx.x] = a;
+          GuideEnt e;
+          e.k0 = a;
+          e.c0 = a < len - 1 ? cum_lds[a] : INFINITY;
+          e.c1 = a + 1 < len - 1 ? cum_lds[a + 1] : INFINITY;
+          e.pad0 = e.pad1 = e.pad2 = 0;
+          guide[threadIdx.x] = e;
         }
         __syncthreads();
       }
@@ -1037,8 +1080,13 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     // cells; TL: the tables are in LDS (separate instantiations, so every table
     // read is a plain LDS or global load, never a generic one); NPC: candidates
     // per thread (kTabPer, or 2 kTabPer for a tile pair)
-    auto cells_pass = [&](auto TL, auto NPC) {
+    // FASTC: the production case (tables in LDS, device draws from the staged
+    // sampler, no per-candidate outputs) in phases without branches — every
+    // candidate's guide lookup, then its sampler row and inverse CDF, then its
+    // two cell rows — so the thread's candidates' LDS reads overlap
+    auto cells_pass = [&](auto TL, auto NPC, auto FASTC) {
         constexpr int NP = decltype(NPC)::value;
+        constexpr bool kFast = decltype(FASTC)::value;
         const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
         const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
         const int n0 = p.tab_n[0], n1 = p.tab_n[1];
@@ -1066,8 +1114,42 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             for (int j = 0; j < NP; ++j) du[j] = draw_uniforms(p, first + j, TPE_PREC_F32);
           }
         }
+        if constexpr (kFast) {
+          static_assert(kL, "the fast cells pass reads LDS tables");
+          int kc[NP];
+          unsigned more = 0;
 #pragma unroll
-        for (int j = 0; j < NP; ++j) {
+          for (int j = 0; j < NP; ++j) {
+            bool m;
+            kc[j] = guided_comp(guide, du[j].us, m);
+            more |= (unsigned)m << j;
+          }
+          if (__ballot(more != 0u)) {                 // (rare: a guide slice with 2+ component edges)
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+              if ((more >> j) & 1u) kc[j] = guided_more(cum_lds, p.samp_len, du[j].us, kc[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            const float4 s = row_lds[kc[j]];
+            const float pr = s.z + du[j].uf * (s.w - s.z);
+            const float z = ndtri_f32(pr);
+            const float xf = s.x + s.y * z;
+            tj[j] = fminf(fmaxf(xf == xf ? xf : s.x, lo_f), hi_f);
+          }
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            const int i = first + j;
+            const float t = tj[j];
+            const float lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, r0, stride, t),
+                        la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, r1, stride, t);
+            const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
+            exact |= (unsigned)(valid && !ok) << j;
+            if (valid && ok) track(i, lb2, la2, t);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NP && !kFast; ++j) {
           const int i = first + j;
           tj[j] = NAN;
           if (i >= p.n_cand) continue;
@@ -1076,7 +1158,9 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           if (!draw) {
             t = coord[o];
           } else if (in_lds) {
-            const int a = guided_comp(cum_lds, guide, p.samp_len, du[j].us);
+            bool more;
+            int a = guided_comp(guide, du[j].us, more);
+            if (more) a = guided_more(cum_lds, p.samp_len, du[j].us, a);
             const float4 s = row_lds[a];
             const float pr = s.z + du[j].uf * (s.w - s.z);
             const float z = ndtri_f32(pr);
@@ -1134,8 +1218,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       if (cells) {
         using P2 = std::integral_constant<int, kTabPer>;
         using P4 = std::integral_constant<int, 2 * kTabPer>;
-        if (tab_in_lds) { if (pair) cells_pass(std::true_type{}, P4{}); else cells_pass(std::true_type{}, P2{}); }
-        else { if (pair) cells_pass(std::false_type{}, P4{}); else cells_pass(std::false_type{}, P2{}); }
+        using T = std::true_type;
+        using F = std::false_type;
+#ifndef TPE_NO_FAST_CELLS                           // (A/B builds: the general pass only)
+        if (tab_in_lds && draw && in_lds && !need_x) { if (pair) cells_pass(T{}, P4{}, T{}); else cells_pass(T{}, P2{}, T{}); }
+        else
+#endif
+        if (tab_in_lds) { if (pair) cells_pass(T{}, P4{}, F{}); else cells_pass(T{}, P2{}, F{}); }
+        else { if (pair) cells_pass(F{}, P4{}, F{}); else cells_pass(F{}, P2{}, F{}); }
       }
     }
     if (pair) ++gi;                                  // the pair's second tile is done
@@ -1163,7 +1253,9 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       for (int j = 0; j < kTabPer; ++j) {
         const int i = first + j;
         if (i >= p.n_cand) break;
-        const int a = guided_comp(cum_lds, guide, p.samp_len, du[j].us);
+        bool more;
+        int a = guided_comp(guide, du[j].us, more);
+        if (more) a = guided_more(cum_lds, p.samp_len, du[j].us, a);
         const float4 sr = row_lds[a];
         const float pr = sr.z + du[j].uf * (sr.w - sr.z);
         const float z = ndtri_f32(pr);
@@ -2613,21 +2705,25 @@ __device__ __forceinline__ const uint32_t* ord_idx(const tpe_fit_job& j) {
 // Per-job scalars of the build, at the head of the job's fit_keys segment
 // (free once the merge has run): the prior's position, the combined chunk
 // statistics, then the chunks' statistics (FitPart, 12 doubles each).
-constexpr int kFitHdrPos = 0, kFitHdrStats = 1, kFitHdrParts = 8;
+constexpr int kFitHdrPos = 0, kFitHdrStats = 1, kFitHdrGrid = 6, kFitHdrParts = 8;
 
 // position of each below observation in the job's order (binary search for its
-// own (t, i) pair) -> pos[seg_off + b]; and the prior's position among the
-// above observations (np.searchsorted(side='left') of prior_mu, tpe.py:427-431):
-// the observations < prior_mu in the whole order less the below ones
+// own (t, i) pair), written SORTED and as adj[k] = pos_k - k (pos_k: the k-th
+// smallest position) -> adj[seg_off + k]: the above observation q of the order
+// (the compacted index) sits at position q + #{k : adj[k] <= q}; and the
+// prior's position among the above observations (np.searchsorted(side='left')
+// of prior_mu, tpe.py:427-431): the observations < prior_mu in the whole order
+// less the below ones
 constexpr int kFitMaxBelow = 64;
 __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* __restrict__ J,
                                                             const int32_t* __restrict__ below_idx,
-                                                            uint32_t* __restrict__ pos, double* __restrict__ hdr) {
+                                                            uint32_t* __restrict__ adj, double* __restrict__ hdr) {
   const tpe_fit_job& j = J[blockIdx.x];
   const int b = threadIdx.x;
   const double* __restrict__ ok = ord_keys(j);
   const uint32_t* __restrict__ ov = ord_idx(j);
   bool under = false;
+  uint32_t mine = 0xFFFFFFFFu;
   if (b < j.n_below) {
     const uint32_t i = (uint32_t)below_idx[j.below_off + b];
     const double t = fit_coord(j, i);
@@ -2638,8 +2734,11 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
       if (ord_lt(ok[md], ov[md], t, i)) lo = md + 1;
       else hi = md;
     }
-    pos[j.seg_off + b] = (uint32_t)lo;
+    mine = (uint32_t)lo;
   }
+  int r = 0;                                        // rank of this position (positions are distinct)
+  for (int q = 0; q < j.n_below; ++q) r += __shfl(mine, q) < mine;
+  if (b < j.n_below) adj[j.seg_off + r] = mine - (uint32_t)r;
   const int n_under = __popcll(__ballot(under));
   if (b == 0) {
     int64_t lo = 0, hi = j.n_obs;                   // observations with t < prior_mu (NaN last)
@@ -2652,56 +2751,28 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
   }
 }
 
-// compact: the order without the below observations, each with its rank among
-// the above observations in tid order -> (keys_sorted, ranks) at seg_off
-constexpr int kCompactThreads = 256;
-constexpr int kCompactTile = 4096;
-__global__ __launch_bounds__(kCompactThreads) void k_ord_compact(const tpe_fit_job* __restrict__ J,
-                                                                 const int32_t* __restrict__ below_idx,
-                                                                 const uint32_t* __restrict__ pos,
-                                                                 double* __restrict__ keys_sorted,
-                                                                 uint32_t* __restrict__ ranks) {
-  const tpe_fit_job& j = J[blockIdx.y];
-  const int64_t s0 = (int64_t)blockIdx.x * kCompactTile;
-  if (s0 >= j.n_obs) return;
-  __shared__ uint32_t bp[kFitMaxBelow], bi[kFitMaxBelow];
-  const int nb = j.n_below;
-  if (threadIdx.x < nb) {
-    bp[threadIdx.x] = pos[j.seg_off + threadIdx.x];
-    bi[threadIdx.x] = (uint32_t)below_idx[j.below_off + threadIdx.x];
-  }
-  __syncthreads();
-  const double* __restrict__ ok = ord_keys(j);
-  const uint32_t* __restrict__ ov = ord_idx(j);
-  const int64_t s1 = min(s0 + kCompactTile, j.n_obs);
-  for (int64_t s = s0 + threadIdx.x; s < s1; s += kCompactThreads) {
-    const uint32_t i = ov[s];
-    int before = 0, older = 0;
-    bool below = false;
-    for (int b = 0; b < nb; ++b) {
-      before += bp[b] < (uint32_t)s;
-      below = below || bp[b] == (uint32_t)s;
-      older += bi[b] < i;
-    }
-    if (below) continue;
-    const int64_t o = j.seg_off + s - before;
-    keys_sorted[o] = ok[s];
-    ranks[o] = i - (uint32_t)older;
-  }
-}
-
-// ---- build: adaptive_parzen_normal over the compacted above order ----
-// Three launches over (chunk of kFitChunk components) x job, so a 100k-
-// component mixture spreads over ~50 workgroups instead of one:
-//   k_fit_stats  per chunk: the normaliser W, the acceptance mass M, the
-//                shift cm = max log2(w / sigma), the wide-threshold statistics
-//   k_fit_emit   the job's chunk statistics combined (fixed chunk order, the
-//                same in every workgroup), then the chunk's {mu, a, c} rows,
-//                its wide candidates and its grid buckets
-//   k_fit_wide   the wide list (fixed index order) and the problem rows
+// ---- build: adaptive_parzen_normal over the above observations of the order ----
+// The order holds every observation; the above ones are those at positions not
+// in the job's below list (k_ord_below).  Nothing is compacted in HBM: each
+// chunk's workgroup stages its above observations — keys, and their ranks among
+// the above observations in tid order (the linear-forgetting weight index) —
+// into LDS from the contiguous stretch of the order that holds them.  Launches
+// over (chunk of kFitChunk components) x job, so a 100k-component mixture
+// spreads over ~50 workgroups instead of one:
+//   k_fit_stats   per chunk: the normaliser W, the acceptance mass M, the
+//                 shift cm = max log2(w / sigma), the wide-threshold statistics
+//   k_fit_combine the job's chunk statistics combined (fixed chunk order)
+//   k_fit_emit    the chunk's {mu, a, c} rows, its wide candidates and the grid
+//                 buckets whose first component lies in the chunk
+//   k_fit_wide    the wide list (fixed index order) and the problem rows
 constexpr int kFitChunk = 2048;
 constexpr int kFitThreads = 256;
 constexpr int kFitPer = kFitChunk / kFitThreads;
+constexpr int kFitStage = kFitChunk + 3;         // a chunk's above observations and their neighbours
+// positions of the order a staging thread reads: the stretch holding kFitStage
+// above observations holds at most kFitMaxBelow below ones too
+constexpr int kFitStagePer = 9;
+static_assert(kFitStagePer * 256 >= kFitChunk + 3 + 64, "staging covers the stretch");
 constexpr int kThr = 5;                          // wide if sigma > smin * 2^(m+1), m < kThr
 struct FitPart {                                 // one chunk's statistics (fit scratch, 8-B aligned)
   double W, M;
@@ -2712,17 +2783,57 @@ struct FitPart {                                 // one chunk's statistics (fit 
   int32_t pad;
 };
 
+// above observation q of a job (its order index among the above observations)
+// read through the sorted below positions in global memory: position q +
+// #{k : adj[k] <= q} of the order (the wide list, the grid bounds)
+struct AboveSrc {
+  const double* ok;
+  const uint32_t* ov;
+  const uint32_t* adj;       // k_ord_below
+  const int32_t* bidx;       // the job's below indices into obs, ascending
+  int nb;
+  __device__ __forceinline__ int64_t at(int64_t q) const {
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)adj[m] <= q) lo = m + 1; else hi = m;
+    }
+    return q + lo;
+  }
+  __device__ __forceinline__ double key(int64_t q) const { return ok[at(q)]; }
+  __device__ __forceinline__ uint32_t rank(int64_t q) const {   // its index in obs less the older below ones
+    const uint32_t i = ov[at(q)];
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((uint32_t)bidx[m] < i) lo = m + 1; else hi = m;
+    }
+    return i - (uint32_t)lo;
+  }
+};
+
+// a chunk's above observations [qa, qa + kFitStage) staged in LDS (fit_stage)
+struct LdsSrc {
+  const double* k;
+  const uint32_t* r;
+  int64_t qa;
+  __device__ __forceinline__ double key(int64_t q) const { return k[q - qa]; }
+  __device__ __forceinline__ uint32_t rank(int64_t q) const { return r[q - qa]; }
+};
+
 // the view of one job's sorted above observations with the prior inserted at
 // pos (np.searchsorted(side='left'), tpe.py:427-431) and its bandwidth rules
+template <class Src>
 struct FitCtx {
-  const double* s;       // sorted above observations
-  const uint32_t* rank;  // their ranks in tid order
+  Src src;               // sorted above observations and their ranks in tid order
   int64_t n, K, pos;
   double pmu, psig, pw, smin, smax, start, step;
   int64_t num;
   bool ramp, bounded;
   double low, high;
-  __device__ __forceinline__ double mu(int64_t i) const { return i < pos ? s[i] : (i == pos ? pmu : s[i - 1]); }
+  __device__ __forceinline__ double mu(int64_t i) const {
+    return i < pos ? src.key(i) : (i == pos ? pmu : src.key(i - 1));
+  }
   __device__ __forceinline__ double sigma(int64_t i) const {          // tpe.py:441-470
     if (i == pos) return psig;
     double sg;
@@ -2734,7 +2845,7 @@ struct FitCtx {
   __device__ __forceinline__ double weight(int64_t i) const {         // tpe.py:381-394, 454-460
     if (i == pos) return pw;
     if (!ramp) return 1.0;
-    const int64_t r = rank[i < pos ? i : i - 1];
+    const int64_t r = src.rank(i < pos ? i : i - 1);
     if (r >= num) return 1.0;
     if (r == num - 1) return 1.0;
     if (num == 1) return start;
@@ -2751,13 +2862,12 @@ __device__ __forceinline__ double ncdf(double x, double mu, double sigma) {   //
   return 0.5 * (1.0 + erf_sat((x - mu) / fmax(1.4142135623730951 * sigma, kEPS)));
 }
 
-__device__ FitCtx fit_ctx(const tpe_fit_job& j, const double* __restrict__ keys_sorted,
-                          const uint32_t* __restrict__ ranks, int64_t pos) {
-  FitCtx c;
+template <class Src>
+__device__ __forceinline__ FitCtx<Src> fit_ctx(const tpe_fit_job& j, Src src, int64_t pos) {
+  FitCtx<Src> c;
+  c.src = src;
   c.n = j.n_obs - j.n_below;
   c.K = c.n + 1;
-  c.s = keys_sorted + j.seg_off;
-  c.rank = ranks + j.seg_off;
   c.pos = pos;
   c.pmu = j.prior_mu; c.psig = j.prior_sigma; c.pw = j.prior_weight;
   c.smax = j.prior_sigma;
@@ -2771,25 +2881,97 @@ __device__ FitCtx fit_ctx(const tpe_fit_job& j, const double* __restrict__ keys_
   return c;
 }
 
+__device__ __forceinline__ AboveSrc above_src(const tpe_fit_job& j, const int32_t* __restrict__ below_idx,
+                                              const uint32_t* __restrict__ adj) {
+  return AboveSrc{ord_keys(j), ord_idx(j), adj + j.seg_off, below_idx + j.below_off, j.n_below};
+}
+
+// Stages the above observations q in [qa, qb) of job j (qb - qa <= kFitStage)
+// into lk / lr: every position of the order's stretch that holds them, less
+// the below positions (s_bp: sorted, LDS), keys and ranks (s_bi: the below
+// indices into obs, ascending, LDS).  Block-wide; the caller synchronises.
+__device__ void fit_stage(const tpe_fit_job& j, const uint32_t* s_bp, const uint32_t* s_bi, int64_t qa, int64_t qb,
+                          double* lk, uint32_t* lr) {
+  const double* __restrict__ ok = ord_keys(j);
+  const uint32_t* __restrict__ ov = ord_idx(j);
+  const int nb = j.n_below;
+  auto at = [&](int64_t q) {                          // position of above observation q
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)s_bp[m] - m <= q) lo = m + 1; else hi = m;
+    }
+    return q + lo;
+  };
+  const int64_t fa = at(qa), fb = at(qb - 1) + 1;
+  // every position's loads first (independent), then the searches and stores
+  double kv[kFitStagePer];
+  uint32_t iv[kFitStagePer];
+#pragma unroll
+  for (int e = 0; e < kFitStagePer; ++e) {
+    const int64_t f = fa + e * kFitThreads + threadIdx.x;
+    if (f < fb) { kv[e] = ok[f]; iv[e] = ov[f]; }
+  }
+#pragma unroll
+  for (int e = 0; e < kFitStagePer; ++e) {
+    const int64_t f = fa + e * kFitThreads + threadIdx.x;
+    if (f >= fb) break;
+    int lo = 0, hi = nb;                              // below positions before f
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)s_bp[m] < f) lo = m + 1; else hi = m;
+    }
+    if (lo < nb && (int64_t)s_bp[lo] == f) continue;
+    const int64_t q = f - lo;
+    const uint32_t i = iv[e];
+    int a = 0, b = nb;                                // below indices older than i
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      if (s_bi[m] < i) a = m + 1; else b = m;
+    }
+    lk[q - qa] = kv[e];
+    lr[q - qa] = i - (uint32_t)a;
+  }
+}
+
+// the job's sorted below positions and below indices into LDS (block-wide)
+__device__ __forceinline__ void fit_below_lds(const tpe_fit_job& j, const int32_t* __restrict__ below_idx,
+                                              const uint32_t* __restrict__ adj, uint32_t* s_bp, uint32_t* s_bi) {
+  if ((int)threadIdx.x < j.n_below) {
+    s_bp[threadIdx.x] = adj[j.seg_off + threadIdx.x] + threadIdx.x;
+    s_bi[threadIdx.x] = (uint32_t)below_idx[j.below_off + threadIdx.x];
+  }
+}
+
 __device__ __forceinline__ FitPart* fit_parts(const tpe_fit_job& j, double* scratch) {
   return reinterpret_cast<FitPart*>(scratch + j.seg_off + kFitHdrParts);
 }
 static_assert(sizeof(FitPart) == 12 * sizeof(double), "FitPart: 12 doubles");
+static_assert(kFitThreads >= kFitMaxBelow, "a fit workgroup stages the below list in one round");
 
 struct FitStats {
   double W, M, cm, thr, s_narrow;
 };
 
 __global__ __launch_bounds__(kFitThreads) void k_fit_stats(const tpe_fit_job* __restrict__ J,
-                                                           const double* __restrict__ keys_sorted,
-                                                           const uint32_t* __restrict__ ranks,
+                                                           const int32_t* __restrict__ below_idx,
+                                                           const uint32_t* __restrict__ adj,
                                                            double* __restrict__ scratch,
                                                            uint32_t* __restrict__ wide_scratch) {
   const tpe_fit_job& j = J[blockIdx.y];
   const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
   if (c0 >= K) return;
+  const int64_t c1 = min(c0 + kFitChunk, K);
   if (blockIdx.x == 0 && threadIdx.x == 0) wide_scratch[j.seg_off] = 0u;   // the wide list's counter
-  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)scratch[j.seg_off + kFitHdrPos]);
+  __shared__ uint32_t s_bp[kFitMaxBelow], s_bi[kFitMaxBelow];
+  __shared__ double lk[kFitStage];
+  __shared__ uint32_t lr[kFitStage];
+  fit_below_lds(j, below_idx, adj, s_bp, s_bi);
+  __syncthreads();
+  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
+  fit_stage(j, s_bp, s_bi, qa, qb, lk, lr);
+  __syncthreads();
+  const FitCtx<LdsSrc> c = fit_ctx(j, LdsSrc{lk, lr, qa}, (int64_t)scratch[j.seg_off + kFitHdrPos]);
   double W = 0, M = 0, cm = 0.0, sm_all = 0;      // (cm: the largest ratio w / sigma)
   double sm[kThr];
   int cnt[kThr];
@@ -2798,7 +2980,7 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_stats(const tpe_fit_job* __
 #pragma unroll 1
   for (int e = 0; e < kFitPer; ++e) {
     const int64_t i = c0 + e * kFitThreads + threadIdx.x;
-    if (i >= K) break;
+    if (i >= c1) break;
     const double sg = c.sigma(i), w = c.weight(i);
     W += w;
     if (c.bounded) {
@@ -2842,9 +3024,17 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_stats(const tpe_fit_job* __
 }
 
 // the job's chunk statistics combined once (fixed chunk order) into the header
-__global__ __launch_bounds__(64) void k_fit_combine(const tpe_fit_job* __restrict__ J, double* __restrict__ scratch) {
+__global__ __launch_bounds__(64) void k_fit_combine(const tpe_fit_job* __restrict__ J,
+                                                    const int32_t* __restrict__ below_idx,
+                                                    const uint32_t* __restrict__ adj, double* __restrict__ scratch) {
   const tpe_fit_job& j = J[blockIdx.x];
   const int64_t K = j.n_obs - j.n_below + 1;
+  if (threadIdx.x == 0) {
+    // the grid's bounds, the f32 means of the first and last component (emit, wide)
+    const FitCtx<AboveSrc> cg = fit_ctx(j, above_src(j, below_idx, adj), (int64_t)scratch[j.seg_off + kFitHdrPos]);
+    scratch[j.seg_off + kFitHdrGrid] = (double)(float)cg.mu(0);
+    scratch[j.seg_off + kFitHdrGrid + 1] = (double)(float)cg.mu(K - 1);
+  }
   const int nc = (int)((K + kFitChunk - 1) / kFitChunk);
   const FitPart* __restrict__ parts = fit_parts(j, scratch);
   __shared__ FitPart lp[64];
@@ -2875,26 +3065,41 @@ __global__ __launch_bounds__(64) void k_fit_combine(const tpe_fit_job* __restric
   }
 }
 
+// The chunk's rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and
+// sigma > thr) get c = -inf in the sorted list and are listed apart.  Grid over
+// the f32 means: grid[g] = the first component with mu32 >= edge_g, edge_g =
+// glo + g / ginv (grid[G] = K); the chunk writes the buckets whose answer lies
+// in it (a binary search over its staged means) — the buckets g with
+// mu32[c0 - 1] < edge_g <= mu32[c1 - 1] (the last chunk: every g from there up,
+// K when no mean reaches edge_g).
 __global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __restrict__ J,
-                                                          const double* __restrict__ keys_sorted,
-                                                          const uint32_t* __restrict__ ranks,
+                                                          const int32_t* __restrict__ below_idx,
+                                                          const uint32_t* __restrict__ adj,
                                                           const double* __restrict__ scratch,
                                                           uint32_t* __restrict__ wide_scratch,
-                                                          float4* __restrict__ comp) {
+                                                          float4* __restrict__ comp, int32_t* __restrict__ grid) {
   const tpe_fit_job& j = J[blockIdx.y];
   const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
   if (c0 >= K) return;
+  const int64_t c1 = min(c0 + kFitChunk, K);
+  __shared__ uint32_t s_bp[kFitMaxBelow], s_bi[kFitMaxBelow];
+  __shared__ double lk[kFitStage];
+  __shared__ uint32_t lr[kFitStage];
+  fit_below_lds(j, below_idx, adj, s_bp, s_bi);
+  __syncthreads();
+  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
+  fit_stage(j, s_bp, s_bi, qa, qb, lk, lr);
+  __syncthreads();
   const double* __restrict__ hdr = scratch + j.seg_off;
-  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)hdr[kFitHdrPos]);
+  const int64_t pos = (int64_t)hdr[kFitHdrPos];
+  const FitCtx<LdsSrc> c = fit_ctx(j, LdsSrc{lk, lr, qa}, pos);
   const double cm = hdr[kFitHdrStats + 2], thr = hdr[kFitHdrStats + 3];
-  // rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and sigma >
-  // thr) get c = -inf in the sorted list and are listed apart
   float4* __restrict__ C = comp + j.above_off;
   uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
 #pragma unroll 2
   for (int e = 0; e < kFitPer; ++e) {
     const int64_t i = c0 + e * kFitThreads + threadIdx.x;
-    if (i >= K) break;
+    if (i >= c1) break;
     const double sg = c.sigma(i), w = c.weight(i), mu = c.mu(i);
     const double se = fmax(sg, kEPS);
     const float hi = (float)mu;
@@ -2906,49 +3111,59 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __r
       if (slot < (uint32_t)kPruneWide) wl[1 + slot] = (uint32_t)i;
     }
   }
-}
-
-// grid over the f32 means: grid[g] = the first component with mu32 >= edge_g,
-// edge_g = glo + g / ginv — a binary search per bucket over the sorted means
-// (the prior inserted), grid[G] = K
-constexpr int kGridThreads = 256;
-constexpr int kFitMaxGrid = 4096;                // grid_n = min(4096, 4K) (tpe_host_pack_level)
-__global__ __launch_bounds__(kGridThreads) void k_fit_grid(const tpe_fit_job* __restrict__ J,
-                                                           const double* __restrict__ keys_sorted,
-                                                           const uint32_t* __restrict__ ranks,
-                                                           const double* __restrict__ scratch,
-                                                           int32_t* __restrict__ grid) {
-  const tpe_fit_job& j = J[blockIdx.y];
+  // ---- grid buckets of this chunk ----
   const int G = j.grid_n;
-  const int g = (int)blockIdx.x * kGridThreads + (int)threadIdx.x;
-  if (g > G) return;
-  const int64_t n = j.n_obs - j.n_below, K = n + 1;
-  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)scratch[j.seg_off + kFitHdrPos]);
   int32_t* __restrict__ Gp = grid + j.grid_off;
-  if (g == G) { Gp[G] = (int32_t)K; return; }
-  const double glo = (double)(float)c.mu(0), ghi = (double)(float)c.mu(K - 1);
-  const float ginv = ghi > glo ? (float)((double)G / (ghi - glo)) : 0.f;
-  if (!(ginv > 0.f)) { Gp[g] = 0; return; }
-  const double edge = glo + (double)g / (double)ginv;
-  int64_t lo = 0, hi = K;                        // first i with !(mu32[i] < edge)
-  while (lo < hi) {
-    const int64_t md = (lo + hi) >> 1;
-    if ((double)(float)c.mu(md) < edge) lo = md + 1;
-    else hi = md;
+  __shared__ int s_ga, s_gb;
+  __shared__ double s_glo;
+  __shared__ float s_ginv;
+  if (threadIdx.x == 0) {
+    const double glo = hdr[kFitHdrGrid], ghi = hdr[kFitHdrGrid + 1];
+    const float ginv = ghi > glo ? (float)((double)G / (ghi - glo)) : 0.f;
+    int ga, gb;
+    if (!(ginv > 0.f)) {
+      ga = 0; gb = c0 == 0 ? G : 0;                  // every bucket 0, written by the first chunk
+    } else {
+      auto first_above = [&](double m) {             // first g in [0, G] with edge_g > m (G: none)
+        int lo = 0, hi = G;
+        while (lo < hi) {
+          const int md = (lo + hi) >> 1;
+          if (glo + (double)md / (double)ginv > m) hi = md; else lo = md + 1;
+        }
+        return lo;
+      };
+      ga = c0 == 0 ? 0 : first_above((double)(float)c.mu(c0 - 1));
+      gb = c1 == K ? G : first_above((double)(float)c.mu(c1 - 1));
+    }
+    s_ga = ga; s_gb = gb; s_glo = glo; s_ginv = ginv;
+    if (c0 == 0) Gp[G] = (int32_t)K;
   }
-  Gp[g] = (int32_t)lo;
+  __syncthreads();
+  const int ga = s_ga, gb = s_gb;
+  const double glo = s_glo;
+  const float ginv = s_ginv;
+  for (int g = ga + (int)threadIdx.x; g < gb; g += kFitThreads) {
+    if (!(ginv > 0.f)) { Gp[g] = 0; continue; }
+    const double edge = glo + (double)g / (double)ginv;
+    int64_t lo = c0, hi = c1;                      // first i with !(mu32[i] < edge) (c1: none in the chunk)
+    while (lo < hi) {
+      const int64_t md = (lo + hi) >> 1;
+      if ((double)(float)c.mu(md) < edge) lo = md + 1;
+      else hi = md;
+    }
+    Gp[g] = (int32_t)lo;
+  }
 }
 
 // the wide list in index order, its rows, and the job's problem rows:
 // lpdf = ln2 * log2(sum) + base; base = ln2*cm - ln(W sqrt(2 pi) p_accept)
 __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__ J,
-                                                 const double* __restrict__ keys_sorted,
-                                                 const uint32_t* __restrict__ ranks,
+                                                 const int32_t* __restrict__ below_idx,
+                                                 const uint32_t* __restrict__ adj,
                                                  const double* __restrict__ scratch,
                                                  const uint32_t* __restrict__ wide_scratch,
                                                  tpe_problem* __restrict__ P, float4* __restrict__ comp) {
   const tpe_fit_job& j = J[blockIdx.x];
-  const int64_t n = j.n_obs - j.n_below, K = n + 1;
   __shared__ int64_t wide_ix[kPruneWide];
   __shared__ int s_nw;
   const uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
@@ -2963,7 +3178,7 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
     s_nw = nw;
   }
   __syncthreads();
-  const FitCtx c = fit_ctx(j, keys_sorted, ranks, (int64_t)hdr[kFitHdrPos]);
+  const FitCtx<AboveSrc> c = fit_ctx(j, above_src(j, below_idx, adj), (int64_t)hdr[kFitHdrPos]);
   const FitStats st{hdr[kFitHdrStats], hdr[kFitHdrStats + 1], hdr[kFitHdrStats + 2], hdr[kFitHdrStats + 3],
                     hdr[kFitHdrStats + 4]};
   const int nw = s_nw;
@@ -2975,7 +3190,7 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
         make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - st.cm));
   }
   if ((int)threadIdx.x < j.n_problems) {
-    const double glo = (double)(float)c.mu(0), ghi = (double)(float)c.mu(K - 1);
+    const double glo = hdr[kFitHdrGrid], ghi = hdr[kFitHdrGrid + 1];
     const float ginv = ghi > glo ? (float)((double)j.grid_n / (ghi - glo)) : 0.f;
     const double pa = c.bounded ? st.M / st.W : 1.0;
     tpe_problem& p = P[j.problem_first + threadIdx.x];
@@ -3178,27 +3393,21 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
                (double*)nullptr, (uint32_t*)nullptr, (int64_t)0);
     if ((rc = hip_check("tpe_fit_above/merge"))) return rc;
   }
-  // below positions in fit_vals (free once the merge has run), compaction into
-  // the sorted buffers, then the build
-  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, b->fit_vals, b->fit_keys);
-  const unsigned tiles_c = (unsigned)((b->fit_max_obs + kCompactTile - 1) / kCompactTile);
-  TPE_LAUNCH(k_ord_compact, dim3(tiles_c, b->n_fit), dim3(kCompactThreads), 0, s, b->fit, b->below_idx, b->fit_vals,
-             b->fit_keys_sorted, b->fit_vals_sorted);
-  if ((rc = hip_check("tpe_fit_above/compact"))) return rc;
-  // the build: chunk statistics (into fit_keys, free once the merge has run),
-  // rows + grid, the wide list (its counter and indices in fit_vals, free once
-  // the compaction has run) and the problem rows
+  // the sorted below positions (adj) in fit_vals_sorted (free once the merge
+  // has run), then the build over the order itself (no compaction): chunk
+  // statistics (into fit_keys, free once the merge has run), rows + grid
+  // buckets, the wide list (its counter and indices in fit_vals) and the
+  // problem rows
+  uint32_t* adj = b->fit_vals_sorted;
+  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, adj, b->fit_keys);
   const unsigned chunks_k = (unsigned)((b->fit_max_obs + 1 + kFitChunk - 1) / kFitChunk);
-  TPE_LAUNCH(k_fit_stats, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
-             b->fit_vals_sorted, b->fit_keys, b->fit_vals);
-  TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys);
-  TPE_LAUNCH(k_fit_emit, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->fit_keys_sorted,
-             b->fit_vals_sorted, b->fit_keys, b->fit_vals, (float4*)b->comp32);
-  TPE_LAUNCH(k_fit_wide, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys_sorted, b->fit_vals_sorted,
-             b->fit_keys, b->fit_vals, const_cast<tpe_problem*>(b->problems), (float4*)b->comp32);
-  const unsigned gblocks = (unsigned)((kFitMaxGrid + 1 + kGridThreads - 1) / kGridThreads);
-  TPE_LAUNCH(k_fit_grid, dim3(gblocks, b->n_fit), dim3(kGridThreads), 0, s, b->fit, b->fit_keys_sorted,
-             b->fit_vals_sorted, b->fit_keys, const_cast<int32_t*>(b->grid));
+  TPE_LAUNCH(k_fit_stats, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
+             b->fit_vals);
+  TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->below_idx, adj, b->fit_keys);
+  TPE_LAUNCH(k_fit_emit, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
+             b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid));
+  TPE_LAUNCH(k_fit_wide, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->below_idx, adj, b->fit_keys, b->fit_vals,
+             const_cast<tpe_problem*>(b->problems), (float4*)b->comp32);
   return hip_check("tpe_fit_above/build");
 }
 
@@ -3441,6 +3650,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   int rc = tpe_host_pack_level(labels, n_labels, n_cand, seed, cand_base, n_cand_global, precision, ws->pinned,
                                ws->pinned_bytes, &info);
   if (rc != TPE_OK && rc != TPE_E_SPACE) return fail(rc, "tpe_host_pack_level: bad level description");
+  tpe_internal_phase(TPE_PHASE_PACK);
   const int64_t P = info.n_problems, C = P * (int64_t)n_cand;
   const int64_t res_off = (info.blob_bytes + 255) & ~(int64_t)255;
   // early selection's per-run bests follow the results (host-visible)
@@ -3617,8 +3827,10 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     return rc;
   }
   e = rd ? hipSuccess : hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
+  tpe_internal_phase(TPE_PHASE_LAUNCHED);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+  tpe_internal_phase(TPE_PHASE_SYNCED);
   if (b.early_select) {
     // each tabulated problem: the best of its runs (np.argmax order), runs
     // enumerated exactly as the sample stage partitions the tile list
@@ -3640,6 +3852,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     }
   }
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));
+  tpe_internal_phase(TPE_PHASE_LEVEL);
   return g_prof.on ? profile_collect(b, info, xtmpl ? xtmpl : hp, xfirst, n_cand) : TPE_OK;
 }
 

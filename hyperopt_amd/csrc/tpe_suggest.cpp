@@ -13,6 +13,8 @@
 // decisions hyperopt_amd.tpe._choices_fused / _choices_philox make, without a
 // Python round trip per label.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -26,6 +28,17 @@ extern "C" int tpe_internal_exchange(const tpe_exchange* ex, void* stream, int32
                                      int64_t P, int32_t* status);     // tpe_kernels.hip (hidden)
 
 namespace {
+
+// host phase clock (include/tpe_hip.h "Host phase clock")
+std::atomic<int> g_ph_on{0};
+double g_ph[TPE_N_PHASES];
+std::chrono::steady_clock::time_point g_ph_t0;
+
+void phase_start() {
+  if (!g_ph_on.load(std::memory_order_relaxed)) return;
+  g_ph_t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < TPE_N_PHASES; ++i) g_ph[i] = -1.0;
+}
 
 constexpr int kInactive = -2;   // label not active (None)
 constexpr int kActive = -1;     // active label that gates nothing (placeholder)
@@ -277,12 +290,25 @@ void label_rec(const Tree& T, const tpe_tree_label& L, const Fit& f, const int64
 
 extern "C" {
 
-int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
-                     double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
-                     int64_t cand_base, int64_t n_cand_global, const tpe_exchange* ex,
-                     uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
-                     const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
-                     int32_t* path, int8_t* need_fit) {
+// phase mark for tpe_level_run (tpe_kernels.hip)
+__attribute__((visibility("hidden"))) void tpe_internal_phase(int i) {
+  if (!g_ph_on.load(std::memory_order_relaxed) || i < 0 || i >= TPE_N_PHASES) return;
+  g_ph[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g_ph_t0).count();
+}
+
+int tpe_host_phases(int32_t enable, double* last, int32_t n) {
+  if (last && n > 0) memcpy(last, g_ph, sizeof(double) * (size_t)std::min<int32_t>(n, TPE_N_PHASES));
+  if (enable && !g_ph_on.load()) for (int i = 0; i < TPE_N_PHASES; ++i) g_ph[i] = -1.0;
+  g_ph_on.store(enable ? 1 : 0);
+  return TPE_OK;
+}
+
+static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
+                        double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
+                        int64_t cand_base, int64_t n_cand_global, const tpe_exchange* ex,
+                        uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
+                        const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
+                        int32_t* path, int8_t* need_fit) {
   if (n_labels < 0 || n_ids < 0 || n_cand < 0 || n_below < 0 || (n_labels > 0 && !labels) || (n_ids > 0 && !ids) ||
       (n_below > 0 && !below_tids) || !ws || !need || !path || (n_labels > 0 && n_ids > 0 && (!values || !active)) ||
       cand_base < 0 || n_cand_global < 0 || (n_cand_global > 0 && cand_base + n_cand > n_cand_global) ||
@@ -325,6 +351,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
   }
   if (n_labels == 0 || n_ids == 0) return TPE_OK;
   prefit(T);
+  tpe_internal_phase(TPE_PHASE_PREFIT);
   const int32_t run_flags = flags & ~TPE_TREE_NO_SPECULATE;
   std::vector<tpe_label_in>& recs = recs_tl;
   std::vector<tpe_result>& res = res_tl;
@@ -451,6 +478,20 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
     }
   }
   return TPE_OK;
+}
+
+int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64_t* below_tids, int64_t n_below,
+                     double prior_weight, int32_t lf, const int64_t* ids, int32_t n_ids, int32_t n_cand,
+                     int64_t cand_base, int64_t n_cand_global, const tpe_exchange* ex,
+                     uint64_t seed, double speculate_min_draws, int64_t device_fit_min, int32_t flags,
+                     const tpe_level_ws* ws, tpe_level_need* need, void* stream, double* values, int8_t* active,
+                     int32_t* path, int8_t* need_fit) {
+  phase_start();
+  const int rc = suggest_tree(labels, n_labels, below_tids, n_below, prior_weight, lf, ids, n_ids, n_cand, cand_base,
+                              n_cand_global, ex, seed, speculate_min_draws, device_fit_min, flags, ws, need, stream,
+                              values, active, path, need_fit);
+  tpe_internal_phase(TPE_PHASE_RETURN);
+  return rc;
 }
 
 }  // extern "C"

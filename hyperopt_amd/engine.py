@@ -132,6 +132,24 @@ class LevelProblem(object):
         self.inject = inject
 
 
+class _TreeIO(object):
+    """Engine.suggest_tree's argument and result arrays (grown, never shrunk)
+    with their addresses looked up once."""
+
+    def __init__(self, n, nl, nb, old=None):
+        if old is not None:
+            n, nl, nb = max(n, old.n_cap), max(nl, old.l_cap), max(nb, old.b_cap)
+        self.n_cap, self.l_cap, self.b_cap = n, nl, max(nb, 64)
+        self.ids = np.zeros(n, dtype=np.int64)
+        self.below = np.zeros(self.b_cap, dtype=np.int64)
+        self.values = np.zeros(n * nl)
+        self.active = np.ones(n * nl, dtype=np.int8)
+        self.need_fit = np.zeros(nl, dtype=np.int8)
+        self.ids_ptr, self.below_ptr = self.ids.ctypes.data, self.below.ctypes.data
+        self.values_ptr, self.active_ptr = self.values.ctypes.data, self.active.ctypes.data
+        self.need_fit_ptr = self.need_fit.ctypes.data
+
+
 class Engine(object):
     """Per-device engine.  ``precision`` is 'fp32' (default, performance) or
     'fp64' (parity mode: float64 continuous families)."""
@@ -154,6 +172,7 @@ class Engine(object):
         self._pinned = None
         self._ws = None                   # cached tpe_level_ws (run_level)
         self._tree_out = ((ctypes.c_int32 * 2)(), N.LevelNeed())   # suggest_tree's path / need records
+        self._tree_io = None              # suggest_tree's argument / result buffers (_TreeIO)
         # when a dict: every run() times each stage with HIP events on the
         # launch stream and appends (ms, CE of the launch) under the kernel name;
         # profile_repeat > 1 re-issues each (idempotent) stage back to back and
@@ -627,26 +646,34 @@ class Engine(object):
         return out
 
     def suggest_tree(self, labels, below_sorted, prior_weight, lf, ids, n_cand, seed, min_draws, flags=0,
-                     shard=None, exchange=None):
+                     shard=None, exchange=None, labels_ptr=None):
         """A whole tpe.suggest of a tree space in one native call
         (tpe_suggest_tree): fits, gate prediction and level runs.  ``labels``:
-        TREE_LABEL_DTYPE records in label order; ``below_sorted``: int64
-        ascending below tids; ``shard`` = (rank, world) with ``exchange`` (a
-        dist._Exchange): this rank scores its range of the ``n_cand``
-        candidates and the native call exchanges every level's results.
-        Returns (values, active) [n_ids x n_labels], or (None, need_fit) on
-        TPE_E_FALLBACK: need_fit [n_labels] flags the labels the caller must
-        fit and pass back (none: take the general path)."""
+        TREE_LABEL_DTYPE records in label order (``labels_ptr``: their address,
+        when the caller keeps it); ``below_sorted``: int64 ascending below
+        tids; ``shard`` = (rank, world) with ``exchange`` (a dist._Exchange):
+        this rank scores its range of the ``n_cand`` candidates and the native
+        call exchanges every level's results.
+        Returns (values, active) [n_ids x n_labels] — views of the engine's
+        result buffers, valid until its next suggest_tree — or (None,
+        need_fit) on TPE_E_FALLBACK: need_fit [n_labels] flags the labels the
+        caller must fit and pass back (none: take the general path)."""
         if self.precision != 'fp32':
             return None, np.zeros(len(labels), dtype=np.int8)
-        ids = np.ascontiguousarray(ids, dtype=np.int64)
         n_cand = int(n_cand)
         if n_cand < 0 or n_cand >= 2 ** 31:
             raise ValueError('n_EI_candidates out of range: %r' % n_cand)
-        nl, n = len(labels), len(ids)
-        values = np.empty((n, nl))
-        active = np.empty((n, nl), dtype=np.int8)
-        need_fit = np.zeros(nl, dtype=np.int8)
+        nl, n, nb = len(labels), len(ids), len(below_sorted)
+        io = self._tree_io
+        if io is None or io.n_cap < n or io.l_cap < nl or io.b_cap < nb:
+            io = self._tree_io = _TreeIO(n, nl, nb, io)
+        # arguments into the persistent buffers (their addresses are cached:
+        # an ndarray's .ctypes costs microseconds per access)
+        io.ids[:n] = ids
+        io.below[:nb] = below_sorted
+        io.need_fit[:nl] = 0
+        if labels_ptr is None:
+            labels_ptr = labels.ctypes.data
         path, need = self._tree_out
         seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
         stream = self._stream()
@@ -662,23 +689,22 @@ class Engine(object):
             ex = exchange.ptr(nl * n)
         for attempt in range(8):          # a later tree level may need larger pools than the first
             ws = self._level_ws()
-            rc = self.lib.tpe_suggest_tree(labels.ctypes.data, nl, below_sorted.ctypes.data, len(below_sorted),
-                                           float(prior_weight), int(lf), ids.ctypes.data, n, c_loc, base, c_glob, ex,
-                                           seed64, float(min_draws), int(self.device_fit_min), fl, ctypes.byref(ws),
-                                           ctypes.byref(need), stream, values.ctypes.data, active.ctypes.data, path,
-                                           need_fit.ctypes.data)
+            rc = self.lib.tpe_suggest_tree(labels_ptr, nl, io.below_ptr, nb, float(prior_weight), int(lf), io.ids_ptr,
+                                           n, c_loc, base, c_glob, ex, seed64, float(min_draws),
+                                           int(self.device_fit_min), fl, ctypes.byref(ws), ctypes.byref(need), stream,
+                                           io.values_ptr, io.active_ptr, path, io.need_fit_ptr)
             if rc != N.E_SPACE:
                 break
             self._grow(need)
         if prof:
             self.lib.tpe_level_profile(0)
         if rc == N.E_FALLBACK:
-            return None, need_fit
+            return None, io.need_fit[:nl].copy()
         N.check(rc, self.lib, 'tpe_suggest_tree')
         self.last_tree_path = (int(path[0]), int(path[1]))
         if prof and path[1]:
             self._record_level_profile()
-        return values, active
+        return io.values[:n * nl].reshape(n, nl), io.active[:n * nl].reshape(n, nl)
 
     def _record_level_profile(self):
         """profile[stage] gets (ms, units, algorithmic CE) of every stage the

@@ -314,7 +314,7 @@ def _tree_labels(table, hist, engine=None):
     columns and orders stay put (DeviceColumns.version).  Quantized labels
     carry no columns: tpe_suggest_tree sends them to the caller whenever they
     need a fit.  Returns (records, keep-alive list, [(ValueOrder, n_obs) of
-    the device-fitted labels by label index]) or None."""
+    the device-fitted labels by label index], the records' address) or None."""
     st = _tree_static(table)
     if st is None:
         return None
@@ -371,7 +371,7 @@ def _tree_labels(table, hist, engine=None):
                     keep.append(o)
                     cols = cols[:2] + (o.ctypes.data,)
             rec['tids'], rec['values'], rec['order'] = cols
-    out = (arr, keep, devs)
+    out = (arr, keep, devs, arr.ctypes.data)
     holder.tree_memo = (table, n_docs, dev_min, out, dc.version if dc is not None else None)
     return out
 
@@ -409,13 +409,14 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
         fl &= ~N.F_PREFIT
         fl[list(hint)] |= N.F_PREFIT
         table._prefit_applied = (tl[0], hint)
-    st = {'arr': tl[0]}
+    st = {'arr': tl[0], 'ptr': tl[3]}
     host = {}
 
     def give(ix):                              # the general path's fit of label ix, for the native call
         if not host and 'fits' not in st:
             st['fits'] = _Fits(table, hist, below_tids, prior_weight, engine)
             st['arr'] = st['arr'].copy()
+            st['ptr'] = None
         row = table.rows[ix]
         post = st['fits'].get(row)
         if post.above is None:                 # (device-fitted: the general path)
@@ -440,7 +441,7 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     for attempt in range(table.n_levels + 1):
         values, active = engine.suggest_tree(st['arr'], below, prior_weight, DEFAULT_LF, new_ids, C, seed,
                                              SPECULATE_MIN_DRAWS if SPECULATE else -1.0, shard=shard,
-                                             exchange=ex)
+                                             exchange=ex, labels_ptr=st['ptr'])
         if values is not None:
             break
         need = np.flatnonzero(active)          # (need_fit on TPE_E_FALLBACK)
@@ -451,23 +452,25 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
                 return None
     else:
         return None
+    # (values / active: the engine's result buffers, consumed or copied here)
+    act_rows = active.tolist()
     # (only labels some id used: a branch switch drops the old branch's)
-    used = np.asarray(active).any(axis=0)
+    used = act_rows[0] if len(act_rows) == 1 else np.asarray(active).any(axis=0).tolist()
     table.native_fit_hint = tuple(ix for ix in host if used[ix])
-    table.native_used = tuple(np.flatnonzero(used).tolist())
+    table.native_used = tuple(i for i, u in enumerate(used) if u)
     # the device-fitted labels that ran hold their merged value orders now
     for ix, (order, n) in tl[2].items():
         if used[ix]:
             order.commit(n)
     if columns:
-        return ChoiceColumns(table.labels, values, np.asarray(active, dtype=bool))
+        return ChoiceColumns(table.labels, values.copy(), np.asarray(active, dtype=bool))
     order = table.level_order()
     cols = _tree_static(table)[2]
     if len(values) > 4:
         return _choice_dicts(order, cols, values, active)
     i64, f64 = np.int64, np.float64
     out = []
-    for act, v in zip(active.tolist(), values.tolist()):
+    for act, v in zip(act_rows, values.tolist()):
         d = dict.fromkeys(order)
         for label, ix, fam in cols:
             if act[ix]:              # the reference's value types: np.int64 categories, np.float64 values

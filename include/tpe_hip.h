@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 15
+#define TPE_ABI_VERSION 16
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -762,6 +762,24 @@ int tpe_level_profile(int32_t enable);
 /* the last profiled tpe_level_run: min(n, TPE_N_STAGES) records in stage
  * order; TPE_E_ARG if no run completed since the profiler was enabled */
 int tpe_level_profile_read(tpe_stage_prof* out, int32_t n);
+
+/* ------------------------------------------------------------------------
+ * Host phase clock of tpe_suggest_tree (tools/native_split.py).  While
+ * enabled, a call records the steady-clock microseconds since its entry at
+ * each phase below (a tree of several level runs: the last run's phases);
+ * phases a call does not reach stay -1.  Process-wide; profiling only.
+ * ---------------------------------------------------------------------- */
+#define TPE_PHASE_PREFIT   0   /* the up-front fits on the worker threads done   */
+#define TPE_PHASE_PACK     1   /* the level packed into the staging buffer       */
+#define TPE_PHASE_LAUNCHED 2   /* every kernel of the level issued               */
+#define TPE_PHASE_SYNCED   3   /* the stream synchronise returned                */
+#define TPE_PHASE_LEVEL    4   /* the level's results assembled                  */
+#define TPE_PHASE_RETURN   5   /* tpe_suggest_tree returns                       */
+#define TPE_N_PHASES       6
+
+/* enable (1) / disable (0); *last (if not NULL) gets min(n, TPE_N_PHASES)
+ * phase times of the last call (before this one changes the setting) */
+int tpe_host_phases(int32_t enable, double* last, int32_t n);
 
 #ifdef __cplusplus
 }

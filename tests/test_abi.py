@@ -165,7 +165,7 @@ def test_tree_labels_dtype_matches_ctypes():
 
 def _tree_call(table, hist, C, min_draws=64.0, flags=0, shard=None, ex=None, fit_min=16384, engine=None):
     from hyperopt_amd import history as H, tpe
-    arr, keep, _ = tpe._tree_labels(table, hist, engine)
+    arr, keep = tpe._tree_labels(table, hist, engine)[:2]
     below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
     ws, need = N.LevelWS(), N.LevelNeed()
     vals = np.empty((1, len(arr)))
@@ -228,7 +228,7 @@ def test_suggest_tree_hands_quantized_labels_back():
     from hyperopt_amd import tpe
     fits = tpe._Fits(domain.table, hist, H.split_below(hist, 0.25), 1.0, None)
     post = fits.get(domain.table.by_label['q'])
-    arr, keep, _ = tpe._tree_labels(domain.table, hist)
+    arr, keep = tpe._tree_labels(domain.table, hist)[:2]
     arr = arr.copy()
     cols = [[np.ascontiguousarray(c) for c in side] for side in (post.below, post.above)]
     for sd in range(2):
@@ -341,7 +341,7 @@ def test_suggest_tree_sizes_device_fits_without_gpu():
     labels = ['x%d' % i for i in range(3)]
     hist = bench.soa_history(labels, 400, 1, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
     table = bench.flat_uniform_table(labels)
-    arr, keep, devs = tpe._tree_labels(table, hist, _Eng())
+    arr, keep, devs = tpe._tree_labels(table, hist, _Eng())[:3]
     assert sorted(devs) == [0, 1, 2] and all(n == 400 for _, n in devs.values())
     assert np.all(arr['dev_obs'] != 0) and np.all(arr['n_ord_in'] == 0) and np.all(arr['ord_key_out'] != 0)
     rc, need, path, need_fit = _tree_call(table, hist, 4096, fit_min=100, engine=_Eng())

@@ -36,7 +36,7 @@ def main():
     hist = H.extract(domain, trials)
     table = domain.table
     below = np.sort(H.split_below(hist, 0.25)).astype(np.int64)
-    arr, keep, _ = tpe._tree_labels(table, hist)
+    arr, keep = tpe._tree_labels(table, hist)[:2]
     tot_fit = 0.0
     for lab in ('model', 'svm_kernel', 'svm_C', 'svm_rbf_gamma'):
         r = arr[table.by_label[lab].index]
@@ -67,12 +67,6 @@ def main():
     probs = [LevelProblem(fits.get(table.by_label[l]), table.by_label[l].index, [bench.N_HISTORY])
              for l in ('model', 'svm_C', 'svm_kernel', 'svm_rbf_gamma')]
     labels_in, keep_in = eng._labels(probs)
-    info = N.PackInfo()
-    pin = eng._pinned
-    if pin is not None:
-        t = best_of(lambda: lib.tpe_host_pack_level(labels_in, len(probs), bench.C_PER_GPU, 5, 0, 0, 0,
-                                                    pin.data_ptr(), pin.numel(), ctypes.byref(info)), reps)
-        print('  tpe_host_pack_level (4 labels)  %7.1f us' % t)
     ids = np.array([bench.N_HISTORY], dtype=np.int64)
     C = bench.C_PER_GPU
 
@@ -88,6 +82,24 @@ def main():
         lat.append(time.perf_counter() - t0)
     print('  tpe_suggest_tree (Engine.suggest_tree)  p50 %7.1f us  min %7.1f us' %
           (1e6 * np.median(lat), 1e6 * np.min(lat)))
+    # host phases of the same call (tpe_host_phases: us since the call's entry)
+    ph = []
+    buf = (ctypes.c_double * len(N.PHASES))()
+    lib.tpe_host_phases(1, None, 0)
+    for i in range(reps):
+        sug()
+        lib.tpe_host_phases(1, buf, len(N.PHASES))
+        ph.append(list(buf))
+    lib.tpe_host_phases(0, None, 0)
+    med = np.median(np.array(ph), axis=0)
+    print('  host phases (median us since entry): ' +
+          '  '.join('%s %.1f' % (k, v) for k, v in zip(N.PHASES, med)))
+    info = N.PackInfo()
+    pin = eng._pinned
+    if pin is not None:
+        t = best_of(lambda: lib.tpe_host_pack_level(labels_in, len(probs), bench.C_PER_GPU, 5, 0, 0, 0,
+                                                    pin.data_ptr(), pin.numel(), ctypes.byref(info)), reps)
+        print('  tpe_host_pack_level (4 labels)  %7.1f us' % t)
     eng.profile = {}
     for _ in range(20):
         sug()
