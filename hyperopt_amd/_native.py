@@ -11,11 +11,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 16
+ABI_VERSION = 17
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT = 1, 2, 4, 8, 16, 32
+F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT, F_FGT = 1, 2, 4, 8, 16, 32, 64
 TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
 TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
@@ -37,9 +37,10 @@ PROBLEM_DTYPE = np.dtype([
     ('key_lo', '<f4'), ('key_inv', '<f4'), ('pool_first', '<i4'),
     ('key0', '<u4'), ('key1', '<u4'), ('ctr2', '<u4'), ('ctr3', '<u4'),
     ('tab_mode', '<i4'), ('tab_off', '<i4', (2,)), ('tab_n', '<i4', (2,)), ('tab_lo', '<f4', (2,)),
-    ('tab_inv', '<f4', (2,)), ('reserved6', '<i4'), ('lat_lo', '<i8'),
+    ('tab_inv', '<f4', (2,)), ('fgt_a', '<f4'), ('lat_lo', '<i8'), ('fgt_off', '<i4'), ('fgt_n', '<i4'),
+    ('fgt_lo', '<f8'),
 ])
-assert PROBLEM_DTYPE.itemsize == 240
+assert PROBLEM_DTYPE.itemsize == 256
 TAB_JOB_DTYPE = np.dtype([('problem', '<i4'), ('side', '<i4'), ('kind', '<i4'), ('n', '<i4'), ('off', '<i4'),
                           ('block0', '<i4')])
 TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4'), ('work_first', '<i4'), ('n_splits', '<i4')])
@@ -75,7 +76,7 @@ class Batch(ctypes.Structure):
         ('sort_count', ctypes.c_int64), ('fin_tiles', ctypes.c_void_p),
         ('work', ctypes.c_void_p),
         ('n_work_cont', ctypes.c_int32), ('n_work_qgauss', ctypes.c_int32),
-        ('n_work_qlog', ctypes.c_int32), ('reserved3', ctypes.c_int32),
+        ('n_work_qlog', ctypes.c_int32), ('fgt_max_boxes', ctypes.c_int32),
         ('part', ctypes.c_void_p), ('l_out', ctypes.c_void_p), ('g_out', ctypes.c_void_p),
         ('tile_best', ctypes.c_void_p), ('result', ctypes.c_void_p),
         ('ce_count', ctypes.c_void_p),
@@ -137,7 +138,7 @@ class PackInfo(ctypes.Structure):
         ('any_pruned', ctypes.c_int32), ('part_total', ctypes.c_int64), ('blob_bytes', ctypes.c_int64),
         ('key_bits', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
         ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
-        ('n_fit', ctypes.c_int32), ('reserved', ctypes.c_int32), ('fit_total', ctypes.c_int64),
+        ('n_fit', ctypes.c_int32), ('fgt_max_boxes', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
         ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_new', ctypes.c_int64),
         ('fit_max_obs', ctypes.c_int64),

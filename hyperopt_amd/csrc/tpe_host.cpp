@@ -72,6 +72,29 @@ bool tables_enabled() {
   const char* e = getenv("TPE_TABLES");
   return !(e && e[0] == '0');
 }
+// box moments for device-fitted labels ("Box moments"); TPE_FGT=0 turns them off (A/B, tests)
+bool fgt_enabled() {
+  const char* e = getenv("TPE_FGT");
+  return !(e && e[0] == '0');
+}
+constexpr double kTabMinRatioFgt = 1.0;          // candidates per cell row for box-moment tables
+constexpr int64_t kFgtMaxBoxes = 4096;
+// a of the device fit's narrowest components: (float)(sqrt(log2(e) / 2) / max(smin, EPS)),
+// smin = prior_sigma / min(100, 1 + K) (tpe.py:465-470), as k_fit_emit rounds it
+float fgt_a(double prior_sigma, int64_t K) {
+  const double smin = prior_sigma / std::min(100.0, 1.0 + (double)K);
+  return (float)(0.84932180028801907 / std::max(smin, kEPS));
+}
+// the box width d = 1 / (a sqrt(ln 2)): a term 2^-(a (t - mu))^2 = e^-((t - mu) / d)^2
+double fgt_width(double prior_sigma, int64_t K) {
+  return 1.0 / ((double)fgt_a(prior_sigma, K) * std::sqrt(kLn2));
+}
+// candidates per cell row from which a device-fitted label tabulates
+// (TPE_TAB_DEVFIT_RATIO overrides: A/B of the cost model)
+double devfit_ratio() {
+  const char* e = getenv("TPE_TAB_DEVFIT_RATIO");
+  return e && *e ? atof(e) : kTabMinRatioDevFit;
+}
 // cells of one side: a_max * h <= kTabEta over [lo, hi) (sig_min: the side's smallest bandwidth)
 int64_t tab_cells(double lo, double hi, double sig_min) {
   const double a_max = kAScale / std::max(sig_min, kEPS);
@@ -756,6 +779,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<int32_t> tmode((size_t)n_labels, TPE_TAB_NONE);
   std::vector<int64_t> tn0((size_t)n_labels, 0), tn1((size_t)n_labels, 0), tlat((size_t)n_labels, 0);
   std::vector<double> tklo((size_t)n_labels, 0), tkhi((size_t)n_labels, 0);
+  std::vector<int64_t> fgt_boxes((size_t)n_labels, 0);   // box-moment labels: their boxes
   for (int32_t li = 0; li < n_labels && tab_on && n_cand > 0; ++li) {
     const tpe_label_in& L = labels[li];
     const double ct = (double)L.n_ids * (double)n_cand;     // candidates of the label in this level
@@ -775,9 +799,19 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       // a cell row costs ~10x a candidate's score (two passes plus the f64
       // moments), more against the pruned, locally expanded per-candidate path
       // of a device-fitted mixture: tables pay from kTabMinRatio candidates a cell
-      const double ratio = dev_fit[li] ? kTabMinRatioDevFit : kTabMinRatio;
+      // a device-fitted mixture's above cells built from box moments ("Box
+      // moments": ~16 boxes per cell instead of every component within reach)
+      // pay from about one candidate a cell
+      int64_t nbox = 0;
+      if (dev_fit[li] && fgt_enabled() && n1 > 0) {
+        const double d = fgt_width(L.prior_sigma, L.above_k);
+        const double nb = std::ceil((khi - klo) / d) + 1.0;
+        if (d > 0 && nb >= 1.0 && nb <= (double)kFgtMaxBoxes) nbox = (int64_t)nb;
+      }
+      const double ratio = nbox > 0 ? kTabMinRatioFgt : dev_fit[li] ? devfit_ratio() : kTabMinRatio;
       if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= ratio * (double)(n0 + n1)) {
         tmode[li] = TPE_TAB_CELLS; tn0[li] = n0; tn1[li] = n1;
+        fgt_boxes[li] = nbox;
       }
     } else if ((L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) && L.q > 0 && L.above_k > 0 &&
                !(L.flags & TPE_F_NO_TABLE)) {
@@ -917,7 +951,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
   if (below_idx.empty()) below_idx.push_back(0);
   // ---- score tables: 16-B units (a cell row is 3 units, a lattice row 1) ----
-  int64_t tab_units = 0;
+  int64_t tab_units = 0, fgt_max_boxes = 0;
   for (int32_t li = 0; li < n_labels; ++li) {
     tpe_problem& p = lab[li];
     p.tab_mode = tmode[li];
@@ -929,6 +963,16 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         p.tab_lo[sd] = (float)tklo[li];
         p.tab_inv[sd] = (float)((double)n / (tkhi[li] - tklo[li]));
         tab_units += kTabRowUnits * n;
+      }
+      if (fgt_boxes[li] > 0) {              // box records after the label's cells ("Box moments")
+        const tpe_label_in& L = labels[li];
+        p.flags |= TPE_F_FGT;
+        p.fgt_a = fgt_a(L.prior_sigma, L.above_k);
+        p.fgt_off = (int32_t)tab_units;
+        p.fgt_n = (int32_t)fgt_boxes[li];
+        p.fgt_lo = tklo[li];
+        tab_units += 1 + TPE_FGT_BOX_UNITS * fgt_boxes[li];
+        fgt_max_boxes = std::max(fgt_max_boxes, fgt_boxes[li]);
       }
     } else if (tmode[li] == TPE_TAB_LATTICE) {
       p.tab_off[0] = (int32_t)tab_units;
@@ -1198,7 +1242,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->key_bits = key_bits;
   info->sort_end_bit = any_pruned ? sort_end_bit : 0;
   info->part_total = part_total;
-  info->n_fit = (int32_t)fit.size(); info->reserved = 0;
+  info->n_fit = (int32_t)fit.size();
+  info->fgt_max_boxes = (int32_t)fgt_max_boxes;
   info->fit_total = fit_seg.back();
   info->copy_end = off[13] + len[13];
   info->sort_count = n_sorted_prob * (int64_t)n_cand;

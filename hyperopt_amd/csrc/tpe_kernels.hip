@@ -2331,6 +2331,180 @@ __device__ __forceinline__ void pruned_range(const tpe_problem& p, const float4*
   k0 = __builtin_amdgcn_readfirstlane(k0); n0 = __builtin_amdgcn_readfirstlane(n0);
 }
 
+// ---------------------------------------------------------------- box moments
+// (include/tpe_hip.h "Box moments").  Widths in d = 1 / (fgt_a sqrt(ln 2)):
+// a term 2^(c - (a (t - mu))^2) of the narrowest width is 2^c e^-((t - mu) / d)^2.
+constexpr int kFgtP = TPE_FGT_P;
+constexpr int kFgtJ = kFgtP + kTabMoments - 1;      // Hermite functions h_0 .. h_(P+9)
+constexpr double kFgtReach = 8.0;                   // boxes within 8 widths of the cell
+// Cramer's 1.0865 times sum_(n >= P) (sqrt2 rho)^n / sqrt(n!), rho = 1/2 (a box's
+// half-width in d): a box's truncation error is below this times W_b e^(-x^2 / 2)
+constexpr double kFgtEps = 1.0865 * 1.0296e-9;
+constexpr double kSqrtLn2 = 0.83255461115769775;
+static_assert(kFgtP == 16, "kFgtEps is the P = 16 tail");
+static_assert(TPE_FGT_BOX_UNITS * 16 >= kFgtP * 8 + 16, "a box record: the moments and four int32");
+
+__device__ __forceinline__ double fgt_width(const tpe_problem& p) { return 1.0 / ((double)p.fgt_a * kSqrtLn2); }
+
+// One wave per box b of a TPE_F_FGT label: its components [k_lo, k_hi) (f64
+// means in [fgt_lo + b d, fgt_lo + (b + 1) d)), A_n = sum 2^c y^n / n! over
+// those of the narrowest width (y = (mu - centre) / d), the others counted
+// (n_odd: the cells sum them directly); wave butterflies, so a record is the
+// same every run.  Block (0, job) also writes the label's header: ok when the
+// boxes hold every component.  Grid (ceil(fgt_max_boxes / 4), n_tab_jobs).
+__global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P, const tpe_tab_job* __restrict__ J,
+                                               const float4* __restrict__ comp32, float4* __restrict__ tab) {
+  const tpe_tab_job jb = J[blockIdx.y];
+  if (jb.kind != TPE_TAB_CELLS || jb.side != 1) return;
+  const tpe_problem& p = P[jb.problem];
+  if (!(p.flags & TPE_F_FGT)) return;
+  const int lane = threadIdx.x & 63;
+  const int b = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const float4* __restrict__ rows = comp32 + p.above_off;
+  const int K = p.above_len;
+  const double d = fgt_width(p), lo = p.fgt_lo;
+  auto mu_of = [&](int k) { const float4 q = rows[k]; return (double)q.x + (double)q.y; };
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const bool ok = K > 0 && mu_of(0) >= lo && mu_of(K - 1) < lo + (double)p.fgt_n * d;
+    reinterpret_cast<int*>(tab + p.fgt_off)[0] = ok ? 1 : 0;
+  }
+  if (b >= p.fgt_n) return;
+  // [k_lo, k_hi): lanes 0 and 1 search the two edges
+  int kb = 0;
+  if (lane < 2) {
+    const double edge = lo + (double)(b + lane) * d;
+    int a = 0, z = K;                               // first k with mu_k >= edge
+    while (a < z) {
+      const int m = (a + z) >> 1;
+      if (mu_of(m) < edge) a = m + 1; else z = m;
+    }
+    kb = a;
+  }
+  const int k_lo = __shfl(kb, 0), k_hi = __shfl(kb, 1);
+  const double centre = lo + ((double)b + 0.5) * d;
+  double A[kFgtP];
+#pragma unroll
+  for (int n = 0; n < kFgtP; ++n) A[n] = 0.0;
+  int odd = 0;
+  for (int k = k_lo + lane; k < k_hi; k += 64) {
+    const float4 q = rows[k];
+    if (!(q.w > -INFINITY)) continue;                 // listed apart (the wide list)
+    if (q.z != p.fgt_a) { ++odd; continue; }
+    const double y = ((double)q.x + (double)q.y - centre) / d;
+    double t = exp2((double)q.w);
+    A[0] += t;
+#pragma unroll
+    for (int n = 1; n < kFgtP; ++n) {
+      t *= y * (1.0 / (double)n);
+      A[n] += t;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < kFgtP; ++n)
+    for (int off = 32; off > 0; off >>= 1) A[n] += __shfl_xor(A[n], off);
+  for (int off = 32; off > 0; off >>= 1) odd += __shfl_xor(odd, off);
+  double* rec = reinterpret_cast<double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
+  if (lane < kFgtP) {
+    double v = A[0];
+#pragma unroll
+    for (int n = 1; n < kFgtP; ++n) v = lane == n ? A[n] : v;
+    rec[lane] = v;
+  }
+  if (lane == 0) {
+    int* ri = reinterpret_cast<int*>(rec + kFgtP);
+    ri[0] = k_lo; ri[1] = k_hi; ri[2] = odd; ri[3] = 0;
+  }
+}
+
+// A cell's moments from the box moments within reach (one box per lane,
+// Hermite -> Taylor, reduced by butterflies), plus the wide list and the boxes'
+// odd components summed directly at the shift mx = log2 of the boxes' sum at
+// the centre.  false (nothing written) when the label's boxes do not hold every
+// component, the sum is not positive or its truncation bound exceeds 2^-25 of
+// it: the caller builds the cell directly.  Wave-uniform.
+__device__ bool cell_moments_fgt(const tpe_problem& p, const float4* __restrict__ tab,
+                                 const float4* __restrict__ comp32, float c, float h, double (&M)[kTabMoments],
+                                 float& mx_out, bool& bad_out) {
+  const int lane = threadIdx.x & 63;
+  if (reinterpret_cast<const int*>(tab + p.fgt_off)[0] != 1) return false;
+  const double d = fgt_width(p), cd = (double)c;
+  const double pos = (cd - p.fgt_lo) / d - 0.5;        // the cell centre in box-centre units
+  const int b0 = max(0, (int)floor(pos - kFgtReach)), b1 = min(p.fgt_n - 1, (int)ceil(pos + kFgtReach));
+  const int nb = b1 - b0 + 1;
+  double B[kTabMoments];
+#pragma unroll
+  for (int m = 0; m < kTabMoments; ++m) B[m] = 0.0;
+  double err = 0.0;
+  int odd = 0, k_lo = 0, k_hi = 0;
+  if (lane < nb) {
+    const int b = b0 + lane;
+    const double* __restrict__ rec = reinterpret_cast<const double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
+    const int* __restrict__ ri = reinterpret_cast<const int*>(rec + kFgtP);
+    k_lo = ri[0]; k_hi = ri[1]; odd = ri[2];
+    const double x = (cd - (p.fgt_lo + ((double)b + 0.5) * d)) / d;
+    const double e = exp(-x * x);
+    double hj[kFgtJ + 1];                             // h_j(x) = e^-x^2 H_j(x)
+    hj[0] = e;
+    hj[1] = 2.0 * x * e;
+#pragma unroll
+    for (int j = 1; j < kFgtJ; ++j) hj[j + 1] = 2.0 * x * hj[j] - 2.0 * (double)j * hj[j - 1];
+    double A[kFgtP];
+#pragma unroll
+    for (int n = 0; n < kFgtP; ++n) A[n] = rec[n];
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) {
+      double sm = 0.0;
+#pragma unroll
+      for (int n = 0; n < kFgtP; ++n) sm += A[n] * hj[n + m];
+      B[m] = sm;
+    }
+    err = A[0] * exp(-0.5 * x * x) * kFgtEps;
+  }
+#pragma unroll
+  for (int m = 0; m < kTabMoments; ++m)
+    for (int off = 32; off > 0; off >>= 1) B[m] += __shfl_xor(B[m], off);
+  for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
+  const double S0 = B[0];
+  // (2^-25: the cells' own Taylor truncation is 4e-8 relative)
+  if (!(S0 > 0.0) || !(err <= S0 * 0x1p-25)) return false;
+  const float mx = (float)log2(S0);
+  // the boxes' part in the cell's u = (t - c) / h: B_m (-1)^m / m! (h / d)^m 2^-mx
+  if (lane == 0) {
+    const double r = (double)h / d, sc = exp2(-(double)mx);
+    double f = sc;
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) {
+      M[m] += B[m] * f;
+      f *= -r / (double)(m + 1);
+    }
+  }
+  // directly: the wide list and the boxes' odd components (rare)
+  bool bad = false;
+  const float cut = mx - kTabDrop;
+  for (int i = lane; i < p.wide_len; i += 64) {
+    const float4 q = comp32[p.wide_off + i];
+    const float z = ((c - q.x) - q.y) * q.z;
+    const float v = q.w - z * z;
+    if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
+  }
+  unsigned long long with_odd = __ballot(lane < nb && odd > 0);
+  while (with_odd) {
+    const int src = __builtin_ctzll(with_odd);
+    with_odd &= with_odd - 1;
+    const int lo_k = __shfl(k_lo, src), hi_k = __shfl(k_hi, src);
+    for (int k = lo_k + lane; k < hi_k; k += 64) {
+      const float4 q = comp32[p.above_off + k];
+      if (!(q.w > -INFINITY) || q.z == p.fgt_a) continue;
+      const float z = ((c - q.x) - q.y) * q.z;
+      const float v = q.w - z * z;
+      if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
+    }
+  }
+  mx_out = mx;
+  bad_out = __ballot(bad) != 0ull;
+  return true;
+}
+
 // one workgroup: {l, g} of lattice value lat_lo + j of a quantized problem, the
 // reference's per-component mass terms (tpe.py:147-159 / :285-298) summed in a
 // fixed order (thread-strided, a butterfly per wave, the waves' partials in
@@ -2431,7 +2605,7 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
         cell_moments_chunked(rows_lds, n0 + n1, meta_lds, c, h, M, mx, bad);
       } else if (!pruned) {
         cell_moments<false>(comp32 + k0, n0, comp32 + k1, n1, c, h, M, mx, bad);
-      } else {
+      } else if (!(side == 1 && (p.flags & TPE_F_FGT) && cell_moments_fgt(p, tab, comp32, c, h, M, mx, bad))) {
         int kk, nn;
         pruned_range(p, comp32, grid, c, kk, nn);
         cell_moments<false>(comp32 + kk, nn, comp32 + k1, n1, c, h, M, mx, bad);
@@ -3416,6 +3590,9 @@ int tpe_tables(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
   const int extra = b->early_select ? b->n_problems : 0;
+  if (b->fgt_max_boxes > 0)                   // box moments of the TPE_F_FGT labels first
+    TPE_LAUNCH(k_boxes, dim3((unsigned)((b->fgt_max_boxes + 3) / 4), b->n_tab_jobs), dim3(256), 0,
+               (hipStream_t)stream, b->problems, b->tab_jobs, (const float4*)b->comp32, (float4*)b->tab);
   TPE_LAUNCH(k_tables, dim3(b->tab_blocks + extra), dim3(kTabTblThreads), 0, (hipStream_t)stream,
                        b->problems, b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64,
                        b->grid, (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0, b->tab_blocks, b->samp,
@@ -3787,6 +3964,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.tab_blocks = (int32_t)info.tab_blocks;
     b.tab = ws->tab;
     b.tab_units = info.tab_units;
+    b.fgt_max_boxes = info.fgt_max_boxes;
   }
   // the select stage writes the results straight into the pinned staging
   // buffer when the device can address it (no readback copy)

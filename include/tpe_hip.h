@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 16
+#define TPE_ABI_VERSION 17
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -69,10 +69,16 @@ enum {
                           undrawn category can still win (usually one 1024-draw chunk) */
   TPE_F_NO_TABLE = 16, /* tpe_label_in: score this label per candidate (no lattice table), e.g. when
                           the caller supplies candidates that need not lie on the quantization lattice */
-  TPE_F_PREFIT = 32    /* tpe_tree_label: fit this label up front on the host worker threads (the
+  TPE_F_PREFIT = 32,   /* tpe_tree_label: fit this label up front on the host worker threads (the
                           caller's hint: the labels its previous suggest on the space used); no label
                           flagged: every natively fitted label with enough observations */
+  TPE_F_FGT = 64       /* tpe_problem (set by the packer): a device-fitted TPE_TAB_CELLS label whose
+                          above cells are built from Hermite box moments (see "Box moments") */
 };
+
+/* box moments (see "Box moments" below): Hermite terms per box, 16-B units per box record */
+#define TPE_FGT_P 16
+#define TPE_FGT_BOX_UNITS 9
 
 /* tabulated scoring of a problem (tpe_problem.tab_mode, see "Tabulated scoring") */
 enum {
@@ -103,7 +109,7 @@ enum { TPE_PREC_F32 = 0, TPE_PREC_F64 = 1 };
 enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE = -4 };
 
 /*
- * One problem (192 bytes).  Component tables (device, caller-owned):
+ * One problem (256 bytes).  Component tables (device, caller-owned):
  *   comp32[k] = float4 {mu_hi, mu_lo, a, c}      families 0/1 at TPE_PREC_F32
  *   comp64[k] = double4 {mu, a, c, 0}            families 0/1 at TPE_PREC_F64
  *   comp64[k] = double4 {mu, b, w, 0}            families 2/3 (b = max(sqrt2*sigma, EPS))
@@ -177,6 +183,26 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  * Tables live in `tab` (16-B units; tab_off[s] = first unit) and are built by
  * the table stage from the problem's component rows (after the device fit).
  *
+ * Box moments (TPE_F_FGT: device-fitted above mixtures of a TPE_TAB_CELLS
+ * label).  adaptive_parzen_normal clips every bandwidth to >= prior_sigma /
+ * min(100, 1 + K) (tpe.py:465-470), so a large history's above components
+ * share that narrowest sigma (a = fgt_a in the rows) almost everywhere: their
+ * sum is a Gauss transform with one width d = 1 / (fgt_a sqrt(ln 2)).  The
+ * box stage (k_boxes) cuts [fgt_lo, fgt_lo + fgt_n d) into boxes of width d
+ * and gives each box its Hermite moments A_n = sum_k 2^c_k y_k^n / n!
+ * (y_k = (mu_k - centre) / d, n < TPE_FGT_P, f64, fixed-order reductions);
+ * a cell then gets its Taylor moments from the boxes within reach,
+ * B_m = (-1)^m / m! sum_b sum_n A_bn h_(n+m)(x_b) (h_j(x) = e^-x^2 H_j(x),
+ * x_b = (centre_cell - centre_b) / d) — about 16 boxes per cell instead of
+ * every component within reach — plus the components of other widths (the
+ * wide list, and any "odd" component a box counts) summed directly.  A cell
+ * whose truncation bound (Cramer: sum_b 1.09 W_b e^(-x_b^2 / 2) eps_P) is not
+ * below 2^-25 of its sum, and every cell of a label whose components do not
+ * all lie in the boxes, is built by the direct path instead.  Box records
+ * follow the label's above cells in `tab` at fgt_off: one header unit {int32
+ * ok, ...} and TPE_FGT_BOX_UNITS units per box {double A[TPE_FGT_P]; int32
+ * k_lo, k_hi, n_odd, 0}.
+ *
  * samp[k] = double[8] {cum, mu, sigma, fa, fb, flip, 0, 0}: below-mixture
  * sampler table; cum = selection CDF (∝ w_k * mass_k when bounded); fa, fb =
  * Phi of the (mirrored if flip) standardised truncation bounds; family 4 uses cum.
@@ -215,8 +241,11 @@ typedef struct tpe_problem {
   int32_t tab_off[2];    /* first 16-B unit of the below / above table in `tab` (lattice: [0]) */
   int32_t tab_n[2];      /* cells per side (lattice: tab_n[0] = lattice values) */
   float tab_lo[2], tab_inv[2];  /* cell j of side s: [tab_lo[s] + j / tab_inv[s], + 1 / tab_inv[s]) */
-  int32_t reserved6;
+  float fgt_a;           /* TPE_F_FGT: a of the narrowest (sigma-clipped) components  */
   int64_t lat_lo;        /* lattice: index m of table row 0 (value lat_lo * q) */
+  int32_t fgt_off;       /* TPE_F_FGT: first 16-B unit of the box records in `tab`    */
+  int32_t fgt_n;         /* TPE_F_FGT: boxes of width 1/(fgt_a sqrt(ln 2)) from fgt_lo */
+  double fgt_lo;
 } tpe_problem;
 
 /* one table of the table stage: a side of a TPE_TAB_CELLS label (4 cells per
@@ -345,7 +374,8 @@ typedef struct tpe_batch {
                                NULL: every tile */
   /* above-mixture work list, ordered [continuous | quantized Gauss | quantized log] */
   const tpe_work* work;
-  int32_t n_work_cont, n_work_qgauss, n_work_qlog, reserved3;
+  int32_t n_work_cont, n_work_qgauss, n_work_qlog;
+  int32_t fgt_max_boxes; /* most boxes of a TPE_F_FGT problem (0: none; the box stage's grid) */
   double* part;          /* above-mixture partial sums: [n_work][2048]          */
   double* l_out;         /* optional [total_cand] (original order); NULL to skip */
   double* g_out;         /* optional [total_cand]; NULL to skip                 */
@@ -461,7 +491,7 @@ typedef struct tpe_pack_info {
   int64_t part_total, blob_bytes;
   int32_t key_bits, sort_end_bit;   /* sort-key layout for tpe_batch (sort_end_bit 0: no sort) */
   int64_t off_fit, off_below_idx, off_fit_seg;
-  int32_t n_fit, reserved;
+  int32_t n_fit, fgt_max_boxes;     /* device fits; most boxes of a TPE_F_FGT label */
   int64_t fit_total;
   int64_t copy_end, copy2_len;
   int64_t sort_count;               /* candidates of the sorted (pruned) problems */

@@ -425,6 +425,58 @@ def test_device_fit_matches_oracle(engine, dist, args, scoring):
     assert res_d2[0]['idx'] == res_d[0]['idx'] and res_d2[0]['score'] == res_d[0]['score']
 
 
+@pytest.mark.parametrize('case', ['uniform_dense', 'clustered', 'loguniform'])
+def test_box_moment_tables_match_direct_tables(engine, monkeypatch, case):
+    """Box-moment cells (include/tpe_hip.h "Box moments": Hermite moments per
+    box of the narrowest width, translated to each cell's Taylor moments) of a
+    device-fitted above mixture against the same cells built directly from
+    every component within reach (TPE_FGT=0 with tables forced): the same
+    draws, the above lpdf within 2e-6 relative of each other on every sampled
+    candidate and both within the fp32 tolerance of the oracle; the argmax
+    inside the eps-tie set.  'clustered' mixes narrow clusters with isolated
+    points, so boxes hold components of other widths (summed directly)."""
+    from hyperopt_amd import _native as N
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(77)
+    n = 40000
+    if case == 'uniform_dense':          # config 5's shape: every bandwidth at the clip
+        dist, args, obs = 'uniform', dict(low=-5.0, high=5.0), rs.uniform(-5, 5, n)
+    elif case == 'clustered':
+        dist, args = 'uniform', dict(low=-5.0, high=5.0)
+        obs = np.clip(np.concatenate([rs.normal(-2, 0.05, n // 2), rs.uniform(-5, 5, n // 2 - 3),
+                                      [-4.9, 4.95, 0.0]]), -5, 5)
+    else:
+        dist, args, obs = 'loguniform', dict(low=-4.0, high=3.0), np.exp(rs.uniform(-4, 3, n))
+    rs.shuffle(obs)
+    bidx = np.sort(rs.choice(n, 25, replace=False)).astype(np.int32)
+    m = np.zeros(n, bool)
+    m[bidx] = True
+    dev, _ = _device_post(engine, dist, args, obs, bidx)
+    logf = dist == 'loguniform'
+    tr = np.log if logf else (lambda v: v)
+    pmu, psig = 0.5 * (args['low'] + args['high']), args['high'] - args['low']
+    above = O.adaptive_parzen_normal(tr(obs[~m]), 1.0, pmu, psig)
+    lpdf = O.lgmm1_lpdf if logf else O.gmm1_lpdf
+    C = 1 << 16
+    monkeypatch.setenv('TPE_TAB_DEVFIT_RATIO', '1')
+    out = {}
+    for fgt in ('1', '0'):
+        monkeypatch.setenv('TPE_FGT', fgt)
+        res, cand, l, g = engine.run([LevelProblem(dev, 0, [3])], C, seed=9, want_lg=True, return_cand=True)
+        prob, _ = engine.device_tables()
+        assert prob[0]['tab_mode'] == N.TAB_CELLS
+        assert bool(prob[0]['flags'] & N.F_FGT) == (fgt == '1')
+        out[fgt] = (res, cand[0], l[0], g[0])
+    np.testing.assert_array_equal(out['1'][1], out['0'][1])
+    np.testing.assert_array_equal(out['1'][2], out['0'][2])        # the below side: the same cells
+    gf, gd = out['1'][3], out['0'][3]
+    assert np.all(np.abs(gf - gd) <= 2e-6 * np.maximum(1.0, np.abs(gd))), np.max(np.abs(gf - gd))
+    x = out['1'][1]
+    sub = rs.choice(C, 3000, replace=False)
+    _check_lpdf(gf[sub], lpdf(x[sub], *above, low=dev.low, high=dev.high), 1e-5, (case, 'g'))
+    _check_argmax(int(out['1'][0][0]['idx']), out['1'][2], gd, 1e-5, case)
+
+
 def test_device_fit_batched_labels_and_suggest():
     """Several device-fitted labels (and host-fitted ones) in one level, through
     tpe.suggest_choices: identical to suggest_choices with every fit on the host
