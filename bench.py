@@ -623,6 +623,24 @@ def run_other(args, rank, world, device):
     stages = {k: float(np.sum([a[0] for a in v])) for k, v in eng.profile.items()}
     eng.profile = None
     extra = {}
+    # host phases of the native suggest (tpe_host_phases: us since its entry) over a
+    # few more steps, and the step's wall time outside that call (Python)
+    import ctypes
+    from hyperopt_amd import _native as N
+    buf = (ctypes.c_double * len(N.PHASES))()
+    eng.lib.tpe_host_phases(1, None, 0)
+    ph, wall = [], []
+    for i in range(3):
+        s0 = time.perf_counter()
+        step(300 + i)
+        wall.append(1e6 * (time.perf_counter() - s0))
+        eng.lib.tpe_host_phases(1, buf, len(N.PHASES))
+        ph.append(list(buf))
+    eng.lib.tpe_host_phases(0, None, 0)
+    med = np.median(np.array(ph), axis=0)
+    if med[-1] > 0:
+        extra['host_phases_us'] = {k: round(float(v), 1) for k, v in zip(N.PHASES, med)}
+        extra['host_phases_us']['step_wall'] = round(float(np.median(wall)), 1)
     if args.config == 4:
         # the same batched suggest returning per-id dicts (numpy scalars per value)
         lat_d = []

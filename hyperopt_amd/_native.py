@@ -80,7 +80,7 @@ class Batch(ctypes.Structure):
         ('part', ctypes.c_void_p), ('l_out', ctypes.c_void_p), ('g_out', ctypes.c_void_p),
         ('tile_best', ctypes.c_void_p), ('result', ctypes.c_void_p),
         ('ce_count', ctypes.c_void_p),
-        ('fit', ctypes.c_void_p), ('n_fit', ctypes.c_int32), ('reserved4', ctypes.c_int32),
+        ('fit', ctypes.c_void_p), ('n_fit', ctypes.c_int32), ('fgt_max_cells', ctypes.c_int32),
         ('below_idx', ctypes.c_void_p), ('fit_seg', ctypes.c_void_p), ('fit_total', ctypes.c_int64),
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
@@ -148,6 +148,7 @@ class PackInfo(ctypes.Structure):
         ('off_samp_tiles', ctypes.c_int64), ('n_samp_tiles', ctypes.c_int64), ('n_samp_eager', ctypes.c_int64),
         ('off_tab_tiles', ctypes.c_int64), ('n_tab_tiles', ctypes.c_int64),
         ('off_expand', ctypes.c_int64), ('n_expand', ctypes.c_int64), ('copy_start', ctypes.c_int64),
+        ('fgt_max_cells', ctypes.c_int64),
     ]
 
 

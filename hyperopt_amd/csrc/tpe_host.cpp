@@ -1146,7 +1146,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   // (TPE_TAB_PER_BLOCK rows per block); `problem` = the label's first row
   auto& tab_jobs = ps.tab_jobs;
   tab_jobs.clear();
-  int64_t tab_blocks = 0;
+  int64_t tab_blocks = 0, fgt_max_cells = 0;
   for (int32_t li = 0, r = 0; li < n_labels; r += (int32_t)labels[li].n_ids, ++li) {
     const tpe_problem& p = lab[li];
     if (p.tab_mode == TPE_TAB_NONE || labels[li].n_ids <= 0) continue;
@@ -1156,7 +1156,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       j.problem = r; j.side = sd; j.kind = p.tab_mode; j.n = p.tab_n[sd]; j.off = p.tab_off[sd];
       j.block0 = (int32_t)tab_blocks;
       // cells: TPE_TAB_PER_BLOCK rows per block; lattice: one block per value
-      tab_blocks += j.kind == TPE_TAB_CELLS ? (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK : j.n;
+      // (a box-moment label's above cells are built by their own stage: no blocks here)
+      if (sd == 1 && (p.flags & TPE_F_FGT)) fgt_max_cells = std::max<int64_t>(fgt_max_cells, j.n);
+      else tab_blocks += j.kind == TPE_TAB_CELLS ? (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK : j.n;
       tab_jobs.push_back(j);
     }
   }
@@ -1244,6 +1246,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->part_total = part_total;
   info->n_fit = (int32_t)fit.size();
   info->fgt_max_boxes = (int32_t)fgt_max_boxes;
+  info->fgt_max_cells = fgt_max_cells;
   info->fit_total = fit_seg.back();
   info->copy_end = off[13] + len[13];
   info->sort_count = n_sorted_prob * (int64_t)n_cand;

@@ -2336,7 +2336,6 @@ __device__ __forceinline__ void pruned_range(const tpe_problem& p, const float4*
 // a term 2^(c - (a (t - mu))^2) of the narrowest width is 2^c e^-((t - mu) / d)^2.
 constexpr int kFgtP = TPE_FGT_P;
 constexpr int kFgtJ = kFgtP + kTabMoments - 1;      // Hermite functions h_0 .. h_(P+9)
-constexpr double kFgtReach = 8.0;                   // boxes within 8 widths of the cell
 // Cramer's 1.0865 times sum_(n >= P) (sqrt2 rho)^n / sqrt(n!), rho = 1/2 (a box's
 // half-width in d): a box's truncation error is below this times W_b e^(-x^2 / 2)
 constexpr double kFgtEps = 1.0865 * 1.0296e-9;
@@ -2353,7 +2352,8 @@ __device__ __forceinline__ double fgt_width(const tpe_problem& p) { return 1.0 /
 // same every run.  Block (0, job) also writes the label's header: ok when the
 // boxes hold every component.  Grid (ceil(fgt_max_boxes / 4), n_tab_jobs).
 __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P, const tpe_tab_job* __restrict__ J,
-                                               const float4* __restrict__ comp32, float4* __restrict__ tab) {
+                                               const float4* __restrict__ comp32, const int32_t* __restrict__ grid,
+                                               float4* __restrict__ tab) {
   const tpe_tab_job jb = J[blockIdx.y];
   if (jb.kind != TPE_TAB_CELLS || jb.side != 1) return;
   const tpe_problem& p = P[jb.problem];
@@ -2369,11 +2369,21 @@ __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P
     reinterpret_cast<int*>(tab + p.fgt_off)[0] = ok ? 1 : 0;
   }
   if (b >= p.fgt_n) return;
-  // [k_lo, k_hi): lanes 0 and 1 search the two edges
+  // [k_lo, k_hi): lanes 0 and 1 search the two edges, inside the range the
+  // fit's grid over the f32 means gives (a bucket either side of the edge's)
   int kb = 0;
   if (lane < 2) {
     const double edge = lo + (double)(b + lane) * d;
+    const int32_t* __restrict__ G = grid + p.grid_off;
     int a = 0, z = K;                               // first k with mu_k >= edge
+    if (p.grid_inv > 0.f && p.grid_n > 0) {
+      const float gf = floorf(((float)edge - p.grid_lo) * p.grid_inv);
+      const int gb = (int)fminf(fmaxf(gf, 0.f), (float)(p.grid_n - 1));
+      a = G[max(gb - 1, 0)];
+      z = G[min(gb + 2, p.grid_n)];
+      if (a > 0 && !(mu_of(a - 1) < edge)) a = 0;   // (outside the bucket bounds: search everything)
+      if (z < K && mu_of(z) < edge) z = K;
+    }
     while (a < z) {
       const int m = (a + z) >> 1;
       if (mu_of(m) < edge) a = m + 1; else z = m;
@@ -2386,17 +2396,23 @@ __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P
 #pragma unroll
   for (int n = 0; n < kFgtP; ++n) A[n] = 0.0;
   int odd = 0;
-  for (int k = k_lo + lane; k < k_hi; k += 64) {
-    const float4 q = rows[k];
-    if (!(q.w > -INFINITY)) continue;                 // listed apart (the wide list)
-    if (q.z != p.fgt_a) { ++odd; continue; }
-    const double y = ((double)q.x + (double)q.y - centre) / d;
-    double t = exp2((double)q.w);
-    A[0] += t;
+  const double id = 1.0 / d;
+  // two components per lane in flight (their terms added in index order)
+  for (int k = k_lo + lane; k < k_hi; k += 128) {
+    const bool two = k + 64 < k_hi;
+    const float4 q0 = rows[k], q1 = rows[two ? k + 64 : k];
+    const bool u0 = q0.w > -INFINITY && q0.z == p.fgt_a, u1 = two && q1.w > -INFINITY && q1.z == p.fgt_a;
+    odd += (q0.w > -INFINITY && q0.z != p.fgt_a) + (two && q1.w > -INFINITY && q1.z != p.fgt_a);
+    const double y0 = ((double)q0.x + (double)q0.y - centre) * id, y1 = ((double)q1.x + (double)q1.y - centre) * id;
+    double t0 = u0 ? exp2((double)q0.w) : 0.0, t1 = u1 ? exp2((double)q1.w) : 0.0;
+    A[0] += t0;
+    A[0] += t1;
 #pragma unroll
     for (int n = 1; n < kFgtP; ++n) {
-      t *= y * (1.0 / (double)n);
-      A[n] += t;
+      t0 *= y0 * (1.0 / (double)n);
+      t1 *= y1 * (1.0 / (double)n);
+      A[n] += t0;
+      A[n] += t1;
     }
   }
 #pragma unroll
@@ -2416,28 +2432,58 @@ __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P
   }
 }
 
-// A cell's moments from the box moments within reach (one box per lane,
-// Hermite -> Taylor, reduced by butterflies), plus the wide list and the boxes'
-// odd components summed directly at the shift mx = log2 of the boxes' sum at
-// the centre.  false (nothing written) when the label's boxes do not hold every
-// component, the sum is not positive or its truncation bound exceeds 2^-25 of
-// it: the caller builds the cell directly.  Wave-uniform.
-__device__ bool cell_moments_fgt(const tpe_problem& p, const float4* __restrict__ tab,
-                                 const float4* __restrict__ comp32, float c, float h, double (&M)[kTabMoments],
-                                 float& mx_out, bool& bad_out) {
-  const int lane = threadIdx.x & 63;
-  if (reinterpret_cast<const int*>(tab + p.fgt_off)[0] != 1) return false;
+// Cells of the TPE_F_FGT labels' above sides, four per wave (16 lanes each):
+// a cell's Taylor moments from the box moments within reach (one box per lane,
+// Hermite -> Taylor, reduced over the 16 lanes), plus the wide list and the
+// boxes' odd components summed directly at the shift mx = log2 of the boxes'
+// sum at the centre.  A cell is built directly instead (pruned window, the
+// whole wave) when the label's boxes do not hold every component, the sum is
+// not positive, or the truncation bound (boxes within reach, Cramer) plus the
+// bound on the boxes out of reach (K e^-(R - 1/2)^2) exceeds 2^-25 of the sum
+// (the cells' own Taylor truncation is 4e-8 relative).  Grid
+// (ceil(fgt_max_cells / 32), n_tab_jobs), 8 waves per block; the other jobs'
+// blocks return at once (k_tables builds those).
+constexpr int kFgtCellsPerWave = 4;
+constexpr int kFgtLanes = 64 / kFgtCellsPerWave;     // boxes within reach: at most 16
+constexpr double kFgtReach = 7.0;                    // box centres within 7 widths of the cell centre
+constexpr double kFgtFar = 2.35e-19;                 // e^-(7 - 1/2)^2: a box out of reach, per unit weight
+
+template <int W>
+__device__ __forceinline__ double group_sum(double v) {          // over aligned groups of W lanes
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict__ P,
+                                                   const tpe_tab_job* __restrict__ J,
+                                                   const float4* __restrict__ comp32,
+                                                   const int32_t* __restrict__ grid, float4* __restrict__ tab,
+                                                   bool all_exact) {
+  const tpe_tab_job jb = J[blockIdx.y];
+  if (jb.kind != TPE_TAB_CELLS || jb.side != 1) return;
+  const tpe_problem& p = P[jb.problem];
+  if (!(p.flags & TPE_F_FGT)) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane / kFgtLanes, gl = lane % kFgtLanes;            // cell of the wave, lane in its group
+  const int j0 = ((int)blockIdx.x * 8 + wave) * kFgtCellsPerWave;     // the wave's first cell
+  if (j0 >= jb.n) return;                                              // (wave-uniform)
+  const int j = j0 + g;
+  const bool live = j < jb.n;
+  const bool boxes_ok = reinterpret_cast<const int*>(tab + p.fgt_off)[0] == 1;
+  const float w = 1.f / p.tab_inv[1];
+  const float c = __builtin_fmaf((float)j + 0.5f, w, p.tab_lo[1]);   // as cell_log2_lds forms them
+  const float h = 0.5f * w;
   const double d = fgt_width(p), cd = (double)c;
-  const double pos = (cd - p.fgt_lo) / d - 0.5;        // the cell centre in box-centre units
-  const int b0 = max(0, (int)floor(pos - kFgtReach)), b1 = min(p.fgt_n - 1, (int)ceil(pos + kFgtReach));
-  const int nb = b1 - b0 + 1;
   double B[kTabMoments];
 #pragma unroll
   for (int m = 0; m < kTabMoments; ++m) B[m] = 0.0;
   double err = 0.0;
   int odd = 0, k_lo = 0, k_hi = 0;
-  if (lane < nb) {
-    const int b = b0 + lane;
+  const double pos = (cd - p.fgt_lo) / d - 0.5;                      // the cell centre in box-centre units
+  const int b0 = max(0, (int)ceil(pos - kFgtReach)), b1 = min(p.fgt_n - 1, (int)floor(pos + kFgtReach));
+  if (live && boxes_ok && gl <= b1 - b0) {
+    const int b = b0 + gl;
     const double* __restrict__ rec = reinterpret_cast<const double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
     const int* __restrict__ ri = reinterpret_cast<const int*>(rec + kFgtP);
     k_lo = ri[0]; k_hi = ri[1]; odd = ri[2];
@@ -2447,7 +2493,7 @@ __device__ bool cell_moments_fgt(const tpe_problem& p, const float4* __restrict_
     hj[0] = e;
     hj[1] = 2.0 * x * e;
 #pragma unroll
-    for (int j = 1; j < kFgtJ; ++j) hj[j + 1] = 2.0 * x * hj[j] - 2.0 * (double)j * hj[j - 1];
+    for (int q = 1; q < kFgtJ; ++q) hj[q + 1] = 2.0 * x * hj[q] - 2.0 * (double)q * hj[q - 1];
     double A[kFgtP];
 #pragma unroll
     for (int n = 0; n < kFgtP; ++n) A[n] = rec[n];
@@ -2461,48 +2507,91 @@ __device__ bool cell_moments_fgt(const tpe_problem& p, const float4* __restrict_
     err = A[0] * exp(-0.5 * x * x) * kFgtEps;
   }
 #pragma unroll
-  for (int m = 0; m < kTabMoments; ++m)
-    for (int off = 32; off > 0; off >>= 1) B[m] += __shfl_xor(B[m], off);
-  for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
+  for (int m = 0; m < kTabMoments; ++m) B[m] = group_sum<kFgtLanes>(B[m]);
+  err = group_sum<kFgtLanes>(err) + (double)p.above_len * kFgtFar;
   const double S0 = B[0];
-  // (2^-25: the cells' own Taylor truncation is 4e-8 relative)
-  if (!(S0 > 0.0) || !(err <= S0 * 0x1p-25)) return false;
-  const float mx = (float)log2(S0);
-  // the boxes' part in the cell's u = (t - c) / h: B_m (-1)^m / m! (h / d)^m 2^-mx
-  if (lane == 0) {
-    const double r = (double)h / d, sc = exp2(-(double)mx);
-    double f = sc;
+  const bool ok = live && boxes_ok && S0 > 0.0 && err <= S0 * 0x1p-25;   // (group-uniform)
+  float* row = reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * j);
+  if (ok) {
+    const float mx = (float)log2(S0);
+    double M[kTabMoments];
 #pragma unroll
-    for (int m = 0; m < kTabMoments; ++m) {
-      M[m] += B[m] * f;
-      f *= -r / (double)(m + 1);
+    for (int m = 0; m < kTabMoments; ++m) M[m] = 0.0;
+    if (gl == 0) {       // the boxes' part in u = (t - c) / h: B_m (-1)^m / m! (h / d)^m 2^-mx
+      const double r = (double)h / d;
+      double f = exp2(-(double)mx);
+#pragma unroll
+      for (int m = 0; m < kTabMoments; ++m) {
+        M[m] = B[m] * f;
+        f *= -r / (double)(m + 1);
+      }
     }
-  }
-  // directly: the wide list and the boxes' odd components (rare)
-  bool bad = false;
-  const float cut = mx - kTabDrop;
-  for (int i = lane; i < p.wide_len; i += 64) {
-    const float4 q = comp32[p.wide_off + i];
-    const float z = ((c - q.x) - q.y) * q.z;
-    const float v = q.w - z * z;
-    if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
-  }
-  unsigned long long with_odd = __ballot(lane < nb && odd > 0);
-  while (with_odd) {
-    const int src = __builtin_ctzll(with_odd);
-    with_odd &= with_odd - 1;
-    const int lo_k = __shfl(k_lo, src), hi_k = __shfl(k_hi, src);
-    for (int k = lo_k + lane; k < hi_k; k += 64) {
-      const float4 q = comp32[p.above_off + k];
-      if (!(q.w > -INFINITY) || q.z == p.fgt_a) continue;
+    // directly: the wide list and the boxes' odd components (rare)
+    bool bad = false;
+    const float cut = mx - kTabDrop;
+    for (int i = gl; i < p.wide_len; i += kFgtLanes) {
+      const float4 q = comp32[p.wide_off + i];
       const float z = ((c - q.x) - q.y) * q.z;
       const float v = q.w - z * z;
       if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
     }
+    // odd components reach as far as their own width: boxes within 7 of the
+    // label's widest non-wide width (narrow_amin) hold every one that can matter
+    const double ro = kFgtReach * fmax((double)p.fgt_a / (double)p.narrow_amin, 1.0) + 1.0;
+    const int ob0 = max(0, (int)ceil(pos - ro)), ob1 = min(p.fgt_n - 1, (int)floor(pos + ro));
+    for (int bb = ob0; bb <= ob1; bb += kFgtLanes) {
+      int no = 0, lo_k = 0, hi_k = 0;
+      if (bb + gl <= ob1) {
+        const int* __restrict__ ri = reinterpret_cast<const int*>(
+            reinterpret_cast<const double*>(tab + p.fgt_off + 1 + (int64_t)(bb + gl) * TPE_FGT_BOX_UNITS) + kFgtP);
+        lo_k = ri[0]; hi_k = ri[1]; no = ri[2];
+      }
+      unsigned long long with_odd = (__ballot(no > 0) >> (g * kFgtLanes)) & ((1ull << kFgtLanes) - 1);
+      while (with_odd) {
+        const int src = g * kFgtLanes + __builtin_ctzll(with_odd);
+        with_odd &= with_odd - 1;
+        const int k0 = __shfl(lo_k, src), k1 = __shfl(hi_k, src);
+        for (int k = k0 + gl; k < k1; k += kFgtLanes) {
+          const float4 q = comp32[p.above_off + k];
+          if (!(q.w > -INFINITY) || q.z == p.fgt_a) continue;
+          const float z = ((c - q.x) - q.y) * q.z;
+          const float v = q.w - z * z;
+          if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) M[m] = group_sum<kFgtLanes>(M[m]);
+    bad = group_sum<kFgtLanes>(bad ? 1.0 : 0.0) > 0.0;
+    float out = 0.f;
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) out = gl == m ? (float)M[m] : out;
+    if (gl == kTabMoments) out = bad || all_exact ? NAN : mx;
+    if (gl <= kTabMoments) row[gl] = out;
   }
-  mx_out = mx;
-  bad_out = __ballot(bad) != 0ull;
-  return true;
+  // the cells the boxes cannot build: directly, the whole wave per cell
+  const unsigned long long direct = __ballot(live && !ok && gl == 0);
+  for (int q = 0; q < kFgtCellsPerWave; ++q) {
+    if (!((direct >> (q * kFgtLanes)) & 1ull)) continue;
+    const int jq = j0 + q;
+    const float cq = __builtin_fmaf((float)jq + 0.5f, w, p.tab_lo[1]);
+    double M[kTabMoments];
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) M[m] = 0.0;
+    float mx = -INFINITY;
+    bool bad = false;
+    int kk, nn;
+    pruned_range(p, comp32, grid, cq, kk, nn);
+    cell_moments<false>(comp32 + kk, nn, comp32 + p.wide_off, p.wide_len, cq, h, M, mx, bad);
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) M[m] = group_sum<64>(M[m]);
+    float out = 0.f;
+#pragma unroll
+    for (int m = 0; m < kTabMoments; ++m) out = lane == m ? (float)M[m] : out;
+    if (lane == kTabMoments) out = bad || all_exact ? NAN : mx;
+    float* rq = reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * jq);
+    if (lane <= kTabMoments) rq[lane] = out;
+  }
 }
 
 // one workgroup: {l, g} of lattice value lat_lo + j of a quantized problem, the
@@ -2605,7 +2694,7 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
         cell_moments_chunked(rows_lds, n0 + n1, meta_lds, c, h, M, mx, bad);
       } else if (!pruned) {
         cell_moments<false>(comp32 + k0, n0, comp32 + k1, n1, c, h, M, mx, bad);
-      } else if (!(side == 1 && (p.flags & TPE_F_FGT) && cell_moments_fgt(p, tab, comp32, c, h, M, mx, bad))) {
+      } else {
         int kk, nn;
         pruned_range(p, comp32, grid, c, kk, nn);
         cell_moments<false>(comp32 + kk, nn, comp32 + k1, n1, c, h, M, mx, bad);
@@ -3588,11 +3677,17 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
 int tpe_tables(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
-  if (b->n_tab_jobs == 0 || b->tab_blocks == 0) return TPE_OK;
+  if (b->n_tab_jobs == 0 || (b->tab_blocks == 0 && b->fgt_max_cells == 0)) return TPE_OK;
   const int extra = b->early_select ? b->n_problems : 0;
-  if (b->fgt_max_boxes > 0)                   // box moments of the TPE_F_FGT labels first
+  if (b->fgt_max_boxes > 0 && b->fgt_max_cells > 0) {
+    // the TPE_F_FGT labels' above cells: box moments, then the cells from them
     TPE_LAUNCH(k_boxes, dim3((unsigned)((b->fgt_max_boxes + 3) / 4), b->n_tab_jobs), dim3(256), 0,
-               (hipStream_t)stream, b->problems, b->tab_jobs, (const float4*)b->comp32, (float4*)b->tab);
+               (hipStream_t)stream, b->problems, b->tab_jobs, (const float4*)b->comp32, b->grid, (float4*)b->tab);
+    TPE_LAUNCH(k_cells_fgt, dim3((unsigned)((b->fgt_max_cells + 8 * kFgtCellsPerWave - 1) / (8 * kFgtCellsPerWave)),
+                                 b->n_tab_jobs), dim3(512), 0, (hipStream_t)stream, b->problems, b->tab_jobs,
+               (const float4*)b->comp32, b->grid, (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0);
+  }
+  if (b->tab_blocks == 0 && extra == 0) return hip_check("tpe_tables");
   TPE_LAUNCH(k_tables, dim3(b->tab_blocks + extra), dim3(kTabTblThreads), 0, (hipStream_t)stream,
                        b->problems, b->tab_jobs, b->n_tab_jobs, (const float4*)b->comp32, (const double4*)b->comp64,
                        b->grid, (float4*)b->tab, (b->flags & TPE_BATCH_TAB_EXACT) != 0, b->tab_blocks, b->samp,
@@ -3965,6 +4060,7 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.tab = ws->tab;
     b.tab_units = info.tab_units;
     b.fgt_max_boxes = info.fgt_max_boxes;
+    b.fgt_max_cells = (int32_t)info.fgt_max_cells;
   }
   // the select stage writes the results straight into the pinned staging
   // buffer when the device can address it (no readback copy)

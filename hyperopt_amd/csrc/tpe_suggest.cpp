@@ -167,8 +167,9 @@ int fit_label(Tree& T, int i, bool spec = false) {
 }
 
 // Labels worth a speculative fit on the pool: the natively fitted ones with
-// enough observations for the fit to cost more than a dispatch (categorical, and
-// continuous with a value order below the device-fit size).  Every label of a
+// enough observations for the fit to cost more than a dispatch (categorical,
+// continuous with a value order, and the device-fitted ones' host part: the
+// below positions among the label's tids and the below side's fit).  Every label of a
 // flat space is needed; in a tree the inactive branches' labels are fitted too
 // (their observations are the trials that took that branch, so the extra work
 // is bounded by the history) — what matters is that the suggest waits for the
@@ -180,8 +181,9 @@ bool prefit_worthy(const Tree& T, int i) {
   if (L.host_k[0] > 0 || L.n_obs < kPrefitMinObs || !L.tids || !L.values) return false;
   if (L.family == TPE_FAM_CATEGORICAL) return L.upper > 0;
   if (L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) return false;
-  if (!L.order) return false;
-  return !(T.device_fit_min > 0 && L.n_obs >= std::max<int64_t>(T.device_fit_min, 64));
+  const bool dev = T.device_fit_min > 0 && L.n_obs >= std::max<int64_t>(T.device_fit_min, 64);
+  if (dev) return L.dev_obs != nullptr;         // the below side's fit and its positions among the tids
+  return L.order != nullptr;
 }
 
 struct PrefitCtx {

@@ -819,6 +819,7 @@ class Engine(object):
             b.tab = self._buf('tab', 4 * int(info.tab_units), torch.float32).data_ptr()
             b.tab_units = info.tab_units
             b.fgt_max_boxes = info.fgt_max_boxes
+            b.fgt_max_cells = info.fgt_max_cells
         if info.n_sorted and not inject and not info.n_pooled:
             b.n_sorted, b.draw_blocks = info.n_sorted, info.draw_blocks
             b.draw_pref = self._buf('draw_pref', int(info.n_sorted) * (int(info.draw_blocks) + 1),

@@ -385,7 +385,8 @@ typedef struct tpe_batch {
                                    kernel, {exactly evaluated component x candidate pairs,
                                    components summed by the local expansion}; NULL to skip */
   /* device Parzen fits (n_fit == 0: none); they patch rows of `problems` */
-  const tpe_fit_job* fit; int32_t n_fit; int32_t reserved4;
+  const tpe_fit_job* fit; int32_t n_fit;
+  int32_t fgt_max_cells; /* most above cells of a TPE_F_FGT problem (built by the box stage) */
   const int32_t* below_idx;   /* below indices of every job                        */
   const int64_t* fit_seg;     /* [n_fit + 1] segment offsets into the fit scratch: a job's
                                  segment holds max(n_obs - n_below, n_obs - n_ord_in, n_below) */
@@ -507,6 +508,7 @@ typedef struct tpe_pack_info {
    * then (at the next 256-B boundary) uint32 new_id[n_problems]; the problems and tiles sections
    * (and the tabulated tile list, the identity) are device-only: the upload starts at copy_start */
   int64_t off_expand, n_expand, copy_start;
+  int64_t fgt_max_cells;                /* most above cells of a TPE_F_FGT label (tpe_batch) */
 } tpe_pack_info;
 
 /* ------------------------------------------------------------------------
