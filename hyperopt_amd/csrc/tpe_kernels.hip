@@ -2479,14 +2479,11 @@ __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict
 #pragma unroll
   for (int m = 0; m < kTabMoments; ++m) B[m] = 0.0;
   double err = 0.0;
-  int odd = 0, k_lo = 0, k_hi = 0;
   const double pos = (cd - p.fgt_lo) / d - 0.5;                      // the cell centre in box-centre units
   const int b0 = max(0, (int)ceil(pos - kFgtReach)), b1 = min(p.fgt_n - 1, (int)floor(pos + kFgtReach));
   if (live && boxes_ok && gl <= b1 - b0) {
     const int b = b0 + gl;
     const double* __restrict__ rec = reinterpret_cast<const double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
-    const int* __restrict__ ri = reinterpret_cast<const int*>(rec + kFgtP);
-    k_lo = ri[0]; k_hi = ri[1]; odd = ri[2];
     const double x = (cd - (p.fgt_lo + ((double)b + 0.5) * d)) / d;
     const double e = exp(-x * x);
     double hj[kFgtJ + 1];                             // h_j(x) = e^-x^2 H_j(x)
@@ -3003,6 +3000,11 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
   for (int q = 0; q < j.n_below; ++q) r += __shfl(mine, q) < mine;
   if (b < j.n_below) adj[j.seg_off + r] = mine - (uint32_t)r;
   const int n_under = __popcll(__ballot(under));
+  // the first and last above observations' positions: past the below positions
+  // that open the order (positions 0, 1, ..) and before those that close it
+  const int nb = j.n_below;
+  const int head = __popcll(__ballot(b < nb && mine == (uint32_t)r));
+  const int tail = __popcll(__ballot(b < nb && (int64_t)mine == j.n_obs - nb + r));
   if (b == 0) {
     int64_t lo = 0, hi = j.n_obs;                   // observations with t < prior_mu (NaN last)
     while (lo < hi) {
@@ -3010,7 +3012,13 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
       if (ok[md] < j.prior_mu) lo = md + 1;
       else hi = md;
     }
-    hdr[j.seg_off + kFitHdrPos] = (double)(lo - n_under);
+    const int64_t pos = lo - n_under, n = j.n_obs - nb;
+    hdr[j.seg_off + kFitHdrPos] = (double)pos;
+    // the grid's bounds: the f32 means of the first and last component (the prior inserted)
+    const double m0 = pos == 0 ? j.prior_mu : ok[head];
+    const double m1 = pos == n ? j.prior_mu : ok[j.n_obs - 1 - tail];
+    hdr[j.seg_off + kFitHdrGrid] = (double)(float)m0;
+    hdr[j.seg_off + kFitHdrGrid + 1] = (double)(float)m1;
   }
 }
 
@@ -3022,12 +3030,13 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
 // into LDS from the contiguous stretch of the order that holds them.  Launches
 // over (chunk of kFitChunk components) x job, so a 100k-component mixture
 // spreads over ~50 workgroups instead of one:
-//   k_fit_stats   per chunk: the normaliser W, the acceptance mass M, the
-//                 shift cm = max log2(w / sigma), the wide-threshold statistics
+//   k_fit_main    per chunk, one pass: its {mu, a, c} rows (c shifted by an
+//                 upper bound of max log2(w / sigma), so no pass waits for the
+//                 data's maximum), its wide candidates, its statistics (W, the
+//                 acceptance mass M, the wide-threshold counts), its grid buckets
 //   k_fit_combine the job's chunk statistics combined (fixed chunk order)
-//   k_fit_emit    the chunk's {mu, a, c} rows, its wide candidates and the grid
-//                 buckets whose first component lies in the chunk
-//   k_fit_wide    the wide list (fixed index order) and the problem rows
+//   k_fit_wide    the wide list (fixed index order), c = -inf for its members in
+//                 the sorted rows, the problem rows
 constexpr int kFitChunk = 2048;
 constexpr int kFitThreads = 256;
 constexpr int kFitPer = kFitChunk / kFitThreads;
@@ -3216,129 +3225,42 @@ struct FitStats {
   double W, M, cm, thr, s_narrow;
 };
 
-__global__ __launch_bounds__(kFitThreads) void k_fit_stats(const tpe_fit_job* __restrict__ J,
-                                                           const int32_t* __restrict__ below_idx,
-                                                           const uint32_t* __restrict__ adj,
-                                                           double* __restrict__ scratch,
-                                                           uint32_t* __restrict__ wide_scratch) {
-  const tpe_fit_job& j = J[blockIdx.y];
-  const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
-  if (c0 >= K) return;
-  const int64_t c1 = min(c0 + kFitChunk, K);
-  if (blockIdx.x == 0 && threadIdx.x == 0) wide_scratch[j.seg_off] = 0u;   // the wide list's counter
-  __shared__ uint32_t s_bp[kFitMaxBelow], s_bi[kFitMaxBelow];
-  __shared__ double lk[kFitStage];
-  __shared__ uint32_t lr[kFitStage];
-  fit_below_lds(j, below_idx, adj, s_bp, s_bi);
-  __syncthreads();
-  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
-  fit_stage(j, s_bp, s_bi, qa, qb, lk, lr);
-  __syncthreads();
-  const FitCtx<LdsSrc> c = fit_ctx(j, LdsSrc{lk, lr, qa}, (int64_t)scratch[j.seg_off + kFitHdrPos]);
-  double W = 0, M = 0, cm = 0.0, sm_all = 0;      // (cm: the largest ratio w / sigma)
-  double sm[kThr];
-  int cnt[kThr];
-#pragma unroll
-  for (int m = 0; m < kThr; ++m) { sm[m] = 0; cnt[m] = 0; }
-#pragma unroll 1
-  for (int e = 0; e < kFitPer; ++e) {
-    const int64_t i = c0 + e * kFitThreads + threadIdx.x;
-    if (i >= c1) break;
-    const double sg = c.sigma(i), w = c.weight(i);
-    W += w;
-    if (c.bounded) {
-      const double mu = c.mu(i);
-      M += w * (ncdf(c.high, mu, sg) - ncdf(c.low, mu, sg));
-    }
-    cm = fmax(cm, w / fmax(sg, kEPS));
-    if (i != c.pos) {
-      sm_all = fmax(sm_all, sg);
-#pragma unroll
-      for (int m = 0; m < kThr; ++m) {
-        const double thr = c.smin * (double)(2 << m);
-        if (sg > thr) ++cnt[m]; else sm[m] = fmax(sm[m], sg);
-      }
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    W += __shfl_xor(W, o); M += __shfl_xor(M, o);
-    cm = fmax(cm, __shfl_xor(cm, o)); sm_all = fmax(sm_all, __shfl_xor(sm_all, o));
-#pragma unroll
-    for (int m = 0; m < kThr; ++m) { sm[m] = fmax(sm[m], __shfl_xor(sm[m], o)); cnt[m] += __shfl_xor(cnt[m], o); }
-  }
-  __shared__ FitPart wp[kFitThreads / 64];
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    wp[wave].W = W; wp[wave].M = M; wp[wave].rmax = cm; wp[wave].sm_all = sm_all;
-#pragma unroll
-    for (int m = 0; m < kThr; ++m) { wp[wave].sm[m] = sm[m]; wp[wave].cnt[m] = cnt[m]; }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    FitPart r = wp[0];
-    for (int w = 1; w < kFitThreads / 64; ++w) {
-      r.W += wp[w].W; r.M += wp[w].M; r.rmax = fmax(r.rmax, wp[w].rmax); r.sm_all = fmax(r.sm_all, wp[w].sm_all);
-#pragma unroll
-      for (int m = 0; m < kThr; ++m) { r.sm[m] = fmax(r.sm[m], wp[w].sm[m]); r.cnt[m] += wp[w].cnt[m]; }
-    }
-    r.pad = 0;
-    fit_parts(j, scratch)[blockIdx.x] = r;
-  }
+// the wide candidates' counter of every job (k_fit_main appends to it)
+__global__ __launch_bounds__(256) void k_fit_wide_reset(const tpe_fit_job* __restrict__ J, int n_fit,
+                                                        uint32_t* __restrict__ wide_scratch) {
+  const int q = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (q < n_fit) wide_scratch[J[q].seg_off] = 0u;
 }
 
-// the job's chunk statistics combined once (fixed chunk order) into the header
-__global__ __launch_bounds__(64) void k_fit_combine(const tpe_fit_job* __restrict__ J,
-                                                    const int32_t* __restrict__ below_idx,
-                                                    const uint32_t* __restrict__ adj, double* __restrict__ scratch) {
-  const tpe_fit_job& j = J[blockIdx.x];
-  const int64_t K = j.n_obs - j.n_below + 1;
-  if (threadIdx.x == 0) {
-    // the grid's bounds, the f32 means of the first and last component (emit, wide)
-    const FitCtx<AboveSrc> cg = fit_ctx(j, above_src(j, below_idx, adj), (int64_t)scratch[j.seg_off + kFitHdrPos]);
-    scratch[j.seg_off + kFitHdrGrid] = (double)(float)cg.mu(0);
-    scratch[j.seg_off + kFitHdrGrid + 1] = (double)(float)cg.mu(K - 1);
-  }
-  const int nc = (int)((K + kFitChunk - 1) / kFitChunk);
-  const FitPart* __restrict__ parts = fit_parts(j, scratch);
-  __shared__ FitPart lp[64];
-  __shared__ FitPart acc;
-  for (int c0 = 0; c0 < nc; c0 += 64) {
-    const int m = min(64, nc - c0);
-    if ((int)threadIdx.x < m) lp[threadIdx.x] = parts[c0 + threadIdx.x];      // one round of loads
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      FitPart r = c0 ? acc : lp[0];
-      for (int q = c0 ? 0 : 1; q < m; ++q) {
-        const FitPart& p = lp[q];
-        r.W += p.W; r.M += p.M; r.rmax = fmax(r.rmax, p.rmax); r.sm_all = fmax(r.sm_all, p.sm_all);
-#pragma unroll
-        for (int t = 0; t < kThr; ++t) { r.sm[t] = fmax(r.sm[t], p.sm[t]); r.cnt[t] += p.cnt[t]; }
-      }
-      acc = r;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const double smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);
-    double thr = INFINITY, s_narrow = acc.sm_all;
-    for (int m = 0; m < kThr; ++m)
-      if (thr == INFINITY && acc.cnt[m] <= kPruneWide - 1) { thr = smin * (double)(2 << m); s_narrow = acc.sm[m]; }
-    double* __restrict__ hdr = scratch + j.seg_off + kFitHdrStats;
-    hdr[0] = acc.W; hdr[1] = acc.M; hdr[2] = log2(acc.rmax); hdr[3] = thr; hdr[4] = s_narrow;
-  }
+// the shift of the rows' c: an upper bound of max log2(w / sigma) (LF weights
+// <= 1, the prior's pw; every sigma >= smin), so every c <= 0 without waiting
+// for the data's maximum — the rows and the statistics come out of one pass
+__device__ __forceinline__ double fit_cm_bound(const tpe_fit_job& j, int64_t K) {
+  const double smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);
+  return log2(fmax(1.0, j.prior_weight) / fmax(smin, kEPS));
 }
 
-// The chunk's rows {mu_hi, mu_lo, a, c - shift}; wide components (the prior and
-// sigma > thr) get c = -inf in the sorted list and are listed apart.  Grid over
-// the f32 means: grid[g] = the first component with mu32 >= edge_g, edge_g =
-// glo + g / ginv (grid[G] = K); the chunk writes the buckets whose answer lies
-// in it (a binary search over its staged means) — the buckets g with
-// mu32[c0 - 1] < edge_g <= mu32[c1 - 1] (the last chunk: every g from there up,
-// K when no mean reaches edge_g).
-__global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __restrict__ J,
+// wide candidates of a job: sigma above the lowest wide threshold (2 smin) or
+// the prior — their indices in wide_scratch[seg_off + 1 ..] (counter at
+// [seg_off]), their sigmas in the fit scratch after the chunk statistics
+constexpr int kWideCap = 8192;
+__device__ __forceinline__ double* wide_sigmas(const tpe_fit_job& j, double* scratch, int64_t K) {
+  const int64_t nc = (K + kFitChunk - 1) / kFitChunk;
+  return scratch + j.seg_off + kFitHdrParts + 12 * nc;
+}
+
+// One pass per chunk: its rows {mu_hi, mu_lo, a, c = log2(w / sigma) - shift}
+// (every one finite; k_fit_wide marks the wide ones), its wide candidates, its
+// statistics (normaliser W, acceptance mass M, the wide-threshold counts) and
+// its grid buckets.  Grid over the f32 means: grid[g] = the first component
+// with mu32 >= edge_g, edge_g = glo + g / ginv (grid[G] = K); the chunk writes
+// the buckets whose answer lies in it (a binary search over its staged means) —
+// the buckets g with mu32[c0 - 1] < edge_g <= mu32[c1 - 1] (the last chunk:
+// every g from there up, K when no mean reaches edge_g).
+__global__ __launch_bounds__(kFitThreads) void k_fit_main(const tpe_fit_job* __restrict__ J,
                                                           const int32_t* __restrict__ below_idx,
                                                           const uint32_t* __restrict__ adj,
-                                                          const double* __restrict__ scratch,
+                                                          double* __restrict__ scratch,
                                                           uint32_t* __restrict__ wide_scratch,
                                                           float4* __restrict__ comp, int32_t* __restrict__ grid) {
   const tpe_fit_job& j = J[blockIdx.y];
@@ -3356,23 +3278,49 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __r
   const double* __restrict__ hdr = scratch + j.seg_off;
   const int64_t pos = (int64_t)hdr[kFitHdrPos];
   const FitCtx<LdsSrc> c = fit_ctx(j, LdsSrc{lk, lr, qa}, pos);
-  const double cm = hdr[kFitHdrStats + 2], thr = hdr[kFitHdrStats + 3];
+  const double cm = fit_cm_bound(j, K), thr0 = 2.0 * c.smin;
   float4* __restrict__ C = comp + j.above_off;
   uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
-#pragma unroll 2
+  double* __restrict__ wsg = wide_sigmas(j, scratch, K);
+  double W = 0, M = 0, sm_all = 0;
+  double sm[kThr];
+  int cnt[kThr];
+#pragma unroll
+  for (int m = 0; m < kThr; ++m) { sm[m] = 0; cnt[m] = 0; }
+#pragma unroll 1
   for (int e = 0; e < kFitPer; ++e) {
     const int64_t i = c0 + e * kFitThreads + threadIdx.x;
     if (i >= c1) break;
     const double sg = c.sigma(i), w = c.weight(i), mu = c.mu(i);
     const double se = fmax(sg, kEPS);
     const float hi = (float)mu;
-    const bool wide = i == c.pos || sg > thr;
-    C[i] = make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se),
-                       wide ? -INFINITY : (float)(log2(w / se) - cm));
-    if (wide) {
+    C[i] = make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - cm));
+    W += w;
+    if (c.bounded) M += w * (ncdf(c.high, mu, sg) - ncdf(c.low, mu, sg));
+    if (i == c.pos || sg > thr0) {
       const uint32_t slot = atomicAdd(&wl[0], 1u);
-      if (slot < (uint32_t)kPruneWide) wl[1 + slot] = (uint32_t)i;
+      if (slot < (uint32_t)kWideCap) { wl[1 + slot] = (uint32_t)i; wsg[slot] = i == c.pos ? INFINITY : sg; }
     }
+    if (i != c.pos) {
+      sm_all = fmax(sm_all, sg);
+#pragma unroll
+      for (int m = 0; m < kThr; ++m) {
+        const double thr = c.smin * (double)(2 << m);
+        if (sg > thr) ++cnt[m]; else sm[m] = fmax(sm[m], sg);
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    W += __shfl_xor(W, o); M += __shfl_xor(M, o); sm_all = fmax(sm_all, __shfl_xor(sm_all, o));
+#pragma unroll
+    for (int m = 0; m < kThr; ++m) { sm[m] = fmax(sm[m], __shfl_xor(sm[m], o)); cnt[m] += __shfl_xor(cnt[m], o); }
+  }
+  __shared__ FitPart wp[kFitThreads / 64];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    wp[wave].W = W; wp[wave].M = M; wp[wave].rmax = 0.0; wp[wave].sm_all = sm_all;
+#pragma unroll
+    for (int m = 0; m < kThr; ++m) { wp[wave].sm[m] = sm[m]; wp[wave].cnt[m] = cnt[m]; }
   }
   // ---- grid buckets of this chunk ----
   const int G = j.grid_n;
@@ -3402,6 +3350,16 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __r
     if (c0 == 0) Gp[G] = (int32_t)K;
   }
   __syncthreads();
+  if (threadIdx.x == 0) {
+    FitPart r = wp[0];
+    for (int w2 = 1; w2 < kFitThreads / 64; ++w2) {
+      r.W += wp[w2].W; r.M += wp[w2].M; r.sm_all = fmax(r.sm_all, wp[w2].sm_all);
+#pragma unroll
+      for (int m = 0; m < kThr; ++m) { r.sm[m] = fmax(r.sm[m], wp[w2].sm[m]); r.cnt[m] += wp[w2].cnt[m]; }
+    }
+    r.pad = 0;
+    fit_parts(j, scratch)[blockIdx.x] = r;
+  }
   const int ga = s_ga, gb = s_gb;
   const double glo = s_glo;
   const float ginv = s_ginv;
@@ -3418,22 +3376,75 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_emit(const tpe_fit_job* __r
   }
 }
 
-// the wide list in index order, its rows, and the job's problem rows:
+// the job's chunk statistics combined once (fixed chunk order) into the header
+__global__ __launch_bounds__(64) void k_fit_combine(const tpe_fit_job* __restrict__ J, double* __restrict__ scratch) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  const int64_t K = j.n_obs - j.n_below + 1;
+  const int nc = (int)((K + kFitChunk - 1) / kFitChunk);
+  const FitPart* __restrict__ parts = fit_parts(j, scratch);
+  __shared__ FitPart lp[64];
+  __shared__ FitPart acc;
+  for (int c0 = 0; c0 < nc; c0 += 64) {
+    const int m = min(64, nc - c0);
+    if ((int)threadIdx.x < m) lp[threadIdx.x] = parts[c0 + threadIdx.x];      // one round of loads
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      FitPart r = c0 ? acc : lp[0];
+      for (int q = c0 ? 0 : 1; q < m; ++q) {
+        const FitPart& p = lp[q];
+        r.W += p.W; r.M += p.M; r.sm_all = fmax(r.sm_all, p.sm_all);
+#pragma unroll
+        for (int t = 0; t < kThr; ++t) { r.sm[t] = fmax(r.sm[t], p.sm[t]); r.cnt[t] += p.cnt[t]; }
+      }
+      acc = r;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K);
+    double thr = INFINITY, s_narrow = acc.sm_all;
+    for (int m = 0; m < kThr; ++m)
+      if (thr == INFINITY && acc.cnt[m] <= kPruneWide - 1) { thr = smin * (double)(2 << m); s_narrow = acc.sm[m]; }
+    double* __restrict__ hdr = scratch + j.seg_off + kFitHdrStats;
+    hdr[0] = acc.W; hdr[1] = acc.M; hdr[2] = fit_cm_bound(j, K); hdr[3] = thr; hdr[4] = s_narrow;
+  }
+}
+
+// the wide list (the prior and sigma > thr, index order): its rows, c = -inf
+// for them in the sorted list, and the job's problem rows:
 // lpdf = ln2 * log2(sum) + base; base = ln2*cm - ln(W sqrt(2 pi) p_accept)
 __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__ J,
                                                  const int32_t* __restrict__ below_idx,
                                                  const uint32_t* __restrict__ adj,
-                                                 const double* __restrict__ scratch,
+                                                 double* __restrict__ scratch,
                                                  const uint32_t* __restrict__ wide_scratch,
                                                  tpe_problem* __restrict__ P, float4* __restrict__ comp) {
   const tpe_fit_job& j = J[blockIdx.x];
+  const int64_t K = j.n_obs - j.n_below + 1;
   __shared__ int64_t wide_ix[kPruneWide];
   __shared__ int s_nw;
   const uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
   const double* __restrict__ hdr = scratch + j.seg_off;
+  const double thr = hdr[kFitHdrStats + 3];
+  const FitCtx<AboveSrc> c = fit_ctx(j, above_src(j, below_idx, adj), (int64_t)hdr[kFitHdrPos]);
+  const uint32_t n_cand = wl[0];
+  const double* __restrict__ wsg = wide_sigmas(j, scratch, K);
+  if (threadIdx.x == 0) s_nw = 0;
+  __syncthreads();
+  // the candidates above thr (at most 15 and the prior: thr's definition); past
+  // the candidate list's capacity every component is examined
+  const int64_t m = n_cand <= (uint32_t)kWideCap ? (int64_t)n_cand : K;
+  for (int64_t q = threadIdx.x; q < m; q += 64) {
+    const int64_t i = n_cand <= (uint32_t)kWideCap ? (int64_t)wl[1 + q] : q;
+    const double sg = n_cand <= (uint32_t)kWideCap ? wsg[q] : (i == c.pos ? INFINITY : c.sigma(i));
+    if (sg > thr) {
+      const int slot = atomicAdd(&s_nw, 1);
+      if (slot < kPruneWide) wide_ix[slot] = i;
+    }
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const int nw = (int)min(wl[0], (uint32_t)kPruneWide);
-    for (int a = 0; a < nw; ++a) wide_ix[a] = wl[1 + a];
+    const int nw = min(s_nw, kPruneWide);
     for (int a = 1; a < nw; ++a)                  // fixed order of the wide list
       for (int b = a; b > 0 && wide_ix[b - 1] > wide_ix[b]; --b) {
         const int64_t t = wide_ix[b]; wide_ix[b] = wide_ix[b - 1]; wide_ix[b - 1] = t;
@@ -3441,7 +3452,6 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
     s_nw = nw;
   }
   __syncthreads();
-  const FitCtx<AboveSrc> c = fit_ctx(j, above_src(j, below_idx, adj), (int64_t)hdr[kFitHdrPos]);
   const FitStats st{hdr[kFitHdrStats], hdr[kFitHdrStats + 1], hdr[kFitHdrStats + 2], hdr[kFitHdrStats + 3],
                     hdr[kFitHdrStats + 4]};
   const int nw = s_nw;
@@ -3451,6 +3461,7 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
     const float hi = (float)mu;
     comp[j.wide_off + threadIdx.x] =
         make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - st.cm));
+    comp[j.above_off + i].w = -INFINITY;          // listed apart
   }
   if ((int)threadIdx.x < j.n_problems) {
     const double glo = hdr[kFitHdrGrid], ghi = hdr[kFitHdrGrid + 1];
@@ -3463,7 +3474,7 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
     p.prior_mu = (float)j.prior_mu;
     p.prior_a = (float)(kAScale / pse);
     p.prior_c = (float)(log2(j.prior_weight / pse) - st.cm);
-    p.narrow_cmax = 0.f;                           // max over all c after the shift: an upper bound
+    p.narrow_cmax = 0.f;                           // every c <= 0 (the shift is an upper bound)
     p.narrow_amin = (float)(kAScale / fmax(st.s_narrow, kEPS));
     p.grid_lo = (float)glo;
     p.grid_inv = ginv;
@@ -3664,11 +3675,11 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   uint32_t* adj = b->fit_vals_sorted;
   TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, adj, b->fit_keys);
   const unsigned chunks_k = (unsigned)((b->fit_max_obs + 1 + kFitChunk - 1) / kFitChunk);
-  TPE_LAUNCH(k_fit_stats, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
-             b->fit_vals);
-  TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->below_idx, adj, b->fit_keys);
-  TPE_LAUNCH(k_fit_emit, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
+  // the wide candidates' counters (one per job, at its segment's head)
+  TPE_LAUNCH(k_fit_wide_reset, dim3((unsigned)((b->n_fit + 255) / 256)), dim3(256), 0, s, b->fit, b->n_fit, b->fit_vals);
+  TPE_LAUNCH(k_fit_main, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
              b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid));
+  TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys);
   TPE_LAUNCH(k_fit_wide, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->below_idx, adj, b->fit_keys, b->fit_vals,
              const_cast<tpe_problem*>(b->problems), (float4*)b->comp32);
   return hip_check("tpe_fit_above/build");
