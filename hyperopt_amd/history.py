@@ -18,6 +18,7 @@ replacing documents) and every change to a pending document (values or
 loss) is picked up.  A completed document edited in place must be replaced
 in the Trials list (then ``refresh()``), not mutated.
 """
+import bisect
 import weakref
 
 import numpy as np
@@ -104,6 +105,16 @@ class History(object):
         return len(self.tids)
 
 
+def _insert1(a, at, v):
+    """np.insert(a, at, v) for one value (a new array; without np.insert's
+    per-call Python overhead, which dominates at these sizes)."""
+    out = np.empty(len(a) + 1, dtype=a.dtype)
+    out[:at] = a[:at]
+    out[at] = v
+    out[at + 1:] = a[at:]
+    return out
+
+
 class _Grow(object):
     """Append-only column; ``addr`` = host address of its buffer (kept with
     the buffer, so native calls need no per-call pointer lookup)."""
@@ -139,11 +150,17 @@ class _Cache(object):
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
         self.orders = {}               # label -> value-sorting permutation of its observations
+        self.sorted_vals = {}          # label -> its values in that order
+        self.order_ok = {}             # label -> the permutation, or None when a value is NaN
         self.order_addrs = {}          # label -> (that permutation, its address)
         self.logs = {}                 # label -> _Grow of np.log of its observation values
         self.top = None                # positions of the smallest losses, sorted by (loss, position)
         self.top_n = 0                 # documents merged into `top`
+        self.top_pos = []              # the same as lists (top is True: only the lists are current)
+        self.top_keys = []             # ... and their losses
         self.hist = None               # History view of the current documents (no pending losses)
+        self.changed = set(labels)     # labels whose column views are stale (obs_views)
+        self._views = dict.fromkeys(labels)     # (label order)
 
     def extend(self, docs, start):
         for i in range(start, len(docs)):
@@ -170,6 +187,17 @@ class _Cache(object):
                 if v:
                     self.obs_tid[k].append(tid)
                     self.obs_val[k].append(v[0])
+                    self.changed.add(k)
+
+    def obs_views(self):
+        """{label: (tids, values)} views of the columns; only the labels that
+        gained observations since the last call get new views (a new dict per
+        call: a History keeps the one it was given)."""
+        ov = self._views
+        for k in self.changed:
+            ov[k] = (self.obs_tid[k].view(), self.obs_val[k].view())
+        self.changed.clear()
+        return dict(ov)
 
     def _snap(self, vals):
         return tuple(tuple(vals.get(k) or ()) for k in self.labels)
@@ -216,21 +244,35 @@ class _Cache(object):
         observations appended since the last call (O(n) per suggest instead of
         a sort).  Any sort of a column without repeated values is the one
         np.argsort gives; the fit checks each side for repeats itself."""
-        vals = self.obs_val[k].view()
-        n = len(vals)
+        g = self.obs_val[k]
+        n = g.n
         perm = self.orders.get(k)
+        if perm is not None and len(perm) == n:
+            return self.order_ok[k]
+        vals = g.view()
         if perm is None:
             perm = np.argsort(vals)
-        elif len(perm) < n:
-            new = np.arange(len(perm), n)
-            nv = vals[new]
-            o = np.argsort(nv, kind='stable')
-            at = np.searchsorted(vals[perm], nv[o], side='right')
-            perm = np.insert(perm, at, new[o])
+            sv = vals[perm]
+        else:
+            # (the sorted values are kept beside the permutation: the insertion
+            # points are a binary search, not a gather of the whole column)
+            m = len(perm)
+            nv = vals[m:]
+            if n - m == 1:
+                sv = self.sorted_vals[k]
+                at = int(sv.searchsorted(nv[0], side='right'))
+                perm = _insert1(perm, at, m)
+                sv = _insert1(sv, at, nv[0])
+            else:
+                o = np.argsort(nv, kind='stable')
+                sv = self.sorted_vals[k]
+                at = np.searchsorted(sv, nv[o], side='right')
+                perm = np.insert(perm, at, o + m)
+                sv = np.insert(sv, at, nv[o])
         self.orders[k] = perm
-        if n and np.isnan(vals[perm[-1]]):       # NaN sorts last
-            return None
-        return perm
+        self.sorted_vals[k] = sv
+        ok = self.order_ok[k] = None if n and sv[-1] != sv[-1] else perm     # NaN sorts last
+        return ok
 
     TOP = 64
 
@@ -244,7 +286,30 @@ class _Cache(object):
         L = self.losses.view()
         if self.top is None or self.top_n > n:
             self.top, self.top_n = np.zeros(0, dtype=np.int64), 0
+        if 0 < n - self.top_n <= 8 and self.top_n:
+            # a few appended documents (FMinIter: one per suggest): merged into the
+            # (loss, position) order one at a time — a new position follows every
+            # kept one, so it goes after equal losses (bisect_right)
+            keys, pos = self.top_keys, self.top_pos
+            for p in range(self.top_n, n):
+                v = float(L[p])
+                if v != v:
+                    self.top = None
+                    return None
+                if len(pos) == self.TOP and v >= keys[-1]:
+                    continue
+                j = bisect.bisect_right(keys, v)
+                keys.insert(j, v)
+                pos.insert(j, p)
+                if len(pos) > self.TOP:
+                    keys.pop()
+                    pos.pop()
+            self.top_n = n
+            self.top = True
+            return pos[:m]
         if self.top_n < n:
+            if self.top is True:
+                self.top = np.asarray(self.top_pos, dtype=np.int64)
             new = np.arange(self.top_n, n, dtype=np.int64)
             if np.isnan(L[new]).any():
                 self.top = None
@@ -255,7 +320,9 @@ class _Cache(object):
             cand = np.concatenate([self.top, new])
             o = np.lexsort((cand, L[cand]))[:self.TOP]
             self.top, self.top_n = cand[o], n
-        return self.top[:m]
+            self.top_pos = self.top.tolist()
+            self.top_keys = L[self.top].tolist()
+        return self.top_pos[:m] if self.top is True else self.top[:m]
 
     def refresh_pending(self):
         if not self.pending:
@@ -341,8 +408,7 @@ def extract(domain, trials):
     _CACHES[trials] = cache
     cache.refresh_pending()
     tids = cache.tids.view()
-    obs = dict((k, (cache.obs_tid[k].view(), cache.obs_val[k].view())) for k in labels)
-    hist = History(tids, cache.losses.view(), obs, dev=cache.dev, cache=cache)
+    hist = History(tids, cache.losses.view(), cache.obs_views(), dev=cache.dev, cache=cache)
     cache.hist = hist if not cache.pending else None
     return hist
 

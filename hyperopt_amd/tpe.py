@@ -326,10 +326,17 @@ def _tree_labels(table, hist, engine=None):
     # keyed on the table OBJECT (the memo keeps it alive, so a new table can
     # never reuse its id), the document count and the device state's version
     memo = getattr(holder, 'tree_memo', None)
-    if (memo is not None and memo[0] is table and memo[1] == n_docs and memo[2] == dev_min
-            and (dc is None or memo[4] == dc.version)):
-        return memo[3]
-    arr = arr0.copy()
+    dver = dc.version if dc is not None else None
+    if memo is not None and memo[0] is table and memo[2] == dev_min and memo[4] == dver:
+        if memo[1] == n_docs:
+            return memo[3]
+        # documents appended (FMinIter: one per suggest), no device-fitted label:
+        # the records are updated in place — only the labels that gained
+        # observations, through the field views (no structured-scalar writes)
+        if cache is not None and n_docs > memo[1] and not memo[3][2] and _tree_refill(memo[5], meta, hist):
+            holder.tree_memo = (table, n_docs, dev_min, memo[3], dver, memo[5])
+            return memo[3]
+    arr = arr0.view(np.uint8).copy().view(arr0.dtype)      # (a byte copy: the record dtype copies field by field)
     keep, devs = [], {}
     for label, ix, fam in meta:
         rec = arr[ix]
@@ -372,8 +379,40 @@ def _tree_labels(table, hist, engine=None):
                     cols = cols[:2] + (o.ctypes.data,)
             rec['tids'], rec['values'], rec['order'] = cols
     out = (arr, keep, devs, arr.ctypes.data)
-    holder.tree_memo = (table, n_docs, dev_min, out, dc.version if dc is not None else None)
+    fv = None
+    if cache is not None and not devs and not keep:
+        fv = {f: arr[f] for f in ('tids', 'values', 'order', 'n_obs')}
+        fv['n'] = arr['n_obs'].tolist()
+    # (the version after the columns and orders above were looked up: that may move it)
+    holder.tree_memo = (table, n_docs, dev_min, out, dc.version if dc is not None else None, fv)
     return out
+
+
+def _tree_refill(fv, meta, hist):
+    """In-place update of memoised tree records (_tree_labels) after appended
+    documents: the labels whose observation count changed get their columns'
+    current addresses (a grown buffer moves) and merged value order.  False
+    (nothing written that matters: the caller rebuilds) when the records were
+    not built from the Trials cache or a value order is unavailable."""
+    if fv is None:
+        return False
+    f_tids, f_vals, f_ord, f_n, last = fv['tids'], fv['values'], fv['order'], fv['n_obs'], fv['n']
+    for label, ix, fam in meta:
+        cat = fam == N.FAM_CATEGORICAL
+        if not cat and fam != N.FAM_GAUSS and fam != N.FAM_LOGGAUSS:
+            continue                         # (quantized labels carry no columns)
+        n = len(hist.obs[label][0])
+        if n == last[ix]:
+            continue
+        if cat:
+            f_tids[ix], f_vals[ix] = hist.cat_columns(label)
+        else:
+            if hist.value_order(label) is None:
+                return False
+            f_tids[ix], f_vals[ix], f_ord[ix] = hist.native_columns(label, log=fam == N.FAM_LOGGAUSS)
+        f_n[ix] = n
+        last[ix] = n
+    return True
 
 
 def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None, columns=False):

@@ -143,6 +143,52 @@ def test_history_cache_rebuilds_on_view_changes():
     assert history._CACHES[t] is cache and len(h5) == len(h4) + 1
 
 
+def test_appended_documents_update_tree_records_in_place():
+    """FMinIter's flow — one or a few finished documents appended before each
+    suggest: the tree records updated in place (tpe._tree_refill), the merged
+    value orders and the below set kept incrementally (one-document fast
+    paths) equal a rebuild from scratch and the reference's argsort below set
+    (tpe.py:625-636) — including tied losses."""
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(600, 3)
+    table = domain.table
+    rs = np.random.RandomState(0)
+    tid = 10 ** 6
+    in_place = 0
+    for i in range(40):
+        hist = history.extract(domain, trials)
+        below = history.split_below(hist, 0.25)
+        memo = getattr(hist._cache, 'tree_memo', None)
+        tl = tpe._tree_labels(table, hist, None)
+        in_place += memo is not None and memo[3][0] is tl[0]
+        # a rebuild from scratch gives the same records
+        cache = hist._cache
+        kept = cache.tree_memo
+        cache.tree_memo = None
+        assert tpe._tree_labels(table, hist, None)[0].tobytes() == tl[0].tobytes(), i
+        cache.tree_memo = kept[:3] + (tl,) + kept[4:]
+        n_below = min(int(np.ceil(0.25 * np.sqrt(len(hist)))), 25)
+        L = hist.losses
+        order = np.argsort(L)
+        if L[order[n_below - 1]] != L[order[n_below]]:
+            assert sorted(below.tolist()) == sorted(hist.tids[order[:n_below]].tolist()), i
+        for k in table.labels:
+            o = hist.value_order(k)
+            if o is not None:
+                v = np.asarray(hist.obs[k][1], dtype=np.float64)
+                assert len(o) == len(v) and np.all(np.diff(v[o]) >= 0), (i, k)
+                assert sorted(o.tolist()) == list(range(len(v)))
+        for _ in range(rs.randint(1, 4)):
+            d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
+            d['state'] = base.JOB_STATE_DONE
+            d['result'] = {'status': 'ok', 'loss': float(rs.choice([0.0, 0.5, rs.uniform()]))}
+            tid += 1
+            trials.insert_trial_docs([d])
+        trials.refresh()
+    assert in_place >= 30
+
+
 def test_fit_posterior_exact(golden):
     for case in golden('kernel_vectors.json'):
         post = parzen.fit_posterior(case['dist'], case['args'], np.asarray(case['below']),
