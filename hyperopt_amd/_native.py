@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 17
+ABI_VERSION = 18
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -42,7 +42,9 @@ PROBLEM_DTYPE = np.dtype([
 ])
 assert PROBLEM_DTYPE.itemsize == 256
 TAB_JOB_DTYPE = np.dtype([('problem', '<i4'), ('side', '<i4'), ('kind', '<i4'), ('n', '<i4'), ('off', '<i4'),
-                          ('block0', '<i4')])
+                          ('block0', '<i4'), ('rows_off', '<i4'), ('rows_n', '<i4'), ('wide_off', '<i4'),
+                          ('wide_n', '<i4'), ('lo', '<f4'), ('inv', '<f4')])
+assert TAB_JOB_DTYPE.itemsize == 48
 TILE_DTYPE = np.dtype([('problem', '<i4'), ('cand_start', '<i4'), ('work_first', '<i4'), ('n_splits', '<i4')])
 WORK_DTYPE = np.dtype([('problem', '<i4'), ('split', '<i4'), ('cand_start', '<i4'),
                        ('k_start', '<i4'), ('k_end', '<i4'), ('n_splits', '<i4')])
@@ -91,7 +93,7 @@ class Batch(ctypes.Structure):
         ('tab', ctypes.c_void_p), ('tab_units', ctypes.c_int64),
         ('samp_tiles', ctypes.c_void_p), ('n_samp_tiles', ctypes.c_int32), ('n_samp_eager', ctypes.c_int32),
         ('tab_tiles', ctypes.c_void_p), ('n_tab_tiles', ctypes.c_int32), ('early_select', ctypes.c_int32),
-        ('run_best', ctypes.c_void_p), ('n_late', ctypes.c_int32), ('reserved8', ctypes.c_int32),
+        ('run_best', ctypes.c_void_p), ('n_late', ctypes.c_int32), ('tiles_per_problem', ctypes.c_int32),
     ]
 
 

@@ -1153,8 +1153,18 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     const int sides = p.tab_mode == TPE_TAB_CELLS ? 2 : 1;
     for (int sd = 0; sd < sides; ++sd) {
       tpe_tab_job j;
+      memset(&j, 0, sizeof(j));
       j.problem = r; j.side = sd; j.kind = p.tab_mode; j.n = p.tab_n[sd]; j.off = p.tab_off[sd];
       j.block0 = (int32_t)tab_blocks;
+      if (j.kind == TPE_TAB_CELLS) {
+        // the rows the side's cells sum (a device-fitted above side: its fit writes them)
+        j.rows_off = sd ? p.above_off : p.below_off;
+        j.rows_n = sd && dev_fit[li] ? -1 : sd ? p.above_len : p.below_len;
+        j.wide_off = sd ? p.wide_off : 0;
+        j.wide_n = sd ? p.wide_len : 0;
+        j.lo = p.tab_lo[sd];
+        j.inv = p.tab_inv[sd];
+      }
       // cells: TPE_TAB_PER_BLOCK rows per block; lattice: one block per value
       // (a box-moment label's above cells are built by their own stage: no blocks here)
       if (sd == 1 && (p.flags & TPE_F_FGT)) fgt_max_cells = std::max<int64_t>(fgt_max_cells, j.n);
@@ -1191,7 +1201,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
                 n_tab_tiles = expand ? P * n_tiles_p : (int64_t)tab_tiles.size();
   if (samp_tiles.empty()) samp_tiles.push_back(0);
   if (tab_tiles.empty()) tab_tiles.push_back(0);
-  if (tab_jobs.empty()) tab_jobs.push_back(tpe_tab_job{0, 0, 0, 0, 0, 0});
+  if (tab_jobs.empty()) tab_jobs.push_back(tpe_tab_job{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0.f, 0.f});
   const int64_t n_fin = (int64_t)fin_tiles.size();
   if (fin_tiles.empty()) fin_tiles.push_back(0);
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and

@@ -124,6 +124,24 @@ __device__ __forceinline__ bool better32(float d, int i, float bd, int bi) {
   return d > bd || (d == bd && i < bi);
 }
 
+// better32's order as one unsigned key, larger = better, 0 = no candidate: the
+// f32 key's bits made monotone (every NaN above +inf and equal to each other;
+// -0 as +0, which compares equal to it) over the complemented index (the first
+// index wins a tie)
+__device__ __forceinline__ unsigned long long key32(float d, int i) {
+  if (i < 0) return 0ull;
+  uint32_t hi = 0xffffffffu;
+  if (d == d) {
+    const uint32_t b = __float_as_uint(d + 0.f);
+    hi = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  }
+  return ((unsigned long long)hi << 32) | (unsigned long long)(~(uint32_t)i);
+}
+// DPP wave reductions of the device libraries (ockl)
+extern "C" __device__ unsigned long long __ockl_wfred_max_u64(unsigned long long);
+extern "C" __device__ float __ockl_wfred_min_f32(float);
+extern "C" __device__ float __ockl_wfred_max_f32(float);
+
 // np.argmax: NaN is the maximum (first NaN wins), otherwise the largest value,
 // first index on ties.
 __device__ __forceinline__ bool better(double s, int64_t i, double bs, int64_t bi) {
@@ -355,17 +373,17 @@ __device__ __forceinline__ float ndtri_f32(float pr) {
 // Philox block — g even: words (x, y) of block g / 2, g odd: (z, w) — a 32-bit
 // selection uniform and 23 bits of inversion; f64 draws and categories take one
 // block per candidate (53-bit selection, 53-bit inversion).
-struct DrawU { double us; float uf; double ud; };
+struct DrawU { double us; float uf; double ud; uint32_t ws; };   // ws: us's 32-bit word (f32 draws)
 __device__ __forceinline__ DrawU draw_uniforms(const tpe_problem& p, int64_t i, int precision) {
   const uint64_t g = (uint64_t)p.cand_base + (uint64_t)i;
   if (precision == TPE_PREC_F32 && p.family != TPE_FAM_CATEGORICAL) {
     const uint64_t blk = g >> 1;
     const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
     const bool odd = g & 1;
-    return DrawU{u01w(odd ? r.z : r.x), u01f(odd ? r.w : r.y), 0.0};
+    return DrawU{u01w(odd ? r.z : r.x), u01f(odd ? r.w : r.y), 0.0, odd ? r.z : r.x};
   }
   const U4 r = philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-  return DrawU{u01d(r.x, r.y), u01f(r.z), u01d(r.z, r.w)};
+  return DrawU{u01d(r.x, r.y), u01f(r.z), u01d(r.z, r.w), 0u};
 }
 
 // f32 truncation bounds of a problem: smallest float >= low, largest float < high
@@ -749,20 +767,31 @@ constexpr int kTabPer = kTile / kTabThreads;         // candidates per thread pe
 static_assert(kTabPer % 2 == 0, "a thread draws its candidates in Philox pairs");
 
 // Guide entry b of a selection CDF: k0 = the first k with cum_k > b / kGuide
-// (where the answer for any u in [b, b + 1) / kGuide starts) and the CDF values
-// of its first two steps, +inf where a step would pass the last component.
+// (where the answer for any u in [b, b + 1) / kGuide starts) and its first two
+// steps as thresholds on the 32-bit word w the uniform comes from: u = (w +
+// 0.5) 2^-32 < c  <=>  w < T(c) = ceil(c 2^32 - 0.5) (both sides exact in
+// f64), so a step is passed when w >= T; `never` flags a step past the last
+// component or a T of 2^32 (no w reaches it).  One 16-B LDS read per lookup.
 struct GuideEnt {
-  double c0, c1;          // cum[k0], cum[k0 + 1] (or +inf)
-  int k0, pad0, pad1, pad2;
+  uint32_t t0, t1;        // T(cum[k0]), T(cum[k0 + 1])
+  int32_t k0;
+  uint32_t never;         // bit 0: step 0 never passed, bit 1: step 1
 };
-static_assert(sizeof(GuideEnt) == 32, "guide entries: two 16-B LDS reads");
+static_assert(sizeof(GuideEnt) == 16, "guide entries: one 16-B LDS read");
 
-// first k with u < cum_k (k <= len - 1): the binary search's answer
-// (find_comp) on a non-decreasing CDF.  The guide entry settles it in two
-// steps; `more` flags the (rare) u that needs a third (guided_more).
-__device__ __forceinline__ int guided_comp(const GuideEnt* __restrict__ guide, double u, bool& more) {
-  const GuideEnt e = guide[min((int)(u * (double)kGuide), kGuide - 1)];
-  const bool s0 = !(u < e.c0), s1 = s0 && !(u < e.c1);
+__device__ __forceinline__ uint32_t guide_thresh(double c, uint32_t& never, uint32_t bit) {
+  const double t = ceil(c * 4294967296.0 - 0.5);
+  if (!(t < 4294967296.0)) { never |= bit; return 0xffffffffu; }
+  return t > 0.0 ? (uint32_t)t : 0u;
+}
+
+// first k with u < cum_k (k <= len - 1), u = u01w(w): the binary search's
+// answer (find_comp) on a non-decreasing CDF.  The guide entry (w's top 8
+// bits: floor(u kGuide)) settles it in two steps; `more` flags the (rare) w
+// that needs a third (guided_more).
+__device__ __forceinline__ int guided_comp(const GuideEnt* __restrict__ guide, uint32_t w, bool& more) {
+  const GuideEnt e = guide[w >> 24];
+  const bool s0 = !(e.never & 1u) && w >= e.t0, s1 = s0 && !(e.never & 2u) && w >= e.t1;
   more = s1;
   return e.k0 + (int)s0 + (int)s1;
 }
@@ -777,10 +806,10 @@ __device__ __forceinline__ int guided_more(const double* __restrict__ cum, int l
 // replaced by NAN when t lies outside the cells, in a flagged cell or the
 // series is not positive (the same arithmetic for every t inside)
 __device__ __forceinline__ float cell_log2_nb(float lo, float inv, float w, float ih, int n,
-                                              const float4* __restrict__ rows, int stride, float t) {
+                                              const float4* __restrict__ rows, int stride, int step, float t) {
   const float gj = floorf((t - lo) * inv);
   const bool in = gj >= 0.f && gj < (float)n;
-  const float4* __restrict__ r = rows + (in ? (int)gj : 0);
+  const float4* __restrict__ r = rows + step * (in ? (int)gj : 0);
   const float4 a = r[0], b = r[stride], c = r[2 * stride];
   const float u = (t - __builtin_fmaf(gj + 0.5f, w, lo)) * ih;
   float sm = c.z;
@@ -796,9 +825,10 @@ __device__ __forceinline__ float cell_log2_nb(float lo, float inv, float w, floa
 // when t lies outside the cells, in a flagged cell (NaN shift), or the series is
 // not positive (the caller then sums the mixture exactly).  w = 1 / inv, ih =
 // 1 / h: the cell centre and u as k_tables forms them.
-// (row j's k-th float4 at rows[k * stride + j * step]: global rows are
-// contiguous, stride 1 / step 3; LDS rows are split in planes, stride
-// kTabLdsCells / step 1, so random rows of a wave spread over the banks)
+// (row j's k-th float4 at rows[k * stride + j * step]: rows are contiguous,
+// stride 1 / step 3, in global memory and LDS alike — a 48-B row j starts at
+// 16-B slot 3 j mod 16 of the banks, a permutation of j mod 16, so random rows
+// of a wave spread over the banks as planes would)
 __device__ __forceinline__ float cell_log2_lds(float lo, float inv, float w, float ih, int n,
                                                const float4* __restrict__ rows, int stride, int step, float t) {
   const float gj = floorf((t - lo) * inv);
@@ -835,7 +865,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
                                                             int draw, int flags,
                                                             const float4* __restrict__ comp32,
                                                             const float4* __restrict__ tab,
-                                                            tpe_result* __restrict__ run_best) {
+                                                            tpe_result* __restrict__ run_best, int tpp) {
   __shared__ float4 tab_lds[TPE_TAB_ROW_UNITS * kTabLdsCells];
   __shared__ double cum_lds[kCumLds];
 #ifdef TPE_SAMPLE_TRACE                      // debug builds only: per-phase workgroup timing
@@ -900,7 +930,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     }
   };
   __shared__ float wf[4][kTabThreads / 64];
-  __shared__ int wfi[kTabThreads / 64];
+  __shared__ unsigned long long wkey[kTabThreads / 64];
   // the run's best -> its record (block reduction)
   auto flush = [&]() {
 #ifdef TPE_SAMPLE_TRACE
@@ -912,35 +942,23 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wave = tid >> 6;
     if (run_cells) {
-      // cells run: argmax of the f32 keys (two 32-bit shuffles per round, not five
-      // 64-bit ones), then the winner's log2 sums and draw by lane read-out
-      float d = fd;
-      int i = fi;
-      for (int off = 32; off > 0; off >>= 1) {
-        const float od = __shfl_xor(d, off);
-        const int oi = __shfl_xor(i, off);
-        if (better32(od, oi, d, i)) { d = od; i = oi; }
-      }
-      const unsigned long long m = __ballot(i >= 0 && fi == i);
-      const int src = m ? (int)__builtin_ctzll(m) : 0;
-      const float wlb = __shfl(flb, src), wla = __shfl(fla, src), wt = __shfl(ft, src);
-      if (lane == 0) { wf[0][wave] = d; wf[1][wave] = wlb; wf[2][wave] = wla; wf[3][wave] = wt; wfi[wave] = i; }
+      // cells run: better32's order as one 64-bit key per lane, reduced by the
+      // wave's DPP max (no LDS permutes); the winning lane (candidate indices are
+      // unique) leaves its log2 sums and draw for the workgroup's reduction
+      const unsigned long long key = key32(fd, fi);
+      const unsigned long long wk = __ockl_wfred_max_u64(key);
+      if (wk != 0ull && key == wk) { wf[1][wave] = flb; wf[2][wave] = fla; wf[3][wave] = ft; }
+      if (lane == 0) wkey[wave] = wk;
       __syncthreads();
 #ifdef TPE_SAMPLE_TRACE
       if (threadIdx.x == 0) g_ft[1] = wall_clock64();
 #endif
       if (wave == 0) {                       // lanes 0..15 hold the waves' bests
-        const bool in = lane < kTabThreads / 64;
-        const int q = in ? lane : 0;
-        float d2 = wf[0][q];
-        int i2 = in ? wfi[q] : -1;
-        for (int off = 8; off > 0; off >>= 1) {
-          const float od = __shfl_xor(d2, off);
-          const int oi = __shfl_xor(i2, off);
-          if (better32(od, oi, d2, i2)) { d2 = od; i2 = oi; }
-        }
-        const unsigned long long m2 = __ballot(in && i2 >= 0 && wfi[q] == i2);
+        const unsigned long long k2 = lane < kTabThreads / 64 ? wkey[lane] : 0ull;
+        const unsigned long long bk = __ockl_wfred_max_u64(k2);
+        const unsigned long long m2 = __ballot(bk != 0ull && k2 == bk);
         const int w2 = m2 ? (int)__builtin_ctzll(m2) : 0;
+        const int i2 = bk != 0ull ? (int)~(uint32_t)bk : -1;
         if (lane == 0) {
           double s2 = 0.0, l2 = 0.0, g2 = 0.0, v2 = 0.0;
           if (i2 >= 0) {
@@ -989,8 +1007,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   if ((int)threadIdx.x < n_my) {
     const int li = (int)blockIdx.x * per_wg + (int)threadIdx.x;
     const int tile = list ? list[li] : li;
-    const tpe_tile tl = tiles[tile];
-    s_tile[threadIdx.x] = tile; s_prob[threadIdx.x] = tl.problem; s_start[threadIdx.x] = tl.cand_start;
+    s_tile[threadIdx.x] = tile;
+    if (tpp > 0) {                      // uniform tiles: no descriptor round trip
+      const int r = tile / tpp;
+      s_prob[threadIdx.x] = r; s_start[threadIdx.x] = (tile - r * tpp) * kTile;
+    } else {
+      const tpe_tile tl = tiles[tile];
+      s_prob[threadIdx.x] = tl.problem; s_start[threadIdx.x] = tl.cand_start;
+    }
   }
   __syncthreads();
   for (int gi = 0; gi < n_my; ++gi) {
@@ -1009,28 +1033,34 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         __syncthreads();                               // LDS free for the next label's rows
         const double* S = samp + 8 * (int64_t)p.samp_off;
         in_lds = draw && p.samp_len > 0 && p.samp_len <= kCumLds;
-        if (in_lds) {
-          for (int q = threadIdx.x; q < p.samp_len; q += kTabThreads) {
-            const double* s = S + 8 * q;
-            cum_lds[q] = s[0];
-            const float sg = (float)s[2];
-            row_lds[q] = make_float4((float)s[1], s[5] != 0.0 ? -sg : sg, (float)s[3], (float)s[4]);
-          }
-        }
         tab_in_lds = PREC == TPE_PREC_F32 && cells && p.tab_n[0] + p.tab_n[1] <= kTabLdsCells;
-        if (tab_in_lds) {                              // plane k of cell j at tab_lds[k * kTabLdsCells + j]
-          // workgroups start at different 16-KiB windows of the tables (every CU
-          // of the problem stages the same rows: spread the first touches)
-          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], n1 = TPE_TAB_ROW_UNITS * p.tab_n[1];
-          const int nw = (n0 + n1 + kTabThreads - 1) / kTabThreads;
-          const int rot = (int)blockIdx.x % nw;
-          for (int u = 0; u < nw; ++u) {
-            const int q = ((u + rot) % nw) * kTabThreads + (int)threadIdx.x;
-            if (q >= n0 + n1) continue;
-            const float4 v = q < n0 ? tab[(int64_t)p.tab_off[0] + q] : tab[(int64_t)p.tab_off[1] + q - n0];
-            tab_lds[(q % TPE_TAB_ROW_UNITS) * kTabLdsCells + q / TPE_TAB_ROW_UNITS] = v;
+        // the table units straight from global memory into LDS (LDS-DMA: no
+        // registers, no store instructions; row-major, unit q at tab_lds[q] —
+        // a wave's 64 consecutive units land at consecutive 16-B slots), the
+        // sampler rows of threads below samp_len through registers; one round
+        // of memory latency for all of it
+        constexpr int kStageU = TPE_TAB_ROW_UNITS * kTabLdsCells / kTabThreads;
+        static_assert(kCumLds <= kTabThreads, "one sampler row per thread");
+        if (tab_in_lds) {
+          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], nu = n0 + TPE_TAB_ROW_UNITS * p.tab_n[1];
+          const int wv = (int)(threadIdx.x >> 6);
+#pragma unroll
+          for (int u = 0; u < kStageU; ++u) {
+            if (u * kTabThreads >= nu) break;          // (uniform; units past nu: a clamped load, unused slots)
+            const int q = min(u * kTabThreads + (int)threadIdx.x, nu - 1);
+            const float4* src = q < n0 ? tab + (int64_t)p.tab_off[0] + q : tab + (int64_t)p.tab_off[1] + (q - n0);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(tab_lds + u * kTabThreads + 64 * wv),
+                                             16, 0, 0);
           }
         }
+        if (in_lds && (int)threadIdx.x < p.samp_len) {
+          const double* sr = S + 8 * (int)threadIdx.x;
+          cum_lds[threadIdx.x] = sr[0];
+          const float sg = (float)sr[2];
+          row_lds[threadIdx.x] = make_float4((float)sr[1], sr[5] != 0.0 ? -sg : sg, (float)sr[3], (float)sr[4]);
+        }
+        __builtin_amdgcn_s_waitcnt(0);                 // (the LDS-DMA loads: vmcnt)
         __syncthreads();
         if (in_lds && threadIdx.x < kGuide) {          // first k with cum_k > b / kGuide, its two steps
           const double v = (double)threadIdx.x / (double)kGuide;
@@ -1039,9 +1069,9 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
           GuideEnt e;
           e.k0 = a;
-          e.c0 = a < len - 1 ? cum_lds[a] : INFINITY;
-          e.c1 = a + 1 < len - 1 ? cum_lds[a + 1] : INFINITY;
-          e.pad0 = e.pad1 = e.pad2 = 0;
+          e.never = 0u;
+          e.t0 = guide_thresh(a < len - 1 ? cum_lds[a] : INFINITY, e.never, 1u);
+          e.t1 = guide_thresh(a + 1 < len - 1 ? cum_lds[a + 1] : INFINITY, e.never, 2u);
           guide[threadIdx.x] = e;
         }
         __syncthreads();
@@ -1091,10 +1121,10 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
         const int n0 = p.tab_n[0], n1 = p.tab_n[1];
         constexpr bool kL = decltype(TL)::value;
-        constexpr int stride = kL ? kTabLdsCells : 1, step = kL ? 1 : TPE_TAB_ROW_UNITS;
+        constexpr int stride = 1, step = TPE_TAB_ROW_UNITS;      // row-major rows in LDS and global memory
         const float4* __restrict__ r0;
         const float4* __restrict__ r1;
-        if constexpr (kL) { r0 = tab_lds; r1 = tab_lds + n0; }
+        if constexpr (kL) { r0 = tab_lds; r1 = tab_lds + TPE_TAB_ROW_UNITS * n0; }
         else { r0 = tab + p.tab_off[0]; r1 = tab + p.tab_off[1]; }
         // the pair's uniforms (draw_uniforms' f32 definition): one Philox block
         // per two candidates when the first one's global index is even
@@ -1106,8 +1136,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             for (int j = 0; j < NP; j += 2) {
               const uint64_t blk = (g0 + (uint64_t)j) >> 1;
               const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-              du[j] = DrawU{u01w(r.x), u01f(r.y), 0.0};
-              du[j + 1] = DrawU{u01w(r.z), u01f(r.w), 0.0};
+              du[j] = DrawU{0.0, u01f(r.y), 0.0, r.x};
+              du[j + 1] = DrawU{0.0, u01f(r.w), 0.0, r.z};
             }
           } else {
 #pragma unroll
@@ -1121,13 +1151,13 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 #pragma unroll
           for (int j = 0; j < NP; ++j) {
             bool m;
-            kc[j] = guided_comp(guide, du[j].us, m);
+            kc[j] = guided_comp(guide, du[j].ws, m);
             more |= (unsigned)m << j;
           }
           if (__ballot(more != 0u)) {                 // (rare: a guide slice with 2+ component edges)
 #pragma unroll
             for (int j = 0; j < NP; ++j)
-              if ((more >> j) & 1u) kc[j] = guided_more(cum_lds, p.samp_len, du[j].us, kc[j]);
+              if ((more >> j) & 1u) kc[j] = guided_more(cum_lds, p.samp_len, u01w(du[j].ws), kc[j]);
           }
 #pragma unroll
           for (int j = 0; j < NP; ++j) {
@@ -1141,8 +1171,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           for (int j = 0; j < NP; ++j) {
             const int i = first + j;
             const float t = tj[j];
-            const float lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, r0, stride, t),
-                        la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, r1, stride, t);
+            const float lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, r0, stride, step, t),
+                        la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, r1, stride, step, t);
             const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
             exact |= (unsigned)(valid && !ok) << j;
             if (valid && ok) track(i, lb2, la2, t);
@@ -1159,8 +1189,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             t = coord[o];
           } else if (in_lds) {
             bool more;
-            int a = guided_comp(guide, du[j].us, more);
-            if (more) a = guided_more(cum_lds, p.samp_len, du[j].us, a);
+            int a = guided_comp(guide, du[j].ws, more);
+            if (more) a = guided_more(cum_lds, p.samp_len, u01w(du[j].ws), a);
             const float4 s = row_lds[a];
             const float pr = s.z + du[j].uf * (s.w - s.z);
             const float z = ndtri_f32(pr);
@@ -1240,8 +1270,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         for (int j = 0; j < kTabPer; j += 2) {
           const uint64_t blk = (g0 + (uint64_t)j) >> 1;
           const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-          du[j] = DrawU{u01w(r.x), u01f(r.y), 0.0};
-          du[j + 1] = DrawU{u01w(r.z), u01f(r.w), 0.0};
+          du[j] = DrawU{0.0, u01f(r.y), 0.0, r.x};
+          du[j + 1] = DrawU{0.0, u01f(r.w), 0.0, r.z};
         }
       } else {
 #pragma unroll
@@ -1254,8 +1284,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         const int i = first + j;
         if (i >= p.n_cand) break;
         bool more;
-        int a = guided_comp(guide, du[j].us, more);
-        if (more) a = guided_more(cum_lds, p.samp_len, du[j].us, a);
+        int a = guided_comp(guide, du[j].ws, more);
+        if (more) a = guided_more(cum_lds, p.samp_len, u01w(du[j].ws), a);
         const float4 sr = row_lds[a];
         const float pr = sr.z + du[j].uf * (sr.w - sr.z);
         const float z = ndtri_f32(pr);
@@ -2106,6 +2136,10 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
 
 // ============================================================ score tables
 // (include/tpe_hip.h "Tabulated scoring")
+// the job of table block b, fetched in one load round when there are <= 64
+// jobs (each lane loads a whole record; the block's is read out by lane)
+static_assert(sizeof(tpe_tab_job) == 48, "a table job: three 16-B loads");
+__device__ __forceinline__ tpe_tab_job tab_job_at(const tpe_tab_job* __restrict__ J, int n, int b);
 __device__ __forceinline__ int tab_job_of(const tpe_tab_job* __restrict__ J, int n, int b) {
   if (n <= 64) {                                    // one load round: the last job starting at or before b
     const int lane = threadIdx.x & 63;
@@ -2118,6 +2152,21 @@ __device__ __forceinline__ int tab_job_of(const tpe_tab_job* __restrict__ J, int
     if (J[m].block0 <= b) lo = m; else hi = m - 1;
   }
   return lo;
+}
+__device__ __forceinline__ tpe_tab_job tab_job_at(const tpe_tab_job* __restrict__ J, int n, int b) {
+  if (n > 64) return J[tab_job_of(J, n, b)];
+  const int lane = threadIdx.x & 63;
+  const int4* __restrict__ r = reinterpret_cast<const int4*>(J + (lane < n ? lane : 0));
+  const int4 a = r[0], c = r[1], d = r[2];
+  const unsigned long long m = __ballot(lane < n && c.y <= b);     // block0 = c.y
+  const int k = m ? 63 - __builtin_clzll(m) : 0;
+  auto rd = [&](int v) { return __builtin_amdgcn_readlane(v, k); };
+  tpe_tab_job j;
+  j.problem = rd(a.x); j.side = rd(a.y); j.kind = rd(a.z); j.n = rd(a.w);
+  j.off = rd(c.x); j.block0 = rd(c.y); j.rows_off = rd(c.z); j.rows_n = rd(c.w);
+  j.wide_off = rd(d.x); j.wide_n = rd(d.y);
+  j.lo = __int_as_float(rd(d.z)); j.inv = __int_as_float(rd(d.w));
+  return j;
 }
 
 // Taylor moments of one significant term (v >= cut) into M
@@ -2211,29 +2260,6 @@ __device__ __forceinline__ float chunk_bound(const float4 m, float c) {
   const float d = fmaxf(fmaxf(m.x - c, c - m.y), 0.f);
   const float ad = m.z * d;
   return d > 0.f ? m.w - ad * ad : m.w;
-}
-
-// one wave: {min mu, max mu, min a, max c} of chunks lane, lane + 64, ... (each
-// lane walks its chunk's rows in a rotated order: conflict-free LDS banks)
-__device__ __forceinline__ void chunk_meta(const float4* __restrict__ rows, int n, float4* __restrict__ meta,
-                                           int first_chunk, int step) {
-  const int lane = threadIdx.x & 63;
-  const int nch = (n + 63) / 64;
-  for (int g = first_chunk * 64 + lane; g < nch; g += step * 64) {
-    float lo = INFINITY, hi = -INFINITY, amin = INFINITY, cmax = -INFINITY;
-    const int last = min(n, g * 64 + 64) - 1;          // rows past n read the last row again
-    for (int i0 = 0; i0 < 64; i0 += 8) {
-      float4 q[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) q[u] = rows[min(g * 64 + ((i0 + u + lane) & 63), last)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float mu = q[u].x + q[u].y;
-        lo = fminf(lo, mu); hi = fmaxf(hi, mu); amin = fminf(amin, q[u].z); cmax = fmaxf(cmax, q[u].w);
-      }
-    }
-    meta[g] = make_float4(lo, hi, amin, cmax);
-  }
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -2654,32 +2680,56 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
 #else
 #define TT(k) (void)0
 #endif
-  const tpe_tab_job jb = J[tab_job_of(J, n_jobs, (int)blockIdx.x)];
+  const tpe_tab_job jb = tab_job_at(J, n_jobs, (int)blockIdx.x);
   const tpe_problem& p = P[jb.problem];
   const int b = (int)blockIdx.x - jb.block0;
   const int j = b * TPE_TAB_PER_BLOCK + (int)(threadIdx.x >> 6);
   if (jb.kind == TPE_TAB_CELLS) {
-    const int side = jb.side;
-    const bool pruned = side == 1 && p.narrow_amin > 0.f;
-    const int k0 = side ? p.above_off : p.below_off, n0 = side ? p.above_len : p.below_len;
-    const int k1 = side ? p.wide_off : 0, n1 = side ? p.wide_len : 0;
+    // (the job carries the rows and geometry: no problem row on this path, but
+    // for a device-fitted above side, rows_n < 0, whose fit wrote them there)
+    [[maybe_unused]] const int side = jb.side;
+    const bool pruned = jb.rows_n < 0;
+    const int k0 = pruned ? p.above_off : jb.rows_off, n0 = pruned ? p.above_len : jb.rows_n;
+    const int k1 = pruned ? p.wide_off : jb.wide_off, n1 = pruned ? p.wide_len : jb.wide_n;
     const bool stage = !pruned && n0 + n1 <= kTabStageRows;      // workgroup-uniform
     __shared__ float4 meta_lds[kChunkMax];
     TT(1);
     if (stage) {
-      for (int q = threadIdx.x; q < n0 + n1; q += kTabTblThreads)
-        rows_lds[q] = q < n0 ? comp32[k0 + q] : comp32[k1 + q - n0];
+      // every row loaded first (all in flight), then stored; wave w's rows of a
+      // round are chunk 8 u + w, summarised from registers by its DPP reductions
+      constexpr int kIters = kTabStageRows / kTabTblThreads;
+      const int n = n0 + n1, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+      float4 v[kIters];
+#pragma unroll
+      for (int u = 0; u < kIters; ++u) {
+        if (u * kTabTblThreads >= n) break;                     // (workgroup-uniform)
+        const int q = min(u * kTabTblThreads + (int)threadIdx.x, n - 1);   // (past the end: loaded, not used)
+        v[u] = q < n0 ? comp32[k0 + q] : comp32[k1 + q - n0];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < kIters; ++u) {
+        const int q0 = u * kTabTblThreads, q = q0 + (int)threadIdx.x;
+        if (q0 >= n) break;                                      // (workgroup-uniform)
+        const bool in = q < n;
+        if (in) rows_lds[q] = v[u];
+        if (q0 + 64 * wave < n) {                                // (wave-uniform: the chunk exists)
+          const float lo = __ockl_wfred_min_f32(in ? v[u].x + v[u].y : INFINITY);
+          const float hi = __ockl_wfred_max_f32(in ? v[u].x + v[u].y : -INFINITY);
+          const float amin = __ockl_wfred_min_f32(in ? v[u].z : INFINITY);
+          const float cmax = __ockl_wfred_max_f32(in ? v[u].w : -INFINITY);
+          if (lane == 0) meta_lds[(q0 >> 6) + wave] = make_float4(lo, hi, amin, cmax);
+        }
+      }
       __syncthreads();
       TT(2);
-      if (threadIdx.x < 128) chunk_meta(rows_lds, n0 + n1, meta_lds, (int)(threadIdx.x >> 6), 2);
-      __syncthreads();
     }
     TT(3);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool live = j < jb.n;                                   // wave-uniform
     // cell centre and half-width exactly as the sample stage forms them (cell_log2_lds)
-    const float w = 1.f / p.tab_inv[side];
-    const float c = __builtin_fmaf((float)j + 0.5f, w, p.tab_lo[side]);
+    const float w = 1.f / jb.inv;
+    const float c = __builtin_fmaf((float)j + 0.5f, w, jb.lo);
     const float h = 0.5f * w;
     double M[kTabMoments];
 #pragma unroll
@@ -3743,12 +3793,12 @@ int tpe_sample(const tpe_batch* b, void* stream) {
       TPE_LAUNCH(k_sample_tab<TPE_PREC_F64>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
-                         run_best);
+                         run_best, b->tiles_per_problem);
     else
       TPE_LAUNCH(k_sample_tab<TPE_PREC_F32>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
-                         run_best);
+                         run_best, b->tiles_per_problem);
   }
   return hip_check("tpe_sample");
 }
@@ -4052,6 +4102,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   b.sort_count = info.sort_count;
   b.tiles = (const tpe_tile*)(dev + info.off_tiles);
   b.n_tiles = (int32_t)info.n_tiles;
+  // (the packer gives every problem n_tiles_p tiles {r, j * kTile}, in order)
+  b.tiles_per_problem = n_tiles_p * P == info.n_tiles ? (int32_t)n_tiles_p : 0;
   b.fin_tiles = (const int32_t*)(dev + info.off_fin_tiles);
   b.n_fin_tiles = (int32_t)info.n_fin_tiles;
   b.work = (const tpe_work*)(dev + info.off_work);

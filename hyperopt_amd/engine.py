@@ -334,14 +334,18 @@ class Engine(object):
                 units += pl['n'][0]
             if pl['mode'] != N.TAB_NONE and len(lp.ids):
                 for sd in range(2 if pl['mode'] == N.TAB_CELLS else 1):
-                    jobs.append((r0, sd, pl['mode'], info['tab_n'][sd], info['tab_off'][sd], blocks))
+                    geo = (0, 0, 0, 0, 0.0, 0.0)
+                    if pl['mode'] == N.TAB_CELLS:     # the side's rows and cell geometry
+                        side = 'above' if sd else 'below'
+                        geo = (info[side + '_off'], info[side + '_len'], info.get('wide_off', 0) if sd else 0,
+                               info.get('wide_len', 0) if sd else 0, info['tab_lo'][sd], info['tab_inv'][sd])
+                    jobs.append((r0, sd, pl['mode'], info['tab_n'][sd], info['tab_off'][sd], blocks) + geo)
                     n = info['tab_n'][sd]        # cells: TAB_PER_BLOCK rows a block; lattice: a block a value
                     blocks += -(-n // N.TAB_PER_BLOCK) if pl['mode'] == N.TAB_CELLS else n
             r0 += len(lp.ids)
-        tab_jobs = np.array(jobs, dtype=np.int64).reshape(-1, 6)
-        tj = np.zeros(len(tab_jobs), dtype=N.TAB_JOB_DTYPE)
+        tj = np.zeros(len(jobs), dtype=N.TAB_JOB_DTYPE)
         for c, f in enumerate(N.TAB_JOB_DTYPE.names):
-            tj[f] = tab_jobs[:, c]
+            tj[f] = [jb[c] for jb in jobs]
 
         # problems: one row per (LevelProblem, id)
         counts = np.array([len(lp.ids) for lp in problems], dtype=np.int64)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 17
+#define TPE_ABI_VERSION 18
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -258,6 +258,12 @@ typedef struct tpe_tab_job {
   int32_t n;             /* cells / lattice values                              */
   int32_t off;           /* first 16-B unit of the table                        */
   int32_t block0;        /* first block of this job in the table stage's grid   */
+  /* cells: the side's component rows (comp32 [rows_off, rows_off + rows_n) then
+   * [wide_off, wide_off + wide_n)) and cell geometry (the problem's tab_lo /
+   * tab_inv of this side), so the table stage reads no problem row; rows_n < 0:
+   * read them from the problem (a device-fitted above side: the fit writes them) */
+  int32_t rows_off, rows_n, wide_off, wide_n;
+  float lo, inv;
 } tpe_tab_job;
 
 /* candidate tile: 2048 consecutive candidates of one problem; its above-mixture
@@ -417,7 +423,10 @@ typedef struct tpe_batch {
    * at all when n_late == 0).  0: the select stage selects every problem. */
   int32_t early_select;
   tpe_result* run_best;  /* [n_tiles], device address of host-visible memory */
-  int32_t n_late; int32_t reserved8;
+  int32_t n_late;
+  int32_t tiles_per_problem;   /* > 0: every problem has this many tiles, tile t = {t / tiles_per_problem,
+                                  (t % tiles_per_problem) * 2048} (the sample stage then reads no
+                                  tile descriptors); 0: read them */
 } tpe_batch;
 
 /* ABI version (TPE_ABI_VERSION) of the loaded library */
