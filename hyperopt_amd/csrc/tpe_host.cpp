@@ -1266,8 +1266,29 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->copy2_len = len[14];
   info->blob_bytes = end;
   if (!blob || blob_cap < end) return TPE_E_SPACE;
-  for (int i = 0; i < NS; ++i)
-    if (len[i] && src[i]) memcpy((unsigned char*)blob + off[i], src[i], (size_t)len[i]);
+  {
+    // the sections into the blob; a large level's in 256-KiB pieces on the
+    // worker pool (a batched level packs megabytes of component rows)
+    struct Piece { unsigned char* dst; const unsigned char* src; size_t n; };
+    static thread_local std::vector<Piece> pieces_tl;
+    std::vector<Piece>& pieces = pieces_tl;
+    pieces.clear();
+    constexpr size_t kPiece = 256 << 10;
+    size_t total = 0;
+    for (int i = 0; i < NS; ++i) {
+      if (!len[i] || !src[i]) continue;
+      for (size_t o = 0; o < (size_t)len[i]; o += kPiece)
+        pieces.push_back(Piece{(unsigned char*)blob + off[i] + o, (const unsigned char*)src[i] + o,
+                               std::min(kPiece, (size_t)len[i] - o)});
+      total += (size_t)len[i];
+    }
+    auto copy = [](void* c, int k) {
+      const Piece& q = (*(const std::vector<Piece>*)c)[(size_t)k];
+      memcpy(q.dst, q.src, q.n);
+    };
+    if (total >= (1u << 20) && pieces.size() > 1) tpe_pool::parallel_for((int)pieces.size(), copy, &pieces);
+    else for (size_t k = 0; k < pieces.size(); ++k) copy(&pieces, (int)k);
+  }
   if (expand) {
     unsigned char* x = (unsigned char*)blob + off[12];
     memcpy(x, xtmpl.data(), (size_t)x_tmpl);

@@ -35,6 +35,8 @@
 #include <type_traits>
 #include <vector>
 
+#include "tpe_pool.h"
+
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -910,27 +912,38 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   int64_t run_cand_base = 0, run_cand_off = 0;
   double run_bb = 0.0, run_ab = 0.0;
   bool run_logc = false, run_exp = false, run_drawn = false, run_cells = false;
-  // the run's best -> slot 0 of its first tile (block reduction)
-  // the run's record (lane 0 of wave 0): l, g and the f64 score of its best
-  auto record = [&](double s2, double l2, double g2, int64_t i2, double v2) {
+  // a run's record (one lane): l, g and the f64 score of its best -> slot 0 of
+  // its first tile, or with early selection its best with the value (the draw
+  // it kept — what the select stage's redraw would give) straight to
+  // host-visible memory
+  auto record_to = [&](int tile_r, int64_t cbase, int64_t coff, bool drawn, bool ex, double s2, double l2,
+                       double g2, int64_t i2, double v2) {
     if (run_best) {
-      // early selection: the run's best with its value (the draw it kept — what
-      // the select stage's redraw would give), straight to host-visible memory
       tpe_result r;
       r.score = s2; r.l = l2; r.g = g2; r.idx = i2; r.value = 0.0;
-      r.global_idx = i2 >= 0 ? run_cand_base + i2 : -1;
-      if (i2 >= 0) r.value = run_drawn ? (run_exp ? exp_call(v2) : v2) : cand[run_cand_off + i2];
-      run_best[run_tile] = r;
+      r.global_idx = i2 >= 0 ? cbase + i2 : -1;
+      if (i2 >= 0) r.value = drawn ? (ex ? exp_call(v2) : v2) : cand[coff + i2];
+      run_best[tile_r] = r;
 #ifdef TPE_SAMPLE_TRACE
       g_ft[2] = wall_clock64();
 #endif
     } else {
-      tpe_best* __restrict__ d = tile_best + (int64_t)run_tile * TPE_BEST_PER_TILE;
+      tpe_best* __restrict__ d = tile_best + (int64_t)tile_r * TPE_BEST_PER_TILE;
       d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
     }
   };
-  __shared__ float wf[4][kTabThreads / 64];
-  __shared__ unsigned long long wkey[kTabThreads / 64];
+  auto record = [&](double s2, double l2, double g2, int64_t i2, double v2) {
+    record_to(run_tile, run_cand_base, run_cand_off, run_drawn, run_exp, s2, l2, g2, i2, v2);
+  };
+  // cells runs are combined once, at the workgroup's end (no barrier per run:
+  // a batched level's workgroup runs through up to kTabMaxTilesPerWg problems
+  // and a per-run barrier exposed each run's slowest wave): each wave leaves
+  // its best per run — key, log2 sums, coordinate — and the run's fields
+  struct RunRec { int64_t cand_base, cand_off; double bb, ab; int tile, flags; };   // flags: 1 log, 2 exp, 4 drawn
+  __shared__ RunRec s_run[kTabMaxTilesPerWg];
+  __shared__ unsigned long long s_rk[kTabMaxTilesPerWg][kTabThreads / 64];
+  __shared__ float s_rv[kTabMaxTilesPerWg][3][kTabThreads / 64];
+  int n_def = 0;                          // cells runs deferred so far (workgroup-uniform)
   // the run's best -> its record (block reduction)
   auto flush = [&]() {
 #ifdef TPE_SAMPLE_TRACE
@@ -944,34 +957,12 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     if (run_cells) {
       // cells run: better32's order as one 64-bit key per lane, reduced by the
       // wave's DPP max (no LDS permutes); the winning lane (candidate indices are
-      // unique) leaves its log2 sums and draw for the workgroup's reduction
+      // unique) leaves its log2 sums and draw for the end-of-workgroup combine
       const unsigned long long key = key32(fd, fi);
       const unsigned long long wk = __ockl_wfred_max_u64(key);
-      if (wk != 0ull && key == wk) { wf[1][wave] = flb; wf[2][wave] = fla; wf[3][wave] = ft; }
-      if (lane == 0) wkey[wave] = wk;
-      __syncthreads();
-#ifdef TPE_SAMPLE_TRACE
-      if (threadIdx.x == 0) g_ft[1] = wall_clock64();
-#endif
-      if (wave == 0) {                       // lanes 0..15 hold the waves' bests
-        const unsigned long long k2 = lane < kTabThreads / 64 ? wkey[lane] : 0ull;
-        const unsigned long long bk = __ockl_wfred_max_u64(k2);
-        const unsigned long long m2 = __ballot(bk != 0ull && k2 == bk);
-        const int w2 = m2 ? (int)__builtin_ctzll(m2) : 0;
-        const int i2 = bk != 0ull ? (int)~(uint32_t)bk : -1;
-        if (lane == 0) {
-          double s2 = 0.0, l2 = 0.0, g2 = 0.0, v2 = 0.0;
-          if (i2 >= 0) {
-            const float t = wf[3][w2];
-            const double lnx = run_logc ? (double)t : 0.0;
-            l2 = (double)wf[1][w2] * kLn2 + run_bb - lnx;
-            g2 = (double)wf[2][w2] * kLn2 + run_ab - lnx;
-            s2 = l2 - g2;
-            v2 = (double)t;
-          }
-          record(s2, l2, g2, (int64_t)i2, v2);
-        }
-      }
+      if (wk != 0ull && key == wk) { s_rv[n_def][0][wave] = flb; s_rv[n_def][1][wave] = fla; s_rv[n_def][2][wave] = ft; }
+      if (lane == 0) s_rk[n_def][wave] = wk;
+      ++n_def;
       fi = -1;
       return;
     }
@@ -1084,6 +1075,9 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       run_exp = cells && run_logc;
       run_drawn = draw && p.samp_len > 0;
       run_cells = PREC == TPE_PREC_F32 && cells;
+      if (run_cells && threadIdx.x == 0)
+        s_run[n_def] = RunRec{run_cand_base, run_cand_off, run_bb, run_ab, run_tile,
+                              (run_logc ? 1 : 0) | (run_exp ? 2 : 0) | (run_drawn ? 4 : 0)};
 #ifdef TPE_SAMPLE_TRACE
       if (!st[1]) st[1] = wall_clock64();
 #endif
@@ -1347,6 +1341,33 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   for (int q = 0; q < kTabThreads / 64; ++q) st[4] = st[4] > s_wend[q] ? st[4] : s_wend[q];
 #endif
   if (cur >= 0) flush();
+  if (n_def > 0) {                       // the deferred cells runs: wave r combines run r
+    __syncthreads();
+#ifdef TPE_SAMPLE_TRACE
+    if (threadIdx.x == 0) g_ft[1] = wall_clock64();
+#endif
+    for (int r = wave; r < n_def; r += kTabThreads / 64) {
+      const unsigned long long k2 = lane < kTabThreads / 64 ? s_rk[r][lane] : 0ull;
+      const unsigned long long bk = __ockl_wfred_max_u64(k2);
+      const unsigned long long m2 = __ballot(bk != 0ull && k2 == bk);
+      const int w2 = m2 ? (int)__builtin_ctzll(m2) : 0;
+      const int i2 = bk != 0ull ? (int)~(uint32_t)bk : -1;
+      if (lane == 0) {
+        const RunRec rr = s_run[r];
+        double s2 = 0.0, l2 = 0.0, g2 = 0.0, v2 = 0.0;
+        if (i2 >= 0) {
+          const float t = s_rv[r][2][w2];
+          const double lnx = (rr.flags & 1) ? (double)t : 0.0;
+          l2 = (double)s_rv[r][0][w2] * kLn2 + rr.bb - lnx;
+          g2 = (double)s_rv[r][1][w2] * kLn2 + rr.ab - lnx;
+          s2 = l2 - g2;
+          v2 = (double)t;
+        }
+        record_to(rr.tile, rr.cand_base, rr.cand_off, (rr.flags & 4) != 0, (rr.flags & 2) != 0, s2, l2, g2,
+                  (int64_t)i2, v2);
+      }
+    }
+  }
 #ifdef TPE_SAMPLE_TRACE
   st[3] = wall_clock64();
   if (threadIdx.x == 0 && (blockIdx.x % 16) == 0)
@@ -4178,6 +4199,20 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     auto tile_of = [&](int i) { return list ? list[i] : i; };
     auto prob_of = [&](int t) { return tl ? tl[t].problem : (int)(t / n_tiles_p); };
     const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab);
+    if (xtmpl && n_tiles_p > 0 && per % n_tiles_p == 0) {
+      // expanded level (every problem tabulated, tiles in order) whose workgroups
+      // hold whole problems: each problem is one run, recorded at its first
+      // tile — gathered straight into `out`, in slices on the worker pool (a
+      // batched level has ~10^5 of them)
+      struct Gather { const tpe_result* rb; tpe_result* out; int64_t P, ntp, slice; } g{rb, out, P, n_tiles_p, 4096};
+      tpe_pool::parallel_for((int)((P + g.slice - 1) / g.slice), [](void* c, int k) {
+        const Gather& q = *(const Gather*)c;
+        const int64_t r1 = std::min(q.P, (k + 1) * q.slice);
+        for (int64_t r = k * q.slice; r < r1; ++r) q.out[r] = q.rb[r * q.ntp];
+      }, &g);
+      tpe_internal_phase(TPE_PHASE_LEVEL);
+      return g_prof.on ? profile_collect(b, info, xtmpl, xfirst, n_cand) : TPE_OK;
+    }
     for (int64_t r = 0; r < P; ++r)
       if (!hp || hp[r].tab_mode != TPE_TAB_NONE) { rh[r] = tpe_result{0, 0, 0, 0, -1, -1}; }
     for (int i = 0; i < n_tab; ++i) {

@@ -41,6 +41,7 @@ void phase_start() {
 }
 
 constexpr int kInactive = -2;   // label not active (None)
+constexpr int kIdBlock = 512;   // ids per block of a batched suggest's result assembly (worker pool)
 constexpr int kActive = -1;     // active label that gates nothing (placeholder)
 
 // fitted posterior of one label: continuous (w, mu, sigma) per side or the
@@ -398,27 +399,49 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       }
       if (pending) return TPE_E_FALLBACK;
       if ((rc = run(nr)) != TPE_OK) return rc;
-      bool verified = true;
+      // the prediction checked and the values written in one pass: ids in
+      // blocks (each block's rows of values/active are its own: no cache lines
+      // shared between workers; its result reads are runs of consecutive ids
+      // per label), a batched suggest's blocks in parallel on the worker pool.
+      // A failed check leaves the level-by-level path below, which rewrites
+      // every value.  rows[i]: label i's result row (-1: predicted inactive).
+      std::vector<int32_t> rows((size_t)n_labels);
       int32_t r = 0;
-      for (int i = 0; i < n_labels && verified; ++i) {
-        if (pred[(size_t)i] == kInactive) continue;
-        for (int j = 0; j < n_ids; ++j) {
-          const tpe_result& q = res[(size_t)r * n_ids + j];
-          if (q.idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
-          if (pred[(size_t)i] >= 0 && (int64_t)q.value != pred[(size_t)i]) verified = false;
-        }
-        ++r;
-      }
-      if (verified) {
-        r = 0;
-        for (int i = 0; i < n_labels; ++i) {
-          const bool on = pred[(size_t)i] != kInactive;
-          for (int j = 0; j < n_ids; ++j) {
-            values[(size_t)j * n_labels + i] = on ? res[(size_t)r * n_ids + j].value : NAN;
-            active[(size_t)j * n_labels + i] = on ? 1 : 0;
+      for (int i = 0; i < n_labels; ++i) rows[(size_t)i] = pred[(size_t)i] != kInactive ? r++ : -1;
+      const int nb = (n_ids + kIdBlock - 1) / kIdBlock;
+      std::vector<int8_t> flag((size_t)std::max(nb, 1), 0);     // per block: 1 misprediction, 2 no candidate
+      struct Col {
+        const tpe_result* res; const int32_t* rows; const int* pred; double* values; int8_t* active; int8_t* flag;
+        int n_ids, n_labels;
+      };
+      Col cx{res.data(), rows.data(), pred.data(), values, active, flag.data(), n_ids, n_labels};
+      auto blk = [](void* c, int k) {
+        const Col& q = *(const Col*)c;
+        const int j0 = k * kIdBlock, j1 = std::min(q.n_ids, j0 + kIdBlock);
+        int8_t f = 0;
+        for (int i = 0; i < q.n_labels; ++i) {
+          const int32_t rr = q.rows[i];
+          const int pd = q.pred[i];
+          for (int j = j0; j < j1; ++j) {
+            double v = NAN;
+            if (rr >= 0) {
+              const tpe_result& x = q.res[(size_t)rr * q.n_ids + j];
+              if (x.idx < 0) f |= 2;
+              if (pd >= 0 && (int64_t)x.value != pd) f |= 1;
+              v = x.value;
+            }
+            q.values[(size_t)j * q.n_labels + i] = v;
+            q.active[(size_t)j * q.n_labels + i] = rr >= 0 ? 1 : 0;
           }
-          r += on;
         }
+        q.flag[k] = f;
+      };
+      if (nb > 1) tpe_pool::parallel_for(nb, blk, &cx);
+      else blk(&cx, 0);
+      int8_t f = 0;
+      for (int k = 0; k < nb; ++k) f |= flag[(size_t)k];
+      if (f & 2) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
+      if (!(f & 1)) {
         path[0] = 1;
         return TPE_OK;
       }
@@ -466,18 +489,35 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     for (size_t q = 0; q < lvl_ids.size(); ++q) {
       if (res[q].idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
     }
-    for (size_t m = 0; m < members.size(); ++m) {
-      const int i = members[m].first;
-      const int64_t first = members[m].second;
-      const int64_t end = m + 1 < members.size() ? members[m + 1].second : (int64_t)lvl_ids.size();
-      for (int64_t q = first; q < end; ++q) {
-        const int64_t j = lvl_ids[(size_t)q];
-        const double v = res[(size_t)q].value;
-        values[(size_t)j * n_labels + i] = v;
-        active[(size_t)j * n_labels + i] = 1;
-        chosen[(size_t)j * n_labels + i] = T.gate[(size_t)i] ? (int)(int64_t)v : kActive;
+    // the members' results into their columns, ids in blocks (a block's rows
+    // are its own: no cache lines shared between workers); a member's positions
+    // hold its ids ascending, so a block's are one range, found by bisection
+    struct Mem {
+      const std::pair<int, int64_t>* members; int n_mem; const int64_t* lvl_ids; int64_t n_lvl;
+      const tpe_result* res; double* values; int8_t* active; int* chosen; const char* gate; int n_ids, n_labels;
+    };
+    Mem mx{members.data(), (int)members.size(), lvl_ids.data(), (int64_t)lvl_ids.size(), res.data(), values, active,
+           chosen.data(), T.gate.data(), n_ids, n_labels};
+    auto put = [](void* c, int k) {
+      const Mem& x = *(const Mem*)c;
+      const int64_t j0 = (int64_t)k * kIdBlock, j1 = std::min<int64_t>(x.n_ids, j0 + kIdBlock);
+      for (int m = 0; m < x.n_mem; ++m) {
+        const int i = x.members[m].first;
+        const int64_t first = x.members[m].second, end = m + 1 < x.n_mem ? x.members[m + 1].second : x.n_lvl;
+        const int64_t* lo = std::lower_bound(x.lvl_ids + first, x.lvl_ids + end, j0);
+        const int64_t* hi = std::lower_bound(lo, x.lvl_ids + end, j1);
+        for (const int64_t* p = lo; p < hi; ++p) {
+          const int64_t q = p - x.lvl_ids, j = *p;
+          const double v = x.res[(size_t)q].value;
+          x.values[(size_t)j * x.n_labels + i] = v;
+          x.active[(size_t)j * x.n_labels + i] = 1;
+          x.chosen[(size_t)j * x.n_labels + i] = x.gate[i] ? (int)(int64_t)v : kActive;
+        }
       }
-    }
+    };
+    const int nb = (n_ids + kIdBlock - 1) / kIdBlock;
+    if (nb > 1) tpe_pool::parallel_for(nb, put, &mx);
+    else put(&mx, 0);
   }
   return TPE_OK;
 }

@@ -492,9 +492,10 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     else:
         return None
     # (values / active: the engine's result buffers, consumed or copied here)
-    act_rows = active.tolist()
-    # (only labels some id used: a branch switch drops the old branch's)
-    used = act_rows[0] if len(act_rows) == 1 else np.asarray(active).any(axis=0).tolist()
+    # (only labels some id used: a branch switch drops the old branch's; a
+    # batch's rows are not turned into Python lists)
+    act_rows = active.tolist() if len(values) <= 4 else None
+    used = act_rows[0] if len(values) == 1 else np.asarray(active).any(axis=0).tolist()
     table.native_fit_hint = tuple(ix for ix in host if used[ix])
     table.native_used = tuple(i for i, u in enumerate(used) if u)
     # the device-fitted labels that ran hold their merged value orders now
