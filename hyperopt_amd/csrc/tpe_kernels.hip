@@ -2283,6 +2283,29 @@ __device__ __forceinline__ float chunk_bound(const float4 m, float c) {
   return d > 0.f ? m.w - ad * ad : m.w;
 }
 
+// one wave: {min mu, max mu, min a, max c} of chunks lane, lane + 64, ... (each
+// lane walks its chunk's rows in a rotated order: conflict-free LDS banks)
+__device__ __forceinline__ void chunk_meta(const float4* __restrict__ rows, int n, float4* __restrict__ meta,
+                                           int first_chunk, int step) {
+  const int lane = threadIdx.x & 63;
+  const int nch = (n + 63) / 64;
+  for (int g = first_chunk * 64 + lane; g < nch; g += step * 64) {
+    float lo = INFINITY, hi = -INFINITY, amin = INFINITY, cmax = -INFINITY;
+    const int last = min(n, g * 64 + 64) - 1;          // rows past n read the last row again
+    for (int i0 = 0; i0 < 64; i0 += 8) {
+      float4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = rows[min(g * 64 + ((i0 + u + lane) & 63), last)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float mu = q[u].x + q[u].y;
+        lo = fminf(lo, mu); hi = fmaxf(hi, mu); amin = fminf(amin, q[u].z); cmax = fmaxf(cmax, q[u].w);
+      }
+    }
+    meta[g] = make_float4(lo, hi, amin, cmax);
+  }
+}
+
 __device__ __forceinline__ float wave_max(float v) {
   for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
   return v;
@@ -2716,34 +2739,12 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     __shared__ float4 meta_lds[kChunkMax];
     TT(1);
     if (stage) {
-      // every row loaded first (all in flight), then stored; wave w's rows of a
-      // round are chunk 8 u + w, summarised from registers by its DPP reductions
-      constexpr int kIters = kTabStageRows / kTabTblThreads;
-      const int n = n0 + n1, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-      float4 v[kIters];
-#pragma unroll
-      for (int u = 0; u < kIters; ++u) {
-        if (u * kTabTblThreads >= n) break;                     // (workgroup-uniform)
-        const int q = min(u * kTabTblThreads + (int)threadIdx.x, n - 1);   // (past the end: loaded, not used)
-        v[u] = q < n0 ? comp32[k0 + q] : comp32[k1 + q - n0];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < kIters; ++u) {
-        const int q0 = u * kTabTblThreads, q = q0 + (int)threadIdx.x;
-        if (q0 >= n) break;                                      // (workgroup-uniform)
-        const bool in = q < n;
-        if (in) rows_lds[q] = v[u];
-        if (q0 + 64 * wave < n) {                                // (wave-uniform: the chunk exists)
-          const float lo = __ockl_wfred_min_f32(in ? v[u].x + v[u].y : INFINITY);
-          const float hi = __ockl_wfred_max_f32(in ? v[u].x + v[u].y : -INFINITY);
-          const float amin = __ockl_wfred_min_f32(in ? v[u].z : INFINITY);
-          const float cmax = __ockl_wfred_max_f32(in ? v[u].w : -INFINITY);
-          if (lane == 0) meta_lds[(q0 >> 6) + wave] = make_float4(lo, hi, amin, cmax);
-        }
-      }
+      for (int q = threadIdx.x; q < n0 + n1; q += kTabTblThreads)
+        rows_lds[q] = q < n0 ? comp32[k0 + q] : comp32[k1 + q - n0];
       __syncthreads();
       TT(2);
+      if (threadIdx.x < 128) chunk_meta(rows_lds, n0 + n1, meta_lds, (int)(threadIdx.x >> 6), 2);
+      __syncthreads();
     }
     TT(3);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
