@@ -994,6 +994,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   };
   // this workgroup's tile descriptors, fetched in one round
   __shared__ int s_tile[kTabMaxTilesPerWg], s_prob[kTabMaxTilesPerWg], s_start[kTabMaxTilesPerWg];
+  __shared__ int s_unit[kTabMaxTilesPerWg];              // per run: units handed out (dynamic pairs)
+  if ((int)threadIdx.x < kTabMaxTilesPerWg) s_unit[threadIdx.x] = 0;
   const int n_my = min(per_wg, n_list - (int)blockIdx.x * per_wg);
   if ((int)threadIdx.x < n_my) {
     const int li = (int)blockIdx.x * per_wg + (int)threadIdx.x;
@@ -1098,7 +1100,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     const double* S = samp + 8 * (int64_t)p.samp_off;
     const bool logc = p.family == TPE_FAM_LOGGAUSS;
     // a thread's candidates are consecutive: an f32 Philox block serves two of them
-    const int first = cand_start + (pair ? 2 * kTabPer : kTabPer) * (int)threadIdx.x;
+    int first = cand_start + (pair ? 2 * kTabPer : kTabPer) * (int)threadIdx.x;
+    int adv = pair ? 1 : 0;                          // tiles done beyond this one
     uint32_t exact = 0;                              // candidates the cell tables do not cover (rare)
     float tj[2 * kTabPer];
     // cells; TL: the tables are in LDS (separate instantiations, so every table
@@ -1245,14 +1248,42 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         using T = std::true_type;
         using F = std::false_type;
 #ifndef TPE_NO_FAST_CELLS                           // (A/B builds: the general pass only)
-        if (tab_in_lds && draw && in_lds && !need_x) { if (pair) cells_pass(T{}, P4{}, T{}); else cells_pass(T{}, P2{}, T{}); }
+        if (tab_in_lds && draw && in_lds && !need_x) {
+          // a run of several tile pairs (early selection): its pairs handed out
+          // to the waves in units of (pair, 64-thread slot) from an LDS counter,
+          // so waves that run ahead take more units and the run ends near the
+          // waves' mean instead of their slowest (a thread's best carries over
+          // units: the run's combine reduces every thread, whatever it drew)
+          int npairs = 0;
+          if (pair && run_best) {
+            int k = gi;
+            while (k + 1 < n_my && __builtin_amdgcn_readfirstlane(s_prob[k + 1]) == pid &&
+                   __builtin_amdgcn_readfirstlane(s_start[k + 1]) == cand_start + (k + 1 - gi) * kTile)
+              ++k;
+            npairs = (k - gi + 1) / 2;
+          }
+          if (npairs > 1) {
+            const int nu = npairs * (kTabThreads / 64);
+            for (;;) {
+              int u = 0;
+              if (lane == 0) u = atomicAdd(&s_unit[n_def], 1);
+              u = __builtin_amdgcn_readlane(u, 0);
+              if (u >= nu) break;
+              const int pr = u / (kTabThreads / 64), slot = u - pr * (kTabThreads / 64);
+              first = __builtin_amdgcn_readfirstlane(s_start[gi + 2 * pr]) + 2 * kTabPer * (slot * 64 + lane);
+              exact = 0;
+              cells_pass(T{}, P4{}, T{});
+            }
+            adv = 2 * npairs - 1;
+          } else if (pair) cells_pass(T{}, P4{}, T{}); else cells_pass(T{}, P2{}, T{});
+        }
         else
 #endif
         if (tab_in_lds) { if (pair) cells_pass(T{}, P4{}, F{}); else cells_pass(T{}, P2{}, F{}); }
         else { if (pair) cells_pass(F{}, P4{}, F{}); else cells_pass(F{}, P2{}, F{}); }
       }
     }
-    if (pair) ++gi;                                  // the pair's second tile is done
+    gi += adv;                                       // the pair's (the run's pairs') other tiles are done
     if (!cells && PREC == TPE_PREC_F32 && draw && in_lds) {
       // lattice, f32 draws: drawn as the cells path draws (draw_uniforms' pairs,
       // the staged sampler rows, ndtri_f32), quantised as draw_comp quantises
