@@ -185,6 +185,7 @@ class Engine(object):
         # continuous f32 tiles with one split: score in the above kernel (False:
         # always in the finalize stage)
         self.fuse = True
+        self.debug_flags = int(os.environ.get('TPE_DEBUG_FLAGS', '0'))   # (read once: not per call)
 
     def _stream(self):
         """The device's current torch stream as a raw hipStream_t (the same
@@ -549,8 +550,7 @@ class Engine(object):
         return info
 
     def _flags(self):
-        return (0 if self.expand else N.BATCH_NO_EXPAND) | (0 if self.fuse else N.BATCH_NO_FUSE) | \
-            int(os.environ.get('TPE_DEBUG_FLAGS', '0'))
+        return (0 if self.expand else N.BATCH_NO_EXPAND) | (0 if self.fuse else N.BATCH_NO_FUSE) | self.debug_flags
 
     # ----------------------------------------------------- one-call level
     def _level_ws(self):
@@ -943,6 +943,7 @@ class Engine(object):
 
 
 _ENGINES = {}
+_CURRENT = {}      # device index -> its engine key (get_engine without a device)
 
 
 def get_engine(device=None, precision='fp32'):
@@ -950,9 +951,15 @@ def get_engine(device=None, precision='fp32'):
     if torch is None:
         raise N.NativeUnavailable('torch is required for device memory')
     if device is None:
+        # (an engine already made for the current device: no availability query per suggest)
+        eng = _ENGINES.get(_CURRENT.get(torch.cuda.current_device()) if _CURRENT else None)
+        if eng is not None:
+            eng.set_precision(precision)
+            return eng
         if not torch.cuda.is_available():
             raise N.NativeUnavailable('no HIP device visible: the TPE engine has no CPU fallback')
         device = torch.device('cuda', torch.cuda.current_device())
+        _CURRENT[device.index] = str(device)
     key = str(device)
     eng = _ENGINES.get(key)
     if eng is None:
