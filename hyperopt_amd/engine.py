@@ -185,7 +185,6 @@ class Engine(object):
         # continuous f32 tiles with one split: score in the above kernel (False:
         # always in the finalize stage)
         self.fuse = True
-        self.debug_flags = int(os.environ.get('TPE_DEBUG_FLAGS', '0'))   # (read once: not per call)
 
     def _stream(self):
         """The device's current torch stream as a raw hipStream_t (the same
@@ -550,7 +549,9 @@ class Engine(object):
         return info
 
     def _flags(self):
-        return (0 if self.expand else N.BATCH_NO_EXPAND) | (0 if self.fuse else N.BATCH_NO_FUSE) | self.debug_flags
+        # (TPE_DEBUG_FLAGS is read per call: tests switch it on around single runs)
+        return (0 if self.expand else N.BATCH_NO_EXPAND) | (0 if self.fuse else N.BATCH_NO_FUSE) | \
+            int(os.environ.get('TPE_DEBUG_FLAGS', '0'))
 
     # ----------------------------------------------------- one-call level
     def _level_ws(self):
