@@ -21,6 +21,10 @@ cpu_baseline: the CPU oracle (numpy restatement of the reference) on a bounded
           sweep (the best pool is the figure; 1 core beside it).
 p50_suggest_ms_appending: the same suggest in an FMinIter loop (one finished
           document inserted before every suggest, fmin.py:88-92).
+config4_strong: BASELINE config 4 (4096 new ids x 4096 candidates x 20 dims)
+          with the ids split over the N ranks and one all-gather of the chosen
+          values (tpe.suggest_choices(shard_ids=...)): strong scaling of the axis
+          that shards without a per-level exchange.
 """
 import argparse
 import json
@@ -371,29 +375,34 @@ def config_workload(config, rank, world, args):
         hist = soa_history(labels, 10000, SEED, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
         table = flat_uniform_table(labels)
         n_ids, C = 4096, 4096
-        mine = np.arange(10000, 10000 + n_ids)[rank::world]
+        ids = np.arange(10000, 10000 + n_ids)
+        sid = (rank, world) if world > 1 else None
 
         def step(i, columns=True):
-            # SoA in, SoA out (tpe.ChoiceColumns); columns=False: per-id dicts
-            tpe.suggest_choices(table, hist, mine, SEED + i, n_EI_candidates=C, columns=columns)
-            return len(labels) * n_ids * C          # whole job (every rank does its share)
+            # SoA in, SoA out (tpe.ChoiceColumns); columns=False: per-id dicts.  N > 1:
+            # each rank suggests its block of the ids, one all-gather of the chosen
+            # values (tpe_exchange_allgather) — every rank holds all 4096 x 20
+            tpe.suggest_choices(table, hist, ids, SEED + i, n_EI_candidates=C, columns=columns, shard_ids=sid)
+            return len(labels) * n_ids * C          # whole job
         return ('config4: batched suggest, 4096 new_ids x 4096 candidates, 20-dim U(-5,5), 10k-trial '
-                'history, new_ids sharded over ranks, columnar results'), step, None
+                'history, new_ids sharded over ranks + one all-gather of the chosen values, columnar results'), \
+            step, None
     if config == 5:
         D, N, C = args.dims, args.history5, 4096
         labels = ['x%04d' % i for i in range(D)]
-        mine_labels = labels[rank::world]
-        hist = soa_history(mine_labels, N, SEED, lambda v: np.zeros(N))
-        # the loss must be common to all ranks: recompute it from all dims deterministically
+        hist = soa_history(labels, N, SEED, lambda v: np.zeros(N))
         rs = np.random.RandomState(SEED + 1)
         hist.losses[:] = rs.uniform(size=N) + 1e-9 * np.arange(N)
-        table = flat_uniform_table(mine_labels)
+        table = flat_uniform_table(labels)
+        sid = (rank, world) if world > 1 else None
 
         def step(i):
-            tpe.suggest_choices(table, hist, [N], SEED + i, n_EI_candidates=C)
+            # N > 1: each rank fits and scores its labels (dist.label_owners), one
+            # all-gather of the chosen values — every rank holds the whole suggestion
+            tpe.suggest_choices(table, hist, [N], SEED + i, n_EI_candidates=C, shard_labels=sid)
             return D * C
         return ('config5: %d-dim U(-5,5), %d-trial history, n_EI_candidates=4096, hyperparameters sharded '
-                'over ranks' % (D, N)), step, None
+                'over ranks + one all-gather of the chosen values' % (D, N)), step, None
     raise ValueError(config)
 
 
@@ -406,6 +415,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-quantized', action='store_true', help='skip the rf-branch (quantized) report')
     ap.add_argument('--no-appending', action='store_true', help='skip the FMinIter-style appending loop')
+    ap.add_argument('--no-config4', action='store_true', help='skip the config-4 strong-scaling record')
     ap.add_argument('--history', type=int, default=N_HISTORY)
     ap.add_argument('--cands', type=int, default=C_PER_GPU)
     ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
@@ -427,8 +437,16 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(*pre)
     if world > 1:
+        if os.environ.get('TPE_BENCH_BACKEND', 'nccl') != 'nccl':
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        # TPE_BENCH_BACKEND=gloo: a rehearsal of the N > 1 flow with several ranks on
+        # one GPU (RCCL takes one rank per device); the driver's runs use nccl (RCCL)
+        backend = os.environ.get('TPE_BENCH_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device('cuda', local)
     torch.cuda.set_device(device)
 
@@ -558,6 +576,29 @@ def main():
                          note='one evaluated document inserted (and trials.refresh()) before every suggest, '
                               'as FMinIter.run does; the suggest alone is timed')
 
+    # config 4 (BASELINE configs[3]: the batched suggest that shards naturally)
+    # beside the line: 4096 new ids x 4096 candidates x 20 dims in total, the ids
+    # split over the N ranks (strong scaling) and one all-gather of the results
+    cfg4 = None
+    if not args.no_config4:
+        desc4, step4, _ = config_workload(4, rank, world, args)
+        for i in range(2):
+            step4(i)
+        barrier()
+        t0 = time.perf_counter()
+        n4, units4 = 5, 0
+        for i in range(n4):
+            units4 = step4(100 + i)
+        barrier()
+        el4 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el4], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el4 = float(t.item())
+        cfg4 = dict(workload=desc4, value=units4 * n4 / el4, unit='candidate-scores/s', steps=n4,
+                    ms_per_step=1e3 * el4 / n4, scaling='strong', n_gpus=world,
+                    parallelism='new-id shard x%d' % world)
+
     if rank == 0:
         out = {
             'metric': 'EI candidates scored/sec (node) + tpe.suggest p50 latency, 1M cands x 10k trials',
@@ -575,6 +616,7 @@ def main():
             'active_hyperparameters_per_suggest': n_active / args.steps,
             'stage_ms': stages, 'roofline': roof, 'kernels': kernels, 'cpu_baseline': cpu,
             'quantized_branch': quant,
+            'config4_strong': cfg4,
             # the same 2^20 candidates in total over N ranks (N = 1: the line itself)
             'strong_scaling': strong if strong is not None else dict(
                 n_EI_candidates_total=C_total, per_rank=C_total, value=value, unit='candidate-scores/s',

@@ -11,11 +11,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 18
+ABI_VERSION = 19
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT, F_FGT = 1, 2, 4, 8, 16, 32, 64
+F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT, F_FGT, F_REMOTE = 1, 2, 4, 8, 16, 32, 64, 128
 TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
 TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
@@ -234,7 +234,7 @@ EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_si
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
            'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read',
            'tpe_suggest_tree', 'tpe_comm_unique_id', 'tpe_comm_init', 'tpe_comm_destroy', 'tpe_combine_results',
-           'tpe_host_threads', 'tpe_host_phases')
+           'tpe_host_threads', 'tpe_host_phases', 'tpe_exchange_allgather')
 
 # host phases of tpe_suggest_tree (tpe_host_phases order)
 PHASES = ('prefit', 'pack', 'launched', 'synced', 'level', 'return')
@@ -325,6 +325,8 @@ def load(path=LIB_PATH):
     lib.tpe_comm_destroy.restype = ctypes.c_int
     lib.tpe_combine_results.argtypes = [P, I32, I64, P]
     lib.tpe_combine_results.restype = ctypes.c_int
+    lib.tpe_exchange_allgather.argtypes = [ctypes.POINTER(Exchange), P, I64, P, P]
+    lib.tpe_exchange_allgather.restype = ctypes.c_int
     lib.tpe_host_threads.argtypes = [I32, ctypes.POINTER(I32)]
     lib.tpe_host_threads.restype = ctypes.c_int
     lib.tpe_host_phases.argtypes = [I32, P, I32]

@@ -4346,6 +4346,33 @@ int tpe_combine_results(const tpe_result* all, int32_t world, int64_t P, tpe_res
   return TPE_OK;
 }
 
+int tpe_exchange_allgather(const tpe_exchange* ex, const void* mine, int64_t bytes, void* all, void* stream) {
+  if (!ex || bytes < 0 || (bytes > 0 && (!mine || !all)) || ex->world < 1 || ex->rank < 0 || ex->rank >= ex->world)
+    return fail(TPE_E_ARG, "tpe_exchange_allgather: bad arguments");
+  const int W = ex->world;
+  if (ex->comm) {
+    Rccl& r = rccl();
+    if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
+    if (!ex->dev || ex->dev_bytes < bytes * W) return fail(TPE_E_ARG, "tpe_exchange: device scratch too small");
+    if (bytes == 0) return TPE_OK;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned char* d = (unsigned char*)ex->dev;
+    hipError_t e = hipMemcpyAsync(d + (size_t)bytes * ex->rank, mine, (size_t)bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    // in place: rank r's block already sits at its slot of the receive buffer
+    const ncclResult_t ne = r.all_gather(d + (size_t)bytes * ex->rank, d, (size_t)bytes, ncclUint8,
+                                         (ncclComm_t)ex->comm, s);
+    if (ne != ncclSuccess) return rccl_fail("ncclAllGather", ne);
+    e = hipMemcpyAsync(all, d, (size_t)bytes * W, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    return TPE_OK;
+  }
+  if (!ex->gather) return fail(TPE_E_ARG, "tpe_exchange: neither a communicator nor a gather function");
+  if (ex->gather(ex->ctx, mine, bytes, all) != 0) return fail(TPE_E_HIP, "tpe_exchange: gather failed");
+  return TPE_OK;
+}
+
 // one exchange of a sharded level (tpe_suggest.cpp): every rank's status and
 // P results -> the global winners in res, the worst status in *status
 __attribute__((visibility("hidden"))) int tpe_internal_exchange(const tpe_exchange* ex, void* stream, int32_t my_status,
@@ -4357,24 +4384,8 @@ __attribute__((visibility("hidden"))) int tpe_internal_exchange(const tpe_exchan
   all.resize((size_t)per * W);
   memcpy(mine.data(), &my_status, sizeof(my_status));
   if (P > 0) memcpy(mine.data() + TPE_EXCHANGE_HEADER, res, (size_t)P * sizeof(tpe_result));
-  if (ex->comm) {
-    Rccl& r = rccl();
-    if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
-    if (!ex->dev || ex->dev_bytes < per * W) return fail(TPE_E_ARG, "tpe_exchange: device scratch too small");
-    hipStream_t s = (hipStream_t)stream;
-    unsigned char* d = (unsigned char*)ex->dev;
-    hipError_t e = hipMemcpyAsync(d + (size_t)per * ex->rank, mine.data(), (size_t)per, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
-    // in place: rank r's block already sits at its slot of the receive buffer
-    const ncclResult_t ne = r.all_gather(d + (size_t)per * ex->rank, d, (size_t)per, ncclUint8, (ncclComm_t)ex->comm, s);
-    if (ne != ncclSuccess) return rccl_fail("ncclAllGather", ne);
-    e = hipMemcpyAsync(all.data(), d, (size_t)per * W, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
-  } else {
-    if (!ex->gather) return fail(TPE_E_ARG, "tpe_exchange: neither a communicator nor a gather function");
-    if (ex->gather(ex->ctx, mine.data(), per, all.data()) != 0) return fail(TPE_E_HIP, "tpe_exchange: gather failed");
-  }
+  const int xrc = tpe_exchange_allgather(ex, mine.data(), per, all.data(), stream);
+  if (xrc != TPE_OK) return xrc;
   int32_t worst = TPE_OK;
   static thread_local std::vector<tpe_result> recs;
   recs.resize((size_t)std::max<int64_t>(P * W, 1));

@@ -39,6 +39,7 @@ struct Pool {
   std::atomic<int> left{0};                 // jobs of the current generation not yet returned
   std::atomic<int> sleepers{0};
   std::atomic<bool> stop{false};
+  std::atomic<bool> retired{false};         // replaced by tpe_host_threads: dispatch nothing more to it
   uint32_t gen = 0;                         // dispatcher's generation counter
   int64_t spin_ns = 200000;
   std::vector<std::thread> th;
@@ -105,6 +106,10 @@ void after_fork_child() {        // the workers do not exist in the child: start
   g_pool = nullptr;
 }
 
+// joins the workers of a retired pool.  The Pool object itself is never
+// freed: a concurrent parallel_for may still hold its pointer (from get_pool,
+// before the swap) and will find it retired under `busy` — a few hundred
+// bytes per tpe_host_threads change, which is a configuration call
 void stop_pool(Pool* p) {
   {
     std::lock_guard<std::mutex> lk(p->m);
@@ -112,7 +117,7 @@ void stop_pool(Pool* p) {
   }
   p->cv.notify_all();
   for (auto& t : p->th) t.join();
-  delete p;
+  p->th.clear();
 }
 
 int total_threads() {            // under g_mu
@@ -147,7 +152,12 @@ void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
   std::unique_lock<std::mutex> own;
   if (p) {
     own = std::unique_lock<std::mutex>(p->busy, std::try_to_lock);
-    if (!own.owns_lock()) p = nullptr;
+    if (!own.owns_lock()) {
+      p = nullptr;
+    } else if (p->retired.load()) {                 // replaced since get_pool: run here
+      own.unlock();
+      p = nullptr;
+    }
   }
   if (!p) {
     for (int i = 0; i < n; ++i) fn(ctx, i);
@@ -193,7 +203,10 @@ extern "C" int tpe_host_threads(int32_t n, int32_t* previous) {
     }
   }
   if (old) {
-    { std::lock_guard<std::mutex> busy(old->busy); }  // a dispatch in flight finishes first
+    {
+      std::lock_guard<std::mutex> busy(old->busy);   // a dispatch in flight finishes first
+      old->retired.store(true);                      // later dispatchers holding `old` run serially
+    }
     stop_pool(old);
   }
   return TPE_OK;

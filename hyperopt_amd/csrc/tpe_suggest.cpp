@@ -43,6 +43,7 @@ void phase_start() {
 constexpr int kInactive = -2;   // label not active (None)
 constexpr int kIdBlock = 512;   // ids per block of a batched suggest's result assembly (worker pool)
 constexpr int kActive = -1;     // active label that gates nothing (placeholder)
+constexpr int32_t kRemoteRow = -2;   // fused batch: an active label another rank evaluates (TPE_F_REMOTE)
 
 // fitted posterior of one label: continuous (w, mu, sigma) per side or the
 // categorical probabilities (mu / sigma null)
@@ -179,7 +180,7 @@ constexpr int64_t kPrefitMinObs = 256;
 
 bool prefit_worthy(const Tree& T, int i) {
   const tpe_tree_label& L = T.L[i];
-  if (L.host_k[0] > 0 || L.n_obs < kPrefitMinObs || !L.tids || !L.values) return false;
+  if ((L.flags & TPE_F_REMOTE) || L.host_k[0] > 0 || L.n_obs < kPrefitMinObs || !L.tids || !L.values) return false;
   if (L.family == TPE_FAM_CATEGORICAL) return L.upper > 0;
   if (L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) return false;
   const bool dev = T.device_fit_min > 0 && L.n_obs >= std::max<int64_t>(T.device_fit_min, 64);
@@ -343,11 +344,16 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     }
     T.max_depth = std::max(T.max_depth, L.depth);
   }
+  for (int i = 0; i < n_labels; ++i)
+    if ((labels[i].flags & TPE_F_REMOTE) && T.gate[(size_t)i])
+      return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: a gate cannot be remote (every rank evaluates the gates)");
   // spaces for the general path, refused before any fit or run: non-categorical
-  // gates, and continuous labels large enough for the device Parzen fit
+  // gates, and continuous labels large enough for the device Parzen fit (labels
+  // another rank evaluates are never fitted here)
   for (int i = 0; i < n_labels; ++i) {
     const tpe_tree_label& L = labels[i];
     if (T.gate[(size_t)i] && L.family != TPE_FAM_CATEGORICAL) return TPE_E_FALLBACK;
+    if (L.flags & TPE_F_REMOTE) continue;
     if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && L.host_k[0] <= 0 && !L.dev_obs &&
         device_fit_min > 0 && L.n_obs >= std::max<int64_t>(device_fit_min, 64))
       return TPE_E_FALLBACK;
@@ -390,7 +396,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       int32_t nr = 0;
       bool pending = false;                 // labels flagged for the caller's fit: all of them at once
       for (int i = 0; i < n_labels; ++i) {
-        if (pred[(size_t)i] == kInactive) continue;
+        if (pred[(size_t)i] == kInactive || (labels[i].flags & TPE_F_REMOTE)) continue;
         if ((rc = fit_label(T, i)) != TPE_OK) {
           if (rc == TPE_E_FALLBACK && need_fit && need_fit[i]) { pending = true; continue; }
           return rc;
@@ -404,10 +410,12 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       // shared between workers; its result reads are runs of consecutive ids
       // per label), a batched suggest's blocks in parallel on the worker pool.
       // A failed check leaves the level-by-level path below, which rewrites
-      // every value.  rows[i]: label i's result row (-1: predicted inactive).
+      // every value.  rows[i]: label i's result row (-1: predicted inactive,
+      // kRemoteRow: active, evaluated by another rank).
       std::vector<int32_t> rows((size_t)n_labels);
       int32_t r = 0;
-      for (int i = 0; i < n_labels; ++i) rows[(size_t)i] = pred[(size_t)i] != kInactive ? r++ : -1;
+      for (int i = 0; i < n_labels; ++i)
+        rows[(size_t)i] = pred[(size_t)i] == kInactive ? -1 : (labels[i].flags & TPE_F_REMOTE) ? kRemoteRow : r++;
       const int nb = (n_ids + kIdBlock - 1) / kIdBlock;
       std::vector<int8_t> flag((size_t)std::max(nb, 1), 0);     // per block: 1 misprediction, 2 no candidate
       struct Col {
@@ -431,7 +439,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
               v = x.value;
             }
             q.values[(size_t)j * q.n_labels + i] = v;
-            q.active[(size_t)j * q.n_labels + i] = rr >= 0 ? 1 : 0;
+            q.active[(size_t)j * q.n_labels + i] = rr >= 0 || rr == kRemoteRow ? 1 : 0;
           }
         }
         q.flag[k] = f;
@@ -461,6 +469,14 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     for (int i = 0; i < n_labels; ++i) {
       const tpe_tree_label& L = labels[i];
       if (L.depth != d) continue;
+      if (L.flags & TPE_F_REMOTE) {         // active where the tree says, evaluated by another rank
+        for (int j = 0; j < n_ids; ++j)
+          if (is_active(L, chosen.data() + (size_t)j * n_labels)) {
+            active[(size_t)j * n_labels + i] = 1;
+            chosen[(size_t)j * n_labels + i] = kActive;
+          }
+        continue;
+      }
       const int64_t first = (int64_t)lvl_ids.size();
       for (int j = 0; j < n_ids; ++j)
         if (is_active(L, chosen.data() + (size_t)j * n_labels)) lvl_ids.push_back(j);

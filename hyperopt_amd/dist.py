@@ -15,6 +15,13 @@ it an RCCL communicator (nccl process groups: an all-gather over xGMI on a
 device buffer, issued from C on the suggest's stream) or a host all-gather
 through ``torch.distributed`` (gloo groups).  ``allgather_results`` is the
 same combine for the Python general path.
+
+The other two axes (include/tpe_hip.h, "Shard axes") exchange once, after the
+whole suggest: ``gather_id_blocks`` (new-id axis: every rank's block of ids)
+and ``gather_label_columns`` (hyperparameter axis: every rank's labels), both
+through ``tpe_exchange_allgather`` on the same exchange.  A rank whose own
+part failed still takes part (status word), so no rank waits forever and every
+rank raises.
 """
 import ctypes
 import os
@@ -27,6 +34,22 @@ from . import _native as N
 def shard_range(n_total, rank, world):
     """Contiguous [start, stop) of the candidate index range owned by ``rank``."""
     return (n_total * rank) // world, (n_total * (rank + 1)) // world
+
+
+def label_owners(table, world):
+    """Hyperparameter-axis shard of a ParamTable over ``world`` ranks: per label
+    (table order) the rank that evaluates it, -1 for the gates — every rank
+    evaluates those, so every rank knows which labels are active.  The other
+    labels go round-robin in table order (config 5: 1000 labels, 125 a rank)."""
+    gates = set(table.parent_labels)
+    owner, k = [], 0
+    for r in table.rows:
+        if r.label in gates:
+            owner.append(-1)
+        else:
+            owner.append(k % world)
+            k += 1
+    return owner
 
 
 def combine_results(stacked):
@@ -76,13 +99,14 @@ class _Exchange(object):
         import torch.distributed as dist
         self.engine, self.group = engine, group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
-        self.lib = engine.lib
+        # (no engine: a host-gather exchange, e.g. the CPU tests of the gathers)
+        self.lib = engine.lib if engine is not None else N.load()
         self.comm = None
         self.scratch = None
         self.ex = N.Exchange()
         self.ex.rank, self.ex.world, self.ex.always = self.rank, self.world, 1 if always else 0
         mode = os.environ.get('TPE_EXCHANGE', 'auto')
-        if dist.get_backend(group) == 'nccl' and mode != 'host':
+        if dist.get_backend(group) == 'nccl' and mode != 'host' and engine is not None:
             # RCCL communicator of this process group: rank 0's id, broadcast
             idb = ctypes.create_string_buffer(N.COMM_ID_BYTES)
             if self.rank == 0:
@@ -98,7 +122,8 @@ class _Exchange(object):
             self.ex.comm = comm.value
             self.ex.gather = N.GATHER_FN()
         else:
-            torch_dev = torch.device('cuda', engine._dev_index) if dist.get_backend(group) == 'nccl' else None
+            torch_dev = torch.device('cuda', engine._dev_index) if dist.get_backend(group) == 'nccl' and \
+                engine is not None else None
 
             def gather(ctx, mine, nbytes, out):
                 try:
@@ -116,15 +141,31 @@ class _Exchange(object):
             self._gather = N.GATHER_FN(gather)   # (kept alive with the struct)
             self.ex.gather = self._gather
 
+    def allgather(self, buf, stream=None):
+        """All-gather of a host byte buffer (one per rank, equal sizes) through
+        tpe_exchange_allgather: uint8 [world, nbytes] in rank order."""
+        buf = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+        n = buf.nbytes
+        out = np.empty((self.world, n), dtype=np.uint8)
+        if self.comm is not None:
+            self._scratch(self.world * n)
+        N.check(self.lib.tpe_exchange_allgather(ctypes.byref(self.ex), buf.ctypes.data, n, out.ctypes.data,
+                                                stream if stream is not None or self.engine is None
+                                                else self.engine._stream()),
+                self.lib, 'tpe_exchange_allgather')
+        return out
+
+    def _scratch(self, need):
+        import torch
+        if self.scratch is None or self.scratch.numel() < need:
+            self.scratch = torch.empty(max(need, 2 * (self.scratch.numel() if self.scratch is not None else 0)),
+                                       dtype=torch.uint8, device=self.engine.device)
+            self.ex.dev, self.ex.dev_bytes = self.scratch.data_ptr(), self.scratch.numel()
+
     def ptr(self, max_problems):
         """The struct for a suggest of at most ``max_problems`` problems per level."""
         if self.comm is not None:
-            import torch
-            need = self.world * (N.EXCHANGE_HEADER + max(int(max_problems), 1) * N.RESULT_DTYPE.itemsize)
-            if self.scratch is None or self.scratch.numel() < need:
-                self.scratch = torch.empty(max(need, 2 * (self.scratch.numel() if self.scratch is not None else 0)),
-                                           dtype=torch.uint8, device=self.engine.device)
-                self.ex.dev, self.ex.dev_bytes = self.scratch.data_ptr(), self.scratch.numel()
+            self._scratch(self.world * (N.EXCHANGE_HEADER + max(int(max_problems), 1) * N.RESULT_DTYPE.itemsize))
         return ctypes.byref(self.ex)
 
     def close(self):
@@ -149,3 +190,68 @@ def exchange_for(engine, group=None, always=None):
     if ex is None:
         ex = _EXCHANGES[key] = _Exchange(engine, group, always)
     return ex
+
+
+# ------------------------------------------------------------ id / label axes
+_HDR = 8        # per-rank payload header: int64 status (0 ok, 1 failed)
+
+
+def _exchange_status(ex, payload, failed):
+    """All-gather ``payload`` (bytes, equal size on every rank) after an int64
+    status word; raises on every rank when some rank failed."""
+    buf = np.zeros(_HDR + payload.nbytes, dtype=np.uint8)
+    buf[:_HDR].view(np.int64)[0] = 1 if failed else 0
+    buf[_HDR:] = payload.view(np.uint8).reshape(-1)
+    allb = ex.allgather(buf)
+    bad = [r for r in range(ex.world) if allb[r, :_HDR].view(np.int64)[0] != 0]
+    if bad:
+        raise RuntimeError('sharded suggest failed on rank(s) %s' % bad)
+    return allb[:, _HDR:]
+
+
+def gather_id_blocks(ex, values, active, n_ids, n_labels, failed=False):
+    """New-id axis: rank r computed ids [shard_range(n_ids, r, world)) —
+    ``values`` float64 / ``active`` bool [block x n_labels] — and every rank
+    gets the whole [n_ids x n_labels] pair (one all-gather, blocks padded to
+    the largest)."""
+    world = ex.world
+    blocks = [shard_range(n_ids, r, world) for r in range(world)]
+    m = max(hi - lo for lo, hi in blocks)
+    per = m * n_labels
+    pay = np.zeros(per * 9, dtype=np.uint8)
+    if not failed:
+        lo, hi = blocks[ex.rank]
+        k = (hi - lo) * n_labels
+        pay[:8 * per].view(np.float64)[:k] = np.asarray(values, dtype=np.float64).reshape(-1)
+        pay[8 * per:8 * per + k] = np.asarray(active, dtype=bool).reshape(-1)
+    allb = _exchange_status(ex, pay, failed)
+    out_v = np.empty((n_ids, n_labels))
+    out_a = np.empty((n_ids, n_labels), dtype=bool)
+    for r, (lo, hi) in enumerate(blocks):
+        k = (hi - lo) * n_labels
+        out_v[lo:hi] = allb[r, :8 * per].view(np.float64)[:k].reshape(hi - lo, n_labels)
+        out_a[lo:hi] = allb[r, 8 * per:8 * per + k].view(bool).reshape(hi - lo, n_labels)
+    return out_v, out_a
+
+
+def gather_label_columns(ex, values, owner, failed=False):
+    """Hyperparameter axis: ``values`` float64 [n_ids x n_labels] holds this
+    rank's labels (``owner[ix] == rank``; the gates, owner -1, everywhere);
+    the other columns are filled from their owners (one all-gather of each
+    rank's columns, padded to the largest share).  Activity needs no exchange:
+    every rank evaluated the gates.  (A failed rank passes NaN values of the
+    right shape.)"""
+    world, rank = ex.world, ex.rank
+    values = np.asarray(values, dtype=np.float64)
+    n = values.shape[0]
+    cols = [[ix for ix, o in enumerate(owner) if o == r] for r in range(world)]
+    m = max(len(c) for c in cols)
+    pay = np.zeros((n, m))
+    if not failed and cols[rank]:
+        pay[:, :len(cols[rank])] = values[:, cols[rank]]
+    allb = _exchange_status(ex, pay, failed)
+    out = values.copy()
+    for r in range(world):
+        if r != rank and cols[r]:
+            out[:, cols[r]] = allb[r].view(np.float64).reshape(n, m)[:, :len(cols[r])]
+    return out

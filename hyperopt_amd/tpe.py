@@ -27,6 +27,10 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
   * ``precision``: 'fp32' (default) or 'fp64' for the continuous families.
   * ``shard=(rank, world)``: split every problem's candidates over ranks of
     the default ``torch.distributed`` group (see dist.py).
+  * ``shard_ids=(rank, world)`` / ``shard_labels=(rank, world)``: split a
+    batched suggest's new ids / its hyperparameters over the ranks; one
+    all-gather of the chosen values after the suggest, every rank returns the
+    whole result (include/tpe_hip.h "Shard axes").
 
 ``linear_forgetting`` is accepted and, as in the reference, not used: the
 forgetting window is fixed at DEFAULT_LF=25 (tpe.py:27-29).
@@ -81,10 +85,10 @@ class _Fits(object):
             eng = self.engine
             f32 = eng is not None and eng.precision == 'fp32'
             bidx = None
-            if (f32 and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES
-                    and len(ovals) >= max(eng.device_fit_min, 64)):
+            dmin = _dev_fit_min(eng)
+            if dmin is not None and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and len(ovals) >= dmin:
                 bidx = _history.below_index(otids, self.below_tids, self.hist.sorted_obs)
-                if len(ovals) - len(bidx) >= max(eng.device_fit_min, 64):
+                if device_fits(len(ovals), len(bidx), dmin):
                     dc = devhist.columns(self.hist, eng.device)
                     # the kernel coordinate (numpy's log for the log families, as the host fits use)
                     logc = _FAMILY[row.dist] == N.FAM_LOGGAUSS
@@ -184,7 +188,7 @@ def _predict_activity(table, fits, C):
     return chosen
 
 
-def _choices_fused(table, fits, new_ids, seed, C, engine, shard):
+def _choices_fused(table, fits, new_ids, seed, C, engine, shard, remote=()):
     """Every tree level in ONE device batch under the predicted activity; the
     gates' device winners are then checked against the prediction.  A problem's
     draws depend only on (seed, label, new_id) and its scores on the fits, so a
@@ -196,12 +200,16 @@ def _choices_fused(table, fits, new_ids, seed, C, engine, shard):
     if pred is None:
         return None
     ids = np.asarray(new_ids, dtype=np.int64)
-    rows = [r for r in table.rows if pred[r.label] is not None]
+    rows = [r for r in table.rows if pred[r.label] is not None and r.index not in remote]
     problems = [LevelProblem(fits.get(r), r.index, ids) for r in rows]
     res = _run(engine, problems, C, seed, shard)
     n = len(ids)
     order = table.level_order()
     chosen = [dict.fromkeys(order) for _ in new_ids]
+    for r in table.rows:                     # active here, evaluated by another rank
+        if r.index in remote and pred[r.label] is not None:
+            for d in chosen:
+                d[r.label] = np.nan
     idx = res['idx']
     for k, row in enumerate(rows):
         if (idx[k * n:(k + 1) * n] < 0).any():
@@ -215,9 +223,12 @@ def _choices_fused(table, fits, new_ids, seed, C, engine, shard):
     return chosen
 
 
-def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
+def _choices_philox(table, fits, new_ids, seed, C, engine, shard, remote=()):
+    """Level by level over the tree (after the fused batch when it applies).
+    ``remote``: label indices another rank evaluates (hyperparameter-axis
+    shard, never a gate): active ones get NaN here."""
     if SPECULATE and table.n_levels > 1:
-        fused = _choices_fused(table, fits, new_ids, seed, C, engine, shard)
+        fused = _choices_fused(table, fits, new_ids, seed, C, engine, shard, remote)
         if fused is not None:
             return fused
     ids = np.asarray(new_ids, dtype=np.int64)
@@ -231,6 +242,10 @@ def _choices_philox(table, fits, new_ids, seed, C, engine, shard):
             else:
                 act = [i for i, c in enumerate(chosen) if table.active(row, c)]
             if not act:
+                continue
+            if row.index in remote:
+                for i in act:
+                    chosen[i][row.label] = np.nan
                 continue
             problems.append(LevelProblem(fits.get(row), row.index, ids if act is every else ids[act]))
             rows.append(row)
@@ -305,7 +320,15 @@ def _dev_fit_min(engine):
     return max(int(engine.device_fit_min), 64)
 
 
-def _tree_labels(table, hist, engine=None):
+def device_fits(n_obs, n_below, dev_min):
+    """Whether a continuous label's above side gets the device Parzen fit: the
+    one predicate of both paths (tpe_suggest.cpp fit_label: n_obs >= dev_min,
+    at most 64 below observations, more than 64 above components), so a
+    suggest fits a label the same way whichever path takes it."""
+    return dev_min is not None and n_obs >= dev_min and n_below <= 64 and n_obs - n_below + 1 > 64
+
+
+def _tree_labels(table, hist, engine=None, remote=()):
     """The table's tree records with the history's observation columns filled
     in (tids, kernel coordinate, value order) and, for the continuous labels
     large enough for the device Parzen fit, the device column and resident
@@ -314,7 +337,8 @@ def _tree_labels(table, hist, engine=None):
     columns and orders stay put (DeviceColumns.version).  Quantized labels
     carry no columns: tpe_suggest_tree sends them to the caller whenever they
     need a fit.  Returns (records, keep-alive list, [(ValueOrder, n_obs) of
-    the device-fitted labels by label index], the records' address) or None."""
+    the device-fitted labels by label index], the records' address) or None.
+    ``remote`` labels (another rank's, TPE_F_REMOTE) get no device column."""
     st = _tree_static(table)
     if st is None:
         return None
@@ -327,14 +351,15 @@ def _tree_labels(table, hist, engine=None):
     # never reuse its id), the document count and the device state's version
     memo = getattr(holder, 'tree_memo', None)
     dver = dc.version if dc is not None else None
-    if memo is not None and memo[0] is table and memo[2] == dev_min and memo[4] == dver:
+    mkey = (dev_min, remote)
+    if memo is not None and memo[0] is table and memo[2] == mkey and memo[4] == dver:
         if memo[1] == n_docs:
             return memo[3]
         # documents appended (FMinIter: one per suggest), no device-fitted label:
         # the records are updated in place — only the labels that gained
         # observations, through the field views (no structured-scalar writes)
         if cache is not None and n_docs > memo[1] and not memo[3][2] and _tree_refill(memo[5], meta, hist):
-            holder.tree_memo = (table, n_docs, dev_min, memo[3], dver, memo[5])
+            holder.tree_memo = (table, n_docs, mkey, memo[3], dver, memo[5])
             return memo[3]
     arr = arr0.view(np.uint8).copy().view(arr0.dtype)      # (a byte copy: the record dtype copies field by field)
     keep, devs = [], {}
@@ -352,6 +377,8 @@ def _tree_labels(table, hist, engine=None):
             rec['n_obs'] = n = len(otids)
             logc = fam == N.FAM_LOGGAUSS
             if dev_min is not None and n >= dev_min:
+                if ix in remote:                 # (another rank's label: never fitted here)
+                    continue
                 # device fit of the above side: the device column (kernel coordinate)
                 # and its resident order; the host keeps the columns for the below side
                 x = np.ascontiguousarray(hist.log_values(label) if logc else ovals, dtype=np.float64)
@@ -384,7 +411,7 @@ def _tree_labels(table, hist, engine=None):
         fv = {f: arr[f] for f in ('tids', 'values', 'order', 'n_obs')}
         fv['n'] = arr['n_obs'].tolist()
     # (the version after the columns and orders above were looked up: that may move it)
-    holder.tree_memo = (table, n_docs, dev_min, out, dc.version if dc is not None else None, fv)
+    holder.tree_memo = (table, n_docs, mkey, out, dc.version if dc is not None else None, fv)
     return out
 
 
@@ -415,26 +442,35 @@ def _tree_refill(fv, meta, hist):
     return True
 
 
-def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None, columns=False):
+def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None, columns=False,
+                    remote=()):
     """``_choices_philox`` in one native call (tpe_suggest_tree), or None when
     the space or history needs the general path.  Labels the native fits cannot
     reproduce (quantized ones, sides with repeated values: numpy's argsort tie
     order decides their weights) come back flagged; they are fitted here
     exactly as the general path fits them and handed to a second call.
     ``shard`` = (rank, world): candidate-sharded over the default process
-    group, the level results exchanged inside the native call (dist.py)."""
-    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns)
+    group, the level results exchanged inside the native call (dist.py).
+    ``remote``: label indices another rank evaluates (TPE_F_REMOTE)."""
+    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns, remote)
     if out is None:
         table.native_fit_hint = ()             # the general path takes it: nothing to pre-fit next time
     return out
 
 
-def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False):
+def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False, remote=()):
     if not hist.sorted_obs:
         return None
-    tl = _tree_labels(table, hist, engine)
+    tl = _tree_labels(table, hist, engine, remote)
     if tl is None:
         return None
+    rm = getattr(table, '_remote_applied', None)
+    if rm is None or rm[0] is not tl[0] or rm[1] != remote:
+        fl = tl[0]['flags']
+        fl &= ~N.F_REMOTE
+        if remote:
+            fl[list(remote)] |= N.F_REMOTE
+        table._remote_applied = (tl[0], remote)
     ex = None
     if shard is not None:
         ex = _dist.exchange_for(engine)
@@ -498,9 +534,11 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     used = act_rows[0] if len(values) == 1 else np.asarray(active).any(axis=0).tolist()
     table.native_fit_hint = tuple(ix for ix in host if used[ix])
     table.native_used = tuple(i for i, u in enumerate(used) if u)
-    # the device-fitted labels that ran hold their merged value orders now
+    # the device-fitted labels that ran hold their merged value orders now (a
+    # label the call took a host fit for, give(), did not run the device fit:
+    # its order buffers were not written)
     for ix, (order, n) in tl[2].items():
-        if used[ix]:
+        if used[ix] and ix not in host:
             order.commit(n)
     if columns:
         return ChoiceColumns(table.labels, values.copy(), np.asarray(active, dtype=bool))
@@ -528,9 +566,12 @@ def _choice_dicts(order, cols, values, active):
     by_label = {}
     for label, ix, fam in cols:
         col = values[:, ix]
-        vals = list(col.astype(np.int64)) if fam == N.FAM_CATEGORICAL else list(col)
         a = act[:, ix]
-        if not a.all():
+        full = a.all()
+        if fam == N.FAM_CATEGORICAL:         # (inactive entries are NaN: cast only the active ones)
+            col = col.astype(np.int64) if full else np.where(a, col, 0.0).astype(np.int64)
+        vals = list(col)
+        if not full:
             vals = [v if on else None for v, on in zip(vals, a.tolist())]
         by_label[label] = vals
     return [dict(zip(order, t)) for t in zip(*[by_label[k] for k in order])]
@@ -575,7 +616,7 @@ def suggest(new_ids, domain, trials, seed,
             n_EI_candidates=_default_n_EI_candidates,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
-            sampler='philox', precision='fp32', device=None, shard=None):
+            sampler='philox', precision='fp32', device=None, shard=None, shard_ids=None, shard_labels=None):
     new_ids = list(new_ids)
     if not new_ids:
         return []
@@ -591,7 +632,8 @@ def suggest(new_ids, domain, trials, seed,
         return rand.suggest(new_ids, domain, trials, seed)
     choices = suggest_choices(domain.table, hist, new_ids, seed, prior_weight=prior_weight,
                               n_EI_candidates=n_EI_candidates, gamma=gamma, sampler=sampler,
-                              precision=precision, device=device, shard=shard)
+                              precision=precision, device=device, shard=shard, shard_ids=shard_ids,
+                              shard_labels=shard_labels)
     logger.info('tpe.suggest took %f seconds', time.time() - t0)
     return rand.docs_from_choices(new_ids, domain, trials, choices)
 
@@ -623,7 +665,7 @@ class ChoiceColumns(object):
         for j, d in enumerate(dicts):
             for r in table.rows:
                 v = d.get(r.label)
-                if v is not None:
+                if v is not None:            # (NaN: active, evaluated by another rank)
                     values[j, r.index] = float(v)
                     active[j, r.index] = True
         return cls(table.labels, values, active)
@@ -631,30 +673,101 @@ class ChoiceColumns(object):
 
 def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weight,
                     n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
-                    sampler='philox', precision='fp32', device=None, shard=None, columns=False):
+                    sampler='philox', precision='fp32', device=None, shard=None, columns=False,
+                    shard_ids=None, shard_labels=None):
     """The suggest core on a structure-of-arrays history (``history.History``):
     per new id a {label: value or None} dict.  ``suggest`` wraps it with the
     Trials document layout; columnar callers (and bench.py's large configs)
     use it directly.  ``columns=True``: the same choices as one ChoiceColumns
-    (SoA in, SoA out — no per-id Python objects for a batch of thousands)."""
+    (SoA in, SoA out — no per-id Python objects for a batch of thousands).
+
+    At most one shard axis (rank, world) over the default process group:
+    ``shard`` splits every problem's candidates (one exchange per tree level),
+    ``shard_ids`` the new ids (contiguous blocks) and ``shard_labels`` the
+    hyperparameters (dist.label_owners) — those two exchange the chosen values
+    once, after the suggest; every rank returns the whole result, equal to the
+    unsharded suggest's (the candidates are keyed on seed, label, new id and
+    global index)."""
     if sampler not in ('philox', 'replay'):
         raise ValueError("sampler must be 'philox' or 'replay'")
+    if sum(a is not None for a in (shard, shard_ids, shard_labels)) > 1:
+        raise ValueError('shard, shard_ids and shard_labels are exclusive: one shard axis per suggest')
+    if (shard_ids is not None or shard_labels is not None) and sampler == 'replay':
+        raise ValueError("sampler='replay' draws on the host from one RandomState stream; it does not shard")
+    new_ids = list(new_ids)
+    if shard_ids is not None or shard_labels is not None:
+        return _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, precision, device,
+                                columns, shard_ids, shard_labels)
+    return _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, sampler, precision,
+                          device, shard, columns)
+
+
+def _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, sampler, precision, device,
+                   shard, columns, remote=()):
     engine = get_engine(device, precision)
     below_tids = _history.split_below(hist, gamma)
     C = int(n_EI_candidates)
     if sampler == 'philox' and NATIVE_TREE and precision == 'fp32':
-        out = _choices_native(table, hist, below_tids, list(new_ids), seed, C, engine, prior_weight, shard,
-                              columns)
+        out = _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard,
+                              columns, remote)
         if out is not None:
             return out
     fits = _Fits(table, hist, below_tids, prior_weight, engine)
     if sampler == 'philox':
-        out = _choices_philox(table, fits, list(new_ids), seed, C, engine, shard)
+        out = _choices_philox(table, fits, new_ids, seed, C, engine, shard, remote)
     elif shard is not None:
         raise ValueError("sampler='replay' draws on the host; it does not shard")
     else:
-        out = _choices_replay(table, fits, list(new_ids), seed, C, engine)
+        out = _choices_replay(table, fits, new_ids, seed, C, engine)
     return ChoiceColumns.from_dicts(table, out) if columns else out
+
+
+def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, precision, device, columns,
+                     shard_ids, shard_labels):
+    """New-id or hyperparameter axis (dist.py): this rank's part of the
+    suggest as columns, then one all-gather of the chosen values."""
+    rank, world = shard_ids if shard_ids is not None else shard_labels
+    engine = get_engine(device, precision)
+    ex = _dist.exchange_for(engine)          # (collective on the first sharded call)
+    if ex.world != world or ex.rank != rank:
+        raise ValueError('shard (%d, %d) is not this process group (rank %d of %d)'
+                         % (rank, world, ex.rank, ex.world))
+    n, L = len(new_ids), len(table.rows)
+    failed, err = False, None
+    if shard_ids is not None:
+        lo, hi = _dist.shard_range(n, rank, world)
+        vals, act = np.zeros((0, L)), np.zeros((0, L), dtype=bool)
+        try:
+            if hi > lo:
+                cc = _suggest_local(table, hist, new_ids[lo:hi], seed, prior_weight, n_EI_candidates, gamma,
+                                    'philox', precision, device, None, True)
+                vals, act = cc.values, cc.active
+        except Exception as e:               # (still takes part in the gather: no rank waits forever)
+            failed, err = True, e
+        try:
+            vals, act = _dist.gather_id_blocks(ex, vals, act, n, L, failed)
+        except RuntimeError:
+            if err is not None:
+                raise err
+            raise
+    else:
+        owner = _dist.label_owners(table, world)
+        remote = tuple(ix for ix, o in enumerate(owner) if o >= 0 and o != rank)
+        vals, act = np.full((n, L), np.nan), np.zeros((n, L), dtype=bool)
+        try:
+            cc = _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, 'philox',
+                                precision, device, None, True, remote)
+            vals, act = cc.values, np.asarray(cc.active, dtype=bool)
+        except Exception as e:
+            failed, err = True, e
+        try:
+            vals = _dist.gather_label_columns(ex, vals, owner, failed)
+        except RuntimeError:
+            if err is not None:
+                raise err
+            raise
+    cc = ChoiceColumns(table.labels, vals, act)
+    return cc if columns else cc.dicts(table)
 
 
 def suggest_replay(new_ids, domain, trials, seed, **kw):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 18
+#define TPE_ABI_VERSION 19
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -72,8 +72,11 @@ enum {
   TPE_F_PREFIT = 32,   /* tpe_tree_label: fit this label up front on the host worker threads (the
                           caller's hint: the labels its previous suggest on the space used); no label
                           flagged: every natively fitted label with enough observations */
-  TPE_F_FGT = 64       /* tpe_problem (set by the packer): a device-fitted TPE_TAB_CELLS label whose
+  TPE_F_FGT = 64,      /* tpe_problem (set by the packer): a device-fitted TPE_TAB_CELLS label whose
                           above cells are built from Hermite box moments (see "Box moments") */
+  TPE_F_REMOTE = 128   /* tpe_tree_label: another rank evaluates this label (hyperparameter-axis
+                          shard, see "Shard axes"): it is neither fitted nor run here; its values
+                          are NaN and its activity is the tree's.  Not allowed on a gate. */
 };
 
 /* box moments (see "Box moments" below): Hermite terms per box, 16-B units per box record */
@@ -734,6 +737,29 @@ int tpe_comm_destroy(void* comm);
 /* the exchange's reduction on the host: all[world][P] -> out[P], np.argmax
  * order over (score, global_idx), empty records (idx < 0) skipped */
 int tpe_combine_results(const tpe_result* all, int32_t world, int64_t P, tpe_result* out);
+
+/* ------------------------------------------------------------------------
+ * Shard axes.  Besides the candidate axis above, a batched suggest shards
+ * with no exchange inside the suggest:
+ *   new-id axis          every new id is an independent suggest on the same
+ *                        history (the reference's one-id call, tpe.py:812,
+ *                        repeated): rank r takes a contiguous block of the ids;
+ *   hyperparameter axis  broadcast_best is per hyperparameter
+ *                        (tpe.py:749-759): rank r evaluates the non-gate labels
+ *                        it owns, every rank evaluates the gates (so every rank
+ *                        knows which labels are active), the others are
+ *                        TPE_F_REMOTE.
+ * Candidates are keyed on (seed, label, new id, global index), so each rank
+ * computes exactly what one device computes for its part.  The chosen values
+ * are then all-gathered once (tpe_exchange_allgather) and every rank holds
+ * the whole result.
+ * ---------------------------------------------------------------------- */
+
+/* all-gather of `bytes` host bytes per rank through the exchange: all[world *
+ * bytes] in rank order.  RCCL (ex->comm): the bytes go through ex->dev (at
+ * least world * bytes) on `stream` — one copy in, an in-place ncclAllGather, one
+ * copy out, a stream synchronise; else ex->gather.  Rank-collective. */
+int tpe_exchange_allgather(const tpe_exchange* ex, const void* mine, int64_t bytes, void* all, void* stream);
 
 /* below_tids ascending (the n_below best trials, tpe.py:625-629); ids: the
  * n_ids new trial ids; n_cand candidates per problem on this rank, global

@@ -127,3 +127,79 @@ def test_gloo_world2_combines_recorded_engine_shards():
             full = case['full']
             assert g['global_idx'] == full['global_idx'], (rank, case['C'], case['seed'])
             assert g['value'] == full['value'] and g['score'] == full['score']
+
+
+# ------------------------------------------------------------ id / label axes
+def _axes_worker(rank, world, port, q):
+    """The new-id and hyperparameter gathers (dist.gather_id_blocks /
+    gather_label_columns) through the C exchange (tpe_exchange_allgather, host
+    gather over gloo — the RCCL path runs the same call on a device buffer)."""
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hyperopt_amd import dist as D
+        ex = D._Exchange(None, None)
+        out = {}
+        # new-id axis: 11 ids x 3 labels, the full matrix is a known function
+        n, L = 11, 3
+        full_v = np.arange(n * L, dtype=np.float64).reshape(n, L) * 0.5
+        full_a = (np.arange(n * L).reshape(n, L) % 3) != 0
+        full_v[~full_a] = np.nan
+        lo, hi = D.shard_range(n, rank, world)
+        v, a = D.gather_id_blocks(ex, full_v[lo:hi], full_a[lo:hi], n, L)
+        out['ids'] = (np.array_equal(v, full_v, equal_nan=True), bool((a == full_a).all()))
+        # hyperparameter axis: each rank knows only its own columns (and the gates)
+        owner = [-1, 0, 1, 2, 0, 1, 2, 0][:8]
+        owner = [o if o < world else o % world for o in owner]
+        full = np.random.RandomState(5).uniform(size=(4, 8))
+        mine = np.where([o in (-1, rank) for o in owner], full, np.nan)
+        got = D.gather_label_columns(ex, mine, owner)
+        out['labels'] = bool(np.array_equal(got, full))
+        # a failed rank: every rank raises, none waits
+        try:
+            D.gather_id_blocks(ex, full_v[lo:hi], full_a[lo:hi], n, L, failed=(rank == world - 1))
+            out['failure'] = 'no error'
+        except RuntimeError as e:
+            out['failure'] = str(e)
+        q.put((rank, out, None))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_gloo_id_and_label_axis_gathers(world):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_axes_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got, err in out:
+        assert err is None, (rank, err)
+        assert got['ids'] == (True, True), (rank, got)
+        assert got['labels'], rank
+        assert 'failed on rank(s) [%d]' % (world - 1) in got['failure'], (rank, got['failure'])
+
+
+def test_label_owners_round_robin_non_gates():
+    """Hyperparameter axis: the gates on every rank, the other labels
+    round-robin in table order."""
+    import bench
+    from hyperopt_amd import hp
+    from hyperopt_amd.space import ParamTable
+    from hyperopt_amd.dist import label_owners
+    T = ParamTable(bench.tree_space(hp))
+    for world in (1, 2, 3, 8):
+        own = label_owners(T, world)
+        gates = set(T.parent_labels)
+        assert [o == -1 for o in own] == [r.label in gates for r in T.rows]
+        ng = [o for o in own if o >= 0]
+        assert ng == [k % world for k in range(len(ng))]

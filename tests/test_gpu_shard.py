@@ -149,3 +149,118 @@ def test_rccl_exchange_one_rank():
     assert err is None, err
     assert rccl, 'the exchange did not take the RCCL path'
     assert ref == got
+
+
+# ------------------------------------------------ new-id and hyperparameter axes
+N5, D5 = 100000, 200
+
+
+def _cfg4():
+    import bench
+    labels = ['x%02d' % i for i in range(20)]
+    hist = bench.soa_history(labels, 10000, 7, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+    return bench.flat_uniform_table(labels), hist
+
+
+def _cfg5():
+    import bench
+    labels = ['x%04d' % i for i in range(D5)]
+    hist = bench.soa_history(labels, N5, 8, lambda v: np.zeros(N5))
+    hist.losses[:] = np.random.RandomState(9).uniform(size=N5) + 1e-9 * np.arange(N5)
+    return bench.flat_uniform_table(labels), hist
+
+
+def _axes_cases(rank, world):
+    """(name, result) of every axis case; rank/world None: unsharded."""
+    import bench
+    from hyperopt_amd import tpe
+    sid = None if rank is None else (rank, world)
+    out = []
+    t4, h4 = _cfg4()
+    ids = np.arange(10000, 10000 + 4096)
+    cc = tpe.suggest_choices(t4, h4, ids, 31, n_EI_candidates=4096, columns=True, shard_ids=sid)
+    out.append(('config4 ids', (cc.values, cc.active)))
+    t5, h5 = _cfg5()
+    cc = tpe.suggest_choices(t5, h5, [N5, N5 + 1], 41, n_EI_candidates=4096, columns=True, shard_labels=sid)
+    out.append(('config5 labels', (cc.values, cc.active)))
+    domain, trials = bench.make_history(N_HIST, 0)
+    for name, kw, new_ids, seed, C in (('tree ids', 'shard_ids', list(range(N_HIST, N_HIST + 64)), 51, 1 << 14),
+                                       ('tree labels', 'shard_labels', [N_HIST, N_HIST + 1, N_HIST + 2], 52, 1 << 18)):
+        docs = tpe.suggest(new_ids, domain, trials, seed, n_EI_candidates=C, **{kw: sid})
+        out.append((name, [(d['tid'], {k: [float(x) for x in v] for k, v in d['misc']['vals'].items()})
+                           for d in docs]))
+    return out
+
+
+def _axes_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        q.put((rank, _axes_cases(rank, world), None))
+    except Exception as e:          # report, do not hang the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_id_and_label_axes_match_unsharded():
+    """Two processes (gloo, both on the one GPU): the new-id axis (config 4:
+    4096 ids x 4096 candidates x 20 dims, and 64 ids of the config-3 tree) and
+    the hyperparameter axis (a config-5-shaped 200-dim space at 100k trials
+    with device Parzen fits, and the config-3 tree: gates on both ranks) each
+    return, on every rank, exactly the unsharded suggest (values and activity
+    bit for bit: the candidates are keyed on seed, label, new id and index)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_axes_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        rank, out, err = q.get(timeout=280)
+        assert err is None, (rank, err)
+        got[rank] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import bench
+    from hyperopt_amd import history as H, tpe
+    from hyperopt_amd.engine import get_engine
+    ref = _axes_cases(None, None)
+    domain, trials = bench.make_history(N_HIST, 0)
+    T = domain.table
+    hist = H.extract(domain, trials)
+    fits = tpe._Fits(T, hist, H.split_below(hist, 0.25), 1.0, get_engine())
+    for rank in (0, 1):
+        for (name, want), (name2, have) in zip(ref, got[rank]):
+            assert name == name2
+            if isinstance(want, tuple):           # tabulated labels: bit for bit
+                assert np.array_equal(want[0], have[0], equal_nan=True), (rank, name)
+                assert np.array_equal(want[1], have[1]), (rank, name)
+                continue
+            # the tree at these sizes has pooled (untabulated) continuous labels,
+            # whose fp32 above sums follow the batch layout: activity and
+            # categories exact, a continuous value equal or within the eps-tie
+            # tolerance of the unsharded winner's score
+            assert len(want) == len(have)
+            for (tid, wv), (tid2, hv) in zip(want, have):
+                assert tid == tid2 and set(wv) == set(hv)
+                for k, v in wv.items():
+                    assert len(v) == len(hv[k]), (rank, name, tid, k)
+                    if not v or v == hv[k]:
+                        continue
+                    row = T.by_label[k]
+                    assert not row.categorical, (rank, name, tid, k, v, hv[k])
+                    post = fits.get(row)
+                    s_ref, s_got = _score(post, v[0]), _score(post, hv[k][0])
+                    assert abs(s_ref - s_got) <= 1e-5 * max(1.0, abs(s_ref)), (rank, name, tid, k, v, hv[k])
+    # the ranks agree with each other exactly (every rank returns the gathered result)
+    for (name, a), (_, b) in zip(got[0], got[1]):
+        if isinstance(a, tuple):
+            assert np.array_equal(a[0], b[0], equal_nan=True) and np.array_equal(a[1], b[1]), name
+        else:
+            assert a == b, name

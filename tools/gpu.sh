@@ -10,7 +10,8 @@
 #   trace      rocprofv3 --kernel-trace --stats of a short headline bench run (BENCH_ARGS)
 #   pmc        PMC counter passes on the headline bench, one rocprofv3 run per group
 #   stage      steady-state per-stage device times        (REP)
-#   configs    bench.py --config 1, 2, 4, 5
+#   configs    bench.py --config 1, 2, 4, 5 (CONFIGS)
+#   rehearse   bench.py --gpus 2 over gloo, two ranks on the one GPU (REH_CONFIGS)
 #   hostsplit  host-side time split of the headline suggest
 #   nativesplit native fits / tpe_suggest_tree / device stages of the headline suggest
 #   hostprof   cProfile of the headline suggest on the device
@@ -25,7 +26,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r02}
+TAG=${TAG:-r04}
 O=gpurun_out
 
 step() {  # limit_seconds logfile cmd...
@@ -76,9 +77,17 @@ for task in "$@"; do
       step 300 $O/stage_${TAG}.txt python tools/stage_bench.py ${REP:-20}
       cat $O/stage_${TAG}.txt ;;
     configs)
-      for c in 1 2 4 5; do
+      for c in ${CONFIGS:-1 2 4 5}; do
         step 600 $O/cfg${c}_${TAG}.err python bench.py --config $c --steps ${CFG_STEPS:-5} --warmup 1
         grep '^{' $O/cfg${c}_${TAG}.err > $O/cfg${c}_${TAG}.json; cat $O/cfg${c}_${TAG}.json
+      done ;;
+    rehearse)
+      # the N > 1 flow with 2 ranks on the box's one GPU (gloo: RCCL takes one rank per device)
+      for c in ${REH_CONFIGS:-3 4 5}; do
+        step 600 $O/rehearse${c}_${TAG}.err env TPE_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29500 + c)) bench.py --gpus 2 --config $c \
+            --steps ${CFG_STEPS:-5} --warmup 2 --no-cpu-baseline --no-quantized --no-appending
+        grep '^{' $O/rehearse${c}_${TAG}.err > $O/rehearse${c}_${TAG}.json; cat $O/rehearse${c}_${TAG}.json
       done ;;
     cfgprof)
       step 600 $O/cfgprof${CONFIG:-5}_${TAG}.txt python tools/config_prof.py ${CONFIG:-5} --steps ${STEPS:-5}
