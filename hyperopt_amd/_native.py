@@ -19,7 +19,8 @@ F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT, F_FGT, F_REMO
 TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
 TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
-BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS, BATCH_TAB_EXACT = 1, 2, 4, 8, 16
+BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS, BATCH_TAB_EXACT, BATCH_NO_TAB_FAST = \
+    1, 2, 4, 8, 16, 32
 PREC_F32, PREC_F64 = 0, 1
 
 # numpy mirrors of the C structs (the host builds arrays of them and copies
@@ -88,7 +89,7 @@ class Batch(ctypes.Structure):
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
         ('fit_max_new', ctypes.c_int64), ('fit_max_obs', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_blocks', ctypes.c_int64), ('n_sorted', ctypes.c_int32),
-        ('reserved5', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
+        ('tab_fast', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
         ('tab_jobs', ctypes.c_void_p), ('n_tab_jobs', ctypes.c_int32), ('tab_blocks', ctypes.c_int32),
         ('tab', ctypes.c_void_p), ('tab_units', ctypes.c_int64),
         ('samp_tiles', ctypes.c_void_p), ('n_samp_tiles', ctypes.c_int32), ('n_samp_eager', ctypes.c_int32),
@@ -204,6 +205,7 @@ class TreeLabel(ctypes.Structure):
         ('host_k', ctypes.c_int64 * 2),
         ('dev_obs', ctypes.c_void_p), ('ord_key_in', ctypes.c_void_p), ('ord_idx_in', ctypes.c_void_p),
         ('n_ord_in', ctypes.c_int64), ('ord_key_out', ctypes.c_void_p), ('ord_idx_out', ctypes.c_void_p),
+        ('side_order', ctypes.c_void_p * 2), ('side_n', ctypes.c_int64 * 2),
     ]
 
 
@@ -225,7 +227,7 @@ TREE_LABEL_DTYPE = np.dtype(dict(
     names=[f for f, _ in TreeLabel._fields_],
     formats=['<i4', '<i4', '<i4', '<i4', '<f8', '<f8', '<f8', '<f8', '<u8', '<u8', '<u8', '<u8', '<i8', '<i4', '<i4',
              ('<i4', (TREE_MAX_PARENTS,)), ('<i4', (TREE_MAX_PARENTS,)), '<f8', ('<u8', (2,)), ('<u8', (2,)),
-             ('<u8', (2,)), ('<i8', (2,)), '<u8', '<u8', '<u8', '<i8', '<u8', '<u8'],
+             ('<u8', (2,)), ('<i8', (2,)), '<u8', '<u8', '<u8', '<i8', '<u8', '<u8', ('<u8', (2,)), ('<i8', (2,))],
     offsets=[getattr(TreeLabel, f).offset for f, _ in TreeLabel._fields_], itemsize=ctypes.sizeof(TreeLabel)))
 
 EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_size', 'tpe_pinned_device_address',

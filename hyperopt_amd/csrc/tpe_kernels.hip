@@ -855,7 +855,13 @@ __device__ __noinline__ double exp_call(double x) { return exp(x); }
 // (likewise the empty slot's constant, stored out of line)
 __device__ __noinline__ void clear_best(tpe_best* d) { *d = tpe_best{0, 0, 0, -1}; }
 
-template <int PREC>
+// FAST: the production case only — f32 cells tables that fit in LDS, device
+// draws from the staged sampler, early selection, no per-candidate outputs
+// (the host sets tpe_batch.tab_fast when every tabulated problem of the level
+// is one).  Its instantiation carries none of the other paths' registers, and
+// a label's staging overlaps the first unit's Philox draws (the table rows are
+// waited for only before the first cell look-up).
+template <int PREC, bool FAST = false>
 __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* __restrict__ P,
                                                             const tpe_tile* __restrict__ tiles,
                                                             const int32_t* __restrict__ list, int n_list,
@@ -954,7 +960,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     int tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wave = tid >> 6;
-    if (run_cells) {
+    if (FAST || run_cells) {
       // cells run: better32's order as one 64-bit key per lane, reduced by the
       // wave's DPP max (no LDS permutes); the winning lane (candidate indices are
       // unique) leaves its log2 sums and draw for the end-of-workgroup combine
@@ -1010,7 +1016,210 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     }
   }
   __syncthreads();
-  for (int gi = 0; gi < n_my; ++gi) {
+  if constexpr (FAST) {
+    // ---- the production cells loop (see FAST above) ----
+    // per unit of a thread: NP consecutive candidates from `first`; phases:
+    // uniforms (Philox, no LDS) -> draws (guide, sampler row, ndtri_f32) ->
+    // the two cell look-ups, with the exact fallback for the rare candidate
+    // outside the cells or in a flagged cell
+    for (int gi = 0; gi < n_my; ++gi) {
+      const int tile = __builtin_amdgcn_readfirstlane(s_tile[gi]), pid = __builtin_amdgcn_readfirstlane(s_prob[gi]);
+      const tpe_problem& p = P[pid];
+      bool staged = false;
+      double scum = 0.0;
+      float4 srow = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (pid != cur) {
+        if (cur >= 0) flush();
+        const bool same = p.samp_off == st_samp && p.samp_len == st_len && p.tab_off[0] == st_t0 &&
+                          p.tab_off[1] == st_t1 && p.tab_n[0] == st_n0 && p.tab_n[1] == st_n1;
+        if (!same) {
+          st_samp = p.samp_off; st_len = p.samp_len; st_t0 = p.tab_off[0]; st_t1 = p.tab_off[1];
+          st_n0 = p.tab_n[0]; st_n1 = p.tab_n[1];
+          __syncthreads();                               // LDS free for the next label's rows
+          // sampler rows into registers first, then the table units by LDS-DMA:
+          // every one of the kStageU rounds issued (units past the table: a
+          // clamped load into unused slots), so the sampler rows' use below waits
+          // for their own loads only, and the tables land while the first unit's
+          // Philox draws are computed
+          if ((int)threadIdx.x < p.samp_len) {
+            const double* sr = samp + 8 * (int64_t)p.samp_off + 8 * (int)threadIdx.x;
+            scum = sr[0];
+            const float sg = (float)sr[2];
+            srow = make_float4((float)sr[1], sr[5] != 0.0 ? -sg : sg, (float)sr[3], (float)sr[4]);
+          }
+          constexpr int kStageU = TPE_TAB_ROW_UNITS * kTabLdsCells / kTabThreads;
+          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], nu = n0 + TPE_TAB_ROW_UNITS * p.tab_n[1];
+          const int wv = (int)(threadIdx.x >> 6);
+#pragma unroll
+          for (int u = 0; u < kStageU; ++u) {
+            const int q = min(u * kTabThreads + (int)threadIdx.x, nu - 1);
+            const float4* src = q < n0 ? tab + (int64_t)p.tab_off[0] + q : tab + (int64_t)p.tab_off[1] + (q - n0);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(tab_lds + u * kTabThreads + 64 * wv),
+                                             16, 0, 0);
+          }
+          staged = true;
+        }
+        cur = pid;
+        run_tile = tile;
+        run_cand_base = p.cand_base; run_cand_off = p.cand_off;
+        run_bb = p.below_base; run_ab = p.above_base;
+        run_logc = p.family == TPE_FAM_LOGGAUSS;
+        run_exp = run_logc;
+        run_drawn = true;
+        run_cells = true;
+        if (threadIdx.x == 0)
+          s_run[n_def] = RunRec{run_cand_base, run_cand_off, run_bb, run_ab, run_tile, (run_logc ? 1 : 0) | (run_exp ? 2 : 0) | 4};
+      }
+      const int cand_start = __builtin_amdgcn_readfirstlane(s_start[gi]);
+      const bool pair = gi + 1 < n_my && __builtin_amdgcn_readfirstlane(s_prob[gi + 1]) == pid &&
+                        __builtin_amdgcn_readfirstlane(s_start[gi + 1]) == cand_start + kTile;
+      // a run of several tile pairs: (pair, 64-thread slot) units handed out from
+      // an LDS counter (waves that run ahead take more; see the general pass)
+      int npairs = 0;
+      if (pair) {
+        int k = gi;
+        while (k + 1 < n_my && __builtin_amdgcn_readfirstlane(s_prob[k + 1]) == pid &&
+               __builtin_amdgcn_readfirstlane(s_start[k + 1]) == cand_start + (k + 1 - gi) * kTile)
+          ++k;
+        npairs = (k - gi + 1) / 2;
+      }
+      const bool dyn = npairs > 1;
+      const int nunits = npairs * (kTabThreads / 64);
+      float lo_f, hi_f;
+      f32_bounds(p, lo_f, hi_f);
+      const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
+      const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
+      const int n0 = p.tab_n[0], n1 = p.tab_n[1];
+      const float4* __restrict__ r0 = tab_lds;
+      const float4* __restrict__ r1 = tab_lds + TPE_TAB_ROW_UNITS * n0;
+      // the next unit of this wave: false when the run has none left (dynamic)
+      int first = 0;
+      auto next_unit = [&](bool initial) -> bool {
+        if (!dyn) {
+          if (!initial) return false;
+          first = cand_start + (pair ? 2 * kTabPer : kTabPer) * (int)threadIdx.x;
+          return true;
+        }
+        int u = 0;
+        if (lane == 0) u = atomicAdd(&s_unit[n_def], 1);
+        u = __builtin_amdgcn_readlane(u, 0);
+        if (u >= nunits) return false;
+        const int pr = u / (kTabThreads / 64), slot = u - pr * (kTabThreads / 64);
+        first = __builtin_amdgcn_readfirstlane(s_start[gi + 2 * pr]) + 2 * kTabPer * (slot * 64 + lane);
+        return true;
+      };
+      auto run_units = [&](auto NPC) {
+        constexpr int NP = decltype(NPC)::value;
+        // the first unit's uniforms are computed while the label's rows are on
+        // their way (every wave has a first unit: a dynamic run has >= 2 pairs,
+        // 32 units for 16 waves)
+        bool first_unit = true;
+        next_unit(true);
+        for (;;) {
+          uint32_t ws[NP];
+          float uf[NP], tj[NP];
+          {
+            const uint64_t g0 = (uint64_t)p.cand_base + (uint64_t)first;
+            if ((g0 & 1) == 0) {
+#pragma unroll
+              for (int j = 0; j < NP; j += 2) {
+                const uint64_t blk = (g0 + (uint64_t)j) >> 1;
+                const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+                ws[j] = r.x; uf[j] = u01f(r.y);
+                ws[j + 1] = r.z; uf[j + 1] = u01f(r.w);
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < NP; ++j) {
+                const DrawU d = draw_uniforms(p, first + j, TPE_PREC_F32);
+                ws[j] = d.ws; uf[j] = d.uf;
+              }
+            }
+          }
+          if (first_unit && staged) {
+            if ((int)threadIdx.x < p.samp_len) { cum_lds[threadIdx.x] = scum; row_lds[threadIdx.x] = srow; }
+            __syncthreads();
+            if (threadIdx.x < kGuide) {                  // first k with cum_k > b / kGuide, its two steps
+              const double v = (double)threadIdx.x / (double)kGuide;
+              const int len = p.samp_len;
+              int a = 0, b = len - 1;
+              while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
+              GuideEnt e;
+              e.k0 = a;
+              e.never = 0u;
+              e.t0 = guide_thresh(a < len - 1 ? cum_lds[a] : INFINITY, e.never, 1u);
+              e.t1 = guide_thresh(a + 1 < len - 1 ? cum_lds[a + 1] : INFINITY, e.never, 2u);
+              guide[threadIdx.x] = e;
+            }
+            __syncthreads();
+          }
+          {
+            int kc[NP];
+            unsigned more = 0;
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+              bool m;
+              kc[j] = guided_comp(guide, ws[j], m);
+              more |= (unsigned)m << j;
+            }
+            if (__ballot(more != 0u)) {                 // (rare: a guide slice with 2+ component edges)
+#pragma unroll
+              for (int j = 0; j < NP; ++j)
+                if ((more >> j) & 1u) kc[j] = guided_more(cum_lds, p.samp_len, u01w(ws[j]), kc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+              const float4 sv = row_lds[kc[j]];
+              const float pr = sv.z + uf[j] * (sv.w - sv.z);
+              const float z = ndtri_f32(pr);
+              const float xf = sv.x + sv.y * z;
+              tj[j] = fminf(fmaxf(xf == xf ? xf : sv.x, lo_f), hi_f);
+            }
+          }
+          if (first_unit && staged) {
+            __builtin_amdgcn_s_waitcnt(0);               // (the LDS-DMA loads: vmcnt)
+            __syncthreads();
+          }
+#ifdef TPE_SAMPLE_TRACE
+          if (!st[1]) st[1] = wall_clock64();            // (FAST: the tables landed, the first draws made)
+#endif
+          first_unit = false;
+          uint32_t exact = 0;
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            const int i = first + j;
+            const float t = tj[j];
+            const float lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, r0, 1, TPE_TAB_ROW_UNITS, t),
+                        la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, r1, 1, TPE_TAB_ROW_UNITS, t);
+            const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
+            exact |= (unsigned)(valid && !ok) << j;
+            if (valid && ok) track(i, lb2, la2, t);
+          }
+          // outside the cells or in flagged ones: summed exactly by the whole wave
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            unsigned long long need = __ballot((exact >> j) & 1u);
+            while (need) {
+              const int src = __builtin_ctzll(need);
+              need &= need - 1;
+              const float t = __shfl(tj[j], src);
+              float lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, r0, 1, TPE_TAB_ROW_UNITS, t),
+                    la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, r1, 1, TPE_TAB_ROW_UNITS, t);
+              if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
+              if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
+              if (lane == src) track(first + j, lb2, la2, t);
+            }
+          }
+          if (!next_unit(false)) break;
+        }
+      };
+      if (pair) run_units(std::integral_constant<int, 2 * kTabPer>{});
+      else run_units(std::integral_constant<int, kTabPer>{});
+      gi += dyn ? 2 * npairs - 1 : (pair ? 1 : 0);     // the run's other tiles are done
+    }
+  }
+  for (int gi = 0; gi < n_my && !FAST; ++gi) {
     // (uniform: readfirstlane keeps the problem's fields in scalar registers)
     const int tile = __builtin_amdgcn_readfirstlane(s_tile[gi]), pid = __builtin_amdgcn_readfirstlane(s_prob[gi]);
     const tpe_problem& p = P[pid];
@@ -3685,6 +3894,12 @@ int cu_count() {
   return cache[dev];
 }
 
+// TPE_TAB_FAST=0: the general sample-stage kernel for every level (A/B, tests)
+bool tab_fast_disabled() {
+  static const int v = [] { const char* e = getenv("TPE_TAB_FAST"); return e && e[0] == '0' ? 1 : 0; }();
+  return v != 0;
+}
+
 // tabulated tiles per sample-stage workgroup (the early selection's run
 // enumeration on the host uses the same partition)
 int tab_tiles_per_wg(int n_tab) {
@@ -3842,7 +4057,13 @@ int tpe_sample(const tpe_batch* b, void* stream) {
     const int per = tab_tiles_per_wg(n_tab);
     const int wgs = (n_tab + per - 1) / per;
     tpe_result* run_best = b->early_select ? b->run_best : nullptr;
-    if (b->precision == TPE_PREC_F64)
+    if (b->tab_fast && run_best && b->precision == TPE_PREC_F32 && b->sample && !b->l_out &&
+        !(b->flags & TPE_BATCH_WRITE_CAND))
+      TPE_LAUNCH((k_sample_tab<TPE_PREC_F32, true>), dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
+                         b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
+                         b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
+                         run_best, b->tiles_per_problem);
+    else if (b->precision == TPE_PREC_F64)
       TPE_LAUNCH(k_sample_tab<TPE_PREC_F64>, dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
@@ -4198,6 +4419,21 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
       late += !(lazy || q.tab_mode != TPE_TAB_NONE);
     }
     b.n_late = late;
+    // the sample stage's specialised kernel: every tabulated problem cells with
+    // both tables within its LDS and a staged sampler (the problem rows: the
+    // host's, or an expanded level's label templates)
+    const bool fast_ok = precision == TPE_PREC_F32 && !(flags & (TPE_BATCH_WRITE_CAND | TPE_BATCH_NO_TAB_FAST)) &&
+                         !tab_fast_disabled();
+    bool fast = fast_ok;
+    const tpe_problem* rows = hp ? hp : xtmpl;
+    const int64_t n_rows = hp ? P : (xtmpl ? info.n_expand : 0);
+    for (int64_t r = 0; fast && r < n_rows; ++r) {
+      const tpe_problem& q = rows[r];
+      if (q.tab_mode == TPE_TAB_NONE) continue;
+      fast = q.tab_mode == TPE_TAB_CELLS && q.tab_n[0] + q.tab_n[1] <= kTabLdsCells && q.samp_len > 0 &&
+             q.samp_len <= kCumLds;
+    }
+    b.tab_fast = fast && n_rows > 0 ? 1 : 0;
   }
   b.result = rd ? rd : ws->result;
   if (info.n_fit > 0) {

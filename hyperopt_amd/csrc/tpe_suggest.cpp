@@ -51,6 +51,7 @@ struct Fit {
   bool done = false;
   bool dev = false;              // above side: the device Parzen fit (below_idx, the record's column)
   std::vector<double> buf;
+  std::vector<double> side_x;      // the two sides' coordinates in tid order (caller-sorted fits)
   std::vector<int32_t> below_idx;
   int64_t k[2] = {0, 0};
   const double* w[2] = {nullptr, nullptr};
@@ -90,6 +91,46 @@ int fit_label(Tree& T, int i, bool spec = false) {
       f.mu[sd] = L.family == TPE_FAM_CATEGORICAL ? nullptr : L.host_mu[sd];
       f.sg[sd] = L.family == TPE_FAM_CATEGORICAL ? nullptr : L.host_sigma[sd];
     }
+    f.done = true;
+    return TPE_OK;
+  }
+  if (L.family != TPE_FAM_CATEGORICAL && (L.side_order[0] || L.side_order[1])) {
+    // the caller's per-side sort permutations (numpy's argsort: the reference's
+    // tie order, tpe.py:427-428): split here (ap_filter_trials, tpe.py:629-636:
+    // below = tid among the below tids, both sides kept in tid order) and fit
+    // each side with its permutation (adaptive_parzen_normal, tpe.py:398-475)
+    if (!L.side_order[0] || !L.side_order[1] || n < 0 || (n > 0 && (!L.tids || !L.values)))
+      return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: a caller-sorted label needs both side orders and columns");
+    const double* x = (const double*)L.values;
+    f.side_x.resize((size_t)n);
+    double* bx = f.side_x.data();
+    f.below_idx.clear();
+    for (int64_t b = 0; b < T.n_below; ++b) {
+      const int64_t* at = std::lower_bound(L.tids, L.tids + n, T.below[b]);
+      if (at != L.tids + n && *at == T.below[b]) f.below_idx.push_back((int32_t)(at - L.tids));
+    }
+    const int64_t nb = (int64_t)f.below_idx.size(), na = n - nb;
+    if (nb != L.side_n[0] || na != L.side_n[1])
+      return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: the caller's side sizes differ from the below split");
+    double* ax = bx + nb;
+    int64_t q = 0, t0 = 0;
+    for (int64_t j = 0; j <= nb; ++j) {                     // above: the runs between the below positions
+      const int64_t t1 = j < nb ? f.below_idx[(size_t)j] : n;
+      for (int64_t t = t0; t < t1; ++t) ax[q++] = x[t];
+      if (j < nb) { bx[j] = x[t1]; t0 = t1 + 1; }
+    }
+    const size_t cb = (size_t)nb + 1, ca = (size_t)na + 1;
+    f.buf.resize(3 * (cb + ca));
+    double* o = f.buf.data();
+    const int64_t r0 = tpe_host_fit_parzen(bx, nb, nb >= 2 ? L.side_order[0] : nullptr, T.prior_weight, L.prior_mu,
+                                           L.prior_sigma, T.lf, o, o + cb, o + 2 * cb);
+    const int64_t r1 = tpe_host_fit_parzen(ax, na, na >= 2 ? L.side_order[1] : nullptr, T.prior_weight, L.prior_mu,
+                                           L.prior_sigma, T.lf, o + 3 * cb, o + 3 * cb + ca, o + 3 * cb + 2 * ca);
+    if (r0 < 0 || r1 < 0)
+      return tpe_internal_fail(TPE_E_ARG, "tpe_host_fit_parzen failed on a caller-sorted side (a bad permutation or a "
+                                          "non-positive Parzen bandwidth)");
+    f.k[0] = nb + 1; f.w[0] = o; f.mu[0] = o + cb; f.sg[0] = o + 2 * cb;
+    f.k[1] = na + 1; f.w[1] = o + 3 * cb; f.mu[1] = o + 3 * cb + ca; f.sg[1] = o + 3 * cb + 2 * ca;
     f.done = true;
     return TPE_OK;
   }
@@ -182,6 +223,7 @@ bool prefit_worthy(const Tree& T, int i) {
   const tpe_tree_label& L = T.L[i];
   if ((L.flags & TPE_F_REMOTE) || L.host_k[0] > 0 || L.n_obs < kPrefitMinObs || !L.tids || !L.values) return false;
   if (L.family == TPE_FAM_CATEGORICAL) return L.upper > 0;
+  if (L.side_order[0] && L.side_order[1]) return true;        // caller-sorted (quantized, repeated values)
   if (L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) return false;
   const bool dev = T.device_fit_min > 0 && L.n_obs >= std::max<int64_t>(T.device_fit_min, 64);
   if (dev) return L.dev_obs != nullptr;         // the below side's fit and its positions among the tids

@@ -167,6 +167,7 @@ class Engine(object):
         self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.tile = self.lib.tpe_tile_size()
         self.device_fit_min = DEVICE_FIT_MIN
+        self.tree_calls = 0              # tpe_suggest_tree calls (tests: one per steady-state suggest)
         self.set_precision(precision)
         self._bufs = {}
         self._pinned = None
@@ -665,6 +666,7 @@ class Engine(object):
         caller must fit and pass back (none: take the general path)."""
         if self.precision != 'fp32':
             return None, np.zeros(len(labels), dtype=np.int8)
+        self.tree_calls += 1
         n_cand = int(n_cand)
         if n_cand < 0 or n_cand >= 2 ** 31:
             raise ValueError('n_EI_candidates out of range: %r' % n_cand)

@@ -81,6 +81,19 @@ class History(object):
             v = self._logs[label] = np.log(np.asarray(self.obs[label][1], dtype=np.float64))
         return v
 
+    def coord_values(self, label, key, fn):
+        """fn(values) of a label's observations for an elementwise ``fn`` (a
+        fit coordinate, parzen.fit_coord), memoised under ``key`` — extended
+        incrementally by the Trials cache, else computed once per History."""
+        if self._cache is not None:
+            return self._cache.coord_values(label, key, fn)
+        if self._logs is None:
+            self._logs = {}
+        v = self._logs.get((key, label))
+        if v is None:
+            v = self._logs[(key, label)] = np.ascontiguousarray(fn(self.obs[label][1]), dtype=np.float64)
+        return v
+
     def value_order(self, label):
         """A permutation sorting the label's (float) observation values
         ascending — kept incrementally by the Trials cache, else computed once
@@ -228,6 +241,24 @@ class _Cache(object):
                 g.a = a
                 g.addr = a.ctypes.data
             g.a[g.n:n] = np.log(vals[g.n:n])
+            g.n = n
+        return g.view()
+
+    def coord_values(self, k, key, fn):
+        """fn(obs_val[k]) for an elementwise fn, the values appended since the
+        last call transformed and appended (equal to fn of the column)."""
+        vals = self.obs_val[k].view()
+        n = len(vals)
+        g = self.logs.get((key, k))
+        if g is None or g.n > n:
+            g = self.logs[(key, k)] = _Grow(np.float64)
+        if g.n < n:
+            if g.a.shape[0] < n:
+                a = np.empty(max(n, 2 * g.a.shape[0]), dtype=np.float64)
+                a[:g.n] = g.a[:g.n]
+                g.a = a
+                g.addr = a.ctypes.data
+            g.a[g.n:n] = fn(vals[g.n:n])
             g.n = n
         return g.view()
 

@@ -189,6 +189,21 @@ def _cat_probs_numpy(dist, args, obs, prior_weight, lf):
 DEVICE_FIT_FAMILIES = (N.FAM_GAUSS, N.FAM_LOGGAUSS)
 
 
+def fit_coord(dist, args, obs):
+    """The coordinate adaptive_parzen_normal fits a continuous label's
+    observations in (tpe.py:485-568): the values, their log for the log
+    families, clipped below first for the quantized log families.  Elementwise
+    (so a column may be transformed in pieces)."""
+    obs = np.asarray(obs, dtype=float)
+    if dist in ('loguniform', 'lognormal'):
+        return np.log(obs)
+    if dist == 'qloguniform':                          # tpe.py:523-532
+        return np.log(np.maximum(obs, np.maximum(EPS, np.exp(args['low']))))
+    if dist == 'qlognormal':                           # tpe.py:564
+        return np.log(np.maximum(obs, EPS))
+    return obs
+
+
 def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT_LF, above_dev=None):
     """Fit the below and above posteriors of one hyperparameter.  With
     ``above_dev`` = (device column, n_obs, below_idx, value order) the above mixture is left
@@ -209,14 +224,7 @@ def fit_posterior(dist, args, below_obs, above_obs, prior_weight=1.0, lf=DEFAULT
     q = None if q is None else float(q)
 
     def tr(obs):
-        obs = np.asarray(obs, dtype=float)
-        if dist in ('loguniform', 'lognormal'):
-            return np.log(obs)
-        if dist == 'qloguniform':                          # tpe.py:523-532
-            return np.log(np.maximum(obs, np.maximum(EPS, np.exp(a['low']))))
-        if dist == 'qlognormal':                           # tpe.py:564
-            return np.log(np.maximum(obs, EPS))
-        return obs
+        return fit_coord(dist, a, obs)
 
     below = fit_parzen(tr(below_obs), prior_weight, pmu, psig, lf)
     if above_dev is not None:

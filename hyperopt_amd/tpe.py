@@ -49,7 +49,7 @@ from . import history as _history
 from . import rand
 from . import replay
 from .engine import LevelProblem, get_engine
-from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, cat_split, fit_posterior, fit_split
+from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, cat_split, fit_coord, fit_posterior, fit_split
 
 logger = logging.getLogger(__name__)
 
@@ -487,25 +487,46 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     st = {'arr': tl[0], 'ptr': tl[3]}
     host = {}
 
-    def give(ix):                              # the general path's fit of label ix, for the native call
-        if not host and 'fits' not in st:
-            st['fits'] = _Fits(table, hist, below_tids, prior_weight, engine)
+    def give(ix):
+        """Label ix for the native call with numpy's argsort of each of its
+        sides (the reference's tie order, tpe.py:427-428): the fit coordinate
+        in tid order and the two permutations (tpe_tree_label.side_order) —
+        the native call then fits it.  (A categorical label: the general
+        path's fit.)  False: the label needs the general path."""
+        if not host and 'copied' not in st:
+            st['copied'] = True
             st['arr'] = st['arr'].copy()
             st['ptr'] = None
         row = table.rows[ix]
-        post = st['fits'].get(row)
-        if post.above is None:                 # (device-fitted: the general path)
-            return False
         rec = st['arr'][ix]
-        keep = host[ix] = []                   # (keeps the fitted arrays alive for the call)
-        for sd, side in enumerate((post.below, post.above)):
-            cols = [np.ascontiguousarray(c, dtype=np.float64) for c in side]
-            keep.append(cols)
-            rec['host_k'][sd] = len(cols[0])
-            rec['host_w'][sd] = cols[0].ctypes.data
-            if not row.categorical:
-                rec['host_mu'][sd] = cols[1].ctypes.data
-                rec['host_sigma'][sd] = cols[2].ctypes.data
+        keep = host[ix] = []                   # (keeps the arrays alive for the call)
+        otids, ovals = hist.obs[row.label]
+        n = len(otids)
+        if row.categorical:
+            if 'fits' not in st:
+                st['fits'] = _Fits(table, hist, below_tids, prior_weight, engine)
+            post = st['fits'].get(row)
+            for sd, side in enumerate((post.below, post.above)):
+                c = np.ascontiguousarray(side[0], dtype=np.float64)
+                keep.append(c)
+                rec['host_k'][sd] = len(c)
+                rec['host_w'][sd] = c.ctypes.data
+            return True
+        dmin = _dev_fit_min(engine)
+        if dmin is not None and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and n >= dmin:
+            return False                       # (device-fit sizes: the general path)
+        a = row.args
+        x = hist.coord_values(row.label, row.dist, lambda v: fit_coord(row.dist, a, v))
+        t = np.ascontiguousarray(otids, dtype=np.int64)
+        bidx = _history.below_index(otids, below_tids, hist.sorted_obs)
+        above = np.ones(n, dtype=bool)
+        above[bidx] = False
+        ob = np.argsort(x[bidx])
+        oa = np.argsort(x[above])
+        keep += [x, t, ob, oa]
+        rec['tids'], rec['values'], rec['n_obs'] = t.ctypes.data, x.ctypes.data, n
+        rec['side_order'] = (ob.ctypes.data, oa.ctypes.data)
+        rec['side_n'] = (len(ob), len(oa))
         return True
     # the labels the previous call had to fit here are fitted up front (the active
     # branch seldom changes between suggests): no refused first call

@@ -100,8 +100,10 @@ enum {
                                in the above kernel) */
   TPE_BATCH_ORDERED_DRAWS = 8, /* sorted problems draw ordered candidates, no sort (else i.i.d.
                                   draws + sort) — see "Ordered draws" below */
-  TPE_BATCH_TAB_EXACT = 16     /* test hook: flag every table cell, so every candidate of a
+  TPE_BATCH_TAB_EXACT = 16,    /* test hook: flag every table cell, so every candidate of a
                                   TPE_TAB_CELLS problem takes the exact-sum fallback */
+  TPE_BATCH_NO_TAB_FAST = 32   /* tpe_level_run: the general sample-stage kernel even where the
+                                  specialised one applies (tpe_batch.tab_fast; A/B, tests) */
 };
 
 /* precision of the continuous (non-quantized) families; quantized families
@@ -405,7 +407,12 @@ typedef struct tpe_batch {
   int64_t fit_max_new;        /* most new observations of one job (n_obs - n_ord_in) */
   int64_t fit_max_obs;        /* most observations of one job                       */
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
-  double* draw_pref; int64_t draw_blocks; int32_t n_sorted; int32_t reserved5;
+  double* draw_pref; int64_t draw_blocks; int32_t n_sorted;
+  int32_t tab_fast;      /* 1: every tabulated problem is TPE_TAB_CELLS with both tables within the sample
+                            stage's LDS (tab_n[0] + tab_n[1] <= 2048) and 1..TPE_SAMPLE_LDS_ROWS sampler
+                            rows, the candidates are device-drawn at TPE_PREC_F32, early selection is on
+                            and nothing per candidate is written: the sample stage's specialised kernel
+                            (tpe_level_run sets it; 0: the general one) */
   unsigned long long* pool_best;   /* [n_problems] (pooled problems; see "Pooled labels") */
   /* tabulated scoring: table jobs and the table storage (16-B units) */
   const tpe_tab_job* tab_jobs; int32_t n_tab_jobs; int32_t tab_blocks;
@@ -666,7 +673,11 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
 #define TPE_TREE_MAX_PARENTS 4
 enum { TPE_E_FALLBACK = -5 };
 
-/* one hyperparameter of the tree, in label order (label_ix = its position) */
+/* one hyperparameter of the tree, in label order (label_ix = its position).
+ * Quantized labels and continuous sides with repeated values are fitted with
+ * numpy's argsort permutation of each side (its tie order decides the linear-
+ * forgetting weights of tied observations, tpe.py:427-428): the caller passes
+ * those permutations (side_order) with the fit coordinate, or gets need_fit. */
 typedef struct tpe_tree_label {
   int32_t family, flags, upper, label_ix;   /* family: TPE_FAM_*; flags: TPE_F_HAS_LOW / TPE_F_HAS_HIGH */
   double low, high;                         /* sampling-space bounds (log space for LOGGAUSS)           */
@@ -691,6 +702,14 @@ typedef struct tpe_tree_label {
   const double* dev_obs;
   const double* ord_key_in; const uint32_t* ord_idx_in; int64_t n_ord_in;
   double* ord_key_out; uint32_t* ord_idx_out;
+  /* the caller's sort of each side (continuous and quantized families): side_order[s] = numpy's
+   * np.argsort of side s's coordinates in tid order (s = 0 below, 1 above; `values` = the
+   * fit coordinate, e.g. log(max(x, max(EPS, e^low))) for qloguniform, tpe.py:517-568), side_n[s]
+   * its length (checked against the split made here).  Both set: the label is fitted here with
+   * those permutations — the reference's tie order — instead of being sent to the caller
+   * (need_fit).  NULL: the label's own rules above. */
+  const int64_t* side_order[2];
+  int64_t side_n[2];
 } tpe_tree_label;
 
 /* tpe_suggest_tree flags: the tpe_level_run flags, plus */

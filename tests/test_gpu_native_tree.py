@@ -249,3 +249,112 @@ def test_expanded_level_matches_host_written_level(monkeypatch):
     assert outs[0].shape == (len(ids), len(labels))
     assert np.array_equal(outs[0], outs[1])
     assert np.all(np.isfinite(outs[0])) and np.all(outs[0] >= -5) and np.all(outs[0] < 5)
+
+
+def test_repeated_values_label_crossing_device_fit_min():
+    """A continuous label with repeated values (its host fits need numpy's tie
+    order: the native call flags it, the next call gets the caller's fit up
+    front) whose history grows across device_fit_min, through the window
+    n_obs in [device_fit_min, device_fit_min + n_below) where both paths must
+    agree on the device fit: every suggest equals the general path's, and the
+    label's resident value order is np.argsort(kind='stable') of its values
+    after every suggest that used it."""
+    from hyperopt_amd import base, devhist, hp, history as H, tpe
+    from hyperopt_amd.engine import get_engine
+    eng = get_engine()
+    old = eng.device_fit_min
+    dmin = 2000
+    table = base.Domain(lambda d: 0.0, {'u': hp.uniform('u', -5, 5), 'v': hp.uniform('v', 0, 1)}).table
+    rs = np.random.RandomState(21)
+    Nt = dmin + 60
+    vals = {'u': np.round(rs.uniform(-5, 5, Nt), 2), 'v': rs.uniform(0, 1, Nt)}
+    tids = np.arange(Nt, dtype=np.int64)
+    losses = rs.uniform(size=Nt) + 1e-9 * tids
+    dev = {}
+    try:
+        eng.device_fit_min = dmin
+        for n in (dmin - 20, dmin - 10, dmin + 2, dmin + 6, dmin + 30, dmin + 60):
+            hist = H.History(tids[:n], losses[:n].copy(), {k: (tids[:n], v[:n]) for k, v in vals.items()}, dev=dev)
+            nb = len(H.split_below(hist, 0.25))
+            got = tpe.suggest_choices(table, hist, [n], 100 + n, n_EI_candidates=4096)[0]
+            fresh = H.History(tids[:n], losses[:n].copy(), {k: (tids[:n], v[:n]) for k, v in vals.items()}, dev={})
+            tpe.NATIVE_TREE = False
+            try:
+                want = tpe.suggest_choices(table, fresh, [n], 100 + n, n_EI_candidates=4096)[0]
+            finally:
+                tpe.NATIVE_TREE = True
+            assert got == want, (n, got, want)
+            if tpe.device_fits(n, nb, dmin):
+                dc = devhist.columns(hist, eng.device)
+                for label in ('u', 'v'):
+                    keys, idx = dc.order(label).host()
+                    w = np.argsort(vals[label][:n], kind='stable')
+                    np.testing.assert_array_equal(idx, w, err_msg='%s n=%d' % (label, n))
+                    np.testing.assert_array_equal(keys, vals[label][:n][w], err_msg='%s n=%d' % (label, n))
+    finally:
+        eng.device_fit_min = old
+
+
+def test_quantized_labels_one_native_call():
+    """Quantized labels (the rf branch, and config 2's mixed space) are fitted
+    inside tpe_suggest_tree from numpy's argsort of each side (the reference's
+    tie order, tpe.py:427-428) that the host passes in: after the first
+    suggest on a space, every suggest is ONE native call, and equal to the
+    general path's suggestion."""
+    import bench
+    from hyperopt_amd import tpe
+    from hyperopt_amd.engine import get_engine
+    eng = get_engine()
+    domain, trials = bench.make_history(3000, 0, loss=bench.rf_loss)
+    tpe.suggest([3000], domain, trials, 1, n_EI_candidates=1 << 16)
+    for seed in (7, 8, 9):
+        c0 = eng.tree_calls
+        nat = doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=1 << 16))
+        assert eng.tree_calls - c0 == 1, seed
+        tpe.NATIVE_TREE = False
+        try:
+            gen = doc_values(tpe.suggest([3000], domain, trials, seed, n_EI_candidates=1 << 16))
+        finally:
+            tpe.NATIVE_TREE = True
+        assert nat == gen and int(nat['model']) == 1, (seed, nat, gen)
+    domain, trials = bench.mixed10_history(1000, 3)
+    tpe.suggest([1000], domain, trials, 1, n_EI_candidates=10000)
+    for seed in (4, 5):
+        c0 = eng.tree_calls
+        nat = doc_values(tpe.suggest([1000], domain, trials, seed, n_EI_candidates=10000))
+        assert eng.tree_calls - c0 == 1, seed
+        tpe.NATIVE_TREE = False
+        try:
+            gen = doc_values(tpe.suggest([1000], domain, trials, seed, n_EI_candidates=10000))
+        finally:
+            tpe.NATIVE_TREE = True
+        assert nat == gen, (seed, nat, gen)
+
+
+@pytest.mark.parametrize('extra', [0, 16])
+def test_fast_sample_kernel_matches_general(monkeypatch, extra):
+    """The sample stage's specialised kernel (tpe_batch.tab_fast: cells tables
+    in LDS, staging overlapped with the first draws) chooses exactly what the
+    general kernel chooses — the same draws, look-ups and run reduction — on
+    the config-3 tree (one id, 2^20 candidates: dynamic pair hand-out), a
+    batched 20-dim level (expanded, one pair per problem) and a tiny C (single
+    tiles); ``extra`` = TPE_BATCH_TAB_EXACT: every candidate through the exact
+    fallback."""
+    import bench
+    from hyperopt_amd import tpe
+    domain, trials = bench.make_history(3000, 0)
+    labels = ['x%02d' % i for i in range(20)]
+    hist = bench.soa_history(labels, 3000, 5, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
+    table = bench.flat_uniform_table(labels)
+
+    def run():
+        out = [doc_values(tpe.suggest([3000], domain, trials, s, n_EI_candidates=1 << 20)) for s in (3, 4)]
+        cc = tpe.suggest_choices(table, hist, np.arange(3000, 3300), 6, n_EI_candidates=4096, columns=True)
+        out.append(cc.values.tolist())
+        out.append(doc_values(tpe.suggest([3000], domain, trials, 7, n_EI_candidates=2048)))
+        return out
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra))
+    fast = run()
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra | 32))
+    gen = run()
+    assert fast == gen

@@ -43,7 +43,7 @@ prof_run() {  # name counters...
   local name=$1; shift
   rm -rf $O/pmc_${TAG}/$name
   step 300 $O/pmc_${TAG}/$name.log rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
-      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-quantized --no-appending ${BENCH_ARGS:-}
+      -d $O/pmc_${TAG}/$name -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-quantized --no-appending --no-config4 ${BENCH_ARGS:-}
 }
 
 for task in "$@"; do
@@ -61,7 +61,7 @@ for task in "$@"; do
     trace)
       rm -rf $O/trace_${TAG}
       step 600 $O/trace_${TAG}.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_${TAG} -o run -- \
-          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-quantized --no-appending ${BENCH_ARGS:-}
+          python3 bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-quantized --no-appending --no-config4 ${BENCH_ARGS:-}
       python3 tools/trace_summary.py $(find $O/trace_${TAG} -name "*kernel_trace.csv") > $O/trace_${TAG}_summary.txt
       head -25 $O/trace_${TAG}_summary.txt ;;
     pmc)
@@ -80,6 +80,16 @@ for task in "$@"; do
       for c in ${CONFIGS:-1 2 4 5}; do
         step 600 $O/cfg${c}_${TAG}.err python bench.py --config $c --steps ${CFG_STEPS:-5} --warmup 1
         grep '^{' $O/cfg${c}_${TAG}.err > $O/cfg${c}_${TAG}.json; cat $O/cfg${c}_${TAG}.json
+      done ;;
+    envab)
+      # stage times + headline p50 per environment setting in ENVAB (space-separated
+      # VAR=value specs, "default" = none), alternating on one box
+      for v in ${ENVAB:-default}; do
+        if [ "$v" = default ]; then e=""; else e="$v"; fi
+        step 300 $O/stage_${TAG}_$v.txt env $e python tools/stage_bench.py ${REP:-20}
+        step 300 $O/bench_${TAG}_$v.err env $e python bench.py --no-cpu-baseline --no-quantized --no-config4 --steps 100
+        echo "$v: $(grep -o '"p50_suggest_ms": [0-9.]*\|"stage_ms": {[^}]*}' $O/bench_${TAG}_$v.err | tr '\n' ' ')"
+        grep -i "k_sample\|k_tables" $O/stage_${TAG}_$v.txt | head -4
       done ;;
     rehearse)
       # the N > 1 flow with 2 ranks on the box's one GPU (gloo: RCCL takes one rank per device)
