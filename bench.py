@@ -119,7 +119,7 @@ def host_cpu():
     return dict(model=model, logical_cpus=os.cpu_count(), usable_cpus=aff)
 
 
-def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64), sweep_s=6.0):
+def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64, 128, 256), sweep_s=5.0):
     """The oracle (numpy restatement of the reference, tools/oracle_vs_reference.py
     times it against the reference itself) on a bounded sample of the same
     workload: whole suggests at C = 16384 on the same 10k-trial history,
@@ -163,7 +163,11 @@ def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64), sweep_s=6.0):
     if limiter is not None:
         limiter.unregister()
     best = max(pts, key=lambda p: p['value'])
+    # the knee: the smallest pool within 5 % of the best (more processes than
+    # the host's CPU share buy nothing)
+    knee = min((p for p in pts if p['value'] >= 0.95 * best['value']), key=lambda p: p['processes'])
     return dict(value=best['value'], unit='candidate-scores/s', cores=best['processes'], kind='port',
+                knee_processes=knee['processes'],
                 sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, candidate scoring chunked '
                        'over %d processes, %.1fs (best of the process sweep)'
                        % (best['calls'], best['processes'], best['secs']),

@@ -15,8 +15,9 @@ ABI_VERSION = 19
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
-F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT, F_FGT, F_REMOTE = 1, 2, 4, 8, 16, 32, 64, 128
-TAB_NONE, TAB_CELLS, TAB_LATTICE = 0, 1, 2
+F_HAS_LOW, F_HAS_HIGH, F_POOLED, F_CAT_LAZY, F_NO_TABLE, F_PREFIT, F_FGT, F_REMOTE, F_LOGPOLY = \
+    1, 2, 4, 8, 16, 32, 64, 128, 256
+TAB_NONE, TAB_CELLS, TAB_LATTICE, TAB_LOGPOLY = 0, 1, 2, 3
 TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
 BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS, BATCH_TAB_EXACT, BATCH_NO_TAB_FAST = \

@@ -78,6 +78,16 @@ bool fgt_enabled() {
   return !(e && e[0] == '0');
 }
 constexpr double kTabMinRatioFgt = 1.0;          // candidates per cell row for box-moment tables
+// log-polynomial rows (TPE_F_LOGPOLY): both sides on the finer side's grid, one
+// 48-B row per cell, at most the sample stage's LDS table rows (kTabLdsCells);
+// TPE_LOGPOLY=0: moment rows for every cells label (A/B, tests)
+constexpr int64_t kLogpolyMaxCells = 2048;
+constexpr int64_t kLpDirectRows = 64;       // a side of <= this many rows: direct sums, no moments
+constexpr int64_t kLpRowsPerWave = 5;       // ... kLpRowsPerWave cell rows per table-stage wave
+bool logpoly_enabled() {
+  const char* e = getenv("TPE_LOGPOLY");
+  return !(e && e[0] == '0');
+}
 constexpr int64_t kFgtMaxBoxes = 4096;
 // a of the device fit's narrowest components: (float)(sqrt(log2(e) / 2) / max(smin, EPS)),
 // smin = prior_sigma / min(100, 1 + K) (tpe.py:465-470), as k_fit_emit rounds it
@@ -780,6 +790,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<int64_t> tn0((size_t)n_labels, 0), tn1((size_t)n_labels, 0), tlat((size_t)n_labels, 0);
   std::vector<double> tklo((size_t)n_labels, 0), tkhi((size_t)n_labels, 0);
   std::vector<int64_t> fgt_boxes((size_t)n_labels, 0);   // box-moment labels: their boxes
+  std::vector<char> logpoly((size_t)n_labels, 0);         // TPE_F_LOGPOLY labels
   for (int32_t li = 0; li < n_labels && tab_on && n_cand > 0; ++li) {
     const tpe_label_in& L = labels[li];
     const double ct = (double)L.n_ids * (double)n_cand;     // candidates of the label in this level
@@ -809,7 +820,16 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         if (d > 0 && nb >= 1.0 && nb <= (double)kFgtMaxBoxes) nbox = (int64_t)nb;
       }
       const double ratio = nbox > 0 ? kTabMinRatioFgt : dev_fit[li] ? devfit_ratio() : kTabMinRatio;
-      if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= ratio * (double)(n0 + n1)) {
+      const int64_t nl = std::max(n0, n1);
+      const double lp_ratio = dev_fit[li] ? devfit_ratio() : kTabMinRatio;   // (moment cells, no boxes)
+      // (box-moment labels keep moment cells: their above cells come from the boxes)
+      if (logpoly_enabled() && nbox == 0 && n0 > 0 && n1 > 0 && nl <= kLogpolyMaxCells &&
+          ct >= lp_ratio * (double)(2 * nl)) {
+        // both sides' log-polynomials on one grid (the finer side's cells): one
+        // row per candidate look-up (include/tpe_hip.h, TPE_F_LOGPOLY)
+        tmode[li] = TPE_TAB_CELLS; tn0[li] = tn1[li] = nl;
+        logpoly[li] = 1;
+      } else if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= ratio * (double)(n0 + n1)) {
         tmode[li] = TPE_TAB_CELLS; tn0[li] = n0; tn1[li] = n1;
         fgt_boxes[li] = nbox;
       }
@@ -955,7 +975,18 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   for (int32_t li = 0; li < n_labels; ++li) {
     tpe_problem& p = lab[li];
     p.tab_mode = tmode[li];
-    if (tmode[li] == TPE_TAB_CELLS) {
+    if (tmode[li] == TPE_TAB_CELLS && logpoly[li]) {
+      // one table, both sides' polynomials in each row
+      const int64_t n = tn0[li];
+      p.flags |= TPE_F_LOGPOLY;
+      for (int sd = 0; sd < 2; ++sd) {
+        p.tab_off[sd] = (int32_t)tab_units;
+        p.tab_n[sd] = (int32_t)n;
+        p.tab_lo[sd] = (float)tklo[li];
+        p.tab_inv[sd] = (float)((double)n / (tkhi[li] - tklo[li]));
+      }
+      tab_units += kTabRowUnits * n;
+    } else if (tmode[li] == TPE_TAB_CELLS) {
       for (int sd = 0; sd < 2; ++sd) {
         const int64_t n = sd ? tn1[li] : tn0[li];
         p.tab_off[sd] = (int32_t)tab_units;
@@ -1157,6 +1188,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       j.problem = r; j.side = sd; j.kind = p.tab_mode; j.n = p.tab_n[sd]; j.off = p.tab_off[sd];
       j.block0 = (int32_t)tab_blocks;
       if (j.kind == TPE_TAB_CELLS) {
+        if (p.flags & TPE_F_LOGPOLY) j.kind = TPE_TAB_LOGPOLY;
         // the rows the side's cells sum (a device-fitted above side: its fit writes them)
         j.rows_off = sd ? p.above_off : p.below_off;
         j.rows_n = sd && dev_fit[li] ? -1 : sd ? p.above_len : p.below_len;
@@ -1168,7 +1200,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       // cells: TPE_TAB_PER_BLOCK rows per block; lattice: one block per value
       // (a box-moment label's above cells are built by their own stage: no blocks here)
       if (sd == 1 && (p.flags & TPE_F_FGT)) fgt_max_cells = std::max<int64_t>(fgt_max_cells, j.n);
-      else tab_blocks += j.kind == TPE_TAB_CELLS ? (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK : j.n;
+      else if (j.kind == TPE_TAB_LOGPOLY && j.rows_n >= 0 && j.rows_n + j.wide_n <= kLpDirectRows)
+        tab_blocks += (j.n + kLpRowsPerWave * TPE_TAB_PER_BLOCK - 1) / (kLpRowsPerWave * TPE_TAB_PER_BLOCK);
+      else tab_blocks += j.kind != TPE_TAB_LATTICE ? (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK : j.n;
       tab_jobs.push_back(j);
     }
   }

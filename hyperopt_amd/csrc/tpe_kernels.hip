@@ -846,6 +846,27 @@ __device__ __forceinline__ float cell_log2_lds(float lo, float inv, float w, flo
   return sm > 0.f ? c.w + __log2f(sm) : NAN;
 }
 
+// log2 of both mixture sides at t from a TPE_F_LOGPOLY row (include/tpe_hip.h,
+// "Tabulated scoring"): {b_0..b_5, a_0..a_5}, degree-5 polynomials in u; NAN
+// for a side outside the cells or flagged (b_0 / a_0 = NaN).  Cell centre and
+// u as cell_log2_lds forms them.
+__device__ __forceinline__ void lp_log2(float lo, float inv, float w, float ih, int n, const float4* __restrict__ rows,
+                                        float t, float& lb2, float& la2) {
+  const float gj = floorf((t - lo) * inv);
+  const bool in = gj >= 0.f && gj < (float)n;
+  const float4* __restrict__ r = rows + TPE_TAB_ROW_UNITS * (in ? (int)gj : 0);
+  const float4 a = r[0], b = r[1], c = r[2];
+  const float u = (t - __builtin_fmaf(gj + 0.5f, w, lo)) * ih;
+  float sb = b.y;
+  sb = __builtin_fmaf(sb, u, b.x); sb = __builtin_fmaf(sb, u, a.w); sb = __builtin_fmaf(sb, u, a.z);
+  sb = __builtin_fmaf(sb, u, a.y); sb = __builtin_fmaf(sb, u, a.x);
+  float sa = c.w;
+  sa = __builtin_fmaf(sa, u, c.z); sa = __builtin_fmaf(sa, u, c.y); sa = __builtin_fmaf(sa, u, c.x);
+  sa = __builtin_fmaf(sa, u, b.w); sa = __builtin_fmaf(sa, u, b.z);
+  lb2 = in ? sb : NAN;
+  la2 = in ? sa : NAN;
+}
+
 // PREC is a template parameter: with the f64 inverse-CDF path reachable, the
 // candidate loop needs several times the registers
 // f64 exp out of line: inlined, its polynomial's f64 constants were hoisted
@@ -1047,14 +1068,14 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             const float sg = (float)sr[2];
             srow = make_float4((float)sr[1], sr[5] != 0.0 ? -sg : sg, (float)sr[3], (float)sr[4]);
           }
+          // (FAST: the label's one TPE_F_LOGPOLY table)
           constexpr int kStageU = TPE_TAB_ROW_UNITS * kTabLdsCells / kTabThreads;
-          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], nu = n0 + TPE_TAB_ROW_UNITS * p.tab_n[1];
+          const int nu = TPE_TAB_ROW_UNITS * p.tab_n[0];
           const int wv = (int)(threadIdx.x >> 6);
 #pragma unroll
           for (int u = 0; u < kStageU; ++u) {
             const int q = min(u * kTabThreads + (int)threadIdx.x, nu - 1);
-            const float4* src = q < n0 ? tab + (int64_t)p.tab_off[0] + q : tab + (int64_t)p.tab_off[1] + (q - n0);
-            __builtin_amdgcn_global_load_lds((const void*)src,
+            __builtin_amdgcn_global_load_lds((const void*)(tab + (int64_t)p.tab_off[0] + q),
                                              (__attribute__((address_space(3))) void*)(tab_lds + u * kTabThreads + 64 * wv),
                                              16, 0, 0);
           }
@@ -1088,11 +1109,10 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       const int nunits = npairs * (kTabThreads / 64);
       float lo_f, hi_f;
       f32_bounds(p, lo_f, hi_f);
-      const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
-      const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
-      const int n0 = p.tab_n[0], n1 = p.tab_n[1];
+      const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0];
+      const float w0 = 1.f / inv0, ih0 = 1.f / (0.5f * w0);
+      const int n0 = p.tab_n[0];
       const float4* __restrict__ r0 = tab_lds;
-      const float4* __restrict__ r1 = tab_lds + TPE_TAB_ROW_UNITS * n0;
       // the next unit of this wave: false when the run has none left (dynamic)
       int first = 0;
       auto next_unit = [&](bool initial) -> bool {
@@ -1190,8 +1210,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           for (int j = 0; j < NP; ++j) {
             const int i = first + j;
             const float t = tj[j];
-            const float lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, r0, 1, TPE_TAB_ROW_UNITS, t),
-                        la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, r1, 1, TPE_TAB_ROW_UNITS, t);
+            float lb2, la2;
+            lp_log2(lo0, inv0, w0, ih0, n0, r0, t, lb2, la2);
             const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
             exact |= (unsigned)(valid && !ok) << j;
             if (valid && ok) track(i, lb2, la2, t);
@@ -1204,8 +1224,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
               const int src = __builtin_ctzll(need);
               need &= need - 1;
               const float t = __shfl(tj[j], src);
-              float lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, r0, 1, TPE_TAB_ROW_UNITS, t),
-                    la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, r1, 1, TPE_TAB_ROW_UNITS, t);
+              float lb2, la2;
+              lp_log2(lo0, inv0, w0, ih0, n0, r0, t, lb2, la2);
               if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
               if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
               if (lane == src) track(first + j, lb2, la2, t);
@@ -1235,7 +1255,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         __syncthreads();                               // LDS free for the next label's rows
         const double* S = samp + 8 * (int64_t)p.samp_off;
         in_lds = draw && p.samp_len > 0 && p.samp_len <= kCumLds;
-        tab_in_lds = PREC == TPE_PREC_F32 && cells && p.tab_n[0] + p.tab_n[1] <= kTabLdsCells;
+        const bool lpt = (p.flags & TPE_F_LOGPOLY) != 0;       // (one table for both sides)
+        tab_in_lds = PREC == TPE_PREC_F32 && cells && (lpt ? p.tab_n[0] : p.tab_n[0] + p.tab_n[1]) <= kTabLdsCells;
         // the table units straight from global memory into LDS (LDS-DMA: no
         // registers, no store instructions; row-major, unit q at tab_lds[q] —
         // a wave's 64 consecutive units land at consecutive 16-B slots), the
@@ -1244,7 +1265,7 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         constexpr int kStageU = TPE_TAB_ROW_UNITS * kTabLdsCells / kTabThreads;
         static_assert(kCumLds <= kTabThreads, "one sampler row per thread");
         if (tab_in_lds) {
-          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], nu = n0 + TPE_TAB_ROW_UNITS * p.tab_n[1];
+          const int n0 = TPE_TAB_ROW_UNITS * p.tab_n[0], nu = lpt ? n0 : n0 + TPE_TAB_ROW_UNITS * p.tab_n[1];
           const int wv = (int)(threadIdx.x >> 6);
 #pragma unroll
           for (int u = 0; u < kStageU; ++u) {
@@ -1326,8 +1347,21 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0], lo1 = p.tab_lo[1], inv1 = p.tab_inv[1];
         const float w0 = 1.f / inv0, w1 = 1.f / inv1, ih0 = 1.f / (0.5f * w0), ih1 = 1.f / (0.5f * w1);
         const int n0 = p.tab_n[0], n1 = p.tab_n[1];
-        constexpr bool kL = decltype(TL)::value;
-        constexpr int stride = 1, step = TPE_TAB_ROW_UNITS;      // row-major rows in LDS and global memory
+        const bool lpt = (p.flags & TPE_F_LOGPOLY) != 0;
+        // both sides' log2 sums at t: a TPE_F_LOGPOLY row, or one moment row per side
+        auto sides_nb = [&](const float4* __restrict__ a0, const float4* __restrict__ a1, float t, float& lb2,
+                            float& la2) {
+          if (lpt) { lp_log2(lo0, inv0, w0, ih0, n0, a0, t, lb2, la2); return; }
+          lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, a0, 1, TPE_TAB_ROW_UNITS, t);
+          la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, a1, 1, TPE_TAB_ROW_UNITS, t);
+        };
+        auto sides = [&](const float4* __restrict__ a0, const float4* __restrict__ a1, float t, float& lb2,
+                         float& la2) {
+          if (lpt) { lp_log2(lo0, inv0, w0, ih0, n0, a0, t, lb2, la2); return; }
+          lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, a0, 1, TPE_TAB_ROW_UNITS, t);
+          la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, a1, 1, TPE_TAB_ROW_UNITS, t);
+        };
+        constexpr bool kL = decltype(TL)::value;              // (rows row-major in LDS and global memory)
         const float4* __restrict__ r0;
         const float4* __restrict__ r1;
         if constexpr (kL) { r0 = tab_lds; r1 = tab_lds + TPE_TAB_ROW_UNITS * n0; }
@@ -1377,8 +1411,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           for (int j = 0; j < NP; ++j) {
             const int i = first + j;
             const float t = tj[j];
-            const float lb2 = cell_log2_nb(lo0, inv0, w0, ih0, n0, r0, stride, step, t),
-                        la2 = cell_log2_nb(lo1, inv1, w1, ih1, n1, r1, stride, step, t);
+            float lb2, la2;
+            sides_nb(r0, r1, t, lb2, la2);
             const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
             exact |= (unsigned)(valid && !ok) << j;
             if (valid && ok) track(i, lb2, la2, t);
@@ -1409,8 +1443,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             t = NAN;
           }
           tj[j] = t;
-          const float lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, r0, stride, step, t),
-                    la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, r1, stride, step, t);
+          float lb2, la2;
+          sides(r0, r1, t, lb2, la2);
           if (!(lb2 == lb2) || !(la2 == la2)) { exact |= 1u << j; continue; }
           track(i, lb2, la2, t);
           if (need_x) {                          // per-candidate outputs on request (tests)
@@ -1432,8 +1466,8 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             const int src = __builtin_ctzll(need);
             need &= need - 1;
             const float t = __shfl(tj[j], src);
-            float lb2 = cell_log2_lds(lo0, inv0, w0, ih0, n0, r0, stride, step, t),
-                    la2 = cell_log2_lds(lo1, inv1, w1, ih1, n1, r1, stride, step, t);
+            float lb2, la2;
+            sides(r0, r1, t, lb2, la2);
             if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
             if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
             if (lane == src) {
@@ -2926,6 +2960,64 @@ __device__ void lattice_row(const tpe_problem& p, int j, const double4* __restri
   }
 }
 
+// ---- TPE_F_LOGPOLY rows (include/tpe_hip.h, "Tabulated scoring") ----
+// nodes: the 6 Chebyshev points cos((2i + 1) pi / 12) of [-1, 1] (interpolation),
+// then the check points 0, 1/2, -1/2, 1, -1; kLpA: monomial coefficients of the
+// degree-5 interpolant from its values at the 6 nodes (the inverse Vandermonde)
+__constant__ double kLpNode[11] = {0.96592582628906831, 0.70710678118654757, 0.25881904510252074, -0.25881904510252063, -0.70710678118654746, -0.9659258262890682, 0, 0.5, -0.5, 1, -1};
+__constant__ double kLpA[6][6] = {
+    {0.044658198738520241, -0.1666666666666663, 0.62200846792814679, 0.62200846792814635, -0.16666666666666655, 0.04465819873852047},
+    {0.046233569414010529, -0.23570226039551737, 2.4032561733691682, -2.4032561733691673, 0.2357022603955134, -0.046233569414008954},
+    {-0.75598306414370686, 2.6666666666666647, -1.9106836025229559, -1.9106836025229608, 2.666666666666667, -0.75598306414370731},
+    {-0.7826512591014102, 3.771236166328257, -7.3823145501758516, 7.3823145501758454, -3.7712361663282445, 0.78265125910140476},
+    {1.3333333333333324, -2.6666666666666647, 1.3333333333333304, 1.333333333333335, -2.666666666666667, 1.3333333333333333},
+    {1.3803682405467783, -3.7712361663282552, 5.1516044068750295, -5.1516044068750251, 3.7712361663282468, -1.3803682405467748}};
+constexpr double kLpTol = 5e-7;        // |fit - value| <= kLpTol (1 + |log2 s|) at the check points
+// a side of at most this many component rows (the below side: <= 26) gets its
+// log-polynomials from direct sums at the nodes, one cell row per thread
+// (tpe_host.cpp kLpDirectRows: its job's blocks hold 512 rows, not 8)
+constexpr int kLpDirectRows = 64;
+constexpr int kLpRowsPerWave = 5;      // (5 rows x 11 nodes = 55 lanes; tpe_host.cpp kLpRowsPerWave)
+
+// log2 of a positive normal double to ~1e-7 absolute (exponent + f32 log2 of the mantissa)
+__device__ __forceinline__ double log2_fast(double x) {
+  int e;
+  const double m = frexp(x, &e);                  // x = m 2^e, m in [0.5, 1)
+  return (double)e + (double)__log2f((float)m);
+}
+
+// one side's log-polynomial from its reduced cell moments (wave-collective):
+// lane 4q holds moment q's f64 sum; m = the cell's log2 shift; flagged: the
+// side takes the exact sum for its candidates.  Lanes 0..5 write c_0..c_5 to
+// out[0..5] (f32), NaN in all six when the side is flagged or fails the check.
+__device__ __forceinline__ void logpoly_side(double sum, float m, bool flagged, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  double M[kTabMoments];
+#pragma unroll
+  for (int q = 0; q < kTabMoments; ++q) M[q] = __shfl(sum, 4 * q);
+  // the moment series and its log2 at this lane's node (lanes 0..10)
+  const double u = kLpNode[lane < 11 ? lane : 0];
+  double sr = M[kTabMoments - 1];
+#pragma unroll
+  for (int q = kTabMoments - 2; q >= 0; --q) sr = __builtin_fma(sr, u, M[q]);
+  const bool pos = sr > 0.0 && sr < INFINITY;
+  const double y = (double)m + log2_fast(pos ? sr : 1.0);
+  // interpolant coefficients (lanes 0..5) and its value at every node
+  const int r = lane < 6 ? lane : 0;
+  double c = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c = __builtin_fma(kLpA[r][i], __shfl(y, i), c);
+  double C[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) C[k] = __shfl(c, k);
+  double pv = C[5];
+#pragma unroll
+  for (int k = 4; k >= 0; --k) pv = __builtin_fma(pv, u, C[k]);
+  const bool bad = lane < 11 && (!pos || !(fabs(pv - y) <= kLpTol * (1.0 + fabs(y))));
+  const bool any = __ballot(bad) != 0ull || flagged || !(m == m);
+  if (lane < 6) out[lane] = any ? NAN : (float)c;
+}
+
 // 512-thread workgroups, one wave per cell row / lattice value
 // (TPE_TAB_PER_BLOCK per workgroup).  A cell job's workgroup first stages its
 // side's component rows in LDS (unless pruned or too many), so both passes of
@@ -2968,7 +3060,54 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
   const tpe_problem& p = P[jb.problem];
   const int b = (int)blockIdx.x - jb.block0;
   const int j = b * TPE_TAB_PER_BLOCK + (int)(threadIdx.x >> 6);
-  if (jb.kind == TPE_TAB_CELLS) {
+  if (jb.kind == TPE_TAB_LOGPOLY && jb.rows_n >= 0 && jb.rows_n + jb.wide_n <= kLpDirectRows) {
+    // a short side (the below mixture): its log-polynomials from the exact
+    // max-shifted sums at the nodes, no moments — a wave holds kLpRowsPerWave
+    // cell rows, one lane per (row, node); node positions and exponents in f64
+    // (an f32 t would move a node of a narrow cell by a sizeable part of it)
+    const int nr = jb.rows_n + jb.wide_n;
+    if ((int)threadIdx.x < nr)
+      rows_lds[threadIdx.x] = (int)threadIdx.x < jb.rows_n ? comp32[jb.rows_off + threadIdx.x]
+                                                           : comp32[jb.wide_off + threadIdx.x - jb.rows_n];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int rl = lane / 11, k = lane - 11 * rl;               // (row of the wave, node)
+    const int jr = (b * TPE_TAB_PER_BLOCK + wave) * kLpRowsPerWave + rl;
+    const bool live = rl < kLpRowsPerWave && jr < jb.n;
+    const float w = 1.f / jb.inv;
+    const double c = (double)__builtin_fmaf((float)(live ? jr : 0) + 0.5f, w, jb.lo);   // (as the sample stage forms it)
+    const double h = 0.5 * (double)w;
+    const double t = c + h * kLpNode[live ? k : 0];
+    double m = -INFINITY;
+    for (int q = 0; q < nr; ++q) {
+      const float4 r = rows_lds[q];
+      const double z = ((t - (double)r.x) - (double)r.y) * (double)r.z;
+      m = fmax(m, (double)r.w - z * z);
+    }
+    double sm = 0.0;
+    for (int q = 0; q < nr; ++q) {
+      const float4 r = rows_lds[q];
+      const double z = ((t - (double)r.x) - (double)r.y) * (double)r.z;
+      sm += (double)__builtin_amdgcn_exp2f((float)((double)r.w - z * z - m));
+    }
+    const bool ok = !all_exact && m > -INFINITY && m < INFINITY && sm > 0.0;
+    const double y = m + log2_fast(sm > 0.0 ? sm : 1.0);
+    // the row's interpolant: lane (rl, k < 6) forms c_k, lanes (rl, k >= 6) check it
+    const int b0 = 11 * (rl < kLpRowsPerWave ? rl : 0);
+    double cf = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) cf = __builtin_fma(kLpA[k < 6 ? k : 0][i], __shfl(y, b0 + i), cf);
+    double pv = __shfl(cf, b0 + 5);
+#pragma unroll
+    for (int n = 4; n >= 0; --n) pv = __builtin_fma(pv, kLpNode[live ? k : 0], __shfl(cf, b0 + n));
+    const bool bad = live && (!ok || (k >= 6 && !(fabs(pv - y) <= kLpTol * (1.0 + fabs(y)))));
+    const unsigned long long bm = __ballot(bad);
+    const bool row_bad = rl < kLpRowsPerWave && ((bm >> b0) & 0x7FFull) != 0ull;
+    if (live && k < 6)
+      reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * jr)[6 * jb.side + k] = row_bad ? NAN : (float)cf;
+    return;
+  }
+  if (jb.kind == TPE_TAB_CELLS || jb.kind == TPE_TAB_LOGPOLY) {
     // (the job carries the rows and geometry: no problem row on this path, but
     // for a device-fitted above side, rows_n < 0, whose fit wrote them there)
     [[maybe_unused]] const int side = jb.side;
@@ -3027,10 +3166,18 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       for (int i = 0; i < 16; ++i) sum += red[q * 64 + part * 16 + i];
     sum += __shfl_xor(sum, 1);
     sum += __shfl_xor(sum, 2);
+    float* row = reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * j);
+    if (jb.kind == TPE_TAB_LOGPOLY) {
+      // this side's half of the label's row: its log-polynomial (lane 11's
+      // shift and flag, as the moment row takes them)
+      const float m = __shfl(mx, kTabMoments);
+      const bool fl = __shfl(bad || all_exact ? 1 : 0, kTabMoments) != 0;
+      logpoly_side(sum, m, fl, row + 6 * jb.side);
+      return;
+    }
     float val = 0.f;
     if (part == 0 && q < kTabMoments) val = (float)sum;
     // row lanes: moment q from lane 4q, then the shift mx (NaN: the cell is flagged)
-    float* row = reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * j);
     const float mv = __shfl(val, 4 * (lane < kTabMoments ? lane : 0));
     float out = lane < kTabMoments ? mv : 0.f;
     if (lane == kTabMoments) out = bad || all_exact ? NAN : mx;
@@ -4430,8 +4577,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     for (int64_t r = 0; fast && r < n_rows; ++r) {
       const tpe_problem& q = rows[r];
       if (q.tab_mode == TPE_TAB_NONE) continue;
-      fast = q.tab_mode == TPE_TAB_CELLS && q.tab_n[0] + q.tab_n[1] <= kTabLdsCells && q.samp_len > 0 &&
-             q.samp_len <= kCumLds;
+      fast = q.tab_mode == TPE_TAB_CELLS && (q.flags & TPE_F_LOGPOLY) && q.tab_n[0] <= kTabLdsCells &&
+             q.samp_len > 0 && q.samp_len <= kCumLds;
     }
     b.tab_fast = fast && n_rows > 0 ? 1 : 0;
   }

@@ -59,6 +59,9 @@ TAB_ETA = 0.05                     # tpe_host.cpp kTabEta: a_max * h <= eta per 
 TAB_MAX_CELLS = 65536
 TAB_MAX_LATTICE = 1 << 18
 TAB_MIN_RATIO, TAB_MIN_RATIO_DEVFIT = 8.0, 64.0   # tpe_host.cpp kTabMinRatio*: candidates per cell row
+LOGPOLY_MAX_CELLS = 2048           # tpe_host.cpp kLogpolyMaxCells (TPE_F_LOGPOLY: one grid for both sides)
+LP_DIRECT_ROWS = 64                # tpe_host.cpp kLpDirectRows
+LP_ROWS_PER_WAVE = 5               # tpe_host.cpp kLpRowsPerWave
 A_SCALE_LIT = 0.84932180028801907  # tpe_host.cpp kAScale (the same double)
 
 
@@ -89,6 +92,12 @@ def _tab_plan(lp, n_cand, f64):
             s1 = float(np.min(post.above[2]))
         n0, n1 = cells(s0), cells(s1)
         ratio = TAB_MIN_RATIO_DEVFIT if post.above_dev is not None else TAB_MIN_RATIO
+        nl = max(n0, n1)
+        # (a device-fitted label takes box-moment cells when TPE_FGT allows: tpe_host.cpp)
+        boxes = post.above_dev is not None and not os.environ.get('TPE_FGT', '1').startswith('0')
+        if (not os.environ.get('TPE_LOGPOLY', '1').startswith('0') and not boxes and n0 > 0 and n1 > 0
+                and nl <= LOGPOLY_MAX_CELLS and ct >= ratio * 2 * nl):
+            return dict(mode=N.TAB_CELLS, n=(nl, nl), lo=klo, hi=khi, lat_lo=0, logpoly=True)
         if 0 < n0 <= TAB_MAX_CELLS and 0 < n1 <= TAB_MAX_CELLS and ct >= ratio * (n0 + n1):
             return dict(mode=N.TAB_CELLS, n=(n0, n1), lo=klo, hi=khi, lat_lo=0)
     elif fam in (N.FAM_QGAUSS, N.FAM_QLOGGAUSS) and post.q and post.q > 0 and lp.inject is None:
@@ -323,7 +332,15 @@ class Engine(object):
         for lp, pl, info in zip(problems, plans, rows):
             info['tab_mode'], info['tab_off'], info['tab_n'] = pl['mode'], [0, 0], [0, 0]
             info['tab_lo'], info['tab_inv'], info['lat_lo'] = [0.0, 0.0], [0.0, 0.0], 0
-            if pl['mode'] == N.TAB_CELLS:
+            if pl['mode'] == N.TAB_CELLS and pl.get('logpoly'):
+                n = pl['n'][0]                  # one table, both sides' polynomials in each row
+                info['flags'] = info['flags'] | N.F_LOGPOLY
+                for sd in range(2):
+                    info['tab_off'][sd], info['tab_n'][sd] = units, n
+                    info['tab_lo'][sd] = float(np.float32(pl['lo']))
+                    info['tab_inv'][sd] = float(np.float32(n / (pl['hi'] - pl['lo'])))
+                units += N.TAB_ROW_UNITS * n
+            elif pl['mode'] == N.TAB_CELLS:
                 for sd in range(2):
                     n = pl['n'][sd]
                     info['tab_off'][sd], info['tab_n'][sd] = units, n
@@ -340,9 +357,13 @@ class Engine(object):
                         side = 'above' if sd else 'below'
                         geo = (info[side + '_off'], info[side + '_len'], info.get('wide_off', 0) if sd else 0,
                                info.get('wide_len', 0) if sd else 0, info['tab_lo'][sd], info['tab_inv'][sd])
-                    jobs.append((r0, sd, pl['mode'], info['tab_n'][sd], info['tab_off'][sd], blocks) + geo)
+                    kind = N.TAB_LOGPOLY if pl.get('logpoly') else pl['mode']
+                    jobs.append((r0, sd, kind, info['tab_n'][sd], info['tab_off'][sd], blocks) + geo)
                     n = info['tab_n'][sd]        # cells: TAB_PER_BLOCK rows a block; lattice: a block a value
-                    blocks += -(-n // N.TAB_PER_BLOCK) if pl['mode'] == N.TAB_CELLS else n
+                    if kind == N.TAB_LOGPOLY and geo[1] >= 0 and geo[1] + geo[3] <= LP_DIRECT_ROWS:
+                        blocks += -(-n // (LP_ROWS_PER_WAVE * N.TAB_PER_BLOCK))    # (a short side: direct sums)
+                    else:
+                        blocks += -(-n // N.TAB_PER_BLOCK) if pl['mode'] == N.TAB_CELLS else n
             r0 += len(lp.ids)
         tj = np.zeros(len(jobs), dtype=N.TAB_JOB_DTYPE)
         for c, f in enumerate(N.TAB_JOB_DTYPE.names):

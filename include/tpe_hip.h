@@ -74,9 +74,12 @@ enum {
                           flagged: every natively fitted label with enough observations */
   TPE_F_FGT = 64,      /* tpe_problem (set by the packer): a device-fitted TPE_TAB_CELLS label whose
                           above cells are built from Hermite box moments (see "Box moments") */
-  TPE_F_REMOTE = 128   /* tpe_tree_label: another rank evaluates this label (hyperparameter-axis
+  TPE_F_REMOTE = 128,  /* tpe_tree_label: another rank evaluates this label (hyperparameter-axis
                           shard, see "Shard axes"): it is neither fitted nor run here; its values
                           are NaN and its activity is the tree's.  Not allowed on a gate. */
+  TPE_F_LOGPOLY = 256  /* tpe_problem (set by the packer): a TPE_TAB_CELLS label whose table holds
+                          log-polynomial rows of both sides on one cell grid (see "Tabulated
+                          scoring"; its two table jobs have kind TPE_TAB_LOGPOLY) */
 };
 
 /* box moments (see "Box moments" below): Hermite terms per box, 16-B units per box record */
@@ -87,7 +90,9 @@ enum {
 enum {
   TPE_TAB_NONE = 0,     /* scored by the above / finalize stages (per candidate)                  */
   TPE_TAB_CELLS = 1,    /* continuous f32: per-cell Taylor moment tables of both mixtures          */
-  TPE_TAB_LATTICE = 2   /* quantized: exact {l, g} per lattice value of the candidate range        */
+  TPE_TAB_LATTICE = 2,  /* quantized: exact {l, g} per lattice value of the candidate range        */
+  TPE_TAB_LOGPOLY = 3   /* tpe_tab_job kind of a TPE_F_LOGPOLY label's sides (problems keep
+                           TPE_TAB_CELLS)                                                         */
 };
 
 /* tpe_batch.flags / tpe_level_run flags */
@@ -181,6 +186,16 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  *     w = 1 / tab_inv, all in f32 (the table and the sample stages compute them
  *     alike).  m = NaN (a significant term too narrow to expand) and t outside
  *     the cells fall back to the exact sum.
+ *     TPE_F_LOGPOLY (both sides fit the sample stage's LDS on one grid: the
+ *     finer side's cells for both): one table of 48-B rows, row j = {b_0..b_5,
+ *     a_0..a_5}: the degree-5 polynomials in u of log2 s_below(t) and log2
+ *     s_above(t) (shift included) on cell j — the table stage evaluates each
+ *     side's moment series in f64 at the 6 Chebyshev nodes of [-1, 1],
+ *     interpolates, and checks the polynomial at u = 0, +-1/2, +-1 against the
+ *     series (|error| <= 1e-7 (1 + |log2 s|)); a side that fails, or whose
+ *     cell is flagged, gets b_0 (a_0) = NaN and its candidates the exact sum.
+ *     One row, two degree-5 Horner sums and no log2 per candidate instead of
+ *     two rows, two degree-10 sums and two log2.
  *   TPE_TAB_LATTICE (families 2/3): every candidate is x = m q (np.round,
  *     tpe.py:90-93, 248-249); row m - lat_lo of the table (tab_n[0] rows of
  *     double2 {l, g}, float64, reference operation order per component) holds

@@ -459,6 +459,7 @@ def test_box_moment_tables_match_direct_tables(engine, monkeypatch, case):
     lpdf = O.lgmm1_lpdf if logf else O.gmm1_lpdf
     C = 1 << 16
     monkeypatch.setenv('TPE_TAB_DEVFIT_RATIO', '1')
+    monkeypatch.setenv('TPE_LOGPOLY', '0')          # direct cells: moment rows, as the boxes give
     out = {}
     for fgt in ('1', '0'):
         monkeypatch.setenv('TPE_FGT', fgt)
@@ -551,18 +552,24 @@ def test_local_expansion_matches_exact_and_is_used(engine, monkeypatch):
                                        ('qloguniform', dict(low=0.0, high=5.0, q=2.0)),
                                        ('qnormal', dict(mu=2.0, sigma=4.0, q=0.5)),
                                        ('qlognormal', dict(mu=1.0, sigma=0.7, q=0.25))])
-def test_tabulated_scoring_matches_oracle(engine, dist, args):
-    """Tabulated scoring (cells: Taylor moments per value cell, fp32; lattice:
-    exact {l, g} per quantized value, fp64) on device draws against the
-    oracle's lpdf, the argmax inside the oracle's eps-tie set, the table mode
-    actually taken, and the result equal to the per-candidate path's up to
-    the tolerance."""
+@pytest.mark.parametrize('logpoly', ['1', '0'])
+def test_tabulated_scoring_matches_oracle(engine, dist, args, logpoly, monkeypatch):
+    """Tabulated scoring (cells: Taylor moments per value cell — or, the
+    default where both sides fit one grid, the log-polynomial rows built from
+    them (TPE_F_LOGPOLY; TPE_LOGPOLY=0: moment rows) — fp32; lattice: exact
+    {l, g} per quantized value, fp64) on device draws against the oracle's
+    lpdf, the argmax inside the oracle's eps-tie set, the table mode actually
+    taken, and the result equal to the per-candidate path's up to the
+    tolerance."""
     import os
     from hyperopt_amd import _native as N
     from hyperopt_amd import parzen
     from hyperopt_amd.engine import LevelProblem
     rs = np.random.RandomState(61)
     q = args.get('q')
+    if q and logpoly == '0':
+        pytest.skip('lattice tables have no log-polynomial variant')
+    monkeypatch.setenv('TPE_LOGPOLY', logpoly)
     log = dist.startswith('log') or dist.startswith('qlog')
     lo, hi = (args['low'], args['high']) if 'low' in args else (args['mu'] - 3 * args['sigma'],
                                                                args['mu'] + 3 * args['sigma'])
@@ -575,6 +582,12 @@ def test_tabulated_scoring_matches_oracle(engine, dist, args):
     res, cand, l, g = engine.run([LevelProblem(post, 5, [11])], C, seed=13, want_lg=True, return_cand=True)
     prob, _ = engine.device_tables()
     assert prob[0]['tab_mode'] == (N.TAB_LATTICE if q else N.TAB_CELLS), dist
+    if not q:                                          # (log-polynomial rows: both sides on one grid <= 2048 cells)
+        lpf = bool(prob[0]['flags'] & N.F_LOGPOLY)
+        assert lpf == (logpoly == '1' and max(prob[0]['tab_n']) <= 2048) or (lpf and logpoly == '1'), \
+            (dist, prob[0]['tab_n'])
+        if lpf:
+            assert prob[0]['tab_n'][0] == prob[0]['tab_n'][1] <= 2048, (dist, prob[0]['tab_n'])
     tol = 1e-9 if q else 1e-5
     lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
     kw = dict(low=post.low, high=post.high, q=q)
