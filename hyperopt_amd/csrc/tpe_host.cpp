@@ -157,17 +157,41 @@ inline double np_min(double a, double b) { return (a != a || b != b) ? NAN : (a 
 // erf(z) bit for bit: libm's erf is exactly +-1 from |z| = 6 on (erfc(6) < 2^-55),
 // so the (common) far-from-the-bound components skip the call
 inline double erf_fast(double z) { return fabs(z) >= 6.0 ? copysign(1.0, z) : erf(z); }
+// erfc(x) bit for bit: libm's erfc is exactly 2 from x = -6 down and exactly 0
+// from x = 27.3 up (checked over fine grids of both ranges), so the sampler
+// rows of components far from a bound skip the call
+inline double erfc_fast(double x) { return x <= -6.0 ? 2.0 : (x >= 27.3 ? 0.0 : erfc(x)); }
 
 double normal_cdf(double x, double mu, double sigma) {   // tpe.py:96-101
   const double bottom = np_max(sqrt(2.0) * sigma, kEPS);
   return 0.5 * (1 + erf_fast((x - mu) / bottom));
 }
 
+// sum_k w_k (Phi_k(hi) - Phi_k(lo)) (tpe.py:130-136): the standardised bounds
+// in one vectorisable pass, libm's erf only where it is not exactly +-1 (a
+// component within 6 sqrt2 sigma of a bound); the same values as normal_cdf
+__attribute__((target_clones("avx512f", "avx2", "default")))
 double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi) {
   if (!bounded) return 1.0;
-  std::vector<double> t((size_t)k);
-  for (int64_t i = 0; i < k; ++i) t[i] = w[i] * (normal_cdf(hi, mu[i], sg[i]) - normal_cdf(lo, mu[i], sg[i]));
-  return np_sum(t.data(), k);
+  static thread_local std::vector<double> zl_tl, zh_tl;
+  std::vector<double>& zl = zl_tl;
+  std::vector<double>& zh = zh_tl;
+  zl.resize((size_t)k);
+  zh.resize((size_t)k);
+  double* __restrict__ a = zl.data();
+  double* __restrict__ b = zh.data();
+  const double s2 = sqrt(2.0);
+  for (int64_t i = 0; i < k; ++i) {
+    const double t = s2 * sg[i];
+    const double bottom = t != t ? t : (t > kEPS ? t : kEPS);       // np_max(sqrt2 sigma, EPS)
+    a[i] = (lo - mu[i]) / bottom;
+    b[i] = (hi - mu[i]) / bottom;
+  }
+  for (int64_t i = 0; i < k; ++i) {
+    const double eh = erf_fast(b[i]), el = erf_fast(a[i]);
+    a[i] = w[i] * (0.5 * (1 + eh) - 0.5 * (1 + el));
+  }
+  return np_sum(a, k);
 }
 
 // log2 of a positive normal double: exponent bits + atanh series of the
@@ -389,8 +413,8 @@ void fill_label(const FillCtx& cx, int32_t li) {
       if (bounded) { za = (L.low - L.below_mu[i]) / L.below_sigma[i]; zb = (L.high - L.below_mu[i]) / L.below_sigma[i]; }
       const bool fl = za > 0;
       const double a = fl ? -zb : za, b = fl ? -za : zb;
-      fa[i] = 0.5 * erfc(-a / sqrt(2.0));
-      fb[i] = 0.5 * erfc(-b / sqrt(2.0));
+      fa[i] = 0.5 * erfc_fast(-a / sqrt(2.0));
+      fb[i] = 0.5 * erfc_fast(-b / sqrt(2.0));
       flip[i] = fl ? 1.0 : 0.0;
       sel[i] = bounded ? L.below_w[i] * std::max(fb[i] - fa[i], 0.0) : L.below_w[i];
       any = any || sel[i] > 0;

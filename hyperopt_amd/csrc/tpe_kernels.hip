@@ -3197,6 +3197,82 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
   }
 }
 
+// ============================================================ shard combine on the device
+// A candidate-sharded level (tpe_suggest_tree over RCCL, include/tpe_hip.h
+// "Candidate-shard exchange") combined without a host round trip: the
+// early-selection run records (device memory) reduced per problem straight
+// into this rank's exchange slot, an in-place ncclAllGather, and k_combine
+// reducing the ranks' records per problem (np.argmax order: NaN, score, lowest
+// global index, tpe.py:749-759) into the host-visible results, the worst
+// status beside them — one stream synchronise per level.
+constexpr int kCombThreads = 256;
+
+// (host-written pinned memory: system-scope loads, as k_upload)
+__device__ __forceinline__ int32_t sys_load_i32(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// one wave per problem: span[2p] = the list position of its first tabulated
+// tile, span[2p + 1] = its tabulated tiles (0: its result is res_dev[p]); a
+// run starts at the problem's first position and at every multiple of `per`
+// (the sample stage's workgroup partition); list = NULL: the identity
+__global__ __launch_bounds__(kCombThreads) void k_runs_reduce(const int32_t* __restrict__ span,
+                                                               const int32_t* __restrict__ list, int per,
+                                                               const tpe_result* __restrict__ run_best,
+                                                               const tpe_result* __restrict__ res_dev, int64_t P,
+                                                               unsigned char* __restrict__ slot, int32_t status) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<int32_t*>(slot) = status;
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * (kCombThreads / 64) + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const int32_t a = sys_load_i32(span + 2 * p), n = sys_load_i32(span + 2 * p + 1);
+  tpe_result* dst = reinterpret_cast<tpe_result*>(slot + TPE_EXCHANGE_HEADER) + p;
+  if (n == 0) {
+    if (lane == 0) *dst = res_dev[p];
+    return;
+  }
+  double bs = 0.0;
+  int64_t bi = -1;
+  int bt = -1;                                     // the best run's tile
+  for (int k = lane; k < n; k += 64) {
+    const int pos = a + k;
+    if (k != 0 && pos % per != 0) continue;        // not a run's first tile
+    const int t = list ? list[pos] : pos;
+    const tpe_result c = run_best[t];
+    if (better(c.score, c.idx, bs, bi)) { bs = c.score; bi = c.idx; bt = t; }
+  }
+  for (int off = 32; off > 0; off >>= 1) {         // (np.argmax order: unique indices, any order of reduction)
+    const double os = __shfl_xor(bs, off);
+    const int64_t oi = __shfl_xor(bi, off);
+    const int ot = __shfl_xor(bt, off);
+    if (better(os, oi, bs, bi)) { bs = os; bi = oi; bt = ot; }
+  }
+  if (lane == 0) *dst = bt >= 0 ? run_best[bt] : tpe_result{0, 0, 0, 0, -1, -1};
+}
+
+__global__ __launch_bounds__(kCombThreads) void k_combine(const unsigned char* __restrict__ all, int W, int64_t per,
+                                                           int64_t P, tpe_result* __restrict__ out,
+                                                           int32_t* __restrict__ status) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int32_t worst = TPE_OK;                        // a hard error outranks a workspace retry
+    for (int r = 0; r < W; ++r) {
+      const int32_t st = *reinterpret_cast<const int32_t*>(all + (int64_t)r * per);
+      if (st != TPE_OK && (worst == TPE_OK || worst == TPE_E_SPACE)) worst = st;
+    }
+    *status = worst;
+  }
+  const int64_t p = (int64_t)blockIdx.x * kCombThreads + threadIdx.x;
+  if (p >= P) return;
+  auto rec = [&](int r) { return reinterpret_cast<const tpe_result*>(all + (int64_t)r * per + TPE_EXCHANGE_HEADER)[p]; };
+  tpe_result w = rec(0);
+  for (int r = 1; r < W; ++r) {                    // tpe_combine_results' order
+    const tpe_result c = rec(r);
+    if (c.idx < 0) continue;
+    if (w.idx < 0 || better(c.score, c.global_idx, w.score, w.global_idx)) w = c;
+  }
+  out[p] = w;
+}
+
 // ============================================================ level upload
 // The packed level (pinned host memory, device-addressable) copied into the
 // device blob by the compute queue itself: the first stage then follows in
@@ -4392,9 +4468,48 @@ static int profile_collect(const tpe_batch& b, const tpe_pack_info& info, const 
   return TPE_OK;
 }
 
+// the device exchange of a sharded level (tpe_internal_level_run_ex): the
+// exchange, the problems every rank runs, and where the outcome goes
+struct LevelEx {
+  const tpe_exchange* ex;
+  int64_t P;
+  int32_t* all_status;   // the worst status over the ranks
+  int32_t* done;         // 1: the exchange ran (out holds the global winners); 0: the caller exchanges
+};
+
+static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
+                          int64_t cand_base, int64_t n_cand_global, int32_t precision, int32_t flags,
+                          const tpe_level_ws* ws, tpe_level_need* need, void* stream, tpe_result* out,
+                          const LevelEx* lx);
+
 int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
                   int64_t n_cand_global, int32_t precision, int32_t flags, const tpe_level_ws* ws,
                   tpe_level_need* need, void* stream, tpe_result* out) {
+  return level_run_impl(labels, n_labels, n_cand, seed, cand_base, n_cand_global, precision, flags, ws, need, stream,
+                        out, nullptr);
+}
+
+// tpe_level_run of one rank of a candidate-sharded suggest with the RCCL
+// exchange done on the device (see k_runs_reduce / k_combine); *done = 0 when
+// the level could not take that path (nothing launched, no exchange made:
+// the caller exchanges on the host as before)
+__attribute__((visibility("hidden"))) int tpe_internal_level_run_ex(
+    const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed, int64_t cand_base,
+    int64_t n_cand_global, int32_t precision, int32_t flags, const tpe_level_ws* ws, tpe_level_need* need,
+    void* stream, tpe_result* out, const tpe_exchange* ex, int64_t P_expected, int32_t* all_status, int32_t* done) {
+  *done = 0;
+  const LevelEx lx{ex, P_expected, all_status, done};
+  return level_run_impl(labels, n_labels, n_cand, seed, cand_base, n_cand_global, precision, flags, ws, need, stream,
+                        out, &lx);
+}
+
+__attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_exchange* ex, int64_t per,
+                                                                 hipStream_t s);   // (after the RCCL loader)
+
+static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
+                          int64_t cand_base, int64_t n_cand_global, int32_t precision, int32_t flags,
+                          const tpe_level_ws* ws, tpe_level_need* need, void* stream, tpe_result* out,
+                          const LevelEx* lx) {
   if (!ws || !need || (n_labels > 0 && !out)) return fail(TPE_E_ARG, "null workspace/need/out");
   memset(need, 0, sizeof(*need));
   tpe_pack_info info;
@@ -4408,7 +4523,8 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
   const int64_t P = info.n_problems, C = P * (int64_t)n_cand;
   const int64_t res_off = (info.blob_bytes + 255) & ~(int64_t)255;
   // early selection's per-run bests follow the results (host-visible)
-  const int64_t rb_off = (res_off + P * (int64_t)sizeof(tpe_result) + 255) & ~(int64_t)255;
+  // (+ 64: the device exchange's status word between them)
+  const int64_t rb_off = (res_off + P * (int64_t)sizeof(tpe_result) + 64 + 255) & ~(int64_t)255;
   need->pinned_bytes = rb_off + (info.n_tab_jobs > 0 ? info.n_tiles * (int64_t)sizeof(tpe_result) : 0);
   need->blob_bytes = info.blob_bytes;
   need->cand = C;
@@ -4583,6 +4699,22 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     b.tab_fast = fast && n_rows > 0 ? 1 : 0;
   }
   b.result = rd ? rd : ws->result;
+  // device exchange (sharded level over RCCL): run records and results in
+  // device scratch after the exchange slots, combined on the device
+  const int64_t xper = TPE_EXCHANGE_HEADER + P * (int64_t)sizeof(tpe_result);
+  unsigned char* xrun = nullptr;
+  bool dex = false;
+  if (lx && lx->ex && lx->ex->comm && dbase && b.early_select && lx->P == P) {
+    const int64_t base = ((int64_t)lx->ex->world * xper + 255) & ~(int64_t)255;
+    const int64_t need_x = base + (info.n_tiles + P) * (int64_t)sizeof(tpe_result);
+    const int64_t runs_bytes = 2 * P * (int64_t)sizeof(int32_t);
+    if (lx->ex->dev && lx->ex->dev_bytes >= need_x && runs_bytes <= info.n_tiles * (int64_t)sizeof(tpe_result)) {
+      dex = true;
+      xrun = (unsigned char*)lx->ex->dev + base;
+      b.run_best = (tpe_result*)xrun;
+      b.result = (tpe_result*)(xrun + info.n_tiles * (int64_t)sizeof(tpe_result));
+    }
+  }
   if (info.n_fit > 0) {
     b.fit = (const tpe_fit_job*)(dev + info.off_fit);
     b.n_fit = info.n_fit;
@@ -4598,6 +4730,45 @@ int tpe_level_run(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, 
     if ((rc = check_batch(&b)) || (rc = run_batch_profiled(&b, stream))) return rc;
   } else if ((rc = tpe_run_batch(&b, stream))) {
     return rc;
+  }
+  if (dex) {
+    // each problem's span of the tabulated tile list (host-visible: the
+    // run-record area is free in this mode): its runs are enumerated on the
+    // device as the host reduction below enumerates them
+    int32_t* span = (int32_t*)(host + rb_off);
+    const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab);
+    if (xtmpl) {                                     // expanded: every problem's tiles, in order
+      for (int64_t r = 0; r < P; ++r) { span[2 * r] = (int32_t)(r * n_tiles_p); span[2 * r + 1] = (int32_t)n_tiles_p; }
+    } else {
+      for (int64_t r = 0; r < P; ++r) span[2 * r] = span[2 * r + 1] = 0;
+      const int32_t* list = (const int32_t*)(host + info.off_tab_tiles);
+      const tpe_tile* tl = (const tpe_tile*)(host + info.off_tiles);
+      for (int i = 0; i < n_tab; ++i) {
+        const int pr = tl[list[i]].problem;
+        if (span[2 * pr + 1]++ == 0) span[2 * pr] = i;
+      }
+    }
+    const int32_t* d_span = (const int32_t*)(dbase + rb_off);
+    const unsigned int blocks = (unsigned int)((P + kCombThreads / 64 - 1) / (kCombThreads / 64));
+    unsigned char* slot = (unsigned char*)lx->ex->dev + (int64_t)lx->ex->rank * xper;
+    TPE_LAUNCH(k_runs_reduce, dim3(blocks), dim3(kCombThreads), 0, s, d_span, xtmpl ? nullptr : b.tab_tiles, per,
+               (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK);
+    if ((rc = hip_check("k_runs_reduce"))) return rc;
+    if ((rc = rccl_allgather_inplace(lx->ex, xper, s))) return rc;
+    int32_t* st_host = (int32_t*)(host + res_off + P * (int64_t)sizeof(tpe_result));   // (the pad before rb_off)
+    int32_t* st_dev = (int32_t*)(dbase + res_off + P * (int64_t)sizeof(tpe_result));
+    TPE_LAUNCH(k_combine, dim3(blocks), dim3(kCombThreads), 0, s, (const unsigned char*)lx->ex->dev,
+               lx->ex->world, xper, P, rd, st_dev);
+    if ((rc = hip_check("k_combine"))) return rc;
+    tpe_internal_phase(TPE_PHASE_LAUNCHED);
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    tpe_internal_phase(TPE_PHASE_SYNCED);
+    memcpy(out, rh, (size_t)P * sizeof(tpe_result));
+    *lx->all_status = *(volatile int32_t*)st_host;
+    *lx->done = 1;
+    tpe_internal_phase(TPE_PHASE_LEVEL);
+    return g_prof.on ? profile_collect(b, info, xtmpl ? xtmpl : hp, xfirst, n_cand) : TPE_OK;
   }
   e = rd ? hipSuccess : hipMemcpyAsync(rh, ws->result, (size_t)P * sizeof(tpe_result), hipMemcpyDeviceToHost, s);
   tpe_internal_phase(TPE_PHASE_LAUNCHED);
@@ -4679,7 +4850,18 @@ int rccl_fail(const char* what, ncclResult_t e) {
 }
 }  // namespace
 
+
+
 extern "C" {
+
+// every rank's `per` bytes at its slot of ex->dev gathered in place on stream s
+__attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_exchange* ex, int64_t per, hipStream_t s) {
+  Rccl& r = rccl();
+  if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
+  unsigned char* d = (unsigned char*)ex->dev;
+  const ncclResult_t ne = r.all_gather(d + (size_t)per * ex->rank, d, (size_t)per, ncclUint8, (ncclComm_t)ex->comm, s);
+  return ne == ncclSuccess ? TPE_OK : rccl_fail("ncclAllGather", ne);
+}
 
 int tpe_comm_unique_id(void* id) {
   if (!id) return fail(TPE_E_ARG, "tpe_comm_unique_id: null id");

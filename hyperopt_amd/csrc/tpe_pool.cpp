@@ -9,6 +9,7 @@
 #include "tpe_pool.h"
 
 #include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -124,8 +125,12 @@ int total_threads() {            // under g_mu
   if (g_threads < 0) {
     static bool atfork = [] { return pthread_atfork(nullptr, nullptr, after_fork_child) == 0; }();
     (void)atfork;
-    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    g_threads = std::min({env_int("TPE_HOST_THREADS", 4), hw, kMaxThreads});
+    int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;                       // (the CPUs this process may run on, when restricted)
+    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) hw = std::min(hw, (int)CPU_COUNT(&set));
+    // (16: a GPU's share of the host's CPUs; the large levels of configs 4 and 5
+    // fit and pack their labels on them, a 4-label suggest uses what it needs)
+    g_threads = std::min({env_int("TPE_HOST_THREADS", 16), hw, kMaxThreads});
   }
   return g_threads;
 }

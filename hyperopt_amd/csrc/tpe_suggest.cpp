@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -26,6 +27,11 @@
 extern "C" int tpe_internal_fail(int code, const char* what);   // tpe_kernels.hip (hidden)
 extern "C" int tpe_internal_exchange(const tpe_exchange* ex, void* stream, int32_t my_status, tpe_result* res,
                                      int64_t P, int32_t* status);     // tpe_kernels.hip (hidden)
+extern "C" int tpe_internal_level_run_ex(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
+                                         int64_t cand_base, int64_t n_cand_global, int32_t precision, int32_t flags,
+                                         const tpe_level_ws* ws, tpe_level_need* need, void* stream, tpe_result* out,
+                                         const tpe_exchange* ex, int64_t P_expected, int32_t* all_status,
+                                         int32_t* done);              // tpe_kernels.hip (hidden)
 
 namespace {
 
@@ -38,6 +44,12 @@ void phase_start() {
   if (!g_ph_on.load(std::memory_order_relaxed)) return;
   g_ph_t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < TPE_N_PHASES; ++i) g_ph[i] = -1.0;
+}
+
+// TPE_DEVICE_COMBINE=0: sharded levels exchange through the host (A/B)
+bool device_combine() {
+  static const bool on = [] { const char* e = getenv("TPE_DEVICE_COMBINE"); return !(e && e[0] == '0'); }();
+  return on;
 }
 
 constexpr int kInactive = -2;   // label not active (None)
@@ -411,6 +423,29 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     for (int32_t r = 0; r < n_recs; ++r) P += recs[(size_t)r].n_ids;
     res.resize((size_t)std::max<int64_t>(P, 1));
     ++path[1];
+    if (exchange && ex->comm && device_combine()) {
+      // RCCL: the level's runs reduced, gathered and combined on the device, one
+      // stream synchronise (falls back to the host exchange below when the level
+      // cannot take that path: then nothing was launched or exchanged)
+      int32_t all_rc = TPE_OK, done = 0;
+      const int rc = tpe_internal_level_run_ex(recs.data(), n_recs, n_cand, seed, cand_base, n_cand_global, TPE_PREC_F32,
+                                               run_flags, ws, need, stream, res.data(), ex, P, &all_rc, &done);
+      if (done) {
+        if (rc != TPE_OK) return rc;
+        if (all_rc == TPE_E_SPACE) return tpe_internal_fail(TPE_E_SPACE, "another rank needs a larger workspace");
+        if (all_rc != TPE_OK) return tpe_internal_fail(all_rc, "a level run failed on another rank");
+        return TPE_OK;
+      }
+      if (rc != TPE_OK)
+        for (int64_t q = 0; q < P; ++q) res[(size_t)q] = tpe_result{0, 0, 0, 0, -1, -1};
+      int32_t all2 = TPE_OK;
+      const int xrc = tpe_internal_exchange(ex, stream, rc, res.data(), P, &all2);
+      if (xrc != TPE_OK) return xrc;
+      if (rc != TPE_OK) return rc;
+      if (all2 == TPE_E_SPACE) return tpe_internal_fail(TPE_E_SPACE, "another rank needs a larger workspace");
+      if (all2 != TPE_OK) return tpe_internal_fail(all2, "a level run failed on another rank");
+      return TPE_OK;
+    }
     int rc = tpe_level_run(recs.data(), n_recs, n_cand, seed, cand_base, n_cand_global, TPE_PREC_F32, run_flags, ws,
                            need, stream, res.data());
     if (!exchange) return rc;

@@ -162,10 +162,17 @@ class _Exchange(object):
                                        dtype=torch.uint8, device=self.engine.device)
             self.ex.dev, self.ex.dev_bytes = self.scratch.data_ptr(), self.scratch.numel()
 
-    def ptr(self, max_problems):
-        """The struct for a suggest of at most ``max_problems`` problems per level."""
+    def ptr(self, max_problems, n_cand=0):
+        """The struct for a suggest of at most ``max_problems`` problems per
+        level and ``n_cand`` candidates per problem on this rank (RCCL: device
+        scratch for the exchange slots, and for the level's run records and
+        results that the device combine reduces: tpe_internal_level_run_ex)."""
         if self.comm is not None:
-            self._scratch(self.world * (N.EXCHANGE_HEADER + max(int(max_problems), 1) * N.RESULT_DTYPE.itemsize))
+            P = max(int(max_problems), 1)
+            rec = N.RESULT_DTYPE.itemsize
+            slots = (self.world * (N.EXCHANGE_HEADER + P * rec) + 255) // 256 * 256
+            tiles = P * (-(-max(int(n_cand), 1) // N.tile_size()))
+            self._scratch(slots + (tiles + P) * rec)
         return ctypes.byref(self.ex)
 
     def close(self):

@@ -714,7 +714,7 @@ class Engine(object):
             from .dist import shard_range
             base, hi = shard_range(n_cand, shard[0], shard[1])
             c_loc, c_glob = hi - base, n_cand
-            ex = exchange.ptr(nl * n)
+            ex = exchange.ptr(nl * n, c_loc)
         for attempt in range(8):          # a later tree level may need larger pools than the first
             ws = self._level_ws()
             rc = self.lib.tpe_suggest_tree(labels_ptr, nl, io.below_ptr, nb, float(prior_weight), int(lf), io.ids_ptr,

@@ -817,7 +817,7 @@ int tpe_suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const int64
                      int32_t* path, int8_t* need_fit);
 
 /* Host worker threads of the native runtime, the calling thread included
- * (default: TPE_HOST_THREADS, else 4; at most 16).  tpe_suggest_tree fits the
+ * (default: TPE_HOST_THREADS, else 16 — at most the host's CPUs; at most 16).  tpe_suggest_tree fits the
  * labels of a suggest on them in parallel (each label's fit is the same
  * single-threaded computation wherever it runs, so results do not depend on
  * the count).  n <= 1: everything on the calling thread; n < 0: query only.

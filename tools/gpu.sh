@@ -106,7 +106,7 @@ for task in "$@"; do
       step 300 $O/hostprof_${TAG}.txt python tools/host_prof.py ${STEPS:-300}
       head -60 $O/hostprof_${TAG}.txt ;;
     nativesplit)
-      step 300 $O/nativesplit_${TAG}.txt python tools/native_split.py ${STEPS:-200}
+      step 300 $O/nativesplit_${TAG}.txt python tools/native_split.py ${STEPS:-200} ${NS_ARGS:-}
       cat $O/nativesplit_${TAG}.txt ;;
     hostsplit)
       step 300 $O/hostsplit_${TAG}.txt python tools/host_split.py ${STEPS:-200}

@@ -107,6 +107,61 @@ def main():
     eng.profile = None
     for k, v in prof.items():
         print('  device stage %-10s %7.1f us' % (k, 1e3 * np.median([a[0] for a in v])))
+    if '--exchange' in sys.argv:
+        exchange_overhead(eng, lib, arr, below, ids, C, reps, sug)
+
+
+def exchange_overhead(eng, lib, arr, below, ids, C, reps, sug):
+    """The candidate-shard exchange forced on a one-rank RCCL group (the
+    device combine: run records reduced, all-gathered and combined on the
+    device, one synchronise per level) against the plain call, alternating."""
+    import torch.distributed as dist
+    from hyperopt_amd import dist as D
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29533')
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
+    ex = D.exchange_for(eng, always=True)
+
+    def sug_x():
+        eng.suggest_tree(arr, below, 1.0, 25, ids, C, 5, tpe.SPECULATE_MIN_DRAWS, shard=(0, 1), exchange=ex)
+    for _ in range(20):
+        sug_x()
+    a, b = [], []
+    for i in range(reps):
+        t0 = time.perf_counter()
+        sug()
+        a.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        sug_x()
+        b.append(time.perf_counter() - t0)
+    mode = 'host' if os.environ.get('TPE_DEVICE_COMBINE', '1') == '0' else 'device'
+    print('  exchange forced (RCCL, world 1, %s combine): p50 %7.1f us vs plain %7.1f us: +%.1f us'
+          % (mode, 1e6 * np.median(b), 1e6 * np.median(a), 1e6 * (np.median(b) - np.median(a))))
+    # RCCL's own latency: one small in-place all-gather on the stream, synchronised
+    t = torch.zeros(256, dtype=torch.uint8, device='cuda')
+    out = torch.empty(256, dtype=torch.uint8, device='cuda')
+    lat = []
+    for i in range(50):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.all_gather_into_tensor(out, t)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    print('  torch.distributed all_gather_into_tensor (256 B, world 1, synchronised): p50 %.1f us' %
+          (1e6 * np.median(lat)))
+    ph = []
+    buf = (ctypes.c_double * len(N.PHASES))()
+    lib.tpe_host_phases(1, None, 0)
+    for i in range(reps):
+        sug_x()
+        lib.tpe_host_phases(1, buf, len(N.PHASES))
+        ph.append(list(buf))
+    lib.tpe_host_phases(0, None, 0)
+    med = np.median(np.array(ph), axis=0)
+    print('  exchange host phases (median us since entry): ' +
+          '  '.join('%s %.1f' % (k, v) for k, v in zip(N.PHASES, med)))
+    ex.close()
+    dist.destroy_process_group()
 
 
 if __name__ == '__main__':
