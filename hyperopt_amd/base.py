@@ -91,6 +91,221 @@ def spec_from_misc(misc):
     return spec
 
 
+def _logging(base_cls, name, hook):
+    """``base_cls.name`` calling ``self.<hook>()`` first."""
+    f = getattr(base_cls, name)
+
+    def g(self, *a, **kw):
+        getattr(self, hook)()
+        return f(self, *a, **kw)
+    g.__name__ = name
+    return g
+
+
+class _Doc(dict):
+    """A trial document held by a ``Trials``: a dict whose in-place edits —
+    at any depth through the dicts and lists it holds — put it in the
+    mutation log of each Trials holding it (``Trials._mutated``, id ->
+    document).  The SoA history cache (history.py) reads that log, so an edit
+    of a completed document it has already consumed rebuilds the cache
+    instead of serving a stale history (the reference re-reads every
+    document, tpe.py:820-842).  Values assigned into a tracked document are
+    stored as tracked copies; pickles and deep copies are plain dicts (a
+    Trials re-tracks its documents when unpickled)."""
+    __slots__ = ('_ts',)
+
+    def _log(self):
+        for t in getattr(self, '_ts', ()):
+            t[id(self)] = self
+
+    def __reduce_ex__(self, protocol):
+        return dict, (dict(self),)
+
+    def __setitem__(self, k, v):
+        dict.__setitem__(self, k, _wrap(v, self))
+        if k not in _UNTRACKED_KEYS:
+            self._log()
+
+    def __delitem__(self, k):
+        dict.__delitem__(self, k)
+        self._log()
+
+    def update(self, *a, **kw):
+        for k, v in dict(*a, **kw).items():
+            self[k] = v
+
+    def setdefault(self, k, v=None):
+        if k not in self:
+            self[k] = v
+        return dict.__getitem__(self, k)
+
+    def pop(self, *a):
+        self._log()
+        return dict.pop(self, *a)
+
+    def popitem(self):
+        self._log()
+        return dict.popitem(self)
+
+    def clear(self):
+        self._log()
+        dict.clear(self)
+
+    def __ior__(self, other):
+        self.update(other)
+        return self
+
+
+# bookkeeping keys FMinIter / workers write that no history reads
+_UNTRACKED_KEYS = frozenset(('owner', 'book_time', 'refresh_time', 'version'))
+
+
+class _Part(dict):
+    """A dict inside a tracked document (``result``, ``misc``, ``misc['vals']`` …)."""
+    __slots__ = ('_root',)
+
+    def _log(self):
+        self._root._log()
+
+    def __reduce_ex__(self, protocol):
+        return dict, (dict(self),)
+
+    def __setitem__(self, k, v):
+        dict.__setitem__(self, k, _wrap(v, self._root))
+        self._log()
+
+    def __delitem__(self, k):
+        dict.__delitem__(self, k)
+        self._log()
+
+    update, setdefault, pop, popitem, clear, __ior__ = (
+        _Doc.update, _Doc.setdefault, _Doc.pop, _Doc.popitem, _Doc.clear, _Doc.__ior__)
+
+
+class _PartList(list):
+    """A list inside a tracked document (``misc['vals'][label]`` …)."""
+    __slots__ = ('_root',)
+
+    def _log(self):
+        self._root._log()
+
+    def __reduce_ex__(self, protocol):
+        return list, (list(self),)
+
+    def __setitem__(self, i, v):
+        r = self._root
+        list.__setitem__(self, i, [_wrap(x, r) for x in v] if isinstance(i, slice) else _wrap(v, r))
+        self._log()
+
+    def __delitem__(self, i):
+        list.__delitem__(self, i)
+        self._log()
+
+    def append(self, v):
+        list.append(self, _wrap(v, self._root))
+        self._log()
+
+    def extend(self, vs):
+        list.extend(self, [_wrap(v, self._root) for v in vs])
+        self._log()
+
+    def insert(self, i, v):
+        list.insert(self, i, _wrap(v, self._root))
+        self._log()
+
+    def __iadd__(self, vs):
+        self.extend(vs)
+        return self
+
+    def __imul__(self, n):
+        list.__imul__(self, n)
+        self._log()
+        return self
+
+    pop, remove, clear, sort, reverse = (_logging(list, n, '_log')
+                                         for n in ('pop', 'remove', 'clear', 'sort', 'reverse'))
+
+
+# value types stored as they are (checked first: most values in a document)
+_PLAIN = frozenset((float, int, str, bool, type(None), np.float64, np.int64, np.float32, np.int32,
+                    np.bool_, datetime.datetime))
+
+
+def _wrap(v, root):
+    """``v`` as part of the tracked document ``root`` (dicts and lists copied
+    into tracked ones at any depth; everything else stored as it is)."""
+    t = type(v)
+    if t in _PLAIN:
+        return v
+    if isinstance(v, dict):
+        if t is _Part and v._root is root:
+            return v
+        p = _Part(v)
+        p._root = root
+        for k, x in v.items():
+            tx = type(x)
+            if tx in _PLAIN:
+                continue
+            if tx is list and len(x) <= 1 and (not x or type(x[0]) in _PLAIN):
+                q = _PartList(x)       # (misc['idxs'/'vals'] entries: inline)
+                q._root = root
+            else:
+                q = _wrap(x, root)
+            dict.__setitem__(p, k, q)
+        return p
+    if isinstance(v, list):
+        if t is _PartList and v._root is root:
+            return v
+        p = _PartList(v)
+        p._root = root
+        for i, x in enumerate(v):
+            if type(x) not in _PLAIN:
+                list.__setitem__(p, i, _wrap(x, root))
+        return p
+    return v
+
+
+def _track(doc, log):
+    """``doc`` as a document logging into ``log``: a tracked document gains
+    the log (it may belong to several Trials), anything else becomes a
+    tracked copy."""
+    if type(doc) is _Doc:
+        ts = getattr(doc, '_ts', None)
+        if ts is None:
+            doc._ts = [log]
+        elif not any(t is log for t in ts):
+            ts.append(log)
+        return doc
+    d = _Doc(doc)
+    for k, v in doc.items():
+        if type(v) not in _PLAIN:
+            dict.__setitem__(d, k, _wrap(v, d))
+    d._ts = [log]
+    return d
+
+
+def _tracked_by(doc, log):
+    return type(doc) is _Doc and any(t is log for t in getattr(doc, '_ts', ()))
+
+
+class _View(list):
+    """``Trials.trials``: a list whose edits other than appends (an element
+    replaced, removed, inserted or reordered) move the owner's ``_view_gen``,
+    as a refresh that changes the view does (history.py rebuilds on it)."""
+    __slots__ = ('_owner',)
+
+    def __reduce_ex__(self, protocol):
+        return list, (list(self),)
+
+    def _moved(self):
+        o = self._owner
+        o._view_gen = getattr(o, '_view_gen', 0) + 1
+
+    __setitem__, __delitem__, insert, pop, remove, clear, sort, reverse, __imul__ = (
+        _logging(list, n, '_moved') for n in ('__setitem__', '__delitem__', 'insert', 'pop', 'remove',
+                                              'clear', 'sort', 'reverse', '__imul__'))
+
+
 def coarse_utcnow():
     """utils.py:127-136: UTC now rounded down to milliseconds."""
     now = datetime.datetime.utcnow()
@@ -103,6 +318,7 @@ class Trials(object):
     def __init__(self, exp_key=None, refresh=True):
         self._ids = set()
         self._dynamic_trials = []
+        self._mutated = {}             # id -> tracked document edited in place (see _Doc)
         self._exp_key = exp_key
         self.attachments = {}
         if refresh:
@@ -112,7 +328,35 @@ class Trials(object):
     def __getstate__(self):
         d = dict(self.__dict__)
         d.pop('_tpe_history', None)
+        d.pop('_mutated', None)
         return d
+
+    def __setstate__(self, d):
+        # documents come back as plain dicts (_Doc.__reduce_ex__): tracked again,
+        # the view keeping its documents (the same objects as _dynamic_trials')
+        self.__dict__.update(d)
+        self._mutated = {}
+        new = {}
+        dyn = self._dynamic_trials
+        for i, tt in enumerate(dyn):
+            dyn[i] = new[id(tt)] = _track(tt, self._mutated)
+        old = self.__dict__.get('_trials')
+        if old is not None:
+            self._trials = self._view([new.get(id(tt)) or _track(tt, self._mutated) for tt in old])
+
+    def _view(self, docs):
+        v = _View(docs)
+        v._owner = self
+        return v
+
+    def _track_all(self):
+        """Track every document of _dynamic_trials in this Trials' log (a
+        document put there directly, a deep copy, another Trials' document)."""
+        log = self.__dict__.setdefault('_mutated', {})
+        dyn = self._dynamic_trials
+        for i, tt in enumerate(dyn):
+            if not _tracked_by(tt, log):
+                dyn[i] = _track(tt, log)
 
     def aname(self, trial, name):
         return 'ATTACH::%s::%s' % (trial['tid'], name)
@@ -150,13 +394,19 @@ class Trials(object):
         plus appended documents (a document dropped, replaced or reordered):
         derived caches of the view (history.py) rebuild when it moves."""
         old = getattr(self, '_trials', None)
-        if self._exp_key is None:
-            self._trials = [tt for tt in self._dynamic_trials if tt['state'] != JOB_STATE_ERROR]
-        else:
-            self._trials = [tt for tt in self._dynamic_trials
-                            if tt['state'] != JOB_STATE_ERROR and tt['exp_key'] == self._exp_key]
-        new = self._trials
-        if old is not None and not (len(new) >= len(old) and all(map(operator.is_, old, new))):
+        log = self.__dict__.setdefault('_mutated', {})
+        for attempt in (0, 1):
+            if self._exp_key is None:
+                new = [tt for tt in self._dynamic_trials if tt['state'] != JOB_STATE_ERROR]
+            else:
+                new = [tt for tt in self._dynamic_trials
+                       if tt['state'] != JOB_STATE_ERROR and tt['exp_key'] == self._exp_key]
+            appended = old is not None and len(new) >= len(old) and all(map(operator.is_, old, new))
+            if attempt or all(_tracked_by(tt, log) for tt in new[len(old) if appended else 0:]):
+                break
+            self._track_all()          # untracked documents (put in _dynamic_trials directly)
+        self._trials = self._view(new)
+        if old is not None and not appended:
             self._view_gen = getattr(self, '_view_gen', 0) + 1
         self._ids.update([tt['tid'] for tt in self._trials])
 
@@ -208,13 +458,23 @@ class Trials(object):
         return trial
 
     def _insert_trial_docs(self, docs):
+        """Appends ``docs`` as tracked documents (_Doc); a list passed in is
+        updated in place to hold them, so the caller's list keeps naming the
+        documents this Trials holds."""
+        log = self.__dict__.setdefault('_mutated', {})
         rval = [doc['tid'] for doc in docs]
-        self._dynamic_trials.extend(docs)
+        tracked = [_track(doc, log) for doc in docs]
+        if type(docs) is list:
+            docs[:] = tracked
+        self._dynamic_trials.extend(tracked)
         return rval
 
     def insert_trial_docs(self, docs):
-        docs = [self.assert_valid_trial(SONify(doc)) for doc in docs]
-        return self._insert_trial_docs(docs)
+        checked = [self.assert_valid_trial(SONify(doc)) for doc in docs]
+        rval = self._insert_trial_docs(checked)
+        if type(docs) is list:
+            docs[:] = checked
+        return rval
 
     def new_trial_ids(self, N):
         aa = len(self._ids)

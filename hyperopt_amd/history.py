@@ -12,11 +12,14 @@ Fast path requirements (else the generic reference-order walk is used):
 documents in increasing tid order, unique tids, no ``misc['from_tid']``,
 and ``Domain.loss`` not overridden.
 
-Completed documents are treated as immutable once seen, as FMinIter treats
-them; every change that goes through ``Trials`` (insert, refresh dropping or
-replacing documents) and every change to a pending document (values or
-loss) is picked up.  A completed document edited in place must be replaced
-in the Trials list (then ``refresh()``), not mutated.
+Staleness: ``Trials`` holds its documents as tracked dicts (base._Doc)
+whose in-place edits, at any depth, land in ``Trials._mutated``; a view edit
+that is not an append, or a refresh that changes the view, moves
+``Trials._view_gen``.  The cache rebuilds when a completed document it has
+consumed appears in the mutation log or the view generation moved; pending
+documents (values and loss) are re-read on every call.  So every edit the
+reference's per-call walk would see (tpe.py:820-842) is seen here, without a
+pass over the documents.
 """
 import bisect
 import weakref
@@ -153,6 +156,7 @@ class _Cache(object):
     def __init__(self, labels, categorical, gen=0):
         self.gen = gen                 # Trials._view_gen the cache was built against
         self.docs = []                 # document objects in list order
+        self.pos = {}                  # id(document) -> its position in docs
         self.tids = _Grow(np.int64)
         self.losses = _Grow(np.float64)
         self.pending = []              # positions whose loss may still change
@@ -175,7 +179,7 @@ class _Cache(object):
         self.changed = set(labels)     # labels whose column views are stale (obs_views)
         self._views = dict.fromkeys(labels)     # (label order)
 
-    def extend(self, docs, start):
+    def extend(self, docs, start, log):
         for i in range(start, len(docs)):
             d = docs[i]
             misc = d['misc']
@@ -186,6 +190,10 @@ class _Cache(object):
             if self.tids.n and tid <= self.tids.a[self.tids.n - 1]:
                 self.ok = False
                 return
+            if not base._tracked_by(d, log):
+                self.ok = False        # not a document of this Trials (edits would go unseen)
+                return
+            self.pos[id(d)] = len(self.docs)
             self.docs.append(d)
             self.tids.append(tid)
             loss = d['result'].get('loss')
@@ -413,18 +421,24 @@ def extract(domain, trials):
     gen = getattr(trials, '_view_gen', 0)
     if cache is not None and (cache.labels != labels or not cache.ok or cache.gen != gen):
         cache = None
+    log = getattr(trials, '_mutated', None)
     if cache is not None:
-        n = len(cache.docs)
-        # the cache follows an append-only view (FMinIter's use): completed
-        # documents stay where they are and keep their values.  A refresh that
-        # drops, replaces or reorders documents moves Trials._view_gen (above);
-        # a view list edited without a refresh shifts or changes the documents
-        # checked here — both ends and 7 evenly spaced positions; a pending
+        # the cache follows an append-only view (FMinIter's use).  A refresh or
+        # view edit that drops, replaces or reorders documents moves
+        # Trials._view_gen (above); an in-place edit of a completed document
+        # the cache has consumed is in the Trials' mutation log; a pending
         # document is re-read in full (its values and, below, its loss).
-        if n > len(docs) or (n and any(docs[i] is not cache.docs[i] for i in
-                                       {0, n - 1, n // 8, n // 4, 3 * n // 8, n // 2, 5 * n // 8, 3 * n // 4,
-                                        7 * n // 8})) or cache.pending_vals_changed():
+        if len(cache.docs) > len(docs) or cache.pending_vals_changed():
             cache = None
+        elif log:
+            pos, pend = cache.pos, set(cache.pending)
+            for k, doc in log.items():
+                p = pos.get(k)
+                if p is not None and p not in pend and cache.docs[p] is doc:
+                    cache = None
+                    break
+    if log:
+        log.clear()
     if cache is None:
         cache = _Cache(labels, {r.label: r.categorical for r in table.rows}, gen)
         start = 0
@@ -432,7 +446,7 @@ def extract(domain, trials):
         start = len(cache.docs)
         if start == len(docs) and not cache.pending and cache.hist is not None:
             return cache.hist             # nothing appended, no loss can change: the same view
-    cache.extend(docs, start)
+    cache.extend(docs, start, log)
     if not cache.ok:
         _CACHES.pop(trials, None)
         return _generic(domain, docs, table)

@@ -143,6 +143,76 @@ def test_history_cache_rebuilds_on_view_changes():
     assert history._CACHES[t] is cache and len(h5) == len(h4) + 1
 
 
+def test_history_cache_sees_in_place_edits_of_completed_documents():
+    """Completed documents the cache has consumed, edited in place at any
+    depth (values, loss, state), through a view edit without refresh, after
+    a pickle round trip, or through the caller's own inserted list: each
+    extract equals the reference walk (tpe.py:820-842); edits of bookkeeping
+    keys and of pending documents keep the cache."""
+    import copy
+    import pickle
+    d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1), 'c': H.hp.choice('c', [0, 1, 2])})
+    t = _done_trials(d, 300)
+    _same_as_walk(d, t)
+    cache = history._CACHES[t]
+    t.trials[150]['refresh_time'] = 1.0             # bookkeeping: no rebuild
+    _same_as_walk(d, t)
+    assert history._CACHES[t] is cache
+    t.trials[151]['misc']['vals']['x'][0] = 0.987654  # a value, two levels down
+    h = _same_as_walk(d, t)
+    assert 0.987654 in list(h.obs['x'][1]) and history._CACHES[t] is not cache
+    t.trials[77]['result']['loss'] = -5.0             # a loss
+    h = _same_as_walk(d, t)
+    assert -5.0 in list(h.losses)
+    t.trials[78]['result'] = {'status': 'ok', 'loss': -6.0}    # a new result dict, then edited
+    _same_as_walk(d, t)
+    t.trials[78]['result']['loss'] = -7.0
+    h = _same_as_walk(d, t)
+    assert -7.0 in list(h.losses) and -6.0 not in list(h.losses)
+    t.trials[79]['state'] = base.JOB_STATE_RUNNING    # back to pending, then its loss edited
+    _same_as_walk(d, t)
+    t.trials[79]['result']['loss'] = -8.0
+    h = _same_as_walk(d, t)
+    assert h.losses[79] == -8.0
+    k = 'c' if t.trials[80]['misc']['vals']['c'] else 'x'
+    del t.trials[80]['misc']['vals'][k][:]            # an observation removed
+    t.trials[80]['misc']['idxs'][k].clear()
+    _same_as_walk(d, t)
+    new = copy.deepcopy(t.trials[90])                 # the view edited without refresh
+    new['misc']['vals']['x'] = [0.5555]
+    t.trials[90] = new
+    h = _same_as_walk(d, t)
+    assert 0.5555 in list(h.obs['x'][1])
+    t._dynamic_trials[90] = t.trials[90]
+    t.refresh()                                       # a deep copy: tracked from the refresh on
+    _same_as_walk(d, t)
+    t.trials[90]['misc']['vals']['x'][0] = 0.6666
+    h = _same_as_walk(d, t)
+    assert 0.6666 in list(h.obs['x'][1])
+    t2 = pickle.loads(pickle.dumps(t))                 # a pickle round trip stays tracked
+    _same_as_walk(d, t2)
+    t2.trials[200]['misc']['vals']['x'] = [0.1234]
+    h = _same_as_walk(d, t2)
+    assert 0.1234 in list(h.obs['x'][1])
+    docs = rand.suggest([1000], d, t2, 9)             # the caller's list names the held documents
+    docs[0]['state'] = base.JOB_STATE_DONE
+    docs[0]['result'] = {'status': 'ok', 'loss': 0.5}
+    t2.insert_trial_docs(docs)
+    t2.refresh()
+    _same_as_walk(d, t2)
+    docs[0]['result']['loss'] = -9.0
+    h = _same_as_walk(d, t2)
+    assert h.losses[-1] == -9.0
+    plain = rand.suggest([1001], d, t2, 10)[0]
+    plain.update(state=base.JOB_STATE_DONE, result={'status': 'ok', 'loss': 0.5})
+    t2._dynamic_trials.append(plain)
+    t2.refresh()                                      # put in directly: tracked at refresh
+    _same_as_walk(d, t2)
+    t2.trials[-1]['result']['loss'] = -11.0
+    h = _same_as_walk(d, t2)
+    assert h.losses[-1] == -11.0
+
+
 def test_appended_documents_update_tree_records_in_place():
     """FMinIter's flow — one or a few finished documents appended before each
     suggest: the tree records updated in place (tpe._tree_refill), the merged
