@@ -22,6 +22,7 @@ reference's per-call walk would see (tpe.py:820-842) is seen here, without a
 pass over the documents.
 """
 import bisect
+import math
 import weakref
 
 import numpy as np
@@ -176,6 +177,7 @@ class _Cache(object):
         self.top_pos = []              # the same as lists (top is True: only the lists are current)
         self.top_keys = []             # ... and their losses
         self.hist = None               # History view of the current documents (no pending losses)
+        self.below_memo = None         # (top_n, n_below, below tids) of split_below
         self.changed = set(labels)     # labels whose column views are stale (obs_views)
         self._views = dict.fromkeys(labels)     # (label order)
 
@@ -333,7 +335,7 @@ class _Cache(object):
             for p in range(self.top_n, n):
                 v = float(L[p])
                 if v != v:
-                    self.top = None
+                    self.top = self.below_memo = None
                     return None
                 if len(pos) == self.TOP and v >= keys[-1]:
                     continue
@@ -351,7 +353,7 @@ class _Cache(object):
                 self.top = np.asarray(self.top_pos, dtype=np.int64)
             new = np.arange(self.top_n, n, dtype=np.int64)
             if np.isnan(L[new]).any():
-                self.top = None
+                self.top = self.below_memo = None
                 return None
             if len(new) > 4 * self.TOP:      # (re)build: every loss <= the TOP-th smallest
                 kth = np.partition(L[new], self.TOP - 1)[self.TOP - 1]
@@ -366,7 +368,7 @@ class _Cache(object):
     def refresh_pending(self):
         if not self.pending:
             return
-        self.top = None                # pending losses may change: rebuild the ranking
+        self.top = self.below_memo = None     # pending losses may change: rebuild the ranking
         keep = []
         L = self.losses.a
         for i in self.pending:
@@ -458,6 +460,20 @@ def extract(domain, trials):
     return hist
 
 
+class BelowTids(np.ndarray):
+    """Below-set tids in the reference's order with their ascending copy
+    (``sorted_view``) made once — the native tree call takes them sorted."""
+
+    @classmethod
+    def of(cls, tids):
+        b = tids.view(cls)
+        b.sorted_view = np.sort(tids)
+        return b
+
+    def __array_finalize__(self, obj):
+        self.sorted_view = None
+
+
 def split_below(history, gamma, gamma_cap=25):
     """Tids of the ``n_below`` best losses (ap_filter_trials, tpe.py:625-629).
 
@@ -467,14 +483,27 @@ def split_below(history, gamma, gamma_cap=25):
     numpy call on the same float64 array) decides, as in the reference."""
     losses = history.losses
     n = len(losses)
-    n_below = min(int(np.ceil(gamma * np.sqrt(n))), gamma_cap)
+    n_below = min(int(math.ceil(gamma * math.sqrt(n))), gamma_cap)
     if n_below <= 0:
         return history.tids[:0]
     if n_below >= n:
         return history.tids.copy()
+    c = history._cache
+    if c is not None:
+        memo = c.below_memo
+        if memo is not None and memo[0] == c.top_n and memo[1] == n_below and c.top is not None and n == c.top_n:
+            return memo[2]
     top = history.smallest(n_below + 1)
-    if top is not None and len(top) == n_below + 1 and losses[top[n_below - 1]] != losses[top[n_below]]:
-        return history.tids[top[:n_below]]           # the same set as below, without a pass over N
+    if top is not None and len(top) == n_below + 1:
+        keys = c.top_keys if c is not None and c.top is True else None
+        if (keys[n_below - 1] != keys[n_below]) if keys is not None else \
+                (losses[top[n_below - 1]] != losses[top[n_below]]):
+            # the same set as below, without a pass over N (ascending: the
+            # native call takes it sorted, BelowTids.sorted_view)
+            b = BelowTids.of(history.tids[np.asarray(top[:n_below], dtype=np.int64)])
+            if c is not None and c.top is not None:
+                c.below_memo = (c.top_n, n_below, b)
+            return b
     part = np.argpartition(losses, n_below - 1)
     kth = losses[part[n_below - 1]]
     rest = losses[part[n_below:]]

@@ -54,14 +54,8 @@ def docs_from_choices(new_ids, domain, trials, choices):
     rval = []
     for new_id, chosen in zip(new_ids, choices):
         # the misc miscs_update_idxs_vals builds for one id (base.py:77-105), directly
-        idxs, vals = {}, {}
-        for k, v in chosen.items():
-            if v is None:
-                idxs[k] = []
-                vals[k] = []
-            else:
-                idxs[k] = [new_id]
-                vals[k] = [v]
+        idxs = {k: [] if v is None else [new_id] for k, v in chosen.items()}
+        vals = {k: [] if v is None else [v] for k, v in chosen.items()}
         misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir, idxs=idxs, vals=vals)
         rval.extend(trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc]))
     return rval

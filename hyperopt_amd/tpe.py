@@ -474,7 +474,9 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     ex = None
     if shard is not None:
         ex = _dist.exchange_for(engine)
-    below = np.sort(np.asarray(below_tids, dtype=np.int64))
+    below = getattr(below_tids, 'sorted_view', None)
+    if below is None:
+        below = np.sort(np.asarray(below_tids, dtype=np.int64))
     # the labels the previous suggest used are fitted up front on the native
     # worker threads (TPE_F_PREFIT; the active branch seldom changes)
     hint = getattr(table, 'native_used', None)
@@ -553,8 +555,10 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     # batch's rows are not turned into Python lists)
     act_rows = active.tolist() if len(values) <= 4 else None
     used = act_rows[0] if len(values) == 1 else np.asarray(active).any(axis=0).tolist()
-    table.native_fit_hint = tuple(ix for ix in host if used[ix])
-    table.native_used = tuple(i for i, u in enumerate(used) if u)
+    table.native_fit_hint = tuple(ix for ix in host if used[ix]) if host else ()
+    if used != getattr(table, '_used_list', None):      # (the active branch seldom changes)
+        table._used_list = used
+        table.native_used = tuple(i for i, u in enumerate(used) if u)
     # the device-fitted labels that ran hold their merged value orders now (a
     # label the call took a host fit for, give(), did not run the device fit:
     # its order buffers were not written)
@@ -567,13 +571,17 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     cols = _tree_static(table)[2]
     if len(values) > 4:
         return _choice_dicts(order, cols, values, active)
-    i64, f64 = np.int64, np.float64
+    # (the reference's value types: np.int64 categories, np.float64 values)
+    conv = table.__dict__.get('_value_conv')
+    if conv is None:
+        conv = table._value_conv = [(label, np.int64 if fam == N.FAM_CATEGORICAL else np.float64)
+                                    for label, ix, fam in sorted(cols, key=lambda c: c[1])]
     out = []
     for act, v in zip(act_rows, values.tolist()):
         d = dict.fromkeys(order)
-        for label, ix, fam in cols:
-            if act[ix]:              # the reference's value types: np.int64 categories, np.float64 values
-                d[label] = i64(v[ix]) if fam == N.FAM_CATEGORICAL else f64(v[ix])
+        for ix in (table.native_used if len(values) == 1 else [i for i, a in enumerate(act) if a]):
+            label, f = conv[ix]
+            d[label] = f(v[ix])
         out.append(d)
     return out
 

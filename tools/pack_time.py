@@ -38,11 +38,12 @@ def main():
     recs, keep = Engine._labels(problems)
     info = N.PackInfo()
     cap = 64 << 20
+    NC = int(sys.argv[3]) if len(sys.argv) > 3 else bench.C_PER_GPU
     blob = np.empty(cap, dtype=np.uint8)
     ts = []
     for _ in range(reps):
         s = time.perf_counter()
-        rc = lib.tpe_host_pack_level(recs, len(problems), 1 << 20, 7, 0, 0, N.PREC_F32, blob.ctypes.data, cap,
+        rc = lib.tpe_host_pack_level(recs, len(problems), NC, 7, 0, 0, N.PREC_F32, blob.ctypes.data, cap,
                                      ctypes.byref(info))
         ts.append(time.perf_counter() - s)
         assert rc == 0, rc
