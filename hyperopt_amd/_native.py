@@ -240,7 +240,7 @@ EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_si
            'tpe_host_threads', 'tpe_host_phases', 'tpe_exchange_allgather')
 
 # host phases of tpe_suggest_tree (tpe_host_phases order)
-PHASES = ('prefit', 'pack', 'launched', 'synced', 'level', 'return')
+PHASES = ('prefit', 'pack', 'launched', 'synced', 'level', 'return', 'recs')
 
 # tpe_level_run stages (tpe_level_profile_read order)
 STAGES = ('fit', 'k_tables', 'k_sample', 'sort', 'above', 'k_finalize', 'k_select')

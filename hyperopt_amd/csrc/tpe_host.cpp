@@ -14,6 +14,8 @@
 // comes from the caller (np.argsort) so tie order is the reference's.
 #include <math.h>
 
+#include <chrono>
+#include <stdio.h>
 #include <cmath>
 #include <stdint.h>
 #include <stdlib.h>
@@ -314,6 +316,7 @@ inline double min_of(const double* __restrict__ v, int64_t n) {
   return std::min(std::min(m[0], m[1]), std::min(m[2], m[3]));
 }
 
+
 // per-thread staging of tpe_host_pack_level, reused across calls (no
 // first-touch page faults on the large tables of a batched level)
 struct PackScratch {
@@ -339,6 +342,95 @@ void coord_range(const tpe_label_in& L, double& klo, double& khi) {
   for (int64_t i = 0; i < L.below_k; ++i) {
     klo = std::min(klo, L.below_mu[i] - 8 * L.below_sigma[i]);
     khi = std::max(khi, L.below_mu[i] + 8 * L.below_sigma[i]);
+  }
+}
+
+// the table decision of one label (tpe_host_pack_level): which scoring its
+// candidates get — cells (moment rows or TPE_F_LOGPOLY rows), box-moment
+// cells, a lattice or none — and the geometry; labels are independent
+struct TabCtx {
+  const tpe_label_in* labels;
+  const char* dev_fit;
+  int32_t n_cand;
+  bool f64, lp_on, fgt_on;
+  double dv_ratio;
+  int32_t* tmode;
+  int64_t *tn0, *tn1, *tlat;
+  double *tklo, *tkhi;
+  int64_t* fgt_boxes;
+  char* logpoly;
+};
+
+void decide_table(const TabCtx& cx, int32_t li) {
+  const tpe_label_in* labels = cx.labels;
+  const char* dev_fit = cx.dev_fit;
+  const int32_t n_cand = cx.n_cand;
+  const bool f64 = cx.f64;
+  int32_t* tmode = cx.tmode;
+  int64_t *tn0 = cx.tn0, *tn1 = cx.tn1, *tlat = cx.tlat, *fgt_boxes = cx.fgt_boxes;
+  double *tklo = cx.tklo, *tkhi = cx.tkhi;
+  char* logpoly = cx.logpoly;
+  const tpe_label_in& L = labels[li];
+  const double ct = (double)L.n_ids * (double)n_cand;     // candidates of the label in this level
+  if (L.n_ids <= 0 || L.family == TPE_FAM_CATEGORICAL || L.below_k <= 0) return;
+  double klo, khi;
+  coord_range(L, klo, khi);
+  if (!(std::isfinite(klo) && std::isfinite(khi) && khi > klo)) return;
+  tklo[li] = klo; tkhi[li] = khi;
+  if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && !f64) {
+    double s0 = INFINITY, s1 = INFINITY;
+    s0 = min_of(L.below_sigma, L.below_k);
+    if (dev_fit[li])           // the device fit clips every bandwidth to >= prior_sigma / min(100, 1 + K)
+      s1 = L.prior_sigma / std::min(100.0, 1.0 + (double)L.above_k);
+    else
+      s1 = min_of(L.above_sigma, L.above_k);
+    const int64_t n0 = tab_cells(klo, khi, s0), n1 = L.above_k > 0 ? tab_cells(klo, khi, s1) : -1;
+    // a cell row costs ~10x a candidate's score (two passes plus the f64
+    // moments), more against the pruned, locally expanded per-candidate path
+    // of a device-fitted mixture: tables pay from kTabMinRatio candidates a cell
+    // a device-fitted mixture's above cells built from box moments ("Box
+    // moments": ~16 boxes per cell instead of every component within reach)
+    // pay from about one candidate a cell
+    int64_t nbox = 0;
+    if (dev_fit[li] && cx.fgt_on && n1 > 0) {
+      const double d = fgt_width(L.prior_sigma, L.above_k);
+      const double nb = std::ceil((khi - klo) / d) + 1.0;
+      if (d > 0 && nb >= 1.0 && nb <= (double)kFgtMaxBoxes) nbox = (int64_t)nb;
+    }
+    const double ratio = nbox > 0 ? kTabMinRatioFgt : dev_fit[li] ? cx.dv_ratio : kTabMinRatio;
+    const int64_t nl = std::max(n0, n1);
+    const double lp_ratio = dev_fit[li] ? cx.dv_ratio : kTabMinRatio;   // (moment cells, no boxes)
+    // (box-moment labels keep moment cells: their above cells come from the boxes)
+    if (cx.lp_on && nbox == 0 && n0 > 0 && n1 > 0 && nl <= kLogpolyMaxCells &&
+        ct >= lp_ratio * (double)(2 * nl)) {
+      // both sides' log-polynomials on one grid (the finer side's cells): one
+      // row per candidate look-up (include/tpe_hip.h, TPE_F_LOGPOLY)
+      tmode[li] = TPE_TAB_CELLS; tn0[li] = tn1[li] = nl;
+      logpoly[li] = 1;
+    } else if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= ratio * (double)(n0 + n1)) {
+      tmode[li] = TPE_TAB_CELLS; tn0[li] = n0; tn1[li] = n1;
+      fgt_boxes[li] = nbox;
+    }
+  } else if ((L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) && L.q > 0 && L.above_k > 0 &&
+             !(L.flags & TPE_F_NO_TABLE)) {
+    // every value a device draw can take: bounded draws stay in [low, high];
+    // unbounded ones within 8.3 sigma of their component (53-bit uniforms)
+    double tlo = klo, thi = khi;
+    if (!((L.flags & TPE_F_HAS_LOW) && (L.flags & TPE_F_HAS_HIGH))) {
+      tlo = INFINITY; thi = -INFINITY;
+      for (int64_t i = 0; i < L.below_k; ++i) {
+        tlo = std::min(tlo, L.below_mu[i] - 9 * L.below_sigma[i]);
+        thi = std::max(thi, L.below_mu[i] + 9 * L.below_sigma[i]);
+      }
+    }
+    const bool lg = L.family == TPE_FAM_QLOGGAUSS;
+    const double xlo = lg ? exp(tlo) : tlo, xhi = lg ? exp(thi) : thi;
+    const double mlo = std::floor(xlo / L.q) - 1.0, mhi = std::ceil(xhi / L.q) + 1.0;
+    const double nl = mhi - mlo + 1.0;
+    if (std::isfinite(nl) && nl >= 1.0 && nl <= (double)kTabMaxLattice && std::fabs(mlo) < 9e15 &&
+        ct >= 2.0 * nl) {
+      tmode[li] = TPE_TAB_LATTICE; tn0[li] = (int64_t)nl; tlat[li] = (int64_t)mlo;
+    }
   }
 }
 
@@ -776,9 +868,27 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
 // load time on hosts that have it (-ffp-contract=off holds in both clones, so
 // the tables are bit-identical)
 __attribute__((target_clones("avx512f", "avx2", "default")))
+// (TPE_PACK_TRACE builds, tools/pack_time*.py: the packer's sections timed)
+#ifdef TPE_PACK_TRACE
+#define PACK_MARK(name) pack_marks.emplace_back(name, std::chrono::steady_clock::now())
+#define PACK_DONE()                                                                              \
+  do {                                                                                           \
+    for (size_t i_ = 1; i_ < pack_marks.size(); ++i_)                                            \
+      fprintf(stderr, "pack %-16s %8.1f us\n", pack_marks[i_].first,                             \
+              std::chrono::duration<double, std::micro>(pack_marks[i_].second - pack_marks[i_ - 1].second).count()); \
+  } while (0)
+#else
+#define PACK_MARK(name) (void)0
+#define PACK_DONE() (void)0
+#endif
+
 int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
                         int64_t cand_base, int64_t n_cand_global, int32_t precision, void* blob, int64_t blob_cap,
                         tpe_pack_info* info) {
+#ifdef TPE_PACK_TRACE
+  std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> pack_marks;
+  PACK_MARK("entry");
+#endif
   if (!info || n_labels < 0 || n_cand < 0 || (n_labels && !labels)) return TPE_E_ARG;
   const bool f64 = precision == TPE_PREC_F64;
   const int T = 2048;
@@ -808,6 +918,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       dev_fit[li] = 1;
     }
   }
+  PACK_MARK("devfit");
   // ---- tabulated scoring: which labels score from tables, and their geometry ----
   const bool tab_on = tables_enabled();
   std::vector<int32_t> tmode((size_t)n_labels, TPE_TAB_NONE);
@@ -815,70 +926,21 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<double> tklo((size_t)n_labels, 0), tkhi((size_t)n_labels, 0);
   std::vector<int64_t> fgt_boxes((size_t)n_labels, 0);   // box-moment labels: their boxes
   std::vector<char> logpoly((size_t)n_labels, 0);         // TPE_F_LOGPOLY labels
-  for (int32_t li = 0; li < n_labels && tab_on && n_cand > 0; ++li) {
-    const tpe_label_in& L = labels[li];
-    const double ct = (double)L.n_ids * (double)n_cand;     // candidates of the label in this level
-    if (L.n_ids <= 0 || L.family == TPE_FAM_CATEGORICAL || L.below_k <= 0) continue;
-    double klo, khi;
-    coord_range(L, klo, khi);
-    if (!(std::isfinite(klo) && std::isfinite(khi) && khi > klo)) continue;
-    tklo[li] = klo; tkhi[li] = khi;
-    if ((L.family == TPE_FAM_GAUSS || L.family == TPE_FAM_LOGGAUSS) && !f64) {
-      double s0 = INFINITY, s1 = INFINITY;
-      s0 = min_of(L.below_sigma, L.below_k);
-      if (dev_fit[li])           // the device fit clips every bandwidth to >= prior_sigma / min(100, 1 + K)
-        s1 = L.prior_sigma / std::min(100.0, 1.0 + (double)L.above_k);
-      else
-        s1 = min_of(L.above_sigma, L.above_k);
-      const int64_t n0 = tab_cells(klo, khi, s0), n1 = L.above_k > 0 ? tab_cells(klo, khi, s1) : -1;
-      // a cell row costs ~10x a candidate's score (two passes plus the f64
-      // moments), more against the pruned, locally expanded per-candidate path
-      // of a device-fitted mixture: tables pay from kTabMinRatio candidates a cell
-      // a device-fitted mixture's above cells built from box moments ("Box
-      // moments": ~16 boxes per cell instead of every component within reach)
-      // pay from about one candidate a cell
-      int64_t nbox = 0;
-      if (dev_fit[li] && fgt_enabled() && n1 > 0) {
-        const double d = fgt_width(L.prior_sigma, L.above_k);
-        const double nb = std::ceil((khi - klo) / d) + 1.0;
-        if (d > 0 && nb >= 1.0 && nb <= (double)kFgtMaxBoxes) nbox = (int64_t)nb;
-      }
-      const double ratio = nbox > 0 ? kTabMinRatioFgt : dev_fit[li] ? devfit_ratio() : kTabMinRatio;
-      const int64_t nl = std::max(n0, n1);
-      const double lp_ratio = dev_fit[li] ? devfit_ratio() : kTabMinRatio;   // (moment cells, no boxes)
-      // (box-moment labels keep moment cells: their above cells come from the boxes)
-      if (logpoly_enabled() && nbox == 0 && n0 > 0 && n1 > 0 && nl <= kLogpolyMaxCells &&
-          ct >= lp_ratio * (double)(2 * nl)) {
-        // both sides' log-polynomials on one grid (the finer side's cells): one
-        // row per candidate look-up (include/tpe_hip.h, TPE_F_LOGPOLY)
-        tmode[li] = TPE_TAB_CELLS; tn0[li] = tn1[li] = nl;
-        logpoly[li] = 1;
-      } else if (n0 > 0 && n1 > 0 && n0 <= kTabMaxCells && n1 <= kTabMaxCells && ct >= ratio * (double)(n0 + n1)) {
-        tmode[li] = TPE_TAB_CELLS; tn0[li] = n0; tn1[li] = n1;
-        fgt_boxes[li] = nbox;
-      }
-    } else if ((L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) && L.q > 0 && L.above_k > 0 &&
-               !(L.flags & TPE_F_NO_TABLE)) {
-      // every value a device draw can take: bounded draws stay in [low, high];
-      // unbounded ones within 8.3 sigma of their component (53-bit uniforms)
-      double tlo = klo, thi = khi;
-      if (!((L.flags & TPE_F_HAS_LOW) && (L.flags & TPE_F_HAS_HIGH))) {
-        tlo = INFINITY; thi = -INFINITY;
-        for (int64_t i = 0; i < L.below_k; ++i) {
-          tlo = std::min(tlo, L.below_mu[i] - 9 * L.below_sigma[i]);
-          thi = std::max(thi, L.below_mu[i] + 9 * L.below_sigma[i]);
-        }
-      }
-      const bool lg = L.family == TPE_FAM_QLOGGAUSS;
-      const double xlo = lg ? exp(tlo) : tlo, xhi = lg ? exp(thi) : thi;
-      const double mlo = std::floor(xlo / L.q) - 1.0, mhi = std::ceil(xhi / L.q) + 1.0;
-      const double nl = mhi - mlo + 1.0;
-      if (std::isfinite(nl) && nl >= 1.0 && nl <= (double)kTabMaxLattice && std::fabs(mlo) < 9e15 &&
-          ct >= 2.0 * nl) {
-        tmode[li] = TPE_TAB_LATTICE; tn0[li] = (int64_t)nl; tlat[li] = (int64_t)mlo;
-      }
-    }
+  if (tab_on && n_cand > 0) {
+    const TabCtx tcx{labels, dev_fit.data(), n_cand, f64, logpoly_enabled(), fgt_enabled(), devfit_ratio(),
+                     tmode.data(), tn0.data(), tn1.data(), tlat.data(), tklo.data(), tkhi.data(), fgt_boxes.data(),
+                     logpoly.data()};
+    // (a label's decision reads its whole above mixture: thousands of
+    // components per label make a worker's hand-off worth it)
+    int64_t comps = 0;
+    for (int32_t li = 0; li < n_labels; ++li) comps += labels[li].above_k;
+    if (n_labels >= 2 && comps >= 16384)
+      tpe_pool::parallel_for(n_labels, [](void* c, int i) { decide_table(*(const TabCtx*)c, (int32_t)i); },
+                             (void*)&tcx);
+    else
+      for (int32_t li = 0; li < n_labels; ++li) decide_table(tcx, li);
   }
+  PACK_MARK("tmode");
   // Pruned problems (continuous f32 above mixtures of more than kPruneMinK
   // components, not tabulated) are the only ones whose candidates are sorted; they own the
   // candidate range [0, sort_count).  Sort key = sort_slot << key_bits | value
@@ -906,6 +968,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   int key_bits = std::max(5, 8 - pbits);
   if (max_slot_cand >= kFineKeyMinCand) key_bits = std::max(key_bits, std::min(fine_key_bits(), 16 - pbits));
   const int sort_end_bit = S > 0 && key_bits + pbits <= 32 ? key_bits + pbits : 0;
+  PACK_MARK("prune");
   // ---- per-label sections: every label's sampler rows, component rows, wide
   // rows and pruning grid get their offsets first (label order, as appended
   // one after another), then each label fills its own sections — on the host
@@ -930,6 +993,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       }
     }
   }
+  PACK_MARK("sizing");
   // (trivially typed: a resize to the same size as the last call touches nothing)
   comp32.resize((size_t)(4 * n_c32));
   comp64.resize((size_t)(4 * n_c64));
@@ -946,6 +1010,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     else
       for (int32_t li = 0; li < n_labels; ++li) fill_label(fcx, li);
   }
+  PACK_MARK("fill");
   // ---- device-fitted above mixtures: rows and grids after the host ones, fit jobs ----
   const int64_t host_rows = n_c32, host_grid = (int64_t)grid.size();
   std::vector<tpe_fit_job> fit;
@@ -994,6 +1059,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
   if (below_idx.empty()) below_idx.push_back(0);
+  PACK_MARK("devrows");
   // ---- score tables: 16-B units (a cell row is 3 units, a lattice row 1) ----
   int64_t tab_units = 0, fgt_max_boxes = 0;
   for (int32_t li = 0; li < n_labels; ++li) {
@@ -1037,6 +1103,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
   }
   if (tab_units >= ((int64_t)1 << 31)) return TPE_E_ARG;
+  PACK_MARK("tabunits");
   // ---- problems, tiles, work ----
   const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
   auto& prob = ps.prob;
@@ -1080,6 +1147,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
     xfirst[(size_t)n_labels] = (int32_t)r;
   }
+  PACK_MARK("expand");
   const int64_t Ph = expand ? 0 : P;      // problems (and their tiles) the host writes
   prob.resize((size_t)Ph);
   if (!expand) {
@@ -1108,6 +1176,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       }
     }
   }
+  PACK_MARK("prob");
   // splits of the above mixture per tile.  Bulk tiles: enough work items to fill
   // the chip (a function of the GLOBAL candidate count).  Pruned problems with
   // many tiles: the bulk is cheap (local expansion), so one split, and the
@@ -1197,6 +1266,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     for (int64_t t = r * n_tiles_p; t < (r + 1) * n_tiles_p; ++t)
       if (!(cont && tiles[t].n_splits == 1)) fin_tiles.push_back((int32_t)t);
   }
+  PACK_MARK("tiles_work_fin");
   // table jobs: per tabulated label, one per cell side or one lattice job
   // (TPE_TAB_PER_BLOCK rows per block); `problem` = the label's first row
   auto& tab_jobs = ps.tab_jobs;
@@ -1262,6 +1332,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   if (tab_jobs.empty()) tab_jobs.push_back(tpe_tab_job{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0.f, 0.f});
   const int64_t n_fin = (int64_t)fin_tiles.size();
   if (fin_tiles.empty()) fin_tiles.push_back(0);
+  PACK_MARK("jobs_lists");
   // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
   // comp32 rows sit at the END of the last two sections and are not copied ----
   const int NS = 15;
@@ -1323,6 +1394,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->draw_blocks = (C_ref + 1 + 63) / 64;
   info->copy2_len = len[14];
   info->blob_bytes = end;
+  PACK_MARK("offsets");
   if (!blob || blob_cap < end) return TPE_E_SPACE;
   {
     // the sections into the blob; a large level's in 256-KiB pieces on the
@@ -1347,12 +1419,15 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     if (total >= (1u << 20) && pieces.size() > 1) tpe_pool::parallel_for((int)pieces.size(), copy, &pieces);
     else for (size_t k = 0; k < pieces.size(); ++k) copy(&pieces, (int)k);
   }
+  PACK_MARK("copy");
   if (expand) {
     unsigned char* x = (unsigned char*)blob + off[12];
     memcpy(x, xtmpl.data(), (size_t)x_tmpl);
     memcpy(x + x_first_off, xfirst.data(), xfirst.size() * sizeof(int32_t));
     memcpy(x + x_ctr_off, xctr.data(), xctr.size() * sizeof(uint32_t));
   }
+  PACK_MARK("xcopy");
+  PACK_DONE();
   return TPE_OK;
 }
 

@@ -2557,26 +2557,29 @@ __device__ __forceinline__ float chunk_bound(const float4 m, float c) {
   return d > 0.f ? m.w - ad * ad : m.w;
 }
 
-// one wave: {min mu, max mu, min a, max c} of chunks lane, lane + 64, ... (each
-// lane walks its chunk's rows in a rotated order: conflict-free LDS banks)
-__device__ __forceinline__ void chunk_meta(const float4* __restrict__ rows, int n, float4* __restrict__ meta,
-                                           int first_chunk, int step) {
-  const int lane = threadIdx.x & 63;
+// {min mu, max mu, min a, max c} of every chunk, by the whole workgroup: 8
+// lanes per chunk (8 rows each, consecutive lanes on consecutive rows)
+// combined by three xor shuffles (rows past n: the last row again)
+__device__ __forceinline__ void chunk_meta_wg(const float4* __restrict__ rows, int n, float4* __restrict__ meta) {
   const int nch = (n + 63) / 64;
-  for (int g = first_chunk * 64 + lane; g < nch; g += step * 64) {
+  for (int x = (int)threadIdx.x; x < nch * 8; x += (int)blockDim.x) {    // (whole 8-lane groups)
+    const int g = x >> 3, s = x & 7;
+    const int last = min(n, g * 64 + 64) - 1;
     float lo = INFINITY, hi = -INFINITY, amin = INFINITY, cmax = -INFINITY;
-    const int last = min(n, g * 64 + 64) - 1;          // rows past n read the last row again
-    for (int i0 = 0; i0 < 64; i0 += 8) {
-      float4 q[8];
+    float4 q[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) q[u] = rows[min(g * 64 + ((i0 + u + lane) & 63), last)];
+    for (int i = 0; i < 8; ++i) q[i] = rows[min(g * 64 + i * 8 + s, last)];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float mu = q[u].x + q[u].y;
-        lo = fminf(lo, mu); hi = fmaxf(hi, mu); amin = fminf(amin, q[u].z); cmax = fmaxf(cmax, q[u].w);
-      }
+    for (int i = 0; i < 8; ++i) {
+      const float mu = q[i].x + q[i].y;
+      lo = fminf(lo, mu); hi = fmaxf(hi, mu); amin = fminf(amin, q[i].z); cmax = fmaxf(cmax, q[i].w);
     }
-    meta[g] = make_float4(lo, hi, amin, cmax);
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      lo = fminf(lo, __shfl_xor(lo, off)); hi = fmaxf(hi, __shfl_xor(hi, off));
+      amin = fminf(amin, __shfl_xor(amin, off)); cmax = fmaxf(cmax, __shfl_xor(cmax, off));
+    }
+    if (s == 0) meta[g] = make_float4(lo, hi, amin, cmax);
   }
 }
 
@@ -2620,6 +2623,10 @@ __device__ __forceinline__ void cell_moments_chunked(const float4* __restrict__ 
     }
   }
   const float mx = wave_max(m);
+#ifdef TPE_TABLES_TRACE
+  int n_p1 = 0, n_p2 = 0, n_terms = 0;
+  for (int half = 0; half < 2; ++half) n_p1 += __popcll(__ballot((half ? b1 : b0) > m0 - kChunkSlack));
+#endif
   // pass 2: chunks that could hold a term within 2^-50 of the maximum
   bool bad = !(mx > -INFINITY);
   const float cut = mx - kTabDrop;
@@ -2634,8 +2641,17 @@ __device__ __forceinline__ void cell_moments_chunked(const float4* __restrict__ 
       const float z = ((c - q.x) - q.y) * q.z;
       const float v = q.w - z * z;
       if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
+#ifdef TPE_TABLES_TRACE
+      ++n_p2;
+      n_terms += __popcll(__ballot(v >= cut));
+#endif
     }
   }
+#ifdef TPE_TABLES_TRACE
+  if ((threadIdx.x & 63) == 0 && (blockIdx.x % 8) == 0 && (threadIdx.x >> 6) < 2)
+    printf("k_tables chunks blk %d wave %d nch %d pass1 %d pass2 %d terms %d\n", (int)blockIdx.x,
+           (int)(threadIdx.x >> 6), nch, n_p1, n_p2, n_terms);
+#endif
   mx_out = mx;
   bad_out = __ballot(bad) != 0ull;
 }
@@ -3070,6 +3086,7 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       rows_lds[threadIdx.x] = (int)threadIdx.x < jb.rows_n ? comp32[jb.rows_off + threadIdx.x]
                                                            : comp32[jb.wide_off + threadIdx.x - jb.rows_n];
     __syncthreads();
+    TT(1);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int rl = lane / 11, k = lane - 11 * rl;               // (row of the wave, node)
     const int jr = (b * TPE_TAB_PER_BLOCK + wave) * kLpRowsPerWave + rl;
@@ -3105,6 +3122,12 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     const bool row_bad = rl < kLpRowsPerWave && ((bm >> b0) & 0x7FFull) != 0ull;
     if (live && k < 6)
       reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * jr)[6 * jb.side + k] = row_bad ? NAN : (float)cf;
+#ifdef TPE_TABLES_TRACE
+    TT(2);
+    if (lane == 0 && (blockIdx.x % 4) == 0 && wave < 2)
+      printf("k_tables direct blk %d wave %d rows %d: lookup+stage %llu sums+fit %llu\n", (int)blockIdx.x, wave, nr,
+             (unsigned long long)(tt[1] - tt[0]), (unsigned long long)(tt[2] - tt[1]));
+#endif
     return;
   }
   if (jb.kind == TPE_TAB_CELLS || jb.kind == TPE_TAB_LOGPOLY) {
@@ -3118,11 +3141,20 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     __shared__ float4 meta_lds[kChunkMax];
     TT(1);
     if (stage) {
-      for (int q = threadIdx.x; q < n0 + n1; q += kTabTblThreads)
-        rows_lds[q] = q < n0 ? comp32[k0 + q] : comp32[k1 + q - n0];
+      // the rows by LDS-DMA: every round's loads issued before the one wait
+      // (rounds past the rows: clamped loads into unused slots)
+      const int nr = n0 + n1, wv = (int)(threadIdx.x >> 6);
+      for (int u = 0; u * kTabTblThreads < nr; ++u) {
+        const int q = min(u * kTabTblThreads + (int)threadIdx.x, nr - 1);
+        const float4* src = q < n0 ? comp32 + k0 + q : comp32 + k1 + (q - n0);
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(rows_lds + u * kTabTblThreads + 64 * wv),
+                                         16, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
       TT(2);
-      if (threadIdx.x < 128) chunk_meta(rows_lds, n0 + n1, meta_lds, (int)(threadIdx.x >> 6), 2);
+      chunk_meta_wg(rows_lds, nr, meta_lds);
       __syncthreads();
     }
     TT(3);
@@ -3173,6 +3205,14 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       const float m = __shfl(mx, kTabMoments);
       const bool fl = __shfl(bad || all_exact ? 1 : 0, kTabMoments) != 0;
       logpoly_side(sum, m, fl, row + 6 * jb.side);
+#ifdef TPE_TABLES_TRACE
+      TT(5);
+      if (lane == 0 && (blockIdx.x % 8) == 0 && wave < 2)
+        printf("k_tables lp blk %d wave %d side %d rows %d: lookup %llu stage %llu meta %llu passes %llu reduce+fit %llu\n",
+               (int)blockIdx.x, wave, side, n0 + n1, (unsigned long long)(tt[1] - tt[0]),
+               (unsigned long long)(stage ? tt[2] - tt[1] : 0), (unsigned long long)(stage ? tt[3] - tt[2] : 0),
+               (unsigned long long)(tt[4] - tt[3]), (unsigned long long)(tt[5] - tt[4]));
+#endif
       return;
     }
     float val = 0.f;

@@ -419,6 +419,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
   std::vector<tpe_label_in>& recs = recs_tl;
   std::vector<tpe_result>& res = res_tl;
   auto run = [&](int32_t n_recs) -> int {
+    tpe_internal_phase(TPE_PHASE_RECS);
     int64_t P = 0;
     for (int32_t r = 0; r < n_recs; ++r) P += recs[(size_t)r].n_ids;
     res.resize((size_t)std::max<int64_t>(P, 1));

@@ -876,7 +876,8 @@ int tpe_level_profile_read(tpe_stage_prof* out, int32_t n);
 #define TPE_PHASE_SYNCED   3   /* the stream synchronise returned                */
 #define TPE_PHASE_LEVEL    4   /* the level's results assembled                  */
 #define TPE_PHASE_RETURN   5   /* tpe_suggest_tree returns                       */
-#define TPE_N_PHASES       6
+#define TPE_PHASE_RECS     6   /* the level's fits and label records ready (before its pack) */
+#define TPE_N_PHASES       7
 
 /* enable (1) / disable (0); *last (if not NULL) gets min(n, TPE_N_PHASES)
  * phase times of the last call (before this one changes the setting) */
