@@ -539,10 +539,16 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
   chosen.assign((size_t)n_ids * n_labels, kInactive);
   for (size_t q = 0; q < (size_t)n_ids * n_labels; ++q) { values[q] = NAN; active[q] = 0; }
   std::vector<int64_t>& lvl_ids = ids_tl;
+  // a member of a level: its label, its problems' first row in the level's
+  // results, their count, and where its id positions start in lvl_ids (-1: every
+  // id — a label without parents — whose positions are 0 .. n_ids - 1 and whose
+  // records take the caller's id array as it is)
+  struct Member { int label; int64_t res_off, count, lvl_first; };
   for (int d = 0; d <= T.max_depth; ++d) {
     recs.clear();
     lvl_ids.clear();
-    std::vector<std::pair<int, int64_t>> members;   // (label, first position in lvl_ids)
+    std::vector<Member> members;
+    int64_t n_res = 0;
     bool pending = false;                   // labels flagged for the caller's fit: all of the level's at once
     for (int i = 0; i < n_labels; ++i) {
       const tpe_tree_label& L = labels[i];
@@ -555,58 +561,68 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
           }
         continue;
       }
-      const int64_t first = (int64_t)lvl_ids.size();
-      for (int j = 0; j < n_ids; ++j)
-        if (is_active(L, chosen.data() + (size_t)j * n_labels)) lvl_ids.push_back(j);
-      if ((int64_t)lvl_ids.size() == first) continue;
+      Member m{i, n_res, n_ids, -1};
+      if (L.n_parents > 0) {
+        m.lvl_first = (int64_t)lvl_ids.size();
+        for (int j = 0; j < n_ids; ++j)
+          if (is_active(L, chosen.data() + (size_t)j * n_labels)) lvl_ids.push_back(j);
+        m.count = (int64_t)lvl_ids.size() - m.lvl_first;
+        if (m.count == 0) continue;
+      }
       const int rc = fit_label(T, i);
       if (rc != TPE_OK) {
         if (rc == TPE_E_FALLBACK && need_fit && need_fit[i]) { pending = true; continue; }
         return rc;
       }
-      members.emplace_back(i, first);
+      members.push_back(m);
+      n_res += m.count;
     }
     if (pending) return TPE_E_FALLBACK;
     if (members.empty()) continue;
-    // the level's id arrays (positions -> new ids), stable now that lvl_ids is complete
+    // the gated members' id arrays (positions -> new ids), stable now that lvl_ids is complete
     std::vector<int64_t> lvl_new((size_t)lvl_ids.size());
     for (size_t q = 0; q < lvl_ids.size(); ++q) lvl_new[q] = ids[lvl_ids[q]];
     recs.resize(members.size());
-    for (size_t m = 0; m < members.size(); ++m) {
-      const int64_t first = members[m].second;
-      const int64_t end = m + 1 < members.size() ? members[m + 1].second : (int64_t)lvl_ids.size();
-      label_rec(T, labels[members[m].first], fits[(size_t)members[m].first], lvl_new.data() + first, end - first,
-                recs[m]);
+    for (size_t k = 0; k < members.size(); ++k) {
+      const Member& m = members[k];
+      label_rec(T, labels[m.label], fits[(size_t)m.label], m.lvl_first < 0 ? ids : lvl_new.data() + m.lvl_first,
+                m.count, recs[k]);
     }
     const int rc = run((int32_t)members.size());
     if (rc != TPE_OK) return rc;
-    for (size_t q = 0; q < lvl_ids.size(); ++q) {
-      if (res[q].idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
+    for (int64_t q = 0; q < n_res; ++q) {
+      if (res[(size_t)q].idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
     }
     // the members' results into their columns, ids in blocks (a block's rows
-    // are its own: no cache lines shared between workers); a member's positions
-    // hold its ids ascending, so a block's are one range, found by bisection
+    // are its own: no cache lines shared between workers); a gated member's
+    // positions hold its ids ascending, so a block's are one range, found by
+    // bisection
     struct Mem {
-      const std::pair<int, int64_t>* members; int n_mem; const int64_t* lvl_ids; int64_t n_lvl;
+      const Member* members; int n_mem; const int64_t* lvl_ids;
       const tpe_result* res; double* values; int8_t* active; int* chosen; const char* gate; int n_ids, n_labels;
     };
-    Mem mx{members.data(), (int)members.size(), lvl_ids.data(), (int64_t)lvl_ids.size(), res.data(), values, active,
-           chosen.data(), T.gate.data(), n_ids, n_labels};
+    Mem mx{members.data(), (int)members.size(), lvl_ids.data(), res.data(), values, active, chosen.data(),
+           T.gate.data(), n_ids, n_labels};
     auto put = [](void* c, int k) {
       const Mem& x = *(const Mem*)c;
       const int64_t j0 = (int64_t)k * kIdBlock, j1 = std::min<int64_t>(x.n_ids, j0 + kIdBlock);
-      for (int m = 0; m < x.n_mem; ++m) {
-        const int i = x.members[m].first;
-        const int64_t first = x.members[m].second, end = m + 1 < x.n_mem ? x.members[m + 1].second : x.n_lvl;
-        const int64_t* lo = std::lower_bound(x.lvl_ids + first, x.lvl_ids + end, j0);
-        const int64_t* hi = std::lower_bound(lo, x.lvl_ids + end, j1);
-        for (const int64_t* p = lo; p < hi; ++p) {
-          const int64_t q = p - x.lvl_ids, j = *p;
+      for (int mi = 0; mi < x.n_mem; ++mi) {
+        const Member& m = x.members[mi];
+        const int i = m.label;
+        auto set = [&](int64_t q, int64_t j) {
           const double v = x.res[(size_t)q].value;
           x.values[(size_t)j * x.n_labels + i] = v;
           x.active[(size_t)j * x.n_labels + i] = 1;
           x.chosen[(size_t)j * x.n_labels + i] = x.gate[i] ? (int)(int64_t)v : kActive;
+        };
+        if (m.lvl_first < 0) {
+          for (int64_t j = j0; j < j1; ++j) set(m.res_off + j, j);
+          continue;
         }
+        const int64_t* base = x.lvl_ids + m.lvl_first;
+        const int64_t* lo = std::lower_bound(base, base + m.count, j0);
+        const int64_t* hi = std::lower_bound(lo, base + m.count, j1);
+        for (const int64_t* p = lo; p < hi; ++p) set(m.res_off + (p - base), *p);
       }
     };
     const int nb = (n_ids + kIdBlock - 1) / kIdBlock;
