@@ -265,22 +265,22 @@ def _wrap(v, root):
     return v
 
 
-def _track(doc, log):
-    """``doc`` as a document logging into ``log``: a tracked document gains
-    the log (it may belong to several Trials), anything else becomes a
-    tracked copy."""
+def _track(doc, logs):
+    """``doc`` as a document logging into each of ``logs`` (a Trials'
+    mutation logs): a tracked document gains the logs (it may belong to
+    several Trials), anything else becomes a tracked copy."""
     if type(doc) is _Doc:
         ts = getattr(doc, '_ts', None)
         if ts is None:
-            doc._ts = [log]
-        elif not any(t is log for t in ts):
-            ts.append(log)
+            doc._ts = list(logs)
+        else:
+            ts.extend(lg for lg in logs if not any(t is lg for t in ts))
         return doc
     d = _Doc(doc)
     for k, v in doc.items():
         if type(v) not in _PLAIN:
             dict.__setitem__(d, k, _wrap(v, d))
-    d._ts = [log]
+    d._ts = list(logs)
     return d
 
 
@@ -306,6 +306,23 @@ class _View(list):
                                               'clear', 'sort', 'reverse', '__imul__'))
 
 
+class _DynList(list):
+    """``Trials._dynamic_trials``: appends (insert_trial_docs) keep the next
+    refresh incremental; any other edit (an element replaced, removed,
+    inserted or reordered) makes it rebuild the view from every document."""
+    __slots__ = ('_owner',)
+
+    def __reduce_ex__(self, protocol):
+        return list, (list(self),)
+
+    def _moved(self):
+        self._owner._dyn_dirty = True
+
+    __setitem__, __delitem__, insert, pop, remove, clear, sort, reverse, __imul__ = (
+        _logging(list, n, '_moved') for n in ('__setitem__', '__delitem__', 'insert', 'pop', 'remove',
+                                              'clear', 'sort', 'reverse', '__imul__'))
+
+
 def coarse_utcnow():
     """utils.py:127-136: UTC now rounded down to milliseconds."""
     now = datetime.datetime.utcnow()
@@ -317,8 +334,9 @@ class Trials(object):
 
     def __init__(self, exp_key=None, refresh=True):
         self._ids = set()
-        self._dynamic_trials = []
-        self._mutated = {}             # id -> tracked document edited in place (see _Doc)
+        self._dynamic_trials = self._dyn_list([])
+        self._mutated = {}             # id -> tracked document edited in place (see _Doc): history.py's
+        self._rlog = {}                # ... and refresh's (each consumer clears its own)
         self._exp_key = exp_key
         self.attachments = {}
         if refresh:
@@ -328,21 +346,33 @@ class Trials(object):
     def __getstate__(self):
         d = dict(self.__dict__)
         d.pop('_tpe_history', None)
-        d.pop('_mutated', None)
+        for k in ('_mutated', '_rlog', '_dyn_ref', '_dyn_dirty', '_excluded', '_n_dyn', '_gen_seen'):
+            d.pop(k, None)            # (refresh bookkeeping: rebuilt by the first refresh)
         return d
 
     def __setstate__(self, d):
         # documents come back as plain dicts (_Doc.__reduce_ex__): tracked again,
         # the view keeping its documents (the same objects as _dynamic_trials')
         self.__dict__.update(d)
-        self._mutated = {}
+        self._mutated, self._rlog = {}, {}
         new = {}
-        dyn = self._dynamic_trials
+        dyn = self._dyn_list(self._dynamic_trials)
         for i, tt in enumerate(dyn):
-            dyn[i] = new[id(tt)] = _track(tt, self._mutated)
+            t = new[id(tt)] = _track(tt, self._logs())
+            list.__setitem__(dyn, i, t)
+        self._dynamic_trials = dyn
+        self._dyn_ref = None           # the next refresh rebuilds the view
         old = self.__dict__.get('_trials')
         if old is not None:
-            self._trials = self._view([new.get(id(tt)) or _track(tt, self._mutated) for tt in old])
+            self._trials = self._view([new.get(id(tt)) or _track(tt, self._logs()) for tt in old])
+
+    def _logs(self):
+        return (self.__dict__.setdefault('_mutated', {}), self.__dict__.setdefault('_rlog', {}))
+
+    def _dyn_list(self, docs):
+        v = _DynList(docs)
+        v._owner = self
+        return v
 
     def _view(self, docs):
         v = _View(docs)
@@ -352,11 +382,11 @@ class Trials(object):
     def _track_all(self):
         """Track every document of _dynamic_trials in this Trials' log (a
         document put there directly, a deep copy, another Trials' document)."""
-        log = self.__dict__.setdefault('_mutated', {})
+        logs = self._logs()
         dyn = self._dynamic_trials
         for i, tt in enumerate(dyn):
-            if not _tracked_by(tt, log):
-                dyn[i] = _track(tt, log)
+            if not _tracked_by(tt, logs[0]):
+                dyn[i] = _track(tt, logs)
 
     def aname(self, trial, name):
         return 'ATTACH::%s::%s' % (trial['tid'], name)
@@ -392,23 +422,56 @@ class Trials(object):
 
         ``_view_gen`` counts the refreshes whose view is NOT the previous view
         plus appended documents (a document dropped, replaced or reordered):
-        derived caches of the view (history.py) rebuild when it moves."""
+        derived caches of the view (history.py) rebuild when it moves.
+
+        Incremental when nothing but appends happened since the last refresh
+        (FMinIter's use): the view list is extended in place by the appended
+        documents that qualify — unless a document already seen was edited
+        into or out of the view (its state or exp_key, in the refresh log), or
+        ``_dynamic_trials`` / the view were edited otherwise; then the view is
+        rebuilt from every document, as the reference does (base.py:183-194)."""
         old = getattr(self, '_trials', None)
-        log = self.__dict__.setdefault('_mutated', {})
-        for attempt in (0, 1):
-            if self._exp_key is None:
-                new = [tt for tt in self._dynamic_trials if tt['state'] != JOB_STATE_ERROR]
-            else:
-                new = [tt for tt in self._dynamic_trials
-                       if tt['state'] != JOB_STATE_ERROR and tt['exp_key'] == self._exp_key]
-            appended = old is not None and len(new) >= len(old) and all(map(operator.is_, old, new))
-            if attempt or all(_tracked_by(tt, log) for tt in new[len(old) if appended else 0:]):
-                break
-            self._track_all()          # untracked documents (put in _dynamic_trials directly)
+        logs = self._logs()
+        log, rlog = logs
+        dyn = self._dynamic_trials
+        d = self.__dict__
+        n0 = d.get('_n_dyn', 0)
+        ek = self._exp_key
+        gen = getattr(self, '_view_gen', 0)
+
+        def keep(tt):
+            return tt['state'] != JOB_STATE_ERROR and (ek is None or tt['exp_key'] == ek)
+        if (old is not None and type(old) is _View and dyn is d.get('_dyn_ref') and not d.get('_dyn_dirty')
+                and d.get('_gen_seen') == gen and len(dyn) >= n0):
+            excluded = d.get('_excluded', ())
+            if all(keep(tt) and id(tt) not in excluded for tt in rlog.values()):
+                rlog.clear()
+                add = []
+                for i in range(n0, len(dyn)):
+                    tt = dyn[i]
+                    if not _tracked_by(tt, log):       # (put in _dynamic_trials directly)
+                        tt = _track(tt, logs)
+                        list.__setitem__(dyn, i, tt)
+                    if keep(tt):
+                        add.append(tt)
+                    else:
+                        excluded = d['_excluded'] = set(excluded) | {id(tt)}
+                list.extend(old, add)
+                self._ids.update([tt['tid'] for tt in add])
+                self._n_dyn = len(dyn)
+                return
+        rlog.clear()
+        if type(dyn) is not _DynList or dyn._owner is not self:
+            dyn = self._dynamic_trials = self._dyn_list(dyn)
+        self._track_all()              # (documents put in _dynamic_trials directly)
+        new = [tt for tt in dyn if keep(tt)]
+        appended = old is not None and len(new) >= len(old) and all(map(operator.is_, old, new))
         self._trials = self._view(new)
         if old is not None and not appended:
-            self._view_gen = getattr(self, '_view_gen', 0) + 1
+            self._view_gen = gen = gen + 1
         self._ids.update([tt['tid'] for tt in self._trials])
+        self._excluded = {id(tt) for tt in dyn if not keep(tt)}
+        self._dyn_ref, self._dyn_dirty, self._n_dyn, self._gen_seen = dyn, False, len(dyn), gen
 
     @property
     def trials(self):
@@ -461,9 +524,9 @@ class Trials(object):
         """Appends ``docs`` as tracked documents (_Doc); a list passed in is
         updated in place to hold them, so the caller's list keeps naming the
         documents this Trials holds."""
-        log = self.__dict__.setdefault('_mutated', {})
+        logs = self._logs()
         rval = [doc['tid'] for doc in docs]
-        tracked = [_track(doc, log) for doc in docs]
+        tracked = [_track(doc, logs) for doc in docs]
         if type(docs) is list:
             docs[:] = tracked
         self._dynamic_trials.extend(tracked)

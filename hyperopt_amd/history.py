@@ -22,6 +22,7 @@ reference's per-call walk would see (tpe.py:820-842) is seen here, without a
 pass over the documents.
 """
 import bisect
+import ctypes
 import math
 import weakref
 
@@ -122,16 +123,6 @@ class History(object):
         return len(self.tids)
 
 
-def _insert1(a, at, v):
-    """np.insert(a, at, v) for one value (a new array; without np.insert's
-    per-call Python overhead, which dominates at these sizes)."""
-    out = np.empty(len(a) + 1, dtype=a.dtype)
-    out[:at] = a[:at]
-    out[at] = v
-    out[at + 1:] = a[at:]
-    return out
-
-
 class _Grow(object):
     """Append-only column; ``addr`` = host address of its buffer (kept with
     the buffer, so native calls need no per-call pointer lookup)."""
@@ -152,6 +143,21 @@ class _Grow(object):
     def view(self):
         return self.a[:self.n]
 
+    def reserve(self, cap):
+        if cap > self.a.shape[0]:
+            a = np.empty(cap, dtype=self.a.dtype)
+            a[:self.n] = self.a[:self.n]
+            self.a, self.addr = a, a.ctypes.data
+
+    @classmethod
+    def of(cls, arr):
+        """A column holding ``arr`` (with room to grow)."""
+        g = cls(arr.dtype)
+        g.reserve(max(64, 2 * len(arr)))
+        g.a[:len(arr)] = arr
+        g.n = len(arr)
+        return g
+
 
 class _Cache(object):
     def __init__(self, labels, categorical, gen=0):
@@ -167,10 +173,9 @@ class _Cache(object):
         self.labels = labels
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
-        self.orders = {}               # label -> value-sorting permutation of its observations
+        self.orders = {}               # label -> _Grow: value-sorting permutation of its observations
         self.sorted_vals = {}          # label -> its values in that order
         self.order_ok = {}             # label -> the permutation, or None when a value is NaN
-        self.order_addrs = {}          # label -> (that permutation, its address)
         self.logs = {}                 # label -> _Grow of np.log of its observation values
         self.top = None                # positions of the smallest losses, sorted by (loss, position)
         self.top_n = 0                 # documents merged into `top`
@@ -274,45 +279,50 @@ class _Cache(object):
 
     def order_addr(self, k):
         """Address of value_order(k)'s array (valid right after that call)."""
-        perm = self.orders.get(k)
-        a = self.order_addrs.get(k)
-        if a is None or a[0] is not perm:
-            a = self.order_addrs[k] = (perm, perm.ctypes.data)
-        return a[1]
+        return self.orders[k].addr
 
     def value_order(self, k):
         """Sorting permutation of obs_val[k], extended by a merge of the
         observations appended since the last call (O(n) per suggest instead of
         a sort).  Any sort of a column without repeated values is the one
-        np.argsort gives; the fit checks each side for repeats itself."""
+        np.argsort gives; the fit checks each side for repeats itself.
+        (One appended value — FMinIter's case — is inserted in place: the tail
+        of the permutation and of the sorted values moves up one slot.)"""
         g = self.obs_val[k]
         n = g.n
-        perm = self.orders.get(k)
-        if perm is not None and len(perm) == n:
+        pg = self.orders.get(k)
+        if pg is not None and pg.n == n:
             return self.order_ok[k]
         vals = g.view()
-        if perm is None:
-            perm = np.argsort(vals)
-            sv = vals[perm]
+        sg = self.sorted_vals.get(k)
+        if pg is not None and n - pg.n == 1 and pg.n > 0:
+            m = pg.n
+            v = vals[m]
+            at = int(sg.view().searchsorted(v, side='right'))
+            for q, x in ((pg, m), (sg, v)):
+                if q.n == q.a.shape[0]:
+                    q.reserve(2 * q.n)
+                w = q.a.itemsize
+                ctypes.memmove(q.addr + (at + 1) * w, q.addr + at * w, (m - at) * w)
+                q.a[at] = x
+                q.n = m + 1
         else:
-            # (the sorted values are kept beside the permutation: the insertion
-            # points are a binary search, not a gather of the whole column)
-            m = len(perm)
-            nv = vals[m:]
-            if n - m == 1:
-                sv = self.sorted_vals[k]
-                at = int(sv.searchsorted(nv[0], side='right'))
-                perm = _insert1(perm, at, m)
-                sv = _insert1(sv, at, nv[0])
+            if pg is None:
+                perm = np.argsort(vals)
+                sv = vals[perm]
             else:
+                # (the sorted values are kept beside the permutation: the insertion
+                # points are a binary search, not a gather of the whole column)
+                m = pg.n
+                nv = vals[m:]
                 o = np.argsort(nv, kind='stable')
-                sv = self.sorted_vals[k]
-                at = np.searchsorted(sv, nv[o], side='right')
-                perm = np.insert(perm, at, o + m)
-                sv = np.insert(sv, at, nv[o])
-        self.orders[k] = perm
-        self.sorted_vals[k] = sv
-        ok = self.order_ok[k] = None if n and sv[-1] != sv[-1] else perm     # NaN sorts last
+                at = np.searchsorted(sg.view(), nv[o], side='right')
+                perm = np.insert(pg.view(), at, o + m)
+                sv = np.insert(sg.view(), at, nv[o])
+            pg = self.orders[k] = _Grow.of(perm)
+            sg = self.sorted_vals[k] = _Grow.of(sv)
+        perm = pg.view()
+        ok = self.order_ok[k] = None if n and sg.a[n - 1] != sg.a[n - 1] else perm     # NaN sorts last
         return ok
 
     TOP = 64
