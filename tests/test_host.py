@@ -213,6 +213,42 @@ def test_history_cache_sees_in_place_edits_of_completed_documents():
     assert h.losses[-1] == -11.0
 
 
+def test_incremental_refresh_equals_full_filter():
+    """Trials.refresh extends the view in place after appends and rebuilds it
+    after any other change: over a random sequence of appends, state edits
+    (into and out of ERROR), direct _dynamic_trials edits and view edits the
+    view always equals the reference's filter of every document
+    (base.py:183-194), and the history equals the reference walk."""
+    rs = np.random.RandomState(7)
+    d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1)})
+    t = base.Trials()
+    tid = 0
+    for step in range(300):
+        op = rs.randint(6)
+        if op <= 2 or len(t._dynamic_trials) < 5:
+            docs = rand.suggest(list(range(tid, tid + rs.randint(1, 4))), d, t, rs.randint(1000))
+            tid += len(docs)
+            for doc in docs:
+                doc['state'] = base.JOB_STATE_DONE
+                doc['result'] = {'status': 'ok', 'loss': float(rs.uniform())}
+            t.insert_trial_docs(docs)
+            if rs.rand() < 0.2:          # an appended document failing before the refresh
+                docs[-1]['state'] = base.JOB_STATE_ERROR
+        elif op == 3:                    # a seen document into or out of ERROR
+            doc = t._dynamic_trials[rs.randint(len(t._dynamic_trials))]
+            doc['state'] = base.JOB_STATE_ERROR if doc['state'] != base.JOB_STATE_ERROR else base.JOB_STATE_DONE
+        elif op == 4 and rs.rand() < 0.3:   # a direct edit of the document list
+            i = rs.randint(len(t._dynamic_trials))
+            t._dynamic_trials[i] = dict(t._dynamic_trials[i])
+        elif op == 5 and rs.rand() < 0.3 and len(t.trials):    # a view edit
+            del t.trials[rs.randint(len(t.trials))]
+        t.refresh()
+        want = [x for x in t._dynamic_trials if x['state'] != base.JOB_STATE_ERROR]
+        assert len(t.trials) == len(want) and all(a is b for a, b in zip(t.trials, want)), step
+        if step % 10 == 0 and len(t.trials):
+            _same_as_walk(d, t)
+
+
 def test_appended_documents_update_tree_records_in_place():
     """FMinIter's flow — one or a few finished documents appended before each
     suggest: the tree records updated in place (tpe._tree_refill), the merged
