@@ -66,6 +66,14 @@ class History(object):
             xa = c.obs_val[label].addr
         return c.obs_tid[label].addr, xa, c.order_addr(label)
 
+    def coord_addr(self, label, key):
+        """Address of coord_values(label, key, ...)'s array (valid right after
+        that call; None without a Trials cache)."""
+        c = self._cache
+        if c is None:
+            return None
+        return c.logs[(key, label)].addr
+
     def cat_columns(self, label):
         """(tids, values) addresses of a categorical label (see native_columns)."""
         c = self._cache
@@ -478,10 +486,12 @@ class BelowTids(np.ndarray):
     def of(cls, tids):
         b = tids.view(cls)
         b.sorted_view = np.sort(tids)
+        b.positions = {}               # label -> (column length, History, below positions): tpe._below_positions
         return b
 
     def __array_finalize__(self, obj):
         self.sorted_view = None
+        self.positions = None
 
 
 def split_below(history, gamma, gamma_cap=25):

@@ -458,6 +458,37 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     return out
 
 
+_GIVEN_FIELDS = ('tids', 'values', 'n_obs', 'side_order', 'side_n', 'host_k', 'host_w')
+
+
+def _coord_fn(table, row):
+    """The row's fit coordinate as an elementwise function (parzen.fit_coord),
+    made once per table row."""
+    fns = table.__dict__.setdefault('_coord_fns', {})
+    f = fns.get(row.index)
+    if f is None:
+        a, dist = row.args, row.dist
+        f = fns[row.index] = lambda v: fit_coord(dist, a, v)
+    return f
+
+
+def _below_positions(hist, label, otids, below_tids):
+    """(positions of the below observations among a label's, history.below_index;
+    the mask of the others), kept on the below set itself for the History and
+    column length they were computed for."""
+    memo = getattr(below_tids, 'positions', None)
+    if memo is not None:
+        p = memo.get(label)
+        if p is not None and p[0] == len(otids) and p[1] is hist:
+            return p[2], p[3]
+    b = _history.below_index(otids, below_tids, hist.sorted_obs)
+    above = np.ones(len(otids), dtype=bool)
+    above[b] = False
+    if memo is not None:
+        memo[label] = (len(otids), hist, b, above)
+    return b, above
+
+
 def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False, remote=()):
     if not hist.sorted_obs:
         return None
@@ -496,11 +527,20 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
         the native call then fits it.  (A categorical label: the general
         path's fit.)  False: the label needs the general path."""
         if not host and 'copied' not in st:
+            # the call's records: a per-table copy of the memoised ones (the given
+            # labels' fields point at this call's arrays), its field views and
+            # address kept with it
+            g = table.__dict__.get('_given')
+            if g is None or g[0] is not tl[0]:
+                arr2 = tl[0].copy()
+                g = table._given = (tl[0], arr2, {f: arr2[f] for f in _GIVEN_FIELDS},
+                                    arr2.__array_interface__['data'][0])
+            else:
+                np.copyto(g[1], tl[0])
             st['copied'] = True
-            st['arr'] = st['arr'].copy()
-            st['ptr'] = None
+            st['arr'], st['fv'], st['ptr'] = g[1], g[2], g[3]
+        fv = st['fv']
         row = table.rows[ix]
-        rec = st['arr'][ix]
         keep = host[ix] = []                   # (keeps the arrays alive for the call)
         otids, ovals = hist.obs[row.label]
         n = len(otids)
@@ -511,24 +551,30 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
             for sd, side in enumerate((post.below, post.above)):
                 c = np.ascontiguousarray(side[0], dtype=np.float64)
                 keep.append(c)
-                rec['host_k'][sd] = len(c)
-                rec['host_w'][sd] = c.ctypes.data
+                fv['host_k'][ix, sd] = len(c)
+                fv['host_w'][ix, sd] = c.__array_interface__['data'][0]
             return True
         dmin = _dev_fit_min(engine)
         if dmin is not None and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and n >= dmin:
             return False                       # (device-fit sizes: the general path)
-        a = row.args
-        x = hist.coord_values(row.label, row.dist, lambda v: fit_coord(row.dist, a, v))
-        t = np.ascontiguousarray(otids, dtype=np.int64)
-        bidx = _history.below_index(otids, below_tids, hist.sorted_obs)
-        above = np.ones(n, dtype=bool)
-        above[bidx] = False
+        x = hist.coord_values(row.label, row.dist, _coord_fn(table, row))
+        bidx, above = _below_positions(hist, row.label, otids, below_tids)
         ob = np.argsort(x[bidx])
         oa = np.argsort(x[above])
-        keep += [x, t, ob, oa]
-        rec['tids'], rec['values'], rec['n_obs'] = t.ctypes.data, x.ctypes.data, n
-        rec['side_order'] = (ob.ctypes.data, oa.ctypes.data)
-        rec['side_n'] = (len(ob), len(oa))
+        cols = hist.cat_columns(row.label)     # (the cache's column addresses: tids, raw values)
+        if cols is None:
+            t = np.ascontiguousarray(otids, dtype=np.int64)
+            x = np.ascontiguousarray(x, dtype=np.float64)
+            keep += [t, x]
+            ta, xa_ = t.__array_interface__['data'][0], x.__array_interface__['data'][0]
+        else:
+            ta, xa_ = cols[0], hist.coord_addr(row.label, row.dist)
+        keep += [ob, oa]
+        fv['tids'][ix], fv['values'][ix], fv['n_obs'][ix] = ta, xa_, n
+        so = fv['side_order']
+        so[ix, 0], so[ix, 1] = ob.__array_interface__['data'][0], oa.__array_interface__['data'][0]
+        sn = fv['side_n']
+        sn[ix, 0], sn[ix, 1] = len(ob), len(oa)
         return True
     # the labels the previous call had to fit here are fitted up front (the active
     # branch seldom changes between suggests): no refused first call

@@ -1,6 +1,7 @@
 """cProfile of the config-3 tree's rf-branch suggest (quantized labels at 2^20
 candidates): where the host time of a quantized suggest goes."""
 import cProfile
+import ctypes
 import os
 import pstats
 import sys
@@ -35,6 +36,29 @@ def main():
     prof, eng.profile = eng.profile, None
     for k, v in prof.items():
         print('  device stage %-10s %7.1f us (%d launches)' % (k, 1e3 * np.median([a[0] for a in v]), len(v)))
+    # host phases of the native call (tpe_host_phases) and numpy's argsort of
+    # the quantized labels' columns (the caller's part of their fits)
+    from hyperopt_amd import _native as N, history as H
+    buf = (ctypes.c_double * len(N.PHASES))()
+    eng.lib.tpe_host_phases(1, None, 0)
+    ph = []
+    for i in range(50):
+        tpe.suggest([bench.N_HISTORY], domain, trials, 700 + i, n_EI_candidates=bench.C_PER_GPU)
+        eng.lib.tpe_host_phases(1, buf, len(N.PHASES))
+        ph.append(list(buf))
+    eng.lib.tpe_host_phases(0, None, 0)
+    med = np.median(np.array(ph), axis=0)
+    print('  host phases (us since entry): ' + '  '.join('%s %.1f' % (k, v) for k, v in zip(N.PHASES, med)))
+    hist = H.extract(domain, trials)
+    for r in domain.table.rows:
+        if r.dist.startswith('q'):
+            x = np.asarray(hist.obs[r.label][1], dtype=np.float64)
+            ts = []
+            for _ in range(50):
+                s0 = time.perf_counter()
+                np.argsort(x)
+                ts.append(time.perf_counter() - s0)
+            print('  np.argsort %-16s n %6d: %6.1f us' % (r.label, len(x), 1e6 * np.median(ts)))
     pr = cProfile.Profile()
     pr.enable()
     for i in range(n):
