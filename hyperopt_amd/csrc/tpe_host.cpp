@@ -86,6 +86,9 @@ constexpr double kTabMinRatioFgt = 1.0;          // candidates per cell row for 
 constexpr int64_t kLogpolyMaxCells = 2048;
 constexpr int64_t kLpDirectRows = 64;       // a side of <= this many rows: direct sums, no moments
 constexpr int64_t kLpRowsPerWave = 5;       // ... kLpRowsPerWave cell rows per table-stage wave
+// a TPE_F_LOGPOLY row in cell rows: its above side's moments (one cell row)
+// plus the short below side's direct sums at the nodes (5 rows a wave) and the fit
+constexpr double kLpRowCost = 1.25;
 bool logpoly_enabled() {
   const char* e = getenv("TPE_LOGPOLY");
   return !(e && e[0] == '0');
@@ -402,7 +405,7 @@ void decide_table(const TabCtx& cx, int32_t li) {
     const double lp_ratio = dev_fit[li] ? cx.dv_ratio : kTabMinRatio;   // (moment cells, no boxes)
     // (box-moment labels keep moment cells: their above cells come from the boxes)
     if (cx.lp_on && nbox == 0 && n0 > 0 && n1 > 0 && nl <= kLogpolyMaxCells &&
-        ct >= lp_ratio * (double)(2 * nl)) {
+        ct >= lp_ratio * kLpRowCost * (double)nl) {
       // both sides' log-polynomials on one grid (the finer side's cells): one
       // row per candidate look-up (include/tpe_hip.h, TPE_F_LOGPOLY)
       tmode[li] = TPE_TAB_CELLS; tn0[li] = tn1[li] = nl;
@@ -1397,13 +1400,13 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   PACK_MARK("offsets");
   if (!blob || blob_cap < end) return TPE_E_SPACE;
   {
-    // the sections into the blob; a large level's in 256-KiB pieces on the
+    // the sections into the blob; a large level's in 64-KiB pieces on the
     // worker pool (a batched level packs megabytes of component rows)
     struct Piece { unsigned char* dst; const unsigned char* src; size_t n; };
     static thread_local std::vector<Piece> pieces_tl;
     std::vector<Piece>& pieces = pieces_tl;
     pieces.clear();
-    constexpr size_t kPiece = 256 << 10;
+    constexpr size_t kPiece = 64 << 10;
     size_t total = 0;
     for (int i = 0; i < NS; ++i) {
       if (!len[i] || !src[i]) continue;
@@ -1416,7 +1419,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       const Piece& q = (*(const std::vector<Piece>*)c)[(size_t)k];
       memcpy(q.dst, q.src, q.n);
     };
-    if (total >= (1u << 20) && pieces.size() > 1) tpe_pool::parallel_for((int)pieces.size(), copy, &pieces);
+    if (total >= (128u << 10) && pieces.size() > 1) tpe_pool::parallel_for((int)pieces.size(), copy, &pieces);
     else for (size_t k = 0; k < pieces.size(); ++k) copy(&pieces, (int)k);
   }
   PACK_MARK("copy");

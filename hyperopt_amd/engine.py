@@ -60,6 +60,7 @@ TAB_MAX_CELLS = 65536
 TAB_MAX_LATTICE = 1 << 18
 TAB_MIN_RATIO, TAB_MIN_RATIO_DEVFIT = 8.0, 64.0   # tpe_host.cpp kTabMinRatio*: candidates per cell row
 LOGPOLY_MAX_CELLS = 2048           # tpe_host.cpp kLogpolyMaxCells (TPE_F_LOGPOLY: one grid for both sides)
+LP_ROW_COST = 1.25                 # tpe_host.cpp kLpRowCost (a LOGPOLY row in cell rows)
 LP_DIRECT_ROWS = 64                # tpe_host.cpp kLpDirectRows
 LP_ROWS_PER_WAVE = 5               # tpe_host.cpp kLpRowsPerWave
 A_SCALE_LIT = 0.84932180028801907  # tpe_host.cpp kAScale (the same double)
@@ -96,7 +97,7 @@ def _tab_plan(lp, n_cand, f64):
         # (a device-fitted label takes box-moment cells when TPE_FGT allows: tpe_host.cpp)
         boxes = post.above_dev is not None and not os.environ.get('TPE_FGT', '1').startswith('0')
         if (not os.environ.get('TPE_LOGPOLY', '1').startswith('0') and not boxes and n0 > 0 and n1 > 0
-                and nl <= LOGPOLY_MAX_CELLS and ct >= ratio * 2 * nl):
+                and nl <= LOGPOLY_MAX_CELLS and ct >= ratio * LP_ROW_COST * nl):
             return dict(mode=N.TAB_CELLS, n=(nl, nl), lo=klo, hi=khi, lat_lo=0, logpoly=True)
         if 0 < n0 <= TAB_MAX_CELLS and 0 < n1 <= TAB_MAX_CELLS and ct >= ratio * (n0 + n1):
             return dict(mode=N.TAB_CELLS, n=(n0, n1), lo=klo, hi=khi, lat_lo=0)
