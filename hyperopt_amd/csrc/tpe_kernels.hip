@@ -1654,6 +1654,239 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 #endif
 }
 
+// ---- the fast sample kernel, small-workgroup form (k_sample_fast) ----
+// The production case of k_sample_tab<F32, true> (every tabulated problem a
+// TPE_F_LOGPOLY cells table, device draws, early selection, nothing per
+// candidate written) in 512-thread workgroups whose table takes only the
+// level's largest table in LDS (dynamic shared memory, tpe_batch.tab_fast rows)
+// and whose sampler rows are at most kFastSamp: three workgroups share a CU,
+// 24 waves instead of 16, and a workgroup's staging and barriers overlap the
+// others' candidate loops.  A thread's unit is two candidates (one Philox
+// block); a run's units (its consecutive tiles of one problem, 128 candidates
+// a unit) are handed out to the waves from an LDS counter.  Same draws, same
+// f32 arithmetic and same selection order as k_sample_tab's FAST pass.
+constexpr int kFastThreads = 512;
+constexpr int kFastSamp = 64;                  // sampler rows (below components) in LDS
+constexpr int kFastUnit = 128;                 // candidates a wave's unit covers (64 lanes x 2)
+constexpr int kFastWgsPerCu = 3;
+constexpr int kFastMaxCells = 896;             // 42 KiB of table rows: three workgroups' LDS in a CU
+static_assert(kTile % kFastUnit == 0, "fast units tile the tiles");
+
+__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(6)))
+void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict__ tiles,
+                   const int32_t* __restrict__ list, int n_list, int per_wg, const double* __restrict__ samp,
+                   const float4* __restrict__ comp32, const float4* __restrict__ tab,
+                   tpe_result* __restrict__ run_best, int tpp) {
+  extern __shared__ float4 fast_tab[];                       // the label's LOGPOLY rows (tab_fast of them at most)
+  __shared__ double cum_lds[kFastSamp];
+  __shared__ float4 row_lds[kFastSamp];
+  __shared__ GuideEnt guide[kGuide];
+  constexpr int kW = kFastThreads / 64;
+  struct RunRec { int64_t cand_base; double bb, ab; int tile, logc; };
+  __shared__ RunRec s_run[kTabMaxTilesPerWg];
+  __shared__ unsigned long long s_rk[kTabMaxTilesPerWg][kW];
+  __shared__ float s_rv[kTabMaxTilesPerWg][3][kW];
+  __shared__ int s_tile[kTabMaxTilesPerWg], s_prob[kTabMaxTilesPerWg], s_start[kTabMaxTilesPerWg];
+  __shared__ int s_unit[kTabMaxTilesPerWg];
+  const int lane = threadIdx.x & 63;
+  int st_samp = -1, st_len = -1, st_t0 = -1, st_n0 = -1;
+  int n_def = 0;                                             // runs so far (workgroup-uniform)
+  float fd = 0.f, flb = 0.f, fla = 0.f, ft = 0.f;
+  int fi = -1;
+  if ((int)threadIdx.x < kTabMaxTilesPerWg) s_unit[threadIdx.x] = 0;
+  const int n_my = min(per_wg, n_list - (int)blockIdx.x * per_wg);
+  if ((int)threadIdx.x < n_my) {
+    const int li = (int)blockIdx.x * per_wg + (int)threadIdx.x;
+    const int tile = list ? list[li] : li;
+    s_tile[threadIdx.x] = tile;
+    if (tpp > 0) {
+      const int r = tile / tpp;
+      s_prob[threadIdx.x] = r; s_start[threadIdx.x] = (tile - r * tpp) * kTile;
+    } else {
+      const tpe_tile tl = tiles[tile];
+      s_prob[threadIdx.x] = tl.problem; s_start[threadIdx.x] = tl.cand_start;
+    }
+  }
+  __syncthreads();
+  for (int gi = 0; gi < n_my;) {
+    const int tile = __builtin_amdgcn_readfirstlane(s_tile[gi]), pid = __builtin_amdgcn_readfirstlane(s_prob[gi]);
+    int gk = gi;                                             // the run: tiles gi .. gk, one problem
+    while (gk + 1 < n_my && __builtin_amdgcn_readfirstlane(s_prob[gk + 1]) == pid) ++gk;
+    const tpe_problem& p = P[pid];
+    bool staged = false;
+    double scum = 0.0;
+    float4 srow = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool same = p.samp_off == st_samp && p.samp_len == st_len && p.tab_off[0] == st_t0 && p.tab_n[0] == st_n0;
+    if (!same) {
+      st_samp = p.samp_off; st_len = p.samp_len; st_t0 = p.tab_off[0]; st_n0 = p.tab_n[0];
+      __syncthreads();                                       // LDS free for the next label's rows
+      if ((int)threadIdx.x < p.samp_len) {
+        const double* sr = samp + 8 * (int64_t)p.samp_off + 8 * (int)threadIdx.x;
+        scum = sr[0];
+        const float sg = (float)sr[2];
+        srow = make_float4((float)sr[1], sr[5] != 0.0 ? -sg : sg, (float)sr[3], (float)sr[4]);
+      }
+      // the table rows by LDS-DMA, every round's loads issued before the one
+      // wait (the last round's lanes past the rows: a clamped load, unused slots)
+      const int nu = TPE_TAB_ROW_UNITS * p.tab_n[0];
+      const int wv = (int)(threadIdx.x >> 6);
+      for (int u = 0; u * kFastThreads < nu; ++u) {
+        const int q = min(u * kFastThreads + (int)threadIdx.x, nu - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(tab + (int64_t)p.tab_off[0] + q),
+                                         (__attribute__((address_space(3))) void*)(fast_tab + u * kFastThreads + 64 * wv),
+                                         16, 0, 0);
+      }
+      staged = true;
+    }
+    if (threadIdx.x == 0)
+      s_run[n_def] = RunRec{(int64_t)p.cand_base, p.below_base, p.above_base, tile, p.family == TPE_FAM_LOGGAUSS ? 1 : 0};
+    const int nunits = (gk - gi + 1) * (kTile / kFastUnit);
+    float lo_f, hi_f;
+    f32_bounds(p, lo_f, hi_f);
+    const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0];
+    const float w0 = 1.f / inv0, ih0 = 1.f / (0.5f * w0);
+    const int n0 = p.tab_n[0];
+    bool first_unit = true;
+    for (;;) {
+      int u = 0;
+      if (lane == 0) u = atomicAdd(&s_unit[n_def], 1);
+      u = __builtin_amdgcn_readlane(u, 0);
+      // (a wave without a unit still takes part in the staging barriers below)
+      const bool have = u < nunits;
+      constexpr int kUnitsPerTile = kTile / kFastUnit;
+      const int ut = have ? u / kUnitsPerTile : 0;
+      const int first = __builtin_amdgcn_readfirstlane(s_start[gi + ut]) + kFastUnit * (u - ut * kUnitsPerTile) + 2 * lane;
+      uint32_t ws[2];
+      float uf[2], tj[2];
+      if (have) {
+        const uint64_t g0 = (uint64_t)p.cand_base + (uint64_t)first;
+        if ((g0 & 1) == 0) {
+          const uint64_t blk = g0 >> 1;
+          const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+          ws[0] = r.x; uf[0] = u01f(r.y);
+          ws[1] = r.z; uf[1] = u01f(r.w);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const DrawU d = draw_uniforms(p, first + j, TPE_PREC_F32);
+            ws[j] = d.ws; uf[j] = d.uf;
+          }
+        }
+      }
+      if (first_unit && staged) {
+        if ((int)threadIdx.x < p.samp_len) { cum_lds[threadIdx.x] = scum; row_lds[threadIdx.x] = srow; }
+        __syncthreads();
+        if (threadIdx.x < kGuide) {                  // first k with cum_k > b / kGuide, its two steps
+          const double v = (double)threadIdx.x / (double)kGuide;
+          const int len = p.samp_len;
+          int a = 0, b = len - 1;
+          while (a < b) { const int m = (a + b) >> 1; if (v < cum_lds[m]) b = m; else a = m + 1; }
+          GuideEnt e;
+          e.k0 = a;
+          e.never = 0u;
+          e.t0 = guide_thresh(a < len - 1 ? cum_lds[a] : INFINITY, e.never, 1u);
+          e.t1 = guide_thresh(a + 1 < len - 1 ? cum_lds[a + 1] : INFINITY, e.never, 2u);
+          guide[threadIdx.x] = e;
+        }
+        __builtin_amdgcn_s_waitcnt(0);               // (the LDS-DMA loads: vmcnt)
+        __syncthreads();
+      }
+      first_unit = false;
+      if (!have) break;
+      {
+        int kc[2];
+        unsigned more = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          bool m;
+          kc[j] = guided_comp(guide, ws[j], m);
+          more |= (unsigned)m << j;
+        }
+        if (__ballot(more != 0u)) {                 // (rare: a guide slice with 2+ component edges)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            if ((more >> j) & 1u) kc[j] = guided_more(cum_lds, p.samp_len, u01w(ws[j]), kc[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 sv = row_lds[kc[j]];
+          const float pr = sv.z + uf[j] * (sv.w - sv.z);
+          const float z = ndtri_f32(pr);
+          const float xf = sv.x + sv.y * z;
+          tj[j] = fminf(fmaxf(xf == xf ? xf : sv.x, lo_f), hi_f);
+        }
+      }
+      uint32_t exact = 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = first + j;
+        float lb2, la2;
+        lp_log2(lo0, inv0, w0, ih0, n0, fast_tab, tj[j], lb2, la2);
+        const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
+        exact |= (unsigned)(valid && !ok) << j;
+        const float d = lb2 - la2;
+        if (valid && ok && better32(d, i, fd, fi)) { fd = d; fi = i; flb = lb2; fla = la2; ft = tj[j]; }
+      }
+      // outside the cells or in flagged ones: summed exactly by the whole wave
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        unsigned long long need = __ballot((exact >> j) & 1u);
+        while (need) {
+          const int src = __builtin_ctzll(need);
+          need &= need - 1;
+          const float t = __shfl(tj[j], src);
+          float lb2, la2;
+          lp_log2(lo0, inv0, w0, ih0, n0, fast_tab, t, lb2, la2);
+          if (!(lb2 == lb2)) lb2 = lse2_wave(comp32, p.below_off, p.below_len, 0, 0, t);
+          if (!(la2 == la2)) la2 = lse2_wave(comp32, p.above_off, p.above_len, p.wide_off, p.wide_len, t);
+          const int i = __shfl(first, src) + j;
+          const float d = lb2 - la2;
+          if (lane == src && better32(d, i, fd, fi)) { fd = d; fi = i; flb = lb2; fla = la2; ft = t; }
+        }
+      }
+    }
+    // the run's best of this wave: better32's order as one key (DPP max); the
+    // winning lane (indices are unique) leaves its log2 sums and draw
+    {
+      int tid = (int)threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      const int wave = tid >> 6;
+      const unsigned long long key = key32(fd, fi);
+      const unsigned long long wk = __ockl_wfred_max_u64(key);
+      if (wk != 0ull && key == wk) { s_rv[n_def][0][wave] = flb; s_rv[n_def][1][wave] = fla; s_rv[n_def][2][wave] = ft; }
+      if ((tid & 63) == 0) s_rk[n_def][wave] = wk;
+      fi = -1;
+    }
+    ++n_def;
+    gi = gk + 1;
+  }
+  // the runs: wave r combines run r into its record (host-visible)
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  for (int r = wave; r < n_def; r += kW) {
+    const unsigned long long k2 = lane < kW ? s_rk[r][lane] : 0ull;
+    const unsigned long long bk = __ockl_wfred_max_u64(k2);
+    const unsigned long long m2 = __ballot(bk != 0ull && k2 == bk);
+    const int w2 = m2 ? (int)__builtin_ctzll(m2) : 0;
+    const int i2 = bk != 0ull ? (int)~(uint32_t)bk : -1;
+    if (lane == 0) {
+      const RunRec rr = s_run[r];
+      tpe_result res;
+      res.score = 0.0; res.l = 0.0; res.g = 0.0; res.idx = i2; res.value = 0.0; res.global_idx = -1;
+      if (i2 >= 0) {
+        const float t = s_rv[r][2][w2];
+        const double lnx = rr.logc ? (double)t : 0.0;
+        res.l = (double)s_rv[r][0][w2] * kLn2 + rr.bb - lnx;
+        res.g = (double)s_rv[r][1][w2] * kLn2 + rr.ab - lnx;
+        res.score = res.l - res.g;
+        res.value = rr.logc ? exp_call((double)t) : (double)t;
+        res.global_idx = rr.cand_base + i2;
+      }
+      run_best[rr.tile] = res;
+    }
+  }
+}
+
 // row of `part` a work item writes: its tile's first work item + its split
 __device__ __forceinline__ int64_t part_row(const tpe_problem* __restrict__ P, const tpe_tile* __restrict__ tiles,
                                             const tpe_work& w) {
@@ -4165,8 +4398,17 @@ bool tab_fast_disabled() {
 
 // tabulated tiles per sample-stage workgroup (the early selection's run
 // enumeration on the host uses the same partition)
-int tab_tiles_per_wg(int n_tab) {
-  return std::min(kTabMaxTilesPerWg, std::max(1, (n_tab + cu_count() - 1) / cu_count()));
+int tab_tiles_per_wg(int n_tab, int wgs_per_cu) {
+  const int slots = cu_count() * wgs_per_cu;
+  return std::min(kTabMaxTilesPerWg, std::max(1, (n_tab + slots - 1) / slots));
+}
+// sample-stage workgroups a CU holds: k_sample_fast's three (tab_fast >= 2), else one
+int tab_wgs_per_cu(const tpe_batch* b) { return b->tab_fast >= 2 ? kFastWgsPerCu : 1; }
+
+// TPE_SAMPLE_FAST2=0: k_sample_tab's FAST pass instead of k_sample_fast (A/B, tests)
+bool fast2_disabled() {
+  static const int v = [] { const char* e = getenv("TPE_SAMPLE_FAST2"); return e && e[0] == '0' ? 1 : 0; }();
+  return v != 0;
 }
 
 // np.argmax order of (score, index) on the host: better() of the kernels
@@ -4317,11 +4559,17 @@ int tpe_sample(const tpe_batch* b, void* stream) {
   if (n_tab > 0) {
     if (!b->tab) return fail(TPE_E_ARG, "tabulated tiles without score tables");
     // one workgroup per CU-sized group of tiles (each stages its problem once)
-    const int per = tab_tiles_per_wg(n_tab);
+    const int per = tab_tiles_per_wg(n_tab, tab_wgs_per_cu(b));
     const int wgs = (n_tab + per - 1) / per;
     tpe_result* run_best = b->early_select ? b->run_best : nullptr;
-    if (b->tab_fast && run_best && b->precision == TPE_PREC_F32 && b->sample && !b->l_out &&
-        !(b->flags & TPE_BATCH_WRITE_CAND))
+    const bool fast = b->tab_fast && run_best && b->precision == TPE_PREC_F32 && b->sample && !b->l_out &&
+                      !(b->flags & TPE_BATCH_WRITE_CAND);
+    if (fast && b->tab_fast >= 2) {
+      if (b->tab_fast - 1 > kFastMaxCells) return fail(TPE_E_ARG, "tpe_sample: tab_fast rows past the fast kernel's LDS");
+      TPE_LAUNCH(k_sample_fast, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48, (hipStream_t)stream,
+                 b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, (const float4*)b->comp32,
+                 (const float4*)b->tab, run_best, b->tiles_per_problem);
+    } else if (fast)
       TPE_LAUNCH((k_sample_tab<TPE_PREC_F32, true>), dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
@@ -4730,13 +4978,18 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     bool fast = fast_ok;
     const tpe_problem* rows = hp ? hp : xtmpl;
     const int64_t n_rows = hp ? P : (xtmpl ? info.n_expand : 0);
+    int max_cells = 0, max_samp = 0;
     for (int64_t r = 0; fast && r < n_rows; ++r) {
       const tpe_problem& q = rows[r];
       if (q.tab_mode == TPE_TAB_NONE) continue;
       fast = q.tab_mode == TPE_TAB_CELLS && (q.flags & TPE_F_LOGPOLY) && q.tab_n[0] <= kTabLdsCells &&
              q.samp_len > 0 && q.samp_len <= kCumLds;
+      max_cells = std::max(max_cells, q.tab_n[0]);
+      max_samp = std::max(max_samp, q.samp_len);
     }
-    b.tab_fast = fast && n_rows > 0 ? 1 : 0;
+    // (the small-workgroup kernel when the level's tables and sampler rows fit its LDS)
+    const bool fast2 = fast && !fast2_disabled() && max_cells <= kFastMaxCells && max_samp <= kFastSamp;
+    b.tab_fast = fast && n_rows > 0 ? (fast2 ? 1 + max_cells : 1) : 0;
   }
   b.result = rd ? rd : ws->result;
   // device exchange (sharded level over RCCL): run records and results in
@@ -4776,7 +5029,7 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     // run-record area is free in this mode): its runs are enumerated on the
     // device as the host reduction below enumerates them
     int32_t* span = (int32_t*)(host + rb_off);
-    const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab);
+    const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab, tab_wgs_per_cu(&b));
     if (xtmpl) {                                     // expanded: every problem's tiles, in order
       for (int64_t r = 0; r < P; ++r) { span[2 * r] = (int32_t)(r * n_tiles_p); span[2 * r + 1] = (int32_t)n_tiles_p; }
     } else {
@@ -4824,7 +5077,7 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     const tpe_tile* tl = xtmpl ? nullptr : (const tpe_tile*)(host + info.off_tiles);
     auto tile_of = [&](int i) { return list ? list[i] : i; };
     auto prob_of = [&](int t) { return tl ? tl[t].problem : (int)(t / n_tiles_p); };
-    const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab);
+    const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab, tab_wgs_per_cu(&b));
     if (xtmpl && n_tiles_p > 0 && per % n_tiles_p == 0) {
       // expanded level (every problem tabulated, tiles in order) whose workgroups
       // hold whole problems: each problem is one run, recorded at its first

@@ -423,11 +423,13 @@ typedef struct tpe_batch {
   int64_t fit_max_obs;        /* most observations of one job                       */
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
   double* draw_pref; int64_t draw_blocks; int32_t n_sorted;
-  int32_t tab_fast;      /* 1: every tabulated problem is TPE_TAB_CELLS with both tables within the sample
-                            stage's LDS (tab_n[0] + tab_n[1] <= 2048) and 1..TPE_SAMPLE_LDS_ROWS sampler
-                            rows, the candidates are device-drawn at TPE_PREC_F32, early selection is on
-                            and nothing per candidate is written: the sample stage's specialised kernel
-                            (tpe_level_run sets it; 0: the general one) */
+  int32_t tab_fast;      /* >= 1: every tabulated problem is a TPE_F_LOGPOLY cells table within the sample
+                            stage's LDS (tab_n[0] <= 2048) with 1..TPE_SAMPLE_LDS_ROWS sampler rows, the
+                            candidates are device-drawn at TPE_PREC_F32, early selection is on and nothing
+                            per candidate is written: the sample stage's specialised kernel — 1: in
+                            1024-thread workgroups; 1 + R (R <= 896 table rows, <= 64 sampler rows): in
+                            512-thread workgroups taking R rows of LDS, three a CU (tpe_level_run sets it;
+                            0: the general kernel) */
   unsigned long long* pool_best;   /* [n_problems] (pooled problems; see "Pooled labels") */
   /* tabulated scoring: table jobs and the table storage (16-B units) */
   const tpe_tab_job* tab_jobs; int32_t n_tab_jobs; int32_t tab_blocks;
