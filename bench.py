@@ -13,7 +13,8 @@ value  = sum over steps of (active hyperparameters x total candidates) / time
 roofline: the dominant stage by device time (k_sample_tab on config 3),
           timed per launch with HIP events the level runner records on its own
           stream (tpe_level_profile), priced by the ALGORITHMIC VALU work of its
-          candidates (TAB_CAND_OPS per candidate) against the issue peak; the
+          candidates (TAB_CAND_OPS, or TAB_CAND_OPS_LOGPOLY for the format the
+          labels tabulate in, per candidate) against the issue peak; the
           executed-instruction fraction (SQ_INSTS_VALU of a separate PMC pass of
           the same build, pmc_stale flags a mismatch) beside it.
 cpu_baseline: the CPU oracle (numpy restatement of the reference) on a bounded
@@ -184,7 +185,7 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 # x 4 SIMDs x 256 CUs x 2.4 GHz
 PEAK_VALU_GINST = 0.5 * 4 * 256 * 2.4      # = 1228.8 G wave-instructions/s
 # counter summary of the same bench command (tools/gpu.sh pmc -> tools/pmc_summary.py)
-PMC_SUMMARY_REL = 'profiles/r03_pmc_summary.json'
+PMC_SUMMARY_REL = 'profiles/r04_pmc_summary.json'
 PMC_SUMMARY = os.path.join(ROOT, PMC_SUMMARY_REL)
 VALU_KERNELS = ('k_sample', 'k_tables', 'k_select', 'above', 'k_finalize')
 
@@ -206,6 +207,39 @@ TAB_CAND_OPS = {
     'compare': 6,        # l2 - g2, flag tests, running best (value, index)
 }
 TAB_CAND_OPS_TOTAL = sum(TAB_CAND_OPS.values())
+# ... the same with TPE_F_LOGPOLY rows (include/tpe_hip.h "Tabulated scoring"),
+# the format the headline's labels tabulate in: one cell look-up for both
+# sides, two degree-5 polynomials that are the log2 sums themselves
+TAB_CAND_OPS_LOGPOLY = dict(TAB_CAND_OPS, cells=13, horner=10, log2=0)
+
+
+def tab_format(domain, trials, n_cand):
+    """'logpoly' when every tabulated label of the headline suggest's level
+    packs TPE_F_LOGPOLY rows (tpe_host_pack_level on the host, as the suggest
+    packs it), else 'moments' — the format whose operations price the sample
+    stage's algorithmic work."""
+    import ctypes
+    from hyperopt_amd import _native as N, history as H, tpe
+    from hyperopt_amd.engine import Engine, LevelProblem
+    lib = N.load()
+    T = domain.table
+    hist = H.extract(domain, trials)
+    below = H.split_below(hist, 0.25)
+    fits = tpe._Fits(T, hist, below, 1.0, None)
+    rows = [T.by_label[k] for k in ('model', 'svm_kernel', 'svm_C', 'svm_rbf_gamma')]
+    ids = np.array([len(hist)], dtype=np.int64)
+    problems = [LevelProblem(fits.get(r), r.index, ids) for r in rows]
+    recs, keep = Engine._labels(problems)
+    info = N.PackInfo()
+    cap = 64 << 20
+    blob = np.empty(cap, dtype=np.uint8)
+    rc = lib.tpe_host_pack_level(recs, len(problems), int(n_cand), 7, 0, 0, N.PREC_F32, blob.ctypes.data, cap,
+                                 ctypes.byref(info))
+    if rc != 0:
+        return 'moments'
+    prob = np.frombuffer(blob, dtype=N.PROBLEM_DTYPE, count=int(info.n_problems), offset=int(info.off_problems))
+    tab = prob[prob['tab_mode'] == N.TAB_CELLS]
+    return 'logpoly' if len(tab) and np.all(tab['flags'] & N.F_LOGPOLY) else 'moments'
 
 
 def lib_hash(path=LIB_PATH):
@@ -224,7 +258,7 @@ def _pmc():
 
 
 # a profiled stage and the kernels it launches (counters are summed per dispatch)
-STAGE_KERNELS = {'k_sample': ('k_sample', 'k_sample_tab'),
+STAGE_KERNELS = {'k_sample': ('k_sample', 'k_sample_tab', 'k_sample_fast'),
                  'above': ('k_above_f32', 'k_above_f64', 'k_above_q')}
 
 
@@ -235,7 +269,7 @@ def _stage_counters(pmc, stage):
     return {c: sum(p.get(c, 0.0) for p in parts) for c in set().union(*parts) if c != 'dispatches'}
 
 
-def roofline(prof):
+def roofline(prof, fmt='moments'):
     """Roofline of every measured stage and of the dominant one (largest total
     device time): work per launch / the launch's average duration, the
     duration timed live with HIP events on the engine stream.
@@ -266,12 +300,13 @@ def roofline(prof):
             # tabulated scoring: the algorithmic VALU work of the candidates
             # (TAB_CAND_OPS per candidate) / the launch time / the issue peak
             cands = float(np.mean([r[1] for r in recs]))
-            alg = cands * TAB_CAND_OPS_TOTAL / 64.0
+            ops = TAB_CAND_OPS_LOGPOLY if fmt == 'logpoly' else TAB_CAND_OPS
+            alg = cands * sum(ops.values()) / 64.0
             ach = alg / (ms.mean() * 1e-3) / 1e9
             k.update(bound='valu', achieved=ach, peak=PEAK_VALU_GINST, unit='G VALU wave-instructions/s',
-                     frac=ach / PEAK_VALU_GINST, work='algorithmic',
+                     frac=ach / PEAK_VALU_GINST, work='algorithmic', table_format=fmt,
                      algorithmic_valu_per_launch=alg, candidates_per_launch=cands,
-                     ops_per_candidate=TAB_CAND_OPS_TOTAL, ops_model=TAB_CAND_OPS)
+                     ops_per_candidate=sum(ops.values()), ops_model=ops)
             if 'SQ_INSTS_VALU' in c:
                 inst = float(c['SQ_INSTS_VALU'])
                 exe = inst / (ms.mean() * 1e-3) / 1e9
@@ -529,7 +564,7 @@ def main():
     torch.cuda.synchronize()
     prof = eng.profile
     eng.profile = None
-    roof, kernels = roofline(prof)
+    roof, kernels = roofline(prof, tab_format(domain, trials, C_total))
     stages = {k: float(np.mean([a[0] for a in v])) for k, v in prof.items()}
 
 

@@ -1668,11 +1668,17 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 constexpr int kFastThreads = 512;
 constexpr int kFastSamp = 64;                  // sampler rows (below components) in LDS
 constexpr int kFastUnit = 128;                 // candidates a wave's unit covers (64 lanes x 2)
-constexpr int kFastWgsPerCu = 3;
+#ifndef TPE_FAST_WPC
+#define TPE_FAST_WPC 3
+#endif
+constexpr int kFastWgsPerCu = TPE_FAST_WPC;
 constexpr int kFastMaxCells = 896;             // 42 KiB of table rows: three workgroups' LDS in a CU
 static_assert(kTile % kFastUnit == 0, "fast units tile the tiles");
 
-__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(6)))
+#ifndef TPE_FAST_WAVES
+#define TPE_FAST_WAVES 6
+#endif
+__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(TPE_FAST_WAVES)))
 void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict__ tiles,
                    const int32_t* __restrict__ list, int n_list, int per_wg, const double* __restrict__ samp,
                    const float4* __restrict__ comp32, const float4* __restrict__ tab,

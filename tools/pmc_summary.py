@@ -8,7 +8,8 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ('k_above_f32', 'k_above_f64', 'k_above_q', 'k_sample_tab', 'k_sample', 'k_tables', 'k_finalize', 'k_select',
+    for k in ('k_above_f32', 'k_above_f64', 'k_above_q', 'k_sample_fast', 'k_sample_tab', 'k_sample', 'k_tables',
+              'k_finalize', 'k_select',
               'k_fit_stats', 'k_fit_emit', 'k_fit_combine', 'k_fit_wide', 'k_ord_chunks', 'k_ord_merge', 'k_ord_below',
               'k_ord_compact', 'k_upload'):
         if k in name:
@@ -31,7 +32,7 @@ def main(root):
     # exact for 16-B stores).  'sort' = every rocPRIM dispatch of one tpe_sort
     # call; the bench makes one sort per suggest, i.e. per k_select dispatch.
     traffic = {}
-    for k in ('k_above_f32', 'k_sample', 'k_sample_tab', 'k_tables', 'k_finalize', 'k_select'):
+    for k in ('k_above_f32', 'k_sample', 'k_sample_fast', 'k_sample_tab', 'k_tables', 'k_finalize', 'k_select'):
         a = out.get(k, {})
         if 'FETCH_SIZE' in a and 'WRITE_SIZE' in a:
             traffic[k] = dict(kernel=k, fetch_kb=a['FETCH_SIZE'], write_kb=a['WRITE_SIZE'],
