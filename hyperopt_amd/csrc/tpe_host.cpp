@@ -364,6 +364,8 @@ struct TabCtx {
   char* logpoly;
 };
 
+constexpr int32_t kTabChunk = 16;
+
 void decide_table(const TabCtx& cx, int32_t li) {
   const tpe_label_in* labels = cx.labels;
   const char* dev_fit = cx.dev_fit;
@@ -937,9 +939,15 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     // components per label make a worker's hand-off worth it)
     int64_t comps = 0;
     for (int32_t li = 0; li < n_labels; ++li) comps += labels[li].above_k;
+    // (in chunks of kTabChunk labels: a thousand-label level's decisions are
+    // sub-microsecond each, too small to hand out one by one)
+    struct Chunked { const TabCtx* cx; int32_t n; };
+    const Chunked ch{&tcx, n_labels};
     if (n_labels >= 2 && comps >= 16384)
-      tpe_pool::parallel_for(n_labels, [](void* c, int i) { decide_table(*(const TabCtx*)c, (int32_t)i); },
-                             (void*)&tcx);
+      tpe_pool::parallel_for((n_labels + kTabChunk - 1) / kTabChunk, [](void* c, int k) {
+        const Chunked& q = *(const Chunked*)c;
+        for (int32_t li = k * kTabChunk; li < std::min(q.n, (k + 1) * kTabChunk); ++li) decide_table(*q.cx, li);
+      }, (void*)&ch);
     else
       for (int32_t li = 0; li < n_labels; ++li) decide_table(tcx, li);
   }
@@ -1019,6 +1027,12 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   std::vector<tpe_fit_job> fit;
   std::vector<int32_t> below_idx;
   std::vector<int64_t> fit_seg(1, 0);
+  {
+    int64_t nf = 0, nb = 0;
+    for (int32_t li = 0; li < n_labels; ++li)
+      if (dev_fit[li]) { ++nf; nb += std::max<int32_t>(labels[li].n_below, 0); }
+    fit.reserve((size_t)nf); below_idx.reserve((size_t)nb + 1); fit_seg.reserve((size_t)nf + 1);
+  }
   int64_t dev_rows = 0, dev_grid = 0, fit_max_new = 0, fit_max_obs = 0;
   {
     int64_t r = 0;
