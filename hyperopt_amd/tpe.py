@@ -608,9 +608,14 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     # the device-fitted labels that ran hold their merged value orders now (a
     # label the call took a host fit for, give(), did not run the device fit:
     # its order buffers were not written)
-    for ix, (order, n) in tl[2].items():
-        if used[ix] and ix not in host:
-            order.commit(n)
+    # (a call on the same records, branch and host fits as the last committed one
+    # finds every order already at its length: nothing to walk)
+    done = getattr(table, '_committed', None)
+    if tl[2] and (host or done is None or done[0] is not tl[0] or done[1] is not table._used_list):
+        for ix, (order, n) in tl[2].items():
+            if used[ix] and ix not in host:
+                order.commit(n)
+        table._committed = None if host else (tl[0], table._used_list)
     if columns:
         return ChoiceColumns(table.labels, values.copy(), np.asarray(active, dtype=bool))
     order = table.level_order()
