@@ -1667,22 +1667,23 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 // f32 arithmetic and same selection order as k_sample_tab's FAST pass.
 constexpr int kFastThreads = 512;
 constexpr int kFastSamp = 64;                  // sampler rows (below components) in LDS
-constexpr int kFastUnit = 128;                 // candidates a wave's unit covers (64 lanes x 2)
+// (a thread's unit: NP candidates, NP / 2 Philox blocks; a wave's covers 64 NP)
 #ifndef TPE_FAST_WPC
 #define TPE_FAST_WPC 3
 #endif
 constexpr int kFastWgsPerCu = TPE_FAST_WPC;
 constexpr int kFastMaxCells = 896;             // 42 KiB of table rows: three workgroups' LDS in a CU
-static_assert(kTile % kFastUnit == 0, "fast units tile the tiles");
-
-#ifndef TPE_FAST_WAVES
-#define TPE_FAST_WAVES 6
-#endif
-__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(TPE_FAST_WAVES)))
+// NP = 2: 80 VGPRs, six waves a SIMD (three workgroups a CU: batched levels);
+// NP = 4: two candidate pairs in flight per lane for levels of at most two
+// workgroups a CU (config 3's 2^21 candidates), four waves a SIMD
+template <int NP>
+__global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(NP == 2 ? 6 : 4)))
 void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict__ tiles,
                    const int32_t* __restrict__ list, int n_list, int per_wg, const double* __restrict__ samp,
                    const float4* __restrict__ comp32, const float4* __restrict__ tab,
                    tpe_result* __restrict__ run_best, int tpp) {
+  constexpr int kFastUnit = 64 * NP;
+  static_assert(NP % 2 == 0 && kTile % kFastUnit == 0, "fast units: Philox pairs tiling the tiles");
   extern __shared__ float4 fast_tab[];                       // the label's LOGPOLY rows (tab_fast of them at most)
   __shared__ double cum_lds[kFastSamp];
   __shared__ float4 row_lds[kFastSamp];
@@ -1752,28 +1753,48 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
     const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0];
     const float w0 = 1.f / inv0, ih0 = 1.f / (0.5f * w0);
     const int n0 = p.tab_n[0];
+    // a run whose tiles are one candidate range (the packer's order): wave w takes
+    // units w, w + kW, ... with no LDS traffic for the hand-out or the addresses
+    // (TPE_FAST_DYNAMIC builds: units from an LDS counter, as k_sample_tab)
+    const int start0 = __builtin_amdgcn_readfirstlane(s_start[gi]);
+#ifndef TPE_FAST_DYNAMIC
+    const int ntl = gk - gi + 1;
+    const int tl = min(lane, ntl - 1);
+    const bool contig = __ballot(s_start[gi + tl] != start0 + tl * kTile) == 0ull;
+    const int wave0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#else
+    constexpr bool contig = false;
+    const int wave0 = 0;
+#endif
     bool first_unit = true;
-    for (;;) {
-      int u = 0;
-      if (lane == 0) u = atomicAdd(&s_unit[n_def], 1);
-      u = __builtin_amdgcn_readlane(u, 0);
+    for (int k = 0;; ++k) {
+      int u = wave0 + k * kW;
+      if (!contig) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(&s_unit[n_def], 1);
+        u = __builtin_amdgcn_readlane(v, 0);
+      }
       // (a wave without a unit still takes part in the staging barriers below)
       const bool have = u < nunits;
       constexpr int kUnitsPerTile = kTile / kFastUnit;
       const int ut = have ? u / kUnitsPerTile : 0;
-      const int first = __builtin_amdgcn_readfirstlane(s_start[gi + ut]) + kFastUnit * (u - ut * kUnitsPerTile) + 2 * lane;
-      uint32_t ws[2];
-      float uf[2], tj[2];
+      const int first = (contig ? start0 + ut * kTile : __builtin_amdgcn_readfirstlane(s_start[gi + ut])) +
+                        kFastUnit * (u - ut * kUnitsPerTile) + NP * lane;
+      uint32_t ws[NP];
+      float uf[NP], tj[NP];
       if (have) {
         const uint64_t g0 = (uint64_t)p.cand_base + (uint64_t)first;
         if ((g0 & 1) == 0) {
-          const uint64_t blk = g0 >> 1;
-          const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-          ws[0] = r.x; uf[0] = u01f(r.y);
-          ws[1] = r.z; uf[1] = u01f(r.w);
+#pragma unroll
+          for (int j = 0; j < NP; j += 2) {
+            const uint64_t blk = (g0 + (uint64_t)j) >> 1;
+            const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+            ws[j] = r.x; uf[j] = u01f(r.y);
+            ws[j + 1] = r.z; uf[j + 1] = u01f(r.w);
+          }
         } else {
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < NP; ++j) {
             const DrawU d = draw_uniforms(p, first + j, TPE_PREC_F32);
             ws[j] = d.ws; uf[j] = d.uf;
           }
@@ -1800,21 +1821,21 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
       first_unit = false;
       if (!have) break;
       {
-        int kc[2];
+        int kc[NP];
         unsigned more = 0;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NP; ++j) {
           bool m;
           kc[j] = guided_comp(guide, ws[j], m);
           more |= (unsigned)m << j;
         }
         if (__ballot(more != 0u)) {                 // (rare: a guide slice with 2+ component edges)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NP; ++j)
             if ((more >> j) & 1u) kc[j] = guided_more(cum_lds, p.samp_len, u01w(ws[j]), kc[j]);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NP; ++j) {
           const float4 sv = row_lds[kc[j]];
           const float pr = sv.z + uf[j] * (sv.w - sv.z);
           const float z = ndtri_f32(pr);
@@ -1824,7 +1845,7 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
       }
       uint32_t exact = 0;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NP; ++j) {
         const int i = first + j;
         float lb2, la2;
         lp_log2(lo0, inv0, w0, ih0, n0, fast_tab, tj[j], lb2, la2);
@@ -1835,7 +1856,7 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
       }
       // outside the cells or in flagged ones: summed exactly by the whole wave
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NP; ++j) {
         unsigned long long need = __ballot((exact >> j) & 1u);
         while (need) {
           const int src = __builtin_ctzll(need);
@@ -4411,6 +4432,12 @@ int tab_tiles_per_wg(int n_tab, int wgs_per_cu) {
 // sample-stage workgroups a CU holds: k_sample_fast's three (tab_fast >= 2), else one
 int tab_wgs_per_cu(const tpe_batch* b) { return b->tab_fast >= 2 ? kFastWgsPerCu : 1; }
 
+// TPE_FAST_NP2=1: k_sample_fast's two-candidate units on every level (A/B)
+bool fast_np2_forced() {
+  static const int v = [] { const char* e = getenv("TPE_FAST_NP2"); return e && e[0] == '1' ? 1 : 0; }();
+  return v != 0;
+}
+
 // TPE_SAMPLE_FAST2=0: k_sample_tab's FAST pass instead of k_sample_fast (A/B, tests)
 bool fast2_disabled() {
   static const int v = [] { const char* e = getenv("TPE_SAMPLE_FAST2"); return e && e[0] == '0' ? 1 : 0; }();
@@ -4572,9 +4599,15 @@ int tpe_sample(const tpe_batch* b, void* stream) {
                       !(b->flags & TPE_BATCH_WRITE_CAND);
     if (fast && b->tab_fast >= 2) {
       if (b->tab_fast - 1 > kFastMaxCells) return fail(TPE_E_ARG, "tpe_sample: tab_fast rows past the fast kernel's LDS");
-      TPE_LAUNCH(k_sample_fast, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48, (hipStream_t)stream,
-                 b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, (const float4*)b->comp32,
-                 (const float4*)b->tab, run_best, b->tiles_per_problem);
+      // (two candidate pairs per lane when the level fills at most two workgroups a CU)
+      if (wgs <= 2 * cu_count() && !fast_np2_forced())
+        TPE_LAUNCH(k_sample_fast<4>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
+                   (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
+                   (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
+      else
+        TPE_LAUNCH(k_sample_fast<2>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
+                   (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
+                   (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
     } else if (fast)
       TPE_LAUNCH((k_sample_tab<TPE_PREC_F32, true>), dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
