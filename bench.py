@@ -287,8 +287,18 @@ def roofline(prof, fmt='moments'):
         ms = np.array([r[0] for r in recs])
         if not len(ms) or name == 'fit':
             continue
+        stage_ms = ms
+        # the sample stage's tabulated pass is timed by its own launch's start /
+        # stop events (tpe_stage_prof.kernel_ns): the kernel as rocprofv3 sees it,
+        # without the dispatch after the table stage the stage's events include
+        kms = np.array([r[3] if len(r) > 3 else 0.0 for r in recs])
+        if np.all(kms > 0):
+            ms = kms
         secs = ms.sum() * 1e-3
         k = dict(avg_launch_ms=float(ms.mean()), launches=int(len(ms)), total_ms=float(ms.sum()))
+        if ms is not stage_ms:
+            k.update(timing='kernel start/stop events (hipExtLaunchKernel)',
+                     avg_stage_ms=float(stage_ms.mean()))
         c = _stage_counters(pmc, name)
         if name == 'sort':
             nbytes = np.array([r[1] for r in recs])

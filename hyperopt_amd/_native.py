@@ -249,7 +249,7 @@ STAGES = ('fit', 'k_tables', 'k_sample', 'sort', 'above', 'k_finalize', 'k_selec
 class StageProf(ctypes.Structure):
     """tpe_stage_prof: one stage of the last profiled tpe_level_run."""
     _fields_ = [('ms', ctypes.c_double), ('units', ctypes.c_double), ('ce', ctypes.c_double),
-                ('launches', ctypes.c_int32), ('reserved', ctypes.c_int32)]
+                ('launches', ctypes.c_int32), ('kernel_ns', ctypes.c_int32)]
 
 
 class MTState(ctypes.Structure):

@@ -25,6 +25,7 @@
 // No atomics: every reduction is in a fixed order, so results are bitwise
 // reproducible run to run and identical for any candidate sharding.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <limits.h>
 #include <math.h>
 #include <stdint.h>
@@ -4562,6 +4563,23 @@ int tpe_tables(const tpe_batch* b, void* stream) {
   return hip_check("tpe_tables");
 }
 
+// the stage profiler's kernel-bracketing events (tpe_stage_prof.kernel_ns): set
+// by run_batch_profiled around the sample stage, null otherwise
+static hipEvent_t g_kev[2] = {nullptr, nullptr};
+static bool g_kev_on = false;
+
+// the sample stage's tabulated pass: timed by its own launch's start / stop
+// events while the profiler brackets the stage
+#define TPE_LAUNCH_TIMED(kern, grid, block, shmem, stream, ...)                                           \
+  do {                                                                                                  \
+    ++g_launches;                                                                                       \
+    if (g_kev_on)                                                                                       \
+      hipExtLaunchKernelGGL(kern, grid, block, (std::uint32_t)(shmem), stream, g_kev[0], g_kev[1], 0u,  \
+                            __VA_ARGS__);                                                               \
+    else                                                                                                \
+      hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                                \
+  } while (0)
+
 int tpe_sample(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
@@ -4601,15 +4619,15 @@ int tpe_sample(const tpe_batch* b, void* stream) {
       if (b->tab_fast - 1 > kFastMaxCells) return fail(TPE_E_ARG, "tpe_sample: tab_fast rows past the fast kernel's LDS");
       // (two candidate pairs per lane when the level fills at most two workgroups a CU)
       if (wgs <= 2 * cu_count() && !fast_np2_forced())
-        TPE_LAUNCH(k_sample_fast<4>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
-                   (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
-                   (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
+        TPE_LAUNCH_TIMED(k_sample_fast<4>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
+                         (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
+                         (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
       else
-        TPE_LAUNCH(k_sample_fast<2>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
-                   (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
-                   (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
+        TPE_LAUNCH_TIMED(k_sample_fast<2>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
+                         (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
+                         (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
     } else if (fast)
-      TPE_LAUNCH((k_sample_tab<TPE_PREC_F32, true>), dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
+      TPE_LAUNCH_TIMED((k_sample_tab<TPE_PREC_F32, true>), dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
                          b->l_out, b->g_out, b->sample, b->flags, (const float4*)b->comp32, (const float4*)b->tab,
                          run_best, b->tiles_per_problem);
@@ -4717,12 +4735,17 @@ static struct {
   int valid;
   hipEvent_t ev[TPE_N_STAGES + 1];
   tpe_stage_prof last[TPE_N_STAGES];
+  int kev_used;                           // the sample stage's pass was launched with g_kev
 } g_prof;
 
 int tpe_level_profile(int32_t enable) {
   if (enable && !g_prof.ev[0]) {
     for (int i = 0; i <= TPE_N_STAGES; ++i) {
       hipError_t e = hipEventCreate(&g_prof.ev[i]);
+      if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    }
+    for (int i = 0; i < 2; ++i) {
+      hipError_t e = hipEventCreate(&g_kev[i]);
       if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
     }
   }
@@ -4745,9 +4768,13 @@ static int run_batch_profiled(const tpe_batch* b, void* stream) {
                                              tpe_score_above, tpe_finalize, tpe_select};
   hipStream_t s = (hipStream_t)stream;
   if (hipEventRecord(g_prof.ev[0], s) != hipSuccess) return hip_check("tpe_level_profile");
+  g_prof.kev_used = 0;
   for (int i = 0; i < TPE_N_STAGES; ++i) {
     const int64_t n0 = g_launches;
+    g_kev_on = i == TPE_STAGE_SAMPLE && b->n_tab_jobs > 0 && b->early_select && b->tab_fast;
     int rc = fns[i](b, stream);
+    if (g_kev_on) g_prof.kev_used = 1;
+    g_kev_on = false;
     if (rc) return rc;
     g_prof.last[i].launches = (int32_t)(g_launches - n0);
     if (hipEventRecord(g_prof.ev[i + 1], s) != hipSuccess) return hip_check("tpe_level_profile");
@@ -4789,7 +4816,11 @@ static int profile_collect(const tpe_batch& b, const tpe_pack_info& info, const 
     q.ms = ms;
     q.units = units[i];
     q.ce = i == TPE_STAGE_SAMPLE ? ce_tab : (i == TPE_STAGE_ABOVE ? ce_above : 0.0);
-    q.reserved = 0;
+    q.kernel_ns = 0;
+    if (i == TPE_STAGE_SAMPLE && g_prof.kev_used) {
+      float kms = 0.f;
+      if (hipEventElapsedTime(&kms, g_kev[0], g_kev[1]) == hipSuccess) q.kernel_ns = (int32_t)(kms * 1e6f);
+    }
   }
   g_prof.valid = 1;
   return TPE_OK;

@@ -743,7 +743,8 @@ class Engine(object):
         N.check(self.lib.tpe_level_profile_read(recs, len(N.STAGES)), self.lib, 'tpe_level_profile_read')
         for name, r in zip(N.STAGES, recs):
             if r.launches:
-                self.profile.setdefault(name, []).append((float(r.ms), float(r.units), float(r.ce)))
+                self.profile.setdefault(name, []).append((float(r.ms), float(r.units), float(r.ce),
+                                                          1e-6 * float(r.kernel_ns)))
 
     # ---------------------------------------------------------------- run
     def run(self, problems, n_cand, seed, cand_base=0, want_lg=False, return_cand=False, n_cand_global=None):

@@ -856,7 +856,9 @@ typedef struct tpe_stage_prof {
                         sample = tabulated problems' (K_below + K_above) x C,
                         above = scored problems' K_above x C; else 0                */
   int32_t launches;  /* kernels (and library sorts) the stage launched             */
-  int32_t reserved;
+  int32_t kernel_ns; /* sample stage: its tabulated pass's kernel alone, timed by the
+                        start / stop events of its own launch (hipExtLaunchKernel) on
+                        the stage's stream, in ns; 0 where not timed               */
 } tpe_stage_prof;
 
 /* enable (1) / disable (0) the profiler; creates its events on first use */
