@@ -1738,12 +1738,16 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
       // wait (the last round's lanes past the rows: a clamped load, unused slots)
       const int nu = TPE_TAB_ROW_UNITS * p.tab_n[0];
       const int wv = (int)(threadIdx.x >> 6);
+#ifndef TPE_DIAG_NO_STAGE
       for (int u = 0; u * kFastThreads < nu; ++u) {
         const int q = min(u * kFastThreads + (int)threadIdx.x, nu - 1);
         __builtin_amdgcn_global_load_lds((const void*)(tab + (int64_t)p.tab_off[0] + q),
                                          (__attribute__((address_space(3))) void*)(fast_tab + u * kFastThreads + 64 * wv),
                                          16, 0, 0);
       }
+#else
+      (void)nu; (void)wv;                          // (diagnostic builds only: the staging's cost)
+#endif
       staged = true;
     }
     if (threadIdx.x == 0)
@@ -1789,7 +1793,12 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
 #pragma unroll
           for (int j = 0; j < NP; j += 2) {
             const uint64_t blk = (g0 + (uint64_t)j) >> 1;
+#ifndef TPE_DIAG_NO_PHILOX
             const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
+#else                                              // (diagnostic builds only: the draws' cost)
+            const uint32_t h = (uint32_t)blk * 2654435761u;
+            const U4 r{h, h ^ 0x9e3779b9u, h * 3u, h ^ 0x85ebca6bu};
+#endif
             ws[j] = r.x; uf[j] = u01f(r.y);
             ws[j + 1] = r.z; uf[j + 1] = u01f(r.w);
           }
@@ -1839,7 +1848,11 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
         for (int j = 0; j < NP; ++j) {
           const float4 sv = row_lds[kc[j]];
           const float pr = sv.z + uf[j] * (sv.w - sv.z);
+#ifndef TPE_DIAG_NO_NDTRI
           const float z = ndtri_f32(pr);
+#else                                              // (diagnostic builds only: the inversion's cost)
+          const float z = pr - 0.5f;
+#endif
           const float xf = sv.x + sv.y * z;
           tj[j] = fminf(fmaxf(xf == xf ? xf : sv.x, lo_f), hi_f);
         }
@@ -1849,7 +1862,11 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
       for (int j = 0; j < NP; ++j) {
         const int i = first + j;
         float lb2, la2;
+#ifndef TPE_DIAG_NO_CELLS
         lp_log2(lo0, inv0, w0, ih0, n0, fast_tab, tj[j], lb2, la2);
+#else                                              // (diagnostic builds only: the look-up's cost)
+        lb2 = tj[j]; la2 = 0.5f * tj[j];
+#endif
         const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
         exact |= (unsigned)(valid && !ok) << j;
         const float d = lb2 - la2;
