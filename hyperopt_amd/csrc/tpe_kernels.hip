@@ -1752,7 +1752,11 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
     }
     if (threadIdx.x == 0)
       s_run[n_def] = RunRec{(int64_t)p.cand_base, p.below_base, p.above_base, tile, p.family == TPE_FAM_LOGGAUSS ? 1 : 0};
+#ifndef TPE_DIAG_NO_UNITS
     const int nunits = (gk - gi + 1) * (kTile / kFastUnit);
+#else                                              // (diagnostic builds only: the pass without candidates)
+    const int nunits = 0;
+#endif
     float lo_f, hi_f;
     f32_bounds(p, lo_f, hi_f);
     const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0];
