@@ -3897,9 +3897,9 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
 constexpr int kFitChunk = 2048;
 constexpr int kFitThreads = 256;
 constexpr int kFitPer = kFitChunk / kFitThreads;
-constexpr int kFitStage = kFitChunk + 3;         // a chunk's above observations and their neighbours
-// positions of the order a staging thread reads: the stretch holding kFitStage
-// above observations holds at most kFitMaxBelow below ones too
+// positions of the order a staging thread reads: the stretch holding a chunk's
+// above observations and their neighbours (kFitChunk + 3) holds at most
+// kFitMaxBelow below ones too
 constexpr int kFitStagePer = 9;
 static_assert(kFitStagePer * 256 >= kFitChunk + 3 + 64, "staging covers the stretch");
 constexpr int kThr = 5;                          // wide if sigma > smin * 2^(m+1), m < kThr
@@ -3941,15 +3941,6 @@ struct AboveSrc {
   }
 };
 
-// a chunk's above observations [qa, qa + kFitStage) staged in LDS (fit_stage)
-struct LdsSrc {
-  const double* k;
-  const uint32_t* r;
-  int64_t qa;
-  __device__ __forceinline__ double key(int64_t q) const { return k[q - qa]; }
-  __device__ __forceinline__ uint32_t rank(int64_t q) const { return r[q - qa]; }
-};
-
 // the view of one job's sorted above observations with the prior inserted at
 // pos (np.searchsorted(side='left'), tpe.py:427-431) and its bandwidth rules
 template <class Src>
@@ -3986,10 +3977,6 @@ struct FitCtx {
 // into VGPR pairs and took the stats kernel to 143 VGPRs)
 // |z| >= 6: erf(z) rounds to +-1 in f64 (1 - erf(6) = 2.2e-17 < half an ulp of 1)
 __device__ __noinline__ double erf_call(double z) { return erf(z); }
-__device__ __forceinline__ double erf_sat(double z) { return fabs(z) >= 6.0 ? copysign(1.0, z) : erf_call(z); }
-__device__ __forceinline__ double ncdf(double x, double mu, double sigma) {   // tpe.py:96-101
-  return 0.5 * (1.0 + erf_sat((x - mu) / fmax(1.4142135623730951 * sigma, kEPS)));
-}
 
 template <class Src>
 __device__ __forceinline__ FitCtx<Src> fit_ctx(const tpe_fit_job& j, Src src, int64_t pos) {
@@ -4015,25 +4002,52 @@ __device__ __forceinline__ AboveSrc above_src(const tpe_fit_job& j, const int32_
   return AboveSrc{ord_keys(j), ord_idx(j), adj + j.seg_off, below_idx + j.below_off, j.n_below};
 }
 
-// Stages the above observations q in [qa, qb) of job j (qb - qa <= kFitStage)
-// into lk / lr: every position of the order's stretch that holds them, less
-// the below positions (s_bp: sorted, LDS), keys and ranks (s_bi: the below
-// indices into obs, ascending, LDS).  Block-wide; the caller synchronises.
-__device__ void fit_stage(const tpe_fit_job& j, const uint32_t* s_bp, const uint32_t* s_bi, int64_t qa, int64_t qb,
-                          double* lk, uint32_t* lr) {
+// Below indices per bucket of the observation indices (bucket b = i >> bsh,
+// at most kFitBuckets of them): s_bk[b] = #{k : s_bi[k] < b << bsh}, so an
+// observation's count of older below ones is s_bk[b] plus a scan of its own
+// bucket's few (usually no) entries instead of a search of the whole list.
+constexpr int kFitBuckets = 256;
+__device__ __forceinline__ int fit_bucket_shift(int64_t n_obs) {
+  int s = 0;
+  while (((n_obs - 1) >> s) >= kFitBuckets) ++s;
+  return s;
+}
+__device__ __forceinline__ void fit_rank_buckets(int nb, const uint32_t* s_bi, int bsh, uint32_t* s_bk) {
+  for (int b = threadIdx.x; b <= kFitBuckets; b += kFitThreads) {
+    const uint64_t edge = (uint64_t)b << bsh;
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((uint64_t)s_bi[m] < edge) lo = m + 1; else hi = m;
+    }
+    s_bk[b] = (uint32_t)lo;
+  }
+}
+
+// Stages components [c0 - 1, c1] of job j (the chunk's and one neighbour on
+// each side; the prior inserted at pos) into lmu (means) and lrk (an
+// observation's rank among the above ones in tid order: its LF weight index),
+// indexed by i - c0 + 1.  They come from the order's stretch holding above
+// observations [qa, qb), less the below positions in it (s_bp, sorted: the
+// stretch holds entries [la, lb) of it, usually none), loads first.
+// Block-wide; the caller synchronises.
+__device__ void fit_stage_rows(const tpe_fit_job& j, const uint32_t* s_bp, const uint32_t* s_bi,
+                               const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1, int64_t n, int64_t pos,
+                               double* lmu, uint32_t* lrk) {
   const double* __restrict__ ok = ord_keys(j);
   const uint32_t* __restrict__ ov = ord_idx(j);
   const int nb = j.n_below;
-  auto at = [&](int64_t q) {                          // position of above observation q
+  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
+  auto n_before = [&](int64_t q) {                    // below positions before above observation q
     int lo = 0, hi = nb;
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
       if ((int64_t)s_bp[m] - m <= q) lo = m + 1; else hi = m;
     }
-    return q + lo;
+    return lo;
   };
-  const int64_t fa = at(qa), fb = at(qb - 1) + 1;
-  // every position's loads first (independent), then the searches and stores
+  const int la = n_before(qa), lb = n_before(qb - 1);
+  const int64_t fa = qa + la, fb = qb + lb;
   double kv[kFitStagePer];
   uint32_t iv[kFitStagePer];
 #pragma unroll
@@ -4045,22 +4059,53 @@ __device__ void fit_stage(const tpe_fit_job& j, const uint32_t* s_bp, const uint
   for (int e = 0; e < kFitStagePer; ++e) {
     const int64_t f = fa + e * kFitThreads + threadIdx.x;
     if (f >= fb) break;
-    int lo = 0, hi = nb;                              // below positions before f
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if ((int64_t)s_bp[m] < f) lo = m + 1; else hi = m;
+    int lo = la;
+    bool below = false;
+    for (int k = la; k < lb; ++k) {                   // uniform trip count
+      const int64_t p = s_bp[k];
+      lo += p < f;
+      below |= p == f;
     }
-    if (lo < nb && (int64_t)s_bp[lo] == f) continue;
+    if (below) continue;
     const int64_t q = f - lo;
-    const uint32_t i = iv[e];
-    int a = 0, b = nb;                                // below indices older than i
-    while (a < b) {
-      const int m = (a + b) >> 1;
-      if (s_bi[m] < i) a = m + 1; else b = m;
-    }
-    lk[q - qa] = kv[e];
-    lr[q - qa] = i - (uint32_t)a;
+    const int64_t i = q + (q >= pos);
+    if (i < c0 - 1 || i > c1) continue;
+    const uint32_t o = iv[e];
+    uint32_t k = s_bk[o >> bsh];
+    const uint32_t ke = s_bk[(o >> bsh) + 1];
+    while (k < ke && s_bi[k] < o) ++k;
+    lmu[i - c0 + 1] = kv[e];
+    lrk[i - c0 + 1] = o - k;
   }
+  if (threadIdx.x == 0 && pos >= c0 - 1 && pos <= c1) lmu[pos - c0 + 1] = j.prior_mu;
+}
+
+// log2 of a positive finite double: its exponent exactly plus the f32 log2 of
+// its mantissa (in [-1, 0): |error| < 3e-7, under the f32 rounding of a row's c
+// at |c| >= 4)
+__device__ __forceinline__ double log2_rows(double x) {
+  return (double)__builtin_amdgcn_frexp_exp(x) + (double)__builtin_amdgcn_logf((float)__builtin_amdgcn_frexp_mant(x));
+}
+
+// a component's row {mu_hi, mu_lo, a, c}: a = A / max(sigma, EPS) rounded from
+// f64 (the pruning bound narrow_amin is rounded the same way), c = log2(w / se)
+// - cm, at most 0 (cm bounds it).  k_fit_main writes the same bits (its
+// smallest-sigma shortcut takes the same values precomputed).
+__device__ __forceinline__ float4 fit_row(double mu, double se, double w, double cm) {
+  const float hi = (float)mu;
+  return make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se),
+                     fminf((float)(log2_rows(w) - log2_rows(se) - cm), 0.f));
+}
+
+// 0.5 * (1 + erf((x - mu) / max(sqrt2 sigma, EPS))) (tpe.py:96-101); |z| >= 6
+// tested as |x - mu| >= 6 den, so a wave whose lanes all saturate divides
+// nothing (where the two tests disagree z rounds to within an ulp of 6 and
+// erf(z) rounds to +-1 all the same)
+__device__ __forceinline__ double ncdf_fit(double x, double mu, double sigma) {
+  const double d = x - mu, den = fmax(1.4142135623730951 * sigma, kEPS);
+  double e = copysign(1.0, d);
+  if (!(fabs(d) >= 6.0 * den)) e = erf_call(d / den);
+  return 0.5 * (1.0 + e);
 }
 
 // the job's sorted below positions and below indices into LDS (block-wide)
@@ -4114,7 +4159,7 @@ __device__ __forceinline__ double* wide_sigmas(const tpe_fit_job& j, double* scr
 // the buckets whose answer lies in it (a binary search over its staged means) —
 // the buckets g with mu32[c0 - 1] < edge_g <= mu32[c1 - 1] (the last chunk:
 // every g from there up, K when no mean reaches edge_g).
-__global__ __launch_bounds__(kFitThreads) void k_fit_main(const tpe_fit_job* __restrict__ J,
+__global__ __launch_bounds__(kFitThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_fit_main(const tpe_fit_job* __restrict__ J,
                                                           const int32_t* __restrict__ below_idx,
                                                           const uint32_t* __restrict__ adj,
                                                           double* __restrict__ scratch,
@@ -4125,21 +4170,33 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_main(const tpe_fit_job* __r
   if (c0 >= K) return;
   const int64_t c1 = min(c0 + kFitChunk, K);
   __shared__ uint32_t s_bp[kFitMaxBelow], s_bi[kFitMaxBelow];
-  __shared__ double lk[kFitStage];
-  __shared__ uint32_t lr[kFitStage];
+  __shared__ uint32_t s_bk[kFitBuckets + 1];
+  __shared__ double lmu[kFitChunk + 2];
+  __shared__ uint32_t lrk[kFitChunk + 2];
   fit_below_lds(j, below_idx, adj, s_bp, s_bi);
   __syncthreads();
-  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
-  fit_stage(j, s_bp, s_bi, qa, qb, lk, lr);
+  const int bsh = fit_bucket_shift(j.n_obs);
+  fit_rank_buckets(j.n_below, s_bi, bsh, s_bk);
   __syncthreads();
   const double* __restrict__ hdr = scratch + j.seg_off;
   const int64_t pos = (int64_t)hdr[kFitHdrPos];
-  const FitCtx<LdsSrc> c = fit_ctx(j, LdsSrc{lk, lr, qa}, pos);
-  const double cm = fit_cm_bound(j, K), thr0 = 2.0 * c.smin;
+  fit_stage_rows(j, s_bp, s_bi, s_bk, bsh, c0, c1, n, pos, lmu, lrk);
+  __syncthreads();
+  // the bandwidth and weight rules of fit_ctx (tpe.py:381-394, 441-470) over
+  // the staged means, the prior already in place
+  const double smin = j.prior_sigma / fmin(100.0, 1.0 + (double)K), smax = j.prior_sigma;
+  const bool ramp = j.lf > 0 && j.lf < n;
+  const int64_t num = n - j.lf;
+  const double start = 1.0 / (double)n, step = num > 1 ? (1.0 - start) / (double)(num - 1) : 0.0;
+  const bool bounded = j.family != TPE_FAM_LOGGAUSS && (j.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH));
+  const double cm = fit_cm_bound(j, K), thr0 = 2.0 * smin;
+  // most components sit at the clip: their a and log2(se) once (fit_row's values)
+  const double se_min = fmax(smin, kEPS), ls_min = log2_rows(se_min);
+  const float a_min = (float)(kAScale / se_min);
   float4* __restrict__ C = comp + j.above_off;
   uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
   double* __restrict__ wsg = wide_sigmas(j, scratch, K);
-  double W = 0, M = 0, sm_all = 0;
+  double W = 0, M = 0, sm_all = 0, s_lo = 0;
   double sm[kThr];
   int cnt[kThr];
 #pragma unroll
@@ -4148,25 +4205,54 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_main(const tpe_fit_job* __r
   for (int e = 0; e < kFitPer; ++e) {
     const int64_t i = c0 + e * kFitThreads + threadIdx.x;
     if (i >= c1) break;
-    const double sg = c.sigma(i), w = c.weight(i), mu = c.mu(i);
-    const double se = fmax(sg, kEPS);
-    const float hi = (float)mu;
-    C[i] = make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - cm));
-    W += w;
-    if (c.bounded) M += w * (ncdf(c.high, mu, sg) - ncdf(c.low, mu, sg));
-    if (i == c.pos || sg > thr0) {
-      const uint32_t slot = atomicAdd(&wl[0], 1u);
-      if (slot < (uint32_t)kWideCap) { wl[1 + slot] = (uint32_t)i; wsg[slot] = i == c.pos ? INFINITY : sg; }
+    const int li = (int)(i - c0) + 1;
+    const double mu = lmu[li];
+    double sg, w;
+    if (i == pos) {
+      sg = j.prior_sigma;
+      w = j.prior_weight;
+    } else {
+      // an edge component has one gap (-inf for the missing one: the clip
+      // below gives what the one-gap rule gives, NaN gaps included)
+      const double gl = i > 0 ? mu - lmu[li - 1] : -INFINITY;
+      const double gr = i < K - 1 ? lmu[li + 1] - mu : -INFINITY;
+      sg = fmin(fmax(fmax(gl, gr), smin), smax);
+      w = 1.0;
+      if (ramp) {
+        const int64_t r = lrk[li];
+        if (r < num - 1) w = __dadd_rn(__dmul_rn((double)r, step), start);    // linspace: i * step + start
+      }
     }
-    if (i != c.pos) {
+    const double se = fmax(sg, kEPS);
+    float a = a_min;
+    double ls = ls_min;
+    if (se != se_min) {
+      a = (float)(kAScale / se);
+      ls = log2_rows(se);
+    }
+    const float hi = (float)mu;
+    C[i] = make_float4(hi, (float)(mu - (double)hi), a, fminf((float)(log2_rows(w) - ls - cm), 0.f));
+    W += w;
+    if (bounded) M += w * (ncdf_fit(j.high, mu, sg) - ncdf_fit(j.low, mu, sg));
+    if (i == pos || sg > thr0) {
+      const uint32_t slot = atomicAdd(&wl[0], 1u);
+      if (slot < (uint32_t)kWideCap) { wl[1 + slot] = (uint32_t)i; wsg[slot] = i == pos ? INFINITY : sg; }
+    }
+    if (i != pos) {
       sm_all = fmax(sm_all, sg);
+      if (sg > thr0) {
 #pragma unroll
-      for (int m = 0; m < kThr; ++m) {
-        const double thr = c.smin * (double)(2 << m);
-        if (sg > thr) ++cnt[m]; else sm[m] = fmax(sm[m], sg);
+        for (int m = 0; m < kThr; ++m) {
+          const double thr = smin * (double)(2 << m);
+          if (sg > thr) ++cnt[m]; else sm[m] = fmax(sm[m], sg);
+        }
+      } else {
+        s_lo = fmax(s_lo, sg);                      // under every threshold
       }
     }
   }
+#pragma unroll
+  for (int m = 0; m < kThr; ++m) sm[m] = fmax(sm[m], s_lo);
   for (int o = 32; o > 0; o >>= 1) {
     W += __shfl_xor(W, o); M += __shfl_xor(M, o); sm_all = fmax(sm_all, __shfl_xor(sm_all, o));
 #pragma unroll
@@ -4200,8 +4286,8 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_main(const tpe_fit_job* __r
         }
         return lo;
       };
-      ga = c0 == 0 ? 0 : first_above((double)(float)c.mu(c0 - 1));
-      gb = c1 == K ? G : first_above((double)(float)c.mu(c1 - 1));
+      ga = c0 == 0 ? 0 : first_above((double)(float)lmu[0]);
+      gb = c1 == K ? G : first_above((double)(float)lmu[c1 - c0]);
     }
     s_ga = ga; s_gb = gb; s_glo = glo; s_ginv = ginv;
     if (c0 == 0) Gp[G] = (int32_t)K;
@@ -4226,7 +4312,7 @@ __global__ __launch_bounds__(kFitThreads) void k_fit_main(const tpe_fit_job* __r
     int64_t lo = c0, hi = c1;                      // first i with !(mu32[i] < edge) (c1: none in the chunk)
     while (lo < hi) {
       const int64_t md = (lo + hi) >> 1;
-      if ((double)(float)c.mu(md) < edge) lo = md + 1;
+      if ((double)(float)lmu[md - c0 + 1] < edge) lo = md + 1;
       else hi = md;
     }
     Gp[g] = (int32_t)lo;
@@ -4315,9 +4401,7 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
   if ((int)threadIdx.x < nw) {
     const int64_t i = wide_ix[threadIdx.x];
     const double sg = c.sigma(i), w = c.weight(i), mu = c.mu(i), se = fmax(sg, kEPS);
-    const float hi = (float)mu;
-    comp[j.wide_off + threadIdx.x] =
-        make_float4(hi, (float)(mu - (double)hi), (float)(kAScale / se), (float)(log2(w / se) - st.cm));
+    comp[j.wide_off + threadIdx.x] = fit_row(mu, se, w, st.cm);
     comp[j.above_off + i].w = -INFINITY;          // listed apart
   }
   if ((int)threadIdx.x < j.n_problems) {
