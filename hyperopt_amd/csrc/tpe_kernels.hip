@@ -3039,20 +3039,23 @@ __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P
   for (int n = 0; n < kFgtP; ++n) A[n] = 0.0;
   int odd = 0;
   const double id = 1.0 / d;
-  // two components per lane in flight (their terms added in index order)
+  // two components per lane in flight (their terms added in index order);
+  // sums of 2^c y^n, the 1 / n! applied once to the reduced sums; 2^c from the
+  // f32 exp (c is an f32 row value: its own rounding, up to 2^-19 at |c| >= 16,
+  // is larger than the f32 exp's 2^-23)
   for (int k = k_lo + lane; k < k_hi; k += 128) {
     const bool two = k + 64 < k_hi;
     const float4 q0 = rows[k], q1 = rows[two ? k + 64 : k];
     const bool u0 = q0.w > -INFINITY && q0.z == p.fgt_a, u1 = two && q1.w > -INFINITY && q1.z == p.fgt_a;
     odd += (q0.w > -INFINITY && q0.z != p.fgt_a) + (two && q1.w > -INFINITY && q1.z != p.fgt_a);
     const double y0 = ((double)q0.x + (double)q0.y - centre) * id, y1 = ((double)q1.x + (double)q1.y - centre) * id;
-    double t0 = u0 ? exp2((double)q0.w) : 0.0, t1 = u1 ? exp2((double)q1.w) : 0.0;
+    double t0 = u0 ? (double)exp2f(q0.w) : 0.0, t1 = u1 ? (double)exp2f(q1.w) : 0.0;
     A[0] += t0;
     A[0] += t1;
 #pragma unroll
     for (int n = 1; n < kFgtP; ++n) {
-      t0 *= y0 * (1.0 / (double)n);
-      t1 *= y1 * (1.0 / (double)n);
+      t0 *= y0;
+      t1 *= y1;
       A[n] += t0;
       A[n] += t1;
     }
@@ -3063,10 +3066,13 @@ __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P
   for (int off = 32; off > 0; off >>= 1) odd += __shfl_xor(odd, off);
   double* rec = reinterpret_cast<double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
   if (lane < kFgtP) {
-    double v = A[0];
+    double v = A[0], f = 1.0;                       // f = 1 / lane!
 #pragma unroll
-    for (int n = 1; n < kFgtP; ++n) v = lane == n ? A[n] : v;
-    rec[lane] = v;
+    for (int n = 1; n < kFgtP; ++n) {
+      v = lane == n ? A[n] : v;
+      f = lane >= n ? f / (double)n : f;
+    }
+    rec[lane] = v * f;
   }
   if (lane == 0) {
     int* ri = reinterpret_cast<int*>(rec + kFgtP);
@@ -3096,6 +3102,26 @@ __device__ __forceinline__ double group_sum(double v) {          // over aligned
   for (int off = W / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
+
+// v of the lane N below within each row of 16 lanes (DPP row_shr: no LDS
+// permute; the row's first N lanes read 0)
+template <int N>
+__device__ __forceinline__ double row_shr(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x110 + N, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x110 + N, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// the sum over each aligned row of 16 lanes, complete in the row's last lane
+// (a fixed order: the same bits every run)
+__device__ __forceinline__ double row_sum_last(double v) {
+  v += row_shr<8>(v);
+  v += row_shr<4>(v);
+  v += row_shr<2>(v);
+  v += row_shr<1>(v);
+  return v;
+}
+static_assert(kFgtLanes == 16, "a cell's lanes are one DPP row");
 
 __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict__ P,
                                                    const tpe_tab_job* __restrict__ J,
@@ -3127,7 +3153,7 @@ __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict
     const int b = b0 + gl;
     const double* __restrict__ rec = reinterpret_cast<const double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
     const double x = (cd - (p.fgt_lo + ((double)b + 0.5) * d)) / d;
-    const double e = exp(-x * x);
+    const double eh = exp(-0.5 * x * x), e = eh * eh;
     double hj[kFgtJ + 1];                             // h_j(x) = e^-x^2 H_j(x)
     hj[0] = e;
     hj[1] = 2.0 * x * e;
@@ -3143,12 +3169,14 @@ __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict
       for (int n = 0; n < kFgtP; ++n) sm += A[n] * hj[n + m];
       B[m] = sm;
     }
-    err = A[0] * exp(-0.5 * x * x) * kFgtEps;
+    err = A[0] * eh * kFgtEps;
   }
+  // the cell's sums in its row's last lane; S0 and the error bound broadcast
 #pragma unroll
-  for (int m = 0; m < kTabMoments; ++m) B[m] = group_sum<kFgtLanes>(B[m]);
-  err = group_sum<kFgtLanes>(err) + (double)p.above_len * kFgtFar;
-  const double S0 = B[0];
+  for (int m = 0; m < kTabMoments; ++m) B[m] = row_sum_last(B[m]);
+  const int last = g * kFgtLanes + kFgtLanes - 1;
+  err = __shfl(row_sum_last(err), last) + (double)p.above_len * kFgtFar;
+  const double S0 = __shfl(B[0], last);
   const bool ok = live && boxes_ok && S0 > 0.0 && err <= S0 * 0x1p-25;   // (group-uniform)
   float* row = reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * j);
   if (ok) {
@@ -3156,7 +3184,7 @@ __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict
     double M[kTabMoments];
 #pragma unroll
     for (int m = 0; m < kTabMoments; ++m) M[m] = 0.0;
-    if (gl == 0) {       // the boxes' part in u = (t - c) / h: B_m (-1)^m / m! (h / d)^m 2^-mx
+    if (gl == kFgtLanes - 1) {   // the boxes' part in u = (t - c) / h: B_m (-1)^m / m! (h / d)^m 2^-mx
       const double r = (double)h / d;
       double f = exp2(-(double)mx);
 #pragma unroll
@@ -3200,13 +3228,15 @@ __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict
       }
     }
 #pragma unroll
-    for (int m = 0; m < kTabMoments; ++m) M[m] = group_sum<kFgtLanes>(M[m]);
-    bad = group_sum<kFgtLanes>(bad ? 1.0 : 0.0) > 0.0;
-    float out = 0.f;
-#pragma unroll
-    for (int m = 0; m < kTabMoments; ++m) out = gl == m ? (float)M[m] : out;
-    if (gl == kTabMoments) out = bad || all_exact ? NAN : mx;
-    if (gl <= kTabMoments) row[gl] = out;
+    for (int m = 0; m < kTabMoments; ++m) M[m] = row_sum_last(M[m]);
+    bad = ((__ballot(bad) >> (g * kFgtLanes)) & 0xFFFFull) != 0;
+    if (gl == kFgtLanes - 1) {                     // the row from the lane holding the sums
+      static_assert(kTabMoments == 11 && TPE_TAB_ROW_UNITS == 3, "a moment row: 11 moments and the shift");
+      float4* r4 = reinterpret_cast<float4*>(row);
+      r4[0] = make_float4((float)M[0], (float)M[1], (float)M[2], (float)M[3]);
+      r4[1] = make_float4((float)M[4], (float)M[5], (float)M[6], (float)M[7]);
+      r4[2] = make_float4((float)M[8], (float)M[9], (float)M[10], bad || all_exact ? NAN : mx);
+    }
   }
   // the cells the boxes cannot build: directly, the whole wave per cell
   const unsigned long long direct = __ballot(live && !ok && gl == 0);

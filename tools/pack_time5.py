@@ -18,7 +18,14 @@ def main():
     D = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     n_obs = int(sys.argv[2]) if len(sys.argv) > 2 else 100000
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
-    lib = N.load()
+    if os.environ.get('TPE_PACK_LIB'):       # host-only build with the section clock (tools/build_pack_trace.sh)
+        lib = ctypes.CDLL(os.environ['TPE_PACK_LIB'])
+        lib.tpe_host_pack_level.restype = ctypes.c_int
+        lib.tpe_host_pack_level.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                                            ctypes.c_int64, ctypes.c_void_p]
+    else:
+        lib = N.load()
     rs = np.random.RandomState(0)
     recs = np.zeros(D, dtype=N.LABEL_DTYPE)
     keep = [recs]
