@@ -86,6 +86,8 @@ constexpr double kTabMinRatioFgt = 1.0;          // candidates per cell row for 
 constexpr int64_t kLogpolyMaxCells = 2048;
 constexpr int64_t kLpDirectRows = 64;       // a side of <= this many rows: direct sums, no moments
 constexpr int64_t kLpRowsPerWave = 5;       // ... kLpRowsPerWave cell rows per table-stage wave
+constexpr int64_t kMomDirectRows = 64;      // a moment side of <= this many rows: direct sums,
+constexpr int64_t kMomCellsPerWave = 4;     // ... kMomCellsPerWave cell rows per table-stage wave
 // a TPE_F_LOGPOLY row in cell rows: its above side's moments (one cell row)
 // plus the short below side's direct sums at the nodes (5 rows a wave) and the fit
 constexpr double kLpRowCost = 1.25;
@@ -1313,6 +1315,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       if (sd == 1 && (p.flags & TPE_F_FGT)) fgt_max_cells = std::max<int64_t>(fgt_max_cells, j.n);
       else if (j.kind == TPE_TAB_LOGPOLY && j.rows_n >= 0 && j.rows_n + j.wide_n <= kLpDirectRows)
         tab_blocks += (j.n + kLpRowsPerWave * TPE_TAB_PER_BLOCK - 1) / (kLpRowsPerWave * TPE_TAB_PER_BLOCK);
+      else if (j.kind == TPE_TAB_CELLS && j.rows_n >= 0 && j.rows_n + j.wide_n <= kMomDirectRows)
+        tab_blocks += (j.n + kMomCellsPerWave * TPE_TAB_PER_BLOCK - 1) / (kMomCellsPerWave * TPE_TAB_PER_BLOCK);
       else tab_blocks += j.kind != TPE_TAB_LATTICE ? (j.n + TPE_TAB_PER_BLOCK - 1) / TPE_TAB_PER_BLOCK : j.n;
       tab_jobs.push_back(j);
     }

@@ -3346,6 +3346,22 @@ __device__ __forceinline__ void logpoly_side(double sum, float m, bool flagged, 
   if (lane < 6) out[lane] = any ? NAN : (float)c;
 }
 
+// a moment-cell side of at most this many component rows (the below side: <=
+// 26) is summed directly, kMomCellsPerWave cell rows per wave, 16 lanes each
+// (tpe_host.cpp kMomDirectRows: its job's blocks hold 32 rows, not 8)
+constexpr int kMomDirectRows = 64;
+constexpr int kMomCellsPerWave = 4;
+
+// the max over each aligned row of 16 lanes, in every lane of the row (DPP:
+// quad xor 1 and 2, then row rotations by 4 and 8)
+__device__ __forceinline__ float row_max_all(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false)));
+  return v;
+}
+
 // 512-thread workgroups, one wave per cell row / lattice value
 // (TPE_TAB_PER_BLOCK per workgroup).  A cell job's workgroup first stages its
 // side's component rows in LDS (unless pruned or too many), so both passes of
@@ -3440,6 +3456,51 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       printf("k_tables direct blk %d wave %d rows %d: lookup+stage %llu sums+fit %llu\n", (int)blockIdx.x, wave, nr,
              (unsigned long long)(tt[1] - tt[0]), (unsigned long long)(tt[2] - tt[1]));
 #endif
+    return;
+  }
+  if (jb.kind == TPE_TAB_CELLS && jb.rows_n >= 0 && jb.rows_n + jb.wide_n <= kMomDirectRows) {
+    // a short moment side (the below mixture of a box-moment label): a cell
+    // per 16 lanes, its rows' passes as cell_moments makes them (the largest
+    // term, then the moments of the terms within 2^-kTabDrop of it), the sums
+    // by DPP row shifts into the row's last lane, which writes the row
+    const int nr = jb.rows_n + jb.wide_n;
+    if ((int)threadIdx.x < nr)
+      rows_lds[threadIdx.x] = (int)threadIdx.x < jb.rows_n ? comp32[jb.rows_off + threadIdx.x]
+                                                           : comp32[jb.wide_off + threadIdx.x - jb.rows_n];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, gl = lane & 15;
+    const int jr = (b * TPE_TAB_PER_BLOCK + wave) * kMomCellsPerWave + g;
+    const bool live = jr < jb.n;
+    const float w = 1.f / jb.inv;
+    const float c = __builtin_fmaf((float)(live ? jr : 0) + 0.5f, w, jb.lo);   // as cell_log2_lds forms it
+    const float h = 0.5f * w;
+    float mx = -INFINITY;
+    for (int q = gl; q < nr; q += 16) {
+      const float4 r = rows_lds[q];
+      const float z = ((c - r.x) - r.y) * r.z;
+      mx = fmaxf(mx, r.w - z * z);
+    }
+    mx = row_max_all(mx);
+    double M[kTabMoments];
+#pragma unroll
+    for (int q = 0; q < kTabMoments; ++q) M[q] = 0.0;
+    bool bad = !(mx > -INFINITY);
+    const float cut = mx - kTabDrop;
+    for (int q = gl; q < nr && !bad; q += 16) {
+      const float4 r = rows_lds[q];
+      const float z = ((c - r.x) - r.y) * r.z;
+      const float v = r.w - z * z;
+      if (v >= cut) add_moments(M, v, z, r.z, h, mx, bad);
+    }
+#pragma unroll
+    for (int q = 0; q < kTabMoments; ++q) M[q] = row_sum_last(M[q]);
+    bad = ((__ballot(bad) >> (g * 16)) & 0xFFFFull) != 0;
+    if (live && gl == 15) {
+      float4* r4 = reinterpret_cast<float4*>(tab + jb.off + TPE_TAB_ROW_UNITS * jr);
+      r4[0] = make_float4((float)M[0], (float)M[1], (float)M[2], (float)M[3]);
+      r4[1] = make_float4((float)M[4], (float)M[5], (float)M[6], (float)M[7]);
+      r4[2] = make_float4((float)M[8], (float)M[9], (float)M[10], bad || all_exact ? NAN : mx);
+    }
     return;
   }
   if (jb.kind == TPE_TAB_CELLS || jb.kind == TPE_TAB_LOGPOLY) {
@@ -4256,9 +4317,11 @@ __global__ __launch_bounds__(kFitThreads) __attribute__((amdgpu_waves_per_eu(6))
     const double se = fmax(sg, kEPS);
     float a = a_min;
     double ls = ls_min;
-    if (se != se_min) {
-      a = (float)(kAScale / se);
-      ls = log2_rows(se);
+    if (__ballot(se != se_min)) {                   // (a wave-uniform branch: no division when all clip)
+      if (se != se_min) {
+        a = (float)(kAScale / se);
+        ls = log2_rows(se);
+      }
     }
     const float hi = (float)mu;
     C[i] = make_float4(hi, (float)(mu - (double)hi), a, fminf((float)(log2_rows(w) - ls - cm), 0.f));

@@ -62,6 +62,8 @@ TAB_MIN_RATIO, TAB_MIN_RATIO_DEVFIT = 8.0, 64.0   # tpe_host.cpp kTabMinRatio*: 
 LOGPOLY_MAX_CELLS = 2048           # tpe_host.cpp kLogpolyMaxCells (TPE_F_LOGPOLY: one grid for both sides)
 LP_ROW_COST = 1.25                 # tpe_host.cpp kLpRowCost (a LOGPOLY row in cell rows)
 LP_DIRECT_ROWS = 64                # tpe_host.cpp kLpDirectRows
+MOM_DIRECT_ROWS = 64               # tpe_host.cpp kMomDirectRows
+MOM_CELLS_PER_WAVE = 4             # tpe_host.cpp kMomCellsPerWave
 LP_ROWS_PER_WAVE = 5               # tpe_host.cpp kLpRowsPerWave
 A_SCALE_LIT = 0.84932180028801907  # tpe_host.cpp kAScale (the same double)
 
@@ -363,6 +365,8 @@ class Engine(object):
                     n = info['tab_n'][sd]        # cells: TAB_PER_BLOCK rows a block; lattice: a block a value
                     if kind == N.TAB_LOGPOLY and geo[1] >= 0 and geo[1] + geo[3] <= LP_DIRECT_ROWS:
                         blocks += -(-n // (LP_ROWS_PER_WAVE * N.TAB_PER_BLOCK))    # (a short side: direct sums)
+                    elif kind == N.TAB_CELLS and geo[1] >= 0 and geo[1] + geo[3] <= MOM_DIRECT_ROWS:
+                        blocks += -(-n // (MOM_CELLS_PER_WAVE * N.TAB_PER_BLOCK))  # (a short moment side)
                     else:
                         blocks += -(-n // N.TAB_PER_BLOCK) if pl['mode'] == N.TAB_CELLS else n
             r0 += len(lp.ids)
