@@ -35,6 +35,7 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
 ``linear_forgetting`` is accepted and, as in the reference, not used: the
 forgetting window is fixed at DEFAULT_LF=25 (tpe.py:27-29).
 """
+import itertools
 import logging
 import os
 import math
@@ -643,9 +644,10 @@ def _choice_dicts(order, cols, values, active):
     values, the reference's types) and one ``dict(zip(...))`` per id assembles
     them in level order — no per-label Python work per id."""
     act = np.asarray(active, dtype=bool)
+    vt = np.ascontiguousarray(values.T)      # (a contiguous column makes its scalars faster)
     by_label = {}
     for label, ix, fam in cols:
-        col = values[:, ix]
+        col = vt[ix]
         a = act[:, ix]
         full = a.all()
         if fam == N.FAM_CATEGORICAL:         # (inactive entries are NaN: cast only the active ones)
@@ -654,7 +656,8 @@ def _choice_dicts(order, cols, values, active):
         if not full:
             vals = [v if on else None for v, on in zip(vals, a.tolist())]
         by_label[label] = vals
-    return [dict(zip(order, t)) for t in zip(*[by_label[k] for k in order])]
+    keys = tuple(order)
+    return list(map(dict, map(zip, itertools.repeat(keys), zip(*[by_label[k] for k in keys]))))
 
 
 def _choices_replay(table, fits, new_ids, seed, C, engine):
