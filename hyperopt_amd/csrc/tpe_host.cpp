@@ -177,15 +177,14 @@ double normal_cdf(double x, double mu, double sigma) {   // tpe.py:96-101
 // sum_k w_k (Phi_k(hi) - Phi_k(lo)) (tpe.py:130-136): the standardised bounds
 // in one vectorisable pass, libm's erf only where it is not exactly +-1 (a
 // component within 6 sqrt2 sigma of a bound); the same values as normal_cdf
+// (the terms into a[0, k); p_accept sums them, the packer's parallel pass
+// computes a large side's in chunks)
 __attribute__((target_clones("avx512f", "avx2", "default")))
-double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi) {
-  if (!bounded) return 1.0;
-  static thread_local std::vector<double> zl_tl, zh_tl;
-  std::vector<double>& zl = zl_tl;
+void p_accept_terms(const double* w, const double* mu, const double* sg, int64_t k, double lo, double hi,
+                    double* __restrict__ a) {
+  static thread_local std::vector<double> zh_tl;
   std::vector<double>& zh = zh_tl;
-  zl.resize((size_t)k);
   zh.resize((size_t)k);
-  double* __restrict__ a = zl.data();
   double* __restrict__ b = zh.data();
   const double s2 = sqrt(2.0);
   for (int64_t i = 0; i < k; ++i) {
@@ -198,7 +197,14 @@ double p_accept(const double* w, const double* mu, const double* sg, int64_t k, 
     const double eh = erf_fast(b[i]), el = erf_fast(a[i]);
     a[i] = w[i] * (0.5 * (1 + eh) - 0.5 * (1 + el));
   }
-  return np_sum(a, k);
+}
+
+double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi) {
+  if (!bounded) return 1.0;
+  static thread_local std::vector<double> zl_tl;
+  zl_tl.resize((size_t)k);
+  p_accept_terms(w, mu, sg, k, lo, hi, zl_tl.data());
+  return np_sum(zl_tl.data(), k);
 }
 
 // log2 of a positive normal double: exponent bits + atanh series of the
@@ -322,6 +328,11 @@ inline double min_of(const double* __restrict__ v, int64_t n) {
 }
 
 
+// the packer's parallel pass over the large bounded sides' acceptance terms
+constexpr int64_t kPaParallelMin = 2048;    // a side of at least this many components
+constexpr int64_t kPaChunk = 512;           // ... in chunks of this many
+struct PaTask { int32_t li, side; int64_t i0, i1, off; };
+
 // per-thread staging of tpe_host_pack_level, reused across calls (no
 // first-touch page faults on the large tables of a batched level)
 struct PackScratch {
@@ -335,6 +346,9 @@ struct PackScratch {
   std::vector<tpe_problem> xtmpl;       // expanded levels: one problem template per label
   std::vector<int32_t> xfirst;          // ... each label's first problem (n_labels + 1)
   std::vector<uint32_t> xctr;           // ... each problem's new id (Philox counter word 3)
+  std::vector<int64_t> pa_off;          // acceptance terms of the large bounded sides
+  std::vector<double> pa_terms;
+  std::vector<PaTask> pa_tasks;
 };
 
 // value range of a label's kernel coordinate (x, or ln x for log families)
@@ -458,7 +472,26 @@ struct FillCtx {
   const int32_t* tmode;
   int key_bits;
   bool f64;
+  const double* pa_terms;      // a large bounded side's acceptance terms (the packer's parallel pass)
+  const int64_t* pa_off;       // [2 * label + side]: their offset in pa_terms, -1: none
 };
+
+// the acceptance mass of label li's side: the terms the parallel pass made, or p_accept
+inline double side_accept(const FillCtx& cx, int32_t li, int side, const double* w, const double* mu,
+                          const double* sg, int64_t k, bool bounded, double lo, double hi) {
+  const int64_t o = cx.pa_off[2 * (size_t)li + side];
+  return o >= 0 ? np_sum(cx.pa_terms + o, k) : p_accept(w, mu, sg, k, bounded, lo, hi);
+}
+
+struct PaCtx { const tpe_label_in* labels; const PaTask* tasks; double* terms; };
+void pa_chunk(const PaCtx& cx, int t) {
+  const PaTask& q = cx.tasks[t];
+  const tpe_label_in& L = cx.labels[q.li];
+  const double* w = q.side ? L.above_w : L.below_w;
+  const double* mu = q.side ? L.above_mu : L.below_mu;
+  const double* sg = q.side ? L.above_sigma : L.below_sigma;
+  p_accept_terms(w + q.i0, mu + q.i0, sg + q.i0, q.i1 - q.i0, L.low, L.high, cx.terms + q.off + q.i0);
+}
 
 __attribute__((target_clones("avx512f", "avx2", "default")))
 void fill_label(const FillCtx& cx, int32_t li) {
@@ -551,7 +584,7 @@ void fill_label(const FillCtx& cx, int32_t li) {
       }
     } else if (L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) {
       off = (int32_t)sc.c64[side]; len = (int32_t)k;
-      base = -log(p_accept(w, mu, sg, k, bounded, L.low, L.high));
+      base = -log(side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high));
       double* r = cx.comp64 + 4 * (size_t)off;
       for (int64_t i = 0; i < k; ++i) {
         const double row[4] = {mu[i], np_max(sqrt(2.0) * sg[i], kEPS), w[i], 0};
@@ -560,7 +593,7 @@ void fill_label(const FillCtx& cx, int32_t li) {
     } else {
       const bool logf = L.family == TPE_FAM_LOGGAUSS;
       std::vector<double> a((size_t)k), c((size_t)k);
-      const double pa = logf ? 1.0 : p_accept(w, mu, sg, k, bounded, L.low, L.high);
+      const double pa = logf ? 1.0 : side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high);
       double shift = -INFINITY;
       if (f64) {
         for (int64_t i = 0; i < k; ++i) {
@@ -1013,8 +1046,37 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   samp.resize((size_t)(8 * n_samp));
   grid.resize((size_t)std::max<int64_t>(n_grid, 1));
   grid[0] = 0;
+  // the acceptance terms of the large bounded sides in chunks on the workers
+  // (libm erf for every component near a bound: the largest label's would
+  // otherwise be its fill's critical path); the fill sums them in order
+  auto& pa_off = ps.pa_off;
+  auto& pa_terms = ps.pa_terms;
+  auto& pa_tasks = ps.pa_tasks;
+  pa_off.assign(2 * (size_t)n_labels, -1);
+  pa_tasks.clear();
+  int64_t pa_total = 0;
+  for (int32_t li = 0; li < n_labels; ++li) {
+    const tpe_label_in& L = labels[li];
+    if (!(L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) || L.family == TPE_FAM_CATEGORICAL ||
+        L.family == TPE_FAM_LOGGAUSS)
+      continue;
+    for (int side = 0; side < 2 - dev_fit[li]; ++side) {
+      const int64_t k = side ? L.above_k : L.below_k;
+      if (k < kPaParallelMin) continue;
+      pa_off[2 * (size_t)li + side] = pa_total;
+      for (int64_t i0 = 0; i0 < k; i0 += kPaChunk)
+        pa_tasks.push_back(PaTask{li, side, i0, std::min(k, i0 + kPaChunk), pa_total});
+      pa_total += k;
+    }
+  }
+  if (!pa_tasks.empty()) {
+    pa_terms.resize((size_t)pa_total);
+    const PaCtx pcx{labels, pa_tasks.data(), pa_terms.data()};
+    tpe_pool::parallel_for((int)pa_tasks.size(), [](void* c, int i) { pa_chunk(*(const PaCtx*)c, i); }, (void*)&pcx);
+  }
+  PACK_MARK("accept");
   const FillCtx fcx{labels, sec.data(), lab.data(), samp.data(), comp64.data(), comp32.data(), grid.data(),
-                    dev_fit.data(), tmode.data(), key_bits, f64};
+                    dev_fit.data(), tmode.data(), key_bits, f64, pa_terms.data(), pa_off.data()};
   {
     // (a few hundred components per label make a worker's hand-off worth it)
     if (n_labels >= 2 && work_k >= 4096)
