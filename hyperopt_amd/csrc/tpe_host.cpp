@@ -169,14 +169,10 @@ inline double erf_fast(double z) { return fabs(z) >= 6.0 ? copysign(1.0, z) : er
 // rows of components far from a bound skip the call
 inline double erfc_fast(double x) { return x <= -6.0 ? 2.0 : (x >= 27.3 ? 0.0 : erfc(x)); }
 
-double normal_cdf(double x, double mu, double sigma) {   // tpe.py:96-101
-  const double bottom = np_max(sqrt(2.0) * sigma, kEPS);
-  return 0.5 * (1 + erf_fast((x - mu) / bottom));
-}
-
 // sum_k w_k (Phi_k(hi) - Phi_k(lo)) (tpe.py:130-136): the standardised bounds
 // in one vectorisable pass, libm's erf only where it is not exactly +-1 (a
-// component within 6 sqrt2 sigma of a bound); the same values as normal_cdf
+// component within 6 sqrt2 sigma of a bound); the same values as the reference's
+// normal_cdf (tpe.py:96-101): 0.5 (1 + erf((x - mu) / max(sqrt2 sigma, EPS)))
 // (the terms into a[0, k); p_accept sums them, the packer's parallel pass
 // computes a large side's in chunks)
 __attribute__((target_clones("avx512f", "avx2", "default")))
