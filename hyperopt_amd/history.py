@@ -50,7 +50,7 @@ class History(object):
         self.tree_memo = None          # tpe._tree_labels of this (immutable) view without a Trials cache
 
     def smallest(self, m):
-        return None if self._cache is None else self._cache.smallest(m)
+        return _smallest_plain(self.losses, m) if self._cache is None else self._cache.smallest(m)
 
     def native_columns(self, label, log=False):
         """(tids, coordinate, value order) host addresses of a label's columns
@@ -476,6 +476,27 @@ def extract(domain, trials):
     hist = History(tids, cache.losses.view(), cache.obs_views(), dev=cache.dev, cache=cache)
     cache.hist = hist if not cache.pending else None
     return hist
+
+
+def _smallest_plain(losses, m, stride=64):
+    """Positions of the m smallest losses ordered by (loss, position) — NaN
+    never among them, as np.argsort puts it last — without an O(N) selection:
+    the m-th smallest of a strided sample is at least the m-th smallest of all,
+    so every loss up to it (about m * stride of them, ties included) holds the
+    m smallest, and a stable sort of those orders them.  None for short
+    histories or when the sample cannot bound them (NaN)."""
+    n = len(losses)
+    if m <= 0 or n < 2 * stride * m:
+        return None
+    t = np.partition(losses[::stride], m - 1)[m - 1]
+    if not t == t:
+        return None
+    cand = np.flatnonzero(losses <= t)
+    lc = losses[cand]
+    if len(cand) > 4 * m:                  # (ties at the m-th value all kept, then the stable sort)
+        keep = lc <= lc[np.argpartition(lc, m - 1)[m - 1]]
+        cand, lc = cand[keep], lc[keep]
+    return cand[np.argsort(lc, kind='stable')[:m]]
 
 
 class BelowTids(np.ndarray):

@@ -372,3 +372,38 @@ def test_tree_memo_follows_the_table_object():
     ix = d2.table.by_label['x'].index
     assert (a2[ix]['low'], a2[ix]['high'], a2[ix]['prior_mu']) == (-1.0, 2.0, 0.5)
     assert (a1[ix]['low'], a1[ix]['high']) == (-5.0, 5.0)
+
+
+def test_plain_history_below_split_from_sampled_bound():
+    """A History without a Trials cache takes its n_below smallest losses from
+    a strided sample's bound (history._smallest_plain) instead of an O(N)
+    argpartition: the same positions, ordered by (loss, position), as a stable
+    argsort (NaN last) — ties at the boundary, NaN and +inf losses included —
+    and split_below gives the reference's below set."""
+    from hyperopt_amd import history as H
+    rs = np.random.RandomState(5)
+    checked = 0
+    for trial in range(200):
+        n = int(rs.randint(2000, 60000))
+        L = rs.uniform(size=n)
+        if trial % 3 == 0:
+            L = np.round(L * rs.randint(5, 400)) / 7.0           # heavy ties
+        if trial % 5 == 0:
+            L[rs.choice(n, rs.randint(1, 40))] = np.nan
+        if trial % 7 == 0:
+            L[rs.choice(n, rs.randint(1, 40))] = np.inf
+        m = int(rs.randint(1, 27))
+        got = H._smallest_plain(L, m)
+        if got is None:
+            continue
+        checked += 1
+        np.testing.assert_array_equal(got, np.argsort(L, kind='stable')[:m])
+        tids = np.arange(n, dtype=np.int64) * 3
+        hist = H.History(tids, L, {})
+        b = H.split_below(hist, 0.25)
+        nb = min(int(np.ceil(0.25 * np.sqrt(n))), 25)
+        ref = tids[np.argsort(L, kind='stable')[:nb]]
+        Ls = np.sort(np.where(np.isnan(L), np.inf, L))
+        if nb < n and Ls[nb - 1] != Ls[nb]:                     # (a boundary tie: the reference's argsort order decides)
+            assert set(np.asarray(b).tolist()) == set(ref.tolist())
+    assert checked > 150
