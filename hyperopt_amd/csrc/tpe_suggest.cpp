@@ -88,6 +88,28 @@ struct Tree {
 // spec: a speculative fit on a pool worker (prefit): labels the caller must
 // fit are left alone (no need_fit flag), and a failure only leaves the fit
 // undone — the label's real fit, on the calling thread, reports it
+// each below tid's position among a label's ascending tids (ap_filter_trials,
+// tpe.py:629-636), in the below set's (ascending) order.  Tids one apart from
+// first to last (every trial observed the label: a flat space's columns) are
+// indexed directly instead of searched: 25 searches over a 10^5-tid column
+// were most of a device-fitted label's host fit
+inline void below_positions(const int64_t* tids, int64_t n, const int64_t* below, int64_t nb,
+                            std::vector<int32_t>& out) {
+  out.clear();
+  if (n <= 0) return;
+  const int64_t t0 = tids[0];
+  const bool dense = tids[n - 1] - t0 == n - 1;           // (strictly ascending: tids[k] = t0 + k)
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t t = below[b];
+    if (dense) {
+      if (t >= t0 && t - t0 < n) out.push_back((int32_t)(t - t0));
+      continue;
+    }
+    const int64_t* at = std::lower_bound(tids, tids + n, t);
+    if (at != tids + n && *at == t) out.push_back((int32_t)(at - tids));
+  }
+}
+
 int fit_label(Tree& T, int i, bool spec = false) {
   Fit& f = (*T.fits)[(size_t)i];
   if (f.done) return TPE_OK;
@@ -116,11 +138,7 @@ int fit_label(Tree& T, int i, bool spec = false) {
     const double* x = (const double*)L.values;
     f.side_x.resize((size_t)n);
     double* bx = f.side_x.data();
-    f.below_idx.clear();
-    for (int64_t b = 0; b < T.n_below; ++b) {
-      const int64_t* at = std::lower_bound(L.tids, L.tids + n, T.below[b]);
-      if (at != L.tids + n && *at == T.below[b]) f.below_idx.push_back((int32_t)(at - L.tids));
-    }
+    below_positions(L.tids, n, T.below, T.n_below, f.below_idx);
     const int64_t nb = (int64_t)f.below_idx.size(), na = n - nb;
     if (nb != L.side_n[0] || na != L.side_n[1])
       return tpe_internal_fail(TPE_E_ARG, "tpe_suggest_tree: the caller's side sizes differ from the below split");
@@ -169,12 +187,8 @@ int fit_label(Tree& T, int i, bool spec = false) {
     // at most 25 observations, all of weight 1 (no linear-forgetting ramp below
     // 26, tpe.py:381-394), so any sort of it gives numpy's fit: tied values are
     // interchangeable
-    f.below_idx.clear();
     const double* x = (const double*)L.values;
-    for (int64_t b = 0; b < T.n_below; ++b) {              // each below tid among the ascending tids
-      const int64_t* at = std::lower_bound(L.tids, L.tids + n, T.below[b]);
-      if (at != L.tids + n && *at == T.below[b]) f.below_idx.push_back((int32_t)(at - L.tids));
-    }
+    below_positions(L.tids, n, T.below, T.n_below, f.below_idx);
     const int64_t nb = (int64_t)f.below_idx.size();
     if (nb > 64 || n - nb + 1 <= 64) return TPE_E_FALLBACK;
     std::vector<double> bx((size_t)nb);
