@@ -1685,6 +1685,9 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
                    tpe_result* __restrict__ run_best, int tpp) {
   constexpr int kFastUnit = 64 * NP;
   static_assert(NP % 2 == 0 && kTile % kFastUnit == 0, "fast units: Philox pairs tiling the tiles");
+#ifdef TPE_DIAG_EMPTY
+  return;                                          // (diagnostic builds only: the launch's own cost)
+#endif
   extern __shared__ float4 fast_tab[];                       // the label's LOGPOLY rows (tab_fast of them at most)
   __shared__ double cum_lds[kFastSamp];
   __shared__ float4 row_lds[kFastSamp];
