@@ -42,9 +42,14 @@ extern "C" {
 /* categorical problems with at most this many categories are scored by the
  * sample stage itself (device-drawn candidates) */
 #define TPE_SAMPLE_LDS_ROWS 1024
-/* cell rows a table workgroup computes; a lattice value takes a whole
- * workgroup (tpe_batch.tab_blocks = sum over cell jobs of ceil(n /
- * TPE_TAB_PER_BLOCK) + sum over lattice jobs of n) */
+/* cell rows a table workgroup computes (one per wave); a lattice value takes
+ * a whole workgroup.  A short side (at most 64 component rows + wide rows,
+ * rows_n >= 0) is summed directly, several rows a wave: 5 for a log-polynomial
+ * job, 4 for a moment-cell job.  tpe_batch.tab_blocks = sum over such
+ * log-polynomial jobs of ceil(n / (5 TPE_TAB_PER_BLOCK)) + over such moment
+ * jobs of ceil(n / (4 TPE_TAB_PER_BLOCK)) + over the other cell jobs of
+ * ceil(n / TPE_TAB_PER_BLOCK) + over lattice jobs of n (a TPE_F_FGT label's
+ * above cells: none, the box stage builds them) */
 #define TPE_TAB_PER_BLOCK 8
 /* 16-B units of one cell row of a TPE_TAB_CELLS table */
 #define TPE_TAB_ROW_UNITS 3
