@@ -848,7 +848,7 @@ __device__ __forceinline__ float cell_log2_lds(float lo, float inv, float w, flo
 }
 
 // log2 of both mixture sides at t from a TPE_F_LOGPOLY row (include/tpe_hip.h,
-// "Tabulated scoring"): {b_0..b_5, a_0..a_5}, degree-5 polynomials in u; NAN
+// "Tabulated scoring"): {b_0, a_0, .., b_5, a_5}, degree-5 polynomials in u; NAN
 // for a side outside the cells or flagged (b_0 / a_0 = NaN).  Cell centre and
 // u as cell_log2_lds forms them.
 __device__ __forceinline__ void lp_log2(float lo, float inv, float w, float ih, int n, const float4* __restrict__ rows,
@@ -858,14 +858,17 @@ __device__ __forceinline__ void lp_log2(float lo, float inv, float w, float ih, 
   const float4* __restrict__ r = rows + TPE_TAB_ROW_UNITS * (in ? (int)gj : 0);
   const float4 a = r[0], b = r[1], c = r[2];
   const float u = (t - __builtin_fmaf(gj + 0.5f, w, lo)) * ih;
-  float sb = b.y;
-  sb = __builtin_fmaf(sb, u, b.x); sb = __builtin_fmaf(sb, u, a.w); sb = __builtin_fmaf(sb, u, a.z);
-  sb = __builtin_fmaf(sb, u, a.y); sb = __builtin_fmaf(sb, u, a.x);
-  float sa = c.w;
-  sa = __builtin_fmaf(sa, u, c.z); sa = __builtin_fmaf(sa, u, c.y); sa = __builtin_fmaf(sa, u, c.x);
-  sa = __builtin_fmaf(sa, u, b.w); sa = __builtin_fmaf(sa, u, b.z);
-  lb2 = in ? sb : NAN;
-  la2 = in ? sa : NAN;
+  // the row interleaves the sides, {b_k, a_k} at 2k: both Horner sums as one
+  // packed chain (v_pk_fma_f32 on register pairs, the same fma per side)
+  const f2 uu = {u, u};
+  f2 s = {c.z, c.w};
+  s = __builtin_elementwise_fma(s, uu, f2{c.x, c.y});
+  s = __builtin_elementwise_fma(s, uu, f2{b.z, b.w});
+  s = __builtin_elementwise_fma(s, uu, f2{b.x, b.y});
+  s = __builtin_elementwise_fma(s, uu, f2{a.z, a.w});
+  s = __builtin_elementwise_fma(s, uu, f2{a.x, a.y});
+  lb2 = in ? s.x : NAN;
+  la2 = in ? s.y : NAN;
 }
 
 // PREC is a template parameter: with the f64 inverse-CDF path reachable, the
@@ -3320,7 +3323,8 @@ __device__ __forceinline__ double log2_fast(double x) {
 // one side's log-polynomial from its reduced cell moments (wave-collective):
 // lane 4q holds moment q's f64 sum; m = the cell's log2 shift; flagged: the
 // side takes the exact sum for its candidates.  Lanes 0..5 write c_0..c_5 to
-// out[0..5] (f32), NaN in all six when the side is flagged or fails the check.
+// out[0], out[2], .. out[10] (f32; the row interleaves the two sides), NaN in
+// all six when the side is flagged or fails the check.
 __device__ __forceinline__ void logpoly_side(double sum, float m, bool flagged, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   double M[kTabMoments];
@@ -3346,7 +3350,7 @@ __device__ __forceinline__ void logpoly_side(double sum, float m, bool flagged, 
   for (int k = 4; k >= 0; --k) pv = __builtin_fma(pv, u, C[k]);
   const bool bad = lane < 11 && (!pos || !(fabs(pv - y) <= kLpTol * (1.0 + fabs(y))));
   const bool any = __ballot(bad) != 0ull || flagged || !(m == m);
-  if (lane < 6) out[lane] = any ? NAN : (float)c;
+  if (lane < 6) out[2 * lane] = any ? NAN : (float)c;         // (the sides interleaved: {b_k, a_k} at 2k)
 }
 
 // a moment-cell side of at most this many component rows (the below side: <=
@@ -3452,7 +3456,7 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     const unsigned long long bm = __ballot(bad);
     const bool row_bad = rl < kLpRowsPerWave && ((bm >> b0) & 0x7FFull) != 0ull;
     if (live && k < 6)
-      reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * jr)[6 * jb.side + k] = row_bad ? NAN : (float)cf;
+      reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * jr)[2 * k + jb.side] = row_bad ? NAN : (float)cf;
 #ifdef TPE_TABLES_TRACE
     TT(2);
     if (lane == 0 && (blockIdx.x % 4) == 0 && wave < 2)
@@ -3580,7 +3584,7 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       // shift and flag, as the moment row takes them)
       const float m = __shfl(mx, kTabMoments);
       const bool fl = __shfl(bad || all_exact ? 1 : 0, kTabMoments) != 0;
-      logpoly_side(sum, m, fl, row + 6 * jb.side);
+      logpoly_side(sum, m, fl, row + jb.side);
 #ifdef TPE_TABLES_TRACE
       TT(5);
       if (lane == 0 && (blockIdx.x % 8) == 0 && wave < 2)

@@ -192,8 +192,9 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  *     alike).  m = NaN (a significant term too narrow to expand) and t outside
  *     the cells fall back to the exact sum.
  *     TPE_F_LOGPOLY (both sides fit the sample stage's LDS on one grid: the
- *     finer side's cells for both): one table of 48-B rows, row j = {b_0..b_5,
- *     a_0..a_5}: the degree-5 polynomials in u of log2 s_below(t) and log2
+ *     finer side's cells for both): one table of 48-B rows, row j = {b_0, a_0,
+ *     b_1, a_1, .., b_5, a_5} (the sides interleaved: one packed Horner chain
+ *     evaluates both): the degree-5 polynomials in u of log2 s_below(t) and log2
  *     s_above(t) (shift included) on cell j — the table stage evaluates each
  *     side's moment series in f64 at the 6 Chebyshev nodes of [-1, 1],
  *     interpolates, and checks the polynomial at u = 0, +-1/2, +-1 against the
