@@ -283,6 +283,7 @@ def roofline(prof, fmt='moments'):
     direct-evaluation ceiling and is context, not a roofline fraction."""
     pmc = _pmc()
     kernels = {}
+    stage_total = {}           # every stage's time on the stream, measured alike (the dominant one's pick)
     for name, recs in prof.items():
         ms = np.array([r[0] for r in recs])
         if not len(ms) or name == 'fit':
@@ -296,6 +297,7 @@ def roofline(prof, fmt='moments'):
             ms = kms
         secs = ms.sum() * 1e-3
         k = dict(avg_launch_ms=float(ms.mean()), launches=int(len(ms)), total_ms=float(ms.sum()))
+        stage_total[name] = float(stage_ms.sum())
         if ms is not stage_ms:
             k.update(timing='kernel start/stop events (hipExtLaunchKernel)',
                      avg_stage_ms=float(stage_ms.mean()))
@@ -338,7 +340,9 @@ def roofline(prof, fmt='moments'):
         if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
             k['traffic'] = (2 * c['FETCH_SIZE'] + c['WRITE_SIZE']) * 1024.0
         kernels[name] = k
-    dom = max((n for n in kernels if kernels[n].get('bound')), key=lambda n: kernels[n]['total_ms'], default=None)
+    # (by the stages' stream times: the sample stage's kernel-only time would
+    # otherwise be compared with the table stage's time including its dispatch)
+    dom = max((n for n in kernels if kernels[n].get('bound')), key=lambda n: stage_total[n], default=None)
     if dom is None:
         return None, kernels
     r = dict(kernels[dom])
