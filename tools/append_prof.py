@@ -41,7 +41,12 @@ def main():
         tid += 1
     torch.cuda.synchronize()
     print('appending suggest p50 %.1f us (profiled)' % (1e6 * np.median(lat)))
-    pstats.Stats(pr).sort_stats('tottime').print_stats(30)
+    st = pstats.Stats(pr)
+    rows = sorted(st.stats.items(), key=lambda kv: -kv[1][2])[:30]
+    print('%8s %10s %10s  %s' % ('calls', 'own us', 'cum us', 'function (per suggest)'))
+    for (f, line, name), (cc, nc, tt, ct, _) in rows:
+        print('%8.1f %10.2f %10.2f  %s:%d(%s)' % (nc / len(lat), 1e6 * tt / len(lat), 1e6 * ct / len(lat),
+                                                  os.path.basename(f), line, name))
 
 
 if __name__ == '__main__':
