@@ -131,7 +131,11 @@ def test_native_pack_matches_numpy_packer(precision):
                                   np.round(np.exp(rs.normal(1, .5, 9)) / .25) * .25,
                                   np.round(np.exp(rs.normal(1, .5, 90)) / .25) * .25, 1.0),
              parzen.fit_posterior('categorical', dict(p=[.2, .3, .5], upper=3), rs.randint(0, 3, 9),
-                                  rs.randint(0, 3, 90), 1.0)]
+                                  rs.randint(0, 3, 90), 1.0),
+             # (a bounded side of >= 2048 components: its acceptance terms come from
+             # the packer's parallel pass, summed in numpy's order)
+             parzen.fit_posterior('quniform', dict(low=-3.0, high=3.0, q=0.01), np.round(rs.uniform(-3, 3, 9), 2),
+                                  np.round(np.clip(rs.normal(2.5, 0.4, 3000), -3, 3), 2), 1.0)]
     lps = [LevelProblem(p, i + 3, np.arange(i + 1) + 100) for i, p in enumerate(posts)]
     e = _engine(precision)
     for C in (24, 5000, 1 << 17):      # 2^17: fine sort keys and per-tile tail splits
@@ -145,6 +149,8 @@ def test_native_pack_matches_numpy_packer(precision):
         for f in N.PROBLEM_DTYPE.names:
             np.testing.assert_allclose(prob[f].astype(float), ref['prob'][f].astype(float), rtol=1e-6, atol=0,
                                        err_msg=f)
+        # the large bounded quantized side's -log(acceptance mass): the same bits as numpy's
+        assert prob['above_base'][-1] == ref['prob']['above_base'][-1]
         np.testing.assert_array_equal(_blob(e, info, info.off_tiles, N.TILE_DTYPE, info.n_tiles), ref['tiles'])
         nw = sum(ref['counts_w'])
         np.testing.assert_array_equal(_blob(e, info, info.off_work, N.WORK_DTYPE, nw), ref['work'])
