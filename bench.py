@@ -85,20 +85,37 @@ def rf_loss(v, tid):
     return loss + 1e-9 * tid
 
 
+def loss_domain(space, loss):
+    """A Domain whose objective is ``loss(flat values, tid)``: called with the
+    trial's {label: value} spec and its Ctrl (pass_expr_memo_ctrl)."""
+    from hyperopt_amd import base
+
+    def fn(expr, memo, ctrl):
+        return loss(memo, ctrl.current_trial['tid'])
+    return base.Domain(fn, space, pass_expr_memo_ctrl=True)
+
+
+def evaluate(domain, trials, d):
+    """Evaluate document ``d`` and store its result as FMinIter.serial_evaluate
+    does (fmin.py:40-70): Domain.evaluate's result dict, state DONE."""
+    from hyperopt_amd import base
+    result = domain.evaluate(base.spec_from_misc(d['misc']), base.Ctrl(trials, current_trial=d))
+    d['state'] = base.JOB_STATE_DONE
+    d['result'] = result
+
+
 def make_history(n, seed, loss=None):
     """``n`` prior draws of the config-3 tree space (rand.suggest) with losses
-    from ``loss(vals, tid)`` (default synthetic_loss)."""
+    from ``loss(vals, tid)`` (default synthetic_loss), evaluated as fmin
+    evaluates them."""
     from hyperopt_amd import base, hp, rand
-    loss = synthetic_loss if loss is None else loss
-    domain = base.Domain(lambda d: 0.0, tree_space(hp))
+    domain = loss_domain(tree_space(hp), synthetic_loss if loss is None else loss)
     trials = base.Trials()
     rs = np.random.RandomState(seed)
     docs = []
     for tid in range(n):
         d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
-        v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
-        d['state'] = base.JOB_STATE_DONE
-        d['result'] = {'status': 'ok', 'loss': loss(v, tid)}
+        evaluate(domain, trials, d)
         docs.append(d)
     trials.insert_trial_docs(docs)
     trials.refresh()
@@ -387,15 +404,13 @@ def mixed10_history(n, seed):
     """Config 2's history: ``n`` prior draws of the 10-dim mixed space with
     loss sum((v - 0.3)^2) + 1e-9 * tid."""
     from hyperopt_amd import base, hp, rand
-    domain = base.Domain(lambda d: 0.0, mixed10_space(hp))
+    domain = loss_domain(mixed10_space(hp), lambda v, tid: sum((float(x) - 0.3) ** 2 for x in v.values()) + 1e-9 * tid)
     trials = base.Trials()
     rs = np.random.RandomState(seed)
     docs = []
     for tid in range(n):
         d = rand.suggest([tid], domain, trials, rs.randint(2 ** 31 - 1))[0]
-        v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
-        d['state'] = base.JOB_STATE_DONE
-        d['result'] = {'status': 'ok', 'loss': sum((float(x) - 0.3) ** 2 for x in v.values()) + 1e-9 * tid}
+        evaluate(domain, trials, d)
         docs.append(d)
     trials.insert_trial_docs(docs)
     trials.refresh()
@@ -607,7 +622,6 @@ def main():
     # cache, its value orders and the tree records instead of reusing them
     appending = None
     if not args.no_appending:
-        from hyperopt_amd import base as base_mod
         n_app = max(10, min(args.steps, 50))
         lat_a, tid = [], new_id
         for i in range(n_app + 2):
@@ -618,10 +632,7 @@ def main():
                 lat_a.append(dt)
             trials.insert_trial_docs(docs)
             trials.refresh()
-            d = trials.trials[-1]
-            v = {k: x[0] for k, x in d['misc']['vals'].items() if x}
-            d['state'] = base_mod.JOB_STATE_DONE
-            d['result'] = {'status': 'ok', 'loss': synthetic_loss(v, tid)}
+            evaluate(domain, trials, trials.trials[-1])
             tid += 1
         appending = dict(p50_suggest_ms=1e3 * float(np.median(lat_a)),
                          p99_suggest_ms=1e3 * float(np.percentile(lat_a, 99)), suggests=n_app,

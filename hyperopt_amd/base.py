@@ -102,17 +102,33 @@ def _logging(base_cls, name, hook):
     return g
 
 
+# Document tracking.  A Trials stores the objects it is given (the reference
+# appends the caller's documents, base.py:295-307, and a value assigned into a
+# document is that object).  The suggest path keeps a SoA cache of the history
+# (history.py) and must see every edit the reference's per-call walk would see
+# (tpe.py:820-842).  Documents and the containers inside them that this module
+# builds (rand / tpe suggestions, Domain results, unpickled Trials) are
+# *tracked*: dict / list subclasses whose edits, at any depth, put the document
+# in the mutation logs of each Trials holding it.  Anything else a document
+# reaches — the caller's own dict or list, assigned or inserted — is stored as
+# it is, and the document is marked *watched* (``_fx``): the cache re-reads it
+# on every suggest instead of trusting the log — only its loss when the one
+# such container is its result (``_fx == 'result'``: the ask-tell pattern
+# ``doc['result'] = {...}``), else all it reads.  A document that is not
+# tracked at all (a plain dict inserted by the caller) is watched in full by
+# the cache and re-filtered by every refresh.
+#
+# Each tracked container points at the container holding it (``_up``, unset =
+# not yet part of a document); a tracked container assigned into a document
+# while unowned becomes part of it (no copy).  ``_fx`` goes up the chain to the
+# document when a watched value is stored anywhere below it.
+
+
 class _Doc(dict):
-    """A trial document held by a ``Trials``: a dict whose in-place edits —
-    at any depth through the dicts and lists it holds — put it in the
-    mutation log of each Trials holding it (``Trials._mutated``, id ->
-    document).  The SoA history cache (history.py) reads that log, so an edit
-    of a completed document it has already consumed rebuilds the cache
-    instead of serving a stale history (the reference re-reads every
-    document, tpe.py:820-842).  Values assigned into a tracked document are
-    stored as tracked copies; pickles and deep copies are plain dicts (a
-    Trials re-tracks its documents when unpickled)."""
-    __slots__ = ('_ts',)
+    """A tracked trial document (see above); ``_ts`` = the mutation logs of
+    the Trials holding it, ``_fx`` set once it holds a container it cannot
+    track.  Pickles and copies are plain dicts."""
+    __slots__ = ('_ts', '_fx')
 
     def _log(self):
         for t in getattr(self, '_ts', ()):
@@ -122,9 +138,11 @@ class _Doc(dict):
         return dict, (dict(self),)
 
     def __setitem__(self, k, v):
-        dict.__setitem__(self, k, _wrap(v, self))
-        if k not in _UNTRACKED_KEYS:
-            self._log()
+        if k in _UNTRACKED_KEYS:
+            dict.__setitem__(self, k, v)
+            return
+        dict.__setitem__(self, k, _attach(v, self, k) if k in _READ_KEYS else v)
+        self._log()
 
     def __delitem__(self, k):
         dict.__delitem__(self, k)
@@ -158,60 +176,94 @@ class _Doc(dict):
 
 # bookkeeping keys FMinIter / workers write that no history reads
 _UNTRACKED_KEYS = frozenset(('owner', 'book_time', 'refresh_time', 'version'))
+# the document keys a history or a refresh reads (tpe.py:820-842, base.py:183-194)
+_READ_KEYS = frozenset(('tid', 'state', 'result', 'misc', 'exp_key'))
+
+
+def _log_up(c):
+    u = getattr(c, '_up', None)
+    while u is not None:
+        if type(u) is _Doc:
+            u._log()
+            return
+        u = getattr(u, '_up', None)
 
 
 class _Part(dict):
-    """A dict inside a tracked document (``result``, ``misc``, ``misc['vals']`` …)."""
-    __slots__ = ('_root',)
+    """A tracked dict inside a document (``result``, ``misc``, ``misc['vals']`` …)."""
+    __slots__ = ('_up', '_fx')
 
-    def _log(self):
-        self._root._log()
+    _log = _log_up
+    _reads = None                      # the keys a history reads (None: all)
 
     def __reduce_ex__(self, protocol):
         return dict, (dict(self),)
 
     def __setitem__(self, k, v):
-        dict.__setitem__(self, k, _wrap(v, self._root))
-        self._log()
+        r = self._reads
+        dict.__setitem__(self, k, _attach(v, self) if r is None or k in r else v)
+        _log_up(self)
 
     def __delitem__(self, k):
         dict.__delitem__(self, k)
-        self._log()
+        _log_up(self)
 
     update, setdefault, pop, popitem, clear, __ior__ = (
         _Doc.update, _Doc.setdefault, _Doc.pop, _Doc.popitem, _Doc.clear, _Doc.__ior__)
 
 
-class _PartList(list):
-    """A list inside a tracked document (``misc['vals'][label]`` …)."""
-    __slots__ = ('_root',)
+class _Result(_Part):
+    """A result dict made here (Domain.evaluate / new_result): of its values
+    only the loss is read by a history (Domain.loss, tpe.py:820-842), so the
+    caller's other values (nested dicts included) are stored without
+    watching the document."""
+    __slots__ = ()
+    _reads = frozenset(('loss',))
 
-    def _log(self):
-        self._root._log()
+    @classmethod
+    def of(cls, d):
+        r = cls(d)
+        r._up, r._fx = None, False
+        for k in cls._reads:
+            if k in r:
+                _attach(dict.__getitem__(r, k), r)
+        return r
+
+    @classmethod
+    def new(cls, **kw):
+        r = cls(kw)
+        r._up, r._fx = None, False
+        return r
+
+
+class _PartList(list):
+    """A tracked list inside a document (``misc['vals'][label]`` …)."""
+    __slots__ = ('_up', '_fx')
+
+    _log = _log_up
 
     def __reduce_ex__(self, protocol):
         return list, (list(self),)
 
     def __setitem__(self, i, v):
-        r = self._root
-        list.__setitem__(self, i, [_wrap(x, r) for x in v] if isinstance(i, slice) else _wrap(v, r))
-        self._log()
+        list.__setitem__(self, i, [_attach(x, self) for x in v] if isinstance(i, slice) else _attach(v, self))
+        _log_up(self)
 
     def __delitem__(self, i):
         list.__delitem__(self, i)
-        self._log()
+        _log_up(self)
 
     def append(self, v):
-        list.append(self, _wrap(v, self._root))
-        self._log()
+        list.append(self, _attach(v, self))
+        _log_up(self)
 
     def extend(self, vs):
-        list.extend(self, [_wrap(v, self._root) for v in vs])
-        self._log()
+        list.extend(self, [_attach(v, self) for v in vs])
+        _log_up(self)
 
     def insert(self, i, v):
-        list.insert(self, i, _wrap(v, self._root))
-        self._log()
+        list.insert(self, i, _attach(v, self))
+        _log_up(self)
 
     def __iadd__(self, vs):
         self.extend(vs)
@@ -219,79 +271,143 @@ class _PartList(list):
 
     def __imul__(self, n):
         list.__imul__(self, n)
-        self._log()
+        _log_up(self)
         return self
 
     pop, remove, clear, sort, reverse = (_logging(list, n, '_log')
                                          for n in ('pop', 'remove', 'clear', 'sort', 'reverse'))
 
 
-# value types stored as they are (checked first: most values in a document)
-_PLAIN = frozenset((float, int, str, bool, type(None), np.float64, np.int64, np.float32, np.int32,
+# value types that hold no container (stored as they are, nothing to watch)
+_PLAIN = frozenset((float, int, str, bool, type(None), tuple, np.float64, np.int64, np.float32, np.int32,
                     np.bool_, datetime.datetime))
 
 
-def _wrap(v, root):
-    """``v`` as part of the tracked document ``root`` (dicts and lists copied
-    into tracked ones at any depth; everything else stored as it is)."""
+def _mark(c):
+    """``c`` (and every container above it, up to its document) holds a value
+    it cannot track: the document is watched."""
+    while c is not None and getattr(c, '_fx', False) is not True:
+        c._fx = True
+        if type(c) is _Doc:
+            return
+        c = getattr(c, '_up', None)
+
+
+def _attach(v, parent, key=None):
+    """``v`` stored into the tracked container ``parent`` (under ``key``), as
+    the same object: an unowned tracked container becomes part of parent's
+    document; any other container (the caller's own dict or list, or a
+    tracked part of another document) marks the document watched — for its
+    loss only when it is a document's result."""
+    t = type(v)
+    if t in _PLAIN:
+        return v
+    if t in _TRACKED:
+        up = getattr(v, '_up', None)
+        if up is None:
+            v._up = parent
+            if getattr(v, '_fx', False):
+                _mark(parent)
+            return v
+        if up is parent:
+            return v
+    elif isinstance(v, np.generic):
+        return v
+    if key == 'result' and type(parent) is _Doc and isinstance(v, dict):
+        if not getattr(parent, '_fx', False):
+            parent._fx = 'result'
+        return v
+    _mark(parent)
+    return v
+
+
+_TRACKED = frozenset((_Part, _Result, _PartList))
+
+
+def _fresh(v, up=None):
+    """A tracked copy of ``v`` (dicts and lists at any depth) that no caller
+    holds: for values this module creates (results, suggestions, unpickled
+    documents).  Unowned unless ``up`` is given."""
     t = type(v)
     if t in _PLAIN:
         return v
     if isinstance(v, dict):
-        if t is _Part and v._root is root:
-            return v
-        p = _Part(v)
-        p._root = root
+        p = _Part()
         for k, x in v.items():
-            tx = type(x)
-            if tx in _PLAIN:
-                continue
-            if tx is list and len(x) <= 1 and (not x or type(x[0]) in _PLAIN):
-                q = _PartList(x)       # (misc['idxs'/'vals'] entries: inline)
-                q._root = root
-            else:
-                q = _wrap(x, root)
-            dict.__setitem__(p, k, q)
-        return p
-    if isinstance(v, list):
-        if t is _PartList and v._root is root:
-            return v
-        p = _PartList(v)
-        p._root = root
-        for i, x in enumerate(v):
-            if type(x) not in _PLAIN:
-                list.__setitem__(p, i, _wrap(x, root))
-        return p
-    return v
+            dict.__setitem__(p, k, _fresh(x, p))
+    elif isinstance(v, list):
+        p = _PartList()
+        list.extend(p, [_fresh(x, p) for x in v])
+    else:
+        return v
+    if up is not None:
+        p._up = up
+    return p
+
+
+def _fresh_doc(d):
+    """A tracked document copied from ``d`` (unpickled Trials only)."""
+    doc = _Doc()
+    for k, v in d.items():
+        dict.__setitem__(doc, k, _fresh(v, doc) if k in _READ_KEYS else v)
+    return doc
+
+
+def tracked_misc(tid, cmd, workdir, chosen):
+    """The misc of one suggested id (miscs_update_idxs_vals for one id,
+    base.py:77-105: idxs [tid] / vals [value] per active label, [] per
+    inactive one), built tracked and unowned (rand / tpe suggestions)."""
+    idxs, vals = _Part(), _Part()
+    for k, v in chosen.items():
+        if v is None:
+            a, b = _PartList(), _PartList()
+        else:
+            a, b = _PartList((tid,)), _PartList((v,))
+        a._up = idxs
+        b._up = vals
+        dict.__setitem__(idxs, k, a)
+        dict.__setitem__(vals, k, b)
+    misc = _Part(tid=tid, cmd=cmd, workdir=workdir, idxs=idxs, vals=vals)
+    idxs._up = vals._up = misc
+    misc._up, misc._fx = None, False      # (set: a getattr default on an unset slot raises inside)
+    return misc
 
 
 def _track(doc, logs):
-    """``doc`` as a document logging into each of ``logs`` (a Trials'
-    mutation logs): a tracked document gains the logs (it may belong to
-    several Trials), anything else becomes a tracked copy."""
+    """Register ``doc`` with a Trials' mutation ``logs`` (a document may
+    belong to several Trials); a plain dict stays as it is (watched)."""
     if type(doc) is _Doc:
         ts = getattr(doc, '_ts', None)
         if ts is None:
             doc._ts = list(logs)
         else:
             ts.extend(lg for lg in logs if not any(t is lg for t in ts))
-        return doc
-    d = _Doc(doc)
-    for k, v in doc.items():
-        if type(v) not in _PLAIN:
-            dict.__setitem__(d, k, _wrap(v, d))
-    d._ts = list(logs)
-    return d
+    return doc
 
 
 def _tracked_by(doc, log):
     return type(doc) is _Doc and any(t is log for t in getattr(doc, '_ts', ()))
 
 
+def watched(doc, log):
+    """What a history must re-read of ``doc`` on every suggest: 0 nothing (a
+    tracked document of the Trials whose mutation log is ``log``), 1 its loss
+    (its result is the caller's dict), 2 everything it reads (a plain
+    document, another Trials' one, or one holding another container it
+    cannot track)."""
+    if log is None or type(doc) is not _Doc or not any(t is log for t in getattr(doc, '_ts', ())):
+        return 2
+    fx = getattr(doc, '_fx', False)
+    return 0 if not fx else 1 if fx == 'result' else 2
+
+
 class _View(list):
-    """``Trials.trials``: a list whose edits other than appends (an element
-    replaced, removed, inserted or reordered) move the owner's ``_view_gen``,
-    as a refresh that changes the view does (history.py rebuilds on it)."""
+    """``Trials.trials``: a list whose edits (an element appended, replaced,
+    removed, inserted or reordered) move the owner's ``_view_gen``, as a
+    refresh that changes the view does (history.py rebuilds on it), and make
+    the next refresh rebuild the view from ``_dynamic_trials`` as the
+    reference's does (base.py:231-242: a document appended to the view alone
+    is gone after it).  Refresh itself extends the view with list.extend."""
     __slots__ = ('_owner',)
 
     def __reduce_ex__(self, protocol):
@@ -301,9 +417,10 @@ class _View(list):
         o = self._owner
         o._view_gen = getattr(o, '_view_gen', 0) + 1
 
-    __setitem__, __delitem__, insert, pop, remove, clear, sort, reverse, __imul__ = (
-        _logging(list, n, '_moved') for n in ('__setitem__', '__delitem__', 'insert', 'pop', 'remove',
-                                              'clear', 'sort', 'reverse', '__imul__'))
+    (__setitem__, __delitem__, insert, pop, remove, clear, sort, reverse, __imul__, append, extend,
+     __iadd__) = (_logging(list, n, '_moved') for n in ('__setitem__', '__delitem__', 'insert', 'pop', 'remove',
+                                                         'clear', 'sort', 'reverse', '__imul__', 'append',
+                                                         'extend', '__iadd__'))
 
 
 class _DynList(list):
@@ -330,7 +447,17 @@ def coarse_utcnow():
 
 
 class Trials(object):
-    """History of evaluated and scheduled trials (base.py:138-438)."""
+    """History of evaluated and scheduled trials (base.py:138-438).
+
+    Holds the caller's objects, as the reference does: ``insert_trial_docs``
+    appends the documents themselves (the caller's list is not touched) and a
+    value assigned into a document is stored as that object, so an edit made
+    later through any handle the caller kept is this Trials' state.  The
+    documents this package builds (``new_trial_docs``, rand / tpe
+    suggestions, ``Domain.evaluate`` / ``new_result`` dicts) are tracked dict
+    and list subclasses, so the suggest path's history cache learns of their
+    edits from a log; documents or values of the caller's own are re-read by
+    it on every suggest (see _Doc, history.py)."""
 
     def __init__(self, exp_key=None, refresh=True):
         self._ids = set()
@@ -346,25 +473,30 @@ class Trials(object):
     def __getstate__(self):
         d = dict(self.__dict__)
         d.pop('_tpe_history', None)
-        for k in ('_mutated', '_rlog', '_dyn_ref', '_dyn_dirty', '_excluded', '_n_dyn', '_gen_seen'):
+        for k in ('_mutated', '_rlog', '_dyn_ref', '_dyn_dirty', '_excluded', '_n_dyn', '_gen_seen', '_plain'):
             d.pop(k, None)            # (refresh bookkeeping: rebuilt by the first refresh)
         return d
 
     def __setstate__(self, d):
-        # documents come back as plain dicts (_Doc.__reduce_ex__): tracked again,
-        # the view keeping its documents (the same objects as _dynamic_trials')
+        # documents come back as plain dicts (_Doc.__reduce_ex__) that nobody
+        # else holds: tracked copies, the view keeping its documents (the same
+        # objects as _dynamic_trials')
         self.__dict__.update(d)
         self._mutated, self._rlog = {}, {}
         new = {}
-        dyn = self._dyn_list(self._dynamic_trials)
-        for i, tt in enumerate(dyn):
-            t = new[id(tt)] = _track(tt, self._logs())
-            list.__setitem__(dyn, i, t)
+        logs = self._logs()
+
+        def fresh(tt):
+            t = new.get(id(tt))
+            if t is None:
+                t = new[id(tt)] = _track(_fresh_doc(tt), logs)
+            return t
+        dyn = self._dyn_list([fresh(tt) for tt in self._dynamic_trials])
         self._dynamic_trials = dyn
         self._dyn_ref = None           # the next refresh rebuilds the view
         old = self.__dict__.get('_trials')
         if old is not None:
-            self._trials = self._view([new.get(id(tt)) or _track(tt, self._logs()) for tt in old])
+            self._trials = self._view([fresh(tt) for tt in old])
 
     def _logs(self):
         return (self.__dict__.setdefault('_mutated', {}), self.__dict__.setdefault('_rlog', {}))
@@ -380,13 +512,16 @@ class Trials(object):
         return v
 
     def _track_all(self):
-        """Track every document of _dynamic_trials in this Trials' log (a
-        document put there directly, a deep copy, another Trials' document)."""
+        """Register every tracked document of _dynamic_trials with this
+        Trials' logs (one put there directly, another Trials' document) and
+        collect the plain ones (watched: re-filtered by every refresh)."""
         logs = self._logs()
-        dyn = self._dynamic_trials
-        for i, tt in enumerate(dyn):
-            if not _tracked_by(tt, logs[0]):
-                dyn[i] = _track(tt, logs)
+        plain = self._plain = {}
+        for tt in self._dynamic_trials:
+            if type(tt) is not _Doc:
+                plain[id(tt)] = tt
+            elif not _tracked_by(tt, logs[0]):
+                _track(tt, logs)
 
     def aname(self, trial, name):
         return 'ATTACH::%s::%s' % (trial['tid'], name)
@@ -427,9 +562,10 @@ class Trials(object):
         Incremental when nothing but appends happened since the last refresh
         (FMinIter's use): the view list is extended in place by the appended
         documents that qualify — unless a document already seen was edited
-        into or out of the view (its state or exp_key, in the refresh log), or
+        into or out of the view (a tracked document's state or exp_key, in the
+        refresh log; a plain document's, re-read here), or
         ``_dynamic_trials`` / the view were edited otherwise; then the view is
-        rebuilt from every document, as the reference does (base.py:183-194)."""
+        rebuilt from every document, as the reference does (base.py:231-242)."""
         old = getattr(self, '_trials', None)
         logs = self._logs()
         log, rlog = logs
@@ -444,14 +580,17 @@ class Trials(object):
         if (old is not None and type(old) is _View and dyn is d.get('_dyn_ref') and not d.get('_dyn_dirty')
                 and d.get('_gen_seen') == gen and len(dyn) >= n0):
             excluded = d.get('_excluded', ())
-            if all(keep(tt) and id(tt) not in excluded for tt in rlog.values()):
+            plain = d.setdefault('_plain', {})
+            if all(keep(tt) and id(tt) not in excluded for tt in rlog.values()) and \
+                    all(keep(tt) != (id(tt) in excluded) for tt in plain.values()):
                 rlog.clear()
                 add = []
                 for i in range(n0, len(dyn)):
                     tt = dyn[i]
-                    if not _tracked_by(tt, log):       # (put in _dynamic_trials directly)
-                        tt = _track(tt, logs)
-                        list.__setitem__(dyn, i, tt)
+                    if type(tt) is not _Doc:
+                        plain[id(tt)] = tt
+                    elif not _tracked_by(tt, log):     # (put in _dynamic_trials directly)
+                        _track(tt, logs)
                     if keep(tt):
                         add.append(tt)
                     else:
@@ -521,23 +660,19 @@ class Trials(object):
         return trial
 
     def _insert_trial_docs(self, docs):
-        """Appends ``docs`` as tracked documents (_Doc); a list passed in is
-        updated in place to hold them, so the caller's list keeps naming the
-        documents this Trials holds."""
+        """Appends the documents themselves (base.py:295-300): a tracked one
+        (new_trial_docs, rand / tpe suggestions) logs its edits into this
+        Trials; a plain dict is watched (see _Doc)."""
         logs = self._logs()
         rval = [doc['tid'] for doc in docs]
-        tracked = [_track(doc, logs) for doc in docs]
-        if type(docs) is list:
-            docs[:] = tracked
-        self._dynamic_trials.extend(tracked)
+        for doc in docs:
+            _track(doc, logs)
+        self._dynamic_trials.extend(docs)
         return rval
 
     def insert_trial_docs(self, docs):
-        checked = [self.assert_valid_trial(SONify(doc)) for doc in docs]
-        rval = self._insert_trial_docs(checked)
-        if type(docs) is list:
-            docs[:] = checked
-        return rval
+        docs = [self.assert_valid_trial(SONify(doc)) for doc in docs]
+        return self._insert_trial_docs(docs)
 
     def new_trial_ids(self, N):
         aa = len(self._ids)
@@ -546,15 +681,17 @@ class Trials(object):
         return rval
 
     def new_trial_docs(self, tids, specs, results, miscs):
+        """Documents holding the given spec / result / misc objects
+        (base.py:315-331), as tracked documents (_Doc)."""
         assert len(tids) == len(specs) == len(results) == len(miscs)
         rval = []
+        ek = self._exp_key
         for tid, spec, result, misc in zip(tids, specs, results, miscs):
-            doc = dict(state=JOB_STATE_NEW, tid=tid, spec=spec, result=result, misc=misc)
-            doc['exp_key'] = self._exp_key
-            doc['owner'] = None
-            doc['version'] = 0
-            doc['book_time'] = None
-            doc['refresh_time'] = None
+            doc = _Doc(state=JOB_STATE_NEW, tid=tid, spec=spec, result=result, misc=misc, exp_key=ek,
+                       owner=None, version=0, book_time=None, refresh_time=None)
+            doc._fx = False
+            _attach(result, doc)
+            _attach(misc, doc)
             rval.append(doc)
         return rval
 
@@ -648,10 +785,11 @@ class Domain(object):
             rval = self.fn(expr=self.expr, memo=self.memo_from_config(config), ctrl=ctrl)
         else:
             rval = self.fn(_space.evaluate(self.expr, config))
+        # (a new dict, as in the reference: returned tracked, see _Doc)
         if isinstance(rval, (float, int, np.number)):
-            dict_rval = {'loss': float(rval), 'status': STATUS_OK}
+            dict_rval = _Result.new(loss=float(rval), status=STATUS_OK)
         else:
-            dict_rval = dict(rval)
+            dict_rval = _Result.of(rval)
             status = dict_rval['status']
             if status not in STATUS_STRINGS:
                 raise InvalidResultStatus(dict_rval)
@@ -682,4 +820,4 @@ class Domain(object):
         return result['status']
 
     def new_result(self):
-        return {'status': STATUS_NEW}
+        return _Result.new(status=STATUS_NEW)

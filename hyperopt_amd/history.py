@@ -12,17 +12,21 @@ Fast path requirements (else the generic reference-order walk is used):
 documents in increasing tid order, unique tids, no ``misc['from_tid']``,
 and ``Domain.loss`` not overridden.
 
-Staleness: ``Trials`` holds its documents as tracked dicts (base._Doc)
-whose in-place edits, at any depth, land in ``Trials._mutated``; a view edit
-that is not an append, or a refresh that changes the view, moves
+Staleness: a ``Trials`` stores the caller's documents as they are; the ones
+built by this package (suggestions, Domain results) are tracked dicts
+(base._Doc) whose in-place edits, at any depth, land in ``Trials._mutated``.
+A view edit, or a refresh that changes the view other than by appends, moves
 ``Trials._view_gen``.  The cache rebuilds when a completed document it has
-consumed appears in the mutation log or the view generation moved; pending
-documents (values and loss) are re-read on every call.  So every edit the
-reference's per-call walk would see (tpe.py:820-842) is seen here, without a
-pass over the documents.
+consumed appears in the mutation log or the view generation moved.  Pending
+documents (values and loss) and *watched* documents — plain dicts, or tracked
+ones holding a container of the caller's (base.watched) — are re-read on every
+call and compared with what the cache consumed.  So every edit the
+reference's per-call walk would see (tpe.py:820-842) is seen here, with a
+pass over the watched documents only.
 """
 import bisect
 import ctypes
+import itertools
 import math
 import weakref
 
@@ -176,6 +180,9 @@ class _Cache(object):
         self.losses = _Grow(np.float64)
         self.pending = []              # positions whose loss may still change
         self.pending_vals = {}         # position -> (misc['vals'] object, its values) of a pending document
+        self.watch = []                # (document, snapshot) of the completed watched documents
+        self.watch_res = []            # result dicts of the completed loss-watched documents ...
+        self.watch_loss = []           # ... and the losses read from them
         self.obs_tid = {k: _Grow(np.int64) for k in labels}     # tid of each observation (append-only)
         self.obs_val = {k: _Grow(np.int64 if categorical[k] else np.float64) for k in labels}
         self.labels = labels
@@ -205,9 +212,6 @@ class _Cache(object):
             if self.tids.n and tid <= self.tids.a[self.tids.n - 1]:
                 self.ok = False
                 return
-            if not base._tracked_by(d, log):
-                self.ok = False        # not a document of this Trials (edits would go unseen)
-                return
             self.pos[id(d)] = len(self.docs)
             self.docs.append(d)
             self.tids.append(tid)
@@ -218,6 +222,8 @@ class _Cache(object):
             if not final:
                 self.pending.append(self.tids.n - 1)
                 self.pending_vals[self.tids.n - 1] = (vals, self._snap(vals))
+            else:
+                self._watch(d, log)
             for k in self.labels:
                 v = vals.get(k)
                 if v:
@@ -237,6 +243,31 @@ class _Cache(object):
 
     def _snap(self, vals):
         return tuple(tuple(vals.get(k) or ()) for k in self.labels)
+
+    def doc_snap(self, d):
+        """What the cache reads of a document (tid, state, loss, from_tid,
+        values; tuple equality: identical objects compare equal, NaN too)."""
+        misc = d['misc']
+        return (d['tid'], d['state'], d['result'].get('loss'), 'from_tid' in misc, self._snap(misc['vals']))
+
+    def _watch(self, d, log):
+        w = base.watched(d, log)
+        if w == 1:
+            r = d['result']
+            self.watch_res.append(r)
+            self.watch_loss.append(r.get('loss'))
+        elif w:
+            self.watch.append((d, self.doc_snap(d)))
+
+    def watch_changed(self):
+        """A watched document no longer reads as it did when consumed."""
+        if self.watch_res and list(map(dict.get, self.watch_res, itertools.repeat('loss'))) != self.watch_loss:
+            return True
+        snap = self.doc_snap
+        for d, s in self.watch:
+            if snap(d) != s:
+                return True
+        return False
 
     def pending_vals_changed(self):
         """A pending document's values were edited or replaced (a running
@@ -383,7 +414,7 @@ class _Cache(object):
             self.top_keys = L[self.top].tolist()
         return self.top_pos[:m] if self.top is True else self.top[:m]
 
-    def refresh_pending(self):
+    def refresh_pending(self, log):
         if not self.pending:
             return
         self.top = self.below_memo = None     # pending losses may change: rebuild the ranking
@@ -397,6 +428,7 @@ class _Cache(object):
                 keep.append(i)
             else:
                 self.pending_vals.pop(i, None)
+                self._watch(d, log)
         self.pending = keep
 
 
@@ -445,10 +477,11 @@ def extract(domain, trials):
     if cache is not None:
         # the cache follows an append-only view (FMinIter's use).  A refresh or
         # view edit that drops, replaces or reorders documents moves
-        # Trials._view_gen (above); an in-place edit of a completed document
-        # the cache has consumed is in the Trials' mutation log; a pending
-        # document is re-read in full (its values and, below, its loss).
-        if len(cache.docs) > len(docs) or cache.pending_vals_changed():
+        # Trials._view_gen (above); an in-place edit of a completed tracked
+        # document the cache has consumed is in the Trials' mutation log; a
+        # pending document is re-read in full (its values and, below, its
+        # loss), a watched one compared with what was consumed.
+        if len(cache.docs) > len(docs) or cache.pending_vals_changed() or cache.watch_changed():
             cache = None
         elif log:
             pos, pend = cache.pos, set(cache.pending)
@@ -471,7 +504,7 @@ def extract(domain, trials):
         _CACHES.pop(trials, None)
         return _generic(domain, docs, table)
     _CACHES[trials] = cache
-    cache.refresh_pending()
+    cache.refresh_pending(log)
     tids = cache.tids.view()
     hist = History(tids, cache.losses.view(), cache.obs_views(), dev=cache.dev, cache=cache)
     cache.hist = hist if not cache.pending else None

@@ -8,6 +8,7 @@ to the reference's.  Prior draws follow pyll/stochastic.py:30-142.
 """
 import numpy as np
 
+from . import base
 
 
 def prior_draw(rng, dist, a, size):
@@ -54,9 +55,8 @@ def docs_from_choices(new_ids, domain, trials, choices):
     rval = []
     for new_id, chosen in zip(new_ids, choices):
         # the misc miscs_update_idxs_vals builds for one id (base.py:77-105), directly
-        idxs = {k: [] if v is None else [new_id] for k, v in chosen.items()}
-        vals = {k: [] if v is None else [v] for k, v in chosen.items()}
-        misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir, idxs=idxs, vals=vals)
+        # (tracked: edits of the returned documents reach the Trials' history cache)
+        misc = base.tracked_misc(new_id, domain.cmd, domain.workdir, chosen)
         rval.extend(trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc]))
     return rval
 

@@ -87,13 +87,20 @@ def _same_as_walk(d, t):
     return h
 
 
-def _done_trials(d, n, seed=3):
+def _done_trials(d, n, seed=3, tracked=False):
+    """``n`` random-search documents, DONE; their results the caller's plain
+    dicts (loss-watched documents), or with ``tracked`` Domain.new_result()
+    dicts updated in place (tracked documents, as fmin's)."""
     t = base.Trials()
     rs = np.random.RandomState(seed)
     for tid in range(n):
         doc = rand.suggest([tid], d, t, rs.randint(2 ** 31 - 1))[0]
         doc['state'] = base.JOB_STATE_DONE
-        doc['result'] = {'status': 'ok', 'loss': float(rs.uniform())}
+        if tracked:
+            doc['result'] = d.new_result()
+            doc['result'].update(status='ok', loss=float(rs.uniform()))
+        else:
+            doc['result'] = {'status': 'ok', 'loss': float(rs.uniform())}
         t.insert_trial_docs([doc])
     t.refresh()
     return t
@@ -143,18 +150,21 @@ def test_history_cache_rebuilds_on_view_changes():
     assert history._CACHES[t] is cache and len(h5) == len(h4) + 1
 
 
-def test_history_cache_sees_in_place_edits_of_completed_documents():
+@pytest.mark.parametrize('tracked', [False, True])
+def test_history_cache_sees_in_place_edits_of_completed_documents(tracked):
     """Completed documents the cache has consumed, edited in place at any
     depth (values, loss, state), through a view edit without refresh, after
     a pickle round trip, or through the caller's own inserted list: each
     extract equals the reference walk (tpe.py:820-842); edits of bookkeeping
-    keys and of pending documents keep the cache."""
+    keys and of pending documents keep the cache.  Results the caller's
+    plain dicts (loss-watched documents) or tracked ones."""
     import copy
     import pickle
     d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1), 'c': H.hp.choice('c', [0, 1, 2])})
-    t = _done_trials(d, 300)
+    t = _done_trials(d, 300, tracked=tracked)
     _same_as_walk(d, t)
     cache = history._CACHES[t]
+    assert len(cache.watch_res) == (0 if tracked else 300) and not cache.watch
     t.trials[150]['refresh_time'] = 1.0             # bookkeeping: no rebuild
     _same_as_walk(d, t)
     assert history._CACHES[t] is cache
@@ -211,6 +221,132 @@ def test_history_cache_sees_in_place_edits_of_completed_documents():
     t2.trials[-1]['result']['loss'] = -11.0
     h = _same_as_walk(d, t2)
     assert h.losses[-1] == -11.0
+
+
+def _fresh_trials_like(d, t):
+    """A new Trials holding plain copies of ``t``'s view (the reference's
+    state after the same edits)."""
+    import copy
+    t2 = base.Trials()
+    t2.insert_trial_docs([copy.deepcopy(dict(x)) for x in t.trials])
+    t2.refresh()
+    return t2
+
+
+def test_trials_store_the_callers_objects():
+    """insert_trial_docs stores the caller's documents and an assignment into
+    a document stores the assigned object (reference base.py:295-307, 315-331):
+    edits made later through the caller's own handles — the document after
+    insert_trial_docs, a result dict after assignment, a misc held before the
+    insertion, a values list assigned into it, a plain dict document — are the
+    Trials' state, and the history equals the reference walk and a Trials
+    built afresh from that state."""
+    d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1), 'c': H.hp.choice('c', [0, 1, 2])})
+    for tracked in (False, True):
+        tr = _done_trials(d, 60, tracked=tracked)
+        _same_as_walk(d, tr)
+        # 1. the verdict's pattern: edit after insert_trial_docs([doc]), then refresh
+        doc = rand.suggest([60], d, tr, 11)[0]
+        lst = [doc]
+        tr.insert_trial_docs(lst)
+        assert lst[0] is doc and tr._dynamic_trials[-1] is doc
+        doc['state'] = base.JOB_STATE_DONE
+        doc['result'] = {'status': 'ok', 'loss': 0.125}
+        tr.refresh()
+        assert tr.trials[-1] is doc and tr.losses()[-1] == 0.125
+        h = _same_as_walk(d, tr)
+        assert h.losses[-1] == 0.125
+        # 2. a result dict assigned, then mutated through the caller's handle
+        r = {'status': 'ok', 'loss': 2.0}
+        tr.trials[0]['result'] = r
+        assert tr.trials[0]['result'] is r
+        _same_as_walk(d, tr)
+        r['loss'] = 3.0
+        assert tr.losses()[0] == 3.0
+        h = _same_as_walk(d, tr)
+        assert h.losses[0] == 3.0
+        r['loss'] = -1.0                                  # twice: the loss-watch follows the object
+        assert _same_as_walk(d, tr).losses[0] == -1.0
+        # 3. a misc held before the insertion, edited after it
+        doc2 = rand.suggest([61], d, tr, 12)[0]
+        m = doc2['misc']
+        doc2['state'] = base.JOB_STATE_DONE
+        doc2['result'] = {'status': 'ok', 'loss': 0.75}
+        tr.insert_trial_docs([doc2])
+        tr.refresh()
+        _same_as_walk(d, tr)
+        m['vals']['x'] = [0.4242]
+        m['idxs']['x'] = [61]
+        assert tr.trials[-1]['misc'] is m
+        h = _same_as_walk(d, tr)
+        assert 0.4242 in list(h.obs['x'][1])
+        # 4. a values list of the caller's assigned into a document, then edited
+        L = [0.31]
+        tr.trials[5]['misc']['vals']['x'] = L
+        tr.trials[5]['misc']['idxs']['x'] = [tr.trials[5]['tid']]
+        _same_as_walk(d, tr)
+        L[0] = 0.32
+        h = _same_as_walk(d, tr)
+        assert 0.32 in list(h.obs['x'][1]) and 0.31 not in list(h.obs['x'][1])
+        # 5. a plain dict document of the caller's: stored as it is, edits seen
+        plain = dict(rand.suggest([62], d, tr, 13)[0])
+        plain['misc'] = {'tid': 62, 'cmd': None, 'workdir': None, 'idxs': {'x': [62], 'c': []},
+                         'vals': {'x': [0.5], 'c': []}}
+        plain['state'] = base.JOB_STATE_DONE
+        plain['result'] = {'status': 'ok', 'loss': 0.01}
+        tr.insert_trial_docs([plain])
+        tr.refresh()
+        assert tr.trials[-1] is plain and type(plain) is dict
+        _same_as_walk(d, tr)
+        plain['misc']['vals']['x'][0] = 0.55
+        plain['result']['loss'] = 0.02
+        h = _same_as_walk(d, tr)
+        assert h.losses[-1] == 0.02 and 0.55 in list(h.obs['x'][1])
+        plain['state'] = base.JOB_STATE_ERROR             # a plain document leaves the view at refresh
+        tr.refresh()
+        assert plain not in tr.trials
+        _same_as_walk(d, tr)
+        plain['state'] = base.JOB_STATE_DONE              # ... and comes back
+        tr.refresh()
+        assert tr.trials[-1] is plain
+        # the same history as a Trials built afresh from the final state
+        h = _same_as_walk(d, tr)
+        h2 = history.extract(d, _fresh_trials_like(d, tr))
+        assert list(h.losses) == list(h2.losses) and list(h.tids) == list(h2.tids)
+        for k in d.table.labels:
+            assert list(map(float, h.obs[k][1])) == list(map(float, h2.obs[k][1]))
+
+
+def test_fmin_documents_are_tracked():
+    """fmin's own documents (rand / tpe suggestions, Domain.evaluate results)
+    are tracked: the history cache re-reads none of them per suggest, and a
+    result edited through the Trials afterwards is still seen."""
+    from hyperopt_amd.fmin import fmin
+    t = base.Trials()
+    fmin(lambda x: (x - 0.3) ** 2, H.hp.uniform('x', 0, 1), algo=rand.suggest, max_evals=40, trials=t,
+         rstate=np.random.RandomState(0))
+    d = base.Domain(lambda x: 0.0, H.hp.uniform('x', 0, 1))
+    _same_as_walk(d, t)
+    c = history._CACHES[t]
+    assert not c.watch and not c.watch_res
+    t.trials[10]['result']['loss'] = -4.0
+    assert _same_as_walk(d, t).losses[10] == -4.0
+
+
+def test_view_append_is_dropped_at_refresh():
+    """A document appended to ``trials.trials`` alone is gone after the next
+    refresh, which rebuilds the view from the documents (base.py:231-242)."""
+    d = base.Domain(lambda x: 0.0, {'x': H.hp.uniform('x', 0, 1)})
+    t = _done_trials(d, 30, tracked=True)
+    _same_as_walk(d, t)
+    extra = rand.suggest([99], d, t, 3)[0]
+    extra['state'] = base.JOB_STATE_DONE
+    extra['result'] = {'status': 'ok', 'loss': 0.5}
+    t.trials.append(extra)
+    assert _same_as_walk(d, t).tids[-1] == 99       # (the view as it stands)
+    t.refresh()
+    assert extra not in t.trials and len(t.trials) == 30
+    assert 99 not in list(_same_as_walk(d, t).tids)
 
 
 def test_incremental_refresh_equals_full_filter():
