@@ -1176,7 +1176,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       p.tab_off[0] = (int32_t)tab_units;
       p.tab_n[0] = (int32_t)tn0[li];
       p.lat_lo = tlat[li];
-      tab_units += tn0[li];
+      tab_units += tn0[li] + (tn0[li] + 1 + 3) / 4;      // {l, g} rows, then n + 1 f32 entry thresholds
     }
   }
   if (tab_units >= ((int64_t)1 << 31)) return TPE_E_ARG;

@@ -1659,44 +1659,73 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 }
 
 // ---- the fast sample kernel, small-workgroup form (k_sample_fast) ----
-// The production case of k_sample_tab<F32, true> (every tabulated problem a
-// TPE_F_LOGPOLY cells table, device draws, early selection, nothing per
-// candidate written) in 512-thread workgroups whose table takes only the
-// level's largest table in LDS (dynamic shared memory, tpe_batch.tab_fast rows)
+// The production sample pass of tabulated levels whose labels are TPE_F_LOGPOLY
+// cells tables or lattices (device draws at f32, early selection, nothing per
+// candidate written), in 512-thread workgroups whose LDS takes only the level's
+// largest table (dynamic shared memory, tpe_batch.tab_fast - 1 units of 16 B)
 // and whose sampler rows are at most kFastSamp: three workgroups share a CU,
 // 24 waves instead of 16, and a workgroup's staging and barriers overlap the
-// others' candidate loops.  A thread's unit is two candidates (one Philox
-// block); a run's units (its consecutive tiles of one problem, 128 candidates
-// a unit) are handed out to the waves from an LDS counter.  Same draws, same
-// f32 arithmetic and same selection order as k_sample_tab's FAST pass.
+// others' candidate loops.  A thread's unit is NP candidates (NP / 2 Philox
+// blocks); a run's units (its consecutive tiles of one problem) are handed to
+// the waves statically (wave w: units w, w + 8, ..) or, when its tiles are not
+// one candidate range, from an LDS counter.  Cells: the same draws, the same f32
+// arithmetic and the same selection order as k_sample_tab's cells passes.
+// Lattice (quantized labels): drawn alike, quantised as draw_comp quantises
+// (np.round(x / q) * q, after exp for the log family), scored by the value's
+// exact f64 {l, g} row; a candidate's f64 score l - g enters the run's argmax
+// through its rank among the lattice's scores (lattice_ranks: the same order
+// as better() on the f64 scores, so the winner is k_sample_tab's), and the run
+// record carries the f64 l, g and score.  LG (debug builds of the stage,
+// tpe_debug_fast_lg): every candidate's {value, l, g, label} written besides.
 constexpr int kFastThreads = 512;
 constexpr int kFastSamp = 64;                  // sampler rows (below components) in LDS
-// (a thread's unit: NP candidates, NP / 2 Philox blocks; a wave's covers 64 NP)
-#ifndef TPE_FAST_WPC
-#define TPE_FAST_WPC 3
-#endif
-constexpr int kFastWgsPerCu = TPE_FAST_WPC;
+constexpr int kFastWgsPerCu = 3;
 constexpr int kFastMaxCells = 896;             // 42 KiB of table rows: three workgroups' LDS in a CU
+constexpr int kFastMaxUnits = TPE_TAB_ROW_UNITS * kFastMaxCells;   // 16-B LDS units of the staged table
+constexpr int kFastLatMax = 1024;              // lattice values the pass ranks in LDS
+// LDS units (16 B) a lattice of n values takes: its {l, g} rows and n + 1 f32
+// entry thresholds (the table's, lat_thresh_units), then an int rank per value
+__host__ __device__ constexpr int lat_thresh_units(int n) { return (n + 1 + 3) / 4; }
+__host__ __device__ constexpr int fast_lat_units(int n) { return n + lat_thresh_units(n) + (n + 3) / 4; }
+
+// rank of each lattice value's score s_j = l_j - g_j, in better()'s order on
+// f64 scores: NaN above every number; else #{k : s_k < s_j} + [s_j > -inf] —
+// 0 for -inf, the score of a draw outside the lattice (l = -inf, g = 0) — so
+// equal scores share a rank and a larger score has a larger one (workgroup-
+// collective; O(n) LDS reads per value)
+__device__ void lattice_ranks(const double2* __restrict__ rows, int n, int* __restrict__ rank) {
+  for (int j = threadIdx.x; j < n; j += kFastThreads) {
+    const double2 r = rows[j];
+    const double s = r.x - r.y;
+    int k = n + 2;
+    if (s == s) {
+      k = s > -INFINITY ? 1 : 0;
+      for (int m = 0; m < n; ++m) {
+        const double2 o = rows[m];
+        k += (o.x - o.y) < s;
+      }
+    }
+    rank[j] = k;
+  }
+}
+
 // NP = 2: 80 VGPRs, six waves a SIMD (three workgroups a CU: batched levels);
 // NP = 4: two candidate pairs in flight per lane for levels of at most two
 // workgroups a CU (config 3's 2^21 candidates), four waves a SIMD
-template <int NP>
+template <int NP, bool LG>
 __global__ __launch_bounds__(kFastThreads) __attribute__((amdgpu_waves_per_eu(NP == 2 ? 6 : 4)))
 void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict__ tiles,
                    const int32_t* __restrict__ list, int n_list, int per_wg, const double* __restrict__ samp,
                    const float4* __restrict__ comp32, const float4* __restrict__ tab,
-                   tpe_result* __restrict__ run_best, int tpp) {
+                   tpe_result* __restrict__ run_best, int tpp, double* __restrict__ lg_out) {
   constexpr int kFastUnit = 64 * NP;
   static_assert(NP % 2 == 0 && kTile % kFastUnit == 0, "fast units: Philox pairs tiling the tiles");
-#ifdef TPE_DIAG_EMPTY
-  return;                                          // (diagnostic builds only: the launch's own cost)
-#endif
-  extern __shared__ float4 fast_tab[];                       // the label's LOGPOLY rows (tab_fast of them at most)
+  extern __shared__ float4 fast_tab[];                       // the label's table (tab_fast - 1 units at most)
   __shared__ double cum_lds[kFastSamp];
   __shared__ float4 row_lds[kFastSamp];
   __shared__ GuideEnt guide[kGuide];
   constexpr int kW = kFastThreads / 64;
-  struct RunRec { int64_t cand_base; double bb, ab; int tile, logc; };
+  struct RunRec { int64_t cand_base, lat_lo; double bb, ab, q; int tile, logc, lat, tab_off; };
   __shared__ RunRec s_run[kTabMaxTilesPerWg];
   __shared__ unsigned long long s_rk[kTabMaxTilesPerWg][kW];
   __shared__ float s_rv[kTabMaxTilesPerWg][3][kW];
@@ -1705,6 +1734,9 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
   const int lane = threadIdx.x & 63;
   int st_samp = -1, st_len = -1, st_t0 = -1, st_n0 = -1;
   int n_def = 0;                                             // runs so far (workgroup-uniform)
+  // the thread's best: cells — score fd (better32 order), index fi, log2 sums
+  // flb / fla, draw ft; lattice — index fi, score rank and row (-1: outside the
+  // lattice) as the bits of flb and fla, draw ft
   float fd = 0.f, flb = 0.f, fla = 0.f, ft = 0.f;
   int fi = -1;
   if ((int)threadIdx.x < kTabMaxTilesPerWg) s_unit[threadIdx.x] = 0;
@@ -1727,12 +1759,14 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
     int gk = gi;                                             // the run: tiles gi .. gk, one problem
     while (gk + 1 < n_my && __builtin_amdgcn_readfirstlane(s_prob[gk + 1]) == pid) ++gk;
     const tpe_problem& p = P[pid];
+    const bool lat = p.tab_mode == TPE_TAB_LATTICE;         // (run-uniform)
+    const int n0 = p.tab_n[0];
     bool staged = false;
     double scum = 0.0;
     float4 srow = make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool same = p.samp_off == st_samp && p.samp_len == st_len && p.tab_off[0] == st_t0 && p.tab_n[0] == st_n0;
+    const bool same = p.samp_off == st_samp && p.samp_len == st_len && p.tab_off[0] == st_t0 && n0 == st_n0;
     if (!same) {
-      st_samp = p.samp_off; st_len = p.samp_len; st_t0 = p.tab_off[0]; st_n0 = p.tab_n[0];
+      st_samp = p.samp_off; st_len = p.samp_len; st_t0 = p.tab_off[0]; st_n0 = n0;
       __syncthreads();                                       // LDS free for the next label's rows
       if ((int)threadIdx.x < p.samp_len) {
         const double* sr = samp + 8 * (int64_t)p.samp_off + 8 * (int)threadIdx.x;
@@ -1740,47 +1774,41 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
         const float sg = (float)sr[2];
         srow = make_float4((float)sr[1], sr[5] != 0.0 ? -sg : sg, (float)sr[3], (float)sr[4]);
       }
-      // the table rows by LDS-DMA, every round's loads issued before the one
-      // wait (the last round's lanes past the rows: a clamped load, unused slots)
-      const int nu = TPE_TAB_ROW_UNITS * p.tab_n[0];
+      // the table rows (cells: 3 units a row; lattice: one {l, g} unit a value) by
+      // LDS-DMA, every round's loads issued before the one wait; the last round's
+      // lanes past the rows issue nothing (an LDS-DMA lane writes its slot
+      // whatever its address: the dynamic LDS holds exactly the rows)
+      const int nu = lat ? n0 + lat_thresh_units(n0) : TPE_TAB_ROW_UNITS * n0;
       const int wv = (int)(threadIdx.x >> 6);
-#ifndef TPE_DIAG_NO_STAGE
       for (int u = 0; u * kFastThreads < nu; ++u) {
-        const int q = min(u * kFastThreads + (int)threadIdx.x, nu - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(tab + (int64_t)p.tab_off[0] + q),
-                                         (__attribute__((address_space(3))) void*)(fast_tab + u * kFastThreads + 64 * wv),
-                                         16, 0, 0);
+        const int q = u * kFastThreads + (int)threadIdx.x;
+        if (q < nu)
+          __builtin_amdgcn_global_load_lds((const void*)(tab + (int64_t)p.tab_off[0] + q),
+                                           (__attribute__((address_space(3))) void*)(fast_tab + u * kFastThreads + 64 * wv),
+                                           16, 0, 0);
       }
-#else
-      (void)nu; (void)wv;                          // (diagnostic builds only: the staging's cost)
-#endif
       staged = true;
     }
-    if (threadIdx.x == 0)
-      s_run[n_def] = RunRec{(int64_t)p.cand_base, p.below_base, p.above_base, tile, p.family == TPE_FAM_LOGGAUSS ? 1 : 0};
-#ifndef TPE_DIAG_NO_UNITS
+    if (threadIdx.x == 0) {
+      const bool lgf = p.family == TPE_FAM_LOGGAUSS || p.family == TPE_FAM_QLOGGAUSS;
+      s_run[n_def] = RunRec{(int64_t)p.cand_base, p.lat_lo, p.below_base, p.above_base, p.q, tile, lgf ? 1 : 0,
+                            lat ? 1 : 0, p.tab_off[0]};
+    }
     const int nunits = (gk - gi + 1) * (kTile / kFastUnit);
-#else                                              // (diagnostic builds only: the pass without candidates)
-    const int nunits = 0;
-#endif
     float lo_f, hi_f;
     f32_bounds(p, lo_f, hi_f);
     const float lo0 = p.tab_lo[0], inv0 = p.tab_inv[0];
     const float w0 = 1.f / inv0, ih0 = 1.f / (0.5f * w0);
-    const int n0 = p.tab_n[0];
+    const double2* __restrict__ lrow = reinterpret_cast<const double2*>(fast_tab);
+    const float* __restrict__ lthr = reinterpret_cast<const float*>(fast_tab + n0);
+    const int* __restrict__ lrank = reinterpret_cast<const int*>(fast_tab + n0 + lat_thresh_units(n0));
     // a run whose tiles are one candidate range (the packer's order): wave w takes
     // units w, w + kW, ... with no LDS traffic for the hand-out or the addresses
-    // (TPE_FAST_DYNAMIC builds: units from an LDS counter, as k_sample_tab)
     const int start0 = __builtin_amdgcn_readfirstlane(s_start[gi]);
-#ifndef TPE_FAST_DYNAMIC
     const int ntl = gk - gi + 1;
     const int tl = min(lane, ntl - 1);
     const bool contig = __ballot(s_start[gi + tl] != start0 + tl * kTile) == 0ull;
     const int wave0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-#else
-    constexpr bool contig = false;
-    const int wave0 = 0;
-#endif
     bool first_unit = true;
     for (int k = 0;; ++k) {
       int u = wave0 + k * kW;
@@ -1803,12 +1831,7 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
 #pragma unroll
           for (int j = 0; j < NP; j += 2) {
             const uint64_t blk = (g0 + (uint64_t)j) >> 1;
-#ifndef TPE_DIAG_NO_PHILOX
             const U4 r = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), p.ctr2, p.ctr3, p.key0, p.key1);
-#else                                              // (diagnostic builds only: the draws' cost)
-            const uint32_t h = (uint32_t)blk * 2654435761u;
-            const U4 r{h, h ^ 0x9e3779b9u, h * 3u, h ^ 0x85ebca6bu};
-#endif
             ws[j] = r.x; uf[j] = u01f(r.y);
             ws[j + 1] = r.z; uf[j + 1] = u01f(r.w);
           }
@@ -1837,6 +1860,10 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
         }
         __builtin_amdgcn_s_waitcnt(0);               // (the LDS-DMA loads: vmcnt)
         __syncthreads();
+        if (lat) {                                   // the values' score ranks after the rows
+          lattice_ranks(lrow, n0, const_cast<int*>(lrank));
+          __syncthreads();
+        }
       }
       first_unit = false;
       if (!have) break;
@@ -1858,29 +1885,62 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
         for (int j = 0; j < NP; ++j) {
           const float4 sv = row_lds[kc[j]];
           const float pr = sv.z + uf[j] * (sv.w - sv.z);
-#ifndef TPE_DIAG_NO_NDTRI
           const float z = ndtri_f32(pr);
-#else                                              // (diagnostic builds only: the inversion's cost)
-          const float z = pr - 0.5f;
-#endif
           const float xf = sv.x + sv.y * z;
           tj[j] = fminf(fmaxf(xf == xf ? xf : sv.x, lo_f), hi_f);
         }
+      }
+      if (lat) {
+        // the lattice row of np.round(x / q) (k_sample_tab's quantisation) from the
+        // table's entry thresholds: row c - 1 for c = #{m : thr_m <= t}, outside
+        // the lattice for c = 0 or n + 1 (no f64 per candidate); the key:
+        // (score rank + 1, ~index)
+        int c[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) c[j] = 0;
+        for (int span = n0 + 1; span > 0;) {       // (the same steps for every lane)
+          const int h = span >> 1;
+#pragma unroll
+          for (int j = 0; j < NP; ++j) c[j] += lthr[c[j] + h] <= tj[j] ? span - h : 0;
+          span = h;
+        }
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+          const int i = first + j;
+          const bool in = c[j] >= 1 && c[j] <= n0;
+          const int r = in ? c[j] - 1 : -1;
+          const int rk = in ? lrank[r] : 0;
+          const int brk = __float_as_int(flb);
+          if (i < p.n_cand && (fi < 0 || rk > brk || (rk == brk && i < fi))) {
+            fi = i; flb = __int_as_float(rk); fla = __int_as_float(r); ft = tj[j];
+          }
+          if (LG && i < p.n_cand) {
+            const double xu = p.family == TPE_FAM_QLOGGAUSS ? exp_call((double)tj[j]) : (double)tj[j];
+            const double2 lg = in ? lrow[r] : make_double2(-INFINITY, 0.0);
+            double* o = lg_out + 4 * (p.cand_off + i);
+            o[0] = rint(xu / p.q) * p.q; o[1] = lg.x; o[2] = lg.y; o[3] = (double)p.ctr2;
+          }
+        }
+        continue;
       }
       uint32_t exact = 0;
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
         const int i = first + j;
         float lb2, la2;
-#ifndef TPE_DIAG_NO_CELLS
         lp_log2(lo0, inv0, w0, ih0, n0, fast_tab, tj[j], lb2, la2);
-#else                                              // (diagnostic builds only: the look-up's cost)
-        lb2 = tj[j]; la2 = 0.5f * tj[j];
-#endif
         const bool valid = i < p.n_cand, ok = lb2 == lb2 && la2 == la2;
         exact |= (unsigned)(valid && !ok) << j;
         const float d = lb2 - la2;
         if (valid && ok && better32(d, i, fd, fi)) { fd = d; fi = i; flb = lb2; fla = la2; ft = tj[j]; }
+        if (LG && valid && ok) {
+          const bool lgf = p.family == TPE_FAM_LOGGAUSS;
+          const double lnx = lgf ? (double)tj[j] : 0.0;
+          double* o = lg_out + 4 * (p.cand_off + i);
+          o[0] = lgf ? exp_call((double)tj[j]) : (double)tj[j];
+          o[1] = (double)lb2 * kLn2 + p.below_base - lnx; o[2] = (double)la2 * kLn2 + p.above_base - lnx;
+          o[3] = (double)p.ctr2;
+        }
       }
       // outside the cells or in flagged ones: summed exactly by the whole wave
 #pragma unroll
@@ -1897,16 +1957,29 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
           const int i = __shfl(first, src) + j;
           const float d = lb2 - la2;
           if (lane == src && better32(d, i, fd, fi)) { fd = d; fi = i; flb = lb2; fla = la2; ft = t; }
+          if (LG && lane == src) {
+            const bool lgf = p.family == TPE_FAM_LOGGAUSS;
+            const double lnx = lgf ? (double)t : 0.0;
+            double* o = lg_out + 4 * (p.cand_off + i);
+            o[0] = lgf ? exp_call((double)t) : (double)t;
+            o[1] = (double)lb2 * kLn2 + p.below_base - lnx; o[2] = (double)la2 * kLn2 + p.above_base - lnx;
+            o[3] = (double)p.ctr2;
+          }
         }
       }
     }
-    // the run's best of this wave: better32's order as one key (DPP max); the
-    // winning lane (indices are unique) leaves its log2 sums and draw
+    // the run's best of this wave as one key (DPP max; indices are unique): the
+    // winning lane leaves its log2 sums and draw (cells) or its draw and lattice
+    // row (lattice)
     {
       int tid = (int)threadIdx.x;
       asm volatile("" : "+v"(tid));
       const int wave = tid >> 6;
-      const unsigned long long key = key32(fd, fi);
+      // (lattice: the key of (rank + 1, ~index))
+      const unsigned long long key =
+          !lat ? key32(fd, fi)
+               : fi < 0 ? 0ull
+                        : ((unsigned long long)(__float_as_int(flb) + 1) << 32) | (unsigned long long)(~(uint32_t)fi);
       const unsigned long long wk = __ockl_wfred_max_u64(key);
       if (wk != 0ull && key == wk) { s_rv[n_def][0][wave] = flb; s_rv[n_def][1][wave] = fla; s_rv[n_def][2][wave] = ft; }
       if ((tid & 63) == 0) s_rk[n_def][wave] = wk;
@@ -1928,7 +2001,21 @@ void k_sample_fast(const tpe_problem* __restrict__ P, const tpe_tile* __restrict
       const RunRec rr = s_run[r];
       tpe_result res;
       res.score = 0.0; res.l = 0.0; res.g = 0.0; res.idx = i2; res.value = 0.0; res.global_idx = -1;
-      if (i2 >= 0) {
+      if (i2 >= 0 && rr.lat) {
+        // the winner's value and exact {l, g} (the lattice rows in global memory:
+        // the LDS holds the last staged label)
+        const float t = s_rv[r][2][w2];
+        const int jq = __float_as_int(s_rv[r][1][w2]);
+        const double xu = rr.logc ? exp_call((double)t) : (double)t;
+        const double mq = rint(xu / rr.q);
+        const double2 lg = jq >= 0 ? reinterpret_cast<const double2*>(tab)[rr.tab_off + jq]
+                                   : make_double2(-INFINITY, 0.0);
+        res.l = lg.x;
+        res.g = lg.y;
+        res.score = lg.x - lg.y;
+        res.value = mq * rr.q;
+        res.global_idx = rr.cand_base + i2;
+      } else if (i2 >= 0) {
         const float t = s_rv[r][2][w2];
         const double lnx = rr.logc ? (double)t : 0.0;
         res.l = (double)s_rv[r][0][w2] * kLn2 + rr.bb - lnx;
@@ -3294,6 +3381,55 @@ __device__ void lattice_row(const tpe_problem& p, int j, const double4* __restri
   }
 }
 
+// np.round(x / q) of a device draw with coordinate t (k_sample_tab's lattice pass)
+__device__ __forceinline__ double lattice_qidx(const tpe_problem& p, float t) {
+  const double xu = p.family == TPE_FAM_QLOGGAUSS ? exp((double)t) : (double)t;
+  return rint(xu / p.q);
+}
+// f32 order as an unsigned order (and back)
+__device__ __forceinline__ uint32_t f32_okey(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float f32_from_okey(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// entry threshold of lattice row m (wave-collective, lane 0 writes thr[m]): the
+// smallest f32 coordinate t in the clip range [lo_f, hi_f] whose value
+// np.round(x / q) is at least lat_lo + m (lo_f when every t is; +inf when none
+// is), so a draw t takes row #{m : thr_m <= t} - 1 (k_sample_fast).  The value
+// is non-decreasing in t (consecutive f32 coordinates are far more than an
+// ulp of exp apart), so a 64-ary search over the f32 order finds it exactly:
+// each round's lanes test 64 evenly spaced points, ~6 rounds.
+__device__ void lattice_thresh(const tpe_problem& p, int m, float* __restrict__ thr) {
+  const int lane = threadIdx.x & 63;
+  float lo_f, hi_f;
+  f32_bounds(p, lo_f, hi_f);
+  const double target = (double)(p.lat_lo + (int64_t)m);
+  float T;
+  if (lattice_qidx(p, lo_f) >= target) {
+    T = lo_f;
+  } else if (!(lattice_qidx(p, hi_f) >= target)) {
+    T = INFINITY;
+  } else {
+    uint32_t a = f32_okey(lo_f), b = f32_okey(hi_f);       // below a: no; at b: yes
+    while (b - a > 1u) {
+      const uint64_t step = ((uint64_t)(b - a) + 63) / 64;
+      const uint64_t kk = (uint64_t)a + (uint64_t)(lane + 1) * step;
+      const uint32_t k = kk >= (uint64_t)b ? b : (uint32_t)kk;      // (lane 63 tests b: always yes)
+      const unsigned long long yes = __ballot(lattice_qidx(p, f32_from_okey(k)) >= target);
+      const int f = (int)__builtin_ctzll(yes);
+      const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)k, f);
+      const uint32_t na = f > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)k, f - 1) : a;
+      a = na;
+      b = nb;
+    }
+    T = f32_from_okey(b);
+  }
+  if (lane == 0) thr[m] = T;
+}
+
 // ---- TPE_F_LOGPOLY rows (include/tpe_hip.h, "Tabulated scoring") ----
 // nodes: the 6 Chebyshev points cos((2i + 1) pi / 12) of [-1, 1] (interpolation),
 // then the check points 0, 1/2, -1/2, 1, -1; kLpA: monomial coefficients of the
@@ -3614,6 +3750,12 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     double* lds = reinterpret_cast<double*>(rows_lds);
     if (p.family == TPE_FAM_QLOGGAUSS) lattice_row<true>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off), lds);
     else lattice_row<false>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off), lds);
+    // ... and its entry threshold after the rows (the last block: the exit too)
+    if (threadIdx.x < 64) {
+      float* thr = reinterpret_cast<float*>(tab + jb.off + jb.n);
+      lattice_thresh(p, b, thr);
+      if (b == jb.n - 1) lattice_thresh(p, jb.n, thr);
+    }
   }
 }
 
@@ -4785,6 +4927,28 @@ static bool g_kev_on = false;
       hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                                \
   } while (0)
 
+// tpe_debug_fast_lg's buffer: k_sample_fast writes {value, l, g, label} of every
+// candidate there (null: the production kernel, nothing per candidate)
+static struct { double* dev; int64_t n; } g_fast_lg = {nullptr, 0};
+
+int tpe_debug_fast_lg(void* dev, int64_t n_records) {
+  if (dev && n_records <= 0) return fail(TPE_E_ARG, "tpe_debug_fast_lg: no records");
+  g_fast_lg.dev = (double*)dev;
+  g_fast_lg.n = dev ? n_records : 0;
+  return TPE_OK;
+}
+
+extern "C++" {
+// k_sample_fast<NP, LG> over the level's tabulated tiles
+template <int NP, bool LG>
+void launch_fast(const tpe_batch* b, int wgs, size_t lds, hipStream_t s, int n_tab, int per, tpe_result* run_best,
+                 double* lg) {
+  TPE_LAUNCH_TIMED((k_sample_fast<NP, LG>), dim3(wgs), dim3(kFastThreads), lds, s, b->problems, b->tiles,
+                   b->tab_tiles, n_tab, per, b->samp, (const float4*)b->comp32, (const float4*)b->tab, run_best,
+                   b->tiles_per_problem, lg);
+}
+}
+
 int tpe_sample(const tpe_batch* b, void* stream) {
   int rc = check_batch(b);
   if (rc) return rc;
@@ -4821,16 +4985,16 @@ int tpe_sample(const tpe_batch* b, void* stream) {
     const bool fast = b->tab_fast && run_best && b->precision == TPE_PREC_F32 && b->sample && !b->l_out &&
                       !(b->flags & TPE_BATCH_WRITE_CAND);
     if (fast && b->tab_fast >= 2) {
-      if (b->tab_fast - 1 > kFastMaxCells) return fail(TPE_E_ARG, "tpe_sample: tab_fast rows past the fast kernel's LDS");
+      if (b->tab_fast - 1 > kFastMaxUnits) return fail(TPE_E_ARG, "tpe_sample: tab_fast units past the fast kernel's LDS");
+      double* lg = g_fast_lg.dev;                  // (debug: every candidate's value, l, g)
+      if (lg && g_fast_lg.n < b->total_cand) return fail(TPE_E_ARG, "tpe_sample: tpe_debug_fast_lg buffer too small");
+      const size_t lds = (size_t)(b->tab_fast - 1) * 16;
       // (two candidate pairs per lane when the level fills at most two workgroups a CU)
-      if (wgs <= 2 * cu_count() && !fast_np2_forced())
-        TPE_LAUNCH_TIMED(k_sample_fast<4>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
-                         (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
-                         (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
-      else
-        TPE_LAUNCH_TIMED(k_sample_fast<2>, dim3(wgs), dim3(kFastThreads), (size_t)(b->tab_fast - 1) * 48,
-                         (hipStream_t)stream, b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp,
-                         (const float4*)b->comp32, (const float4*)b->tab, run_best, b->tiles_per_problem);
+      const bool np4 = wgs <= 2 * cu_count() && !fast_np2_forced();
+      if (lg && np4) launch_fast<4, true>(b, wgs, lds, (hipStream_t)stream, n_tab, per, run_best, lg);
+      else if (lg) launch_fast<2, true>(b, wgs, lds, (hipStream_t)stream, n_tab, per, run_best, lg);
+      else if (np4) launch_fast<4, false>(b, wgs, lds, (hipStream_t)stream, n_tab, per, run_best, nullptr);
+      else launch_fast<2, false>(b, wgs, lds, (hipStream_t)stream, n_tab, per, run_best, nullptr);
     } else if (fast)
       TPE_LAUNCH_TIMED((k_sample_tab<TPE_PREC_F32, true>), dim3(wgs), dim3(kTabThreads), 0, (hipStream_t)stream,
                          b->problems, b->tiles, b->tab_tiles, n_tab, per, b->samp, b->cand, b->coord, b->tile_best,
@@ -5250,21 +5414,28 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     // host's, or an expanded level's label templates)
     const bool fast_ok = precision == TPE_PREC_F32 && !(flags & (TPE_BATCH_WRITE_CAND | TPE_BATCH_NO_TAB_FAST)) &&
                          !tab_fast_disabled();
-    bool fast = fast_ok;
+    // k_sample_fast: every tabulated problem a log-polynomial cells table or a
+    // lattice within its LDS; k_sample_tab's FAST pass: log-polynomial cells only
+    bool fast = fast_ok, fast_lp = fast_ok;
     const tpe_problem* rows = hp ? hp : xtmpl;
     const int64_t n_rows = hp ? P : (xtmpl ? info.n_expand : 0);
-    int max_cells = 0, max_samp = 0;
-    for (int64_t r = 0; fast && r < n_rows; ++r) {
+    int max_cells = 0, max_units = 0, max_samp = 0;
+    for (int64_t r = 0; (fast || fast_lp) && r < n_rows; ++r) {
       const tpe_problem& q = rows[r];
       if (q.tab_mode == TPE_TAB_NONE) continue;
-      fast = q.tab_mode == TPE_TAB_CELLS && (q.flags & TPE_F_LOGPOLY) && q.tab_n[0] <= kTabLdsCells &&
-             q.samp_len > 0 && q.samp_len <= kCumLds;
-      max_cells = std::max(max_cells, q.tab_n[0]);
+      const bool samp_ok = q.samp_len > 0 && q.samp_len <= kCumLds;
+      const bool lp = q.tab_mode == TPE_TAB_CELLS && (q.flags & TPE_F_LOGPOLY) && q.tab_n[0] <= kTabLdsCells && samp_ok;
+      const bool lat = q.tab_mode == TPE_TAB_LATTICE && q.tab_n[0] <= kFastLatMax && samp_ok;
+      fast_lp = fast_lp && lp;
+      fast = fast && (lp || lat);
+      max_cells = std::max(max_cells, lp ? q.tab_n[0] : 0);
+      max_units = std::max(max_units, lp ? TPE_TAB_ROW_UNITS * q.tab_n[0] : fast_lat_units(q.tab_n[0]));
       max_samp = std::max(max_samp, q.samp_len);
     }
     // (the small-workgroup kernel when the level's tables and sampler rows fit its LDS)
-    const bool fast2 = fast && !fast2_disabled() && max_cells <= kFastMaxCells && max_samp <= kFastSamp;
-    b.tab_fast = fast && n_rows > 0 ? (fast2 ? 1 + max_cells : 1) : 0;
+    const bool fast2 = fast && !fast2_disabled() && max_cells <= kFastMaxCells && max_units <= kFastMaxUnits &&
+                       max_samp <= kFastSamp;
+    b.tab_fast = n_rows > 0 ? (fast2 ? 1 + max_units : fast_lp ? 1 : 0) : 0;
   }
   b.result = rd ? rd : ws->result;
   // device exchange (sharded level over RCCL): run records and results in

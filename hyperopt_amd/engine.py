@@ -352,7 +352,7 @@ class Engine(object):
                     units += N.TAB_ROW_UNITS * n
             elif pl['mode'] == N.TAB_LATTICE:
                 info['tab_off'][0], info['tab_n'][0], info['lat_lo'] = units, pl['n'][0], pl['lat_lo']
-                units += pl['n'][0]
+                units += pl['n'][0] + (pl['n'][0] + 1 + 3) // 4      # rows, then n + 1 f32 entry thresholds
             if pl['mode'] != N.TAB_NONE and len(lp.ids):
                 for sd in range(2 if pl['mode'] == N.TAB_CELLS else 1):
                     geo = (0, 0, 0, 0, 0.0, 0.0)

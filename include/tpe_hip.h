@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 19
+#define TPE_ABI_VERSION 20
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -206,6 +206,11 @@ enum { TPE_OK = 0, TPE_E_ARG = -1, TPE_E_HIP = -2, TPE_E_NODEV = -3, TPE_E_SPACE
  *     tpe.py:90-93, 248-249); row m - lat_lo of the table (tab_n[0] rows of
  *     double2 {l, g}, float64, reference operation order per component) holds
  *     its scores; other values (injected candidates) are scored directly.
+ *     ABI 20: the rows are followed by tab_n[0] + 1 float entry thresholds
+ *     (ceil((tab_n[0] + 1) / 4) units): thr[m] = the smallest f32 coordinate t
+ *     in the clip range whose np.round(x / q) >= lat_lo + m (+inf: none), so a
+ *     device draw t takes row #{m : thr[m] <= t} - 1 with no f64 arithmetic
+ *     (k_sample_fast; k_sample_tab quantises directly, with the same result).
  * Tables live in `tab` (16-B units; tab_off[s] = first unit) and are built by
  * the table stage from the problem's component rows (after the device fit).
  *
@@ -429,13 +434,15 @@ typedef struct tpe_batch {
   int64_t fit_max_obs;        /* most observations of one job                       */
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
   double* draw_pref; int64_t draw_blocks; int32_t n_sorted;
-  int32_t tab_fast;      /* >= 1: every tabulated problem is a TPE_F_LOGPOLY cells table within the sample
-                            stage's LDS (tab_n[0] <= 2048) with 1..TPE_SAMPLE_LDS_ROWS sampler rows, the
-                            candidates are device-drawn at TPE_PREC_F32, early selection is on and nothing
-                            per candidate is written: the sample stage's specialised kernel — 1: in
-                            1024-thread workgroups; 1 + R (R <= 896 table rows, <= 64 sampler rows): in
-                            512-thread workgroups taking R rows of LDS, three a CU (tpe_level_run sets it;
-                            0: the general kernel) */
+  int32_t tab_fast;      /* >= 1: the candidates are device-drawn at TPE_PREC_F32, early selection is on,
+                            nothing per candidate is written and every tabulated problem has
+                            1..TPE_SAMPLE_LDS_ROWS sampler rows: the sample stage's specialised kernels —
+                            1 + U (ABI 20; every tabulated problem a TPE_F_LOGPOLY cells table of <= 896
+                            rows or a lattice of <= 1024 values, <= 64 sampler rows): k_sample_fast in
+                            512-thread workgroups taking U 16-B units of LDS (3 per cell row; a lattice
+                            value's {l, g} unit plus its 4-B score rank), three a CU; 1: every tabulated
+                            problem a TPE_F_LOGPOLY cells table of <= 2048 rows, in 1024-thread
+                            workgroups (tpe_level_run sets it; 0: the general kernel) */
   unsigned long long* pool_best;   /* [n_problems] (pooled problems; see "Pooled labels") */
   /* tabulated scoring: table jobs and the table storage (16-B units) */
   const tpe_tab_job* tab_jobs; int32_t n_tab_jobs; int32_t tab_blocks;
@@ -869,6 +876,12 @@ typedef struct tpe_stage_prof {
 
 /* enable (1) / disable (0) the profiler; creates its events on first use */
 int tpe_level_profile(int32_t enable);
+
+/* Debug (tests): while `dev` is set, the sample stage's k_sample_fast pass also
+ * writes every candidate's {value, l, g, label index} as four doubles at
+ * dev[4 * (cand_off + i)] (device memory, n_records >= the level's candidates;
+ * the run records are unchanged).  NULL: the production kernel.  Process-wide. */
+int tpe_debug_fast_lg(void* dev, int64_t n_records);
 
 /* the last profiled tpe_level_run: min(n, TPE_N_STAGES) records in stage
  * order; TPE_E_ARG if no run completed since the profiler was enabled */

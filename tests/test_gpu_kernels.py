@@ -643,3 +643,164 @@ def test_tabulated_exact_fallback_matches_oracle(engine, dist, args, monkeypatch
     k = int(res[0]['idx'])
     assert res[0]['value'] == cand[0][k] and int(np.argmax(l[0] - g[0])) == k
     assert abs(base[0]['score'] - res[0]['score']) <= 4e-5 * max(1.0, abs(res[0]['score'])), dist
+
+
+# ---------------------------------------------------------------- dense table checks
+def _f32_bounds(post):
+    """f32_bounds (tpe_kernels.hip): the f32 clip range of a problem's coordinate."""
+    lo, hi = -np.inf, np.inf
+    if post.low is not None:
+        lo = np.float32(post.low)
+        if float(lo) < post.low:
+            lo = np.nextafter(lo, np.float32(np.inf))
+    if post.high is not None:
+        hi = np.float32(post.high)
+        while float(hi) >= post.high:
+            hi = np.nextafter(hi, np.float32(-np.inf))
+    return float(lo), float(hi)
+
+
+def _dense_cells(row, tab4, post, log, what, n_u=33, tol=1e-5):
+    """Every log-polynomial cell row of a label (TPE_F_LOGPOLY) evaluated at
+    ``n_u`` points of its cell (the kernel's f32 cell geometry, lp_log2) in
+    f64 on the host, against the oracle's lpdf at the same f32 coordinates;
+    flagged sides (NaN: exact fallback) skipped and counted."""
+    from hyperopt_amd import _native as N
+    assert row['tab_mode'] == N.TAB_CELLS and row['flags'] & N.F_LOGPOLY, what
+    n, off = int(row['tab_n'][0]), int(row['tab_off'][0])
+    rows = tab4[off:off + 3 * n].reshape(n, 12).astype(np.float64)
+    b, a = rows[:, 0::2], rows[:, 1::2]                 # {b_k, a_k} interleaved
+    lo, inv = np.float32(row['tab_lo'][0]), np.float32(row['tab_inv'][0])
+    w = np.float32(1) / inv
+    ih = np.float32(1) / (np.float32(0.5) * w)
+    j = np.arange(n)
+    c = ((j + 0.5) * np.float64(w) + np.float64(lo)).astype(np.float32)      # fmaf(j + 0.5, w, lo)
+    h = np.float32(0.5) * w
+    uk = np.linspace(-1, 1, n_u).astype(np.float32)
+    t = (c[:, None] + h * uk[None, :]).astype(np.float32)                   # f32 coordinates in each cell
+    gj = np.floor((t - lo) * inv)
+    u = ((t - c[:, None]) * ih).astype(np.float64)
+    lo_f, hi_f = _f32_bounds(post)
+    ok = (gj == j[:, None]) & (t >= lo_f) & (t <= hi_f)
+    ok_b = ok & np.isfinite(b[:, :1])
+    ok_a = ok & np.isfinite(a[:, :1])
+
+    def horner(cf):
+        s = cf[:, 5:6]
+        for k in range(4, -1, -1):
+            s = s * u + cf[:, k:k + 1]
+        return s
+    lnx = t.astype(np.float64) if log else 0.0
+    lb = horner(b) * np.log(2.0) + float(row['below_base']) - lnx
+    la = horner(a) * np.log(2.0) + float(row['above_base']) - lnx
+    x = np.exp(t.astype(np.float64)) if log else t.astype(np.float64)
+    lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
+    kw = dict(low=post.low, high=post.high, q=None)
+    for side, ok_s, got, mix in (('l', ok_b, lb, post.below), ('g', ok_a, la, post.above)):
+        xs = x[ok_s]
+        ref = lpdf(xs, *mix, **kw)
+        _check_lpdf(got[ok_s], ref, tol, (what, side, n, int(ok_s.sum())))
+    flagged = int((~np.isfinite(b[:, 0])).sum() + (~np.isfinite(a[:, 0])).sum())
+    assert flagged <= max(4, n // 10), (what, 'flagged sides', flagged, n)     # (exact fallback: tested apart)
+    return int(ok_b.sum() + ok_a.sum())
+
+
+def _dense_lattice(row, tab4, post, log, what, tol=1e-9):
+    """Every lattice row {l, g} of a quantized label against the oracle's lpdf
+    at its value, and every entry threshold (ABI 20) against the host's
+    quantisation of the f32 coordinates either side of it."""
+    from hyperopt_amd import _native as N
+    assert row['tab_mode'] == N.TAB_LATTICE, what
+    n, off = int(row['tab_n'][0]), int(row['tab_off'][0])
+    lg = tab4[off:off + n].view(np.float64).reshape(n, 2)
+    q = float(row['q'])
+    x = (int(row['lat_lo']) + np.arange(n)).astype(np.float64) * q
+    lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
+    kw = dict(low=post.low, high=post.high, q=q)
+    lo_f, hi_f = _f32_bounds(post)
+    thr = tab4[off + n:off + n + (n + 4) // 4].reshape(-1)[:n + 1]
+    reach = thr[:-1] < thr[1:]                     # rows some f32 draw in the clip range takes
+    assert reach.sum() >= 2, what
+    with np.errstate(divide='ignore', invalid='ignore'):
+        _check_lpdf(lg[reach, 0], lpdf(x[reach], *post.below, **kw), tol, (what, 'l', n))
+        _check_lpdf(lg[reach, 1], lpdf(x[reach], *post.above, **kw), tol, (what, 'g', n))
+
+    def qidx(t):
+        t = np.float64(t)
+        return np.round((np.exp(t) if log else t) / q)
+    for m in range(n + 1):
+        T = thr[m]
+        target = int(row['lat_lo']) + m
+        if T == np.inf:
+            assert qidx(np.float32(hi_f)) < target, (what, m)
+        else:
+            assert qidx(T) >= target, (what, m, T)
+            if T > lo_f:
+                assert qidx(np.nextafter(np.float32(T), np.float32(-np.inf))) < target, (what, m, T)
+    assert np.all(np.diff(thr) >= 0), what
+    return n
+
+
+@pytest.mark.parametrize('dist,args', [('uniform', dict(low=-5.0, high=5.0)),
+                                       ('loguniform', dict(low=-4.0, high=3.0)),
+                                       ('normal', dict(mu=1.0, sigma=3.0)),
+                                       ('lognormal', dict(mu=0.0, sigma=1.0)),
+                                       ('quniform', dict(low=0.0, high=20.0, q=1.0)),
+                                       ('qloguniform', dict(low=0.0, high=5.0, q=2.0)),
+                                       ('qnormal', dict(mu=2.0, sigma=4.0, q=0.5)),
+                                       ('qlognormal', dict(mu=1.0, sigma=0.7, q=0.25))])
+def test_table_rows_dense_against_oracle(engine, dist, args):
+    """Every table row the table stage builds for the 8 families, read back:
+    each log-polynomial cell evaluated at 33 points of the cell in f64 against
+    the oracle's gmm1_lpdf / lgmm1_lpdf (1e-5 max(|ref|, 1)); each lattice row
+    exactly against the oracle (1e-9) and its entry thresholds against the
+    host's quantisation (tpe.py:104-166, 259-301)."""
+    from hyperopt_amd import parzen
+    from hyperopt_amd.engine import LevelProblem
+    rs = np.random.RandomState(61)
+    q = args.get('q')
+    log = dist.startswith('log') or dist.startswith('qlog')
+    lo, hi = (args['low'], args['high']) if 'low' in args else (args['mu'] - 3 * args['sigma'],
+                                                               args['mu'] + 3 * args['sigma'])
+    obs = rs.uniform(lo, hi, 4000)
+    obs = np.exp(obs) if log else obs
+    if q:
+        obs = np.round(obs / q) * q
+    post = parzen.fit_posterior(dist, args, obs[:30], obs[30:], 1.0)
+    engine.run([LevelProblem(post, 5, [11])], 1 << 18, seed=13)
+    prob, _ = engine.device_tables()
+    tab4 = engine._bufs['tab'][:4 * int(engine._last_info.tab_units)].cpu().numpy().reshape(-1, 4)
+    if q:
+        assert _dense_lattice(prob[0], tab4, post, log, dist) > 0
+    else:
+        assert _dense_cells(prob[0], tab4, post, log, dist) > 1000
+
+
+@pytest.mark.parametrize('branch', ['svm', 'rf'])
+def test_headline_table_rows_dense_against_oracle(engine, branch):
+    """The headline's labels (config 3 at 10k trials and 2^20 candidates): the
+    svm branch's log-polynomial tables (svm_C, svm_rbf_gamma) and the rf
+    branch's lattices (rf_n_est, rf_depth_n), fitted as tpe.suggest fits them,
+    every row checked densely against the oracle as above."""
+    import bench
+    from hyperopt_amd import history as H, tpe
+    from hyperopt_amd.engine import LevelProblem
+    domain, trials = bench.make_history(10000, bench.SEED, loss=None if branch == 'svm' else bench.rf_loss)
+    T = domain.table
+    hist = H.extract(domain, trials)
+    below = H.split_below(hist, 0.25)
+    fits = tpe._Fits(T, hist, below, 1.0, None)
+    labels = ('svm_C', 'svm_rbf_gamma') if branch == 'svm' else ('rf_n_est', 'rf_depth_n')
+    rows = [T.by_label[k] for k in labels]
+    posts = [fits.get(r) for r in rows]
+    engine.run([LevelProblem(p, r.index, [10000]) for p, r in zip(posts, rows)], 1 << 20, seed=3)
+    prob, _ = engine.device_tables()
+    tab4 = engine._bufs['tab'][:4 * int(engine._last_info.tab_units)].cpu().numpy().reshape(-1, 4)
+    by_ix = {int(p['ctr2']): p for p in prob}
+    for r, post in zip(rows, posts):
+        log = r.dist.startswith('log') or r.dist.startswith('qlog')
+        row = by_ix[r.index]
+        if branch == 'svm':
+            assert _dense_cells(row, tab4, post, log, r.label) > 10000
+        else:
+            assert _dense_lattice(row, tab4, post, log, r.label) > 10

@@ -11,6 +11,8 @@ import pytest
 
 from tests.helpers import doc_values
 
+from hyperopt_amd import _native as N
+
 pytestmark = pytest.mark.gpu
 
 
@@ -358,3 +360,104 @@ def test_fast_sample_kernel_matches_general(monkeypatch, extra):
     monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra | 32))
     gen = run()
     assert fast == gen
+
+
+@pytest.fixture(scope='module')
+def quantized_workloads():
+    """The rf-steered config-3 history (quantized rf_n_est / rf_depth_n labels,
+    lattices) and config 2's 10-dim mixed space (cells and lattices in one
+    level), smaller histories."""
+    import bench
+    qdom, qtr = bench.make_history(3000, 1, loss=bench.rf_loss)
+    mdom, mtr = bench.mixed10_history(1000, 2)
+    return qdom, qtr, mdom, mtr
+
+
+def test_fast_sample_kernel_lattices_match_general(monkeypatch, quantized_workloads):
+    """k_sample_fast's lattice path (ABI 20: quantised by the table's entry
+    thresholds, argmax by score rank) chooses exactly what the general kernel
+    chooses (np.round(x / q) per candidate, f64 score order) on the rf branch
+    at 2^20 candidates and on config 2's mixed level (10^4 candidates) —
+    several seeds, the fast path confirmed by the profiler's kernel timing."""
+    from hyperopt_amd import tpe
+    from hyperopt_amd.engine import get_engine
+    qdom, qtr, mdom, mtr = quantized_workloads
+
+    def run():
+        out = [doc_values(tpe.suggest([3000], qdom, qtr, s, n_EI_candidates=1 << 20)) for s in (3, 4, 5)]
+        out += [doc_values(tpe.suggest([1000], mdom, mtr, s, n_EI_candidates=10000)) for s in (6, 7, 8)]
+        return [{k: float(v) for k, v in d.items()} for d in out]
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', '0')
+    fast = run()
+    eng = get_engine()
+    eng.lib.tpe_level_profile(1)
+    try:
+        tpe.suggest([3000], qdom, qtr, 3, n_EI_candidates=1 << 20)
+        prof = (N.StageProf * len(N.STAGES))()
+        N.check(eng.lib.tpe_level_profile_read(prof, len(N.STAGES)), eng.lib, 'profile')
+        assert prof[N.STAGES.index('k_sample')].kernel_ns > 0      # (the specialised pass ran)
+    finally:
+        eng.lib.tpe_level_profile(0)
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', '32')                    # TPE_BATCH_NO_TAB_FAST: the general kernel
+    gen = run()
+    assert fast == gen
+    assert any(int(d.get('model', -1)) == 1 for d in fast[:3])     # (the rf branch was suggested)
+
+
+@pytest.mark.parametrize('branch', ['svm', 'rf'])
+def test_fast_sample_kernel_lg_against_oracle(branch):
+    """tpe_debug_fast_lg: k_sample_fast itself writes every candidate's value,
+    l and g; on the headline (config 3, 10k trials, 2^20 candidates; svm
+    branch: log-polynomial cells, rf branch: lattices) 3000 of each label's
+    are checked against the oracle's lpdf with the host fits of the same
+    suggest (1e-5 relative, lattices 1e-9), and the suggested value is the
+    argmax of l - g over the label's candidates (within the eps-tie set)."""
+    import torch
+    import bench
+    from hyperopt_amd import history as H, tpe
+    from hyperopt_amd.engine import get_engine
+    from oracle import tpe_oracle as O
+    eng = get_engine()
+    domain, trials = bench.make_history(10000, bench.SEED, loss=None if branch == 'svm' else bench.rf_loss)
+    T = domain.table
+    C = 1 << 20
+    buf = torch.full((4 * 8 * C,), float('nan'), dtype=torch.float64, device=eng.device)
+    N.check(eng.lib.tpe_debug_fast_lg(buf.data_ptr(), 8 * C), eng.lib, 'tpe_debug_fast_lg')
+    try:
+        doc = tpe.suggest([10000], domain, trials, 77, n_EI_candidates=C)[0]
+        torch.cuda.synchronize()
+    finally:
+        N.check(eng.lib.tpe_debug_fast_lg(None, 0), eng.lib, 'tpe_debug_fast_lg')
+    rec = buf.cpu().numpy().reshape(-1, 4)
+    rec = rec[np.isfinite(rec[:, 3])]
+    hist = H.extract(domain, trials)
+    fits = tpe._Fits(T, hist, H.split_below(hist, 0.25), 1.0, None)
+    chosen = {k: v[0] for k, v in doc['misc']['vals'].items() if v}
+    rs = np.random.RandomState(5)
+    seen = 0
+    for r in T.rows:
+        mine = rec[rec[:, 3] == r.index]
+        if not len(mine) or r.categorical or r.label not in chosen:
+            continue
+        assert len(mine) == C, r.label
+        post = fits.get(r)
+        q = r.args.get('q')
+        log = r.dist.startswith('log') or r.dist.startswith('qlog')
+        lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
+        kw = dict(low=post.low, high=post.high, q=q)
+        tol = 1e-9 if q else 1e-5
+        sub = rs.choice(len(mine), 3000, replace=False)
+        x = mine[sub, 0]
+        for col, mix in ((1, post.below), (2, post.above)):
+            ref = lpdf(x, *mix, **kw)
+            got = mine[sub, col]
+            fin = np.isfinite(ref)
+            err = np.abs(got[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1.0)
+            assert err.max() <= tol, (r.label, col, float(err.max()))
+        score = mine[:, 1] - mine[:, 2]
+        m = np.nanmax(score)
+        eps = 4 * tol * max(1.0, float(np.nanmax(np.abs(mine[:, 1:3]))))
+        ties = np.nonzero(score >= m - eps)[0]
+        assert float(chosen[r.label]) in set(mine[ties, 0].tolist()), r.label
+        seen += 1
+    assert seen >= (2 if branch == 'svm' else 1), seen
