@@ -22,6 +22,7 @@ TAB_PER_BLOCK = 8                  # include/tpe_hip.h TPE_TAB_PER_BLOCK
 TAB_ROW_UNITS = 3                  # include/tpe_hip.h TPE_TAB_ROW_UNITS: 16-B units of a cell row
 BATCH_NO_EXPAND, BATCH_WRITE_CAND, BATCH_NO_FUSE, BATCH_ORDERED_DRAWS, BATCH_TAB_EXACT, BATCH_NO_TAB_FAST = \
     1, 2, 4, 8, 16, 32
+BATCH_NO_FAST2 = 64
 PREC_F32, PREC_F64 = 0, 1
 
 # numpy mirrors of the C structs (the host builds arrays of them and copies

@@ -901,12 +901,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
                                                             tpe_result* __restrict__ run_best, int tpp) {
   __shared__ float4 tab_lds[TPE_TAB_ROW_UNITS * kTabLdsCells];
   __shared__ double cum_lds[kCumLds];
-#ifdef TPE_SAMPLE_TRACE                      // debug builds only: per-phase workgroup timing
-  uint64_t st[5] = {(uint64_t)wall_clock64(), 0, 0, 0, 0};
-  __shared__ int s_exact;
-  if (threadIdx.x == 0) s_exact = 0;
-  uint64_t g_ft[3] = {0, 0, 0};              // flush: after the fold, after its barrier, after the record
-#endif
   __shared__ float4 row_lds[kCumLds];     // {mu, +-sigma (sign = mirrored), Phi(a), Phi(b)} as f32
   __shared__ GuideEnt guide[kGuide];
   __shared__ tpe_best wb[kTabThreads / 64];
@@ -955,9 +949,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       r.global_idx = i2 >= 0 ? cbase + i2 : -1;
       if (i2 >= 0) r.value = drawn ? (ex ? exp_call(v2) : v2) : cand[coff + i2];
       run_best[tile_r] = r;
-#ifdef TPE_SAMPLE_TRACE
-      g_ft[2] = wall_clock64();
-#endif
     } else {
       tpe_best* __restrict__ d = tile_best + (int64_t)tile_r * TPE_BEST_PER_TILE;
       d->score = s2; d->l = l2; d->g = g2; d->idx = i2;
@@ -977,9 +968,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
   int n_def = 0;                          // cells runs deferred so far (workgroup-uniform)
   // the run's best -> its record (block reduction)
   auto flush = [&]() {
-#ifdef TPE_SAMPLE_TRACE
-    if (threadIdx.x == 0) g_ft[0] = wall_clock64();
-#endif
     // lane, wave and their LDS addresses formed here (hoisted to the kernel's
     // start they stayed live across the candidate loops and were spilled)
     int tid = (int)threadIdx.x;
@@ -1006,9 +994,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
     __shared__ double wv[kTabThreads / 64];
     if (lane == 0) { wb[wave].score = bs; wb[wave].l = bl; wb[wave].g = bg; wb[wave].idx = bi; wv[wave] = bv; }
     __syncthreads();
-#ifdef TPE_SAMPLE_TRACE
-    if (threadIdx.x == 0) g_ft[1] = wall_clock64();
-#endif
     if (wave == 0) {                         // lanes 0..15 hold the waves' bests
       const int q = lane < kTabThreads / 64 ? lane : 0;
       double s2 = wb[q].score, l2 = wb[q].l, g2 = wb[q].g, v2 = wv[q];
@@ -1205,9 +1190,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
             __builtin_amdgcn_s_waitcnt(0);               // (the LDS-DMA loads: vmcnt)
             __syncthreads();
           }
-#ifdef TPE_SAMPLE_TRACE
-          if (!st[1]) st[1] = wall_clock64();            // (FAST: the tables landed, the first draws made)
-#endif
           first_unit = false;
           uint32_t exact = 0;
 #pragma unroll
@@ -1314,9 +1296,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       if (run_cells && threadIdx.x == 0)
         s_run[n_def] = RunRec{run_cand_base, run_cand_off, run_bb, run_ab, run_tile,
                               (run_logc ? 1 : 0) | (run_exp ? 2 : 0) | (run_drawn ? 4 : 0)};
-#ifdef TPE_SAMPLE_TRACE
-      if (!st[1]) st[1] = wall_clock64();
-#endif
     }
     const int cand_start = __builtin_amdgcn_readfirstlane(s_start[gi]);
     // cells: the next listed tile continuing this one is taken along (4
@@ -1463,9 +1442,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
           unsigned long long need = __ballot((exact >> j) & 1u);
-#ifdef TPE_SAMPLE_TRACE
-          if (lane == 0) atomicAdd(&s_exact, (int)__popcll(need));
-#endif
           while (need) {
             const int src = __builtin_ctzll(need);
             need &= need - 1;
@@ -1494,7 +1470,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
         using P4 = std::integral_constant<int, 2 * kTabPer>;
         using T = std::true_type;
         using F = std::false_type;
-#ifndef TPE_NO_FAST_CELLS                           // (A/B builds: the general pass only)
         if (tab_in_lds && draw && in_lds && !need_x) {
           // a run of several tile pairs (early selection): its pairs handed out
           // to the waves in units of (pair, 64-thread slot) from an LDS counter,
@@ -1525,7 +1500,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
           } else if (pair) cells_pass(T{}, P4{}, T{}); else cells_pass(T{}, P2{}, T{});
         }
         else
-#endif
         if (tab_in_lds) { if (pair) cells_pass(T{}, P4{}, F{}); else cells_pass(T{}, P2{}, F{}); }
         else { if (pair) cells_pass(F{}, P4{}, F{}); else cells_pass(F{}, P2{}, F{}); }
       }
@@ -1610,20 +1584,9 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       }
     }
   }
-#ifdef TPE_SAMPLE_TRACE
-  st[2] = wall_clock64();
-  __shared__ unsigned long long s_wend[kTabThreads / 64];
-  if (lane == 0) s_wend[wave] = st[2];
-  __syncthreads();
-  st[4] = 0;
-  for (int q = 0; q < kTabThreads / 64; ++q) st[4] = st[4] > s_wend[q] ? st[4] : s_wend[q];
-#endif
   if (cur >= 0) flush();
   if (n_def > 0) {                       // the deferred cells runs: wave r combines run r
     __syncthreads();
-#ifdef TPE_SAMPLE_TRACE
-    if (threadIdx.x == 0) g_ft[1] = wall_clock64();
-#endif
     for (int r = wave; r < n_def; r += kTabThreads / 64) {
       const unsigned long long k2 = lane < kTabThreads / 64 ? s_rk[r][lane] : 0ull;
       const unsigned long long bk = __ockl_wfred_max_u64(k2);
@@ -1646,16 +1609,6 @@ __global__ __launch_bounds__(kTabThreads) void k_sample_tab(const tpe_problem* _
       }
     }
   }
-#ifdef TPE_SAMPLE_TRACE
-  st[3] = wall_clock64();
-  if (threadIdx.x == 0 && (blockIdx.x % 16) == 0)
-    printf("k_sample_tab wg %d start %llu stage %llu tiles %llu flush %llu slowest_wave_tiles %llu exact %d "
-           "fold %llu wave-reduce+barrier %llu wg-reduce+record %llu\n",
-           (int)blockIdx.x, (unsigned long long)st[0], (unsigned long long)(st[1] - st[0]),
-           (unsigned long long)(st[2] - st[1]), (unsigned long long)(st[3] - st[2]),
-           (unsigned long long)(st[4] - st[1]), s_exact, (unsigned long long)(g_ft[0] - st[4]),
-           (unsigned long long)(g_ft[1] - g_ft[0]), (unsigned long long)(g_ft[2] - g_ft[1]));
-#endif
 }
 
 // ---- the fast sample kernel, small-workgroup form (k_sample_fast) ----
@@ -2779,18 +2732,6 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const tpe_problem* __res
                                                      const double4* __restrict__ comp64, int lazy_ok,
                                                      int early, tpe_result* __restrict__ result) {
   const tpe_problem& p = P[blockIdx.x];
-#ifdef TPE_SELECT_TRACE                    // debug builds only: per-block path and duration
-  const uint64_t t_start = wall_clock64();
-  struct Tr {
-    uint64_t t0; const tpe_problem& q;
-    __device__ ~Tr() {
-      if (threadIdx.x == 0)
-        printf("k_select blk %d fam %d flags %d samp_len %d n_tiles %d n_cand %d ticks %llu\n", (int)blockIdx.x,
-               (int)q.family, (int)q.flags, (int)q.samp_len, (int)q.n_tiles, (int)q.n_cand,
-               (unsigned long long)(wall_clock64() - t0));
-    }
-  } tr{t_start, p};
-#endif
   const bool lazy = lazy_ok && sampled && lazy_eligible(p);
   if (early && (lazy || p.tab_mode != TPE_TAB_NONE)) return;   // selected by the table / sample stage
   if (lazy) {
@@ -2998,10 +2939,6 @@ __device__ __forceinline__ void cell_moments_chunked(const float4* __restrict__ 
     }
   }
   const float mx = wave_max(m);
-#ifdef TPE_TABLES_TRACE
-  int n_p1 = 0, n_p2 = 0, n_terms = 0;
-  for (int half = 0; half < 2; ++half) n_p1 += __popcll(__ballot((half ? b1 : b0) > m0 - kChunkSlack));
-#endif
   // pass 2: chunks that could hold a term within 2^-50 of the maximum
   bool bad = !(mx > -INFINITY);
   const float cut = mx - kTabDrop;
@@ -3016,17 +2953,8 @@ __device__ __forceinline__ void cell_moments_chunked(const float4* __restrict__ 
       const float z = ((c - q.x) - q.y) * q.z;
       const float v = q.w - z * z;
       if (v >= cut) add_moments(M, v, z, q.z, h, mx, bad);
-#ifdef TPE_TABLES_TRACE
-      ++n_p2;
-      n_terms += __popcll(__ballot(v >= cut));
-#endif
     }
   }
-#ifdef TPE_TABLES_TRACE
-  if ((threadIdx.x & 63) == 0 && (blockIdx.x % 8) == 0 && (threadIdx.x >> 6) < 2)
-    printf("k_tables chunks blk %d wave %d nch %d pass1 %d pass2 %d terms %d\n", (int)blockIdx.x,
-           (int)(threadIdx.x >> 6), nch, n_p1, n_p2, n_terms);
-#endif
   mx_out = mx;
   bad_out = __ballot(bad) != 0ull;
 }
@@ -3525,24 +3453,9 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     // early selection: one block per problem selects a lazy categorical
     // problem right here (it needs no tables)
     const tpe_problem& q = P[(int)blockIdx.x - tab_blocks];
-#ifdef TPE_TABLES_TRACE
-    const uint64_t t_lazy = wall_clock64();
-#endif
     if (lazy_ok && lazy_eligible(q)) select_cat_lazy(q, samp, comp64, result + ((int)blockIdx.x - tab_blocks));
-#ifdef TPE_TABLES_TRACE
-    if (threadIdx.x == 0)
-      printf("k_tables lazy blk %d problem %d: %llu\n", (int)blockIdx.x, (int)blockIdx.x - tab_blocks,
-             (unsigned long long)(wall_clock64() - t_lazy));
-#endif
     return;
   }
-#ifdef TPE_TABLES_TRACE                     // debug builds only: per-phase wave timing
-  uint64_t tt[6];
-  tt[0] = wall_clock64();
-#define TT(k) tt[k] = wall_clock64()
-#else
-#define TT(k) (void)0
-#endif
   const tpe_tab_job jb = tab_job_at(J, n_jobs, (int)blockIdx.x);
   const tpe_problem& p = P[jb.problem];
   const int b = (int)blockIdx.x - jb.block0;
@@ -3557,7 +3470,6 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       rows_lds[threadIdx.x] = (int)threadIdx.x < jb.rows_n ? comp32[jb.rows_off + threadIdx.x]
                                                            : comp32[jb.wide_off + threadIdx.x - jb.rows_n];
     __syncthreads();
-    TT(1);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int rl = lane / 11, k = lane - 11 * rl;               // (row of the wave, node)
     const int jr = (b * TPE_TAB_PER_BLOCK + wave) * kLpRowsPerWave + rl;
@@ -3593,12 +3505,6 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     const bool row_bad = rl < kLpRowsPerWave && ((bm >> b0) & 0x7FFull) != 0ull;
     if (live && k < 6)
       reinterpret_cast<float*>(tab + jb.off + TPE_TAB_ROW_UNITS * jr)[2 * k + jb.side] = row_bad ? NAN : (float)cf;
-#ifdef TPE_TABLES_TRACE
-    TT(2);
-    if (lane == 0 && (blockIdx.x % 4) == 0 && wave < 2)
-      printf("k_tables direct blk %d wave %d rows %d: lookup+stage %llu sums+fit %llu\n", (int)blockIdx.x, wave, nr,
-             (unsigned long long)(tt[1] - tt[0]), (unsigned long long)(tt[2] - tt[1]));
-#endif
     return;
   }
   if (jb.kind == TPE_TAB_CELLS && jb.rows_n >= 0 && jb.rows_n + jb.wide_n <= kMomDirectRows) {
@@ -3655,7 +3561,6 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     const int k1 = pruned ? p.wide_off : jb.wide_off, n1 = pruned ? p.wide_len : jb.wide_n;
     const bool stage = !pruned && n0 + n1 <= kTabStageRows;      // workgroup-uniform
     __shared__ float4 meta_lds[kChunkMax];
-    TT(1);
     if (stage) {
       // the rows by LDS-DMA: every round's loads issued before the one wait
       // (rounds past the rows: clamped loads into unused slots)
@@ -3669,11 +3574,9 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       }
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      TT(2);
       chunk_meta_wg(rows_lds, nr, meta_lds);
       __syncthreads();
     }
-    TT(3);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool live = j < jb.n;                                   // wave-uniform
     // cell centre and half-width exactly as the sample stage forms them (cell_log2_lds)
@@ -3696,7 +3599,6 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
         cell_moments<false>(comp32 + kk, nn, comp32 + k1, n1, c, h, M, mx, bad);
       }
     }
-    TT(4);
     // every wave is past its passes: the staged rows' LDS takes each wave's
     // per-lane moments, and 4 lanes per moment sum them (16 lanes each, then
     // two shuffles) — no 64-lane butterflies of 11 doubles
@@ -3721,14 +3623,6 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
       const float m = __shfl(mx, kTabMoments);
       const bool fl = __shfl(bad || all_exact ? 1 : 0, kTabMoments) != 0;
       logpoly_side(sum, m, fl, row + jb.side);
-#ifdef TPE_TABLES_TRACE
-      TT(5);
-      if (lane == 0 && (blockIdx.x % 8) == 0 && wave < 2)
-        printf("k_tables lp blk %d wave %d side %d rows %d: lookup %llu stage %llu meta %llu passes %llu reduce+fit %llu\n",
-               (int)blockIdx.x, wave, side, n0 + n1, (unsigned long long)(tt[1] - tt[0]),
-               (unsigned long long)(stage ? tt[2] - tt[1] : 0), (unsigned long long)(stage ? tt[3] - tt[2] : 0),
-               (unsigned long long)(tt[4] - tt[3]), (unsigned long long)(tt[5] - tt[4]));
-#endif
       return;
     }
     float val = 0.f;
@@ -3738,14 +3632,6 @@ __global__ __launch_bounds__(kTabTblThreads) void k_tables(const tpe_problem* __
     float out = lane < kTabMoments ? mv : 0.f;
     if (lane == kTabMoments) out = bad || all_exact ? NAN : mx;
     if (lane <= kTabMoments) row[lane] = out;
-#ifdef TPE_TABLES_TRACE
-    TT(5);
-    if (lane == 0 && (blockIdx.x % 16) == 0 && wave < 2)
-      printf("k_tables blk %d wave %d side %d rows %d: lookup %llu stage %llu meta %llu passes %llu reduce %llu\n",
-             (int)blockIdx.x, wave, side, n0 + n1, (unsigned long long)(tt[1] - tt[0]),
-             (unsigned long long)(stage ? tt[2] - tt[1] : 0), (unsigned long long)(stage ? tt[3] - tt[2] : 0),
-             (unsigned long long)(tt[4] - tt[3]), (unsigned long long)(tt[5] - tt[4]));
-#endif
   } else if (b < jb.n) {                             // lattice: block b computes value b
     double* lds = reinterpret_cast<double*>(rows_lds);
     if (p.family == TPE_FAM_QLOGGAUSS) lattice_row<true>(p, b, comp64, reinterpret_cast<double2*>(tab + jb.off), lds);
@@ -5433,7 +5319,8 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
       max_samp = std::max(max_samp, q.samp_len);
     }
     // (the small-workgroup kernel when the level's tables and sampler rows fit its LDS)
-    const bool fast2 = fast && !fast2_disabled() && max_cells <= kFastMaxCells && max_units <= kFastMaxUnits &&
+    const bool fast2 = fast && !fast2_disabled() && !(flags & TPE_BATCH_NO_FAST2) && max_cells <= kFastMaxCells &&
+                       max_units <= kFastMaxUnits &&
                        max_samp <= kFastSamp;
     b.tab_fast = n_rows > 0 ? (fast2 ? 1 + max_units : fast_lp ? 1 : 0) : 0;
   }
@@ -5494,14 +5381,22 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
                (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK);
     if ((rc = hip_check("k_runs_reduce"))) return rc;
     if ((rc = rccl_allgather_inplace(lx->ex, xper, s))) return rc;
+    // the level's collective is issued: from here every failure is this level's
+    // status (done = 1), so the caller never issues a second collective for it
+    // that the other ranks would not join
+    auto gathered_fail = [&](int code) {
+      *lx->all_status = code;
+      *lx->done = 1;
+      return code;
+    };
     int32_t* st_host = (int32_t*)(host + res_off + P * (int64_t)sizeof(tpe_result));   // (the pad before rb_off)
     int32_t* st_dev = (int32_t*)(dbase + res_off + P * (int64_t)sizeof(tpe_result));
     TPE_LAUNCH(k_combine, dim3(blocks), dim3(kCombThreads), 0, s, (const unsigned char*)lx->ex->dev,
                lx->ex->world, xper, P, rd, st_dev);
-    if ((rc = hip_check("k_combine"))) return rc;
+    if ((rc = hip_check("k_combine"))) return gathered_fail(rc);
     tpe_internal_phase(TPE_PHASE_LAUNCHED);
     e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
+    if (e != hipSuccess) return gathered_fail(fail(TPE_E_HIP, hipGetErrorString(e)));
     tpe_internal_phase(TPE_PHASE_SYNCED);
     memcpy(out, rh, (size_t)P * sizeof(tpe_result));
     *lx->all_status = *(volatile int32_t*)st_host;

@@ -41,6 +41,7 @@ struct Pool {
   std::atomic<int> sleepers{0};
   std::atomic<bool> stop{false};
   std::atomic<bool> retired{false};         // replaced by tpe_host_threads: dispatch nothing more to it
+  std::atomic<int> refs{1};                 // holders: g_pool's slot + every get_pool caller not yet done
   uint32_t gen = 0;                         // dispatcher's generation counter
   int64_t spin_ns = 200000;
   std::vector<std::thread> th;
@@ -107,10 +108,15 @@ void after_fork_child() {        // the workers do not exist in the child: start
   g_pool = nullptr;
 }
 
-// joins the workers of a retired pool.  The Pool object itself is never
-// freed: a concurrent parallel_for may still hold its pointer (from get_pool,
-// before the swap) and will find it retired under `busy` — a few hundred
-// bytes per tpe_host_threads change, which is a configuration call
+// drops one reference: the last holder frees the pool (its workers were
+// joined when it was retired: the slot's reference is dropped after that)
+void release(Pool* p) {
+  if (p && p->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete p;
+}
+
+// joins the workers of a retired pool; a concurrent parallel_for that took its
+// pointer from get_pool before the swap holds a reference and finds it retired
+// under `busy`, so the pool is freed by whichever of them releases it last
 void stop_pool(Pool* p) {
   {
     std::lock_guard<std::mutex> lk(p->m);
@@ -129,8 +135,12 @@ int total_threads() {            // under g_mu
     cpu_set_t set;                       // (the CPUs this process may run on, when restricted)
     if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) hw = std::min(hw, (int)CPU_COUNT(&set));
     // (16: a GPU's share of the host's CPUs; the large levels of configs 4 and 5
-    // fit and pack their labels on them, a 4-label suggest uses what it needs)
-    g_threads = std::min({env_int("TPE_HOST_THREADS", 16), hw, kMaxThreads});
+    // fit and pack their labels on them, a 4-label suggest uses what it needs;
+    // ranks sharing the host under torchrun take their share of its CPUs)
+    int dflt = 16;
+    const int lws = env_int("LOCAL_WORLD_SIZE", 1);
+    if (lws > 1) dflt = std::min(dflt, std::max(2, hw / lws));
+    g_threads = std::min({env_int("TPE_HOST_THREADS", dflt), hw, kMaxThreads});
   }
   return g_threads;
 }
@@ -145,6 +155,7 @@ Pool* get_pool() {
     for (int i = 0; i < t - 1; ++i) p->th.emplace_back(worker, p);
     g_pool = p;
   }
+  g_pool->refs.fetch_add(1, std::memory_order_relaxed);     // (the caller's; release() when done)
   return g_pool;
 }
 
@@ -153,7 +164,8 @@ Pool* get_pool() {
 namespace tpe_pool {
 
 void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
-  Pool* p = n >= 2 ? get_pool() : nullptr;
+  Pool* const held = n >= 2 ? get_pool() : nullptr;
+  Pool* p = held;
   std::unique_lock<std::mutex> own;
   if (p) {
     own = std::unique_lock<std::mutex>(p->busy, std::try_to_lock);
@@ -166,6 +178,7 @@ void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
   }
   if (!p) {
     for (int i = 0; i < n; ++i) fn(ctx, i);
+    release(held);
     return;
   }
   uint32_t g = ++p->gen;
@@ -184,6 +197,8 @@ void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
   }
   run_jobs(p, g);
   while (p->left.load(std::memory_order_acquire) > 0) cpu_relax();
+  own.unlock();
+  release(held);
 }
 
 int workers() {
@@ -213,6 +228,7 @@ extern "C" int tpe_host_threads(int32_t n, int32_t* previous) {
       old->retired.store(true);                      // later dispatchers holding `old` run serially
     }
     stop_pool(old);
+    release(old);                                    // (g_pool's reference)
   }
   return TPE_OK;
 }

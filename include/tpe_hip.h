@@ -112,8 +112,10 @@ enum {
                                   draws + sort) — see "Ordered draws" below */
   TPE_BATCH_TAB_EXACT = 16,    /* test hook: flag every table cell, so every candidate of a
                                   TPE_TAB_CELLS problem takes the exact-sum fallback */
-  TPE_BATCH_NO_TAB_FAST = 32   /* tpe_level_run: the general sample-stage kernel even where the
+  TPE_BATCH_NO_TAB_FAST = 32, /* tpe_level_run: the general sample-stage kernel even where the
                                   specialised one applies (tpe_batch.tab_fast; A/B, tests) */
+  TPE_BATCH_NO_FAST2 = 64      /* tpe_level_run: k_sample_tab's 1024-thread FAST pass where
+                                  k_sample_fast applies (tab_fast = 1 for log-polynomial levels; tests) */
 };
 
 /* precision of the continuous (non-quantized) families; quantized families

@@ -357,9 +357,12 @@ def test_fast_sample_kernel_matches_general(monkeypatch, extra):
         return out
     monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra))
     fast = run()
-    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra | 32))
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra | N.BATCH_NO_FAST2))     # k_sample_tab's 1024-thread FAST pass
+    fast1024 = run()
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(extra | N.BATCH_NO_TAB_FAST))
     gen = run()
     assert fast == gen
+    assert fast1024 == gen
 
 
 @pytest.fixture(scope='module')

@@ -1,6 +1,8 @@
 """The native host runtime (tpe_host.cpp) against its numpy specification:
 bit-exact Parzen fits and categorical posteriors, and the packed level tables
 equal to the numpy packer (no GPU needed)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -173,6 +175,48 @@ def test_native_pack_matches_numpy_packer(precision):
             assert N.TAB_LATTICE in modes and (N.TAB_CELLS in modes) == (precision == 'fp32'), modes
         if C == 24:           # fewer candidates than cells: per-candidate scoring
             assert N.TAB_CELLS not in modes
+
+
+def test_host_pool_swaps_under_concurrent_dispatch():
+    """tpe_host_threads replaces the worker pool while other threads dispatch
+    to it (the packer's parallel label fills): every pack stays identical to
+    a serial one, and retired pools are freed by their last holder (no
+    use-after-free: the dispatchers still holding one run serially)."""
+    import threading
+    rs = np.random.RandomState(9)
+    posts = [parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 5), rs.uniform(-1, 2, 400),
+                                  1.0) for _ in range(12)]
+    lps = [LevelProblem(p, i, [100 + i]) for i, p in enumerate(posts)]
+    lib = N.load()
+    prev = ctypes.c_int32(0)
+    assert lib.tpe_host_threads(-1, ctypes.byref(prev)) == 0
+    ref_e = _engine('fp32')
+    info = ref_e._pack(lps, 4096, 5, 0, None)
+    ref = bytes(ref_e._pinned.numpy()[:int(info.blob_bytes)])
+    errors = []
+    stop = threading.Event()
+
+    def dispatcher():
+        e = _engine('fp32')
+        try:
+            while not stop.is_set():
+                inf = e._pack(lps, 4096, 5, 0, None)
+                if bytes(e._pinned.numpy()[:int(inf.blob_bytes)]) != ref:
+                    errors.append('pack differs')
+        except Exception as ex:          # pragma: no cover
+            errors.append(repr(ex))
+    ts = [threading.Thread(target=dispatcher) for _ in range(3)]
+    for t in ts:
+        t.start()
+    try:
+        for k in range(60):
+            assert lib.tpe_host_threads((2, 5, 3, 8)[k % 4], None) == 0
+    finally:
+        stop.set()
+        for t in ts:
+            t.join()
+        lib.tpe_host_threads(prev.value, None)
+    assert not errors, errors[:3]
 
 
 class _FakeColumn(object):
