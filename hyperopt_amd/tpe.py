@@ -639,10 +639,11 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
 
 
 def _choice_dicts(order, cols, values, active):
-    """Per-id {label: value or None} dicts of a batched suggest, built column
-    by column: numpy makes each column's scalars (np.int64 categories, np.float64
-    values, the reference's types) and one ``dict(zip(...))`` per id assembles
-    them in level order — no per-label Python work per id."""
+    """Per-id {label: value or None} dicts of a batched suggest (more than a
+    few ids: the reference suggests one id at a time, tpe.py:812), built column
+    by column: each column's Python scalars (int categories, float values: no
+    numpy scalar per value) and one ``dict(zip(...))`` per id assembles them
+    in level order — no per-label Python work per id."""
     act = np.asarray(active, dtype=bool)
     vt = np.ascontiguousarray(values.T)      # (a contiguous column makes its scalars faster)
     by_label = {}
@@ -652,7 +653,7 @@ def _choice_dicts(order, cols, values, active):
         full = a.all()
         if fam == N.FAM_CATEGORICAL:         # (inactive entries are NaN: cast only the active ones)
             col = col.astype(np.int64) if full else np.where(a, col, 0.0).astype(np.int64)
-        vals = list(col)
+        vals = col.tolist()
         if not full:
             vals = [v if on else None for v, on in zip(vals, a.tolist())]
         by_label[label] = vals
