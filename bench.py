@@ -455,6 +455,40 @@ def config_workload(config, rank, world, args):
         return ('config4: batched suggest, 4096 new_ids x 4096 candidates, 20-dim U(-5,5), 10k-trial '
                 'history, new_ids sharded over ranks + one all-gather of the chosen values, columnar results'), \
             step, None
+    if config == 5 and args.appending:
+        # FMinIter's flow on the columnar history (fmin.py:88-92): every suggest
+        # follows the evaluation of the previous one, appended as one observation
+        # of every label — the history views grow by one and share the device
+        # columns and resident value orders (History.dev), as a Trials cache's do
+        from hyperopt_amd.history import History
+        D, N, C = args.dims, args.history5, 4096
+        labels = ['x%04d' % i for i in range(D)]
+        cap = N + args.steps + args.warmup + 64
+        rs = np.random.RandomState(SEED)
+        tids = np.arange(cap, dtype=np.int64)
+        cols = {k: np.empty(cap) for k in labels}
+        for k in labels:
+            cols[k][:N] = rs.uniform(-5, 5, N)
+        rl = np.random.RandomState(SEED + 1)
+        losses = np.empty(cap)
+        losses[:N] = rl.uniform(size=N) + 1e-9 * np.arange(N)
+        table = flat_uniform_table(labels)
+        sid = (rank, world) if world > 1 else None
+        dev = {}
+        state = dict(n=N)
+
+        def step(i):
+            n = state['n']
+            hist = History(tids[:n], losses[:n], {k: (tids[:n], cols[k][:n]) for k in labels}, dev=dev)
+            cc = tpe.suggest_choices(table, hist, [n], SEED + i, n_EI_candidates=C, shard_labels=sid, columns=True)
+            v = cc.values[0]
+            for j, k in enumerate(cc.labels):       # the suggestion, evaluated (synthetic loss)
+                cols[k][n] = v[j]
+            losses[n] = rl.uniform() + 1e-9 * n
+            state['n'] = n + 1
+            return D * C
+        return ('config5 appending: %d-dim U(-5,5), %d-trial history growing by one evaluated suggestion per '
+                'step (FMinIter flow), n_EI_candidates=4096' % (D, N)), step, None
     if config == 5:
         D, N, C = args.dims, args.history5, 4096
         labels = ['x%04d' % i for i in range(D)]
@@ -489,6 +523,8 @@ def main():
     ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
     ap.add_argument('--dims', type=int, default=1000, help='config 5 dimensions')
     ap.add_argument('--history5', type=int, default=100000, help='config 5 history length')
+    ap.add_argument('--appending', action='store_true',
+                    help='config 5: one evaluated suggestion appended to the history before every suggest')
     args = ap.parse_args()
 
     import torch
@@ -760,7 +796,8 @@ def run_other(args, rank, world, device):
                'unit': 'candidate-scores/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
                'ms_per_step': 1e3 * elapsed / args.steps, 'higher_is_better': True,
                'scaling': 'strong' if args.config in (4, 5) else 'weak', 'vs_baseline': None, 'dtype': 'f32',
-               'data': 'synthetic', 'config': {'workload': desc, 'config': args.config},
+               'data': 'synthetic', 'config': {'workload': desc, 'config': args.config,
+                                               'appending': bool(args.appending)},
                'p50_step_ms': 1e3 * float(np.median(lat)), 'stage_ms_per_step': stages}
         out.update(extra)
         print(json.dumps(out))
