@@ -660,49 +660,62 @@ def _f32_bounds(post):
     return float(lo), float(hi)
 
 
+def _lpdf_chunked(lpdf, x, mix, kw, chunk=2048):
+    """The oracle's lpdf of many points, in chunks (it forms points x components)."""
+    return np.concatenate([lpdf(x[i:i + chunk], *mix, **kw) for i in range(0, len(x), chunk)] or [np.zeros(0)])
+
+
 def _dense_cells(row, tab4, post, log, what, n_u=33, tol=1e-5):
-    """Every log-polynomial cell row of a label (TPE_F_LOGPOLY) evaluated at
-    ``n_u`` points of its cell (the kernel's f32 cell geometry, lp_log2) in
-    f64 on the host, against the oracle's lpdf at the same f32 coordinates;
+    """Every cell row of a label evaluated at ``n_u`` points of its cell (the
+    kernel's f32 cell geometry: lp_log2 / cell_log2_lds) in f64 on the host,
+    against the oracle's lpdf at the same f32 coordinates — log-polynomial rows
+    (TPE_F_LOGPOLY: both sides' degree-5 polynomials of log2 s interleaved in
+    one row) or moment rows (11 Taylor moments and the shift per side);
     flagged sides (NaN: exact fallback) skipped and counted."""
     from hyperopt_amd import _native as N
-    assert row['tab_mode'] == N.TAB_CELLS and row['flags'] & N.F_LOGPOLY, what
-    n, off = int(row['tab_n'][0]), int(row['tab_off'][0])
-    rows = tab4[off:off + 3 * n].reshape(n, 12).astype(np.float64)
-    b, a = rows[:, 0::2], rows[:, 1::2]                 # {b_k, a_k} interleaved
-    lo, inv = np.float32(row['tab_lo'][0]), np.float32(row['tab_inv'][0])
-    w = np.float32(1) / inv
-    ih = np.float32(1) / (np.float32(0.5) * w)
-    j = np.arange(n)
-    c = ((j + 0.5) * np.float64(w) + np.float64(lo)).astype(np.float32)      # fmaf(j + 0.5, w, lo)
-    h = np.float32(0.5) * w
-    uk = np.linspace(-1, 1, n_u).astype(np.float32)
-    t = (c[:, None] + h * uk[None, :]).astype(np.float32)                   # f32 coordinates in each cell
-    gj = np.floor((t - lo) * inv)
-    u = ((t - c[:, None]) * ih).astype(np.float64)
+    assert row['tab_mode'] == N.TAB_CELLS, what
+    lp = bool(row['flags'] & N.F_LOGPOLY)
     lo_f, hi_f = _f32_bounds(post)
-    ok = (gj == j[:, None]) & (t >= lo_f) & (t <= hi_f)
-    ok_b = ok & np.isfinite(b[:, :1])
-    ok_a = ok & np.isfinite(a[:, :1])
-
-    def horner(cf):
-        s = cf[:, 5:6]
-        for k in range(4, -1, -1):
-            s = s * u + cf[:, k:k + 1]
-        return s
-    lnx = t.astype(np.float64) if log else 0.0
-    lb = horner(b) * np.log(2.0) + float(row['below_base']) - lnx
-    la = horner(a) * np.log(2.0) + float(row['above_base']) - lnx
-    x = np.exp(t.astype(np.float64)) if log else t.astype(np.float64)
     lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
     kw = dict(low=post.low, high=post.high, q=None)
-    for side, ok_s, got, mix in (('l', ok_b, lb, post.below), ('g', ok_a, la, post.above)):
-        xs = x[ok_s]
-        ref = lpdf(xs, *mix, **kw)
-        _check_lpdf(got[ok_s], ref, tol, (what, side, n, int(ok_s.sum())))
-    flagged = int((~np.isfinite(b[:, 0])).sum() + (~np.isfinite(a[:, 0])).sum())
-    assert flagged <= max(4, n // 10), (what, 'flagged sides', flagged, n)     # (exact fallback: tested apart)
-    return int(ok_b.sum() + ok_a.sum())
+    checked = flagged = 0
+    for sd, mix, base in ((0, post.below, float(row['below_base'])), (1, post.above, float(row['above_base']))):
+        g = 0 if lp else sd                                     # (log-polynomial: one table for both)
+        n, off = int(row['tab_n'][g]), int(row['tab_off'][g])
+        rows = tab4[off:off + 3 * n].reshape(n, 12).astype(np.float64)
+        lo, inv = np.float32(row['tab_lo'][g]), np.float32(row['tab_inv'][g])
+        w = np.float32(1) / inv
+        ih = np.float32(1) / (np.float32(0.5) * w)
+        j = np.arange(n)
+        c = ((j + 0.5) * np.float64(w) + np.float64(lo)).astype(np.float32)      # fmaf(j + 0.5, w, lo)
+        uk = np.linspace(-1, 1, n_u).astype(np.float32)
+        t = (c[:, None] + (np.float32(0.5) * w) * uk[None, :]).astype(np.float32)   # f32 points of each cell
+        u = ((t - c[:, None]) * ih).astype(np.float64)
+        ok = (np.floor((t - lo) * inv) == j[:, None]) & (t >= lo_f) & (t <= hi_f)
+        if lp:
+            cf = rows[:, sd::2]                                  # {b_k, a_k} at 2k
+            good = np.isfinite(cf[:, 0])
+            s2 = cf[:, 5:6]
+            for k in range(4, -1, -1):
+                s2 = s2 * u + cf[:, k:k + 1]
+        else:
+            M, m = rows[:, :11], rows[:, 11]
+            good = np.isfinite(m)
+            sm = M[:, 10:11]
+            for k in range(9, -1, -1):
+                sm = sm * u + M[:, k:k + 1]
+            ok &= sm > 0
+            s2 = m[:, None] + np.log2(np.where(sm > 0, sm, 1.0))
+        ok &= good[:, None]
+        flagged += int((~good).sum())
+        lnx = t.astype(np.float64) if log else 0.0
+        got = s2 * np.log(2.0) + base - lnx
+        x = np.exp(t.astype(np.float64)) if log else t.astype(np.float64)
+        _check_lpdf(got[ok], _lpdf_chunked(lpdf, x[ok], mix, kw), tol, (what, 'lg'[sd], n, int(ok.sum()), lp))
+        checked += int(ok.sum())
+    n_all = int(row['tab_n'][0]) + (0 if lp else int(row['tab_n'][1]))
+    assert flagged <= max(4, n_all // 10), (what, 'flagged sides', flagged, n_all)   # (exact fallback: tested apart)
+    return checked
 
 
 def _dense_lattice(row, tab4, post, log, what, tol=1e-9):
@@ -762,7 +775,7 @@ def test_table_rows_dense_against_oracle(engine, dist, args):
     log = dist.startswith('log') or dist.startswith('qlog')
     lo, hi = (args['low'], args['high']) if 'low' in args else (args['mu'] - 3 * args['sigma'],
                                                                args['mu'] + 3 * args['sigma'])
-    obs = rs.uniform(lo, hi, 4000)
+    obs = rs.uniform(lo, hi, 1500)                     # (~1500 cells x 33 points x 1500 components: seconds)
     obs = np.exp(obs) if log else obs
     if q:
         obs = np.round(obs / q) * q
