@@ -750,7 +750,7 @@ def _dense_lattice(row, tab4, post, log, what, tol=1e-9):
             assert qidx(T) >= target, (what, m, T)
             if T > lo_f:
                 assert qidx(np.nextafter(np.float32(T), np.float32(-np.inf))) < target, (what, m, T)
-    assert np.all(np.diff(thr) >= 0), what
+    assert np.all(thr[1:] >= thr[:-1]), what
     return n
 
 
