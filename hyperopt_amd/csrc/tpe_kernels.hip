@@ -286,6 +286,10 @@ __device__ __forceinline__ double lse2_exact64(const double4* __restrict__ comp,
 // (tpe.py:147-159 / :285-298).  LOG selects lognormal_cdf's constant folding.
 template <bool LOG>
 __device__ __forceinline__ double qterm(const double4& c, double tu, double tl) {
+  // (no contraction, as numpy evaluates it: an fma of inc's product with -dec
+  // would leave dec's rounding error where tu == tl and the mass is exactly 0 —
+  // a tiny negative sum whose log is NaN instead of the reference's -inf)
+#pragma clang fp contract(off)
   const double zu = (tu - c.x) / c.y;
   const double zl = (tl - c.x) / c.y;
   double inc, dec;
