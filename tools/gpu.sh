@@ -13,6 +13,7 @@
 #   configs    bench.py --config 1, 2, 4, 5 (CONFIGS)
 #   rehearse   bench.py --gpus 2 over gloo, two ranks on the one GPU (REH_CONFIGS)
 #   hostsplit  host-side time split of the headline suggest
+#   phases     tools/phase_prof.py per workload (PHASE_WL) under the kernel trace
 #   nativesplit native fits / tpe_suggest_tree / device stages of the headline suggest
 #   hostprof   cProfile of the headline suggest on the device
 #   cfgprof    cProfile of one step of config CONFIG (default 5)
@@ -105,6 +106,15 @@ for task in "$@"; do
     hostprof)
       step 300 $O/hostprof_${TAG}.txt python tools/host_prof.py ${STEPS:-300}
       head -60 $O/hostprof_${TAG}.txt ;;
+    phases)
+      # host phases of one suggest per workload, under the kernel trace (device times)
+      for w in ${PHASE_WL:-svm rf cfg2 app}; do
+        rm -rf $O/phases_${TAG}_$w
+        step 300 $O/phases_${TAG}_$w.txt rocprofv3 --kernel-trace --stats --output-format csv \
+            -d $O/phases_${TAG}_$w -o run -- python3 tools/phase_prof.py $w ${STEPS:-200}
+        python3 tools/trace_summary.py $(find $O/phases_${TAG}_$w -name "*kernel_trace.csv") >> $O/phases_${TAG}_$w.txt
+        grep -v "^\[" $O/phases_${TAG}_$w.txt | head -20
+      done ;;
     nativesplit)
       step 300 $O/nativesplit_${TAG}.txt python tools/native_split.py ${STEPS:-200} ${NS_ARGS:-}
       cat $O/nativesplit_${TAG}.txt ;;
