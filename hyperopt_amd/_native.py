@@ -144,7 +144,7 @@ class PackInfo(ctypes.Structure):
         ('key_bits', ctypes.c_int32), ('sort_end_bit', ctypes.c_int32),
         ('off_fit', ctypes.c_int64), ('off_below_idx', ctypes.c_int64), ('off_fit_seg', ctypes.c_int64),
         ('n_fit', ctypes.c_int32), ('fgt_max_boxes', ctypes.c_int32), ('fit_total', ctypes.c_int64),
-        ('copy_end', ctypes.c_int64), ('copy2_len', ctypes.c_int64), ('sort_count', ctypes.c_int64),
+        ('sort_count', ctypes.c_int64),
         ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_new', ctypes.c_int64),
         ('fit_max_obs', ctypes.c_int64),
         ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64), ('n_pooled', ctypes.c_int64),
@@ -152,8 +152,10 @@ class PackInfo(ctypes.Structure):
         ('tab_units', ctypes.c_int64),
         ('off_samp_tiles', ctypes.c_int64), ('n_samp_tiles', ctypes.c_int64), ('n_samp_eager', ctypes.c_int64),
         ('off_tab_tiles', ctypes.c_int64), ('n_tab_tiles', ctypes.c_int64),
-        ('off_expand', ctypes.c_int64), ('n_expand', ctypes.c_int64), ('copy_start', ctypes.c_int64),
+        ('off_expand', ctypes.c_int64), ('n_expand', ctypes.c_int64),
         ('fgt_max_cells', ctypes.c_int64),
+        ('up_off', ctypes.c_int64 * 4), ('up_len', ctypes.c_int64 * 4), ('n_up', ctypes.c_int32),
+        ('pad_', ctypes.c_int32), ('off_patch', ctypes.c_int64),
     ]
 
 

@@ -325,7 +325,7 @@ inline double min_of(const double* __restrict__ v, int64_t n) {
 
 
 // the packer's parallel pass over the large bounded sides' acceptance terms
-constexpr int64_t kPaParallelMin = 2048;    // a side of at least this many components
+constexpr int64_t kPaParallelMin = 1024;    // a side of at least this many components
 constexpr int64_t kPaChunk = 512;           // ... in chunks of this many
 struct PaTask { int32_t li, side; int64_t i0, i1, off; };
 
@@ -900,6 +900,13 @@ int tpe_host_cat_split(const int64_t* obs, const int64_t* tids, int64_t n, const
   return tpe_host_cat_probs(ap, n - nb, upper, p_prior, prior_weight, lf, out_above);
 }
 
+// the level runner's early-fit hook (tpe_level_run): called on the packing
+// thread once the blob's leading sections are placed and the fit jobs written,
+// before the fill — so the device fit runs while the host fills the rest
+static thread_local TpePackHook g_pack_hook = {nullptr, nullptr};
+
+__attribute__((visibility("hidden"))) void tpe_internal_pack_hook(TpePackHook h) { g_pack_hook = h; }
+
 // the pack's straight-line table loops vectorise: an AVX2 clone is picked at
 // load time on hosts that have it (-ffp-contract=off holds in both clones, so
 // the tables are bit-identical)
@@ -1036,12 +1043,132 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
   }
   PACK_MARK("sizing");
-  // (trivially typed: a resize to the same size as the last call touches nothing)
-  comp32.resize((size_t)(4 * n_c32));
-  comp64.resize((size_t)(4 * n_c64));
-  samp.resize((size_t)(8 * n_samp));
-  grid.resize((size_t)std::max<int64_t>(n_grid, 1));
-  grid[0] = 0;
+  // ---- device-fitted above mixtures: rows and grids after the host ones, fit
+  // jobs (before the fill: the level runner may launch the fit right away) ----
+  // (the device grid starts 256-B aligned: the host part's upload never
+  // touches a word the fit wrote)
+  const int64_t host_rows = n_c32, host_grid = std::max<int64_t>(n_grid, 1);
+  const int64_t host_grid_pad = (host_grid + 63) & ~(int64_t)63;
+  std::vector<tpe_fit_job> fit;
+  std::vector<int32_t> below_idx;
+  std::vector<int64_t> fit_seg(1, 0);
+  std::vector<int32_t> fit_li;          // each fit job's label
+  {
+    int64_t nf = 0, nb = 0;
+    for (int32_t li = 0; li < n_labels; ++li)
+      if (dev_fit[li]) { ++nf; nb += std::max<int32_t>(labels[li].n_below, 0); }
+    fit.reserve((size_t)nf); below_idx.reserve((size_t)nb + 1); fit_seg.reserve((size_t)nf + 1);
+  }
+  int64_t dev_rows = 0, dev_grid = 0, fit_max_new = 0, fit_max_obs = 0;
+  {
+    int64_t r = 0;
+    for (int32_t li = 0; li < n_labels; ++li) {
+      const tpe_label_in& L = labels[li];
+      if (dev_fit[li]) {
+        const int64_t K = L.above_k, G = std::min<int64_t>(4096, 4 * K);
+        tpe_fit_job j;
+        memset(&j, 0, sizeof(j));
+        j.obs = L.dev_obs; j.n_obs = L.n_obs; j.seg_off = fit_seg.back();
+        j.below_off = (int32_t)below_idx.size(); j.n_below = L.n_below;
+        j.family = L.family; j.flags = L.flags; j.lf = L.lf;
+        j.problem_first = (int32_t)r; j.n_problems = (int32_t)L.n_ids;
+        j.above_off = (int32_t)(host_rows + dev_rows); j.wide_off = (int32_t)(host_rows + dev_rows + K);
+        j.grid_off = (int32_t)(host_grid_pad + dev_grid); j.grid_n = (int32_t)G;
+        j.prior_mu = L.prior_mu; j.prior_sigma = L.prior_sigma; j.prior_weight = L.prior_weight;
+        j.low = L.low; j.high = L.high;
+        j.ord_key_in = L.ord_key_in; j.ord_idx_in = L.ord_idx_in; j.n_ord_in = L.n_ord_in;
+        j.ord_key_out = L.ord_key_out; j.ord_idx_out = L.ord_idx_out;
+        for (int32_t b = 0; b < L.n_below; ++b) {
+          if (L.below_idx[b] < 0 || L.below_idx[b] >= L.n_obs || (b && L.below_idx[b] <= L.below_idx[b - 1]))
+            return TPE_E_ARG;
+          below_idx.push_back(L.below_idx[b]);
+        }
+        fit.push_back(j);
+        fit_li.push_back(li);
+        // scratch segment: the compacted above order, the new observations' merge
+        // passes and the below positions all fit in it
+        const int64_t n_new = L.n_obs - L.n_ord_in;
+        fit_seg.push_back(fit_seg.back() + std::max<int64_t>(std::max<int64_t>(K - 1, n_new), L.n_below));
+        fit_max_new = std::max(fit_max_new, n_new);
+        fit_max_obs = std::max<int64_t>(fit_max_obs, L.n_obs);
+        dev_rows += K + kPruneWide;
+        dev_grid += G + 1;
+      }
+      r += L.n_ids;
+    }
+  }
+  if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid_pad + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
+  if (below_idx.empty()) below_idx.push_back(0);
+  PACK_MARK("devrows");
+  // ---- expanded levels (include/tpe_hip.h "Expanded levels"): when every label
+  // of a large level scores from tables, its problems differ from their label's
+  // only in (cand_off, ctr3, tile_off) and its tiles are {problem, j * T, 0, 0}
+  // in order: the host writes one template per label and the new ids, the
+  // device (k_expand) writes the problems and tiles — ~240 B + 32 B per (label,
+  // id) neither packed nor uploaded ----
+  const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
+  bool expand = expand_enabled() && !f64 && P >= kExpandMinProblems && n_tiles_p > 0;
+  for (int32_t li = 0; li < n_labels && expand; ++li)
+    if (labels[li].n_ids > 0 && tmode[li] == TPE_TAB_NONE) expand = false;
+  // ---- the blob's leading sections, placed before the fill (the fill writes
+  // its sections in place; the device fit may run while it does):
+  //   fit jobs | below positions | fit segments | grid (host | device, 256-B
+  //   aligned) | comp32 (host | device) | fit patches (device only: the problem
+  //   fields the fit writes, applied after the upload) | problems | tiles
+  //   (device only when expanded) | comp64 | sampler rows
+  // then the later sections (work, finalize tiles, table jobs, tile lists, the
+  // expanded level's templates) after them ----
+  const int NL = 10;
+  const int64_t len_lead[NL] = {(int64_t)(fit.size() * sizeof(tpe_fit_job)), (int64_t)(below_idx.size() * sizeof(int32_t)),
+                                (int64_t)(fit_seg.size() * sizeof(int64_t)), (host_grid_pad + dev_grid) * 4,
+                                (host_rows + dev_rows) * 16, fit.empty() ? 0 : P * (int64_t)sizeof(tpe_problem),
+                                P * (int64_t)sizeof(tpe_problem), P * n_tiles_p * (int64_t)sizeof(tpe_tile),
+                                n_c64 * 32, n_samp * 64};
+  int64_t off_lead[NL], lead_end = 0;
+  for (int i = 0; i < NL; ++i) {
+    off_lead[i] = (lead_end + 255) & ~(int64_t)255;
+    lead_end = off_lead[i] + len_lead[i];
+  }
+  enum { L_FIT, L_BIDX, L_FSEG, L_GRID, L_C32, L_PATCH, L_PROB, L_TILES, L_C64, L_SAMP };
+  // the fill's targets: the blob itself when it holds the leading sections,
+  // else the scratch (the call then only sizes the level: TPE_E_SPACE)
+  const bool direct = blob != nullptr && blob_cap >= lead_end;
+  unsigned char* const bb = (unsigned char*)blob;
+  float* f_comp32;
+  double *f_comp64, *f_samp;
+  int32_t* f_grid;
+  if (direct) {
+    f_comp32 = (float*)(bb + off_lead[L_C32]);
+    f_comp64 = (double*)(bb + off_lead[L_C64]);
+    f_samp = (double*)(bb + off_lead[L_SAMP]);
+    f_grid = (int32_t*)(bb + off_lead[L_GRID]);
+  } else {
+    // (trivially typed: a resize to the same size as the last call touches nothing)
+    comp32.resize((size_t)(4 * n_c32));
+    comp64.resize((size_t)(4 * n_c64));
+    samp.resize((size_t)(8 * n_samp));
+    grid.resize((size_t)host_grid);
+    f_comp32 = comp32.data(); f_comp64 = comp64.data(); f_samp = samp.data(); f_grid = grid.data();
+  }
+  f_grid[0] = 0;
+  if (direct && !fit.empty()) {
+    memcpy(bb + off_lead[L_FIT], fit.data(), (size_t)len_lead[L_FIT]);
+    memcpy(bb + off_lead[L_BIDX], below_idx.data(), (size_t)len_lead[L_BIDX]);
+    memcpy(bb + off_lead[L_FSEG], fit_seg.data(), (size_t)len_lead[L_FSEG]);
+    if (g_pack_hook.fn) {
+      // the level runner uploads the fit sections and launches the device fit
+      tpe_pack_info e;
+      memset(&e, 0, sizeof(e));
+      e.off_fit = off_lead[L_FIT]; e.off_below_idx = off_lead[L_BIDX]; e.off_fit_seg = off_lead[L_FSEG];
+      e.off_grid = off_lead[L_GRID]; e.off_comp32 = off_lead[L_C32]; e.off_patch = off_lead[L_PATCH];
+      e.n_fit = (int32_t)fit.size(); e.fit_total = fit_seg.back();
+      e.fit_max_new = fit_max_new; e.fit_max_obs = fit_max_obs; e.n_problems = P;
+      e.up_off[0] = 0; e.up_len[0] = off_lead[L_FSEG] + len_lead[L_FSEG]; e.n_up = 1;
+      e.blob_bytes = off_lead[L_PATCH] + len_lead[L_PATCH];     // (the device bytes the fit touches)
+      g_pack_hook.fn(g_pack_hook.ctx, &e);
+    }
+  }
+  PACK_MARK("lead");
   // the acceptance terms of the large bounded sides in chunks on the workers
   // (libm erf for every component near a bound: the largest label's would
   // otherwise be its fill's critical path); the fill sums them in order
@@ -1071,7 +1198,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     tpe_pool::parallel_for((int)pa_tasks.size(), [](void* c, int i) { pa_chunk(*(const PaCtx*)c, i); }, (void*)&pcx);
   }
   PACK_MARK("accept");
-  const FillCtx fcx{labels, sec.data(), lab.data(), samp.data(), comp64.data(), comp32.data(), grid.data(),
+  const FillCtx fcx{labels, sec.data(), lab.data(), f_samp, f_comp64, f_comp32, f_grid,
                     dev_fit.data(), tmode.data(), key_bits, f64, pa_terms.data(), pa_off.data()};
   {
     // (a few hundred components per label make a worker's hand-off worth it)
@@ -1082,61 +1209,15 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       for (int32_t li = 0; li < n_labels; ++li) fill_label(fcx, li);
   }
   PACK_MARK("fill");
-  // ---- device-fitted above mixtures: rows and grids after the host ones, fit jobs ----
-  const int64_t host_rows = n_c32, host_grid = (int64_t)grid.size();
-  std::vector<tpe_fit_job> fit;
-  std::vector<int32_t> below_idx;
-  std::vector<int64_t> fit_seg(1, 0);
-  {
-    int64_t nf = 0, nb = 0;
-    for (int32_t li = 0; li < n_labels; ++li)
-      if (dev_fit[li]) { ++nf; nb += std::max<int32_t>(labels[li].n_below, 0); }
-    fit.reserve((size_t)nf); below_idx.reserve((size_t)nb + 1); fit_seg.reserve((size_t)nf + 1);
+  // the device-fitted labels' problem fields (the fill cleared their rows)
+  for (size_t k = 0; k < fit.size(); ++k) {
+    const tpe_fit_job& j = fit[k];
+    tpe_problem& p = lab[fit_li[k]];
+    p.above_off = j.above_off; p.above_len = (int32_t)(j.n_obs - j.n_below + 1);
+    p.wide_off = j.wide_off;
+    p.grid_off = j.grid_off; p.grid_n = j.grid_n;
+    p.narrow_amin = 1.f;       // pruned; the fit stage writes the real value
   }
-  int64_t dev_rows = 0, dev_grid = 0, fit_max_new = 0, fit_max_obs = 0;
-  {
-    int64_t r = 0;
-    for (int32_t li = 0; li < n_labels; ++li) {
-      const tpe_label_in& L = labels[li];
-      if (dev_fit[li]) {
-        tpe_problem& p = lab[li];
-        const int64_t K = L.above_k, G = std::min<int64_t>(4096, 4 * K);
-        p.above_off = (int32_t)(host_rows + dev_rows); p.above_len = (int32_t)K;
-        p.wide_off = (int32_t)(host_rows + dev_rows + K);
-        p.grid_off = (int32_t)(host_grid + dev_grid); p.grid_n = (int32_t)G;
-        p.narrow_amin = 1.f;       // pruned; the fit stage writes the real value
-        tpe_fit_job j;
-        memset(&j, 0, sizeof(j));
-        j.obs = L.dev_obs; j.n_obs = L.n_obs; j.seg_off = fit_seg.back();
-        j.below_off = (int32_t)below_idx.size(); j.n_below = L.n_below;
-        j.family = L.family; j.flags = L.flags; j.lf = L.lf;
-        j.problem_first = (int32_t)r; j.n_problems = (int32_t)L.n_ids;
-        j.above_off = p.above_off; j.wide_off = p.wide_off; j.grid_off = p.grid_off; j.grid_n = p.grid_n;
-        j.prior_mu = L.prior_mu; j.prior_sigma = L.prior_sigma; j.prior_weight = L.prior_weight;
-        j.low = L.low; j.high = L.high;
-        j.ord_key_in = L.ord_key_in; j.ord_idx_in = L.ord_idx_in; j.n_ord_in = L.n_ord_in;
-        j.ord_key_out = L.ord_key_out; j.ord_idx_out = L.ord_idx_out;
-        for (int32_t b = 0; b < L.n_below; ++b) {
-          if (L.below_idx[b] < 0 || L.below_idx[b] >= L.n_obs || (b && L.below_idx[b] <= L.below_idx[b - 1]))
-            return TPE_E_ARG;
-          below_idx.push_back(L.below_idx[b]);
-        }
-        fit.push_back(j);
-        // scratch segment: the compacted above order, the new observations' merge
-        // passes and the below positions all fit in it
-        const int64_t n_new = L.n_obs - L.n_ord_in;
-        fit_seg.push_back(fit_seg.back() + std::max<int64_t>(std::max<int64_t>(K - 1, n_new), L.n_below));
-        fit_max_new = std::max(fit_max_new, n_new);
-        fit_max_obs = std::max<int64_t>(fit_max_obs, L.n_obs);
-        dev_rows += K + kPruneWide;
-        dev_grid += G + 1;
-      }
-      r += L.n_ids;
-    }
-  }
-  if (host_rows + dev_rows >= ((int64_t)1 << 31) || host_grid + dev_grid >= ((int64_t)1 << 31)) return TPE_E_ARG;
-  if (below_idx.empty()) below_idx.push_back(0);
-  PACK_MARK("devrows");
   // ---- score tables: 16-B units (a cell row is 3 units, a lattice row 1) ----
   int64_t tab_units = 0, fgt_max_boxes = 0;
   for (int32_t li = 0; li < n_labels; ++li) {
@@ -1181,20 +1262,9 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   if (tab_units >= ((int64_t)1 << 31)) return TPE_E_ARG;
   PACK_MARK("tabunits");
-  // ---- problems, tiles, work ----
-  const int64_t n_tiles_p = n_cand > 0 ? (n_cand + T - 1) / T : 0;
-  auto& prob = ps.prob;
+  // ---- problems, tiles, work (problem rows and tiles straight into the blob) ----
   int64_t scored = 0;
   const int64_t C_ref = n_cand_global > 0 ? n_cand_global : n_cand;
-  // ---- expanded levels (include/tpe_hip.h "Expanded levels"): when every label
-  // of a large level scores from tables, its problems differ from their label's
-  // only in (cand_off, ctr3, tile_off) and its tiles are {problem, j * T, 0, 0}
-  // in order: the host writes one template per label and the new ids, the
-  // device (k_expand) writes the problems and tiles — ~240 B + 32 B per (label,
-  // id) neither packed nor uploaded ----
-  bool expand = expand_enabled() && !f64 && P >= kExpandMinProblems && n_tiles_p > 0;
-  for (int32_t li = 0; li < n_labels && expand; ++li)
-    if (labels[li].n_ids > 0 && tmode[li] == TPE_TAB_NONE) expand = false;
   auto& xtmpl = ps.xtmpl;
   auto& xfirst = ps.xfirst;
   auto& xctr = ps.xctr;
@@ -1226,7 +1296,13 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   PACK_MARK("expand");
   const int64_t Ph = expand ? 0 : P;      // problems (and their tiles) the host writes
-  prob.resize((size_t)Ph);
+  tpe_problem* prob;
+  if (direct) {
+    prob = (tpe_problem*)(bb + off_lead[L_PROB]);
+  } else {
+    ps.prob.resize((size_t)Ph);
+    prob = ps.prob.data();
+  }
   if (!expand) {
     int64_t r = 0, s_next = 0, u_next = n_sorted_prob * (int64_t)n_cand;
     int32_t slot = 0;
@@ -1268,7 +1344,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   const int64_t target = std::max<int64_t>(1, (target_work() + std::max<int64_t>(scored_tiles, 1) - 1) /
                                                   std::max<int64_t>(scored_tiles, 1));
   bool any_pruned = false;
-  for (auto& q : prob) {
+  for (int64_t r = 0; r < Ph; ++r) {
+    tpe_problem& q = prob[r];
     if (q.family == TPE_FAM_CATEGORICAL || q.tab_mode != TPE_TAB_NONE) { q.n_splits = 0; continue; }
     const int64_t ks = (q.above_len + kMinComponentsPerSplit - 1) / kMinComponentsPerSplit;
     const bool tails = q.sort_slot >= 0 && tiles_ref >= kTailMinTiles;
@@ -1283,10 +1360,15 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     const int64_t cap = std::max<int64_t>(1, (q.above_len + 63) / 64);
     return (int32_t)std::max<int64_t>(1, std::min(ns, cap));
   };
-  auto& tiles = ps.tiles;
-  tiles.resize((size_t)(Ph * n_tiles_p));
+  tpe_tile* tiles;
+  if (direct) {
+    tiles = (tpe_tile*)(bb + off_lead[L_TILES]);
+  } else {
+    ps.tiles.resize((size_t)(Ph * n_tiles_p));
+    tiles = ps.tiles.data();
+  }
   {
-    tpe_tile* __restrict__ tp = tiles.data();
+    tpe_tile* __restrict__ tp = tiles;
     for (int64_t r = 0; r < Ph; ++r) {
       tpe_tile* __restrict__ row = tp + r * n_tiles_p;
       const bool none = prob[r].family == TPE_FAM_CATEGORICAL || prob[r].tab_mode != TPE_TAB_NONE;
@@ -1304,7 +1386,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   work.clear();
   {
     int64_t nw = 0;
-    for (const tpe_tile& tl : tiles) nw += tl.n_splits;
+    for (int64_t t = 0; t < Ph * n_tiles_p; ++t) nw += tiles[t].n_splits;
     work.reserve((size_t)nw);
   }
   int32_t counts[3] = {0, 0, 0};
@@ -1412,49 +1494,48 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   const int64_t n_fin = (int64_t)fin_tiles.size();
   if (fin_tiles.empty()) fin_tiles.push_back(0);
   PACK_MARK("jobs_lists");
-  // ---- blob: sections at 256-B aligned offsets; the device-fitted grid and
-  // comp32 rows sit at the END of the last two sections and are not copied ----
-  const int NS = 15;
+  // ---- the later sections after the leading ones (256-B aligned) ----
+  const int NS = 6;
   // expanded levels: templates, first problems, new ids (one section, 256-B aligned parts)
   const int64_t x_tmpl = (int64_t)(xtmpl.size() * sizeof(tpe_problem));
   const int64_t x_first_off = (x_tmpl + 255) & ~(int64_t)255;
   const int64_t x_ctr_off = (x_first_off + (int64_t)(xfirst.size() * sizeof(int32_t)) + 255) & ~(int64_t)255;
   const int64_t x_len = expand ? x_ctr_off + (int64_t)(xctr.size() * sizeof(uint32_t)) : 0;
-  const void* src[NS] = {prob.data(), tiles.data(), work.data(), comp64.data(), samp.data(), fit.data(),
-                         below_idx.data(), fit_seg.data(), fin_tiles.data(), tab_jobs.data(), samp_tiles.data(),
-                         tab_tiles.data(), nullptr, grid.data(), comp32.data()};
-  const int64_t len[NS] = {(int64_t)(prob.size() * sizeof(tpe_problem)), (int64_t)(tiles.size() * sizeof(tpe_tile)),
-                           (int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(comp64.size() * sizeof(double)),
-                           (int64_t)(samp.size() * sizeof(double)), (int64_t)(fit.size() * sizeof(tpe_fit_job)),
-                           (int64_t)(below_idx.size() * sizeof(int32_t)), (int64_t)(fit_seg.size() * sizeof(int64_t)),
-                           (int64_t)(fin_tiles.size() * sizeof(int32_t)),
+  const void* src[NS] = {work.data(), fin_tiles.data(), tab_jobs.data(), samp_tiles.data(), tab_tiles.data(), nullptr};
+  const int64_t len[NS] = {(int64_t)(work.size() * sizeof(tpe_work)), (int64_t)(fin_tiles.size() * sizeof(int32_t)),
                            (int64_t)(tab_jobs.size() * sizeof(tpe_tab_job)),
                            (int64_t)(samp_tiles.size() * sizeof(int32_t)),
-                           expand ? 0 : (int64_t)(tab_tiles.size() * sizeof(int32_t)), x_len,
-                           (int64_t)(grid.size() * sizeof(int32_t)), (int64_t)(comp32.size() * sizeof(float))};
-  // device-only space: the expanded problems and tiles (k_expand) at the start,
-  // the device-fitted grid and comp32 rows at the end
-  const int64_t reserve[NS] = {expand ? P * (int64_t)sizeof(tpe_problem) : 0,
-                               expand ? P * n_tiles_p * (int64_t)sizeof(tpe_tile) : 0,
-                               0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, dev_grid * (int64_t)sizeof(int32_t), dev_rows * 16};
-  int64_t off[NS], end = 0;
+                           expand ? 0 : (int64_t)(tab_tiles.size() * sizeof(int32_t)), x_len};
+  int64_t off[NS], end = lead_end;
   for (int i = 0; i < NS; ++i) {
     off[i] = (end + 255) & ~(int64_t)255;
-    end = off[i] + len[i] + reserve[i];
+    end = off[i] + len[i];
   }
-  info->off_problems = off[0]; info->off_tiles = off[1]; info->off_work = off[2]; info->off_comp64 = off[3];
-  info->off_samp = off[4]; info->off_fit = off[5]; info->off_below_idx = off[6]; info->off_fit_seg = off[7];
-  info->off_fin_tiles = off[8]; info->n_fin_tiles = n_fin;
+  info->off_fit = off_lead[L_FIT]; info->off_below_idx = off_lead[L_BIDX]; info->off_fit_seg = off_lead[L_FSEG];
+  info->off_grid = off_lead[L_GRID]; info->off_comp32 = off_lead[L_C32];
+  info->off_patch = fit.empty() ? 0 : off_lead[L_PATCH];
+  info->off_problems = off_lead[L_PROB]; info->off_tiles = off_lead[L_TILES];
+  info->off_comp64 = off_lead[L_C64]; info->off_samp = off_lead[L_SAMP];
+  info->off_work = off[0];
+  info->off_fin_tiles = off[1]; info->n_fin_tiles = n_fin;
   info->fit_max_new = fit_max_new;
   info->fit_max_obs = fit_max_obs;
-  info->off_tab_jobs = off[9]; info->n_tab_jobs = n_tab_jobs; info->tab_blocks = tab_blocks;
+  info->off_tab_jobs = off[2]; info->n_tab_jobs = n_tab_jobs; info->tab_blocks = tab_blocks;
   info->tab_units = tab_units;
-  info->off_samp_tiles = off[10]; info->n_samp_tiles = n_samp_tiles; info->n_samp_eager = n_samp_eager;
-  info->off_tab_tiles = off[11]; info->n_tab_tiles = n_tab_tiles;
-  info->off_grid = off[13]; info->off_comp32 = off[14];
-  info->off_expand = expand ? off[12] : 0;
+  info->off_samp_tiles = off[3]; info->n_samp_tiles = n_samp_tiles; info->n_samp_eager = n_samp_eager;
+  info->off_tab_tiles = off[4]; info->n_tab_tiles = n_tab_tiles;
+  info->off_expand = expand ? off[5] : 0;
   info->n_expand = expand ? n_labels : 0;
-  info->copy_start = expand ? off[2] : 0;
+  // host-written ranges (the upload): fit sections + host grid, host comp32
+  // rows, then problems (unless expanded: device-only) through the end
+  info->n_up = 0;
+  auto up = [&](int64_t o, int64_t n) {
+    if (n > 0) { info->up_off[info->n_up] = o; info->up_len[info->n_up] = n; ++info->n_up; }
+  };
+  up(0, off_lead[L_GRID] + host_grid * 4);
+  up(off_lead[L_C32], host_rows * 16);
+  const int64_t r3 = expand ? off_lead[L_C64] : off_lead[L_PROB];
+  up(r3, end - r3);
   info->n_problems = P;
   info->n_tiles = P * n_tiles_p;
   info->n_work_cont = counts[0]; info->n_work_qgauss = counts[1]; info->n_work_qlog = counts[2];
@@ -1466,18 +1547,16 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->fgt_max_boxes = (int32_t)fgt_max_boxes;
   info->fgt_max_cells = fgt_max_cells;
   info->fit_total = fit_seg.back();
-  info->copy_end = off[13] + len[13];
   info->sort_count = n_sorted_prob * (int64_t)n_cand;
   info->n_sorted = S;
   info->n_pooled = n_pooled;
   info->draw_blocks = (C_ref + 1 + 63) / 64;
-  info->copy2_len = len[14];
   info->blob_bytes = end;
   PACK_MARK("offsets");
-  if (!blob || blob_cap < end) return TPE_E_SPACE;
+  if (!direct || blob_cap < end) return TPE_E_SPACE;
   {
-    // the sections into the blob; a large level's in 64-KiB pieces on the
-    // worker pool (a batched level packs megabytes of component rows)
+    // the later sections into the blob; a large level's in 64-KiB pieces on the
+    // worker pool (a batched level's work items)
     struct Piece { unsigned char* dst; const unsigned char* src; size_t n; };
     static thread_local std::vector<Piece> pieces_tl;
     std::vector<Piece>& pieces = pieces_tl;
@@ -1487,8 +1566,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     for (int i = 0; i < NS; ++i) {
       if (!len[i] || !src[i]) continue;
       for (size_t o = 0; o < (size_t)len[i]; o += kPiece)
-        pieces.push_back(Piece{(unsigned char*)blob + off[i] + o, (const unsigned char*)src[i] + o,
-                               std::min(kPiece, (size_t)len[i] - o)});
+        pieces.push_back(Piece{bb + off[i] + o, (const unsigned char*)src[i] + o, std::min(kPiece, (size_t)len[i] - o)});
       total += (size_t)len[i];
     }
     auto copy = [](void* c, int k) {
@@ -1500,7 +1578,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   }
   PACK_MARK("copy");
   if (expand) {
-    unsigned char* x = (unsigned char*)blob + off[12];
+    unsigned char* x = bb + off[5];
     memcpy(x, xtmpl.data(), (size_t)x_tmpl);
     memcpy(x + x_first_off, xfirst.data(), xfirst.size() * sizeof(int32_t));
     memcpy(x + x_ctr_off, xctr.data(), xctr.size() * sizeof(uint32_t));

@@ -3733,17 +3733,41 @@ __global__ __launch_bounds__(kCombThreads) void k_combine(const unsigned char* _
 // System-scope loads: the host rewrites the staging buffer every level.
 constexpr int kUploadThreads = 256;
 
+// the blob's host-written ranges (tpe_pack_info.up_off / up_len, in 8-byte words)
+struct UploadRanges {
+  int64_t w0[4], n8[4];
+  int32_t n;
+};
+
 __global__ __launch_bounds__(kUploadThreads) void k_upload(const unsigned long long* __restrict__ src,
-                                                           unsigned long long* __restrict__ dst, int64_t n8,
-                                                           const unsigned long long* __restrict__ src2,
-                                                           unsigned long long* __restrict__ dst2, int64_t m8) {
+                                                           unsigned long long* __restrict__ dst, UploadRanges r) {
+  int64_t total = 0;
+  for (int k = 0; k < r.n; ++k) total += r.n8[k];
   const int64_t stride = (int64_t)gridDim.x * kUploadThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kUploadThreads + threadIdx.x; i < n8 + m8; i += stride) {
-    const bool first = i < n8;
-    const unsigned long long* s = first ? src + i : src2 + (i - n8);
-    const unsigned long long v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (first) dst[i] = v;
-    else dst2[i - n8] = v;
+  for (int64_t i = (int64_t)blockIdx.x * kUploadThreads + threadIdx.x; i < total; i += stride) {
+    int k = 0;
+    int64_t j = i;
+    while (k < r.n - 1 && j >= r.n8[k]) { j -= r.n8[k]; ++k; }
+    const int64_t w = r.w0[k] + j;
+    dst[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// a device fit that ran before the upload (tpe_level_run's early fit) wrote its
+// problem fields into the patch rows: copied into the problem rows here (the
+// fields k_fit_wide writes), after the upload and k_expand
+__global__ __launch_bounds__(64) void k_fit_patch(const tpe_fit_job* __restrict__ J,
+                                                  const tpe_problem* __restrict__ patch,
+                                                  tpe_problem* __restrict__ prob) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  for (int t = threadIdx.x; t < j.n_problems; t += 64) {
+    const tpe_problem& s = patch[j.problem_first + t];
+    tpe_problem& d = prob[j.problem_first + t];
+    d.above_base = s.above_base;
+    d.wide_len = s.wide_len;
+    d.prior_mu = s.prior_mu; d.prior_a = s.prior_a; d.prior_c = s.prior_c;
+    d.narrow_cmax = s.narrow_cmax; d.narrow_amin = s.narrow_amin;
+    d.grid_lo = s.grid_lo; d.grid_inv = s.grid_inv;
   }
 }
 
@@ -4540,7 +4564,7 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
     const double glo = hdr[kFitHdrGrid], ghi = hdr[kFitHdrGrid + 1];
     const float ginv = ghi > glo ? (float)((double)j.grid_n / (ghi - glo)) : 0.f;
     const double pa = c.bounded ? st.M / st.W : 1.0;
-    tpe_problem& p = P[j.problem_first + threadIdx.x];
+    tpe_problem& p = P[j.problem_first + threadIdx.x];     // (these fields: k_fit_patch copies them too)
     p.above_base = kLn2 * st.cm - log(st.W) - 0.91893853320467274 - log(pa);
     p.wide_len = nw;
     const double pse = fmax(j.prior_sigma, kEPS);
@@ -4608,7 +4632,15 @@ int check_batch(const tpe_batch* b) {
   return TPE_OK;
 }
 
-constexpr int64_t kOneCopyMaxGap = 256 << 10;    // bytes a single upload may carry over
+// TPE_EARLY_FIT=0: a level's device fit runs after its upload (else it starts
+// while the host packs the rest of the level: early_fit_hook; A/B, tests)
+bool early_fit_enabled() {
+  static const int on = [] {
+    const char* v = getenv("TPE_EARLY_FIT");
+    return !(v && v[0] == '0');
+  }();
+  return on != 0;
+}
 
 // TPE_RESULT_COPY=1: read the results back with a copy (else the select stage
 // writes them into the pinned buffer directly)
@@ -5123,6 +5155,70 @@ __attribute__((visibility("hidden"))) int tpe_internal_level_run_ex(
 __attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_exchange* ex, int64_t per,
                                                                  hipStream_t s);   // (after the RCCL loader)
 
+// host-written byte ranges of the packed level as k_upload's 8-byte words; false
+// when a rounded range would pass the device blob (the caller copies instead)
+static bool upload_ranges(const tpe_pack_info& info, int64_t blob_cap, UploadRanges& r, int64_t& words) {
+  memset(&r, 0, sizeof(r));
+  words = 0;
+  for (int k = 0; k < info.n_up && k < 4; ++k) {
+    const int64_t o = info.up_off[k], n = (info.up_len[k] + 7) & ~(int64_t)7;
+    if ((o & 7) || o + n > blob_cap) return false;
+    r.w0[r.n] = o / 8;
+    r.n8[r.n] = n / 8;
+    words += n / 8;
+    ++r.n;
+  }
+  return true;
+}
+
+// the early device fit (tpe_host_pack_level's hook): the fit sections uploaded
+// and tpe_fit_above launched — its problem fields into the patch rows — while
+// the host packs the rest of the level; k_fit_patch applies them after the
+// level's upload.  Nothing happens (the fit stage runs after the upload, as
+// without the hook) unless the workspace holds what it touches.
+struct EarlyFit {
+  const tpe_level_ws* ws;
+  hipStream_t s;
+  const char* dbase;            // the pinned staging buffer's device address
+  int launched;
+  int rc;
+};
+
+static void early_fit_hook(void* c, const tpe_pack_info* e) {
+  EarlyFit& x = *(EarlyFit*)c;
+  const tpe_level_ws* ws = x.ws;
+  if (x.launched || e->n_fit <= 0 || !x.dbase || !kernel_upload() || e->fit_total > ws->fit_cap ||
+      e->blob_bytes > ws->blob_bytes || e->n_problems <= 0)
+    return;
+  UploadRanges r;
+  int64_t words;
+  if (!upload_ranges(*e, ws->blob_bytes, r, words) || words * 8 > ws->pinned_bytes) return;
+  unsigned char* dev = (unsigned char*)ws->blob;
+  const int grid = (int)std::min<int64_t>(std::max<int64_t>((words + kUploadThreads - 1) / kUploadThreads, 1), 2048);
+  TPE_LAUNCH(k_upload, dim3(grid), dim3(kUploadThreads), 0, x.s, (const unsigned long long*)x.dbase,
+             (unsigned long long*)dev, r);
+  if ((x.rc = hip_check("k_upload (early fit)"))) return;
+  tpe_batch b;
+  memset(&b, 0, sizeof(b));
+  b.problems = (const tpe_problem*)(dev + e->off_patch);      // (the fit's problem fields: patch rows)
+  b.n_problems = (int32_t)e->n_problems;
+  b.result = (tpe_result*)dev;                                // (unused by the fit)
+  b.precision = TPE_PREC_F32;
+  b.comp32 = (const float*)(dev + e->off_comp32);
+  b.grid = (const int32_t*)(dev + e->off_grid);
+  b.keys_sorted = b.keys; b.vals_sorted = b.vals;
+  b.fit = (const tpe_fit_job*)(dev + e->off_fit);
+  b.n_fit = e->n_fit;
+  b.below_idx = (const int32_t*)(dev + e->off_below_idx);
+  b.fit_seg = (const int64_t*)(dev + e->off_fit_seg);
+  b.fit_total = e->fit_total;
+  b.fit_keys = ws->fit_keys; b.fit_keys_sorted = ws->fit_keys_sorted;
+  b.fit_vals = ws->fit_vals; b.fit_vals_sorted = ws->fit_vals_sorted;
+  b.fit_max_new = e->fit_max_new; b.fit_max_obs = e->fit_max_obs;
+  x.rc = tpe_fit_above(&b, x.s);
+  x.launched = x.rc == TPE_OK;
+}
+
 static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t n_cand, uint64_t seed,
                           int64_t cand_base, int64_t n_cand_global, int32_t precision, int32_t flags,
                           const tpe_level_ws* ws, tpe_level_need* need, void* stream, tpe_result* out,
@@ -5132,9 +5228,18 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
   tpe_pack_info info;
   memset(&info, 0, sizeof(info));
   // pack straight into the pinned staging buffer; the result readback area
-  // follows the blob
+  // follows the blob.  A level with device fits launches them from inside the
+  // pack, as soon as their jobs are placed (early_fit_hook), unless profiling
+  EarlyFit ef{ws, (hipStream_t)stream, nullptr, 0, TPE_OK};
+  const bool hook = !g_prof.on && precision == TPE_PREC_F32 && direct_results() && early_fit_enabled();
+  if (hook) {
+    ef.dbase = ws->pinned_dev ? (const char*)ws->pinned_dev : device_alias(ws->pinned);
+    tpe_internal_pack_hook(TpePackHook{early_fit_hook, &ef});
+  }
   int rc = tpe_host_pack_level(labels, n_labels, n_cand, seed, cand_base, n_cand_global, precision, ws->pinned,
                                ws->pinned_bytes, &info);
+  if (hook) tpe_internal_pack_hook(TpePackHook{nullptr, nullptr});
+  if (ef.rc != TPE_OK) return ef.rc;
   if (rc != TPE_OK && rc != TPE_E_SPACE) return fail(rc, "tpe_host_pack_level: bad level description");
   tpe_internal_phase(TPE_PHASE_PACK);
   const int64_t P = info.n_problems, C = P * (int64_t)n_cand;
@@ -5171,39 +5276,24 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
   hipStream_t s = (hipStream_t)stream;
   unsigned char* host = (unsigned char*)ws->pinned;
   unsigned char* dev = (unsigned char*)ws->blob;
-  // host-written ranges: [0, copy_end) and the host comp32 rows.  One copy
-  // spanning both when the reserve between them (the device-fitted grid) is
-  // small: what it carries there is overwritten by the fit stage, which runs
-  // after the copy in stream order
-  hipError_t e;
-  const int64_t gap = info.off_comp32 - info.copy_end;
+  // the host-written ranges (tpe_pack_info.up_*): by k_upload, a copy kernel on
+  // the compute queue, or by the copy engine (TPE_UPLOAD_COPY=1)
+  hipError_t e = hipSuccess;
   char* dbase = !direct_results() ? nullptr : (ws->pinned_dev ? (char*)ws->pinned_dev : device_alias(ws->pinned));
-  // ranges to upload: [c0, n1) and [o2, o2 + n2) (one range when the gap is
-  // small); c0 = copy_start: an expanded level's problems and tiles are the
-  // device's (k_expand below)
-  const int64_t c0 = info.copy_start;
-  if (c0 < 0 || (c0 & 255) || c0 > info.copy_end || (info.n_expand > 0) != (c0 > 0))
-    return fail(TPE_E_ARG, "tpe_level_run: bad copy_start");
-  int64_t n1 = info.copy_end, o2 = info.off_comp32, n2 = info.copy2_len;
-  if (n2 > 0 && gap <= kOneCopyMaxGap) { n1 = o2 + n2; n2 = 0; }
-  const int64_t n1r = (n1 - c0 + 7) & ~(int64_t)7, n2r = (n2 + 7) & ~(int64_t)7;
-  if (dbase && kernel_upload() && c0 + n1r <= ws->blob_bytes && (n2 == 0 || o2 + n2r <= ws->blob_bytes) &&
-      n1r + n2r <= ((int64_t)64 << 20)) {
-    const int64_t n8 = n1r / 8, m8 = n2r / 8;
-    const int grid = (int)std::min<int64_t>(std::max<int64_t>((n8 + m8 + kUploadThreads - 1) / kUploadThreads, 1),
-                                            2048);
-    TPE_LAUNCH(k_upload, dim3(grid), dim3(kUploadThreads), 0, s, (const unsigned long long*)(dbase + c0),
-               (unsigned long long*)(dev + c0), n8, (const unsigned long long*)(dbase + o2),
-               (unsigned long long*)(dev + o2), m8);
-    if ((rc = hip_check("k_upload"))) return rc;
-    e = hipSuccess;
-  } else if (info.copy2_len > 0 && gap <= kOneCopyMaxGap) {
-    e = hipMemcpyAsync(dev + c0, host + c0, (size_t)(info.off_comp32 + info.copy2_len - c0), hipMemcpyHostToDevice, s);
-  } else {
-    e = hipMemcpyAsync(dev + c0, host + c0, (size_t)(info.copy_end - c0), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && info.copy2_len > 0)
-      e = hipMemcpyAsync(dev + info.off_comp32, host + info.off_comp32, (size_t)info.copy2_len,
-                         hipMemcpyHostToDevice, s);
+  {
+    UploadRanges r;
+    int64_t words = 0;
+    if (dbase && kernel_upload() && upload_ranges(info, ws->blob_bytes, r, words) && words <= ((int64_t)8 << 20)) {
+      const int grid = (int)std::min<int64_t>(std::max<int64_t>((words + kUploadThreads - 1) / kUploadThreads, 1),
+                                              2048);
+      TPE_LAUNCH(k_upload, dim3(grid), dim3(kUploadThreads), 0, s, (const unsigned long long*)dbase,
+                 (unsigned long long*)dev, r);
+      if ((rc = hip_check("k_upload"))) return rc;
+    } else {
+      for (int k = 0; k < info.n_up && e == hipSuccess; ++k)
+        e = hipMemcpyAsync(dev + info.up_off[k], host + info.up_off[k], (size_t)info.up_len[k], hipMemcpyHostToDevice,
+                           s);
+    }
   }
   if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));
   // expanded level: the templates, first problems and new ids (uploaded above)
@@ -5228,6 +5318,11 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
                (int)nl, (const uint32_t*)(dev + info.off_expand + ctr_off), (tpe_problem*)(dev + info.off_problems),
                (tpe_tile*)(dev + info.off_tiles), P, (int32_t)n_tiles_p, n_cand);
     if ((rc = hip_check("k_expand"))) return rc;
+  }
+  if (ef.launched) {                           // the early fit's problem fields into the rows
+    TPE_LAUNCH(k_fit_patch, dim3(info.n_fit), dim3(64), 0, s, (const tpe_fit_job*)(dev + info.off_fit),
+               (const tpe_problem*)(dev + info.off_patch), (tpe_problem*)(dev + info.off_problems));
+    if ((rc = hip_check("k_fit_patch"))) return rc;
   }
   tpe_batch b;
   memset(&b, 0, sizeof(b));
@@ -5345,7 +5440,7 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
       b.result = (tpe_result*)(xrun + info.n_tiles * (int64_t)sizeof(tpe_result));
     }
   }
-  if (info.n_fit > 0) {
+  if (info.n_fit > 0 && !ef.launched) {
     b.fit = (const tpe_fit_job*)(dev + info.off_fit);
     b.n_fit = info.n_fit;
     b.below_idx = (const int32_t*)(dev + info.off_below_idx);

@@ -21,3 +21,16 @@ void parallel_for(int n, void (*fn)(void* ctx, int i), void* ctx);
 int workers();
 
 }  // namespace tpe_pool
+
+// tpe_host_pack_level's early hook (internal, per thread): tpe_level_run sets it
+// around its pack; the packer calls fn once the blob's leading sections are
+// placed and its device-fit jobs written, before the fill — `early` holds the
+// leading offsets, the fit counts, the bytes to upload (up_off / up_len[0]) and
+// the device bytes the fit touches (blob_bytes) — so the device fit can run
+// while the host fills the rest.  {nullptr, nullptr}: no hook.
+struct tpe_pack_info;
+struct TpePackHook {
+  void (*fn)(void* ctx, const struct tpe_pack_info* early);
+  void* ctx;
+};
+extern "C" void tpe_internal_pack_hook(TpePackHook h);

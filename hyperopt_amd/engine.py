@@ -770,10 +770,9 @@ class Engine(object):
         nbytes = int(info.blob_bytes)
         dev = self._buf('blob', nbytes, torch.uint8)
         # host-written ranges only: device-fitted rows are produced by tpe_fit_above
-        c0, o2, c2 = int(info.copy_end), int(info.off_comp32), int(info.copy2_len)
-        dev[:c0].copy_(self._pinned[:c0], non_blocking=True)
-        if c2:
-            dev[o2:o2 + c2].copy_(self._pinned[o2:o2 + c2], non_blocking=True)
+        for i in range(int(info.n_up)):
+            o, n = int(info.up_off[i]), int(info.up_len[i])
+            dev[o:o + n].copy_(self._pinned[o:o + n], non_blocking=True)
         base = dev.data_ptr()
         prob = np.frombuffer(self._pinned.numpy(), dtype=N.PROBLEM_DTYPE, count=P, offset=int(info.off_problems))
         d_cand = self._buf('cand', C_total, torch.float64)

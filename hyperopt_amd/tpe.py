@@ -490,6 +490,25 @@ def _below_positions(hist, label, otids, below_tids):
     return b, above
 
 
+def _side_orders(hist, label, otids, x, below_tids):
+    """numpy's argsort of a label's below and above sides (the reference's tie
+    order, tpe.py:427-428), kept on the below set beside the positions for the
+    same History and column length (a History's columns are fixed): a suggest
+    on an unchanged history and below set — the same inputs — reuses them."""
+    bidx, above = _below_positions(hist, label, otids, below_tids)
+    memo = getattr(below_tids, 'positions', None)
+    key = ('orders', label)
+    if memo is not None:
+        p = memo.get(key)
+        if p is not None and p[0] == len(otids) and p[1] is hist:
+            return p[2], p[3]
+    ob = np.argsort(x[bidx])
+    oa = np.argsort(x[above])
+    if memo is not None:
+        memo[key] = (len(otids), hist, ob, oa)
+    return ob, oa
+
+
 def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False, remote=()):
     if not hist.sorted_obs:
         return None
@@ -559,9 +578,7 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
         if dmin is not None and _FAMILY[row.dist] in DEVICE_FIT_FAMILIES and n >= dmin:
             return False                       # (device-fit sizes: the general path)
         x = hist.coord_values(row.label, row.dist, _coord_fn(table, row))
-        bidx, above = _below_positions(hist, row.label, otids, below_tids)
-        ob = np.argsort(x[bidx])
-        oa = np.argsort(x[above])
+        ob, oa = _side_orders(hist, row.label, otids, x, below_tids)
         cols = hist.cat_columns(row.label)     # (the cache's column addresses: tids, raw values)
         if cols is None:
             t = np.ascontiguousarray(otids, dtype=np.int64)

@@ -545,7 +545,6 @@ typedef struct tpe_pack_info {
   int64_t off_fit, off_below_idx, off_fit_seg;
   int32_t n_fit, fgt_max_boxes;     /* device fits; most boxes of a TPE_F_FGT label */
   int64_t fit_total;
-  int64_t copy_end, copy2_len;
   int64_t sort_count;               /* candidates of the sorted (pruned) problems */
   int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
   int64_t fit_max_new;                  /* tpe_batch.fit_max_new */
@@ -557,9 +556,19 @@ typedef struct tpe_pack_info {
   /* expanded level (see "Expanded levels"; n_expand = 0: not expanded): off_expand holds
    * tpe_problem templates[n_expand], then (at the next 256-B boundary) int32 first[n_expand + 1],
    * then (at the next 256-B boundary) uint32 new_id[n_problems]; the problems and tiles sections
-   * (and the tabulated tile list, the identity) are device-only: the upload starts at copy_start */
-  int64_t off_expand, n_expand, copy_start;
+   * (and the tabulated tile list, the identity) are device-only */
+  int64_t off_expand, n_expand;
   int64_t fgt_max_cells;                /* most above cells of a TPE_F_FGT label (tpe_batch) */
+  /* ABI 20: the blob's host-written byte ranges [up_off[i], up_off[i] + up_len[i]), i < n_up
+   * (the upload; everything else is device-only: the device-fitted rows and grid, the fit
+   * patches, an expanded level's problems and tiles).  Layout: fit jobs, below positions,
+   * fit segments, grid (host | device from a 256-B boundary), comp32 (host | device), fit
+   * patches (off_patch: one tpe_problem per problem, the fields the device fit writes,
+   * applied to the problem rows after the upload), problems, tiles, comp64, sampler rows,
+   * then work, finalize tiles, table jobs, tile lists and the expanded templates. */
+  int64_t up_off[4], up_len[4];
+  int32_t n_up, pad_;
+  int64_t off_patch;                    /* 0: no device fit */
 } tpe_pack_info;
 
 /* ------------------------------------------------------------------------

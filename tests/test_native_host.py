@@ -244,7 +244,9 @@ class _FakeOrder(object):
 
 def test_pack_reserves_device_fit_rows():
     """A device-fitted above mixture (tpe_fit_job) gets its comp32 rows, wide
-    rows and grid at the END of those sections, outside the host copy ranges."""
+    rows and grid at the END of those sections (the grid's from a 256-B
+    boundary), outside the host-written upload ranges, and a patch area for the
+    problem fields the fit writes (the early fit: tpe_level_run)."""
     rs = np.random.RandomState(5)
     n_obs, bidx = 500, np.array([3, 10, 77], dtype=np.int32)
     host = parzen.fit_posterior('normal', dict(mu=0.0, sigma=2.0), rs.normal(0, 2, 9), rs.normal(0, 2, 300), 1.0)
@@ -268,7 +270,8 @@ def test_pack_reserves_device_fit_rows():
     np.testing.assert_array_equal(_blob(e, info, info.off_below_idx, np.int32, 3), bidx)
     np.testing.assert_array_equal(_blob(e, info, info.off_fit_seg, np.int64, 2), [0, n_obs])
     prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, 5)
-    host_rows = info.copy2_len // 16
+    ups = [(int(info.up_off[i]), int(info.up_len[i])) for i in range(info.n_up)]
+    host_rows = dict(ups)[info.off_comp32] // 16
     for p in prob[2:]:
         assert p['above_len'] == K and p['above_off'] == host_rows == j['above_off']
         assert p['wide_off'] == host_rows + K == j['wide_off']
@@ -277,8 +280,13 @@ def test_pack_reserves_device_fit_rows():
     # host rows of the other label lie before the device region, its grid too
     assert prob[0]['above_off'] + prob[0]['above_len'] <= host_rows
     assert prob[0]['grid_off'] + prob[0]['grid_n'] + 1 <= j['grid_off']
-    assert info.copy_end == info.off_grid + 4 * j['grid_off']
-    assert info.blob_bytes == info.off_comp32 + 16 * (host_rows + K + 16)
+    assert j['grid_off'] % 64 == 0 and ups[0] == (0, info.off_grid + 4 * (prob[0]['grid_off'] + prob[0]['grid_n'] + 1))
+    dev_ranges = [(info.off_grid + 4 * j['grid_off'], 4 * (j['grid_n'] + 1)),
+                  (info.off_comp32 + 16 * host_rows, 16 * (K + 16)), (info.off_patch, 5 * N.PROBLEM_DTYPE.itemsize)]
+    for o, n in dev_ranges:                                  # (device-only bytes: in no upload range)
+        assert all(o + n <= uo or o >= uo + un for uo, un in ups), (o, n, ups)
+    assert info.off_patch >= info.off_comp32 + 16 * (host_rows + K + 16)
+    assert ups[-1][0] == info.off_problems and ups[-1][0] + ups[-1][1] == info.blob_bytes
     with pytest.raises(RuntimeError):
         _engine('fp64')._pack(lps, 4096, 1, 0, None)
 
