@@ -22,6 +22,8 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     OUT = out
     deps = [SRC, HOST_SRC, SUGGEST_SRC, POOL_SRC, os.path.join(HERE, 'csrc', 'tpe_pool.h'),
             os.path.join(HERE, '..', 'include', 'tpe_hip.h'), os.path.abspath(__file__)]
+    if out == os.path.join(HERE, 'libtpe_hip.so'):
+        build_hostaddr(force, verbose)
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
@@ -58,6 +60,26 @@ def build(force=False, verbose=False, out=OUT, defines=()):
             raise RuntimeError('build step failed: %s' % cmd[0])
     os.replace(tmp, OUT)
     return OUT
+
+
+def build_hostaddr(force=False, verbose=False):
+    """gcc the _hostaddr CPython module (csrc/hostaddr.c) in-tree."""
+    import sysconfig
+    import numpy
+    src = os.path.join(HERE, 'csrc', 'hostaddr.c')
+    out = os.path.join(HERE, '_hostaddr' + sysconfig.get_config_var('EXT_SUFFIX'))
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    cmd = [os.environ.get('CC', 'gcc'), '-O2', '-shared', '-fPIC', '-Wall', '-I', sysconfig.get_paths()['include'],
+           '-I', numpy.get_include(), src, '-o', out + '.tmp']
+    if verbose:
+        print(' '.join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError('build step failed: %s' % cmd[0])
+    os.replace(out + '.tmp', out)
+    return out
 
 
 if __name__ == '__main__':

@@ -8,6 +8,13 @@ mixture on the device (tpe_fit_above).  A column is append-only: each call
 uploads only the observations it has not seen yet, so a 100k-trial history
 costs its upload once, not per suggest — and so is the label's value order
 (ValueOrder): each observation is sorted into it once.
+
+Every label's column is a segment of ONE flat device tensor per History (and
+every label's value order a segment of two more), so a suggest that appends
+an observation to a thousand labels uploads them with one scatter, and the
+columns' and orders' addresses come out of numpy arrays (a thousand labels'
+records are filled without a per-label device call).  Segments keep spare
+room; one that outgrows it re-lays out the tensor (every segment doubles).
 """
 import numpy as np
 
@@ -17,98 +24,241 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
 
+def _room(n):
+    """Segment capacity for n entries (room to append)."""
+    return int(n + max(1024, n // 8))
+
+
+def _positions(off, n):
+    """Concatenated ranges [off[i], off[i] + n[i]) (int64)."""
+    off = np.asarray(off, dtype=np.int64)
+    n = np.asarray(n, dtype=np.int64)
+    tot = int(n.sum())
+    if tot == 0:
+        return np.zeros(0, dtype=np.int64)
+    start = np.repeat(off - np.concatenate([[0], np.cumsum(n)[:-1]]), n)
+    return start + np.arange(tot, dtype=np.int64)
+
+
+class _Orders(object):
+    """The resident value orders of a DeviceColumns' labels: per slot a
+    segment of two (t: float64, position: int32) buffer pairs — the current
+    pair holds the order of the first ``n`` observations; a level run that sees
+    more merges the new ones into the other pair (tpe_fit_above) and
+    ``commit`` makes it current."""
+
+    def __init__(self, device, owner):
+        self.device, self.owner = device, owner
+        self.keys = self.idx = None            # [2 x TC] float64 / int32
+        self.tc = 0
+        self.off = np.zeros(0, dtype=np.int64)
+        self.cap = np.zeros(0, dtype=np.int64)
+        self.cur = np.zeros(0, dtype=np.int64)
+        self.n = np.zeros(0, dtype=np.int64)
+        self.kbase = self.ibase = 0
+
+    def add(self):
+        self.off = np.append(self.off, 0)
+        self.cap = np.append(self.cap, 0)
+        self.cur = np.append(self.cur, 0)
+        self.n = np.append(self.n, 0)
+        return len(self.n) - 1
+
+    def ensure(self, slots, n_obs):
+        """Room for n_obs[i] entries in slot slots[i] (a re-layout moves every
+        slot's current order; the owner's version moves)."""
+        slots = np.asarray(slots, dtype=np.int64)
+        n_obs = np.asarray(n_obs, dtype=np.int64)
+        if self.keys is not None and not np.any(n_obs > self.cap[slots]):
+            return
+        cap = self.cap.copy()
+        grow = np.zeros(len(cap), dtype=bool)
+        grow[slots[n_obs > cap[slots]]] = True
+        want = np.zeros(len(cap), dtype=np.int64)
+        np.maximum.at(want, slots, n_obs)
+        cap[grow] = np.maximum(np.array([_room(int(w)) for w in want[grow]], dtype=np.int64), 2 * cap[grow])
+        off = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64)
+        tc = int(cap.sum())
+        keys = torch.empty(2 * max(tc, 1), dtype=torch.float64, device=self.device)
+        idx = torch.empty(2 * max(tc, 1), dtype=torch.int32, device=self.device)
+        if self.keys is not None and int(self.n.sum()):
+            # every slot's current order into its new place (one gather each)
+            src = _positions(self.cur * self.tc + self.off, self.n)
+            dst = _positions(self.cur * tc + off, self.n)
+            si = torch.from_numpy(src).to(self.device)
+            di = torch.from_numpy(dst).to(self.device)
+            keys[di] = self.keys[si]
+            idx[di] = self.idx[si]
+        self.keys, self.idx, self.tc, self.off, self.cap = keys, idx, tc, off, cap
+        self.kbase, self.ibase = keys.data_ptr(), idx.data_ptr()
+        self.owner.version += 1
+
+    def ptrs_many(self, slots, n_obs):
+        """(key_in, idx_in, n_in, key_out, idx_out) device addresses, as int64
+        arrays, for runs that fit slot slots[i]'s first n_obs[i] observations."""
+        slots = np.asarray(slots, dtype=np.int64)
+        n_obs = np.asarray(n_obs, dtype=np.int64)
+        self.ensure(slots, n_obs)
+        on, cur, off = self.n[slots], self.cur[slots], self.off[slots]
+        n_in = np.where(on <= n_obs, on, 0)              # (a longer order is of another column)
+        has = n_in > 0
+        kin = np.where(has, self.kbase + 8 * (cur * self.tc + off), 0)
+        iin = np.where(has, self.ibase + 4 * (cur * self.tc + off), 0)
+        out = n_in != n_obs
+        kout = np.where(out, self.kbase + 8 * ((1 - cur) * self.tc + off), 0)
+        iout = np.where(out, self.ibase + 4 * ((1 - cur) * self.tc + off), 0)
+        return kin, iin, n_in, kout, iout
+
+    def commit_many(self, slots, n_obs):
+        slots = np.asarray(slots, dtype=np.int64)
+        n_obs = np.asarray(n_obs, dtype=np.int64)
+        mv = self.n[slots] != n_obs
+        if mv.any():
+            s = slots[mv]
+            self.cur[s] = 1 - self.cur[s]
+            self.n[s] = n_obs[mv]
+            self.owner.version += 1
+
+
 class ValueOrder(object):
     """Resident value order of one device-fitted label (include/tpe_hip.h,
     "Device value order"): the label's observations as (t, position) pairs
     sorted by t, where t is the kernel coordinate (x, or ln x for the log
-    families).  Two float64/int32 buffer pairs: the current pair holds the
-    order of the first ``n`` observations; a level run that sees more
-    observations merges the new ones into the other pair (tpe_fit_above), and
-    ``commit`` makes that pair current.  The reference re-sorts every
-    suggest (tpe.py:427); this sorts each observation once."""
-    __slots__ = ('device', 'keys', 'idx', 'cur', 'n', 'owner')
+    families) — a slot of its DeviceColumns' order buffers.  The reference
+    re-sorts every suggest (tpe.py:427); this sorts each observation once."""
+    __slots__ = ('group', 'slot')
 
-    def __init__(self, device, owner=None):
-        self.device = device
-        self.owner = owner            # the DeviceColumns whose version a change bumps
-        self.keys = [None, None]
-        self.idx = [None, None]
-        self.cur = 0
-        self.n = 0
+    def __init__(self, group, slot):
+        self.group, self.slot = group, slot
 
-    def _room(self, side, n):
-        t = self.keys[side]
-        if t is None or t.numel() < n:
-            cap = max(n, 1024, 2 * (t.numel() if t is not None else 0))
-            self.keys[side] = torch.empty(cap, dtype=torch.float64, device=self.device)
-            self.idx[side] = torch.empty(cap, dtype=torch.int32, device=self.device)
-            self._bump()
+    @property
+    def n(self):
+        return int(self.group.n[self.slot])
 
     def ptrs(self, n_obs):
         """(key_in, idx_in, n_in, key_out, idx_out) device addresses for a run
         that fits the label's first ``n_obs`` observations."""
-        n_in = self.n if self.n <= n_obs else 0          # (a longer order is of another column)
-        cur, nxt = self.cur, 1 - self.cur
-        kin = self.keys[cur].data_ptr() if n_in else 0
-        iin = self.idx[cur].data_ptr() if n_in else 0
-        if n_in == n_obs:
-            return kin, iin, n_in, 0, 0
-        self._room(nxt, n_obs)
-        return kin, iin, n_in, self.keys[nxt].data_ptr(), self.idx[nxt].data_ptr()
+        return tuple(int(a[0]) for a in self.group.ptrs_many([self.slot], [n_obs]))
 
     def commit(self, n_obs):
         """A run with ``ptrs(n_obs)`` was enqueued: its output is the order."""
-        if self.n != n_obs:
-            self.cur, self.n = 1 - self.cur, n_obs
-            self._bump()
-
-    def _bump(self):
-        if self.owner is not None:
-            self.owner.version += 1
+        self.group.commit_many([self.slot], [n_obs])
 
     def host(self):
         """(t, position) of the current order, copied to the host (tests)."""
-        n = self.n
+        g, s = self.group, self.slot
+        n = int(g.n[s])
         if n == 0:
             return np.zeros(0), np.zeros(0, dtype=np.int64)
-        return (self.keys[self.cur][:n].cpu().numpy(),
-                self.idx[self.cur][:n].cpu().numpy().astype(np.int64) & 0xFFFFFFFF)
+        o = int(g.cur[s]) * g.tc + int(g.off[s])
+        return g.keys[o:o + n].cpu().numpy(), g.idx[o:o + n].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
 
 
 class DeviceColumns(object):
     """float64 device copies of a History's observation columns (one device),
     in the kernel coordinate (x, or np.log(x) for the log families), and the
-    labels' resident value orders."""
+    labels' resident value orders: segments of flat device tensors, slot s of
+    the column store and slot s of the order group belonging to one label."""
 
     def __init__(self, device):
         self.device = device
-        self.cols = {}                # label -> [tensor, n uploaded, ValueOrder]
         self.version = 0              # bumped whenever a column or an order moves (memos of their addresses)
+        self.store = None
+        self.base = 0
+        self.slot = {}                # label -> slot
+        self.views = []               # slot -> the store's segment (a tensor view)
+        self.off = np.zeros(0, dtype=np.int64)
+        self.cap = np.zeros(0, dtype=np.int64)
+        self.n = np.zeros(0, dtype=np.int64)        # values uploaded per slot
+        self.orders = _Orders(device, self)
+
+    def _add(self, label):
+        s = self.slot[label] = len(self.views)
+        self.views.append(None)
+        self.off = np.append(self.off, 0)
+        self.cap = np.append(self.cap, 0)
+        self.n = np.append(self.n, 0)
+        assert self.orders.add() == s
+        return s
+
+    def _relayout(self, want):
+        """Every slot to a segment of at least want[s] (doubling the grown ones),
+        the uploaded values kept (one gather)."""
+        cap = self.cap.copy()
+        grow = want > cap
+        cap[grow] = np.maximum(np.array([_room(int(w)) for w in want[grow]], dtype=np.int64), 2 * cap[grow])
+        off = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64)
+        store = torch.empty(max(int(cap.sum()), 1), dtype=torch.float64, device=self.device)
+        if self.store is not None and int(self.n.sum()):
+            si = torch.from_numpy(_positions(self.off, self.n)).to(self.device)
+            di = torch.from_numpy(_positions(off, self.n)).to(self.device)
+            store[di] = self.store[si]
+        self.store, self.off, self.cap = store, off, cap
+        self.base = store.data_ptr()
+        self.views = [store[o:o + c] for o, c in zip(off.tolist(), cap.tolist())]
+        self.version += 1
+
+    def upload(self, labels, values):
+        """Make the column of labels[i] hold values[i] (a float64 array that
+        extends what earlier calls for the label passed; a shorter one — another
+        History's — starts the label over, its order too); the values not
+        uploaded yet go up in one scatter.  Returns the labels' slots (int64)."""
+        get = self.slot.get
+        slots = np.fromiter((get(k, -1) for k in labels), dtype=np.int64, count=len(labels))
+        nv = np.fromiter(map(len, values), dtype=np.int64, count=len(values))
+        if len(slots) and slots.min() < 0:
+            for i in np.flatnonzero(slots < 0).tolist():
+                s = get(labels[i])
+                slots[i] = s if s is not None else self._add(labels[i])
+        m = self.n[slots]
+        short = m > nv
+        if short.any():
+            s = slots[short]
+            self.n[s] = 0
+            self.orders.n[s] = 0
+            self.orders.cur[s] = 0
+            m = self.n[slots]
+        if self.store is None or np.any(nv > self.cap[slots]):
+            want = np.zeros(len(self.cap), dtype=np.int64)
+            np.maximum.at(want, slots, nv)
+            self._relayout(want)
+        up = np.flatnonzero(nv > m)
+        if len(up):
+            ml, nl = m.tolist(), nv.tolist()
+            vals = np.concatenate([values[i][ml[i]:nl[i]] for i in up.tolist()]).astype(np.float64, copy=False)
+            su = slots[up]
+            pos = _positions(self.off[su] + m[up], nv[up] - m[up])
+            self.store[torch.from_numpy(pos).to(self.device)] = torch.from_numpy(vals).to(self.device)
+            self.n[su] = nv[up]
+            self.version += 1
+        return slots
+
+    def columns(self, items):
+        """Device tensors (store segments) whose first ``len(values)`` entries
+        are ``values``, for every (label, values) of ``items`` (``upload``)."""
+        slots = self.upload([k for k, _ in items], [v for _, v in items])
+        return [self.views[s] for s in slots.tolist()]
 
     def column(self, label, values):
         """Device tensor whose first ``len(values)`` entries are ``values``
         (values must extend what earlier calls for this label passed)."""
-        n = len(values)
-        ent = self.cols.get(label)
-        if ent is None or ent[1] > n:
-            ent = self.cols[label] = [torch.empty(max(n, 1024), dtype=torch.float64, device=self.device), 0,
-                                      ValueOrder(self.device, self)]
-            self.version += 1
-        t, m = ent[0], ent[1]
-        if n > m:
-            if n > t.numel():
-                grown = torch.empty(max(n, 2 * t.numel()), dtype=torch.float64, device=self.device)
-                grown[:m].copy_(t[:m])
-                t = ent[0] = grown
-            src = torch.from_numpy(np.ascontiguousarray(values[m:n], dtype=np.float64))
-            t[m:n].copy_(src)
-            ent[1] = n
-            self.version += 1
-        return t
+        return self.columns([(label, values)])[0]
 
     def order(self, label):
         """The label's ValueOrder (after ``column`` for that label)."""
-        return self.cols[label][2]
+        return ValueOrder(self.orders, self.slot[label])
+
+    def count(self, label):
+        """Values of the label uploaded so far."""
+        return int(self.n[self.slot[label]])
+
+    def view(self, label):
+        """The label's segment of the store."""
+        return self.views[self.slot[label]]
+
+    def addresses(self, slots):
+        """Device addresses of the slots' columns (int64 array)."""
+        return self.base + 8 * self.off[slots]
 
 
 def columns(hist, device):

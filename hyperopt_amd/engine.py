@@ -496,6 +496,18 @@ class Engine(object):
         recs = np.zeros(max(n, 1), dtype=N.LABEL_DTYPE)
         keep = [recs]
         id_addr = {}                              # the level's problems usually share one ids array
+        # room for every device-fitted label's merged order first: making room can
+        # re-lay out the History's order buffers, which would move addresses
+        # already taken (devhist)
+        grow = {}
+        for lp in problems:
+            ad = lp.post.above_dev
+            if ad is not None:
+                g = grow.setdefault(id(ad[3].group), (ad[3].group, [], []))
+                g[1].append(ad[3].slot)
+                g[2].append(ad[1])
+        for g, slots, ns in grow.values():
+            g.ensure(slots, ns)
         for i, lp in enumerate(problems):
             post = lp.post
             flags = (N.F_HAS_LOW if post.low is not None else 0) | (N.F_HAS_HIGH if post.high is not None else 0)

@@ -43,6 +43,7 @@ import time
 
 import numpy as np
 
+from . import _hostaddr
 from . import _native as N
 from . import devhist
 from . import dist as _dist
@@ -337,8 +338,9 @@ def _tree_labels(table, hist, engine=None, remote=()):
     Trials cache, or on the History itself without one, while the device
     columns and orders stay put (DeviceColumns.version).  Quantized labels
     carry no columns: tpe_suggest_tree sends them to the caller whenever they
-    need a fit.  Returns (records, keep-alive list, [(ValueOrder, n_obs) of
-    the device-fitted labels by label index], the records' address) or None.
+    need a fit.  Returns (records, keep-alive list, the device-fitted labels
+    as (label indices, order slots, n_obs, devhist order group) or None, the
+    records' address) or None.
     ``remote`` labels (another rank's, TPE_F_REMOTE) get no device column."""
     st = _tree_static(table)
     if st is None:
@@ -359,13 +361,12 @@ def _tree_labels(table, hist, engine=None, remote=()):
         # documents appended (FMinIter: one per suggest), no device-fitted label:
         # the records are updated in place — only the labels that gained
         # observations, through the field views (no structured-scalar writes)
-        if cache is not None and n_docs > memo[1] and not memo[3][2] and _tree_refill(memo[5], meta, hist):
+        if cache is not None and n_docs > memo[1] and memo[3][2] is None and _tree_refill(memo[5], meta, hist):
             holder.tree_memo = (table, n_docs, mkey, memo[3], dver, memo[5])
             return memo[3]
     arr = arr0.view(np.uint8).copy().view(arr0.dtype)      # (a byte copy: the record dtype copies field by field)
-    keep, devs = [], {}
+    keep, dix, dn, dlab, dx, dt, gix, gn = [], [], [], [], [], [], [], []
     for label, ix, fam in meta:
-        rec = arr[ix]
         otids, ovals = hist.obs[label]
         if fam == N.FAM_CATEGORICAL:
             cols = hist.cat_columns(label)
@@ -373,26 +374,24 @@ def _tree_labels(table, hist, engine=None, remote=()):
                 t, v = np.ascontiguousarray(otids, dtype=np.int64), np.ascontiguousarray(ovals, dtype=np.int64)
                 keep += [t, v]
                 cols = (t.ctypes.data, v.ctypes.data)
+            rec = arr[ix]
             rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
         elif fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
-            rec['n_obs'] = n = len(otids)
+            n = len(otids)
+            gix.append(ix)
+            gn.append(n)
             logc = fam == N.FAM_LOGGAUSS
             if dev_min is not None and n >= dev_min:
                 if ix in remote:                 # (another rank's label: never fitted here)
                     continue
                 # device fit of the above side: the device column (kernel coordinate)
-                # and its resident order; the host keeps the columns for the below side
-                x = np.ascontiguousarray(hist.log_values(label) if logc else ovals, dtype=np.float64)
-                t = np.ascontiguousarray(otids, dtype=np.int64)
-                keep += [t, x]
-                col = dc.column(label, x)
-                order = dc.order(label)
-                kin, iin, n_in, kout, iout = order.ptrs(n)
-                rec['tids'], rec['values'], rec['order'] = t.ctypes.data, x.ctypes.data, 0
-                rec['dev_obs'], rec['ord_key_in'], rec['ord_idx_in'], rec['n_ord_in'] = col.data_ptr(), kin, iin, n_in
-                rec['ord_key_out'], rec['ord_idx_out'] = kout, iout
-                keep.append(col)
-                devs[ix] = (order, n)
+                # and its resident order, filled in below for all such labels at once;
+                # the host keeps the columns for the below side
+                dix.append(ix)
+                dn.append(n)
+                dlab.append(label)
+                dx.append(np.ascontiguousarray(hist.log_values(label) if logc else ovals, dtype=np.float64))
+                dt.append(np.ascontiguousarray(otids, dtype=np.int64))
                 continue
             order = hist.value_order(label)
             cols = hist.native_columns(label, log=logc) if order is not None else None
@@ -405,10 +404,27 @@ def _tree_labels(table, hist, engine=None, remote=()):
                     o = np.ascontiguousarray(order, dtype=np.int64)
                     keep.append(o)
                     cols = cols[:2] + (o.ctypes.data,)
+            rec = arr[ix]
             rec['tids'], rec['values'], rec['order'] = cols
+    if gix:
+        arr['n_obs'][gix] = gn
+    devs = None
+    if dix:
+        # the new observations of every device-fitted label up in one scatter, room
+        # for their orders made, then the addresses (a re-layout moves them all)
+        slots = dc.upload(dlab, dx)
+        keep += [dt, dx, dc.store]
+        ixs = np.asarray(dix, dtype=np.int64)
+        ns = np.asarray(dn, dtype=np.int64)
+        kin, iin, n_in, kout, iout = dc.orders.ptrs_many(slots, ns)
+        for f, v in (('tids', _hostaddr.addresses(dt)), ('values', _hostaddr.addresses(dx)), ('order', 0),
+                     ('dev_obs', dc.addresses(slots)), ('ord_key_in', kin), ('ord_idx_in', iin), ('n_ord_in', n_in),
+                     ('ord_key_out', kout), ('ord_idx_out', iout)):
+            arr[f][ixs] = v
+        devs = (ixs, slots, ns, dc.orders)
     out = (arr, keep, devs, arr.ctypes.data)
     fv = None
-    if cache is not None and not devs and not keep:
+    if cache is not None and devs is None and not keep:
         fv = {f: arr[f] for f in ('tids', 'values', 'order', 'n_obs')}
         fv['n'] = arr['n_obs'].tolist()
     # (the version after the columns and orders above were looked up: that may move it)
@@ -629,10 +645,12 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
     # (a call on the same records, branch and host fits as the last committed one
     # finds every order already at its length: nothing to walk)
     done = getattr(table, '_committed', None)
-    if tl[2] and (host or done is None or done[0] is not tl[0] or done[1] is not table._used_list):
-        for ix, (order, n) in tl[2].items():
-            if used[ix] and ix not in host:
-                order.commit(n)
+    dv = tl[2]
+    if dv is not None and (host or done is None or done[0] is not tl[0] or done[1] is not table._used_list):
+        ok = np.asarray(used, dtype=bool)[dv[0]]
+        if host:
+            ok &= ~np.isin(dv[0], np.fromiter(host, dtype=np.int64, count=len(host)))
+        dv[3].commit_many(dv[1][ok], dv[2][ok])
         table._committed = None if host else (tl[0], table._used_list)
     if columns:
         return ChoiceColumns(table.labels, values.copy(), np.asarray(active, dtype=bool))

@@ -235,7 +235,7 @@ def test_suggest_tree_hands_quantized_labels_back():
         arr[q]['host_k'][sd] = len(cols[sd][0])
         arr[q]['host_w'][sd], arr[q]['host_mu'][sd], arr[q]['host_sigma'][sd] = [c.ctypes.data for c in cols[sd]]
     orig = tpe._tree_labels
-    tpe._tree_labels = lambda t, h, e=None: (arr, keep, {})
+    tpe._tree_labels = lambda t, h, e=None: (arr, keep, None)
     try:
         rc, need, path, need_fit = _tree_call(domain.table, hist, 1024)
     finally:
@@ -342,8 +342,15 @@ def test_suggest_tree_sizes_device_fits_without_gpu():
     hist = bench.soa_history(labels, 400, 1, lambda v: sum((x - 0.3) ** 2 for x in v.values()))
     table = bench.flat_uniform_table(labels)
     arr, keep, devs = tpe._tree_labels(table, hist, _Eng())[:3]
-    assert sorted(devs) == [0, 1, 2] and all(n == 400 for _, n in devs.values())
+    ixs, slots, ns, group = devs
+    assert sorted(ixs.tolist()) == [0, 1, 2] and ns.tolist() == [400] * 3
     assert np.all(arr['dev_obs'] != 0) and np.all(arr['n_ord_in'] == 0) and np.all(arr['ord_key_out'] != 0)
+    # one flat column store: the labels' columns are its segments, holding the values
+    dc = devhist.columns(hist, torch.device('cpu'))
+    for k, label in enumerate(labels):
+        seg = dc.view(label)
+        assert int(arr[table.by_label[label].index]['dev_obs']) == seg.data_ptr()
+        np.testing.assert_array_equal(seg[:400].numpy(), hist.obs[label][1])
     rc, need, path, need_fit = _tree_call(table, hist, 4096, fit_min=100, engine=_Eng())
     # (pruned above mixtures: without a device the sort-workspace query that
     # follows the sizing fails instead of returning TPE_E_SPACE)
@@ -351,7 +358,7 @@ def test_suggest_tree_sizes_device_fits_without_gpu():
     assert need.result == 3 and need.fit >= 3 * 400          # every label's fit scratch (all observations new)
     # the memo: the same records while nothing moved; a committed order moves them
     assert tpe._tree_labels(table, hist, _Eng())[0] is arr
-    devs[0][0].commit(400)
+    group.commit_many(slots[ixs == 0], ns[ixs == 0])
     arr2 = tpe._tree_labels(table, hist, _Eng())[0]
     assert arr2 is not arr and arr2[0]['n_ord_in'] == 400 and arr2[0]['ord_key_out'] == 0
     assert devhist.columns(hist, torch.device('cpu')).order('x0').n == 400

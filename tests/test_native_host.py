@@ -234,8 +234,13 @@ class _FakeColumn(object):
 class _FakeOrder(object):
     """Stand-in for a devhist.ValueOrder with ``n`` observations already sorted."""
 
+    class _Group(object):
+        def ensure(self, slots, n_obs):
+            pass
+
     def __init__(self, n):
         self.n = n
+        self.group, self.slot = self._Group(), 0
 
     def ptrs(self, n_obs):
         return (0xE0000000 if self.n else 0, 0xE1000000 if self.n else 0, self.n,

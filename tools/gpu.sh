@@ -16,6 +16,7 @@
 #   phases     tools/phase_prof.py per workload (PHASE_WL) under the kernel trace
 #   nativesplit native fits / tpe_suggest_tree / device stages of the headline suggest
 #   hostprof   cProfile of the headline suggest on the device
+#   app5       config 5 appending: cProfile + bench line (STEPS, CFG_STEPS)
 #   cfgprof    cProfile of one step of config CONFIG (default 5)
 #   pmcloop    PMC counter passes on tools/suggest_loop.py (the real suggest flow)
 #   apitrace   HIP API + kernel + copy trace of tools/suggest_loop.py -> timeline of the last suggests
@@ -100,6 +101,12 @@ for task in "$@"; do
             --steps ${CFG_STEPS:-5} --warmup 2 --no-cpu-baseline --no-quantized --no-appending
         grep '^{' $O/rehearse${c}_${TAG}.err > $O/rehearse${c}_${TAG}.json; cat $O/rehearse${c}_${TAG}.json
       done ;;
+    app5)
+      # config 5 appending: cProfile of its steps, then the bench line
+      step 300 $O/cfg5_app_prof_${TAG}.txt python tools/cfg5_app_prof.py ${STEPS:-8}
+      head -30 $O/cfg5_app_prof_${TAG}.txt
+      step 600 $O/cfg5app_${TAG}.err python bench.py --config 5 --appending --steps ${CFG_STEPS:-20} --warmup 2
+      grep '^{' $O/cfg5app_${TAG}.err > $O/cfg5app_${TAG}.json; cat $O/cfg5app_${TAG}.json ;;
     cfgprof)
       step 600 $O/cfgprof${CONFIG:-5}_${TAG}.txt python tools/config_prof.py ${CONFIG:-5} --steps ${STEPS:-5}
       head -45 $O/cfgprof${CONFIG:-5}_${TAG}.txt ;;
