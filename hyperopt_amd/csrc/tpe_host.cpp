@@ -331,6 +331,13 @@ struct PaTask { int32_t li, side; int64_t i0, i1, off; };
 
 // per-thread staging of tpe_host_pack_level, reused across calls (no
 // first-touch page faults on the large tables of a batched level)
+// A large tabulated continuous f32 side (no wide list or grid: its cells sum
+// every component) is filled in chunks on the worker threads, two passes:
+// terms (a and the unshifted c into scratch, the chunk's largest c), then rows
+// once the side's shift (the largest c of all chunks) is known.
+constexpr int64_t kFillChunk = 1024;
+struct ChunkTask { int32_t li, side; int64_t i0, i1; int64_t scr; };
+
 struct PackScratch {
   std::vector<float> comp32;
   std::vector<double> comp64, samp;
@@ -345,6 +352,9 @@ struct PackScratch {
   std::vector<int64_t> pa_off;          // acceptance terms of the large bounded sides
   std::vector<double> pa_terms;
   std::vector<PaTask> pa_tasks;
+  std::vector<char> chunked;            // chunked fills (ChunkTask)
+  std::vector<ChunkTask> ch_tasks;
+  std::vector<double> ch_a, ch_c, ch_max, side_ipa, side_shift;
 };
 
 // value range of a label's kernel coordinate (x, or ln x for log families)
@@ -451,6 +461,78 @@ void decide_table(const TabCtx& cx, int32_t li) {
   }
 }
 
+// the largest finite value of c[0, n) (-inf: none) — four lanes at a time in
+// GCC vector types, so that every clone vectorises it (the max of finite values
+// is exact in any order)
+inline __attribute__((always_inline)) double finite_max(const double* __restrict__ c, int64_t n) {
+  typedef double v4d __attribute__((vector_size(32)));
+  const v4d ninf = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, pinf = {INFINITY, INFINITY, INFINITY, INFINITY};
+  v4d m = ninf;
+  int64_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    v4d v;
+    memcpy(&v, c + i, sizeof(v));
+    v = (v > ninf) & (v < pinf) ? v : ninf;
+    m = v > m ? v : m;
+  }
+  double r = std::max(std::max(m[0], m[1]), std::max(m[2], m[3]));
+  for (; i < n; ++i) {
+    const double v = (c[i] > -INFINITY) & (c[i] < INFINITY) ? c[i] : -INFINITY;
+    r = v > r ? v : r;
+  }
+  return r;
+}
+
+// f32 component terms of a continuous side's components [0, n) (pointers
+// already offset): a = sqrt(log2e / 2) / max(sigma, EPS) and the unshifted
+// c = log2(w / (sigma sqrt(2 pi)) / p_accept) (the log family: no p_accept);
+// straight-line passes the compiler vectorises, the bit-level log2 for normal
+// positive ratios, libm for the rest.  Returns the largest finite c.
+inline __attribute__((always_inline)) double comp_terms_f32(const double* __restrict__ w, const double* __restrict__ sg,
+                                                            int64_t n, bool logf, double ipa, double* __restrict__ ap,
+                                                            double* __restrict__ cp) {
+  const double s2pi = sqrt(2 * M_PI), as = sqrt(0.5 * kLog2e);
+  // one division per component: 1 / max(sigma, EPS) (the rows are f32; the
+  // ratio's double rounding differs from w / (sigma sqrt(2 pi)) by an ulp)
+  {
+    const double cst = logf ? 1.0 / s2pi : ipa / s2pi;
+    int tiny = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const double se = sg[i] > kEPS ? sg[i] : kEPS;
+      const double inv = 1.0 / se;
+      tiny |= !(sg[i] > kEPS);
+      cp[i] = w[i] * inv * cst;
+      ap[i] = as * inv;
+    }
+    if (tiny && !logf)       // |sigma| < EPS: the reference divides by |sigma| itself
+      for (int64_t i = 0; i < n; ++i)
+        if (!(sg[i] > kEPS)) cp[i] = w[i] / (s2pi * fabs(sg[i])) * ipa;
+  }
+  int odd = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double r = cp[i];
+    odd |= !((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308));
+    cp[i] = log2_normal(r > 0 ? r : 1.0);
+  }
+  if (odd)
+    for (int64_t i = 0; i < n; ++i) {
+      const double r = w[i] / (logf ? ((sg[i] > kEPS ? sg[i] : kEPS) * s2pi) : (s2pi * fabs(sg[i]))) *
+                       (logf ? 1.0 : ipa);
+      if (!((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308))) cp[i] = log2(r);
+    }
+  return finite_max(cp, n);
+}
+
+// f32 component rows {mu_hi, mu_lo, a, c - shift} of components [0, n)
+inline __attribute__((always_inline)) void comp_rows_f32(const double* __restrict__ mu, const double* __restrict__ a,
+                                                         const double* __restrict__ c, int64_t n, double shift,
+                                                         float* __restrict__ r) {
+  for (int64_t i = 0; i < n; ++i, r += 4) {
+    const float hi = (float)mu[i];
+    r[0] = hi; r[1] = (float)(mu[i] - (double)hi); r[2] = (float)a[i]; r[3] = (float)(c[i] - shift);
+  }
+}
+
 // one label's sections of tpe_host_pack_level (sampler rows, component rows,
 // wide rows, pruning grid) at the offsets the packer assigned; labels are
 // independent, so the packer runs this on its worker threads.  (A function of
@@ -470,6 +552,7 @@ struct FillCtx {
   bool f64;
   const double* pa_terms;      // a large bounded side's acceptance terms (the packer's parallel pass)
   const int64_t* pa_off;       // [2 * label + side]: their offset in pa_terms, -1: none
+  const char* chunked;         // [2 * label + side]: rows filled by chunk tasks (ChunkTask)
 };
 
 // the acceptance mass of label li's side: the terms the parallel pass made, or p_accept
@@ -491,6 +574,16 @@ void pa_chunk(const PaCtx& cx, int t) {
 
 __attribute__((target_clones("avx512f", "avx2", "default")))
 void fill_label(const FillCtx& cx, int32_t li) {
+#ifdef TPE_PACK_TRACE
+  const auto t_fill0 = std::chrono::steady_clock::now();
+  struct Done {
+    std::chrono::steady_clock::time_point t0; int32_t li;
+    ~Done() {
+      fprintf(stderr, "fill_label %d %.1f us\n", li,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+  } done_{t_fill0, li};
+#endif
   const tpe_label_in* labels = cx.labels;
   const bool f64 = cx.f64;
   const int key_bits = cx.key_bits;
@@ -588,6 +681,10 @@ void fill_label(const FillCtx& cx, int32_t li) {
       }
     } else {
       const bool logf = L.family == TPE_FAM_LOGGAUSS;
+      if (cx.chunked[2 * (size_t)li + side]) {      // (its terms and rows: the chunk tasks; its base: the packer)
+        off = (int32_t)sc.c32[side]; len = (int32_t)k;
+        continue;
+      }
       std::vector<double> a((size_t)k), c((size_t)k);
       const double pa = logf ? 1.0 : side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high);
       double shift = -INFINITY;
@@ -598,57 +695,9 @@ void fill_label(const FillCtx& cx, int32_t li) {
           c[i] = log(arg) * kLog2e;
           a[i] = sqrt(0.5 * kLog2e) / se;
         }
+        shift = finite_max(c.data(), k);
       } else {
-        // f32 tables: straight-line passes the compiler vectorises, the bit-level
-        // log2 for normal positive arguments, libm for the rest
-        double* __restrict__ cp = c.data();
-        double* __restrict__ ap = a.data();
-        const double s2pi = sqrt(2 * M_PI), as = sqrt(0.5 * kLog2e), ipa = 1.0 / pa;
-        // one division per component: 1 / max(sigma, EPS) (the rows are f32; the
-        // ratio's double rounding differs from w / (sigma sqrt(2 pi)) by an ulp)
-        {
-          const double cst = logf ? 1.0 / s2pi : ipa / s2pi;
-          int tiny = 0;
-          for (int64_t i = 0; i < k; ++i) {
-            const double se = sg[i] > kEPS ? sg[i] : kEPS;
-            const double inv = 1.0 / se;
-            tiny |= !(sg[i] > kEPS);
-            cp[i] = w[i] * inv * cst;
-            ap[i] = as * inv;
-          }
-          if (tiny && !logf)       // |sigma| < EPS: the reference divides by |sigma| itself
-            for (int64_t i = 0; i < k; ++i)
-              if (!(sg[i] > kEPS)) cp[i] = w[i] / (s2pi * fabs(sg[i])) * ipa;
-        }
-        // normal positive ratios (the rule): one branch-free pass; libm for the rest
-        int odd = 0;
-        for (int64_t i = 0; i < k; ++i) {
-          const double r = cp[i];
-          odd |= !((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308));
-          cp[i] = log2_normal(r > 0 ? r : 1.0);
-        }
-        if (odd)
-          for (int64_t i = 0; i < k; ++i) {
-            const double r = w[i] / (logf ? ((sg[i] > kEPS ? sg[i] : kEPS) * s2pi) : (s2pi * fabs(sg[i]))) *
-                             (logf ? 1.0 : ipa);
-            if (!((r >= 2.2250738585072014e-308) & (r <= 1.7976931348623157e308))) cp[i] = log2(r);
-          }
-      }
-      {
-        // the largest finite c (four chains: vectorisable)
-        double m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        const double* __restrict__ cc = c.data();
-        int64_t i = 0;
-        for (; i + 4 <= k; i += 4)
-          for (int j = 0; j < 4; ++j) {
-            const double v = (cc[i + j] > -INFINITY) & (cc[i + j] < INFINITY) ? cc[i + j] : -INFINITY;
-            m4[j] = v > m4[j] ? v : m4[j];
-          }
-        for (; i < k; ++i) {
-          const double v = (cc[i] > -INFINITY) & (cc[i] < INFINITY) ? cc[i] : -INFINITY;
-          m4[0] = v > m4[0] ? v : m4[0];
-        }
-        shift = std::max(std::max(m4[0], m4[1]), std::max(m4[2], m4[3]));
+        shift = comp_terms_f32(w, sg, k, logf, 1.0 / pa, a.data(), c.data());
       }
       if (!std::isfinite(shift)) shift = 0;
       for (int64_t i = 0; i < k; ++i) c[i] -= shift;
@@ -744,6 +793,40 @@ void fill_label(const FillCtx& cx, int32_t li) {
       }
     }
   }
+}
+
+// the chunk tasks' two passes (ChunkTask; tpe_host_pack_level)
+struct ChunkCtx {
+  const tpe_label_in* labels;
+  const ChunkTask* tasks;
+  double* a;                   // scratch: each chunked side's a and unshifted c at ChunkTask.scr
+  double* c;
+  double* cmax;                // per task: the chunk's largest finite c
+  const double* ipa;           // [2 * label + side]: 1 / p_accept
+  const double* shift;         // [2 * label + side]: the side's shift (rows pass)
+  const LabelSec* sec;
+  float* comp32;
+};
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+void chunk_terms(const ChunkCtx& x, int t) {
+  const ChunkTask& q = x.tasks[t];
+  const tpe_label_in& L = x.labels[q.li];
+  const double* w = q.side ? L.above_w : L.below_w;
+  const double* sg = q.side ? L.above_sigma : L.below_sigma;
+  const size_t s = 2 * (size_t)q.li + q.side;
+  x.cmax[t] = comp_terms_f32(w + q.i0, sg + q.i0, q.i1 - q.i0, L.family == TPE_FAM_LOGGAUSS, x.ipa[s],
+                             x.a + q.scr + q.i0, x.c + q.scr + q.i0);
+}
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+void chunk_rows(const ChunkCtx& x, int t) {
+  const ChunkTask& q = x.tasks[t];
+  const tpe_label_in& L = x.labels[q.li];
+  const double* mu = q.side ? L.above_mu : L.below_mu;
+  const size_t s = 2 * (size_t)q.li + q.side;
+  comp_rows_f32(mu + q.i0, x.a + q.scr + q.i0, x.c + q.scr + q.i0, q.i1 - q.i0, x.shift[s],
+                x.comp32 + 4 * (size_t)(x.sec[q.li].c32[q.side] + q.i0));
 }
 
 }  // namespace
@@ -1198,15 +1281,84 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     tpe_pool::parallel_for((int)pa_tasks.size(), [](void* c, int i) { pa_chunk(*(const PaCtx*)c, i); }, (void*)&pcx);
   }
   PACK_MARK("accept");
+  // large tabulated continuous f32 sides: in chunks (ChunkTask), their
+  // acceptance mass first (from the parallel pass's terms)
+  auto& chunked = ps.chunked;
+  auto& ch_tasks = ps.ch_tasks;
+  auto& side_ipa = ps.side_ipa;
+  auto& side_shift = ps.side_shift;
+  chunked.assign(2 * (size_t)n_labels, 0);
+  ch_tasks.clear();
+  int64_t ch_total = 0;
+  if (!f64)
+    for (int32_t li = 0; li < n_labels; ++li) {
+      const tpe_label_in& L = labels[li];
+      if ((L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) || tmode[li] == TPE_TAB_NONE) continue;
+      for (int side = 0; side < 2 - dev_fit[li]; ++side) {
+        const int64_t k = side ? L.above_k : L.below_k;
+        if (k <= kFillChunk) continue;
+        chunked[2 * (size_t)li + side] = 1;
+        const int64_t nch = (k + kFillChunk - 1) / kFillChunk;
+        for (int64_t j = 0; j < nch; ++j)
+          ch_tasks.push_back(ChunkTask{li, side, k * j / nch, k * (j + 1) / nch, ch_total});
+        ch_total += k;
+      }
+    }
   const FillCtx fcx{labels, sec.data(), lab.data(), f_samp, f_comp64, f_comp32, f_grid,
-                    dev_fit.data(), tmode.data(), key_bits, f64, pa_terms.data(), pa_off.data()};
+                    dev_fit.data(), tmode.data(), key_bits, f64, pa_terms.data(), pa_off.data(), chunked.data()};
+  const int n_ch = (int)ch_tasks.size();
+  ChunkCtx ccx{labels, ch_tasks.data(), nullptr, nullptr, nullptr, nullptr, nullptr, sec.data(), f_comp32};
+  if (n_ch) {
+    ps.ch_a.resize((size_t)ch_total);
+    ps.ch_c.resize((size_t)ch_total);
+    ps.ch_max.resize((size_t)n_ch);
+    side_ipa.assign(2 * (size_t)n_labels, 1.0);
+    side_shift.assign(2 * (size_t)n_labels, 0.0);
+    for (int32_t li = 0; li < n_labels; ++li)
+      for (int side = 0; side < 2; ++side) {
+        const size_t q = 2 * (size_t)li + side;
+        const tpe_label_in& L = labels[li];
+        if (!chunked[q] || L.family == TPE_FAM_LOGGAUSS) continue;
+        const bool bounded = (L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) != 0;
+        side_ipa[q] = 1.0 / side_accept(fcx, li, side, side ? L.above_w : L.below_w, side ? L.above_mu : L.below_mu,
+                                        side ? L.above_sigma : L.below_sigma, side ? L.above_k : L.below_k, bounded,
+                                        L.low, L.high);
+      }
+    ccx.a = ps.ch_a.data(); ccx.c = ps.ch_c.data(); ccx.cmax = ps.ch_max.data();
+    ccx.ipa = side_ipa.data(); ccx.shift = side_shift.data();
+  }
   {
-    // (a few hundred components per label make a worker's hand-off worth it)
-    if (n_labels >= 2 && work_k >= 4096)
-      tpe_pool::parallel_for(n_labels, [](void* c, int i) { fill_label(*(const FillCtx*)c, (int32_t)i); },
-                             (void*)&fcx);
+    // the labels' fills and the chunks' terms, one task each (a few hundred
+    // components per label make a worker's hand-off worth it)
+    struct Both { const FillCtx* f; const ChunkCtx* c; int32_t n_labels; };
+    const Both both{&fcx, &ccx, n_labels};
+    auto task = [](void* v, int i) {
+      const Both& b = *(const Both*)v;
+      if (i < b.n_labels) fill_label(*b.f, (int32_t)i);
+      else chunk_terms(*b.c, i - b.n_labels);
+    };
+    const int n_tasks = n_labels + n_ch;
+    if (n_tasks >= 2 && work_k >= 4096) tpe_pool::parallel_for(n_tasks, task, (void*)&both);
     else
-      for (int32_t li = 0; li < n_labels; ++li) fill_label(fcx, li);
+      for (int i = 0; i < n_tasks; ++i) task((void*)&both, i);
+  }
+  if (n_ch) {
+    // each chunked side's shift (the largest finite c of its chunks) and base,
+    // then its rows
+    for (int t = 0; t < n_ch; ++t) {
+      const size_t q = 2 * (size_t)ch_tasks[t].li + ch_tasks[t].side;
+      side_shift[q] = ch_tasks[t].i0 == 0 ? ps.ch_max[t] : std::max(side_shift[q], ps.ch_max[t]);
+    }
+    for (int32_t li = 0; li < n_labels; ++li)
+      for (int side = 0; side < 2; ++side) {
+        const size_t q = 2 * (size_t)li + side;
+        if (!chunked[q]) continue;
+        if (!std::isfinite(side_shift[q])) side_shift[q] = 0;
+        (side ? lab[li].above_base : lab[li].below_base) = side_shift[q] * kLn2;
+      }
+    auto rows = [](void* v, int t) { chunk_rows(*(const ChunkCtx*)v, t); };
+    if (n_ch >= 2) tpe_pool::parallel_for(n_ch, rows, (void*)&ccx);
+    else rows((void*)&ccx, 0);
   }
   PACK_MARK("fill");
   // the device-fitted labels' problem fields (the fill cleared their rows)

@@ -502,7 +502,7 @@ def test_device_fit_batched_labels_and_suggest():
         engine.device_fit_min = 1000
         got = tpe.suggest_choices(table, hist, [N, N + 1], 5, n_EI_candidates=4096)
         dc = hist.dev[str(engine.device)]
-        assert set(dc.cols) == {'a', 'b', 'c'} and all(v[1] == N for v in dc.cols.values())
+        assert set(dc.slot) == {'a', 'b', 'c'} and all(dc.count(k) == N for k in dc.slot)
         engine.device_fit_min = 10 ** 9
         ref = tpe.suggest_choices(table, hist, [N, N + 1], 5, n_EI_candidates=4096)
     finally:

@@ -107,6 +107,14 @@ for task in "$@"; do
       head -30 $O/cfg5_app_prof_${TAG}.txt
       step 600 $O/cfg5app_${TAG}.err python bench.py --config 5 --appending --steps ${CFG_STEPS:-20} --warmup 2
       grep '^{' $O/cfg5app_${TAG}.err > $O/cfg5app_${TAG}.json; cat $O/cfg5app_${TAG}.json ;;
+    packtime)
+      # the headline level's packer sections on the box's host CPU (no GPU; the
+      # TPE_PACK_TRACE library from tools/build_pack_trace.sh)
+      for t in ${PACK_THREADS:-16}; do
+        TPE_HOST_THREADS=$t TPE_PACK_LIB=$PWD/hyperopt_amd/libtpe_host_ptrace.so step 120 $O/packtime_${TAG}_$t.txt \
+            python tools/pack_time3.py 400
+        python3 tools/pack_sections.py $O/packtime_${TAG}_$t.txt | tee -a $O/packtime_${TAG}_$t.txt
+      done ;;
     cfgprof)
       step 600 $O/cfgprof${CONFIG:-5}_${TAG}.txt python tools/config_prof.py ${CONFIG:-5} --steps ${STEPS:-5}
       head -45 $O/cfgprof${CONFIG:-5}_${TAG}.txt ;;
