@@ -336,6 +336,7 @@ struct PaTask { int32_t li, side; int64_t i0, i1, off; };
 // terms (a and the unshifted c into scratch, the chunk's largest c), then rows
 // once the side's shift (the largest c of all chunks) is known.
 constexpr int64_t kFillChunk = 1024;
+constexpr int64_t kFillChunkMinLevel = 16384;   // the level's chunkable components, at least
 struct ChunkTask { int32_t li, side; int64_t i0, i1; int64_t scr; };
 
 struct PackScratch {
@@ -1290,7 +1291,18 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   chunked.assign(2 * (size_t)n_labels, 0);
   ch_tasks.clear();
   int64_t ch_total = 0;
-  if (!f64)
+  // (only a level with many such components: a chunked side costs a second
+  // hand-off to the workers, more than it saves on the headline's few thousand)
+  int64_t chunkable = 0;
+  for (int32_t li = 0; li < n_labels && !f64; ++li) {
+    const tpe_label_in& L = labels[li];
+    if ((L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) || tmode[li] == TPE_TAB_NONE) continue;
+    for (int side = 0; side < 2 - dev_fit[li]; ++side) {
+      const int64_t k = side ? L.above_k : L.below_k;
+      if (k > kFillChunk) chunkable += k;
+    }
+  }
+  if (chunkable >= kFillChunkMinLevel)
     for (int32_t li = 0; li < n_labels; ++li) {
       const tpe_label_in& L = labels[li];
       if ((L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) || tmode[li] == TPE_TAB_NONE) continue;

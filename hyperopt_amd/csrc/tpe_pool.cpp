@@ -1,11 +1,17 @@
 // tpe_pool.cpp — resident worker threads of the host runtime (tpe_pool.h).
 //
-// A suggest's host work is a handful of per-label jobs of 5-30 us each, so the
-// pool is built for latency: workers spin on a generation word for a while
+// A suggest's host work is a handful of per-label jobs of 1-30 us each, so the
+// pool is built for dispatch latency: workers spin on a control word for a while
 // after their last job (a back-to-back suggest loop finds them awake), then
-// sleep on a condition variable.  Jobs are claimed by compare-and-swap on a
-// (generation << 32 | next index) word, so a worker that wakes late can never
-// run a job of a generation it did not read the job function of.
+// sleep on a condition variable.  A dispatch touches few shared cache lines:
+// the caller publishes the job and, in the same 64-bit control word, its
+// generation and the set of PARTICIPANTS — itself and the workers that are
+// awake (spinning), at most one per job.  Participant r runs job r straight
+// away (no claim), the jobs past the participants are claimed from a counter
+// with fetch_add, and each participant reports completion in its own cache
+// line, which is all the caller waits on.  A generation cannot end before
+// every participant has reported, so no worker ever runs a job of a
+// generation it was not given.
 #include "tpe_pool.h"
 
 #include <pthread.h>
@@ -24,73 +30,86 @@
 
 namespace {
 
-constexpr int kMaxThreads = 16;
+constexpr int kMaxThreads = 16;          // caller + 15 workers (participant masks: bits 1..15)
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
+
+struct alignas(64) Slot {
+  std::atomic<uint32_t> done{0};         // the last generation this worker finished as a participant
+  std::atomic<int> awake{0};             // spinning (1) or about to sleep / asleep (0)
+};
 
 struct Pool {
   std::mutex busy;                          // held by the dispatching caller
   std::mutex m;                             // sleep / wake
   std::condition_variable cv;
-  std::atomic<uint64_t> next{0};            // generation << 32 | next job index
-  std::atomic<int> n{0};
-  std::atomic<void (*)(void*, int)> fn{nullptr};
-  std::atomic<void*> ctx{nullptr};
-  std::atomic<uint32_t> stamp{0};           // generation whose fn / ctx / n are written (0: being written)
-  std::atomic<int> left{0};                 // jobs of the current generation not yet returned
-  std::atomic<int> sleepers{0};
+  // the job and its control word share one cache line: a worker that sees the
+  // new generation has the job's fields with it
+  alignas(64) std::atomic<uint64_t> ctl{0}; // generation << 32 | participant mask (bit w: worker w)
+  void (*fn)(void*, int) = nullptr;
+  void* ctx = nullptr;
+  int n = 0;
+  int n_part = 0;                           // participants, the caller included
+  alignas(64) std::atomic<int> next{0};     // the next job to claim (past the participants' first jobs)
+  alignas(64) std::atomic<int> sleepers{0};
   std::atomic<bool> stop{false};
   std::atomic<bool> retired{false};         // replaced by tpe_host_threads: dispatch nothing more to it
   std::atomic<int> refs{1};                 // holders: g_pool's slot + every get_pool caller not yet done
   uint32_t gen = 0;                         // dispatcher's generation counter
+  int n_workers = 0;
   int64_t spin_ns = 200000;
+  Slot slot[kMaxThreads];
   std::vector<std::thread> th;
 };
 
-// claim and run jobs of generation `g` until none is left
-void run_jobs(Pool* p, uint32_t g) {
-  // (seqlock: the job fields are g's only if g's stamp is there before and after)
-  if (p->stamp.load(std::memory_order_acquire) != g) return;
-  void (*fn)(void*, int) = p->fn.load(std::memory_order_relaxed);
-  void* ctx = p->ctx.load(std::memory_order_relaxed);
-  const int n = p->n.load(std::memory_order_relaxed);
-  std::atomic_thread_fence(std::memory_order_acquire);
-  if (p->stamp.load(std::memory_order_relaxed) != g) return;
-  uint64_t v = p->next.load(std::memory_order_acquire);
+// participant `rank` of the current generation: its own job, then claimed ones
+void run_jobs(Pool* p, int rank) {
+  if (rank < p->n) p->fn(p->ctx, rank);
+  if (p->n <= p->n_part) return;            // (one job each: no claims)
   for (;;) {
-    if ((uint32_t)(v >> 32) != g || (int)(uint32_t)v >= n) return;
-    if (!p->next.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
-    fn(ctx, (int)(uint32_t)v);
-    p->left.fetch_sub(1, std::memory_order_acq_rel);
-    v = p->next.load(std::memory_order_acquire);
+    const int i = p->next.fetch_add(1, std::memory_order_relaxed);
+    if (i >= p->n) return;
+    p->fn(p->ctx, i);
   }
 }
 
-void worker(Pool* p) {
-  uint32_t seen = (uint32_t)(p->next.load() >> 32);
+void worker(Pool* p, int id) {
+  Slot& me = p->slot[id];
+  uint32_t seen = (uint32_t)(p->ctl.load() >> 32);
   for (;;) {
     // spin for a while, then sleep until the generation moves
+    me.awake.store(1);
     const auto t0 = std::chrono::steady_clock::now();
-    uint32_t g = seen;
+    uint64_t c = 0;
     int k = 0;
     while (!p->stop.load(std::memory_order_relaxed)) {
-      g = (uint32_t)(p->next.load(std::memory_order_acquire) >> 32);
-      if (g != seen) break;
+      c = p->ctl.load(std::memory_order_acquire);
+      if ((uint32_t)(c >> 32) != seen) break;
       cpu_relax();
       if (++k == 256) {
         k = 0;
         if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
             p->spin_ns) {
+          me.awake.store(0);                // (seq_cst: before the generation check under the lock)
           std::unique_lock<std::mutex> lk(p->m);
           p->sleepers.fetch_add(1);
-          while (!p->stop.load() && (uint32_t)(p->next.load() >> 32) == seen) p->cv.wait(lk);
+          while (!p->stop.load() && (uint32_t)(p->ctl.load() >> 32) == seen) p->cv.wait(lk);
           p->sleepers.fetch_sub(1);
+          lk.unlock();
+          me.awake.store(1);
         }
       }
     }
     if (p->stop.load()) return;
+    const uint32_t g = (uint32_t)(c >> 32);
+    const uint32_t mask = (uint32_t)c;
     seen = g;
-    run_jobs(p, g);
+    if (!(mask >> id & 1)) continue;        // not a participant of g
+    // (the job fields were written before the control word; they stay until
+    // every participant has reported)
+    const int rank = 1 + __builtin_popcount(mask & ((1u << id) - 1));
+    run_jobs(p, rank);
+    me.done.store(g, std::memory_order_release);
   }
 }
 
@@ -152,7 +171,8 @@ Pool* get_pool() {
   if (!g_pool) {
     Pool* p = new Pool();
     p->spin_ns = (int64_t)std::max(0, env_int("TPE_POOL_SPIN_US", 200)) * 1000;
-    for (int i = 0; i < t - 1; ++i) p->th.emplace_back(worker, p);
+    p->n_workers = t - 1;
+    for (int i = 1; i < t; ++i) p->th.emplace_back(worker, p, i);
     g_pool = p;
   }
   g_pool->refs.fetch_add(1, std::memory_order_relaxed);     // (the caller's; release() when done)
@@ -182,21 +202,26 @@ void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
     return;
   }
   uint32_t g = ++p->gen;
-  if (g == 0) g = p->gen = 1;                       // (0 marks a job being written)
-  p->stamp.store(0, std::memory_order_relaxed);
-  std::atomic_thread_fence(std::memory_order_release);
-  p->fn.store(fn, std::memory_order_relaxed);
-  p->ctx.store(ctx, std::memory_order_relaxed);
-  p->n.store(n, std::memory_order_relaxed);
-  p->left.store(n, std::memory_order_relaxed);
-  p->stamp.store(g, std::memory_order_release);
-  p->next.store((uint64_t)g << 32);                 // publishes the job (seq_cst)
-  if (p->sleepers.load()) {
+  if (g == 0) g = p->gen = 1;                       // (0: no generation yet)
+  // participants: the caller and up to n - 1 awake workers
+  uint32_t mask = 0;
+  int part = 1;
+  for (int w = 1; w <= p->n_workers && part < n; ++w)
+    if (p->slot[w].awake.load(std::memory_order_relaxed)) { mask |= 1u << w; ++part; }
+  p->fn = fn;
+  p->ctx = ctx;
+  p->n = n;
+  p->n_part = part;
+  p->next.store(part, std::memory_order_relaxed);
+  p->ctl.store((uint64_t)g << 32 | mask);           // publishes the job (seq_cst)
+  if (p->sleepers.load()) {                         // (a participant may have gone to sleep since)
     { std::lock_guard<std::mutex> lk(p->m); }
     p->cv.notify_all();
   }
-  run_jobs(p, g);
-  while (p->left.load(std::memory_order_acquire) > 0) cpu_relax();
+  run_jobs(p, 0);
+  for (int w = 1; w <= p->n_workers; ++w)
+    if (mask >> w & 1)
+      while (p->slot[w].done.load(std::memory_order_acquire) != g) cpu_relax();
   own.unlock();
   release(held);
 }

@@ -43,7 +43,6 @@ import time
 
 import numpy as np
 
-from . import _hostaddr
 from . import _native as N
 from . import devhist
 from . import dist as _dist
@@ -51,6 +50,10 @@ from . import history as _history
 from . import rand
 from . import replay
 from .engine import LevelProblem, get_engine
+try:
+    from . import _hostaddr          # (csrc/hostaddr.c, built with the library: hyperopt_amd.build)
+except ImportError:                  # pragma: no cover - the package is importable before its build
+    _hostaddr = None
 from .parzen import _FAMILY, DEFAULT_LF, DEVICE_FIT_FAMILIES, cat_split, fit_coord, fit_posterior, fit_split
 
 logger = logging.getLogger(__name__)
@@ -417,6 +420,8 @@ def _tree_labels(table, hist, engine=None, remote=()):
         ixs = np.asarray(dix, dtype=np.int64)
         ns = np.asarray(dn, dtype=np.int64)
         kin, iin, n_in, kout, iout = dc.orders.ptrs_many(slots, ns)
+        if _hostaddr is None:
+            raise N.NativeUnavailable('hyperopt_amd._hostaddr is not built (python -m hyperopt_amd.build)')
         for f, v in (('tids', _hostaddr.addresses(dt)), ('values', _hostaddr.addresses(dx)), ('order', 0),
                      ('dev_obs', dc.addresses(slots)), ('ord_key_in', kin), ('ord_idx_in', iin), ('n_ord_in', n_in),
                      ('ord_key_out', kout), ('ord_idx_out', iout)):

@@ -140,8 +140,10 @@ for task in "$@"; do
       for v in ${LIBS:-default}; do
         if [ "$v" = default ]; then lib=$PWD/hyperopt_amd/libtpe_hip.so; else lib=$PWD/hyperopt_amd/libtpe_hip_$v.so; fi
         step 300 $O/stage_${TAG}_$v.txt env TPE_HIP_LIB=$lib python tools/stage_bench.py ${REP:-20}
-        step 300 $O/bench_${TAG}_$v.err env TPE_HIP_LIB=$lib python bench.py --no-cpu-baseline --no-quantized --steps 100
+        step 300 $O/bench_${TAG}_$v.err env TPE_HIP_LIB=$lib python bench.py --no-cpu-baseline --no-quantized --no-config4 --steps ${AB_STEPS:-200}
         echo "$v: $(grep -o '"p50_suggest_ms": [0-9.]*\|"stage_ms": {[^}]*}' $O/bench_${TAG}_$v.err | tr '\n' ' ')"
+        step 120 $O/phab_${TAG}_$v.txt env TPE_HIP_LIB=$lib python tools/phase_prof.py svm 300
+        grep "p50\|phases" $O/phab_${TAG}_$v.txt
       done ;;
     pmcloop)
       # counters of the suggest flow itself (cold kernels between host phases)
