@@ -11,7 +11,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 20
+ABI_VERSION = 21
+FIT_DELTA_MAX = 64             # TPE_FIT_DELTA_MAX: new observations read as a delta (no merge)
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)
@@ -89,7 +90,8 @@ class Batch(ctypes.Structure):
         ('below_idx', ctypes.c_void_p), ('fit_seg', ctypes.c_void_p), ('fit_total', ctypes.c_int64),
         ('fit_keys', ctypes.c_void_p), ('fit_keys_sorted', ctypes.c_void_p),
         ('fit_vals', ctypes.c_void_p), ('fit_vals_sorted', ctypes.c_void_p),
-        ('fit_max_new', ctypes.c_int64), ('fit_max_obs', ctypes.c_int64),
+        ('fit_max_new', ctypes.c_int64), ('fit_max_obs', ctypes.c_int64), ('fit_max_merge', ctypes.c_int64),
+        ('fit_n_delta', ctypes.c_int64),
         ('draw_pref', ctypes.c_void_p), ('draw_blocks', ctypes.c_int64), ('n_sorted', ctypes.c_int32),
         ('tab_fast', ctypes.c_int32), ('pool_best', ctypes.c_void_p),
         ('tab_jobs', ctypes.c_void_p), ('n_tab_jobs', ctypes.c_int32), ('tab_blocks', ctypes.c_int32),
@@ -146,7 +148,7 @@ class PackInfo(ctypes.Structure):
         ('n_fit', ctypes.c_int32), ('fgt_max_boxes', ctypes.c_int32), ('fit_total', ctypes.c_int64),
         ('sort_count', ctypes.c_int64),
         ('off_fin_tiles', ctypes.c_int64), ('n_fin_tiles', ctypes.c_int64), ('fit_max_new', ctypes.c_int64),
-        ('fit_max_obs', ctypes.c_int64),
+        ('fit_max_obs', ctypes.c_int64), ('fit_max_merge', ctypes.c_int64), ('fit_n_delta', ctypes.c_int64),
         ('n_sorted', ctypes.c_int64), ('draw_blocks', ctypes.c_int64), ('n_pooled', ctypes.c_int64),
         ('off_tab_jobs', ctypes.c_int64), ('n_tab_jobs', ctypes.c_int64), ('tab_blocks', ctypes.c_int64),
         ('tab_units', ctypes.c_int64),

@@ -9,11 +9,16 @@
 #include <Python.h>
 #define NPY_NO_DEPRECATED_API NPY_2_0_API_VERSION
 #include <numpy/arrayobject.h>
+#include <string.h>
 
-/* addresses(seq) -> int64 array of the items' data addresses (each item a
- * C-contiguous numpy array; anything else raises TypeError). */
-static PyObject *addresses(PyObject *self, PyObject *arg) {
+/* addresses(seq[, typenum]) -> int64 array of the items' data addresses (each
+ * item a C-contiguous numpy array — of dtype typenum when given; anything else
+ * raises TypeError, which callers take as "convert first"). */
+static PyObject *addresses(PyObject *self, PyObject *args) {
   (void)self;
+  PyObject *arg;
+  int typenum = -1;
+  if (!PyArg_ParseTuple(args, "O|i", &arg, &typenum)) return NULL;
   PyObject *seq = PySequence_Fast(arg, "addresses() takes a sequence of numpy arrays");
   if (!seq) return NULL;
   Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
@@ -24,8 +29,9 @@ static PyObject *addresses(PyObject *self, PyObject *arg) {
   PyObject **items = PySequence_Fast_ITEMS(seq);
   for (Py_ssize_t i = 0; i < n; ++i) {
     PyObject *a = items[i];
-    if (!PyArray_Check(a) || !PyArray_IS_C_CONTIGUOUS((PyArrayObject *)a)) {
-      PyErr_Format(PyExc_TypeError, "item %zd is not a C-contiguous numpy array", i);
+    if (!PyArray_Check(a) || !PyArray_IS_C_CONTIGUOUS((PyArrayObject *)a) ||
+        (typenum >= 0 && !PyArray_EquivTypenums(PyArray_TYPE((PyArrayObject *)a), typenum))) {
+      PyErr_Format(PyExc_TypeError, "item %zd is not a C-contiguous numpy array of the type asked", i);
       Py_DECREF(out);
       Py_DECREF(seq);
       return NULL;
@@ -36,8 +42,60 @@ static PyObject *addresses(PyObject *self, PyObject *arg) {
   return out;
 }
 
+/* tails(seq, start, stop) -> float64 array: seq[i][start[i]:stop[i]] for every
+ * i, concatenated (each item a 1-D C-contiguous float64 array of at least
+ * stop[i] values; start, stop int64 arrays of len(seq)). */
+static PyObject *tails(PyObject *self, PyObject *args) {
+  (void)self;
+  PyObject *arg, *a0, *a1;
+  if (!PyArg_ParseTuple(args, "OOO", &arg, &a0, &a1)) return NULL;
+  PyObject *seq = PySequence_Fast(arg, "tails() takes a sequence of numpy arrays");
+  if (!seq) return NULL;
+  PyArrayObject *st = (PyArrayObject *)PyArray_FROMANY(a0, NPY_INT64, 1, 1, NPY_ARRAY_IN_ARRAY);
+  PyArrayObject *sp = st ? (PyArrayObject *)PyArray_FROMANY(a1, NPY_INT64, 1, 1, NPY_ARRAY_IN_ARRAY) : NULL;
+  PyObject *out = NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  if (!sp) goto done;
+  if (PyArray_DIM(st, 0) != n || PyArray_DIM(sp, 0) != n) {
+    PyErr_SetString(PyExc_ValueError, "tails(): start / stop length");
+    goto done;
+  }
+  {
+    const npy_int64 *b = (const npy_int64 *)PyArray_DATA(st), *e = (const npy_int64 *)PyArray_DATA(sp);
+    PyObject **items = PySequence_Fast_ITEMS(seq);
+    npy_intp tot = 0;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject *a = items[i];
+      if (!PyArray_Check(a) || PyArray_NDIM((PyArrayObject *)a) != 1 ||
+          !PyArray_IS_C_CONTIGUOUS((PyArrayObject *)a) || PyArray_TYPE((PyArrayObject *)a) != NPY_FLOAT64 ||
+          b[i] < 0 || e[i] < b[i] || e[i] > PyArray_DIM((PyArrayObject *)a, 0)) {
+        PyErr_Format(PyExc_ValueError, "tails(): item %zd is not a float64 column holding [start, stop)", i);
+        goto done;
+      }
+      tot += (npy_intp)(e[i] - b[i]);
+    }
+    npy_intp dims[1] = {tot};
+    out = PyArray_SimpleNew(1, dims, NPY_FLOAT64);
+    if (!out) goto done;
+    double *o = (double *)PyArray_DATA((PyArrayObject *)out);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      const npy_int64 k = e[i] - b[i];
+      if (k == 1) *o = ((const double *)PyArray_DATA((PyArrayObject *)items[i]))[b[i]];
+      else if (k > 1) memcpy(o, (const double *)PyArray_DATA((PyArrayObject *)items[i]) + b[i], (size_t)k * sizeof(double));
+      o += k;
+    }
+  }
+done:
+  Py_XDECREF(st);
+  Py_XDECREF(sp);
+  Py_DECREF(seq);
+  return out;
+}
+
 static PyMethodDef methods[] = {
-    {"addresses", addresses, METH_O, "int64 array of the data addresses of a sequence of C-contiguous numpy arrays"},
+    {"addresses", addresses, METH_VARARGS,
+     "int64 array of the data addresses of a sequence of C-contiguous numpy arrays (of dtype typenum)"},
+    {"tails", tails, METH_VARARGS, "float64 concatenation of seq[i][start[i]:stop[i]]"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_hostaddr", NULL, -1, methods,

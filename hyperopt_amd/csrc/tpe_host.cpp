@@ -1040,7 +1040,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
           (L.n_below > 0 && !L.below_idx) || L.n_obs - L.n_below + 1 != L.above_k || L.above_k <= kPruneMinK ||
           L.n_obs >= ((int64_t)1 << 31) || L.n_ord_in < 0 || L.n_ord_in > L.n_obs ||
           (L.n_ord_in > 0 && (!L.ord_key_in || !L.ord_idx_in)) ||
-          (L.n_ord_in < L.n_obs && (!L.ord_key_out || !L.ord_idx_out)))
+          (L.n_ord_in < L.n_obs && (!L.ord_key_out || !L.ord_idx_out) &&
+           !(L.n_ord_in > 0 && L.n_obs - L.n_ord_in <= TPE_FIT_DELTA_MAX && !L.ord_key_out && !L.ord_idx_out)))
         return TPE_E_ARG;
       dev_fit[li] = 1;
     }
@@ -1143,7 +1144,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       if (dev_fit[li]) { ++nf; nb += std::max<int32_t>(labels[li].n_below, 0); }
     fit.reserve((size_t)nf); below_idx.reserve((size_t)nb + 1); fit_seg.reserve((size_t)nf + 1);
   }
-  int64_t dev_rows = 0, dev_grid = 0, fit_max_new = 0, fit_max_obs = 0;
+  int64_t dev_rows = 0, dev_grid = 0, fit_max_new = 0, fit_max_obs = 0, fit_max_merge = 0, fit_n_delta = 0;
   {
     int64_t r = 0;
     for (int32_t li = 0; li < n_labels; ++li) {
@@ -1172,8 +1173,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         // scratch segment: the compacted above order, the new observations' merge
         // passes and the below positions all fit in it
         const int64_t n_new = L.n_obs - L.n_ord_in;
-        fit_seg.push_back(fit_seg.back() + std::max<int64_t>(std::max<int64_t>(K - 1, n_new), L.n_below));
+        fit_seg.push_back(fit_seg.back() + std::max<int64_t>(std::max<int64_t>(K - 1, n_new),
+                                                             std::max<int64_t>(L.n_below, 64 + 2 * TPE_FIT_DELTA_MAX)));
         fit_max_new = std::max(fit_max_new, n_new);
+        if (L.ord_key_out) fit_max_merge = std::max(fit_max_merge, n_new);
+        else fit_n_delta += n_new > 0;          // (delta mode)
         fit_max_obs = std::max<int64_t>(fit_max_obs, L.n_obs);
         dev_rows += K + kPruneWide;
         dev_grid += G + 1;
@@ -1246,7 +1250,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       e.off_fit = off_lead[L_FIT]; e.off_below_idx = off_lead[L_BIDX]; e.off_fit_seg = off_lead[L_FSEG];
       e.off_grid = off_lead[L_GRID]; e.off_comp32 = off_lead[L_C32]; e.off_patch = off_lead[L_PATCH];
       e.n_fit = (int32_t)fit.size(); e.fit_total = fit_seg.back();
-      e.fit_max_new = fit_max_new; e.fit_max_obs = fit_max_obs; e.n_problems = P;
+      e.fit_max_new = fit_max_new; e.fit_max_obs = fit_max_obs; e.fit_max_merge = fit_max_merge;
+      e.fit_n_delta = fit_n_delta; e.n_problems = P;
       e.up_off[0] = 0; e.up_len[0] = off_lead[L_FSEG] + len_lead[L_FSEG]; e.n_up = 1;
       e.blob_bytes = off_lead[L_PATCH] + len_lead[L_PATCH];     // (the device bytes the fit touches)
       g_pack_hook.fn(g_pack_hook.ctx, &e);
@@ -1683,6 +1688,8 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
   info->off_work = off[0];
   info->off_fin_tiles = off[1]; info->n_fin_tiles = n_fin;
   info->fit_max_new = fit_max_new;
+  info->fit_max_merge = fit_max_merge;
+  info->fit_n_delta = fit_n_delta;
   info->fit_max_obs = fit_max_obs;
   info->off_tab_jobs = off[2]; info->n_tab_jobs = n_tab_jobs; info->tab_blocks = tab_blocks;
   info->tab_units = tab_units;

@@ -3821,6 +3821,7 @@ constexpr int kPruneWide = 16;
 constexpr double kAScale = 0.84932180028801907;   // sqrt(0.5 * log2(e))
 
 // ---- resident value order (include/tpe_hip.h "Device value order") ----
+constexpr int kFitMaxBelow_ = 64;               // (kFitMaxBelow, below)
 // The order of the reference's argsort of the above observations (tpe.py:427),
 // stable: t ascending, NaN last (np.argsort), equal t by position in tid order.
 __device__ __forceinline__ bool ord_lt(double ka, uint32_t ia, double kb, uint32_t ib) {
@@ -3835,13 +3836,35 @@ __device__ __forceinline__ bool ord_lt(double ka, uint32_t ia, double kb, uint32
 // families, tpe.py:523 / :556), so the order and the rows see numpy's values
 __device__ __forceinline__ double fit_coord(const tpe_fit_job& j, int64_t i) { return j.obs[i]; }
 
+// Delta mode (include/tpe_hip.h "Device value order"): a job whose few new
+// observations (at most kFitMaxDelta) are not merged into its resident order
+// (no ord_key_out) reads the order and its sorted new observations as one
+// VIRTUAL order: new observation k (k-th smallest) at position dp[k] = its rank
+// among the resident ones + k, resident entry e at e + #{k : dp[k] <= e + k}.
+// The merge — a pass over the whole order for a handful of values — waits
+// until the new ones outgrow the delta.  Its arrays in the fit scratch: keys in
+// fit_keys_sorted[seg_off ..], indices and positions in fit_vals_sorted after
+// the below positions (adj).
+constexpr int kFitMaxDelta = TPE_FIT_DELTA_MAX;
+__device__ __forceinline__ bool fit_delta(const tpe_fit_job& j) { return j.n_ord_in < j.n_obs && !j.ord_key_out; }
+__device__ __forceinline__ double* delta_keys(const tpe_fit_job& j, double* fks) { return fks + j.seg_off; }
+__device__ __forceinline__ uint32_t* delta_idx(const tpe_fit_job& j, uint32_t* fvs) {
+  return fvs + j.seg_off + kFitMaxBelow_;
+}
+__device__ __forceinline__ uint32_t* delta_pos(const tpe_fit_job& j, uint32_t* fvs) {
+  return fvs + j.seg_off + kFitMaxBelow_ + kFitMaxDelta;
+}
+
 // chunks: the new observations obs[n_ord_in ..] of each job, kOrdChunk at a
 // time, sorted in LDS by a bitonic network on (t, i) -> fit scratch buffer 0
+// (delta mode: -> the delta arrays, with each one's virtual position)
 constexpr int kOrdChunk = 8192;
 constexpr int kOrdChunkThreads = 1024;
 __global__ __launch_bounds__(kOrdChunkThreads) void k_ord_chunks(const tpe_fit_job* __restrict__ J,
                                                                  double* __restrict__ keys,
-                                                                 uint32_t* __restrict__ idx) {
+                                                                 uint32_t* __restrict__ idx,
+                                                                 double* __restrict__ dkeys,
+                                                                 uint32_t* __restrict__ dvals) {
   const tpe_fit_job& j = J[blockIdx.y];
   const int64_t m = j.n_ord_in, k = j.n_obs - m, c0 = (int64_t)blockIdx.x * kOrdChunk;
   if (c0 >= k) return;
@@ -3869,6 +3892,23 @@ __global__ __launch_bounds__(kOrdChunkThreads) void k_ord_chunks(const tpe_fit_j
       __syncthreads();
     }
   }
+  if (fit_delta(j)) {                               // (k <= kFitMaxDelta: one chunk)
+    const int i = threadIdx.x;
+    if (i < n) {
+      const double t = sk[i];
+      const uint32_t v = sv[i];
+      int64_t lo = 0, hi = m;                       // resident entries before it
+      while (lo < hi) {
+        const int64_t md = (lo + hi) >> 1;
+        if (ord_lt(j.ord_key_in[md], j.ord_idx_in[md], t, v)) lo = md + 1;
+        else hi = md;
+      }
+      delta_keys(j, dkeys)[i] = t;
+      delta_idx(j, dvals)[i] = v;
+      delta_pos(j, dvals)[i] = (uint32_t)(lo + i);
+    }
+    return;
+  }
   double* __restrict__ ok = keys + j.seg_off + c0;
   uint32_t* __restrict__ ov = idx + j.seg_off + c0;
   for (int i = threadIdx.x; i < n; i += kOrdChunkThreads) { ok[i] = sk[i]; ov[i] = sv[i]; }
@@ -3893,7 +3933,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_ord_merge(const tpe_fit_job* 
                                                              int64_t L) {
   const tpe_fit_job& j = J[blockIdx.y];
   const int64_t k = j.n_obs - j.n_ord_in, t0 = (int64_t)blockIdx.x * kMergeTile;
-  if (k <= 0) return;
+  if (k <= 0 || fit_delta(j)) return;
   const double *ak, *bk;
   const uint32_t *av, *bv;
   double* ok;
@@ -3967,10 +4007,51 @@ __global__ __launch_bounds__(kMergeThreads) void k_ord_merge(const tpe_fit_job* 
 
 // the job's current order (merged this level, or the resident one)
 __device__ __forceinline__ const double* ord_keys(const tpe_fit_job& j) {
-  return j.n_ord_in < j.n_obs ? j.ord_key_out : j.ord_key_in;
+  return j.n_ord_in < j.n_obs && j.ord_key_out ? j.ord_key_out : j.ord_key_in;
 }
 __device__ __forceinline__ const uint32_t* ord_idx(const tpe_fit_job& j) {
-  return j.n_ord_in < j.n_obs ? j.ord_idx_out : j.ord_idx_in;
+  return j.n_ord_in < j.n_obs && j.ord_key_out ? j.ord_idx_out : j.ord_idx_in;
+}
+
+// the job's virtual order (delta mode) or its order as it is (nd = 0): entry f
+// of the n_obs sorted (t, i) pairs
+struct VOrd {
+  const double* ok;
+  const uint32_t* ov;
+  const double* dk;          // the delta (LDS): keys, indices, virtual positions
+  const uint32_t* dv;
+  const uint32_t* dp;
+  int nd;
+  __device__ __forceinline__ int before(int64_t f) const {      // delta entries at positions < f
+    int lo = 0, hi = nd;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)dp[m] < f) lo = m + 1; else hi = m;
+    }
+    return lo;
+  }
+  __device__ __forceinline__ double key(int64_t f) const {
+    const int c = before(f);
+    return c < nd && (int64_t)dp[c] == f ? dk[c] : ok[f - c];
+  }
+  __device__ __forceinline__ uint32_t idx(int64_t f) const {
+    const int c = before(f);
+    return c < nd && (int64_t)dp[c] == f ? dv[c] : ov[f - c];
+  }
+};
+
+// the job's delta into LDS (block-wide, at least kFitMaxDelta threads; the
+// caller synchronises) and its virtual order
+__device__ __forceinline__ VOrd vord_lds(const tpe_fit_job& j, const double* __restrict__ dkeys,
+                                         const uint32_t* __restrict__ dvals, double* l_dk, uint32_t* l_dv,
+                                         uint32_t* l_dp) {
+  const int nd = fit_delta(j) ? (int)(j.n_obs - j.n_ord_in) : 0;
+  if ((int)threadIdx.x < nd) {
+    l_dk[threadIdx.x] = dkeys[j.seg_off + threadIdx.x];
+    l_dv[threadIdx.x] = dvals[j.seg_off + kFitMaxBelow_ + threadIdx.x];
+    l_dp[threadIdx.x] = dvals[j.seg_off + kFitMaxBelow_ + kFitMaxDelta + threadIdx.x];
+  }
+  return VOrd{ord_keys(j), ord_idx(j), l_dk, l_dv, l_dp, nd};
 }
 
 // Per-job scalars of the build, at the head of the job's fit_keys segment
@@ -3986,13 +4067,17 @@ constexpr int kFitHdrPos = 0, kFitHdrStats = 1, kFitHdrGrid = 6, kFitHdrParts = 
 // of prior_mu, tpe.py:427-431): the observations < prior_mu in the whole order
 // less the below ones
 constexpr int kFitMaxBelow = 64;
+static_assert(kFitMaxBelow == kFitMaxBelow_ && kFitMaxDelta <= kFitMaxBelow, "one delta entry per thread");
 __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* __restrict__ J,
                                                             const int32_t* __restrict__ below_idx,
-                                                            uint32_t* __restrict__ adj, double* __restrict__ hdr) {
+                                                            uint32_t* __restrict__ adj, double* __restrict__ hdr,
+                                                            const double* __restrict__ dkeys) {
   const tpe_fit_job& j = J[blockIdx.x];
   const int b = threadIdx.x;
-  const double* __restrict__ ok = ord_keys(j);
-  const uint32_t* __restrict__ ov = ord_idx(j);
+  __shared__ double l_dk[kFitMaxDelta];
+  __shared__ uint32_t l_dv[kFitMaxDelta], l_dp[kFitMaxDelta];
+  const VOrd V = vord_lds(j, dkeys, adj, l_dk, l_dv, l_dp);
+  __syncthreads();
   bool under = false;
   uint32_t mine = 0xFFFFFFFFu;
   if (b < j.n_below) {
@@ -4002,7 +4087,7 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
     int64_t lo = 0, hi = j.n_obs;
     while (lo < hi) {
       const int64_t md = (lo + hi) >> 1;
-      if (ord_lt(ok[md], ov[md], t, i)) lo = md + 1;
+      if (ord_lt(V.key(md), V.idx(md), t, i)) lo = md + 1;
       else hi = md;
     }
     mine = (uint32_t)lo;
@@ -4020,14 +4105,14 @@ __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* _
     int64_t lo = 0, hi = j.n_obs;                   // observations with t < prior_mu (NaN last)
     while (lo < hi) {
       const int64_t md = (lo + hi) >> 1;
-      if (ok[md] < j.prior_mu) lo = md + 1;
+      if (V.key(md) < j.prior_mu) lo = md + 1;
       else hi = md;
     }
     const int64_t pos = lo - n_under, n = j.n_obs - nb;
     hdr[j.seg_off + kFitHdrPos] = (double)pos;
     // the grid's bounds: the f32 means of the first and last component (the prior inserted)
-    const double m0 = pos == 0 ? j.prior_mu : ok[head];
-    const double m1 = pos == n ? j.prior_mu : ok[j.n_obs - 1 - tail];
+    const double m0 = pos == 0 ? j.prior_mu : V.key(head);
+    const double m1 = pos == n ? j.prior_mu : V.key(j.n_obs - 1 - tail);
     hdr[j.seg_off + kFitHdrGrid] = (double)(float)m0;
     hdr[j.seg_off + kFitHdrGrid + 1] = (double)(float)m1;
   }
@@ -4070,8 +4155,7 @@ struct FitPart {                                 // one chunk's statistics (fit 
 // read through the sorted below positions in global memory: position q +
 // #{k : adj[k] <= q} of the order (the wide list, the grid bounds)
 struct AboveSrc {
-  const double* ok;
-  const uint32_t* ov;
+  VOrd V;                    // the job's (virtual) order
   const uint32_t* adj;       // k_ord_below
   const int32_t* bidx;       // the job's below indices into obs, ascending
   int nb;
@@ -4083,9 +4167,9 @@ struct AboveSrc {
     }
     return q + lo;
   }
-  __device__ __forceinline__ double key(int64_t q) const { return ok[at(q)]; }
+  __device__ __forceinline__ double key(int64_t q) const { return V.key(at(q)); }
   __device__ __forceinline__ uint32_t rank(int64_t q) const {   // its index in obs less the older below ones
-    const uint32_t i = ov[at(q)];
+    const uint32_t i = V.idx(at(q));
     int lo = 0, hi = nb;
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
@@ -4152,8 +4236,8 @@ __device__ __forceinline__ FitCtx<Src> fit_ctx(const tpe_fit_job& j, Src src, in
 }
 
 __device__ __forceinline__ AboveSrc above_src(const tpe_fit_job& j, const int32_t* __restrict__ below_idx,
-                                              const uint32_t* __restrict__ adj) {
-  return AboveSrc{ord_keys(j), ord_idx(j), adj + j.seg_off, below_idx + j.below_off, j.n_below};
+                                              const uint32_t* __restrict__ adj, const VOrd& V) {
+  return AboveSrc{V, adj + j.seg_off, below_idx + j.below_off, j.n_below};
 }
 
 // Below indices per bucket of the observation indices (bucket b = i >> bsh,
@@ -4185,23 +4269,35 @@ __device__ __forceinline__ void fit_rank_buckets(int nb, const uint32_t* s_bi, i
 // observations [qa, qb), less the below positions in it (s_bp, sorted: the
 // stretch holds entries [la, lb) of it, usually none), loads first.
 // Block-wide; the caller synchronises.
-__device__ void fit_stage_rows(const tpe_fit_job& j, const uint32_t* s_bp, const uint32_t* s_bi,
-                               const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1, int64_t n, int64_t pos,
-                               double* lmu, uint32_t* lrk) {
-  const double* __restrict__ ok = ord_keys(j);
-  const uint32_t* __restrict__ ov = ord_idx(j);
-  const int nb = j.n_below;
-  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
-  auto n_before = [&](int64_t q) {                    // below positions before above observation q
-    int lo = 0, hi = nb;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if ((int64_t)s_bp[m] - m <= q) lo = m + 1; else hi = m;
-    }
-    return lo;
-  };
-  const int la = n_before(qa), lb = n_before(qb - 1);
-  const int64_t fa = qa + la, fb = qb + lb;
+// one staged entry f of the stretch: below ones skipped, the rest into lmu / lrk
+__device__ __forceinline__ void fit_stage_put(int64_t f, double kv, uint32_t o, const uint32_t* s_bp,
+                                              const uint32_t* s_bi, const uint32_t* s_bk, int bsh, int64_t c0,
+                                              int64_t c1, int64_t pos, int la, int lb, double* lmu, uint32_t* lrk) {
+  int lo = la;
+  bool below = false;
+  for (int k = la; k < lb; ++k) {                     // uniform trip count
+    const int64_t p = s_bp[k];
+    lo += p < f;
+    below |= p == f;
+  }
+  if (below) return;
+  const int64_t q = f - lo;
+  const int64_t i = q + (q >= pos);
+  if (i < c0 - 1 || i > c1) return;
+  uint32_t k = s_bk[o >> bsh];
+  const uint32_t ke = s_bk[(o >> bsh) + 1];
+  while (k < ke && s_bi[k] < o) ++k;
+  lmu[i - c0 + 1] = kv;
+  lrk[i - c0 + 1] = o - k;
+}
+
+// the stretch without delta entries: every load issued first
+__device__ __forceinline__ void fit_stage_plain(const VOrd& V, const uint32_t* s_bp, const uint32_t* s_bi,
+                                                const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1, int64_t pos,
+                                                int la, int lb, int64_t fa, int64_t fb, int da, double* lmu,
+                                                uint32_t* lrk) {
+  const double* __restrict__ ok = V.ok - da;
+  const uint32_t* __restrict__ ov = V.ov - da;
   double kv[kFitStagePer];
   uint32_t iv[kFitStagePer];
 #pragma unroll
@@ -4213,24 +4309,79 @@ __device__ void fit_stage_rows(const tpe_fit_job& j, const uint32_t* s_bp, const
   for (int e = 0; e < kFitStagePer; ++e) {
     const int64_t f = fa + e * kFitThreads + threadIdx.x;
     if (f >= fb) break;
-    int lo = la;
-    bool below = false;
-    for (int k = la; k < lb; ++k) {                   // uniform trip count
-      const int64_t p = s_bp[k];
-      lo += p < f;
-      below |= p == f;
-    }
-    if (below) continue;
-    const int64_t q = f - lo;
-    const int64_t i = q + (q >= pos);
-    if (i < c0 - 1 || i > c1) continue;
-    const uint32_t o = iv[e];
-    uint32_t k = s_bk[o >> bsh];
-    const uint32_t ke = s_bk[(o >> bsh) + 1];
-    while (k < ke && s_bi[k] < o) ++k;
-    lmu[i - c0 + 1] = kv[e];
-    lrk[i - c0 + 1] = o - k;
+    fit_stage_put(f, kv[e], iv[e], s_bp, s_bi, s_bk, bsh, c0, c1, pos, la, lb, lmu, lrk);
   }
+}
+
+// the stretch holding delta entries (a few chunks of a job in delta mode): one
+// entry at a time, few registers
+__device__ __forceinline__ void fit_stage_delta(const VOrd& V, const uint32_t* s_bp, const uint32_t* s_bi,
+                                                const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1, int64_t pos,
+                                                int la, int lb, int64_t fa, int64_t fb, int da, int db, double* lmu,
+                                                uint32_t* lrk) {
+#pragma unroll 1
+  for (int e = 0; e < kFitStagePer; ++e) {
+    const int64_t f = fa + e * kFitThreads + threadIdx.x;
+    if (f >= fb) break;
+    int c = da;
+    bool in_delta = false;
+    for (int k = da; k < db; ++k) {                   // uniform trip count
+      const int64_t p = V.dp[k];
+      c += p < f;
+      in_delta |= p == f;
+    }
+    double kv;
+    uint32_t o;
+    if (in_delta) { kv = V.dk[c]; o = V.dv[c]; }
+    else { kv = V.ok[f - c]; o = V.ov[f - c]; }
+    fit_stage_put(f, kv, o, s_bp, s_bi, s_bk, bsh, c0, c1, pos, la, lb, lmu, lrk);
+  }
+}
+
+// The stretch of the (virtual) order holding a chunk's above observations
+// [c0 - 2, c1 + 1): positions [fa, fb), its below entries [la, lb) of s_bp and
+// its delta entries [da, db) (usually none).  Workgroup-uniform (scalars).
+struct FitStretch {
+  int la, lb, da, db;
+  int64_t fa, fb;
+};
+__device__ __forceinline__ FitStretch fit_stretch(const tpe_fit_job& j, const VOrd& V, const uint32_t* s_bp, int64_t c0,
+                                                  int64_t c1, int64_t n) {
+  const int nb = j.n_below;
+  const int64_t qa = max<int64_t>(0, c0 - 2), qb = min<int64_t>(n, c1 + 1);
+  auto n_before = [&](int64_t q) {                    // below positions before above observation q
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)s_bp[m] - m <= q) lo = m + 1; else hi = m;
+    }
+    return lo;
+  };
+  FitStretch t;
+  t.la = __builtin_amdgcn_readfirstlane(n_before(qa));
+  t.lb = __builtin_amdgcn_readfirstlane(n_before(qb - 1));
+  t.fa = qa + t.la;
+  t.fb = qb + t.lb;
+  t.da = __builtin_amdgcn_readfirstlane(V.before(t.fa));
+  t.db = __builtin_amdgcn_readfirstlane(V.before(t.fb));
+  return t;
+}
+
+// k_fit_main's modes: every job's order as it is (no delta anywhere), or a
+// level with delta-mode jobs run in two launches — the chunks whose stretch
+// holds no delta entry (the order shifted by the ones before it), then the few
+// that hold some (staged one entry at a time, more registers: its own instance)
+enum { kFitPlain = 0, kFitShift = 1, kFitDeltaChunks = 2 };
+
+template <int MODE>
+__device__ void fit_stage_rows(const tpe_fit_job& j, const VOrd& V, const FitStretch& t, const uint32_t* s_bp,
+                               const uint32_t* s_bi, const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1,
+                               int64_t pos, double* lmu, uint32_t* lrk) {
+  if (MODE == kFitDeltaChunks)
+    fit_stage_delta(V, s_bp, s_bi, s_bk, bsh, c0, c1, pos, t.la, t.lb, t.fa, t.fb, t.da, t.db, lmu, lrk);
+  else
+    fit_stage_plain(V, s_bp, s_bi, s_bk, bsh, c0, c1, pos, t.la, t.lb, t.fa, t.fb, MODE == kFitPlain ? 0 : t.da, lmu,
+                    lrk);
   if (threadIdx.x == 0 && pos >= c0 - 1 && pos <= c1) lmu[pos - c0 + 1] = j.prior_mu;
 }
 
@@ -4313,12 +4464,14 @@ __device__ __forceinline__ double* wide_sigmas(const tpe_fit_job& j, double* scr
 // the buckets whose answer lies in it (a binary search over its staged means) —
 // the buckets g with mu32[c0 - 1] < edge_g <= mu32[c1 - 1] (the last chunk:
 // every g from there up, K when no mean reaches edge_g).
+template <int MODE>
 __global__ __launch_bounds__(kFitThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_fit_main(const tpe_fit_job* __restrict__ J,
                                                           const int32_t* __restrict__ below_idx,
                                                           const uint32_t* __restrict__ adj,
                                                           double* __restrict__ scratch,
                                                           uint32_t* __restrict__ wide_scratch,
-                                                          float4* __restrict__ comp, int32_t* __restrict__ grid) {
+                                                          float4* __restrict__ comp, int32_t* __restrict__ grid,
+                                                          const double* __restrict__ dkeys) {
   const tpe_fit_job& j = J[blockIdx.y];
   const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
   if (c0 >= K) return;
@@ -4327,14 +4480,20 @@ __global__ __launch_bounds__(kFitThreads) __attribute__((amdgpu_waves_per_eu(6))
   __shared__ uint32_t s_bk[kFitBuckets + 1];
   __shared__ double lmu[kFitChunk + 2];
   __shared__ uint32_t lrk[kFitChunk + 2];
+  __shared__ double l_dk[kFitMaxDelta];
+  __shared__ uint32_t l_dv[kFitMaxDelta], l_dp[kFitMaxDelta];
   fit_below_lds(j, below_idx, adj, s_bp, s_bi);
+  const VOrd V = MODE != kFitPlain ? vord_lds(j, dkeys, adj, l_dk, l_dv, l_dp)
+                                   : VOrd{ord_keys(j), ord_idx(j), l_dk, l_dv, l_dp, 0};
   __syncthreads();
+  const FitStretch t = fit_stretch(j, V, s_bp, c0, c1, n);
+  if (MODE != kFitPlain && (MODE == kFitDeltaChunks) != (t.da != t.db)) return;   // (the other launch's chunk)
   const int bsh = fit_bucket_shift(j.n_obs);
   fit_rank_buckets(j.n_below, s_bi, bsh, s_bk);
   __syncthreads();
   const double* __restrict__ hdr = scratch + j.seg_off;
   const int64_t pos = (int64_t)hdr[kFitHdrPos];
-  fit_stage_rows(j, s_bp, s_bi, s_bk, bsh, c0, c1, n, pos, lmu, lrk);
+  fit_stage_rows<MODE>(j, V, t, s_bp, s_bi, s_bk, bsh, c0, c1, pos, lmu, lrk);
   __syncthreads();
   // the bandwidth and weight rules of fit_ctx (tpe.py:381-394, 441-470) over
   // the staged means, the prior already in place
@@ -4517,15 +4676,19 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
                                                  const uint32_t* __restrict__ adj,
                                                  double* __restrict__ scratch,
                                                  const uint32_t* __restrict__ wide_scratch,
-                                                 tpe_problem* __restrict__ P, float4* __restrict__ comp) {
+                                                 tpe_problem* __restrict__ P, float4* __restrict__ comp,
+                                                 const double* __restrict__ dkeys) {
   const tpe_fit_job& j = J[blockIdx.x];
   const int64_t K = j.n_obs - j.n_below + 1;
   __shared__ int64_t wide_ix[kPruneWide];
   __shared__ int s_nw;
+  __shared__ double l_dk[kFitMaxDelta];
+  __shared__ uint32_t l_dv[kFitMaxDelta], l_dp[kFitMaxDelta];
+  const VOrd V = vord_lds(j, dkeys, adj, l_dk, l_dv, l_dp);
   const uint32_t* __restrict__ wl = wide_scratch + j.seg_off;
   const double* __restrict__ hdr = scratch + j.seg_off;
   const double thr = hdr[kFitHdrStats + 3];
-  const FitCtx<AboveSrc> c = fit_ctx(j, above_src(j, below_idx, adj), (int64_t)hdr[kFitHdrPos]);
+  const FitCtx<AboveSrc> c = fit_ctx(j, above_src(j, below_idx, adj, V), (int64_t)hdr[kFitHdrPos]);
   const uint32_t n_cand = wl[0];
   const double* __restrict__ wsg = wide_sigmas(j, scratch, K);
   if (threadIdx.x == 0) s_nw = 0;
@@ -4767,31 +4930,34 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   if (rc) return rc;
   if (b->n_fit == 0) return TPE_OK;
   if (b->fit_total >= ((int64_t)1 << 32)) return fail(TPE_E_ARG, "more than 2^32 fit observations");
-  if (b->fit_max_new < 0 || b->fit_max_obs < b->fit_max_new || b->fit_max_obs >= ((int64_t)1 << 31))
-    return fail(TPE_E_ARG, "bad fit_max_new / fit_max_obs");
+  if (b->fit_max_new < 0 || b->fit_max_obs < b->fit_max_new || b->fit_max_obs >= ((int64_t)1 << 31) ||
+      b->fit_max_merge < 0 || b->fit_max_merge > b->fit_max_new || b->fit_n_delta < 0 || b->fit_n_delta > b->n_fit)
+    return fail(TPE_E_ARG, "bad fit_max_new / fit_max_obs / fit_max_merge");
   hipStream_t s = (hipStream_t)stream;
   if (b->fit_max_new > 0) {
     // the observations appended since each order was written: sorted chunks,
     // merged pairwise until one run per job, then merged into the resident order
     const int64_t chunks = (b->fit_max_new + kOrdChunk - 1) / kOrdChunk;
     TPE_LAUNCH(k_ord_chunks, dim3((unsigned)chunks, b->n_fit), dim3(kOrdChunkThreads), 0, s, b->fit, b->fit_keys,
-               b->fit_vals);
+               b->fit_vals, b->fit_keys_sorted, b->fit_vals_sorted);
     if ((rc = hip_check("tpe_fit_above/chunks"))) return rc;
     double* src_k = b->fit_keys;
     uint32_t* src_v = b->fit_vals;
     double* dst_k = b->fit_keys_sorted;
     uint32_t* dst_v = b->fit_vals_sorted;
-    const unsigned tiles_new = (unsigned)((b->fit_max_new + kMergeTile - 1) / kMergeTile);
-    for (int64_t L = kOrdChunk; L < b->fit_max_new; L *= 2) {
-      TPE_LAUNCH(k_ord_merge, dim3(tiles_new, b->n_fit), dim3(kMergeThreads), 0, s, b->fit, src_k, src_v, dst_k,
-                 dst_v, L);
-      std::swap(src_k, dst_k);
-      std::swap(src_v, dst_v);
+    if (b->fit_max_merge > 0) {               // (none when every job with new observations is in delta mode)
+      const unsigned tiles_new = (unsigned)((b->fit_max_merge + kMergeTile - 1) / kMergeTile);
+      for (int64_t L = kOrdChunk; L < b->fit_max_merge; L *= 2) {
+        TPE_LAUNCH(k_ord_merge, dim3(tiles_new, b->n_fit), dim3(kMergeThreads), 0, s, b->fit, src_k, src_v, dst_k,
+                   dst_v, L);
+        std::swap(src_k, dst_k);
+        std::swap(src_v, dst_v);
+      }
+      const unsigned tiles_obs = (unsigned)((b->fit_max_obs + kMergeTile - 1) / kMergeTile);
+      TPE_LAUNCH(k_ord_merge, dim3(tiles_obs, b->n_fit), dim3(kMergeThreads), 0, s, b->fit, src_k, src_v,
+                 (double*)nullptr, (uint32_t*)nullptr, (int64_t)0);
+      if ((rc = hip_check("tpe_fit_above/merge"))) return rc;
     }
-    const unsigned tiles_obs = (unsigned)((b->fit_max_obs + kMergeTile - 1) / kMergeTile);
-    TPE_LAUNCH(k_ord_merge, dim3(tiles_obs, b->n_fit), dim3(kMergeThreads), 0, s, b->fit, src_k, src_v,
-               (double*)nullptr, (uint32_t*)nullptr, (int64_t)0);
-    if ((rc = hip_check("tpe_fit_above/merge"))) return rc;
   }
   // the sorted below positions (adj) in fit_vals_sorted (free once the merge
   // has run), then the build over the order itself (no compaction): chunk
@@ -4799,15 +4965,26 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   // buckets, the wide list (its counter and indices in fit_vals) and the
   // problem rows
   uint32_t* adj = b->fit_vals_sorted;
-  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, adj, b->fit_keys);
+  TPE_LAUNCH(k_ord_below, dim3(b->n_fit), dim3(kFitMaxBelow), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
+             (const double*)b->fit_keys_sorted);
   const unsigned chunks_k = (unsigned)((b->fit_max_obs + 1 + kFitChunk - 1) / kFitChunk);
   // the wide candidates' counters (one per job, at its segment's head)
   TPE_LAUNCH(k_fit_wide_reset, dim3((unsigned)((b->n_fit + 255) / 256)), dim3(256), 0, s, b->fit, b->n_fit, b->fit_vals);
-  TPE_LAUNCH(k_fit_main, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj, b->fit_keys,
-             b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid));
+  if (b->fit_n_delta > 0) {                   // (jobs in delta mode)
+    TPE_LAUNCH(k_fit_main<kFitShift>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
+               b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid),
+               (const double*)b->fit_keys_sorted);
+    TPE_LAUNCH(k_fit_main<kFitDeltaChunks>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx,
+               adj, b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid),
+               (const double*)b->fit_keys_sorted);
+  } else {
+    TPE_LAUNCH(k_fit_main<kFitPlain>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
+               b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid),
+               (const double*)b->fit_keys_sorted);
+  }
   TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys);
   TPE_LAUNCH(k_fit_wide, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->below_idx, adj, b->fit_keys, b->fit_vals,
-             const_cast<tpe_problem*>(b->problems), (float4*)b->comp32);
+             const_cast<tpe_problem*>(b->problems), (float4*)b->comp32, (const double*)b->fit_keys_sorted);
   return hip_check("tpe_fit_above/build");
 }
 
@@ -5214,7 +5391,8 @@ static void early_fit_hook(void* c, const tpe_pack_info* e) {
   b.fit_total = e->fit_total;
   b.fit_keys = ws->fit_keys; b.fit_keys_sorted = ws->fit_keys_sorted;
   b.fit_vals = ws->fit_vals; b.fit_vals_sorted = ws->fit_vals_sorted;
-  b.fit_max_new = e->fit_max_new; b.fit_max_obs = e->fit_max_obs;
+  b.fit_max_new = e->fit_max_new; b.fit_max_obs = e->fit_max_obs; b.fit_max_merge = e->fit_max_merge;
+  b.fit_n_delta = e->fit_n_delta;
   x.rc = tpe_fit_above(&b, x.s);
   x.launched = x.rc == TPE_OK;
 }
@@ -5448,7 +5626,8 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     b.fit_total = info.fit_total;
     b.fit_keys = ws->fit_keys; b.fit_keys_sorted = ws->fit_keys_sorted;
     b.fit_vals = ws->fit_vals; b.fit_vals_sorted = ws->fit_vals_sorted;
-    b.fit_max_new = info.fit_max_new; b.fit_max_obs = info.fit_max_obs;
+    b.fit_max_new = info.fit_max_new; b.fit_max_obs = info.fit_max_obs; b.fit_max_merge = info.fit_max_merge;
+    b.fit_n_delta = info.fit_n_delta;
   }
   if (g_prof.on) {
     g_prof.valid = 0;

@@ -7,11 +7,13 @@
 // the caller publishes the job and, in the same 64-bit control word, its
 // generation and the set of PARTICIPANTS — itself and the workers that are
 // awake (spinning), at most one per job.  Participant r runs job r straight
-// away (no claim), the jobs past the participants are claimed from a counter
-// with fetch_add, and each participant reports completion in its own cache
-// line, which is all the caller waits on.  A generation cannot end before
-// every participant has reported, so no worker ever runs a job of a
-// generation it was not given.
+// away (no claim) and reports completion in its own cache line.  The jobs past
+// the participants' (a wide dispatch: a thousand labels' fits) are claimed by
+// compare-and-swap on a word that carries the generation and the job count —
+// by the participants and by every other worker, the ones woken from sleep
+// included — and counted down as they return.  A generation cannot end before
+// every participant has reported and every claimed job has returned, so no
+// worker ever runs a job of a generation it was not given.
 #include "tpe_pool.h"
 
 #include <pthread.h>
@@ -50,7 +52,12 @@ struct Pool {
   void* ctx = nullptr;
   int n = 0;
   int n_part = 0;                           // participants, the caller included
-  alignas(64) std::atomic<int> next{0};     // the next job to claim (past the participants' first jobs)
+  // the jobs past the participants' first ones, claimed by compare-and-swap on
+  // (generation mod 2^24, job count, next job) — by the participants and by any
+  // other worker, awake or woken, so a wide dispatch uses every thread; a claim
+  // can only succeed while its generation's jobs are not all taken
+  alignas(64) std::atomic<uint64_t> next{0};
+  alignas(64) std::atomic<int> left{0};     // claimed jobs not yet returned
   alignas(64) std::atomic<int> sleepers{0};
   std::atomic<bool> stop{false};
   std::atomic<bool> retired{false};         // replaced by tpe_host_threads: dispatch nothing more to it
@@ -62,14 +69,23 @@ struct Pool {
   std::vector<std::thread> th;
 };
 
-// participant `rank` of the current generation: its own job, then claimed ones
-void run_jobs(Pool* p, int rank) {
-  if (rank < p->n) p->fn(p->ctx, rank);
-  if (p->n <= p->n_part) return;            // (one job each: no claims)
+constexpr int kJobBits = 20;                // jobs per dispatch < 2^20 (more: run serially)
+inline uint64_t claim_word(uint32_t g, int n, int i) {
+  return (uint64_t)(g & 0xFFFFFFu) << (2 * kJobBits) | (uint64_t)n << kJobBits | (uint64_t)i;
+}
+
+// claim and run the jobs of generation g past the participants' first ones
+void claim_jobs(Pool* p, uint32_t g) {
+  uint64_t v = p->next.load(std::memory_order_acquire);
   for (;;) {
-    const int i = p->next.fetch_add(1, std::memory_order_relaxed);
-    if (i >= p->n) return;
+    if ((uint32_t)(v >> (2 * kJobBits)) != (g & 0xFFFFFFu)) return;
+    const int i = (int)(v & ((1u << kJobBits) - 1)), n = (int)((v >> kJobBits) & ((1u << kJobBits) - 1));
+    if (i >= n) return;
+    if (!p->next.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+    // (the claim holds the generation open: its job fields are current)
     p->fn(p->ctx, i);
+    p->left.fetch_sub(1, std::memory_order_acq_rel);
+    v = p->next.load(std::memory_order_acquire);
   }
 }
 
@@ -104,12 +120,16 @@ void worker(Pool* p, int id) {
     const uint32_t g = (uint32_t)(c >> 32);
     const uint32_t mask = (uint32_t)c;
     seen = g;
-    if (!(mask >> id & 1)) continue;        // not a participant of g
-    // (the job fields were written before the control word; they stay until
-    // every participant has reported)
-    const int rank = 1 + __builtin_popcount(mask & ((1u << id) - 1));
-    run_jobs(p, rank);
-    me.done.store(g, std::memory_order_release);
+    if (mask >> id & 1) {
+      // a participant: its own job (the job fields were written before the
+      // control word; they stay until every participant has reported), then claims
+      const int rank = 1 + __builtin_popcount(mask & ((1u << id) - 1));
+      if (rank < p->n) p->fn(p->ctx, rank);
+      claim_jobs(p, g);
+      me.done.store(g, std::memory_order_release);
+    } else {
+      claim_jobs(p, g);                     // (nothing when every job has a participant)
+    }
   }
 }
 
@@ -184,7 +204,7 @@ Pool* get_pool() {
 namespace tpe_pool {
 
 void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
-  Pool* const held = n >= 2 ? get_pool() : nullptr;
+  Pool* const held = n >= 2 && n < (1 << kJobBits) ? get_pool() : nullptr;
   Pool* p = held;
   std::unique_lock<std::mutex> own;
   if (p) {
@@ -212,16 +232,19 @@ void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
   p->ctx = ctx;
   p->n = n;
   p->n_part = part;
-  p->next.store(part, std::memory_order_relaxed);
+  p->left.store(n - part, std::memory_order_relaxed);
+  p->next.store(claim_word(g, n, part), std::memory_order_relaxed);
   p->ctl.store((uint64_t)g << 32 | mask);           // publishes the job (seq_cst)
-  if (p->sleepers.load()) {                         // (a participant may have gone to sleep since)
+  if (p->sleepers.load()) {                         // (a participant may have gone to sleep; helpers)
     { std::lock_guard<std::mutex> lk(p->m); }
     p->cv.notify_all();
   }
-  run_jobs(p, 0);
+  fn(ctx, 0);
+  claim_jobs(p, g);
   for (int w = 1; w <= p->n_workers; ++w)
     if (mask >> w & 1)
       while (p->slot[w].done.load(std::memory_order_acquire) != g) cpu_relax();
+  while (p->left.load(std::memory_order_acquire) > 0) cpu_relax();
   own.unlock();
   release(held);
 }

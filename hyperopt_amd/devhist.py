@@ -18,6 +18,13 @@ room; one that outgrows it re-lays out the tensor (every segment doubles).
 """
 import numpy as np
 
+from . import _native as N
+
+try:
+    from . import _hostaddr               # (csrc/hostaddr.c, built with the library)
+except ImportError:                       # pragma: no cover - before the build
+    _hostaddr = None
+
 try:
     import torch
 except ImportError:  # pragma: no cover - torch is part of the image
@@ -93,26 +100,41 @@ class _Orders(object):
         self.kbase, self.ibase = keys.data_ptr(), idx.data_ptr()
         self.owner.version += 1
 
+    @staticmethod
+    def _runs(on, n_obs):
+        """(n_in, merged) of runs over n_obs observations given orders of on:
+        the order's length when it is a prefix (a longer one is another
+        column's: none), and whether the run merges into the other buffer pair
+        — not when it is in delta mode (a few new observations read beside the
+        order, include/tpe_hip.h TPE_FIT_DELTA_MAX)."""
+        n_in = np.where(on <= n_obs, on, 0)
+        new = n_obs - n_in
+        return n_in, (new > 0) & ((n_in == 0) | (new > N.FIT_DELTA_MAX))
+
     def ptrs_many(self, slots, n_obs):
         """(key_in, idx_in, n_in, key_out, idx_out) device addresses, as int64
-        arrays, for runs that fit slot slots[i]'s first n_obs[i] observations."""
+        arrays, for runs that fit slot slots[i]'s first n_obs[i] observations
+        (key_out = 0: no merge)."""
         slots = np.asarray(slots, dtype=np.int64)
         n_obs = np.asarray(n_obs, dtype=np.int64)
-        self.ensure(slots, n_obs)
+        on = self.n[slots]
+        n_in, out = self._runs(on, n_obs)
+        if out.any():
+            self.ensure(slots[out], n_obs[out])
         on, cur, off = self.n[slots], self.cur[slots], self.off[slots]
-        n_in = np.where(on <= n_obs, on, 0)              # (a longer order is of another column)
         has = n_in > 0
         kin = np.where(has, self.kbase + 8 * (cur * self.tc + off), 0)
         iin = np.where(has, self.ibase + 4 * (cur * self.tc + off), 0)
-        out = n_in != n_obs
         kout = np.where(out, self.kbase + 8 * ((1 - cur) * self.tc + off), 0)
         iout = np.where(out, self.ibase + 4 * ((1 - cur) * self.tc + off), 0)
         return kin, iin, n_in, kout, iout
 
     def commit_many(self, slots, n_obs):
+        """Runs with ``ptrs_many(slots, n_obs)`` were enqueued: the merged
+        orders are now current (delta-mode runs left theirs as they were)."""
         slots = np.asarray(slots, dtype=np.int64)
         n_obs = np.asarray(n_obs, dtype=np.int64)
-        mv = self.n[slots] != n_obs
+        mv = self._runs(self.n[slots], n_obs)[1]
         if mv.any():
             s = slots[mv]
             self.cur[s] = 1 - self.cur[s]
@@ -171,6 +193,7 @@ class DeviceColumns(object):
         self.cap = np.zeros(0, dtype=np.int64)
         self.n = np.zeros(0, dtype=np.int64)        # values uploaded per slot
         self.orders = _Orders(device, self)
+        self._last_labels, self._last_slots = None, None
 
     def _add(self, label):
         s = self.slot[label] = len(self.views)
@@ -198,18 +221,23 @@ class DeviceColumns(object):
         self.views = [store[o:o + c] for o, c in zip(off.tolist(), cap.tolist())]
         self.version += 1
 
-    def upload(self, labels, values):
+    def upload(self, labels, values, lengths=None):
         """Make the column of labels[i] hold values[i] (a float64 array that
         extends what earlier calls for the label passed; a shorter one — another
         History's — starts the label over, its order too); the values not
-        uploaded yet go up in one scatter.  Returns the labels' slots (int64)."""
+        uploaded yet go up in one scatter (``lengths``: len(values[i]) when the
+        caller has them).  Returns the labels' slots (int64)."""
         get = self.slot.get
-        slots = np.fromiter((get(k, -1) for k in labels), dtype=np.int64, count=len(labels))
-        nv = np.fromiter(map(len, values), dtype=np.int64, count=len(values))
-        if len(slots) and slots.min() < 0:
-            for i in np.flatnonzero(slots < 0).tolist():
-                s = get(labels[i])
-                slots[i] = s if s is not None else self._add(labels[i])
+        if labels is self._last_labels:          # (the caller's same list: its slots are known)
+            slots = self._last_slots
+        else:
+            slots = np.fromiter((get(k, -1) for k in labels), dtype=np.int64, count=len(labels))
+            if len(slots) and slots.min() < 0:
+                for i in np.flatnonzero(slots < 0).tolist():
+                    s = get(labels[i])
+                    slots[i] = s if s is not None else self._add(labels[i])
+            self._last_labels, self._last_slots = labels, slots
+        nv = np.fromiter(map(len, values), dtype=np.int64, count=len(values)) if lengths is None else lengths
         m = self.n[slots]
         short = m > nv
         if short.any():
@@ -224,8 +252,11 @@ class DeviceColumns(object):
             self._relayout(want)
         up = np.flatnonzero(nv > m)
         if len(up):
-            ml, nl = m.tolist(), nv.tolist()
-            vals = np.concatenate([values[i][ml[i]:nl[i]] for i in up.tolist()]).astype(np.float64, copy=False)
+            try:                                 # (float64 columns: their new values gathered natively)
+                vals = _hostaddr.tails(values, m, nv)
+            except (ValueError, AttributeError):
+                ml, nl = m.tolist(), nv.tolist()
+                vals = np.concatenate([values[i][ml[i]:nl[i]] for i in up.tolist()]).astype(np.float64, copy=False)
             su = slots[up]
             pos = _positions(self.off[su] + m[up], nv[up] - m[up])
             self.store[torch.from_numpy(pos).to(self.device)] = torch.from_numpy(vals).to(self.device)

@@ -879,7 +879,8 @@ class Engine(object):
             b.below_idx, b.fit_seg, b.fit_total = base + info.off_below_idx, base + info.off_fit_seg, ft
             b.fit_keys, b.fit_keys_sorted = d_fk.data_ptr(), d_fks.data_ptr()
             b.fit_vals, b.fit_vals_sorted = d_fv.data_ptr(), d_fvs.data_ptr()
-            b.fit_max_new, b.fit_max_obs = info.fit_max_new, info.fit_max_obs
+            b.fit_max_new, b.fit_max_obs, b.fit_max_merge = info.fit_max_new, info.fit_max_obs, info.fit_max_merge
+            b.fit_n_delta = info.fit_n_delta
         stream = self._stream()
         if self.profile is None:
             N.check(self.lib.tpe_run_batch(ctypes.byref(b), ctypes.c_void_p(stream)), self.lib, 'tpe_run_batch')

@@ -317,6 +317,22 @@ def _tree_static(table):
     return st
 
 
+_I64, _F64 = np.dtype(np.int64).num, np.dtype(np.float64).num
+
+
+def _tree_groups(table, meta):
+    """The tree records' labels by kind, once per table: the categorical ones
+    [(label, index)] and the continuous ones (labels, their record indices,
+    which are log families) — the quantized ones take no columns."""
+    g = table.__dict__.get('_tree_groups')
+    if g is None:
+        cats = [(label, ix) for label, ix, fam in meta if fam == N.FAM_CATEGORICAL]
+        gm = [(label, ix, fam == N.FAM_LOGGAUSS) for label, ix, fam in meta if fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS)]
+        g = table._tree_groups = (cats, [m[0] for m in gm], np.array([m[1] for m in gm], dtype=np.int64),
+                                  np.array([m[2] for m in gm], dtype=bool))
+    return g
+
+
 def _dev_fit_min(engine):
     """Observations from which a continuous label's above side is fitted on
     the device (Engine.device_fit_min, fp32 only), or None."""
@@ -368,34 +384,31 @@ def _tree_labels(table, hist, engine=None, remote=()):
             holder.tree_memo = (table, n_docs, mkey, memo[3], dver, memo[5])
             return memo[3]
     arr = arr0.view(np.uint8).copy().view(arr0.dtype)      # (a byte copy: the record dtype copies field by field)
-    keep, dix, dn, dlab, dx, dt, gix, gn = [], [], [], [], [], [], [], []
-    for label, ix, fam in meta:
+    keep = []
+    cats, glab, gix, glogc = _tree_groups(table, meta)
+    for label, ix in cats:
         otids, ovals = hist.obs[label]
-        if fam == N.FAM_CATEGORICAL:
-            cols = hist.cat_columns(label)
-            if cols is None:
-                t, v = np.ascontiguousarray(otids, dtype=np.int64), np.ascontiguousarray(ovals, dtype=np.int64)
-                keep += [t, v]
-                cols = (t.ctypes.data, v.ctypes.data)
-            rec = arr[ix]
-            rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
-        elif fam in (N.FAM_GAUSS, N.FAM_LOGGAUSS):
-            n = len(otids)
-            gix.append(ix)
-            gn.append(n)
-            logc = fam == N.FAM_LOGGAUSS
-            if dev_min is not None and n >= dev_min:
-                if ix in remote:                 # (another rank's label: never fitted here)
-                    continue
-                # device fit of the above side: the device column (kernel coordinate)
-                # and its resident order, filled in below for all such labels at once;
-                # the host keeps the columns for the below side
-                dix.append(ix)
-                dn.append(n)
-                dlab.append(label)
-                dx.append(np.ascontiguousarray(hist.log_values(label) if logc else ovals, dtype=np.float64))
-                dt.append(np.ascontiguousarray(otids, dtype=np.int64))
-                continue
+        cols = hist.cat_columns(label)
+        if cols is None:
+            t, v = np.ascontiguousarray(otids, dtype=np.int64), np.ascontiguousarray(ovals, dtype=np.int64)
+            keep += [t, v]
+            cols = (t.ctypes.data, v.ctypes.data)
+        rec = arr[ix]
+        rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
+    devs = None
+    if glab:
+        obs = hist.obs
+        pairs = [obs[k] for k in glab]
+        tl = [p[0] for p in pairs]
+        ns = np.fromiter(map(len, tl), dtype=np.int64, count=len(tl))
+        arr['n_obs'][gix] = ns
+        big = ns >= dev_min if dev_min is not None else np.zeros(len(ns), dtype=bool)
+        host, dev = ~big, big
+        if remote and big.any():                 # (another rank's labels: never fitted here)
+            dev = big & ~np.isin(gix, np.asarray(remote, dtype=np.int64))
+        for q in np.flatnonzero(host).tolist():
+            label, ix, logc = glab[q], int(gix[q]), bool(glogc[q])
+            otids, ovals = pairs[q]
             order = hist.value_order(label)
             cols = hist.native_columns(label, log=logc) if order is not None else None
             if cols is None:
@@ -409,24 +422,43 @@ def _tree_labels(table, hist, engine=None, remote=()):
                     cols = cols[:2] + (o.ctypes.data,)
             rec = arr[ix]
             rec['tids'], rec['values'], rec['order'] = cols
-    if gix:
-        arr['n_obs'][gix] = gn
-    devs = None
-    if dix:
-        # the new observations of every device-fitted label up in one scatter, room
-        # for their orders made, then the addresses (a re-layout moves them all)
-        slots = dc.upload(dlab, dx)
-        keep += [dt, dx, dc.store]
-        ixs = np.asarray(dix, dtype=np.int64)
-        ns = np.asarray(dn, dtype=np.int64)
-        kin, iin, n_in, kout, iout = dc.orders.ptrs_many(slots, ns)
-        if _hostaddr is None:
-            raise N.NativeUnavailable('hyperopt_amd._hostaddr is not built (python -m hyperopt_amd.build)')
-        for f, v in (('tids', _hostaddr.addresses(dt)), ('values', _hostaddr.addresses(dx)), ('order', 0),
-                     ('dev_obs', dc.addresses(slots)), ('ord_key_in', kin), ('ord_idx_in', iin), ('n_ord_in', n_in),
-                     ('ord_key_out', kout), ('ord_idx_out', iout)):
-            arr[f][ixs] = v
-        devs = (ixs, slots, ns, dc.orders)
+        if dev.any():
+            # device fit of the above side: the device column (kernel coordinate)
+            # and its resident order — every such label's new observations up in
+            # one scatter, room for their orders made, then the addresses (a
+            # re-layout moves them all); the host keeps the columns for the below side
+            if _hostaddr is None:
+                raise N.NativeUnavailable('hyperopt_amd._hostaddr is not built (python -m hyperopt_amd.build)')
+            if dev.all():
+                dq, dlab, dns, ixs = None, glab, ns, gix
+            else:
+                dq = np.flatnonzero(dev)
+                dlab, dns, ixs = [glab[q] for q in dq.tolist()], ns[dq], gix[dq]
+            sel = pairs if dq is None else [pairs[q] for q in dq.tolist()]
+            dt = tl if dq is None else [p[0] for p in sel]
+            if glogc.any():
+                lg = glogc if dq is None else glogc[dq]
+                dx = [hist.log_values(k) if l else p[1] for k, l, p in zip(dlab, lg.tolist(), sel)]
+            else:
+                dx = [p[1] for p in sel]
+            try:
+                ta = _hostaddr.addresses(dt, _I64)
+            except TypeError:
+                dt = [np.ascontiguousarray(a, dtype=np.int64) for a in dt]
+                ta = _hostaddr.addresses(dt)
+            try:
+                xa = _hostaddr.addresses(dx, _F64)
+            except TypeError:
+                dx = [np.ascontiguousarray(a, dtype=np.float64) for a in dx]
+                xa = _hostaddr.addresses(dx)
+            slots = dc.upload(dlab, dx, dns)
+            keep += [dt, dx, dc.store]
+            kin, iin, n_in, kout, iout = dc.orders.ptrs_many(slots, dns)
+            for f, v in (('tids', ta), ('values', xa), ('order', 0), ('dev_obs', dc.addresses(slots)),
+                         ('ord_key_in', kin), ('ord_idx_in', iin), ('n_ord_in', n_in), ('ord_key_out', kout),
+                         ('ord_idx_out', iout)):
+                arr[f][ixs] = v
+            devs = (ixs, slots, dns, dc.orders)
     out = (arr, keep, devs, arr.ctypes.data)
     fv = None
     if cache is not None and devs is None and not keep:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 20
+#define TPE_ABI_VERSION 21
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -360,12 +360,19 @@ typedef struct tpe_result {
  *            from neighbour gaps, clip, LF weights, normalisation, {mu, a, c}
  *            rows, wide list, grid; patches the job's problem rows (above_base,
  *            wide_len, prior_*, narrow_*, grid_lo/inv)
- * No sort of the whole history runs after the first suggest: a steady-state
- * suggest costs one merge pass over each label's order (none when nothing was
- * appended) plus the compaction and the build.
+ * No sort of the whole history runs after the first suggest.  DELTA MODE: a job
+ * with 1 .. TPE_FIT_DELTA_MAX new observations and ord_*_out NULL is not merged:
+ * its new observations are sorted and placed among the resident ones (their
+ * ranks), and the build reads the resident order and them as one virtual order
+ * — the merge pass over the whole order waits until the new ones outgrow the
+ * delta (FMinIter's one observation per suggest: one merge every
+ * TPE_FIT_DELTA_MAX suggests); ord_*_in stays the caller's order of the first
+ * n_ord_in.  A steady-state suggest costs the build (plus, every
+ * TPE_FIT_DELTA_MAX appends, one merge pass over each label's order).
  * The host reserves above_off[0 .. K) + wide_off[0 .. 16) rows and grid_n + 1
  * grid entries (K = n_obs - n_below + 1, grid_n = min(4096, 4K)).
  */
+#define TPE_FIT_DELTA_MAX 64
 typedef struct tpe_fit_job {
   const double* obs;     /* device: the label's observations in tid order, in the kernel
                             coordinate t (x, or the caller's np.log(x) for LOGGAUSS) */
@@ -428,12 +435,15 @@ typedef struct tpe_batch {
   int32_t fgt_max_cells; /* most above cells of a TPE_F_FGT problem (built by the box stage) */
   const int32_t* below_idx;   /* below indices of every job                        */
   const int64_t* fit_seg;     /* [n_fit + 1] segment offsets into the fit scratch: a job's
-                                 segment holds max(n_obs - n_below, n_obs - n_ord_in, n_below) */
+                                 segment holds max(n_obs - n_below, n_obs - n_ord_in, n_below,
+                                 64 + 2 * TPE_FIT_DELTA_MAX) */
   int64_t fit_total;          /* fit_seg[n_fit]                                    */
   double* fit_keys; double* fit_keys_sorted;        /* [fit_total] scratch (ping-pong) */
   uint32_t* fit_vals; uint32_t* fit_vals_sorted;    /* [fit_total]                */
   int64_t fit_max_new;        /* most new observations of one job (n_obs - n_ord_in) */
   int64_t fit_max_obs;        /* most observations of one job                       */
+  int64_t fit_max_merge;      /* most new observations of a job that merges them (0: none) */
+  int64_t fit_n_delta;        /* jobs in delta mode (new observations, no ord_*_out) */
   /* ordered draws: [n_sorted][draw_blocks + 1] doubles, draw_blocks = ceil((C_global + 1) / 64) */
   double* draw_pref; int64_t draw_blocks; int32_t n_sorted;
   int32_t tab_fast;      /* >= 1: the candidates are device-drawn at TPE_PREC_F32, early selection is on,
@@ -517,8 +527,9 @@ int tpe_select(const tpe_batch* batch, void* stream);
  * below observations in it, above_k = n_obs - n_below + 1; prior_* and lf are
  * the fit parameters; ord_* = the label's resident value order (tpe_fit_job:
  * ord_*_in may be NULL when n_ord_in = 0, ord_*_out may be NULL when
- * n_ord_in = n_obs).  After the level has run, ord_*_out holds the order of
- * all n_obs observations whenever n_ord_in < n_obs. */
+ * n_ord_in = n_obs or, delta mode, when 0 < n_obs - n_ord_in <= TPE_FIT_DELTA_MAX
+ * and n_ord_in > 0).  After the level has run, ord_*_out holds the order of
+ * all n_obs observations whenever it was given. */
 typedef struct tpe_label_in {
   int32_t family, flags, upper, label_ix;
   double low, high, q;
@@ -549,6 +560,8 @@ typedef struct tpe_pack_info {
   int64_t off_fin_tiles, n_fin_tiles;   /* tpe_batch.fin_tiles */
   int64_t fit_max_new;                  /* tpe_batch.fit_max_new */
   int64_t fit_max_obs;                  /* tpe_batch.fit_max_obs */
+  int64_t fit_max_merge;                /* tpe_batch.fit_max_merge */
+  int64_t fit_n_delta;                  /* tpe_batch.fit_n_delta */
   int64_t n_sorted, draw_blocks;        /* tpe_batch.n_sorted / draw_blocks */
   int64_t n_pooled;                     /* pooled problems (tpe_batch.pool_best needed) */
   int64_t off_tab_jobs, n_tab_jobs, tab_blocks, tab_units;   /* tabulated scoring (tpe_batch.tab_*) */

@@ -67,3 +67,25 @@ def test_orders_ensure_keeps_current_side():
     kin, iin, n_in, kout, iout = g.ptrs_many([sa, sb], [100, 50000])
     assert n_in.tolist() == [100, 50] and kout[0] == 0 and kout[1] != 0
     assert g.keys[(kin[1] - g.kbase) // 8].item() == 0.25
+
+
+def test_delta_mode_runs_leave_the_order():
+    """A run with at most FIT_DELTA_MAX new observations over a resident order
+    gets no merge buffers and its commit leaves the order as it was (the
+    kernels read the new ones beside it); more new ones, or no order, merge."""
+    from hyperopt_amd import _native as N
+    dc = devhist.DeviceColumns(torch.device('cpu'))
+    dc.columns([('a', np.zeros(1000))])
+    g, sa = dc.orders, dc.order('a').slot
+    kin, iin, n_in, kout, iout = g.ptrs_many([sa], [1000])
+    assert n_in[0] == 0 and kout[0] != 0                # no order yet: a merge of everything
+    g.commit_many([sa], [1000])
+    for n in (1001, 1000 + N.FIT_DELTA_MAX):
+        kin, iin, n_in, kout, iout = g.ptrs_many([sa], [n])
+        assert n_in[0] == 1000 and kin[0] != 0 and kout[0] == 0 and iout[0] == 0
+        g.commit_many([sa], [n])
+        assert dc.order('a').n == 1000
+    kin, iin, n_in, kout, iout = g.ptrs_many([sa], [1001 + N.FIT_DELTA_MAX])
+    assert n_in[0] == 1000 and kout[0] != 0
+    g.commit_many([sa], [1001 + N.FIT_DELTA_MAX])
+    assert dc.order('a').n == 1001 + N.FIT_DELTA_MAX

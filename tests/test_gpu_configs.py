@@ -292,44 +292,58 @@ O_A_SCALE = float(np.sqrt(0.5 / np.log(2.0)))      # sqrt(log2(e) / 2): a_k = A 
 
 def test_device_value_order_incremental():
     """The resident device value order of device-fitted labels (tpe_fit_above:
-    chunk sort -> merge passes -> merge into the resident order) over 5
-    suggests that each append 200 observations (1,000 in all): after every
-    suggest each label's order is np.argsort(kind='stable') of its kernel
-    coordinate (ties by tid order; repeated values included), the suggestion
-    equals a from-scratch fit's bit for bit, and at the end the device rows
-    match the oracle's adaptive_parzen_normal."""
-    from hyperopt_amd import base, devhist, hp, history as H, tpe
+    chunk sort -> merge passes -> merge into the resident order, or DELTA MODE:
+    at most TPE_FIT_DELTA_MAX new observations read beside the order as one
+    virtual order, no merge) over suggests that append 200, 1, 1, 30, 33, 64
+    and 1 observations (FMinIter appends one per suggest): after every suggest
+    each label's order is np.argsort(kind='stable') of the kernel coordinate of
+    the observations it holds (ties by tid order; repeated values included) —
+    all of them after a merge, the last merged prefix in delta mode — the
+    suggestion equals a from-scratch fit's (a full sort and merge) bit for bit,
+    and at the end the device rows match the oracle's adaptive_parzen_normal."""
+    from hyperopt_amd import _native as N, base, devhist, hp, history as H, tpe
     from hyperopt_amd.engine import LevelProblem, get_engine
     eng = get_engine()
-    N0, step, n_steps, C, seed = 20000, 200, 5, 4096, 17
-    Nt = N0 + step * n_steps
-    assert N0 - 25 >= eng.device_fit_min
+    N0, C, seed = 20000, 4096, 17
+    steps = [0, 200, 1, 1, 30, 33, 64, 1]
+    Nt = N0 + sum(steps)
+    assert N0 - 25 >= eng.device_fit_min and N.FIT_DELTA_MAX == 64
     table = base.Domain(lambda d: 0.0, {'u': hp.uniform('u', -5, 5), 'l': hp.loguniform('l', -3, 2)}).table
     rs = np.random.RandomState(3)
     u = rs.uniform(-5, 5, Nt)
     u[::7] = np.round(u[::7], 1)                     # repeated values: ties broken by tid order
+    u[N0 + 200:N0 + 202] = u[5]                      # new observations equal to resident ones
     lv = np.exp(rs.uniform(-3, 2, Nt))
     lv[::13] = np.round(lv[::13], 2)
     tids = np.arange(Nt, dtype=np.int64)
     losses = rs.uniform(size=Nt) + 1e-9 * tids
+    losses[N0 + 230] = -1.0                          # a new observation in the below set (delta mode)
     dev = {}                                         # the Trials cache's device state, kept across suggests
     vals = {'u': u, 'l': lv}
 
     def hist_of(n, d):
         return H.History(tids[:n], losses[:n].copy(), {k: (tids[:n], v[:n]) for k, v in vals.items()}, dev=d)
-    for s in range(n_steps + 1):
-        n = N0 + s * step
+    n, held, deltas = N0, N0, 0
+    for s, inc in enumerate(steps):
+        n += inc
+        if n - held > N.FIT_DELTA_MAX:
+            held = n                                 # a merge: the order holds all of them
+        else:
+            deltas += n > held
         hist = hist_of(n, dev)
         got = tpe.suggest_choices(table, hist, [n], seed + s, n_EI_candidates=C)[0]
         dc = devhist.columns(hist, eng.device)
         for label, v in vals.items():
-            t = np.log(v[:n]) if label == 'l' else v[:n]
-            keys, idx = dc.order(label).host()
+            o = dc.order(label)
+            assert o.n == held, (label, s, o.n, held)
+            t = np.log(v[:held]) if label == 'l' else v[:held]
+            keys, idx = o.host()
             want = np.argsort(t, kind='stable')
             np.testing.assert_array_equal(idx, want, err_msg='%s step %d' % (label, s))
             np.testing.assert_array_equal(keys, t[want], err_msg='%s step %d' % (label, s))
         fresh = tpe.suggest_choices(table, hist_of(n, {}), [n], seed + s, n_EI_candidates=C)[0]
-        assert got == fresh, (s, got, fresh)
+        assert got == fresh, (s, n, got, fresh)
+    assert deltas == 4 and n == Nt == held
     # the device rows of the final history against the oracle
     hist = hist_of(Nt, dev)
     fits = tpe._Fits(table, hist, H.split_below(hist, 0.25), 1.0, eng)

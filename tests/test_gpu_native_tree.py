@@ -295,10 +295,12 @@ def test_repeated_values_label_crossing_device_fit_min():
             if tpe.device_fits(n, nb, dmin):
                 dc = devhist.columns(hist, eng.device)
                 for label in ('u', 'v'):
-                    keys, idx = dc.order(label).host()
-                    w = np.argsort(vals[label][:n], kind='stable')
+                    o = dc.order(label)        # (delta mode: the last merged prefix)
+                    assert 0 < o.n <= n and n - o.n <= N.FIT_DELTA_MAX, (label, n, o.n)
+                    keys, idx = o.host()
+                    w = np.argsort(vals[label][:o.n], kind='stable')
                     np.testing.assert_array_equal(idx, w, err_msg='%s n=%d' % (label, n))
-                    np.testing.assert_array_equal(keys, vals[label][:n][w], err_msg='%s n=%d' % (label, n))
+                    np.testing.assert_array_equal(keys, vals[label][:o.n][w], err_msg='%s n=%d' % (label, n))
     finally:
         eng.device_fit_min = old
 

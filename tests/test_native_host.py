@@ -309,14 +309,26 @@ def test_pack_device_fit_resident_order():
         e = _engine('fp32')
         info = e._pack([LevelProblem(dev, 0, [9])], 4096, 1, 0, None)
         assert info.fit_total == K - 1 and info.fit_max_new == n_obs - n_sorted and info.fit_max_obs == n_obs
+        assert info.fit_max_merge == n_obs - n_sorted and info.fit_n_delta == 0
         j = _blob(e, info, info.off_fit, N.FIT_JOB_DTYPE, 1)[0]
         assert (j['ord_key_in'], j['ord_idx_in'], j['n_ord_in']) == (0xE0000000, 0xE1000000, n_sorted)
         assert (j['ord_key_out'] != 0) == out and (j['ord_idx_out'] != 0) == out
-    # an order whose output buffers are missing is refused
-    bad = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 2), None, 1.0,
-                               above_dev=(_FakeColumn(), n_obs, bidx, _NoOut(n_obs - 1)))
-    with pytest.raises(RuntimeError):
-        _engine('fp32')._pack([LevelProblem(bad, 0, [9])], 4096, 1, 0, None)
+    # delta mode: at most TPE_FIT_DELTA_MAX new observations and no output
+    # buffers — the job reads them beside the order (no merge)
+    for n_new in (1, N.FIT_DELTA_MAX):
+        dl = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 2), None, 1.0,
+                                  above_dev=(_FakeColumn(), n_obs, bidx, _NoOut(n_obs - n_new)))
+        e = _engine('fp32')
+        info = e._pack([LevelProblem(dl, 0, [9])], 4096, 1, 0, None)
+        j = _blob(e, info, info.off_fit, N.FIT_JOB_DTYPE, 1)[0]
+        assert j['n_ord_in'] == n_obs - n_new and j['ord_key_out'] == 0 and j['ord_idx_out'] == 0
+        assert info.fit_max_new == n_new and info.fit_max_merge == 0 and info.fit_n_delta == 1
+    # more new observations than that (or no order at all) without output buffers: refused
+    for n_in in (n_obs - N.FIT_DELTA_MAX - 1, 0):
+        bad = parzen.fit_posterior('uniform', dict(low=-1.0, high=2.0), rs.uniform(-1, 2, 2), None, 1.0,
+                                   above_dev=(_FakeColumn(), n_obs, bidx, _NoOut(n_in)))
+        with pytest.raises(RuntimeError):
+            _engine('fp32')._pack([LevelProblem(bad, 0, [9])], 4096, 1, 0, None)
 
 
 class _NoOut(_FakeOrder):

@@ -107,6 +107,13 @@ for task in "$@"; do
       head -30 $O/cfg5_app_prof_${TAG}.txt
       step 600 $O/cfg5app_${TAG}.err python bench.py --config 5 --appending --steps ${CFG_STEPS:-20} --warmup 2
       grep '^{' $O/cfg5app_${TAG}.err > $O/cfg5app_${TAG}.json; cat $O/cfg5app_${TAG}.json ;;
+    trace5)
+      # kernel trace of config 5 (APP5=--appending: the FMinIter flow)
+      rm -rf $O/trace5_${TAG}
+      step 600 $O/trace5_${TAG}.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace5_${TAG} -o run -- \
+          python3 bench.py --config 5 ${APP5:-} --steps ${CFG_STEPS:-10} --warmup 2
+      python3 tools/trace_summary.py $(find $O/trace5_${TAG} -name "*kernel_trace.csv") > $O/trace5_${TAG}_summary.txt
+      head -30 $O/trace5_${TAG}_summary.txt ;;
     packtime)
       # the headline level's packer sections on the box's host CPU (no GPU; the
       # TPE_PACK_TRACE library from tools/build_pack_trace.sh)
