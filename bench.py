@@ -466,7 +466,9 @@ def config_workload(config, rank, world, args):
         cap = N + args.steps + args.warmup + 64
         rs = np.random.RandomState(SEED)
         tids = np.arange(cap, dtype=np.int64)
-        cols = {k: np.empty(cap) for k in labels}
+        vals2d = np.empty((D, cap))                    # (one row per label: the evaluation writes a column)
+        cols = {k: vals2d[i] for i, k in enumerate(labels)}
+        row = {k: i for i, k in enumerate(labels)}
         for k in labels:
             cols[k][:N] = rs.uniform(-5, 5, N)
         rl = np.random.RandomState(SEED + 1)
@@ -481,9 +483,9 @@ def config_workload(config, rank, world, args):
             n = state['n']
             hist = History(tids[:n], losses[:n], {k: (tids[:n], cols[k][:n]) for k in labels}, dev=dev)
             cc = tpe.suggest_choices(table, hist, [n], SEED + i, n_EI_candidates=C, shard_labels=sid, columns=True)
-            v = cc.values[0]
-            for j, k in enumerate(cc.labels):       # the suggestion, evaluated (synthetic loss)
-                cols[k][n] = v[j]
+            if state.get('lab') != cc.labels:        # (the suggestion's label order -> rows, once)
+                state['lab'], state['ri'] = cc.labels, np.array([row[k] for k in cc.labels], dtype=np.int64)
+            vals2d[state['ri'], n] = cc.values[0]    # the suggestion, evaluated (synthetic loss)
             losses[n] = rl.uniform() + 1e-9 * n
             state['n'] = n + 1
             return D * C

@@ -12,7 +12,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
 ABI_VERSION = 21
-FIT_DELTA_MAX = 64             # TPE_FIT_DELTA_MAX: new observations read as a delta (no merge)
+FIT_DELTA_MAX = 16             # TPE_FIT_DELTA_MAX: new observations read as a delta (no merge)
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
 FAM_GAUSS, FAM_LOGGAUSS, FAM_QGAUSS, FAM_QLOGGAUSS, FAM_CATEGORICAL = range(5)

@@ -336,6 +336,7 @@ struct PaTask { int32_t li, side; int64_t i0, i1, off; };
 // terms (a and the unshifted c into scratch, the chunk's largest c), then rows
 // once the side's shift (the largest c of all chunks) is known.
 constexpr int64_t kFillChunk = 1024;
+constexpr int64_t kFitStageStretch = 9 * 256;    // tpe_kernels.hip kFitStretch (a chunk's staged stretch)
 constexpr int64_t kFillChunkMinLevel = 16384;   // the level's chunkable components, at least
 struct ChunkTask { int32_t li, side; int64_t i0, i1; int64_t scr; };
 
@@ -579,9 +580,11 @@ void fill_label(const FillCtx& cx, int32_t li) {
   const auto t_fill0 = std::chrono::steady_clock::now();
   struct Done {
     std::chrono::steady_clock::time_point t0; int32_t li;
-    ~Done() {
-      fprintf(stderr, "fill_label %d %.1f us\n", li,
-              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    ~Done() {                 // (TPE_PACK_TRACE_LABELS=1: each label's fill time too)
+      static const bool on = getenv("TPE_PACK_TRACE_LABELS") != nullptr;
+      if (on)
+        fprintf(stderr, "fill_label %d %.1f us\n", li,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     }
   } done_{t_fill0, li};
 #endif
@@ -1173,8 +1176,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         // scratch segment: the compacted above order, the new observations' merge
         // passes and the below positions all fit in it
         const int64_t n_new = L.n_obs - L.n_ord_in;
+        // (delta mode: the delta arrays, then a slot of kFitStageStretch entries per
+        // 2048-component chunk for the chunks whose stretch holds a delta entry)
+        const int64_t slots = !L.ord_key_out && n_new > 0 ? ((K + 2047) / 2048) * kFitStageStretch : 0;
         fit_seg.push_back(fit_seg.back() + std::max<int64_t>(std::max<int64_t>(K - 1, n_new),
-                                                             std::max<int64_t>(L.n_below, 64 + 2 * TPE_FIT_DELTA_MAX)));
+                                                             std::max<int64_t>(L.n_below, 64 + 2 * TPE_FIT_DELTA_MAX + slots)));
         fit_max_new = std::max(fit_max_new, n_new);
         if (L.ord_key_out) fit_max_merge = std::max(fit_max_merge, n_new);
         else fit_n_delta += n_new > 0;          // (delta mode)

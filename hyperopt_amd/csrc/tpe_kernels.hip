@@ -3914,6 +3914,34 @@ __global__ __launch_bounds__(kOrdChunkThreads) void k_ord_chunks(const tpe_fit_j
   for (int i = threadIdx.x; i < n; i += kOrdChunkThreads) { ok[i] = sk[i]; ov[i] = sv[i]; }
 }
 
+// delta mode only (no job of the level merges): each job's few new
+// observations sorted by rank (one wave; every pair compared) and placed among
+// the resident ones (their virtual positions) — k_ord_chunks' delta branch
+// without its 96-KiB LDS sort
+__global__ __launch_bounds__(64) void k_ord_delta(const tpe_fit_job* __restrict__ J, double* __restrict__ dkeys,
+                                                  uint32_t* __restrict__ dvals) {
+  const tpe_fit_job& j = J[blockIdx.x];
+  if (!fit_delta(j)) return;
+  const int n = (int)(j.n_obs - j.n_ord_in), i = threadIdx.x;
+  __shared__ double sk[kFitMaxDelta];
+  if (i < n) sk[i] = fit_coord(j, j.n_ord_in + i);
+  __syncthreads();
+  if (i >= n) return;
+  const double t = sk[i];
+  const uint32_t v = (uint32_t)(j.n_ord_in + i);
+  int r = 0;                                          // its rank among the new ones (indices break ties)
+  for (int q = 0; q < n; ++q) r += ord_lt(sk[q], (uint32_t)(j.n_ord_in + q), t, v);
+  int64_t lo = 0, hi = j.n_ord_in;                    // resident entries before it
+  while (lo < hi) {
+    const int64_t md = (lo + hi) >> 1;
+    if (ord_lt(j.ord_key_in[md], j.ord_idx_in[md], t, v)) lo = md + 1;
+    else hi = md;
+  }
+  delta_keys(j, dkeys)[r] = t;
+  delta_idx(j, dvals)[r] = v;
+  delta_pos(j, dvals)[r] = (uint32_t)(lo + r);
+}
+
 // merge-path merge, one tile of kMergeTile outputs per workgroup: the tile's
 // A and B ranges (found by a binary search on each tile edge's diagonal) are
 // staged in LDS, each thread merges kMergePer outputs from its own diagonal,
@@ -4067,7 +4095,8 @@ constexpr int kFitHdrPos = 0, kFitHdrStats = 1, kFitHdrGrid = 6, kFitHdrParts = 
 // of prior_mu, tpe.py:427-431): the observations < prior_mu in the whole order
 // less the below ones
 constexpr int kFitMaxBelow = 64;
-static_assert(kFitMaxBelow == kFitMaxBelow_ && kFitMaxDelta <= kFitMaxBelow, "one delta entry per thread");
+static_assert(kFitMaxBelow == kFitMaxBelow_ && kFitMaxDelta <= kFitMaxBelow && kFitMaxDelta <= 64,
+              "one delta entry per thread");
 __global__ __launch_bounds__(kFitMaxBelow) void k_ord_below(const tpe_fit_job* __restrict__ J,
                                                             const int32_t* __restrict__ below_idx,
                                                             uint32_t* __restrict__ adj, double* __restrict__ hdr,
@@ -4291,13 +4320,11 @@ __device__ __forceinline__ void fit_stage_put(int64_t f, double kv, uint32_t o, 
   lrk[i - c0 + 1] = o - k;
 }
 
-// the stretch without delta entries: every load issued first
-__device__ __forceinline__ void fit_stage_plain(const VOrd& V, const uint32_t* s_bp, const uint32_t* s_bi,
-                                                const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1, int64_t pos,
-                                                int la, int lb, int64_t fa, int64_t fb, int da, double* lmu,
-                                                uint32_t* lrk) {
-  const double* __restrict__ ok = V.ok - da;
-  const uint32_t* __restrict__ ov = V.ov - da;
+// the stretch's entries from ok[f], ov[f] (f in [fa, fb)): every load issued first
+__device__ __forceinline__ void fit_stage_plain(const double* __restrict__ ok, const uint32_t* __restrict__ ov,
+                                                const uint32_t* s_bp, const uint32_t* s_bi, const uint32_t* s_bk,
+                                                int bsh, int64_t c0, int64_t c1, int64_t pos, int la, int lb,
+                                                int64_t fa, int64_t fb, double* lmu, uint32_t* lrk) {
   double kv[kFitStagePer];
   uint32_t iv[kFitStagePer];
 #pragma unroll
@@ -4313,29 +4340,43 @@ __device__ __forceinline__ void fit_stage_plain(const VOrd& V, const uint32_t* s
   }
 }
 
-// the stretch holding delta entries (a few chunks of a job in delta mode): one
-// entry at a time, few registers
-__device__ __forceinline__ void fit_stage_delta(const VOrd& V, const uint32_t* s_bp, const uint32_t* s_bi,
-                                                const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1, int64_t pos,
-                                                int la, int lb, int64_t fa, int64_t fb, int da, int db, double* lmu,
-                                                uint32_t* lrk) {
-#pragma unroll 1
+// a stretch holding delta entries (a few chunks of a job in delta mode): the
+// virtual order's entries [fa, fb) gathered into the job's fit scratch (the
+// chunk's slot, see fit_slot) by k_fit_gather, where k_fit_main's staging then
+// reads them — so the staging stays the common case's code and registers.
+constexpr int kFitStretch = kFitStagePer * kFitThreads;
+static_assert(kFitStretch == 2304 && kFitChunk == 2048, "tpe_host.cpp sizes the delta slots (kFitStageStretch)");
+__device__ __forceinline__ void fit_gather_stretch(const VOrd& V, int64_t fa, int64_t fb, int da, int db,
+                                                   double* __restrict__ sk, uint32_t* __restrict__ sv) {
+  double kv[kFitStagePer];
+  uint32_t iv[kFitStagePer];
+#pragma unroll
+  for (int e = 0; e < kFitStagePer; ++e) {            // every load issued first
+    const int64_t f = fa + e * kFitThreads + threadIdx.x;
+    if (f < fb) {
+      int c = da;
+      bool in_delta = false;
+      for (int k = da; k < db; ++k) {                 // uniform trip count
+        const int64_t p = V.dp[k];
+        c += p < f;
+        in_delta |= p == f;
+      }
+      kv[e] = in_delta ? V.dk[c] : V.ok[f - c];
+      iv[e] = in_delta ? V.dv[c] : V.ov[f - c];
+    }
+  }
+#pragma unroll
   for (int e = 0; e < kFitStagePer; ++e) {
     const int64_t f = fa + e * kFitThreads + threadIdx.x;
-    if (f >= fb) break;
-    int c = da;
-    bool in_delta = false;
-    for (int k = da; k < db; ++k) {                   // uniform trip count
-      const int64_t p = V.dp[k];
-      c += p < f;
-      in_delta |= p == f;
-    }
-    double kv;
-    uint32_t o;
-    if (in_delta) { kv = V.dk[c]; o = V.dv[c]; }
-    else { kv = V.ok[f - c]; o = V.ov[f - c]; }
-    fit_stage_put(f, kv, o, s_bp, s_bi, s_bk, bsh, c0, c1, pos, la, lb, lmu, lrk);
+    if (f < fb) { sk[f - fa] = kv[e]; sv[f - fa] = iv[e]; }
   }
+}
+
+// a delta-mode job's chunk slot for its gathered stretch: in its fit scratch
+// segment after the delta arrays (fit_keys_sorted / fit_vals_sorted; the host
+// sizes the segment for one slot per chunk)
+__device__ __forceinline__ int64_t fit_slot(const tpe_fit_job& j, int64_t chunk) {
+  return j.seg_off + kFitMaxBelow_ + 2 * kFitMaxDelta + chunk * kFitStretch;
 }
 
 // The stretch of the (virtual) order holding a chunk's above observations
@@ -4367,21 +4408,17 @@ __device__ __forceinline__ FitStretch fit_stretch(const tpe_fit_job& j, const VO
   return t;
 }
 
-// k_fit_main's modes: every job's order as it is (no delta anywhere), or a
-// level with delta-mode jobs run in two launches — the chunks whose stretch
-// holds no delta entry (the order shifted by the ones before it), then the few
-// that hold some (staged one entry at a time, more registers: its own instance)
-enum { kFitPlain = 0, kFitShift = 1, kFitDeltaChunks = 2 };
-
-template <int MODE>
+template <bool DELTA>
 __device__ void fit_stage_rows(const tpe_fit_job& j, const VOrd& V, const FitStretch& t, const uint32_t* s_bp,
                                const uint32_t* s_bi, const uint32_t* s_bk, int bsh, int64_t c0, int64_t c1,
-                               int64_t pos, double* lmu, uint32_t* lrk) {
-  if (MODE == kFitDeltaChunks)
-    fit_stage_delta(V, s_bp, s_bi, s_bk, bsh, c0, c1, pos, t.la, t.lb, t.fa, t.fb, t.da, t.db, lmu, lrk);
-  else
-    fit_stage_plain(V, s_bp, s_bi, s_bk, bsh, c0, c1, pos, t.la, t.lb, t.fa, t.fb, MODE == kFitPlain ? 0 : t.da, lmu,
-                    lrk);
+                               int64_t pos, double* lmu, uint32_t* lrk, const double* dkeys, const uint32_t* dvals) {
+  const double* ok = V.ok - t.da;                    // (the order shifted by the delta entries before the stretch)
+  const uint32_t* ov = V.ov - t.da;
+  if (DELTA && t.da != t.db) {                       // (the stretch k_fit_gather gathered)
+    ok = dkeys + fit_slot(j, (int64_t)blockIdx.x) - t.fa;
+    ov = dvals + fit_slot(j, (int64_t)blockIdx.x) - t.fa;
+  }
+  fit_stage_plain(ok, ov, s_bp, s_bi, s_bk, bsh, c0, c1, pos, t.la, t.lb, t.fa, t.fb, lmu, lrk);
   if (threadIdx.x == 0 && pos >= c0 - 1 && pos <= c1) lmu[pos - c0 + 1] = j.prior_mu;
 }
 
@@ -4456,6 +4493,45 @@ __device__ __forceinline__ double* wide_sigmas(const tpe_fit_job& j, double* scr
   return scratch + j.seg_off + kFitHdrParts + 12 * nc;
 }
 
+// Delta mode: the stretches of the chunks that hold delta entries gathered
+// into their slots, before k_fit_main.  Workgroup (k, job): delta entry k's
+// chunk by its above index and the two beside it (the stretches overlap), each
+// gathered when k is the first delta entry of its stretch — every such chunk
+// exactly once.
+__global__ __launch_bounds__(kFitThreads) void k_fit_gather(const tpe_fit_job* __restrict__ J,
+                                                            const int32_t* __restrict__ below_idx,
+                                                            const uint32_t* __restrict__ adj,
+                                                            const double* __restrict__ scratch,
+                                                            double* __restrict__ dkeys, uint32_t* __restrict__ dvals) {
+  const tpe_fit_job& j = J[blockIdx.y];
+  if (!fit_delta(j)) return;
+  const int nd = (int)(j.n_obs - j.n_ord_in), k = (int)blockIdx.x;
+  if (k >= nd) return;
+  __shared__ uint32_t s_bp[kFitMaxBelow], s_bi[kFitMaxBelow];
+  __shared__ double l_dk[kFitMaxDelta];
+  __shared__ uint32_t l_dv[kFitMaxDelta], l_dp[kFitMaxDelta];
+  fit_below_lds(j, below_idx, adj, s_bp, s_bi);
+  const VOrd V = vord_lds(j, dkeys, dvals, l_dk, l_dv, l_dp);
+  __syncthreads();
+  const int64_t n = j.n_obs - j.n_below, K = n + 1;
+  const int64_t pos = (int64_t)scratch[j.seg_off + kFitHdrPos];
+  const int64_t p = V.dp[k];
+  int lo = 0, hi = j.n_below;                       // below positions before p
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if ((int64_t)s_bp[m] < p) lo = m + 1; else hi = m;
+  }
+  const int64_t q = p - lo, i = q + (q >= pos);
+  for (int side = -1; side <= 1; ++side) {
+    const int64_t c = i / kFitChunk + side;
+    if (c < 0 || c * kFitChunk >= K) continue;
+    const int64_t c0 = c * kFitChunk, c1 = min(c0 + kFitChunk, K);
+    const FitStretch t = fit_stretch(j, V, s_bp, c0, c1, n);
+    if (t.da != k || t.db == t.da) continue;        // (another workgroup's chunk, or none)
+    fit_gather_stretch(V, t.fa, t.fb, t.da, t.db, dkeys + fit_slot(j, c), dvals + fit_slot(j, c));
+  }
+}
+
 // One pass per chunk: its rows {mu_hi, mu_lo, a, c = log2(w / sigma) - shift}
 // (every one finite; k_fit_wide marks the wide ones), its wide candidates, its
 // statistics (normaliser W, acceptance mass M, the wide-threshold counts) and
@@ -4464,14 +4540,16 @@ __device__ __forceinline__ double* wide_sigmas(const tpe_fit_job& j, double* scr
 // the buckets whose answer lies in it (a binary search over its staged means) —
 // the buckets g with mu32[c0 - 1] < edge_g <= mu32[c1 - 1] (the last chunk:
 // every g from there up, K when no mean reaches edge_g).
-template <int MODE>
+// (DELTA: a level with delta-mode jobs; the instance for one without keeps the
+// common case's code)
+template <bool DELTA>
 __global__ __launch_bounds__(kFitThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_fit_main(const tpe_fit_job* __restrict__ J,
                                                           const int32_t* __restrict__ below_idx,
                                                           const uint32_t* __restrict__ adj,
                                                           double* __restrict__ scratch,
                                                           uint32_t* __restrict__ wide_scratch,
                                                           float4* __restrict__ comp, int32_t* __restrict__ grid,
-                                                          const double* __restrict__ dkeys) {
+                                                          const double* __restrict__ dkeys, const uint32_t* __restrict__ dvals) {
   const tpe_fit_job& j = J[blockIdx.y];
   const int64_t n = j.n_obs - j.n_below, K = n + 1, c0 = (int64_t)blockIdx.x * kFitChunk;
   if (c0 >= K) return;
@@ -4483,17 +4561,15 @@ __global__ __launch_bounds__(kFitThreads) __attribute__((amdgpu_waves_per_eu(6))
   __shared__ double l_dk[kFitMaxDelta];
   __shared__ uint32_t l_dv[kFitMaxDelta], l_dp[kFitMaxDelta];
   fit_below_lds(j, below_idx, adj, s_bp, s_bi);
-  const VOrd V = MODE != kFitPlain ? vord_lds(j, dkeys, adj, l_dk, l_dv, l_dp)
-                                   : VOrd{ord_keys(j), ord_idx(j), l_dk, l_dv, l_dp, 0};
+  const VOrd V = DELTA ? vord_lds(j, dkeys, dvals, l_dk, l_dv, l_dp) : VOrd{ord_keys(j), ord_idx(j), l_dk, l_dv, l_dp, 0};
   __syncthreads();
   const FitStretch t = fit_stretch(j, V, s_bp, c0, c1, n);
-  if (MODE != kFitPlain && (MODE == kFitDeltaChunks) != (t.da != t.db)) return;   // (the other launch's chunk)
   const int bsh = fit_bucket_shift(j.n_obs);
   fit_rank_buckets(j.n_below, s_bi, bsh, s_bk);
   __syncthreads();
   const double* __restrict__ hdr = scratch + j.seg_off;
   const int64_t pos = (int64_t)hdr[kFitHdrPos];
-  fit_stage_rows<MODE>(j, V, t, s_bp, s_bi, s_bk, bsh, c0, c1, pos, lmu, lrk);
+  fit_stage_rows<DELTA>(j, V, t, s_bp, s_bi, s_bk, bsh, c0, c1, pos, lmu, lrk, dkeys, dvals);
   __syncthreads();
   // the bandwidth and weight rules of fit_ctx (tpe.py:381-394, 441-470) over
   // the staged means, the prior already in place
@@ -4938,8 +5014,11 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
     // the observations appended since each order was written: sorted chunks,
     // merged pairwise until one run per job, then merged into the resident order
     const int64_t chunks = (b->fit_max_new + kOrdChunk - 1) / kOrdChunk;
-    TPE_LAUNCH(k_ord_chunks, dim3((unsigned)chunks, b->n_fit), dim3(kOrdChunkThreads), 0, s, b->fit, b->fit_keys,
-               b->fit_vals, b->fit_keys_sorted, b->fit_vals_sorted);
+    if (b->fit_max_merge == 0)                // (every job with new observations in delta mode)
+      TPE_LAUNCH(k_ord_delta, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys_sorted, b->fit_vals_sorted);
+    else
+      TPE_LAUNCH(k_ord_chunks, dim3((unsigned)chunks, b->n_fit), dim3(kOrdChunkThreads), 0, s, b->fit, b->fit_keys,
+                 b->fit_vals, b->fit_keys_sorted, b->fit_vals_sorted);
     if ((rc = hip_check("tpe_fit_above/chunks"))) return rc;
     double* src_k = b->fit_keys;
     uint32_t* src_v = b->fit_vals;
@@ -4970,17 +5049,17 @@ int tpe_fit_above(const tpe_batch* b, void* stream) {
   const unsigned chunks_k = (unsigned)((b->fit_max_obs + 1 + kFitChunk - 1) / kFitChunk);
   // the wide candidates' counters (one per job, at its segment's head)
   TPE_LAUNCH(k_fit_wide_reset, dim3((unsigned)((b->n_fit + 255) / 256)), dim3(256), 0, s, b->fit, b->n_fit, b->fit_vals);
-  if (b->fit_n_delta > 0) {                   // (jobs in delta mode)
-    TPE_LAUNCH(k_fit_main<kFitShift>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
-               b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid),
-               (const double*)b->fit_keys_sorted);
-    TPE_LAUNCH(k_fit_main<kFitDeltaChunks>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx,
-               adj, b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid),
-               (const double*)b->fit_keys_sorted);
+  if (b->fit_n_delta > 0) {                   // (jobs in delta mode: their delta chunks' stretches first)
+    const unsigned nd = (unsigned)std::min<int64_t>(b->fit_max_new, kFitMaxDelta);
+    TPE_LAUNCH(k_fit_gather, dim3(nd, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
+               (const double*)b->fit_keys, b->fit_keys_sorted, b->fit_vals_sorted);
+    TPE_LAUNCH(k_fit_main<true>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
+               b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid), b->fit_keys_sorted,
+               b->fit_vals_sorted);
   } else {
-    TPE_LAUNCH(k_fit_main<kFitPlain>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
-               b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid),
-               (const double*)b->fit_keys_sorted);
+    TPE_LAUNCH(k_fit_main<false>, dim3(chunks_k, b->n_fit), dim3(kFitThreads), 0, s, b->fit, b->below_idx, adj,
+               b->fit_keys, b->fit_vals, (float4*)b->comp32, const_cast<int32_t*>(b->grid), b->fit_keys_sorted,
+               b->fit_vals_sorted);
   }
   TPE_LAUNCH(k_fit_combine, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->fit_keys);
   TPE_LAUNCH(k_fit_wide, dim3(b->n_fit), dim3(64), 0, s, b->fit, b->below_idx, adj, b->fit_keys, b->fit_vals,

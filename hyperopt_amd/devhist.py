@@ -194,6 +194,7 @@ class DeviceColumns(object):
         self.n = np.zeros(0, dtype=np.int64)        # values uploaded per slot
         self.orders = _Orders(device, self)
         self._last_labels, self._last_slots = None, None
+        self._pin = self._dbuf = self._ev = None      # (_scatter's staging)
 
     def _add(self, label):
         s = self.slot[label] = len(self.views)
@@ -259,10 +260,34 @@ class DeviceColumns(object):
                 vals = np.concatenate([values[i][ml[i]:nl[i]] for i in up.tolist()]).astype(np.float64, copy=False)
             su = slots[up]
             pos = _positions(self.off[su] + m[up], nv[up] - m[up])
-            self.store[torch.from_numpy(pos).to(self.device)] = torch.from_numpy(vals).to(self.device)
+            self._scatter(pos, vals)
             self.n[su] = nv[up]
             self.version += 1
         return slots
+
+    def _scatter(self, pos, vals):
+        """store[pos] = vals: on a GPU both go up in ONE asynchronous copy from
+        a pinned staging buffer (positions as exact float64), whose reuse waits
+        for the previous copy's event."""
+        k = len(vals)
+        if self.device.type != 'cuda':
+            self.store[torch.from_numpy(pos)] = torch.from_numpy(vals)
+            return
+        if self._pin is None or self._pin.numel() < 2 * k:
+            cap = max(2 * k, 8192)
+            self._pin = torch.empty(cap, dtype=torch.float64, pin_memory=True)
+            self._dbuf = torch.empty(cap, dtype=torch.float64, device=self.device)
+            self._ev = None
+        if self._ev is not None:
+            self._ev.synchronize()                 # (the last copy out of the staging buffer has run)
+        h = self._pin.numpy()
+        h[:k] = vals
+        h[k:2 * k] = pos
+        d = self._dbuf[:2 * k]
+        d.copy_(self._pin[:2 * k], non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+        self.store[d[k:].long()] = d[:k]
 
     def columns(self, items):
         """Device tensors (store segments) whose first ``len(values)`` entries

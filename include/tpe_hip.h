@@ -372,7 +372,7 @@ typedef struct tpe_result {
  * The host reserves above_off[0 .. K) + wide_off[0 .. 16) rows and grid_n + 1
  * grid entries (K = n_obs - n_below + 1, grid_n = min(4096, 4K)).
  */
-#define TPE_FIT_DELTA_MAX 64
+#define TPE_FIT_DELTA_MAX 16
 typedef struct tpe_fit_job {
   const double* obs;     /* device: the label's observations in tid order, in the kernel
                             coordinate t (x, or the caller's np.log(x) for LOGGAUSS) */
@@ -436,7 +436,8 @@ typedef struct tpe_batch {
   const int32_t* below_idx;   /* below indices of every job                        */
   const int64_t* fit_seg;     /* [n_fit + 1] segment offsets into the fit scratch: a job's
                                  segment holds max(n_obs - n_below, n_obs - n_ord_in, n_below,
-                                 64 + 2 * TPE_FIT_DELTA_MAX) */
+                                 64 + 2 * TPE_FIT_DELTA_MAX [+ 2304 per 2048 components of a
+                                 delta-mode job]) */
   int64_t fit_total;          /* fit_seg[n_fit]                                    */
   double* fit_keys; double* fit_keys_sorted;        /* [fit_total] scratch (ping-pong) */
   uint32_t* fit_vals; uint32_t* fit_vals_sorted;    /* [fit_total]                */

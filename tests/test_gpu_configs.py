@@ -294,7 +294,7 @@ def test_device_value_order_incremental():
     """The resident device value order of device-fitted labels (tpe_fit_above:
     chunk sort -> merge passes -> merge into the resident order, or DELTA MODE:
     at most TPE_FIT_DELTA_MAX new observations read beside the order as one
-    virtual order, no merge) over suggests that append 200, 1, 1, 30, 33, 64
+    virtual order, no merge) over suggests that append 200, 1, 1, 10, 5, 16
     and 1 observations (FMinIter appends one per suggest): after every suggest
     each label's order is np.argsort(kind='stable') of the kernel coordinate of
     the observations it holds (ties by tid order; repeated values included) —
@@ -305,9 +305,9 @@ def test_device_value_order_incremental():
     from hyperopt_amd.engine import LevelProblem, get_engine
     eng = get_engine()
     N0, C, seed = 20000, 4096, 17
-    steps = [0, 200, 1, 1, 30, 33, 64, 1]
+    steps = [0, 200, 1, 1, 10, 5, 16, 1]
     Nt = N0 + sum(steps)
-    assert N0 - 25 >= eng.device_fit_min and N.FIT_DELTA_MAX == 64
+    assert N0 - 25 >= eng.device_fit_min and N.FIT_DELTA_MAX == 16
     table = base.Domain(lambda d: 0.0, {'u': hp.uniform('u', -5, 5), 'l': hp.loguniform('l', -3, 2)}).table
     rs = np.random.RandomState(3)
     u = rs.uniform(-5, 5, Nt)
@@ -317,7 +317,7 @@ def test_device_value_order_incremental():
     lv[::13] = np.round(lv[::13], 2)
     tids = np.arange(Nt, dtype=np.int64)
     losses = rs.uniform(size=Nt) + 1e-9 * tids
-    losses[N0 + 230] = -1.0                          # a new observation in the below set (delta mode)
+    losses[N0 + 210] = -1.0                          # a new observation in the below set (delta mode)
     dev = {}                                         # the Trials cache's device state, kept across suggests
     vals = {'u': u, 'l': lv}
 

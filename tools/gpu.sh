@@ -116,10 +116,11 @@ for task in "$@"; do
       head -30 $O/trace5_${TAG}_summary.txt ;;
     packtime)
       # the headline level's packer sections on the box's host CPU (no GPU; the
-      # TPE_PACK_TRACE library from tools/build_pack_trace.sh)
+      # TPE_PACK_TRACE library from tools/build_pack_trace.sh; PACK_TOOL /
+      # PACK_ARGS: another level, e.g. pack_time5.py "1000 100000 30" for config 5)
       for t in ${PACK_THREADS:-16}; do
         TPE_HOST_THREADS=$t TPE_PACK_LIB=$PWD/hyperopt_amd/libtpe_host_ptrace.so step 120 $O/packtime_${TAG}_$t.txt \
-            python tools/pack_time3.py 400
+            python tools/${PACK_TOOL:-pack_time3.py} ${PACK_ARGS:-400}
         python3 tools/pack_sections.py $O/packtime_${TAG}_$t.txt | tee -a $O/packtime_${TAG}_$t.txt
       done ;;
     cfgprof)
