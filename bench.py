@@ -460,7 +460,7 @@ def config_workload(config, rank, world, args):
         # follows the evaluation of the previous one, appended as one observation
         # of every label — the history views grow by one and share the device
         # columns and resident value orders (History.dev), as a Trials cache's do
-        from hyperopt_amd.history import History
+        from hyperopt_amd.history import DenseLayout, DenseObs, History
         D, N, C = args.dims, args.history5, 4096
         labels = ['x%04d' % i for i in range(D)]
         cap = N + args.steps + args.warmup + 64
@@ -469,6 +469,7 @@ def config_workload(config, rank, world, args):
         vals2d = np.empty((D, cap))                    # (one row per label: the evaluation writes a column)
         cols = {k: vals2d[i] for i, k in enumerate(labels)}
         row = {k: i for i, k in enumerate(labels)}
+        layout = DenseLayout(labels)
         for k in labels:
             cols[k][:N] = rs.uniform(-5, 5, N)
         rl = np.random.RandomState(SEED + 1)
@@ -481,7 +482,8 @@ def config_workload(config, rank, world, args):
 
         def step(i):
             n = state['n']
-            hist = History(tids[:n], losses[:n], {k: (tids[:n], cols[k][:n]) for k in labels}, dev=dev)
+            # (the columnar history: every label a row of one matrix — history.DenseObs)
+            hist = History(tids[:n], losses[:n], DenseObs(layout, vals2d, tids[:n]), dev=dev)
             cc = tpe.suggest_choices(table, hist, [n], SEED + i, n_EI_candidates=C, shard_labels=sid, columns=True)
             if state.get('lab') != cc.labels:        # (the suggestion's label order -> rows, once)
                 state['lab'], state['ri'] = cc.labels, np.array([row[k] for k in cc.labels], dtype=np.int64)

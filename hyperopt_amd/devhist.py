@@ -222,7 +222,7 @@ class DeviceColumns(object):
         self.views = [store[o:o + c] for o, c in zip(off.tolist(), cap.tolist())]
         self.version += 1
 
-    def upload(self, labels, values, lengths=None):
+    def upload(self, labels, values, lengths=None, dense=None):
         """Make the column of labels[i] hold values[i] (a float64 array that
         extends what earlier calls for the label passed; a shorter one — another
         History's — starts the label over, its order too); the values not
@@ -238,7 +238,11 @@ class DeviceColumns(object):
                     s = get(labels[i])
                     slots[i] = s if s is not None else self._add(labels[i])
             self._last_labels, self._last_slots = labels, slots
-        nv = np.fromiter(map(len, values), dtype=np.int64, count=len(values)) if lengths is None else lengths
+        if dense is not None:
+            matrix, rows, n_dense = dense
+            nv = np.full(len(labels), n_dense, dtype=np.int64)
+        else:
+            nv = np.fromiter(map(len, values), dtype=np.int64, count=len(values)) if lengths is None else lengths
         m = self.n[slots]
         short = m > nv
         if short.any():
@@ -252,18 +256,32 @@ class DeviceColumns(object):
             np.maximum.at(want, slots, nv)
             self._relayout(want)
         up = np.flatnonzero(nv > m)
-        if len(up):
+        if len(up) and dense is not None:
+            m0 = int(m[up[0]])
+            if len(up) == len(m) and bool((m == m0).all()):
+                vals = matrix[rows, m0:n_dense].ravel()          # (row by row: _positions' order)
+            else:
+                vals = np.concatenate([matrix[rows[i], int(m[i]):n_dense] for i in up.tolist()])
+        elif len(up):
             try:                                 # (float64 columns: their new values gathered natively)
                 vals = _hostaddr.tails(values, m, nv)
             except (ValueError, AttributeError):
                 ml, nl = m.tolist(), nv.tolist()
                 vals = np.concatenate([values[i][ml[i]:nl[i]] for i in up.tolist()]).astype(np.float64, copy=False)
+        if len(up):
             su = slots[up]
             pos = _positions(self.off[su] + m[up], nv[up] - m[up])
             self._scatter(pos, vals)
             self.n[su] = nv[up]
             self.version += 1
         return slots
+
+    def upload_rows(self, labels, matrix, rows, n):
+        """``upload`` for a dense history: the column of labels[i] holds
+        matrix[rows[i], :n] (history.DenseObs) — the new values of every label
+        gathered as one 2-D slice when they start at the same index (FMinIter's
+        appends), else per label."""
+        return self.upload(labels, (), dense=(matrix, rows, n))
 
     def _scatter(self, pos, vals):
         """store[pos] = vals: on a GPU both go up in ONE asynchronous copy from

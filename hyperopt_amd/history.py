@@ -37,6 +37,65 @@ from . import base
 _CACHES = weakref.WeakKeyDictionary()
 
 
+class DenseLayout(object):
+    """The labels of a dense history (DenseObs) and their matrix rows, kept
+    across the histories of one growing matrix (memos of row indices live here)."""
+    __slots__ = ('labels', 'rows', 'memo')
+
+    def __init__(self, labels):
+        self.labels = list(labels)
+        self.rows = {k: i for i, k in enumerate(self.labels)}
+        self.memo = {}
+
+    def row_index(self, labels):
+        """Row indices (int64) of ``labels`` (memoised by the list object: pass
+        the same list to hit)."""
+        m = self.memo.get(id(labels))
+        if m is None or m[0] is not labels:
+            m = self.memo[id(labels)] = (labels, np.array([self.rows[k] for k in labels], dtype=np.int64))
+        return m[1]
+
+
+class DenseObs(object):
+    """Observations of a flat space whose labels are all observed in every
+    trial (a columnar caller's history, config 5): one float64 row per label of
+    a C-contiguous matrix [labels x capacity], the first n values in tid order,
+    and the trials' tids shared by every label.  A mapping label -> (tids,
+    values) like History.obs (views made on access), which tpe._tree_labels
+    reads as the matrix itself — no per-label Python for a thousand labels."""
+    __slots__ = ('layout', 'matrix', 'tids', 'n')
+
+    def __init__(self, layout, matrix, tids):
+        assert matrix.dtype == np.float64 and matrix.flags.c_contiguous and matrix.shape[0] == len(layout.labels)
+        assert matrix.shape[1] >= len(tids)
+        self.layout, self.matrix, self.tids, self.n = layout, matrix, tids, len(tids)
+
+    def __getitem__(self, label):
+        return self.tids, self.matrix[self.layout.rows[label], :self.n]
+
+    def get(self, label, default=None):
+        i = self.layout.rows.get(label)
+        return default if i is None else (self.tids, self.matrix[i, :self.n])
+
+    def __contains__(self, label):
+        return label in self.layout.rows
+
+    def __iter__(self):
+        return iter(self.layout.labels)
+
+    def __len__(self):
+        return len(self.layout.labels)
+
+    def keys(self):
+        return list(self.layout.labels)
+
+    def items(self):
+        return [(k, self[k]) for k in self.layout.labels]
+
+    def values(self):
+        return [self[k] for k in self.layout.labels]
+
+
 class History(object):
     """tids (int64, ascending), losses (float64, +inf for missing), and per
     label the (tid, value) observations in tid order.  ``dev`` holds the

@@ -396,6 +396,27 @@ def _tree_labels(table, hist, engine=None, remote=()):
         rec = arr[ix]
         rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
     devs = None
+    dense = hist.obs if isinstance(hist.obs, _history.DenseObs) else None
+    if glab and dense is not None and dev_min is not None and dense.n >= dev_min and not remote \
+            and not glogc.any():
+        # a dense history (every label in every trial, one matrix row each): the
+        # device labels' records straight from the matrix, no per-label Python
+        n = dense.n
+        ri = dense.layout.row_index(glab)
+        m = dense.matrix
+        slots = dc.upload_rows(glab, m, ri, n)
+        keep += [dense.tids, m, dc.store]
+        ns = np.full(len(glab), n, dtype=np.int64)
+        kin, iin, n_in, kout, iout = dc.orders.ptrs_many(slots, ns)
+        ta = np.ascontiguousarray(dense.tids, dtype=np.int64)
+        if ta is not dense.tids:
+            keep.append(ta)
+        for f, v in (('n_obs', n), ('tids', ta.ctypes.data), ('values', m.ctypes.data + m.strides[0] * ri),
+                     ('order', 0), ('dev_obs', dc.addresses(slots)), ('ord_key_in', kin), ('ord_idx_in', iin),
+                     ('n_ord_in', n_in), ('ord_key_out', kout), ('ord_idx_out', iout)):
+            arr[f][gix] = v
+        devs = (gix, slots, ns, dc.orders)
+        glab = ()
     if glab:
         obs = hist.obs
         pairs = [obs[k] for k in glab]

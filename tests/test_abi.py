@@ -362,3 +362,42 @@ def test_suggest_tree_sizes_device_fits_without_gpu():
     arr2 = tpe._tree_labels(table, hist, _Eng())[0]
     assert arr2 is not arr and arr2[0]['n_ord_in'] == 400 and arr2[0]['ord_key_out'] == 0
     assert devhist.columns(hist, torch.device('cpu')).order('x0').n == 400
+
+
+def test_tree_labels_dense_history_matches_dict_history():
+    """A dense history (history.DenseObs: every label a row of one matrix) gives
+    the same tree records as the same columns passed as a dict — device
+    columns, resident-order pointers and host addresses alike — appended to
+    step by step (FMinIter's one observation per label)."""
+    import bench
+    import torch
+    from hyperopt_amd import tpe
+    from hyperopt_amd.history import DenseLayout, DenseObs, History
+
+    class _Eng(object):
+        precision, device_fit_min, device = 'fp32', 100, torch.device('cpu')
+    labels = ['x%d' % i for i in range(5)]
+    table = bench.flat_uniform_table(labels)
+    rs = np.random.RandomState(2)
+    cap, N0 = 500, 300
+    m = np.ascontiguousarray(rs.uniform(-5, 5, (len(labels), cap)))
+    tids = np.arange(cap, dtype=np.int64)
+    losses = rs.uniform(size=cap)
+    layout = DenseLayout(labels)
+    dev_a, dev_b = {}, {}
+    for n in (N0, N0 + 1, N0 + 2, N0 + 40):
+        ha = History(tids[:n], losses[:n], DenseObs(layout, m, tids[:n]), dev=dev_a)
+        hb = History(tids[:n], losses[:n], {k: (tids[:n], m[i, :n]) for i, k in enumerate(labels)}, dev=dev_b)
+        ta, tb = tpe._tree_labels(table, ha, _Eng()), tpe._tree_labels(table, hb, _Eng())
+        ra, rb = ta[0], tb[0]
+        for f in ('n_obs', 'tids', 'values', 'order', 'n_ord_in'):
+            np.testing.assert_array_equal(ra[f], rb[f], err_msg='%s n=%d' % (f, n))
+        for f in ('dev_obs', 'ord_key_in', 'ord_key_out'):
+            np.testing.assert_array_equal(ra[f] != 0, rb[f] != 0, err_msg=f)
+        ca, cb = dev_a['cpu'], dev_b['cpu']
+        for k in labels:
+            np.testing.assert_array_equal(ca.view(k)[:n].numpy(), cb.view(k)[:n].numpy())
+            assert ca.count(k) == cb.count(k) == n
+        for t in (ta, tb):
+            ixs, slots, ns, g = t[2]
+            g.commit_many(slots, ns)
