@@ -581,6 +581,9 @@ def main():
     barrier()
     lat = []
     n_active = 0
+    import gc
+    _GC_COUNT.clear()
+    gc.callbacks.append(_count_gc)
     t0 = time.perf_counter()
     for i in range(args.steps):
         s0 = time.perf_counter()
@@ -588,6 +591,7 @@ def main():
         lat.append(time.perf_counter() - s0)
         n_active += sum(1 for v in docs[0]['misc']['vals'].values() if v)
     barrier()
+    gc.callbacks.remove(_count_gc)
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -635,6 +639,7 @@ def main():
     eng.profile = None
     roof, kernels = roofline(prof, tab_format(domain, trials, C_total))
     stages = {k: float(np.mean([a[0] for a in v])) for k, v in prof.items()}
+    ranks = rank_report(world, rank, lat, host_phases(eng, step, k=10, base=6000) if world > 1 else None, stages)
 
 
     # one quantized-branch workload beside the line: the same tree and sizes with
@@ -715,6 +720,7 @@ def main():
                        'history': args.history, 'n_EI_candidates': C_total,
                        'parallelism': 'candidate-shard x%d' % world},
             'p50_suggest_ms': 1e3 * float(np.median(lat)), 'p99_suggest_ms': 1e3 * float(np.percentile(lat, 99)),
+            'ranks': ranks,
             'p50_suggest_ms_appending': appending['p50_suggest_ms'] if appending else None,
             'appending': appending,
             'active_hyperparameters_per_suggest': n_active / args.steps,
@@ -734,6 +740,57 @@ def main():
         dist.destroy_process_group()
 
 
+_GC_COUNT = {}
+
+
+def _count_gc(phase, info):
+    """gc.callbacks hook: the collector's runs per generation (the multi-GPU
+    rank report shows whether a step's tail is a collection)."""
+    if phase == 'start':
+        g = 'gen%d' % info['generation']
+        _GC_COUNT[g] = _GC_COUNT.get(g, 0) + 1
+
+
+def host_phases(eng, step, k=3, base=300):
+    """Median host phases of the native suggest (tpe_host_phases: us since its
+    entry) over k more steps, and the steps' wall time ('step_wall'), or None."""
+    import ctypes
+    from hyperopt_amd import _native as N
+    buf = (ctypes.c_double * len(N.PHASES))()
+    eng.lib.tpe_host_phases(1, None, 0)
+    ph, wall = [], []
+    for i in range(k):
+        s0 = time.perf_counter()
+        step(base + i)
+        wall.append(1e6 * (time.perf_counter() - s0))
+        eng.lib.tpe_host_phases(1, buf, len(N.PHASES))
+        ph.append(list(buf))
+    eng.lib.tpe_host_phases(0, None, 0)
+    med = np.median(np.array(ph), axis=0)
+    if not med[-1] > 0:
+        return None
+    out = {k: round(float(v), 1) for k, v in zip(N.PHASES, med)}
+    out['step_wall'] = round(float(np.median(wall)), 1)
+    return out
+
+
+def rank_report(world, rank, lat, phases, stages):
+    """Every rank's step latencies (p50 / mean / p99 / max, ms), host phases and
+    device stage times, gathered to all ranks (world > 1; None otherwise): the
+    per-rank host share of a multi-GPU step."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    a = 1e3 * np.asarray(lat)
+    info = dict(rank=rank, p50_ms=float(np.median(a)), mean_ms=float(np.mean(a)), p99_ms=float(np.percentile(a, 99)),
+                max_ms=float(np.max(a)), steps_over_2x_p50=int(np.sum(a > 2 * np.median(a))),
+                steps_ms=[round(float(x), 3) for x in a[:64]], gc_collections=dict(_GC_COUNT),
+                host_phases_us=phases, stage_ms=stages)
+    got = [None] * world
+    dist.all_gather_object(got, info)
+    return got
+
+
 def run_other(args, rank, world, device):
     """Configs 1, 2, 4, 5: same timing discipline, own metric line."""
     import torch
@@ -749,12 +806,16 @@ def run_other(args, rank, world, device):
         step(i)
     barrier()
     lat, units = [], 0
+    import gc
+    _GC_COUNT.clear()
+    gc.callbacks.append(_count_gc)
     t0 = time.perf_counter()
     for i in range(args.steps):
         s0 = time.perf_counter()
         units = step(100 + i)
         lat.append(time.perf_counter() - s0)
     barrier()
+    gc.callbacks.remove(_count_gc)
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -769,24 +830,14 @@ def run_other(args, rank, world, device):
     stages = {k: float(np.sum([a[0] for a in v])) for k, v in eng.profile.items()}
     eng.profile = None
     extra = {}
-    # host phases of the native suggest (tpe_host_phases: us since its entry) over a
-    # few more steps, and the step's wall time outside that call (Python)
-    import ctypes
-    from hyperopt_amd import _native as N
-    buf = (ctypes.c_double * len(N.PHASES))()
-    eng.lib.tpe_host_phases(1, None, 0)
-    ph, wall = [], []
-    for i in range(3):
-        s0 = time.perf_counter()
-        step(300 + i)
-        wall.append(1e6 * (time.perf_counter() - s0))
-        eng.lib.tpe_host_phases(1, buf, len(N.PHASES))
-        ph.append(list(buf))
-    eng.lib.tpe_host_phases(0, None, 0)
-    med = np.median(np.array(ph), axis=0)
-    if med[-1] > 0:
-        extra['host_phases_us'] = {k: round(float(v), 1) for k, v in zip(N.PHASES, med)}
-        extra['host_phases_us']['step_wall'] = round(float(np.median(wall)), 1)
+    # host phases of the native suggest over a few more steps, and the step's wall
+    # time outside that call (Python)
+    phases = host_phases(eng, step)
+    if phases is not None:
+        extra['host_phases_us'] = phases
+    ranks = rank_report(world, rank, lat, phases, stages)
+    if ranks is not None:
+        extra['ranks'] = ranks
     if args.config == 4:
         # the same batched suggest returning per-id dicts (numpy scalars per value)
         lat_d = []

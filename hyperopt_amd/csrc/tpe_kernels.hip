@@ -3672,13 +3672,17 @@ __global__ __launch_bounds__(kCombThreads) void k_runs_reduce(const int32_t* __r
                                                                const int32_t* __restrict__ list, int per,
                                                                const tpe_result* __restrict__ run_best,
                                                                const tpe_result* __restrict__ res_dev, int64_t P,
-                                                               unsigned char* __restrict__ slot, int32_t status) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<int32_t*>(slot) = status;
+                                                               unsigned char* __restrict__ slot, int32_t status,
+                                                               tpe_result* __restrict__ out1,
+                                                               int32_t* __restrict__ status1) {
+  // (one rank: the gather is the identity and the combine a copy — the records
+  // go straight to the results, out1 / status1, instead of the slot)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *(status1 ? status1 : reinterpret_cast<int32_t*>(slot)) = status;
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * (kCombThreads / 64) + (threadIdx.x >> 6);
   if (p >= P) return;
   const int32_t a = sys_load_i32(span + 2 * p), n = sys_load_i32(span + 2 * p + 1);
-  tpe_result* dst = reinterpret_cast<tpe_result*>(slot + TPE_EXCHANGE_HEADER) + p;
+  tpe_result* dst = out1 ? out1 + p : reinterpret_cast<tpe_result*>(slot + TPE_EXCHANGE_HEADER) + p;
   if (n == 0) {
     if (lane == 0) *dst = res_dev[p];
     return;
@@ -5734,8 +5738,12 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     const int32_t* d_span = (const int32_t*)(dbase + rb_off);
     const unsigned int blocks = (unsigned int)((P + kCombThreads / 64 - 1) / (kCombThreads / 64));
     unsigned char* slot = (unsigned char*)lx->ex->dev + (int64_t)lx->ex->rank * xper;
+    int32_t* st_host = (int32_t*)(host + res_off + P * (int64_t)sizeof(tpe_result));   // (the pad before rb_off)
+    int32_t* st_dev = (int32_t*)(dbase + res_off + P * (int64_t)sizeof(tpe_result));
+    const bool one = lx->ex->world == 1;       // (forced exchange on one rank: no gather, no combine)
     TPE_LAUNCH(k_runs_reduce, dim3(blocks), dim3(kCombThreads), 0, s, d_span, xtmpl ? nullptr : b.tab_tiles, per,
-               (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK);
+               (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK,
+               one ? rd : (tpe_result*)nullptr, one ? st_dev : (int32_t*)nullptr);
     if ((rc = hip_check("k_runs_reduce"))) return rc;
     if ((rc = rccl_allgather_inplace(lx->ex, xper, s))) return rc;
     // the level's collective is issued: from here every failure is this level's
@@ -5746,11 +5754,11 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
       *lx->done = 1;
       return code;
     };
-    int32_t* st_host = (int32_t*)(host + res_off + P * (int64_t)sizeof(tpe_result));   // (the pad before rb_off)
-    int32_t* st_dev = (int32_t*)(dbase + res_off + P * (int64_t)sizeof(tpe_result));
-    TPE_LAUNCH(k_combine, dim3(blocks), dim3(kCombThreads), 0, s, (const unsigned char*)lx->ex->dev,
-               lx->ex->world, xper, P, rd, st_dev);
-    if ((rc = hip_check("k_combine"))) return gathered_fail(rc);
+    if (!one) {
+      TPE_LAUNCH(k_combine, dim3(blocks), dim3(kCombThreads), 0, s, (const unsigned char*)lx->ex->dev,
+                 lx->ex->world, xper, P, rd, st_dev);
+      if ((rc = hip_check("k_combine"))) return gathered_fail(rc);
+    }
     tpe_internal_phase(TPE_PHASE_LAUNCHED);
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) return gathered_fail(fail(TPE_E_HIP, hipGetErrorString(e)));
@@ -5847,6 +5855,7 @@ extern "C" {
 
 // every rank's `per` bytes at its slot of ex->dev gathered in place on stream s
 __attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_exchange* ex, int64_t per, hipStream_t s) {
+  if (ex->world == 1) return TPE_OK;          // (an in-place gather over one rank is the identity)
   Rccl& r = rccl();
   if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
   unsigned char* d = (unsigned char*)ex->dev;
