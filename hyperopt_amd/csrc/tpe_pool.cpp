@@ -23,7 +23,9 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -166,6 +168,29 @@ void stop_pool(Pool* p) {
   p->th.clear();
 }
 
+// CPUs the process's cgroup quota allows (cgroup v2 cpu.max, else v1
+// cfs_quota_us / cfs_period_us), 0 when unlimited or unknown: a container's CPU
+// share is a quota, which neither hardware_concurrency nor the affinity mask
+// shows — and workers that spin past it are descheduled for a whole CFS period
+// (the two-rank rehearsal's 80-ms steps)
+int cgroup_cpus() {
+  long long quota = -1, period = 0;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0) quota = atoll(q);
+    fclose(f);
+  } else if (FILE* g = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    if (fscanf(g, "%lld", &quota) != 1) quota = -1;
+    fclose(g);
+    if (FILE* h = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(h, "%lld", &period) != 1) period = 0;
+      fclose(h);
+    }
+  }
+  if (quota <= 0 || period <= 0) return 0;
+  return (int)std::max<long long>(1, quota / period);
+}
+
 int total_threads() {            // under g_mu
   if (g_threads < 0) {
     static bool atfork = [] { return pthread_atfork(nullptr, nullptr, after_fork_child) == 0; }();
@@ -173,6 +198,7 @@ int total_threads() {            // under g_mu
     int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     cpu_set_t set;                       // (the CPUs this process may run on, when restricted)
     if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) hw = std::min(hw, (int)CPU_COUNT(&set));
+    if (const int q = cgroup_cpus()) hw = std::min(hw, q);
     // (16: a GPU's share of the host's CPUs; the large levels of configs 4 and 5
     // fit and pack their labels on them, a 4-label suggest uses what it needs;
     // ranks sharing the host under torchrun take their share of its CPUs)
