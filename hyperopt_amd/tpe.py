@@ -751,6 +751,8 @@ def _choice_dicts(order, cols, values, active):
             vals = [v if on else None for v, on in zip(vals, a.tolist())]
         by_label[label] = vals
     keys = tuple(order)
+    if _hostaddr is not None:
+        return _hostaddr.row_dicts(keys, [by_label[k] for k in keys])
     return list(map(dict, map(zip, itertools.repeat(keys), zip(*[by_label[k] for k in keys]))))
 
 
