@@ -169,6 +169,45 @@ inline double erf_fast(double z) { return fabs(z) >= 6.0 ? copysign(1.0, z) : er
 // rows of components far from a bound skip the call
 inline double erfc_fast(double x) { return x <= -6.0 ? 2.0 : (x >= 27.3 ? 0.0 : erfc(x)); }
 
+// erf(z) for |z| < 6 within ~2e-16 of libm's: 7-term Taylor expansions about
+// the centres of 1/128-wide intervals, their coefficients erf^(n)(x0) / n! =
+// (-1)^(n-1) 2/sqrt(pi) H_(n-1)(x0) e^(-x0^2) / n! (Hermite H) built once from
+// libm's erf and exp — an order of magnitude cheaper than libm's exp-based
+// branch for |z| >= 1.25.  Only for values that end up in f32 rows (the
+// acceptance mass of a continuous f32 side); exact paths keep libm's erf.
+struct ErfTable {
+  static constexpr int kN = 768, kDeg = 7;          // 6 * 128 intervals
+  double c[kN][kDeg];
+  ErfTable() {
+    const double k2 = 2.0 / sqrt(M_PI);
+    for (int j = 0; j < kN; ++j) {
+      const double x0 = (j + 0.5) / 128.0, e = exp(-x0 * x0);
+      double h0 = 1.0, h1 = 2.0 * x0, fact = 1.0;   // H_0, H_1; n!
+      c[j][0] = erf(x0);
+      for (int n = 1; n < kDeg; ++n) {
+        fact *= n;
+        const double hn = n == 1 ? h0 : h1;          // H_(n-1)
+        c[j][n] = ((n - 1) % 2 ? -1.0 : 1.0) * k2 * hn * e / fact;
+        if (n >= 2) {                                 // H_n = 2 x H_(n-1) - 2 (n-1) H_(n-2)
+          const double h2 = 2.0 * x0 * h1 - 2.0 * (n - 1) * h0;
+          h0 = h1; h1 = h2;
+        }
+      }
+    }
+  }
+};
+const ErfTable g_erf_tab;
+inline double erf_tab(double z) {
+  const double x = fabs(z);
+  if (!(x < 6.0)) return erf_fast(z);               // (+-1, NaN)
+  const int j = (int)(x * 128.0);
+  const double d = x - (j + 0.5) / 128.0;
+  const double* c = g_erf_tab.c[j];
+  double r = c[6];
+  for (int n = 5; n >= 0; --n) r = r * d + c[n];
+  return copysign(r, z);
+}
+
 // sum_k w_k (Phi_k(hi) - Phi_k(lo)) (tpe.py:130-136): the standardised bounds
 // in one vectorisable pass, libm's erf only where it is not exactly +-1 (a
 // component within 6 sqrt2 sigma of a bound); the same values as the reference's
@@ -177,29 +216,54 @@ inline double erfc_fast(double x) { return x <= -6.0 ? 2.0 : (x >= 27.3 ? 0.0 : 
 // computes a large side's in chunks)
 __attribute__((target_clones("avx512f", "avx2", "default")))
 void p_accept_terms(const double* w, const double* mu, const double* sg, int64_t k, double lo, double hi,
-                    double* __restrict__ a) {
-  static thread_local std::vector<double> zh_tl;
-  std::vector<double>& zh = zh_tl;
-  zh.resize((size_t)k);
-  double* __restrict__ b = zh.data();
+                    double* __restrict__ a, bool fast) {
+  static thread_local std::vector<double> z_tl;
+  static thread_local std::vector<unsigned char> near_tl;
+  z_tl.resize(2 * (size_t)k);
+  near_tl.resize((size_t)k);
+  double* __restrict__ za = z_tl.data();
+  double* __restrict__ zb = za + k;
+  unsigned char* __restrict__ near = near_tl.data();
   const double s2 = sqrt(2.0);
+  if (fast)                                          // (one division: within an ulp of the quotients)
+    for (int64_t i = 0; i < k; ++i) {
+      const double t = s2 * sg[i];
+      const double r = 1.0 / (t != t ? t : (t > kEPS ? t : kEPS));
+      za[i] = (lo - mu[i]) * r;
+      zb[i] = (hi - mu[i]) * r;
+    }
+  else
+    for (int64_t i = 0; i < k; ++i) {
+      const double t = s2 * sg[i];
+      const double bottom = t != t ? t : (t > kEPS ? t : kEPS);     // np_max(sqrt2 sigma, EPS)
+      za[i] = (lo - mu[i]) / bottom;
+      zb[i] = (hi - mu[i]) / bottom;
+    }
+  // the terms whose erfs are both exactly +-1, vectorised; the others (a bound
+  // within 6 sqrt2 sigma, or NaN) flagged and made with libm's erf after
+  int64_t n_near = 0;
   for (int64_t i = 0; i < k; ++i) {
-    const double t = s2 * sg[i];
-    const double bottom = t != t ? t : (t > kEPS ? t : kEPS);       // np_max(sqrt2 sigma, EPS)
-    a[i] = (lo - mu[i]) / bottom;
-    b[i] = (hi - mu[i]) / bottom;
-  }
-  for (int64_t i = 0; i < k; ++i) {
-    const double eh = erf_fast(b[i]), el = erf_fast(a[i]);
+    const bool sh = fabs(zb[i]) >= 6.0, sl = fabs(za[i]) >= 6.0;
+    const double eh = sh ? copysign(1.0, zb[i]) : 0.0, el = sl ? copysign(1.0, za[i]) : 0.0;
     a[i] = w[i] * (0.5 * (1 + eh) - 0.5 * (1 + el));
+    near[i] = !(sh & sl);
+    n_near += !(sh & sl);
   }
+  for (int64_t i = 0; n_near > 0 && i < k; ++i)
+    if (near[i]) {
+      const double eh = fast ? erf_tab(zb[i]) : erf_fast(zb[i]), el = fast ? erf_tab(za[i]) : erf_fast(za[i]);
+      a[i] = w[i] * (0.5 * (1 + eh) - 0.5 * (1 + el));
+      --n_near;
+    }
 }
 
-double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi) {
+// (fast: erf_tab for the near terms — an f32 side's mass)
+double p_accept(const double* w, const double* mu, const double* sg, int64_t k, bool bounded, double lo, double hi,
+                bool fast) {
   if (!bounded) return 1.0;
   static thread_local std::vector<double> zl_tl;
   zl_tl.resize((size_t)k);
-  p_accept_terms(w, mu, sg, k, lo, hi, zl_tl.data());
+  p_accept_terms(w, mu, sg, k, lo, hi, zl_tl.data(), fast);
   return np_sum(zl_tl.data(), k);
 }
 
@@ -327,7 +391,7 @@ inline double min_of(const double* __restrict__ v, int64_t n) {
 // the packer's parallel pass over the large bounded sides' acceptance terms
 constexpr int64_t kPaParallelMin = 1024;    // a side of at least this many components
 constexpr int64_t kPaChunk = 512;           // ... in chunks of this many
-struct PaTask { int32_t li, side; int64_t i0, i1, off; };
+struct PaTask { int32_t li, side; int64_t i0, i1, off; bool fast; };
 
 // per-thread staging of tpe_host_pack_level, reused across calls (no
 // first-touch page faults on the large tables of a batched level)
@@ -356,7 +420,8 @@ struct PackScratch {
   std::vector<PaTask> pa_tasks;
   std::vector<char> chunked;            // chunked fills (ChunkTask)
   std::vector<ChunkTask> ch_tasks;
-  std::vector<double> ch_a, ch_c, ch_max, side_ipa, side_shift;
+  std::vector<double> ch_a, ch_c, ch_max, side_shift;
+  std::vector<int> mass_tasks;          // ... each bounded chunked side's mass task (its first chunk)
 };
 
 // value range of a label's kernel coordinate (x, or ln x for log families)
@@ -559,9 +624,9 @@ struct FillCtx {
 
 // the acceptance mass of label li's side: the terms the parallel pass made, or p_accept
 inline double side_accept(const FillCtx& cx, int32_t li, int side, const double* w, const double* mu,
-                          const double* sg, int64_t k, bool bounded, double lo, double hi) {
+                          const double* sg, int64_t k, bool bounded, double lo, double hi, bool fast) {
   const int64_t o = cx.pa_off[2 * (size_t)li + side];
-  return o >= 0 ? np_sum(cx.pa_terms + o, k) : p_accept(w, mu, sg, k, bounded, lo, hi);
+  return o >= 0 ? np_sum(cx.pa_terms + o, k) : p_accept(w, mu, sg, k, bounded, lo, hi, fast);
 }
 
 struct PaCtx { const tpe_label_in* labels; const PaTask* tasks; double* terms; };
@@ -571,7 +636,7 @@ void pa_chunk(const PaCtx& cx, int t) {
   const double* w = q.side ? L.above_w : L.below_w;
   const double* mu = q.side ? L.above_mu : L.below_mu;
   const double* sg = q.side ? L.above_sigma : L.below_sigma;
-  p_accept_terms(w + q.i0, mu + q.i0, sg + q.i0, q.i1 - q.i0, L.low, L.high, cx.terms + q.off + q.i0);
+  p_accept_terms(w + q.i0, mu + q.i0, sg + q.i0, q.i1 - q.i0, L.low, L.high, cx.terms + q.off + q.i0, q.fast);
 }
 
 __attribute__((target_clones("avx512f", "avx2", "default")))
@@ -677,7 +742,7 @@ void fill_label(const FillCtx& cx, int32_t li) {
       }
     } else if (L.family == TPE_FAM_QGAUSS || L.family == TPE_FAM_QLOGGAUSS) {
       off = (int32_t)sc.c64[side]; len = (int32_t)k;
-      base = -log(side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high));
+      base = -log(side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high, false));
       double* r = cx.comp64 + 4 * (size_t)off;
       for (int64_t i = 0; i < k; ++i) {
         const double row[4] = {mu[i], np_max(sqrt(2.0) * sg[i], kEPS), w[i], 0};
@@ -690,7 +755,7 @@ void fill_label(const FillCtx& cx, int32_t li) {
         continue;
       }
       std::vector<double> a((size_t)k), c((size_t)k);
-      const double pa = logf ? 1.0 : side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high);
+      const double pa = logf ? 1.0 : side_accept(cx, li, side, w, mu, sg, k, bounded, L.low, L.high, !f64);
       double shift = -INFINITY;
       if (f64) {
         for (int64_t i = 0; i < k; ++i) {
@@ -806,7 +871,8 @@ struct ChunkCtx {
   double* a;                   // scratch: each chunked side's a and unshifted c at ChunkTask.scr
   double* c;
   double* cmax;                // per task: the chunk's largest finite c
-  const double* ipa;           // [2 * label + side]: 1 / p_accept
+  double* pa_terms;            // the bounded sides' acceptance terms (terms pass) ...
+  const int64_t* pa_off;       // ... at [2 * label + side] (-1: unbounded or the log family)
   const double* shift;         // [2 * label + side]: the side's shift (rows pass)
   const LabelSec* sec;
   float* comp32;
@@ -819,7 +885,13 @@ void chunk_terms(const ChunkCtx& x, int t) {
   const double* w = q.side ? L.above_w : L.below_w;
   const double* sg = q.side ? L.above_sigma : L.below_sigma;
   const size_t s = 2 * (size_t)q.li + q.side;
-  x.cmax[t] = comp_terms_f32(w + q.i0, sg + q.i0, q.i1 - q.i0, L.family == TPE_FAM_LOGGAUSS, x.ipa[s],
+  // the chunk's acceptance terms beside (the side's mass is summed after the
+  // pass: it only moves the side's base, c - shift is the same)
+  if (x.pa_off[s] >= 0) {
+    const double* mu = q.side ? L.above_mu : L.below_mu;
+    p_accept_terms(w + q.i0, mu + q.i0, sg + q.i0, q.i1 - q.i0, L.low, L.high, x.pa_terms + x.pa_off[s] + q.i0, true);
+  }
+  x.cmax[t] = comp_terms_f32(w + q.i0, sg + q.i0, q.i1 - q.i0, L.family == TPE_FAM_LOGGAUSS, 1.0,
                              x.a + q.scr + q.i0, x.c + q.scr + q.i0);
 }
 
@@ -1065,14 +1137,16 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     // components per label make a worker's hand-off worth it)
     int64_t comps = 0;
     for (int32_t li = 0; li < n_labels; ++li) comps += labels[li].above_k;
-    // (in chunks of kTabChunk labels: a thousand-label level's decisions are
-    // sub-microsecond each, too small to hand out one by one)
-    struct Chunked { const TabCtx* cx; int32_t n; };
-    const Chunked ch{&tcx, n_labels};
+    // (in chunks of up to kTabChunk labels: a thousand-label level's decisions
+    // are sub-microsecond each, too small to hand out one by one; a few large
+    // labels — config 4's twenty of 10^4 components — one a task)
+    struct Chunked { const TabCtx* cx; int32_t n, per; };
+    const int32_t per = std::max<int32_t>(1, std::min<int32_t>(kTabChunk, n_labels / (4 * (1 + tpe_pool::workers()))));
+    const Chunked ch{&tcx, n_labels, per};
     if (n_labels >= 2 && comps >= 16384)
-      tpe_pool::parallel_for((n_labels + kTabChunk - 1) / kTabChunk, [](void* c, int k) {
+      tpe_pool::parallel_for((n_labels + per - 1) / per, [](void* c, int k) {
         const Chunked& q = *(const Chunked*)c;
-        for (int32_t li = k * kTabChunk; li < std::min(q.n, (k + 1) * kTabChunk); ++li) decide_table(*q.cx, li);
+        for (int32_t li = k * q.per; li < std::min(q.n, (k + 1) * q.per); ++li) decide_table(*q.cx, li);
       }, (void*)&ch);
     else
       for (int32_t li = 0; li < n_labels; ++li) decide_table(tcx, li);
@@ -1264,40 +1338,10 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     }
   }
   PACK_MARK("lead");
-  // the acceptance terms of the large bounded sides in chunks on the workers
-  // (libm erf for every component near a bound: the largest label's would
-  // otherwise be its fill's critical path); the fill sums them in order
-  auto& pa_off = ps.pa_off;
-  auto& pa_terms = ps.pa_terms;
-  auto& pa_tasks = ps.pa_tasks;
-  pa_off.assign(2 * (size_t)n_labels, -1);
-  pa_tasks.clear();
-  int64_t pa_total = 0;
-  for (int32_t li = 0; li < n_labels; ++li) {
-    const tpe_label_in& L = labels[li];
-    if (!(L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) || L.family == TPE_FAM_CATEGORICAL ||
-        L.family == TPE_FAM_LOGGAUSS)
-      continue;
-    for (int side = 0; side < 2 - dev_fit[li]; ++side) {
-      const int64_t k = side ? L.above_k : L.below_k;
-      if (k < kPaParallelMin) continue;
-      pa_off[2 * (size_t)li + side] = pa_total;
-      for (int64_t i0 = 0; i0 < k; i0 += kPaChunk)
-        pa_tasks.push_back(PaTask{li, side, i0, std::min(k, i0 + kPaChunk), pa_total});
-      pa_total += k;
-    }
-  }
-  if (!pa_tasks.empty()) {
-    pa_terms.resize((size_t)pa_total);
-    const PaCtx pcx{labels, pa_tasks.data(), pa_terms.data()};
-    tpe_pool::parallel_for((int)pa_tasks.size(), [](void* c, int i) { pa_chunk(*(const PaCtx*)c, i); }, (void*)&pcx);
-  }
-  PACK_MARK("accept");
   // large tabulated continuous f32 sides: in chunks (ChunkTask), their
-  // acceptance mass first (from the parallel pass's terms)
+  // acceptance terms in the same tasks as their component terms
   auto& chunked = ps.chunked;
   auto& ch_tasks = ps.ch_tasks;
-  auto& side_ipa = ps.side_ipa;
   auto& side_shift = ps.side_shift;
   chunked.assign(2 * (size_t)n_labels, 0);
   ch_tasks.clear();
@@ -1327,28 +1371,49 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         ch_total += k;
       }
     }
+  // the acceptance terms of the large bounded sides in chunks on the workers
+  // (libm erf for every component near a bound: the largest label's would
+  // otherwise be its fill's critical path); the fill sums them in order
+  auto& pa_off = ps.pa_off;
+  auto& pa_terms = ps.pa_terms;
+  auto& pa_tasks = ps.pa_tasks;
+  pa_off.assign(2 * (size_t)n_labels, -1);
+  pa_tasks.clear();
+  int64_t pa_total = 0;
+  for (int32_t li = 0; li < n_labels; ++li) {
+    const tpe_label_in& L = labels[li];
+    if (!(L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) || L.family == TPE_FAM_CATEGORICAL ||
+        L.family == TPE_FAM_LOGGAUSS)
+      continue;
+    const bool fast = L.family == TPE_FAM_GAUSS && !f64;   // (an f32 side's mass: erf_tab)
+    for (int side = 0; side < 2 - dev_fit[li]; ++side) {
+      const int64_t k = side ? L.above_k : L.below_k;
+      const bool ch = chunked[2 * (size_t)li + side] != 0;     // (its terms: the chunk tasks)
+      if (k < kPaParallelMin && !ch) continue;
+      pa_off[2 * (size_t)li + side] = pa_total;
+      for (int64_t i0 = 0; i0 < k && !ch; i0 += kPaChunk)
+        pa_tasks.push_back(PaTask{li, side, i0, std::min(k, i0 + kPaChunk), pa_total, fast});
+      pa_total += k;
+    }
+  }
+  pa_terms.resize((size_t)pa_total);
+  if (!pa_tasks.empty()) {
+    const PaCtx pcx{labels, pa_tasks.data(), pa_terms.data()};
+    tpe_pool::parallel_for((int)pa_tasks.size(), [](void* c, int i) { pa_chunk(*(const PaCtx*)c, i); }, (void*)&pcx);
+  }
+  PACK_MARK("accept");
   const FillCtx fcx{labels, sec.data(), lab.data(), f_samp, f_comp64, f_comp32, f_grid,
                     dev_fit.data(), tmode.data(), key_bits, f64, pa_terms.data(), pa_off.data(), chunked.data()};
   const int n_ch = (int)ch_tasks.size();
-  ChunkCtx ccx{labels, ch_tasks.data(), nullptr, nullptr, nullptr, nullptr, nullptr, sec.data(), f_comp32};
+  ChunkCtx ccx{labels, ch_tasks.data(), nullptr, nullptr, nullptr, pa_terms.data(), pa_off.data(), nullptr,
+               sec.data(), f_comp32};
   if (n_ch) {
     ps.ch_a.resize((size_t)ch_total);
     ps.ch_c.resize((size_t)ch_total);
     ps.ch_max.resize((size_t)n_ch);
-    side_ipa.assign(2 * (size_t)n_labels, 1.0);
     side_shift.assign(2 * (size_t)n_labels, 0.0);
-    for (int32_t li = 0; li < n_labels; ++li)
-      for (int side = 0; side < 2; ++side) {
-        const size_t q = 2 * (size_t)li + side;
-        const tpe_label_in& L = labels[li];
-        if (!chunked[q] || L.family == TPE_FAM_LOGGAUSS) continue;
-        const bool bounded = (L.flags & (TPE_F_HAS_LOW | TPE_F_HAS_HIGH)) != 0;
-        side_ipa[q] = 1.0 / side_accept(fcx, li, side, side ? L.above_w : L.below_w, side ? L.above_mu : L.below_mu,
-                                        side ? L.above_sigma : L.below_sigma, side ? L.above_k : L.below_k, bounded,
-                                        L.low, L.high);
-      }
     ccx.a = ps.ch_a.data(); ccx.c = ps.ch_c.data(); ccx.cmax = ps.ch_max.data();
-    ccx.ipa = side_ipa.data(); ccx.shift = side_shift.data();
+    ccx.shift = side_shift.data();
   }
   {
     // the labels' fills and the chunks' terms, one task each (a few hundred
@@ -1365,6 +1430,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
     else
       for (int i = 0; i < n_tasks; ++i) task((void*)&both, i);
   }
+  PACK_MARK("fill_terms");
   if (n_ch) {
     // each chunked side's shift (the largest finite c of its chunks) and base,
     // then its rows
@@ -1379,9 +1445,51 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
         if (!std::isfinite(side_shift[q])) side_shift[q] = 0;
         (side ? lab[li].above_base : lab[li].below_base) = side_shift[q] * kLn2;
       }
-    auto rows = [](void* v, int t) { chunk_rows(*(const ChunkCtx*)v, t); };
-    if (n_ch >= 2) tpe_pool::parallel_for(n_ch, rows, (void*)&ccx);
-    else rows((void*)&ccx, 0);
+    // the rows, and each bounded side's mass (its terms summed in numpy's
+    // order) into its base: log2(w / (sigma sqrt(2 pi)) / p) - shift =
+    // c' - shift' with shift = shift' + log2(1 / p), one task a side (named by
+    // its first chunk)
+    auto& mass = ps.mass_tasks;
+    mass.clear();
+    for (int t = 0; t < n_ch; ++t)
+      if (ch_tasks[t].i0 == 0 && pa_off[2 * (size_t)ch_tasks[t].li + ch_tasks[t].side] >= 0) mass.push_back(t);
+    struct Rows { const ChunkCtx* c; tpe_problem* lab; const int* mass; int n_ch; };
+    const Rows rw{&ccx, lab.data(), mass.data(), n_ch};
+    auto rows = [](void* v, int t) {
+      const Rows& r = *(const Rows*)v;
+      if (t < r.n_ch) { chunk_rows(*r.c, t); return; }
+      const ChunkTask& q = r.c->tasks[r.mass[t - r.n_ch]];
+      const size_t sd = 2 * (size_t)q.li + q.side;
+      const tpe_label_in& L = r.c->labels[q.li];
+      const double pa = np_sum(r.c->pa_terms + r.c->pa_off[sd], q.side ? L.above_k : L.below_k);
+      double& base = q.side ? r.lab[q.li].above_base : r.lab[q.li].below_base;
+      base = pa > 0 && pa < INFINITY ? base - log(pa) : NAN;      // (NaN: refilled below)
+    };
+    const int n_rows = n_ch + (int)mass.size();
+    if (n_rows >= 2) tpe_pool::parallel_for(n_rows, rows, (void*)&rw);
+    else rows((void*)&rw, 0);
+    // a side whose mass is 0, inf or NaN: its rows with 1 / p inside c, as
+    // fill_label makes them (the rows carry the non-finite values, base 0)
+    for (int m : mass) {
+      const ChunkTask& q0 = ch_tasks[m];
+      tpe_problem& p = lab[q0.li];
+      double& base = q0.side ? p.above_base : p.below_base;
+      if (base == base) continue;
+      const tpe_label_in& L = labels[q0.li];
+      const size_t sd = 2 * (size_t)q0.li + q0.side;
+      const double ipa = 1.0 / np_sum(pa_terms.data() + pa_off[sd], q0.side ? L.above_k : L.below_k);
+      const double* w = q0.side ? L.above_w : L.below_w;
+      const double* sg = q0.side ? L.above_sigma : L.below_sigma;
+      double sh = -INFINITY;
+      for (int t = m; t < n_ch && ch_tasks[t].li == q0.li && ch_tasks[t].side == q0.side; ++t) {
+        const ChunkTask& q = ch_tasks[t];
+        sh = std::max(sh, comp_terms_f32(w + q.i0, sg + q.i0, q.i1 - q.i0, false, ipa, ccx.a + q.scr + q.i0,
+                                         ccx.c + q.scr + q.i0));
+      }
+      side_shift[sd] = std::isfinite(sh) ? sh : 0.0;
+      base = side_shift[sd] * kLn2;
+      for (int t = m; t < n_ch && ch_tasks[t].li == q0.li && ch_tasks[t].side == q0.side; ++t) chunk_rows(ccx, t);
+    }
   }
   PACK_MARK("fill");
   // the device-fitted labels' problem fields (the fill cleared their rows)

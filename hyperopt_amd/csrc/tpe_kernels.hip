@@ -3690,9 +3690,12 @@ __global__ __launch_bounds__(kCombThreads) void k_runs_reduce(const int32_t* __r
   double bs = 0.0;
   int64_t bi = -1;
   int bt = -1;                                     // the best run's tile
-  for (int k = lane; k < n; k += 64) {
-    const int pos = a + k;
-    if (k != 0 && pos % per != 0) continue;        // not a run's first tile
+  // the runs' first positions: a, then every multiple of per in (a, a + n) —
+  // one lane a run, so a wave's record loads are all in flight at once
+  const int b0 = (a / per + 1) * per;
+  const int n_runs = 1 + (a + n > b0 ? (a + n - b0 + per - 1) / per : 0);
+  for (int j = lane; j < n_runs; j += 64) {
+    const int pos = j == 0 ? a : b0 + (j - 1) * per;
     const int t = list ? list[pos] : pos;
     const tpe_result c = run_best[t];
     if (better(c.score, c.idx, bs, bi)) { bs = c.score; bi = c.idx; bt = t; }
@@ -5755,7 +5758,8 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
       return code;
     };
     if (!one) {
-      TPE_LAUNCH(k_combine, dim3(blocks), dim3(kCombThreads), 0, s, (const unsigned char*)lx->ex->dev,
+      const unsigned int cblocks = (unsigned int)((P + kCombThreads - 1) / kCombThreads);   // (a thread a problem)
+      TPE_LAUNCH(k_combine, dim3(cblocks), dim3(kCombThreads), 0, s, (const unsigned char*)lx->ex->dev,
                  lx->ex->world, xper, P, rd, st_dev);
       if ((rc = hip_check("k_combine"))) return gathered_fail(rc);
     }

@@ -117,13 +117,16 @@ def _rccl_worker(port, q):
         from hyperopt_amd import dist as D, tpe
         from hyperopt_amd.engine import get_engine
         domain, trials = bench.make_history(N_HIST, 0)
-        ref = [doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=1 << 18)) for s in (21, 22)]
+        # (2^18 candidates: every label tabulated, the runs reduced on the device;
+        # 64: pruned labels selected late, by the select stage)
+        cases = [(21, 1 << 18), (22, 1 << 18), (23, 64)]
+        ref = [doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=c)) for s, c in cases]
         D.EXCHANGE_ALWAYS = True
         eng = get_engine()
         got = []
-        for s in (21, 22):
+        for s, c in cases:
             eng.last_tree_path = None
-            got.append(doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=1 << 18, shard=(0, 1))))
+            got.append(doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=c, shard=(0, 1))))
             assert eng.last_tree_path is not None
         ex = D.exchange_for(eng)
         q.put(([{k: float(v) for k, v in r.items()} for r in ref], [{k: float(v) for k, v in g.items()} for g in got],
@@ -136,10 +139,11 @@ def _rccl_worker(port, q):
 
 
 def test_rccl_exchange_one_rank():
-    """The RCCL exchange path of the native tree (tpe_comm_init from C, an
-    in-place ncclAllGather of the level results on the suggest's stream, the
-    host reduction) on a one-rank nccl group — the one GPU of the box — with
-    the exchange forced on: the suggestions equal the unsharded ones."""
+    """The RCCL exchange path of the native tree (tpe_comm_init from C, the
+    device run reduction k_runs_reduce straight into the results, as at world
+    1 the all-gather is the identity) on a one-rank
+    nccl group — the one GPU of the box — with the exchange forced on: the
+    suggestions equal the unsharded ones."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))

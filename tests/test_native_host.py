@@ -177,6 +177,31 @@ def test_native_pack_matches_numpy_packer(precision):
             assert N.TAB_CELLS not in modes
 
 
+def test_native_pack_chunked_sides_match_numpy_packer():
+    """A level with >= 16384 components of large tabulated f32 sides: their
+    rows and acceptance terms come from the chunk tasks (the mass folded into
+    the side's base after the terms pass) and match the numpy packer's rows
+    and bases."""
+    rs = np.random.RandomState(4)
+    posts = [parzen.fit_posterior('uniform', dict(low=-5.0, high=5.0), rs.uniform(-5, 5, 25), rs.uniform(-5, 5, 9000),
+                                  1.0),
+             parzen.fit_posterior('normal', dict(mu=0.0, sigma=2.0), rs.normal(0, 2, 20), rs.normal(0, 2, 6000), 1.0),
+             parzen.fit_posterior('uniform', dict(low=0.0, high=1.0), rs.uniform(0, 1, 9), rs.uniform(0, 1, 4000),
+                                  1.0)]
+    lps = [LevelProblem(p, i + 3, np.arange(i + 1) + 100) for i, p in enumerate(posts)]
+    e = _engine('fp32')
+    C = 1 << 17
+    ref = e._build_numpy(lps, C, 77, 10, None)
+    info = e._pack(lps, C, 77, 10, None)
+    P = ref['P']
+    prob = _blob(e, info, info.off_problems, N.PROBLEM_DTYPE, P)
+    assert set(prob['tab_mode'].tolist()) == {N.TAB_CELLS}
+    for f in ('below_base', 'above_base', 'above_len', 'below_len'):
+        np.testing.assert_allclose(prob[f].astype(float), ref['prob'][f].astype(float), rtol=1e-6, atol=0, err_msg=f)
+    c32 = _blob(e, info, info.off_comp32, np.float32, ref['comp32'].size)
+    np.testing.assert_allclose(c32, ref['comp32'].reshape(-1), rtol=1e-6, atol=1e-6)
+
+
 def test_host_pool_swaps_under_concurrent_dispatch():
     """tpe_host_threads replaces the worker pool while other threads dispatch
     to it (the packer's parallel label fills): every pack stays identical to
