@@ -3667,9 +3667,17 @@ __device__ __forceinline__ int32_t sys_load_i32(const int32_t* p) {
 // one wave per problem: span[2p] = the list position of its first tabulated
 // tile, span[2p + 1] = its tabulated tiles (0: its result is res_dev[p]); a
 // run starts at the problem's first position and at every multiple of `per`
-// (the sample stage's workgroup partition); list = NULL: the identity
+// (the sample stage's workgroup partition); list = NULL: the identity.
+// span = NULL (a level of at most kRunsDevMax problems): the spans from the
+// packer's layout instead — every problem tpp tiles, the tile list the
+// tabulated problems' tiles in problem order — so no host memory is read and
+// a run's first tile is p * tpp + (pos - a): the wave's chain is one load of
+// the problems' modes, one of its runs' records, the record itself carried
+// through the reduction
+constexpr int64_t kRunsDevMax = 256;
 __global__ __launch_bounds__(kCombThreads) void k_runs_reduce(const int32_t* __restrict__ span,
                                                                const int32_t* __restrict__ list, int per,
+                                                               const tpe_problem* __restrict__ prob, int tpp,
                                                                const tpe_result* __restrict__ run_best,
                                                                const tpe_result* __restrict__ res_dev, int64_t P,
                                                                unsigned char* __restrict__ slot, int32_t status,
@@ -3681,32 +3689,42 @@ __global__ __launch_bounds__(kCombThreads) void k_runs_reduce(const int32_t* __r
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * (kCombThreads / 64) + (threadIdx.x >> 6);
   if (p >= P) return;
-  const int32_t a = sys_load_i32(span + 2 * p), n = sys_load_i32(span + 2 * p + 1);
   tpe_result* dst = out1 ? out1 + p : reinterpret_cast<tpe_result*>(slot + TPE_EXCHANGE_HEADER) + p;
+  int32_t a, n;
+  if (span) {
+    a = sys_load_i32(span + 2 * p);
+    n = sys_load_i32(span + 2 * p + 1);
+  } else {
+    int before = 0;                                // tabulated problems before p
+    for (int64_t q0 = 0; q0 < p; q0 += 64) {
+      const int64_t q = q0 + lane;
+      before += __popcll(__ballot(q < p && prob[q].tab_mode != TPE_TAB_NONE));
+    }
+    a = before * tpp;
+    n = prob[p].tab_mode != TPE_TAB_NONE ? tpp : 0;
+  }
   if (n == 0) {
     if (lane == 0) *dst = res_dev[p];
     return;
   }
-  double bs = 0.0;
-  int64_t bi = -1;
-  int bt = -1;                                     // the best run's tile
+  tpe_result w{0, 0, 0, 0, -1, -1};
   // the runs' first positions: a, then every multiple of per in (a, a + n) —
   // one lane a run, so a wave's record loads are all in flight at once
   const int b0 = (a / per + 1) * per;
   const int n_runs = 1 + (a + n > b0 ? (a + n - b0 + per - 1) / per : 0);
   for (int j = lane; j < n_runs; j += 64) {
     const int pos = j == 0 ? a : b0 + (j - 1) * per;
-    const int t = list ? list[pos] : pos;
+    const int t = span ? (list ? list[pos] : pos) : (int)(p * tpp + (pos - a));
     const tpe_result c = run_best[t];
-    if (better(c.score, c.idx, bs, bi)) { bs = c.score; bi = c.idx; bt = t; }
+    if (better(c.score, c.idx, w.score, w.idx)) w = c;
   }
   for (int off = 32; off > 0; off >>= 1) {         // (np.argmax order: unique indices, any order of reduction)
-    const double os = __shfl_xor(bs, off);
-    const int64_t oi = __shfl_xor(bi, off);
-    const int ot = __shfl_xor(bt, off);
-    if (better(os, oi, bs, bi)) { bs = os; bi = oi; bt = ot; }
+    tpe_result o;
+    o.score = __shfl_xor(w.score, off); o.l = __shfl_xor(w.l, off); o.g = __shfl_xor(w.g, off);
+    o.value = __shfl_xor(w.value, off); o.idx = __shfl_xor(w.idx, off); o.global_idx = __shfl_xor(w.global_idx, off);
+    if (better(o.score, o.idx, w.score, w.idx)) w = o;
   }
-  if (lane == 0) *dst = bt >= 0 ? run_best[bt] : tpe_result{0, 0, 0, 0, -1, -1};
+  if (lane == 0) *dst = w;
 }
 
 __global__ __launch_bounds__(kCombThreads) void k_combine(const unsigned char* __restrict__ all, int W, int64_t per,
@@ -5722,30 +5740,36 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     return rc;
   }
   if (dex) {
-    // each problem's span of the tabulated tile list (host-visible: the
-    // run-record area is free in this mode): its runs are enumerated on the
-    // device as the host reduction below enumerates them
-    int32_t* span = (int32_t*)(host + rb_off);
+    // each problem's span of the tabulated tile list: from the packer's layout
+    // on the device (a level of at most kRunsDevMax problems with tpp tiles
+    // each), else written by the host (host-visible: the run-record area is
+    // free in this mode) — its runs are enumerated on the device as the host
+    // reduction below enumerates them
     const int n_tab = (int)info.n_tab_tiles, per = tab_tiles_per_wg(n_tab, tab_wgs_per_cu(&b));
-    if (xtmpl) {                                     // expanded: every problem's tiles, in order
-      for (int64_t r = 0; r < P; ++r) { span[2 * r] = (int32_t)(r * n_tiles_p); span[2 * r + 1] = (int32_t)n_tiles_p; }
-    } else {
-      for (int64_t r = 0; r < P; ++r) span[2 * r] = span[2 * r + 1] = 0;
-      const int32_t* list = (const int32_t*)(host + info.off_tab_tiles);
-      const tpe_tile* tl = (const tpe_tile*)(host + info.off_tiles);
-      for (int i = 0; i < n_tab; ++i) {
-        const int pr = tl[list[i]].problem;
-        if (span[2 * pr + 1]++ == 0) span[2 * pr] = i;
+    const int tpp = b.tiles_per_problem;
+    const int32_t* d_span = nullptr;
+    if (P > kRunsDevMax || tpp <= 0) {
+      int32_t* span = (int32_t*)(host + rb_off);
+      if (xtmpl) {                                   // expanded: every problem's tiles, in order
+        for (int64_t r = 0; r < P; ++r) { span[2 * r] = (int32_t)(r * n_tiles_p); span[2 * r + 1] = (int32_t)n_tiles_p; }
+      } else {
+        for (int64_t r = 0; r < P; ++r) span[2 * r] = span[2 * r + 1] = 0;
+        const int32_t* list = (const int32_t*)(host + info.off_tab_tiles);
+        const tpe_tile* tl = (const tpe_tile*)(host + info.off_tiles);
+        for (int i = 0; i < n_tab; ++i) {
+          const int pr = tl[list[i]].problem;
+          if (span[2 * pr + 1]++ == 0) span[2 * pr] = i;
+        }
       }
+      d_span = (const int32_t*)(dbase + rb_off);
     }
-    const int32_t* d_span = (const int32_t*)(dbase + rb_off);
     const unsigned int blocks = (unsigned int)((P + kCombThreads / 64 - 1) / (kCombThreads / 64));
     unsigned char* slot = (unsigned char*)lx->ex->dev + (int64_t)lx->ex->rank * xper;
     int32_t* st_host = (int32_t*)(host + res_off + P * (int64_t)sizeof(tpe_result));   // (the pad before rb_off)
     int32_t* st_dev = (int32_t*)(dbase + res_off + P * (int64_t)sizeof(tpe_result));
     const bool one = lx->ex->world == 1;       // (forced exchange on one rank: no gather, no combine)
     TPE_LAUNCH(k_runs_reduce, dim3(blocks), dim3(kCombThreads), 0, s, d_span, xtmpl ? nullptr : b.tab_tiles, per,
-               (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK,
+               b.problems, tpp, (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK,
                one ? rd : (tpe_result*)nullptr, one ? st_dev : (int32_t*)nullptr);
     if ((rc = hip_check("k_runs_reduce"))) return rc;
     if ((rc = rccl_allgather_inplace(lx->ex, xper, s))) return rc;
