@@ -23,9 +23,10 @@ cpu_baseline: the CPU oracle (numpy restatement of the reference) on a bounded
 p50_suggest_ms_appending: the same suggest in an FMinIter loop (one finished
           document inserted before every suggest, fmin.py:88-92).
 config4_strong: BASELINE config 4 (4096 new ids x 4096 candidates x 20 dims)
-          with the ids split over the N ranks and one all-gather of the chosen
-          values (tpe.suggest_choices(shard_ids=...)): strong scaling of the axis
-          that shards without a per-level exchange.
+          with the hyperparameters (--axis4 labels, the default) or the ids
+          (--axis4 ids) split over the N ranks and one all-gather of the chosen
+          values (tpe.suggest_choices(shard_labels= / shard_ids=...)): strong
+          scaling of the axes that shard without a per-level exchange.
 """
 import argparse
 import json
@@ -445,16 +446,21 @@ def config_workload(config, rank, world, args):
         n_ids, C = 4096, 4096
         ids = np.arange(10000, 10000 + n_ids)
         sid = (rank, world) if world > 1 else None
+        # N > 1: the hyperparameter axis (each rank fits, packs, tabulates and
+        # samples its labels for every id: no per-rank work left unsharded but the
+        # Python around the call) or the new-id axis (each rank its block of ids,
+        # every label's fits and tables on every rank); one all-gather of the
+        # chosen values either way — every rank holds all 4096 x 20
+        by_labels = getattr(args, 'axis4', 'labels') == 'labels'
+        kw = {'shard_labels' if by_labels else 'shard_ids': sid}
 
         def step(i, columns=True):
-            # SoA in, SoA out (tpe.ChoiceColumns); columns=False: per-id dicts.  N > 1:
-            # each rank suggests its block of the ids, one all-gather of the chosen
-            # values (tpe_exchange_allgather) — every rank holds all 4096 x 20
-            tpe.suggest_choices(table, hist, ids, SEED + i, n_EI_candidates=C, columns=columns, shard_ids=sid)
+            # SoA in, SoA out (tpe.ChoiceColumns); columns=False: per-id dicts
+            tpe.suggest_choices(table, hist, ids, SEED + i, n_EI_candidates=C, columns=columns, **kw)
             return len(labels) * n_ids * C          # whole job
         return ('config4: batched suggest, 4096 new_ids x 4096 candidates, 20-dim U(-5,5), 10k-trial '
-                'history, new_ids sharded over ranks + one all-gather of the chosen values, columnar results'), \
-            step, None
+                'history, %s sharded over ranks + one all-gather of the chosen values, columnar results'
+                % ('hyperparameters' if by_labels else 'new_ids')), step, None
     if config == 5 and args.appending:
         # FMinIter's flow on the columnar history (fmin.py:88-92): every suggest
         # follows the evaluation of the previous one, appended as one observation
@@ -525,6 +531,8 @@ def main():
     ap.add_argument('--history', type=int, default=N_HISTORY)
     ap.add_argument('--cands', type=int, default=C_PER_GPU)
     ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
+    ap.add_argument('--axis4', choices=('labels', 'ids'), default='labels',
+                    help='config 4 over N > 1 ranks: shard the hyperparameters or the new ids')
     ap.add_argument('--dims', type=int, default=1000, help='config 5 dimensions')
     ap.add_argument('--history5', type=int, default=100000, help='config 5 history length')
     ap.add_argument('--appending', action='store_true',
@@ -706,7 +714,7 @@ def main():
             el4 = float(t.item())
         cfg4 = dict(workload=desc4, value=units4 * n4 / el4, unit='candidate-scores/s', steps=n4,
                     ms_per_step=1e3 * el4 / n4, scaling='strong', n_gpus=world,
-                    parallelism='new-id shard x%d' % world)
+                    parallelism='%s shard x%d' % ('hyperparameter' if args.axis4 == 'labels' else 'new-id', world))
 
     if rank == 0:
         out = {

@@ -184,6 +184,8 @@ def _axes_cases(rank, world):
     ids = np.arange(10000, 10000 + 4096)
     cc = tpe.suggest_choices(t4, h4, ids, 31, n_EI_candidates=4096, columns=True, shard_ids=sid)
     out.append(('config4 ids', (cc.values, cc.active)))
+    cc = tpe.suggest_choices(t4, h4, ids, 32, n_EI_candidates=4096, columns=True, shard_labels=sid)
+    out.append(('config4 labels', (cc.values, cc.active)))
     t5, h5 = _cfg5()
     cc = tpe.suggest_choices(t5, h5, [N5, N5 + 1], 41, n_EI_candidates=4096, columns=True, shard_labels=sid)
     out.append(('config5 labels', (cc.values, cc.active)))
@@ -213,8 +215,9 @@ def _axes_worker(rank, world, port, q):
 def test_two_process_id_and_label_axes_match_unsharded():
     """Two processes (gloo, both on the one GPU): the new-id axis (config 4:
     4096 ids x 4096 candidates x 20 dims, and 64 ids of the config-3 tree) and
-    the hyperparameter axis (a config-5-shaped 200-dim space at 100k trials
-    with device Parzen fits, and the config-3 tree: gates on both ranks) each
+    the hyperparameter axis (config 4's 20 labels over all 4096 ids, a
+    config-5-shaped 200-dim space at 100k trials with device Parzen fits, and
+    the config-3 tree: gates on both ranks) each
     return, on every rank, exactly the unsharded suggest (values and activity
     bit for bit: the candidates are keyed on seed, label, new id and index)."""
     ctx = mp.get_context('spawn')

@@ -9,13 +9,16 @@ any 8-GPU run).  Model, per config, from the bench line's host phases
       prediction fails: the gate level, then the branch level), x1 the forced
       one-rank exchange's cost per level (k_runs_reduce, measured), a the
       per-hop latency of a small RCCL all-gather ring over xGMI (assumed).
-  config 4 (new-id axis, strong: 4096 ids over the ranks)
+  config 4 (new-id axis, strong: 4096 ids over the ranks; --axis4 ids)
       T(N) = F + V / N + X(N)
       F (every rank, unsharded): the label fits (prefit), the pack of the
       labels' component rows (pack - prefit) and the label tables (k_tables);
       V (sharded): the rest of the step (the id-block's sample pass, records,
       result assembly); X(N) the all-gather of the id blocks' values and
       activity (ids * labels * 9 B) at bandwidth bw after one latency.
+  config 4 (hyperparameter axis, strong: the 20 labels over the ranks; the
+      default --axis4 labels): F the Python around the native call, V the
+      native call times ceil(20 / N) / 20, X(N) as above.
   config 5 (hyperparameter axis, strong: 1000 labels over the ranks)
       T(N) = F + V / N + X(N)
       F: the Python around the native call (history view, below split over
@@ -59,7 +62,15 @@ def main():
     for n in Ns:
         x = 0 if n == 1 else a.hop_us * (n - 1) + nbytes4 * (n - 1) / n / (a.bw_gbs * 1e3)
         t = F4 + V4 / n + x
-        rows.append(('4 strong', n, t, T4 / (n * t)))
+        rows.append(('4 ids', n, t, T4 / (n * t)))
+    # config 4 over the hyperparameter axis (bench.py --axis4 labels): every
+    # native part shards with the labels (ceil(20 / N) a rank), the Python
+    # around the call does not
+    F4l, V4l = T4 - h4['return'], h4['return']
+    for n in Ns:
+        x = 0 if n == 1 else a.hop_us * (n - 1) + nbytes4 * (n - 1) / n / (a.bw_gbs * 1e3)
+        t = F4l + V4l * (-(-20 // n)) / 20 + x
+        rows.append(('4 labels', n, t, T4 / (n * t)))
     c5 = last_json(a.cfg5)
     h5 = c5['host_phases_us']
     T5 = c5['p50_step_ms'] * 1e3
@@ -70,8 +81,8 @@ def main():
         x = 0 if n == 1 else a.hop_us * (n - 1) + nbytes5 * (n - 1) / n / (a.bw_gbs * 1e3)
         t = F5 + V5 / n + x
         rows.append(('5 strong', n, t, T5 / (n * t)))
-    print('inputs: cfg3 p50 %.1f us; cfg4 F %.0f V %.0f us; cfg5 F %.0f V %.0f us; x1 %.2f us/level, '
-          'hop %.1f us, bw %.0f GB/s' % (t1, F4, V4, F5, V5, a.x1_us, a.hop_us, a.bw_gbs))
+    print('inputs: cfg3 p50 %.1f us; cfg4 ids F %.0f V %.0f us, labels F %.0f V %.0f us; cfg5 F %.0f V %.0f us; '
+          'x1 %.2f us/level, hop %.1f us, bw %.0f GB/s' % (t1, F4, V4, F4l, V4l, F5, V5, a.x1_us, a.hop_us, a.bw_gbs))
     print('%-9s %3s %10s %10s' % ('config', 'N', 'T(N) us', 'eff'))
     for name, n, t, e in rows:
         print('%-9s %3d %10.1f %10.2f' % (name, n, t, e))

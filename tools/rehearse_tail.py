@@ -26,7 +26,7 @@ def main():
     from hyperopt_amd import _native as N, dist as D, engine as E
 
     class _Args(object):
-        dims, history5, appending = 1000, 100000, False
+        dims, history5, appending, axis4 = 1000, 100000, False, 'ids'
     _, step, _ = bench.config_workload(4, rank, world, _Args())
     gather_s = []
     orig = D.gather_id_blocks
