@@ -135,7 +135,15 @@ def host_cpu():
     except OSError:
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
-    return dict(model=model, logical_cpus=os.cpu_count(), usable_cpus=aff)
+    quota = None                      # the cgroup's CPU share (cpu.max quota / period), if any
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, per = f.read().split()[:2]
+        if q != 'max' and float(per) > 0:
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return dict(model=model, logical_cpus=os.cpu_count(), usable_cpus=aff, cgroup_cpu_quota=quota)
 
 
 def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64, 128, 256), sweep_s=5.0):
@@ -185,11 +193,15 @@ def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64, 128, 256), sweep_
     # the knee: the smallest pool within 5 % of the best (more processes than
     # the host's CPU share buy nothing)
     knee = min((p for p in pts if p['value'] >= 0.95 * best['value']), key=lambda p: p['processes'])
-    return dict(value=best['value'], unit='candidate-scores/s', cores=best['processes'], kind='port',
+    # (cores: the CPU time the pool could use — a cgroup quota caps it below the
+    # process count)
+    quota = cpu.get('cgroup_cpu_quota')
+    cores = min(best['processes'], int(math.ceil(quota))) if quota else best['processes']
+    return dict(value=best['value'], unit='candidate-scores/s', cores=cores, processes=best['processes'], kind='port',
                 knee_processes=knee['processes'],
                 sample='%d oracle tpe_suggest calls, C=16384, same 10k-trial history, candidate scoring chunked '
-                       'over %d processes, %.1fs (best of the process sweep)'
-                       % (best['calls'], best['processes'], best['secs']),
+                       'over %d processes on %d cores, %.1fs (best of the process sweep)'
+                       % (best['calls'], best['processes'], cores, best['secs']),
                 sweep=[dict(processes=p['processes'], value=p['value']) for p in pts],
                 single_core=dict(value=v1, cores=1,
                                  sample='%d oracle tpe_suggest calls, C=16384, %.1fs, 1 core' % (c1, d1)),
