@@ -373,6 +373,29 @@ def test_fast_sample_kernel_matches_general(monkeypatch, extra):
     assert fast1024 == gen
 
 
+def test_fast_sample_kernel_single_label_partial_staging_round(monkeypatch):
+    """A level of ONE tabulated label — its table is the level's largest, so the
+    dynamic LDS holds exactly its 3 * n0 row units, and 3 * n0 is (for these
+    histories) not a multiple of the 512-lane staging round: the LDS-DMA lanes
+    past the rows must issue nothing.  Several history sizes
+    (different cell counts); k_sample_fast chooses exactly what the general
+    kernel chooses, so neither the staged rows nor the static LDS after them
+    (guide, run records) were overwritten."""
+    import bench
+    from hyperopt_amd import tpe
+    table = bench.flat_uniform_table(['x'])
+    hists = [bench.soa_history(['x'], n, 11 + n, lambda v: (v['x'] - 0.3) ** 2) for n in (40, 160, 700, 2500)]
+
+    def run():
+        return [tpe.suggest_choices(table, h, np.arange(len(h.losses), len(h.losses) + 3), 9,
+                                    n_EI_candidates=1 << 18, columns=True).values.tolist() for h in hists]
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', '0')
+    fast = run()
+    monkeypatch.setenv('TPE_DEBUG_FLAGS', str(N.BATCH_NO_TAB_FAST))
+    gen = run()
+    assert fast == gen
+
+
 @pytest.fixture(scope='module')
 def quantized_workloads():
     """The rf-steered config-3 history (quantized rf_n_est / rf_depth_n labels,
