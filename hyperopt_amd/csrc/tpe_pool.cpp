@@ -76,17 +76,23 @@ inline uint64_t claim_word(uint32_t g, int n, int i) {
   return (uint64_t)(g & 0xFFFFFFu) << (2 * kJobBits) | (uint64_t)n << kJobBits | (uint64_t)i;
 }
 
-// claim and run the jobs of generation g past the participants' first ones
+// claim and run the jobs of generation g past the participants' first ones, a
+// guided share at a time (the remaining jobs / twice the threads, at least one):
+// a thousand one-microsecond jobs (config 5's label fits and fills) would
+// otherwise pass the claim word's cache line between the threads once a job
 void claim_jobs(Pool* p, uint32_t g) {
+  const int share = 2 * (p->n_workers + 1);
   uint64_t v = p->next.load(std::memory_order_acquire);
   for (;;) {
     if ((uint32_t)(v >> (2 * kJobBits)) != (g & 0xFFFFFFu)) return;
     const int i = (int)(v & ((1u << kJobBits) - 1)), n = (int)((v >> kJobBits) & ((1u << kJobBits) - 1));
     if (i >= n) return;
-    if (!p->next.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+    const int b = std::max(1, (n - i) / share);
+    if (!p->next.compare_exchange_weak(v, v + (uint64_t)b, std::memory_order_acq_rel, std::memory_order_acquire))
+      continue;
     // (the claim holds the generation open: its job fields are current)
-    p->fn(p->ctx, i);
-    p->left.fetch_sub(1, std::memory_order_acq_rel);
+    for (int j = i; j < i + b; ++j) p->fn(p->ctx, j);
+    p->left.fetch_sub(b, std::memory_order_acq_rel);
     v = p->next.load(std::memory_order_acquire);
   }
 }

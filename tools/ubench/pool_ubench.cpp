@@ -26,7 +26,7 @@ void job(void* c, int) {
 
 int main(int argc, char** argv) {
   Ctx c{argc > 1 ? atoll(argv[1]) : 0};
-  for (int n : {2, 4, 8, 10, 16, 32, 64}) {
+  for (int n : {2, 4, 8, 10, 16, 32, 64, 256, 1000}) {
     std::vector<double> t;
     for (int it = 0; it < 3000; ++it) {
       const auto a = clk::now();
