@@ -402,6 +402,14 @@ struct PaTask { int32_t li, side; int64_t i0, i1, off; bool fast; };
 constexpr int64_t kFillChunk = 1024;
 constexpr int64_t kFitStageStretch = 9 * 256;    // tpe_kernels.hip kFitStretch (a chunk's staged stretch)
 constexpr int64_t kFillChunkMinLevel = 16384;   // the level's chunkable components, at least
+// (TPE_FILL_CHUNK_MIN: another threshold, A/B)
+inline int64_t fill_chunk_min_level() {
+  static const int64_t v = [] {
+    const char* e = getenv("TPE_FILL_CHUNK_MIN");
+    return e && *e ? (int64_t)atoll(e) : kFillChunkMinLevel;
+  }();
+  return v;
+}
 struct ChunkTask { int32_t li, side; int64_t i0, i1; int64_t scr; };
 
 struct PackScratch {
@@ -1357,7 +1365,7 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
       if (k > kFillChunk) chunkable += k;
     }
   }
-  if (chunkable >= kFillChunkMinLevel)
+  if (chunkable >= fill_chunk_min_level())
     for (int32_t li = 0; li < n_labels; ++li) {
       const tpe_label_in& L = labels[li];
       if ((L.family != TPE_FAM_GAUSS && L.family != TPE_FAM_LOGGAUSS) || tmode[li] == TPE_TAB_NONE) continue;
