@@ -356,7 +356,11 @@ def _fresh_doc(d):
 def tracked_misc(tid, cmd, workdir, chosen):
     """The misc of one suggested id (miscs_update_idxs_vals for one id,
     base.py:77-105: idxs [tid] / vals [value] per active label, [] per
-    inactive one), built tracked and unowned (rand / tpe suggestions)."""
+    inactive one), built tracked and unowned (rand / tpe suggestions); built
+    by _hostaddr.tracked_misc when the extension is there (the same objects,
+    no Python-level construction of the per-label lists)."""
+    if _ha_misc is not None and type(chosen) is dict:
+        return _ha_misc(tid, cmd, workdir, chosen, _Part, _PartList)
     idxs, vals = _Part(), _Part()
     for k, v in chosen.items():
         if v is None:
@@ -371,6 +375,12 @@ def tracked_misc(tid, cmd, workdir, chosen):
     idxs._up = vals._up = misc
     misc._up, misc._fx = None, False      # (set: a getattr default on an unset slot raises inside)
     return misc
+
+
+try:                                   # (optional until built: python -m hyperopt_amd.build)
+    from hyperopt_amd._hostaddr import tracked_misc as _ha_misc
+except ImportError:                    # pragma: no cover
+    _ha_misc = None
 
 
 def _track(doc, logs):

@@ -7,8 +7,11 @@
  * PyArray_DATA directly. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <structmember.h>
 #define NPY_NO_DEPRECATED_API NPY_2_0_API_VERSION
 #include <numpy/arrayobject.h>
+#include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* addresses(seq[, typenum]) -> int64 array of the items' data addresses (each
@@ -132,11 +135,145 @@ static PyObject *row_dicts(PyObject *self, PyObject *args) {
   return out;
 }
 
+/* a fresh empty instance of a list subclass (zeroed by tp_alloc: an empty
+ * list, its slots unset) — no __new__ / __init__ dispatch */
+static PyObject *new_list_of(PyTypeObject *t) { return t->tp_alloc(t, 0); }
+
+static int set_up(PyObject *o, PyObject *name, PyObject *v) { return PyObject_SetAttr(o, name, v); }
+
+/* the byte offset of a type's __slots__ member `name` (its member
+ * descriptor), or -1: written directly, as the descriptor's __set__ writes */
+static Py_ssize_t slot_offset(PyTypeObject *t, const char *name) {
+  PyObject *d = PyObject_GetAttrString((PyObject *)t, name);
+  if (!d) { PyErr_Clear(); return -1; }
+  Py_ssize_t off = -1;
+  if (Py_IS_TYPE(d, &PyMemberDescr_Type)) {
+    PyMemberDef *m = ((PyMemberDescrObject *)d)->d_member;
+    if (m->type == T_OBJECT_EX && !(m->flags & READONLY)) off = m->offset;
+  }
+  Py_DECREF(d);
+  return off;
+}
+
+static void put_slot(PyObject *o, Py_ssize_t off, PyObject *v) {
+  PyObject **p = (PyObject **)((char *)o + off);
+  PyObject *old = *p;
+  Py_INCREF(v);
+  *p = v;
+  Py_XDECREF(old);
+}
+
+/* tracked_misc(tid, cmd, workdir, chosen, Part, PartList) -> the misc of one
+ * suggested id (base.tracked_misc): idxs [tid] / vals [value] per active
+ * label, [] per inactive one (value None), every list a PartList whose _up is
+ * its dict, the dicts Parts whose _up is the misc, misc._up None and
+ * misc._fx False.  The dict entries go in through the base dict (no tracked
+ * __setitem__), as the Python version's dict.__setitem__. */
+static PyObject *tracked_misc(PyObject *self, PyObject *args) {
+  (void)self;
+  PyObject *tid, *cmd, *workdir, *chosen, *part, *plist;
+  if (!PyArg_ParseTuple(args, "OOOO!O!O!", &tid, &cmd, &workdir, &PyDict_Type, &chosen, &PyType_Type, &part,
+                        &PyType_Type, &plist))
+    return NULL;
+  PyTypeObject *PT = (PyTypeObject *)plist;
+  if (!PyType_IsSubtype(PT, &PyList_Type) || !PyType_IsSubtype((PyTypeObject *)part, &PyDict_Type)) {
+    PyErr_SetString(PyExc_TypeError, "tracked_misc(): Part must subclass dict, PartList list");
+    return NULL;
+  }
+  static PyObject *s_up = NULL, *s_fx = NULL;
+  if (!s_up && !(s_up = PyUnicode_InternFromString("_up"))) return NULL;
+  if (!s_fx && !(s_fx = PyUnicode_InternFromString("_fx"))) return NULL;
+  static PyTypeObject *s_pt = NULL;                /* the PartList type whose _up offset is cached */
+  static Py_ssize_t s_pt_up = -1;
+  if (s_pt != PT) {
+    s_pt_up = slot_offset(PT, "_up");
+    s_pt = PT;
+  }
+  PyObject *idxs = PyObject_CallNoArgs(part), *vals = idxs ? PyObject_CallNoArgs(part) : NULL;
+  PyObject *misc = NULL, *kw = NULL;
+  if (!vals) goto fail;
+  PyObject *k, *v;
+  Py_ssize_t pos = 0;
+  while (PyDict_Next(chosen, &pos, &k, &v)) {
+    PyObject *a = new_list_of(PT), *b = a ? new_list_of(PT) : NULL;
+    if (!b) { Py_XDECREF(a); goto fail; }
+    int bad = v != Py_None && (PyList_Append(a, tid) < 0 || PyList_Append(b, v) < 0);
+    if (!bad && s_pt_up >= 0) {
+      put_slot(a, s_pt_up, idxs);
+      put_slot(b, s_pt_up, vals);
+    } else {
+      bad = bad || set_up(a, s_up, idxs) < 0 || set_up(b, s_up, vals) < 0;
+    }
+    bad = bad || PyDict_SetItem(idxs, k, a) < 0 || PyDict_SetItem(vals, k, b) < 0;
+    Py_DECREF(a);
+    Py_DECREF(b);
+    if (bad) goto fail;
+  }
+  kw = Py_BuildValue("{sOsOsOsOsO}", "tid", tid, "cmd", cmd, "workdir", workdir, "idxs", idxs, "vals", vals);
+  if (!kw) goto fail;
+  {
+    PyObject *empty = PyTuple_New(0);
+    misc = empty ? PyObject_Call(part, empty, kw) : NULL;
+    Py_XDECREF(empty);
+  }
+  if (!misc || set_up(idxs, s_up, misc) < 0 || set_up(vals, s_up, misc) < 0 || set_up(misc, s_up, Py_None) < 0 ||
+      set_up(misc, s_fx, Py_False) < 0)
+    goto fail;
+  Py_DECREF(kw);
+  Py_DECREF(idxs);
+  Py_DECREF(vals);
+  return misc;
+fail:
+  Py_XDECREF(kw);
+  Py_XDECREF(misc);
+  Py_XDECREF(idxs);
+  Py_XDECREF(vals);
+  return NULL;
+}
+
+/* call_tree(fn, ...): tpe_suggest_tree (include/tpe_hip.h) called through its
+ * address with the engine's 23 arguments as Python ints / floats, the GIL
+ * released — ctypes spent microseconds converting them per suggest.  The
+ * TPE_DEBUG_FLAGS environment bits are OR-ed into `flags` here (read per call,
+ * as Engine._flags reads them). */
+typedef int (*tree_fn)(const void *, int32_t, const int64_t *, int64_t, double, int32_t, const int64_t *, int32_t,
+                       int32_t, int64_t, int64_t, const void *, uint64_t, double, int64_t, int32_t, const void *, void *,
+                       void *, double *, int8_t *, int32_t *, int8_t *);
+static PyObject *call_tree(PyObject *self, PyObject *args) {
+  (void)self;
+  unsigned long long fn, labels, below, ids, ex, seed, ws, need, stream, values, active, path, need_fit;
+  int n_labels, lf, n_ids, n_cand, flags;
+  long long n_below, cand_base, n_cand_global, dev_fit_min;
+  double prior_weight, min_draws;
+  if (!PyArg_ParseTuple(args, "KKiKLdiKiiLLKKdLiKKKKKKK", &fn, &labels, &n_labels, &below, &n_below, &prior_weight,
+                        &lf, &ids, &n_ids, &n_cand, &cand_base, &n_cand_global, &ex, &seed, &min_draws,
+                        &dev_fit_min, &flags, &ws, &need, &stream, &values, &active, &path, &need_fit))
+    return NULL;
+  if (!fn) {
+    PyErr_SetString(PyExc_ValueError, "call_tree(): null function");
+    return NULL;
+  }
+  const char *e = getenv("TPE_DEBUG_FLAGS");
+  if (e && *e) flags |= (int)strtol(e, NULL, 10);
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = ((tree_fn)(uintptr_t)fn)((const void *)(uintptr_t)labels, n_labels, (const int64_t *)(uintptr_t)below,
+                                n_below, prior_weight, lf, (const int64_t *)(uintptr_t)ids, n_ids, n_cand, cand_base,
+                                n_cand_global, (const void *)(uintptr_t)ex, (uint64_t)seed, min_draws, dev_fit_min,
+                                flags, (const void *)(uintptr_t)ws, (void *)(uintptr_t)need, (void *)(uintptr_t)stream,
+                                (double *)(uintptr_t)values, (int8_t *)(uintptr_t)active, (int32_t *)(uintptr_t)path,
+                                (int8_t *)(uintptr_t)need_fit);
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
 static PyMethodDef methods[] = {
     {"addresses", addresses, METH_VARARGS,
      "int64 array of the data addresses of a sequence of C-contiguous numpy arrays (of dtype typenum)"},
     {"tails", tails, METH_VARARGS, "float64 concatenation of seq[i][start[i]:stop[i]]"},
     {"row_dicts", row_dicts, METH_VARARGS, "[dict(zip(keys, row)) for row in zip(*columns)]"},
+    {"tracked_misc", tracked_misc, METH_VARARGS, "base.tracked_misc: the tracked misc of one suggested id"},
+    {"call_tree", call_tree, METH_VARARGS, "tpe_suggest_tree through its address (Engine.suggest_tree)"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_hostaddr", NULL, -1, methods,

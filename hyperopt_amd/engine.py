@@ -32,6 +32,10 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 # raw current-stream accessor of the torch build (None: go through torch.cuda.current_stream)
 _RAW_STREAM = getattr(torch._C, '_cuda_getCurrentRawStream', None) if torch is not None else None
+try:                                    # (the native trampoline of tpe_suggest_tree; optional until built)
+    from ._hostaddr import call_tree as _CALL_TREE
+except ImportError:                     # pragma: no cover
+    _CALL_TREE = None
 
 # target number of above-mixture work items per launch (>= 8 per CU on 256 CUs)
 TARGET_WORK = 2048
@@ -185,6 +189,9 @@ class Engine(object):
         self._pinned = None
         self._ws = None                   # cached tpe_level_ws (run_level)
         self._tree_out = ((ctypes.c_int32 * 2)(), N.LevelNeed())   # suggest_tree's path / need records
+        # (their addresses and tpe_suggest_tree's, for the native trampoline)
+        self._tree_addr = (ctypes.addressof(self._tree_out[0]), ctypes.addressof(self._tree_out[1]),
+                           ctypes.cast(self.lib.tpe_suggest_tree, ctypes.c_void_p).value)
         self._tree_io = None              # suggest_tree's argument / result buffers (_TreeIO)
         # when a dict: every run() times each stage with HIP events on the
         # launch stream and appends (ms, CE of the launch) under the kernel name;
@@ -725,19 +732,30 @@ class Engine(object):
         prof = self.profile is not None
         if prof:
             N.check(self.lib.tpe_level_profile(1), self.lib, 'tpe_level_profile')
-        fl = self._flags() | int(flags)
         c_loc, base, c_glob, ex = n_cand, 0, 0, None
         if shard is not None:
             from .dist import shard_range
             base, hi = shard_range(n_cand, shard[0], shard[1])
             c_loc, c_glob = hi - base, n_cand
             ex = exchange.ptr(nl * n, c_loc)
+        # an unsharded call through the trampoline (it ORs in TPE_DEBUG_FLAGS);
+        # a sharded one through ctypes (the exchange struct is a ctypes object)
+        tramp = _CALL_TREE is not None and ex is None
+        fl = ((0 if self.expand else N.BATCH_NO_EXPAND) | (0 if self.fuse else N.BATCH_NO_FUSE) | int(flags)) \
+            if tramp else self._flags() | int(flags)
         for attempt in range(8):          # a later tree level may need larger pools than the first
             ws = self._level_ws()
-            rc = self.lib.tpe_suggest_tree(labels_ptr, nl, io.below_ptr, nb, float(prior_weight), int(lf), io.ids_ptr,
-                                           n, c_loc, base, c_glob, ex, seed64, float(min_draws),
-                                           int(self.device_fit_min), fl, ctypes.byref(ws), ctypes.byref(need), stream,
-                                           io.values_ptr, io.active_ptr, path, io.need_fit_ptr)
+            if tramp:
+                a_path, a_need, fn = self._tree_addr
+                rc = _CALL_TREE(fn, labels_ptr, nl, io.below_ptr, nb, float(prior_weight), int(lf), io.ids_ptr, n,
+                                c_loc, base, c_glob, 0, seed64, float(min_draws), int(self.device_fit_min), fl,
+                                ctypes.addressof(ws), a_need, stream or 0, io.values_ptr, io.active_ptr, a_path,
+                                io.need_fit_ptr)
+            else:
+                rc = self.lib.tpe_suggest_tree(labels_ptr, nl, io.below_ptr, nb, float(prior_weight), int(lf),
+                                               io.ids_ptr, n, c_loc, base, c_glob, ex, seed64, float(min_draws),
+                                               int(self.device_fit_min), fl, ctypes.byref(ws), ctypes.byref(need),
+                                               stream, io.values_ptr, io.active_ptr, path, io.need_fit_ptr)
             if rc != N.E_SPACE:
                 break
             self._grow(need)

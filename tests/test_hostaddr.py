@@ -1,0 +1,66 @@
+"""The _hostaddr CPython extension (hyperopt_amd/csrc/hostaddr.c): each
+function against the Python it replaces."""
+import ctypes
+
+import numpy as np
+import pytest
+
+_ha = pytest.importorskip('hyperopt_amd._hostaddr')
+
+
+def test_addresses_and_tails():
+    arrs = [np.arange(5, dtype=np.float64) + k for k in range(4)]
+    assert _ha.addresses(arrs).tolist() == [a.ctypes.data for a in arrs]
+    got = _ha.tails(arrs, np.array([1, 0, 3, 5]), np.array([3, 2, 5, 5]))
+    np.testing.assert_array_equal(got, np.concatenate([arrs[0][1:3], arrs[1][0:2], arrs[2][3:5]]))
+
+
+def test_row_dicts():
+    keys = ('a', 'b', 'c')
+    cols = [[1, 2, 3], [None, 0.5, 1.5], [7, None, 9]]
+    assert _ha.row_dicts(keys, cols) == [dict(zip(keys, row)) for row in zip(*cols)]
+
+
+def test_tracked_misc_matches_python():
+    """The native misc of a suggested id has the Python version's contents,
+    key order, types and parent links (tracked lists under tracked dicts
+    under the misc, misc._up None, misc._fx False)."""
+    from hyperopt_amd import base
+    chosen = {'m': 1, 'a': None, 'b': 2.5, 'c': None, 'd': np.float64(0.25)}
+    nat = base.tracked_misc(7, ('cmd',), 'wd', chosen)
+    saved = base._ha_misc
+    base._ha_misc = None
+    try:
+        ref = base.tracked_misc(7, ('cmd',), 'wd', chosen)
+    finally:
+        base._ha_misc = saved
+    assert saved is not None
+    for m in (nat, ref):
+        assert type(m) is base._Part and m._up is None and m._fx is False
+        assert list(m) == ['tid', 'cmd', 'workdir', 'idxs', 'vals']
+        for k in ('idxs', 'vals'):
+            assert type(m[k]) is base._Part and m[k]._up is m
+            assert list(m[k]) == list(chosen)
+            for lab, lst in m[k].items():
+                assert type(lst) is base._PartList and lst._up is m[k]
+    assert nat == ref
+    assert type(nat['vals']['d'][0]) is np.float64
+    # the lists are tracked: an edit reaches the misc's log like the Python ones'
+    nat['vals']['b'].append(3.0)
+    assert nat['vals']['b'] == [2.5, 3.0]
+
+
+def test_call_tree_matches_ctypes_on_refused_arguments():
+    """The trampoline passes the same arguments through: a refused call (a
+    negative label count) returns what the ctypes call returns."""
+    from hyperopt_amd import _native as N
+    lib = N.load()
+    fn = ctypes.cast(lib.tpe_suggest_tree, ctypes.c_void_p).value
+    ws, need, path = N.LevelWS(), N.LevelNeed(), (ctypes.c_int32 * 2)()
+    rc_ct = lib.tpe_suggest_tree(0, -1, 0, 0, 1.0, 25, 0, 1, 2048, 0, 0, None, 5, 64.0, 0, 0, ctypes.byref(ws),
+                                 ctypes.byref(need), 0, 0, 0, path, 0)
+    rc_tr = _ha.call_tree(fn, 0, -1, 0, 0, 1.0, 25, 0, 1, 2048, 0, 0, 0, 5, 64.0, 0, 0, ctypes.addressof(ws),
+                          ctypes.addressof(need), 0, 0, 0, ctypes.addressof(path), 0)
+    assert rc_ct == rc_tr == -1                    # TPE_E_ARG
+    with pytest.raises(ValueError):
+        _ha.call_tree(0, 0, -1, 0, 0, 1.0, 25, 0, 1, 2048, 0, 0, 0, 5, 64.0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
