@@ -5436,6 +5436,13 @@ __attribute__((visibility("hidden"))) int tpe_internal_level_run_ex(
 __attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_exchange* ex, int64_t per,
                                                                  hipStream_t s);   // (after the RCCL loader)
 
+// TPE_FORCE_COMBINE=1: a one-rank exchange takes the N-rank device combine
+// (read per call: the tests switch it around single suggests)
+static bool force_combine() {
+  const char* e = getenv("TPE_FORCE_COMBINE");
+  return e && e[0] == '1';
+}
+
 // host-written byte ranges of the packed level as k_upload's 8-byte words; false
 // when a rounded range would pass the device blob (the caller copies instead)
 static bool upload_ranges(const tpe_pack_info& info, int64_t blob_cap, UploadRanges& r, int64_t& words) {
@@ -5767,7 +5774,10 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
     unsigned char* slot = (unsigned char*)lx->ex->dev + (int64_t)lx->ex->rank * xper;
     int32_t* st_host = (int32_t*)(host + res_off + P * (int64_t)sizeof(tpe_result));   // (the pad before rb_off)
     int32_t* st_dev = (int32_t*)(dbase + res_off + P * (int64_t)sizeof(tpe_result));
-    const bool one = lx->ex->world == 1;       // (forced exchange on one rank: no gather, no combine)
+    // (forced exchange on one rank: no gather, no combine — unless
+    // TPE_FORCE_COMBINE=1, the tests' way to run the N > 1 device combine,
+    // slot → in-place all-gather → k_combine, on the box's one GPU)
+    const bool one = lx->ex->world == 1 && !force_combine();
     TPE_LAUNCH(k_runs_reduce, dim3(blocks), dim3(kCombThreads), 0, s, d_span, xtmpl ? nullptr : b.tab_tiles, per,
                b.problems, tpp, (const tpe_result*)b.run_best, (const tpe_result*)b.result, P, slot, (int32_t)TPE_OK,
                one ? rd : (tpe_result*)nullptr, one ? st_dev : (int32_t*)nullptr);

@@ -118,19 +118,30 @@ def _rccl_worker(port, q):
         from hyperopt_amd.engine import get_engine
         domain, trials = bench.make_history(N_HIST, 0)
         # (2^18 candidates: every label tabulated, the runs reduced on the device;
-        # 64: pruned labels selected late, by the select stage)
-        cases = [(21, 1 << 18), (22, 1 << 18), (23, 64)]
-        ref = [doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=c)) for s, c in cases]
+        # 64: pruned labels selected late, by the select stage; 320 ids: a level
+        # of more than 256 problems, whose run spans the host writes; each once
+        # more with TPE_FORCE_COMBINE=1: the N-rank combine — the rank's slot, the
+        # in-place all-gather, k_combine — on one rank)
+        cases = [(21, 1 << 18, 1), (22, 1 << 18, 1), (23, 64, 1), (24, 4096, 320)]
+
+        def run(s, c, n, **kw):
+            docs = tpe.suggest(list(range(N_HIST, N_HIST + n)), domain, trials, s, n_EI_candidates=c, **kw)
+            return [doc_values([d]) for d in docs]
+        ref = [run(*a) for a in cases]
         D.EXCHANGE_ALWAYS = True
         eng = get_engine()
         got = []
-        for s, c in cases:
-            eng.last_tree_path = None
-            got.append(doc_values(tpe.suggest([N_HIST], domain, trials, s, n_EI_candidates=c, shard=(0, 1))))
-            assert eng.last_tree_path is not None
+        for force in ('0', '1'):
+            os.environ['TPE_FORCE_COMBINE'] = force
+            for a in cases:
+                eng.last_tree_path = None
+                got.append(run(*a, shard=(0, 1)))
+                assert eng.last_tree_path is not None
+        os.environ['TPE_FORCE_COMBINE'] = '0'
+        ref = ref + ref
         ex = D.exchange_for(eng)
-        q.put(([{k: float(v) for k, v in r.items()} for r in ref], [{k: float(v) for k, v in g.items()} for g in got],
-               ex.comm is not None, None))
+        q.put(([[{k: float(v) for k, v in d.items()} for d in r] for r in ref],
+               [[{k: float(v) for k, v in d.items()} for d in g] for g in got], ex.comm is not None, None))
         ex.close()
     except Exception as e:
         q.put((None, None, None, repr(e)))
