@@ -267,6 +267,41 @@ static PyObject *call_tree(PyObject *self, PyObject *args) {
   return PyLong_FromLong(rc);
 }
 
+/* insert_sorted(perm, sorted, m, value, index) -> at: one appended value into
+ * a column's sorting permutation (int64) and its sorted values (float64), both
+ * holding m entries and room for one more — at = np.searchsorted(sorted[:m],
+ * value, side='right') (numpy's order: NaN after every number), then the tails
+ * from `at` move up one slot and perm[at] = index, sorted[at] = value
+ * (history.value_order's one-observation case, without the numpy and ctypes
+ * calls per suggest). */
+static int npy_lt(double a, double b) { return a < b || (b != b && a == a); }
+static PyObject *insert_sorted(PyObject *self, PyObject *args) {
+  (void)self;
+  PyArrayObject *perm, *sorted;
+  Py_ssize_t m;
+  double v;
+  long long index;
+  if (!PyArg_ParseTuple(args, "O!O!ndL", &PyArray_Type, &perm, &PyArray_Type, &sorted, &m, &v, &index)) return NULL;
+  if (PyArray_TYPE(perm) != NPY_INT64 || PyArray_TYPE(sorted) != NPY_FLOAT64 || !PyArray_IS_C_CONTIGUOUS(perm) ||
+      !PyArray_IS_C_CONTIGUOUS(sorted) || !PyArray_ISWRITEABLE(perm) || !PyArray_ISWRITEABLE(sorted) || m < 0 ||
+      PyArray_SIZE(perm) < m + 1 || PyArray_SIZE(sorted) < m + 1) {
+    PyErr_SetString(PyExc_ValueError, "insert_sorted(): int64 / float64 contiguous arrays with room for m + 1");
+    return NULL;
+  }
+  int64_t *p = (int64_t *)PyArray_DATA(perm);
+  double *a = (double *)PyArray_DATA(sorted);
+  Py_ssize_t lo = 0, hi = m;
+  while (lo < hi) {                                   /* first i with value < a[i] */
+    const Py_ssize_t mid = lo + ((hi - lo) >> 1);
+    if (npy_lt(v, a[mid])) hi = mid; else lo = mid + 1;
+  }
+  memmove(p + lo + 1, p + lo, (size_t)(m - lo) * sizeof(int64_t));
+  memmove(a + lo + 1, a + lo, (size_t)(m - lo) * sizeof(double));
+  p[lo] = (int64_t)index;
+  a[lo] = v;
+  return PyLong_FromSsize_t(lo);
+}
+
 static PyMethodDef methods[] = {
     {"addresses", addresses, METH_VARARGS,
      "int64 array of the data addresses of a sequence of C-contiguous numpy arrays (of dtype typenum)"},
@@ -274,6 +309,7 @@ static PyMethodDef methods[] = {
     {"row_dicts", row_dicts, METH_VARARGS, "[dict(zip(keys, row)) for row in zip(*columns)]"},
     {"tracked_misc", tracked_misc, METH_VARARGS, "base.tracked_misc: the tracked misc of one suggested id"},
     {"call_tree", call_tree, METH_VARARGS, "tpe_suggest_tree through its address (Engine.suggest_tree)"},
+    {"insert_sorted", insert_sorted, METH_VARARGS, "one value into a sorting permutation and its sorted values"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_hostaddr", NULL, -1, methods,

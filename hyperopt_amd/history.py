@@ -34,6 +34,12 @@ import numpy as np
 
 from . import base
 
+try:                                   # (optional until built: python -m hyperopt_amd.build)
+    from ._hostaddr import insert_sorted as _insert_sorted
+except ImportError:                    # pragma: no cover
+    _insert_sorted = None
+_I64, _F64 = np.dtype(np.int64), np.dtype(np.float64)
+
 _CACHES = weakref.WeakKeyDictionary()
 
 
@@ -396,14 +402,18 @@ class _Cache(object):
         if pg is not None and n - pg.n == 1 and pg.n > 0:
             m = pg.n
             v = vals[m]
-            at = int(sg.view().searchsorted(v, side='right'))
-            for q, x in ((pg, m), (sg, v)):
+            for q in (pg, sg):
                 if q.n == q.a.shape[0]:
                     q.reserve(2 * q.n)
-                w = q.a.itemsize
-                ctypes.memmove(q.addr + (at + 1) * w, q.addr + at * w, (m - at) * w)
-                q.a[at] = x
-                q.n = m + 1
+            if _insert_sorted is not None and pg.a.dtype == _I64 and sg.a.dtype == _F64:
+                _insert_sorted(pg.a, sg.a, m, float(v), m)    # (_hostaddr: the same search and moves)
+            else:
+                at = int(sg.view().searchsorted(v, side='right'))
+                for q, x in ((pg, m), (sg, v)):
+                    w = q.a.itemsize
+                    ctypes.memmove(q.addr + (at + 1) * w, q.addr + at * w, (m - at) * w)
+                    q.a[at] = x
+            pg.n = sg.n = m + 1
         else:
             if pg is None:
                 perm = np.argsort(vals)

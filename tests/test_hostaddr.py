@@ -64,3 +64,24 @@ def test_call_tree_matches_ctypes_on_refused_arguments():
     assert rc_ct == rc_tr == -1                    # TPE_E_ARG
     with pytest.raises(ValueError):
         _ha.call_tree(0, 0, -1, 0, 0, 1.0, 25, 0, 1, 2048, 0, 0, 0, 5, 64.0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+
+
+def test_insert_sorted_matches_numpy():
+    """One value into a sorting permutation and its sorted values: numpy's
+    searchsorted(side='right') position (ties: after the equal ones; NaN after
+    every number) and np.insert's arrays."""
+    rs = np.random.RandomState(1)
+    for _ in range(500):
+        m = rs.randint(0, 40)
+        col = np.sort(np.concatenate([rs.choice([0.5, 1.0, 2.0, np.nan], m // 2), rs.uniform(0, 3, m - m // 2)]))
+        v = float(rs.choice([0.5, 1.0, 2.0, np.nan, rs.uniform(0, 3)]))
+        perm = np.zeros(m + 1, dtype=np.int64)
+        perm[:m] = np.arange(m)
+        sv = np.zeros(m + 1)
+        sv[:m] = col
+        at_ref = int(np.searchsorted(col, v, side='right'))
+        assert _ha.insert_sorted(perm, sv, m, v, m) == at_ref
+        np.testing.assert_array_equal(sv, np.insert(col, at_ref, v))
+        np.testing.assert_array_equal(perm, np.insert(np.arange(m), at_ref, m))
+    with pytest.raises(ValueError):
+        _ha.insert_sorted(np.zeros(3, dtype=np.int64), np.zeros(3), 3, 1.0, 3)     # no room
