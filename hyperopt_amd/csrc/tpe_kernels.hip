@@ -5836,14 +5836,35 @@ static int level_run_impl(const tpe_label_in* labels, int32_t n_labels, int32_t 
       tpe_internal_phase(TPE_PHASE_LEVEL);
       return g_prof.on ? profile_collect(b, info, xtmpl, xfirst, n_cand) : TPE_OK;
     }
-    for (int64_t r = 0; r < P; ++r)
-      if (!hp || hp[r].tab_mode != TPE_TAB_NONE) { rh[r] = tpe_result{0, 0, 0, 0, -1, -1}; }
-    for (int i = 0; i < n_tab; ++i) {
-      const int t = tile_of(i), pr = prob_of(t);
-      if (i % per != 0 && prob_of(tile_of(i - 1)) == pr) continue;        // not a run's first tile
-      const tpe_result& c = rb[t];
-      tpe_result& w = rh[pr];
-      if (host_better(c.score, c.idx, w.score, w.idx)) w = c;
+    const int tpp = b.tiles_per_problem;
+    if (tpp > 0) {
+      // the packer's layout (every problem tpp tiles, the list the tabulated
+      // problems' tiles in problem order): a problem's runs start at its first
+      // list position and at every multiple of per after it — visited directly,
+      // not found by a scan of the whole list (the headline's 5 problems have
+      // ~5000 tabulated tiles and a few hundred runs)
+      int rank = 0;
+      for (int64_t r = 0; r < P; ++r) {
+        if (hp && hp[r].tab_mode == TPE_TAB_NONE) continue;
+        tpe_result w{0, 0, 0, 0, -1, -1};
+        const int a = rank * tpp, e = a + tpp;
+        for (int pos = a; pos < e; pos = (pos / per + 1) * per) {
+          const tpe_result& c = rb[r * tpp + (pos - a)];
+          if (host_better(c.score, c.idx, w.score, w.idx)) w = c;
+        }
+        rh[r] = w;
+        ++rank;
+      }
+    } else {
+      for (int64_t r = 0; r < P; ++r)
+        if (!hp || hp[r].tab_mode != TPE_TAB_NONE) { rh[r] = tpe_result{0, 0, 0, 0, -1, -1}; }
+      for (int i = 0; i < n_tab; ++i) {
+        const int t = tile_of(i), pr = prob_of(t);
+        if (i % per != 0 && prob_of(tile_of(i - 1)) == pr) continue;      // not a run's first tile
+        const tpe_result& c = rb[t];
+        tpe_result& w = rh[pr];
+        if (host_better(c.score, c.idx, w.score, w.idx)) w = c;
+      }
     }
   }
   memcpy(out, rh, (size_t)P * sizeof(tpe_result));
