@@ -4021,11 +4021,45 @@ __global__ __launch_bounds__(kMergeThreads) void k_ord_merge(const tpe_fit_job* 
   __syncthreads();
   const int64_t a0 = split[0], b0 = d0 - a0;
   const int nA = (int)(split[1] - a0), n = (int)(d1 - d0), nB = n - nA;
+  // a tile drawn from one input only is a straight coalesced copy, no LDS
+  // merge (a level that merges a few new observations into a resident order
+  // of 10^5 leaves almost every tile pure A: the merge's LDS bank conflicts
+  // were most of its time)
+  if (nA == 0 || nB == 0) {                          // (block-uniform)
+    const double* ck = nB == 0 ? ak + a0 : bk + b0;
+    const uint32_t* cv = nB == 0 ? av + a0 : bv + b0;
+    double tk[kMergePer];
+    uint32_t tv[kMergePer];
+#pragma unroll
+    for (int e = 0; e < kMergePer; ++e) {            // every load issued before the stores
+      const int i = (int)threadIdx.x + e * kMergeThreads;
+      if (i < n) { tk[e] = ck[i]; tv[e] = cv[i]; }
+    }
+#pragma unroll
+    for (int e = 0; e < kMergePer; ++e) {
+      const int i = (int)threadIdx.x + e * kMergeThreads;
+      if (i < n) { ok[d0 + i] = tk[e]; ov[d0 + i] = tv[e]; }
+    }
+    return;
+  }
   __shared__ double lk[kMergeTile];
   __shared__ uint32_t lv[kMergeTile];
-  for (int i = threadIdx.x; i < n; i += kMergeThreads) {
-    if (i < nA) { lk[i] = ak[a0 + i]; lv[i] = av[a0 + i]; }
-    else { lk[i] = bk[b0 + i - nA]; lv[i] = bv[b0 + i - nA]; }
+  {
+    double tk[kMergePer];
+    uint32_t tv[kMergePer];
+#pragma unroll
+    for (int e = 0; e < kMergePer; ++e) {            // every load issued before the LDS stores
+      const int i = (int)threadIdx.x + e * kMergeThreads;
+      if (i < n) {
+        tk[e] = i < nA ? ak[a0 + i] : bk[b0 + i - nA];
+        tv[e] = i < nA ? av[a0 + i] : bv[b0 + i - nA];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < kMergePer; ++e) {
+      const int i = (int)threadIdx.x + e * kMergeThreads;
+      if (i < n) { lk[i] = tk[e]; lv[i] = tv[e]; }
+    }
   }
   __syncthreads();
   const int dd = min(threadIdx.x * kMergePer, n);
