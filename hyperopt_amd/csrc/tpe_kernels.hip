@@ -3068,9 +3068,20 @@ __global__ __launch_bounds__(256) void k_boxes(const tpe_problem* __restrict__ P
   // sums of 2^c y^n, the 1 / n! applied once to the reduced sums; 2^c from the
   // f32 exp (c is an f32 row value: its own rounding, up to 2^-19 at |c| >= 16,
   // is larger than the f32 exp's 2^-23)
+  // (the next pair's rows loaded before this pair's terms: one row latency per
+  // pair instead of one on every pair's critical path)
+  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0;
+  if (k_lo + lane < k_hi) {
+    n0 = rows[k_lo + lane];
+    n1 = rows[k_lo + lane + 64 < k_hi ? k_lo + lane + 64 : k_lo + lane];
+  }
   for (int k = k_lo + lane; k < k_hi; k += 128) {
     const bool two = k + 64 < k_hi;
-    const float4 q0 = rows[k], q1 = rows[two ? k + 64 : k];
+    const float4 q0 = n0, q1 = n1;
+    if (k + 128 < k_hi) {
+      n0 = rows[k + 128];
+      n1 = rows[k + 192 < k_hi ? k + 192 : k + 128];
+    }
     const bool u0 = q0.w > -INFINITY && q0.z == p.fgt_a, u1 = two && q1.w > -INFINITY && q1.z == p.fgt_a;
     odd += (q0.w > -INFINITY && q0.z != p.fgt_a) + (two && q1.w > -INFINITY && q1.z != p.fgt_a);
     const double y0 = ((double)q0.x + (double)q0.y - centre) * id, y1 = ((double)q1.x + (double)q1.y - centre) * id;
