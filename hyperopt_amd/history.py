@@ -267,6 +267,8 @@ class _Cache(object):
         self._views = dict.fromkeys(labels)     # (label order)
 
     def extend(self, docs, start, log):
+        tids, losses, obs_tid, obs_val, changed = self.tids, self.losses, self.obs_tid, self.obs_val, self.changed
+        last = int(tids.a[tids.n - 1]) if tids.n else None
         for i in range(start, len(docs)):
             d = docs[i]
             misc = d['misc']
@@ -274,27 +276,28 @@ class _Cache(object):
                 self.ok = False
                 return
             tid = d['tid']
-            if self.tids.n and tid <= self.tids.a[self.tids.n - 1]:
+            if last is not None and tid <= last:
                 self.ok = False
                 return
+            last = int(tid)
             self.pos[id(d)] = len(self.docs)
             self.docs.append(d)
-            self.tids.append(tid)
+            tids.append(tid)
             loss = d['result'].get('loss')
             final = d['state'] == base.JOB_STATE_DONE and loss is not None
-            self.losses.append(np.inf if loss is None else float(loss))
+            losses.append(np.inf if loss is None else float(loss))
             vals = misc['vals']
             if not final:
-                self.pending.append(self.tids.n - 1)
-                self.pending_vals[self.tids.n - 1] = (vals, self._snap(vals))
+                self.pending.append(tids.n - 1)
+                self.pending_vals[tids.n - 1] = (vals, self._snap(vals))
             else:
                 self._watch(d, log)
             for k in self.labels:
                 v = vals.get(k)
                 if v:
-                    self.obs_tid[k].append(tid)
-                    self.obs_val[k].append(v[0])
-                    self.changed.add(k)
+                    obs_tid[k].append(tid)
+                    obs_val[k].append(v[0])
+                    changed.add(k)
 
     def obs_views(self):
         """{label: (tids, values)} views of the columns; only the labels that
