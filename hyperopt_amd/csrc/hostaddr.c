@@ -302,6 +302,95 @@ static PyObject *insert_sorted(PyObject *self, PyObject *args) {
   return PyLong_FromSsize_t(lo);
 }
 
+/* obs_append(labels, vals, tid, tcols, vcols, changed): History._Cache.extend's
+   per-label loop for one document (history.py) — for each label k with a truthy
+   vals[k] (a dict or dict subclass read without its methods: the caller passes
+   plain dicts and the package's tracked ones only), tid and vals[k][0] appended to
+   the label's _Grow columns (a[n] = value, n += 1, numpy's item assignment) and k
+   added to `changed`.  Returns -1, or the position of the first label whose
+   column is full (nothing of it written: the caller grows it and goes on). */
+static PyObject *s_a, *s_n;
+
+static int grow_put(PyObject *g, PyObject *value, Py_ssize_t *full) {
+  PyObject *a = PyObject_GetAttr(g, s_a), *nobj = a ? PyObject_GetAttr(g, s_n) : NULL;
+  int rc = -1;
+  if (nobj) {
+    const Py_ssize_t n = PyLong_AsSsize_t(nobj), cap = PyObject_Size(a);
+    if (!(n == -1 && PyErr_Occurred()) && cap >= 0) {
+      if (n >= cap) {
+        *full = 1;
+        rc = 0;
+      } else if (PyObject_SetItem(a, nobj, value) == 0) {
+        PyObject *n1 = PyLong_FromSsize_t(n + 1);
+        rc = n1 ? PyObject_SetAttr(g, s_n, n1) : -1;
+        Py_XDECREF(n1);
+      }
+    }
+  }
+  Py_XDECREF(a);
+  Py_XDECREF(nobj);
+  return rc;
+}
+
+static PyObject *obs_append(PyObject *self, PyObject *args) {
+  (void)self;
+  PyObject *labels, *vals, *tid, *tcols, *vcols, *changed;
+  if (!PyArg_ParseTuple(args, "OO!OO!O!O!", &labels, &PyDict_Type, &vals, &tid, &PyList_Type, &tcols, &PyList_Type,
+                        &vcols, &PySet_Type, &changed))
+    return NULL;
+  PyObject *seq = PySequence_Fast(labels, "obs_append(): labels must be a sequence");
+  if (!seq) return NULL;
+  const Py_ssize_t L = PySequence_Fast_GET_SIZE(seq);
+  if (PyList_GET_SIZE(tcols) != L || PyList_GET_SIZE(vcols) != L) {
+    Py_DECREF(seq);
+    PyErr_SetString(PyExc_ValueError, "obs_append(): one tid and one value column per label");
+    return NULL;
+  }
+  for (Py_ssize_t i = 0; i < L; ++i) {
+    PyObject *k = PySequence_Fast_GET_ITEM(seq, i);
+    PyObject *v = PyDict_GetItemWithError(vals, k);           /* borrowed */
+    if (!v) {
+      if (PyErr_Occurred()) goto fail;
+      continue;
+    }
+    const int t = PyObject_IsTrue(v);
+    if (t < 0) goto fail;
+    if (!t) continue;
+    PyObject *tc = PyList_GET_ITEM(tcols, i), *vc = PyList_GET_ITEM(vcols, i);
+    /* both columns have room (they grow together), else hand the label back */
+    Py_ssize_t full = 0;
+    {
+      PyObject *a = PyObject_GetAttr(tc, s_a), *nobj = a ? PyObject_GetAttr(tc, s_n) : NULL;
+      Py_ssize_t n = nobj ? PyLong_AsSsize_t(nobj) : -1, cap = a ? PyObject_Size(a) : -1;
+      Py_XDECREF(a);
+      Py_XDECREF(nobj);
+      if (PyErr_Occurred()) goto fail;
+      PyObject *b = PyObject_GetAttr(vc, s_a), *mobj = b ? PyObject_GetAttr(vc, s_n) : NULL;
+      Py_ssize_t m = mobj ? PyLong_AsSsize_t(mobj) : -1, capb = b ? PyObject_Size(b) : -1;
+      Py_XDECREF(b);
+      Py_XDECREF(mobj);
+      if (PyErr_Occurred()) goto fail;
+      if (n >= cap || m >= capb) {
+        Py_DECREF(seq);
+        return PyLong_FromSsize_t(i);
+      }
+    }
+    PyObject *x = PySequence_GetItem(v, 0);
+    if (!x) goto fail;
+    if (grow_put(tc, tid, &full) < 0 || grow_put(vc, x, &full) < 0) {
+      Py_DECREF(x);
+      goto fail;
+    }
+    Py_DECREF(x);
+    if (PySet_Add(changed, k) < 0) goto fail;
+  }
+  Py_DECREF(seq);
+  return PyLong_FromLong(-1);
+fail:
+  Py_DECREF(seq);
+  return NULL;
+}
+
 static PyMethodDef methods[] = {
     {"addresses", addresses, METH_VARARGS,
      "int64 array of the data addresses of a sequence of C-contiguous numpy arrays (of dtype typenum)"},
@@ -310,6 +399,7 @@ static PyMethodDef methods[] = {
     {"tracked_misc", tracked_misc, METH_VARARGS, "base.tracked_misc: the tracked misc of one suggested id"},
     {"call_tree", call_tree, METH_VARARGS, "tpe_suggest_tree through its address (Engine.suggest_tree)"},
     {"insert_sorted", insert_sorted, METH_VARARGS, "one value into a sorting permutation and its sorted values"},
+    {"obs_append", obs_append, METH_VARARGS, "one document's observations appended to the label columns"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_hostaddr", NULL, -1, methods,
@@ -317,5 +407,8 @@ static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_hostaddr", NULL, -1
 
 PyMODINIT_FUNC PyInit__hostaddr(void) {
   import_array();
+  s_a = PyUnicode_InternFromString("a");
+  s_n = PyUnicode_InternFromString("n");
+  if (!s_a || !s_n) return NULL;
   return PyModule_Create(&module);
 }

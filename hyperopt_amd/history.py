@@ -35,9 +35,9 @@ import numpy as np
 from . import base
 
 try:                                   # (optional until built: python -m hyperopt_amd.build)
-    from ._hostaddr import insert_sorted as _insert_sorted
+    from ._hostaddr import insert_sorted as _insert_sorted, obs_append as _obs_append
 except ImportError:                    # pragma: no cover
-    _insert_sorted = None
+    _insert_sorted = _obs_append = None
 _I64, _F64 = np.dtype(np.int64), np.dtype(np.float64)
 
 _CACHES = weakref.WeakKeyDictionary()
@@ -251,6 +251,7 @@ class _Cache(object):
         self.obs_tid = {k: _Grow(np.int64) for k in labels}     # tid of each observation (append-only)
         self.obs_val = {k: _Grow(np.int64 if categorical[k] else np.float64) for k in labels}
         self.labels = labels
+        self._cols = ([self.obs_tid[k] for k in labels], [self.obs_val[k] for k in labels])     # (label order)
         self.ok = True                 # fast path still valid
         self.dev = {}                  # device mirrors of the (append-only) columns
         self.orders = {}               # label -> _Grow: value-sorting permutation of its observations
@@ -292,7 +293,13 @@ class _Cache(object):
                 self.pending_vals[tids.n - 1] = (vals, self._snap(vals))
             else:
                 self._watch(d, log)
-            for k in self.labels:
+            # (the loop below in C for the dicts it reads as they read: from the
+            # label it hands back, a column to grow, on in Python)
+            j = _obs_append(self.labels, vals, tid, *self._cols, changed) \
+                if _obs_append is not None and (type(vals) is dict or type(vals) is base._Part) else 0
+            if j < 0:
+                continue
+            for k in self.labels[j:]:
                 v = vals.get(k)
                 if v:
                     obs_tid[k].append(tid)

@@ -85,3 +85,48 @@ def test_insert_sorted_matches_numpy():
         np.testing.assert_array_equal(perm, np.insert(np.arange(m), at_ref, m))
     with pytest.raises(ValueError):
         _ha.insert_sorted(np.zeros(3, dtype=np.int64), np.zeros(3), 3, 1.0, 3)     # no room
+
+
+def test_obs_append_matches_python_loop():
+    """History._Cache.extend's per-label loop in C: the same columns, counts and
+    changed labels as the Python loop, and the first full column handed back
+    with nothing of its label written."""
+    from hyperopt_amd.history import _Grow
+    rs = np.random.RandomState(2)
+    labels = ['a', 'b', 'c', 'd']
+    kinds = {'a': np.float64, 'b': np.int64, 'c': np.float64, 'd': np.float64}
+
+    def cols():
+        return {k: _Grow(np.int64) for k in labels}, {k: _Grow(kinds[k]) for k in labels}
+
+    ct, cv = cols()
+    pt, pv = cols()
+    for tid in range(200):
+        vals = {}
+        for k in labels:
+            r = rs.randint(4)
+            if r == 1:
+                vals[k] = []
+            elif r >= 2:
+                vals[k] = [int(rs.randint(5)) if k == 'b' else (np.float64(rs.uniform()) if r == 3 else rs.uniform())]
+        ch_c, ch_p = set(), set()
+        j = _ha.obs_append(labels, vals, tid, [ct[k] for k in labels], [cv[k] for k in labels], ch_c)
+        for k in (labels[j:] if j >= 0 else []):     # (a full column: Python from there, as extend goes on)
+            v = vals.get(k)
+            if v:
+                ct[k].append(tid); cv[k].append(v[0]); ch_c.add(k)
+        for k in labels:
+            v = vals.get(k)
+            if v:
+                pt[k].append(tid); pv[k].append(v[0]); ch_p.add(k)
+        assert ch_c == ch_p
+    for k in labels:
+        assert ct[k].n == pt[k].n and cv[k].n == pv[k].n
+        np.testing.assert_array_equal(ct[k].view(), pt[k].view())
+        np.testing.assert_array_equal(cv[k].view(), pv[k].view())
+        assert cv[k].view().dtype == pv[k].view().dtype
+    # a full column comes back untouched
+    g_t, g_v = _Grow(np.int64), _Grow(np.float64)
+    g_t.n = g_v.n = g_t.a.shape[0]
+    assert _ha.obs_append(['x'], {'x': [1.5]}, 7, [g_t], [g_v], set()) == 0
+    assert g_t.n == g_t.a.shape[0]
