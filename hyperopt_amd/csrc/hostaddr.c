@@ -311,20 +311,15 @@ static PyObject *insert_sorted(PyObject *self, PyObject *args) {
    column is full (nothing of it written: the caller grows it and goes on). */
 static PyObject *s_a, *s_n;
 
-static int grow_put(PyObject *g, PyObject *value, Py_ssize_t *full) {
+static int grow_put(PyObject *g, PyObject *value) {      /* g.a[g.n] = value; g.n += 1 (room checked) */
   PyObject *a = PyObject_GetAttr(g, s_a), *nobj = a ? PyObject_GetAttr(g, s_n) : NULL;
   int rc = -1;
   if (nobj) {
-    const Py_ssize_t n = PyLong_AsSsize_t(nobj), cap = PyObject_Size(a);
-    if (!(n == -1 && PyErr_Occurred()) && cap >= 0) {
-      if (n >= cap) {
-        *full = 1;
-        rc = 0;
-      } else if (PyObject_SetItem(a, nobj, value) == 0) {
-        PyObject *n1 = PyLong_FromSsize_t(n + 1);
-        rc = n1 ? PyObject_SetAttr(g, s_n, n1) : -1;
-        Py_XDECREF(n1);
-      }
+    const Py_ssize_t n = PyLong_AsSsize_t(nobj);
+    if (!(n == -1 && PyErr_Occurred()) && PyObject_SetItem(a, nobj, value) == 0) {
+      PyObject *n1 = PyLong_FromSsize_t(n + 1);
+      rc = n1 ? PyObject_SetAttr(g, s_n, n1) : -1;
+      Py_XDECREF(n1);
     }
   }
   Py_XDECREF(a);
@@ -357,8 +352,7 @@ static PyObject *obs_append(PyObject *self, PyObject *args) {
     if (t < 0) goto fail;
     if (!t) continue;
     PyObject *tc = PyList_GET_ITEM(tcols, i), *vc = PyList_GET_ITEM(vcols, i);
-    /* both columns have room (they grow together), else hand the label back */
-    Py_ssize_t full = 0;
+    /* both columns have room, else the label is handed back */
     {
       PyObject *a = PyObject_GetAttr(tc, s_a), *nobj = a ? PyObject_GetAttr(tc, s_n) : NULL;
       Py_ssize_t n = nobj ? PyLong_AsSsize_t(nobj) : -1, cap = a ? PyObject_Size(a) : -1;
@@ -377,7 +371,7 @@ static PyObject *obs_append(PyObject *self, PyObject *args) {
     }
     PyObject *x = PySequence_GetItem(v, 0);
     if (!x) goto fail;
-    if (grow_put(tc, tid, &full) < 0 || grow_put(vc, x, &full) < 0) {
+    if (grow_put(tc, tid) < 0 || grow_put(vc, x) < 0) {
       Py_DECREF(x);
       goto fail;
     }
