@@ -596,12 +596,13 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    import gc
+    cg0 = cgroup_cpu_stat()      # (read before the warm-up: nothing between it and the timed steps)
     for i in range(args.warmup):
         step(i)
     barrier()
     lat = []
     n_active = 0
-    import gc
     _GC_COUNT.clear()
     gc.callbacks.append(_count_gc)
     t0 = time.perf_counter()
@@ -611,8 +612,10 @@ def main():
         lat.append(time.perf_counter() - s0)
         n_active += sum(1 for v in docs[0]['misc']['vals'].values() if v)
     barrier()
-    gc.callbacks.remove(_count_gc)
     elapsed = time.perf_counter() - t0
+    cg1 = cgroup_cpu_stat()
+    gc.callbacks.remove(_count_gc)
+    gc_timed = dict(_GC_COUNT)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -660,6 +663,14 @@ def main():
     roof, kernels = roofline(prof, tab_format(domain, trials, C_total))
     stages = {k: float(np.mean([a[0] for a in v])) for k, v in prof.items()}
     ranks = rank_report(world, rank, lat, host_phases(eng, step, k=10, base=6000) if world > 1 else None, stages)
+    # the timed loop's own record (N = 1): every step's latency, the collections
+    # and the cgroup's CPU throttling over it, and — from a separate untimed pass
+    # of 200 more steps — the host phases of the slowest steps
+    tail = None
+    if world == 1:
+        tail = dict(steps_ms=[round(1e3 * x, 4) for x in lat], gc_collections=gc_timed,
+                    cgroup_cpu_stat_warmup_and_timed={k: cg1.get(k, 0) - cg0.get(k, 0) for k in cg1},
+                    slowest_of_200=slow_steps(eng, step, 200, base=30000))
 
 
     # one quantized-branch workload beside the line: the same tree and sizes with
@@ -740,6 +751,8 @@ def main():
                        'history': args.history, 'n_EI_candidates': C_total,
                        'parallelism': 'candidate-shard x%d' % world},
             'p50_suggest_ms': 1e3 * float(np.median(lat)), 'p99_suggest_ms': 1e3 * float(np.percentile(lat, 99)),
+            'mean_suggest_ms': 1e3 * float(np.mean(lat)),
+            'tail': tail,
             'ranks': ranks,
             'p50_suggest_ms_appending': appending['p50_suggest_ms'] if appending else None,
             'appending': appending,
@@ -769,6 +782,52 @@ def _count_gc(phase, info):
     if phase == 'start':
         g = 'gen%d' % info['generation']
         _GC_COUNT[g] = _GC_COUNT.get(g, 0) + 1
+
+
+def cgroup_cpu_stat():
+    """The cgroup's cpu.stat counters (cgroup v2: nr_periods, nr_throttled,
+    throttled_usec, usage_usec, ...), {} where absent."""
+    out = {}
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as f:
+            for line in f:
+                k, v = line.split()
+                out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def slow_steps(eng, step, k=200, base=30000, n_show=5):
+    """k more (untimed-loop) steps with the native host phase clock on: the
+    p50 / mean / p99 of their walls and the phases of the n_show slowest —
+    which part of a slow step grew (Python outside the native call, the fits,
+    the pack, the device round trip)."""
+    import ctypes
+    import gc
+    from hyperopt_amd import _native as N
+    buf = (ctypes.c_double * len(N.PHASES))()
+    ev = []
+    cb = (lambda phase, info: ev.append((len(rows), info['generation'])) if phase == 'start' else None)
+    rows = []
+    gc.callbacks.append(cb)
+    eng.lib.tpe_host_phases(1, None, 0)
+    for i in range(k):
+        s0 = time.perf_counter()
+        step(base + i)
+        w = 1e6 * (time.perf_counter() - s0)
+        eng.lib.tpe_host_phases(1, buf, len(N.PHASES))
+        rows.append((w, [round(float(v), 1) for v in buf]))
+    eng.lib.tpe_host_phases(0, None, 0)
+    gc.callbacks.remove(cb)
+    w = np.array([r[0] for r in rows])
+    order = np.argsort(-w)[:n_show]
+    med = np.median(np.array([r[1] for r in rows]), axis=0)
+    return dict(steps=k, p50_us=round(float(np.median(w)), 1), mean_us=round(float(w.mean()), 1),
+                p99_us=round(float(np.percentile(w, 99)), 1), phase_names=list(N.PHASES),
+                median_phases_us=[round(float(x), 1) for x in med],
+                slowest=[dict(step=int(j), wall_us=round(float(w[j]), 1), phases_us=rows[j][1],
+                              gc=[g for s, g in ev if s == j]) for j in order])
 
 
 def host_phases(eng, step, k=3, base=300):

@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('TPE_HIP_LIB') or os.path.join(HERE, 'libtpe_hip.so')   # override: A/B builds
-ABI_VERSION = 21
+ABI_VERSION = 22
 FIT_DELTA_MAX = 16             # TPE_FIT_DELTA_MAX: new observations read as a delta (no merge)
 BEST_PER_TILE = 8         # TPE_BEST_PER_TILE: tile_best slots per candidate tile
 
@@ -242,7 +242,8 @@ EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_si
            'tpe_host_cat_probs', 'tpe_host_cat_split', 'tpe_host_pack_level', 'tpe_level_run',
            'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read',
            'tpe_suggest_tree', 'tpe_comm_unique_id', 'tpe_comm_init', 'tpe_comm_destroy', 'tpe_combine_results',
-           'tpe_host_threads', 'tpe_host_phases', 'tpe_exchange_allgather', 'tpe_debug_fast_lg')
+           'tpe_host_threads', 'tpe_host_phases', 'tpe_exchange_allgather', 'tpe_debug_fast_lg',
+           'tpe_collectives_issued')
 
 # host phases of tpe_suggest_tree (tpe_host_phases order)
 PHASES = ('prefit', 'pack', 'launched', 'synced', 'level', 'return', 'recs')
@@ -341,6 +342,8 @@ def load(path=LIB_PATH):
     lib.tpe_host_phases.restype = ctypes.c_int
     lib.tpe_debug_fast_lg.argtypes = [P, I64]
     lib.tpe_debug_fast_lg.restype = ctypes.c_int
+    lib.tpe_collectives_issued.argtypes = [ctypes.POINTER(I64)]
+    lib.tpe_collectives_issued.restype = ctypes.c_int
     lib.tpe_level_profile.argtypes = [ctypes.c_int32]
     lib.tpe_level_profile.restype = ctypes.c_int
     lib.tpe_level_profile_read.argtypes = [ctypes.POINTER(StageProf), ctypes.c_int32]
@@ -359,3 +362,12 @@ def check(rc, lib, what):
 
 def tile_size():
     return load().tpe_tile_size()
+
+
+def collectives_issued(lib=None):
+    """ncclAllGather calls the library has issued in this process
+    (tpe_collectives_issued)."""
+    lib = lib or load()
+    n = ctypes.c_int64(0)
+    check(lib.tpe_collectives_issued(ctypes.byref(n)), lib, 'tpe_collectives_issued')
+    return int(n.value)

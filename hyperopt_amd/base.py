@@ -10,6 +10,7 @@ derivable SoA cache of the history for the suggest hot path (``history``).
 import datetime
 import logging
 import operator
+import weakref
 
 import numpy as np
 
@@ -118,9 +119,12 @@ def _logging(base_cls, name, hook):
 # tracked at all (a plain dict inserted by the caller) is watched in full by
 # the cache and re-filtered by every refresh.
 #
-# Each tracked container points at the container holding it (``_up``, unset =
-# not yet part of a document); a tracked container assigned into a document
-# while unowned becomes part of it (no copy).  ``_fx`` goes up the chain to the
+# Each tracked container points at the container holding it (``_up``: a weak
+# reference, None or unset = not yet part of a document — weak, so a document's
+# containers hold no reference cycle and are freed by their reference counts,
+# not by the cyclic collector: a suggestion's misc is 25+ containers, and their
+# collections were the headline suggest's latency tail); a tracked container
+# assigned into a document while unowned becomes part of it (no copy).  ``_fx`` goes up the chain to the
 # document when a watched value is stored anywhere below it.
 
 
@@ -128,7 +132,7 @@ class _Doc(dict):
     """A tracked trial document (see above); ``_ts`` = the mutation logs of
     the Trials holding it, ``_fx`` set once it holds a container it cannot
     track.  Pickles and copies are plain dicts."""
-    __slots__ = ('_ts', '_fx')
+    __slots__ = ('_ts', '_fx', '__weakref__')
 
     def _log(self):
         for t in getattr(self, '_ts', ()):
@@ -180,18 +184,24 @@ _UNTRACKED_KEYS = frozenset(('owner', 'book_time', 'refresh_time', 'version'))
 _READ_KEYS = frozenset(('tid', 'state', 'result', 'misc', 'exp_key'))
 
 
+def _parent(c):
+    """The tracked container holding ``c`` (its ``_up`` weak reference), or None."""
+    r = getattr(c, '_up', None)
+    return r() if r is not None else None
+
+
 def _log_up(c):
-    u = getattr(c, '_up', None)
+    u = _parent(c)
     while u is not None:
         if type(u) is _Doc:
             u._log()
             return
-        u = getattr(u, '_up', None)
+        u = _parent(u)
 
 
 class _Part(dict):
     """A tracked dict inside a document (``result``, ``misc``, ``misc['vals']`` …)."""
-    __slots__ = ('_up', '_fx')
+    __slots__ = ('_up', '_fx', '__weakref__')
 
     _log = _log_up
     _reads = None                      # the keys a history reads (None: all)
@@ -238,7 +248,7 @@ class _Result(_Part):
 
 class _PartList(list):
     """A tracked list inside a document (``misc['vals'][label]`` …)."""
-    __slots__ = ('_up', '_fx')
+    __slots__ = ('_up', '_fx', '__weakref__')
 
     _log = _log_up
 
@@ -290,7 +300,7 @@ def _mark(c):
         c._fx = True
         if type(c) is _Doc:
             return
-        c = getattr(c, '_up', None)
+        c = _parent(c)
 
 
 def _attach(v, parent, key=None):
@@ -303,9 +313,9 @@ def _attach(v, parent, key=None):
     if t in _PLAIN:
         return v
     if t in _TRACKED:
-        up = getattr(v, '_up', None)
+        up = _parent(v)
         if up is None:
-            v._up = parent
+            v._up = weakref.ref(parent)
             if getattr(v, '_fx', False):
                 _mark(parent)
             return v
@@ -341,7 +351,7 @@ def _fresh(v, up=None):
     else:
         return v
     if up is not None:
-        p._up = up
+        p._up = weakref.ref(up)
     return p
 
 
@@ -362,17 +372,18 @@ def tracked_misc(tid, cmd, workdir, chosen):
     if _ha_misc is not None and type(chosen) is dict:
         return _ha_misc(tid, cmd, workdir, chosen, _Part, _PartList)
     idxs, vals = _Part(), _Part()
+    wi, wv = weakref.ref(idxs), weakref.ref(vals)
     for k, v in chosen.items():
         if v is None:
             a, b = _PartList(), _PartList()
         else:
             a, b = _PartList((tid,)), _PartList((v,))
-        a._up = idxs
-        b._up = vals
+        a._up = wi
+        b._up = wv
         dict.__setitem__(idxs, k, a)
         dict.__setitem__(vals, k, b)
     misc = _Part(tid=tid, cmd=cmd, workdir=workdir, idxs=idxs, vals=vals)
-    idxs._up = vals._up = misc
+    idxs._up = vals._up = weakref.ref(misc)
     misc._up, misc._fx = None, False      # (set: a getattr default on an unset slot raises inside)
     return misc
 

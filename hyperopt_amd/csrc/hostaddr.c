@@ -166,8 +166,9 @@ static void put_slot(PyObject *o, Py_ssize_t off, PyObject *v) {
 /* tracked_misc(tid, cmd, workdir, chosen, Part, PartList) -> the misc of one
  * suggested id (base.tracked_misc): idxs [tid] / vals [value] per active
  * label, [] per inactive one (value None), every list a PartList whose _up is
- * its dict, the dicts Parts whose _up is the misc, misc._up None and
- * misc._fx False.  The dict entries go in through the base dict (no tracked
+ * a weak reference to its dict, the dicts Parts whose _up is a weak reference
+ * to the misc, misc._up None and misc._fx False (weak: no reference cycle, see
+ * base.py).  The dict entries go in through the base dict (no tracked
  * __setitem__), as the Python version's dict.__setitem__. */
 static PyObject *tracked_misc(PyObject *self, PyObject *args) {
   (void)self;
@@ -183,15 +184,21 @@ static PyObject *tracked_misc(PyObject *self, PyObject *args) {
   static PyObject *s_up = NULL, *s_fx = NULL;
   if (!s_up && !(s_up = PyUnicode_InternFromString("_up"))) return NULL;
   if (!s_fx && !(s_fx = PyUnicode_InternFromString("_fx"))) return NULL;
-  static PyTypeObject *s_pt = NULL;                /* the PartList type whose _up offset is cached */
+  /* the PartList type whose _up offset is cached: held (a strong reference),
+   * so another type can never reuse its address while the offset is kept */
+  static PyTypeObject *s_pt = NULL;
   static Py_ssize_t s_pt_up = -1;
   if (s_pt != PT) {
-    s_pt_up = slot_offset(PT, "_up");
+    Py_INCREF(PT);
+    Py_XDECREF(s_pt);
     s_pt = PT;
+    s_pt_up = slot_offset(PT, "_up");
   }
   PyObject *idxs = PyObject_CallNoArgs(part), *vals = idxs ? PyObject_CallNoArgs(part) : NULL;
-  PyObject *misc = NULL, *kw = NULL;
+  PyObject *misc = NULL, *kw = NULL, *wi = NULL, *wv = NULL, *wm = NULL;
   if (!vals) goto fail;
+  /* (one weak reference per parent, shared by its lists) */
+  if (!(wi = PyWeakref_NewRef(idxs, NULL)) || !(wv = PyWeakref_NewRef(vals, NULL))) goto fail;
   PyObject *k, *v;
   Py_ssize_t pos = 0;
   while (PyDict_Next(chosen, &pos, &k, &v)) {
@@ -199,10 +206,10 @@ static PyObject *tracked_misc(PyObject *self, PyObject *args) {
     if (!b) { Py_XDECREF(a); goto fail; }
     int bad = v != Py_None && (PyList_Append(a, tid) < 0 || PyList_Append(b, v) < 0);
     if (!bad && s_pt_up >= 0) {
-      put_slot(a, s_pt_up, idxs);
-      put_slot(b, s_pt_up, vals);
+      put_slot(a, s_pt_up, wi);
+      put_slot(b, s_pt_up, wv);
     } else {
-      bad = bad || set_up(a, s_up, idxs) < 0 || set_up(b, s_up, vals) < 0;
+      bad = bad || set_up(a, s_up, wi) < 0 || set_up(b, s_up, wv) < 0;
     }
     bad = bad || PyDict_SetItem(idxs, k, a) < 0 || PyDict_SetItem(vals, k, b) < 0;
     Py_DECREF(a);
@@ -216,14 +223,20 @@ static PyObject *tracked_misc(PyObject *self, PyObject *args) {
     misc = empty ? PyObject_Call(part, empty, kw) : NULL;
     Py_XDECREF(empty);
   }
-  if (!misc || set_up(idxs, s_up, misc) < 0 || set_up(vals, s_up, misc) < 0 || set_up(misc, s_up, Py_None) < 0 ||
-      set_up(misc, s_fx, Py_False) < 0)
+  if (!misc || !(wm = PyWeakref_NewRef(misc, NULL)) || set_up(idxs, s_up, wm) < 0 || set_up(vals, s_up, wm) < 0 ||
+      set_up(misc, s_up, Py_None) < 0 || set_up(misc, s_fx, Py_False) < 0)
     goto fail;
   Py_DECREF(kw);
+  Py_DECREF(wi);
+  Py_DECREF(wv);
+  Py_DECREF(wm);
   Py_DECREF(idxs);
   Py_DECREF(vals);
   return misc;
 fail:
+  Py_XDECREF(wi);
+  Py_XDECREF(wv);
+  Py_XDECREF(wm);
   Py_XDECREF(kw);
   Py_XDECREF(misc);
   Py_XDECREF(idxs);

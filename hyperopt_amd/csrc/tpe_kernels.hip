@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <vector>
 
@@ -4869,11 +4870,12 @@ __global__ __launch_bounds__(64) void k_fit_wide(const tpe_fit_job* __restrict__
     comp[j.wide_off + threadIdx.x] = fit_row(mu, se, w, st.cm);
     comp[j.above_off + i].w = -INFINITY;          // listed apart
   }
-  if ((int)threadIdx.x < j.n_problems) {
+  // every problem of the job (a batched level: one per active id, any count)
+  for (int t = threadIdx.x; t < j.n_problems; t += 64) {
     const double glo = hdr[kFitHdrGrid], ghi = hdr[kFitHdrGrid + 1];
     const float ginv = ghi > glo ? (float)((double)j.grid_n / (ghi - glo)) : 0.f;
     const double pa = c.bounded ? st.M / st.W : 1.0;
-    tpe_problem& p = P[j.problem_first + threadIdx.x];     // (these fields: k_fit_patch copies them too)
+    tpe_problem& p = P[j.problem_first + t];     // (these fields: k_fit_patch copies them too)
     p.above_base = kLn2 * st.cm - log(st.W) - 0.91893853320467274 - log(pa);
     p.wide_len = nw;
     const double pse = fmax(j.prior_sigma, kEPS);
@@ -4943,12 +4945,9 @@ int check_batch(const tpe_batch* b) {
 
 // TPE_EARLY_FIT=0: a level's device fit runs after its upload (else it starts
 // while the host packs the rest of the level: early_fit_hook; A/B, tests)
-bool early_fit_enabled() {
-  static const int on = [] {
-    const char* v = getenv("TPE_EARLY_FIT");
-    return !(v && v[0] == '0');
-  }();
-  return on != 0;
+bool early_fit_enabled() {           // (read per level: the tests switch it)
+  const char* v = getenv("TPE_EARLY_FIT");
+  return !(v && v[0] == '0');
 }
 
 // TPE_RESULT_COPY=1: read the results back with a copy (else the select stage
@@ -5957,14 +5956,26 @@ int rccl_fail(const char* what, ncclResult_t e) {
 
 extern "C" {
 
+static std::atomic<int64_t> g_collectives{0};       // ncclAllGather calls issued (tpe_collectives_issued)
+
 // every rank's `per` bytes at its slot of ex->dev gathered in place on stream s
+// (one rank: the identity, skipped — unless TPE_FORCE_COMBINE=1 runs the
+// N-rank combine on one GPU, where the collective itself is issued too)
 __attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_exchange* ex, int64_t per, hipStream_t s) {
-  if (ex->world == 1) return TPE_OK;          // (an in-place gather over one rank is the identity)
+  if (ex->world == 1 && !(force_combine() && ex->comm)) return TPE_OK;
   Rccl& r = rccl();
   if (!r.ok) return fail(TPE_E_HIP, "librccl not found");
   unsigned char* d = (unsigned char*)ex->dev;
   const ncclResult_t ne = r.all_gather(d + (size_t)per * ex->rank, d, (size_t)per, ncclUint8, (ncclComm_t)ex->comm, s);
-  return ne == ncclSuccess ? TPE_OK : rccl_fail("ncclAllGather", ne);
+  if (ne != ncclSuccess) return rccl_fail("ncclAllGather", ne);
+  g_collectives.fetch_add(1, std::memory_order_relaxed);
+  return TPE_OK;
+}
+
+int tpe_collectives_issued(int64_t* n) {
+  if (!n) return fail(TPE_E_ARG, "tpe_collectives_issued: null");
+  *n = g_collectives.load(std::memory_order_relaxed);
+  return TPE_OK;
 }
 
 int tpe_comm_unique_id(void* id) {
@@ -6032,6 +6043,7 @@ int tpe_exchange_allgather(const tpe_exchange* ex, const void* mine, int64_t byt
     const ncclResult_t ne = r.all_gather(d + (size_t)bytes * ex->rank, d, (size_t)bytes, ncclUint8,
                                          (ncclComm_t)ex->comm, s);
     if (ne != ncclSuccess) return rccl_fail("ncclAllGather", ne);
+    g_collectives.fetch_add(1, std::memory_order_relaxed);
     e = hipMemcpyAsync(all, d, (size_t)bytes * W, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(TPE_E_HIP, hipGetErrorString(e));

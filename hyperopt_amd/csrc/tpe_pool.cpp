@@ -236,6 +236,15 @@ Pool* get_pool() {
 namespace tpe_pool {
 
 void parallel_for(int n, void (*fn)(void*, int), void* ctx) {
+  // TPE_POOL_TRACE=1: every dispatch's job count and the participants it
+  // found awake, on stderr (diagnostic)
+  static const bool trace = [] { const char* e = getenv("TPE_POOL_TRACE"); return e && e[0] == '1'; }();
+  if (trace) {
+    int awake = 0;
+    if (g_pool)
+      for (int w = 1; w <= g_pool->n_workers; ++w) awake += g_pool->slot[w].awake.load(std::memory_order_relaxed);
+    fprintf(stderr, "[tpe_pool] dispatch n=%d awake=%d\n", n, awake);
+  }
   Pool* const held = n >= 2 && n < (1 << kJobBits) ? get_pool() : nullptr;
   Pool* p = held;
   std::unique_lock<std::mutex> own;

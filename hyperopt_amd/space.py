@@ -209,19 +209,29 @@ class ParamTable(object):
     def rng_order(self):
         """Order in which the reference's shared RandomState is consumed:
         labels visited in descending order (rec_eval pops the sorted vals-dict
-        inputs LIFO, pyll/base.py:179-190, 794-797), ancestors first."""
+        inputs LIFO, pyll/base.py:179-190, 794-797), ancestors first.  Static
+        per table: computed once (an iterative walk — a recursive closure is a
+        reference cycle, garbage for the collector on every call)."""
+        order = self.__dict__.get('_rng_order')
+        if order is not None:
+            return order
         order, seen = [], set()
-
-        def visit(r):
-            if r.label in seen:
-                return
-            for p in r.parents:
-                if p is not None:
-                    visit(self.by_label[p[0]])
-            seen.add(r.label)
-            order.append(r)
-        for r in reversed(self.rows):
-            visit(r)
+        for r0 in reversed(self.rows):
+            stack = [(r0, False)]
+            while stack:
+                r, expanded = stack.pop()
+                if r.label in seen:
+                    continue
+                if expanded:
+                    seen.add(r.label)
+                    order.append(r)
+                    continue
+                stack.append((r, True))
+                # (the parents visited first, in their listed order)
+                for p in reversed(r.parents):
+                    if p is not None and p[0] not in seen:
+                        stack.append((self.by_label[p[0]], False))
+        self._rng_order = order
         return order
 
     def active(self, row, chosen):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 21
+#define TPE_ABI_VERSION 22
 
 /* finalize slots per candidate tile: tile_best holds n_tiles * TPE_BEST_PER_TILE entries */
 #define TPE_BEST_PER_TILE 8
@@ -807,6 +807,14 @@ typedef struct tpe_exchange {
 int tpe_comm_unique_id(void* id);
 int tpe_comm_init(int32_t rank, int32_t world, const void* id, int32_t device, void** comm);
 int tpe_comm_destroy(void* comm);
+
+/* collectives (ncclAllGather calls) this library has issued in this process,
+ * in *n: the device combine of candidate-sharded levels and
+ * tpe_exchange_allgather over RCCL.  A one-rank exchange (world 1, `always`)
+ * issues its in-place all-gather only under TPE_FORCE_COMBINE=1 (the N-rank
+ * combine run on one GPU: tests), else the gather is the identity and is
+ * skipped.  (ABI 22) */
+int tpe_collectives_issued(int64_t* n);
 
 /* the exchange's reduction on the host: all[world][P] -> out[P], np.argmax
  * order over (score, global_idx), empty records (idx < 0) skipped */

@@ -513,6 +513,44 @@ def test_device_fit_batched_labels_and_suggest():
             assert abs(g[k] - r[k]) <= 1e-3 * max(1.0, abs(r[k])), (k, g[k], r[k])
 
 
+@pytest.mark.parametrize('early', ['1', '0'])
+def test_device_fit_more_than_64_ids(monkeypatch, early):
+    """A device-fitted label active for 130 ids in one batched level (260 problems: an expanded level where the labels tabulate; ADVICE r5:
+    k_fit_wide wrote the problem fields of the first 64 ids only), with the fit
+    launched from inside the pack (early fit, k_fit_patch) and after the upload:
+    every id's choice equals the host-fitted suggest's (eps-tie set) and the
+    device-fitted labels' values are the same for a 1-id suggest of that id."""
+    from hyperopt_amd import hp, tpe
+    from hyperopt_amd.engine import get_engine
+    from hyperopt_amd.history import History
+    from hyperopt_amd.space import ParamTable
+    monkeypatch.setenv('TPE_EARLY_FIT', early)
+    rs = np.random.RandomState(43)
+    N, n_ids = 5000, 130
+    labels = {'a': hp.uniform('a', -5, 5), 'b': hp.loguniform('b', -3, 2)}
+    vals = {'a': rs.uniform(-5, 5, N), 'b': np.exp(rs.uniform(-3, 2, N))}
+    tids = np.arange(N)
+    losses = (vals['a'] - 1) ** 2 + 0.1 * np.log(vals['b']) ** 2 + rs.uniform(0, 1e-3, N)
+    hist = History(tids, losses, {k: (tids, v) for k, v in vals.items()})
+    table = ParamTable(labels)
+    ids = list(range(N, N + n_ids))
+    engine = get_engine()
+    old = engine.device_fit_min
+    try:
+        engine.device_fit_min = 1000
+        got = tpe.suggest_choices(table, hist, ids, 7, n_EI_candidates=1024)
+        one = tpe.suggest_choices(table, hist, [ids[-1]], 7, n_EI_candidates=1024)
+        engine.device_fit_min = 10 ** 9
+        ref = tpe.suggest_choices(table, hist, ids, 7, n_EI_candidates=1024)
+    finally:
+        engine.device_fit_min = old
+    assert len(got) == len(ref) == n_ids
+    for g, r in zip(got, ref):
+        for k in 'ab':
+            assert np.isfinite(g[k]) and abs(g[k] - r[k]) <= 1e-3 * max(1.0, abs(r[k])), (k, g[k], r[k])
+    assert got[-1] == one[0]
+
+
 def test_local_expansion_matches_exact_and_is_used(engine, monkeypatch):
     """The pruned f32 kernel's local (Taylor) expansion: above-lpdf of 2^20
     sampled candidates within 1e-5 of the all-exact kernel and within the fp32

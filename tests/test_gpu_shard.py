@@ -114,7 +114,7 @@ def _rccl_worker(port, q):
     dist.init_process_group('nccl', rank=0, world_size=1)
     try:
         import bench
-        from hyperopt_amd import dist as D, tpe
+        from hyperopt_amd import _native as N, dist as D, tpe
         from hyperopt_amd.engine import get_engine
         domain, trials = bench.make_history(N_HIST, 0)
         # (2^18 candidates: every label tabulated, the runs reduced on the device;
@@ -130,21 +130,24 @@ def _rccl_worker(port, q):
         ref = [run(*a) for a in cases]
         D.EXCHANGE_ALWAYS = True
         eng = get_engine()
-        got = []
+        got, issued = [], {}
         for force in ('0', '1'):
             os.environ['TPE_FORCE_COMBINE'] = force
+            n0 = N.collectives_issued(eng.lib)
             for a in cases:
                 eng.last_tree_path = None
                 got.append(run(*a, shard=(0, 1)))
                 assert eng.last_tree_path is not None
+            issued[force] = N.collectives_issued(eng.lib) - n0
         os.environ['TPE_FORCE_COMBINE'] = '0'
         ref = ref + ref
         ex = D.exchange_for(eng)
         q.put(([[{k: float(v) for k, v in d.items()} for d in r] for r in ref],
-               [[{k: float(v) for k, v in d.items()} for d in g] for g in got], ex.comm is not None, None))
+               [[{k: float(v) for k, v in d.items()} for d in g] for g in got], ex.comm is not None, issued, None))
         ex.close()
     except Exception as e:
-        q.put((None, None, None, repr(e)))
+        import traceback
+        q.put((None, None, None, None, traceback.format_exc()))
     finally:
         dist.destroy_process_group()
 
@@ -159,11 +162,74 @@ def test_rccl_exchange_one_rank():
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
     p.start()
-    ref, got, rccl, err = q.get(timeout=240)
+    ref, got, rccl, issued, err = q.get(timeout=240)
     p.join(timeout=60)
     assert err is None, err
     assert rccl, 'the exchange did not take the RCCL path'
     assert ref == got
+    # ncclAllGather itself ran: the device combine of a one-rank exchange skips
+    # its identity gather (the pruned 64-candidate levels still exchange through
+    # tpe_exchange_allgather over RCCL), and TPE_FORCE_COMBINE=1 issues the
+    # in-place all-gather of every device-combined level as well (>= 3 suggests)
+    assert issued['0'] >= 1, issued
+    assert issued['1'] - issued['0'] >= 3, issued
+
+
+def _rccl_axes_worker(port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1)
+    try:
+        from hyperopt_amd import _native as N, dist as D, tpe
+        from hyperopt_amd.engine import get_engine
+        eng = get_engine()
+        t4, h4 = _cfg4()
+        ids = np.arange(10000, 10000 + 600)
+        out = {}
+        for name, kw in (('ids', 'shard_ids'), ('labels', 'shard_labels')):
+            ref = tpe.suggest_choices(t4, h4, ids, 61, n_EI_candidates=4096, columns=True)
+            n0 = N.collectives_issued(eng.lib)
+            cc = tpe.suggest_choices(t4, h4, ids, 61, n_EI_candidates=4096, columns=True, **{kw: (0, 1)})
+            out[name] = (np.array_equal(ref.values, cc.values, equal_nan=True), np.array_equal(ref.active, cc.active),
+                         N.collectives_issued(eng.lib) - n0)
+        ex = D.exchange_for(eng)
+        # the gathers themselves on a device buffer: rank 0's block comes back as is
+        v = np.random.RandomState(5).uniform(size=(37, 20))
+        a = v > 0.3
+        gv, ga = D.gather_id_blocks(ex, v, a, 37, 20)
+        gl = D.gather_label_columns(ex, v, [0] * 20)
+        out['direct'] = (np.array_equal(gv, v) and np.array_equal(ga, a) and np.array_equal(gl, v), True, 0)
+        q.put((out, ex.comm is not None, None))
+        ex.close()
+    except Exception:
+        import traceback
+        q.put((None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_id_and_label_axes_one_rank():
+    """The new-id and hyperparameter axes' one all-gather over RCCL
+    (tpe_exchange_allgather on a device buffer: copy in, in-place ncclAllGather,
+    copy out) on a one-rank nccl group: config-4-shaped batched suggests
+    (600 ids x 20 labels) equal the unsharded ones bit for bit, and each sharded
+    suggest issued exactly one collective."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_axes_worker, args=(_free_port(), q))
+    p.start()
+    out, rccl, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    assert rccl, 'the exchange did not take the RCCL path'
+    for name in ('ids', 'labels'):
+        same_v, same_a, n = out[name]
+        assert same_v and same_a, name
+        assert n == 1, (name, n)
+    assert out['direct'][0]
 
 
 # ------------------------------------------------ new-id and hyperparameter axes

@@ -39,10 +39,10 @@ def test_tracked_misc_matches_python():
         assert type(m) is base._Part and m._up is None and m._fx is False
         assert list(m) == ['tid', 'cmd', 'workdir', 'idxs', 'vals']
         for k in ('idxs', 'vals'):
-            assert type(m[k]) is base._Part and m[k]._up is m
+            assert type(m[k]) is base._Part and m[k]._up() is m
             assert list(m[k]) == list(chosen)
             for lab, lst in m[k].items():
-                assert type(lst) is base._PartList and lst._up is m[k]
+                assert type(lst) is base._PartList and lst._up() is m[k]
     assert nat == ref
     assert type(nat['vals']['d'][0]) is np.float64
     # the lists are tracked: an edit reaches the misc's log like the Python ones'
@@ -130,3 +130,35 @@ def test_obs_append_matches_python_loop():
     g_t.n = g_v.n = g_t.a.shape[0]
     assert _ha.obs_append(['x'], {'x': [1.5]}, 7, [g_t], [g_v], set()) == 0
     assert g_t.n == g_t.a.shape[0]
+
+
+def test_suggestion_documents_hold_no_reference_cycles():
+    """A suggestion's document (tracked misc, result, the doc itself) is freed
+    by reference counting: the parent links are weak, and the tree walk of
+    ParamTable.rng_order is no recursive closure — nothing per suggest is
+    left for the cyclic collector (whose collections were the headline
+    suggest's latency tail)."""
+    import gc
+    import bench
+    from hyperopt_amd import base, rand
+    domain, trials = bench.make_history(60, 3)
+    d = rand.suggest([500], domain, trials, 1)     # (first call: caches)
+    del d
+    gc.collect()
+    gc.disable()
+    gc.set_debug(gc.DEBUG_SAVEALL)
+    try:
+        for i in range(40):
+            d = rand.suggest([600 + i], domain, trials, i)
+            # the links still lead up to the document, for the mutation logs
+            lst = d[0]['misc']['vals']['model']
+            assert lst._up() is d[0]['misc']['vals'] and d[0]['misc']['vals']._up() is d[0]['misc']
+            del d, lst
+        gc.collect()
+        # (other tests' objects may be collected here too: only this loop's count)
+        ours = [o for o in gc.garbage if type(o) in (base._Doc, base._Part) and 600 <= o.get('tid', -1) < 640]
+    finally:
+        gc.set_debug(0)
+        gc.garbage.clear()
+        gc.enable()
+    assert not ours, len(ours)
