@@ -23,10 +23,12 @@ cpu_baseline: the CPU oracle (numpy restatement of the reference) on a bounded
 p50_suggest_ms_appending: the same suggest in an FMinIter loop (one finished
           document inserted before every suggest, fmin.py:88-92).
 config4_strong: BASELINE config 4 (4096 new ids x 4096 candidates x 20 dims)
-          with the hyperparameters (--axis4 labels, the default) or the ids
-          (--axis4 ids) split over the N ranks and one all-gather of the chosen
-          values (tpe.suggest_choices(shard_labels= / shard_ids=...)): strong
-          scaling of the axes that shard without a per-level exchange.
+          with its (label x id) problem grid cut into label groups x id blocks
+          (--axis4 grid, the default: dist.grid_shape, 4 x 2 at 8 ranks), or
+          the hyperparameters (--axis4 labels) or the ids (--axis4 ids) alone,
+          split over the N ranks and one all-gather of the chosen values
+          (tpe.suggest_choices(shard_grid= / shard_labels= / shard_ids=...)):
+          strong scaling of the axes that shard without a per-level exchange.
 """
 import argparse
 import json
@@ -458,21 +460,23 @@ def config_workload(config, rank, world, args):
         n_ids, C = 4096, 4096
         ids = np.arange(10000, 10000 + n_ids)
         sid = (rank, world) if world > 1 else None
-        # N > 1: the hyperparameter axis (each rank fits, packs, tabulates and
-        # samples its labels for every id: no per-rank work left unsharded but the
-        # Python around the call) or the new-id axis (each rank its block of ids,
-        # every label's fits and tables on every rank); one all-gather of the
-        # chosen values either way — every rank holds all 4096 x 20
-        by_labels = getattr(args, 'axis4', 'labels') == 'labels'
-        kw = {'shard_labels' if by_labels else 'shard_ids': sid}
+        # N > 1: the 2-D grid (each rank a label group's fits, rows and tables and
+        # its id block's sample pass: every rank the same problem count), the
+        # hyperparameter axis (each rank its labels for every id) or the new-id
+        # axis (each rank its block of ids, every label's fits and tables on
+        # every rank); one all-gather of the chosen values either way — every
+        # rank holds all 4096 x 20
+        axis = getattr(args, 'axis4', 'grid')
+        kw = {dict(grid='shard_grid', labels='shard_labels', ids='shard_ids')[axis]: sid}
 
         def step(i, columns=True):
             # SoA in, SoA out (tpe.ChoiceColumns); columns=False: per-id dicts
             tpe.suggest_choices(table, hist, ids, SEED + i, n_EI_candidates=C, columns=columns, **kw)
             return len(labels) * n_ids * C          # whole job
+        what = dict(grid='(label group x id block) grid', labels='hyperparameters', ids='new_ids')[axis]
         return ('config4: batched suggest, 4096 new_ids x 4096 candidates, 20-dim U(-5,5), 10k-trial '
                 'history, %s sharded over ranks + one all-gather of the chosen values, columnar results'
-                % ('hyperparameters' if by_labels else 'new_ids')), step, None
+                % what), step, None
     if config == 5 and args.appending:
         # FMinIter's flow on the columnar history (fmin.py:88-92): every suggest
         # follows the evaluation of the previous one, appended as one observation
@@ -543,8 +547,8 @@ def main():
     ap.add_argument('--history', type=int, default=N_HISTORY)
     ap.add_argument('--cands', type=int, default=C_PER_GPU)
     ap.add_argument('--config', type=int, default=3, help='BASELINE.json config (3 = headline)')
-    ap.add_argument('--axis4', choices=('labels', 'ids'), default='labels',
-                    help='config 4 over N > 1 ranks: shard the hyperparameters or the new ids')
+    ap.add_argument('--axis4', choices=('grid', 'labels', 'ids'), default='grid',
+                    help='config 4 over N > 1 ranks: shard the (label x id) grid, the hyperparameters or the new ids')
     ap.add_argument('--dims', type=int, default=1000, help='config 5 dimensions')
     ap.add_argument('--history5', type=int, default=100000, help='config 5 history length')
     ap.add_argument('--appending', action='store_true',
@@ -737,7 +741,8 @@ def main():
             el4 = float(t.item())
         cfg4 = dict(workload=desc4, value=units4 * n4 / el4, unit='candidate-scores/s', steps=n4,
                     ms_per_step=1e3 * el4 / n4, scaling='strong', n_gpus=world,
-                    parallelism='%s shard x%d' % ('hyperparameter' if args.axis4 == 'labels' else 'new-id', world))
+                    parallelism='%s shard x%d' % (dict(grid='label-group x id-block', labels='hyperparameter',
+                                                       ids='new-id')[args.axis4], world))
 
     if rank == 0:
         out = {
@@ -918,7 +923,8 @@ def run_other(args, rank, world, device):
     if ranks is not None:
         extra['ranks'] = ranks
     if args.config == 4:
-        # the same batched suggest returning per-id dicts (numpy scalars per value)
+        # the same batched suggest returning per-id dicts (Python int / float values:
+        # a batch of more than 4 ids, tpe._result_dicts)
         lat_d = []
         for i in range(3):
             s0 = time.perf_counter()

@@ -243,7 +243,7 @@ EXPORTS = ('tpe_abi_version', 'tpe_last_error', 'tpe_device_count', 'tpe_tile_si
            'tpe_replay_mixture', 'tpe_replay_categorical', 'tpe_level_profile', 'tpe_level_profile_read',
            'tpe_suggest_tree', 'tpe_comm_unique_id', 'tpe_comm_init', 'tpe_comm_destroy', 'tpe_combine_results',
            'tpe_host_threads', 'tpe_host_phases', 'tpe_exchange_allgather', 'tpe_debug_fast_lg',
-           'tpe_collectives_issued')
+           'tpe_collectives_issued', 'tpe_scatter_f64', 'tpe_move_ranges')
 
 # host phases of tpe_suggest_tree (tpe_host_phases order)
 PHASES = ('prefit', 'pack', 'launched', 'synced', 'level', 'return', 'recs')
@@ -344,6 +344,10 @@ def load(path=LIB_PATH):
     lib.tpe_debug_fast_lg.restype = ctypes.c_int
     lib.tpe_collectives_issued.argtypes = [ctypes.POINTER(I64)]
     lib.tpe_collectives_issued.restype = ctypes.c_int
+    lib.tpe_scatter_f64.argtypes = [P, I64, P, P]
+    lib.tpe_scatter_f64.restype = ctypes.c_int
+    lib.tpe_move_ranges.argtypes = [P, ctypes.c_int32, ctypes.c_int32, P, P, P]
+    lib.tpe_move_ranges.restype = ctypes.c_int
     lib.tpe_level_profile.argtypes = [ctypes.c_int32]
     lib.tpe_level_profile.restype = ctypes.c_int
     lib.tpe_level_profile_read.argtypes = [ctypes.POINTER(StageProf), ctypes.c_int32]

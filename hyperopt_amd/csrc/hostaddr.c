@@ -10,6 +10,7 @@
 #include <structmember.h>
 #define NPY_NO_DEPRECATED_API NPY_2_0_API_VERSION
 #include <numpy/arrayobject.h>
+#include <numpy/arrayscalars.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -132,6 +133,79 @@ static PyObject *row_dicts(PyObject *self, PyObject *args) {
     }
     PyList_SET_ITEM(out, i, d);
   }
+  return out;
+}
+
+/* typed_dicts(keys, ix, cat, values, active) -> per row i of values / active
+ * ([n x L] float64 / int8, C-contiguous) the dict {keys[j]: value} in the
+ * order of `keys` (k labels; ix: their k table indices, int64; cat: k bytes, 1
+ * for a categorical label): np.int64(values[i, ix[j]]) for a categorical,
+ * np.float64 for any other, None where active[i, ix[j]] == 0 — the reference's
+ * value types (its vals come out of numpy arrays), made without a Python call
+ * per value (a suggest of a 1000-dim space: 1000 scalars). */
+static PyObject *typed_dicts(PyObject *self, PyObject *args) {
+  (void)self;
+  PyObject *keys, *ao, *co, *vo, *acto;
+  if (!PyArg_ParseTuple(args, "O!OOOO", &PyTuple_Type, &keys, &ao, &co, &vo, &acto)) return NULL;
+  PyArrayObject *ix = (PyArrayObject *)PyArray_FROMANY(ao, NPY_INT64, 1, 1, NPY_ARRAY_IN_ARRAY);
+  PyArrayObject *cat = ix ? (PyArrayObject *)PyArray_FROMANY(co, NPY_INT8, 1, 1, NPY_ARRAY_IN_ARRAY) : NULL;
+  PyObject *out = NULL;
+  if (!cat) goto done;
+  if (!PyArray_Check(vo) || !PyArray_Check(acto)) {
+    PyErr_SetString(PyExc_TypeError, "typed_dicts(): values / active must be numpy arrays");
+    goto done;
+  }
+  {
+    PyArrayObject *va = (PyArrayObject *)vo, *aa = (PyArrayObject *)acto;
+    const Py_ssize_t k = PyTuple_GET_SIZE(keys);
+    if (PyArray_NDIM(va) != 2 || PyArray_NDIM(aa) != 2 || PyArray_TYPE(va) != NPY_FLOAT64 ||
+        (PyArray_TYPE(aa) != NPY_INT8 && PyArray_TYPE(aa) != NPY_BOOL) || !PyArray_IS_C_CONTIGUOUS(va) ||
+        !PyArray_IS_C_CONTIGUOUS(aa) || PyArray_DIM(va, 0) != PyArray_DIM(aa, 0) ||
+        PyArray_DIM(va, 1) != PyArray_DIM(aa, 1) || PyArray_DIM(ix, 0) != k || PyArray_DIM(cat, 0) != k) {
+      PyErr_SetString(PyExc_ValueError, "typed_dicts(): values / active [n x L] float64 / int8, k keys");
+      goto done;
+    }
+    const npy_intp n = PyArray_DIM(va, 0), L = PyArray_DIM(va, 1);
+    const npy_int64 *ixp = (const npy_int64 *)PyArray_DATA(ix);
+    const npy_int8 *cp = (const npy_int8 *)PyArray_DATA(cat);
+    for (Py_ssize_t j = 0; j < k; ++j)
+      if (ixp[j] < 0 || ixp[j] >= L) {
+        PyErr_SetString(PyExc_ValueError, "typed_dicts(): index out of range");
+        goto done;
+      }
+    out = PyList_New(n);
+    if (!out) goto done;
+    const double *v = (const double *)PyArray_DATA(va);
+    const npy_int8 *a = (const npy_int8 *)PyArray_DATA(aa);
+    for (npy_intp i = 0; i < n; ++i) {
+      PyObject *d = _PyDict_NewPresized(k);
+      if (!d) { Py_CLEAR(out); goto done; }
+      PyList_SET_ITEM(out, i, d);
+      for (Py_ssize_t j = 0; j < k; ++j) {
+        const npy_intp t = (npy_intp)ixp[j];
+        PyObject *o;
+        if (!a[i * L + t]) {
+          o = Py_None;
+          Py_INCREF(o);
+        } else if (cp[j]) {
+          o = PyArrayScalar_New(Long);
+          if (o) PyArrayScalar_ASSIGN(o, Long, (npy_long)v[i * L + t]);
+        } else {
+          o = PyArrayScalar_New(Double);
+          if (o) PyArrayScalar_ASSIGN(o, Double, v[i * L + t]);
+        }
+        if (!o || PyDict_SetItem(d, PyTuple_GET_ITEM(keys, j), o) < 0) {
+          Py_XDECREF(o);
+          Py_CLEAR(out);
+          goto done;
+        }
+        Py_DECREF(o);
+      }
+    }
+  }
+done:
+  Py_XDECREF(ix);
+  Py_XDECREF(cat);
   return out;
 }
 
@@ -403,6 +477,7 @@ static PyMethodDef methods[] = {
      "int64 array of the data addresses of a sequence of C-contiguous numpy arrays (of dtype typenum)"},
     {"tails", tails, METH_VARARGS, "float64 concatenation of seq[i][start[i]:stop[i]]"},
     {"row_dicts", row_dicts, METH_VARARGS, "[dict(zip(keys, row)) for row in zip(*columns)]"},
+    {"typed_dicts", typed_dicts, METH_VARARGS, "per-row {label: np.int64 / np.float64 / None} dicts"},
     {"tracked_misc", tracked_misc, METH_VARARGS, "base.tracked_misc: the tracked misc of one suggested id"},
     {"call_tree", call_tree, METH_VARARGS, "tpe_suggest_tree through its address (Engine.suggest_tree)"},
     {"insert_sorted", insert_sorted, METH_VARARGS, "one value into a sorting permutation and its sorted values"},

@@ -3790,6 +3790,36 @@ __global__ __launch_bounds__(kUploadThreads) void k_upload(const unsigned long l
   }
 }
 
+// ============================================================ column store
+// (include/tpe_hip.h "Device column store").  k_scatter_f64: the appended
+// observations of a history's device columns, k values then k int64 positions
+// in pinned host memory (system-scope loads, as k_upload), stored into the
+// flat column store; k_move_ranges: a store re-layout, every segment's live
+// prefix moved to its new offset (element size 4 or 8), the ranges' {src, dst,
+// n} triples in pinned host memory, one range per workgroup-stride.
+constexpr int kColThreads = 256;
+
+__global__ __launch_bounds__(kColThreads) void k_scatter_f64(const unsigned long long* __restrict__ src, int64_t k,
+                                                             double* __restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * kColThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kColThreads + threadIdx.x; i < k; i += stride) {
+    const unsigned long long v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long pos = (long long)__hip_atomic_load(src + k + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    dst[pos] = __longlong_as_double((long long)v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kColThreads) void k_move_ranges(const long long* __restrict__ ranges, int32_t n_ranges,
+                                                             const T* __restrict__ src, T* __restrict__ dst) {
+  for (int r = blockIdx.x; r < n_ranges; r += gridDim.x) {
+    const long long so = __hip_atomic_load(ranges + 3 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long d0 = __hip_atomic_load(ranges + 3 * r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long n = __hip_atomic_load(ranges + 3 * r + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (long long i = threadIdx.x; i < n; i += kColThreads) dst[d0 + i] = src[so + i];
+  }
+}
+
 // a device fit that ran before the upload (tpe_level_run's early fit) wrote its
 // problem fields into the patch rows: copied into the problem rows here (the
 // fields k_fit_wide writes), after the upload and k_expand
@@ -5970,6 +6000,31 @@ __attribute__((visibility("hidden"))) int rccl_allgather_inplace(const tpe_excha
   if (ne != ncclSuccess) return rccl_fail("ncclAllGather", ne);
   g_collectives.fetch_add(1, std::memory_order_relaxed);
   return TPE_OK;
+}
+
+int tpe_scatter_f64(const void* src, int64_t k, double* dst, void* stream) {
+  if (k < 0 || (k > 0 && (!src || !dst))) return fail(TPE_E_ARG, "tpe_scatter_f64: bad arguments");
+  if (k == 0) return TPE_OK;
+  const unsigned int grid = (unsigned int)std::min<int64_t>((k + kColThreads - 1) / kColThreads, 1024);
+  TPE_LAUNCH(k_scatter_f64, dim3(grid), dim3(kColThreads), 0, (hipStream_t)stream,
+             (const unsigned long long*)src, k, dst);
+  return hip_check("k_scatter_f64");
+}
+
+int tpe_move_ranges(const void* ranges, int32_t n_ranges, int32_t elem_bytes, const void* src, void* dst,
+                    void* stream) {
+  if (n_ranges < 0 || (elem_bytes != 4 && elem_bytes != 8) || (n_ranges > 0 && (!ranges || !src || !dst)) ||
+      src == dst)
+    return fail(TPE_E_ARG, "tpe_move_ranges: bad arguments");
+  if (n_ranges == 0) return TPE_OK;
+  const unsigned int grid = (unsigned int)std::min<int32_t>(n_ranges, 2048);
+  if (elem_bytes == 8)
+    TPE_LAUNCH(k_move_ranges<unsigned long long>, dim3(grid), dim3(kColThreads), 0, (hipStream_t)stream,
+               (const long long*)ranges, n_ranges, (const unsigned long long*)src, (unsigned long long*)dst);
+  else
+    TPE_LAUNCH(k_move_ranges<uint32_t>, dim3(grid), dim3(kColThreads), 0, (hipStream_t)stream,
+               (const long long*)ranges, n_ranges, (const uint32_t*)src, (uint32_t*)dst);
+  return hip_check("k_move_ranges");
 }
 
 int tpe_collectives_issued(int64_t* n) {

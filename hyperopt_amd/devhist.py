@@ -31,6 +31,62 @@ except ImportError:  # pragma: no cover - torch is part of the image
     torch = None
 
 
+def _stream(device):
+    """The device's current stream as a raw hipStream_t (the engine's stream:
+    engine.Engine._stream)."""
+    raw = getattr(torch._C, '_cuda_getCurrentRawStream', None)
+    return raw(device.index or 0) if raw is not None else torch.cuda.current_stream(device).cuda_stream
+
+
+class _Staging(object):
+    """Pinned host memory the column kernels read in place (tpe_scatter_f64,
+    tpe_move_ranges: system-scope loads through its device address), reused
+    once the stream has passed the last launch that read it (its event)."""
+
+    def __init__(self):
+        self.pin = self.dev = self.ev = None
+
+    def get(self, n_words):
+        """(int64 host view of >= n_words words, its device address)."""
+        if self.pin is None or self.pin.numel() < n_words:
+            if self.ev is not None:
+                self.ev.synchronize()               # (the old buffer goes back to torch's pinned pool)
+            self.pin = torch.empty(max(int(n_words), 8192), dtype=torch.int64, pin_memory=True)
+            import ctypes
+            dp = ctypes.c_void_p()
+            lib = N.load()
+            N.check(lib.tpe_pinned_device_address(self.pin.data_ptr(), ctypes.byref(dp)), lib,
+                    'tpe_pinned_device_address')
+            if not dp.value:
+                raise N.NativeUnavailable('pinned staging is not device-addressable')
+            self.dev, self.ev = dp.value, None
+        elif self.ev is not None:
+            self.ev.synchronize()                   # (the last kernel reading it has run)
+        return self.pin.numpy(), self.dev
+
+    def used(self):
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+
+def _move(device, staging, src, dst, src_off, dst_off, n, elem_bytes):
+    """dst[dst_off[i] + j] = src[src_off[i] + j], j < n[i], on the device
+    (tpe_move_ranges; src / dst distinct device tensors)."""
+    keep = n > 0
+    src_off, dst_off, n = src_off[keep], dst_off[keep], n[keep]
+    if not len(n):
+        return
+    if device.type != 'cuda':                      # (CPU tensors: the tests of the bookkeeping)
+        dst[torch.from_numpy(_positions(dst_off, n))] = src[torch.from_numpy(_positions(src_off, n))]
+        return
+    h, dev = staging.get(3 * len(n))
+    h[0:3 * len(n):3], h[1:3 * len(n):3], h[2:3 * len(n):3] = src_off, dst_off, n
+    lib = N.load()
+    N.check(lib.tpe_move_ranges(dev, len(n), elem_bytes, src.data_ptr(), dst.data_ptr(), _stream(device)), lib,
+            'tpe_move_ranges')
+    staging.used()
+
+
 def _room(n):
     """Segment capacity for n entries (room to append)."""
     return int(n + max(1024, n // 8))
@@ -89,13 +145,10 @@ class _Orders(object):
         keys = torch.empty(2 * max(tc, 1), dtype=torch.float64, device=self.device)
         idx = torch.empty(2 * max(tc, 1), dtype=torch.int32, device=self.device)
         if self.keys is not None and int(self.n.sum()):
-            # every slot's current order into its new place (one gather each)
-            src = _positions(self.cur * self.tc + self.off, self.n)
-            dst = _positions(self.cur * tc + off, self.n)
-            si = torch.from_numpy(src).to(self.device)
-            di = torch.from_numpy(dst).to(self.device)
-            keys[di] = self.keys[si]
-            idx[di] = self.idx[si]
+            # every slot's current order into its new place (one range each)
+            so, do = self.cur * self.tc + self.off, self.cur * tc + off
+            _move(self.device, self.owner._staging, self.keys, keys, so, do, self.n, 8)
+            _move(self.device, self.owner._staging, self.idx, idx, so, do, self.n, 4)
         self.keys, self.idx, self.tc, self.off, self.cap = keys, idx, tc, off, cap
         self.kbase, self.ibase = keys.data_ptr(), idx.data_ptr()
         self.owner.version += 1
@@ -194,7 +247,7 @@ class DeviceColumns(object):
         self.n = np.zeros(0, dtype=np.int64)        # values uploaded per slot
         self.orders = _Orders(device, self)
         self._last_labels, self._last_slots = None, None
-        self._pin = self._dbuf = self._ev = None      # (_scatter's staging)
+        self._staging = _Staging()                    # (_scatter's and the re-layouts' pinned ranges)
 
     def _add(self, label):
         s = self.slot[label] = len(self.views)
@@ -214,9 +267,7 @@ class DeviceColumns(object):
         off = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.int64)
         store = torch.empty(max(int(cap.sum()), 1), dtype=torch.float64, device=self.device)
         if self.store is not None and int(self.n.sum()):
-            si = torch.from_numpy(_positions(self.off, self.n)).to(self.device)
-            di = torch.from_numpy(_positions(off, self.n)).to(self.device)
-            store[di] = self.store[si]
+            _move(self.device, self._staging, self.store, store, self.off, off, self.n, 8)
         self.store, self.off, self.cap = store, off, cap
         self.base = store.data_ptr()
         self.views = [store[o:o + c] for o, c in zip(off.tolist(), cap.tolist())]
@@ -284,28 +335,19 @@ class DeviceColumns(object):
         return self.upload(labels, (), dense=(matrix, rows, n))
 
     def _scatter(self, pos, vals):
-        """store[pos] = vals: on a GPU both go up in ONE asynchronous copy from
-        a pinned staging buffer (positions as exact float64), whose reuse waits
-        for the previous copy's event."""
+        """store[pos] = vals: on a GPU one kernel (tpe_scatter_f64) reads the
+        values and positions from a pinned staging buffer in place — no copy,
+        no framework op; the buffer's reuse waits for that launch's event."""
         k = len(vals)
-        if self.device.type != 'cuda':
+        if self.device.type != 'cuda':             # (CPU tensors: the tests of the bookkeeping)
             self.store[torch.from_numpy(pos)] = torch.from_numpy(vals)
             return
-        if self._pin is None or self._pin.numel() < 2 * k:
-            cap = max(2 * k, 8192)
-            self._pin = torch.empty(cap, dtype=torch.float64, pin_memory=True)
-            self._dbuf = torch.empty(cap, dtype=torch.float64, device=self.device)
-            self._ev = None
-        if self._ev is not None:
-            self._ev.synchronize()                 # (the last copy out of the staging buffer has run)
-        h = self._pin.numpy()
-        h[:k] = vals
+        h, dev = self._staging.get(2 * k)
+        h[:k].view(np.float64)[:] = vals
         h[k:2 * k] = pos
-        d = self._dbuf[:2 * k]
-        d.copy_(self._pin[:2 * k], non_blocking=True)
-        self._ev = torch.cuda.Event()
-        self._ev.record()
-        self.store[d[k:].long()] = d[:k]
+        lib = N.load()
+        N.check(lib.tpe_scatter_f64(dev, k, self.base, _stream(self.device)), lib, 'tpe_scatter_f64')
+        self._staging.used()
 
     def columns(self, items):
         """Device tensors (store segments) whose first ``len(values)`` entries

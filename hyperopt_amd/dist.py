@@ -52,6 +52,33 @@ def label_owners(table, world):
     return owner
 
 
+def grid_shape(n_labels, n_ids, world):
+    """(G, B) of the 2-D shard of a batched suggest's (label x new id) problem
+    grid over ``world`` ranks: G label groups (dist.label_owners over G) times
+    B id blocks (shard_range over B), G * B = world.  Chosen so the largest
+    rank share of problems, ceil(n_labels / G) * ceil(n_ids / B), is smallest
+    (every rank the same count where the grid divides evenly); among equal
+    shares the most label groups — a label's fit, component rows and table are
+    made on each of the B ranks of its group, so fewer id blocks repeat less.
+    ``n_labels``: the labels that shard (the non-gates)."""
+    best = None
+    for g in range(1, world + 1):
+        if world % g or (g > max(1, n_labels)):
+            continue
+        b = world // g
+        share = -(-max(n_labels, 1) // g) * -(-max(n_ids, 1) // b)
+        key = (share, -g)
+        if best is None or key < best[0]:
+            best = (key, g, b)
+    return best[1], best[2]
+
+
+def grid_cell(rank, shape):
+    """(label group, id block) of ``rank`` in a (G, B) grid: the B ranks of a
+    label group are consecutive."""
+    return rank // shape[1], rank % shape[1]
+
+
 def combine_results(stacked):
     """[world, P] RESULT_DTYPE -> [P]: the global winner of every problem."""
     stacked = np.asarray(stacked)
@@ -238,6 +265,43 @@ def gather_id_blocks(ex, values, active, n_ids, n_labels, failed=False):
         k = (hi - lo) * n_labels
         out_v[lo:hi] = allb[r, :8 * per].view(np.float64)[:k].reshape(hi - lo, n_labels)
         out_a[lo:hi] = allb[r, 8 * per:8 * per + k].view(bool).reshape(hi - lo, n_labels)
+    return out_v, out_a
+
+
+def gather_grid_blocks(ex, shape, values, active, n_ids, owner, failed=False):
+    """2-D axis: rank r = (g, b) computed the ids of block b (shard_range over
+    B) for the labels of group g (``owner[ix] == g``; the gates, owner -1, on
+    every rank) — ``values`` float64 / ``active`` bool [block x n_labels] —
+    and every rank gets the whole [n_ids x n_labels] pair: one all-gather of
+    every rank's block (padded to the largest), each label's column from its
+    group's rank of that block, the activity from the block's group-0 rank
+    (every rank of a block evaluated the same gates)."""
+    G, B = shape
+    world = ex.world
+    L = len(owner)
+    blocks = [shard_range(n_ids, b, B) for b in range(B)]
+    m = max(hi - lo for lo, hi in blocks)
+    per = m * L
+    pay = np.zeros(per * 9, dtype=np.uint8)
+    if not failed:
+        g, b = grid_cell(ex.rank, shape)
+        lo, hi = blocks[b]
+        k = (hi - lo) * L
+        pay[:8 * per].view(np.float64)[:k] = np.asarray(values, dtype=np.float64).reshape(-1)
+        pay[8 * per:8 * per + k] = np.asarray(active, dtype=bool).reshape(-1)
+    allb = _exchange_status(ex, pay, failed)
+    out_v = np.empty((n_ids, L))
+    out_a = np.empty((n_ids, L), dtype=bool)
+    own = np.asarray(owner)
+    cols = [np.flatnonzero((own == g) | ((own < 0) & (g == 0))) for g in range(G)]
+    for r in range(world):
+        g, b = grid_cell(r, shape)
+        lo, hi = blocks[b]
+        k = (hi - lo) * L
+        v = allb[r, :8 * per].view(np.float64)[:k].reshape(hi - lo, L)
+        out_v[lo:hi, cols[g]] = v[:, cols[g]]
+        if g == 0:
+            out_a[lo:hi] = allb[r, 8 * per:8 * per + k].view(bool).reshape(hi - lo, L)
     return out_v, out_a
 
 

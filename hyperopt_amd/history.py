@@ -119,7 +119,19 @@ class History(object):
         self.tree_memo = None          # tpe._tree_labels of this (immutable) view without a Trials cache
 
     def smallest(self, m):
-        return _smallest_plain(self.losses, m) if self._cache is None else self._cache.smallest(m)
+        if self._cache is not None:
+            return self._cache.smallest(m)
+        return self._top_state().smallest(self.losses, m)
+
+    def _top_state(self):
+        """The incremental loss ranking of this History's append-only source
+        (_TopState), kept in ``dev`` — the dict Histories over one append-only
+        source share (a columnar FMinIter loop makes a History per suggest over
+        growing views of the same buffers, bench.py config 5 --appending)."""
+        st = self.dev.get('_top')
+        if st is None:
+            st = self.dev['_top'] = _TopState()
+        return st
 
     def native_columns(self, label, log=False):
         """(tids, coordinate, value order) host addresses of a label's columns
@@ -611,6 +623,54 @@ def _smallest_plain(losses, m, stride=64):
     return cand[np.argsort(lc, kind='stable')[:m]]
 
 
+class _TopState(object):
+    """The m smallest losses of an append-only loss buffer, ordered by (loss,
+    position), kept across suggests: one appended loss (FMinIter: a suggest
+    follows every evaluation) is merged in by one bisection instead of a pass
+    over all N (the reference's argsort over every loss, tpe.py:625-629 — the
+    same positions).  Rebuilt when the buffer (its data address) changes, when
+    it is shorter than before, or when more than 8 losses were appended; a
+    History is an immutable view of its source (its value orders and tree
+    records are memoised on it too), so the prefix seen so far is not re-read.
+    ``below``: the split_below result for (n, n_below) of the current ranking."""
+    __slots__ = ('addr', 'n', 'pos', 'keys', 'below')
+    TOP = 64
+
+    def __init__(self):
+        self.addr, self.n, self.pos, self.keys, self.below = None, 0, None, None, None
+
+    def smallest(self, L, m):
+        n = len(L)
+        if m > self.TOP:
+            return _smallest_plain(L, m)
+        addr = L.__array_interface__['data'][0] if n else None
+        if self.addr is None or self.addr != addr or n < self.n or n - self.n > 8:
+            top = _smallest_plain(L, self.TOP)
+            if top is None:
+                top = np.argsort(L, kind='stable')[:self.TOP]
+            self.pos, self.keys, self.n, self.below = top.tolist(), L[top].tolist(), n, None
+            # (a NaN ranks last, as in np.argsort: kept out of the incremental order)
+            self.addr = addr if all(k == k for k in self.keys) else None
+            return self.pos[:m]
+        if n > self.n:
+            keys, pos = self.keys, self.pos
+            for p in range(self.n, n):
+                v = float(L[p])
+                if v != v:
+                    self.addr = None              # (rebuilt next time)
+                    return _smallest_plain(L, m) if n >= 2 * 64 * m else np.argsort(L, kind='stable')[:m]
+                if len(pos) == self.TOP and v >= keys[-1]:
+                    continue
+                j = bisect.bisect_right(keys, v)  # (a new position follows every kept one)
+                keys.insert(j, v)
+                pos.insert(j, p)
+                if len(pos) > self.TOP:
+                    keys.pop()
+                    pos.pop()
+            self.n, self.below = n, None
+        return self.pos[:m]
+
+
 class BelowTids(np.ndarray):
     """Below-set tids in the reference's order with their ascending copy
     (``sorted_view``) made once — the native tree call takes them sorted."""
@@ -647,6 +707,10 @@ def split_below(history, gamma, gamma_cap=25):
         if memo is not None and memo[0] == c.top_n and memo[1] == n_below and c.top is not None and n == c.top_n:
             return memo[2]
     top = history.smallest(n_below + 1)
+    st = history.dev.get('_top') if c is None else None
+    if st is not None and st.below is not None and st.below[0] == (n, n_below) and st.addr is not None \
+            and st.below[1] is history.tids:
+        return st.below[2]
     if top is not None and len(top) == n_below + 1:
         keys = c.top_keys if c is not None and c.top is True else None
         if (keys[n_below - 1] != keys[n_below]) if keys is not None else \
@@ -656,6 +720,8 @@ def split_below(history, gamma, gamma_cap=25):
             b = BelowTids.of(history.tids[np.asarray(top[:n_below], dtype=np.int64)])
             if c is not None and c.top is not None:
                 c.below_memo = (c.top_n, n_below, b)
+            elif st is not None and st.addr is not None:
+                st.below = ((n, n_below), history.tids, b)
             return b
     part = np.argpartition(losses, n_below - 1)
     kth = losses[part[n_below - 1]]

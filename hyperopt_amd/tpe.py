@@ -690,9 +690,15 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
         return None
     # (values / active: the engine's result buffers, consumed or copied here)
     # (only labels some id used: a branch switch drops the old branch's; a
-    # batch's rows are not turned into Python lists)
-    act_rows = active.tolist() if len(values) <= 4 else None
-    used = act_rows[0] if len(values) == 1 else np.asarray(active).any(axis=0).tolist()
+    # batch's rows are not turned into Python lists — and a batch whose every
+    # label is active, a flat space, is told by one contiguous pass)
+    av = active.view(np.bool_)
+    if len(values) == 1:
+        used = av[0].tolist()
+    elif av.all():
+        used = [True] * av.shape[1]
+    else:
+        used = np.ascontiguousarray(av.T).any(axis=1).tolist()
     table.native_fit_hint = tuple(ix for ix in host if used[ix]) if host else ()
     if used != getattr(table, '_used_list', None):      # (the active branch seldom changes)
         table._used_list = used
@@ -711,24 +717,49 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
         dv[3].commit_many(dv[1][ok], dv[2][ok])
         table._committed = None if host else (tl[0], table._used_list)
     if columns:
-        return ChoiceColumns(table.labels, values.copy(), np.asarray(active, dtype=bool))
+        return ChoiceColumns(table.labels, values.copy(), av.copy())
+    return _result_dicts(table, values, av)
+
+
+def _result_dicts(table, values, active):
+    """Per-id {label: value or None} dicts in level order from [n x L] values
+    (float64) and activity (bool or int8).  Up to 4 ids (the reference
+    suggests one id per call, tpe.py:812): the reference's value types —
+    np.int64 categories, np.float64 values — made natively (a 1000-dim space
+    is 1000 scalars per suggest); a batch: Python int / float values, built
+    column by column (_choice_dicts)."""
     order = table.level_order()
-    cols = _tree_static(table)[2]
     if len(values) > 4:
-        return _choice_dicts(order, cols, values, active)
-    # (the reference's value types: np.int64 categories, np.float64 values)
-    conv = table.__dict__.get('_value_conv')
-    if conv is None:
-        conv = table._value_conv = [(label, np.int64 if fam == N.FAM_CATEGORICAL else np.float64)
-                                    for label, ix, fam in sorted(cols, key=lambda c: c[1])]
+        return _choice_dicts(order, _tree_static_meta(table), values, active)
+    tm = table.__dict__.get('_typed_meta')
+    if tm is None:
+        cat = {r.label: r.categorical for r in table.rows}
+        tm = table._typed_meta = (tuple(order), np.array([table.by_label[k].index for k in order], dtype=np.int64),
+                                  np.array([cat[k] for k in order], dtype=np.int8))
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    act = np.ascontiguousarray(active)
+    if act.dtype != np.int8 and act.dtype != np.bool_:
+        act = act.astype(np.bool_)
+    if _hostaddr is not None:
+        return _hostaddr.typed_dicts(tm[0], tm[1], tm[2], values, act)
     out = []
-    for act, v in zip(act_rows, values.tolist()):
+    for a, v in zip(act.tolist(), values.tolist()):
         d = dict.fromkeys(order)
-        for ix in (table.native_used if len(values) == 1 else [i for i, a in enumerate(act) if a]):
-            label, f = conv[ix]
-            d[label] = f(v[ix])
+        for label, ix, c in zip(tm[0], tm[1].tolist(), tm[2].tolist()):
+            if a[ix]:
+                d[label] = np.int64(v[ix]) if c else np.float64(v[ix])
         out.append(d)
     return out
+
+
+def _tree_static_meta(table):
+    """(label, index, family) of every label, table order (the families the
+    result dicts type values by)."""
+    meta = table.__dict__.get('_result_meta')
+    if meta is None:
+        meta = table._result_meta = [(r.label, r.index, N.FAM_CATEGORICAL if r.categorical else N.FAM_GAUSS)
+                                     for r in table.rows]
+    return meta
 
 
 def _choice_dicts(order, cols, values, active):
@@ -795,7 +826,8 @@ def suggest(new_ids, domain, trials, seed,
             n_EI_candidates=_default_n_EI_candidates,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
-            sampler='philox', precision='fp32', device=None, shard=None, shard_ids=None, shard_labels=None):
+            sampler='philox', precision='fp32', device=None, shard=None, shard_ids=None, shard_labels=None,
+            shard_grid=None):
     new_ids = list(new_ids)
     if not new_ids:
         return []
@@ -812,7 +844,7 @@ def suggest(new_ids, domain, trials, seed,
     choices = suggest_choices(domain.table, hist, new_ids, seed, prior_weight=prior_weight,
                               n_EI_candidates=n_EI_candidates, gamma=gamma, sampler=sampler,
                               precision=precision, device=device, shard=shard, shard_ids=shard_ids,
-                              shard_labels=shard_labels)
+                              shard_labels=shard_labels, shard_grid=shard_grid)
     logger.info('tpe.suggest took %f seconds', time.time() - t0)
     return rand.docs_from_choices(new_ids, domain, trials, choices)
 
@@ -833,8 +865,7 @@ class ChoiceColumns(object):
         return len(self.values)
 
     def dicts(self, table):
-        cols = [(r.label, r.index, N.FAM_CATEGORICAL if r.categorical else N.FAM_GAUSS) for r in table.rows]
-        return _choice_dicts(table.level_order(), cols, self.values, self.active)
+        return _result_dicts(table, self.values, self.active)
 
     @classmethod
     def from_dicts(cls, table, dicts):
@@ -853,7 +884,7 @@ class ChoiceColumns(object):
 def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weight,
                     n_EI_candidates=_default_n_EI_candidates, gamma=_default_gamma,
                     sampler='philox', precision='fp32', device=None, shard=None, columns=False,
-                    shard_ids=None, shard_labels=None):
+                    shard_ids=None, shard_labels=None, shard_grid=None):
     """The suggest core on a structure-of-arrays history (``history.History``):
     per new id a {label: value or None} dict.  ``suggest`` wraps it with the
     Trials document layout; columnar callers (and bench.py's large configs)
@@ -862,21 +893,25 @@ def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weig
 
     At most one shard axis (rank, world) over the default process group:
     ``shard`` splits every problem's candidates (one exchange per tree level),
-    ``shard_ids`` the new ids (contiguous blocks) and ``shard_labels`` the
-    hyperparameters (dist.label_owners) — those two exchange the chosen values
-    once, after the suggest; every rank returns the whole result, equal to the
-    unsharded suggest's (the candidates are keyed on seed, label, new id and
-    global index)."""
+    ``shard_ids`` the new ids (contiguous blocks), ``shard_labels`` the
+    hyperparameters (dist.label_owners) and ``shard_grid`` both at once — the
+    (label x new id) problem grid cut into label groups x id blocks
+    (dist.grid_shape: every rank the same problem count where the grid
+    divides) — those three exchange the chosen values once, after the
+    suggest; every rank returns the whole result, equal to the unsharded
+    suggest's (the candidates are keyed on seed, label, new id and global
+    index)."""
     if sampler not in ('philox', 'replay'):
         raise ValueError("sampler must be 'philox' or 'replay'")
-    if sum(a is not None for a in (shard, shard_ids, shard_labels)) > 1:
-        raise ValueError('shard, shard_ids and shard_labels are exclusive: one shard axis per suggest')
-    if (shard_ids is not None or shard_labels is not None) and sampler == 'replay':
+    if sum(a is not None for a in (shard, shard_ids, shard_labels, shard_grid)) > 1:
+        raise ValueError('shard, shard_ids, shard_labels and shard_grid are exclusive: one shard axis per suggest')
+    if (shard_ids is not None or shard_labels is not None or shard_grid is not None) and sampler == 'replay':
         raise ValueError("sampler='replay' draws on the host from one RandomState stream; it does not shard")
-    new_ids = list(new_ids)
-    if shard_ids is not None or shard_labels is not None:
+    # (an id array stays one: list() of 4096 numpy ints is ~0.2 ms of objects)
+    new_ids = new_ids.reshape(-1) if isinstance(new_ids, np.ndarray) else list(new_ids)
+    if shard_ids is not None or shard_labels is not None or shard_grid is not None:
         return _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, precision, device,
-                                columns, shard_ids, shard_labels)
+                                columns, shard_ids, shard_labels, shard_grid)
     return _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, sampler, precision,
                           device, shard, columns)
 
@@ -902,10 +937,10 @@ def _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, ga
 
 
 def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, precision, device, columns,
-                     shard_ids, shard_labels):
-    """New-id or hyperparameter axis (dist.py): this rank's part of the
+                     shard_ids, shard_labels, shard_grid=None):
+    """New-id, hyperparameter or 2-D axis (dist.py): this rank's part of the
     suggest as columns, then one all-gather of the chosen values."""
-    rank, world = shard_ids if shard_ids is not None else shard_labels
+    rank, world = next(a for a in (shard_ids, shard_labels, shard_grid) if a is not None)[:2]
     engine = get_engine(device, precision)
     ex = _dist.exchange_for(engine)          # (collective on the first sharded call)
     if ex.world != world or ex.rank != rank:
@@ -913,7 +948,33 @@ def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, 
                          % (rank, world, ex.rank, ex.world))
     n, L = len(new_ids), len(table.rows)
     failed, err = False, None
-    if shard_ids is not None:
+    if shard_grid is not None:
+        gates = set(table.parent_labels)
+        if len(shard_grid) > 2:              # (rank, world, G): the label groups given (tests)
+            if world % shard_grid[2]:
+                raise ValueError('shard_grid: %d label groups do not divide %d ranks' % (shard_grid[2], world))
+            shape = (shard_grid[2], world // shard_grid[2])
+        else:
+            shape = _dist.grid_shape(sum(1 for r in table.rows if r.label not in gates), n, world)
+        g, b = _dist.grid_cell(rank, shape)
+        owner = _dist.label_owners(table, shape[0])
+        remote = tuple(ix for ix, o in enumerate(owner) if o >= 0 and o != g)
+        lo, hi = _dist.shard_range(n, b, shape[1])
+        vals, act = np.zeros((0, L)), np.zeros((0, L), dtype=bool)
+        try:
+            if hi > lo:
+                cc = _suggest_local(table, hist, new_ids[lo:hi], seed, prior_weight, n_EI_candidates, gamma,
+                                    'philox', precision, device, None, True, remote)
+                vals, act = cc.values, np.asarray(cc.active, dtype=bool)
+        except Exception as e:               # (still takes part in the gather: no rank waits forever)
+            failed, err = True, e
+        try:
+            vals, act = _dist.gather_grid_blocks(ex, shape, vals, act, n, owner, failed)
+        except RuntimeError:
+            if err is not None:
+                raise err
+            raise
+    elif shard_ids is not None:
         lo, hi = _dist.shard_range(n, rank, world)
         vals, act = np.zeros((0, L)), np.zeros((0, L), dtype=bool)
         try:

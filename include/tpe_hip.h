@@ -808,6 +808,22 @@ int tpe_comm_unique_id(void* id);
 int tpe_comm_init(int32_t rank, int32_t world, const void* id, int32_t device, void** comm);
 int tpe_comm_destroy(void* comm);
 
+/* ------------------------------------------------------------------------
+ * Device column store (hyperopt_amd/devhist.py; ABI 22).  The observation
+ * columns of device-fitted labels are segments of one flat float64 store.
+ * tpe_scatter_f64: dst[pos[i]] = val[i] for the k appended observations of a
+ * suggest; `src` is the DEVICE address (tpe_pinned_device_address) of pinned
+ * host memory holding k doubles then k int64 positions, read by the kernel
+ * itself (no copy): the caller keeps it unchanged until the stream has passed
+ * the launch.  tpe_move_ranges: a re-layout of a store (or of the value
+ * orders' key / position buffers, elem_bytes 8 / 4): for each of n_ranges
+ * {src_off, dst_off, n} int64 triples (pinned, device-addressable, as above)
+ * dst[dst_off + i] = src[src_off + i], i < n; src and dst distinct buffers.
+ * ---------------------------------------------------------------------- */
+int tpe_scatter_f64(const void* src, int64_t k, double* dst, void* stream);
+int tpe_move_ranges(const void* ranges, int32_t n_ranges, int32_t elem_bytes, const void* src, void* dst,
+                    void* stream);
+
 /* collectives (ncclAllGather calls) this library has issued in this process,
  * in *n: the device combine of candidate-sharded levels and
  * tpe_exchange_allgather over RCCL.  A one-rank exchange (world 1, `always`)

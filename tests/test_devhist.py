@@ -7,10 +7,15 @@ from hyperopt_amd import devhist
 
 
 def test_columns_append_grow_and_restart():
+    columns_case(torch.device('cpu'))
+
+
+def columns_case(device):
     """Labels appended to in one batch keep every uploaded value across
     re-layouts; a shorter column (another History's) starts its label over;
-    the segment addresses are the views' addresses."""
-    dc = devhist.DeviceColumns(torch.device('cpu'))
+    the segment addresses are the views' addresses.  (tests/test_gpu_devhist.py
+    runs it on the device: the scatter and re-layout kernels.)"""
+    dc = devhist.DeviceColumns(device)
     rs = np.random.RandomState(0)
     full = {('l%d' % i): rs.uniform(size=6000) for i in range(5)}
     n = {k: 0 for k in full}
@@ -20,24 +25,28 @@ def test_columns_append_grow_and_restart():
             n[k] = min(len(full[k]), n[k] + int(rs.randint(1, 400)))
         views = dc.columns([(k, full[k][:n[k]]) for k in labels])
         for k, v in zip(labels, views):
-            np.testing.assert_array_equal(v[:n[k]].numpy(), full[k][:n[k]])
+            np.testing.assert_array_equal(v[:n[k]].cpu().numpy(), full[k][:n[k]])
             assert dc.count(k) == n[k]
         if labels:
             assert dc.addresses([dc.slot[k] for k in labels]).tolist() == [v.data_ptr() for v in views]
         for k in full:                      # untouched labels survive re-layouts
             if k in dc.slot:
-                np.testing.assert_array_equal(dc.view(k)[:dc.count(k)].numpy(), full[k][:dc.count(k)])
+                np.testing.assert_array_equal(dc.view(k)[:dc.count(k)].cpu().numpy(), full[k][:dc.count(k)])
     short = rs.uniform(size=10)
     v = dc.column('l0', short)
-    np.testing.assert_array_equal(v[:10].numpy(), short)
+    np.testing.assert_array_equal(v[:10].cpu().numpy(), short)
     assert dc.order('l0').n == 0
 
 
 def test_orders_ensure_keeps_current_side():
+    orders_case(torch.device('cpu'))
+
+
+def orders_case(device):
     """Value orders: ptrs of a longer run point at the other side, commit
     flips it, and making room for one label moves every label's current order
     with its contents (what a level run reads next)."""
-    dc = devhist.DeviceColumns(torch.device('cpu'))
+    dc = devhist.DeviceColumns(device)
     dc.columns([('a', np.zeros(100)), ('b', np.zeros(50))])
     g = dc.orders
     sa, sb = dc.order('a').slot, dc.order('b').slot

@@ -157,6 +157,20 @@ def _axes_worker(rank, world, port, q):
         mine = np.where([o in (-1, rank) for o in owner], full, np.nan)
         got = D.gather_label_columns(ex, mine, owner)
         out['labels'] = bool(np.array_equal(got, full))
+        # 2-D axis: 9 ids x 8 labels (one gate) over (G, B) = grid_shape, and a
+        # forced (G, B) = (world, 1) and (1, world): each rank its labels of its ids
+        n2, own1 = 9, [-1] + list(range(7))
+        full2 = np.random.RandomState(6).uniform(size=(n2, 8))
+        act2 = np.random.RandomState(7).uniform(size=(n2, 8)) > 0.3
+        ok = []
+        for shape in (D.grid_shape(7, n2, world), (world, 1), (1, world)):
+            g, b = D.grid_cell(rank, shape)
+            owner = [o if o < 0 else o % shape[0] for o in own1]
+            lo2, hi2 = D.shard_range(n2, b, shape[1])
+            mine = np.where([o in (-1, g) for o in owner], full2[lo2:hi2], np.nan)
+            v, a = D.gather_grid_blocks(ex, shape, mine, act2[lo2:hi2], n2, owner)
+            ok.append(bool(np.array_equal(v, full2) and np.array_equal(a, act2)))
+        out['grid'] = ok
         # a failed rank: every rank raises, none waits
         try:
             D.gather_id_blocks(ex, full_v[lo:hi], full_a[lo:hi], n, L, failed=(rank == world - 1))
@@ -170,7 +184,7 @@ def _axes_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('world', [2, 3, 4])
 def test_gloo_id_and_label_axis_gathers(world):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
@@ -186,6 +200,7 @@ def test_gloo_id_and_label_axis_gathers(world):
         assert err is None, (rank, err)
         assert got['ids'] == (True, True), (rank, got)
         assert got['labels'], rank
+        assert got['grid'] == [True, True, True], (rank, got['grid'])
         assert 'failed on rank(s) [%d]' % (world - 1) in got['failure'], (rank, got['failure'])
 
 
@@ -203,3 +218,23 @@ def test_label_owners_round_robin_non_gates():
         assert [o == -1 for o in own] == [r.label in gates for r in T.rows]
         ng = [o for o in own if o >= 0]
         assert ng == [k % world for k in range(len(ng))]
+
+
+def test_grid_shape_balances_problems():
+    """2-D shard shape: the smallest largest per-rank problem share, the most
+    label groups among equal shares (config 4 at 8 ranks: 4 groups of 5
+    labels x 2 blocks of 2048 ids — 10240 problems a rank, where the label
+    axis alone gives 3 labels x 4096 ids = 12288 to the fullest rank)."""
+    from hyperopt_amd.dist import grid_shape
+    assert grid_shape(20, 4096, 8) == (4, 2)
+    assert grid_shape(20, 4096, 4) == (4, 1)
+    assert grid_shape(20, 4096, 2) == (2, 1)
+    assert grid_shape(20, 4096, 1) == (1, 1)
+    assert grid_shape(1000, 1, 8) == (8, 1)
+    assert grid_shape(3, 4096, 8) == (1, 8)
+    assert grid_shape(6, 512, 4) == (2, 2)
+    for L, n, w in ((20, 4096, 8), (7, 100, 6), (1000, 2, 4), (5, 5, 8)):
+        G, B = grid_shape(L, n, w)
+        assert G * B == w and G <= max(L, 1)
+        share = -(-L // G) * -(-n // B)
+        assert all(share <= -(-L // g) * -(-n // (w // g)) for g in range(1, w + 1) if w % g == 0 and g <= L)

@@ -348,3 +348,72 @@ def test_two_process_id_and_label_axes_match_unsharded():
             assert np.array_equal(a[0], b[0], equal_nan=True) and np.array_equal(a[1], b[1]), name
         else:
             assert a == b, name
+
+
+# ------------------------------------------------------------------ 2-D axis
+def _grid_cases(rank, world):
+    """(name, (values, active)) of the 2-D shard cases; rank None: unsharded."""
+    from hyperopt_amd import tpe
+    out = []
+    t4, h4 = _cfg4()
+    ids = np.arange(10000, 10000 + 4096)
+    for name, G, seed in (('config4 2x2', 2, 71), ('config4 auto', None, 72)):
+        sg = None if rank is None else ((rank, world) if G is None else (rank, world, G))
+        cc = tpe.suggest_choices(t4, h4, ids, seed, n_EI_candidates=4096, columns=True, shard_grid=sg)
+        out.append((name, (cc.values, cc.active)))
+    # a small batch whose grid divides unevenly: 6 labels x 77 ids
+    t6, h6 = bench_flat(6)
+    sg = None if rank is None else (rank, world, 2)
+    cc = tpe.suggest_choices(t6, h6, np.arange(5000, 5077), 73, n_EI_candidates=2048, columns=True, shard_grid=sg)
+    out.append(('6 labels x 77 ids 2x2', (cc.values, cc.active)))
+    return out
+
+
+def bench_flat(L):
+    import bench
+    labels = ['y%d' % i for i in range(L)]
+    hist = bench.soa_history(labels, 5000, 17, lambda v: sum((x - 1.0) ** 2 for x in v.values()))
+    return bench.flat_uniform_table(labels), hist
+
+
+def _grid_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        q.put((rank, _grid_cases(rank, world), None))
+    except Exception:
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_four_process_grid_axis_matches_unsharded():
+    """Four processes (gloo, all on the one GPU): the 2-D shard of a batched
+    suggest's (label x new id) grid — config 4 (20 labels x 4096 ids x 4096
+    candidates) as 2 label groups x 2 id blocks and as grid_shape's choice,
+    and 6 labels x 77 ids (uneven blocks) — returns on every rank exactly the
+    unsharded suggest (values and activity bit for bit)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        rank, out, err = q.get(timeout=280)
+        assert err is None, (rank, err)
+        got[rank] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _grid_cases(None, None)
+    for rank in range(world):
+        for (name, want), (name2, have) in zip(ref, got[rank]):
+            assert name == name2
+            assert np.array_equal(want[0], have[0], equal_nan=True), (rank, name)
+            assert np.array_equal(want[1], have[1]), (rank, name)

@@ -543,3 +543,40 @@ def test_plain_history_below_split_from_sampled_bound():
         if nb < n and Ls[nb - 1] != Ls[nb]:                     # (a boundary tie: the reference's argsort order decides)
             assert set(np.asarray(b).tolist()) == set(ref.tolist())
     assert checked > 150
+
+
+def test_plain_history_ranking_kept_across_appends():
+    """Columnar Histories over one append-only loss buffer (a History per
+    suggest over growing views, sharing ``dev``: bench.py config 5
+    --appending) keep their loss ranking incrementally (history._TopState):
+    after every append of 1-3 losses (ties, +inf, an occasional NaN and a
+    jump of 50 that rebuilds) the m smallest are a stable argsort's, and
+    split_below gives the reference's below set; a History reused as it is
+    returns the same below set object."""
+    from hyperopt_amd import history as H
+    rs = np.random.RandomState(11)
+    cap = 30000
+    L = np.round(rs.uniform(size=cap) * 20000) / 7.0          # (ties, the boundary mostly untied)
+    L[rs.choice(cap, 30)] = np.inf
+    tids = np.arange(cap, dtype=np.int64) * 2
+    dev = {}
+    n = 12000
+    checked = 0
+    for step in range(300):
+        n += 50 if step % 97 == 0 else int(rs.randint(1, 4))
+        if step == 150:
+            L[n - 1] = np.nan
+        hist = H.History(tids[:n], L[:n], {}, dev=dev)
+        m = int(rs.randint(1, 27))
+        got = hist.smallest(m)
+        ref = np.argsort(L[:n], kind='stable')[:m]
+        np.testing.assert_array_equal(np.asarray(got), ref)
+        b = H.split_below(hist, 0.25)
+        nb = min(int(np.ceil(0.25 * np.sqrt(n))), 25)
+        Ls = np.sort(np.where(np.isnan(L[:n]), np.inf, L[:n]))
+        if Ls[nb - 1] != Ls[nb]:
+            assert set(np.asarray(b).tolist()) == set(tids[np.argsort(L[:n], kind='stable')[:nb]].tolist())
+            checked += 1
+        assert H.split_below(hist, 0.25) is b or Ls[nb - 1] == Ls[nb]
+    assert checked > 100
+    assert isinstance(dev['_top'], H._TopState)
