@@ -955,7 +955,8 @@ def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, 
                 raise ValueError('shard_grid: %d label groups do not divide %d ranks' % (shard_grid[2], world))
             shape = (shard_grid[2], world // shard_grid[2])
         else:
-            shape = _dist.grid_shape(sum(1 for r in table.rows if r.label not in gates), n, world)
+            shape = _dist.grid_shape(sum(1 for r in table.rows if r.label not in gates), n, world,
+                                     _dist.label_cost(len(hist), n_EI_candidates))
         g, b = _dist.grid_cell(rank, shape)
         owner = _dist.label_owners(table, shape[0])
         remote = tuple(ix for ix, o in enumerate(owner) if o >= 0 and o != g)

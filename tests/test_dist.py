@@ -225,7 +225,12 @@ def test_grid_shape_balances_problems():
     label groups among equal shares (config 4 at 8 ranks: 4 groups of 5
     labels x 2 blocks of 2048 ids — 10240 problems a rank, where the label
     axis alone gives 3 labels x 4096 ids = 12288 to the fullest rank)."""
-    from hyperopt_amd.dist import grid_shape
+    from hyperopt_amd.dist import grid_shape, label_cost
+    # a label's own part (fits, rows, table) repeated by each id block of its
+    # group: config 4's (10^4 observations, 4096 candidates) keeps whole labels
+    assert grid_shape(20, 4096, 8, label_cost(10000, 4096)) == (8, 1)
+    assert grid_shape(3, 4096, 8, label_cost(10000, 4096)) == (2, 4)
+    assert grid_shape(20, 4096, 8, label_cost(100, 2 ** 20)) == (4, 2)
     assert grid_shape(20, 4096, 8) == (4, 2)
     assert grid_shape(20, 4096, 4) == (4, 1)
     assert grid_shape(20, 4096, 2) == (2, 1)

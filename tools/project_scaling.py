@@ -19,6 +19,12 @@ any 8-GPU run).  Model, per config, from the bench line's host phases
   config 4 (hyperparameter axis, strong: the 20 labels over the ranks; the
       default --axis4 labels): F the Python around the native call, V the
       native call times ceil(20 / N) / 20, X(N) as above.
+  config 4 (2-D axis, strong, the default --axis4 grid: G label groups x B id
+      blocks, dist.grid_shape): T(N) = F + Fl * ceil(20 / G) / 20 + Vp * share
+      + X(N); F the Python around the native call, Fl the per-label native
+      work (prefit + pack + k_tables: made by each of a group's B ranks), Vp
+      the rest of the native call (the sample pass, records and results of
+      the problems), share = ceil(20 / G) * ceil(4096 / B) / (20 * 4096).
   config 5 (hyperparameter axis, strong: 1000 labels over the ranks)
       T(N) = F + V / N + X(N)
       F: the Python around the native call (history view, below split over
@@ -71,6 +77,20 @@ def main():
         x = 0 if n == 1 else a.hop_us * (n - 1) + nbytes4 * (n - 1) / n / (a.bw_gbs * 1e3)
         t = F4l + V4l * (-(-20 // n)) / 20 + x
         rows.append(('4 labels', n, t, T4 / (n * t)))
+    # the 2-D grid: the label part made by every rank of a group, the problem
+    # part divided by the whole grid
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+    from hyperopt_amd.dist import grid_shape
+    Fl = h4['pack'] + 1e3 * c4['stage_ms_per_step']['k_tables']
+    Vp = h4['return'] - Fl
+    for n in Ns:
+        G, B = grid_shape(20, 4096, n)
+        share = (-(-20 // G)) * (-(-4096 // B)) / (20.0 * 4096)
+        x = 0 if n == 1 else a.hop_us * (n - 1) + nbytes4 * (n - 1) / n / (a.bw_gbs * 1e3)
+        t = F4l + Fl * (-(-20 // G)) / 20.0 + Vp * share + x
+        rows.append(('4 grid %dx%d' % (G, B), n, t, T4 / (n * t)))
     c5 = last_json(a.cfg5)
     h5 = c5['host_phases_us']
     T5 = c5['p50_step_ms'] * 1e3
@@ -81,11 +101,12 @@ def main():
         x = 0 if n == 1 else a.hop_us * (n - 1) + nbytes5 * (n - 1) / n / (a.bw_gbs * 1e3)
         t = F5 + V5 / n + x
         rows.append(('5 strong', n, t, T5 / (n * t)))
-    print('inputs: cfg3 p50 %.1f us; cfg4 ids F %.0f V %.0f us, labels F %.0f V %.0f us; cfg5 F %.0f V %.0f us; '
-          'x1 %.2f us/level, hop %.1f us, bw %.0f GB/s' % (t1, F4, V4, F4l, V4l, F5, V5, a.x1_us, a.hop_us, a.bw_gbs))
-    print('%-9s %3s %10s %10s' % ('config', 'N', 'T(N) us', 'eff'))
+    print('inputs: cfg3 p50 %.1f us; cfg4 ids F %.0f V %.0f us, labels F %.0f V %.0f us, grid label part %.0f '
+          'problem part %.0f us; cfg5 F %.0f V %.0f us; x1 %.2f us/level, hop %.1f us, bw %.0f GB/s'
+          % (t1, F4, V4, F4l, V4l, Fl, Vp, F5, V5, a.x1_us, a.hop_us, a.bw_gbs))
+    print('%-14s %3s %10s %10s' % ('config', 'N', 'T(N) us', 'eff'))
     for name, n, t, e in rows:
-        print('%-9s %3d %10.1f %10.2f' % (name, n, t, e))
+        print('%-14s %3d %10.1f %10.2f' % (name, n, t, e))
 
 
 if __name__ == '__main__':
