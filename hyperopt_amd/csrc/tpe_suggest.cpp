@@ -550,8 +550,20 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
 
   // level by level (hyperopt_amd.tpe._choices_philox)
   std::vector<int>& chosen = chosen_tl;
-  chosen.assign((size_t)n_ids * n_labels, kInactive);
-  for (size_t q = 0; q < (size_t)n_ids * n_labels; ++q) { values[q] = NAN; active[q] = 0; }
+  chosen.resize((size_t)n_ids * n_labels);
+  // every (id, label) inactive, in id blocks on the pool (a batched suggest's
+  // rows: 4096 x 20 on config 4)
+  struct Init { double* values; int8_t* active; int* chosen; int n_ids, n_labels; };
+  Init ini{values, active, chosen.data(), n_ids, n_labels};
+  auto init_blk = [](void* c, int k) {
+    const Init& q = *(const Init*)c;
+    const size_t a = (size_t)k * kIdBlock * q.n_labels,
+                 e = (size_t)std::min(q.n_ids, (k + 1) * kIdBlock) * q.n_labels;
+    for (size_t t = a; t < e; ++t) { q.values[t] = NAN; q.active[t] = 0; q.chosen[t] = kInactive; }
+  };
+  const int n_blk = (n_ids + kIdBlock - 1) / kIdBlock;
+  if (n_blk > 1) tpe_pool::parallel_for(n_blk, init_blk, &ini);
+  else if (n_blk == 1) init_blk(&ini, 0);
   std::vector<int64_t>& lvl_ids = ids_tl;
   // a member of a level: its label, its problems' first row in the level's
   // results, their count, and where its id positions start in lvl_ids (-1: every
@@ -564,17 +576,35 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     std::vector<Member> members;
     int64_t n_res = 0;
     bool pending = false;                   // labels flagged for the caller's fit: all of the level's at once
+    // the level's labels another rank evaluates: active where the tree says, in
+    // one row-major pass over the ids below (a remote label is never a gate, so
+    // its `chosen` code is never read; a label a time over 4096 ids strided the
+    // rows: 28 us a label on config 4)
+    std::vector<int> remote;
+    for (int i = 0; i < n_labels; ++i)
+      if (labels[i].depth == d && (labels[i].flags & TPE_F_REMOTE)) remote.push_back(i);
+    if (!remote.empty()) {
+      struct Rem { const tpe_tree_label* labels; const int* remote; int nr; int8_t* active; const int* chosen;
+                   int n_ids, n_labels; };
+      Rem rm{labels, remote.data(), (int)remote.size(), active, chosen.data(), n_ids, n_labels};
+      auto rem_blk = [](void* c, int k) {
+        const Rem& q = *(const Rem*)c;
+        const int j1 = std::min(q.n_ids, (k + 1) * kIdBlock);
+        for (int j = k * kIdBlock; j < j1; ++j) {
+          int8_t* row = q.active + (size_t)j * q.n_labels;
+          const int* ch = q.chosen + (size_t)j * q.n_labels;
+          for (int r = 0; r < q.nr; ++r) {
+            const tpe_tree_label& L = q.labels[q.remote[r]];
+            if (L.n_parents == 0 || is_active(L, ch)) row[q.remote[r]] = 1;
+          }
+        }
+      };
+      if (n_blk > 1) tpe_pool::parallel_for(n_blk, rem_blk, &rm);
+      else rem_blk(&rm, 0);
+    }
     for (int i = 0; i < n_labels; ++i) {
       const tpe_tree_label& L = labels[i];
-      if (L.depth != d) continue;
-      if (L.flags & TPE_F_REMOTE) {         // active where the tree says, evaluated by another rank
-        for (int j = 0; j < n_ids; ++j)
-          if (is_active(L, chosen.data() + (size_t)j * n_labels)) {
-            active[(size_t)j * n_labels + i] = 1;
-            chosen[(size_t)j * n_labels + i] = kActive;
-          }
-        continue;
-      }
+      if (L.depth != d || (L.flags & TPE_F_REMOTE)) continue;
       Member m{i, n_res, n_ids, -1};
       if (L.n_parents > 0) {
         m.lvl_first = (int64_t)lvl_ids.size();
@@ -604,27 +634,31 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     }
     const int rc = run((int32_t)members.size());
     if (rc != TPE_OK) return rc;
-    for (int64_t q = 0; q < n_res; ++q) {
-      if (res[(size_t)q].idx < 0) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
-    }
     // the members' results into their columns, ids in blocks (a block's rows
     // are its own: no cache lines shared between workers); a gated member's
     // positions hold its ids ascending, so a block's are one range, found by
-    // bisection
+    // bisection.  A problem without a selected candidate flags its block (the
+    // check rides along with the one pass over the results)
     struct Mem {
       const Member* members; int n_mem; const int64_t* lvl_ids;
       const tpe_result* res; double* values; int8_t* active; int* chosen; const char* gate; int n_ids, n_labels;
+      int8_t* bad;
     };
+    const int nbk = (n_ids + kIdBlock - 1) / kIdBlock;
+    std::vector<int8_t> bad((size_t)std::max(nbk, 1), 0);
     Mem mx{members.data(), (int)members.size(), lvl_ids.data(), res.data(), values, active, chosen.data(),
-           T.gate.data(), n_ids, n_labels};
+           T.gate.data(), n_ids, n_labels, bad.data()};
     auto put = [](void* c, int k) {
       const Mem& x = *(const Mem*)c;
       const int64_t j0 = (int64_t)k * kIdBlock, j1 = std::min<int64_t>(x.n_ids, j0 + kIdBlock);
+      int8_t b = 0;
       for (int mi = 0; mi < x.n_mem; ++mi) {
         const Member& m = x.members[mi];
         const int i = m.label;
         auto set = [&](int64_t q, int64_t j) {
-          const double v = x.res[(size_t)q].value;
+          const tpe_result& r = x.res[(size_t)q];
+          const double v = r.value;
+          b |= r.idx < 0;
           x.values[(size_t)j * x.n_labels + i] = v;
           x.active[(size_t)j * x.n_labels + i] = 1;
           x.chosen[(size_t)j * x.n_labels + i] = x.gate[i] ? (int)(int64_t)v : kActive;
@@ -638,10 +672,12 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
         const int64_t* hi = std::lower_bound(lo, base + m.count, j1);
         for (const int64_t* p = lo; p < hi; ++p) set(m.res_off + (p - base), *p);
       }
+      x.bad[k] = b;
     };
-    const int nb = (n_ids + kIdBlock - 1) / kIdBlock;
-    if (nb > 1) tpe_pool::parallel_for(nb, put, &mx);
+    if (nbk > 1) tpe_pool::parallel_for(nbk, put, &mx);
     else put(&mx, 0);
+    for (int k = 0; k < nbk; ++k)
+      if (bad[(size_t)k]) return tpe_internal_fail(TPE_E_ARG, "no candidate selected for a label");
   }
   return TPE_OK;
 }
