@@ -293,7 +293,9 @@ inline double log2_normal(double x) {
 // finite and positive, and np.maximum / np.minimum reduce to branch-free
 // max / min that vectorise (same values).
 template <bool CLEAN>
-int64_t fit_sorted(const double* __restrict__ sv, const int64_t* __restrict__ rank, int64_t n, double prior_weight,
+__attribute__((always_inline)) inline int64_t fit_sorted(const double* __restrict__ sv,
+                                                        const int64_t* __restrict__ rank, int64_t n,
+                                                        double prior_weight,
                    double prior_mu, double prior_sigma, int32_t lf, double* __restrict__ w, double* __restrict__ mu,
                    double* __restrict__ sigma) {
   auto mx = [](double a, double b) { return CLEAN ? (a > b ? a : b) : np_max(a, b); };
@@ -321,11 +323,16 @@ int64_t fit_sorted(const double* __restrict__ sv, const int64_t* __restrict__ ra
     const int64_t num = n - lf;
     const double start = 1.0 / (double)n;
     const double step = num > 1 ? (1.0 - start) / (double)(num - 1) : 0.0;
+    // (branch-free and vectorisable: a rank r in [0, 2^52) converted exactly
+    // as the double with r in its mantissa less 2^52 — an integer or and a
+    // subtraction, where the clones' AVX-512F has no int64 -> double)
+    const bool last_one = num > 1;
     auto ramp = [&](int64_t r) -> double {
-      double y = (double)r * step;
+      const double rd = __builtin_bit_cast(double, (uint64_t)r | 0x4330000000000000ull) - 4503599627370496.0;
+      double y = rd * step;
       y += start;
-      y = (r == num - 1 && num > 1) ? 1.0 : y;
-      return r >= num ? 1.0 : y;
+      const bool one = (r >= num) | ((r == num - 1) & last_one);
+      return one ? 1.0 : y;
     };
     for (int64_t i = 0; i < pos; ++i) w[i] = ramp(rank[i]);
     w[pos] = prior_weight;
@@ -975,17 +982,24 @@ int tpe_host_fit_split(const double* x, const int64_t* tids, const int64_t* orde
   int bad = 0;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t t = order[i];
+    // (the gather's address depends on order[i] alone: every iteration's loads
+    // can be in flight at once — a clamp through `bad` chained them, one cache
+    // latency an observation)
     bad |= (uint64_t)t >= (uint64_t)n;
-    const int64_t tt = bad ? 0 : t;
+    const int64_t tt = (uint64_t)t < (uint64_t)n ? t : 0;
     const int64_t c = code[tt];
     const double v = x[tt];
-    // branch-free: write both sides' next slot (each has one spare), advance one
-    sb[cb] = v; rb[cb] = ~c;
-    sa[ca] = v; ra[ca] = c;
-    const int64_t above = c >= 0;
-    ca += above; cb += 1 - above;
-    bad |= (ca > na) | (cb > nb);
+    // (the below side is ~25 of them: a predictable branch, half the stores of
+    // writing both sides; a count past its side stays on that side's spare slot)
+    if (__builtin_expect(c >= 0, 1)) {
+      const int64_t wa = ca < na ? ca : na;
+      sa[wa] = v; ra[wa] = c; ++ca;
+    } else {
+      const int64_t wb = cb < nb ? cb : nb;
+      sb[wb] = v; rb[wb] = ~c; ++cb;
+    }
   }
+  bad |= (ca != na) | (cb != nb);
   if (bad) return TPE_E_ARG;                          // not a permutation
   const int64_t cap = n + 1;
   for (int sd = 0; sd < 2; ++sd) {

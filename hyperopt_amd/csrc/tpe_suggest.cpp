@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -44,6 +45,15 @@ void phase_start() {
   if (!g_ph_on.load(std::memory_order_relaxed)) return;
   g_ph_t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < TPE_N_PHASES; ++i) g_ph[i] = -1.0;
+}
+
+// TPE_TREE_TRACE=1 (with the phase clock on): named marks of tpe_suggest_tree's
+// host steps on stderr, us since the call's entry (diagnostic)
+void trace_mark(const char* what) {
+  static const bool on = [] { const char* e = getenv("TPE_TREE_TRACE"); return e && e[0] == '1'; }();
+  if (!on || !g_ph_on.load(std::memory_order_relaxed)) return;
+  fprintf(stderr, "[tree] %-12s %8.1f us\n", what,
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g_ph_t0).count());
 }
 
 // TPE_DEVICE_COMBINE=0: sharded levels exchange through the host (A/B)
@@ -427,6 +437,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       return TPE_E_FALLBACK;
   }
   if (n_labels == 0 || n_ids == 0) return TPE_OK;
+  trace_mark("checks");
   prefit(T);
   tpe_internal_phase(TPE_PHASE_PREFIT);
   const int32_t run_flags = flags & ~TPE_TREE_NO_SPECULATE;
@@ -549,6 +560,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
   }
 
   // level by level (hyperopt_amd.tpe._choices_philox)
+  trace_mark("level-path");
   std::vector<int>& chosen = chosen_tl;
   chosen.resize((size_t)n_ids * n_labels);
   // every (id, label) inactive, in id blocks on the pool (a batched suggest's
@@ -562,8 +574,15 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     for (size_t t = a; t < e; ++t) { q.values[t] = NAN; q.active[t] = 0; q.chosen[t] = kInactive; }
   };
   const int n_blk = (n_ids + kIdBlock - 1) / kIdBlock;
-  if (n_blk > 1) tpe_pool::parallel_for(n_blk, init_blk, &ini);
-  else if (n_blk == 1) init_blk(&ini, 0);
+  // a flat space (one level, every label parentless, no gate): every entry is
+  // written below — a local label's by the results pass, a remote one's by the
+  // remote pass — and no `chosen` code is ever read: nothing to initialise
+  const bool flat = T.max_depth == 0;
+  if (!flat) {
+    if (n_blk > 1) tpe_pool::parallel_for(n_blk, init_blk, &ini);
+    else if (n_blk == 1) init_blk(&ini, 0);
+  }
+  trace_mark("init");
   std::vector<int64_t>& lvl_ids = ids_tl;
   // a member of a level: its label, its problems' first row in the level's
   // results, their count, and where its id positions start in lvl_ids (-1: every
@@ -584,14 +603,19 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     for (int i = 0; i < n_labels; ++i)
       if (labels[i].depth == d && (labels[i].flags & TPE_F_REMOTE)) remote.push_back(i);
     if (!remote.empty()) {
-      struct Rem { const tpe_tree_label* labels; const int* remote; int nr; int8_t* active; const int* chosen;
-                   int n_ids, n_labels; };
-      Rem rm{labels, remote.data(), (int)remote.size(), active, chosen.data(), n_ids, n_labels};
+      struct Rem { const tpe_tree_label* labels; const int* remote; int nr; int8_t* active; double* values;
+                   const int* chosen; int n_ids, n_labels; bool flat; };
+      Rem rm{labels, remote.data(), (int)remote.size(), active, values, chosen.data(), n_ids, n_labels, flat};
       auto rem_blk = [](void* c, int k) {
         const Rem& q = *(const Rem*)c;
         const int j1 = std::min(q.n_ids, (k + 1) * kIdBlock);
         for (int j = k * kIdBlock; j < j1; ++j) {
           int8_t* row = q.active + (size_t)j * q.n_labels;
+          double* vrow = q.values + (size_t)j * q.n_labels;
+          if (q.flat) {                              // (every remote label active, its value another rank's)
+            for (int r = 0; r < q.nr; ++r) { row[q.remote[r]] = 1; vrow[q.remote[r]] = NAN; }
+            continue;
+          }
           const int* ch = q.chosen + (size_t)j * q.n_labels;
           for (int r = 0; r < q.nr; ++r) {
             const tpe_tree_label& L = q.labels[q.remote[r]];
@@ -601,6 +625,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       };
       if (n_blk > 1) tpe_pool::parallel_for(n_blk, rem_blk, &rm);
       else rem_blk(&rm, 0);
+      trace_mark("remote");
     }
     for (int i = 0; i < n_labels; ++i) {
       const tpe_tree_label& L = labels[i];
@@ -622,6 +647,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       n_res += m.count;
     }
     if (pending) return TPE_E_FALLBACK;
+    trace_mark("members");
     if (members.empty()) continue;
     // the gated members' id arrays (positions -> new ids), stable now that lvl_ids is complete
     std::vector<int64_t> lvl_new((size_t)lvl_ids.size());
@@ -661,7 +687,7 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
           b |= r.idx < 0;
           x.values[(size_t)j * x.n_labels + i] = v;
           x.active[(size_t)j * x.n_labels + i] = 1;
-          x.chosen[(size_t)j * x.n_labels + i] = x.gate[i] ? (int)(int64_t)v : kActive;
+          if (x.gate[i]) x.chosen[(size_t)j * x.n_labels + i] = (int)(int64_t)v;   // (read for a gate only)
         };
         if (m.lvl_first < 0) {
           for (int64_t j = j0; j < j1; ++j) set(m.res_off + j, j);

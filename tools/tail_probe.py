@@ -132,6 +132,13 @@ def main():
     census = collections.Counter(type(o).__name__ for o in gc.garbage).most_common(12)
     gc.set_debug(0)
     gc.garbage.clear()
+    # what stays alive per suggest (tracked objects by type, 50 steps)
+    live0 = collections.Counter(type(o).__name__ for o in gc.get_objects())
+    for i in range(50):
+        step(95000 + i)
+    gc.collect()
+    live1 = collections.Counter(type(o).__name__ for o in gc.get_objects())
+    kept = {k: v - live0.get(k, 0) for k, v in live1.items() if v - live0.get(k, 0) != 0}
     gc.enable()
     th = ctypes.c_int32(0)
     eng.lib.tpe_host_threads(-1, ctypes.byref(th))
@@ -155,7 +162,7 @@ def main():
                    nivcsw_total=int(sum(r['nivcsw'] for r in rows)), wait_us_total=float(sum(r['wait_us'] for r in rows)),
                    phase_names=list(N.PHASES), median_phases=[float(x) for x in np.median([r['ph'] for r in rows], 0)],
                    gc_count_growth_per_step=grown / 20.0, cyclic_garbage_per_step=n_garbage / 20.0,
-                   garbage_census_20_steps=census,
+                   garbage_census_20_steps=census, live_objects_kept_50_steps=kept,
                    slowest=slow)
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
     with open(os.path.join(ROOT, 'gpurun_out', 'tail_%s.json' % args.tag), 'w') as f:
