@@ -518,7 +518,7 @@ def _tree_refill(fv, meta, hist):
 
 
 def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard=None, columns=False,
-                    remote=()):
+                    remote=(), borrow=False):
     """``_choices_philox`` in one native call (tpe_suggest_tree), or None when
     the space or history needs the general path.  Labels the native fits cannot
     reproduce (quantized ones, sides with repeated values: numpy's argsort tie
@@ -527,7 +527,8 @@ def _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_wei
     ``shard`` = (rank, world): candidate-sharded over the default process
     group, the level results exchanged inside the native call (dist.py).
     ``remote``: label indices another rank evaluates (TPE_F_REMOTE)."""
-    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns, remote)
+    out = _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns, remote,
+                       borrow)
     if out is None:
         table.native_fit_hint = ()             # the general path takes it: nothing to pre-fit next time
     return out
@@ -583,7 +584,8 @@ def _side_orders(hist, label, otids, x, below_tids):
     return ob, oa
 
 
-def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False, remote=()):
+def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard, columns=False, remote=(),
+                 borrow=False):
     if not hist.sorted_obs:
         return None
     tl = _tree_labels(table, hist, engine, remote)
@@ -717,7 +719,10 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
         dv[3].commit_many(dv[1][ok], dv[2][ok])
         table._committed = None if host else (tl[0], table._used_list)
     if columns:
-        return ChoiceColumns(table.labels, values.copy(), av.copy())
+        # (borrow: views of the engine's result buffers, consumed by the caller
+        # before the engine's next suggest — the sharded paths' gathers)
+        return ChoiceColumns(table.labels, values, av) if borrow else \
+            ChoiceColumns(table.labels, values.copy(), av.copy())
     return _result_dicts(table, values, av)
 
 
@@ -917,13 +922,13 @@ def suggest_choices(table, hist, new_ids, seed, prior_weight=_default_prior_weig
 
 
 def _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, sampler, precision, device,
-                   shard, columns, remote=()):
+                   shard, columns, remote=(), borrow=False):
     engine = get_engine(device, precision)
     below_tids = _history.split_below(hist, gamma)
     C = int(n_EI_candidates)
     if sampler == 'philox' and NATIVE_TREE and precision == 'fp32':
         out = _choices_native(table, hist, below_tids, new_ids, seed, C, engine, prior_weight, shard,
-                              columns, remote)
+                              columns, remote, borrow)
         if out is not None:
             return out
     fits = _Fits(table, hist, below_tids, prior_weight, engine)
@@ -965,7 +970,7 @@ def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, 
         try:
             if hi > lo:
                 cc = _suggest_local(table, hist, new_ids[lo:hi], seed, prior_weight, n_EI_candidates, gamma,
-                                    'philox', precision, device, None, True, remote)
+                                    'philox', precision, device, None, True, remote, borrow=True)
                 vals, act = cc.values, np.asarray(cc.active, dtype=bool)
         except Exception as e:               # (still takes part in the gather: no rank waits forever)
             failed, err = True, e
@@ -981,7 +986,7 @@ def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, 
         try:
             if hi > lo:
                 cc = _suggest_local(table, hist, new_ids[lo:hi], seed, prior_weight, n_EI_candidates, gamma,
-                                    'philox', precision, device, None, True)
+                                    'philox', precision, device, None, True, borrow=True)
                 vals, act = cc.values, cc.active
         except Exception as e:               # (still takes part in the gather: no rank waits forever)
             failed, err = True, e
@@ -997,8 +1002,8 @@ def _suggest_sharded(table, hist, new_ids, seed, prior_weight, n_EI_candidates, 
         vals, act = np.full((n, L), np.nan), np.zeros((n, L), dtype=bool)
         try:
             cc = _suggest_local(table, hist, new_ids, seed, prior_weight, n_EI_candidates, gamma, 'philox',
-                                precision, device, None, True, remote)
-            vals, act = cc.values, np.asarray(cc.active, dtype=bool)
+                                precision, device, None, True, remote, borrow=True)
+            vals, act = cc.values, np.array(cc.active, dtype=bool)      # (the gather copies the values)
         except Exception as e:
             failed, err = True, e
         try:
