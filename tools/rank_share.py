@@ -59,6 +59,7 @@ def main():
     ap.add_argument('--hop-us', type=float, default=3.0)
     ap.add_argument('--bw-gbs', type=float, default=50.0)
     ap.add_argument('--json', default=None)
+    ap.add_argument('--only-n', type=int, default=0, help='one rank count only (and no unsharded run)')
     args = ap.parse_args()
     from hyperopt_amd import dist as D, tpe
     from hyperopt_amd.engine import get_engine
@@ -85,13 +86,13 @@ def main():
                                True, remote)
         return f
 
-    t1, t1m = timed(local(ids, ()), args.steps, 'unsharded')
+    t1, t1m = timed(local(ids, ()), args.steps, 'unsharded') if not args.only_n else (float('nan'), float('nan'))
     rows = [dict(axis='unsharded', N=1, shape=[1, 1], rank_us=t1, rank_mean_us=t1m, x_us=0.0, T_us=t1, eff=1.0,
                  phases_us=PH.get('unsharded'))]
     axes = [('labels', None), ('ids', None), ('grid', None)] if args.config == 4 else [('labels', None)]
     if args.config == 4:
         axes.append(('grid', 2))
-    for N in (2, 4, 8):
+    for N in (args.only_n,) if args.only_n else (2, 4, 8):
         for axis, G in axes:
             if axis == 'labels':
                 shape = (N, 1)
