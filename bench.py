@@ -210,6 +210,44 @@ def cpu_baseline(domain, trials, budget_s=10.0, sweep=(16, 64, 128, 256), sweep_
                 host=cpu)
 
 
+class CpuBaselineChild:
+    """cpu_baseline in a child process forked before anything initialises the
+    GPU (its pools fork in turn), held on a pipe until the GPU measurements are
+    done: the 10-30 s of host load (a 256-process sweep) then no longer runs
+    just before the timed steps (the first timed suggest after it took 0.21 ms
+    instead of 0.10).  result() starts it and waits; close() ends an unused
+    child (the pipe's end: EOF)."""
+
+    def __init__(self, pre):
+        import multiprocessing as mp
+        ctx = mp.get_context('fork')
+        self.conn, child = ctx.Pipe()
+        self.proc = ctx.Process(target=CpuBaselineChild._main, args=(child, self.conn, pre))
+        self.proc.start()
+        child.close()
+
+    @staticmethod
+    def _main(conn, parent_end, pre):
+        parent_end.close()            # (the fork's copy: the parent's close must reach EOF here)
+        try:
+            conn.recv()
+        except EOFError:
+            return
+        conn.send(cpu_baseline(*pre))
+
+    def result(self):
+        self.conn.send('go')
+        out = self.conn.recv()
+        self.close()
+        return out
+
+    def close(self):
+        if self.proc is not None:
+            self.conn.close()
+            self.proc.join()
+            self.proc = None
+
+
 # ------------------------------------------------------------------ roofline
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 # VALU issue peak: a wave64 VALU instruction issues over 2 cycles on a SIMD32
@@ -562,12 +600,24 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     pre = None
     cpu = None
+    cpu_child = None
     if args.config == 3:
         pre = make_history(args.history, SEED)
-        # the CPU baseline runs first, before anything initialises the GPU
-        # (its process pool forks); rank 0 at N = 1 only
+        # the CPU baseline's process, forked before anything initialises the GPU
+        # (its process pools fork), run after the GPU measurements; rank 0 at N = 1 only
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(*pre)
+            cpu_child = CpuBaselineChild(pre)
+    try:
+        main_gpu(args, world, rank, local, pre, cpu_child)
+    finally:
+        if cpu_child is not None:
+            cpu_child.close()
+
+
+def main_gpu(args, world, rank, local, pre, cpu_child):
+    import torch
+    import torch.distributed as dist
+    cpu = None
     if world > 1:
         if os.environ.get('TPE_BENCH_BACKEND', 'nccl') != 'nccl':
             local %= max(1, torch.cuda.device_count())
@@ -744,6 +794,8 @@ def main():
                     parallelism='%s shard x%d' % (dict(grid='label-group x id-block', labels='hyperparameter',
                                                        ids='new-id')[args.axis4], world))
 
+    if cpu_child is not None:
+        cpu = cpu_child.result()          # (after every GPU measurement of the line)
     if rank == 0:
         out = {
             'metric': 'EI candidates scored/sec (node) + tpe.suggest p50 latency, 1M cands x 10k trials',
