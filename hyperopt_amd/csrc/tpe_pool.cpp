@@ -222,7 +222,11 @@ Pool* get_pool() {
   if (t <= 1) return nullptr;
   if (!g_pool) {
     Pool* p = new Pool();
-    p->spin_ns = (int64_t)std::max(0, env_int("TPE_POOL_SPIN_US", 200)) * 1000;
+    // (a lone rank's workers spin 2 ms: a wake from sleep costs the first
+    // suggest after a pause ~60 us and the steady loop ~5 us of its p50 at 200 us
+    // (tools/g15.sh); ranks sharing the host's CPU quota keep 200 us)
+    const int spin_us = env_int("LOCAL_WORLD_SIZE", 1) > 1 ? 200 : 2000;
+    p->spin_ns = (int64_t)std::max(0, env_int("TPE_POOL_SPIN_US", spin_us)) * 1000;
     p->n_workers = t - 1;
     for (int i = 1; i < t; ++i) p->th.emplace_back(worker, p, i);
     g_pool = p;
