@@ -383,9 +383,20 @@ def _tree_labels(table, hist, engine=None, remote=()):
         if cache is not None and n_docs > memo[1] and memo[3][2] is None and _tree_refill(memo[5], meta, hist):
             holder.tree_memo = (table, n_docs, mkey, memo[3], dver, memo[5])
             return memo[3]
-    arr = arr0.view(np.uint8).copy().view(arr0.dtype)      # (a byte copy: the record dtype copies field by field)
     keep = []
     cats, glab, gix, glogc = _tree_groups(table, meta)
+    dense = hist.obs if isinstance(hist.obs, _history.DenseObs) else None
+    dense_all = (bool(glab) and not cats and dense is not None and dev_min is not None and dense.n >= dev_min
+                 and not remote and not glogc.any())
+    # a dense history's views (FMinIter on columnar data: a new History per
+    # appended trial, one device state shared in hist.dev): every record field
+    # that moves is rewritten below, so the previous view's records are reused
+    # — no copy of the table's records and no flag fix-ups per suggest
+    prev = hist.dev.get('_dense_tree') if dense_all and cache is None else None
+    if prev is not None and prev[0] is table and prev[1] == mkey:
+        arr = prev[2]
+    else:
+        arr = arr0.view(np.uint8).copy().view(arr0.dtype)  # (a byte copy: the record dtype copies field by field)
     for label, ix in cats:
         otids, ovals = hist.obs[label]
         cols = hist.cat_columns(label)
@@ -396,7 +407,6 @@ def _tree_labels(table, hist, engine=None, remote=()):
         rec = arr[ix]
         rec['tids'], rec['values'], rec['n_obs'] = cols[0], cols[1], len(otids)
     devs = None
-    dense = hist.obs if isinstance(hist.obs, _history.DenseObs) else None
     if glab and dense is not None and dev_min is not None and dense.n >= dev_min and not remote \
             and not glogc.any():
         # a dense history (every label in every trial, one matrix row each): the
@@ -417,6 +427,8 @@ def _tree_labels(table, hist, engine=None, remote=()):
             arr[f][gix] = v
         devs = (gix, slots, ns, dc.orders)
         glab = ()
+        if dense_all and cache is None:
+            hist.dev['_dense_tree'] = (table, mkey, arr)
     if glab:
         obs = hist.obs
         pairs = [obs[k] for k in glab]

@@ -385,11 +385,15 @@ def test_tree_labels_dense_history_matches_dict_history():
     losses = rs.uniform(size=cap)
     layout = DenseLayout(labels)
     dev_a, dev_b = {}, {}
+    prev = None
     for n in (N0, N0 + 1, N0 + 2, N0 + 40):
         ha = History(tids[:n], losses[:n], DenseObs(layout, m, tids[:n]), dev=dev_a)
         hb = History(tids[:n], losses[:n], {k: (tids[:n], m[i, :n]) for i, k in enumerate(labels)}, dev=dev_b)
         ta, tb = tpe._tree_labels(table, ha, _Eng()), tpe._tree_labels(table, hb, _Eng())
         ra, rb = ta[0], tb[0]
+        # (the dense views share one device state: their records are reused, rewritten)
+        assert prev is None or ra is prev
+        prev = ra
         for f in ('n_obs', 'tids', 'values', 'order', 'n_ord_in'):
             np.testing.assert_array_equal(ra[f], rb[f], err_msg='%s n=%d' % (f, n))
         for f in ('dev_obs', 'ord_key_in', 'ord_key_out'):
