@@ -975,8 +975,8 @@ def run_other(args, rank, world, device):
     if ranks is not None:
         extra['ranks'] = ranks
     if args.config == 4:
-        # the same batched suggest returning per-id dicts (Python int / float values:
-        # a batch of more than 4 ids, tpe._result_dicts)
+        # the same batched suggest returning per-id dicts (numpy int64 / float64
+        # values, as the reference's: tpe._result_dicts)
         lat_d = []
         for i in range(3):
             s0 = time.perf_counter()

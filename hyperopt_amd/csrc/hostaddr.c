@@ -96,46 +96,6 @@ done:
   return out;
 }
 
-/* row_dicts(keys, columns) -> [dict(zip(keys, row)) for row in zip(*columns)]:
- * the per-id result dicts of a batched suggest (tpe._choice_dicts), built
- * without a zip, a tuple or an iterator per id (keys: a tuple of k keys;
- * columns: k lists of equal length n). */
-static PyObject *row_dicts(PyObject *self, PyObject *args) {
-  (void)self;
-  PyObject *keys, *cols;
-  if (!PyArg_ParseTuple(args, "O!O!", &PyTuple_Type, &keys, &PyList_Type, &cols)) return NULL;
-  const Py_ssize_t k = PyTuple_GET_SIZE(keys);
-  if (PyList_GET_SIZE(cols) != k) {
-    PyErr_SetString(PyExc_ValueError, "row_dicts(): one column per key");
-    return NULL;
-  }
-  Py_ssize_t n = -1;
-  for (Py_ssize_t j = 0; j < k; ++j) {
-    PyObject *c = PyList_GET_ITEM(cols, j);
-    if (!PyList_Check(c) || (n >= 0 && PyList_GET_SIZE(c) != n)) {
-      PyErr_SetString(PyExc_ValueError, "row_dicts(): columns must be lists of one length");
-      return NULL;
-    }
-    n = PyList_GET_SIZE(c);
-  }
-  if (n < 0) n = 0;
-  PyObject *out = PyList_New(n);
-  if (!out) return NULL;
-  for (Py_ssize_t i = 0; i < n; ++i) {
-    PyObject *d = _PyDict_NewPresized(k);
-    if (!d) { Py_DECREF(out); return NULL; }
-    for (Py_ssize_t j = 0; j < k; ++j) {
-      if (PyDict_SetItem(d, PyTuple_GET_ITEM(keys, j), PyList_GET_ITEM(PyList_GET_ITEM(cols, j), i)) < 0) {
-        Py_DECREF(d);
-        Py_DECREF(out);
-        return NULL;
-      }
-    }
-    PyList_SET_ITEM(out, i, d);
-  }
-  return out;
-}
-
 /* typed_dicts(keys, ix, cat, values, active) -> per row i of values / active
  * ([n x L] float64 / int8, C-contiguous) the dict {keys[j]: value} in the
  * order of `keys` (k labels; ix: their k table indices, int64; cat: k bytes, 1
@@ -476,7 +436,6 @@ static PyMethodDef methods[] = {
     {"addresses", addresses, METH_VARARGS,
      "int64 array of the data addresses of a sequence of C-contiguous numpy arrays (of dtype typenum)"},
     {"tails", tails, METH_VARARGS, "float64 concatenation of seq[i][start[i]:stop[i]]"},
-    {"row_dicts", row_dicts, METH_VARARGS, "[dict(zip(keys, row)) for row in zip(*columns)]"},
     {"typed_dicts", typed_dicts, METH_VARARGS, "per-row {label: np.int64 / np.float64 / None} dicts"},
     {"tracked_misc", tracked_misc, METH_VARARGS, "base.tracked_misc: the tracked misc of one suggested id"},
     {"call_tree", call_tree, METH_VARARGS, "tpe_suggest_tree through its address (Engine.suggest_tree)"},

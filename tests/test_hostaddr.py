@@ -15,10 +15,36 @@ def test_addresses_and_tails():
     np.testing.assert_array_equal(got, np.concatenate([arrs[0][1:3], arrs[1][0:2], arrs[2][3:5]]))
 
 
-def test_row_dicts():
-    keys = ('a', 'b', 'c')
-    cols = [[1, 2, 3], [None, 0.5, 1.5], [7, None, 9]]
-    assert _ha.row_dicts(keys, cols) == [dict(zip(keys, row)) for row in zip(*cols)]
+@pytest.mark.parametrize('n_ids', [1, 4, 5, 300])
+def test_result_dicts_keep_numpy_types(n_ids):
+    """A suggest's per-id dicts (tpe._result_dicts, _hostaddr.typed_dicts): level
+    order, None for an inactive label, np.int64 categories and np.float64
+    values — the reference's types whatever the id count."""
+    from hyperopt_amd import hp, tpe
+    from hyperopt_amd.space import ParamTable
+    table = ParamTable({'c': hp.choice('c', [{'x': hp.uniform('x', 0, 1)}, {'y': hp.normal('y', 0, 1)}]),
+                        'z': hp.loguniform('z', -1, 1)})
+    order = table.level_order()
+    rs = np.random.RandomState(n_ids)
+    L = len(table.rows)
+    values = rs.uniform(size=(n_ids, L))
+    active = np.ones((n_ids, L), dtype=np.int8)
+    ci = table.by_label['c'].index
+    values[:, ci] = rs.randint(0, 2, n_ids)
+    for j in range(n_ids):                 # (the branch the choice did not take: inactive)
+        active[j, table.by_label['y' if values[j, ci] == 0 else 'x'].index] = 0
+    got = tpe._result_dicts(table, values, active)
+    assert len(got) == n_ids
+    for j, d in enumerate(got):
+        assert list(d) == list(order)
+        for k, v in d.items():
+            r = table.by_label[k]
+            if not active[j, r.index]:
+                assert v is None
+            elif r.categorical:
+                assert type(v) is np.int64 and v == int(values[j, r.index])
+            else:
+                assert type(v) is np.float64 and v == values[j, r.index]
 
 
 def test_tracked_misc_matches_python():
