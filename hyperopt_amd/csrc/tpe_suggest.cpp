@@ -602,7 +602,13 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     std::vector<int> remote;
     for (int i = 0; i < n_labels; ++i)
       if (labels[i].depth == d && (labels[i].flags & TPE_F_REMOTE)) remote.push_back(i);
-    if (!remote.empty()) {
+    // (a flat space with local members: the remote entries are written by the
+    // results pass below, row by row with the members' — one pass over the rows)
+    bool any_member = false;
+    for (int i = 0; i < n_labels && !any_member; ++i)
+      any_member = labels[i].depth == d && !(labels[i].flags & TPE_F_REMOTE);
+    const bool rem_in_put = flat && any_member && !remote.empty();
+    if (!remote.empty() && !rem_in_put) {
       struct Rem { const tpe_tree_label* labels; const int* remote; int nr; int8_t* active; double* values;
                    const int* chosen; int n_ids, n_labels; bool flat; };
       Rem rm{labels, remote.data(), (int)remote.size(), active, values, chosen.data(), n_ids, n_labels, flat};
@@ -648,7 +654,13 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
     }
     if (pending) return TPE_E_FALLBACK;
     trace_mark("members");
-    if (members.empty()) continue;
+    if (members.empty()) {
+      // (a flat space whose local labels all needed nothing: the remote entries still)
+      if (rem_in_put)
+        for (int j = 0; j < n_ids; ++j)
+          for (int r : remote) { active[(size_t)j * n_labels + r] = 1; values[(size_t)j * n_labels + r] = NAN; }
+      continue;
+    }
     // the gated members' id arrays (positions -> new ids), stable now that lvl_ids is complete
     std::vector<int64_t> lvl_new((size_t)lvl_ids.size());
     for (size_t q = 0; q < lvl_ids.size(); ++q) lvl_new[q] = ids[lvl_ids[q]];
@@ -669,11 +681,12 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
       const Member* members; int n_mem; const int64_t* lvl_ids;
       const tpe_result* res; double* values; int8_t* active; int* chosen; const char* gate; int n_ids, n_labels;
       int8_t* bad;
+      const int* rem; int n_rem;     // (flat space: the remote labels, active with another rank's value)
     };
     const int nbk = (n_ids + kIdBlock - 1) / kIdBlock;
     std::vector<int8_t> bad((size_t)std::max(nbk, 1), 0);
     Mem mx{members.data(), (int)members.size(), lvl_ids.data(), res.data(), values, active, chosen.data(),
-           T.gate.data(), n_ids, n_labels, bad.data()};
+           T.gate.data(), n_ids, n_labels, bad.data(), remote.data(), rem_in_put ? (int)remote.size() : 0};
     auto put = [](void* c, int k) {
       const Mem& x = *(const Mem*)c;
       const int64_t j0 = (int64_t)k * kIdBlock, j1 = std::min<int64_t>(x.n_ids, j0 + kIdBlock);
@@ -697,6 +710,11 @@ static int suggest_tree(const tpe_tree_label* labels, int32_t n_labels, const in
         const int64_t* lo = std::lower_bound(base, base + m.count, j0);
         const int64_t* hi = std::lower_bound(lo, base + m.count, j1);
         for (const int64_t* p = lo; p < hi; ++p) set(m.res_off + (p - base), *p);
+      }
+      for (int64_t j = j0; j < j1 && x.n_rem; ++j) {
+        int8_t* row = x.active + (size_t)j * x.n_labels;
+        double* vrow = x.values + (size_t)j * x.n_labels;
+        for (int r = 0; r < x.n_rem; ++r) { row[x.rem[r]] = 1; vrow[x.rem[r]] = NAN; }
       }
       x.bad[k] = b;
     };
