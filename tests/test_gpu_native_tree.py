@@ -95,14 +95,13 @@ def test_native_tree_columnar_history():
             tpe.NATIVE_TREE = True
         assert cc.labels == table.labels and cc.values.shape == (len(ids), 5) and cc.active.all()
         assert cc.dicts(table) == nat
-        assert all(type(v) is float for v in cc.dicts(table)[0].values())      # (batched: Python scalars)
+        assert all(type(v) is np.float64 for v in cc.dicts(table)[0].values())   # (the reference's types)
 
 
 def test_native_tree_batched_result_types():
-    """More than a few ids take the column-wise dict assembly: the same values
-    as Python scalars (int categories, float values, None when inactive: no
-    numpy scalar per value) in level order; a few ids keep the reference's
-    np.int64 / np.float64 (tpe.py:812 suggests one id at a time)."""
+    """A batch's per-id dicts and a single id's hold the same value types, the
+    reference's np.int64 categories and np.float64 values (None when
+    inactive), in level order (tpe.py:812 suggests one id at a time)."""
     import bench
     from hyperopt_amd import tpe
     domain, trials = bench.make_history(2000, 1)
@@ -115,7 +114,7 @@ def test_native_tree_batched_result_types():
         assert list(d) == order
         for r in domain.table.rows:
             v = d[r.label]
-            assert v is None or type(v) is (int if r.categorical else float), (r.label, type(v))
+            assert v is None or type(v) is (np.int64 if r.categorical else np.float64), (r.label, type(v))
     one = tpe.suggest_choices(domain.table, __import__('hyperopt_amd').history.extract(domain, trials), ids[:1], 4,
                               n_EI_candidates=4096)[0]
     for r in domain.table.rows:
