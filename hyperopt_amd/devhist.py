@@ -65,7 +65,10 @@ class _Staging(object):
         return self.pin.numpy(), self.dev
 
     def used(self):
-        self.ev = torch.cuda.Event()
+        # (one event, re-recorded after each launch that reads the buffer: an
+        # Event object a launch cost ~10 us of Python)
+        if self.ev is None:
+            self.ev = torch.cuda.Event()
         self.ev.record()
 
 

@@ -168,6 +168,7 @@ def test_suggestion_documents_hold_no_reference_cycles():
     import bench
     from hyperopt_amd import base, rand
     domain, trials = bench.make_history(60, 3)
+    T0 = 7_000_000                                 # (tids no other test's documents carry)
     d = rand.suggest([500], domain, trials, 1)     # (first call: caches)
     del d
     gc.collect()
@@ -175,14 +176,15 @@ def test_suggestion_documents_hold_no_reference_cycles():
     gc.set_debug(gc.DEBUG_SAVEALL)
     try:
         for i in range(40):
-            d = rand.suggest([600 + i], domain, trials, i)
+            d = rand.suggest([T0 + i], domain, trials, i)
             # the links still lead up to the document, for the mutation logs
             lst = d[0]['misc']['vals']['model']
             assert lst._up() is d[0]['misc']['vals'] and d[0]['misc']['vals']._up() is d[0]['misc']
             del d, lst
         gc.collect()
-        # (other tests' objects may be collected here too: only this loop's count)
-        ours = [o for o in gc.garbage if type(o) in (base._Doc, base._Part) and 600 <= o.get('tid', -1) < 640]
+        # (other tests' objects may be collected here too — a Trials' cache is a
+        # cycle — so only this loop's documents count: their tids are unique)
+        ours = [o for o in gc.garbage if type(o) in (base._Doc, base._Part) and T0 <= o.get('tid', -1) < T0 + 40]
     finally:
         gc.set_debug(0)
         gc.garbage.clear()

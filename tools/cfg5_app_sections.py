@@ -43,7 +43,9 @@ def main():
     for obj, name in ((tpe, '_tree_labels'), (tpe, '_native_tree'), (tpe, '_suggest_local'), (E.Engine, 'suggest_tree'),
                       (devhist.DeviceColumns, 'upload_rows'), (devhist._Orders, 'ptrs_many'),
                       (devhist._Orders, 'commit_many'), (history, 'split_below'), (history.History, '__init__'),
-                      (tpe, '_result_dicts')):
+                      (tpe, '_result_dicts'), (devhist.DeviceColumns, '_scatter'), (devhist._Staging, 'get'),
+                      (devhist._Staging, 'used'), (devhist, '_positions'), (devhist.DeviceColumns, 'upload'),
+                      (devhist.DeviceColumns, 'addresses'), (tpe, '_tree_groups'), (tpe, '_tree_static')):
         if hasattr(obj, name):
             wrap(obj, name)
     desc, step, _ = bench.config_workload(5, 0, 1, ns)
