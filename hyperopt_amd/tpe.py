@@ -348,6 +348,10 @@ def device_fits(n_obs, n_below, dev_min):
     return dev_min is not None and n_obs >= dev_min and n_below <= 64 and n_obs - n_below + 1 > 64
 
 
+_DENSE_FIELDS = ('n_obs', 'tids', 'values', 'order', 'dev_obs', 'ord_key_in', 'ord_idx_in', 'n_ord_in', 'ord_key_out',
+                 'ord_idx_out')
+
+
 def _tree_labels(table, hist, engine=None, remote=()):
     """The table's tree records with the history's observation columns filled
     in (tids, kernel coordinate, value order) and, for the continuous labels
@@ -420,14 +424,22 @@ def _tree_labels(table, hist, engine=None, remote=()):
         ta = np.ascontiguousarray(dense.tids, dtype=np.int64)
         if ta is not dense.tids:
             keep.append(ta)
+        # (the records' field views kept with the reused records; every label a
+        # device label in table order — config 5 — writes whole fields)
+        fvs = prev[3] if prev is not None and prev[2] is arr else None
+        if fvs is None:
+            whole = len(gix) == len(arr) and bool((gix == np.arange(len(arr))).all())
+            fvs = {f: arr[f] for f in _DENSE_FIELDS}
+            fvs[None] = slice(None) if whole else gix
+        at = fvs[None]
         for f, v in (('n_obs', n), ('tids', ta.ctypes.data), ('values', m.ctypes.data + m.strides[0] * ri),
                      ('order', 0), ('dev_obs', dc.addresses(slots)), ('ord_key_in', kin), ('ord_idx_in', iin),
                      ('n_ord_in', n_in), ('ord_key_out', kout), ('ord_idx_out', iout)):
-            arr[f][gix] = v
+            fvs[f][at] = v
         devs = (gix, slots, ns, dc.orders)
         glab = ()
         if dense_all and cache is None:
-            hist.dev['_dense_tree'] = (table, mkey, arr)
+            hist.dev['_dense_tree'] = (table, mkey, arr, fvs)
     if glab:
         obs = hist.obs
         pairs = [obs[k] for k in glab]
