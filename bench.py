@@ -255,7 +255,7 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 # x 4 SIMDs x 256 CUs x 2.4 GHz
 PEAK_VALU_GINST = 0.5 * 4 * 256 * 2.4      # = 1228.8 G wave-instructions/s
 # counter summary of the same bench command (tools/gpu.sh pmc -> tools/pmc_summary.py)
-PMC_SUMMARY_REL = 'profiles/r05_pmc_summary.json'
+PMC_SUMMARY_REL = 'profiles/r06_pmc_summary.json'
 PMC_SUMMARY = os.path.join(ROOT, PMC_SUMMARY_REL)
 VALU_KERNELS = ('k_sample', 'k_tables', 'k_select', 'above', 'k_finalize')
 
