@@ -3160,7 +3160,9 @@ __device__ __forceinline__ double row_sum_last(double v) {
 }
 static_assert(kFgtLanes == 16, "a cell's lanes are one DPP row");
 
-__global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict__ P,
+// (six waves a SIMD: 80 VGPRs, 6 of them spilled — 373-391 us on config 5
+// against 410-423 at the four waves its 105 VGPRs allowed, tools/g21.sh)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k_cells_fgt(const tpe_problem* __restrict__ P,
                                                    const tpe_tab_job* __restrict__ J,
                                                    const float4* __restrict__ comp32,
                                                    const int32_t* __restrict__ grid, float4* __restrict__ tab,
@@ -3191,20 +3193,25 @@ __global__ __launch_bounds__(512) void k_cells_fgt(const tpe_problem* __restrict
     const double* __restrict__ rec = reinterpret_cast<const double*>(tab + p.fgt_off + 1 + (int64_t)b * TPE_FGT_BOX_UNITS);
     const double x = (cd - (p.fgt_lo + ((double)b + 0.5) * d)) / d;
     const double eh = exp(-0.5 * x * x), e = eh * eh;
-    double hj[kFgtJ + 1];                             // h_j(x) = e^-x^2 H_j(x)
-    hj[0] = e;
-    hj[1] = 2.0 * x * e;
-#pragma unroll
-    for (int q = 1; q < kFgtJ; ++q) hj[q + 1] = 2.0 * x * hj[q] - 2.0 * (double)q * hj[q - 1];
     double A[kFgtP];
 #pragma unroll
     for (int n = 0; n < kFgtP; ++n) A[n] = rec[n];
+    // B_m = sum_n A_n h_(n+m)(x), h_j = e^-x^2 H_j(x) by its recurrence, made
+    // one j at a time and added to every B_m it feeds (n = j - m ascending for
+    // each m: the same sums in the same order as a table of every h_j, without
+    // the 27 doubles that table held: occupancy)
+    double h0 = e, h1 = 2.0 * x * e;
 #pragma unroll
-    for (int m = 0; m < kTabMoments; ++m) {
-      double sm = 0.0;
+    for (int jj = 0; jj <= kFgtJ; ++jj) {
+      const double hv = jj == 0 ? h0 : h1;
 #pragma unroll
-      for (int n = 0; n < kFgtP; ++n) sm += A[n] * hj[n + m];
-      B[m] = sm;
+      for (int m = 0; m < kTabMoments; ++m)
+        if (jj - m >= 0 && jj - m < kFgtP) B[m] += A[jj - m] * hv;
+      if (jj >= 1 && jj < kFgtJ) {                    // h_(jj+1) = 2 x h_jj - 2 jj h_(jj-1)
+        const double h2 = 2.0 * x * h1 - 2.0 * (double)jj * h0;
+        h0 = h1;
+        h1 = h2;
+      }
     }
     err = A[0] * eh * kFgtEps;
   }

@@ -1,6 +1,6 @@
 # round 6, call 17: GPU suite after the dict-type and record-reuse changes;
 # config 5's appended step by section; config 4 / 5-appending lines
-set -o pipefail
+set -eo pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_g17.log 2>&1 &&
