@@ -442,8 +442,9 @@ def test_fast_sample_kernel_lg_against_oracle(branch):
     """tpe_debug_fast_lg: k_sample_fast itself writes every candidate's value,
     l and g; on the headline (config 3, 10k trials, 2^20 candidates; svm
     branch: log-polynomial cells, rf branch: lattices) 3000 of each label's
-    are checked against the oracle's lpdf with the host fits of the same
-    suggest (1e-5 relative, lattices 1e-9), and the suggested value is the
+    are checked against the oracle's lpdf of the oracle's own fits of the
+    history (ap_filter_trials + adaptive_parzen_normal: nothing of this
+    build's fits; 1e-5 relative, lattices 1e-9), and the suggested value is the
     argmax of l - g over the label's candidates (within the eps-tie set)."""
     import torch
     import bench
@@ -464,7 +465,6 @@ def test_fast_sample_kernel_lg_against_oracle(branch):
     rec = buf.cpu().numpy().reshape(-1, 4)
     rec = rec[np.isfinite(rec[:, 3])]
     hist = H.extract(domain, trials)
-    fits = tpe._Fits(T, hist, H.split_below(hist, 0.25), 1.0, None)
     chosen = {k: v[0] for k, v in doc['misc']['vals'].items() if v}
     rs = np.random.RandomState(5)
     seen = 0
@@ -473,16 +473,15 @@ def test_fast_sample_kernel_lg_against_oracle(branch):
         if not len(mine) or r.categorical or r.label not in chosen:
             continue
         assert len(mine) == C, r.label
-        post = fits.get(r)
         q = r.args.get('q')
-        log = r.dist.startswith('log') or r.dist.startswith('qlog')
-        lpdf = O.lgmm1_lpdf if log else O.gmm1_lpdf
-        kw = dict(low=post.low, high=post.high, q=q)
+        otids, ovals = hist.obs[r.label]
+        below, above = O.ap_filter_trials(otids, ovals, hist.tids, hist.losses, 0.25)
+        pb, pa = (O.fit_posterior(r.dist, dict(r.args), o, 1.0) for o in (below, above))
         tol = 1e-9 if q else 1e-5
         sub = rs.choice(len(mine), 3000, replace=False)
         x = mine[sub, 0]
-        for col, mix in ((1, post.below), (2, post.above)):
-            ref = lpdf(x, *mix, **kw)
+        for col, post in ((1, pb), (2, pa)):
+            ref = post.lpdf(x)
             got = mine[sub, col]
             fin = np.isfinite(ref)
             err = np.abs(got[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1.0)
