@@ -91,7 +91,7 @@ def main():
                  phases_us=PH.get('unsharded'))]
     axes = [('labels', None), ('ids', None), ('grid', None)] if args.config == 4 else [('labels', None)]
     if args.config == 4:
-        axes.append(('grid', 2))
+        axes += [('grid', 2), ('grid', 4)]
     for N in (args.only_n,) if args.only_n else (2, 4, 8):
         for axis, G in axes:
             if axis == 'labels':
