@@ -103,6 +103,53 @@ struct Tree {
 // first to last (every trial observed the label: a flat space's columns) are
 // indexed directly instead of searched: 25 searches over a 10^5-tid column
 // were most of a device-fitted label's host fit
+// A below side's sort (at most kSortNet values: ap_filter_trials caps the
+// below count at 25, tpe.py:625-636): Batcher's odd-even merge network over 32
+// keys — the values' order-preserving integer images, NaN after every number,
+// padding after NaN — with the positions swapped alongside, branch-free (the
+// insertion sort it replaces mispredicted its way through ~1.5 us a label on
+// config 5's thousand).  Ties come out in any order: a side of at most 25
+// observations has every weight 1 (no linear-forgetting ramp, tpe.py:381-394),
+// so tied values are interchangeable in the fit.
+constexpr int kSortNet = 32;
+struct SortNet {
+  int n = 0;
+  uint8_t a[256], b[256];
+  SortNet() {                                        // Batcher's odd-even mergesort comparators
+    for (int p = 1; p < kSortNet; p <<= 1)
+      for (int k = p; k >= 1; k >>= 1)
+        for (int j = k % p; j + k < kSortNet; j += 2 * k)
+          for (int i = 0; i < k && i + j + k < kSortNet; ++i)
+            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) { a[n] = (uint8_t)(i + j); b[n] = (uint8_t)(i + j + k); ++n; }
+  }
+};
+const SortNet g_sort_net;
+
+// sorts x[0, n) (n <= kSortNet) into ord: x[ord[0]] <= x[ord[1]] <= .., NaN last
+inline void sort_small(const double* x, int64_t n, int64_t* ord) {
+  uint64_t k[kSortNet];
+  int64_t ix[kSortNet];
+  for (int i = 0; i < kSortNet; ++i) {
+    uint64_t u = ~0ull;                              // (padding: after everything)
+    if (i < n) {
+      const double v = x[i];
+      memcpy(&u, &v, 8);
+      u = v != v ? ~0ull - 1 : (u >> 63 ? ~u : u | (1ull << 63));   // (NaN: after every number)
+    }
+    k[i] = u;
+    ix[i] = i;
+  }
+  for (int c = 0; c < g_sort_net.n; ++c) {
+    const int a = g_sort_net.a[c], b = g_sort_net.b[c];
+    const uint64_t ka = k[a], kb = k[b];
+    const bool sw = ka > kb;
+    const int64_t ia = ix[a], ib = ix[b];
+    k[a] = sw ? kb : ka; k[b] = sw ? ka : kb;
+    ix[a] = sw ? ib : ia; ix[b] = sw ? ia : ib;
+  }
+  for (int64_t i = 0; i < n; ++i) ord[i] = ix[i];
+}
+
 inline void below_positions(const int64_t* tids, int64_t n, const int64_t* below, int64_t nb,
                             std::vector<int32_t>& out) {
   out.clear();
@@ -201,18 +248,23 @@ int fit_label(Tree& T, int i, bool spec = false) {
     below_positions(L.tids, n, T.below, T.n_below, f.below_idx);
     const int64_t nb = (int64_t)f.below_idx.size();
     if (nb > 64 || n - nb + 1 <= 64) return TPE_E_FALLBACK;
-    std::vector<double> bx((size_t)nb);
-    std::vector<int64_t> ord((size_t)nb);
-    for (int64_t q = 0; q < nb; ++q) { bx[(size_t)q] = x[f.below_idx[(size_t)q]]; ord[(size_t)q] = q; }
-    for (int64_t q = 1; q < nb; ++q)                        // stable insertion sort (NaN last)
-      for (int64_t r = q; r > 0; --r) {
-        const double a = bx[(size_t)ord[(size_t)r - 1]], c = bx[(size_t)ord[(size_t)r]];
-        if (!(a > c || (a != a && c == c))) break;
-        std::swap(ord[(size_t)r - 1], ord[(size_t)r]);
-      }
+    double bx[64];
+    int64_t ord[64];
+    for (int64_t q = 0; q < nb; ++q) bx[q] = x[f.below_idx[(size_t)q]];
+    if (nb <= kSortNet && (T.lf <= 0 || nb <= T.lf)) {     // (no linear-forgetting ramp: ties interchangeable)
+      sort_small(bx, nb, ord);
+    } else {                                                // (else: stable insertion sort, NaN last)
+      for (int64_t q = 0; q < nb; ++q) ord[q] = q;
+      for (int64_t q = 1; q < nb; ++q)
+        for (int64_t r = q; r > 0; --r) {
+          const double a = bx[ord[r - 1]], c = bx[ord[r]];
+          if (!(a > c || (a != a && c == c))) break;
+          std::swap(ord[r - 1], ord[r]);
+        }
+    }
     const size_t cap = (size_t)nb + 1;
     f.buf.resize(3 * cap);
-    const int64_t rc = tpe_host_fit_parzen(bx.data(), nb, nb >= 2 ? ord.data() : nullptr, T.prior_weight, L.prior_mu,
+    const int64_t rc = tpe_host_fit_parzen(bx, nb, nb >= 2 ? ord : nullptr, T.prior_weight, L.prior_mu,
                                            L.prior_sigma, T.lf, f.buf.data(), f.buf.data() + cap,
                                            f.buf.data() + 2 * cap);
     if (rc < 0) return tpe_internal_fail(TPE_E_ARG, "tpe_host_fit_parzen failed on a below side");
@@ -269,11 +321,30 @@ bool prefit_worthy(const Tree& T, int i) {
 struct PrefitCtx {
   Tree* T;
   const int* ix;
+  int n, per;                      // labels; labels a task
 };
 
-void prefit_one(void* c, int j) {
+// a device-fitted label's below values touched before its fit: a task's
+// labels issue every such load up front, so their cache and TLB misses (one
+// label column of 10^5 values each: ~1 us a label one at a time) overlap
+void prefetch_below(const Tree& T, int i) {
+  const tpe_tree_label& L = T.L[i];
+  if (!L.dev_obs || !L.tids || !L.values || L.n_obs <= 0 || L.family == TPE_FAM_CATEGORICAL) return;
+  const int64_t t0 = L.tids[0], n = L.n_obs;
+  if (L.tids[n - 1] - t0 != n - 1) return;          // (dense tids only: a position is tid - t0)
+  const double* x = (const double*)L.values;
+  for (int64_t b = 0; b < T.n_below; ++b) {
+    const int64_t t = T.below[b] - t0;
+    if (t >= 0 && t < n) __builtin_prefetch(x + t);
+  }
+}
+
+void prefit_one(void* c, int k) {
   PrefitCtx* p = (PrefitCtx*)c;
-  fit_label(*p->T, p->ix[j], true);
+  const int j0 = k * p->per, j1 = std::min(p->n, j0 + p->per);
+  if (j1 - j0 > 1)
+    for (int j = j0; j < j1; ++j) prefetch_below(*p->T, p->ix[j]);
+  for (int j = j0; j < j1; ++j) fit_label(*p->T, p->ix[j], true);
 }
 
 void prefit(Tree& T) {
@@ -287,8 +358,10 @@ void prefit(Tree& T) {
   if (ix.size() < 2 || tpe_pool::workers() == 0) return;   // (on demand, on this thread)
   // largest first: the slowest fits start first
   std::sort(ix.begin(), ix.end(), [&](int a, int b) { return T.L[a].n_obs > T.L[b].n_obs; });
-  PrefitCtx c{&T, ix.data()};
-  tpe_pool::parallel_for((int)ix.size(), prefit_one, &c);
+  // (a thousand labels: eight a task, their loads issued together; a few: one a task)
+  const int n = (int)ix.size(), per = n >= 256 ? 8 : 1;
+  PrefitCtx c{&T, ix.data(), n, per};
+  tpe_pool::parallel_for((n + per - 1) / per, prefit_one, &c);
 }
 
 // ParamTable.active: some parent chose this label's option (`chosen`: the
