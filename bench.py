@@ -652,6 +652,7 @@ def main_gpu(args, world, rank, local, pre, cpu_child):
 
     import gc
     cg0 = cgroup_cpu_stat()      # (read before the warm-up: nothing between it and the timed steps)
+    hc0 = host_contention()
     for i in range(args.warmup):
         step(i)
     barrier()
@@ -668,6 +669,7 @@ def main_gpu(args, world, rank, local, pre, cpu_child):
     barrier()
     elapsed = time.perf_counter() - t0
     cg1 = cgroup_cpu_stat()
+    hc1 = host_contention()
     gc.callbacks.remove(_count_gc)
     gc_timed = dict(_GC_COUNT)
     if world > 1:
@@ -724,6 +726,8 @@ def main_gpu(args, world, rank, local, pre, cpu_child):
     if world == 1:
         tail = dict(steps_ms=[round(1e3 * x, 4) for x in lat], gc_collections=gc_timed,
                     cgroup_cpu_stat_warmup_and_timed={k: cg1.get(k, 0) - cg0.get(k, 0) for k in cg1},
+                    host_contention_warmup_and_timed={k: (v - hc0[k] if k in hc0 and not isinstance(v, str) else v)
+                                                      for k, v in hc1.items()},
                     slowest_of_200=slow_steps(eng, step, 200, base=30000))
 
 
@@ -852,6 +856,27 @@ def cgroup_cpu_stat():
                 out[k] = int(v)
     except (OSError, ValueError):
         pass
+    return out
+
+
+def host_contention():
+    """Signs of other load on the host's CPUs: this process's involuntary and
+    voluntary context switches (all its threads, getrusage) and the CPU
+    pressure-stall totals (us some task waited for a CPU: the cgroup's
+    cpu.pressure, else the host's /proc/pressure/cpu), {} where absent."""
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out = {'nivcsw': ru.ru_nivcsw, 'nvcsw': ru.ru_nvcsw}
+    for path in ('/sys/fs/cgroup/cpu.pressure', '/proc/pressure/cpu'):
+        try:
+            with open(path) as f:
+                for line in f:
+                    p = line.split()
+                    out['psi_%s_total_us' % p[0]] = int(p[-1].split('=')[1])
+            out['psi_source'] = path
+            break
+        except (OSError, ValueError, IndexError):
+            continue
     return out
 
 

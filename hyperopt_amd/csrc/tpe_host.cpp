@@ -1156,9 +1156,11 @@ int tpe_host_pack_level(const tpe_label_in* labels, int32_t n_labels, int32_t n_
                      tmode.data(), tn0.data(), tn1.data(), tlat.data(), tklo.data(), tkhi.data(), fgt_boxes.data(),
                      logpoly.data()};
     // (a label's decision reads its whole above mixture: thousands of
-    // components per label make a worker's hand-off worth it)
+    // components per label make a worker's hand-off worth it; a device-fitted
+    // label's reads only its below side — config 5's 125 labels a rank decide in
+    // 5 us on one thread, 11-14 us handed out)
     int64_t comps = 0;
-    for (int32_t li = 0; li < n_labels; ++li) comps += labels[li].above_k;
+    for (int32_t li = 0; li < n_labels; ++li) comps += dev_fit[li] ? labels[li].below_k : labels[li].above_k;
     // (in chunks of up to kTabChunk labels: a thousand-label level's decisions
     // are sub-microsecond each, too small to hand out one by one; a few large
     // labels — config 4's twenty of 10^4 components — one a task)
