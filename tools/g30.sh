@@ -1,5 +1,5 @@
-# round 6, call 31: the staged cells shared by two waves (TPE_TAB_CELL_WAVES=2,
-# the in-tree library) — the GPU suite on it, then alternating headline lines
+# round 6, calls 31-32: a k_tables or k_sample_fast variant (the in-tree library,
+# 32: the first draws made while the table lands) — the GPU suite on it, then alternating headline lines
 # and kernel traces against the previous library (libtpe_hip_base.so)
 set -o pipefail
 O=gpurun_out
