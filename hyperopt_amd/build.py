@@ -20,7 +20,7 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     semantics), link both into hyperopt_amd/libtpe_hip.so (or `out`, with extra
     -D `defines` on the kernels: A/B variants for tools/)."""
     OUT = out
-    deps = [SRC, HOST_SRC, SUGGEST_SRC, POOL_SRC, os.path.join(HERE, 'csrc', 'tpe_pool.h'),
+    deps = [SRC, HOST_SRC, SUGGEST_SRC, POOL_SRC, os.path.join(HERE, 'csrc', 'tpe_pool.h'), os.path.join(HERE, 'csrc', 'sort_net.h'),
             os.path.join(HERE, '..', 'include', 'tpe_hip.h'), os.path.abspath(__file__)]
     if out == os.path.join(HERE, 'libtpe_hip.so'):
         build_hostaddr(force, verbose)
@@ -34,7 +34,8 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     suggest_o = os.path.join(HERE, 'csrc', 'tpe_suggest.o')
     pool_o = os.path.join(HERE, 'csrc', 'tpe_pool.o')
     dev_o = os.path.join(HERE, 'csrc', 'tpe_kernels.o' if not defines else tag + '.o')
-    hdr = [os.path.join(HERE, '..', 'include', 'tpe_hip.h'), os.path.join(HERE, 'csrc', 'tpe_pool.h')]
+    hdr = [os.path.join(HERE, '..', 'include', 'tpe_hip.h'), os.path.join(HERE, 'csrc', 'tpe_pool.h'),
+           os.path.join(HERE, 'csrc', 'sort_net.h')]
     host_flags = [gxx, '-O3', '-march=' + HOST_MARCH, '-std=c++17', '-fPIC', '-Wall']
     numpy_fp = ['-ffp-contract=off', '-fno-fast-math', '-fno-trapping-math']
     # (object, its sources, compile command): an object is rebuilt when a source

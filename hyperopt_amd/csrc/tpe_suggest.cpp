@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/tpe_hip.h"
+#include "sort_net.h"
 #include "tpe_pool.h"
 
 extern "C" int tpe_internal_fail(int code, const char* what);   // tpe_kernels.hip (hidden)
@@ -35,6 +36,9 @@ extern "C" int tpe_internal_level_run_ex(const tpe_label_in* labels, int32_t n_l
                                          int32_t* done);              // tpe_kernels.hip (hidden)
 
 namespace {
+
+using tpe_sort_net::kSortNet;
+using tpe_sort_net::sort_small;
 
 // host phase clock (include/tpe_hip.h "Host phase clock")
 std::atomic<int> g_ph_on{0};
@@ -95,61 +99,11 @@ struct Tree {
   int8_t* need_fit;             // labels the caller must fit (TPE_E_FALLBACK)
 };
 
-// spec: a speculative fit on a pool worker (prefit): labels the caller must
-// fit are left alone (no need_fit flag), and a failure only leaves the fit
-// undone — the label's real fit, on the calling thread, reports it
 // each below tid's position among a label's ascending tids (ap_filter_trials,
 // tpe.py:629-636), in the below set's (ascending) order.  Tids one apart from
 // first to last (every trial observed the label: a flat space's columns) are
 // indexed directly instead of searched: 25 searches over a 10^5-tid column
 // were most of a device-fitted label's host fit
-// A below side's sort (at most kSortNet values: ap_filter_trials caps the
-// below count at 25, tpe.py:625-636): Batcher's odd-even merge network over 32
-// keys — the values' order-preserving integer images, NaN after every number,
-// padding after NaN — with the positions swapped alongside, branch-free (the
-// insertion sort it replaces mispredicted its way through ~1.5 us a label on
-// config 5's thousand).  Ties come out in any order: a side of at most 25
-// observations has every weight 1 (no linear-forgetting ramp, tpe.py:381-394),
-// so tied values are interchangeable in the fit.
-constexpr int kSortNet = 32;
-struct SortNet {
-  int n = 0;
-  uint8_t a[256], b[256];
-  SortNet() {                                        // Batcher's odd-even mergesort comparators
-    for (int p = 1; p < kSortNet; p <<= 1)
-      for (int k = p; k >= 1; k >>= 1)
-        for (int j = k % p; j + k < kSortNet; j += 2 * k)
-          for (int i = 0; i < k && i + j + k < kSortNet; ++i)
-            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) { a[n] = (uint8_t)(i + j); b[n] = (uint8_t)(i + j + k); ++n; }
-  }
-};
-const SortNet g_sort_net;
-
-// sorts x[0, n) (n <= kSortNet) into ord: x[ord[0]] <= x[ord[1]] <= .., NaN last
-inline void sort_small(const double* x, int64_t n, int64_t* ord) {
-  uint64_t k[kSortNet];
-  int64_t ix[kSortNet];
-  for (int i = 0; i < kSortNet; ++i) {
-    uint64_t u = ~0ull;                              // (padding: after everything)
-    if (i < n) {
-      const double v = x[i];
-      memcpy(&u, &v, 8);
-      u = v != v ? ~0ull - 1 : (u >> 63 ? ~u : u | (1ull << 63));   // (NaN: after every number)
-    }
-    k[i] = u;
-    ix[i] = i;
-  }
-  for (int c = 0; c < g_sort_net.n; ++c) {
-    const int a = g_sort_net.a[c], b = g_sort_net.b[c];
-    const uint64_t ka = k[a], kb = k[b];
-    const bool sw = ka > kb;
-    const int64_t ia = ix[a], ib = ix[b];
-    k[a] = sw ? kb : ka; k[b] = sw ? ka : kb;
-    ix[a] = sw ? ib : ia; ix[b] = sw ? ia : ib;
-  }
-  for (int64_t i = 0; i < n; ++i) ord[i] = ix[i];
-}
-
 inline void below_positions(const int64_t* tids, int64_t n, const int64_t* below, int64_t nb,
                             std::vector<int32_t>& out) {
   out.clear();
@@ -167,6 +121,9 @@ inline void below_positions(const int64_t* tids, int64_t n, const int64_t* below
   }
 }
 
+// spec: a speculative fit on a pool worker (prefit): labels the caller must
+// fit are left alone (no need_fit flag), and a failure only leaves the fit
+// undone — the label's real fit, on the calling thread, reports it
 int fit_label(Tree& T, int i, bool spec = false) {
   Fit& f = (*T.fits)[(size_t)i];
   if (f.done) return TPE_OK;
